@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py — env-steps/s of the MI355X rollout + GAE + PPO-update path.
+
+Workload (BASELINE.json configs[1], "C2"): CartPole-v1:ppo shapes — MLP 4->256->256->{2,1},
+n_envs=4096 per GPU, n_steps=32, batch 256, 20 epochs (10 240 minibatch steps per rollout),
+gamma 0.98, lambda 0.8, clip 0.1, Adam lr 1e-3, max_grad_norm 0.5 — on the synthetic
+fixed-length-episode env (no gymnasium on the box).  A "step" is one
+reference epoch: one rollout of 4096 x 32 env steps (policy forward + sample + env step
+per vector step, bootstrap value, GAE) followed by the whole PPO update over it.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Multi-GPU: weak scaling — every rank owns its own 4096 envs (global env ids offset by
+rank), runs its own sampler stream, and the flat gradient is all-reduced (RCCL, mean)
+once per minibatch step before the norm clip.  value = all ranks' env steps / max-rank time.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "gymnasium-solver_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
+
+
+def _log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def stage_flops_bytes(D, H1, H2, A, B, P):
+    """Algorithmic work per launch of each minibatch-step kernel."""
+    A1 = A + 1
+    fwd = 2.0 * B * (D * H1 + H1 * H2 + H2 * A1)
+    loss = 2.0 * B * A1 * (H2 // 16) + 30.0 * B
+    bwd = 2.0 * B * H2 * A1 + 2.0 * B * H1 * H2 * 2 + 2.0 * B * H1 * (D + 1) + 2.0 * B * H2 * A1 + B * H2
+    adam_bytes = 4.0 * P * 7      # read p, g, m, v; write p, m, v
+    return {"fwd": ("mfma", fwd), "loss": ("mfma", loss), "bwd": ("mfma", bwd), "adam": ("hbm", adam_bytes)}
+
+
+def time_stages(agent, reps: int):
+    """Average device duration of each minibatch-step kernel, by events on the stream
+    the kernels are launched on (torch's current stream is passed to the C-ABI)."""
+    from gsamd._lib import check, lib
+    coll = agent.get_rollout_collector("train")
+    idx = agent.prefetcher.device_buf
+    pm = agent.policy_model
+    args = lambda st: (st, pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),  # noqa: E731
+                       agent.adam_v.data_ptr(), pm.dims, agent.hparams(), coll.buffer.view(), idx.data_ptr(),
+                       agent.batch_size, max(agent.adam_step, 1), agent.metrics_buf.data_ptr(),
+                       agent.workspace.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    saved = [t.clone() for t in (pm.params, agent.grads, agent.adam_m, agent.adam_v)]
+    out = {}
+    for st, name in enumerate(("fwd", "loss", "bwd", "adam")):
+        for _ in range(5):
+            check(lib.gs_ppo_stage(*args(st)), "gs_ppo_stage")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            check(lib.gs_ppo_stage(*args(st)), "gs_ppo_stage")
+        e1.record()
+        e1.synchronize()
+        out[name] = e0.elapsed_time(e1) / reps * 1e3   # microseconds per launch
+    for t, s in zip((pm.params, agent.grads, agent.adam_m, agent.adam_v), saved):
+        t.copy_(s)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n-envs", type=int, default=4096, help="envs per GPU (weak scaling)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of the hipGraph")
+    ap.add_argument("--stage-reps", type=int, default=200)
+    ap.add_argument("--cpu-minibatches", type=int, default=2000,
+                    help="minibatches in the bounded CPU-baseline sample (0 disables)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device(f"cuda:{local_rank}")
+    comm = None
+    if world > 1:
+        import ctypes
+
+        import torch.distributed as dist
+        from gsamd._lib import check, lib
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            check(lib.gs_comm_unique_id(uid.data_ptr()), "gs_comm_unique_id")
+        uid_d = uid.to(device)
+        dist.broadcast(uid_d, 0)
+        uid = uid_d.cpu().contiguous()
+        h = ctypes.c_void_p()
+        check(lib.gs_comm_init(uid.data_ptr(), world, rank, ctypes.byref(h)), "gs_comm_init")
+        comm = h.value
+
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=args.n_envs))
+    agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world, comm=comm,
+                           use_graph=not args.no_graph, track_stats=False)
+    N, T = cfg.n_envs, cfg.n_steps
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    tw = time.perf_counter()
+    for _ in range(args.warmup):
+        agent.train_epoch()
+    barrier()
+    _log(f"[bench] rank {rank}: warmup {args.warmup} steps {time.perf_counter() - tw:.2f}s")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        agent.train_epoch()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    losses = agent.minibatch_losses()
+    if not (losses == losses).all():
+        raise RuntimeError("non-finite loss in the timed region")
+    total_env_steps = world * N * T * args.steps
+    value = total_env_steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- roofline of the dominant minibatch kernel (device time by events) ----
+    stage_us = time_stages(agent, args.stage_reps)
+    pm = agent.policy_model
+    work = stage_flops_bytes(pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions, agent.batch_size,
+                             pm.n_params)
+    dom = max(stage_us, key=stage_us.get)
+    bound, amount = work[dom]
+    if bound == "mfma":
+        achieved = amount / (stage_us[dom] * 1e-6) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 6), "traffic": None}
+    else:
+        achieved = amount / (stage_us[dom] * 1e-6) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": None}
+    roofline["kernel"] = {"fwd": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}[dom]
+    roofline["avg_us"] = round(stage_us[dom], 3)
+    roofline["work_per_launch"] = amount
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                roofline["traffic"] = json.load(f).get(roofline["kernel"], {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+
+    # ---- CPU baseline (rank 0, N=1 only): oracle restatement on the host cores ----
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_minibatches > 0:
+        from oracle.cpu_ppo import run_cpu_baseline
+        cores = min(len(os.sched_getaffinity(0)), 16)
+        r = run_cpu_baseline(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,
+                             max_minibatches=args.cpu_minibatches, threads=cores)
+        cpu = {"value": round(r["env_steps_per_s"], 2), "unit": "env_steps/s", "cores": r["threads"], "kind": "port",
+               "sample": (f"1 rollout of {N}x{T} env steps (torch-CPU policy, numpy synthetic env, numpy GAE) + "
+                          f"{r['minibatches_timed']} of {r['minibatches_per_rollout']} minibatch steps "
+                          f"(torch-CPU fwd/bwd/clip/Adam), update extrapolated; wall {r['wall_s']:.1f}s"),
+               "collect_s": round(r["collect_s"], 4), "minibatch_ms": round(r["minibatch_s"] * 1e3, 4)}
+
+    if rank == 0:
+        line = {
+            "metric": "env steps/sec (rollout+PPO update), CartPole n_envs=4096, 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "CartPole-v1:ppo C2 (rollout 4096 envs x 32 steps + 20-epoch PPO update, B=256)",
+                       "n_envs_per_gpu": N, "n_steps": T, "batch_size": cfg.batch_size, "n_epochs": cfg.n_epochs,
+                       "minibatches_per_step": agent.n_minibatches, "policy": "MLP 4-256-256-{2,1}",
+                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph},
+            "roofline": roofline,
+            "stages_us": {k: round(v, 3) for k, v in stage_us.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

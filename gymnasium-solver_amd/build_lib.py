@@ -1,0 +1,67 @@
+"""Build libgsamd.so (HIP for gfx950 + host C++) in-tree with plain hipcc command lines.
+
+Objects go to gymnasium-solver_amd/build/, the library to gymnasium-solver_amd/gsamd/libgsamd.so
+(git-ignored; it travels to the GPU box with the gpurun snapshot).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "build")
+LIB = os.path.join(HERE, "gsamd", "libgsamd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+# per-file extra flags: the GAE scan must not contract mul+add into FMA (bit-exactness
+# with the reference's numpy float32 loop)
+EXTRA = {"gs_gae.hip": ["-ffp-contract=off"]}
+
+
+def _sources():
+    return sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+
+
+def _obj(src):
+    return os.path.join(BUILD, src + ".o")
+
+
+def _compile(src):
+    path = os.path.join(CSRC, src)
+    obj = _obj(src)
+    deps = [path, os.path.join(CSRC, "gs_common.h"), os.path.join(HERE, "..", "include", "gsamd.h")]
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
+        return None
+    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-c", path, "-o", obj]
+    if src.endswith(".hip"):
+        cmd[1:1] = [f"--offload-arch={ARCH}", "-x", "hip"]
+    cmd += EXTRA.get(src, [])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return src
+
+
+def build(verbose: bool = False, jobs: int = 8) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    with ThreadPoolExecutor(max_workers=min(jobs, len(srcs))) as ex:
+        done = [s for s in ex.map(_compile, srcs) if s]
+    objs = [_obj(s) for s in srcs]
+    if done or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [
+            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"built {LIB} ({len(done)} objects recompiled)")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True, jobs=int(sys.argv[1]) if len(sys.argv) > 1 else 8)

@@ -1,0 +1,91 @@
+// Multi-GPU exchange: one process per GPU, an RCCL communicator over xGMI, and the
+// single data-path collective of the update — the flat fp32 gradient all-reduce per
+// minibatch step.  Rank 0 makes the unique id, the Python launcher
+// broadcasts it through torch.distributed, every rank then joins here.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include "../../include/gsamd.h"
+
+namespace gs {
+void set_error(const char *fmt, ...);
+}
+
+struct gs_comm {
+    ncclComm_t comm;
+    int nranks;
+    int rank;
+};
+
+#define GS_NCCL(call)                                                                    \
+    do {                                                                                 \
+        ncclResult_t _r = (call);                                                        \
+        if (_r != ncclSuccess) {                                                         \
+            gs::set_error("%s failed: %s", #call, ncclGetErrorString(_r));               \
+            return GS_E_COMM;                                                            \
+        }                                                                                \
+    } while (0)
+
+namespace gs {
+int comm_allreduce_sum(gs_comm *c, float *buf, int64_t n, hipStream_t s, int *world)
+{
+    *world = c->nranks;
+    if (c->nranks == 1) return GS_OK;
+    GS_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, s));
+    return GS_OK;
+}
+}  // namespace gs
+
+extern "C" int gs_comm_unique_id(uint8_t out_id[128])
+{
+    ncclUniqueId id;
+    GS_NCCL(ncclGetUniqueId(&id));
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    memcpy(out_id, &id, 128);
+    return GS_OK;
+}
+
+extern "C" int gs_comm_init(const uint8_t id_bytes[128], int nranks, int rank, gs_comm **out)
+{
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks) {
+        gs::set_error("gs_comm_init: bad rank %d / nranks %d", rank, nranks);
+        return GS_E_INVALID;
+    }
+    gs_comm *c = new gs_comm{};
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclUniqueId id;
+    memcpy(&id, id_bytes, 128);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        gs::set_error("ncclCommInitRank failed: %s", ncclGetErrorString(r));
+        delete c;
+        return GS_E_COMM;
+    }
+    *out = c;
+    return GS_OK;
+}
+
+extern "C" int gs_comm_allreduce_mean_f32(gs_comm *comm, float *buf, int64_t count, void *stream)
+{
+    if (!comm || !buf || count < 0) {
+        gs::set_error("gs_comm_allreduce_mean_f32: bad argument");
+        return GS_E_INVALID;
+    }
+    if (comm->nranks == 1) return GS_OK;
+    GS_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclAvg, comm->comm, (hipStream_t)stream));
+    return GS_OK;
+}
+
+extern "C" int gs_comm_destroy(gs_comm *comm)
+{
+    if (!comm) return GS_OK;
+    ncclResult_t r = ncclCommDestroy(comm->comm);
+    delete comm;
+    if (r != ncclSuccess) {
+        gs::set_error("ncclCommDestroy failed: %s", ncclGetErrorString(r));
+        return GS_E_COMM;
+    }
+    return GS_OK;
+}

@@ -1,0 +1,122 @@
+// Shared declarations for the libgsamd kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/gsamd.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace gs {
+
+// ---- error plumbing (thread-local last error, like cudaGetLastError but with text)
+void set_error(const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what, const char *file, int line);
+
+#define GS_HIP(call)                                                         \
+    do {                                                                     \
+        hipError_t _e = (call);                                              \
+        if (_e != hipSuccess) return gs::hip_fail(_e, #call, __FILE__, __LINE__); \
+    } while (0)
+
+#define GS_REQUIRE(cond, ...)                    \
+    do {                                         \
+        if (!(cond)) {                           \
+            gs::set_error(__VA_ARGS__);          \
+            return GS_E_INVALID;                 \
+        }                                        \
+    } while (0)
+
+#define GS_LAUNCH_CHECK(name)                                                        \
+    do {                                                                             \
+        hipError_t _e = hipGetLastError();                                           \
+        if (_e != hipSuccess) return gs::hip_fail(_e, "launch " name, __FILE__, __LINE__); \
+    } while (0)
+
+// ---- flat parameter layout, reference state_dict order (utils/models.py:285-326)
+struct Layout {
+    int D, H1, H2, A;
+    int64_t oW1, ob1, oW2, ob2, oWp, obp, oWv, obv, P;
+    __host__ __device__ static Layout make(int D, int H1, int H2, int A) {
+        Layout L;
+        L.D = D; L.H1 = H1; L.H2 = H2; L.A = A;
+        L.oW1 = 0;
+        L.ob1 = L.oW1 + (int64_t)H1 * D;
+        L.oW2 = L.ob1 + H1;
+        L.ob2 = L.oW2 + (int64_t)H2 * H1;
+        L.oWp = L.ob2 + H2;
+        L.obp = L.oWp + (int64_t)A * H2;
+        L.oWv = L.obp + A;
+        L.obv = L.oWv + H2;
+        L.P = L.obv + 1;
+        return L;
+    }
+    // head row a in [0, A]: a < A -> policy_head.weight[a], a == A -> value_head.weight
+    __host__ __device__ int64_t head_row(int a) const { return a < A ? oWp + (int64_t)a * H2 : oWv; }
+    __host__ __device__ int64_t head_bias(int a) const { return a < A ? obp + a : obv; }
+};
+
+constexpr int kTile = 16;        // MFMA 16x16x4 f32 output tile
+constexpr int kMaxObsDim = 64;
+constexpr int kMaxHidden = 1024;
+constexpr int kMaxActions = 32;
+
+// Workspace carve-up for one minibatch step (bytes, 256-aligned), see gs_ppo.hip.
+struct Workspace {
+    float *x;        // (B, D)     gathered observations
+    float *h1;       // (B, H1)    post-ReLU
+    float *h2;       // (B, H2)    post-ReLU
+    float *zpart;    // (H2/16, B, A+1) partial head outputs
+    float *dz;       // (B, A+1)   dLoss/dlogits | dLoss/dvalue
+    float *part1;    // (B/16, H1, D+1) dW1|db1 partials per row block
+    float *sumsq;    // (n_slots)  per-tile sum of squared gradients
+    int n_slots;
+    size_t bytes;
+};
+Workspace carve_workspace(void *base, const Layout &L, int64_t B);
+
+struct LossArgs {
+    float clip_lo, clip_hi;     // f32(1 - clip), f32(1 + clip) (torch clamp casts scalars to f32)
+    float clip_vf;              // f32(clip_range_vf)
+    float vf_coef, ent_coef;
+    float target_kl;            // <= 0: None
+    int normalize;
+};
+
+struct AdamArgs {
+    float max_norm;         // <= 0: no clip
+    float one_minus_b1;     // lerp weight f32(1 - beta1)
+    float b2;               // f32(beta2)
+    float one_minus_b2;     // f32(1 - beta2)
+    float neg_step_size;    // f32(-lr / (1 - beta1^t))
+    float bc2_sqrt;         // f32(sqrt(1 - beta2^t))
+    float eps;
+    float grad_scale;       // 1/world for all-reduced sums, else 1
+    int n_slots;
+    int nrb;                // dW1/db1 partial row blocks (0: grads already final in G)
+    const float *sched;     // optional device table {neg_step_size, bc2_sqrt} per step (graph replay)
+    int sched_idx;
+};
+
+inline int n_col_blocks(int H) { return (H + kTile - 1) / kTile; }
+inline int n_sumsq_slots(const Layout &L) { return n_col_blocks(L.H2) * n_col_blocks(L.H1) + 2 * n_col_blocks(L.H2) + 1; }
+
+// kernels' launch helpers (gs_mlp.hip)
+int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, const int32_t *idx,
+                      int64_t T, int64_t N, int64_t rows, float *x_out, float *h1_out, float *h2_out,
+                      float *zpart, float *obs_copy, const int32_t *stop_flag, hipStream_t s);
+int launch_heads_act(const float *P, const Layout &L, const float *zpart, int64_t rows, int mode, uint64_t seed,
+                     uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s);
+int launch_loss(const float *P, const Layout &L, const float *zpart, int64_t B, const gs_rollout_view &ro,
+                const int32_t *idx, const LossArgs &la, float *dz, float *metrics, int32_t *stop, hipStream_t s);
+size_t bwd_lds_bytes(const Layout &L, int64_t B);
+int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
+               hipStream_t s);
+int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
+                     const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s);
+int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);
+int launch_sumsq_flat(const float *G, int64_t n, float *out, int nblocks, hipStream_t s);
+
+}  // namespace gs

@@ -1,0 +1,99 @@
+// Synthetic fixed-length-episode vector env on the device — the twin of
+// gsamd/synthetic_env.py: hashed observations, constant reward,
+// episodes of length L starting e mod L steps in, every `truncate_every`-th episode
+// ending truncated, same-step autoreset.  Writes straight into the time-major rollout
+// rows, so a rollout step never leaves HBM (the reference crosses host<->device three
+// times per step, utils/rollout_collector.py:476-534).
+#include "gs_common.h"
+
+namespace {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ float synth_obs(uint64_t seed, uint64_t env, uint64_t step, uint64_t dim)
+{
+    const uint64_t h = mix64(mix64(mix64(mix64(seed) ^ env) ^ step) ^ dim);
+    return (float)(uint32_t)(h >> 40) * 1.1920928955078125e-07f - 1.0f;   // * 2^-23 - 1, exact
+}
+
+__global__ __launch_bounds__(256) void k_env_reset(int32_t *__restrict__ state, float *__restrict__ ep_ret,
+                                                   float *__restrict__ obs, int64_t N, int D, int L, uint64_t seed,
+                                                   int64_t env_offset)
+{
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= N) return;
+    const uint64_t ge = (uint64_t)(env_offset + e);
+    state[4 * e + 0] = (int32_t)(ge % (uint64_t)L);
+    state[4 * e + 1] = 0;
+    state[4 * e + 2] = 0;
+    state[4 * e + 3] = 0;
+    ep_ret[e] = 0.0f;
+    for (int d = 0; d < D; ++d) obs[e * D + d] = synth_obs(seed, ge, 0, (uint64_t)d);
+}
+
+__global__ __launch_bounds__(256) void k_env_step(int32_t *__restrict__ state, float *__restrict__ ep_ret,
+                                                  float *__restrict__ obs, int64_t N, int D, int L, int trunc_every,
+                                                  float reward, uint64_t seed, int64_t env_offset, uint64_t step_count,
+                                                  float *__restrict__ rew_row, uint8_t *__restrict__ done_row,
+                                                  uint8_t *__restrict__ to_row, int32_t *__restrict__ ep_cnt,
+                                                  float *__restrict__ ep_ret_sum, float *__restrict__ ep_len_sum)
+{
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= N) return;
+    int k = state[4 * e + 0] + 1;
+    int epi = state[4 * e + 1];
+    int len = state[4 * e + 2] + 1;
+    float er = ep_ret[e] + reward;
+    const bool done = k >= L;
+    const bool trunc_ep = trunc_every > 0 && (epi % trunc_every) == trunc_every - 1;
+    rew_row[e] = reward;
+    done_row[e] = done ? 1 : 0;
+    to_row[e] = (done && trunc_ep) ? 1 : 0;
+    if (done) {
+        if (ep_cnt) ep_cnt[e] += 1;
+        if (ep_ret_sum) ep_ret_sum[e] += er;
+        if (ep_len_sum) ep_len_sum[e] += (float)len;
+        k = 0;
+        epi += 1;
+        len = 0;
+        er = 0.0f;
+    }
+    state[4 * e + 0] = k;
+    state[4 * e + 1] = epi;
+    state[4 * e + 2] = len;
+    ep_ret[e] = er;
+    const uint64_t ge = (uint64_t)(env_offset + e);
+    for (int d = 0; d < D; ++d) obs[e * D + d] = synth_obs(seed, ge, step_count, (uint64_t)d);
+}
+
+}  // namespace
+
+extern "C" int gs_env_reset(int32_t *state, float *ep_ret, float *obs, int64_t N, int32_t obs_dim, int32_t episode_len,
+                            uint64_t seed, int64_t env_offset, void *stream)
+{
+    GS_REQUIRE(N > 0 && obs_dim > 0 && episode_len > 0, "gs_env_reset: bad shape");
+    hipLaunchKernelGGL(k_env_reset, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, state,
+                       ep_ret, obs, N, obs_dim, episode_len, seed, env_offset);
+    GS_LAUNCH_CHECK("k_env_reset");
+    return GS_OK;
+}
+
+extern "C" int gs_env_step(int32_t *state, float *ep_ret, float *obs, int64_t N, int32_t obs_dim, int32_t episode_len,
+                           int32_t truncate_every, float reward, uint64_t seed, int64_t env_offset,
+                           uint64_t step_count, float *rewards_row, uint8_t *dones_row, uint8_t *timeouts_row,
+                           int32_t *ep_done_count, float *ep_ret_sum, float *ep_len_sum, void *stream)
+{
+    GS_REQUIRE(N > 0 && obs_dim > 0 && episode_len > 0, "gs_env_step: bad shape");
+    GS_REQUIRE(rewards_row && dones_row && timeouts_row, "gs_env_step: null output row");
+    hipLaunchKernelGGL(k_env_step, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, state,
+                       ep_ret, obs, N, obs_dim, episode_len, truncate_every, reward, seed, env_offset, step_count,
+                       rewards_row, dones_row, timeouts_row, ep_done_count, ep_ret_sum, ep_len_sum);
+    GS_LAUNCH_CHECK("k_env_step");
+    return GS_OK;
+}

@@ -1,0 +1,353 @@
+// Host orchestration of the device PPO path: policy act (rollout step), minibatch
+// step (4 launches), the per-rollout update loop and its hipGraph.
+//
+// Replaces the host loop of the reference:
+//   for batch in DataLoader(IndexDataset, sampler=MultiPassRandomSampler, collate):   dataloaders.py:63-77
+//       BaseAgent.training_step -> losses_for_batch -> _backpropagate_and_step      base_agent.py:330-366,591-621
+// Here the whole loop is enqueued from C++ on one stream (no per-minibatch host sync,
+// no .item() calls: metrics stay on device, one record per minibatch).
+#include <math.h>
+#include <string.h>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "gs_common.h"
+
+struct gs_comm;
+namespace gs {
+int comm_allreduce_sum(gs_comm *c, float *buf, int64_t n, hipStream_t s, int *world);
+}
+
+namespace gs {
+
+static size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+Workspace carve_workspace(void *base, const Layout &L, int64_t B)
+{
+    Workspace w{};
+    char *p = (char *)base;
+    size_t off = 0;
+    auto take = [&](size_t nfloats) {
+        float *r = p ? (float *)(p + off) : nullptr;
+        off += align256(nfloats * sizeof(float));
+        return r;
+    };
+    const int A1 = L.A + 1;
+    const int64_t nrb = (B + kTile - 1) / kTile;
+    w.x = take((size_t)B * L.D);
+    w.h1 = take((size_t)B * L.H1);
+    w.h2 = take((size_t)B * L.H2);
+    w.zpart = take((size_t)n_col_blocks(L.H2) * B * A1);
+    w.dz = take((size_t)B * A1);
+    w.part1 = take((size_t)nrb * L.H1 * (L.D + 1));
+    w.n_slots = n_sumsq_slots(L);
+    const int comm_slots = 64;
+    w.sumsq = take((size_t)(w.n_slots > comm_slots ? w.n_slots : comm_slots));
+    w.bytes = off;
+    return w;
+}
+
+static int check_dims(const gs_mlp_dims &d)
+{
+    GS_REQUIRE(d.obs_dim > 0 && d.obs_dim <= kMaxObsDim, "obs_dim %d outside [1, %d]", d.obs_dim, kMaxObsDim);
+    GS_REQUIRE(d.hidden1 > 0 && d.hidden1 % kTile == 0 && d.hidden1 <= kMaxHidden,
+               "hidden1 %d must be a positive multiple of 16 <= %d", d.hidden1, kMaxHidden);
+    GS_REQUIRE(d.hidden2 > 0 && d.hidden2 % kTile == 0 && d.hidden2 <= kMaxHidden,
+               "hidden2 %d must be a positive multiple of 16 <= %d", d.hidden2, kMaxHidden);
+    GS_REQUIRE(d.n_actions > 0 && d.n_actions <= kMaxActions, "n_actions %d outside [1, %d]", d.n_actions,
+               kMaxActions);
+    return GS_OK;
+}
+
+static Layout layout_of(const gs_mlp_dims &d) { return Layout::make(d.obs_dim, d.hidden1, d.hidden2, d.n_actions); }
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" int64_t gs_mlp_param_count(gs_mlp_dims dims) { return layout_of(dims).P; }
+
+extern "C" size_t gs_policy_scratch_bytes(gs_mlp_dims dims, int64_t N)
+{
+    const Layout L = layout_of(dims);
+    return align256((size_t)n_col_blocks(L.H2) * N * (L.A + 1) * sizeof(float));
+}
+
+extern "C" int gs_policy_act(const float *params, gs_mlp_dims dims, const float *obs, int64_t N, int mode,
+                             uint64_t rng_seed, uint64_t rng_counter, int64_t *actions, float *logp, float *value,
+                             float *obs_store, void *scratch, void *stream)
+{
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    GS_REQUIRE(N > 0, "gs_policy_act: N must be > 0");
+    GS_REQUIRE(mode >= 0 && mode <= 2, "gs_policy_act: mode %d not in {0,1,2}", mode);
+    GS_REQUIRE(params && obs && actions && logp && value && scratch, "gs_policy_act: null buffer");
+    const Layout L = layout_of(dims);
+    hipStream_t s = (hipStream_t)stream;
+    float *zpart = (float *)scratch;
+    rc = launch_fwd_hidden(params, L, obs, nullptr, 1, N, N, nullptr, nullptr, nullptr, zpart, obs_store, nullptr, s);
+    if (rc) return rc;
+    return launch_heads_act(params, L, zpart, N, mode, rng_seed, rng_counter, actions, logp, value, s);
+}
+
+extern "C" int gs_policy_value(const float *params, gs_mlp_dims dims, const float *obs, int64_t N, float *value,
+                               void *scratch, void *stream)
+{
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    GS_REQUIRE(N > 0 && params && obs && value && scratch, "gs_policy_value: bad argument");
+    const Layout L = layout_of(dims);
+    hipStream_t s = (hipStream_t)stream;
+    float *zpart = (float *)scratch;
+    rc = launch_fwd_hidden(params, L, obs, nullptr, 1, N, N, nullptr, nullptr, nullptr, zpart, nullptr, nullptr, s);
+    if (rc) return rc;
+    return launch_heads_act(params, L, zpart, N, 0, 0, 0, nullptr, nullptr, value, s);
+}
+
+extern "C" size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch)
+{
+    return carve_workspace(nullptr, layout_of(dims), batch).bytes;
+}
+
+namespace {
+
+struct StepArgs {
+    LossArgs la;
+    AdamArgs aa;
+};
+
+StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, int64_t t)
+{
+    StepArgs a{};
+    a.la.clip_lo = (float)(1.0 - (double)hp.clip_range);
+    a.la.clip_hi = (float)(1.0 + (double)hp.clip_range);
+    a.la.clip_vf = hp.clip_range_vf;
+    a.la.vf_coef = hp.vf_coef;
+    a.la.ent_coef = hp.ent_coef;
+    a.la.target_kl = hp.target_kl;
+    a.la.normalize = hp.normalize_adv;
+    const double b1 = hp.adam_beta1, b2 = hp.adam_beta2;
+    a.aa.max_norm = hp.max_grad_norm;
+    a.aa.one_minus_b1 = (float)(1.0 - b1);
+    a.aa.b2 = (float)b2;
+    a.aa.one_minus_b2 = (float)(1.0 - b2);
+    const double bc1 = 1.0 - pow(b1, (double)t);
+    const double bc2 = 1.0 - pow(b2, (double)t);
+    a.aa.neg_step_size = (float)(-(double)hp.lr / bc1);
+    a.aa.bc2_sqrt = (float)sqrt(bc2);
+    a.aa.eps = hp.adam_eps;
+    a.aa.grad_scale = 1.0f;
+    a.aa.n_slots = n_sumsq_slots(L);
+    a.aa.nrb = (int)((B + kTile - 1) / kTile);
+    return a;
+}
+
+int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const StepArgs &sa,
+                 const gs_rollout_view &ro, const int32_t *idx, int64_t B, float *metrics, int32_t *stop,
+                 const Workspace &ws, gs_comm *comm, hipStream_t s)
+{
+    int rc = launch_fwd_hidden(P, L, ro.obs, idx, ro.T, ro.N, B, ws.x, ws.h1, ws.h2, ws.zpart, nullptr, stop, s);
+    if (rc) return rc;
+    rc = launch_loss(P, L, ws.zpart, B, ro, idx, sa.la, ws.dz, metrics, stop, s);
+    if (rc) return rc;
+    rc = launch_bwd(P, L, B, ws, G, stop, s);
+    if (rc) return rc;
+    if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
+    // multi-GPU: finish the flat gradient, all-reduce (sum) over ranks, norm of the mean
+    rc = launch_reduce_part1(ws.part1, L, sa.aa.nrb, G, stop, s);
+    if (rc) return rc;
+    int world = 1;
+    rc = comm_allreduce_sum(comm, G, L.P, s, &world);
+    if (rc) return rc;
+    constexpr int kNormBlocks = 64;
+    rc = launch_sumsq_flat(G, L.P, ws.sumsq, kNormBlocks, s);
+    if (rc) return rc;
+    AdamArgs aa = sa.aa;
+    aa.n_slots = kNormBlocks;
+    aa.nrb = 0;
+    aa.grad_scale = 1.0f / (float)world;
+    return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
+}
+
+int validate_update(const gs_mlp_dims &dims, const gs_rollout_view &ro, int64_t batch, const void *ws)
+{
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    GS_REQUIRE(batch >= 2 && batch <= 1024, "batch %lld outside [2, 1024]", (long long)batch);
+    GS_REQUIRE(ro.T > 0 && ro.N > 0, "empty rollout");
+    GS_REQUIRE(ro.obs && ro.actions && ro.logprobs && ro.values && ro.advantages && ro.returns,
+               "rollout view has a null buffer");
+    GS_REQUIRE(ws, "null workspace");
+    const Layout L = layout_of(dims);
+    GS_REQUIRE(bwd_lds_bytes(L, batch) <= 160 * 1024, "batch %lld too large for the LDS budget", (long long)batch);
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" int gs_ppo_minibatch_step(float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
+                                     gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
+                                     int64_t adam_step, float *metrics, int32_t *stop_flag, void *workspace,
+                                     gs_comm *comm, void *stream)
+{
+    int rc = validate_update(dims, ro, batch, workspace);
+    if (rc) return rc;
+    GS_REQUIRE(adam_step >= 1, "adam_step is 1-based");
+    GS_REQUIRE(params && grads && adam_m && adam_v && idx && metrics, "gs_ppo_minibatch_step: null buffer");
+    const Layout L = layout_of(dims);
+    const Workspace ws = carve_workspace(workspace, L, batch);
+    const StepArgs sa = make_step_args(hp, L, batch, adam_step);
+    return enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx, batch, metrics, stop_flag, ws, comm,
+                        (hipStream_t)stream);
+}
+
+extern "C" int gs_ppo_loss(const float *params, gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view ro,
+                           const int32_t *idx, int64_t batch, float *metrics, void *workspace, void *stream)
+{
+    int rc = validate_update(dims, ro, batch, workspace);
+    if (rc) return rc;
+    GS_REQUIRE(params && idx && metrics, "gs_ppo_loss: null buffer");
+    const Layout L = layout_of(dims);
+    const Workspace ws = carve_workspace(workspace, L, batch);
+    const StepArgs sa = make_step_args(hp, L, batch, 1);
+    hipStream_t s = (hipStream_t)stream;
+    rc = launch_fwd_hidden(params, L, ro.obs, idx, ro.T, ro.N, batch, ws.x, ws.h1, ws.h2, ws.zpart, nullptr,
+                           nullptr, s);
+    if (rc) return rc;
+    return launch_loss(params, L, ws.zpart, batch, ro, idx, sa.la, ws.dz, metrics, nullptr, s);
+}
+
+extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
+                            gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
+                            int64_t adam_step, float *metrics, void *workspace, void *stream)
+{
+    int rc = validate_update(dims, ro, batch, workspace);
+    if (rc) return rc;
+    GS_REQUIRE(stage >= 0 && stage <= 3, "gs_ppo_stage: stage %d not in [0, 3]", stage);
+    const Layout L = layout_of(dims);
+    const Workspace ws = carve_workspace(workspace, L, batch);
+    const StepArgs sa = make_step_args(hp, L, batch, adam_step < 1 ? 1 : adam_step);
+    hipStream_t s = (hipStream_t)stream;
+    switch (stage) {
+    case 0:
+        return launch_fwd_hidden(params, L, ro.obs, idx, ro.T, ro.N, batch, ws.x, ws.h1, ws.h2, ws.zpart, nullptr,
+                                 nullptr, s);
+    case 1:
+        return launch_loss(params, L, ws.zpart, batch, ro, idx, sa.la, ws.dz, metrics, nullptr, s);
+    case 2:
+        return launch_bwd(params, L, batch, ws, grads, nullptr, s);
+    default:
+        return launch_clip_adam(params, L, grads, adam_m, adam_v, ws.part1, ws.sumsq, sa.aa, metrics, nullptr, s);
+    }
+}
+
+namespace {
+
+// A captured update phase: keyed by every pointer/shape baked into its nodes.
+struct GraphKey {
+    const void *p[12];
+    int64_t n[6];
+    bool operator==(const GraphKey &o) const
+    {
+        for (int i = 0; i < 12; ++i)
+            if (p[i] != o.p[i]) return false;
+        for (int i = 0; i < 6; ++i)
+            if (n[i] != o.n[i]) return false;
+        return true;
+    }
+};
+struct GraphKeyHash {
+    size_t operator()(const GraphKey &k) const
+    {
+        size_t h = 1469598103934665603ull;
+        for (int i = 0; i < 12; ++i) h = (h ^ (size_t)k.p[i]) * 1099511628211ull;
+        for (int i = 0; i < 6; ++i) h = (h ^ (size_t)k.n[i]) * 1099511628211ull;
+        return h;
+    }
+};
+struct GraphEntry {
+    hipGraphExec_t exec;
+    float *sched;
+};
+std::mutex g_graph_mu;
+std::unordered_map<GraphKey, GraphEntry, GraphKeyHash> g_graphs;
+
+}  // namespace
+
+extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
+                             gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
+                             int64_t n_minibatches, int64_t adam_step0, float *metrics, int32_t *stop_flag,
+                             void *workspace, gs_comm *comm, int use_graph, void *stream)
+{
+    int rc = validate_update(dims, ro, batch, workspace);
+    if (rc) return rc;
+    GS_REQUIRE(n_minibatches >= 0 && adam_step0 >= 0, "bad n_minibatches/adam_step0");
+    GS_REQUIRE(params && grads && adam_m && adam_v && idx && metrics, "gs_ppo_update: null buffer");
+    if (n_minibatches == 0) return GS_OK;
+    const Layout L = layout_of(dims);
+    const Workspace ws = carve_workspace(workspace, L, batch);
+    hipStream_t s = (hipStream_t)stream;
+    // Adam's bias corrections (computed in double on the host, exactly as
+    // torch.optim.Adam's single-tensor path does) change every step; eager launches pass
+    // them as kernel arguments, the graph reads them from a per-step device table that
+    // is refreshed before each replay, so one capture serves every rollout.
+    if (!use_graph || comm) {
+        for (int64_t k = 0; k < n_minibatches; ++k) {
+            const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
+            rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                              metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
+            if (rc) return rc;
+        }
+        return GS_OK;
+    }
+    GraphKey key{};
+    const void *ptrs[12] = {params, grads, adam_m, adam_v, ro.obs, ro.actions, ro.logprobs, ro.values,
+                            ro.advantages, ro.returns, idx, metrics};
+    for (int i = 0; i < 12; ++i) key.p[i] = ptrs[i];
+    key.n[0] = batch;
+    key.n[1] = n_minibatches;
+    key.n[2] = ((int64_t)dims.obs_dim << 48) ^ ((int64_t)dims.hidden1 << 32) ^ ((int64_t)dims.hidden2 << 16) ^ dims.n_actions;
+    key.n[3] = (int64_t)(intptr_t)workspace;
+    key.n[4] = (int64_t)(intptr_t)stop_flag;
+    key.n[5] = ro.T * 1000003 + ro.N;
+    // host-side hyper-parameters are baked into the capture: include them in the key
+    uint32_t hbits[12];
+    memcpy(hbits, &hp, sizeof(hbits));
+    for (int i = 0; i < 12; ++i) key.n[5] = key.n[5] * 31 + hbits[i];
+    std::lock_guard<std::mutex> lk(g_graph_mu);
+    auto it = g_graphs.find(key);
+    if (it == g_graphs.end()) {
+        GraphEntry ent{};
+        GS_HIP(hipMalloc(&ent.sched, sizeof(float) * 2 * (size_t)n_minibatches));
+        hipGraph_t g;
+        GS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        for (int64_t k = 0; k < n_minibatches; ++k) {
+            StepArgs sa = make_step_args(hp, L, batch, 1);
+            sa.aa.sched = ent.sched;
+            sa.aa.sched_idx = (int)k;
+            rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                              metrics + k * GS_NUM_METRICS, stop_flag, ws, nullptr, s);
+            if (rc) {
+                hipGraph_t dummy;
+                (void)hipStreamEndCapture(s, &dummy);
+                (void)hipFree(ent.sched);
+                return rc;
+            }
+        }
+        GS_HIP(hipStreamEndCapture(s, &g));
+        GS_HIP(hipGraphInstantiate(&ent.exec, g, nullptr, nullptr, 0));
+        GS_HIP(hipGraphDestroy(g));
+        it = g_graphs.emplace(key, ent).first;
+    }
+    std::vector<float> tab(2 * (size_t)n_minibatches);
+    for (int64_t k = 0; k < n_minibatches; ++k) {
+        const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
+        tab[2 * k] = sa.aa.neg_step_size;
+        tab[2 * k + 1] = sa.aa.bc2_sqrt;
+    }
+    // pageable source: the runtime stages it before returning, so `tab` may die here
+    GS_HIP(hipMemcpyAsync(it->second.sched, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    GS_HIP(hipGraphLaunch(it->second.exec, s));
+    return GS_OK;
+}

@@ -1,0 +1,116 @@
+"""ctypes binding of libgsamd.so (the C-ABI declared in include/gsamd.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` and linked against the same
+HIP runtime soname torch loads (libamdhip64.so.7), so importing torch first makes both
+share one runtime.  There is no fallback: if the library is missing, importing any
+device module raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before the library)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
+
+GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
+GS_NUM_METRICS = 16
+METRIC_SLOTS = (
+    "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
+    "explained_var", "kl", "approx_kl", "adv_norm_mean", "adv_norm_std", "kl_stop", "grad_norm",
+    "skipped", "res0", "res1",
+)
+M = {name: i for i, name in enumerate(METRIC_SLOTS)}
+
+
+class MlpDims(ctypes.Structure):
+    _fields_ = [("obs_dim", ctypes.c_int32), ("hidden1", ctypes.c_int32), ("hidden2", ctypes.c_int32),
+                ("n_actions", ctypes.c_int32)]
+
+
+class PPOHparams(ctypes.Structure):
+    _fields_ = [("clip_range", ctypes.c_float), ("clip_range_vf", ctypes.c_float), ("vf_coef", ctypes.c_float),
+                ("ent_coef", ctypes.c_float), ("max_grad_norm", ctypes.c_float), ("lr", ctypes.c_float),
+                ("adam_beta1", ctypes.c_float), ("adam_beta2", ctypes.c_float), ("adam_eps", ctypes.c_float),
+                ("target_kl", ctypes.c_float), ("normalize_adv", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class RolloutView(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("actions", ctypes.c_void_p), ("logprobs", ctypes.c_void_p),
+                ("values", ctypes.c_void_p), ("advantages", ctypes.c_void_p), ("returns", ctypes.c_void_p),
+                ("T", ctypes.c_int64), ("N", ctypes.c_int64)]
+
+
+class GsError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is not built: the device path has no CPU fallback. "
+            "Run `python -c 'import __graft_entry__ as g; g.build()'` from the repo root.")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp, i32, i64, u64, f32, f64, sz = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
+                                       ctypes.c_float, ctypes.c_double, ctypes.c_size_t)
+    sig = {
+        "gs_abi_version": (ctypes.c_int, []),
+        "gs_last_error": (ctypes.c_char_p, []),
+        "gs_gae_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i64, f64, f64, vp, vp, vp]),
+        "gs_sampler_stream_i32": (ctypes.c_int, [i64, i64, u64, vp, ctypes.c_int]),
+        "gs_mlp_param_count": (i64, [MlpDims]),
+        "gs_policy_scratch_bytes": (sz, [MlpDims, i64]),
+        "gs_policy_act": (ctypes.c_int, [vp, MlpDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp]),
+        "gs_policy_value": (ctypes.c_int, [vp, MlpDims, vp, i64, vp, vp, vp]),
+        "gs_env_reset": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, u64, i64, vp]),
+        "gs_env_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, f32, u64, i64, u64, vp, vp, vp, vp, vp,
+                                       vp, vp]),
+        "gs_ppo_workspace_bytes": (sz, [MlpDims, i64]),
+        "gs_ppo_minibatch_step": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64,
+                                                 vp, vp, vp, vp, vp]),
+        "gs_ppo_loss": (ctypes.c_int, [vp, MlpDims, PPOHparams, RolloutView, vp, i64, vp, vp, vp]),
+        "gs_ppo_stage": (ctypes.c_int, [ctypes.c_int, vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64,
+                                        i64, vp, vp, vp]),
+        "gs_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64, i64, vp,
+                                         vp, vp, vp, ctypes.c_int, vp]),
+        "gs_comm_unique_id": (ctypes.c_int, [vp]),
+        "gs_comm_init": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
+        "gs_comm_allreduce_mean_f32": (ctypes.c_int, [vp, vp, i64, vp]),
+        "gs_comm_destroy": (ctypes.c_int, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+lib = _load()
+EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
+            "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_env_reset", "gs_env_step",
+            "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_comm_unique_id",
+            "gs_comm_init", "gs_comm_allreduce_mean_f32", "gs_comm_destroy")
+
+
+def check(rc: int, what: str = "") -> None:
+    """Raise on a non-zero status: ValueError for bad arguments (the reference's error
+    type for shape/config problems), GsError for runtime/RCCL failures."""
+    if rc == GS_OK:
+        return
+    msg = (lib.gs_last_error() or b"").decode(errors="replace")
+    if rc == GS_E_INVALID:
+        raise ValueError(f"{what}: {msg}")
+    raise GsError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device/host address of a torch tensor (None passes NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int | None:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

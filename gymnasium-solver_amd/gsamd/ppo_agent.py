@@ -1,0 +1,239 @@
+"""Device PPO agent — the drop-in for the reference's PPOAgent/BaseAgent plugin surface.
+
+Reference surface mirrored (agents/__init__.py:1-8, agents/base_agent.py:26-885,
+agents/ppo/ppo_agent.py:10-152):
+  build_agent(config)                         -> DevicePPOAgent when config.algo_id == "ppo"
+  train_dataloader()                          first rollout + minibatch index stream  (base_agent.py:253-283)
+  on_train_epoch_start()                      re-collect from epoch 1 on             (base_agent.py:284-328)
+  training_step(batch, batch_idx)             one fused minibatch step               (base_agent.py:330-366)
+  losses_for_batch(batch, batch_idx)          {loss, early_stop_epoch}               (ppo_agent.py:21-152)
+  configure_optimizers()                      Adam(lr=policy_lr) state in HBM         (base_agent.py:633-639)
+  get_rollout_collector(stage)                DeviceRolloutCollector
+and the fast path the trainer uses instead of per-minibatch Python:
+  train_epoch()                               rollout + the whole update phase in one C-ABI call
+Metrics are kept on device, one 16-float record per minibatch, and converted to the
+reference's metric keys once per epoch (the reference pays ~20 .item() syncs per
+minibatch, SURVEY.md §3 Boundaries).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+
+from ._lib import GS_NUM_METRICS, M, PPOHparams, check, lib, ptr, stream_handle
+from .policy import DeviceMLPActorCritic
+from .rollout import DeviceRolloutCollector, DeviceSyntheticVecEnv
+from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
+
+STAGES = ("train",)
+
+
+class MinibatchIndices:
+    """A minibatch as the device sees it: B env-major sample indices (int32, in HBM)."""
+
+    def __init__(self, idx: torch.Tensor, trajectories=None):
+        self.idx = idx
+        self.trajectories = trajectories
+
+    def __len__(self):
+        return int(self.idx.numel())
+
+
+class DevicePPOAgent:
+    def __init__(self, config, env=None, device: Optional[str] = None, rank: int = 0, world_size: int = 1,
+                 comm=None, use_graph: bool = True, track_stats: bool = True):
+        self.config = config
+        self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
+        self.rank, self.world_size, self.comm = int(rank), int(world_size), comm
+        self.use_graph = bool(use_graph)
+        self.track_stats = bool(track_stats)
+        # schedulable hyper-parameters (base_agent.py:72-77)
+        self.policy_lr = config.policy_lr
+        self.clip_range = config.clip_range
+        self.vf_coef = config.vf_coef
+        self.ent_coef = config.ent_coef
+        self.n_epochs = config.n_epochs
+        self.current_epoch = 0
+        self._early_stop_epoch = False
+        self._envs: Dict[str, Any] = {}
+        self._rollout_collectors: Dict[str, DeviceRolloutCollector] = {}
+        self.metrics_history = []
+        self.build_env("train", env)
+        self.build_models()
+        self.build_rollout_collector("train")
+        self.configure_optimizers()
+
+    # ---- construction (base_agent.py:103-222) -------------------------------------------
+    def build_env(self, stage: str, env=None):
+        if env is None:
+            c = self.config
+            env = DeviceSyntheticVecEnv(n_envs=c.n_envs, obs_dim=c.resolved_obs_dim(), n_actions=c.resolved_n_actions(),
+                                        episode_len=c.episode_len, seed=c.seed, truncate_every=c.truncate_every,
+                                        env_offset=self.rank * c.n_envs, device=self.device)
+        self._envs[stage] = env
+
+    def get_env(self, stage: str):
+        return self._envs[stage]
+
+    def build_models(self):
+        c = self.config
+        self.policy_model = DeviceMLPActorCritic(c.resolved_obs_dim(), c.hidden_dims, c.resolved_n_actions(),
+                                                 device=self.device)
+
+    def build_rollout_collector(self, stage: str):
+        c = self.config
+        self._rollout_collectors[stage] = DeviceRolloutCollector(
+            self.get_env(stage), self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
+            rng_seed=c.seed + 7919 * self.rank, track_stats=self.track_stats)
+
+    def get_rollout_collector(self, stage: str) -> DeviceRolloutCollector:
+        return self._rollout_collectors[stage]
+
+    def configure_optimizers(self):
+        """Adam(params, lr=policy_lr) (utils/optimizer_factory.py:6-29): state in HBM."""
+        if str(getattr(self.config, "optimizer", "adam")).lower() != "adam":
+            raise ValueError("device path implements the reference's default optimizer 'adam' only")
+        P = self.policy_model.n_params
+        z = dict(dtype=torch.float32, device=self.device)
+        self.grads = torch.zeros(P, **z)
+        self.adam_m = torch.zeros(P, **z)
+        self.adam_v = torch.zeros(P, **z)
+        self.adam_step = 0
+        c = self.config
+        self.batch_size = int(c.batch_size)
+        self.data_len = c.n_envs * c.n_steps
+        if self.data_len % self.batch_size != 0:
+            raise ValueError(f"Batch size must divide rollout size exactly: data_len={self.data_len}, "
+                             f"batch_size={self.batch_size}.")
+        self.n_minibatches = self.data_len // self.batch_size * c.n_epochs
+        ws = int(lib.gs_ppo_workspace_bytes(self.policy_model.dims, self.batch_size))
+        self.workspace = torch.zeros(ws, dtype=torch.uint8, device=self.device)
+        self.stop_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.metrics_buf = torch.zeros(self.n_minibatches, GS_NUM_METRICS, **z)
+        self._step_metrics = torch.zeros(GS_NUM_METRICS, **z)
+        self.prefetcher = IndexStreamPrefetcher(self.data_len, c.n_epochs, int(torch.initial_seed()), self.device)
+        return None
+
+    def hparams(self) -> PPOHparams:
+        c = self.config
+        tkl = c.target_kl if c.target_kl is not None else 0.0
+        return PPOHparams(float(self.clip_range), float(c.clip_range_vf), float(self.vf_coef), float(self.ent_coef),
+                          float(c.max_grad_norm if c.max_grad_norm is not None else 0.0), float(self.policy_lr),
+                          0.9, 0.999, 1e-8, float(tkl), 1 if c.normalize_advantages == "batch" else 0, 0)
+
+    # ---- Lightning-style hooks ------------------------------------------------------------
+    def train_dataloader(self):
+        """Collect the first rollout and return the minibatch index loader of epoch 0."""
+        self._trajectories = self.get_rollout_collector("train").collect()
+        return self._epoch_batches(0)
+
+    def _epoch_batches(self, epoch: int):
+        idx = self.prefetcher.upload(epoch)
+        self.prefetcher.prefetch(epoch + 1)
+        B = self.batch_size
+        return [MinibatchIndices(idx[k * B:(k + 1) * B], self._trajectories) for k in range(self.n_minibatches)]
+
+    def on_train_epoch_start(self):
+        if self.current_epoch > 0:
+            self._trajectories = self.get_rollout_collector("train").collect()
+
+    def losses_for_batch(self, batch: MinibatchIndices, batch_idx: int):
+        """PPOAgent.losses_for_batch: loss + metrics of one minibatch (no optimizer step)."""
+        buf = self.get_rollout_collector("train").buffer
+        check(lib.gs_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(), buf.view(),
+                              ptr(batch.idx), len(batch), ptr(self._step_metrics), ptr(self.workspace),
+                              stream_handle()), "gs_ppo_loss")
+        early = False
+        if self.config.target_kl is not None:
+            early = float(self._step_metrics[M["approx_kl"]].item()) > float(self.config.target_kl)
+        return dict(loss=self._step_metrics[M["loss"]].clone(), early_stop_epoch=early)
+
+    def training_step(self, batch: MinibatchIndices, batch_idx: int):
+        """Forward, loss, backward, clip_grad_norm_(max_grad_norm), Adam.step — fused."""
+        if self._early_stop_epoch:
+            return None
+        buf = self.get_rollout_collector("train").buffer
+        self.adam_step += 1
+        rec = self.metrics_buf[batch_idx % self.n_minibatches]
+        check(lib.gs_ppo_minibatch_step(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                        ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(),
+                                        ptr(batch.idx), len(batch), self.adam_step, ptr(rec), ptr(self.stop_flag),
+                                        ptr(self.workspace), self.comm, stream_handle()), "gs_ppo_minibatch_step")
+        return None
+
+    # ---- fused epoch (the trainer's path) -------------------------------------------------------
+    def train_epoch(self) -> None:
+        """One reference epoch: rollout (epoch > 0) + n_epochs passes of minibatch steps."""
+        epoch = self.current_epoch
+        collector = self.get_rollout_collector("train")
+        if epoch == 0 and collector.total_rollouts == 0:
+            self._trajectories = collector.collect()
+        elif epoch > 0:
+            self._trajectories = collector.collect()
+        idx = self.prefetcher.upload(epoch)
+        self.prefetcher.prefetch(epoch + 1)
+        buf = collector.buffer
+        check(lib.gs_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
+                                self.policy_model.dims, self.hparams(), buf.view(), ptr(idx), self.batch_size,
+                                self.n_minibatches, self.adam_step, ptr(self.metrics_buf), ptr(self.stop_flag),
+                                ptr(self.workspace), self.comm, 1 if self.use_graph else 0, stream_handle()),
+              "gs_ppo_update")
+        self.adam_step += self.n_minibatches
+        self.current_epoch += 1
+
+    def epoch_metrics(self) -> Dict[str, float]:
+        """Reference metric keys (ppo_agent.py:131-146, torch.py:170-173), epoch means."""
+        rec = self.metrics_buf.cpu().numpy()
+        live = rec[rec[:, M["skipped"]] == 0]
+        if len(live) == 0:
+            live = rec[:1] * 0
+        mean = live.mean(axis=0)
+        vf, ent = float(self.vf_coef), float(self.ent_coef)
+        out = {
+            "opt/loss/total": mean[M["loss"]], "opt/loss/policy": mean[M["policy_loss"]],
+            "opt/loss/entropy": -mean[M["entropy"]], "opt/policy/entropy": mean[M["entropy"]],
+            "opt/loss/entropy_scaled": -ent * mean[M["entropy"]], "opt/loss/value": mean[M["value_loss"]],
+            "opt/loss/value_scaled": vf * mean[M["value_loss"]], "opt/ppo/clip_fraction": mean[M["clip_fraction"]],
+            "opt/ppo/clip_fraction_vf": mean[M["clip_fraction_vf"]],
+            "opt/value/explained_var": mean[M["explained_var"]], "opt/ppo/kl": mean[M["kl"]],
+            "opt/ppo/approx_kl": mean[M["approx_kl"]], "opt/ppo/kl_stop_triggered": mean[M["kl_stop"]],
+            "opt/grads/norm/all": mean[M["grad_norm"]],
+        }
+        if self.config.normalize_advantages == "batch":
+            out["roll/adv/norm/mean"] = mean[M["adv_norm_mean"]]
+            out["roll/adv/norm/std"] = mean[M["adv_norm_std"]]
+        return {k: float(v) for k, v in out.items()}
+
+    def minibatch_losses(self) -> np.ndarray:
+        return self.metrics_buf[:, M["loss"]].cpu().numpy().astype(np.float64)
+
+    def learn(self, max_epochs: Optional[int] = None, log=None) -> None:
+        """Lightning-free fit loop: max_env_steps guard (base_agent.py:306-320) + epochs."""
+        c = self.config
+        epochs = 0
+        while max_epochs is None or epochs < max_epochs:
+            if c.max_env_steps is not None:
+                done = self.get_rollout_collector("train").total_steps
+                if done + c.n_envs * c.n_steps * self.world_size > c.max_env_steps:
+                    break
+            self.train_epoch()
+            epochs += 1
+            if log is not None:
+                log({**self.get_rollout_collector("train").get_metrics(), **self.epoch_metrics()})
+
+    # ---- misc -----------------------------------------------------------------------------------
+    def make_sampler(self) -> MultiPassRandomSampler:
+        return MultiPassRandomSampler(self.data_len, self.config.n_epochs)
+
+
+def build_agent(config, *args, **kwargs):
+    """agents/__init__.py:1-8 for the device path."""
+    if config.algo_id != "ppo":
+        raise ValueError(f"device path implements algo_id 'ppo' only, got {config.algo_id!r}")
+    return DevicePPOAgent(config, *args, **kwargs)
+
+
+_ = ctypes

@@ -1,0 +1,314 @@
+"""Device-resident rollout: SoA buffer in HBM, fused policy-act kernels, GAE scan.
+
+Mirrors the reference's RolloutBuffer (utils/rollout_buffer.py:28-173) and
+RolloutCollector (utils/rollout_collector.py:22-777) for the PPO path
+(returns_type "gae:rtg", advantages_type "gae"):
+
+  * buffers are allocated once, time-major ``(T, N, ...)`` like the reference's numpy
+    buffers, but in HBM; a rollout never copies them to the host;
+  * per step: ``gs_policy_act`` (MLP forward + categorical sample + log_prob, writes
+    the step's obs/action/logp/value rows) then the env step;  with the device
+    synthetic env (``env.device_native``) the env step is a kernel writing the
+    reward/done/timeout rows, so the whole rollout is stream-ordered kernels;  a host
+    gymnasium-style env goes through one H2D/D2H per step as in the reference;
+  * last-obs value + ``gs_gae_f32`` produce advantages/returns in place;
+  * ``bootstrapped_values`` stays all-zero: with gymnasium 1.x vector envs the
+    reference never receives ``final_observation``, so its
+    ``bootstrapped_values_buf`` is never written yet IS read at timeouts; this
+    reproduces that behaviour (pass ``bootstrap_timeouts=True`` to opt out is future work).
+
+The returned trajectory keeps the reference's field names; env-major ``(N*T, ...)``
+views (utils/rollout_buffer.py:105-173) are materialised only when accessed — the
+device update reads the time-major buffers directly through sampler indices.
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ._lib import check, lib, ptr, stream_handle
+from .rollout_stats import RollingWindow
+
+
+class DeviceSyntheticVecEnv:
+    """Device twin of gsamd.synthetic_env.SyntheticVecEnv (same hash, same episodes)."""
+
+    device_native = True
+
+    def __init__(self, n_envs, obs_dim, n_actions, episode_len=200, seed=42, truncate_every=0, env_offset=0,
+                 reward=1.0, device="cuda"):
+        self.num_envs, self.obs_dim, self.n_actions = int(n_envs), int(obs_dim), int(n_actions)
+        self.episode_len, self.seed, self.truncate_every = int(episode_len), int(seed), int(truncate_every)
+        self.env_offset, self.reward = int(env_offset), float(reward)
+        self.device = torch.device(device)
+        N = self.num_envs
+        self.state = torch.zeros(4 * N, dtype=torch.int32, device=self.device)
+        self.ep_ret = torch.zeros(N, dtype=torch.float32, device=self.device)
+        self.obs = torch.zeros(N, self.obs_dim, dtype=torch.float32, device=self.device)
+        self.ep_count = torch.zeros(N, dtype=torch.int32, device=self.device)
+        self.ep_ret_sum = torch.zeros(N, dtype=torch.float32, device=self.device)
+        self.ep_len_sum = torch.zeros(N, dtype=torch.float32, device=self.device)
+        self.step_count = 0
+
+    def reset(self):
+        self.step_count = 0
+        check(lib.gs_env_reset(ptr(self.state), ptr(self.ep_ret), ptr(self.obs), self.num_envs, self.obs_dim,
+                               self.episode_len, self.seed, self.env_offset, stream_handle()), "gs_env_reset")
+        return self.obs, {}
+
+    def step_into(self, rewards_row, dones_row, timeouts_row):
+        self.step_count += 1
+        check(lib.gs_env_step(ptr(self.state), ptr(self.ep_ret), ptr(self.obs), self.num_envs, self.obs_dim,
+                              self.episode_len, self.truncate_every, self.reward, self.seed, self.env_offset,
+                              self.step_count, ptr(rewards_row), ptr(dones_row), ptr(timeouts_row),
+                              ptr(self.ep_count), ptr(self.ep_ret_sum), ptr(self.ep_len_sum), stream_handle()),
+              "gs_env_step")
+
+
+class DeviceRolloutBuffer:
+    """Preallocated time-major SoA rollout storage in HBM (utils/rollout_buffer.py:28-80)."""
+
+    def __init__(self, n_envs: int, obs_dim: int, n_steps: int, device):
+        T, N = int(n_steps), int(n_envs)
+        self.T, self.N, self.obs_dim, self.device = T, N, int(obs_dim), torch.device(device)
+        z = dict(device=self.device)
+        self.obs = torch.zeros(T, N, self.obs_dim, dtype=torch.float32, **z)
+        self.actions = torch.zeros(T, N, dtype=torch.int64, **z)
+        self.logprobs = torch.zeros(T, N, dtype=torch.float32, **z)
+        self.values = torch.zeros(T, N, dtype=torch.float32, **z)
+        self.rewards = torch.zeros(T, N, dtype=torch.float32, **z)
+        self.dones = torch.zeros(T, N, dtype=torch.uint8, **z)
+        self.timeouts = torch.zeros(T, N, dtype=torch.uint8, **z)
+        self.bootstrapped_values = torch.zeros(T, N, dtype=torch.float32, **z)
+        self.advantages = torch.zeros(T, N, dtype=torch.float32, **z)
+        self.returns = torch.zeros(T, N, dtype=torch.float32, **z)
+        self.last_values = torch.zeros(N, dtype=torch.float32, **z)
+
+    def view(self):
+        from ._lib import RolloutView
+        return RolloutView(ptr(self.obs), ptr(self.actions), ptr(self.logprobs), ptr(self.values),
+                           ptr(self.advantages), ptr(self.returns), self.T, self.N)
+
+
+def _env_major(t: torch.Tensor) -> torch.Tensor:
+    T, N = t.shape[0], t.shape[1]
+    return t.transpose(0, 1).reshape(N * T, *t.shape[2:])
+
+
+class DeviceTrajectory:
+    """RolloutTrajectory-compatible (utils/rollout_buffer.py:16-25) view of a device rollout."""
+
+    _FIELDS = ("observations", "actions", "rewards", "dones", "logprobs", "values", "advantages", "returns",
+               "next_observations")
+
+    def __init__(self, buf: DeviceRolloutBuffer):
+        self.buffer = buf
+
+    def __len__(self):
+        return self.buffer.T * self.buffer.N
+
+    @property
+    def observations(self):
+        return _env_major(self.buffer.obs)
+
+    @property
+    def actions(self):
+        return _env_major(self.buffer.actions)
+
+    @property
+    def rewards(self):
+        return _env_major(self.buffer.rewards)
+
+    @property
+    def dones(self):
+        return _env_major(self.buffer.dones).bool()
+
+    @property
+    def logprobs(self):
+        return _env_major(self.buffer.logprobs)
+
+    @property
+    def values(self):
+        return _env_major(self.buffer.values)
+
+    @property
+    def advantages(self):
+        return _env_major(self.buffer.advantages)
+
+    @property
+    def returns(self):
+        return _env_major(self.buffer.returns)
+
+    @property
+    def next_observations(self):
+        raise NotImplementedError("next_observations are never read by PPO and are not stored on device")
+
+
+def compute_batched_gae_advantages_and_returns(values, rewards, dones, timeouts, last_values,
+                                               bootstrapped_next_values, gamma, gae_lambda, adv_out=None,
+                                               ret_out=None):
+    """Same signature and result as utils/returns_advantages.py:115-155, on device tensors
+    (T, N); bit-exact with the reference's numpy float32 loop."""
+    T, N = values.shape
+    dev = values.device
+    dones = dones.to(torch.uint8) if dones.dtype != torch.uint8 else dones
+    timeouts = timeouts.to(torch.uint8) if timeouts.dtype != torch.uint8 else timeouts
+    adv = adv_out if adv_out is not None else torch.empty(T, N, dtype=torch.float32, device=dev)
+    ret = ret_out if ret_out is not None else torch.empty(T, N, dtype=torch.float32, device=dev)
+    args = [values, rewards, dones, timeouts, bootstrapped_next_values, last_values]
+    for a in args:
+        if a is not None and not (a.is_cuda and a.is_contiguous()):
+            raise ValueError("GAE inputs must be contiguous device tensors")
+    check(lib.gs_gae_f32(ptr(values), ptr(rewards), ptr(dones), ptr(timeouts), ptr(bootstrapped_next_values),
+                         ptr(last_values), T, N, float(gamma), float(gae_lambda), ptr(adv), ptr(ret),
+                         stream_handle()), "gs_gae_f32")
+    return adv, ret
+
+
+class DeviceRolloutCollector:
+    """RolloutCollector (utils/rollout_collector.py:22-777) for the device path."""
+
+    def __init__(self, env, policy_model, n_steps, *, gamma: float = 0.99, gae_lambda: float = 0.95,
+                 stats_window_size: int = 100, rng_seed: int = 42, track_stats: bool = True, **kwargs):
+        self.env = env
+        self.policy_model = policy_model
+        self.n_steps = int(n_steps)
+        self.gamma, self.gae_lambda = float(gamma), float(gae_lambda)
+        self.n_envs = int(env.num_envs)
+        self.device = policy_model.device
+        self.rng_seed = int(rng_seed)
+        self.track_stats = bool(track_stats)
+        self.total_rollouts = self.total_steps = self.total_vec_steps = self.total_episodes = 0
+        self.rollout_steps = self.rollout_vec_steps = self.rollout_episodes = 0
+        self.rollout_fpss = RollingWindow(stats_window_size)
+        self._best_episode_reward = -float("inf")
+        self._last_episode_reward, self._last_episode_length = 0.0, 0
+        self._buffer: Optional[DeviceRolloutBuffer] = None
+        self._started = False
+        self._stats = None
+        self._ep_seen = None
+
+    # ---- phases --------------------------------------------------------------------
+    def _prepare(self):
+        if self._started:
+            return
+        if getattr(self.env, "device_native", False):
+            self.env.reset()
+            obs_dim = self.env.obs_dim
+        else:
+            obs, _ = self.env.reset()
+            self._host_obs = np.asarray(obs, dtype=np.float32)
+            obs_dim = self._host_obs.shape[1]
+        self._buffer = DeviceRolloutBuffer(self.n_envs, obs_dim, self.n_steps, self.device)
+        self._obs_dev = torch.zeros(self.n_envs, obs_dim, dtype=torch.float32, device=self.device)
+        self._started = True
+
+    @property
+    def buffer(self) -> DeviceRolloutBuffer:
+        self._prepare()
+        return self._buffer
+
+    def collect(self, deterministic: bool = False, replay_actions: Optional[torch.Tensor] = None):
+        """One rollout of n_steps vector steps; returns a DeviceTrajectory.
+
+        replay_actions: optional (T, N) int64 device tensor of actions to take instead of
+        sampling (parity tests replay a recorded reference rollout)."""
+        self._prepare()
+        buf, pm, N, T = self._buffer, self.policy_model, self.n_envs, self.n_steps
+        t0 = time.time()
+        mode = 2 if replay_actions is not None else (1 if deterministic else 0)
+        native = getattr(self.env, "device_native", False)
+        for t in range(T):
+            if replay_actions is not None:
+                buf.actions[t].copy_(replay_actions[t])
+            counter = self.total_vec_steps + t
+            if native:
+                pm.act(self.env.obs, mode=mode, rng_seed=self.rng_seed, rng_counter=counter, actions=buf.actions[t],
+                       logp=buf.logprobs[t], values=buf.values[t], obs_store=buf.obs[t])
+                self.env.step_into(buf.rewards[t], buf.dones[t], buf.timeouts[t])
+            else:
+                self._obs_dev.copy_(torch.from_numpy(self._host_obs))
+                pm.act(self._obs_dev, mode=mode, rng_seed=self.rng_seed, rng_counter=counter, actions=buf.actions[t],
+                       logp=buf.logprobs[t], values=buf.values[t], obs_store=buf.obs[t])
+                actions_np = buf.actions[t].cpu().numpy()
+                next_obs, rew, term, trunc, infos = self.env.step(actions_np)
+                done = np.logical_or(term, trunc)
+                buf.rewards[t].copy_(torch.from_numpy(np.asarray(rew, np.float32)))
+                buf.dones[t].copy_(torch.from_numpy(done.astype(np.uint8)))
+                buf.timeouts[t].copy_(torch.from_numpy(np.asarray(trunc).astype(np.uint8)))
+                self._host_episode_infos(done, infos)
+                self._host_obs = np.asarray(next_obs, dtype=np.float32)
+        last_obs = self.env.obs if native else self._obs_dev.copy_(torch.from_numpy(self._host_obs))
+        pm.predict_values(last_obs, out=buf.last_values)
+        compute_batched_gae_advantages_and_returns(buf.values, buf.rewards, buf.dones, buf.timeouts,
+                                                   buf.last_values, buf.bootstrapped_values, self.gamma,
+                                                   self.gae_lambda, adv_out=buf.advantages, ret_out=buf.returns)
+        self.rollout_steps, self.rollout_vec_steps = N * T, T
+        self.total_steps += N * T
+        self.total_vec_steps += T
+        self.total_rollouts += 1
+        if self.track_stats:
+            self._accumulate_stats()
+        self.rollout_fpss.append(N * T / max(time.time() - t0, 1e-9))
+        return DeviceTrajectory(buf)
+
+    def _host_episode_infos(self, done, infos):
+        ep, mask = infos.get("episode"), infos.get("_episode")
+        for e in np.nonzero(done)[0]:
+            r = float(ep["r"][e]) if ep is not None and mask is not None and mask[e] else 0.0
+            self._best_episode_reward = max(self._best_episode_reward, r)
+            self._last_episode_reward = r
+            self.total_episodes += 1
+
+    def _accumulate_stats(self):
+        """Device-side RunningStats sums (utils/rollout_stats.py:34-67) for get_metrics."""
+        buf = self._buffer
+        if self._stats is None:
+            self._stats = torch.zeros(10, dtype=torch.float64, device=self.device)
+        s = self._stats
+        s[0] += buf.obs.numel()
+        s[1] += buf.obs.sum(dtype=torch.float64)
+        s[2] += (buf.obs.double() ** 2).sum()
+        s[3] += buf.rewards.sum(dtype=torch.float64)
+        s[4] += (buf.rewards.double() ** 2).sum()
+        s[5] += buf.advantages.sum(dtype=torch.float64)
+        s[6] += (buf.advantages.double() ** 2).sum()
+        s[7] += buf.returns.sum(dtype=torch.float64)
+        s[8] += (buf.returns.double() ** 2).sum()
+        s[9] += buf.rewards.numel()
+
+    # ---- API parity ------------------------------------------------------------------
+    def slice_trajectories(self, trajectories, idxs):
+        """utils/rollout_collector.py:657-682 — index the env-major views."""
+        idx = torch.as_tensor(idxs, dtype=torch.int64, device=self.device)
+        from types import SimpleNamespace
+        return SimpleNamespace(**{f: getattr(trajectories, f)[idx] for f in DeviceTrajectory._FIELDS[:-1]})
+
+    def get_metrics(self):
+        """Key-compatible subset of utils/rollout_collector.py:686-760 (one D2H)."""
+        m = {"cnt/total_env_steps": self.total_steps, "cnt/total_vec_steps": self.total_vec_steps,
+             "cnt/total_rollouts": self.total_rollouts, "roll/env_steps": self.rollout_steps,
+             "roll/vec_steps": self.rollout_vec_steps,
+             "roll/fps": float(self.rollout_fpss.mean()) if self.rollout_fpss else 0.0}
+        if self._stats is not None:
+            s = self._stats.cpu().numpy()
+
+            def ms(sum_, sq, n):
+                mean = sum_ / max(n, 1)
+                return float(mean), float(np.sqrt(max(0.0, sq / max(n, 1) - mean * mean)))
+            m["roll/obs/mean"], m["roll/obs/std"] = ms(s[1], s[2], s[0])
+            m["roll/reward/mean"], m["roll/reward/std"] = ms(s[3], s[4], s[9])
+            m["roll/adv/mean"], m["roll/adv/std"] = ms(s[5], s[6], s[9])
+            m["roll/return/mean"], m["roll/return/std"] = ms(s[7], s[8], s[9])
+        env = self.env
+        if getattr(env, "device_native", False):
+            cnt = env.ep_count.sum().item()
+            if cnt > 0:
+                self.total_episodes = int(cnt)
+                m["roll/ep_rew/mean"] = float(env.ep_ret_sum.sum().item() / cnt)
+                m["roll/ep_len/mean"] = int(env.ep_len_sum.sum().item() / cnt)
+        m["cnt/total_episodes"] = self.total_episodes
+        return m

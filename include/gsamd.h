@@ -1,0 +1,201 @@
+/*
+ * gsamd.h — C-ABI of the MI355X-native rollout + GAE + PPO-update path
+ * (libgsamd.so, built from gymnasium-solver_amd/csrc/ for gfx950).
+ *
+ * Conventions (SURVEY.md §8b "What the C-ABI must export"):
+ *   - every pointer argument named *_dev is a caller-owned device (HBM) pointer;
+ *     *_host pointers are caller-owned host memory;
+ *   - kernels are enqueued on the caller's `stream` (a hipStream_t passed as void*;
+ *     NULL = legacy default stream) and return without synchronising;
+ *   - no hidden device allocation: scratch comes from a caller buffer sized by
+ *     gs_ppo_workspace_bytes();
+ *   - every function returns GS_OK (0) or a negative GS_E* code; the message of the
+ *     last failure on the calling thread is returned by gs_last_error().
+ *
+ * Data layout in HBM:
+ *   rollout buffers are time-major SoA: x[t * n_envs + env]; observations
+ *   obs[(t * n_envs + env) * obs_dim + d]; the reference's env-major sample index
+ *   i = env * T + t (utils/rollout_buffer.py:11-13) is mapped inside the kernels.
+ *   Policy parameters are ONE flat fp32 vector in the reference's state_dict order
+ *   (backbone.0.weight[H1][D], backbone.0.bias, backbone.2.weight[H2][H1],
+ *   backbone.2.bias, policy_head.weight[A][H2], policy_head.bias,
+ *   value_head.weight[1][H2], value_head.bias) — utils/models.py:285-326.
+ *   Gradients and Adam moments use the same layout.
+ */
+#ifndef GSAMD_H
+#define GSAMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_OK 0
+#define GS_E_INVALID (-1)   /* bad argument / unsupported shape: like the reference's ValueError */
+#define GS_E_HIP (-2)       /* HIP runtime error */
+#define GS_E_COMM (-3)      /* RCCL error */
+
+/* ---------------------------------------------------------------- misc */
+int gs_abi_version(void);
+const char *gs_last_error(void);
+
+/* ---------------------------------------------------------------- GAE
+ * Replaces utils/returns_advantages.py:115-155
+ * (compute_batched_gae_advantages_and_returns), called from
+ * utils/rollout_collector.py:372-384.  Bit-exact with the reference's float32 numpy
+ * loop.  values/rewards/adv/ret are (T, N) f32, dones/timeouts (T, N) u8 (0/1),
+ * bootstrap (T, N) f32 or NULL (= bootstrapped_next_values None), last_values (N).
+ */
+int gs_gae_f32(const float *values_dev, const float *rewards_dev, const uint8_t *dones_dev,
+               const uint8_t *timeouts_dev, const float *bootstrap_dev, const float *last_values_dev,
+               int64_t T, int64_t N, double gamma, double gae_lambda, float *adv_dev, float *ret_dev,
+               void *stream);
+
+/* ---------------------------------------------------------------- sampler (host)
+ * Replaces utils/samplers.py:25-34 (MultiPassRandomSampler.set_epoch + __iter__):
+ * seeds torch's CPU MT19937 with `seed` (= base_seed + epoch), draws
+ * rand((num_passes, data_len)) and writes the unstable argsort of each row
+ * (torch's introsort tie order) to out_host (num_passes * data_len int32).
+ * Host-side by construction (a sequential generator + introsort); n_threads > 1
+ * sorts passes in parallel.  The stream is then uploaded once per rollout.
+ */
+int gs_sampler_stream_i32(int64_t data_len, int64_t num_passes, uint64_t seed, int32_t *out_host,
+                          int n_threads);
+
+/* ---------------------------------------------------------------- MLP actor-critic
+ * dims: obs_dim D, hidden H1, H2 (two ReLU layers, the reference's mlp_small/medium/
+ * large presets; utils/model_registry.py:21-36), n_actions A.
+ */
+typedef struct gs_mlp_dims {
+    int32_t obs_dim;
+    int32_t hidden1;
+    int32_t hidden2;
+    int32_t n_actions;
+} gs_mlp_dims;
+
+int64_t gs_mlp_param_count(gs_mlp_dims dims);
+
+/* Policy forward for a rollout step — replaces utils/policy_ops.py:14-34 (policy_act)
+ * on MLPActorCritic.forward (utils/models.py:328-346) + Categorical sample / mode /
+ * log_prob.  obs_dev (N, D) f32.  mode: 0 = sample (counter-based RNG, key
+ * (rng_seed, rng_counter, env)), 1 = deterministic (argmax, first max wins),
+ * 2 = replay: actions_dev is an INPUT (recorded actions).  Writes actions (int64),
+ * logp, value (N) and, when obs_store_dev != NULL, copies obs into it (the rollout
+ * buffer slot of this step).  scratch_dev: gs_policy_scratch_bytes(dims, N) bytes.
+ */
+size_t gs_policy_scratch_bytes(gs_mlp_dims dims, int64_t N);
+int gs_policy_act(const float *params_dev, gs_mlp_dims dims, const float *obs_dev, int64_t N, int mode,
+                  uint64_t rng_seed, uint64_t rng_counter, int64_t *actions_dev, float *logp_dev,
+                  float *value_dev, float *obs_store_dev, void *scratch_dev, void *stream);
+
+/* Value-only forward (utils/policy_ops.py:37-42 policy_predict_values), e.g. the
+ * bootstrap value of the last observation (utils/rollout_collector.py:373). */
+int gs_policy_value(const float *params_dev, gs_mlp_dims dims, const float *obs_dev, int64_t N,
+                    float *value_dev, void *scratch_dev, void *stream);
+
+/* ---------------------------------------------------------------- synthetic env
+ * Device twin of gsamd/synthetic_env.py.  state_dev: 4 int32 per env
+ * (k, episode_idx, ep_len, pad) + ep_ret f32 (N); writes next obs into obs_dev (N, D),
+ * reward/done/timeout rows of step t into the (T, N) rollout buffers, and per-env
+ * completed-episode stats (ep_done_count, ep_ret_sum, ep_len_sum: N each, accumulated).
+ */
+int gs_env_reset(int32_t *state_dev, float *ep_ret_dev, float *obs_dev, int64_t N, int32_t obs_dim,
+                 int32_t episode_len, uint64_t seed, int64_t env_offset, void *stream);
+int gs_env_step(int32_t *state_dev, float *ep_ret_dev, float *obs_dev, int64_t N, int32_t obs_dim,
+                int32_t episode_len, int32_t truncate_every, float reward, uint64_t seed,
+                int64_t env_offset, uint64_t step_count, float *rewards_row_dev, uint8_t *dones_row_dev,
+                uint8_t *timeouts_row_dev, int32_t *ep_done_count_dev, float *ep_ret_sum_dev,
+                float *ep_len_sum_dev, void *stream);
+
+/* ---------------------------------------------------------------- PPO update
+ * Replaces the minibatch loop: DataLoader(MultiPassRandomSampler) + collate
+ * (utils/dataloaders.py:20-77, rollout_collector.py:657-682) + PPOAgent.losses_for_batch
+ * (agents/ppo/ppo_agent.py:21-152) + BaseAgent._backpropagate_and_step
+ * (agents/base_agent.py:591-621: backward, clip_grad_norm_, Adam.step).
+ */
+typedef struct gs_ppo_hparams {
+    float clip_range;
+    float clip_range_vf;
+    float vf_coef;
+    float ent_coef;
+    float max_grad_norm;      /* <= 0: no clipping */
+    float lr;
+    float adam_beta1;
+    float adam_beta2;
+    float adam_eps;
+    float target_kl;          /* <= 0: None */
+    int32_t normalize_adv;    /* 1 = "batch" (utils/torch.py:97-99), 0 = off */
+    int32_t pad;
+} gs_ppo_hparams;
+
+/* Per-minibatch metric record written by the loss kernel (floats, GS_NUM_METRICS each). */
+#define GS_NUM_METRICS 16
+enum gs_metric_slot {
+    GS_M_LOSS = 0, GS_M_POLICY_LOSS, GS_M_VALUE_LOSS, GS_M_ENTROPY, GS_M_CLIP_FRAC,
+    GS_M_CLIP_FRAC_VF, GS_M_EXPLAINED_VAR, GS_M_KL, GS_M_APPROX_KL, GS_M_ADV_NORM_MEAN,
+    GS_M_ADV_NORM_STD, GS_M_KL_STOP, GS_M_GRAD_NORM, GS_M_SKIPPED, GS_M_RES0, GS_M_RES1
+};
+
+size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch);
+
+/* Rollout buffers the update reads (time-major (T, N), see header comment). */
+typedef struct gs_rollout_view {
+    const float *obs;        /* (T, N, D) */
+    const int64_t *actions;  /* (T, N) */
+    const float *logprobs;   /* (T, N) */
+    const float *values;     /* (T, N) */
+    const float *advantages; /* (T, N) */
+    const float *returns;    /* (T, N) */
+    int64_t T;
+    int64_t N;
+} gs_rollout_view;
+
+/* One fused PPO minibatch step on rows idx_dev[0:batch) (env-major sample indices into
+ * the rollout, int32): forward, loss, backward, grad-norm clip and Adam update of
+ * params/adam_m/adam_v in place.  adam_step is the 1-based optimizer step count.
+ * metrics_dev receives GS_NUM_METRICS floats; stop_flag_dev is the sticky KL early-stop
+ * flag (int32, agents/base_agent.py:331-355).  comm may be NULL (single GPU) or a
+ * gs_comm handle: gradients are then all-reduced (mean) across ranks before clipping. */
+struct gs_comm;
+int gs_ppo_minibatch_step(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
+                          gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout,
+                          const int32_t *idx_dev, int64_t batch, int64_t adam_step,
+                          float *metrics_dev, int32_t *stop_flag_dev, void *workspace_dev,
+                          struct gs_comm *comm, void *stream);
+
+/* Forward + loss only (PPOAgent.losses_for_batch without the optimizer step): writes the
+ * GS_NUM_METRICS record (loss, policy/value/entropy terms, clip fractions, KL ...). */
+int gs_ppo_loss(const float *params_dev, gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout,
+                const int32_t *idx_dev, int64_t batch, float *metrics_dev, void *workspace_dev, void *stream);
+
+/* Enqueue ONE stage of a minibatch step on the current workspace (0 = k_fwd_hidden,
+ * 1 = k_loss, 2 = k_bwd, 3 = k_clip_adam).  Used by bench.py to time each kernel
+ * with events on the stream it is launched on (roofline measurement). */
+int gs_ppo_stage(int stage, float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
+                 gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout, const int32_t *idx_dev,
+                 int64_t batch, int64_t adam_step, float *metrics_dev, void *workspace_dev, void *stream);
+
+/* The whole update phase of one rollout: n_minibatches consecutive steps over
+ * idx_dev (n_minibatches * batch indices), metrics_dev gets n_minibatches records.
+ * adam_step0 is the optimizer step count BEFORE the first of these steps.
+ * use_graph != 0 replays the per-pass step sequence from a captured hipGraph. */
+int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
+                  gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout, const int32_t *idx_dev,
+                  int64_t batch, int64_t n_minibatches, int64_t adam_step0, float *metrics_dev,
+                  int32_t *stop_flag_dev, void *workspace_dev, struct gs_comm *comm, int use_graph,
+                  void *stream);
+
+/* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI)
+ * One process per GPU.  Rank 0 creates the 128-byte unique id, the launcher
+ * broadcasts it (torch.distributed), every rank calls gs_comm_init. */
+int gs_comm_unique_id(uint8_t out_id[128]);
+int gs_comm_init(const uint8_t id[128], int nranks, int rank, struct gs_comm **out);
+int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
+int gs_comm_destroy(struct gs_comm *comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSAMD_H */

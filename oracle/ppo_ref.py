@@ -1,0 +1,203 @@
+"""ORACLE — test infrastructure only.
+
+May be imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+as the CHECKER.  The product path (gymnasium-solver_amd/) never imports it.
+
+numpy restatement of the reference's PPO minibatch step with analytic gradients:
+  * MLPActorCritic forward                utils/models.py:285-346 (Linear/ReLU backbone, heads)
+  * Categorical log_prob / entropy        torch.distributions.Categorical
+  * batch advantage normalisation         utils/torch.py:97-99, :148-174
+  * PPO clipped surrogate / value / ent   agents/ppo/ppo_agent.py:21-152
+  * KL diagnostics                        utils/torch.py:102-119
+  * clip_grad_norm_(max_norm=0.5)         agents/base_agent.py:612-617 (Lightning -> torch)
+  * torch.optim.Adam defaults             utils/optimizer_factory.py:6-29
+Gradients follow torch's autograd conventions, including the tie rules of
+torch.min / torch.max (a tie splits the gradient in halves) and clamp's inclusive
+pass-through.  Pinned by tests/golden/ppo_step.npz (the reference's own loss/grads).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+F32 = np.float32
+
+
+def param_shapes(dims):
+    """dims = (D, H1, ..., Hk, A) -> list of (name, shape) in reference parameter order."""
+    D, *H, A = dims
+    shapes, last = [], D
+    for i, h in enumerate(H):
+        shapes.append((f"backbone.{2 * i}.weight", (h, last)))
+        shapes.append((f"backbone.{2 * i}.bias", (h,)))
+        last = h
+    shapes += [("policy_head.weight", (A, last)), ("policy_head.bias", (A,)),
+               ("value_head.weight", (1, last)), ("value_head.bias", (1,))]
+    return shapes
+
+
+def unflatten(flat, dims):
+    out, o = {}, 0
+    for name, shp in param_shapes(dims):
+        n = int(np.prod(shp))
+        out[name] = np.asarray(flat[o:o + n], F32).reshape(shp)
+        o += n
+    return out
+
+
+def flatten(d, dims):
+    return np.concatenate([np.asarray(d[n], F32).reshape(-1) for n, _ in param_shapes(dims)])
+
+
+def forward(flat, dims, obs):
+    P = unflatten(flat, dims)
+    nh = len(dims) - 2
+    x = np.asarray(obs, F32)
+    acts = [x]
+    for i in range(nh):
+        x = np.maximum(x @ P[f"backbone.{2 * i}.weight"].T + P[f"backbone.{2 * i}.bias"], F32(0))
+        acts.append(x)
+    logits = x @ P["policy_head.weight"].T + P["policy_head.bias"]
+    value = (x @ P["value_head.weight"].T + P["value_head.bias"])[:, 0]
+    return logits.astype(F32), value.astype(F32), acts
+
+
+def log_softmax(logits):
+    m = logits.max(axis=1, keepdims=True)
+    z = logits - m
+    lse = np.log(np.exp(z).sum(axis=1, keepdims=True))
+    return (z - lse).astype(F32)
+
+
+def _min_grads(a, b):
+    """d min(a,b)/da, d/db with torch's tie rule (halves)."""
+    ga = np.where(a < b, 1.0, np.where(a == b, 0.5, 0.0))
+    gb = np.where(b < a, 1.0, np.where(a == b, 0.5, 0.0))
+    return ga.astype(F32), gb.astype(F32)
+
+
+def _max_grads(a, b):
+    ga = np.where(a > b, 1.0, np.where(a == b, 0.5, 0.0))
+    gb = np.where(b > a, 1.0, np.where(a == b, 0.5, 0.0))
+    return ga.astype(F32), gb.astype(F32)
+
+
+def ppo_loss_and_grads(flat, dims, obs, actions, old_logp, old_values, adv, ret, *, clip, clip_vf,
+                       vf_coef, ent_coef, normalize="batch"):
+    """Return (loss, metrics, flat_grads) of PPOAgent.losses_for_batch + backward."""
+    B = obs.shape[0]
+    P = unflatten(flat, dims)
+    nh = len(dims) - 2
+    logits, value, acts = forward(flat, dims, obs)
+    adv = np.asarray(adv, F32)
+    metrics = {}
+    if normalize == "batch":
+        mu = adv.mean(dtype=np.float64)
+        sd = adv.std(ddof=1, dtype=np.float64)
+        adv_n = ((adv - F32(mu)) / (F32(sd) + F32(1e-8))).astype(F32)
+        metrics["roll/adv/norm/mean"] = float(adv_n.mean(dtype=np.float64))
+        metrics["roll/adv/norm/std"] = float(adv_n.std(ddof=1, dtype=np.float64))
+    else:
+        adv_n = adv
+    ln = log_softmax(logits)
+    p = np.exp(ln).astype(F32)
+    a = np.asarray(actions, np.int64)
+    new_lp = ln[np.arange(B), a]
+    ratio = np.exp(new_lp - old_logp).astype(F32)
+    rc = np.clip(ratio, F32(1 - clip), F32(1 + clip))
+    s1, s2 = adv_n * ratio, adv_n * rc
+    pl = -np.minimum(s1, s2).mean(dtype=np.float64)
+    vdelta = value - old_values
+    vu = (value - ret) ** 2
+    vcl = old_values + np.clip(vdelta, -clip_vf, clip_vf)
+    vc = (vcl - ret) ** 2
+    vl = np.maximum(vu, vc).mean(dtype=np.float64)
+    H = -(p * ln).sum(axis=1)
+    ent = H.mean(dtype=np.float64)
+    loss = pl + vf_coef * vl - ent_coef * ent
+
+    # --- backward (mean over B) ---
+    g1, g2 = _min_grads(s1, s2)
+    in_clip = ((ratio >= F32(1 - clip)) & (ratio <= F32(1 + clip))).astype(F32)
+    dratio = -(adv_n * g1 + adv_n * g2 * in_clip) / B
+    dlp = dratio * ratio
+    onehot = np.zeros_like(p)
+    onehot[np.arange(B), a] = 1.0
+    dlogits = dlp[:, None] * (onehot - p)
+    # entropy term: loss += -ent_coef * mean(H); dH/dl_b = -p_b (ln_b + H)
+    dlogits += (-ent_coef / B) * (-p * (ln + H[:, None]))
+    h1, h2 = _max_grads(vu, vc)
+    vin = ((vdelta >= -clip_vf) & (vdelta <= clip_vf)).astype(F32)
+    dvalue = vf_coef / B * (h1 * 2 * (value - ret) + h2 * 2 * (vcl - ret) * vin)
+
+    G = {}
+    x = acts[-1]
+    G["policy_head.weight"] = dlogits.T @ x
+    G["policy_head.bias"] = dlogits.sum(0)
+    G["value_head.weight"] = (dvalue[:, None] * x).sum(0)[None, :]
+    G["value_head.bias"] = np.array([dvalue.sum()], F32)
+    dx = dlogits @ P["policy_head.weight"] + dvalue[:, None] * P["value_head.weight"]
+    for i in reversed(range(nh)):
+        dx = dx * (acts[i + 1] > 0)
+        G[f"backbone.{2 * i}.weight"] = dx.T @ acts[i]
+        G[f"backbone.{2 * i}.bias"] = dx.sum(0)
+        if i > 0:
+            dx = dx @ P[f"backbone.{2 * i}.weight"]
+
+    with np.errstate(over="ignore"):
+        clipfrac = ((ratio < 1 - clip) | (ratio > 1 + clip)).mean()
+        clipfrac_vf = ((vdelta < -clip_vf) | (vdelta > clip_vf)).mean()
+        ev = 1 - np.var(ret - value, ddof=1) / np.var(ret, ddof=1)
+        diff = np.clip(new_lp - old_logp, -20.0, 20.0)
+        r2 = np.exp(diff)
+        approx_kl = ((r2 - 1) - np.log(r2)).mean()
+    metrics.update({
+        "opt/loss/total": float(loss), "opt/loss/policy": float(pl), "opt/loss/entropy": float(-ent),
+        "opt/policy/entropy": float(ent), "opt/loss/entropy_scaled": float(-ent_coef * ent),
+        "opt/loss/value": float(vl), "opt/loss/value_scaled": float(vf_coef * vl),
+        "opt/ppo/clip_fraction": float(clipfrac), "opt/ppo/clip_fraction_vf": float(clipfrac_vf),
+        "opt/value/explained_var": float(ev), "opt/ppo/kl": float((old_logp - new_lp).mean()),
+        "opt/ppo/approx_kl": float(approx_kl), "opt/ppo/kl_stop_triggered": 0.0,
+    })
+    return float(loss), metrics, flatten(G, dims)
+
+
+def clip_grad_norm(flat_grads, dims, max_norm):
+    """torch.nn.utils.clip_grad_norm_: norm of per-parameter norms, coef clamped to 1."""
+    P = unflatten(flat_grads, dims)
+    norms = [np.linalg.norm(P[n].astype(np.float64)) for n, _ in param_shapes(dims)]
+    total = float(np.linalg.norm(norms))
+    coef = min(1.0, max_norm / (total + 1e-6))
+    return (flat_grads * F32(coef)).astype(F32), total
+
+
+def adam_step(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
+    """torch.optim.Adam single-tensor step (defaults, no weight decay); t is 1-based."""
+    m = (b1 * m + (1 - b1) * g).astype(F32)
+    v = (b2 * v + (1 - b2) * g * g).astype(F32)
+    bc1 = 1 - b1 ** t
+    bc2 = 1 - b2 ** t
+    denom = np.sqrt(v) / np.sqrt(bc2) + eps
+    p = (p - (lr / bc1) * m / denom).astype(F32)
+    return p, m, v
+
+
+def gae_numpy(values, rewards, dones, timeouts, last_values, bootstrap, gamma, lam):
+    """numpy restatement of returns_advantages.py:115-155 (same op order)."""
+    values = np.asarray(values, F32)
+    T, N = values.shape
+    nv = np.empty_like(values)
+    nv[:-1] = values[1:]
+    nv[-1] = last_values
+    dones = np.asarray(dones, bool)
+    timeouts = np.asarray(timeouts, bool)
+    if bootstrap is not None:
+        nv = np.where(timeouts, np.asarray(bootstrap, F32), nv)
+    nt = (~(dones & ~timeouts)).astype(F32)
+    c1, c2 = F32(gamma), F32(gamma * lam)
+    adv = np.zeros_like(values)
+    gae = np.zeros(N, F32)
+    for t in range(T - 1, -1, -1):
+        delta = rewards[t] + (c1 * nv[t]) * nt[t] - values[t]
+        gae = delta + (c2 * gae) * nt[t]
+        adv[t] = gae
+    return adv, adv + values

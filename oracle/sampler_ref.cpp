@@ -1,0 +1,63 @@
+// ORACLE — test infrastructure only (see oracle/README.md): the checker for the
+// product sampler, never linked into gymnasium-solver_amd/.
+//
+// Restatement of the reference's MultiPassRandomSampler index stream
+//   /root/reference/utils/samplers.py:25-34
+//     set_epoch(e): generator.manual_seed(base_seed + e)          (:25-27)
+//     scores = torch.rand((num_passes, data_len), generator)      (:31)
+//     order  = torch.argsort(scores, dim=1).reshape(-1)           (:32)
+// torch's CPU generator is MT19937 seeded with the standard init_genrand recurrence;
+// torch.rand(float32) maps each 32-bit draw x to (x & 0xFFFFFF) * 2^-24 in row-major
+// order; CPU argsort (unstable) is libstdc++ introsort over (key, index) pairs compared
+// on the key only.  All three facts are pinned by tests/golden/sampler.npz, which
+// holds the reference's own streams.
+#include <algorithm>
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+namespace {
+struct MT19937 {
+    uint32_t mt[624];
+    int idx;
+    explicit MT19937(uint64_t seed) {
+        mt[0] = static_cast<uint32_t>(seed);
+        for (int i = 1; i < 624; ++i)
+            mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + static_cast<uint32_t>(i);
+        idx = 624;
+    }
+    uint32_t next() {
+        if (idx >= 624) {
+            for (int i = 0; i < 624; ++i) {
+                uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+                uint32_t v = mt[(i + 397) % 624] ^ (y >> 1);
+                if (y & 1u) v ^= 0x9908b0dfu;
+                mt[i] = v;
+            }
+            idx = 0;
+        }
+        uint32_t y = mt[idx++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
+};
+}  // namespace
+
+extern "C" void oracle_sampler_stream(int64_t data_len, int64_t num_passes, uint64_t seed, int64_t *out)
+{
+    MT19937 g(seed);
+    std::vector<std::pair<float, int64_t>> row(static_cast<size_t>(data_len));
+    std::vector<float> keys(static_cast<size_t>(data_len * num_passes));
+    for (auto &k : keys) k = static_cast<float>(g.next() & 0xFFFFFFu) * (1.0f / 16777216.0f);
+    for (int64_t p = 0; p < num_passes; ++p) {
+        for (int64_t i = 0; i < data_len; ++i) row[i] = {keys[p * data_len + i], i};
+        std::sort(row.begin(), row.end(),
+                  [](const std::pair<float, int64_t> &a, const std::pair<float, int64_t> &b) {
+                      return a.first < b.first;
+                  });
+        for (int64_t i = 0; i < data_len; ++i) out[p * data_len + i] = row[i].second;
+    }
+}

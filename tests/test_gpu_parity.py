@@ -1,0 +1,261 @@
+"""Parity of the HIP path (through the C-ABI) with the reference's golden vectors and the oracle.
+
+Tolerances (BASELINE.json north_star): GAE and sampler indices bit-exact; advantages /
+returns / log-probs / values within 1e-5 fp32; PPO loss trajectory within 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, cuda, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(cuda).contiguous()
+
+
+# ------------------------------------------------------------------------------- GAE
+def test_gae_bit_exact_vs_reference_fixtures(golden, cuda):
+    from gsamd.rollout import compute_batched_gae_advantages_and_returns as gae
+    g = golden("gae.npz")
+    names = sorted({k.split("/")[0] for k in g.files})
+    assert len(names) >= 10
+    for n in names:
+        c = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(n + "/")}
+        boot = None if "no_boot" in c else _dev(c["bootstrap"], cuda)
+        adv, ret = gae(_dev(c["values"], cuda), _dev(c["rewards"], cuda), _dev(c["dones"], cuda),
+                       _dev(c["timeouts"], cuda), _dev(c["last_values"], cuda), boot, float(c["gamma"]),
+                       float(c["lam"]))
+        torch.cuda.synchronize()
+        assert np.array_equal(adv.cpu().numpy().view(np.uint32), c["adv"].view(np.uint32)), n
+        assert np.array_equal(ret.cpu().numpy().view(np.uint32), c["ret"].view(np.uint32)), n
+
+
+@pytest.mark.parametrize("T,N", [(32, 4096), (2048, 1024), (7, 3000), (1, 1)])
+def test_gae_bit_exact_vs_c_oracle_full_size(cuda, T, N):
+    import oracle
+    from gsamd.rollout import compute_batched_gae_advantages_and_returns as gae
+    rng = np.random.default_rng(T * 7 + N)
+    v = rng.standard_normal((T, N)).astype(np.float32)
+    r = rng.standard_normal((T, N)).astype(np.float32)
+    d = (rng.random((T, N)) < 0.05).astype(np.uint8)
+    to = (d.astype(bool) & (rng.random((T, N)) < 0.3)).astype(np.uint8)
+    lv = rng.standard_normal(N).astype(np.float32)
+    b = rng.standard_normal((T, N)).astype(np.float32)
+    a_ref, r_ref = oracle.gae_c(v, r, d, to, lv, b, 0.99, 0.95)
+    adv, ret = gae(_dev(v, cuda), _dev(r, cuda), _dev(d, cuda), _dev(to, cuda), _dev(lv, cuda), _dev(b, cuda),
+                   0.99, 0.95)
+    assert np.array_equal(adv.cpu().numpy().view(np.uint32), a_ref.view(np.uint32))
+    assert np.array_equal(ret.cpu().numpy().view(np.uint32), r_ref.view(np.uint32))
+
+
+def test_gae_empty_is_noop(cuda):
+    from gsamd._lib import check, lib
+    check(lib.gs_gae_f32(None, None, None, None, None, None, 0, 5, 0.99, 0.95, None, None, None))
+
+
+# ------------------------------------------------------------------------------- policy forward
+def test_policy_forward_vs_reference(golden, cuda):
+    from gsamd.policy import DeviceMLPActorCritic
+    z = golden("policy_fwd.npz")
+    pm = DeviceMLPActorCritic(4, (256, 256), 2, device=cuda, init=False)
+    pm.load_flat(z["params"])
+    obs = _dev(z["obs"], cuda)
+    acts = _dev(z["actions"], cuda, torch.int64)
+    a, lp, v = pm.act(obs, mode=2, actions=acts.clone())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(v.cpu().numpy(), z["values"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(lp.cpu().numpy(), z["logp"], atol=1e-5, rtol=0)
+    a_det, lp_det, _ = pm.act(obs, mode=1)
+    probs = z["probs"]
+    np.testing.assert_array_equal(a_det.cpu().numpy(), probs.argmax(axis=1))
+    vv = pm.predict_values(obs)
+    np.testing.assert_allclose(vv.cpu().numpy(), z["values"], atol=1e-5, rtol=0)
+
+
+def test_policy_sampling_follows_probs(cuda):
+    from gsamd.policy import DeviceMLPActorCritic
+    torch.manual_seed(3)
+    pm = DeviceMLPActorCritic(8, (128, 128), 4, device=cuda)
+    obs = torch.rand(1, 8, device=cuda).repeat(8192, 1).contiguous()
+    counts = np.zeros(4)
+    for k in range(8):
+        a, lp, _ = pm.act(obs, mode=0, rng_seed=42, rng_counter=k)
+        counts += np.bincount(a.cpu().numpy(), minlength=4)
+    # probabilities of the single repeated row from the replay path
+    probs = np.zeros(4)
+    for act in range(4):
+        _, lpa, _ = pm.act(obs[:1].contiguous(), mode=2, actions=torch.tensor([act], device=cuda))
+        probs[act] = float(np.exp(lpa.cpu().numpy()[0]))
+    freq = counts / counts.sum()
+    assert np.abs(freq - probs).max() < 0.01, (freq, probs)
+
+
+# ------------------------------------------------------------------------------- synthetic env
+def test_device_env_matches_host_env(cuda):
+    from gsamd.rollout import DeviceSyntheticVecEnv
+    from gsamd.synthetic_env import SyntheticVecEnv
+    host = SyntheticVecEnv(n_envs=37, obs_dim=5, n_actions=2, episode_len=7, seed=42, truncate_every=2, env_offset=11)
+    dev = DeviceSyntheticVecEnv(n_envs=37, obs_dim=5, n_actions=2, episode_len=7, seed=42, truncate_every=2,
+                                env_offset=11, device=cuda)
+    o_h, _ = host.reset()
+    o_d, _ = dev.reset()
+    assert np.array_equal(o_d.cpu().numpy(), o_h)
+    rew = torch.zeros(37, device=cuda)
+    dn = torch.zeros(37, dtype=torch.uint8, device=cuda)
+    to = torch.zeros(37, dtype=torch.uint8, device=cuda)
+    for _ in range(20):
+        o_h, r_h, te, tr, _ = host.step(np.zeros(37, np.int64))
+        dev.step_into(rew, dn, to)
+        assert np.array_equal(dev.obs.cpu().numpy(), o_h)
+        assert np.array_equal(rew.cpu().numpy(), r_h)
+        assert np.array_equal(dn.cpu().numpy().astype(bool), te | tr)
+        assert np.array_equal(to.cpu().numpy().astype(bool), tr)
+
+
+# ------------------------------------------------------------------------------- one PPO step
+def _rollout_view_from_batch(z, tag, cuda):
+    from gsamd._lib import RolloutView
+    B = int(z[f"{tag}/dims"][-1])
+    t = dict(obs=_dev(z[f"{tag}/obs"][None], cuda), actions=_dev(z[f"{tag}/actions"][None], cuda, torch.int64),
+             logprobs=_dev(z[f"{tag}/old_logprobs"][None], cuda), values=_dev(z[f"{tag}/old_values"][None], cuda),
+             advantages=_dev(z[f"{tag}/advantages"][None], cuda), returns=_dev(z[f"{tag}/returns"][None], cuda))
+    view = RolloutView(t["obs"].data_ptr(), t["actions"].data_ptr(), t["logprobs"].data_ptr(),
+                       t["values"].data_ptr(), t["advantages"].data_ptr(), t["returns"].data_ptr(), 1, B)
+    return t, view
+
+
+@pytest.mark.parametrize("tag", ["cartpole", "lunar_ent"])
+def test_ppo_step_vs_reference(golden, cuda, tag):
+    from gsamd._lib import GS_NUM_METRICS, M, MlpDims, PPOHparams, check, lib
+    z = golden("ppo_step.npz")
+    D, H1, H2, A, B = (int(x) for x in z[f"{tag}/dims"])
+    clip, cvf, vf, ent, lr = (float(x) for x in z[f"{tag}/hparams"])
+    dims = MlpDims(D, H1, H2, A)
+    keep, view = _rollout_view_from_batch(z, tag, cuda)
+    P = int(lib.gs_mlp_param_count(dims))
+    params = _dev(z[f"{tag}/params0"], cuda)
+    assert params.numel() == P
+    grads = torch.zeros(P, device=cuda)
+    m = torch.zeros(P, device=cuda)
+    v = torch.zeros(P, device=cuda)
+    ws = torch.zeros(int(lib.gs_ppo_workspace_bytes(dims, B)), dtype=torch.uint8, device=cuda)
+    idx = torch.arange(B, dtype=torch.int32, device=cuda)
+    met = torch.zeros(GS_NUM_METRICS, device=cuda)
+    stop = torch.zeros(1, dtype=torch.int32, device=cuda)
+    hp = PPOHparams(clip, cvf, vf, ent, 0.5, lr, 0.9, 0.999, 1e-8, 0.0, 1, 0)
+    s = torch.cuda.current_stream().cuda_stream
+    check(lib.gs_ppo_loss(params.data_ptr(), dims, hp, view, idx.data_ptr(), B, met.data_ptr(), ws.data_ptr(), s))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(float(met[M["loss"]]), float(z[f"{tag}/loss"]), atol=1e-6, rtol=1e-6)
+    names = [str(x) for x in z[f"{tag}/metric_names"]]
+    ref = dict(zip(names, z[f"{tag}/metric_values"]))
+    mm = met.cpu().numpy()
+    for key, slot in [("opt/loss/policy", "policy_loss"), ("opt/loss/value", "value_loss"),
+                      ("opt/policy/entropy", "entropy"), ("opt/ppo/clip_fraction", "clip_fraction"),
+                      ("opt/ppo/clip_fraction_vf", "clip_fraction_vf"), ("opt/value/explained_var", "explained_var"),
+                      ("opt/ppo/kl", "kl"), ("opt/ppo/approx_kl", "approx_kl"),
+                      ("roll/adv/norm/std", "adv_norm_std")]:
+        np.testing.assert_allclose(mm[M[slot]], ref[key], atol=2e-6, rtol=1e-5, err_msg=key)
+    check(lib.gs_ppo_minibatch_step(params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), dims, hp, view,
+                                    idx.data_ptr(), B, 1, met.data_ptr(), stop.data_ptr(), ws.data_ptr(), None, s))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(float(met[M["grad_norm"]]), float(z[f"{tag}/total_norm"]), rtol=1e-5)
+    g_ref = z[f"{tag}/grads_clipped"]
+    np.testing.assert_allclose(grads.cpu().numpy(), g_ref, atol=2e-6 * max(1.0, np.abs(g_ref).max()), rtol=0)
+    np.testing.assert_allclose(params.cpu().numpy(), z[f"{tag}/params1"], atol=2e-6, rtol=0)
+    del keep
+
+
+# ------------------------------------------------------------------------------- full trajectory
+def test_trajectory_replay_vs_reference(golden, cuda):
+    """3 CartPole-shaped rollouts (N=8, T=32, B=256, E=20) replaying the reference's
+    sampled actions: rollout tensors, sampler order, all 60 minibatch losses, final weights."""
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    z = golden("trajectory.npz")
+    N, T, E, B, D, A = (int(x) for x in z["dims"])
+    L, seed, trunc = (int(x) for x in z["env"])
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(episode_len=L, truncate_every=trunc, obs_dim=D,
+                                                           n_actions=A))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False)
+    np.testing.assert_array_equal(agent.policy_model.params.cpu().numpy(), z["params0"])
+    coll = agent.get_rollout_collector("train")
+    losses = []
+    for ep in range(3):
+        acts = _dev(z["actions"][ep].reshape(N, T).T, cuda, torch.int64)
+        traj = coll.collect(replay_actions=acts)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(traj.observations.cpu().numpy(), z["obs"][ep])
+        np.testing.assert_allclose(traj.logprobs.cpu().numpy(), z["logp"][ep], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(traj.values.cpu().numpy(), z["values"][ep], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(traj.advantages.cpu().numpy(), z["adv"][ep], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(traj.returns.cpu().numpy(), z["ret"][ep], atol=1e-5, rtol=0)
+        np.testing.assert_array_equal(traj.rewards.cpu().numpy(), z["rewards"][ep])
+        np.testing.assert_array_equal(traj.dones.cpu().numpy().astype(np.uint8), z["dones"][ep])
+        idx = agent.prefetcher.upload(ep)
+        np.testing.assert_array_equal(idx.cpu().numpy(), z["order"][ep])
+        from gsamd._lib import check, lib
+        check(lib.gs_ppo_update(agent.policy_model.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                                agent.adam_v.data_ptr(), agent.policy_model.dims, agent.hparams(), coll.buffer.view(),
+                                idx.data_ptr(), B, agent.n_minibatches, agent.adam_step, agent.metrics_buf.data_ptr(),
+                                agent.stop_flag.data_ptr(), agent.workspace.data_ptr(), None, 0,
+                                torch.cuda.current_stream().cuda_stream))
+        agent.adam_step += agent.n_minibatches
+        losses.append(agent.minibatch_losses())
+    losses = np.concatenate(losses)
+    assert losses.shape == z["losses"].shape
+    np.testing.assert_allclose(losses, z["losses"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(agent.policy_model.params.cpu().numpy(), z["params_final"], atol=1e-4, rtol=0)
+
+
+# ------------------------------------------------------------------------------- full-size properties
+def test_c2_update_graph_equals_eager_and_is_deterministic(cuda):
+    """BASELINE config C2 shape: graph replay == eager launches, bitwise, and a rerun is identical."""
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    results = []
+    for use_graph in (False, True, True):
+        torch.manual_seed(42)
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+        agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
+        agent.train_epoch()
+        agent.train_epoch()
+        torch.cuda.synchronize()
+        results.append((agent.policy_model.params.cpu().numpy(), agent.minibatch_losses()))
+        assert np.isfinite(results[-1][1]).all()
+    for p, l in results[1:]:
+        assert np.array_equal(p.view(np.uint32), results[0][0].view(np.uint32))
+        assert np.array_equal(l, results[0][1])
+
+
+def test_c2_minibatch_step_vs_numpy_oracle(cuda):
+    """One C2-shaped minibatch (B=256 rows of a 4096x32 device rollout) against the numpy oracle."""
+    from oracle import ppo_ref as R
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
+    traj = agent.get_rollout_collector("train").collect()
+    batches = agent._epoch_batches(0)
+    p0 = agent.policy_model.params.cpu().numpy()
+    b = batches[5]
+    idx = b.idx.cpu().numpy().astype(np.int64)
+    obs = traj.observations.cpu().numpy()[idx]
+    args = [traj.actions.cpu().numpy()[idx], traj.logprobs.cpu().numpy()[idx], traj.values.cpu().numpy()[idx],
+            traj.advantages.cpu().numpy()[idx], traj.returns.cpu().numpy()[idx]]
+    dims = (4, 256, 256, 2)
+    loss, met, g = R.ppo_loss_and_grads(p0, dims, obs, *args, clip=0.1, clip_vf=0.2, vf_coef=0.5, ent_coef=0.0)
+    gc, total = R.clip_grad_norm(g, dims, 0.5)
+    p1, _, _ = R.adam_step(p0, gc, np.zeros_like(gc), np.zeros_like(gc), 1, 1e-3)
+    agent.training_step(b, 0)
+    torch.cuda.synchronize()
+    rec = agent.metrics_buf[0].cpu().numpy()
+    np.testing.assert_allclose(rec[0], loss, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(agent.grads.cpu().numpy(), gc, atol=1e-6 * max(1, np.abs(gc).max()), rtol=0)
+    np.testing.assert_allclose(agent.policy_model.params.cpu().numpy(), p1, atol=5e-6, rtol=0)

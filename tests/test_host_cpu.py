@@ -1,0 +1,151 @@
+"""CPU: host logic of the product path — library load/exports, sampler, config, env, init."""
+import os
+import re
+import hashlib
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "gsamd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from gsamd import _lib
+    names = _declared_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(_lib.lib, n), f"libgsamd.so does not export {n}"
+    assert set(names) == set(_lib.EXPORTED)
+    assert _lib.lib.gs_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    lib = os.path.join(ROOT, "gymnasium-solver_amd", "gsamd", "libgsamd.so")
+    blob = open(lib, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"sm_" + b"90" not in blob
+
+
+def test_invalid_arguments_raise_value_error():
+    from gsamd._lib import check, lib
+    with pytest.raises(ValueError):
+        check(lib.gs_sampler_stream_i32(0, 1, 42, None, 1), "sampler")
+    with pytest.raises(ValueError):
+        check(lib.gs_gae_f32(None, None, None, None, None, None, -1, 4, 0.9, 0.9, None, None, None), "gae")
+
+
+def test_product_sampler_bit_exact(golden):
+    from gsamd.samplers import MultiPassRandomSampler, index_stream
+    s = golden("sampler.npz")
+    for ep in range(4):
+        assert np.array_equal(index_stream(256, 20, 42 + ep), s[f"n256_p20_e{ep}"])
+    c2 = index_stream(131072, 20, 42).astype(np.int64)
+    assert hashlib.sha256(c2.tobytes()).digest() == bytes(s["n131072_p20_e0/sha256"])
+    assert np.array_equal(c2[-4096:], s["n131072_p20_e0/tail"])
+    import torch
+    torch.manual_seed(42)
+    smp = MultiPassRandomSampler(256, 20)
+    smp.set_epoch(2)
+    assert list(iter(smp)) == s["n256_p20_e2"].tolist()
+
+
+def test_sampler_api_matches_reference_tests():
+    # reference tests/test_multipass_random_sampler.py
+    import torch
+    from gsamd.samplers import MultiPassRandomSampler
+    with pytest.raises(ValueError):
+        MultiPassRandomSampler(data_len=0, num_passes=1)
+    with pytest.raises(ValueError):
+        MultiPassRandomSampler(data_len=5, num_passes=0)
+    smp = MultiPassRandomSampler(10, 4, generator=torch.Generator().manual_seed(42))
+    order = list(iter(smp))
+    assert len(order) == len(smp) == 40
+    for p in range(4):
+        assert sorted(order[p * 10:(p + 1) * 10]) == list(range(10))
+    smp = MultiPassRandomSampler(1, 5, generator=torch.Generator().manual_seed(999))
+    assert list(iter(smp)) == [0] * 5
+    smp = MultiPassRandomSampler(7, 2)
+    smp.set_epoch(0)
+    a = list(iter(smp))
+    smp.set_epoch(0)
+    assert list(iter(smp)) == a
+    smp.set_epoch(1)
+    assert list(iter(smp)) != a
+
+
+def test_config_presets_match_reference_resolution(golden):
+    import json
+    from gsamd.config import load_config
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+    for key, r in ref.items():
+        env, var = key.split(":")
+        c = load_config(env, var)
+        for f in ("n_envs", "n_steps", "batch_size", "n_epochs", "gamma", "gae_lambda", "clip_range",
+                  "clip_range_vf", "ent_coef", "vf_coef", "policy_lr", "max_grad_norm", "model_id", "seed",
+                  "normalize_advantages", "target_kl"):
+            assert getattr(c, f) == r[f], (key, f)
+        assert list(c.hidden_dims) == r["hidden_dims"]
+        assert c.valid_actions == r["valid_actions"]
+        assert c.resolved_n_actions() == r["n_actions"]
+
+
+def test_config_aliases_and_overrides():
+    from gsamd.config import canonical_id, load_config
+    assert canonical_id("LunarLander-v2", "ppo") == ("LunarLander-v3", "ppo")
+    assert canonical_id("ALE/Pong-v5:ppo", None) == ("ALE-Pong-v5", "rgb_ppo")
+    c = load_config("CartPole-v1:ppo", overrides={"n_envs": "4096"})
+    assert c.n_envs == 4096 and c.batch_size == 256
+    with pytest.raises(ValueError):
+        load_config("CartPole-v1", "ppo", overrides={"batch_size": 100})
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/config/environments"), reason="reference tree absent")
+def test_yaml_drop_in_mode_matches_presets():
+    from gsamd.config import load_config
+    for env, var in [("CartPole-v1", "ppo"), ("LunarLander-v3", "ppo")]:
+        a = load_config(env, var, config_dir="/root/reference/config/environments")
+        b = load_config(env, var)
+        for f in ("n_envs", "n_steps", "batch_size", "n_epochs", "gamma", "gae_lambda", "clip_range", "policy_lr",
+                  "model_id", "max_env_steps"):
+            assert getattr(a, f) == getattr(b, f), f
+
+
+def test_synthetic_env_fixture(golden):
+    from gsamd.synthetic_env import SyntheticVecEnv, synth_obs
+    z = golden("synth_env.npz")
+    env = SyntheticVecEnv(n_envs=6, obs_dim=4, n_actions=2, episode_len=5, seed=42, truncate_every=2)
+    o, _ = env.reset()
+    rows = [o]
+    for _ in range(12):
+        o, r, te, tr, _ = env.step(np.zeros(6, np.int64))
+        rows.append(o)
+    assert np.array_equal(np.asarray(rows), z["obs"])
+    probe = synth_obs(42, np.arange(3, dtype=np.uint64)[:, None], np.uint64(77), np.arange(8, dtype=np.uint64)[None, :])
+    assert np.array_equal(probe, z["probe"])
+    assert probe.min() >= -1.0 and probe.max() < 1.0
+
+
+def test_reference_init_reproduces_reference_weights(golden):
+    import torch
+    from gsamd.policy import reference_init
+    z = golden("trajectory.npz")
+    torch.manual_seed(42)
+    sd = reference_init(4, (256, 256), 2)
+    flat = torch.cat([t.reshape(-1) for t in sd.values()]).numpy()
+    assert np.array_equal(flat, z["params0"])
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "gymnasium-solver_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                src = open(os.path.join(dp, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle\b", src, re.M), f
+                assert "liboracle" not in src, f

@@ -1,0 +1,84 @@
+"""CPU: the oracle (oracle/) pinned against the reference's own outputs (tests/golden/)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import ppo_ref as R
+
+
+def _cases(g):
+    names = sorted({k.split("/")[0] for k in g.files})
+    for n in names:
+        yield n, {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(n + "/")}
+
+
+def test_gae_c_oracle_bit_exact(golden):
+    g = golden("gae.npz")
+    n = 0
+    for name, c in _cases(g):
+        boot = None if "no_boot" in c else c["bootstrap"]
+        a, r = oracle.gae_c(c["values"], c["rewards"], c["dones"], c["timeouts"], c["last_values"], boot,
+                            float(c["gamma"]), float(c["lam"]))
+        assert np.array_equal(a.view(np.uint32), c["adv"].view(np.uint32)), name
+        assert np.array_equal(r.view(np.uint32), c["ret"].view(np.uint32)), name
+        n += 1
+    assert n == 11
+
+
+def test_gae_numpy_oracle_bit_exact(golden):
+    for name, c in _cases(golden("gae.npz")):
+        boot = None if "no_boot" in c else c["bootstrap"]
+        a, r = R.gae_numpy(c["values"], c["rewards"], c["dones"], c["timeouts"], c["last_values"], boot,
+                           float(c["gamma"]), float(c["lam"]))
+        assert np.array_equal(a.view(np.uint32), c["adv"].view(np.uint32)), name
+
+
+def test_gae_constants_follow_numpy_weak_scalars():
+    # c2 = f32(gamma*lambda in double), not f32(gamma)*f32(lambda) (SURVEY.md §7 hard part c)
+    assert np.float32(0.98 * 0.8) != np.float32(0.98) * np.float32(0.8)
+
+
+def test_sampler_oracle_bit_exact(golden):
+    s = golden("sampler.npz")
+    for ep in range(4):
+        assert np.array_equal(oracle.sampler_stream(256, 20, 42 + ep), s[f"n256_p20_e{ep}"])
+    assert np.array_equal(oracle.sampler_stream(7, 2, 42), s["n7_p2_e0"])
+    assert np.array_equal(oracle.sampler_stream(1, 5, 42), s["n1_p5_e0"])
+    big = oracle.sampler_stream(131072, 2, 42)
+    assert np.array_equal(big[:4096], s["n131072_p2_e0/head"])
+    assert hashlib.sha256(big.tobytes()).digest() == bytes(s["n131072_p2_e0/sha256"])
+
+
+@pytest.mark.parametrize("tag", ["cartpole", "lunar_ent"])
+def test_ppo_numpy_oracle_vs_reference_step(golden, tag):
+    z = golden("ppo_step.npz")
+    D, H1, H2, A, B = (int(x) for x in z[f"{tag}/dims"])
+    clip, cvf, vf, ent, lr = (float(x) for x in z[f"{tag}/hparams"])
+    dims = (D, H1, H2, A)
+    loss, met, g = R.ppo_loss_and_grads(z[f"{tag}/params0"], dims, z[f"{tag}/obs"], z[f"{tag}/actions"],
+                                        z[f"{tag}/old_logprobs"], z[f"{tag}/old_values"], z[f"{tag}/advantages"],
+                                        z[f"{tag}/returns"], clip=clip, clip_vf=cvf, vf_coef=vf, ent_coef=ent)
+    assert abs(loss - float(z[f"{tag}/loss"])) < 1e-6
+    np.testing.assert_allclose(g, z[f"{tag}/grads_raw"], atol=1e-6, rtol=0)
+    gc, total = R.clip_grad_norm(g, dims, 0.5)
+    assert abs(total - float(z[f"{tag}/total_norm"])) < 1e-6
+    np.testing.assert_allclose(gc, z[f"{tag}/grads_clipped"], atol=1e-6, rtol=0)
+    p1, _, _ = R.adam_step(z[f"{tag}/params0"], gc, np.zeros_like(gc), np.zeros_like(gc), 1, lr)
+    np.testing.assert_allclose(p1, z[f"{tag}/params1"], atol=1e-6, rtol=0)
+    ref = dict(zip([str(x) for x in z[f"{tag}/metric_names"]], z[f"{tag}/metric_values"]))
+    for k, v in ref.items():
+        assert abs(met[k] - v) < 1e-5, k
+
+
+def test_masked_categorical_known_answers():
+    # tests/test_masked_categorical.py of the reference: uniform over 3 valid -> log 3
+    logits = np.zeros((1, 5), np.float32)
+    valid = np.array([True, True, True, False, False])
+    z = np.where(valid, logits, -np.inf)
+    ln = R.log_softmax(z)
+    p = np.exp(ln)
+    H = -(p * np.where(valid, np.log(p + 1e-8), 0)).sum()
+    assert abs(H - np.log(3)) < 1e-5
+    assert abs(ln[0, 0] + np.log(3)) < 1e-6
