@@ -30,16 +30,16 @@ def _obj(src):
     return os.path.join(BUILD, src + ".o")
 
 
-def _compile(src):
+def _compile(src, build_dir=None, defines=()):
     path = os.path.join(CSRC, src)
-    obj = _obj(src)
+    obj = os.path.join(build_dir, src + ".o") if build_dir else _obj(src)
     deps = [path, os.path.join(CSRC, "gs_common.h"), os.path.join(HERE, "..", "include", "gsamd.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return None
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-c", path, "-o", obj]
     if src.endswith(".hip"):
         cmd[1:1] = [f"--offload-arch={ARCH}", "-x", "hip"]
-    cmd += EXTRA.get(src, [])
+    cmd += EXTRA.get(src, []) + [f"-D{d}" for d in defines]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -61,6 +61,22 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     if verbose:
         print(f"built {LIB} ({len(done)} objects recompiled)")
     return LIB
+
+
+def build_variant(out_path: str, defines, jobs: int = 8) -> str:
+    """Diagnostic variant (e.g. GS_STAMPS phase timers) built into its own directory."""
+    bdir = os.path.join(BUILD, "variant_" + "_".join(defines))
+    os.makedirs(bdir, exist_ok=True)
+    srcs = _sources()
+    with ThreadPoolExecutor(max_workers=min(jobs, len(srcs))) as ex:
+        list(ex.map(lambda s: _compile(s, bdir, defines), srcs))
+    objs = [os.path.join(bdir, s + ".o") for s in srcs]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_path] + objs + [
+        "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return out_path
 
 
 if __name__ == "__main__":

@@ -11,6 +11,36 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace gs {
 
+// ---- diagnostic phase stamps (only in a -DGS_STAMPS build; never in the product library)
+#ifdef GS_STAMPS
+extern __device__ unsigned long long g_stamp_acc[8][16];
+extern __device__ unsigned long long g_stamp_cnt[8];
+// timestamps stay in registers; the global atomics happen once, at GS_STAMP_END, so the
+// stamps never add a memory wait to a phase they measure
+#define GS_STAMP_BEGIN_IF(k, cond)                                                 \
+    unsigned long long _st_t[17];                                                  \
+    int _st_n = 0;                                                                 \
+    const bool _st_on = (cond) && threadIdx.x == 0;                                \
+    const int _st_k = (k);                                                         \
+    if (_st_on) _st_t[0] = __builtin_amdgcn_s_memtime();
+#define GS_STAMP_BEGIN(k) GS_STAMP_BEGIN_IF(k, blockIdx.x == 0 && blockIdx.y == 0)
+#define GS_STAMP(i)                                                                \
+    if (_st_on) _st_t[(i) + 1] = __builtin_amdgcn_s_memtime();                     \
+    _st_n = (i) + 1;
+#define GS_STAMP_END(i)                                                            \
+    GS_STAMP(i)                                                                    \
+    if (_st_on) {                                                                  \
+        for (int _j = 0; _j < _st_n; ++_j)                                         \
+            atomicAdd(&g_stamp_acc[_st_k][_j], _st_t[_j + 1] - _st_t[_j]);         \
+        atomicAdd(&g_stamp_cnt[_st_k], 1ull);                                      \
+    }
+#else
+#define GS_STAMP_BEGIN(k)
+#define GS_STAMP_BEGIN_IF(k, cond)
+#define GS_STAMP(i)
+#define GS_STAMP_END(i)
+#endif
+
 // ---- error plumbing (thread-local last error, like cudaGetLastError but with text)
 void set_error(const char *fmt, ...);
 int hip_fail(hipError_t e, const char *what, const char *file, int line);
@@ -39,8 +69,8 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line);
 struct Layout {
     int D, H1, H2, A;
     int64_t oW1, ob1, oW2, ob2, oWp, obp, oWv, obv, P;
-    __host__ __device__ static Layout make(int D, int H1, int H2, int A) {
-        Layout L;
+    __host__ __device__ static constexpr Layout make(int D, int H1, int H2, int A) {
+        Layout L{};
         L.D = D; L.H1 = H1; L.H2 = H2; L.A = A;
         L.oW1 = 0;
         L.ob1 = L.oW1 + (int64_t)H1 * D;
@@ -54,11 +84,29 @@ struct Layout {
         return L;
     }
     // head row a in [0, A]: a < A -> policy_head.weight[a], a == A -> value_head.weight
-    __host__ __device__ int64_t head_row(int a) const { return a < A ? oWp + (int64_t)a * H2 : oWv; }
-    __host__ __device__ int64_t head_bias(int a) const { return a < A ? obp + a : obv; }
+    __host__ __device__ constexpr int64_t head_row(int a) const { return a < A ? oWp + (int64_t)a * H2 : oWv; }
+    __host__ __device__ constexpr int64_t head_bias(int a) const { return a < A ? obp + a : obv; }
+};
+
+// Kernel shape policies.  ShapeC bakes the MLP dims (and optionally the minibatch size)
+// into the kernel, so every loop bound and parameter offset is a compile-time constant
+// (fully unrolled, no integer division, no guard chains); the benchmarked / reference
+// configs are instantiated this way.  ShapeR keeps them runtime (any other MLP shape).
+template <int D_, int H1_, int H2_, int A_, int B_>
+struct ShapeC {
+    static constexpr int AMAX = A_, AEX = A_;
+    __host__ __device__ static constexpr Layout lay(const Layout &) { return Layout::make(D_, H1_, H2_, A_); }
+    __host__ __device__ static constexpr int batch(int b) { return B_ > 0 ? B_ : b; }
+};
+template <int AMAX_>
+struct ShapeR {
+    static constexpr int AMAX = AMAX_, AEX = 0;
+    __host__ __device__ static Layout lay(const Layout &L) { return L; }
+    __host__ __device__ static int batch(int b) { return b; }
 };
 
 constexpr int kTile = 16;        // MFMA 16x16x4 f32 output tile
+
 constexpr int kMaxObsDim = 64;
 constexpr int kMaxHidden = 1024;
 constexpr int kMaxActions = 32;
@@ -70,10 +118,21 @@ struct Workspace {
     float *h2;       // (B, H2)    post-ReLU
     float *zpart;    // (H2/16, B, A+1) partial head outputs
     float *dz;       // (B, A+1)   dLoss/dlogits | dLoss/dvalue
-    float *part1;    // (B/16, H1, D+1) dW1|db1 partials per row block
+    float *part1;    // (ceil(B/64), H1, D+1) dW1|db1 partials per 64-row block
     float *sumsq;    // (n_slots)  per-tile sum of squared gradients
+    int32_t *f_act;  // (B)        gathered minibatch fields (written by k_fwd_hidden)
+    float *f_olp, *f_ov, *f_adv, *f_ret;
     int n_slots;
     size_t bytes;
+};
+constexpr int kRowsB = 64;       // rows per dh1 workgroup in k_bwd (one 16-row slab per wave)
+
+// Minibatch field gather done by the forward kernel (utils/rollout_collector.py:657-682).
+struct RowGather {
+    const int64_t *actions;
+    const float *logprobs, *values, *advantages, *returns;
+    int32_t *f_act;
+    float *f_olp, *f_ov, *f_adv, *f_ret;
 };
 Workspace carve_workspace(void *base, const Layout &L, int64_t B);
 
@@ -98,6 +157,7 @@ struct AdamArgs {
     int nrb;                // dW1/db1 partial row blocks (0: grads already final in G)
     const float *sched;     // optional device table {neg_step_size, bc2_sqrt} per step (graph replay)
     int sched_idx;
+    int stage_lds;          // set by the launcher: stage slots + partials through LDS
 };
 
 inline int n_col_blocks(int H) { return (H + kTile - 1) / kTile; }
@@ -106,12 +166,14 @@ inline int n_sumsq_slots(const Layout &L) { return n_col_blocks(L.H2) * n_col_bl
 // kernels' launch helpers (gs_mlp.hip)
 int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, const int32_t *idx,
                       int64_t T, int64_t N, int64_t rows, float *x_out, float *h1_out, float *h2_out,
-                      float *zpart, float *obs_copy, const int32_t *stop_flag, hipStream_t s);
+                      float *zpart, float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s);
+size_t fwd_lds_bytes(const Layout &L);
 int launch_heads_act(const float *P, const Layout &L, const float *zpart, int64_t rows, int mode, uint64_t seed,
                      uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s);
-int launch_loss(const float *P, const Layout &L, const float *zpart, int64_t B, const gs_rollout_view &ro,
-                const int32_t *idx, const LossArgs &la, float *dz, float *metrics, int32_t *stop, hipStream_t s);
+int launch_loss(const float *P, const Layout &L, int64_t B, const Workspace &ws, const LossArgs &la, float *metrics,
+                int32_t *stop, hipStream_t s);
 size_t bwd_lds_bytes(const Layout &L, int64_t B);
+int prepare_kernels(const Layout &L, int64_t B);
 int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
                hipStream_t s);
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,

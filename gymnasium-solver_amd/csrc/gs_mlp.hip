@@ -9,29 +9,43 @@
 //   slice_trajectories (collate)   utils/rollout_collector.py:657-682
 //
 // All arithmetic is fp32 (the reference never leaves fp32).  The three
-// B x 256 x 256 products of a minibatch step (forward h2, dW2, dh1) run on the exact-f32
-// MFMA v_mfma_f32_16x16x4_f32: one 16x16 output tile per workgroup, K split over the
-// 4 waves (one per SIMD), partial tiles summed through LDS in a fixed order, so
-// results are deterministic run to run.  K = 4 (obs) and N = A+1 (heads) products are
-// VALU dot products fused into the neighbouring kernels.
+// B x H x H products of a minibatch step (forward h2, dW2, dh1) run on the exact-f32
+// MFMA v_mfma_f32_16x16x4_f32 (64 FLOP/clk/SIMD, = the f32 vector peak); partial tiles
+// are summed through LDS in a fixed order, so results are deterministic run to run.
+// K = obs_dim and N = A+1 (heads) products are VALU dot products fused into the
+// neighbouring kernels.
+//
+// At B = 256 every kernel is latency-bound, not throughput-bound: the design rule is
+// that each kernel has at most two dependent global round trips.  Every operand a
+// workgroup needs is fetched in ONE cooperative, vectorised phase into LDS (all loads
+// in flight together), then the math runs out of LDS/registers.
 //
 // One minibatch step = 4 launches (the dependency chain has exactly 3 all-to-all seams:
 // h2 -> logits, loss -> dh2/dh1, grads -> global norm):
-//   k_fwd_hidden  : gather rows by sampler index, h1 = relu(x W1^T + b1) recomputed
-//                   per workgroup, h2 tile on MFMA, per-tile partial head dot products
+//   k_fwd_hidden  : gather rows by sampler index (+ the step's act/logp/value/adv/ret
+//                   fields), h1 = relu(x W1^T + b1) recomputed per workgroup, h2 tile on
+//                   MFMA, per-tile partial head dot products
 //   k_loss        : one workgroup: logits/value, log-softmax, ratio, clipped surrogate,
 //                   clipped value loss, entropy, batch advantage normalisation, all
 //                   metrics, and the analytic dLoss/dlogits, dLoss/dvalue
-//   k_bwd         : dW2 tiles (MFMA, K = batch), dh1 tiles (MFMA, K = H2) + dW1/db1
-//                   partials, head weight/bias grads; dh2 = relu'(h2) (dz Wh) is
-//                   recomputed on the fly, never stored; per-tile sum of squares
+//   k_bwd         : dW2 tiles (MFMA, K = batch), dh1 slabs (MFMA, K = H2) + dW1/db1
+//                   partials per 64 rows, head weight/bias grads; dh2 = relu'(h2) (dz Wh)
+//                   is recomputed on the fly, never stored; per-tile sum of squares
 //   k_clip_adam   : global grad norm from the per-tile sums (identical in every
 //                   workgroup), clip coefficient, torch.optim.Adam update
 #include <float.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "gs_common.h"
 
 namespace gs {
+
+#ifdef GS_STAMPS
+__device__ unsigned long long g_stamp_acc[8][16];
+__device__ unsigned long long g_stamp_cnt[8];
+#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c)
 {
@@ -39,11 +53,11 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c)
 }
 
 // env-major sample index (utils/rollout_buffer.py:11-13) -> time-major buffer row
-__device__ __forceinline__ int64_t sample_row(int32_t s, int64_t T, int64_t N)
+__device__ __forceinline__ int sample_row(int s, int T, int N)
 {
-    const int64_t e = s / T;
-    const int64_t t = s - e * T;
-    return t * N + e;
+    const unsigned e = (unsigned)s / (unsigned)T;
+    const unsigned t = (unsigned)s - e * (unsigned)T;
+    return (int)(t * (unsigned)N + e);
 }
 
 template <typename T>
@@ -54,74 +68,171 @@ __device__ __forceinline__ T wave_sum(T v)
     return v;
 }
 
-// ------------------------------------------------------------------------------------
-// k_fwd_hidden: grid (ceil(H2/16), ceil(rows/16)), 256 threads.
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fwd_hidden(
-    const float *__restrict__ P, Layout L, const float *__restrict__ obs, const int32_t *__restrict__ idx,
-    int64_t T, int64_t N, int64_t rows, float *__restrict__ x_out, float *__restrict__ h1_out,
-    float *__restrict__ h2_out, float *__restrict__ zpart, float *__restrict__ obs_copy,
-    const int32_t *__restrict__ stop)
-{
-    if (stop && *stop) return;
-    extern __shared__ float lds[];
-    const int D = L.D, H1 = L.H1, H2 = L.H2, A1 = L.A + 1;
-    const int cb = blockIdx.x, rb = blockIdx.y;
-    const int64_t r0 = (int64_t)rb * kTile;
-    const int c0 = cb * kTile;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h1s_ld = H1 + 4;
-    float *xs = lds;                        // [16][D]
-    float *h1s = xs + kTile * D;            // [16][H1+4]
-    float *red = h1s + kTile * h1s_ld;      // [4][256]
-    float *h2s = red + 4 * 256;             // [16][17]
+__host__ __device__ constexpr int round4(int n) { return (n + 3) & ~3; }
 
-    // 1. gather the 16 observation rows (minibatch: by sampler index; rollout: direct)
-    for (int u = tid; u < kTile * D; u += 256) {
-        const int i = u / D, d = u - i * D;
-        const int64_t r = r0 + i;
-        float v = 0.0f;
-        if (r < rows) {
-            const int64_t src = idx ? sample_row(idx[r], T, N) : r;
-            v = obs[src * D + d];
-        }
-        xs[u] = v;
+// Sum NV per-thread values over the 256-thread block in a fixed order (deterministic),
+// through LDS (two levels of 16) — __shfl would lower to ds_bpermute chains (~100+ cycles
+// per step).  Every thread returns the totals.  scratch: NV*(256+16) elements of T.
+template <int NV, typename T>
+__device__ __forceinline__ void block_reduce(T (&v)[NV], T *scratch)
+{
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) scratch[k * 256 + tid] = v[k];
+    __syncthreads();
+    T *part = scratch + NV * 256;
+    if (tid < NV * 16) {
+        const int k = tid >> 4, j = tid & 15;
+        T acc = 0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc += scratch[k * 256 + j * 16 + m];
+        part[tid] = acc;
     }
     __syncthreads();
-    if (cb == 0) {
-        for (int u = tid; u < kTile * D; u += 256) {
-            const int64_t r = r0 + u / D;
-            if (r < rows) {
-                if (x_out) x_out[r0 * D + u] = xs[u];
-                if (obs_copy) obs_copy[r0 * D + u] = xs[u];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        T acc = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc += part[k * 16 + j];
+        v[k] = acc;
+    }
+    __syncthreads();
+}
+
+// copy n floats global -> LDS, vectorised when both sides are 16-B aligned
+__device__ __forceinline__ void copy_to_lds(float *dst, const float *src, int n)
+{
+    const int tid = threadIdx.x;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const int n4 = n >> 2;
+#pragma unroll 8
+        for (int u = tid; u < n4; u += 256)
+            reinterpret_cast<float4 *>(dst)[u] = reinterpret_cast<const float4 *>(src)[u];
+        for (int u = (n4 << 2) + tid; u < n; u += 256) dst[u] = src[u];
+    } else {
+#pragma unroll 4
+        for (int u = tid; u < n; u += 256) dst[u] = src[u];
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_fwd_hidden: grid (ceil(H2/16), ceil(rows/16)), 256 threads.
+// LDS (floats): srcs[16] W1s[H1*D] b1s[H1] W2s[16][H1+4] b2s[16] whs[A1][16] xs[16][D]
+//               h1s[16][H1+4] red[4][256] h2s[16][17]
+// ------------------------------------------------------------------------------------
+size_t fwd_lds_bytes(const Layout &L)
+{
+    const int A1 = L.A + 1;
+    size_t n = 16 + round4(L.H1 * L.D) + round4(L.H1) + kTile * (L.H1 + 4) + 16 + round4(A1 * 16) +
+               round4(kTile * L.D) + kTile * (L.H1 + 4) + 1024 + kTile * 17;
+    return n * sizeof(float);
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void k_fwd_hidden(
+    const float *__restrict__ P, Layout Lrt, const float *__restrict__ obs, const int32_t *__restrict__ idx, int T,
+    int N, int rows, float *__restrict__ x_out, float *__restrict__ h1_out, float *__restrict__ h2_out,
+    float *__restrict__ zpart, float *__restrict__ obs_copy, const int32_t *__restrict__ stop, RowGather rg)
+{
+    GS_STAMP_BEGIN(0)
+    if (stop && *stop) return;
+    extern __shared__ float lds[];
+    const Layout L = S::lay(Lrt);
+    const int D = L.D, H1 = L.H1, H2 = L.H2, A1 = L.A + 1;
+    const int cb = blockIdx.x, rb = blockIdx.y;
+    const int r0 = rb * kTile;
+    const int c0 = cb * kTile;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ldh = H1 + 4;
+    int *srcs = reinterpret_cast<int *>(lds);
+    float *W1s = lds + 16;
+    float *b1s = W1s + round4(H1 * D);
+    float *W2s = b1s + round4(H1);
+    float *b2s = W2s + kTile * ldh;
+    float *whs = b2s + 16;
+    float *xs = whs + round4(A1 * 16);
+    float *h1s = xs + round4(kTile * D);
+    float *red = h1s + kTile * ldh;
+    float *h2s = red + 1024;
+
+    // ---- phase 0: every operand of this workgroup, all loads in flight together.
+    //      Threads 0..15 run the dependent idx -> row -> obs/fields chain while the rest
+    //      of the block streams the weights into LDS.
+    if (tid < kTile) {
+        const int r = r0 + tid;
+        const int src = r < rows ? (idx ? sample_row(idx[r], T, N) : r) : -1;
+        srcs[tid] = src;
+        for (int d = 0; d < D; ++d) xs[tid * D + d] = src >= 0 ? obs[(int64_t)src * D + d] : 0.0f;
+        if (cb == 0 && rg.f_act && src >= 0) {
+            rg.f_act[r] = (int32_t)rg.actions[src];
+            rg.f_olp[r] = rg.logprobs[src];
+            rg.f_ov[r] = rg.values[src];
+            rg.f_adv[r] = rg.advantages[src];
+            rg.f_ret[r] = rg.returns[src];
+        }
+    }
+    copy_to_lds(W1s, P + L.oW1, H1 * D);
+    copy_to_lds(b1s, P + L.ob1, H1);
+    {
+        const int k4n = H1 >> 2;
+#pragma unroll 4
+        for (int u = tid; u < kTile * k4n; u += 256) {
+            const int i = u / k4n, k4 = u - i * k4n;
+            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (c0 + i < H2) w = *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)(c0 + i) * H1 + 4 * k4);
+            *reinterpret_cast<float4 *>(W2s + i * ldh + 4 * k4) = w;
+        }
+    }
+    if (tid < kTile) b2s[tid] = c0 + tid < H2 ? P[L.ob2 + c0 + tid] : 0.0f;
+    if (tid < A1 * kTile) {
+        const int a = tid >> 4, j = tid & 15;
+        whs[tid] = c0 + j < H2 ? P[L.head_row(a) + c0 + j] : 0.0f;
+    }
+    __syncthreads();
+    GS_STAMP(0)
+    GS_STAMP(1)
+    // ---- phase 1: h1 = relu(x W1^T + b1) out of LDS; one hidden unit per thread
+    for (int k = tid; k < H1; k += 256) {
+        float w[8];
+        const bool small = D <= 8;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) w[d] = (small && d < D) ? W1s[k * D + d] : 0.0f;
+        const float bk = b1s[k];
+        if (small) {
+#pragma unroll
+            for (int i = 0; i < kTile; ++i) {
+                float xr[8];
+#pragma unroll
+                for (int d = 0; d < 8; ++d) xr[d] = d < D ? xs[i * D + d] : 0.0f;
+                float acc = 0.0f;
+#pragma unroll
+                for (int d = 0; d < 8; ++d)
+                    if (d < D) acc = fmaf(xr[d], w[d], acc);
+                acc += bk;
+                h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
+            }
+        } else {
+            for (int i = 0; i < kTile; ++i) {
+                float acc = 0.0f;
+                for (int d = 0; d < D; ++d) acc = fmaf(xs[i * D + d], W1s[k * D + d], acc);
+                acc += bk;
+                h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
             }
         }
     }
-    // 2. h1 = relu(x W1^T + b1) for the 16 rows (K = D: VALU)
-    for (int u = tid; u < kTile * H1; u += 256) {
-        const int i = u / H1, k = u - i * H1;
-        const float *w = P + L.oW1 + (int64_t)k * D;
-        float acc = 0.0f;
-        for (int d = 0; d < D; ++d) acc = fmaf(xs[i * D + d], w[d], acc);
-        acc += P[L.ob1 + k];
-        const float h = acc > 0.0f ? acc : 0.0f;
-        h1s[i * h1s_ld + k] = h;
-        if (cb == 0 && h1_out && r0 + i < rows) h1_out[(r0 + i) * H1 + k] = h;
-    }
     __syncthreads();
-    // 3. h2 tile = h1[16 x H1] . W2[c0:c0+16, :]^T on MFMA, K split over the 4 waves
+    GS_STAMP(2)
+    // ---- phase 2: h2 tile = h1[16 x H1] . W2[c0:c0+16, :]^T, MFMA, K split over 4 waves
     {
         const int i = lane & 15, q = lane >> 4;
         const int nch = H1 / kTile;
         const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
-        const bool colok = c0 + i < H2;
-        const float *wrow = P + L.oW2 + (int64_t)(colok ? c0 + i : 0) * H1;
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
         for (int ch = ch0; ch < ch1; ++ch) {
             const int k = ch * kTile + 4 * q;
-            const float4 a = *reinterpret_cast<const float4 *>(h1s + i * h1s_ld + k);
-            float4 b = *reinterpret_cast<const float4 *>(wrow + k);
-            if (!colok) b = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 a = *reinterpret_cast<const float4 *>(h1s + i * ldh + k);
+            const float4 b = *reinterpret_cast<const float4 *>(W2s + i * ldh + k);
             acc0 = mfma4(a.x, b.x, acc0);
             acc1 = mfma4(a.y, b.y, acc1);
             acc0 = mfma4(a.z, b.z, acc0);
@@ -132,40 +243,67 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         for (int r = 0; r < 4; ++r) red[wave * 256 + (q * 4 + r) * kTile + i] = acc[r];
     }
     __syncthreads();
+    GS_STAMP(3)
     {
         const int row = tid >> 4, col = tid & 15;
         const float s = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
         float h = 0.0f;
         if (c0 + col < H2) {
-            h = s + P[L.ob2 + c0 + col];
+            h = s + b2s[col];
             h = h > 0.0f ? h : 0.0f;
-            if (h2_out && r0 + row < rows) h2_out[(r0 + row) * H2 + c0 + col] = h;
+            if (h2_out && r0 + row < rows) h2_out[(int64_t)(r0 + row) * H2 + c0 + col] = h;
         }
         h2s[row * 17 + col] = h;
     }
     __syncthreads();
-    // 4. partial head outputs over this tile's 16 hidden units
+    // ---- phase 3: partial head outputs over this tile's 16 hidden units
+    const int ncbz = gridDim.x;
     for (int u = tid; u < kTile * A1; u += 256) {
         const int row = u / A1, a = u - row * A1;
         if (r0 + row >= rows) continue;
-        const float *w = P + L.head_row(a) + c0;
         float z = 0.0f;
-        const int cmax = min(kTile, H2 - c0);
-        for (int c = 0; c < cmax; ++c) z = fmaf(h2s[row * 17 + c], w[c], z);
-        zpart[((int64_t)cb * rows + r0 + row) * A1 + a] = z;
+#pragma unroll
+        for (int c = 0; c < kTile; ++c) z = fmaf(h2s[row * 17 + c], whs[a * 16 + c], z);
+        zpart[((int64_t)(r0 + row) * ncbz + cb) * A1 + a] = z;
     }
+    if (cb == 0) {
+        const int nrow = min(kTile, rows - r0);
+        for (int u = tid; u < nrow * D; u += 256) {
+            if (x_out) x_out[(int64_t)r0 * D + u] = xs[u];
+            if (obs_copy) obs_copy[(int64_t)r0 * D + u] = xs[u];
+        }
+        if (h1_out) {
+            const int k4n = H1 >> 2;
+            for (int u = tid; u < nrow * k4n; u += 256) {
+                const int i = u / k4n, k4 = u - i * k4n;
+                *reinterpret_cast<float4 *>(h1_out + (int64_t)(r0 + i) * H1 + 4 * k4) =
+                    *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
+            }
+        }
+    }
+    GS_STAMP_END(4)
 }
+
+static int set_lds_limit(const void *fn, size_t bytes);
+template <class F>
+static int with_shape(const Layout &L, int64_t B, F &&f);
 
 int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, const int32_t *idx, int64_t T,
                       int64_t N, int64_t rows, float *x_out, float *h1_out, float *h2_out, float *zpart,
-                      float *obs_copy, const int32_t *stop_flag, hipStream_t s)
+                      float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s)
 {
     const dim3 grid((unsigned)((L.H2 + kTile - 1) / kTile), (unsigned)((rows + kTile - 1) / kTile));
-    const size_t lds = sizeof(float) * (kTile * L.D + kTile * (L.H1 + 4) + 4 * 256 + kTile * 17);
-    hipLaunchKernelGGL(k_fwd_hidden, grid, dim3(256), lds, s, params, L, obs, idx, T, N, rows, x_out, h1_out,
-                       h2_out, zpart, obs_copy, stop_flag);
-    GS_LAUNCH_CHECK("k_fwd_hidden");
-    return GS_OK;
+    RowGather g{};
+    if (rg) g = *rg;
+    return with_shape(L, 0, [&](auto sh) {
+        using Sh = decltype(sh);
+        int rc = set_lds_limit((const void *)k_fwd_hidden<Sh>, fwd_lds_bytes(L));
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_fwd_hidden<Sh>, grid, dim3(256), fwd_lds_bytes(L), s, params, L, obs, idx, (int)T,
+                           (int)N, (int)rows, x_out, h1_out, h2_out, zpart, obs_copy, stop_flag, g);
+        GS_LAUNCH_CHECK("k_fwd_hidden");
+        return GS_OK;
+    });
 }
 
 // ------------------------------------------------------------------------------------
@@ -204,6 +342,45 @@ __device__ __forceinline__ HeadRow head_stats(const float (&z)[AMAX + 1], int A)
     return h;
 }
 
+// logits/value of row r from the per-16-column partials (+ bias): the row's partials are
+// contiguous ([row][col-block][A+1]) and are loaded as one burst before any add.
+// AEX = exact action count when known at compile time (static register indexing), else 0.
+template <int AMAX, int AEX>
+__device__ __forceinline__ void gather_head_row(const float *__restrict__ zpart, const float *__restrict__ P,
+                                                const Layout &L, int64_t r, float (&z)[AMAX + 1])
+{
+    const int ncb = (L.H2 + kTile - 1) / kTile;
+#pragma unroll
+    for (int a = 0; a < AMAX + 1; ++a) z[a] = 0.0f;
+    if constexpr (AEX > 0) {
+        constexpr int A1c = AEX + 1;
+        const float *zp = zpart + r * ncb * A1c;
+        for (int cb0 = 0; cb0 < ncb; cb0 += 16) {
+            float buf[16][A1c];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+#pragma unroll
+                for (int a = 0; a < A1c; ++a) buf[j][a] = cb0 + j < ncb ? zp[(cb0 + j) * A1c + a] : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+#pragma unroll
+                for (int a = 0; a < A1c; ++a) z[a] += buf[j][a];
+        }
+    } else {
+        const int A1 = L.A + 1;
+        const float *zp = zpart + r * ncb * A1;
+        for (int cb = 0; cb < ncb; ++cb) {
+#pragma unroll
+            for (int a = 0; a < AMAX + 1; ++a)
+                if (a < A1) z[a] += zp[cb * A1 + a];
+        }
+    }
+    const int A1 = L.A + 1;
+#pragma unroll
+    for (int a = 0; a < AMAX + 1; ++a)
+        if (a < A1) z[a] += P[L.head_bias(a)];
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t x)
 {
     x += 0x9E3779B97F4A7C15ull;
@@ -214,33 +391,25 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x)
 
 // ------------------------------------------------------------------------------------
 // k_heads_act: rollout head — logits/value from partials, action select, log_prob.
-// one thread per env row.  z scratch: the zpart slice of block 0 is reused.
+// one thread per env row.
 // ------------------------------------------------------------------------------------
-template <int AMAX>
-__global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, Layout L,
+template <class S>
+__global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, Layout Lrt,
                                                    const float *__restrict__ zpart, int64_t rows, int mode,
                                                    uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
                                                    float *__restrict__ logp, float *__restrict__ value)
 {
+    constexpr int AMAX = S::AMAX, AEX = S::AEX;
+    const Layout L = S::lay(Lrt);
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= rows) return;
-    const int A = L.A, A1 = A + 1;
-    const int ncb = (L.H2 + kTile - 1) / kTile;
+    const int A = L.A;
     float z[AMAX + 1];
-#pragma unroll
-    for (int a = 0; a < AMAX + 1; ++a) z[a] = 0.0f;
-    for (int cb = 0; cb < ncb; ++cb) {
-        const float *zp = zpart + ((int64_t)cb * rows + r) * A1;
-#pragma unroll
-        for (int a = 0; a < AMAX + 1; ++a)
-            if (a < A1) z[a] += zp[a];
-    }
+    gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
     float v = 0.0f;
 #pragma unroll
-    for (int a = 0; a < AMAX + 1; ++a) {
-        if (a < A1) z[a] += P[L.head_bias(a)];
+    for (int a = 0; a < AMAX + 1; ++a)
         if (a == A) v = z[a];
-    }
     if (value) value[r] = v;
     if (!actions) return;
     const HeadRow h = head_stats<AMAX>(z, A);
@@ -280,21 +449,25 @@ __global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, 
 }
 
 // ------------------------------------------------------------------------------------
-// k_loss: single workgroup of 256 threads over the B minibatch rows.
+// k_loss: single workgroup of 256 threads over the B <= 1024 minibatch rows.
 // ------------------------------------------------------------------------------------
-
-
 constexpr int kNumSums = 14;
 
-template <int AMAX>
-__global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layout L, const float *__restrict__ zpart,
-                                              int64_t B, gs_rollout_view ro, const int32_t *__restrict__ idx,
+
+template <class S>
+__global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layout Lrt, const float *__restrict__ zpart,
+                                              int Brt, const int32_t *__restrict__ f_act,
+                                              const float *__restrict__ f_olp, const float *__restrict__ f_ov,
+                                              const float *__restrict__ f_adv, const float *__restrict__ f_ret,
                                               LossArgs la, float *__restrict__ dz, float *__restrict__ metrics,
                                               int32_t *__restrict__ stop)
 {
-    __shared__ double sred[kNumSums][4];
-    __shared__ double sbc[2];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ double sred[kNumSums * (256 + 16)];
+    constexpr int AMAX = S::AMAX, AEX = S::AEX;
+    const Layout L = S::lay(Lrt);
+    const int B = S::batch(Brt);
+    const int tid = threadIdx.x;
+    GS_STAMP_BEGIN(1)
     if (stop && *stop) {
         if (tid == 0) {
             for (int k = 0; k < GS_NUM_METRICS; ++k) metrics[k] = 0.0f;
@@ -304,72 +477,55 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
         return;
     }
     const int A = L.A, A1 = A + 1;
-    const int ncb = (L.H2 + kTile - 1) / kTile;
     const float invB = 1.0f / (float)B;
 
-    // --- batch advantage normalisation: (a - mean) / (std_unbiased + 1e-8)
+    // ---- batch advantage normalisation: (a - mean) / (std_unbiased + 1e-8)
     float meanf = 0.0f, stdf = 1.0f;
     if (la.normalize) {
-        double s = 0.0;
-        for (int64_t r = tid; r < B; r += 256) s += (double)ro.advantages[sample_row(idx[r], ro.T, ro.N)];
-        s = wave_sum(s);
-        if (lane == 0) sred[0][wave] = s;
-        __syncthreads();
-        if (tid == 0) sbc[0] = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
-        __syncthreads();
-        const double mean = sbc[0] / (double)B;
-        double q = 0.0;
-        for (int64_t r = tid; r < B; r += 256) {
-            const double dv = (double)ro.advantages[sample_row(idx[r], ro.T, ro.N)] - mean;
-            q += dv * dv;
+        double m1[1] = {0.0};
+        for (int r = tid; r < B; r += 256) m1[0] += (double)f_adv[r];
+        block_reduce<1>(m1, sred);
+        const double mean = m1[0] / (double)B;
+        double q[1] = {0.0};
+        for (int r = tid; r < B; r += 256) {
+            const double dv = (double)f_adv[r] - mean;
+            q[0] += dv * dv;
         }
-        q = wave_sum(q);
-        if (lane == 0) sred[1][wave] = q;
-        __syncthreads();
-        if (tid == 0) sbc[1] = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
-        __syncthreads();
+        block_reduce<1>(q, sred);
         meanf = (float)mean;
-        stdf = (float)sqrt(sbc[1] / (double)(B - 1));
+        stdf = (float)sqrt(q[0] / (double)(B - 1));
     }
+    GS_STAMP(0)
 
     double acc[kNumSums];
 #pragma unroll
     for (int k = 0; k < kNumSums; ++k) acc[k] = 0.0;
-    for (int64_t r = tid; r < B; r += 256) {
-        const int64_t src = sample_row(idx[r], ro.T, ro.N);
+    for (int r = tid; r < B; r += 256) {
+        // every input of the row first (one round trip), then the math
         float z[AMAX + 1];
-#pragma unroll
-        for (int a = 0; a < AMAX + 1; ++a) z[a] = 0.0f;
-        for (int cb = 0; cb < ncb; ++cb) {
-            const float *zp = zpart + ((int64_t)cb * B + r) * A1;
-#pragma unroll
-            for (int a = 0; a < AMAX + 1; ++a)
-                if (a < A1) z[a] += zp[a];
-        }
+        gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
+        const int act = f_act[r];
+        const float olp = f_olp[r], ov = f_ov[r], ret = f_ret[r];
+        float adv = f_adv[r];
         float v = 0.0f;
 #pragma unroll
-        for (int a = 0; a < AMAX + 1; ++a) {
-            if (a < A1) z[a] += P[L.head_bias(a)];
+        for (int a = 0; a < AMAX + 1; ++a)
             if (a == A) v = z[a];
-        }
         const HeadRow h = head_stats<AMAX>(z, A);
-        const int act = (int)ro.actions[src];
-        // entropy H = -sum clamp(ln, f32min) * p, p = softmax(ln)
+        const float invS = 1.0f / h.S;
+        // ln = normalised logits, p = softmax(ln) (Categorical.probs), pe = exp(ln)
+        float ln[AMAX], p[AMAX];
         float H = 0.0f, lp = 0.0f;
 #pragma unroll
         for (int a = 0; a < AMAX; ++a) {
+            ln[a] = z[a] - h.lse;
+            p[a] = a < A ? expf(ln[a] - h.m2) * invS : 0.0f;
             if (a < A) {
-                const float ln = z[a] - h.lse;
-                const float p = expf(ln - h.m2) / h.S;
-                H += fmaxf(ln, -FLT_MAX) * p;
-                if (a == act) lp = ln;
+                H += fmaxf(ln[a], -FLT_MAX) * p[a];   // entropy: -sum clamp(ln, f32min) * p
+                if (a == act) lp = ln[a];
             }
         }
         H = -H;
-        const float olp = ro.logprobs[src];
-        const float ov = ro.values[src];
-        const float ret = ro.returns[src];
-        float adv = ro.advantages[src];
         if (la.normalize) adv = (adv - meanf) / (stdf + 1e-8f);
         const float ratio = expf(lp - olp);
         const float rc = fminf(fmaxf(ratio, la.clip_lo), la.clip_hi);
@@ -407,15 +563,13 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
         const float dratio = adv * (g_mn * ga) + adv * (g_mn * gb) * inclip;
         const float dlp = dratio * ratio;
         const float dH = -la.ent_coef * invB;
-        float *dzr = dz + r * A1;
+        float *dzr = dz + (int64_t)r * A1;
 #pragma unroll
         for (int a = 0; a < AMAX; ++a) {
             if (a < A) {
-                const float ln = z[a] - h.lse;
-                const float p = expf(ln - h.m2) / h.S;
-                const float pe = expf(ln);      // softmax(z) as seen by logsumexp backward
+                const float pe = expf(ln[a]);   // softmax(z) as seen by logsumexp backward
                 float g = dlp * ((a == act ? 1.0f : 0.0f) - pe);
-                g += dH * (-p * (ln + H));
+                g += dH * (-p[a] * (ln[a] + H));
                 dzr[a] = g;
             }
         }
@@ -425,17 +579,11 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
         const float gv = la.vf_coef * invB;
         dzr[A] = (gv * hu) * (2.0f * du) + (gv * hc) * (2.0f * dc) * invc;
     }
-    // block reductions (fixed order -> deterministic)
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kNumSums; ++k) {
-        const double s = wave_sum(acc[k]);
-        if (lane == 0) sred[k][wave] = s;
-    }
-    __syncthreads();
+    GS_STAMP(1)
+    block_reduce<kNumSums>(acc, sred);     // fixed order -> deterministic
+    GS_STAMP(2)
     if (tid == 0) {
-        double t[kNumSums];
-        for (int k = 0; k < kNumSums; ++k) t[k] = ((sred[k][0] + sred[k][1]) + sred[k][2]) + sred[k][3];
+        const double *t = acc;
         const double Bd = (double)B;
         const float pl = (float)(-t[0] / Bd);
         const float vl = (float)(t[1] / Bd);
@@ -465,76 +613,141 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
         metrics[GS_M_RES1] = 0.0f;
         if (kl_stop && stop) *stop = 1;
     }
+    GS_STAMP_END(3)
 }
 
 // ------------------------------------------------------------------------------------
 // k_bwd: three roles by block range.
 //   role A: dW2 tile (n-block, k-block), K = batch     -> grads, db2 (k-block 0)
-//   role B: dh1 tile (row block, k-block), K = H2      -> dW1/db1 partial per row block
+//   role B: dh1 slab (64 rows, k-block), K = H2        -> dW1/db1 partial per 64 rows
 //   role C: head grads for an n-block (+ head biases in block 0)
 // sum-of-squares slot map: [0, nA) dW2 tiles, [nA, nA+ncb) db2 blocks,
 //                          [nA+ncb, nA+2ncb) head weight blocks, nA+2ncb head biases.
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void block_sumsq_store(float v, float *slot, float *sbuf)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    v = wave_sum(v);
-    __syncthreads();
-    if (lane == 0) sbuf[wave] = v;
-    __syncthreads();
-    if (tid == 0) *slot = ((sbuf[0] + sbuf[1]) + sbuf[2]) + sbuf[3];
+    float t[1] = {v};
+    block_reduce<1>(t, sbuf);      // sbuf: 272 floats
+    if (threadIdx.x == 0) *slot = t[0];
 }
 
-__global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout L, int64_t B,
+struct BwdShape {
+    int ncb, nkb, nrbB, nA, nB, nC;
+    __host__ __device__ static BwdShape make(const Layout &L, int B)
+    {
+        BwdShape s;
+        s.ncb = (L.H2 + kTile - 1) / kTile;
+        s.nkb = (L.H1 + kTile - 1) / kTile;
+        s.nrbB = (B + kRowsB - 1) / kRowsB;
+        s.nA = s.ncb * s.nkb;
+        s.nB = s.nrbB * s.nkb;
+        s.nC = s.ncb;
+        return s;
+    }
+};
+
+size_t bwd_lds_bytes(const Layout &L, int64_t B)
+{
+    const int A1 = L.A + 1;
+    const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
+    const int64_t H2p = (L.H2 + 63) / 64 * 64;
+    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 2 * kTile * (Bp64 + 4) + 1024;
+    const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
+                          kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17;
+    const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + A1 * 256;
+    int64_t m = roleA;
+    if (roleB > m) m = roleB;
+    if (roleC > m) m = roleC;
+    return (size_t)m * sizeof(float);
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout Lrt, int Brt,
                                              const float *__restrict__ x, const float *__restrict__ h1,
                                              const float *__restrict__ h2, const float *__restrict__ dz,
                                              float *__restrict__ G, float *__restrict__ part1,
                                              float *__restrict__ sumsq, const int32_t *__restrict__ stop)
 {
+    GS_STAMP_BEGIN(2)
     if (stop && *stop) return;
     extern __shared__ float lds[];
-    __shared__ float sbuf[4];
+    __shared__ float sbuf[272];
+    const Layout L = S::lay(Lrt);
+    const int B = S::batch(Brt);
     const int D = L.D, H1 = L.H1, H2 = L.H2, A = L.A, A1 = A + 1;
-    const int ncb = (H2 + kTile - 1) / kTile;   // H2 blocks
-    const int nkb = (H1 + kTile - 1) / kTile;   // H1 blocks
-    const int nrb = (int)((B + kTile - 1) / kTile);
-    const int nA = ncb * nkb, nBr = nrb * nkb;
+    const BwdShape sh = BwdShape::make(L, B);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
     int bid = blockIdx.x;
 
-    if (bid < nA) {
+    if (bid < sh.nA) {
         // ---------------- role A: dW2[n0:n0+16, k0:k0+16] = sum_b dh2[b,n] h1[b,k]
-        const int nb = bid / nkb, kb = bid - nb * nkb;
+        const int nb = bid / sh.nkb, kb = bid - nb * sh.nkb;
         const int n0 = nb * kTile, k0 = kb * kTile;
-        const int Bp = ((int)B + 63) / 64 * 64;      // padded K (batch) for 4 waves x 16
+        const int Bp = (B + 63) / 64 * 64;      // padded K (batch) for 4 waves x 16
         const int ld = Bp + 4;
-        float *dh2T = lds;                // [16][Bp+4]  (n, b)
-        float *h1T = dh2T + kTile * ld;   // [16][Bp+4]  (k, b)
-        float *red = h1T + kTile * ld;    // [4][256]
-        for (int u = tid; u < kTile * Bp; u += 256) {
-            const int b = u >> 4, i = u & 15;
-            float dh = 0.0f, hv = 0.0f;
+        float *dzs = lds;                            // [B][A1]
+        float *whs = dzs + round4(B * A1);           // [A1][16]
+        float *dh2T = whs + round4(A1 * 16);         // [16][Bp+4]  (n, b): h2 first, then dh2
+        float *h1T = dh2T + kTile * ld;              // [16][Bp+4]  (k, b)
+        float *red = h1T + kTile * ld;               // [4][256]
+        copy_to_lds(dzs, dz, B * A1);
+        if (tid < A1 * kTile) {
+            const int a = tid >> 4, j = tid & 15;
+            whs[tid] = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
+        }
+        // h2 / h1 column tiles: 16 contiguous floats per row = 4 float4, transposed into LDS
+#pragma unroll 4
+        for (int u = tid; u < Bp * 4; u += 256) {
+            const int b = u >> 2, c4 = u & 3;
+            float4 hv = make_float4(0.f, 0.f, 0.f, 0.f), gv = make_float4(0.f, 0.f, 0.f, 0.f);
             if (b < B) {
-                const int n = n0 + i, k = k0 + i;
-                if (n < H2) {
-                    const float hh = h2[(int64_t)b * H2 + n];
-                    if (hh > 0.0f) {
-                        const float *dzr = dz + (int64_t)b * A1;
-                        float s = 0.0f;
-                        for (int a = 0; a < A1; ++a) s = fmaf(dzr[a], P[L.head_row(a) + n], s);
-                        dh = s;
-                    }
-                }
-                if (k < H1) hv = h1[(int64_t)b * H1 + k];
+                if (n0 + 4 * c4 < H2) hv = *reinterpret_cast<const float4 *>(h2 + (int64_t)b * H2 + n0 + 4 * c4);
+                if (k0 + 4 * c4 < H1) gv = *reinterpret_cast<const float4 *>(h1 + (int64_t)b * H1 + k0 + 4 * c4);
             }
-            dh2T[i * ld + b] = dh;
-            h1T[i * ld + b] = hv;
+            dh2T[(4 * c4 + 0) * ld + b] = hv.x;
+            dh2T[(4 * c4 + 1) * ld + b] = hv.y;
+            dh2T[(4 * c4 + 2) * ld + b] = hv.z;
+            dh2T[(4 * c4 + 3) * ld + b] = hv.w;
+            h1T[(4 * c4 + 0) * ld + b] = gv.x;
+            h1T[(4 * c4 + 1) * ld + b] = gv.y;
+            h1T[(4 * c4 + 2) * ld + b] = gv.z;
+            h1T[(4 * c4 + 3) * ld + b] = gv.w;
         }
         __syncthreads();
+        GS_STAMP(0)
+        // dh2 = relu'(h2) * (dz . Wh), in place; lane owns hidden unit i, rows stride 16
+        {
+            const int i = tid & 15;
+            float w[kMaxActions + 1];
+#pragma unroll
+            for (int a = 0; a < kMaxActions + 1; ++a) w[a] = a < A1 ? whs[a * 16 + i] : 0.0f;
+            if (A1 <= 5) {
+                // branch-free body so the unrolled iterations' LDS reads issue together
+#pragma unroll 8
+                for (int b = tid >> 4; b < B; b += 16) {
+                    const float h = dh2T[i * ld + b];
+                    float s = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < 5; ++a) s = a < A1 ? fmaf(dzs[b * A1 + a], w[a], s) : s;
+                    dh2T[i * ld + b] = h > 0.0f ? s : 0.0f;
+                }
+            } else {
+                for (int b = tid >> 4; b < B; b += 16) {
+                    const float h = dh2T[i * ld + b];
+                    float s = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < kMaxActions + 1; ++a) s = a < A1 ? fmaf(dzs[b * A1 + a], w[a], s) : s;
+                    dh2T[i * ld + b] = h > 0.0f ? s : 0.0f;
+                }
+            }
+        }
+        __syncthreads();
+        GS_STAMP(1)
         const int nch = Bp / kTile;
         const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
         for (int ch = ch0; ch < ch1; ++ch) {
             const int b = ch * kTile + 4 * lq;
             const float4 a = *reinterpret_cast<const float4 *>(dh2T + li * ld + b);
@@ -548,6 +761,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
         __syncthreads();
+        GS_STAMP(2)
         const int row = tid >> 4, col = tid & 15;
         const float g = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
         float sq = 0.0f;
@@ -557,178 +771,297 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         }
         block_sumsq_store(sq, sumsq + bid, sbuf);
         if (kb == 0) {
-            // db2[n] = sum_b dh2[b, n]: 16 threads per n, then a 16-lane reduction
+            // db2[n] = sum_b dh2[b, n]: 16 partial sums per n in LDS (red), then 16 lanes
             const int i = tid >> 4, j = tid & 15;
             float s = 0.0f;
             for (int b = j; b < Bp; b += 16) s += dh2T[i * ld + b];
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+            red[tid] = s;
+            __syncthreads();
             float sq2 = 0.0f;
-            if (j == 0 && n0 + i < H2) {
-                G[L.ob2 + n0 + i] = s;
-                sq2 = s * s;
-            }
-            block_sumsq_store(sq2, sumsq + nA + nb, sbuf);
-        }
-        return;
-    }
-    bid -= nA;
-    if (bid < nBr) {
-        // ---------------- role B: dh1 tile rows b0..b0+16, cols k0..k0+16 (K = H2)
-        const int rb = bid / nkb, kb = bid - rb * nkb;
-        const int b0 = rb * kTile, k0 = kb * kTile;
-        const int H2p = (H2 + 63) / 64 * 64;
-        const int ld = H2p + 4;
-        float *dh2s = lds;                  // [16][H2p+4]  (b, n)
-        float *red = dh2s + kTile * ld;     // [4][256]
-        float *tile = red + 4 * 256;        // [16][17]
-        for (int u = tid; u < kTile * H2p; u += 256) {
-            const int i = u / H2p, n = u - i * H2p;
-            const int b = b0 + i;
-            float dh = 0.0f;
-            if (b < B && n < H2) {
-                const float hh = h2[(int64_t)b * H2 + n];
-                if (hh > 0.0f) {
-                    const float *dzr = dz + (int64_t)b * A1;
-                    float s = 0.0f;
-                    for (int a = 0; a < A1; ++a) s = fmaf(dzr[a], P[L.head_row(a) + n], s);
-                    dh = s;
+            if (tid < kTile) {
+                float t = 0.0f;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) t += red[tid * 16 + m];
+                if (n0 + tid < H2) {
+                    G[L.ob2 + n0 + tid] = t;
+                    sq2 = t * t;
                 }
             }
-            dh2s[i * ld + n] = dh;
+            block_sumsq_store(sq2, sumsq + sh.nA + nb, sbuf);
         }
-        __syncthreads();
-        const int nch = H2p / kTile;
-        const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
-        const bool colok = k0 + li < H1;
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        for (int ch = ch0; ch < ch1; ++ch) {
-            const int n = ch * kTile + 4 * lq;
-            const float4 a = *reinterpret_cast<const float4 *>(dh2s + li * ld + n);
-            float w[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                w[c] = (colok && n + c < H2) ? P[L.oW2 + (int64_t)(n + c) * H1 + k0 + li] : 0.0f;
-            acc0 = mfma4(a.x, w[0], acc0);
-            acc1 = mfma4(a.y, w[1], acc1);
-            acc0 = mfma4(a.z, w[2], acc0);
-            acc1 = mfma4(a.w, w[3], acc1);
-        }
-        const f32x4 acc = acc0 + acc1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
-        __syncthreads();
-        {
-            const int row = tid >> 4, col = tid & 15;
-            float g = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
-            const int b = b0 + row, k = k0 + col;
-            if (b < B && k < H1) {
-                if (!(h1[(int64_t)b * H1 + k] > 0.0f)) g = 0.0f;
-            } else {
-                g = 0.0f;
-            }
-            tile[row * 17 + col] = g;
-        }
-        __syncthreads();
-        // dW1 / db1 partials over this block's 16 rows
-        for (int u = tid; u < kTile * (D + 1); u += 256) {
-            const int col = u / (D + 1), d = u - col * (D + 1);
-            if (k0 + col >= H1) continue;
-            float s = 0.0f;
-            for (int row = 0; row < kTile; ++row) {
-                const int b = b0 + row;
-                if (b >= B) break;
-                const float xv = d < D ? x[(int64_t)b * D + d] : 1.0f;
-                s = fmaf(tile[row * 17 + col], xv, s);
-            }
-            part1[((int64_t)rb * H1 + k0 + col) * (D + 1) + d] = s;
-        }
+        GS_STAMP_END(3)
         return;
     }
-    bid -= nBr;
+    bid -= sh.nA;
+    if (bid < sh.nB) {
+        // ---------------- role B: dh1 slab rows b0..b0+64, cols k0..k0+16 (K = H2);
+        //                  wave w owns rows b0+16w .. b0+16w+15 with the full K
+        const int rb = bid / sh.nkb, kb = bid - rb * sh.nkb;
+        const int b0 = rb * kRowsB, k0 = kb * kTile;
+        GS_STAMP_BEGIN_IF(4, bid == 0)
+        const int H2p = (H2 + 63) / 64 * 64;
+        const int ld = H2p + 4;
+        float *dh2s = lds;                          // [64][H2p+4]  h2 rows, then dh2
+        float *W2T = dh2s + kRowsB * ld;            // [16][H2p+4]  W2[n][k0+j] -> (j, n)
+        float *whs = W2T + kTile * ld;              // [A1][H2]
+        float *dzs = whs + round4(A1 * H2);         // [64][A1]
+        float *h1m = dzs + round4(kRowsB * A1);     // [64][16]
+        float *xs = h1m + kRowsB * 16;              // [64][D]
+        float *tile = xs + round4(kRowsB * D);      // [64][17]
+        const int n4 = H2p >> 2;
+#pragma unroll 4
+        for (int u = tid; u < kRowsB * n4; u += 256) {
+            const int i = u / n4, c4 = u - i * n4;
+            float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (b0 + i < B && 4 * c4 < H2) hv = *reinterpret_cast<const float4 *>(h2 + (int64_t)(b0 + i) * H2 + 4 * c4);
+            *reinterpret_cast<float4 *>(dh2s + i * ld + 4 * c4) = hv;
+        }
+#pragma unroll 4
+        for (int u = tid; u < H2p * 4; u += 256) {
+            const int n = u >> 2, c4 = u & 3;
+            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n < H2 && k0 + 4 * c4 < H1) w = *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)n * H1 + k0 + 4 * c4);
+            W2T[(4 * c4 + 0) * ld + n] = w.x;
+            W2T[(4 * c4 + 1) * ld + n] = w.y;
+            W2T[(4 * c4 + 2) * ld + n] = w.z;
+            W2T[(4 * c4 + 3) * ld + n] = w.w;
+        }
+        for (int u = tid; u < A1 * H2; u += 256) {
+            const int a = u / H2, n = u - a * H2;
+            whs[u] = P[L.head_row(a) + n];
+        }
+        for (int u = tid; u < kRowsB * A1; u += 256) dzs[u] = b0 * A1 + u < B * A1 ? dz[(int64_t)b0 * A1 + u] : 0.0f;
+        for (int u = tid; u < kRowsB * 16; u += 256) {
+            const int i = u >> 4, j = u & 15;
+            h1m[u] = (b0 + i < B && k0 + j < H1) ? h1[(int64_t)(b0 + i) * H1 + k0 + j] : 0.0f;
+        }
+        for (int u = tid; u < kRowsB * D; u += 256) xs[u] = b0 * D + u < B * D ? x[(int64_t)b0 * D + u] : 0.0f;
+        __syncthreads();
+        GS_STAMP(0)
+        // dh2 = relu'(h2) * (dz . Wh), in place; thread owns hidden unit n, loops the rows
+        for (int n = tid; n < H2; n += 256) {
+            float w[kMaxActions + 1];
+#pragma unroll
+            for (int a = 0; a < kMaxActions + 1; ++a) w[a] = a < A1 ? whs[a * H2 + n] : 0.0f;
+            if (A1 <= 5) {
+#pragma unroll 8
+                for (int i = 0; i < kRowsB; ++i) {
+                    const float h = dh2s[i * ld + n];
+                    float s = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < 5; ++a) s = a < A1 ? fmaf(dzs[i * A1 + a], w[a], s) : s;
+                    dh2s[i * ld + n] = h > 0.0f ? s : 0.0f;
+                }
+            } else {
+                for (int i = 0; i < kRowsB; ++i) {
+                    const float h = dh2s[i * ld + n];
+                    float s = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < kMaxActions + 1; ++a) s = a < A1 ? fmaf(dzs[i * A1 + a], w[a], s) : s;
+                    dh2s[i * ld + n] = h > 0.0f ? s : 0.0f;
+                }
+            }
+        }
+        __syncthreads();
+        GS_STAMP(1)
+        {
+            const int nch = H2p / kTile;
+            const float *arow = dh2s + (wave * 16 + li) * ld;
+            const float *brow = W2T + li * ld;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+            for (int ch = 0; ch < nch; ++ch) {
+                const int n = ch * kTile + 4 * lq;
+                const float4 a = *reinterpret_cast<const float4 *>(arow + n);
+                const float4 w = *reinterpret_cast<const float4 *>(brow + n);
+                acc0 = mfma4(a.x, w.x, acc0);
+                acc1 = mfma4(a.y, w.y, acc1);
+                acc0 = mfma4(a.z, w.z, acc0);
+                acc1 = mfma4(a.w, w.w, acc1);
+            }
+            const f32x4 acc = acc0 + acc1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wave * 16 + lq * 4 + r;
+                const float g = h1m[row * 16 + li] > 0.0f ? acc[r] : 0.0f;   // relu'(h1)
+                tile[row * 17 + li] = g;
+            }
+        }
+        __syncthreads();
+        GS_STAMP(2)
+        // dW1 / db1 partials over this slab's 64 rows: 4 row groups of 16, then combine
+        {
+            float *pr = dh2s;                       // reuse: [4][16*(D+1)]
+            const int nout = kTile * (D + 1);
+            for (int u = tid; u < 4 * nout; u += 256) {
+                const int g = u / nout, o = u - g * nout;
+                const int col = o / (D + 1), d = o - col * (D + 1);
+                float s = 0.0f;
+#pragma unroll 4
+                for (int row = g * 16; row < g * 16 + 16; ++row) {
+                    const float xv = d < D ? xs[row * D + d] : 1.0f;
+                    s = fmaf(tile[row * 17 + col], xv, s);
+                }
+                pr[u] = s;
+            }
+            __syncthreads();
+            for (int o = tid; o < nout; o += 256) {
+                const int col = o / (D + 1), d = o - col * (D + 1);
+                if (k0 + col < H1)
+                    part1[((int64_t)rb * H1 + k0 + col) * (D + 1) + d] =
+                        ((pr[o] + pr[nout + o]) + pr[2 * nout + o]) + pr[3 * nout + o];
+            }
+        }
+        GS_STAMP_END(3)
+        return;
+    }
+    bid -= sh.nB;
     {
         // ---------------- role C: head grads for hidden block nb (+ biases in block 0)
         const int nb = bid;
         const int n0 = nb * kTile;
-        const int Bp = ((int)B + 15) / 16 * 16;
+        const int Bp = (B + 15) / 16 * 16;
+        GS_STAMP_BEGIN_IF(5, bid == 0)
         float *hs = lds;                    // [Bp][17]
         float *dzs = hs + Bp * 17;          // [Bp][A1]
-        for (int u = tid; u < Bp * kTile; u += 256) {
-            const int b = u >> 4, i = u & 15;
-            hs[b * 17 + i] = (b < B && n0 + i < H2) ? h2[(int64_t)b * H2 + n0 + i] : 0.0f;
+#pragma unroll 4
+        for (int u = tid; u < Bp * 4; u += 256) {
+            const int b = u >> 2, c4 = u & 3;
+            float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (b < B && n0 + 4 * c4 < H2) hv = *reinterpret_cast<const float4 *>(h2 + (int64_t)b * H2 + n0 + 4 * c4);
+            hs[b * 17 + 4 * c4 + 0] = hv.x;
+            hs[b * 17 + 4 * c4 + 1] = hv.y;
+            hs[b * 17 + 4 * c4 + 2] = hv.z;
+            hs[b * 17 + 4 * c4 + 3] = hv.w;
         }
-        for (int u = tid; u < Bp * A1; u += 256) {
-            const int b = u / A1;
-            dzs[u] = b < B ? dz[u] : 0.0f;
+        for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
+        __syncthreads();
+        GS_STAMP(0)
+        // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
+        float *partC = dzs + Bp * A1;           // [A1*16][16]
+        const int nout = kTile * A1;
+        for (int u = tid; u < nout * 16; u += 256) {
+            const int o = u >> 4, j = u & 15;
+            const int a = o >> 4, i = o & 15;
+            float s = 0.0f;
+            for (int b = j; b < Bp; b += 16) s = fmaf(dzs[b * A1 + a], hs[b * 17 + i], s);
+            partC[u] = s;
         }
         __syncthreads();
-        const int nout = kTile * A1;
-        int tpo = 1;
-        while (tpo * 2 * nout <= 256 && tpo < 16) tpo *= 2;
         float sq = 0.0f;
-        for (int base = 0; base < nout * tpo; base += 256) {
-            const int u = base + tid;
-            const int o = u / tpo, j = u - o * tpo;
+        for (int o = tid; o < nout; o += 256) {
             float s = 0.0f;
-            const bool ok = o < nout;
-            const int a = ok ? o / kTile : 0, i = ok ? o - a * kTile : 0;
-            if (ok)
-                for (int b = j; b < Bp; b += tpo) s = fmaf(dzs[b * A1 + a], hs[b * 17 + i], s);
-            for (int off = tpo >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-            if (ok && j == 0 && n0 + i < H2) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) s += partC[o * 16 + m];
+            const int a = o >> 4, i = o & 15;
+            if (n0 + i < H2) {
                 G[L.head_row(a) + n0 + i] = s;
                 sq += s * s;
             }
         }
-        block_sumsq_store(sq, sumsq + nA + ncb + nb, sbuf);
+        block_sumsq_store(sq, sumsq + sh.nA + sh.ncb + nb, sbuf);
         if (nb == 0) {
-            float sqb = 0.0f;
-            for (int a = wave; a < A1; a += 4) {
+            __syncthreads();
+            for (int u = tid; u < A1 * 16; u += 256) {
+                const int a = u >> 4, j = u & 15;
                 float s = 0.0f;
-                for (int b = lane; b < Bp; b += 64) s += dzs[b * A1 + a];
-                s = wave_sum(s);
-                if (lane == 0) {
-                    G[L.head_bias(a)] = s;
-                    sqb += s * s;
-                }
+                for (int b = j; b < Bp; b += 16) s += dzs[b * A1 + a];
+                partC[u] = s;
             }
-            block_sumsq_store(sqb, sumsq + nA + 2 * ncb, sbuf);
+            __syncthreads();
+            float sqb = 0.0f;
+            if (tid < A1) {
+                float s = 0.0f;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) s += partC[tid * 16 + m];
+                G[L.head_bias(tid)] = s;
+                sqb = s * s;
+            }
+            block_sumsq_store(sqb, sumsq + sh.nA + 2 * sh.ncb, sbuf);
         }
+        GS_STAMP_END(1)
     }
 }
 
 // ------------------------------------------------------------------------------------
 // k_clip_adam: grid ceil(P / 1024), 256 threads, 4 params per thread (strided).
 // ------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t part1_index(const Layout &L, int64_t p)
+{
+    const int D1 = L.D + 1;
+    if (p < L.ob1) {
+        const int64_t k = p / L.D, d = p - k * L.D;
+        return k * D1 + d;
+    }
+    return (p - L.ob1) * D1 + L.D;
+}
 
-
-__global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layout L, float *__restrict__ G,
+template <class S>
+__global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layout Lrt, float *__restrict__ G,
                                                    float *__restrict__ M, float *__restrict__ V,
                                                    const float *__restrict__ part1, const float *__restrict__ sumsq,
                                                    AdamArgs aa, float *__restrict__ metrics,
                                                    const int32_t *__restrict__ stop)
 {
     if (stop && *stop) return;
-    __shared__ double sred[4];
+    GS_STAMP_BEGIN(3)
+    __shared__ double sred[272];
     __shared__ float s_coef;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int D1 = L.D + 1;
-    const int64_t n1 = (int64_t)L.H1 * D1;
-    // ---- global squared norm (same order in every workgroup -> identical coef)
+    const Layout L = S::lay(Lrt);
+    const int tid = threadIdx.x;
+    const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
+    // ---- this block's parameters and optimizer state: loads issued first
+    const int64_t base = (int64_t)blockIdx.x * 1024;
+    float gv[4], mv[4], vv[4], pv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t p = base + j * 256 + tid;
+        const bool ok = p < L.P;
+        float g = 0.0f;
+        if (ok) {
+            if (aa.nrb > 0 && p < L.oW2) {
+                const int64_t u = part1_index(L, p);
+#pragma unroll 4
+                for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
+            } else {
+                g = G[p];
+            }
+        }
+        gv[j] = g;
+        mv[j] = ok ? M[p] : 0.0f;
+        vv[j] = ok ? V[p] : 0.0f;
+        pv[j] = ok ? Pm[p] : 0.0f;
+    }
+    // ---- global squared norm (same order in every workgroup -> identical coef).  The
+    //      per-tile sums and dW1/db1 partials are staged into LDS in one burst first.
+    extern __shared__ float stage[];
     double ss = 0.0;
-    for (int s = tid; s < aa.n_slots; s += 256) ss += (double)sumsq[s];
-    if (aa.nrb > 0) {
-        for (int64_t u = tid; u < n1; u += 256) {
+    const int64_t npart = (int64_t)aa.nrb * n1;
+    if (aa.stage_lds) {
+        copy_to_lds(stage, sumsq, aa.n_slots);
+        const int off = round4(aa.n_slots);
+        if (npart > 0) copy_to_lds(stage + off, part1, (int)npart);
+        __syncthreads();
+        for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)stage[s0];
+        for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
+            float g = 0.0f;
+            for (int rb = 0; rb < aa.nrb; ++rb) g += stage[off + rb * n1 + u];
+            ss += (double)g * (double)g;
+        }
+    } else {
+        for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)sumsq[s0];
+        for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
             float g = 0.0f;
             for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
             ss += (double)g * (double)g;
         }
     }
-    ss = wave_sum(ss);
-    if (lane == 0) sred[wave] = ss;
-    __syncthreads();
+    GS_STAMP(0)
+    double tt[1] = {ss};
+    block_reduce<1>(tt, sred);
+    GS_STAMP(1)
     if (tid == 0) {
-        const double tot = ((sred[0] + sred[1]) + sred[2]) + sred[3];
+        const double tot = tt[0];
         const float total = (float)sqrt(tot) * aa.grad_scale;
         float coef = 1.0f;
         if (aa.max_norm > 0.0f) {
@@ -742,44 +1075,28 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     const float coef = s_coef * aa.grad_scale;
     const float neg_step = aa.sched ? aa.sched[2 * aa.sched_idx] : aa.neg_step_size;
     const float bc2s = aa.sched ? aa.sched[2 * aa.sched_idx + 1] : aa.bc2_sqrt;
-    // ---- Adam on this block's 1024 parameters
-    const int64_t base = (int64_t)blockIdx.x * 1024;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int64_t p = base + j * 256 + tid;
         if (p >= L.P) break;
-        float g;
-        if (aa.nrb > 0 && p < L.oW2) {
-            // dW1 / db1 live as per-row-block partials: reduce them here
-            int64_t u;
-            if (p < L.ob1) {
-                const int64_t k = p / L.D, d = p - k * L.D;
-                u = k * D1 + d;
-            } else {
-                u = (p - L.ob1) * D1 + L.D;
-            }
-            g = 0.0f;
-            for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
-        } else {
-            g = G[p];
-        }
-        g = g * coef;
+        const float g = gv[j] * coef;
         G[p] = g;
-        float m = M[p], v = V[p];
+        float m = mv[j], v = vv[j];
         m = m + aa.one_minus_b1 * (g - m);            // exp_avg.lerp_(grad, 1 - beta1)
         v = v * aa.b2;                                // exp_avg_sq.mul_(beta2)
         v = v + (aa.one_minus_b2 * g) * g;            //   .addcmul_(grad, grad, 1 - beta2)
         const float denom = sqrtf(v) / bc2s + aa.eps;
-        Pm[p] = Pm[p] + neg_step * (m / denom);
+        Pm[p] = pv[j] + neg_step * (m / denom);
         M[p] = m;
         V[p] = v;
     }
+    GS_STAMP_END(2)
 }
 
 // sum of squares over a flat range (multi-GPU path: norm after the all-reduce)
 __global__ __launch_bounds__(256) void k_sumsq_flat(const float *__restrict__ G, int64_t n, float *__restrict__ out)
 {
-    __shared__ float sbuf[4];
+    __shared__ float sbuf[272];
     float s = 0.0f;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) s += G[i] * G[i];
     block_sumsq_store(s, out + blockIdx.x, sbuf);
@@ -792,15 +1109,8 @@ __global__ __launch_bounds__(256) void k_reduce_part1(const float *__restrict__ 
     if (stop && *stop) return;
     const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= L.oW2) return;
-    const int D1 = L.D + 1;
-    const int64_t n1 = (int64_t)L.H1 * D1;
-    int64_t u;
-    if (p < L.ob1) {
-        const int64_t k = p / L.D, d = p - k * L.D;
-        u = k * D1 + d;
-    } else {
-        u = (p - L.ob1) * D1 + L.D;
-    }
+    const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
+    const int64_t u = part1_index(L, p);
     float g = 0.0f;
     for (int rb = 0; rb < nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
     G[p] = g;
@@ -809,74 +1119,102 @@ __global__ __launch_bounds__(256) void k_reduce_part1(const float *__restrict__ 
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
+// Call f(shape_policy) with the compile-time instantiation matching (L, B), else the
+// runtime fallback.  B <= 0: the minibatch size is not part of the instantiation.
+template <class F>
+static int with_shape(const Layout &L, int64_t B, F &&f)
+{
+    if (L.D == 4 && L.H1 == 256 && L.H2 == 256 && L.A == 2) {        // CartPole-v1:ppo (mlp_medium)
+        if (B == 256) return f(ShapeC<4, 256, 256, 2, 256>{});
+        return f(ShapeC<4, 256, 256, 2, 0>{});
+    }
+    if (L.D == 8 && L.H1 == 128 && L.H2 == 128 && L.A == 4) {        // LunarLander-v3:ppo (mlp_small)
+        if (B == 64) return f(ShapeC<8, 128, 128, 4, 64>{});
+        return f(ShapeC<8, 128, 128, 4, 0>{});
+    }
+    if (L.A <= 4) return f(ShapeR<4>{});
+    return f(ShapeR<kMaxActions>{});
+}
+
+// Raise a kernel's dynamic-LDS limit once (never inside a stream capture: the first
+// eager launch or prepare_kernels() does it before any graph is recorded).
 static int set_lds_limit(const void *fn, size_t bytes)
 {
-    if (bytes > 65536) GS_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    static std::mutex mu;
+    static std::unordered_map<const void *, size_t> done;
+    if (bytes <= 65536) return GS_OK;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = done.find(fn);
+    if (it != done.end() && it->second >= bytes) return GS_OK;
+    GS_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    done[fn] = bytes;
     return GS_OK;
+}
+
+int prepare_kernels(const Layout &L, int64_t B)
+{
+    int rc = with_shape(L, B, [&](auto sh) {
+        return set_lds_limit((const void *)k_bwd<decltype(sh)>, bwd_lds_bytes(L, B));
+    });
+    if (rc) return rc;
+    return with_shape(L, 0, [&](auto sh) {
+        return set_lds_limit((const void *)k_fwd_hidden<decltype(sh)>, fwd_lds_bytes(L));
+    });
 }
 
 int launch_heads_act(const float *P, const Layout &L, const float *zpart, int64_t rows, int mode, uint64_t seed,
                      uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s)
 {
     const dim3 grid((unsigned)((rows + 255) / 256));
-    if (L.A <= 4)
-        hipLaunchKernelGGL(k_heads_act<4>, grid, dim3(256), 0, s, P, L, zpart, rows, mode, seed, counter, actions,
-                           logp, value);
-    else
-        hipLaunchKernelGGL(k_heads_act<kMaxActions>, grid, dim3(256), 0, s, P, L, zpart, rows, mode, seed, counter,
+    return with_shape(L, 0, [&](auto sh) {
+        hipLaunchKernelGGL(k_heads_act<decltype(sh)>, grid, dim3(256), 0, s, P, L, zpart, rows, mode, seed, counter,
                            actions, logp, value);
-    GS_LAUNCH_CHECK("k_heads_act");
-    return GS_OK;
+        GS_LAUNCH_CHECK("k_heads_act");
+        return GS_OK;
+    });
 }
 
-int launch_loss(const float *P, const Layout &L, const float *zpart, int64_t B, const gs_rollout_view &ro,
-                const int32_t *idx, const LossArgs &la, float *dz, float *metrics, int32_t *stop, hipStream_t s)
+int launch_loss(const float *P, const Layout &L, int64_t B, const Workspace &ws, const LossArgs &la, float *metrics,
+                int32_t *stop, hipStream_t s)
 {
-    if (L.A <= 4)
-        hipLaunchKernelGGL(k_loss<4>, dim3(1), dim3(256), 0, s, P, L, zpart, B, ro, idx, la, dz, metrics, stop);
-    else
-        hipLaunchKernelGGL(k_loss<kMaxActions>, dim3(1), dim3(256), 0, s, P, L, zpart, B, ro, idx, la, dz, metrics,
-                           stop);
-    GS_LAUNCH_CHECK("k_loss");
-    return GS_OK;
-}
-
-size_t bwd_lds_bytes(const Layout &L, int64_t B)
-{
-    const int A1 = L.A + 1;
-    const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
-    const int64_t H2p = (L.H2 + 63) / 64 * 64;
-    const int64_t roleA = 2 * kTile * (Bp64 + 4) + 1024;
-    const int64_t roleB = kTile * (H2p + 4) + 1024 + kTile * 17;
-    const int64_t roleC = Bp16 * 17 + Bp16 * A1;
-    int64_t m = roleA;
-    if (roleB > m) m = roleB;
-    if (roleC > m) m = roleC;
-    return (size_t)m * sizeof(float);
+    return with_shape(L, B, [&](auto sh) {
+        hipLaunchKernelGGL(k_loss<decltype(sh)>, dim3(1), dim3(256), 0, s, P, L, ws.zpart, (int)B, ws.f_act,
+                           ws.f_olp, ws.f_ov, ws.f_adv, ws.f_ret, la, ws.dz, metrics, stop);
+        GS_LAUNCH_CHECK("k_loss");
+        return GS_OK;
+    });
 }
 
 int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
                hipStream_t s)
 {
-    const int ncb = n_col_blocks(L.H2), nkb = n_col_blocks(L.H1);
-    const int nrb = (int)((B + kTile - 1) / kTile);
-    const unsigned nblk = (unsigned)(ncb * nkb + nrb * nkb + ncb);
+    const BwdShape sh0 = BwdShape::make(L, (int)B);
+    const unsigned nblk = (unsigned)(sh0.nA + sh0.nB + sh0.nC);
     const size_t lds = bwd_lds_bytes(L, B);
-    int rc = set_lds_limit((const void *)k_bwd, lds);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_bwd, dim3(nblk), dim3(256), lds, s, P, L, B, ws.x, ws.h1, ws.h2, ws.dz, G, ws.part1,
-                       ws.sumsq, stop);
-    GS_LAUNCH_CHECK("k_bwd");
-    return GS_OK;
+    return with_shape(L, B, [&](auto sh) {
+        using Sh = decltype(sh);
+        int rc = set_lds_limit((const void *)k_bwd<Sh>, lds);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_bwd<Sh>, dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2, ws.dz, G,
+                           ws.part1, ws.sumsq, stop);
+        GS_LAUNCH_CHECK("k_bwd");
+        return GS_OK;
+    });
 }
 
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
-                     const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s)
+                     const float *sumsq, const AdamArgs &aa_in, float *metrics, const int32_t *stop, hipStream_t s)
 {
+    AdamArgs aa = aa_in;
+    const size_t stage = sizeof(float) * (round4(aa.n_slots) + (size_t)aa.nrb * L.H1 * (L.D + 1));
+    aa.stage_lds = stage <= 65536 ? 1 : 0;
     const unsigned nblk = (unsigned)((L.P + 1023) / 1024);
-    hipLaunchKernelGGL(k_clip_adam, dim3(nblk), dim3(256), 0, s, P, L, G, M, V, part1, sumsq, aa, metrics, stop);
-    GS_LAUNCH_CHECK("k_clip_adam");
-    return GS_OK;
+    return with_shape(L, 0, [&](auto sh) {
+        hipLaunchKernelGGL(k_clip_adam<decltype(sh)>, dim3(nblk), dim3(256), aa.stage_lds ? stage : 0, s, P, L, G, M,
+                           V, part1, sumsq, aa, metrics, stop);
+        GS_LAUNCH_CHECK("k_clip_adam");
+        return GS_OK;
+    });
 }
 
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s)
@@ -893,5 +1231,14 @@ int launch_sumsq_flat(const float *G, int64_t n, float *out, int nblocks, hipStr
     GS_LAUNCH_CHECK("k_sumsq_flat");
     return GS_OK;
 }
+
+#ifdef GS_STAMPS
+extern "C" int gs_debug_stamps(unsigned long long *acc_out, unsigned long long *cnt_out)
+{
+    GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(g_stamp_acc), sizeof(unsigned long long) * 128));
+    GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(g_stamp_cnt), sizeof(unsigned long long) * 8));
+    return GS_OK;
+}
+#endif
 
 }  // namespace gs

@@ -34,13 +34,18 @@ Workspace carve_workspace(void *base, const Layout &L, int64_t B)
         return r;
     };
     const int A1 = L.A + 1;
-    const int64_t nrb = (B + kTile - 1) / kTile;
+    const int64_t nrb = (B + kRowsB - 1) / kRowsB;
     w.x = take((size_t)B * L.D);
     w.h1 = take((size_t)B * L.H1);
     w.h2 = take((size_t)B * L.H2);
     w.zpart = take((size_t)n_col_blocks(L.H2) * B * A1);
     w.dz = take((size_t)B * A1);
     w.part1 = take((size_t)nrb * L.H1 * (L.D + 1));
+    w.f_act = (int32_t *)take((size_t)B);
+    w.f_olp = take((size_t)B);
+    w.f_ov = take((size_t)B);
+    w.f_adv = take((size_t)B);
+    w.f_ret = take((size_t)B);
     w.n_slots = n_sumsq_slots(L);
     const int comm_slots = 64;
     w.sumsq = take((size_t)(w.n_slots > comm_slots ? w.n_slots : comm_slots));
@@ -61,6 +66,22 @@ static int check_dims(const gs_mlp_dims &d)
 }
 
 static Layout layout_of(const gs_mlp_dims &d) { return Layout::make(d.obs_dim, d.hidden1, d.hidden2, d.n_actions); }
+
+static RowGather gather_of(const gs_rollout_view &ro, const Workspace &ws)
+{
+    RowGather g;
+    g.actions = ro.actions;
+    g.logprobs = ro.logprobs;
+    g.values = ro.values;
+    g.advantages = ro.advantages;
+    g.returns = ro.returns;
+    g.f_act = ws.f_act;
+    g.f_olp = ws.f_olp;
+    g.f_ov = ws.f_ov;
+    g.f_adv = ws.f_adv;
+    g.f_ret = ws.f_ret;
+    return g;
+}
 
 }  // namespace gs
 
@@ -86,7 +107,8 @@ extern "C" int gs_policy_act(const float *params, gs_mlp_dims dims, const float 
     const Layout L = layout_of(dims);
     hipStream_t s = (hipStream_t)stream;
     float *zpart = (float *)scratch;
-    rc = launch_fwd_hidden(params, L, obs, nullptr, 1, N, N, nullptr, nullptr, nullptr, zpart, obs_store, nullptr, s);
+    rc = launch_fwd_hidden(params, L, obs, nullptr, 1, N, N, nullptr, nullptr, nullptr, zpart, obs_store, nullptr,
+                           nullptr, s);
     if (rc) return rc;
     return launch_heads_act(params, L, zpart, N, mode, rng_seed, rng_counter, actions, logp, value, s);
 }
@@ -100,7 +122,8 @@ extern "C" int gs_policy_value(const float *params, gs_mlp_dims dims, const floa
     const Layout L = layout_of(dims);
     hipStream_t s = (hipStream_t)stream;
     float *zpart = (float *)scratch;
-    rc = launch_fwd_hidden(params, L, obs, nullptr, 1, N, N, nullptr, nullptr, nullptr, zpart, nullptr, nullptr, s);
+    rc = launch_fwd_hidden(params, L, obs, nullptr, 1, N, N, nullptr, nullptr, nullptr, zpart, nullptr, nullptr,
+                           nullptr, s);
     if (rc) return rc;
     return launch_heads_act(params, L, zpart, N, 0, 0, 0, nullptr, nullptr, value, s);
 }
@@ -139,7 +162,7 @@ StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, in
     a.aa.eps = hp.adam_eps;
     a.aa.grad_scale = 1.0f;
     a.aa.n_slots = n_sumsq_slots(L);
-    a.aa.nrb = (int)((B + kTile - 1) / kTile);
+    a.aa.nrb = (int)((B + kRowsB - 1) / kRowsB);
     return a;
 }
 
@@ -147,9 +170,10 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
                  const gs_rollout_view &ro, const int32_t *idx, int64_t B, float *metrics, int32_t *stop,
                  const Workspace &ws, gs_comm *comm, hipStream_t s)
 {
-    int rc = launch_fwd_hidden(P, L, ro.obs, idx, ro.T, ro.N, B, ws.x, ws.h1, ws.h2, ws.zpart, nullptr, stop, s);
+    const RowGather rg = gather_of(ro, ws);
+    int rc = launch_fwd_hidden(P, L, ro.obs, idx, ro.T, ro.N, B, ws.x, ws.h1, ws.h2, ws.zpart, nullptr, stop, &rg, s);
     if (rc) return rc;
-    rc = launch_loss(P, L, ws.zpart, B, ro, idx, sa.la, ws.dz, metrics, stop, s);
+    rc = launch_loss(P, L, B, ws, sa.la, metrics, stop, s);
     if (rc) return rc;
     rc = launch_bwd(P, L, B, ws, G, stop, s);
     if (rc) return rc;
@@ -181,6 +205,8 @@ int validate_update(const gs_mlp_dims &dims, const gs_rollout_view &ro, int64_t 
     GS_REQUIRE(ws, "null workspace");
     const Layout L = layout_of(dims);
     GS_REQUIRE(bwd_lds_bytes(L, batch) <= 160 * 1024, "batch %lld too large for the LDS budget", (long long)batch);
+    GS_REQUIRE(fwd_lds_bytes(L) <= 160 * 1024, "obs_dim x hidden1 too large for the LDS budget");
+    GS_REQUIRE(ro.T * ro.N < (int64_t)1 << 31, "rollout larger than 2^31 samples");
     return GS_OK;
 }
 
@@ -212,10 +238,11 @@ extern "C" int gs_ppo_loss(const float *params, gs_mlp_dims dims, gs_ppo_hparams
     const Workspace ws = carve_workspace(workspace, L, batch);
     const StepArgs sa = make_step_args(hp, L, batch, 1);
     hipStream_t s = (hipStream_t)stream;
+    const RowGather rg = gather_of(ro, ws);
     rc = launch_fwd_hidden(params, L, ro.obs, idx, ro.T, ro.N, batch, ws.x, ws.h1, ws.h2, ws.zpart, nullptr,
-                           nullptr, s);
+                           nullptr, &rg, s);
     if (rc) return rc;
-    return launch_loss(params, L, ws.zpart, batch, ro, idx, sa.la, ws.dz, metrics, nullptr, s);
+    return launch_loss(params, L, batch, ws, sa.la, metrics, nullptr, s);
 }
 
 extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
@@ -230,11 +257,13 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
     const StepArgs sa = make_step_args(hp, L, batch, adam_step < 1 ? 1 : adam_step);
     hipStream_t s = (hipStream_t)stream;
     switch (stage) {
-    case 0:
+    case 0: {
+        const RowGather rg = gather_of(ro, ws);
         return launch_fwd_hidden(params, L, ro.obs, idx, ro.T, ro.N, batch, ws.x, ws.h1, ws.h2, ws.zpart, nullptr,
-                                 nullptr, s);
+                                 nullptr, &rg, s);
+    }
     case 1:
-        return launch_loss(params, L, ws.zpart, batch, ro, idx, sa.la, ws.dz, metrics, nullptr, s);
+        return launch_loss(params, L, batch, ws, sa.la, metrics, nullptr, s);
     case 2:
         return launch_bwd(params, L, batch, ws, grads, nullptr, s);
     default:
@@ -318,24 +347,32 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     std::lock_guard<std::mutex> lk(g_graph_mu);
     auto it = g_graphs.find(key);
     if (it == g_graphs.end()) {
+        rc = prepare_kernels(L, batch);   // function attributes may not change inside a capture
+        if (rc) return rc;
         GraphEntry ent{};
         GS_HIP(hipMalloc(&ent.sched, sizeof(float) * 2 * (size_t)n_minibatches));
+        // capture on a private stream (the caller's may be the legacy NULL stream, which
+        // cannot capture); the instantiated graph is then launched on the caller's stream
+        hipStream_t cs;
+        GS_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
         hipGraph_t g;
-        GS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        GS_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
         for (int64_t k = 0; k < n_minibatches; ++k) {
             StepArgs sa = make_step_args(hp, L, batch, 1);
             sa.aa.sched = ent.sched;
             sa.aa.sched_idx = (int)k;
             rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
-                              metrics + k * GS_NUM_METRICS, stop_flag, ws, nullptr, s);
+                              metrics + k * GS_NUM_METRICS, stop_flag, ws, nullptr, cs);
             if (rc) {
                 hipGraph_t dummy;
-                (void)hipStreamEndCapture(s, &dummy);
+                (void)hipStreamEndCapture(cs, &dummy);
+                (void)hipStreamDestroy(cs);
                 (void)hipFree(ent.sched);
                 return rc;
             }
         }
-        GS_HIP(hipStreamEndCapture(s, &g));
+        GS_HIP(hipStreamEndCapture(cs, &g));
+        GS_HIP(hipStreamDestroy(cs));
         GS_HIP(hipGraphInstantiate(&ent.exec, g, nullptr, nullptr, 0));
         GS_HIP(hipGraphDestroy(g));
         it = g_graphs.emplace(key, ent).first;

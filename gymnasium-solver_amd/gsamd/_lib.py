@@ -12,7 +12,8 @@ import os
 
 import torch  # noqa: F401  (load torch's HIP runtime before the library)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
+# GSAMD_LIB selects a diagnostic build of the same library (tools/ phase-timer variant)
+LIB_PATH = os.environ.get("GSAMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
 
 GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
 GS_NUM_METRICS = 16

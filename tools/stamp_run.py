@@ -1,0 +1,56 @@
+"""Diagnostic: per-phase cycle breakdown of the minibatch kernels (GS_STAMPS build).
+
+Usage (on the GPU box):  python tools/stamp_run.py
+Builds nothing; expects tools/libgsamd_stamps.so (made by `python tools/stamp_run.py --build` here).
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gymnasium-solver_amd")]
+VARIANT = os.path.join(ROOT, "tools", "libgsamd_stamps.so")
+
+if "--build" in sys.argv:
+    import build_lib
+    build_lib.build_variant(VARIANT, ["GS_STAMPS"])
+    print("built", VARIANT)
+    sys.exit(0)
+
+os.environ["GSAMD_LIB"] = VARIANT
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from gsamd import _lib  # noqa: E402
+from gsamd.config import load_config  # noqa: E402
+from gsamd.ppo_agent import DevicePPOAgent  # noqa: E402
+
+_lib.lib.gs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+torch.manual_seed(42)
+cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+agent = DevicePPOAgent(cfg, device="cuda:0", use_graph=True, track_stats=False)
+agent.train_epoch()
+torch.cuda.synchronize()
+acc0 = np.zeros(128, np.uint64)
+cnt0 = np.zeros(8, np.uint64)
+_lib.lib.gs_debug_stamps(acc0.ctypes.data, cnt0.ctypes.data)
+agent.train_epoch()
+torch.cuda.synchronize()
+acc = np.zeros(128, np.uint64)
+cnt = np.zeros(8, np.uint64)
+_lib.lib.gs_debug_stamps(acc.ctypes.data, cnt.ctypes.data)
+acc = (acc - acc0).reshape(8, 16).astype(np.float64)
+cnt = (cnt - cnt0).astype(np.float64)
+names = {0: ("k_fwd_hidden", ["load operands", "row gather", "h1", "mfma h2", "h2 out + heads"]),
+         1: ("k_loss", ["inputs + adv norm", "per-row loss/grad", "reduce", "metrics"]),
+         2: ("k_bwd roleA blk0", ["load tiles", "dh2", "mfma dW2", "store + sumsq + db2"]),
+         3: ("k_clip_adam blk0", ["loads + norm partial", "reduce", "adam"]),
+         4: ("k_bwd roleB blk0", ["load slab", "dh2", "mfma dh1", "dW1 partial"]),
+         5: ("k_bwd roleC blk0", ["load", "reduce + store"])}
+for k, (n, phases) in names.items():
+    if cnt[k] == 0:
+        continue
+    per = acc[k] / cnt[k]
+    tot = per[:len(phases)].sum()
+    print(f"{n:18s} launches {int(cnt[k]):6d}  total {tot:8.0f} cyc = {tot / 2.4e3:6.2f} us")
+    for i, ph in enumerate(phases):
+        print(f"    {ph:24s} {per[i]:8.0f} cyc  {per[i] / 2.4e3:6.2f} us")
