@@ -50,8 +50,9 @@ def stage_flops_bytes(D, H1, H2, A, B, P):
 
 
 def time_stages(agent, reps: int):
-    """Average device duration of each minibatch-step kernel, by events on the stream
-    the kernels are launched on (torch's current stream is passed to the C-ABI)."""
+    """Average device duration of each minibatch-step kernel: `reps` launches of one stage
+    captured into a hipGraph (no host launch gaps) and replayed between HIP events recorded on
+    the stream the kernels are launched on (the capture stream's replay target)."""
     from gsamd._lib import check, lib
     coll = agent.get_rollout_collector("train")
     idx = agent.prefetcher.device_buf
@@ -63,15 +64,21 @@ def time_stages(agent, reps: int):
     saved = [t.clone() for t in (pm.params, agent.grads, agent.adam_m, agent.adam_v)]
     out = {}
     for st, name in enumerate(("fwd", "loss", "bwd", "adam")):
-        for _ in range(5):
+        for _ in range(3):
             check(lib.gs_ppo_stage(*args(st)), "gs_ppo_stage")
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for _ in range(reps):
+                check(lib.gs_ppo_stage(*args(st)), "gs_ppo_stage")
+        g.replay()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(reps):
-            check(lib.gs_ppo_stage(*args(st)), "gs_ppo_stage")
+        g.replay()
         e1.record()
         e1.synchronize()
         out[name] = e0.elapsed_time(e1) / reps * 1e3   # microseconds per launch
+        del g
     for t, s in zip((pm.params, agent.grads, agent.adam_m, agent.adam_v), saved):
         t.copy_(s)
     return out
@@ -84,6 +91,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n-envs", type=int, default=4096, help="envs per GPU (weak scaling)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of the hipGraph")
+    ap.add_argument("--local-comm", action="store_true",
+                    help="N=1 only: run the multi-GPU chain through a one-rank RCCL communicator")
     ap.add_argument("--stage-reps", type=int, default=200)
     ap.add_argument("--cpu-minibatches", type=int, default=2000,
                     help="minibatches in the bounded CPU-baseline sample (0 disables)")
@@ -96,20 +105,13 @@ def main():
     device = torch.device(f"cuda:{local_rank}")
     comm = None
     if world > 1:
-        import ctypes
-
         import torch.distributed as dist
-        from gsamd._lib import check, lib
+        from gsamd.distributed import init_device_comm
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
-        uid = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            check(lib.gs_comm_unique_id(uid.data_ptr()), "gs_comm_unique_id")
-        uid_d = uid.to(device)
-        dist.broadcast(uid_d, 0)
-        uid = uid_d.cpu().contiguous()
-        h = ctypes.c_void_p()
-        check(lib.gs_comm_init(uid.data_ptr(), world, rank, ctypes.byref(h)), "gs_comm_init")
-        comm = h.value
+        comm = init_device_comm(rank, world, device)
+    elif args.local_comm:
+        from gsamd.distributed import init_local_comm
+        comm = init_local_comm()
 
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
@@ -130,11 +132,16 @@ def main():
         agent.train_epoch()
     barrier()
     _log(f"[bench] rank {rank}: warmup {args.warmup} steps {time.perf_counter() - tw:.2f}s")
+    agent.phase_events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         agent.train_epoch()
     barrier()
     elapsed = time.perf_counter() - t0
+    phases = agent.phase_events
+    agent.phase_events = None
+    collect_ms = sum(e[0].elapsed_time(e[1]) for e in phases) / len(phases)
+    update_ms = sum(e[1].elapsed_time(e[2]) for e in phases) / len(phases)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -197,9 +204,15 @@ def main():
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph},
             "roofline": roofline,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},
+            "phases_ms": {"collect": round(collect_ms, 3), "update": round(update_ms, 3),
+                          "update_us_per_minibatch": round(update_ms * 1e3 / agent.n_minibatches, 3)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        from gsamd.distributed import destroy_comm
+        del agent
+        destroy_comm(comm)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -321,7 +321,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     // torch.optim.Adam's single-tensor path does) change every step; eager launches pass
     // them as kernel arguments, the graph reads them from a per-step device table that
     // is refreshed before each replay, so one capture serves every rollout.
-    if (!use_graph || comm) {
+    if (!use_graph) {
         for (int64_t k = 0; k < n_minibatches; ++k) {
             const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
             rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
@@ -338,7 +338,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     key.n[1] = n_minibatches;
     key.n[2] = ((int64_t)dims.obs_dim << 48) ^ ((int64_t)dims.hidden1 << 32) ^ ((int64_t)dims.hidden2 << 16) ^ dims.n_actions;
     key.n[3] = (int64_t)(intptr_t)workspace;
-    key.n[4] = (int64_t)(intptr_t)stop_flag;
+    key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1);
     key.n[5] = ro.T * 1000003 + ro.N;
     // host-side hyper-parameters are baked into the capture: include them in the key
     uint32_t hbits[12];
@@ -362,7 +362,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
             sa.aa.sched = ent.sched;
             sa.aa.sched_idx = (int)k;
             rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
-                              metrics + k * GS_NUM_METRICS, stop_flag, ws, nullptr, cs);
+                              metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
             if (rc) {
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(cs, &dummy);

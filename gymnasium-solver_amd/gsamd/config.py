@@ -210,3 +210,18 @@ def apply_overrides(cfg: PPOConfig, overrides: Dict[str, Any]) -> PPOConfig:
     cfg._resolve_batch_size()
     cfg.validate()
     return cfg
+
+
+def from_reference_config(cfg: Any, **extras) -> PPOConfig:
+    """Adapt the reference's own Config/PPOConfig object (utils/config.py:17-885) — whatever
+    ``agents.build_agent`` received from ``train.py`` — into a PPOConfig, reading the
+    fields this path uses by name (enums are reduced to their ``value``)."""
+    if isinstance(cfg, PPOConfig):
+        return apply_overrides(cfg, extras) if extras else cfg
+    kw: Dict[str, Any] = {}
+    for name in _FIELDS:
+        if hasattr(cfg, name):
+            v = getattr(cfg, name)
+            kw[name] = getattr(v, "value", v)
+    kw.update(extras)
+    return PPOConfig(**kw)

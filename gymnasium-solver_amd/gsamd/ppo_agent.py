@@ -61,6 +61,8 @@ class DevicePPOAgent:
         self._envs: Dict[str, Any] = {}
         self._rollout_collectors: Dict[str, DeviceRolloutCollector] = {}
         self.metrics_history = []
+        # optional per-epoch (start, update-start, end) events on the launch stream (bench.py)
+        self.phase_events = None
         self.build_env("train", env)
         self.build_models()
         self.build_rollout_collector("train")
@@ -169,6 +171,10 @@ class DevicePPOAgent:
         """One reference epoch: rollout (epoch > 0) + n_epochs passes of minibatch steps."""
         epoch = self.current_epoch
         collector = self.get_rollout_collector("train")
+        ev = self.phase_events
+        if ev is not None:
+            ev.append([torch.cuda.Event(enable_timing=True) for _ in range(3)])
+            ev[-1][0].record()
         if epoch == 0 and collector.total_rollouts == 0:
             self._trajectories = collector.collect()
         elif epoch > 0:
@@ -176,11 +182,15 @@ class DevicePPOAgent:
         idx = self.prefetcher.upload(epoch)
         self.prefetcher.prefetch(epoch + 1)
         buf = collector.buffer
+        if ev is not None:
+            ev[-1][1].record()
         check(lib.gs_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
                                 self.policy_model.dims, self.hparams(), buf.view(), ptr(idx), self.batch_size,
                                 self.n_minibatches, self.adam_step, ptr(self.metrics_buf), ptr(self.stop_flag),
                                 ptr(self.workspace), self.comm, 1 if self.use_graph else 0, stream_handle()),
               "gs_ppo_update")
+        if ev is not None:
+            ev[-1][2].record()
         self.adam_step += self.n_minibatches
         self.current_epoch += 1
 
@@ -230,10 +240,13 @@ class DevicePPOAgent:
 
 
 def build_agent(config, *args, **kwargs):
-    """agents/__init__.py:1-8 for the device path."""
-    if config.algo_id != "ppo":
-        raise ValueError(f"device path implements algo_id 'ppo' only, got {config.algo_id!r}")
-    return DevicePPOAgent(config, *args, **kwargs)
+    """agents/__init__.py:1-8 for the device path.  Accepts a gsamd PPOConfig or the
+    reference's own Config object (adapted by name, gsamd.config.from_reference_config)."""
+    from .config import from_reference_config
+    algo = getattr(getattr(config, "algo_id", None), "value", getattr(config, "algo_id", None))
+    if algo != "ppo":
+        raise ValueError(f"device path implements algo_id 'ppo' only, got {algo!r}")
+    return DevicePPOAgent(from_reference_config(config), *args, **kwargs)
 
 
 _ = ctypes

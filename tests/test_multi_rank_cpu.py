@@ -1,0 +1,32 @@
+"""CPU, world_size 2 (gloo): the multi-GPU protocol of the device path."""
+import multiprocessing as mp
+import os
+import socket
+
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("world", [2])
+def test_data_parallel_protocol_gloo(tmp_path, world):
+    from _dist_workers import dp_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=dp_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    codes = [p.exitcode for p in procs]
+    assert codes == [0] * world, codes
+    assert sorted(os.listdir(tmp_path)) == [f"ok{r}" for r in range(world)]

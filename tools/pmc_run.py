@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Workload for the rocprofv3 --pmc passes (profiles/pmc_traffic.json): one C2 rollout, then
+`--reps` eager launches of each minibatch-step kernel through gs_ppo_stage (no hipGraph, so
+every dispatch is a separate counter record).  Run under
+  rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d DIR -o pmc_fetch -- python tools/pmc_run.py
+  rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d DIR -o pmc_write -- python tools/pmc_run.py
+and reduce with tools/pmc_summarize.py."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "gymnasium-solver_amd")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=64)
+    ap.add_argument("--n-envs", type=int, default=4096)
+    a = ap.parse_args()
+    from gsamd._lib import check, lib
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=a.n_envs, n_epochs=1))
+    agent = DevicePPOAgent(cfg, device="cuda:0", use_graph=False, track_stats=False)
+    agent.train_epoch()
+    pm = agent.policy_model
+    idx = agent.prefetcher.device_buf
+    for st in range(4):
+        for _ in range(a.reps):
+            check(lib.gs_ppo_stage(st, pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                                   agent.adam_v.data_ptr(), pm.dims, agent.hparams(),
+                                   agent.get_rollout_collector("train").buffer.view(), idx.data_ptr(),
+                                   agent.batch_size, 1, agent.metrics_buf.data_ptr(), agent.workspace.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream), "gs_ppo_stage")
+    torch.cuda.synchronize()
+    print("pmc_run done")
+
+
+if __name__ == "__main__":
+    main()
