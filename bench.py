@@ -89,7 +89,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n-envs", type=int, default=4096, help="envs per GPU (weak scaling)")
+    ap.add_argument("--workload", choices=("C2", "C3"), default="C2",
+                    help="C2: CartPole-v1:ppo (the metric's config); C3: LunarLander-v3:ppo shapes (T=2048, B=64)")
+    ap.add_argument("--n-envs", type=int, default=None, help="envs per GPU (weak scaling); C2 4096, C3 1024")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of the hipGraph")
     ap.add_argument("--local-comm", action="store_true",
                     help="N=1 only: run the multi-GPU chain through a one-rank RCCL communicator")
@@ -116,7 +118,9 @@ def main():
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=args.n_envs))
+    env_id = "CartPole-v1" if args.workload == "C2" else "LunarLander-v3"
+    n_envs = args.n_envs or (4096 if args.workload == "C2" else 1024)
+    cfg = load_config(env_id, "ppo", overrides=dict(n_envs=n_envs))
     agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world, comm=comm,
                            use_graph=not args.no_graph, track_stats=False)
     N, T = cfg.n_envs, cfg.n_steps
@@ -172,7 +176,7 @@ def main():
     roofline["avg_us"] = round(stage_us[dom], 3)
     roofline["work_per_launch"] = amount
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and args.workload == "C2":   # the committed PMC passes are C2-shaped
         try:
             with open(pmc_path) as f:
                 roofline["traffic"] = json.load(f).get(roofline["kernel"], {}).get("hbm_bytes_per_launch")
@@ -185,6 +189,8 @@ def main():
         from oracle.cpu_ppo import run_cpu_baseline
         cores = min(len(os.sched_getaffinity(0)), 16)
         r = run_cpu_baseline(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,
+                             obs_dim=pm.obs_dim, hidden=tuple(pm.hidden_dims), n_actions=pm.n_actions,
+                             gamma=cfg.gamma, lam=cfg.gae_lambda, clip=cfg.clip_range, lr=cfg.policy_lr,
                              max_minibatches=args.cpu_minibatches, threads=cores)
         cpu = {"value": round(r["env_steps_per_s"], 2), "unit": "env_steps/s", "cores": r["threads"], "kind": "port",
                "sample": (f"1 rollout of {N}x{T} env steps (torch-CPU policy, numpy synthetic env, numpy GAE) + "
@@ -198,9 +204,10 @@ def main():
             "value": round(value, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "CartPole-v1:ppo C2 (rollout 4096 envs x 32 steps + 20-epoch PPO update, B=256)",
+            "config": {"workload": (f"{env_id}:ppo {args.workload} (rollout {N} envs x {T} steps + "
+                                    f"{cfg.n_epochs}-epoch PPO update, B={cfg.batch_size})"),
                        "n_envs_per_gpu": N, "n_steps": T, "batch_size": cfg.batch_size, "n_epochs": cfg.n_epochs,
-                       "minibatches_per_step": agent.n_minibatches, "policy": "MLP 4-256-256-{2,1}",
+                       "minibatches_per_step": agent.n_minibatches, "policy": f"MLP {pm.obs_dim}-{pm.hidden_dims[0]}-{pm.hidden_dims[1]}-{{{pm.n_actions},1}}",
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph},
             "roofline": roofline,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},

@@ -133,6 +133,7 @@ struct RowGather {
     const float *logprobs, *values, *advantages, *returns;
     int32_t *f_act;
     float *f_olp, *f_ov, *f_adv, *f_ret;
+    const int64_t *step_base;   // graph chunk replay: minibatch offset read on device (null: 0)
 };
 Workspace carve_workspace(void *base, const Layout &L, int64_t B);
 
@@ -141,6 +142,7 @@ struct LossArgs {
     float clip_vf;              // f32(clip_range_vf)
     float vf_coef, ent_coef;
     float target_kl;            // <= 0: None
+    const int64_t *step_base;   // graph chunk replay: metrics record offset (null: 0)
     int normalize;
 };
 
@@ -157,6 +159,7 @@ struct AdamArgs {
     int nrb;                // dW1/db1 partial row blocks (0: grads already final in G)
     const float *sched;     // optional device table {neg_step_size, bc2_sqrt} per step (graph replay)
     int sched_idx;
+    const int64_t *step_base;   // graph chunk replay: added to sched_idx and the metrics record
     int stage_lds;          // set by the launcher: stage slots + partials through LDS
 };
 

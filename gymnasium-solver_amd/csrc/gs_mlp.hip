@@ -155,6 +155,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     float *red = h1s + kTile * ldh;
     float *h2s = red + 1024;
 
+    if (rg.step_base && idx) idx += *rg.step_base * rows;
     // ---- phase 0: every operand of this workgroup, all loads in flight together.
     //      Threads 0..15 run the dependent idx -> row -> obs/fields chain while the rest
     //      of the block streams the weights into LDS.
@@ -467,6 +468,7 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
     const Layout L = S::lay(Lrt);
     const int B = S::batch(Brt);
     const int tid = threadIdx.x;
+    if (la.step_base) metrics += *la.step_base * GS_NUM_METRICS;
     GS_STAMP_BEGIN(1)
     if (stop && *stop) {
         if (tid == 0) {
@@ -1005,6 +1007,8 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
 {
     if (stop && *stop) return;
     GS_STAMP_BEGIN(3)
+    const int64_t kb = aa.step_base ? *aa.step_base : 0;
+    if (metrics) metrics += kb * GS_NUM_METRICS;
     __shared__ double sred[272];
     __shared__ float s_coef;
     const Layout L = S::lay(Lrt);
@@ -1073,8 +1077,8 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     }
     __syncthreads();
     const float coef = s_coef * aa.grad_scale;
-    const float neg_step = aa.sched ? aa.sched[2 * aa.sched_idx] : aa.neg_step_size;
-    const float bc2s = aa.sched ? aa.sched[2 * aa.sched_idx + 1] : aa.bc2_sqrt;
+    const float neg_step = aa.sched ? aa.sched[2 * (aa.sched_idx + kb)] : aa.neg_step_size;
+    const float bc2s = aa.sched ? aa.sched[2 * (aa.sched_idx + kb) + 1] : aa.bc2_sqrt;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int64_t p = base + j * 256 + tid;

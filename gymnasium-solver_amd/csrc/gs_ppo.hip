@@ -69,7 +69,7 @@ static Layout layout_of(const gs_mlp_dims &d) { return Layout::make(d.obs_dim, d
 
 static RowGather gather_of(const gs_rollout_view &ro, const Workspace &ws)
 {
-    RowGather g;
+    RowGather g{};
     g.actions = ro.actions;
     g.logprobs = ro.logprobs;
     g.values = ro.values;
@@ -170,7 +170,8 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
                  const gs_rollout_view &ro, const int32_t *idx, int64_t B, float *metrics, int32_t *stop,
                  const Workspace &ws, gs_comm *comm, hipStream_t s)
 {
-    const RowGather rg = gather_of(ro, ws);
+    RowGather rg = gather_of(ro, ws);
+    rg.step_base = sa.la.step_base;
     int rc = launch_fwd_hidden(P, L, ro.obs, idx, ro.T, ro.N, B, ws.x, ws.h1, ws.h2, ws.zpart, nullptr, stop, &rg, s);
     if (rc) return rc;
     rc = launch_loss(P, L, B, ws, sa.la, metrics, stop, s);
@@ -297,7 +298,11 @@ struct GraphKeyHash {
 };
 struct GraphEntry {
     hipGraphExec_t exec;
-    float *sched;
+    float *sched;      // per-step {neg_step_size, bc2_sqrt}, n_minibatches entries
+    int64_t *base;     // first minibatch of the replayed chunk (device scalar)
+    int64_t *hbase;    // pinned host table r * chunk, the source of each replay's base copy
+    float *hsched;     // pinned staging for the schedule table
+    hipEvent_t sched_copied;   // the last copy out of hsched (hsched is rewritten after it)
 };
 std::mutex g_graph_mu;
 std::unordered_map<GraphKey, GraphEntry, GraphKeyHash> g_graphs;
@@ -330,6 +335,13 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         }
         return GS_OK;
     }
+    // One graph holds a chunk of kChunk minibatch steps; it is replayed n / kChunk times
+    // with the chunk's first minibatch index in a device scalar (step_base) that the
+    // kernels add to their index-stream, metrics and Adam-schedule offsets.  The tail
+    // (n % kChunk steps) runs eagerly.  Graph size stays bounded for C3's 327 680 steps.
+    constexpr int64_t kChunk = 512;
+    const int64_t chunk = n_minibatches < kChunk ? n_minibatches : kChunk;
+    const int64_t n_full = n_minibatches / chunk;
     GraphKey key{};
     const void *ptrs[12] = {params, grads, adam_m, adam_v, ro.obs, ro.actions, ro.logprobs, ro.values,
                             ro.advantages, ro.returns, idx, metrics};
@@ -350,17 +362,25 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         rc = prepare_kernels(L, batch);   // function attributes may not change inside a capture
         if (rc) return rc;
         GraphEntry ent{};
-        GS_HIP(hipMalloc(&ent.sched, sizeof(float) * 2 * (size_t)n_minibatches));
+        GS_HIP(hipMalloc(&ent.sched, sizeof(float) * 2 * (size_t)n_minibatches + 64));
+        ent.base = (int64_t *)((char *)ent.sched + sizeof(float) * 2 * (size_t)n_minibatches);
+        // pinned and never rewritten: an async copy may read it whenever it executes
+        GS_HIP(hipHostMalloc((void **)&ent.hbase, sizeof(int64_t) * (size_t)(n_full + 1), hipHostMallocDefault));
+        for (int64_t r = 0; r <= n_full; ++r) ent.hbase[r] = r * chunk;
+        GS_HIP(hipHostMalloc((void **)&ent.hsched, sizeof(float) * 2 * (size_t)n_minibatches, hipHostMallocDefault));
+        GS_HIP(hipEventCreateWithFlags(&ent.sched_copied, hipEventDisableTiming));
         // capture on a private stream (the caller's may be the legacy NULL stream, which
         // cannot capture); the instantiated graph is then launched on the caller's stream
         hipStream_t cs;
         GS_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
         hipGraph_t g;
         GS_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-        for (int64_t k = 0; k < n_minibatches; ++k) {
+        for (int64_t k = 0; k < chunk; ++k) {
             StepArgs sa = make_step_args(hp, L, batch, 1);
             sa.aa.sched = ent.sched;
             sa.aa.sched_idx = (int)k;
+            sa.aa.step_base = ent.base;
+            sa.la.step_base = ent.base;
             rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
                               metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
             if (rc) {
@@ -368,6 +388,9 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
                 (void)hipStreamEndCapture(cs, &dummy);
                 (void)hipStreamDestroy(cs);
                 (void)hipFree(ent.sched);
+                (void)hipHostFree(ent.hbase);
+                (void)hipHostFree(ent.hsched);
+                (void)hipEventDestroy(ent.sched_copied);
                 return rc;
             }
         }
@@ -377,14 +400,24 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         GS_HIP(hipGraphDestroy(g));
         it = g_graphs.emplace(key, ent).first;
     }
-    std::vector<float> tab(2 * (size_t)n_minibatches);
+    GraphEntry &e = it->second;
+    GS_HIP(hipEventSynchronize(e.sched_copied));   // the previous call's copy has read hsched
     for (int64_t k = 0; k < n_minibatches; ++k) {
         const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
-        tab[2 * k] = sa.aa.neg_step_size;
-        tab[2 * k + 1] = sa.aa.bc2_sqrt;
+        e.hsched[2 * k] = sa.aa.neg_step_size;
+        e.hsched[2 * k + 1] = sa.aa.bc2_sqrt;
     }
-    // pageable source: the runtime stages it before returning, so `tab` may die here
-    GS_HIP(hipMemcpyAsync(it->second.sched, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
-    GS_HIP(hipGraphLaunch(it->second.exec, s));
+    GS_HIP(hipMemcpyAsync(e.sched, e.hsched, sizeof(float) * 2 * (size_t)n_minibatches, hipMemcpyHostToDevice, s));
+    GS_HIP(hipEventRecord(e.sched_copied, s));
+    for (int64_t r = 0; r < n_full; ++r) {
+        GS_HIP(hipMemcpyAsync(it->second.base, it->second.hbase + r, sizeof(int64_t), hipMemcpyHostToDevice, s));
+        GS_HIP(hipGraphLaunch(it->second.exec, s));
+    }
+    for (int64_t k = n_full * chunk; k < n_minibatches; ++k) {
+        const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
+        rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                          metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
+        if (rc) return rc;
+    }
     return GS_OK;
 }

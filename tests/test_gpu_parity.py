@@ -221,32 +221,41 @@ def test_trajectory_replay_vs_reference(golden, cuda):
 
 
 # ------------------------------------------------------------------------------- full-size properties
-def test_c2_update_graph_equals_eager_and_is_deterministic(cuda):
-    """BASELINE config C2 shape: graph replay == eager launches, bitwise, and a rerun is identical."""
+# (env, variant, n_envs): C2 at full size; C3 shape (T=2048, B=64, E=10) at 32 envs
+CASES = [("CartPole-v1", "ppo", 4096), ("LunarLander-v3", "ppo", 32)]
+
+
+@pytest.mark.parametrize("env,variant,n_envs", CASES)
+def test_update_graph_equals_eager_and_is_deterministic(cuda, env, variant, n_envs):
+    """BASELINE configs C2/C3 shapes: chunked graph replay == eager launches, bitwise, and a
+    rerun is identical (C3: 10 240 minibatches = 20 replays of a 512-step chunk)."""
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     results = []
     for use_graph in (False, True, True):
         torch.manual_seed(42)
-        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+        cfg = load_config(env, variant, overrides=dict(n_envs=n_envs))
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
         agent.train_epoch()
         agent.train_epoch()
         torch.cuda.synchronize()
         results.append((agent.policy_model.params.cpu().numpy(), agent.minibatch_losses()))
         assert np.isfinite(results[-1][1]).all()
+        del agent
     for p, l in results[1:]:
         assert np.array_equal(p.view(np.uint32), results[0][0].view(np.uint32))
         assert np.array_equal(l, results[0][1])
 
 
-def test_c2_minibatch_step_vs_numpy_oracle(cuda):
-    """One C2-shaped minibatch (B=256 rows of a 4096x32 device rollout) against the numpy oracle."""
+@pytest.mark.parametrize("env,variant,n_envs", CASES)
+def test_minibatch_step_vs_numpy_oracle(cuda, env, variant, n_envs):
+    """One C2/C3-shaped minibatch of a device rollout against the numpy oracle (loss 1e-5 rel,
+    clipped grads 1e-6 of max, params after Adam 5e-6)."""
     from oracle import ppo_ref as R
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+    cfg = load_config(env, variant, overrides=dict(n_envs=n_envs))
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
     batches = agent.train_dataloader()
     traj = agent._trajectories
@@ -256,10 +265,12 @@ def test_c2_minibatch_step_vs_numpy_oracle(cuda):
     obs = traj.observations.cpu().numpy()[idx]
     args = [traj.actions.cpu().numpy()[idx], traj.logprobs.cpu().numpy()[idx], traj.values.cpu().numpy()[idx],
             traj.advantages.cpu().numpy()[idx], traj.returns.cpu().numpy()[idx]]
-    dims = (4, 256, 256, 2)
-    loss, met, g = R.ppo_loss_and_grads(p0, dims, obs, *args, clip=0.1, clip_vf=0.2, vf_coef=0.5, ent_coef=0.0)
-    gc, total = R.clip_grad_norm(g, dims, 0.5)
-    p1, _, _ = R.adam_step(p0, gc, np.zeros_like(gc), np.zeros_like(gc), 1, 1e-3)
+    pm = agent.policy_model
+    dims = (pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions)
+    loss, met, g = R.ppo_loss_and_grads(p0, dims, obs, *args, clip=cfg.clip_range, clip_vf=cfg.clip_range_vf,
+                                        vf_coef=cfg.vf_coef, ent_coef=cfg.ent_coef)
+    gc, total = R.clip_grad_norm(g, dims, cfg.max_grad_norm)
+    p1, _, _ = R.adam_step(p0, gc, np.zeros_like(gc), np.zeros_like(gc), 1, cfg.policy_lr)
     agent.training_step(b, 0)
     torch.cuda.synchronize()
     rec = agent.metrics_buf[0].cpu().numpy()
