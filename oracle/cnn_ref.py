@@ -1,0 +1,143 @@
+"""ORACLE — test infrastructure only (tests/, smoke(), bench cpu_baseline may import it; the
+product path never does).
+
+torch-CPU fp32 restatement of the reference's NatureCNN actor-critic PPO minibatch step, the
+floating-point checker for the HIP CNN path (C4/C5 rows of SURVEY.md §8):
+  * CNNActorCritic.forward         utils/models.py:424-455 (u8 / 255, conv 8x8s4 / 4x4s2 / 3x3s1,
+                                   ReLU, flatten (C,H,W), Linear 3136->512 ReLU, heads)
+  * build_cnn                      utils/models.py:56-110 (no padding, ReLU after every conv)
+  * action masking                 utils/policy_ops.py:44-75 (masked_fill(-inf) of invalid actions)
+  * MaskedCategorical              utils/distributions.py:8-82 (entropy over valid actions with
+                                   log(p + 1e-8); log_prob = Categorical's)
+  * PPO losses                     agents/ppo/ppo_agent.py:21-152, batch normalisation
+                                   utils/torch.py:97-99, KL diagnostics utils/torch.py:102-119
+  * clip_grad_norm_ + Adam         agents/base_agent.py:612-617, utils/optimizer_factory.py:6-29
+Gradients come from torch autograd on this restatement (so torch's min/max/clamp tie rules hold
+by construction).  Pinned by tests/golden/cnn_step.npz, generated from the reference itself.
+Parameters are a flat fp32 vector in the reference's state_dict order (cnn.0, cnn.2, cnn.4,
+mlp.0, policy_head, value_head; each weight then bias).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+NATURE = dict(channels=(32, 64, 64), kernels=(8, 4, 3), strides=(4, 2, 1), hidden=512)
+
+
+def cnn_param_shapes(in_shape=(4, 84, 84), n_actions=18, spec=NATURE):
+    C, H, W = in_shape
+    shapes, c, h, w = [], C, H, W
+    for i, (co, k, s) in enumerate(zip(spec["channels"], spec["kernels"], spec["strides"])):
+        shapes += [(f"cnn.{2 * i}.weight", (co, c, k, k)), (f"cnn.{2 * i}.bias", (co,))]
+        c, h, w = co, (h - k) // s + 1, (w - k) // s + 1
+    feat = c * h * w
+    shapes += [("mlp.0.weight", (spec["hidden"], feat)), ("mlp.0.bias", (spec["hidden"],)),
+               ("policy_head.weight", (n_actions, spec["hidden"])), ("policy_head.bias", (n_actions,)),
+               ("value_head.weight", (1, spec["hidden"])), ("value_head.bias", (1,))]
+    return shapes
+
+
+def unflatten(flat, shapes):
+    out, o = {}, 0
+    for n, s in shapes:
+        k = int(np.prod(s))
+        out[n] = torch.as_tensor(np.asarray(flat[o:o + k], np.float32).reshape(s))
+        o += k
+    return out
+
+
+def forward(params: dict, obs_u8, valid=None, spec=NATURE):
+    """-> (masked logits (B,A) with -inf for invalid actions, value (B,), hidden (B,512))."""
+    x = torch.as_tensor(obs_u8)
+    x = x.to(torch.float32) / 255.0 if x.dtype == torch.uint8 else x.to(torch.float32)
+    for i, s in enumerate(spec["strides"]):
+        x = F.relu(F.conv2d(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], stride=s))
+    x = x.flatten(1)
+    h = F.relu(F.linear(x, params["mlp.0.weight"], params["mlp.0.bias"]))
+    logits = F.linear(h, params["policy_head.weight"], params["policy_head.bias"])
+    if valid is not None:
+        mask = torch.ones_like(logits, dtype=torch.bool)
+        mask[:, list(valid)] = False
+        logits = logits.masked_fill(mask, float("-inf"))
+    value = F.linear(h, params["value_head.weight"], params["value_head.bias"]).squeeze(-1)
+    return logits, value, h
+
+
+def dist_terms(logits, actions, valid):
+    """log_prob of actions and entropy: Categorical / MaskedCategorical semantics."""
+    ln = logits - torch.logsumexp(logits, dim=-1, keepdim=True)
+    lp = ln.gather(1, torch.as_tensor(actions, dtype=torch.int64)[:, None]).squeeze(1)
+    p = torch.softmax(logits, dim=-1)
+    if valid is None:
+        fmin = torch.finfo(ln.dtype).min
+        ent = -(p * ln.clamp(min=fmin)).sum(-1)
+    else:
+        vm = torch.isfinite(logits)
+        ent = -(p * torch.where(vm, torch.log(p + 1e-8), torch.zeros_like(p))).sum(-1)
+    return lp, ent
+
+
+def loss_and_grads(flat, shapes, obs_u8, actions, old_logp, old_values, adv, ret, *, valid, clip, clip_vf,
+                   vf_coef, ent_coef, normalize="batch"):
+    """(loss, metrics, flat grads, logits, values) of losses_for_batch + backward."""
+    params = {k: v.clone().requires_grad_(True) for k, v in unflatten(flat, shapes).items()}
+    adv = torch.as_tensor(np.asarray(adv, np.float32))
+    old_logp = torch.as_tensor(np.asarray(old_logp, np.float32))
+    old_values = torch.as_tensor(np.asarray(old_values, np.float32))
+    ret = torch.as_tensor(np.asarray(ret, np.float32))
+    metrics = {}
+    if normalize == "batch":
+        adv_n = (adv - adv.mean()) / (adv.std() + 1e-8)
+        metrics["roll/adv/norm/mean"] = float(adv_n.mean())
+        metrics["roll/adv/norm/std"] = float(adv_n.std())
+    else:
+        adv_n = adv
+    logits, value, _ = forward(params, obs_u8, valid)
+    new_lp, H = dist_terms(logits, actions, valid)
+    ratio = torch.exp(new_lp - old_logp)
+    pl = -torch.min(adv_n * ratio, adv_n * torch.clamp(ratio, 1.0 - clip, 1.0 + clip)).mean()
+    vdelta = value - old_values
+    vl = torch.max((value - ret) ** 2, (old_values + torch.clamp(vdelta, -clip_vf, clip_vf) - ret) ** 2).mean()
+    ent = H.mean()
+    loss = pl + vf_coef * vl + ent_coef * (-ent)
+    loss.backward()
+    g = np.concatenate([params[n].grad.reshape(-1).numpy() for n, _ in shapes]).astype(np.float32)
+    with torch.no_grad():
+        diff = torch.clamp(new_lp - old_logp, -20.0, 20.0)
+        r2 = torch.exp(diff)
+        metrics.update({
+            "opt/loss/total": float(loss), "opt/loss/policy": float(pl), "opt/loss/entropy": float(-ent),
+            "opt/policy/entropy": float(ent), "opt/loss/value": float(vl),
+            "opt/ppo/clip_fraction": float(((ratio < 1 - clip) | (ratio > 1 + clip)).float().mean()),
+            "opt/ppo/clip_fraction_vf": float(((vdelta < -clip_vf) | (vdelta > clip_vf)).float().mean()),
+            "opt/value/explained_var": float(1 - torch.var(ret - value) / torch.var(ret)),
+            "opt/ppo/kl": float((old_logp - new_lp).mean()),
+            "opt/ppo/approx_kl": float(((r2 - 1) - torch.log(r2)).mean()),
+        })
+    return float(loss.detach()), metrics, g, logits.detach().numpy(), value.detach().numpy()
+
+
+def clip_and_adam(flat, g, shapes, m, v, t, lr, max_norm=0.5, b1=0.9, b2=0.999, eps=1e-8):
+    """clip_grad_norm_ (norm of per-tensor norms) then torch Adam; returns (p, m, v, gc, total)."""
+    norms = []
+    o = 0
+    for _, s in shapes:
+        k = int(np.prod(s))
+        norms.append(np.linalg.norm(g[o:o + k].astype(np.float64)))
+        o += k
+    total = float(np.linalg.norm(norms))
+    coef = min(np.float32(max_norm) / (np.float32(total) + np.float32(1e-6)), np.float32(1.0))
+    gc = (g * np.float32(coef)).astype(np.float32)
+    p = torch.as_tensor(np.array(flat, np.float32)).requires_grad_(True)
+    opt = torch.optim.Adam([p], lr=lr, betas=(b1, b2), eps=eps, foreach=False)
+    st = opt.state[p]
+    if t > 1:
+        st["step"] = torch.tensor(float(t - 1))
+        st["exp_avg"] = torch.as_tensor(np.array(m, np.float32))
+        st["exp_avg_sq"] = torch.as_tensor(np.array(v, np.float32))
+    p.grad = torch.as_tensor(gc)
+    opt.step()
+    st = opt.state[p]
+    return (p.detach().numpy().copy(), st["exp_avg"].numpy().copy(), st["exp_avg_sq"].numpy().copy(), gc, total)

@@ -112,7 +112,7 @@ sys.modules["pytorch_lightning"] = _pl
 
 from utils.returns_advantages import compute_batched_gae_advantages_and_returns  # noqa: E402
 from utils.samplers import MultiPassRandomSampler  # noqa: E402
-from utils.models import MLPActorCritic  # noqa: E402
+from utils.models import MLPActorCritic, CNNActorCritic  # noqa: E402
 from utils.rollout_collector import RolloutCollector  # noqa: E402
 from utils.dataloaders import build_index_collate_loader_from_collector  # noqa: E402
 from utils.random import set_random_seed  # noqa: E402
@@ -123,6 +123,15 @@ from agents.ppo.ppo_agent import PPOAgent  # noqa: E402
 # and this generator); it is NOT a reference artefact.
 sys.path.insert(0, os.path.join(HERE, "..", "..", "gymnasium-solver_amd"))
 from gsamd.synthetic_env import SyntheticVecEnv, synth_obs  # noqa: E402
+# deterministic (LAPACK-free) CNN parameters / batches: test infrastructure, shared with tests
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
+from oracle.cnn_case import cnn_batch, cnn_params  # noqa: E402
+
+CNN_CASES = {  # tag: (valid actions, clip, ent_coef, lr, B, params seed, batch seed) — C4 / C5 configs
+    "pong": ([0, 3, 4], 0.2, 0.01, 3e-4, 48, 1, 3),
+    "breakout": ([0, 1, 3, 4], 0.1, 0.01, 3e-4, 40, 2, 5),
+}
+CNN_SAMPLE = 8192   # grad / param entries stored per case (indices from PCG64 seed 11)
 
 
 def _gae_case(rng, T, N, p_done, p_timeout_of_done, gamma, lam, with_boot=True):
@@ -268,6 +277,52 @@ def make_ppo_step():
     print("ppo_step.npz written")
 
 
+def make_cnn_step():
+    """The reference's CNNActorCritic (NatureCNN, masked actions) through
+    PPOAgent.losses_for_batch + backward + clip_grad_norm_ + Adam.  Params/obs are regenerated
+    from oracle.cnn_case, so only outputs are stored (per-tensor grad norms + sampled entries)."""
+    out = {}
+    for tag, (valid, clip, ent, lr, B, pseed, bseed) in CNN_CASES.items():
+        model = CNNActorCritic(input_shape=(4, 84, 84), hidden_dims=(512,), output_shape=(18,),
+                               valid_actions=valid)
+        flat = cnn_params(pseed)
+        o = 0
+        with torch.no_grad():
+            for _, prm in model.named_parameters():
+                n = prm.numel()
+                prm.copy_(torch.as_tensor(flat[o:o + n]).reshape(prm.shape))
+                o += n
+        assert o == flat.size
+        obs, actions, old_lp, old_v, adv, ret = cnn_batch(bseed, B, valid)
+        cfg = dict(normalize="batch", clip=clip, clip_vf=0.2, vf_coef=0.5, ent_coef=ent)
+        agent, recs = _agent(model, cfg)
+        t = torch.as_tensor
+        batch = types.SimpleNamespace(observations=t(obs), actions=t(actions), logprobs=t(old_lp), values=t(old_v),
+                                      advantages=t(adv), returns=t(ret))
+        with torch.no_grad():
+            dist, v = model(t(obs))
+            logits = dist.logits.numpy()
+        opt = torch.optim.Adam(model.parameters(), lr=lr)
+        opt.zero_grad()
+        res = agent.losses_for_batch(batch, 0)
+        res["loss"].backward()
+        g_raw = _flat_grads(model)
+        norms = np.array([p.grad.double().norm().item() for p in model.parameters()], np.float64)
+        total = torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
+        opt.step()
+        p1 = _flat_params(model)
+        sel = np.sort(np.random.default_rng(11).choice(flat.size, CNN_SAMPLE, replace=False))
+        metrics = {k: float(v) for k, v in recs[0].items()}
+        out.update({f"{tag}/loss": np.float32(res["loss"].item()), f"{tag}/total_norm": np.float32(total.item()),
+                    f"{tag}/tensor_norms": norms, f"{tag}/sel": sel.astype(np.int64),
+                    f"{tag}/grads_sel": g_raw[sel], f"{tag}/params1_sel": p1[sel],
+                    f"{tag}/logits": logits, f"{tag}/values": v.numpy(),
+                    f"{tag}/metric_names": np.array(sorted(metrics)),
+                    f"{tag}/metric_values": np.array([metrics[k] for k in sorted(metrics)], np.float64)})
+    np.savez_compressed(os.path.join(HERE, "cnn_step.npz"), **out)
+    print("cnn_step.npz written")
+
+
 def make_policy_fwd():
     out = {}
     torch.manual_seed(42)
@@ -392,6 +447,11 @@ def make_synth_env():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()[f"make_{name}"]()
+        sys.exit(0)
+    make_cnn_step()
     make_gae()
     make_sampler()
     make_ppo_step()

@@ -82,3 +82,43 @@ def test_masked_categorical_known_answers():
     H = -(p * np.where(valid, np.log(p + 1e-8), 0)).sum()
     assert abs(H - np.log(3)) < 1e-5
     assert abs(ln[0, 0] + np.log(3)) < 1e-6
+
+
+@pytest.mark.parametrize("tag", ["pong", "breakout"])
+def test_cnn_oracle_vs_reference_step(golden, tag):
+    """oracle/cnn_ref.py (torch-CPU restatement) against the reference's CNNActorCritic +
+    losses_for_batch + clip_grad_norm_ + Adam on the same deterministic case."""
+    from oracle import cnn_case as K, cnn_ref as C
+    z = golden("cnn_step.npz")
+    valid, clip, ent, lr, B, pseed, bseed = {"pong": ([0, 3, 4], 0.2, 0.01, 3e-4, 48, 1, 3),
+                                             "breakout": ([0, 1, 3, 4], 0.1, 0.01, 3e-4, 40, 2, 5)}[tag]
+    shapes = C.cnn_param_shapes()
+    p0 = K.cnn_params(pseed)
+    loss, met, g, logits, values = C.loss_and_grads(p0, shapes, *K.cnn_batch(bseed, B, valid), valid=valid, clip=clip,
+                                                    clip_vf=0.2, vf_coef=0.5, ent_coef=ent)
+    assert abs(loss - float(z[f"{tag}/loss"])) < 1e-5 * max(1.0, abs(loss))
+    fin = np.isfinite(z[f"{tag}/logits"])
+    assert np.array_equal(fin, np.isfinite(logits))
+    import torch
+    ln = (torch.as_tensor(logits) - torch.logsumexp(torch.as_tensor(logits), -1, keepdim=True)).numpy()
+    np.testing.assert_allclose(ln[fin], z[f"{tag}/logits"][fin], atol=1e-5, rtol=0)   # Categorical.logits
+    np.testing.assert_allclose(values, z[f"{tag}/values"], atol=1e-5, rtol=0)
+    norms, o = [], 0
+    for _, s in shapes:
+        k = int(np.prod(s))
+        norms.append(np.linalg.norm(g[o:o + k].astype(np.float64)))
+        o += k
+    np.testing.assert_allclose(norms, z[f"{tag}/tensor_norms"], rtol=1e-4, atol=1e-7)
+    sel = z[f"{tag}/sel"]
+    gmax = np.abs(g).max()
+    np.testing.assert_allclose(g[sel], z[f"{tag}/grads_sel"], atol=1e-5 * gmax, rtol=0)
+    P = p0.size
+    p1, _, _, _, total = C.clip_and_adam(p0, g, shapes, np.zeros(P, np.float32), np.zeros(P, np.float32), 1, lr)
+    # torch-CPU clip_grad_norm_ accumulates the 1.6M-element mlp.0.weight norm in fp32 (~3e-5
+    # relative off the exact norm of its own per-tensor norms, which match ours to 1e-7 above)
+    assert abs(total - float(z[f"{tag}/total_norm"])) < 1e-4 * total
+    np.testing.assert_allclose(p1[sel], z[f"{tag}/params1_sel"], atol=2e-6, rtol=0)
+    ref = dict(zip([str(x) for x in z[f"{tag}/metric_names"]], z[f"{tag}/metric_values"]))
+    for k, v in met.items():
+        if k in ref:
+            assert abs(v - ref[k]) < 1e-4 * max(1.0, abs(v)), k
