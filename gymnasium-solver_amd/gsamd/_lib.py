@@ -43,6 +43,15 @@ class RolloutView(ctypes.Structure):
                 ("T", ctypes.c_int64), ("N", ctypes.c_int64)]
 
 
+class CnnDims(ctypes.Structure):
+    _fields_ = [("in_c", ctypes.c_int32), ("in_h", ctypes.c_int32), ("in_w", ctypes.c_int32),
+                ("n_actions", ctypes.c_int32), ("hidden", ctypes.c_int32), ("valid_mask", ctypes.c_uint32)]
+
+
+class RolloutViewU8(ctypes.Structure):
+    _fields_ = RolloutView._fields_
+
+
 class GsError(RuntimeError):
     pass
 
@@ -75,6 +84,12 @@ def _load():
                                         i64, vp, vp, vp]),
         "gs_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64, i64, vp,
                                          vp, vp, vp, ctypes.c_int, vp]),
+        "gs_cnn_param_count": (i64, [CnnDims]),
+        "gs_cnn_workspace_bytes": (sz, [CnnDims, i64]),
+        "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp]),
+        "gs_cnn_ppo_loss": (ctypes.c_int, [vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, vp, vp, vp, vp]),
+        "gs_cnn_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, i64, i64,
+                                             vp, vp, vp, vp, vp]),
         "gs_comm_unique_id": (ctypes.c_int, [vp]),
         "gs_comm_init": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
         "gs_comm_allreduce_mean_f32": (ctypes.c_int, [vp, vp, i64, vp]),
@@ -90,7 +105,9 @@ def _load():
 lib = _load()
 EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_env_reset", "gs_env_step",
-            "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_comm_unique_id",
+            "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update",
+            "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
+            "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_allreduce_mean_f32", "gs_comm_destroy")
 
 

@@ -187,6 +187,51 @@ int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float 
                   int32_t *stop_flag_dev, void *workspace_dev, struct gs_comm *comm, int use_graph,
                   void *stream);
 
+/* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)
+ * Replaces CNNActorCritic (utils/models.py:347-455; conv 8x8s4 -> 4x4s2 -> 3x3s1 with 32/64/64
+ * channels, ReLU, Linear F->hidden ReLU, policy/value heads), action masking
+ * (utils/policy_ops.py:44-75 + MaskedCategorical utils/distributions.py:8-82) and the same PPO
+ * minibatch step as gs_ppo_update for image observations.  Observations are the u8 frame
+ * stacks (T, N, in_c, in_h, in_w) exactly as the reference stores them; the model divides by
+ * 255.  Flat parameter layout: the reference's tensor order (cnn.0, cnn.2, cnn.4, mlp.0,
+ * policy_head, value_head; weight then bias) with conv2/conv3 weights stored (out, ky, kx, in)
+ * and the fc weight (hidden, y, x, c) — gsamd.cnn converts state_dicts both ways. */
+typedef struct gs_cnn_dims {
+    int32_t in_c, in_h, in_w;  /* frame stack (4, 84, 84) */
+    int32_t n_actions;         /* full action space (18 for ALE) */
+    int32_t hidden;            /* fc width (512) */
+    uint32_t valid_mask;       /* bit a set = action a valid; 0 = unmasked Categorical */
+} gs_cnn_dims;
+
+typedef struct gs_rollout_view_u8 {
+    const uint8_t *obs;      /* (T, N, in_c, in_h, in_w) */
+    const int64_t *actions;  /* (T, N) */
+    const float *logprobs;   /* (T, N) */
+    const float *values;     /* (T, N) */
+    const float *advantages; /* (T, N) */
+    const float *returns;    /* (T, N) */
+    int64_t T;
+    int64_t N;
+} gs_rollout_view_u8;
+
+int64_t gs_cnn_param_count(gs_cnn_dims dims);
+/* scratch for `rows` rows (the minibatch B for updates, N envs for gs_cnn_policy_act) */
+size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows);
+/* policy_act on N frame stacks obs_dev (N, in_c, in_h, in_w): mode 0 sample / 1 argmax /
+ * 2 replay (as gs_policy_act); masked actions are never drawn. */
+int gs_cnn_policy_act(const float *params_dev, gs_cnn_dims dims, const uint8_t *obs_dev, int64_t N, int mode,
+                      uint64_t rng_seed, uint64_t rng_counter, int64_t *actions_dev, float *logp_dev,
+                      float *value_dev, void *workspace_dev, void *stream);
+/* losses_for_batch on one minibatch: metrics record + (optional) dLoss/dlogits (B, A+1). */
+int gs_cnn_ppo_loss(const float *params_dev, gs_cnn_dims dims, gs_ppo_hparams hp, gs_rollout_view_u8 rollout,
+                    const int32_t *idx_dev, int64_t batch, float *metrics_dev, float *dlogits_dev,
+                    void *workspace_dev, void *stream);
+/* n_minibatches fused steps (forward, loss, backward, optional all-reduce, clip, Adam). */
+int gs_cnn_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev, gs_cnn_dims dims,
+                      gs_ppo_hparams hp, gs_rollout_view_u8 rollout, const int32_t *idx_dev, int64_t batch,
+                      int64_t n_minibatches, int64_t adam_step0, float *metrics_dev, int32_t *stop_flag_dev,
+                      void *workspace_dev, struct gs_comm *comm, void *stream);
+
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI)
  * One process per GPU.  Rank 0 creates the 128-byte unique id, the launcher
  * broadcasts it (torch.distributed), every rank calls gs_comm_init. */

@@ -1,0 +1,103 @@
+"""GPU parity of the NatureCNN / masked-categorical path (C4/C5 rows) through the C-ABI.
+
+Checker: oracle/cnn_ref.py (torch-CPU fp32 restatement, pinned to the reference by
+tests/golden/cnn_step.npz in tests/test_oracle_golden.py) and the fixture itself.
+Tolerances: loss and metrics 1e-5 relative; log-probs / values 1e-5 absolute; gradients
+2e-5 x max|g| (reductions over up to B*400 = 19 200 terms in a different order than
+torch-CPU's); post-Adam parameters 2e-6 except where Adam's first step amplifies gradient noise
+(see _adam_close).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = {"pong": ([0, 3, 4], 0.2, 0.01, 3e-4, 48, 1, 3), "breakout": ([0, 1, 3, 4], 0.1, 0.01, 3e-4, 40, 2, 5)}
+
+
+def _adam_close(p, q, lr):
+    """Adam's first step moves a weight by lr * g / (|g| + eps): for the few weights whose
+    gradient is ~1e-9 (below fp32 reduction noise) the direction itself is noise.  All but
+    1e-4 of the weights must agree to 2e-6 and every weight to 0.1 * lr."""
+    d = np.abs(p - q)
+    assert (d > 2e-6).sum() <= max(1, int(1e-4 * d.size)), (d > 2e-6).sum()
+    assert d.max() <= 0.1 * lr, d.max()
+
+
+def _setup(cuda, tag):
+    from oracle import cnn_case as K
+    from gsamd._lib import PPOHparams, RolloutViewU8
+    from gsamd.cnn import DeviceCNNActorCritic
+    valid, clip, ent, lr, B, pseed, bseed = CASES[tag]
+    obs, act, olp, ov, adv, ret = K.cnn_batch(bseed, B, valid)
+    pm = DeviceCNNActorCritic(valid_actions=valid, device=cuda, init=False)
+    p_ref = K.cnn_params(pseed)
+    pm.load_reference_flat(p_ref)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x))[None].to(cuda).contiguous()  # noqa: E731
+    bufs = [t(obs), t(act), t(olp), t(ov), t(adv), t(ret)]
+    view = RolloutViewU8(*(b.data_ptr() for b in bufs), 1, B)
+    hp = PPOHparams(clip, 0.2, 0.5, ent, 0.5, lr, 0.9, 0.999, 1e-8, 0.0, 1, 0)
+    idx = torch.arange(B, dtype=torch.int32, device=cuda)
+    return pm, p_ref, bufs, view, hp, idx, (obs, act, olp, ov, adv, ret)
+
+
+@pytest.mark.parametrize("tag", list(CASES))
+def test_cnn_update_step_vs_oracle_and_reference(golden, cuda, tag):
+    from oracle import cnn_ref as C
+    from gsamd._lib import GS_NUM_METRICS, check, lib
+    valid, clip, ent, lr, B, _, _ = CASES[tag]
+    pm, p_ref, bufs, view, hp, idx, batch = _setup(cuda, tag)
+    shapes = C.cnn_param_shapes()
+    loss, met, g, logits, values = C.loss_and_grads(p_ref, shapes, *batch, valid=valid, clip=clip, clip_vf=0.2,
+                                                    vf_coef=0.5, ent_coef=ent)
+    P = p_ref.size
+    p1, _, _, gc, total = C.clip_and_adam(p_ref, g, shapes, np.zeros(P, np.float32), np.zeros(P, np.float32), 1, lr)
+    grads, m, v = (torch.zeros(pm.n_params, device=cuda) for _ in range(3))
+    ws = torch.empty(int(lib.gs_cnn_workspace_bytes(pm.dims, B)), dtype=torch.uint8, device=cuda)
+    met_d = torch.zeros(GS_NUM_METRICS, device=cuda)
+    stop = torch.zeros(1, dtype=torch.int32, device=cuda)
+    check(lib.gs_cnn_ppo_update(pm.params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), pm.dims, hp, view,
+                                idx.data_ptr(), B, 1, 0, met_d.data_ptr(), stop.data_ptr(), ws.data_ptr(), None,
+                                torch.cuda.current_stream().cuda_stream), "gs_cnn_ppo_update")
+    torch.cuda.synchronize()
+    rec = met_d.cpu().numpy()
+    assert abs(rec[0] - loss) < 1e-5 * max(1.0, abs(loss))
+    assert abs(rec[12] - total) < 1e-5 * total
+    g_dev = pm.flat_to_reference(grads)
+    np.testing.assert_allclose(g_dev, gc, atol=2e-5 * np.abs(gc).max(), rtol=0)
+    p_dev = pm.flat_to_reference(pm.params)
+    _adam_close(p_dev, p1, lr)
+    # the reference's own outputs on the same case
+    z = golden("cnn_step.npz")
+    assert abs(rec[0] - float(z[f"{tag}/loss"])) < 1e-5 * max(1.0, abs(loss))
+    sel = z[f"{tag}/sel"]
+    _adam_close(p_dev[sel], z[f"{tag}/params1_sel"], lr)
+    ref = dict(zip([str(x) for x in z[f"{tag}/metric_names"]], z[f"{tag}/metric_values"]))
+    for key, slot in (("opt/loss/policy", 1), ("opt/loss/value", 2), ("opt/policy/entropy", 3),
+                      ("opt/ppo/clip_fraction", 4), ("opt/ppo/approx_kl", 8)):
+        assert abs(rec[slot] - ref[key]) < 1e-5 * max(1.0, abs(ref[key])), key
+
+
+@pytest.mark.parametrize("tag", list(CASES))
+def test_cnn_policy_act_vs_oracle(cuda, tag):
+    from oracle import cnn_ref as C
+    valid = CASES[tag][0]
+    pm, p_ref, bufs, view, hp, idx, batch = _setup(cuda, tag)
+    obs = bufs[0][0]
+    logits, values, _ = C.forward(C.unflatten(p_ref, C.cnn_param_shapes()), batch[0], valid)
+    ln = (logits - torch.logsumexp(logits, -1, keepdim=True)).numpy()
+    a, lp, v = pm.act(obs, mode=1)
+    torch.cuda.synchronize()
+    a = a.cpu().numpy()
+    np.testing.assert_allclose(v.cpu().numpy(), values.numpy(), atol=1e-5, rtol=0)
+    assert np.array_equal(a, np.argmax(ln, axis=1))
+    np.testing.assert_allclose(lp.cpu().numpy(), ln[np.arange(len(a)), a], atol=1e-5, rtol=0)
+    # sampling never draws a masked action, and replay reproduces the log-probs
+    rep = obs.repeat(64, 1, 1, 1).contiguous()
+    a_s, lp_s, _ = pm.act(rep, mode=0, rng_seed=7, rng_counter=3)
+    torch.cuda.synchronize()
+    a_s = a_s.cpu().numpy()
+    assert set(np.unique(a_s)) <= set(valid)
+    ln_rep = np.tile(ln, (64, 1))
+    np.testing.assert_allclose(lp_s.cpu().numpy(), ln_rep[np.arange(len(a_s)), a_s], atol=1e-5, rtol=0)
