@@ -1,0 +1,270 @@
+// gs_atari.hip — Atari pixel path: a synthetic ALE-shaped frame source and
+// the observation pipeline the reference gets from ale-py's AtariVectorEnv / gymnasium's
+// AtariPreprocessing + FrameStackObservation (utils/environment.py:240-303, :362-385):
+//   two raw 210x160 RGB frames per env step (the last two of the frameskip)
+//   -> grayscale (OpenCV RGB2GRAY fixed point: (4899 R + 9617 G + 1868 B + 2^13) >> 14)
+//   -> max-pool of the two frames
+//   -> INTER_AREA resize to 84x84 (fractional-coverage box filter, fixed summation order,
+//      round half to even)
+//   -> 4-frame stack, newest last, zero padding after a reset (FrameStackObservation
+//      padding_type="zero").
+// ale-py / OpenCV are not vendored: their exact arithmetic is "parity unpinned"; this file's
+// arithmetic is the spec, restated bit-for-bit in oracle/atari_ref.py.
+// Compiled with -ffp-contract=off (build_lib.py EXTRA) so the resize sums round like numpy.
+#include <math.h>
+
+#include <mutex>
+#include <vector>
+
+#include "gs_common.h"
+
+namespace {
+
+constexpr int kFH = 210, kFW = 160, kFC = 3;
+constexpr int kFrameBytes = kFH * kFW * kFC;   // 100 800
+constexpr int kMaxTaps = 4;
+
+struct AreaTables {
+    int32_t y0[128], ny[128];
+    float wy[128][kMaxTaps];
+    int32_t x0[128], nx[128];
+    float wx[128][kMaxTaps];
+    float inv_area;
+};
+__constant__ AreaTables c_area;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// ---- per-env counters, rewards, dones (fixed-length episodes starting e mod L steps in)
+__global__ __launch_bounds__(256) void k_atari_counters(int32_t *__restrict__ state, float *__restrict__ ep_ret,
+                                                        int64_t N, int L, int trunc_every, uint64_t seed,
+                                                        int64_t env_offset, uint64_t step_count,
+                                                        float *__restrict__ rew_row, uint8_t *__restrict__ done_row,
+                                                        uint8_t *__restrict__ to_row, int32_t *__restrict__ ep_cnt,
+                                                        float *__restrict__ ep_ret_sum, float *__restrict__ ep_len_sum)
+{
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= N) return;
+    const uint64_t ge = (uint64_t)(env_offset + e);
+    int k = state[4 * e + 0] + 1;
+    int epi = state[4 * e + 1];
+    int len = state[4 * e + 2] + 1;
+    const uint64_t h = mix64(mix64(mix64(mix64(seed) ^ ge) ^ step_count) ^ 0xA7A7ull);
+    const float reward = (float)(uint32_t)(h >> 40) * 1.1920928955078125e-07f - 1.0f;
+    float er = ep_ret[e] + reward;
+    const bool done = k >= L;
+    const bool trunc_ep = trunc_every > 0 && (epi % trunc_every) == trunc_every - 1;
+    rew_row[e] = reward;
+    done_row[e] = done ? 1 : 0;
+    to_row[e] = (done && trunc_ep) ? 1 : 0;
+    if (done) {
+        if (ep_cnt) ep_cnt[e] += 1;
+        if (ep_ret_sum) ep_ret_sum[e] += er;
+        if (ep_len_sum) ep_len_sum[e] += (float)len;
+        k = 0;
+        epi += 1;
+        len = 0;
+        er = 0.0f;
+    }
+    state[4 * e + 0] = k;
+    state[4 * e + 1] = epi;
+    state[4 * e + 2] = len;
+    ep_ret[e] = er;
+}
+
+// ---- the frame source: raw RGB frames 2*step and 2*step+1 of every env, 8 bytes per thread
+__global__ __launch_bounds__(256) void k_atari_render(uint8_t *__restrict__ frames, int64_t N, uint64_t seed,
+                                                      int64_t env_offset, uint64_t step_count)
+{
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    constexpr int per_env = 2 * kFrameBytes / 8;
+    if (t >= N * per_env) return;
+    const int64_t e = t / per_env;
+    const int w = (int)(t - e * per_env);
+    const int j = w / (kFrameBytes / 8);
+    const int word = w - j * (kFrameBytes / 8);
+    const uint64_t ge = (uint64_t)(env_offset + e);
+    const uint64_t h = mix64(mix64(mix64(mix64(seed) ^ ge) ^ (2 * step_count + (uint64_t)j)) ^ (uint64_t)word);
+    ((uint64_t *)frames)[t] = h;
+}
+
+__device__ __forceinline__ int gray_at(const uint8_t *f, int y, int x)
+{
+    const uint8_t *p = f + (y * kFW + x) * kFC;
+    return ((int)p[0] * 4899 + (int)p[1] * 9617 + (int)p[2] * 1868 + (1 << 13)) >> 14;
+}
+
+// ---- one 84x84 pixel: gray -> max-pool -> area resize
+__device__ __forceinline__ uint8_t preprocess_px(const uint8_t *f0, const uint8_t *f1, int oy, int ox)
+{
+    float total = 0.0f;
+    const int y0 = c_area.y0[oy], ny = c_area.ny[oy], x0 = c_area.x0[ox], nx = c_area.nx[ox];
+    for (int iy = 0; iy < ny; ++iy) {
+        float row = 0.0f;
+        for (int ix = 0; ix < nx; ++ix) {
+            const int g = max(gray_at(f0, y0 + iy, x0 + ix), gray_at(f1, y0 + iy, x0 + ix));
+            row = row + c_area.wx[ox][ix] * (float)g;
+        }
+        total = total + c_area.wy[oy][iy] * row;
+    }
+    const float v = rintf(total * c_area.inv_area);
+    return (uint8_t)fminf(fmaxf(v, 0.0f), 255.0f);
+}
+
+__global__ __launch_bounds__(256) void k_atari_preprocess(const uint8_t *__restrict__ frames, int64_t N, int OH,
+                                                          int OW, uint8_t *__restrict__ out)
+{
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= N * OH * OW) return;
+    const int64_t e = t / (OH * OW);
+    const int p = (int)(t - e * OH * OW);
+    const int oy = p / OW, ox = p - oy * OW;
+    const uint8_t *f0 = frames + e * 2 * kFrameBytes;
+    out[t] = preprocess_px(f0, f0 + kFrameBytes, oy, ox);
+}
+
+// ---- frame stack update: shift (or zero after a done) and write the new frame last
+__global__ __launch_bounds__(256) void k_atari_stack(const uint8_t *__restrict__ frames,
+                                                     const uint8_t *__restrict__ done_row, int64_t N, int S, int OH,
+                                                     int OW, uint8_t *__restrict__ stack)
+{
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int hw = OH * OW;
+    if (t >= N * hw) return;
+    const int64_t e = t / hw;
+    const int p = (int)(t - e * hw);
+    const bool reset = done_row ? done_row[e] != 0 : true;
+    uint8_t *st = stack + e * (int64_t)S * hw + p;
+    for (int s = 0; s < S - 1; ++s) st[(int64_t)s * hw] = reset ? 0 : st[(int64_t)(s + 1) * hw];
+    const uint8_t *f0 = frames + e * 2 * kFrameBytes;
+    st[(int64_t)(S - 1) * hw] = preprocess_px(f0, f0 + kFrameBytes, p / OW, p - (p / OW) * OW);
+}
+
+std::mutex g_tab_mu;
+int g_tab_dev_mask = 0;
+int g_tab_oh = 0, g_tab_ow = 0;
+
+// area-resize coverage tables (host, double -> f32), uploaded once per device / shape
+int ensure_tables(int OH, int OW)
+{
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    int dev = 0;
+    GS_HIP(hipGetDevice(&dev));
+    if ((g_tab_dev_mask & (1 << dev)) && g_tab_oh == OH && g_tab_ow == OW) return GS_OK;
+    AreaTables t{};
+    const double sy = (double)kFH / OH, sx = (double)kFW / OW;
+    auto fill = [](int n_out, double sc, int n_in, int32_t *o0, int32_t *cnt, float (*w)[kMaxTaps]) {
+        for (int o = 0; o < n_out; ++o) {
+            const double a = o * sc, b = (o + 1) * sc;
+            const int i0 = (int)floor(a);
+            int i1 = (int)ceil(b);
+            if (i1 > n_in) i1 = n_in;
+            o0[o] = i0;
+            cnt[o] = i1 - i0;
+            for (int i = i0; i < i1; ++i) {
+                const double lo = a > i ? a : (double)i, hi = b < i + 1 ? b : (double)(i + 1);
+                w[o][i - i0] = (float)(hi - lo);
+            }
+        }
+    };
+    fill(OH, sy, kFH, t.y0, t.ny, t.wy);
+    fill(OW, sx, kFW, t.x0, t.nx, t.wx);
+    t.inv_area = (float)(1.0 / (sy * sx));
+    GS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_area), &t, sizeof(t)));
+    g_tab_dev_mask |= 1 << dev;
+    g_tab_oh = OH, g_tab_ow = OW;
+    return GS_OK;
+}
+
+int check_out(int OH, int OW)
+{
+    GS_REQUIRE(OH >= 1 && OW >= 1 && OH <= 128 && OW <= 128, "resize target %dx%d outside [1, 128]", OH, OW);
+    GS_REQUIRE((double)kFH / OH <= kMaxTaps - 1 && (double)kFW / OW <= kMaxTaps - 1,
+               "downscale %dx%d needs more than %d taps", OH, OW, kMaxTaps);
+    return GS_OK;
+}
+
+inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+extern "C" int gs_atari_preprocess(const uint8_t *frames, int64_t N, int32_t out_h, int32_t out_w, uint8_t *out,
+                                   void *stream)
+{
+    GS_REQUIRE(N >= 0 && frames && out, "gs_atari_preprocess: bad argument");
+    int rc = check_out(out_h, out_w);
+    if (rc) return rc;
+    if ((rc = ensure_tables(out_h, out_w))) return rc;
+    if (N == 0) return GS_OK;
+    hipLaunchKernelGGL(k_atari_preprocess, dim3(nblk(N * out_h * out_w)), dim3(256), 0, (hipStream_t)stream, frames, N,
+                       out_h, out_w, out);
+    GS_LAUNCH_CHECK("k_atari_preprocess");
+    return GS_OK;
+}
+
+extern "C" int gs_atari_render(uint8_t *frames, int64_t N, uint64_t seed, int64_t env_offset, uint64_t step_count,
+                               void *stream)
+{
+    GS_REQUIRE(N > 0 && frames, "gs_atari_render: bad argument");
+    hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, (hipStream_t)stream, frames,
+                       N, seed, env_offset, step_count);
+    GS_LAUNCH_CHECK("k_atari_render");
+    return GS_OK;
+}
+
+extern "C" int gs_atari_env_reset(int32_t *state, float *ep_ret, uint8_t *stack, uint8_t *frames, int64_t N,
+                                  int32_t stack_n, int32_t out_h, int32_t out_w, int32_t episode_len, uint64_t seed,
+                                  int64_t env_offset, void *stream)
+{
+    GS_REQUIRE(N > 0 && state && ep_ret && stack && frames && stack_n >= 1 && episode_len > 0,
+               "gs_atari_env_reset: bad argument");
+    int rc = check_out(out_h, out_w);
+    if (rc) return rc;
+    if ((rc = ensure_tables(out_h, out_w))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    // counters: same start phases as the vector env (k0 = env mod L)
+    std::vector<int32_t> st(4 * (size_t)N);
+    for (int64_t e = 0; e < N; ++e) {
+        st[4 * e] = (int32_t)((uint64_t)(env_offset + e) % (uint64_t)episode_len);
+        st[4 * e + 1] = st[4 * e + 2] = st[4 * e + 3] = 0;
+    }
+    GS_HIP(hipMemcpyAsync(state, st.data(), st.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    GS_HIP(hipStreamSynchronize(s));   // pageable source: keep it alive until copied
+    GS_HIP(hipMemsetAsync(ep_ret, 0, sizeof(float) * N, s));
+    hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
+                       env_offset, (uint64_t)0);
+    hipLaunchKernelGGL(k_atari_stack, dim3(nblk(N * out_h * out_w)), dim3(256), 0, s, frames, (const uint8_t *)nullptr,
+                       N, stack_n, out_h, out_w, stack);
+    GS_LAUNCH_CHECK("k_atari_stack");
+    return GS_OK;
+}
+
+extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, uint8_t *frames, int64_t N,
+                                 int32_t stack_n, int32_t out_h, int32_t out_w, int32_t episode_len,
+                                 int32_t truncate_every, uint64_t seed, int64_t env_offset, uint64_t step_count,
+                                 float *rewards_row, uint8_t *dones_row, uint8_t *timeouts_row, int32_t *ep_done_count,
+                                 float *ep_ret_sum, float *ep_len_sum, void *stream)
+{
+    GS_REQUIRE(N > 0 && state && ep_ret && stack && frames && stack_n >= 1 && episode_len > 0,
+               "gs_atari_env_step: bad argument");
+    GS_REQUIRE(rewards_row && dones_row && timeouts_row, "gs_atari_env_step: null output row");
+    int rc = check_out(out_h, out_w);
+    if (rc) return rc;
+    if ((rc = ensure_tables(out_h, out_w))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_atari_counters, dim3(nblk(N)), dim3(256), 0, s, state, ep_ret, N, episode_len, truncate_every,
+                       seed, env_offset, step_count, rewards_row, dones_row, timeouts_row, ep_done_count, ep_ret_sum,
+                       ep_len_sum);
+    hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
+                       env_offset, step_count);
+    hipLaunchKernelGGL(k_atari_stack, dim3(nblk(N * out_h * out_w)), dim3(256), 0, s, frames, dones_row, N, stack_n,
+                       out_h, out_w, stack);
+    GS_LAUNCH_CHECK("k_atari_stack");
+    return GS_OK;
+}

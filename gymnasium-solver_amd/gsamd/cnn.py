@@ -163,11 +163,15 @@ class DeviceCNNActorCritic:
         return t
 
     def act(self, obs: torch.Tensor, *, mode: int = 0, rng_seed: int = 0, rng_counter: int = 0,
-            actions: torch.Tensor = None, logp: torch.Tensor = None, values: torch.Tensor = None):
-        """policy_act (utils/policy_ops.py:14-34) on u8 frame stacks (N, C, H, W)."""
+            actions: torch.Tensor = None, logp: torch.Tensor = None, values: torch.Tensor = None,
+            obs_store: torch.Tensor = None):
+        """policy_act (utils/policy_ops.py:14-34) on u8 frame stacks (N, C, H, W); obs_store
+        (the rollout row) receives a copy of the observation."""
         n = obs.shape[0]
         if not (obs.is_contiguous() and obs.dtype == torch.uint8 and obs.device == self.device):
             raise ValueError("obs must be a contiguous uint8 device tensor (N, C, H, W)")
+        if obs_store is not None:
+            obs_store.copy_(obs)
         if actions is None:
             actions = torch.empty(n, dtype=torch.int64, device=self.device)
         if logp is None:

@@ -24,6 +24,8 @@ import numpy as np
 import torch
 
 from ._lib import GS_NUM_METRICS, M, PPOHparams, check, lib, ptr, stream_handle
+from .atari_env import DeviceAtariVecEnv
+from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
 from .rollout import DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
@@ -70,8 +72,12 @@ class DevicePPOAgent:
 
     # ---- construction (base_agent.py:103-222) -------------------------------------------
     def build_env(self, stage: str, env=None):
+        c = self.config
+        if env is None and self.is_pixel:
+            env = DeviceAtariVecEnv(n_envs=c.n_envs, n_actions=c.resolved_n_actions(), episode_len=c.episode_len,
+                                    seed=c.seed, truncate_every=c.truncate_every, env_offset=self.rank * c.n_envs,
+                                    frame_stack=int(c.frame_stack or 4), device=self.device)
         if env is None:
-            c = self.config
             env = DeviceSyntheticVecEnv(n_envs=c.n_envs, obs_dim=c.resolved_obs_dim(), n_actions=c.resolved_n_actions(),
                                         episode_len=c.episode_len, seed=c.seed, truncate_every=c.truncate_every,
                                         env_offset=self.rank * c.n_envs, device=self.device)
@@ -80,10 +86,21 @@ class DevicePPOAgent:
     def get_env(self, stage: str):
         return self._envs[stage]
 
+    @property
+    def is_pixel(self) -> bool:
+        """rgb observations -> NatureCNN + Atari pipeline (C4/C5), else the MLP path."""
+        return str(getattr(self.config, "obs_type", "vector")) == "rgb"
+
     def build_models(self):
         c = self.config
-        self.policy_model = DeviceMLPActorCritic(c.resolved_obs_dim(), c.hidden_dims, c.resolved_n_actions(),
-                                                 device=self.device)
+        if self.is_pixel:
+            env = self.get_env("train")
+            self.policy_model = DeviceCNNActorCritic(in_shape=tuple(env.obs_shape), n_actions=c.resolved_n_actions(),
+                                                     hidden=int(c.hidden_dims[0]), valid_actions=c.valid_actions,
+                                                     device=self.device)
+        else:
+            self.policy_model = DeviceMLPActorCritic(c.resolved_obs_dim(), c.hidden_dims, c.resolved_n_actions(),
+                                                     device=self.device)
 
     def build_rollout_collector(self, stage: str):
         c = self.config
@@ -111,7 +128,10 @@ class DevicePPOAgent:
             raise ValueError(f"Batch size must divide rollout size exactly: data_len={self.data_len}, "
                              f"batch_size={self.batch_size}.")
         self.n_minibatches = self.data_len // self.batch_size * c.n_epochs
-        ws = int(lib.gs_ppo_workspace_bytes(self.policy_model.dims, self.batch_size))
+        if self.is_pixel:
+            ws = int(lib.gs_cnn_workspace_bytes(self.policy_model.dims, self.batch_size))
+        else:
+            ws = int(lib.gs_ppo_workspace_bytes(self.policy_model.dims, self.batch_size))
         self.workspace = torch.zeros(ws, dtype=torch.uint8, device=self.device)
         self.stop_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.metrics_buf = torch.zeros(self.n_minibatches, GS_NUM_METRICS, **z)
@@ -145,9 +165,14 @@ class DevicePPOAgent:
     def losses_for_batch(self, batch: MinibatchIndices, batch_idx: int):
         """PPOAgent.losses_for_batch: loss + metrics of one minibatch (no optimizer step)."""
         buf = self.get_rollout_collector("train").buffer
-        check(lib.gs_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(), buf.view(),
-                              ptr(batch.idx), len(batch), ptr(self._step_metrics), ptr(self.workspace),
-                              stream_handle()), "gs_ppo_loss")
+        if self.is_pixel:
+            check(lib.gs_cnn_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(),
+                                      buf.view(), ptr(batch.idx), len(batch), ptr(self._step_metrics), None,
+                                      ptr(self.workspace), stream_handle()), "gs_cnn_ppo_loss")
+        else:
+            check(lib.gs_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(), buf.view(),
+                                  ptr(batch.idx), len(batch), ptr(self._step_metrics), ptr(self.workspace),
+                                  stream_handle()), "gs_ppo_loss")
         early = False
         if self.config.target_kl is not None:
             early = float(self._step_metrics[M["approx_kl"]].item()) > float(self.config.target_kl)
@@ -160,6 +185,13 @@ class DevicePPOAgent:
         buf = self.get_rollout_collector("train").buffer
         self.adam_step += 1
         rec = self.metrics_buf[batch_idx % self.n_minibatches]
+        if self.is_pixel:
+            check(lib.gs_cnn_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                        ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(),
+                                        ptr(batch.idx), len(batch), 1, self.adam_step - 1, ptr(rec),
+                                        ptr(self.stop_flag), ptr(self.workspace), self.comm, stream_handle()),
+                  "gs_cnn_ppo_update")
+            return None
         check(lib.gs_ppo_minibatch_step(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
                                         ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(),
                                         ptr(batch.idx), len(batch), self.adam_step, ptr(rec), ptr(self.stop_flag),
@@ -184,11 +216,18 @@ class DevicePPOAgent:
         buf = collector.buffer
         if ev is not None:
             ev[-1][1].record()
-        check(lib.gs_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
-                                self.policy_model.dims, self.hparams(), buf.view(), ptr(idx), self.batch_size,
-                                self.n_minibatches, self.adam_step, ptr(self.metrics_buf), ptr(self.stop_flag),
-                                ptr(self.workspace), self.comm, 1 if self.use_graph else 0, stream_handle()),
-              "gs_ppo_update")
+        if self.is_pixel:
+            check(lib.gs_cnn_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                        ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(), ptr(idx),
+                                        self.batch_size, self.n_minibatches, self.adam_step, ptr(self.metrics_buf),
+                                        ptr(self.stop_flag), ptr(self.workspace), self.comm, stream_handle()),
+                  "gs_cnn_ppo_update")
+        else:
+            check(lib.gs_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                    ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(), ptr(idx),
+                                    self.batch_size, self.n_minibatches, self.adam_step, ptr(self.metrics_buf),
+                                    ptr(self.stop_flag), ptr(self.workspace), self.comm,
+                                    1 if self.use_graph else 0, stream_handle()), "gs_ppo_update")
         if ev is not None:
             ev[-1][2].record()
         self.adam_step += self.n_minibatches

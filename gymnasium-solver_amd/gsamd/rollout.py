@@ -43,6 +43,7 @@ class DeviceSyntheticVecEnv:
         self.num_envs, self.obs_dim, self.n_actions = int(n_envs), int(obs_dim), int(n_actions)
         self.episode_len, self.seed, self.truncate_every = int(episode_len), int(seed), int(truncate_every)
         self.env_offset, self.reward = int(env_offset), float(reward)
+        self.obs_shape, self.obs_dtype = (self.obs_dim,), torch.float32
         self.device = torch.device(device)
         N = self.num_envs
         self.state = torch.zeros(4 * N, dtype=torch.int32, device=self.device)
@@ -71,11 +72,14 @@ class DeviceSyntheticVecEnv:
 class DeviceRolloutBuffer:
     """Preallocated time-major SoA rollout storage in HBM (utils/rollout_buffer.py:28-80)."""
 
-    def __init__(self, n_envs: int, obs_dim: int, n_steps: int, device):
+    def __init__(self, n_envs: int, obs_shape, n_steps: int, device, obs_dtype=torch.float32):
         T, N = int(n_steps), int(n_envs)
-        self.T, self.N, self.obs_dim, self.device = T, N, int(obs_dim), torch.device(device)
+        self.obs_shape = (int(obs_shape),) if isinstance(obs_shape, int) else tuple(int(x) for x in obs_shape)
+        self.T, self.N, self.device, self.obs_dtype = T, N, torch.device(device), obs_dtype
+        self.obs_dim = self.obs_shape[0]
         z = dict(device=self.device)
-        self.obs = torch.zeros(T, N, self.obs_dim, dtype=torch.float32, **z)
+        # (T, N, *obs_shape): f32 vectors, or the u8 frame stacks of the pixel path
+        self.obs = torch.zeros(T, N, *self.obs_shape, dtype=obs_dtype, **z)
         self.actions = torch.zeros(T, N, dtype=torch.int64, **z)
         self.logprobs = torch.zeros(T, N, dtype=torch.float32, **z)
         self.values = torch.zeros(T, N, dtype=torch.float32, **z)
@@ -88,8 +92,9 @@ class DeviceRolloutBuffer:
         self.last_values = torch.zeros(N, dtype=torch.float32, **z)
 
     def view(self):
-        from ._lib import RolloutView
-        return RolloutView(ptr(self.obs), ptr(self.actions), ptr(self.logprobs), ptr(self.values),
+        from ._lib import RolloutView, RolloutViewU8
+        V = RolloutViewU8 if self.obs_dtype == torch.uint8 else RolloutView
+        return V(ptr(self.obs), ptr(self.actions), ptr(self.logprobs), ptr(self.values),
                            ptr(self.advantages), ptr(self.returns), self.T, self.N)
 
 
@@ -197,13 +202,15 @@ class DeviceRolloutCollector:
             return
         if getattr(self.env, "device_native", False):
             self.env.reset()
-            obs_dim = self.env.obs_dim
+            obs_shape, obs_dtype = tuple(self.env.obs_shape), self.env.obs_dtype
         else:
             obs, _ = self.env.reset()
-            self._host_obs = np.asarray(obs, dtype=np.float32)
-            obs_dim = self._host_obs.shape[1]
-        self._buffer = DeviceRolloutBuffer(self.n_envs, obs_dim, self.n_steps, self.device)
-        self._obs_dev = torch.zeros(self.n_envs, obs_dim, dtype=torch.float32, device=self.device)
+            obs = np.asarray(obs)
+            obs_dtype = torch.uint8 if obs.dtype == np.uint8 else torch.float32
+            self._host_obs = obs if obs_dtype == torch.uint8 else obs.astype(np.float32)
+            obs_shape = tuple(obs.shape[1:])
+        self._buffer = DeviceRolloutBuffer(self.n_envs, obs_shape, self.n_steps, self.device, obs_dtype)
+        self._obs_dev = torch.zeros(self.n_envs, *obs_shape, dtype=obs_dtype, device=self.device)
         self._started = True
 
     @property
@@ -240,7 +247,7 @@ class DeviceRolloutCollector:
                 buf.dones[t].copy_(torch.from_numpy(done.astype(np.uint8)))
                 buf.timeouts[t].copy_(torch.from_numpy(np.asarray(trunc).astype(np.uint8)))
                 self._host_episode_infos(done, infos)
-                self._host_obs = np.asarray(next_obs, dtype=np.float32)
+                self._host_obs = np.asarray(next_obs, dtype=self._host_obs.dtype)
         last_obs = self.env.obs if native else self._obs_dev.copy_(torch.from_numpy(self._host_obs))
         pm.predict_values(last_obs, out=buf.last_values)
         compute_batched_gae_advantages_and_returns(buf.values, buf.rewards, buf.dones, buf.timeouts,
@@ -270,8 +277,14 @@ class DeviceRolloutCollector:
             self._stats = torch.zeros(10, dtype=torch.float64, device=self.device)
         s = self._stats
         s[0] += buf.obs.numel()
-        s[1] += buf.obs.sum(dtype=torch.float64)
-        s[2] += (buf.obs.double() ** 2).sum()
+        if buf.obs.dtype == torch.uint8:     # exact, without a float copy of the frames
+            cnt = torch.bincount(buf.obs.reshape(-1), minlength=256).double()
+            v = torch.arange(256, dtype=torch.float64, device=self.device)
+            s[1] += (cnt * v).sum()
+            s[2] += (cnt * v * v).sum()
+        else:
+            s[1] += buf.obs.sum(dtype=torch.float64)
+            s[2] += (buf.obs.double() ** 2).sum()
         s[3] += buf.rewards.sum(dtype=torch.float64)
         s[4] += (buf.rewards.double() ** 2).sum()
         s[5] += buf.advantages.sum(dtype=torch.float64)

@@ -232,6 +232,28 @@ int gs_cnn_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, fl
                       int64_t n_minibatches, int64_t adam_step0, float *metrics_dev, int32_t *stop_flag_dev,
                       void *workspace_dev, struct gs_comm *comm, void *stream);
 
+/* ---------------------------------------------------------------- Atari pixel path (a13)
+ * The observation pipeline of ale-py's AtariVectorEnv / gymnasium AtariPreprocessing +
+ * FrameStackObservation (utils/environment.py:240-303, :362-385), on device: two raw
+ * 210x160x3 u8 frames per env step -> OpenCV-RGB2GRAY grayscale -> max of the two -> area
+ * resize to out_h x out_w -> stack of stack_n frames, newest last, zero padding after reset.
+ * The frame source is synthetic (hash of seed, env, frame, byte): ALE itself is not
+ * available offline.  frames_dev: (N, 2, 210, 160, 3) u8 scratch; stack_dev: (N, stack_n,
+ * out_h, out_w) u8 = the observation; state_dev: 4 int32 per env; counters and rows as
+ * gs_env_step. */
+int gs_atari_preprocess(const uint8_t *frames_dev, int64_t N, int32_t out_h, int32_t out_w, uint8_t *out_dev,
+                        void *stream);
+int gs_atari_render(uint8_t *frames_dev, int64_t N, uint64_t seed, int64_t env_offset, uint64_t step_count,
+                    void *stream);
+int gs_atari_env_reset(int32_t *state_dev, float *ep_ret_dev, uint8_t *stack_dev, uint8_t *frames_dev, int64_t N,
+                       int32_t stack_n, int32_t out_h, int32_t out_w, int32_t episode_len, uint64_t seed,
+                       int64_t env_offset, void *stream);
+int gs_atari_env_step(int32_t *state_dev, float *ep_ret_dev, uint8_t *stack_dev, uint8_t *frames_dev, int64_t N,
+                      int32_t stack_n, int32_t out_h, int32_t out_w, int32_t episode_len, int32_t truncate_every,
+                      uint64_t seed, int64_t env_offset, uint64_t step_count, float *rewards_row_dev,
+                      uint8_t *dones_row_dev, uint8_t *timeouts_row_dev, int32_t *ep_done_count_dev,
+                      float *ep_ret_sum_dev, float *ep_len_sum_dev, void *stream);
+
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI)
  * One process per GPU.  Rank 0 creates the 128-byte unique id, the launcher
  * broadcasts it (torch.distributed), every rank calls gs_comm_init. */

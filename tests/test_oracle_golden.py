@@ -122,3 +122,26 @@ def test_cnn_oracle_vs_reference_step(golden, tag):
     for k, v in met.items():
         if k in ref:
             assert abs(v - ref[k]) < 1e-4 * max(1.0, abs(v)), k
+
+
+def test_atari_oracle_known_answers():
+    """OpenCV RGB2GRAY known answers and box-filter invariants of oracle/atari_ref.py."""
+    from oracle import atari_ref as A
+    px = np.array([[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255], [0, 0, 0]], np.uint8)
+    assert A.gray(px).tolist() == [76, 150, 29, 255, 0]
+    for n_out, n_in in ((84, 210), (84, 160)):
+        starts, w, sc = A.area_tables(n_out, n_in)
+        for ws in w:
+            assert abs(sum(float(x) for x in ws) - sc) < 1e-6 and len(ws) <= 4
+    const = np.full((2, 2, 210, 160, 3), 200, np.uint8)
+    g = A.gray(const[0, 0, :1, :1])[0, 0]
+    assert (A.preprocess(const) == g).all()          # a flat image stays flat
+    fr = A.render(42, [0, 1], 5)
+    assert fr.shape == (2, 2, 210, 160, 3) and fr.std() > 50
+    out = A.preprocess(fr)
+    assert out.shape == (2, 84, 84) and out.dtype == np.uint8
+    env = A.AtariEnvTwin(3, episode_len=4)
+    assert (env.stack[:, :3] == 0).all()
+    for _ in range(5):
+        r, d, _ = env.step()
+        assert r.min() >= -1 and r.max() < 1
