@@ -39,6 +39,19 @@ def _log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# workload id -> (env id, variant, envs per GPU)  (BASELINE.json configs)
+WORKLOADS = {"C2": ("CartPole-v1", "ppo", 4096), "C3": ("LunarLander-v3", "ppo", 1024),
+             "C4": ("ALE-Pong-v5", "rgb_ppo", 256), "C5": ("ALE-Breakout-v5", "rgb_ppo", 128)}
+
+
+def cnn_minibatch_flops(B, A):
+    """NatureCNN minibatch step: forward (conv1..3, fc, heads) + backward (wgrad of every
+    layer, dgrad of fc/conv3/conv2, none for conv1): 2 x MACs."""
+    fwd = 400 * 32 * 256 + 81 * 64 * 512 + 49 * 64 * 576 + 3136 * 512 + 512 * (A + 1)
+    bwd = 2 * (3136 * 512 + 49 * 64 * 576 + 81 * 64 * 512 + 512 * (A + 1)) + 400 * 32 * 256
+    return 2.0 * B * (fwd + bwd)
+
+
 def stage_flops_bytes(D, H1, H2, A, B, P):
     """Algorithmic work per launch of each minibatch-step kernel."""
     A1 = A + 1
@@ -89,9 +102,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("C2", "C3"), default="C2",
-                    help="C2: CartPole-v1:ppo (the metric's config); C3: LunarLander-v3:ppo shapes (T=2048, B=64)")
-    ap.add_argument("--n-envs", type=int, default=None, help="envs per GPU (weak scaling); C2 4096, C3 1024")
+    ap.add_argument("--workload", choices=tuple(WORKLOADS), default="C2",
+                    help="C2: CartPole-v1:ppo (the metric's config); C3: LunarLander-v3:ppo shapes (T=2048, B=64); "
+                         "C4/C5: ALE Pong/Breakout rgb_ppo (NatureCNN, Atari pixel pipeline)")
+    ap.add_argument("--n-envs", type=int, default=None, help="envs per GPU (weak scaling; default per workload)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of the hipGraph")
     ap.add_argument("--local-comm", action="store_true",
                     help="N=1 only: run the multi-GPU chain through a one-rank RCCL communicator")
@@ -118,9 +132,10 @@ def main():
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
-    env_id = "CartPole-v1" if args.workload == "C2" else "LunarLander-v3"
-    n_envs = args.n_envs or (4096 if args.workload == "C2" else 1024)
-    cfg = load_config(env_id, "ppo", overrides=dict(n_envs=n_envs))
+    env_id, variant, n_default = WORKLOADS[args.workload]
+    pixel = variant == "rgb_ppo"
+    n_envs = args.n_envs or n_default
+    cfg = load_config(env_id, variant, overrides=dict(n_envs=n_envs))
     agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world, comm=comm,
                            use_graph=not args.no_graph, track_stats=False)
     N, T = cfg.n_envs, cfg.n_steps
@@ -158,23 +173,35 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---- roofline of the dominant minibatch kernel (device time by events) ----
-    stage_us = time_stages(agent, args.stage_reps)
     pm = agent.policy_model
-    work = stage_flops_bytes(pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions, agent.batch_size,
-                             pm.n_params)
-    dom = max(stage_us, key=stage_us.get)
-    bound, amount = work[dom]
-    if bound == "mfma":
-        achieved = amount / (stage_us[dom] * 1e-6) / 1e12
+    stage_us = {}
+    if pixel:
+        # the update is a chain of GEMMs + fused kernels per minibatch: price the whole
+        # minibatch step (events around the update phase of the timed region) against MFMA
+        amount = cnn_minibatch_flops(agent.batch_size, pm.n_actions)
+        mb_us = update_ms * 1e3 / agent.n_minibatches
+        achieved = amount / (mb_us * 1e-6) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 6), "traffic": None}
+                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 6), "traffic": None,
+                    "kernel": "cnn minibatch step (rocBLAS sgemm + gs_cnn kernels)", "avg_us": round(mb_us, 3),
+                    "work_per_launch": amount}
     else:
-        achieved = amount / (stage_us[dom] * 1e-6) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": None}
-    roofline["kernel"] = {"fwd": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}[dom]
-    roofline["avg_us"] = round(stage_us[dom], 3)
-    roofline["work_per_launch"] = amount
+        stage_us = time_stages(agent, args.stage_reps)
+        work = stage_flops_bytes(pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions, agent.batch_size,
+                                 pm.n_params)
+        dom = max(stage_us, key=stage_us.get)
+        bound, amount = work[dom]
+        if bound == "mfma":
+            achieved = amount / (stage_us[dom] * 1e-6) / 1e12
+            roofline = {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32_MFMA_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 6), "traffic": None}
+        else:
+            achieved = amount / (stage_us[dom] * 1e-6) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": None}
+        roofline["kernel"] = {"fwd": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}[dom]
+        roofline["avg_us"] = round(stage_us[dom], 3)
+        roofline["work_per_launch"] = amount
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path) and args.workload == "C2":   # the committed PMC passes are C2-shaped
         try:
@@ -185,7 +212,18 @@ def main():
 
     # ---- CPU baseline (rank 0, N=1 only): oracle restatement on the host cores ----
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_minibatches > 0:
+    if rank == 0 and world == 1 and args.cpu_minibatches > 0 and pixel:
+        from oracle.cpu_ppo import run_cpu_baseline_cnn
+        cores = min(len(os.sched_getaffinity(0)), 16)
+        r = run_cpu_baseline_cnn(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,
+                                 in_shape=tuple(pm.in_shape), n_actions=pm.n_actions, valid=cfg.valid_actions,
+                                 clip=cfg.clip_range, ent_coef=cfg.ent_coef, lr=cfg.policy_lr, threads=cores)
+        cpu = {"value": round(r["env_steps_per_s"], 2), "unit": "env_steps/s", "cores": r["threads"], "kind": "port",
+               "sample": (f"8 vector steps of the torch-CPU NatureCNN policy on {N} envs + 3 of "
+                          f"{r['minibatches_per_rollout']} minibatch steps (B={cfg.batch_size}), extrapolated; env "
+                          f"emulation excluded; wall {r['wall_s']:.1f}s"),
+               "step_ms": round(r["step_s"] * 1e3, 3), "minibatch_ms": round(r["minibatch_s"] * 1e3, 3)}
+    elif rank == 0 and world == 1 and args.cpu_minibatches > 0:
         from oracle.cpu_ppo import run_cpu_baseline
         cores = min(len(os.sched_getaffinity(0)), 16)
         r = run_cpu_baseline(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,
@@ -204,10 +242,12 @@ def main():
             "value": round(value, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": (f"{env_id}:ppo {args.workload} (rollout {N} envs x {T} steps + "
+            "config": {"workload": (f"{env_id}:{variant} {args.workload} (rollout {N} envs x {T} steps + "
                                     f"{cfg.n_epochs}-epoch PPO update, B={cfg.batch_size})"),
                        "n_envs_per_gpu": N, "n_steps": T, "batch_size": cfg.batch_size, "n_epochs": cfg.n_epochs,
-                       "minibatches_per_step": agent.n_minibatches, "policy": f"MLP {pm.obs_dim}-{pm.hidden_dims[0]}-{pm.hidden_dims[1]}-{{{pm.n_actions},1}}",
+                       "minibatches_per_step": agent.n_minibatches, "policy": (f"NatureCNN {pm.in_shape} -> {pm.hidden} -> {{{pm.n_actions} masked to "
+                                  f"{len(cfg.valid_actions or [])},1}}" if pixel else
+                                  f"MLP {pm.obs_dim}-{pm.hidden_dims[0]}-{pm.hidden_dims[1]}-{{{pm.n_actions},1}}"),
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph},
             "roofline": roofline,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},

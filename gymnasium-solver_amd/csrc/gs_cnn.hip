@@ -20,6 +20,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <algorithm>
 #include <mutex>
 #include <unordered_map>
 
@@ -79,14 +80,18 @@ struct CnnLayout {
 };
 
 struct CnnWs {
-    float *cols1, *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dh, *da3, *da2, *da1, *ones;
+    float *cols1, *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dh, *da3, *da2, *da1;
     int32_t *f_act;
     float *f_olp, *f_ov, *f_adv, *f_ret;
     double *norm_part;
+    float *dhead_b;        // column sums of dz (A policy biases + value bias)
+    float *parts;          // split-K weight-gradient partials / bias column-sum partials
     size_t bytes;
 };
 
 constexpr int kNormBlocks = 1024;
+constexpr int kSplitK = 32;     // weight-gradient GEMMs: K = B*positions split into 32 sample groups
+constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
 
 CnnWs carve(void *base, const CnnLayout &L, int64_t R)
 {
@@ -111,13 +116,19 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.da3 = (float *)take(sizeof(float) * R * L.F);
     w.da2 = (float *)take(sizeof(float) * L.rows2(R) * L.c2);
     w.da1 = (float *)take(sizeof(float) * L.rows1(R) * L.c1);
-    w.ones = (float *)take(sizeof(float) * L.rows1(R));
     w.f_act = (int32_t *)take(sizeof(int32_t) * R);
     w.f_olp = (float *)take(sizeof(float) * R);
     w.f_ov = (float *)take(sizeof(float) * R);
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks);
+    w.dhead_b = (float *)take(sizeof(float) * (L.A + 1));
+    {
+        const int64_t wparts = (int64_t)kSplitK * std::max({(int64_t)L.c1 * L.K1, (int64_t)L.c2 * L.K2,
+                                                            (int64_t)L.c3 * L.K3});
+        const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
+        w.parts = (float *)take(sizeof(float) * std::max(wparts, cparts));
+    }
     w.bytes = off;
     return w;
 }
@@ -251,43 +262,74 @@ __global__ __launch_bounds__(256) void k_relu_mask(float *__restrict__ d, const 
     ((float4 *)d)[t] = v;
 }
 
-__global__ void k_fill(float *__restrict__ x, int64_t n, float v)
+// ---- bias gradient: column sums of X[rows][C], deterministic two-pass.  Block p sums rows
+//      [p*chunk, (p+1)*chunk); thread t handles column t % C on row lane t / C (C < 256) or
+//      columns t, t+256, ... (C >= 256); 4 independent accumulators in a fixed pattern.
+__global__ __launch_bounds__(256) void k_colsum_part(const float *__restrict__ X, int64_t rows, int C,
+                                                     float *__restrict__ part)
 {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t < n) x[t] = v;
-}
-
-// ---- heads: z[r][a] = h[r] . Wp[a] + bp[a], z[r][A] = h[r] . Wv + bv.  One wave per row.
-__global__ __launch_bounds__(256) void k_cnn_heads(const float *__restrict__ h, const float *__restrict__ P, CnnLayout L,
-                                                   int64_t R, float *__restrict__ z)
-{
-    __shared__ float red[4][kAMax + 1][64];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * 4 + wv;
-    const int A1 = L.A + 1;
-    float acc[kAMax + 1];
-#pragma unroll
-    for (int a = 0; a < kAMax + 1; ++a) acc[a] = 0.f;
-    if (r < R) {
-        for (int j = lane; j < L.HID; j += 64) {
-            const float hv = h[r * L.HID + j];
-#pragma unroll
-            for (int a = 0; a < kAMax + 1; ++a) {
-                if (a < L.A) acc[a] += hv * P[L.oWp + (int64_t)a * L.HID + j];
-                else if (a == L.A) acc[a] += hv * P[L.oWv + j];
+    const int64_t chunk = (rows + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = (int64_t)blockIdx.x * chunk;
+    const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+    __shared__ float red[256];
+    const bool wide = C >= 256;
+    const int lanes = wide ? 1 : 256 / C;
+    const int lane = wide ? 0 : (int)threadIdx.x / C;
+    for (int c0 = 0; c0 < (wide ? C : 1); c0 += 256) {
+        const int c = wide ? c0 + (int)threadIdx.x : (int)threadIdx.x % C;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        if (c < C && lane < lanes) {
+            int64_t r = r0 + lane;
+            for (; r + 3 * lanes < r1; r += 4 * lanes) {
+                a0 += X[r * C + c];
+                a1 += X[(r + lanes) * C + c];
+                a2 += X[(r + 2 * lanes) * C + c];
+                a3 += X[(r + 3 * lanes) * C + c];
+            }
+            for (; r < r1; r += lanes) a0 += X[r * C + c];
+        }
+        const float acc = (a0 + a1) + (a2 + a3);
+        if (wide) {
+            if (c < C) part[(int64_t)blockIdx.x * C + c] = acc;
+        } else {
+            red[threadIdx.x] = acc;
+            __syncthreads();
+            if ((int)threadIdx.x < C) {
+                float t = 0.f;
+                for (int l = 0; l < lanes; ++l) t += red[l * C + threadIdx.x];
+                part[(int64_t)blockIdx.x * C + threadIdx.x] = t;
             }
         }
     }
-#pragma unroll
-    for (int a = 0; a < kAMax + 1; ++a) red[wv][a][lane] = acc[a];
-    __syncthreads();
-    if (r < R && lane < A1) {
-        float s = 0.f;
-        for (int l = 0; l < 64; ++l) s += red[wv][lane][l];
-        s += lane < L.A ? P[L.obp + lane] : P[L.obv];
-        z[r * A1 + lane] = s;
-    }
 }
+
+__global__ void k_scatter_head_bias(const float *__restrict__ db, CnnLayout L, float *__restrict__ G)
+{
+    const int a = threadIdx.x;
+    if (a < L.A) G[L.obp + a] = db[a];
+    else if (a == L.A) G[L.obv] = db[a];
+}
+
+// out[i] = sum_p parts[p][i] (fixed order)
+__global__ __launch_bounds__(256) void k_sum_parts(const float *__restrict__ parts, int np, int64_t n,
+                                                   float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int p = 0;
+#pragma unroll 4
+    for (; p + 4 <= np; p += 4) {
+        a0 += parts[(int64_t)p * n + i];
+        a1 += parts[(int64_t)(p + 1) * n + i];
+        a2 += parts[(int64_t)(p + 2) * n + i];
+        a3 += parts[(int64_t)(p + 3) * n + i];
+    }
+    for (; p < np; ++p) a0 += parts[(int64_t)p * n + i];
+    out[i] = (a0 + a1) + (a2 + a3);
+}
+
+
 
 // ---- masked categorical row statistics
 struct MRow {
@@ -324,7 +366,8 @@ __device__ __forceinline__ uint64_t mix64d(uint64_t x)
 }
 
 // ---- rollout: action select over the valid set, log_prob, value.  One thread per env.
-__global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, CnnLayout L, int64_t R, int mode,
+__global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
+                                                 int64_t R, int mode,
                                                  uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
                                                  float *__restrict__ logp, float *__restrict__ value)
 {
@@ -332,7 +375,7 @@ __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, Cn
     if (r >= R) return;
     const int A1 = L.A + 1;
     float zr[kAMax + 1];
-    for (int a = 0; a < A1; ++a) zr[a] = z[r * A1 + a];
+    for (int a = 0; a < A1; ++a) zr[a] = z[r * A1 + a] + (a < L.A ? P[L.obp + a] : P[L.obv]);
     if (value) value[r] = zr[L.A];
     if (!actions) return;
     const MRow h = mrow_stats(zr, L);
@@ -410,7 +453,8 @@ __device__ __forceinline__ void wg_reduce(T (&v)[NV], T *scratch)
 constexpr int kSums = 13;
 
 // ---- the PPO loss of one minibatch with (Masked)Categorical heads; one workgroup.
-__global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, CnnLayout L, int B,
+__global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
+                                                  int B,
                                                   const int32_t *__restrict__ f_act, const float *__restrict__ f_olp,
                                                   const float *__restrict__ f_ov, const float *__restrict__ f_adv,
                                                   const float *__restrict__ f_ret, LossArgs la, float *__restrict__ dz,
@@ -449,7 +493,7 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, C
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
     for (int r = tid; r < B; r += 256) {
         float zr[kAMax + 1];
-        for (int a = 0; a < A1; ++a) zr[a] = z[(int64_t)r * A1 + a];
+        for (int a = 0; a < A1; ++a) zr[a] = z[(int64_t)r * A1 + a] + (a < A ? P[L.obp + a] : P[L.obv]);
         const int act = f_act[r];
         const float olp = f_olp[r], ov = f_ov[r], ret = f_ret[r];
         float adv = f_adv[r];
@@ -577,46 +621,6 @@ __global__ __launch_bounds__(256) void k_cnn_dh(const float *__restrict__ dz, co
     dh[t] = h[t] > 0.f ? s : 0.f;
 }
 
-// ---- head grads: dWp[a][j] = sum_r dz[r][a] h[r][j], dWv, dbp, dbv.  Block per 64 columns j.
-__global__ __launch_bounds__(256) void k_cnn_head_grads(const float *__restrict__ dz, const float *__restrict__ h,
-                                                        CnnLayout L, int B, float *__restrict__ G,
-                                                        const int32_t *__restrict__ stop)
-{
-    if (stop && *stop) return;
-    __shared__ float part[4][kAMax + 1][64];
-    const int A1 = L.A + 1;
-    const int j = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int q = threadIdx.x >> 6;     // row quarter
-    float acc[kAMax + 1];
-#pragma unroll
-    for (int a = 0; a < kAMax + 1; ++a) acc[a] = 0.f;
-    if (j < L.HID) {
-        for (int r = q; r < B; r += 4) {
-            const float hv = h[(int64_t)r * L.HID + j];
-#pragma unroll
-            for (int a = 0; a < kAMax + 1; ++a)
-                if (a < A1) acc[a] += dz[(int64_t)r * A1 + a] * hv;
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < kAMax + 1; ++a) part[q][a][threadIdx.x & 63] = acc[a];
-    __syncthreads();
-    if (q == 0 && j < L.HID) {
-        const int l = threadIdx.x & 63;
-        for (int a = 0; a < A1; ++a) {
-            const float s = ((part[0][a][l] + part[1][a][l]) + part[2][a][l]) + part[3][a][l];
-            if (a < L.A) G[L.oWp + (int64_t)a * L.HID + j] = s;
-            else G[L.oWv + j] = s;
-        }
-    }
-    if (blockIdx.x == 0 && threadIdx.x < A1) {     // bias grads: column sums of dz
-        const int a = threadIdx.x;
-        float s = 0.f;
-        for (int r = 0; r < B; ++r) s += dz[(int64_t)r * A1 + a];
-        if (a < L.A) G[L.obp + a] = s;
-        else G[L.obv] = s;
-    }
-}
 
 // ---- global-norm partials (double) of the flat gradient
 __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__ G, int64_t n, double *__restrict__ part,
@@ -718,15 +722,38 @@ int gemm_rm(rocblas_handle hb, bool ta, bool tb, int64_t M, int64_t N, int64_t K
     return GS_OK;
 }
 
-// bias grad: db[c] = sum over rows of X[rows][C] (gemv against the ones vector)
-int colsum(rocblas_handle hb, const float *X, int64_t rows, int C, const float *ones, float *db)
+inline unsigned nblk(int64_t n);
+
+// bias grad: db[c] = sum over rows of X[rows][C] (two deterministic passes)
+int colsum(const float *X, int64_t rows, int C, float *parts, float *db, hipStream_t s)
 {
+    int np = (int)std::min<int64_t>(kColParts, std::max<int64_t>(1, rows / 128));
+    hipLaunchKernelGGL(k_colsum_part, dim3(np), dim3(256), 0, s, X, rows, C, parts);
+    hipLaunchKernelGGL(k_sum_parts, dim3(nblk(C)), dim3(256), 0, s, parts, np, (int64_t)C, db);
+    GS_LAUNCH_CHECK("k_colsum");
+    return GS_OK;
+}
+
+// weight grad dW[Cout][K] = dY[M][Cout]^T cols[M][K] with M = B * positions: split over kSplitK
+// sample groups as one strided-batched GEMM into partials, then a fixed-order sum
+int wgrad(rocblas_handle hb, const float *dY, const float *cols, int64_t B, int64_t hw, int Cout, int K,
+          float *parts, float *dW, hipStream_t s)
+{
+    const int S = (B % kSplitK == 0) ? kSplitK : 1;
+    const int64_t Mc = B / S * hw;
     const float one = 1.0f, zero = 0.0f;
-    const rocblas_status st = rocblas_sgemv(hb, rocblas_operation_none, C, (rocblas_int)rows, &one, X, C, ones, 1,
-                                            &zero, db, 1);
+    const rocblas_status st = rocblas_sgemm_strided_batched(
+        hb, rocblas_operation_none, rocblas_operation_transpose, K, Cout, (rocblas_int)Mc, &one, cols, K,
+        (rocblas_stride)(Mc * K), dY, Cout, (rocblas_stride)(Mc * Cout), &zero, S == 1 ? dW : parts, K,
+        (rocblas_stride)((int64_t)Cout * K), S);
     if (st != rocblas_status_success) {
-        set_error("rocblas_sgemv failed: %s", rocblas_status_to_string(st));
+        set_error("rocblas_sgemm_strided_batched (wgrad) failed: %s", rocblas_status_to_string(st));
         return GS_E_HIP;
+    }
+    if (S > 1) {
+        const int64_t n = (int64_t)Cout * K;
+        hipLaunchKernelGGL(k_sum_parts, dim3(nblk(n)), dim3(256), 0, s, parts, S, n, dW);
+        GS_LAUNCH_CHECK("k_sum_parts");
     }
     return GS_OK;
 }
@@ -782,8 +809,10 @@ int forward(const float *P, const CnnLayout &L, const uint8_t *obs, const int32_
     hipLaunchKernelGGL(k_bias_relu, dim3(nblk(m3 * L.c3 / 4)), dim3(256), 0, s, w.a3, P + L.ob3, m3, L.c3);
     if ((rc = gemm_rm(hb, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, 0.f, w.h, L.HID))) return rc;
     hipLaunchKernelGGL(k_bias_relu, dim3(nblk(R * L.HID / 4)), dim3(256), 0, s, w.h, P + L.obf, R, L.HID);
-    hipLaunchKernelGGL(k_cnn_heads, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, s, w.h, P, L, R, w.z);
-    GS_LAUNCH_CHECK("k_cnn_heads");
+    // heads: z[r][0:A] = h Wp^T, z[r][A] = h Wv^T (row stride A+1); biases are added where z is read
+    if ((rc = gemm_rm(hb, false, true, R, L.A, L.HID, w.h, L.HID, P + L.oWp, L.HID, 0.f, w.z, L.A + 1))) return rc;
+    if ((rc = gemm_rm(hb, false, true, R, 1, L.HID, w.h, L.HID, P + L.oWv, L.HID, 0.f, w.z + L.A, L.A + 1)))
+        return rc;
     return GS_OK;
 }
 
@@ -792,31 +821,34 @@ int backward(const float *P, const CnnLayout &L, int64_t B, const CnnWs &w, floa
 {
     int rc;
     const int64_t m1 = L.rows1(B), m2 = L.rows2(B), m3 = L.rows3(B);
-    hipLaunchKernelGGL(k_cnn_head_grads, dim3((unsigned)((L.HID + 63) / 64)), dim3(256), 0, s, w.dz, w.h, L, (int)B,
-                       G, stop);
-    GS_LAUNCH_CHECK("k_cnn_head_grads");
+    // head grads: dWp = dz[:, :A]^T h, dWv = dz[:, A]^T h, biases = column sums of dz
+    if ((rc = gemm_rm(hb, true, false, L.A, L.HID, B, w.dz, L.A + 1, w.h, L.HID, 0.f, G + L.oWp, L.HID))) return rc;
+    if ((rc = gemm_rm(hb, true, false, 1, L.HID, B, w.dz + L.A, L.A + 1, w.h, L.HID, 0.f, G + L.oWv, L.HID)))
+        return rc;
+    if ((rc = colsum(w.dz, B, L.A + 1, w.parts, w.dhead_b, s))) return rc;
+    hipLaunchKernelGGL(k_scatter_head_bias, dim3(1), dim3(64), 0, s, w.dhead_b, L, G);
     hipLaunchKernelGGL(k_cnn_dh, dim3(nblk(B * L.HID)), dim3(256), 0, s, w.dz, P, L, w.h, B, w.dh, stop);
     // fc
-    if ((rc = colsum(hb, w.dh, B, L.HID, w.ones, G + L.obf))) return rc;
+    if ((rc = colsum(w.dh, B, L.HID, w.parts, G + L.obf, s))) return rc;
     if ((rc = gemm_rm(hb, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, 0.f, G + L.oWf, L.F))) return rc;
     if ((rc = gemm_rm(hb, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, 0.f, w.da3, L.F))) return rc;
     hipLaunchKernelGGL(k_relu_mask, dim3(nblk(B * L.F / 4)), dim3(256), 0, s, w.da3, w.a3, B * L.F / 4);
     // conv3 (dY3 = da3 as [m3][c3])
-    if ((rc = colsum(hb, w.da3, m3, L.c3, w.ones, G + L.ob3))) return rc;
-    if ((rc = gemm_rm(hb, true, false, L.c3, L.K3, m3, w.da3, L.c3, w.cols3, L.K3, 0.f, G + L.oW3, L.K3))) return rc;
+    if ((rc = colsum(w.da3, m3, L.c3, w.parts, G + L.ob3, s))) return rc;
+    if ((rc = wgrad(hb, w.da3, w.cols3, B, (int64_t)L.h3 * L.w3, L.c3, L.K3, w.parts, G + L.oW3, s))) return rc;
     if ((rc = gemm_rm(hb, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, 0.f, w.cols3, L.K3))) return rc;
     hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(m2 * (L.c2 / 4))), dim3(256), 0, s, w.cols3, w.a2, B, L.h2, L.w2,
                        L.c2, L.k3, L.s3, L.h3, L.w3, w.da2);
     GS_LAUNCH_CHECK("k_col2im_relu");
     // conv2
-    if ((rc = colsum(hb, w.da2, m2, L.c2, w.ones, G + L.ob2))) return rc;
-    if ((rc = gemm_rm(hb, true, false, L.c2, L.K2, m2, w.da2, L.c2, w.cols2, L.K2, 0.f, G + L.oW2, L.K2))) return rc;
+    if ((rc = colsum(w.da2, m2, L.c2, w.parts, G + L.ob2, s))) return rc;
+    if ((rc = wgrad(hb, w.da2, w.cols2, B, (int64_t)L.h2 * L.w2, L.c2, L.K2, w.parts, G + L.oW2, s))) return rc;
     if ((rc = gemm_rm(hb, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, 0.f, w.cols2, L.K2))) return rc;
     hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(m1 * (L.c1 / 4))), dim3(256), 0, s, w.cols2, w.a1, B, L.h1, L.w1,
                        L.c1, L.k2, L.s2, L.h2, L.w2, w.da1);
     // conv1 (no input gradient)
-    if ((rc = colsum(hb, w.da1, m1, L.c1, w.ones, G + L.ob1))) return rc;
-    return gemm_rm(hb, true, false, L.c1, L.K1, m1, w.da1, L.c1, w.cols1, L.K1, 0.f, G + L.oW1, L.K1);
+    if ((rc = colsum(w.da1, m1, L.c1, w.parts, G + L.ob1, s))) return rc;
+    return wgrad(hb, w.da1, w.cols1, B, (int64_t)L.h1 * L.w1, L.c1, L.K1, w.parts, G + L.oW1, s);
 }
 
 AdamArgs adam_args(const gs_ppo_hparams &hp, int64_t t)
@@ -871,7 +903,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
                        ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
     GS_LAUNCH_CHECK("k_gather_fields");
     if ((rc = forward(P, L, ro.obs, idx, ro.T, ro.N, B, w, hb, s))) return rc;
-    hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, L, (int)B, w.f_act, w.f_olp, w.f_ov, w.f_adv,
+    hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, P, L, (int)B, w.f_act, w.f_olp, w.f_ov, w.f_adv,
                        w.f_ret, loss_args(hp), w.dz, metrics, stop);
     GS_LAUNCH_CHECK("k_cnn_loss");
     if ((rc = backward(P, L, B, w, G, stop, hb, s))) return rc;
@@ -888,13 +920,6 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     return GS_OK;
 }
 
-int init_ones(const CnnLayout &L, int64_t R, const CnnWs &w, hipStream_t s)
-{
-    const int64_t n = L.rows1(R);
-    hipLaunchKernelGGL(k_fill, dim3(nblk(n)), dim3(256), 0, s, w.ones, n, 1.0f);
-    GS_LAUNCH_CHECK("k_fill");
-    return GS_OK;
-}
 
 }  // namespace
 }  // namespace gs
@@ -930,7 +955,7 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     rocblas_handle hb;
     if ((rc = blas_for(s, &hb))) return rc;
     if ((rc = forward(params, L, obs, nullptr, 1, N, N, w, hb, s))) return rc;
-    hipLaunchKernelGGL(k_cnn_act, dim3(nblk(N)), dim3(256), 0, s, w.z, L, N, mode, rng_seed, rng_counter, actions,
+    hipLaunchKernelGGL(k_cnn_act, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed, rng_counter, actions,
                        logp, value);
     GS_LAUNCH_CHECK("k_cnn_act");
     return GS_OK;
@@ -952,7 +977,7 @@ extern "C" int gs_cnn_ppo_loss(const float *params, gs_cnn_dims dims, gs_ppo_hpa
     hipLaunchKernelGGL(k_gather_fields, dim3(nblk(batch)), dim3(256), 0, s, idx, batch, ro.T, ro.N, ro.actions,
                        ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
     if ((rc = forward(params, L, ro.obs, idx, ro.T, ro.N, batch, w, hb, s))) return rc;
-    hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, L, (int)batch, w.f_act, w.f_olp, w.f_ov, w.f_adv,
+    hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, params, L, (int)batch, w.f_act, w.f_olp, w.f_ov, w.f_adv,
                        w.f_ret, loss_args(hp), dlogits_out ? dlogits_out : w.dz, metrics, nullptr);
     GS_LAUNCH_CHECK("k_cnn_loss");
     return GS_OK;
@@ -972,7 +997,6 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     if ((rc = ensure_lut())) return rc;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
-    if ((rc = init_ones(L, batch, w, s))) return rc;
     for (int64_t k = 0; k < n_minibatches; ++k) {
         rc = cnn_step(params, grads, adam_m, adam_v, L, hp, ro, idx + k * batch, batch, adam_step0 + k + 1,
                       metrics + k * GS_NUM_METRICS, stop_flag, w, comm, s);

@@ -150,4 +150,83 @@ def run_cpu_baseline(n_envs=4096, n_steps=32, batch=256, n_epochs=20, obs_dim=4,
                 wall_s=t4 - t0, threads=torch.get_num_threads())
 
 
+class _CNNActorCritic(nn.Module):
+    """CNNActorCritic restated (utils/models.py:347-455): NatureCNN trunk, fc 512, masked heads."""
+
+    def __init__(self, C, A, hidden, valid):
+        super().__init__()
+        self.cnn = nn.Sequential(nn.Conv2d(C, 32, 8, 4), nn.ReLU(), nn.Conv2d(32, 64, 4, 2), nn.ReLU(),
+                                 nn.Conv2d(64, 64, 3, 1), nn.ReLU(), nn.Flatten())
+        self.mlp = nn.Sequential(nn.Linear(64 * 7 * 7, hidden), nn.ReLU())
+        self.policy_head = nn.Linear(hidden, A)
+        self.value_head = nn.Linear(hidden, 1)
+        self.valid = valid
+
+    def forward(self, obs):
+        from .cnn_ref import dist_terms  # noqa: F401  (same masked-categorical semantics)
+        x = self.mlp(self.cnn(obs.to(torch.float32) / 255.0))
+        logits = self.policy_head(x)
+        if self.valid is not None:
+            mask = torch.ones_like(logits, dtype=torch.bool)
+            mask[:, self.valid] = False
+            logits = logits.masked_fill(mask, float("-inf"))
+        return logits, self.value_head(x).squeeze(-1)
+
+
+def run_cpu_baseline_cnn(n_envs=256, n_steps=256, batch=1024, n_epochs=15, in_shape=(4, 84, 84), n_actions=18,
+                         valid=(0, 3, 4), hidden=512, clip=0.2, ent_coef=0.01, lr=3e-4, sample_steps=8,
+                         sample_minibatches=3, threads=None, seed=42):
+    """Bounded CPU sample of the pixel path (C4/C5): `sample_steps` vector steps of the rollout
+    policy forward + sampling and `sample_minibatches` full minibatch steps (forward, masked PPO
+    loss, backward, clip, Adam), each extrapolated to the full rollout / update.  The frame source
+    is a pre-made u8 stack (the reference's ALE emulation and preprocessing run in ale-py C++,
+    not available here): env cost is EXCLUDED, which flatters the CPU number."""
+    from .cnn_ref import dist_terms
+    if threads:
+        torch.set_num_threads(int(threads))
+    torch.manual_seed(seed)
+    valid = list(valid) if valid is not None else None
+    model = _CNNActorCritic(in_shape[0], n_actions, hidden, valid)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    g = torch.Generator().manual_seed(seed)
+    obs = torch.randint(0, 256, (n_envs, *in_shape), dtype=torch.uint8, generator=g)
+    t0 = time.perf_counter()
+    with torch.inference_mode():
+        for _ in range(sample_steps):
+            logits, v = model(obs)
+            a = torch.distributions.Categorical(logits=logits).sample()
+            dist_terms(logits, a, valid)
+            a.numpy(), v.numpy()
+    t1 = time.perf_counter()
+    mb_obs = torch.randint(0, 256, (batch, *in_shape), dtype=torch.uint8, generator=g)
+    va = torch.tensor(valid if valid is not None else list(range(n_actions)))
+    act = va[torch.randint(0, len(va), (batch,), generator=g)]
+    old_lp = torch.full((batch,), float(np.log(1.0 / len(va))))
+    old_v = torch.zeros(batch)
+    adv = torch.randn(batch, generator=g)
+    ret = adv.clone()
+    t2 = time.perf_counter()
+    for _ in range(sample_minibatches):
+        a_n = (adv - adv.mean()) / (adv.std() + 1e-8)
+        logits, v = model(mb_obs)
+        lp, H = dist_terms(logits, act, valid)
+        ratio = torch.exp(lp - old_lp)
+        pl = -torch.min(a_n * ratio, a_n * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+        vd = v - old_v
+        vl = torch.max((v - ret) ** 2, (old_v + torch.clamp(vd, -0.2, 0.2) - ret) ** 2).mean()
+        loss = pl + 0.5 * vl - ent_coef * H.mean()
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
+        opt.step()
+        loss.item()
+    t3 = time.perf_counter()
+    per_step = (t1 - t0) / sample_steps
+    per_mb = (t3 - t2) / sample_minibatches
+    n_mb = n_envs * n_steps // batch * n_epochs
+    total = per_step * n_steps + per_mb * n_mb
+    return dict(env_steps_per_s=n_envs * n_steps / total, step_s=per_step, minibatch_s=per_mb,
+                minibatches_per_rollout=n_mb, wall_s=t3 - t0, threads=torch.get_num_threads())
+
+
 _ = ppo_ref
