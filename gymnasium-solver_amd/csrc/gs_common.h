@@ -137,6 +137,19 @@ struct RowGather {
 };
 Workspace carve_workspace(void *base, const Layout &L, int64_t B);
 
+// Fused update path (gs_ppo_update): per-update gathered minibatch fields and the in-kernel
+// head combine + row loss of k_fwd_hidden<S, true>.  Arrays are [k][B] over the update's
+// minibatches; k = k_local + *step_base (graph chunk replay) or k_local (eager).
+struct FusedFwd {
+    const float *xg;           // (n, B, D) gathered observations
+    const int32_t *fa;         // (n, B) actions
+    const float *folp, *fov, *fadv, *fret;   // (n, B) old logp, old value, normalised adv, return
+    double *mpart;             // (n, B/16, 14) per-row-block metric sums
+    float *dz;                 // (B, A+1) dLoss/dlogits | dLoss/dvalue of the current step
+    const int64_t *step_base;
+    int k_local;
+};
+
 struct LossArgs {
     float clip_lo, clip_hi;     // f32(1 - clip), f32(1 + clip) (torch clamp casts scalars to f32)
     float clip_vf;              // f32(clip_range_vf)
@@ -167,6 +180,17 @@ inline int n_col_blocks(int H) { return (H + kTile - 1) / kTile; }
 inline int n_sumsq_slots(const Layout &L) { return n_col_blocks(L.H2) * n_col_blocks(L.H1) + 2 * n_col_blocks(L.H2) + 1; }
 
 // kernels' launch helpers (gs_mlp.hip)
+int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
+                     const Workspace &ws, const int32_t *stop, hipStream_t s);
+int launch_loss_rows(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
+                     const Workspace &ws, const int32_t *stop, hipStream_t s);
+int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx, const float *obs,
+                      const int64_t *actions, const float *logprobs, const float *values, const float *advantages,
+                      const float *returns, int64_t T, int64_t N, int normalize, const FusedFwd &ff, float *metrics,
+                      hipStream_t s);
+int launch_metrics_all(const Layout &L, int64_t B, int64_t n, const FusedFwd &ff, const LossArgs &la, float *metrics,
+                       hipStream_t s);
+bool has_fused(const Layout &L, int64_t B);
 int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, const int32_t *idx,
                       int64_t T, int64_t N, int64_t rows, float *x_out, float *h1_out, float *h2_out,
                       float *zpart, float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s);

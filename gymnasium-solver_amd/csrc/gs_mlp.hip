@@ -70,6 +70,8 @@ __device__ __forceinline__ T wave_sum(T v)
 
 __host__ __device__ constexpr int round4(int n) { return (n + 3) & ~3; }
 
+constexpr int kNumSums = 14;   // metric sums of one minibatch (loss_row)
+
 // Sum NV per-thread values over the 256-thread block in a fixed order (deterministic),
 // through LDS (two levels of 16) — __shfl would lower to ds_bpermute chains (~100+ cycles
 // per step).  Every thread returns the totals.  scratch: NV*(256+16) elements of T.
@@ -128,11 +130,24 @@ size_t fwd_lds_bytes(const Layout &L)
     return n * sizeof(float);
 }
 
-template <class S>
+template <int AMAX, int AEX>
+__device__ __forceinline__ void gather_head_row(const float *__restrict__ zpart, const float *__restrict__ P,
+                                                const Layout &L, int64_t r, float (&z)[AMAX + 1]);
+template <int AMAX>
+__device__ __forceinline__ void loss_row(const float (&z)[AMAX + 1], int A, int act, float olp, float ov, float adv,
+                                         float ret, const LossArgs &la, float invB, float *__restrict__ dzr,
+                                         double (&acc)[14]);
+
+// FUSED (gs_ppo_update path): x comes pre-gathered (FusedFwd::xg, one load instead of the
+// index -> row -> obs chain).  The head combine stays in the next launch (k_loss_rows): an
+// in-launch last-arriver combine costs a release + acquire fence pair (~1.7 us each on
+// gfx950) on top of the skew wait, more than the ~1.45 us kernel boundary it would remove.
+template <class S, bool FUSED>
 __global__ __launch_bounds__(256) void k_fwd_hidden(
     const float *__restrict__ P, Layout Lrt, const float *__restrict__ obs, const int32_t *__restrict__ idx, int T,
     int N, int rows, float *__restrict__ x_out, float *__restrict__ h1_out, float *__restrict__ h2_out,
-    float *__restrict__ zpart, float *__restrict__ obs_copy, const int32_t *__restrict__ stop, RowGather rg)
+    float *__restrict__ zpart, float *__restrict__ obs_copy, const int32_t *__restrict__ stop, RowGather rg,
+    FusedFwd ff, LossArgs la)
 {
     GS_STAMP_BEGIN(0)
     if (stop && *stop) return;
@@ -156,10 +171,16 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     float *h2s = red + 1024;
 
     if (rg.step_base && idx) idx += *rg.step_base * rows;
+    const int64_t kstep = FUSED ? ff.k_local + (ff.step_base ? *ff.step_base : 0) : 0;
     // ---- phase 0: every operand of this workgroup, all loads in flight together.
     //      Threads 0..15 run the dependent idx -> row -> obs/fields chain while the rest
     //      of the block streams the weights into LDS.
-    if (tid < kTile) {
+    if (FUSED) {
+        if (tid < kTile * D) {
+            const int i = tid / D;
+            xs[tid] = r0 + i < rows ? ff.xg[(kstep * rows + r0) * D + tid] : 0.0f;
+        }
+    } else if (tid < kTile) {
         const int r = r0 + tid;
         const int src = r < rows ? (idx ? sample_row(idx[r], T, N) : r) : -1;
         srcs[tid] = src;
@@ -298,10 +319,11 @@ int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, co
     if (rg) g = *rg;
     return with_shape(L, 0, [&](auto sh) {
         using Sh = decltype(sh);
-        int rc = set_lds_limit((const void *)k_fwd_hidden<Sh>, fwd_lds_bytes(L));
+        int rc = set_lds_limit((const void *)k_fwd_hidden<Sh, false>, fwd_lds_bytes(L));
         if (rc) return rc;
-        hipLaunchKernelGGL(k_fwd_hidden<Sh>, grid, dim3(256), fwd_lds_bytes(L), s, params, L, obs, idx, (int)T,
-                           (int)N, (int)rows, x_out, h1_out, h2_out, zpart, obs_copy, stop_flag, g);
+        hipLaunchKernelGGL((k_fwd_hidden<Sh, false>), grid, dim3(256), fwd_lds_bytes(L), s, params, L, obs, idx,
+                           (int)T, (int)N, (int)rows, x_out, h1_out, h2_out, zpart, obs_copy, stop_flag, g,
+                           FusedFwd{}, LossArgs{});
         GS_LAUNCH_CHECK("k_fwd_hidden");
         return GS_OK;
     });
@@ -450,9 +472,122 @@ __global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, 
 }
 
 // ------------------------------------------------------------------------------------
+// One minibatch row of PPOAgent.losses_for_batch (agents/ppo/ppo_agent.py:21-152) with its
+// analytic gradients: z = raw logits | value, adv already batch-normalised.  Writes
+// dLoss/dlogits | dLoss/dvalue to dzr and adds the row's terms to the 14 metric sums.
+// ------------------------------------------------------------------------------------
+template <int AMAX>
+__device__ __forceinline__ void loss_row(const float (&z)[AMAX + 1], int A, int act, float olp, float ov, float adv,
+                                         float ret, const LossArgs &la, float invB, float *__restrict__ dzr,
+                                         double (&acc)[kNumSums])
+{
+    float v = 0.0f;
+#pragma unroll
+    for (int a = 0; a < AMAX + 1; ++a)
+        if (a == A) v = z[a];
+    const HeadRow h = head_stats<AMAX>(z, A);
+    const float invS = 1.0f / h.S;
+    // ln = normalised logits, p = softmax(ln) (Categorical.probs), pe = exp(ln)
+    float ln[AMAX], p[AMAX];
+    float H = 0.0f, lp = 0.0f;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+        ln[a] = z[a] - h.lse;
+        p[a] = a < A ? expf(ln[a] - h.m2) * invS : 0.0f;
+        if (a < A) {
+            H += fmaxf(ln[a], -FLT_MAX) * p[a];   // entropy: -sum clamp(ln, f32min) * p
+            if (a == act) lp = ln[a];
+        }
+    }
+    H = -H;
+    const float ratio = expf(lp - olp);
+    const float rc = fminf(fmaxf(ratio, la.clip_lo), la.clip_hi);
+    const float s1 = adv * ratio, s2 = adv * rc;
+    const float mn = fminf(s1, s2);
+    const float vdelta = v - ov;
+    const float du = v - ret;
+    const float vu = du * du;
+    const float vcl = ov + fminf(fmaxf(vdelta, -la.clip_vf), la.clip_vf);
+    const float dc = vcl - ret;
+    const float vc = dc * dc;
+    const float vmax = fmaxf(vu, vc);
+    const float ldiff = fminf(fmaxf(lp - olp, -20.0f), 20.0f);
+    const float r2 = expf(ldiff);
+    const float akl = (r2 - 1.0f) - logf(r2);
+    const float rv = ret - v;
+    acc[0] += (double)mn;
+    acc[1] += (double)vmax;
+    acc[2] += (double)H;
+    acc[3] += (ratio < la.clip_lo || ratio > la.clip_hi) ? 1.0 : 0.0;
+    acc[4] += (vdelta < -la.clip_vf || vdelta > la.clip_vf) ? 1.0 : 0.0;
+    acc[5] += (double)(olp - lp);
+    acc[6] += (double)akl;
+    acc[7] += (double)rv;
+    acc[8] += (double)rv * (double)rv;
+    acc[9] += (double)ret;
+    acc[10] += (double)ret * (double)ret;
+    acc[11] += (double)adv;
+    acc[12] += (double)adv * (double)adv;
+    // ---- analytic gradients (torch autograd tie rules: min/max ties split halves)
+    const float ga = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+    const float gb = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+    const float inclip = (ratio >= la.clip_lo && ratio <= la.clip_hi) ? 1.0f : 0.0f;
+    const float g_mn = -invB;
+    const float dratio = adv * (g_mn * ga) + adv * (g_mn * gb) * inclip;
+    const float dlp = dratio * ratio;
+    const float dH = -la.ent_coef * invB;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+        if (a < A) {
+            const float pe = expf(ln[a]);   // softmax(z) as seen by logsumexp backward
+            float g = dlp * ((a == act ? 1.0f : 0.0f) - pe);
+            g += dH * (-p[a] * (ln[a] + H));
+            dzr[a] = g;
+        }
+    }
+    const float hu = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+    const float hc = vc > vu ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+    const float invc = (vdelta >= -la.clip_vf && vdelta <= la.clip_vf) ? 1.0f : 0.0f;
+    const float gv = la.vf_coef * invB;
+    dzr[A] = (gv * hu) * (2.0f * du) + (gv * hc) * (2.0f * dc) * invc;
+}
+
+// metrics record from the 14 sums (shared by k_loss and the fused path's k_metrics_all)
+__device__ __forceinline__ void write_metrics(const double *t, double Bd, const LossArgs &la, float *metrics,
+                                              bool adv_stats)
+{
+    const float pl = (float)(-t[0] / Bd);
+    const float vl = (float)(t[1] / Bd);
+    const float ent = (float)(t[2] / Bd);
+    const float loss = pl + la.vf_coef * vl + la.ent_coef * (-ent);
+    const double var_rv = (t[8] - t[7] * t[7] / Bd) / (Bd - 1.0);
+    const double var_r = (t[10] - t[9] * t[9] / Bd) / (Bd - 1.0);
+    const float approx_kl = (float)(t[6] / Bd);
+    const bool kl_stop = la.target_kl > 0.0f && approx_kl > la.target_kl;
+    metrics[GS_M_LOSS] = loss;
+    metrics[GS_M_POLICY_LOSS] = pl;
+    metrics[GS_M_VALUE_LOSS] = vl;
+    metrics[GS_M_ENTROPY] = ent;
+    metrics[GS_M_CLIP_FRAC] = (float)(t[3] / Bd);
+    metrics[GS_M_CLIP_FRAC_VF] = (float)(t[4] / Bd);
+    metrics[GS_M_EXPLAINED_VAR] = (float)(1.0 - var_rv / var_r);
+    metrics[GS_M_KL] = (float)(t[5] / Bd);
+    metrics[GS_M_APPROX_KL] = approx_kl;
+    if (adv_stats) {
+        const double amean = t[11] / Bd;
+        const double astd = sqrt(fmax(0.0, (t[12] - t[11] * t[11] / Bd) / (Bd - 1.0)));
+        metrics[GS_M_ADV_NORM_MEAN] = la.normalize ? (float)amean : 0.0f;
+        metrics[GS_M_ADV_NORM_STD] = la.normalize ? (float)astd : 0.0f;
+    }
+    metrics[GS_M_KL_STOP] = kl_stop ? 1.0f : 0.0f;
+    metrics[GS_M_SKIPPED] = kl_stop ? 1.0f : 0.0f;
+    metrics[GS_M_RES0] = 0.0f;
+    metrics[GS_M_RES1] = 0.0f;
+}
+
+// ------------------------------------------------------------------------------------
 // k_loss: single workgroup of 256 threads over the B <= 1024 minibatch rows.
 // ------------------------------------------------------------------------------------
-constexpr int kNumSums = 14;
 
 
 template <class S>
@@ -506,114 +641,18 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
         // every input of the row first (one round trip), then the math
         float z[AMAX + 1];
         gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
-        const int act = f_act[r];
-        const float olp = f_olp[r], ov = f_ov[r], ret = f_ret[r];
         float adv = f_adv[r];
-        float v = 0.0f;
-#pragma unroll
-        for (int a = 0; a < AMAX + 1; ++a)
-            if (a == A) v = z[a];
-        const HeadRow h = head_stats<AMAX>(z, A);
-        const float invS = 1.0f / h.S;
-        // ln = normalised logits, p = softmax(ln) (Categorical.probs), pe = exp(ln)
-        float ln[AMAX], p[AMAX];
-        float H = 0.0f, lp = 0.0f;
-#pragma unroll
-        for (int a = 0; a < AMAX; ++a) {
-            ln[a] = z[a] - h.lse;
-            p[a] = a < A ? expf(ln[a] - h.m2) * invS : 0.0f;
-            if (a < A) {
-                H += fmaxf(ln[a], -FLT_MAX) * p[a];   // entropy: -sum clamp(ln, f32min) * p
-                if (a == act) lp = ln[a];
-            }
-        }
-        H = -H;
         if (la.normalize) adv = (adv - meanf) / (stdf + 1e-8f);
-        const float ratio = expf(lp - olp);
-        const float rc = fminf(fmaxf(ratio, la.clip_lo), la.clip_hi);
-        const float s1 = adv * ratio, s2 = adv * rc;
-        const float mn = fminf(s1, s2);
-        const float vdelta = v - ov;
-        const float du = v - ret;
-        const float vu = du * du;
-        const float vcl = ov + fminf(fmaxf(vdelta, -la.clip_vf), la.clip_vf);
-        const float dc = vcl - ret;
-        const float vc = dc * dc;
-        const float vmax = fmaxf(vu, vc);
-        const float ldiff = fminf(fmaxf(lp - olp, -20.0f), 20.0f);
-        const float r2 = expf(ldiff);
-        const float akl = (r2 - 1.0f) - logf(r2);
-        const float rv = ret - v;
-        acc[0] += (double)mn;
-        acc[1] += (double)vmax;
-        acc[2] += (double)H;
-        acc[3] += (ratio < la.clip_lo || ratio > la.clip_hi) ? 1.0 : 0.0;
-        acc[4] += (vdelta < -la.clip_vf || vdelta > la.clip_vf) ? 1.0 : 0.0;
-        acc[5] += (double)(olp - lp);
-        acc[6] += (double)akl;
-        acc[7] += (double)rv;
-        acc[8] += (double)rv * (double)rv;
-        acc[9] += (double)ret;
-        acc[10] += (double)ret * (double)ret;
-        acc[11] += (double)adv;
-        acc[12] += (double)adv * (double)adv;
-        // ---- analytic gradients (torch autograd tie rules: min/max ties split halves)
-        const float ga = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-        const float gb = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-        const float inclip = (ratio >= la.clip_lo && ratio <= la.clip_hi) ? 1.0f : 0.0f;
-        const float g_mn = -invB;
-        const float dratio = adv * (g_mn * ga) + adv * (g_mn * gb) * inclip;
-        const float dlp = dratio * ratio;
-        const float dH = -la.ent_coef * invB;
-        float *dzr = dz + (int64_t)r * A1;
-#pragma unroll
-        for (int a = 0; a < AMAX; ++a) {
-            if (a < A) {
-                const float pe = expf(ln[a]);   // softmax(z) as seen by logsumexp backward
-                float g = dlp * ((a == act ? 1.0f : 0.0f) - pe);
-                g += dH * (-p[a] * (ln[a] + H));
-                dzr[a] = g;
-            }
-        }
-        const float hu = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
-        const float hc = vc > vu ? 1.0f : (vu == vc ? 0.5f : 0.0f);
-        const float invc = (vdelta >= -la.clip_vf && vdelta <= la.clip_vf) ? 1.0f : 0.0f;
-        const float gv = la.vf_coef * invB;
-        dzr[A] = (gv * hu) * (2.0f * du) + (gv * hc) * (2.0f * dc) * invc;
+        loss_row<AMAX>(z, A, f_act[r], f_olp[r], f_ov[r], adv, f_ret[r], la, invB, dz + (int64_t)r * A1, acc);
     }
     GS_STAMP(1)
     block_reduce<kNumSums>(acc, sred);     // fixed order -> deterministic
     GS_STAMP(2)
     if (tid == 0) {
-        const double *t = acc;
-        const double Bd = (double)B;
-        const float pl = (float)(-t[0] / Bd);
-        const float vl = (float)(t[1] / Bd);
-        const float ent = (float)(t[2] / Bd);
-        const float loss = pl + la.vf_coef * vl + la.ent_coef * (-ent);
-        const double var_rv = (t[8] - t[7] * t[7] / Bd) / (Bd - 1.0);
-        const double var_r = (t[10] - t[9] * t[9] / Bd) / (Bd - 1.0);
-        const double amean = t[11] / Bd;
-        const double astd = sqrt(fmax(0.0, (t[12] - t[11] * t[11] / Bd) / (Bd - 1.0)));
-        const float approx_kl = (float)(t[6] / Bd);
-        const bool kl_stop = la.target_kl > 0.0f && approx_kl > la.target_kl;
-        metrics[GS_M_LOSS] = loss;
-        metrics[GS_M_POLICY_LOSS] = pl;
-        metrics[GS_M_VALUE_LOSS] = vl;
-        metrics[GS_M_ENTROPY] = ent;
-        metrics[GS_M_CLIP_FRAC] = (float)(t[3] / Bd);
-        metrics[GS_M_CLIP_FRAC_VF] = (float)(t[4] / Bd);
-        metrics[GS_M_EXPLAINED_VAR] = (float)(1.0 - var_rv / var_r);
-        metrics[GS_M_KL] = (float)(t[5] / Bd);
-        metrics[GS_M_APPROX_KL] = approx_kl;
-        metrics[GS_M_ADV_NORM_MEAN] = la.normalize ? (float)amean : 0.0f;
-        metrics[GS_M_ADV_NORM_STD] = la.normalize ? (float)astd : 0.0f;
-        metrics[GS_M_KL_STOP] = kl_stop ? 1.0f : 0.0f;
+        write_metrics(acc, (double)B, la, metrics, true);
         metrics[GS_M_GRAD_NORM] = 0.0f;
-        metrics[GS_M_SKIPPED] = kl_stop ? 1.0f : 0.0f;
-        metrics[GS_M_RES0] = 0.0f;
-        metrics[GS_M_RES1] = 0.0f;
-        if (kl_stop && stop) *stop = 1;
+        const float approx_kl = (float)(acc[6] / (double)B);
+        if (la.target_kl > 0.0f && approx_kl > la.target_kl && stop) *stop = 1;
     }
     GS_STAMP_END(3)
 }
@@ -1161,8 +1200,13 @@ int prepare_kernels(const Layout &L, int64_t B)
         return set_lds_limit((const void *)k_bwd<decltype(sh)>, bwd_lds_bytes(L, B));
     });
     if (rc) return rc;
-    return with_shape(L, 0, [&](auto sh) {
-        return set_lds_limit((const void *)k_fwd_hidden<decltype(sh)>, fwd_lds_bytes(L));
+    rc = with_shape(L, 0, [&](auto sh) {
+        return set_lds_limit((const void *)k_fwd_hidden<decltype(sh), false>, fwd_lds_bytes(L));
+    });
+    if (rc) return rc;
+    if (!has_fused(L, B)) return GS_OK;
+    return with_shape(L, B, [&](auto sh) {
+        return set_lds_limit((const void *)k_fwd_hidden<decltype(sh), true>, fwd_lds_bytes(L));
     });
 }
 
@@ -1219,6 +1263,202 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
         GS_LAUNCH_CHECK("k_clip_adam");
         return GS_OK;
     });
+}
+
+// ------------------------------------------------------------------------------------
+// fused update path: per-update gather, per-update metrics
+// ------------------------------------------------------------------------------------
+// One workgroup per minibatch k: gather its B rows through the sampler indices, batch
+// advantage normalisation (utils/torch.py:97-99, same double arithmetic as k_loss), and
+// the ADV_NORM metrics of the normalised advantages.
+template <class S>
+__global__ __launch_bounds__(256) void k_gather_all(const int32_t *__restrict__ idx, int Brt, const float *__restrict__ obs,
+                                                    const int64_t *__restrict__ actions,
+                                                    const float *__restrict__ logprobs, const float *__restrict__ values,
+                                                    const float *__restrict__ advantages,
+                                                    const float *__restrict__ returns, int T, int N, int D,
+                                                    int normalize, FusedFwd ff, float *__restrict__ metrics)
+{
+    __shared__ double sred[2 * (256 + 16)];
+    const int B = S::batch(Brt);
+    const int64_t k = blockIdx.x;
+    const int tid = threadIdx.x;
+    constexpr int kMaxRows = 4;     // B <= 1024
+    float adv[kMaxRows];
+    double m1[1] = {0.0};
+#pragma unroll
+    for (int j = 0; j < kMaxRows; ++j) {
+        const int r = tid + 256 * j;
+        adv[j] = 0.0f;
+        if (r < B) {
+            const int src = sample_row(idx[k * B + r], T, N);
+            const int64_t o = k * B + r;
+            for (int d = 0; d < D; ++d) const_cast<float *>(ff.xg)[o * D + d] = obs[(int64_t)src * D + d];
+            const_cast<int32_t *>(ff.fa)[o] = (int32_t)actions[src];
+            const_cast<float *>(ff.folp)[o] = logprobs[src];
+            const_cast<float *>(ff.fov)[o] = values[src];
+            const_cast<float *>(ff.fret)[o] = returns[src];
+            adv[j] = advantages[src];
+            m1[0] += (double)adv[j];
+        }
+    }
+    if (!normalize) {
+#pragma unroll
+        for (int j = 0; j < kMaxRows; ++j)
+            if (tid + 256 * j < B) const_cast<float *>(ff.fadv)[k * B + tid + 256 * j] = adv[j];
+        if (tid == 0) {
+            metrics[k * GS_NUM_METRICS + GS_M_ADV_NORM_MEAN] = 0.0f;
+            metrics[k * GS_NUM_METRICS + GS_M_ADV_NORM_STD] = 0.0f;
+        }
+        return;
+    }
+    block_reduce<1>(m1, sred);
+    const double mean = m1[0] / (double)B;
+    double q[1] = {0.0};
+#pragma unroll
+    for (int j = 0; j < kMaxRows; ++j)
+        if (tid + 256 * j < B) {
+            const double dv = (double)adv[j] - mean;
+            q[0] += dv * dv;
+        }
+    block_reduce<1>(q, sred);
+    const float meanf = (float)mean;
+    const float stdf = (float)sqrt(q[0] / (double)(B - 1));
+    double st[2] = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < kMaxRows; ++j)
+        if (tid + 256 * j < B) {
+            const float a = (adv[j] - meanf) / (stdf + 1e-8f);
+            const_cast<float *>(ff.fadv)[k * B + tid + 256 * j] = a;
+            st[0] += (double)a;
+            st[1] += (double)a * (double)a;
+        }
+    block_reduce<2>(st, sred);
+    if (tid == 0) {
+        const double Bd = (double)B;
+        metrics[k * GS_NUM_METRICS + GS_M_ADV_NORM_MEAN] = (float)(st[0] / Bd);
+        metrics[k * GS_NUM_METRICS + GS_M_ADV_NORM_STD] =
+            (float)sqrt(fmax(0.0, (st[1] - st[0] * st[0] / Bd) / (Bd - 1.0)));
+    }
+}
+
+// thread per minibatch: the row-block sums (fixed order) -> the metrics record
+__global__ __launch_bounds__(256) void k_metrics_all(const double *__restrict__ mpart, int nrb, int64_t n, int B,
+                                                     LossArgs la, float *__restrict__ metrics,
+                                                     const int32_t *__restrict__ stop)
+{
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    double t[kNumSums];
+#pragma unroll
+    for (int q = 0; q < kNumSums; ++q) t[q] = 0.0;
+    for (int rb = 0; rb < nrb; ++rb)
+#pragma unroll
+        for (int q = 0; q < kNumSums; ++q) t[q] += mpart[(k * nrb + rb) * kNumSums + q];
+    write_metrics(t, (double)B, la, metrics + k * GS_NUM_METRICS, false);
+}
+
+// Fused path's loss: one 64-thread workgroup per 16-row block; rows are independent once the
+// advantages are normalised per minibatch ahead of time (k_gather_all), so there is no
+// block-wide reduction on the critical path: the 14 metric sums of the block go to
+// FusedFwd::mpart and k_metrics_all turns them into records after the update.
+template <class S>
+__global__ __launch_bounds__(64) void k_loss_rows(const float *__restrict__ P, Layout Lrt,
+                                                  const float *__restrict__ zpart, int Brt, FusedFwd ff, LossArgs la,
+                                                  const int32_t *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    __shared__ double dred[kTile * kNumSums];
+    constexpr int AMAX = S::AMAX, AEX = S::AEX;
+    const Layout L = S::lay(Lrt);
+    const int B = S::batch(Brt);
+    const int A1 = L.A + 1;
+    const int tid = threadIdx.x;
+    const int rb = blockIdx.x;
+    const int64_t k = ff.k_local + (ff.step_base ? *ff.step_base : 0);
+    const int r = rb * kTile + tid;
+    if (tid < kTile) {
+        double acc[kNumSums];
+#pragma unroll
+        for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
+        if (r < B) {
+            const int64_t o = k * B + r;
+            const int act = ff.fa[o];
+            const float olp = ff.folp[o], ov = ff.fov[o], adv = ff.fadv[o], ret = ff.fret[o];
+            float z[AMAX + 1];
+            gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
+            loss_row<AMAX>(z, L.A, act, olp, ov, adv, ret, la, 1.0f / (float)B, ff.dz + (int64_t)r * A1, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < kNumSums; ++q) dred[tid * kNumSums + q] = acc[q];
+    }
+    __syncthreads();
+    if (tid < kNumSums) {
+        double t = 0.0;
+        for (int i = 0; i < kTile; ++i) t += dred[i * kNumSums + tid];
+        ff.mpart[(k * gridDim.x + rb) * kNumSums + tid] = t;
+    }
+}
+
+bool has_fused(const Layout &L, int64_t B)
+{
+    bool ok = false;
+    with_shape(L, B, [&](auto sh) {
+        using Sh = decltype(sh);
+        ok = Sh::AEX > 0 && Sh::batch(0) > 0 && B % kTile == 0 && B <= 1024;
+        return GS_OK;
+    });
+    return ok;
+}
+
+int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
+                     const Workspace &ws, const int32_t *stop, hipStream_t s)
+{
+    const dim3 grid((unsigned)((L.H2 + kTile - 1) / kTile), (unsigned)((B + kTile - 1) / kTile));
+    return with_shape(L, B, [&](auto sh) {
+        using Sh = decltype(sh);
+        const float *no_obs = nullptr;
+        const int32_t *no_idx = nullptr;
+        float *no_copy = nullptr;
+        hipLaunchKernelGGL((k_fwd_hidden<Sh, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L, no_obs, no_idx,
+                           0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la);
+        GS_LAUNCH_CHECK("k_fwd_hidden<fused>");
+        return GS_OK;
+    });
+}
+
+int launch_loss_rows(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
+                     const Workspace &ws, const int32_t *stop, hipStream_t s)
+{
+    return with_shape(L, B, [&](auto sh) {
+        hipLaunchKernelGGL(k_loss_rows<decltype(sh)>, dim3((unsigned)(B / kTile)), dim3(64), 0, s, params, L,
+                           ws.zpart, (int)B, ff, la, stop);
+        GS_LAUNCH_CHECK("k_loss_rows");
+        return GS_OK;
+    });
+}
+
+int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx, const float *obs,
+                      const int64_t *actions, const float *logprobs, const float *values, const float *advantages,
+                      const float *returns, int64_t T, int64_t N, int normalize, const FusedFwd &ff, float *metrics,
+                      hipStream_t s)
+{
+    return with_shape(L, B, [&](auto sh) {
+        hipLaunchKernelGGL(k_gather_all<decltype(sh)>, dim3((unsigned)n), dim3(256), 0, s, idx, (int)B, obs, actions,
+                           logprobs, values, advantages, returns, (int)T, (int)N, L.D, normalize, ff, metrics);
+        GS_LAUNCH_CHECK("k_gather_all");
+        return GS_OK;
+    });
+}
+
+int launch_metrics_all(const Layout &L, int64_t B, int64_t n, const FusedFwd &ff, const LossArgs &la, float *metrics,
+                       hipStream_t s)
+{
+    (void)L;
+    hipLaunchKernelGGL(k_metrics_all, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ff.mpart,
+                       (int)(B / kTile), n, (int)B, la, metrics, nullptr);
+    GS_LAUNCH_CHECK("k_metrics_all");
+    return GS_OK;
 }
 
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s)

@@ -135,6 +135,50 @@ extern "C" size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch)
 
 namespace {
 
+constexpr int64_t kChunk = 512;    // minibatch steps per captured graph
+
+// The fused update path's per-update arrays, after the step workspace.
+struct FusedWs {
+    float *xg, *folp, *fov, *fadv, *fret;
+    int32_t *fa;
+    double *mpart;
+    size_t bytes;       // whole update workspace (step + fused)
+};
+
+FusedWs carve_fused(void *base, const Layout &L, int64_t B, int64_t n)
+{
+    const size_t step = carve_workspace(nullptr, L, B).bytes;
+    char *p = (char *)base;
+    size_t off = step;
+    auto take = [&](size_t bytes) {
+        void *q = p ? (void *)(p + off) : nullptr;
+        off += align256(bytes);
+        return q;
+    };
+    FusedWs f{};
+    f.xg = (float *)take(sizeof(float) * (size_t)(n * B * L.D));
+    f.fa = (int32_t *)take(sizeof(int32_t) * (size_t)(n * B));
+    f.folp = (float *)take(sizeof(float) * (size_t)(n * B));
+    f.fov = (float *)take(sizeof(float) * (size_t)(n * B));
+    f.fadv = (float *)take(sizeof(float) * (size_t)(n * B));
+    f.fret = (float *)take(sizeof(float) * (size_t)(n * B));
+    f.mpart = (double *)take(sizeof(double) * (size_t)(n * (B / kTile) * 14));
+    f.bytes = off;
+    return f;
+}
+
+}  // namespace
+
+extern "C" size_t gs_ppo_update_workspace_bytes(gs_mlp_dims dims, int64_t batch, int64_t n_minibatches)
+{
+    if (check_dims(dims) || batch < 1 || n_minibatches < 0) return 0;
+    const Layout L = layout_of(dims);
+    if (!has_fused(L, batch)) return carve_workspace(nullptr, L, batch).bytes;
+    return carve_fused(nullptr, L, batch, n_minibatches).bytes;
+}
+
+namespace {
+
 struct StepArgs {
     LossArgs la;
     AdamArgs aa;
@@ -180,6 +224,34 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
     if (rc) return rc;
     if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
     // multi-GPU: finish the flat gradient, all-reduce (sum) over ranks, norm of the mean
+    rc = launch_reduce_part1(ws.part1, L, sa.aa.nrb, G, stop, s);
+    if (rc) return rc;
+    int world = 1;
+    rc = comm_allreduce_sum(comm, G, L.P, s, &world);
+    if (rc) return rc;
+    constexpr int kNormBlocks = 64;
+    rc = launch_sumsq_flat(G, L.P, ws.sumsq, kNormBlocks, s);
+    if (rc) return rc;
+    AdamArgs aa = sa.aa;
+    aa.n_slots = kNormBlocks;
+    aa.nrb = 0;
+    aa.grad_scale = 1.0f / (float)world;
+    return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
+}
+
+// One minibatch step of the fused chain: k_fwd_hidden<fused> (pre-gathered x), k_loss_rows
+// (per-row loss, no block reduction), k_bwd, then the same clip/Adam tail as enqueue_step.
+int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, const StepArgs &sa, int64_t B,
+                       const FusedFwd &ff, float *metrics, int32_t *stop, const Workspace &ws, gs_comm *comm,
+                       hipStream_t s)
+{
+    int rc = launch_fwd_fused(P, L, B, ff, sa.la, ws, stop, s);
+    if (rc) return rc;
+    rc = launch_loss_rows(P, L, B, ff, sa.la, ws, stop, s);
+    if (rc) return rc;
+    rc = launch_bwd(P, L, B, ws, G, stop, s);
+    if (rc) return rc;
+    if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
     rc = launch_reduce_part1(ws.part1, L, sa.aa.nrb, G, stop, s);
     if (rc) return rc;
     int world = 1;
@@ -312,7 +384,7 @@ std::unordered_map<GraphKey, GraphEntry, GraphKeyHash> g_graphs;
 extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
                              gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
                              int64_t n_minibatches, int64_t adam_step0, float *metrics, int32_t *stop_flag,
-                             void *workspace, gs_comm *comm, int use_graph, void *stream)
+                             void *workspace, size_t workspace_bytes, gs_comm *comm, int use_graph, void *stream)
 {
     int rc = validate_update(dims, ro, batch, workspace);
     if (rc) return rc;
@@ -322,6 +394,34 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
     hipStream_t s = (hipStream_t)stream;
+    // fused chain when this shape has a compile-time instantiation, no KL early stop is
+    // configured (its per-minibatch decision needs the full loss before the backward) and the
+    // caller's workspace holds the per-update arrays
+    const bool fused = has_fused(L, batch) && !(hp.target_kl > 0.0f) &&
+                       workspace_bytes >= carve_fused(nullptr, L, batch, n_minibatches).bytes;
+    FusedWs fw{};
+    FusedFwd ff0{};
+    if (fused) {
+        fw = carve_fused(workspace, L, batch, n_minibatches);
+        ff0.xg = fw.xg, ff0.fa = fw.fa, ff0.folp = fw.folp, ff0.fov = fw.fov, ff0.fadv = fw.fadv, ff0.fret = fw.fret;
+        ff0.mpart = fw.mpart;
+        ff0.dz = ws.dz;
+        rc = launch_gather_all(L, batch, n_minibatches, idx, ro.obs, ro.actions, ro.logprobs, ro.values,
+                               ro.advantages, ro.returns, ro.T, ro.N, hp.normalize_adv, ff0, metrics, s);
+        if (rc) return rc;
+    }
+    auto step_ff = [&](int64_t k_local, int64_t slot, const int64_t *base) {
+        FusedFwd f = ff0;
+        f.k_local = (int)k_local;
+        f.step_base = base;
+        (void)slot;
+        return f;
+    };
+    auto finish = [&]() -> int {
+        if (!fused) return GS_OK;
+        StepArgs sa = make_step_args(hp, L, batch, 1);
+        return launch_metrics_all(L, batch, n_minibatches, ff0, sa.la, metrics, s);
+    };
     // Adam's bias corrections (computed in double on the host, exactly as
     // torch.optim.Adam's single-tensor path does) change every step; eager launches pass
     // them as kernel arguments, the graph reads them from a per-step device table that
@@ -329,17 +429,18 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     if (!use_graph) {
         for (int64_t k = 0; k < n_minibatches; ++k) {
             const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
-            rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
-                              metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
+            rc = fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
+                                            metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
+                       : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                                      metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
             if (rc) return rc;
         }
-        return GS_OK;
+        return finish();
     }
     // One graph holds a chunk of kChunk minibatch steps; it is replayed n / kChunk times
     // with the chunk's first minibatch index in a device scalar (step_base) that the
     // kernels add to their index-stream, metrics and Adam-schedule offsets.  The tail
     // (n % kChunk steps) runs eagerly.  Graph size stays bounded for C3's 327 680 steps.
-    constexpr int64_t kChunk = 512;
     const int64_t chunk = n_minibatches < kChunk ? n_minibatches : kChunk;
     const int64_t n_full = n_minibatches / chunk;
     GraphKey key{};
@@ -350,7 +451,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     key.n[1] = n_minibatches;
     key.n[2] = ((int64_t)dims.obs_dim << 48) ^ ((int64_t)dims.hidden1 << 32) ^ ((int64_t)dims.hidden2 << 16) ^ dims.n_actions;
     key.n[3] = (int64_t)(intptr_t)workspace;
-    key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1);
+    key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1) ^ (fused ? 1 : 0);
     key.n[5] = ro.T * 1000003 + ro.N;
     // host-side hyper-parameters are baked into the capture: include them in the key
     uint32_t hbits[12];
@@ -381,8 +482,17 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
             sa.aa.sched_idx = (int)k;
             sa.aa.step_base = ent.base;
             sa.la.step_base = ent.base;
-            rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
-                              metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
+            if (fused) {
+                LossArgs la_f = sa.la;
+                la_f.step_base = nullptr;      // the fused fwd takes its base from FusedFwd
+                StepArgs saf = sa;
+                saf.la = la_f;
+                rc = enqueue_step_fused(params, grads, adam_m, adam_v, L, saf, batch, step_ff(k, k, ent.base),
+                                        metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
+            } else {
+                rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                                  metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
+            }
             if (rc) {
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(cs, &dummy);
@@ -415,9 +525,11 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     }
     for (int64_t k = n_full * chunk; k < n_minibatches; ++k) {
         const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
-        rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
-                          metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
+        rc = fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
+                                        metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
+                   : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                                  metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
         if (rc) return rc;
     }
-    return GS_OK;
+    return finish();
 }

@@ -130,8 +130,8 @@ class DevicePPOAgent:
         self.n_minibatches = self.data_len // self.batch_size * c.n_epochs
         if self.is_pixel:
             ws = int(lib.gs_cnn_workspace_bytes(self.policy_model.dims, self.batch_size))
-        else:
-            ws = int(lib.gs_ppo_workspace_bytes(self.policy_model.dims, self.batch_size))
+        else:   # the whole update's workspace (fused chain: per-update gathered minibatch fields)
+            ws = int(lib.gs_ppo_update_workspace_bytes(self.policy_model.dims, self.batch_size, self.n_minibatches))
         self.workspace = torch.zeros(ws, dtype=torch.uint8, device=self.device)
         self.stop_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.metrics_buf = torch.zeros(self.n_minibatches, GS_NUM_METRICS, **z)
@@ -226,7 +226,7 @@ class DevicePPOAgent:
             check(lib.gs_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
                                     ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(), ptr(idx),
                                     self.batch_size, self.n_minibatches, self.adam_step, ptr(self.metrics_buf),
-                                    ptr(self.stop_flag), ptr(self.workspace), self.comm,
+                                    ptr(self.stop_flag), ptr(self.workspace), self.workspace.numel(), self.comm,
                                     1 if self.use_graph else 0, stream_handle()), "gs_ppo_update")
         if ev is not None:
             ev[-1][2].record()

@@ -180,12 +180,19 @@ int gs_ppo_stage(int stage, float *params_dev, float *grads_dev, float *adam_m_d
 /* The whole update phase of one rollout: n_minibatches consecutive steps over
  * idx_dev (n_minibatches * batch indices), metrics_dev gets n_minibatches records.
  * adam_step0 is the optimizer step count BEFORE the first of these steps.
- * use_graph != 0 replays the per-pass step sequence from a captured hipGraph. */
+ * use_graph != 0 replays chunks of 512 steps from a captured hipGraph. */
 int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
                   gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout, const int32_t *idx_dev,
                   int64_t batch, int64_t n_minibatches, int64_t adam_step0, float *metrics_dev,
-                  int32_t *stop_flag_dev, void *workspace_dev, struct gs_comm *comm, int use_graph,
-                  void *stream);
+                  int32_t *stop_flag_dev, void *workspace_dev, size_t workspace_bytes, struct gs_comm *comm,
+                  int use_graph, void *stream);
+
+/* Workspace for gs_ppo_update over n_minibatches steps.  When the shape has a compiled
+ * fused chain (the BASELINE configs' MLP shapes) this includes the per-update gathered
+ * minibatch fields and normalised advantages, so the per-step chain reads x in one load and
+ * the loss runs row-parallel with metrics reduced once after the update; a smaller workspace
+ * (>= gs_ppo_workspace_bytes) selects the index-chasing chain with bit-identical parameters. */
+size_t gs_ppo_update_workspace_bytes(gs_mlp_dims dims, int64_t batch, int64_t n_minibatches);
 
 /* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)
  * Replaces CNNActorCritic (utils/models.py:347-455; conv 8x8s4 -> 4x4s2 -> 3x3s1 with 32/64/64

@@ -205,8 +205,8 @@ def test_trajectory_replay_vs_reference(golden, cuda):
         check(lib.gs_ppo_update(agent.policy_model.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
                                 agent.adam_v.data_ptr(), agent.policy_model.dims, agent.hparams(), coll.buffer.view(),
                                 idx.data_ptr(), B, agent.n_minibatches, agent.adam_step, agent.metrics_buf.data_ptr(),
-                                agent.stop_flag.data_ptr(), agent.workspace.data_ptr(), None, 0,
-                                torch.cuda.current_stream().cuda_stream))
+                                agent.stop_flag.data_ptr(), agent.workspace.data_ptr(), agent.workspace.numel(), None,
+                                0, torch.cuda.current_stream().cuda_stream))
         agent.adam_step += agent.n_minibatches
         losses.append(agent.minibatch_losses())
     losses = np.concatenate(losses)
@@ -277,6 +277,41 @@ def test_minibatch_step_vs_numpy_oracle(cuda, env, variant, n_envs):
     np.testing.assert_allclose(rec[0], loss, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(agent.grads.cpu().numpy(), gc, atol=1e-6 * max(1, np.abs(gc).max()), rtol=0)
     np.testing.assert_allclose(agent.policy_model.params.cpu().numpy(), p1, atol=5e-6, rtol=0)
+
+
+@pytest.mark.parametrize("env,variant,n_envs", CASES)
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph):
+    """gs_ppo_update's fused chain (gathered fields, head combine + loss rows inside the
+    forward) against the 4-launch chain on the same rollout: bit-identical parameters and
+    minibatch losses within 1e-6 relative (metric sums are added in another order)."""
+    from gsamd._lib import check, lib
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    out = []
+    for fused in (True, False):
+        torch.manual_seed(42)
+        cfg = load_config(env, variant, overrides=dict(n_envs=n_envs // 8 if env == "CartPole-v1" else n_envs,
+                                                       n_epochs=2))
+        agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
+        coll = agent.get_rollout_collector("train")
+        coll.collect()
+        idx = agent.prefetcher.upload(0)
+        small = int(lib.gs_ppo_workspace_bytes(agent.policy_model.dims, agent.batch_size))
+        assert agent.workspace.numel() > small      # the BASELINE shapes have a fused chain
+        check(lib.gs_ppo_update(agent.policy_model.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                                agent.adam_v.data_ptr(), agent.policy_model.dims, agent.hparams(), coll.buffer.view(),
+                                idx.data_ptr(), agent.batch_size, agent.n_minibatches, 0, agent.metrics_buf.data_ptr(),
+                                agent.stop_flag.data_ptr(), agent.workspace.data_ptr(),
+                                agent.workspace.numel() if fused else small, None, 1 if use_graph else 0,
+                                torch.cuda.current_stream().cuda_stream), "gs_ppo_update")
+        torch.cuda.synchronize()
+        rec = agent.metrics_buf.cpu().numpy()
+        out.append((agent.policy_model.params.cpu().numpy(), rec))
+        del agent
+    (p0, m0), (p1, m1) = out
+    assert np.array_equal(p0.view(np.uint32), p1.view(np.uint32))
+    np.testing.assert_allclose(m0, m1, rtol=1e-6, atol=1e-7)
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
