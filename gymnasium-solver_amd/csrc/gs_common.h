@@ -125,7 +125,7 @@ struct Workspace {
     int n_slots;
     size_t bytes;
 };
-constexpr int kRowsB = 64;       // rows per dh1 workgroup in k_bwd (one 16-row slab per wave)
+constexpr int kRowsB = 32;       // rows per dh1 workgroup in k_bwd (2 row tiles x 2 K halves over 4 waves)
 
 // Minibatch field gather done by the forward kernel (utils/rollout_collector.py:657-682).
 struct RowGather {

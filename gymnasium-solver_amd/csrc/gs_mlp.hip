@@ -694,7 +694,7 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     const int64_t H2p = (L.H2 + 63) / 64 * 64;
     const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 2 * kTile * (Bp64 + 4) + 1024;
     const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
-                          kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17;
+                          kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024;
     const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + A1 * 256;
     int64_t m = roleA;
     if (roleB > m) m = roleB;
@@ -719,7 +719,10 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
     const BwdShape sh = BwdShape::make(L, B);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
-    int bid = blockIdx.x;
+    // dispatch order: role B (the longest) first, then A, then C; bid keeps the A, B, C numbering
+    int bid = (int)blockIdx.x;
+    if (bid < sh.nB) bid += sh.nA;
+    else if (bid < sh.nB + sh.nA) bid -= sh.nB;
 
     if (bid < sh.nA) {
         // ---------------- role A: dW2[n0:n0+16, k0:k0+16] = sum_b dh2[b,n] h1[b,k]
@@ -848,7 +851,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         float *dzs = whs + round4(A1 * H2);         // [64][A1]
         float *h1m = dzs + round4(kRowsB * A1);     // [64][16]
         float *xs = h1m + kRowsB * 16;              // [64][D]
-        float *tile = xs + round4(kRowsB * D);      // [64][17]
+        float *tile = xs + round4(kRowsB * D);      // [32][17]
+        float *kred = tile + kRowsB * 17;           // [4][256] K-half partial tiles
         const int n4 = H2p >> 2;
 #pragma unroll 4
         for (int u = tid; u < kRowsB * n4; u += 256) {
@@ -906,12 +910,15 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         __syncthreads();
         GS_STAMP(1)
         {
+            // 32 rows = 2 row tiles; waves (0,1) / (2,3) split K = H2 of tile 0 / 1 in halves
             const int nch = H2p / kTile;
-            const float *arow = dh2s + (wave * 16 + li) * ld;
+            const int rt = wave >> 1, half = wave & 1;
+            const int chb = half ? nch / 2 : 0, che = half ? nch : nch / 2;
+            const float *arow = dh2s + (rt * 16 + li) * ld;
             const float *brow = W2T + li * ld;
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-            for (int ch = 0; ch < nch; ++ch) {
+            for (int ch = chb; ch < che; ++ch) {
                 const int n = ch * kTile + 4 * lq;
                 const float4 a = *reinterpret_cast<const float4 *>(arow + n);
                 const float4 w = *reinterpret_cast<const float4 *>(brow + n);
@@ -922,19 +929,23 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
             const f32x4 acc = acc0 + acc1;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = wave * 16 + lq * 4 + r;
-                const float g = h1m[row * 16 + li] > 0.0f ? acc[r] : 0.0f;   // relu'(h1)
-                tile[row * 17 + li] = g;
-            }
+            for (int r = 0; r < 4; ++r) kred[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
+        }
+        __syncthreads();
+        for (int u = tid; u < kRowsB * kTile; u += 256) {
+            const int row = u >> 4, col = u & 15;
+            const int t = row >> 4, rr = row & 15;
+            const float g = kred[(2 * t) * 256 + rr * kTile + col] + kred[(2 * t + 1) * 256 + rr * kTile + col];
+            tile[row * 17 + col] = h1m[row * 16 + col] > 0.0f ? g : 0.0f;   // relu'(h1)
         }
         __syncthreads();
         GS_STAMP(2)
-        // dW1 / db1 partials over this slab's 64 rows: 4 row groups of 16, then combine
+        // dW1 / db1 partials over this slab's rows: row groups of 16, then combine in order
         {
-            float *pr = dh2s;                       // reuse: [4][16*(D+1)]
+            constexpr int ng = kRowsB / 16;
+            float *pr = dh2s;                       // reuse: [ng][16*(D+1)]
             const int nout = kTile * (D + 1);
-            for (int u = tid; u < 4 * nout; u += 256) {
+            for (int u = tid; u < ng * nout; u += 256) {
                 const int g = u / nout, o = u - g * nout;
                 const int col = o / (D + 1), d = o - col * (D + 1);
                 float s = 0.0f;
@@ -948,9 +959,10 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             __syncthreads();
             for (int o = tid; o < nout; o += 256) {
                 const int col = o / (D + 1), d = o - col * (D + 1);
-                if (k0 + col < H1)
-                    part1[((int64_t)rb * H1 + k0 + col) * (D + 1) + d] =
-                        ((pr[o] + pr[nout + o]) + pr[2 * nout + o]) + pr[3 * nout + o];
+                float t = 0.0f;
+#pragma unroll
+                for (int g = 0; g < ng; ++g) t += pr[g * nout + o];
+                if (k0 + col < H1) part1[((int64_t)rb * H1 + k0 + col) * (D + 1) + d] = t;
             }
         }
         GS_STAMP_END(3)
