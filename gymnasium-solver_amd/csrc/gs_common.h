@@ -182,8 +182,6 @@ inline int n_sumsq_slots(const Layout &L) { return n_col_blocks(L.H2) * n_col_bl
 // kernels' launch helpers (gs_mlp.hip)
 int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
                      const Workspace &ws, const int32_t *stop, hipStream_t s);
-int launch_loss_rows(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
-                     const Workspace &ws, const int32_t *stop, hipStream_t s);
 int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx, const float *obs,
                       const int64_t *actions, const float *logprobs, const float *values, const float *advantages,
                       const float *returns, int64_t T, int64_t N, int normalize, const FusedFwd &ff, float *metrics,
@@ -202,7 +200,7 @@ int launch_loss(const float *P, const Layout &L, int64_t B, const Workspace &ws,
 size_t bwd_lds_bytes(const Layout &L, int64_t B);
 int prepare_kernels(const Layout &L, int64_t B);
 int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
-               hipStream_t s);
+               hipStream_t s, const FusedFwd *ff = nullptr, const LossArgs *la = nullptr);
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
                      const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s);
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);

@@ -702,12 +702,54 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     return (size_t)m * sizeof(float);
 }
 
+// Fused path: the loss rows a workgroup needs (dLoss/dlogits | dLoss/dvalue) are computed
+// from the forward's partial heads straight into LDS, so the chain has no separate loss
+// launch; mp != nullptr also stores the 14 metric sums of each 16-row block of [r0, r0+n).
+// dscr: >= n * 14 doubles of LDS when mp is set.
 template <class S>
+__device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const Layout &L,
+                                              const float *__restrict__ zpart, const FusedFwd &ff,
+                                              const LossArgs &la, int B, int64_t k, int r0, int n, float *dzs,
+                                              double *mp, double *dscr)
+{
+    constexpr int AMAX = S::AMAX, AEX = S::AEX;
+    const int A1 = L.A + 1;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int r = r0 + i;
+        double acc[kNumSums];
+#pragma unroll
+        for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
+        if (r < B) {
+            const int64_t o = k * B + r;
+            float z[AMAX + 1];
+            gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
+            loss_row<AMAX>(z, L.A, ff.fa[o], ff.folp[o], ff.fov[o], ff.fadv[o], ff.fret[o], la, 1.0f / (float)B,
+                           dzs + i * A1, acc);
+        } else {
+            for (int a = 0; a < A1; ++a) dzs[i * A1 + a] = 0.0f;
+        }
+        if (mp)
+#pragma unroll
+            for (int q = 0; q < kNumSums; ++q) dscr[i * kNumSums + q] = acc[q];
+    }
+    if (!mp) return;
+    __syncthreads();
+    const int ng = n / kTile;
+    if ((int)threadIdx.x < ng * kNumSums) {
+        const int g = threadIdx.x / kNumSums, q = threadIdx.x - g * kNumSums;
+        double t = 0.0;
+        for (int i = 0; i < kTile; ++i) t += dscr[(g * kTile + i) * kNumSums + q];
+        mp[(k * (B / kTile) + r0 / kTile + g) * kNumSums + q] = t;
+    }
+}
+
+template <class S, bool FUSED>
 __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout Lrt, int Brt,
                                              const float *__restrict__ x, const float *__restrict__ h1,
                                              const float *__restrict__ h2, const float *__restrict__ dz,
                                              float *__restrict__ G, float *__restrict__ part1,
-                                             float *__restrict__ sumsq, const int32_t *__restrict__ stop)
+                                             float *__restrict__ sumsq, const int32_t *__restrict__ stop,
+                                             const float *__restrict__ zpart, FusedFwd ff, LossArgs la)
 {
     GS_STAMP_BEGIN(2)
     if (stop && *stop) return;
@@ -735,7 +777,11 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         float *dh2T = whs + round4(A1 * 16);         // [16][Bp+4]  (n, b): h2 first, then dh2
         float *h1T = dh2T + kTile * ld;              // [16][Bp+4]  (k, b)
         float *red = h1T + kTile * ld;               // [4][256]
-        copy_to_lds(dzs, dz, B * A1);
+        if constexpr (FUSED)
+            loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
+                             nullptr, nullptr);
+        else
+            copy_to_lds(dzs, dz, B * A1);
         if (tid < A1 * kTile) {
             const int a = tid >> 4, j = tid & 15;
             whs[tid] = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
@@ -875,7 +921,12 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             const int a = u / H2, n = u - a * H2;
             whs[u] = P[L.head_row(a) + n];
         }
-        for (int u = tid; u < kRowsB * A1; u += 256) dzs[u] = b0 * A1 + u < B * A1 ? dz[(int64_t)b0 * A1 + u] : 0.0f;
+        if constexpr (FUSED)      // the kb == 0 slab also stores its rows' metric sums
+            loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), b0, kRowsB,
+                             dzs, kb == 0 ? ff.mpart : nullptr, reinterpret_cast<double *>(kred));
+        else
+            for (int u = tid; u < kRowsB * A1; u += 256)
+                dzs[u] = b0 * A1 + u < B * A1 ? dz[(int64_t)b0 * A1 + u] : 0.0f;
         for (int u = tid; u < kRowsB * 16; u += 256) {
             const int i = u >> 4, j = u & 15;
             h1m[u] = (b0 + i < B && k0 + j < H1) ? h1[(int64_t)(b0 + i) * H1 + k0 + j] : 0.0f;
@@ -987,7 +1038,11 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             hs[b * 17 + 4 * c4 + 2] = hv.z;
             hs[b * 17 + 4 * c4 + 3] = hv.w;
         }
-        for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
+        if constexpr (FUSED)
+            loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, Bp, dzs,
+                             nullptr, nullptr);
+        else
+            for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
         __syncthreads();
         GS_STAMP(0)
         // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
@@ -1209,9 +1264,15 @@ static int set_lds_limit(const void *fn, size_t bytes)
 int prepare_kernels(const Layout &L, int64_t B)
 {
     int rc = with_shape(L, B, [&](auto sh) {
-        return set_lds_limit((const void *)k_bwd<decltype(sh)>, bwd_lds_bytes(L, B));
+        return set_lds_limit((const void *)k_bwd<decltype(sh), false>, bwd_lds_bytes(L, B));
     });
     if (rc) return rc;
+    if (has_fused(L, B)) {
+        rc = with_shape(L, B, [&](auto sh) {
+            return set_lds_limit((const void *)k_bwd<decltype(sh), true>, bwd_lds_bytes(L, B));
+        });
+        if (rc) return rc;
+    }
     rc = with_shape(L, 0, [&](auto sh) {
         return set_lds_limit((const void *)k_fwd_hidden<decltype(sh), false>, fwd_lds_bytes(L));
     });
@@ -1246,17 +1307,24 @@ int launch_loss(const float *P, const Layout &L, int64_t B, const Workspace &ws,
 }
 
 int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
-               hipStream_t s)
+               hipStream_t s, const FusedFwd *ff, const LossArgs *la)
 {
     const BwdShape sh0 = BwdShape::make(L, (int)B);
     const unsigned nblk = (unsigned)(sh0.nA + sh0.nB + sh0.nC);
     const size_t lds = bwd_lds_bytes(L, B);
     return with_shape(L, B, [&](auto sh) {
         using Sh = decltype(sh);
-        int rc = set_lds_limit((const void *)k_bwd<Sh>, lds);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_bwd<Sh>, dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2, ws.dz, G,
-                           ws.part1, ws.sumsq, stop);
+        if (ff) {
+            int rc = set_lds_limit((const void *)k_bwd<Sh, true>, lds);
+            if (rc) return rc;
+            hipLaunchKernelGGL((k_bwd<Sh, true>), dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2,
+                               ws.dz, G, ws.part1, ws.sumsq, stop, ws.zpart, *ff, *la);
+        } else {
+            int rc = set_lds_limit((const void *)k_bwd<Sh, false>, lds);
+            if (rc) return rc;
+            hipLaunchKernelGGL((k_bwd<Sh, false>), dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2,
+                               ws.dz, G, ws.part1, ws.sumsq, stop, (const float *)nullptr, FusedFwd{}, LossArgs{});
+        }
         GS_LAUNCH_CHECK("k_bwd");
         return GS_OK;
     });
@@ -1370,48 +1438,6 @@ __global__ __launch_bounds__(256) void k_metrics_all(const double *__restrict__ 
     write_metrics(t, (double)B, la, metrics + k * GS_NUM_METRICS, false);
 }
 
-// Fused path's loss: one 64-thread workgroup per 16-row block; rows are independent once the
-// advantages are normalised per minibatch ahead of time (k_gather_all), so there is no
-// block-wide reduction on the critical path: the 14 metric sums of the block go to
-// FusedFwd::mpart and k_metrics_all turns them into records after the update.
-template <class S>
-__global__ __launch_bounds__(64) void k_loss_rows(const float *__restrict__ P, Layout Lrt,
-                                                  const float *__restrict__ zpart, int Brt, FusedFwd ff, LossArgs la,
-                                                  const int32_t *__restrict__ stop)
-{
-    if (stop && *stop) return;
-    __shared__ double dred[kTile * kNumSums];
-    constexpr int AMAX = S::AMAX, AEX = S::AEX;
-    const Layout L = S::lay(Lrt);
-    const int B = S::batch(Brt);
-    const int A1 = L.A + 1;
-    const int tid = threadIdx.x;
-    const int rb = blockIdx.x;
-    const int64_t k = ff.k_local + (ff.step_base ? *ff.step_base : 0);
-    const int r = rb * kTile + tid;
-    if (tid < kTile) {
-        double acc[kNumSums];
-#pragma unroll
-        for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
-        if (r < B) {
-            const int64_t o = k * B + r;
-            const int act = ff.fa[o];
-            const float olp = ff.folp[o], ov = ff.fov[o], adv = ff.fadv[o], ret = ff.fret[o];
-            float z[AMAX + 1];
-            gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
-            loss_row<AMAX>(z, L.A, act, olp, ov, adv, ret, la, 1.0f / (float)B, ff.dz + (int64_t)r * A1, acc);
-        }
-#pragma unroll
-        for (int q = 0; q < kNumSums; ++q) dred[tid * kNumSums + q] = acc[q];
-    }
-    __syncthreads();
-    if (tid < kNumSums) {
-        double t = 0.0;
-        for (int i = 0; i < kTile; ++i) t += dred[i * kNumSums + tid];
-        ff.mpart[(k * gridDim.x + rb) * kNumSums + tid] = t;
-    }
-}
-
 bool has_fused(const Layout &L, int64_t B)
 {
     bool ok = false;
@@ -1435,17 +1461,6 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
         hipLaunchKernelGGL((k_fwd_hidden<Sh, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L, no_obs, no_idx,
                            0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la);
         GS_LAUNCH_CHECK("k_fwd_hidden<fused>");
-        return GS_OK;
-    });
-}
-
-int launch_loss_rows(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
-                     const Workspace &ws, const int32_t *stop, hipStream_t s)
-{
-    return with_shape(L, B, [&](auto sh) {
-        hipLaunchKernelGGL(k_loss_rows<decltype(sh)>, dim3((unsigned)(B / kTile)), dim3(64), 0, s, params, L,
-                           ws.zpart, (int)B, ff, la, stop);
-        GS_LAUNCH_CHECK("k_loss_rows");
         return GS_OK;
     });
 }

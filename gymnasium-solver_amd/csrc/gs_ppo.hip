@@ -239,17 +239,16 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
     return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
 }
 
-// One minibatch step of the fused chain: k_fwd_hidden<fused> (pre-gathered x), k_loss_rows
-// (per-row loss, no block reduction), k_bwd, then the same clip/Adam tail as enqueue_step.
+// One minibatch step of the fused chain: k_fwd_hidden<fused> (pre-gathered x), k_bwd<fused>
+// (each workgroup computes the loss rows it needs from the partial heads: no loss launch,
+// no block reduction; metric sums per 16 rows), then the same clip/Adam tail as enqueue_step.
 int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, const StepArgs &sa, int64_t B,
                        const FusedFwd &ff, float *metrics, int32_t *stop, const Workspace &ws, gs_comm *comm,
                        hipStream_t s)
 {
     int rc = launch_fwd_fused(P, L, B, ff, sa.la, ws, stop, s);
     if (rc) return rc;
-    rc = launch_loss_rows(P, L, B, ff, sa.la, ws, stop, s);
-    if (rc) return rc;
-    rc = launch_bwd(P, L, B, ws, G, stop, s);
+    rc = launch_bwd(P, L, B, ws, G, stop, s, &ff, &sa.la);
     if (rc) return rc;
     if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
     rc = launch_reduce_part1(ws.part1, L, sa.aa.nrb, G, stop, s);
