@@ -1123,6 +1123,8 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     // ---- this block's parameters and optimizer state: loads issued first
     const int64_t base = (int64_t)blockIdx.x * 1024;
     float gv[4], mv[4], vv[4], pv[4];
+    // W1|b1 gradients come from the dW1|db1 partials: summed after they are staged in LDS
+    // (below) when staging is on, instead of 4 x nrb dependent global loads here
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int64_t p = base + j * 256 + tid;
@@ -1130,9 +1132,11 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
         float g = 0.0f;
         if (ok) {
             if (aa.nrb > 0 && p < L.oW2) {
-                const int64_t u = part1_index(L, p);
+                if (!aa.stage_lds) {
+                    const int64_t u = part1_index(L, p);
 #pragma unroll 4
-                for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
+                    for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
+                }
             } else {
                 g = G[p];
             }
@@ -1152,6 +1156,18 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
         const int off = round4(aa.n_slots);
         if (npart > 0) copy_to_lds(stage + off, part1, (int)npart);
         __syncthreads();
+        if (aa.nrb > 0 && base < L.oW2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t p = base + j * 256 + tid;
+                if (p < L.oW2) {
+                    const int64_t u = part1_index(L, p);
+                    float g = 0.0f;
+                    for (int rb = 0; rb < aa.nrb; ++rb) g += stage[off + rb * n1 + u];
+                    gv[j] = g;
+                }
+            }
+        }
         for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)stage[s0];
         for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
             float g = 0.0f;
