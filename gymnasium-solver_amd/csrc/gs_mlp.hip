@@ -195,7 +195,25 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     }
     copy_to_lds(W1s, P + L.oW1, H1 * D);
     copy_to_lds(b1s, P + L.ob1, H1);
-    {
+    if (tid < kTile) b2s[tid] = c0 + tid < H2 ? P[L.ob2 + c0 + tid] : 0.0f;
+    if (tid < A1 * kTile) {
+        const int a = tid >> 4, j = tid & 15;
+        whs[tid] = c0 + j < H2 ? P[L.head_row(a) + c0 + j] : 0.0f;
+    }
+    // W2 tile: with compile-time shapes the loads go to registers AFTER the h1 operands, so the
+    // barrier below waits only for those (in-order vmcnt) and h1 is computed while the 16 KB
+    // tile is still in flight; it is written to LDS after h1.
+    constexpr int kW2v = S::H1c > 0 ? kTile * S::H1c / 4 / 256 : 0;
+    float4 w2r[kW2v > 0 ? kW2v : 1];
+    if constexpr (kW2v > 0) {
+        const int k4n = H1 >> 2;
+#pragma unroll
+        for (int j = 0; j < kW2v; ++j) {
+            const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+            w2r[j] = c0 + i < H2 ? *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)(c0 + i) * H1 + 4 * k4)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    } else {
         const int k4n = H1 >> 2;
 #pragma unroll 4
         for (int u = tid; u < kTile * k4n; u += 256) {
@@ -204,11 +222,6 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             if (c0 + i < H2) w = *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)(c0 + i) * H1 + 4 * k4);
             *reinterpret_cast<float4 *>(W2s + i * ldh + 4 * k4) = w;
         }
-    }
-    if (tid < kTile) b2s[tid] = c0 + tid < H2 ? P[L.ob2 + c0 + tid] : 0.0f;
-    if (tid < A1 * kTile) {
-        const int a = tid >> 4, j = tid & 15;
-        whs[tid] = c0 + j < H2 ? P[L.head_row(a) + c0 + j] : 0.0f;
     }
     __syncthreads();
     GS_STAMP(0)
@@ -240,6 +253,14 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 acc += bk;
                 h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
             }
+        }
+    }
+    if constexpr (kW2v > 0) {
+        const int k4n = H1 >> 2;
+#pragma unroll
+        for (int j = 0; j < kW2v; ++j) {
+            const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+            *reinterpret_cast<float4 *>(W2s + i * ldh + 4 * k4) = w2r[j];
         }
     }
     __syncthreads();
