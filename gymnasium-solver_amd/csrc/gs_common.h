@@ -116,6 +116,7 @@ struct Workspace {
     float *x;        // (B, D)     gathered observations
     float *h1;       // (B, H1)    post-ReLU
     float *h2;       // (B, H2)    post-ReLU
+    uint16_t *h2mask;  // (B, H2/16) relu'(h2) bits per 16-column block (what k_bwd reads instead of h2)
     float *zpart;    // (H2/16, B, A+1) partial head outputs
     float *dz;       // (B, A+1)   dLoss/dlogits | dLoss/dvalue
     float *part1;    // (ceil(B/64), H1, D+1) dW1|db1 partials per 64-row block
@@ -191,7 +192,7 @@ int launch_metrics_all(const Layout &L, int64_t B, int64_t n, const FusedFwd &ff
 bool has_fused(const Layout &L, int64_t B);
 int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, const int32_t *idx,
                       int64_t T, int64_t N, int64_t rows, float *x_out, float *h1_out, float *h2_out,
-                      float *zpart, float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s);
+                      float *zpart, float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s, uint16_t *h2mask = nullptr);
 size_t fwd_lds_bytes(const Layout &L);
 int launch_heads_act(const float *P, const Layout &L, const float *zpart, int64_t rows, int mode, uint64_t seed,
                      uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s);

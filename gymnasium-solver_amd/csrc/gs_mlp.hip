@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     const float *__restrict__ P, Layout Lrt, const float *__restrict__ obs, const int32_t *__restrict__ idx, int T,
     int N, int rows, float *__restrict__ x_out, float *__restrict__ h1_out, float *__restrict__ h2_out,
     float *__restrict__ zpart, float *__restrict__ obs_copy, const int32_t *__restrict__ stop, RowGather rg,
-    FusedFwd ff, LossArgs la)
+    FusedFwd ff, LossArgs la, uint16_t *__restrict__ h2mask)
 {
     GS_STAMP_BEGIN(0)
     if (stop && *stop) return;
@@ -299,6 +299,12 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         h2s[row * 17 + col] = h;
     }
     __syncthreads();
+    if (h2mask && tid < kTile && r0 + tid < rows) {   // relu'(h2) bits of this row's 16 columns
+        unsigned m = 0;
+#pragma unroll
+        for (int c = 0; c < kTile; ++c) m |= (h2s[tid * 17 + c] > 0.0f ? 1u : 0u) << c;
+        h2mask[(int64_t)(r0 + tid) * gridDim.x + cb] = (uint16_t)m;
+    }
     // ---- phase 3: partial head outputs over this tile's 16 hidden units
     const int ncbz = gridDim.x;
     for (int u = tid; u < kTile * A1; u += 256) {
@@ -333,7 +339,8 @@ static int with_shape(const Layout &L, int64_t B, F &&f);
 
 int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, const int32_t *idx, int64_t T,
                       int64_t N, int64_t rows, float *x_out, float *h1_out, float *h2_out, float *zpart,
-                      float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s)
+                      float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s,
+                      uint16_t *h2mask)
 {
     const dim3 grid((unsigned)((L.H2 + kTile - 1) / kTile), (unsigned)((rows + kTile - 1) / kTile));
     RowGather g{};
@@ -344,7 +351,7 @@ int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, co
         if (rc) return rc;
         hipLaunchKernelGGL((k_fwd_hidden<Sh, false>), grid, dim3(256), fwd_lds_bytes(L), s, params, L, obs, idx,
                            (int)T, (int)N, (int)rows, x_out, h1_out, h2_out, zpart, obs_copy, stop_flag, g,
-                           FusedFwd{}, LossArgs{});
+                           FusedFwd{}, LossArgs{}, h2_out ? h2mask : (uint16_t *)nullptr);
         GS_LAUNCH_CHECK("k_fwd_hidden");
         return GS_OK;
     });
@@ -713,9 +720,10 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     const int A1 = L.A + 1;
     const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
     const int64_t H2p = (L.H2 + 63) / 64 * 64;
-    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 2 * kTile * (Bp64 + 4) + 1024;
+    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 2 * kTile * (Bp64 + 4) + 1024 + Bp64;
     const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
-                          kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024;
+                          kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024 +
+                          (int64_t)kRowsB * n_col_blocks(L.H2);
     const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + A1 * 256;
     int64_t m = roleA;
     if (roleB > m) m = roleB;
@@ -725,17 +733,19 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
 
 // Fused path: the loss rows a workgroup needs (dLoss/dlogits | dLoss/dvalue) are computed
 // from the forward's partial heads straight into LDS, so the chain has no separate loss
-// launch; mp != nullptr also stores the 14 metric sums of each 16-row block of [r0, r0+n).
-// dscr: >= n * 14 doubles of LDS when mp is set.
+// launch.  Threads [t0, t0 + nthr) take rows [r0, r0 + n); dscr != nullptr also keeps each
+// row's 14 metric sums (n x 14 doubles of LDS) for store_metric_groups after a barrier.
 template <class S>
 __device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const Layout &L,
                                               const float *__restrict__ zpart, const FusedFwd &ff,
                                               const LossArgs &la, int B, int64_t k, int r0, int n, float *dzs,
-                                              double *mp, double *dscr)
+                                              double *dscr, int t0 = 0, int nthr = 256)
 {
     constexpr int AMAX = S::AMAX, AEX = S::AEX;
     const int A1 = L.A + 1;
-    for (int i = threadIdx.x; i < n; i += 256) {
+    const int me = (int)threadIdx.x - t0;
+    if (me < 0 || me >= nthr) return;
+    for (int i = me; i < n; i += nthr) {
         const int r = r0 + i;
         double acc[kNumSums];
 #pragma unroll
@@ -749,12 +759,16 @@ __device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const
         } else {
             for (int a = 0; a < A1; ++a) dzs[i * A1 + a] = 0.0f;
         }
-        if (mp)
+        if (dscr)
 #pragma unroll
             for (int q = 0; q < kNumSums; ++q) dscr[i * kNumSums + q] = acc[q];
     }
-    if (!mp) return;
-    __syncthreads();
+}
+
+// the 14 metric sums of every 16-row group of [r0, r0 + n) (after a barrier)
+__device__ __forceinline__ void store_metric_groups(const double *dscr, int n, int r0, int B, int64_t k,
+                                                    double *__restrict__ mp)
+{
     const int ng = n / kTile;
     if ((int)threadIdx.x < ng * kNumSums) {
         const int g = threadIdx.x / kNumSums, q = threadIdx.x - g * kNumSums;
@@ -770,7 +784,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                                              const float *__restrict__ h2, const float *__restrict__ dz,
                                              float *__restrict__ G, float *__restrict__ part1,
                                              float *__restrict__ sumsq, const int32_t *__restrict__ stop,
-                                             const float *__restrict__ zpart, FusedFwd ff, LossArgs la)
+                                             const float *__restrict__ zpart, FusedFwd ff, LossArgs la,
+                                             const uint16_t *__restrict__ h2mask)
 {
     GS_STAMP_BEGIN(2)
     if (stop && *stop) return;
@@ -800,26 +815,22 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         float *red = h1T + kTile * ld;               // [4][256]
         if constexpr (FUSED)
             loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
-                             nullptr, nullptr);
+                             nullptr);
         else
             copy_to_lds(dzs, dz, B * A1);
         if (tid < A1 * kTile) {
             const int a = tid >> 4, j = tid & 15;
             whs[tid] = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
         }
-        // h2 / h1 column tiles: 16 contiguous floats per row = 4 float4, transposed into LDS
+        // relu'(h2) bits of this n-block (one word per row) and the h1 column tile (16 contiguous
+        // floats per row = 4 float4, transposed into LDS); dh2T is filled by the dh2 pass
+        int *mkA = reinterpret_cast<int *>(red + 1024);   // [Bp]
+        for (int b = tid; b < Bp; b += 256) mkA[b] = b < B ? (int)h2mask[(int64_t)b * sh.ncb + nb] : 0;
 #pragma unroll 4
         for (int u = tid; u < Bp * 4; u += 256) {
             const int b = u >> 2, c4 = u & 3;
-            float4 hv = make_float4(0.f, 0.f, 0.f, 0.f), gv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (b < B) {
-                if (n0 + 4 * c4 < H2) hv = *reinterpret_cast<const float4 *>(h2 + (int64_t)b * H2 + n0 + 4 * c4);
-                if (k0 + 4 * c4 < H1) gv = *reinterpret_cast<const float4 *>(h1 + (int64_t)b * H1 + k0 + 4 * c4);
-            }
-            dh2T[(4 * c4 + 0) * ld + b] = hv.x;
-            dh2T[(4 * c4 + 1) * ld + b] = hv.y;
-            dh2T[(4 * c4 + 2) * ld + b] = hv.z;
-            dh2T[(4 * c4 + 3) * ld + b] = hv.w;
+            float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (b < B && k0 + 4 * c4 < H1) gv = *reinterpret_cast<const float4 *>(h1 + (int64_t)b * H1 + k0 + 4 * c4);
             h1T[(4 * c4 + 0) * ld + b] = gv.x;
             h1T[(4 * c4 + 1) * ld + b] = gv.y;
             h1T[(4 * c4 + 2) * ld + b] = gv.z;
@@ -836,20 +847,20 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             if (A1 <= 5) {
                 // branch-free body so the unrolled iterations' LDS reads issue together
 #pragma unroll 8
-                for (int b = tid >> 4; b < B; b += 16) {
-                    const float h = dh2T[i * ld + b];
+                for (int b = tid >> 4; b < Bp; b += 16) {
+                    const bool on = (mkA[b] >> i) & 1;
                     float s = 0.0f;
 #pragma unroll
                     for (int a = 0; a < 5; ++a) s = a < A1 ? fmaf(dzs[b * A1 + a], w[a], s) : s;
-                    dh2T[i * ld + b] = h > 0.0f ? s : 0.0f;
+                    dh2T[i * ld + b] = on ? s : 0.0f;
                 }
             } else {
-                for (int b = tid >> 4; b < B; b += 16) {
-                    const float h = dh2T[i * ld + b];
+                for (int b = tid >> 4; b < Bp; b += 16) {
+                    const bool on = (mkA[b] >> i) & 1;
                     float s = 0.0f;
 #pragma unroll
                     for (int a = 0; a < kMaxActions + 1; ++a) s = a < A1 ? fmaf(dzs[b * A1 + a], w[a], s) : s;
-                    dh2T[i * ld + b] = h > 0.0f ? s : 0.0f;
+                    dh2T[i * ld + b] = on ? s : 0.0f;
                 }
             }
         }
@@ -920,64 +931,76 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         float *xs = h1m + kRowsB * 16;              // [64][D]
         float *tile = xs + round4(kRowsB * D);      // [32][17]
         float *kred = tile + kRowsB * 17;           // [4][256] K-half partial tiles
-        const int n4 = H2p >> 2;
+        // waves 0-2 stream the slab's operands into LDS while wave 3 computes its loss rows
+        // (fused path): the loss math overlaps the loads instead of following them
+        constexpr int kLd = FUSED ? 192 : 256;
+        int *mkB = reinterpret_cast<int *>(kred + 1024);   // [32][ncb] relu'(h2) bits
+        if (!FUSED || tid < kLd) {
+            for (int u = tid; u < kRowsB * sh.ncb; u += kLd) {
+                const int i = u / sh.ncb, c = u - i * sh.ncb;
+                mkB[u] = b0 + i < B ? (int)h2mask[(int64_t)(b0 + i) * sh.ncb + c] : 0;
+            }
 #pragma unroll 4
-        for (int u = tid; u < kRowsB * n4; u += 256) {
-            const int i = u / n4, c4 = u - i * n4;
-            float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (b0 + i < B && 4 * c4 < H2) hv = *reinterpret_cast<const float4 *>(h2 + (int64_t)(b0 + i) * H2 + 4 * c4);
-            *reinterpret_cast<float4 *>(dh2s + i * ld + 4 * c4) = hv;
+            for (int u = tid; u < H2p * 4; u += kLd) {
+                const int n = u >> 2, c4 = u & 3;
+                float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (n < H2 && k0 + 4 * c4 < H1)
+                    w = *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)n * H1 + k0 + 4 * c4);
+                W2T[(4 * c4 + 0) * ld + n] = w.x;
+                W2T[(4 * c4 + 1) * ld + n] = w.y;
+                W2T[(4 * c4 + 2) * ld + n] = w.z;
+                W2T[(4 * c4 + 3) * ld + n] = w.w;
+            }
+            for (int u = tid; u < A1 * H2; u += kLd) {
+                const int a = u / H2, n = u - a * H2;
+                whs[u] = P[L.head_row(a) + n];
+            }
+            for (int u = tid; u < kRowsB * 16; u += kLd) {
+                const int i = u >> 4, j = u & 15;
+                h1m[u] = (b0 + i < B && k0 + j < H1) ? h1[(int64_t)(b0 + i) * H1 + k0 + j] : 0.0f;
+            }
+            for (int u = tid; u < kRowsB * D; u += kLd) xs[u] = b0 * D + u < B * D ? x[(int64_t)b0 * D + u] : 0.0f;
         }
-#pragma unroll 4
-        for (int u = tid; u < H2p * 4; u += 256) {
-            const int n = u >> 2, c4 = u & 3;
-            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (n < H2 && k0 + 4 * c4 < H1) w = *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)n * H1 + k0 + 4 * c4);
-            W2T[(4 * c4 + 0) * ld + n] = w.x;
-            W2T[(4 * c4 + 1) * ld + n] = w.y;
-            W2T[(4 * c4 + 2) * ld + n] = w.z;
-            W2T[(4 * c4 + 3) * ld + n] = w.w;
-        }
-        for (int u = tid; u < A1 * H2; u += 256) {
-            const int a = u / H2, n = u - a * H2;
-            whs[u] = P[L.head_row(a) + n];
-        }
-        if constexpr (FUSED)      // the kb == 0 slab also stores its rows' metric sums
+        if constexpr (FUSED)      // the kb == 0 slab also keeps its rows' metric sums
             loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), b0, kRowsB,
-                             dzs, kb == 0 ? ff.mpart : nullptr, reinterpret_cast<double *>(kred));
+                             dzs, kb == 0 ? reinterpret_cast<double *>(kred) : nullptr, kLd, 256 - kLd);
         else
             for (int u = tid; u < kRowsB * A1; u += 256)
                 dzs[u] = b0 * A1 + u < B * A1 ? dz[(int64_t)b0 * A1 + u] : 0.0f;
-        for (int u = tid; u < kRowsB * 16; u += 256) {
-            const int i = u >> 4, j = u & 15;
-            h1m[u] = (b0 + i < B && k0 + j < H1) ? h1[(int64_t)(b0 + i) * H1 + k0 + j] : 0.0f;
-        }
-        for (int u = tid; u < kRowsB * D; u += 256) xs[u] = b0 * D + u < B * D ? x[(int64_t)b0 * D + u] : 0.0f;
         __syncthreads();
         GS_STAMP(0)
+        if constexpr (FUSED)
+            if (kb == 0)
+                store_metric_groups(reinterpret_cast<const double *>(kred), kRowsB, b0, B,
+                                    ff.k_local + (ff.step_base ? *ff.step_base : 0), ff.mpart);
         // dh2 = relu'(h2) * (dz . Wh), in place; thread owns hidden unit n, loops the rows
         for (int n = tid; n < H2; n += 256) {
             float w[kMaxActions + 1];
 #pragma unroll
             for (int a = 0; a < kMaxActions + 1; ++a) w[a] = a < A1 ? whs[a * H2 + n] : 0.0f;
+            const int nb = n >> 4, nbit = n & 15;
             if (A1 <= 5) {
 #pragma unroll 8
                 for (int i = 0; i < kRowsB; ++i) {
-                    const float h = dh2s[i * ld + n];
+                    const bool on = (mkB[i * sh.ncb + nb] >> nbit) & 1;
                     float s = 0.0f;
 #pragma unroll
                     for (int a = 0; a < 5; ++a) s = a < A1 ? fmaf(dzs[i * A1 + a], w[a], s) : s;
-                    dh2s[i * ld + n] = h > 0.0f ? s : 0.0f;
+                    dh2s[i * ld + n] = on ? s : 0.0f;
                 }
             } else {
                 for (int i = 0; i < kRowsB; ++i) {
-                    const float h = dh2s[i * ld + n];
+                    const bool on = (mkB[i * sh.ncb + nb] >> nbit) & 1;
                     float s = 0.0f;
 #pragma unroll
                     for (int a = 0; a < kMaxActions + 1; ++a) s = a < A1 ? fmaf(dzs[i * A1 + a], w[a], s) : s;
-                    dh2s[i * ld + n] = h > 0.0f ? s : 0.0f;
+                    dh2s[i * ld + n] = on ? s : 0.0f;
                 }
             }
+        }
+        for (int u = tid; u < kRowsB * (H2p - H2); u += 256) {      // K padding (runtime shapes)
+            const int i = u / (H2p - H2), n = H2 + (u - i * (H2p - H2));
+            dh2s[i * ld + n] = 0.0f;
         }
         __syncthreads();
         GS_STAMP(1)
@@ -1061,7 +1084,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         }
         if constexpr (FUSED)
             loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, Bp, dzs,
-                             nullptr, nullptr);
+                             nullptr);
         else
             for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
         __syncthreads();
@@ -1355,12 +1378,13 @@ int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, 
             int rc = set_lds_limit((const void *)k_bwd<Sh, true>, lds);
             if (rc) return rc;
             hipLaunchKernelGGL((k_bwd<Sh, true>), dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2,
-                               ws.dz, G, ws.part1, ws.sumsq, stop, ws.zpart, *ff, *la);
+                               ws.dz, G, ws.part1, ws.sumsq, stop, ws.zpart, *ff, *la, ws.h2mask);
         } else {
             int rc = set_lds_limit((const void *)k_bwd<Sh, false>, lds);
             if (rc) return rc;
             hipLaunchKernelGGL((k_bwd<Sh, false>), dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2,
-                               ws.dz, G, ws.part1, ws.sumsq, stop, (const float *)nullptr, FusedFwd{}, LossArgs{});
+                               ws.dz, G, ws.part1, ws.sumsq, stop, (const float *)nullptr, FusedFwd{}, LossArgs{},
+                               ws.h2mask);
         }
         GS_LAUNCH_CHECK("k_bwd");
         return GS_OK;
@@ -1496,7 +1520,8 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
         const int32_t *no_idx = nullptr;
         float *no_copy = nullptr;
         hipLaunchKernelGGL((k_fwd_hidden<Sh, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L, no_obs, no_idx,
-                           0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la);
+                           0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la,
+                           ws.h2mask);
         GS_LAUNCH_CHECK("k_fwd_hidden<fused>");
         return GS_OK;
     });

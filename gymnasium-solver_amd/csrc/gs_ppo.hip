@@ -38,6 +38,7 @@ Workspace carve_workspace(void *base, const Layout &L, int64_t B)
     w.x = take((size_t)B * L.D);
     w.h1 = take((size_t)B * L.H1);
     w.h2 = take((size_t)B * L.H2);
+    w.h2mask = (uint16_t *)take(((size_t)B * n_col_blocks(L.H2) + 1) / 2);
     w.zpart = take((size_t)n_col_blocks(L.H2) * B * A1);
     w.dz = take((size_t)B * A1);
     w.part1 = take((size_t)nrb * L.H1 * (L.D + 1));
@@ -216,7 +217,8 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
 {
     RowGather rg = gather_of(ro, ws);
     rg.step_base = sa.la.step_base;
-    int rc = launch_fwd_hidden(P, L, ro.obs, idx, ro.T, ro.N, B, ws.x, ws.h1, ws.h2, ws.zpart, nullptr, stop, &rg, s);
+    int rc = launch_fwd_hidden(P, L, ro.obs, idx, ro.T, ro.N, B, ws.x, ws.h1, ws.h2, ws.zpart, nullptr, stop, &rg, s,
+                               ws.h2mask);
     if (rc) return rc;
     rc = launch_loss(P, L, B, ws, sa.la, metrics, stop, s);
     if (rc) return rc;
@@ -312,7 +314,7 @@ extern "C" int gs_ppo_loss(const float *params, gs_mlp_dims dims, gs_ppo_hparams
     hipStream_t s = (hipStream_t)stream;
     const RowGather rg = gather_of(ro, ws);
     rc = launch_fwd_hidden(params, L, ro.obs, idx, ro.T, ro.N, batch, ws.x, ws.h1, ws.h2, ws.zpart, nullptr,
-                           nullptr, &rg, s);
+                           nullptr, &rg, s, ws.h2mask);
     if (rc) return rc;
     return launch_loss(params, L, batch, ws, sa.la, metrics, nullptr, s);
 }
@@ -332,7 +334,7 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
     case 0: {
         const RowGather rg = gather_of(ro, ws);
         return launch_fwd_hidden(params, L, ro.obs, idx, ro.T, ro.N, batch, ws.x, ws.h1, ws.h2, ws.zpart, nullptr,
-                                 nullptr, &rg, s);
+                                 nullptr, &rg, s, ws.h2mask);
     }
     case 1:
         return launch_loss(params, L, batch, ws, sa.la, metrics, nullptr, s);
