@@ -109,7 +109,112 @@ class DevicePPOAgent:
             rng_seed=c.seed + 7919 * self.rank, track_stats=self.track_stats)
 
     def get_rollout_collector(self, stage: str) -> DeviceRolloutCollector:
+        if stage not in self._rollout_collectors and stage in ("val", "test"):
+            # evaluation collector: its own env instance (offset seed), same policy
+            c = self.config
+            kw = dict(seed=c.seed + 1000, truncate_every=c.truncate_every, env_offset=self.rank * c.n_envs,
+                      episode_len=c.episode_len, device=self.device)
+            env = (DeviceAtariVecEnv(c.n_envs, n_actions=c.resolved_n_actions(), frame_stack=int(c.frame_stack or 4),
+                                     **kw) if self.is_pixel else
+                   DeviceSyntheticVecEnv(c.n_envs, c.resolved_obs_dim(), c.resolved_n_actions(), **kw))
+            self._envs[stage] = env
+            self._rollout_collectors[stage] = DeviceRolloutCollector(
+                env, self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
+                rng_seed=c.seed + 1000 + 7919 * self.rank, track_stats=False)
         return self._rollout_collectors[stage]
+
+    # ---- checkpoints (agents/base_agent.py:658-885) -----------------------------------------
+    def _adam_state_dicts(self):
+        """Flat HBM moments -> torch.optim.Adam state_dict layout (one entry per tensor in
+        the reference's parameter order)."""
+        pm = self.policy_model
+        to_ref = getattr(pm, "flat_to_reference", None)
+        m = to_ref(self.adam_m) if to_ref else self.adam_m.cpu().numpy()
+        v = to_ref(self.adam_v) if to_ref else self.adam_v.cpu().numpy()
+        state, o = {}, 0
+        for i, (_, shp) in enumerate(pm.shapes()):
+            n = int(np.prod(shp))
+            state[i] = {"step": torch.tensor(float(self.adam_step)),
+                        "exp_avg": torch.as_tensor(m[o:o + n]).reshape(shp).clone(),
+                        "exp_avg_sq": torch.as_tensor(v[o:o + n]).reshape(shp).clone()}
+            o += n
+        group = {"lr": float(self.policy_lr), "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0,
+                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                 "differentiable": False, "fused": None, "params": list(range(len(state)))}
+        return [{"state": state, "param_groups": [group]}]
+
+    def save_checkpoint(self, checkpoint_dir) -> None:
+        """model.pt (reference state_dict keys), optimizer.pt (torch Adam state_dict list),
+        state.json (epoch, counters, config, RNG) — the reference's checkpoint files."""
+        import dataclasses
+        import json
+        import random
+        from pathlib import Path
+        d = Path(checkpoint_dir)
+        d.mkdir(parents=True, exist_ok=True)
+        torch.save(self.policy_model.state_dict(), d / "model.pt")
+        torch.save(self._adam_state_dicts(), d / "optimizer.pt")
+        coll = self.get_rollout_collector("train")
+        np_state = np.random.get_state()
+        state = {
+            "epoch": int(self.current_epoch),
+            "total_env_steps": int(coll.total_steps), "total_vec_steps": int(coll.total_vec_steps),
+            "adam_step": int(self.adam_step), "run_id": None,
+            "config": {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(self.config).items()},
+            "best_train_reward": float(coll._best_episode_reward),
+            "rng_states": {"torch": torch.get_rng_state().tolist(),
+                           "numpy": {"state_type": np_state[0], "state_keys": np_state[1].tolist(),
+                                     "state_pos": int(np_state[2]), "state_has_gauss": int(np_state[3]),
+                                     "state_cached_gaussian": float(np_state[4])},
+                           "random": random.getstate()},
+        }
+        (d / "state.json").write_text(json.dumps(state, default=float))
+
+    def load_checkpoint(self, checkpoint_dir, resume_training: bool = True, strict: bool = True) -> None:
+        """Restore model (and, when resuming, Adam state, counters and RNG) from a checkpoint
+        directory written by save_checkpoint or by the reference (weights_only loads only)."""
+        import json
+        import random
+        from pathlib import Path
+        d = Path(checkpoint_dir)
+        sd = torch.load(d / "model.pt", map_location="cpu", weights_only=True)
+        if strict:
+            self.policy_model.load_state_dict(sd)
+        else:
+            cur = self.policy_model.state_dict()
+            cur.update({k: v for k, v in sd.items() if k in cur and tuple(v.shape) == tuple(cur[k].shape)})
+            self.policy_model.load_state_dict(cur)
+        state = json.loads((d / "state.json").read_text()) if (d / "state.json").exists() else None
+        if not (resume_training and state):
+            return
+        opt_path = d / "optimizer.pt"
+        if opt_path.exists():
+            opt = torch.load(opt_path, map_location="cpu", weights_only=True)
+            opt = opt[0] if isinstance(opt, (list, tuple)) else opt
+            st = opt["state"]
+            m = np.concatenate([np.asarray(st[i]["exp_avg"], np.float32).reshape(-1) for i in sorted(st)])
+            v = np.concatenate([np.asarray(st[i]["exp_avg_sq"], np.float32).reshape(-1) for i in sorted(st)])
+            from_ref = getattr(self.policy_model, "flat_from_reference", None)
+            mt = from_ref(m) if from_ref else torch.as_tensor(m)
+            vt = from_ref(v) if from_ref else torch.as_tensor(v)
+            self.adam_m.copy_(mt.to(self.device))
+            self.adam_v.copy_(vt.to(self.device))
+            steps = {int(float(st[i]["step"])) for i in st}
+            self.adam_step = int(state.get("adam_step", max(steps) if steps else 0))
+        self.current_epoch = int(state.get("epoch", 0))
+        coll = self.get_rollout_collector("train")
+        coll.total_steps = int(state.get("total_env_steps", 0))
+        coll.total_vec_steps = int(state.get("total_vec_steps", 0))
+        if state.get("best_train_reward") is not None:
+            coll._best_episode_reward = float(state["best_train_reward"])
+        rng = state.get("rng_states")
+        if rng:
+            torch.set_rng_state(torch.ByteTensor(rng["torch"]))
+            n = rng["numpy"]
+            np.random.set_state((n["state_type"], np.array(n["state_keys"], dtype=np.uint32), n["state_pos"],
+                                 n["state_has_gauss"], n["state_cached_gaussian"]))
+            r = rng["random"]
+            random.setstate((r[0], tuple(r[1]), r[2]))
 
     def configure_optimizers(self):
         """Adam(params, lr=policy_lr) (utils/optimizer_factory.py:6-29): state in HBM."""

@@ -293,6 +293,57 @@ class DeviceRolloutCollector:
         s[8] += (buf.returns.double() ** 2).sum()
         s[9] += buf.rewards.numel()
 
+    # ---- evaluation (utils/rollout_collector.py:570-655) -----------------------------
+    def evaluate_episodes(self, *, n_episodes: int, deterministic: bool = True,
+                          timeout_seconds: Optional[float] = None) -> dict:
+        """Run the policy (argmax when deterministic) on this collector's device env from a
+        fresh reset until every env finished its balanced share of n_episodes; episode return
+        and length come from the env's completed-episode counters (one small D2H per vector
+        step: evaluation is off the training hot path)."""
+        env = self.env
+        if not getattr(env, "device_native", False):
+            raise ValueError("evaluate_episodes needs a device env")
+        N = self.n_envs
+        base, rem = divmod(int(n_episodes), N)
+        targets = np.array([base + (1 if i < rem else 0) for i in range(N)], np.int64)
+        counts = np.zeros(N, np.int64)
+        rew_sum = len_sum = 0.0
+        env.reset()
+        dev = self.device
+        rew = torch.empty(N, dtype=torch.float32, device=dev)
+        done = torch.empty(N, dtype=torch.uint8, device=dev)
+        tout = torch.empty(N, dtype=torch.uint8, device=dev)
+        act = torch.empty(N, dtype=torch.int64, device=dev)
+        logp = torch.empty(N, dtype=torch.float32, device=dev)
+        val = torch.empty(N, dtype=torch.float32, device=dev)
+        prev_ret = env.ep_ret_sum.double().cpu().numpy()
+        prev_len = env.ep_len_sum.double().cpu().numpy()
+        steps = 0
+        t0 = time.time()
+        while (counts < targets).any():
+            self.policy_model.act(env.obs, mode=1 if deterministic else 0, rng_seed=self.rng_seed + 1,
+                                  rng_counter=steps, actions=act, logp=logp, values=val)
+            env.step_into(rew, done, tout)
+            steps += 1
+            d = done.cpu().numpy().astype(bool)
+            if d.any():
+                r_now = env.ep_ret_sum.double().cpu().numpy()
+                l_now = env.ep_len_sum.double().cpu().numpy()
+                for e in np.nonzero(d)[0]:
+                    if counts[e] < targets[e]:
+                        rew_sum += r_now[e] - prev_ret[e]
+                        len_sum += l_now[e] - prev_len[e]
+                        counts[e] += 1
+                prev_ret, prev_len = r_now, l_now
+            if timeout_seconds is not None and time.time() - t0 >= float(timeout_seconds):
+                break
+        total = int(counts.sum())
+        m = {"cnt/total_episodes": total, "cnt/total_env_steps": int(steps * N), "cnt/total_vec_steps": int(steps)}
+        if total > 0:
+            m["roll/ep_rew/mean"] = float(rew_sum / total)
+            m["roll/ep_len/mean"] = float(len_sum / total)
+        return m
+
     # ---- API parity ------------------------------------------------------------------
     def slice_trajectories(self, trajectories, idxs):
         """utils/rollout_collector.py:657-682 — index the env-major views."""

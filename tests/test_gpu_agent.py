@@ -1,0 +1,50 @@
+"""GPU: agent-level surface — checkpoint files in the reference's format (agents/base_agent.py:
+658-885) round-trip bit-exactly for both policy families, and device evaluate_episodes
+(utils/rollout_collector.py:570-655) returns the reference's keys and episode counts."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _agent(cuda, env="CartPole-v1", variant="ppo", seed=42, **over):
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(seed)
+    base = dict(n_envs=64, n_epochs=2) if variant == "ppo" else dict(n_envs=8, n_steps=16, batch_size=64, n_epochs=1)
+    cfg = load_config(env, variant, overrides=dict(base, **over))
+    return DevicePPOAgent(cfg, device=cuda, track_stats=False)
+
+
+@pytest.mark.parametrize("env,variant", [("CartPole-v1", "ppo"), ("ALE-Pong-v5", "rgb_ppo")])
+def test_checkpoint_round_trip(cuda, tmp_path, env, variant):
+    a = _agent(cuda, env, variant)
+    a.train_epoch()
+    torch.cuda.synchronize()
+    a.save_checkpoint(tmp_path)
+    sd = torch.load(tmp_path / "model.pt", map_location="cpu", weights_only=True)
+    assert list(sd) == [n for n, _ in a.policy_model.shapes()]
+    assert all(tuple(sd[n].shape) == tuple(s) for n, s in a.policy_model.shapes())
+    opt = torch.load(tmp_path / "optimizer.pt", map_location="cpu", weights_only=True)
+    assert isinstance(opt, list) and set(opt[0]) == {"state", "param_groups"}
+    assert len(opt[0]["state"]) == len(sd)
+    b = _agent(cuda, env, variant, seed=7)
+    assert not torch.equal(a.policy_model.params, b.policy_model.params)
+    b.load_checkpoint(tmp_path)
+    torch.cuda.synchronize()
+    for x, y in ((a.policy_model.params, b.policy_model.params), (a.adam_m, b.adam_m), (a.adam_v, b.adam_v)):
+        assert torch.equal(x, y)
+    assert b.adam_step == a.adam_step and b.current_epoch == a.current_epoch
+    assert b.get_rollout_collector("train").total_steps == a.get_rollout_collector("train").total_steps
+    # the state_dict is the reference's layout (the CNN stores conv2/3 and fc permuted inside)
+    for n, t in b.policy_model.state_dict().items():
+        assert torch.equal(t, sd[n])
+
+
+def test_evaluate_episodes_keys_and_counts(cuda):
+    a = _agent(cuda, episode_len=9)
+    out = a.get_rollout_collector("val").evaluate_episodes(n_episodes=100, deterministic=True)
+    assert out["cnt/total_episodes"] == 100
+    assert {"roll/ep_rew/mean", "roll/ep_len/mean", "cnt/total_env_steps", "cnt/total_vec_steps"} <= set(out)
+    assert 1 <= out["roll/ep_len/mean"] <= 9 and out["roll/ep_rew/mean"] == pytest.approx(out["roll/ep_len/mean"])
