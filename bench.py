@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--workload", choices=tuple(WORKLOADS), default="C2",
                     help="C2: CartPole-v1:ppo (the metric's config); C3: LunarLander-v3:ppo shapes (T=2048, B=64); "
                          "C4/C5: ALE Pong/Breakout rgb_ppo (NatureCNN, Atari pixel pipeline)")
+    ap.add_argument("--env-dynamics", choices=("synthetic", "cartpole"), default="synthetic",
+                    help="MLP workloads: SURVEY §8d synthetic fixed-length episodes (default) or device CartPole-v1")
     ap.add_argument("--n-envs", type=int, default=None, help="envs per GPU (weak scaling; default per workload)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of the hipGraph")
     ap.add_argument("--local-comm", action="store_true",
@@ -135,7 +137,10 @@ def main():
     env_id, variant, n_default = WORKLOADS[args.workload]
     pixel = variant == "rgb_ppo"
     n_envs = args.n_envs or n_default
-    cfg = load_config(env_id, variant, overrides=dict(n_envs=n_envs))
+    over = dict(n_envs=n_envs)
+    if not pixel and args.env_dynamics != "synthetic":
+        over["env_dynamics"] = args.env_dynamics
+    cfg = load_config(env_id, variant, overrides=over)
     agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world, comm=comm,
                            use_graph=not args.no_graph, track_stats=False)
     N, T = cfg.n_envs, cfg.n_steps
@@ -241,7 +246,8 @@ def main():
             "metric": "env steps/sec (rollout+PPO update), CartPole n_envs=4096, 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic" if args.env_dynamics == "synthetic" else "device CartPole-v1 dynamics",
             "config": {"workload": (f"{env_id}:{variant} {args.workload} (rollout {N} envs x {T} steps + "
                                     f"{cfg.n_epochs}-epoch PPO update, B={cfg.batch_size})"),
                        "n_envs_per_gpu": N, "n_steps": T, "batch_size": cfg.batch_size, "n_epochs": cfg.n_epochs,

@@ -45,7 +45,7 @@ class DeviceAtariVecEnv:
                                      self.seed, self.env_offset, stream_handle()), "gs_atari_env_reset")
         return self.obs, {}
 
-    def step_into(self, rewards_row, dones_row, timeouts_row):
+    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None):
         self.step_count += 1
         check(lib.gs_atari_env_step(ptr(self.state), ptr(self.ep_ret), ptr(self.obs), ptr(self.frames),
                                     self.num_envs, self.frame_stack, self.out_h, self.out_w, self.episode_len,

@@ -59,6 +59,7 @@ class PPOConfig:
     n_actions: Optional[int] = None
     episode_len: int = 200
     truncate_every: int = 0
+    env_dynamics: str = "synthetic"   # "synthetic" (SURVEY §8d fixed-length episodes) | "cartpole" (f1)
 
     def __post_init__(self):
         self._resolve_numeric_strings()

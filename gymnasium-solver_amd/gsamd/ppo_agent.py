@@ -27,7 +27,7 @@ from ._lib import GS_NUM_METRICS, M, PPOHparams, check, lib, ptr, stream_handle
 from .atari_env import DeviceAtariVecEnv
 from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
-from .rollout import DeviceRolloutCollector, DeviceSyntheticVecEnv
+from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
 
 STAGES = ("train",)
@@ -77,6 +77,10 @@ class DevicePPOAgent:
             env = DeviceAtariVecEnv(n_envs=c.n_envs, n_actions=c.resolved_n_actions(), episode_len=c.episode_len,
                                     seed=c.seed, truncate_every=c.truncate_every, env_offset=self.rank * c.n_envs,
                                     frame_stack=int(c.frame_stack or 4), device=self.device)
+        if env is None and str(getattr(c, "env_dynamics", "synthetic")) == "cartpole":
+            if c.resolved_obs_dim() != 4 or c.resolved_n_actions() != 2:
+                raise ValueError("env_dynamics='cartpole' needs obs_dim 4 and 2 actions")
+            env = DeviceCartPoleVecEnv(c.n_envs, seed=c.seed, env_offset=self.rank * c.n_envs, device=self.device)
         if env is None:
             env = DeviceSyntheticVecEnv(n_envs=c.n_envs, obs_dim=c.resolved_obs_dim(), n_actions=c.resolved_n_actions(),
                                         episode_len=c.episode_len, seed=c.seed, truncate_every=c.truncate_every,

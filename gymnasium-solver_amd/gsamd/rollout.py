@@ -60,13 +60,48 @@ class DeviceSyntheticVecEnv:
                                self.episode_len, self.seed, self.env_offset, stream_handle()), "gs_env_reset")
         return self.obs, {}
 
-    def step_into(self, rewards_row, dones_row, timeouts_row):
+    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None):
         self.step_count += 1
         check(lib.gs_env_step(ptr(self.state), ptr(self.ep_ret), ptr(self.obs), self.num_envs, self.obs_dim,
                               self.episode_len, self.truncate_every, self.reward, self.seed, self.env_offset,
                               self.step_count, ptr(rewards_row), ptr(dones_row), ptr(timeouts_row),
                               ptr(self.ep_count), ptr(self.ep_ret_sum), ptr(self.ep_len_sum), stream_handle()),
               "gs_env_step")
+
+
+class DeviceCartPoleVecEnv:
+    """CartPole-v1 on device (gymnasium 1.x dynamics restated in
+    csrc/gs_cartpole.hip, NEXT_STEP autoreset, TimeLimit 500).  Parity with gymnasium's own
+    episodes is unpinned (reset draws use a counter hash, not PCG64)."""
+
+    device_native = True
+
+    def __init__(self, n_envs, seed=42, env_offset=0, max_steps=500, device="cuda", **_):
+        self.num_envs, self.obs_dim, self.n_actions = int(n_envs), 4, 2
+        self.seed, self.env_offset, self.max_steps = int(seed), int(env_offset), int(max_steps)
+        self.obs_shape, self.obs_dtype = (4,), torch.float32
+        self.device = torch.device(device)
+        N, z = self.num_envs, dict(device=self.device)
+        self.state = torch.zeros(N, 4, dtype=torch.float64, **z)
+        self.meta = torch.zeros(N, 3, dtype=torch.int32, **z)
+        self.ep_ret = torch.zeros(N, dtype=torch.float32, **z)
+        self.obs = torch.zeros(N, 4, dtype=torch.float32, **z)
+        self.ep_count = torch.zeros(N, dtype=torch.int32, **z)
+        self.ep_ret_sum = torch.zeros(N, dtype=torch.float32, **z)
+        self.ep_len_sum = torch.zeros(N, dtype=torch.float32, **z)
+
+    def reset(self):
+        check(lib.gs_cartpole_reset(ptr(self.state), ptr(self.meta), ptr(self.ep_ret), ptr(self.obs), self.num_envs,
+                                    self.seed, self.env_offset, stream_handle()), "gs_cartpole_reset")
+        return self.obs, {}
+
+    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None):
+        if actions is None:
+            raise ValueError("CartPole dynamics need the step's actions")
+        check(lib.gs_cartpole_step(ptr(self.state), ptr(self.meta), ptr(self.ep_ret), ptr(self.obs), ptr(actions),
+                                   self.num_envs, self.max_steps, self.seed, self.env_offset, ptr(rewards_row),
+                                   ptr(dones_row), ptr(timeouts_row), ptr(self.ep_count), ptr(self.ep_ret_sum),
+                                   ptr(self.ep_len_sum), stream_handle()), "gs_cartpole_step")
 
 
 class DeviceRolloutBuffer:
@@ -235,7 +270,7 @@ class DeviceRolloutCollector:
             if native:
                 pm.act(self.env.obs, mode=mode, rng_seed=self.rng_seed, rng_counter=counter, actions=buf.actions[t],
                        logp=buf.logprobs[t], values=buf.values[t], obs_store=buf.obs[t])
-                self.env.step_into(buf.rewards[t], buf.dones[t], buf.timeouts[t])
+                self.env.step_into(buf.rewards[t], buf.dones[t], buf.timeouts[t], actions=buf.actions[t])
             else:
                 self._obs_dev.copy_(torch.from_numpy(self._host_obs))
                 pm.act(self._obs_dev, mode=mode, rng_seed=self.rng_seed, rng_counter=counter, actions=buf.actions[t],
@@ -323,7 +358,7 @@ class DeviceRolloutCollector:
         while (counts < targets).any():
             self.policy_model.act(env.obs, mode=1 if deterministic else 0, rng_seed=self.rng_seed + 1,
                                   rng_counter=steps, actions=act, logp=logp, values=val)
-            env.step_into(rew, done, tout)
+            env.step_into(rew, done, tout, actions=act)
             steps += 1
             d = done.cpu().numpy().astype(bool)
             if d.any():

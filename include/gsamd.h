@@ -239,6 +239,19 @@ int gs_cnn_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, fl
                       int64_t n_minibatches, int64_t adam_step0, float *metrics_dev, int32_t *stop_flag_dev,
                       void *workspace_dev, struct gs_comm *comm, void *stream);
 
+/* ---------------------------------------------------------------- CartPole-v1 dynamics (f1)
+ * gymnasium 1.x CartPoleEnv.step restated on device (double-precision state, Euler, tau 0.02,
+ * TimeLimit max_steps, NEXT_STEP autoreset), for training on real CartPole dynamics without a
+ * host round trip.  state_dev: 4 doubles per env; meta_dev: 3 int32 per env; actions_dev: the
+ * (N) int64 actions of this step (ignored on autoreset steps).  Rows/counters as gs_env_step.
+ * Reset draws come from a counter hash (gymnasium's PCG64 stream is not reproduced). */
+int gs_cartpole_reset(double *state_dev, int32_t *meta_dev, float *ep_ret_dev, float *obs_dev, int64_t N,
+                      uint64_t seed, int64_t env_offset, void *stream);
+int gs_cartpole_step(double *state_dev, int32_t *meta_dev, float *ep_ret_dev, float *obs_dev,
+                     const int64_t *actions_dev, int64_t N, int32_t max_steps, uint64_t seed, int64_t env_offset,
+                     float *rewards_row_dev, uint8_t *dones_row_dev, uint8_t *timeouts_row_dev,
+                     int32_t *ep_done_count_dev, float *ep_ret_sum_dev, float *ep_len_sum_dev, void *stream);
+
 /* ---------------------------------------------------------------- Atari pixel path (a13)
  * The observation pipeline of ale-py's AtariVectorEnv / gymnasium AtariPreprocessing +
  * FrameStackObservation (utils/environment.py:240-303, :362-385), on device: two raw

@@ -48,3 +48,41 @@ def test_evaluate_episodes_keys_and_counts(cuda):
     assert out["cnt/total_episodes"] == 100
     assert {"roll/ep_rew/mean", "roll/ep_len/mean", "cnt/total_env_steps", "cnt/total_vec_steps"} <= set(out)
     assert 1 <= out["roll/ep_len/mean"] <= 9 and out["roll/ep_rew/mean"] == pytest.approx(out["roll/ep_len/mean"])
+
+
+def test_device_cartpole_matches_numpy_twin(cuda):
+    """f1: device CartPole-v1 dynamics vs the float64 numpy restatement over 300 steps of
+    random actions (done/reward rows exact; observations to 1e-5: device cos/sin are not
+    glibc's correctly rounded ones)."""
+    from oracle.cartpole_ref import CartPoleTwin
+    from gsamd.rollout import DeviceCartPoleVecEnv
+    N = 64
+    env = DeviceCartPoleVecEnv(N, seed=3, env_offset=5, max_steps=60, device=cuda)
+    twin = CartPoleTwin(N, seed=3, env_offset=5, max_steps=60)
+    env.reset()
+    rng = np.random.default_rng(0)
+    r = torch.zeros(N, device=cuda)
+    d = torch.zeros(N, dtype=torch.uint8, device=cuda)
+    to = torch.zeros(N, dtype=torch.uint8, device=cuda)
+    n_done = 0
+    for _ in range(300):
+        a = rng.integers(0, 2, N)
+        env.step_into(r, d, to, actions=torch.as_tensor(a).to(cuda))
+        rr, dd, tt = twin.step(a)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d.cpu().numpy().astype(bool), dd)
+        np.testing.assert_array_equal(to.cpu().numpy().astype(bool), tt)
+        np.testing.assert_array_equal(r.cpu().numpy(), rr)
+        np.testing.assert_allclose(env.obs.cpu().numpy(), twin.obs(), atol=1e-5, rtol=0)
+        n_done += int(dd.sum())
+    assert n_done > N     # episodes ended by both termination and truncation
+
+
+def test_agent_trains_on_device_cartpole(cuda):
+    a = _agent(cuda, env_dynamics="cartpole")
+    for _ in range(3):
+        a.train_epoch()
+    torch.cuda.synchronize()
+    assert np.isfinite(a.minibatch_losses()).all()
+    m = a.get_rollout_collector("train").get_metrics()
+    assert m["cnt/total_episodes"] > 0 and m["roll/ep_len/mean"] > 0
