@@ -91,6 +91,8 @@ def _load():
         "gs_cnn_ppo_loss": (ctypes.c_int, [vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, vp, vp, vp, vp]),
         "gs_cnn_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, i64, i64,
                                              vp, vp, vp, vp, vp]),
+        "gs_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64,
+                                       f32, vp, ctypes.c_int, vp]),
         "gs_cartpole_reset": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, vp]),
         "gs_cartpole_step": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, u64, i64, vp, vp, vp, vp, vp, vp, vp]),
         "gs_atari_preprocess": (ctypes.c_int, [vp, i64, i32, i32, vp, vp]),
@@ -115,7 +117,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_env_reset", "gs_env_step",
             "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_ppo_update_workspace_bytes",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
-            "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
+            "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_allreduce_mean_f32", "gs_comm_destroy")
 
 

@@ -252,6 +252,13 @@ int gs_cartpole_step(double *state_dev, int32_t *meta_dev, float *ep_ret_dev, fl
                      float *rewards_row_dev, uint8_t *dones_row_dev, uint8_t *timeouts_row_dev,
                      int32_t *ep_done_count_dev, float *ep_ret_sum_dev, float *ep_len_sum_dev, void *stream);
 
+/* The fp32 MFMA GEMM under the CNN path (convolutions as GEMMs, fc, heads), exported for its
+ * tests: row-major C[M][N] = op(A) op(B) + beta C (+ bias[n]) (ReLU if relu), op(X) = X^T
+ * when t* != 0 (A stored K x M, B stored N x K). */
+int gs_gemm_f32(int ta, int tb, int64_t M, int64_t N, int64_t K, const float *A_dev, int64_t lda,
+                const float *B_dev, int64_t ldb, float *C_dev, int64_t ldc, float beta, const float *bias_dev,
+                int relu, void *stream);
+
 /* ---------------------------------------------------------------- Atari pixel path (a13)
  * The observation pipeline of ale-py's AtariVectorEnv / gymnasium AtariPreprocessing +
  * FrameStackObservation (utils/environment.py:240-303, :362-385), on device: two raw
