@@ -97,6 +97,34 @@ def time_stages(agent, reps: int):
     return out
 
 
+def time_exchange(comm, n: int, reps: int, device, barrier):
+    """Average duration of one gradient exchange of n floats (all ranks replay a graph of
+    `reps` exchanges together after a barrier; HIP events on this rank's stream)."""
+    from gsamd._lib import check, lib
+    buf = torch.zeros(n, dtype=torch.float32, device=device)
+    run = lambda: check(lib.gs_comm_allreduce_mean_f32(comm, buf.data_ptr(), n,  # noqa: E731
+                                                        torch.cuda.current_stream().cuda_stream), "exchange")
+    for _ in range(3):
+        run()
+    barrier()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        for _ in range(reps):
+            run()
+    barrier()
+    g.replay()
+    barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    barrier()
+    del g
+    return us
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,7 +138,12 @@ def main():
     ap.add_argument("--n-envs", type=int, default=None, help="envs per GPU (weak scaling; default per workload)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of the hipGraph")
     ap.add_argument("--local-comm", action="store_true",
-                    help="N=1 only: run the multi-GPU chain through a one-rank RCCL communicator")
+                    help="N=1 only: run the multi-GPU chain through a one-rank communicator")
+    ap.add_argument("--comm", choices=("xgmi", "rccl"), default="xgmi",
+                    help="gradient-exchange transport for N>1 (and --local-comm): one-shot xGMI or RCCL")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a one-GPU box: all ranks share cuda:0 (gloo process group, "
+                         "xGMI exchange through same-device IPC); throughput is not meaningful")
     ap.add_argument("--stage-reps", type=int, default=200)
     ap.add_argument("--cpu-minibatches", type=int, default=2000,
                     help="minibatches in the bounded CPU-baseline sample (0 disables)")
@@ -119,17 +152,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    device = torch.device(f"cuda:{local_rank}")
-    comm = None
+    dev_index = 0 if args.same_device else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device(f"cuda:{dev_index}")
     if world > 1:
         import torch.distributed as dist
-        from gsamd.distributed import init_device_comm
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
-        comm = init_device_comm(rank, world, device)
-    elif args.local_comm:
-        from gsamd.distributed import init_local_comm
-        comm = init_local_comm()
+        if args.same_device:          # rehearsal: every rank on cuda:0, host-side process group
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
@@ -141,8 +172,24 @@ def main():
     if not pixel and args.env_dynamics != "synthetic":
         over["env_dynamics"] = args.env_dynamics
     cfg = load_config(env_id, variant, overrides=over)
-    agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world, comm=comm,
+    agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world,
                            use_graph=not args.no_graph, track_stats=False)
+    comm = None
+    if world > 1 or args.local_comm:      # sized to this policy's flat gradient
+        from gsamd import distributed as gd
+        n_params = agent.policy_model.n_params
+        if world == 1:
+            comm = gd.init_local_comm(args.comm, n_params)
+        elif args.comm == "xgmi":
+            try:
+                comm = gd.init_xgmi_comm(rank, world, n_params, device)
+            except RuntimeError as e:     # every rank raises together: switch transport together
+                _log(f"[bench] {e}; using RCCL for the gradient exchange")
+                args.comm = "rccl (xgmi unavailable)"
+                comm = gd.init_device_comm(rank, world, device)
+        else:
+            comm = gd.init_device_comm(rank, world, device)
+        agent.comm = comm
     N, T = cfg.n_envs, cfg.n_steps
 
     def barrier():
@@ -167,7 +214,7 @@ def main():
     collect_ms = sum(e[0].elapsed_time(e[1]) for e in phases) / len(phases)
     update_ms = sum(e[1].elapsed_time(e[2]) for e in phases) / len(phases)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.same_device else device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     losses = agent.minibatch_losses()
@@ -207,6 +254,8 @@ def main():
         roofline["kernel"] = {"fwd": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}[dom]
         roofline["avg_us"] = round(stage_us[dom], 3)
         roofline["work_per_launch"] = amount
+    if comm is not None:       # every rank takes part (the exchange is collective)
+        stage_us["exchange"] = time_exchange(comm, pm.n_params, args.stage_reps, device, barrier)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path) and args.workload == "C2":   # the committed PMC passes are C2-shaped
         try:
@@ -254,7 +303,8 @@ def main():
                        "minibatches_per_step": agent.n_minibatches, "policy": (f"NatureCNN {pm.in_shape} -> {pm.hidden} -> {{{pm.n_actions} masked to "
                                   f"{len(cfg.valid_actions or [])},1}}" if pixel else
                                   f"MLP {pm.obs_dim}-{pm.hidden_dims[0]}-{pm.hidden_dims[1]}-{{{pm.n_actions},1}}"),
-                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph},
+                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph,
+                       "grad_exchange": args.comm if comm is not None else None},
             "roofline": roofline,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},
             "phases_ms": {"collect": round(collect_ms, 3), "update": round(update_ms, 3),
@@ -263,7 +313,8 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if comm is not None:
-        from gsamd.distributed import destroy_comm
+        from gsamd.distributed import comm_status, destroy_comm
+        comm_status(comm)
         del agent
         destroy_comm(comm)
     if world > 1:

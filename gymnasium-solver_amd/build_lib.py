@@ -34,7 +34,8 @@ def _obj(src):
 def _compile(src, build_dir=None, defines=()):
     path = os.path.join(CSRC, src)
     obj = os.path.join(build_dir, src + ".o") if build_dir else _obj(src)
-    deps = [path, os.path.join(CSRC, "gs_common.h"), os.path.join(HERE, "..", "include", "gsamd.h")]
+    deps = [path, os.path.join(HERE, "..", "include", "gsamd.h")] + [
+        os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return None
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-c", path, "-o", obj]

@@ -24,11 +24,9 @@
 #include <mutex>
 #include <unordered_map>
 
-#include "gs_common.h"
+#include "gs_comm_internal.h"
 
 namespace gs {
-
-int comm_allreduce_sum(::gs_comm *c, float *buf, int64_t n, hipStream_t s, int *world);
 
 namespace {
 
@@ -910,7 +908,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     AdamArgs aa = adam_args(hp, adam_step);
     if (comm) {
         int world = 1;
-        if ((rc = comm_allreduce_sum(comm, G, L.P, s, &world))) return rc;
+        if ((rc = comm_allreduce_sum(comm, G, L.P, s, &world, stop))) return rc;
         aa.grad_scale = 1.0f / (float)world;
     }
     hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop);

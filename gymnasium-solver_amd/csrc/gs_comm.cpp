@@ -1,22 +1,14 @@
-// Multi-GPU exchange: one process per GPU, an RCCL communicator over xGMI, and the
-// single data-path collective of the update — the flat fp32 gradient all-reduce per
-// minibatch step.  Rank 0 makes the unique id, the Python launcher
-// broadcasts it through torch.distributed, every rank then joins here.
+// Multi-GPU exchange: one process per GPU and the single data-path collective of the
+// update — the flat fp32 gradient all-reduce per minibatch step.  This file
+// is the RCCL transport (rank 0 makes the unique id, the Python launcher broadcasts it
+// through torch.distributed, every rank then joins here) and the transport dispatch; the
+// one-shot xGMI transport is gs_xgmi.hip.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
 #include "../../include/gsamd.h"
-
-namespace gs {
-void set_error(const char *fmt, ...);
-}
-
-struct gs_comm {
-    ncclComm_t comm;
-    int nranks;
-    int rank;
-};
+#include "gs_comm_internal.h"
 
 #define GS_NCCL(call)                                                                    \
     do {                                                                                 \
@@ -28,11 +20,14 @@ struct gs_comm {
     } while (0)
 
 namespace gs {
-int comm_allreduce_sum(gs_comm *c, float *buf, int64_t n, hipStream_t s, int *world)
+int xgmi_destroy(gs_comm *c);
+
+int comm_allreduce_sum(gs_comm *c, float *buf, int64_t n, hipStream_t s, int *world, int32_t *stop)
 {
     *world = c->nranks;
+    if (c->kind == kCommXgmi) return xgmi_exchange(c, buf, n, Part1Fold{}, nullptr, nullptr, stop, 1.0f, s);
     // issued for one rank too, so the single-GPU tests run the same RCCL path
-    GS_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm, s));
+    GS_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, (ncclComm_t)c->nccl, s));
     return GS_OK;
 }
 }  // namespace gs
@@ -53,11 +48,14 @@ extern "C" int gs_comm_init(const uint8_t id_bytes[128], int nranks, int rank, g
         return GS_E_INVALID;
     }
     gs_comm *c = new gs_comm{};
+    c->kind = gs::kCommRccl;
     c->nranks = nranks;
     c->rank = rank;
     ncclUniqueId id;
     memcpy(&id, id_bytes, 128);
-    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+    ncclComm_t nc;
+    ncclResult_t r = ncclCommInitRank(&nc, nranks, id, rank);
+    c->nccl = nc;
     if (r != ncclSuccess) {
         gs::set_error("ncclCommInitRank failed: %s", ncclGetErrorString(r));
         delete c;
@@ -73,14 +71,22 @@ extern "C" int gs_comm_allreduce_mean_f32(gs_comm *comm, float *buf, int64_t cou
         gs::set_error("gs_comm_allreduce_mean_f32: bad argument");
         return GS_E_INVALID;
     }
-    GS_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclAvg, comm->comm, (hipStream_t)stream));
+    if (comm->kind == gs::kCommXgmi)
+        return gs::xgmi_exchange(comm, buf, count, gs::Part1Fold{}, nullptr, nullptr, nullptr,
+                                 1.0f / (float)comm->nranks, (hipStream_t)stream);
+    GS_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclAvg, (ncclComm_t)comm->nccl, (hipStream_t)stream));
     return GS_OK;
 }
 
 extern "C" int gs_comm_destroy(gs_comm *comm)
 {
     if (!comm) return GS_OK;
-    ncclResult_t r = ncclCommDestroy(comm->comm);
+    if (comm->kind == gs::kCommXgmi) {
+        const int rc = gs::xgmi_destroy(comm);
+        delete comm;
+        return rc;
+    }
+    ncclResult_t r = ncclCommDestroy((ncclComm_t)comm->nccl);
     delete comm;
     if (r != ncclSuccess) {
         gs::set_error("ncclCommDestroy failed: %s", ncclGetErrorString(r));

@@ -1,0 +1,65 @@
+// gs_comm_internal.h — the communicator behind struct gs_comm (include/gsamd.h) and the
+// exchange entry points the update chains call.  Two transports:
+//   * RCCL (gs_comm_init): ncclAllReduce on the update stream;
+//   * xGMI one-shot (gs_comm_xgmi_create/_connect, gs_xgmi.hip): every rank pushes its
+//     gradient into a slot of every peer's IPC-mapped, uncached exchange region and
+//     raises a per-workgroup flag there; each rank then sums the slots in rank order.
+//     One kernel launch per exchange, graph-capturable, and the sum is bitwise identical
+//     on every rank (fixed order), so replicas never drift apart.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_common.h"
+
+namespace gs {
+
+constexpr int kXgmiMaxRanks = 8;       // one node: 8 MI355X on xGMI
+constexpr int kXgmiMaxWG = 256;        // exchange workgroups: <= one per CU, all co-resident
+constexpr int kXgmiChunk = 1024;       // floats per workgroup chunk (4 per thread)
+// exchange region layout (bytes): flags[src][wg] | err | data[parity][src][cap]
+constexpr size_t kXgmiOffFlags = 0;
+constexpr size_t kXgmiOffErr = kXgmiOffFlags + sizeof(uint32_t) * kXgmiMaxRanks * kXgmiMaxWG;
+constexpr size_t kXgmiOffData = 16384;
+
+enum CommKind { kCommRccl = 0, kCommXgmi = 1 };
+
+// W1/b1 partials folded into the exchanged gradient (MLP chain; part1 == nullptr: none)
+struct Part1Fold {
+    const float *part1;
+    int nrb;
+    Layout L;
+};
+
+}  // namespace gs
+
+struct gs_comm {
+    int kind;
+    int nranks, rank;
+    void *nccl;                                   // ncclComm_t (kCommRccl)
+    // kCommXgmi
+    char *local;                                  // own exchange region (uncached device memory)
+    size_t region_bytes;
+    int64_t cap;                                  // per-rank element capacity (multiple of kXgmiChunk)
+    char *peer[gs::kXgmiMaxRanks];                // region base per rank (peer[rank] == local)
+    bool opened[gs::kXgmiMaxRanks];               // hipIpcOpenMemHandle'd (to close on destroy)
+    bool connected;
+    uint32_t *seq;                                // per-workgroup exchange counters (local, cached)
+    uint64_t timeout_ticks;                       // spin limit, s_memrealtime ticks (100 MHz)
+};
+
+namespace gs {
+// Sum `buf[0:n]` over ranks in place (world returned for the caller's 1/world scale).  The
+// xGMI transport also ORs the ranks' stop flags into *stop (every rank then skips the same
+// optimizer steps) when stop != nullptr.
+int comm_allreduce_sum(gs_comm *c, float *buf, int64_t n, hipStream_t s, int *world, int32_t *stop = nullptr);
+// MLP chain exchange: fold part1 into the gradient, sum over ranks, write one sum-of-squares
+// partial per exchange workgroup into sumsq (their count returned in *n_slots).  RCCL
+// transport: reduce_part1 + ncclAllReduce + sumsq_flat, same outputs.
+int comm_grad_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots,
+                       int32_t *stop, hipStream_t s, int *world);
+// xGMI kernel launcher (gs_xgmi.hip)
+int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
+                  float scale, hipStream_t s);
+}  // namespace gs

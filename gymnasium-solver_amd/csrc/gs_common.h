@@ -88,6 +88,18 @@ struct Layout {
     __host__ __device__ constexpr int64_t head_bias(int a) const { return a < A ? obp + a : obv; }
 };
 
+// W1/b1 gradient partials (part1[rb][H1][D+1], one slab per 32-row block of the minibatch)
+// -> index of flat parameter p < oW2 inside one slab
+__host__ __device__ __forceinline__ int64_t part1_index(const Layout &L, int64_t p)
+{
+    const int D1 = L.D + 1;
+    if (p < L.ob1) {
+        const int64_t k = p / L.D, d = p - k * L.D;
+        return k * D1 + d;
+    }
+    return (p - L.ob1) * D1 + L.D;
+}
+
 // Kernel shape policies.  ShapeC bakes the MLP dims (and optionally the minibatch size)
 // into the kernel, so every loop bound and parameter offset is a compile-time constant
 // (fully unrolled, no integer division, no guard chains); the benchmarked / reference

@@ -1138,15 +1138,6 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
 // ------------------------------------------------------------------------------------
 // k_clip_adam: grid ceil(P / 1024), 256 threads, 4 params per thread (strided).
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t part1_index(const Layout &L, int64_t p)
-{
-    const int D1 = L.D + 1;
-    if (p < L.ob1) {
-        const int64_t k = p / L.D, d = p - k * L.D;
-        return k * D1 + d;
-    }
-    return (p - L.ob1) * D1 + L.D;
-}
 
 template <class S>
 __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layout Lrt, float *__restrict__ G,

@@ -12,12 +12,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "gs_common.h"
-
-struct gs_comm;
-namespace gs {
-int comm_allreduce_sum(gs_comm *c, float *buf, int64_t n, hipStream_t s, int *world);
-}
+#include "gs_comm_internal.h"
 
 namespace gs {
 
@@ -48,7 +43,7 @@ Workspace carve_workspace(void *base, const Layout &L, int64_t B)
     w.f_adv = take((size_t)B);
     w.f_ret = take((size_t)B);
     w.n_slots = n_sumsq_slots(L);
-    const int comm_slots = 64;
+    const int comm_slots = kXgmiMaxWG;   // the xGMI exchange writes one partial per workgroup
     w.sumsq = take((size_t)(w.n_slots > comm_slots ? w.n_slots : comm_slots));
     w.bytes = off;
     return w;
@@ -211,6 +206,23 @@ StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, in
     return a;
 }
 
+// multi-GPU tail of a minibatch step: fold the W1 partials into the flat gradient, sum it
+// over ranks (one xGMI exchange kernel, or reduce_part1 + RCCL + sumsq), then clip/Adam on
+// the mean (grad_scale 1/world) with the exchange's sum-of-squares partials.
+int exchange_and_adam(float *P, float *G, float *M, float *V, const Layout &L, const StepArgs &sa, float *metrics,
+                      int32_t *stop, const Workspace &ws, gs_comm *comm, hipStream_t s)
+{
+    int world = 1, n_slots = 0;
+    int rc = comm_grad_exchange(comm, G, L.P, Part1Fold{ws.part1, sa.aa.nrb, L}, ws.sumsq, &n_slots, stop, s,
+                                &world);
+    if (rc) return rc;
+    AdamArgs aa = sa.aa;
+    aa.n_slots = n_slots;
+    aa.nrb = 0;
+    aa.grad_scale = 1.0f / (float)world;
+    return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
+}
+
 int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const StepArgs &sa,
                  const gs_rollout_view &ro, const int32_t *idx, int64_t B, float *metrics, int32_t *stop,
                  const Workspace &ws, gs_comm *comm, hipStream_t s)
@@ -225,20 +237,7 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
     rc = launch_bwd(P, L, B, ws, G, stop, s);
     if (rc) return rc;
     if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
-    // multi-GPU: finish the flat gradient, all-reduce (sum) over ranks, norm of the mean
-    rc = launch_reduce_part1(ws.part1, L, sa.aa.nrb, G, stop, s);
-    if (rc) return rc;
-    int world = 1;
-    rc = comm_allreduce_sum(comm, G, L.P, s, &world);
-    if (rc) return rc;
-    constexpr int kNormBlocks = 64;
-    rc = launch_sumsq_flat(G, L.P, ws.sumsq, kNormBlocks, s);
-    if (rc) return rc;
-    AdamArgs aa = sa.aa;
-    aa.n_slots = kNormBlocks;
-    aa.nrb = 0;
-    aa.grad_scale = 1.0f / (float)world;
-    return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
+    return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s);
 }
 
 // One minibatch step of the fused chain: k_fwd_hidden<fused> (pre-gathered x), k_bwd<fused>
@@ -253,19 +252,7 @@ int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, 
     rc = launch_bwd(P, L, B, ws, G, stop, s, &ff, &sa.la);
     if (rc) return rc;
     if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
-    rc = launch_reduce_part1(ws.part1, L, sa.aa.nrb, G, stop, s);
-    if (rc) return rc;
-    int world = 1;
-    rc = comm_allreduce_sum(comm, G, L.P, s, &world);
-    if (rc) return rc;
-    constexpr int kNormBlocks = 64;
-    rc = launch_sumsq_flat(G, L.P, ws.sumsq, kNormBlocks, s);
-    if (rc) return rc;
-    AdamArgs aa = sa.aa;
-    aa.n_slots = kNormBlocks;
-    aa.nrb = 0;
-    aa.grad_scale = 1.0f / (float)world;
-    return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
+    return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s);
 }
 
 int validate_update(const gs_mlp_dims &dims, const gs_rollout_view &ro, int64_t batch, const void *ws)

@@ -1,0 +1,336 @@
+// gs_xgmi.hip — one-shot gradient exchange over xGMI.
+//
+// The update's only cross-GPU step is the per-minibatch mean of the flat fp32 gradient
+// (~68k floats for the CartPole MLP).  At that size an all-reduce is pure latency: RCCL's
+// ring/tree protocol pays several link round trips per call, and the step itself is
+// ~25 us.  MI355X GPUs of a node are fully connected by point-to-point xGMI links, so each
+// rank can write its whole gradient straight into every peer in one hop:
+//
+//   region (per rank, hipDeviceMallocUncached, IPC-exported to all peers):
+//       flags[src][wg]  u32   (seq << 1) | stop   written by rank src's workgroup wg
+//       err             u32   sticky: a wait timed out
+//       data[parity][src][cap] f32
+//   seq[wg] (ordinary device memory, never shared): exchanges completed by workgroup wg
+//   k_xgmi_exchange, nwg workgroups (fixed per communicator, <= 256: co-resident):
+//       1. workgroup w takes chunks w, w+nwg, ... of the gradient (folding the MLP's W1
+//          partials on the way), stores them into data[seq&1][rank] of every OTHER rank
+//          (write-through stores over xGMI), waits for their acknowledgements, then raises
+//          flags[rank][w] in those ranks' regions;
+//       2. it waits until flags[src][w] of its own region reach seq for every other src;
+//       3. it sums the sources in rank order, its own chunk re-read locally (bitwise
+//          identical on every rank), writes the chunk back into G and one sum-of-squares
+//          partial for the clip norm.
+//   Two parity slots make back-to-back exchanges safe without a second handshake: a rank
+//   can only start exchange k+1 after every peer has pushed exchange k, and a peer pushes
+//   k only after its kernel for k-1 (the last reader of parity (k+1)&1) has finished.
+// The uncached region keeps every access at the memory side: no L2 line of either GPU ever
+// holds exchange data, so visibility needs only store completion before the flag store and
+// an L1 invalidate after the flag load (no whole-L2 writeback / invalidate).
+#include <stdlib.h>
+#include <string.h>
+
+#include "gs_comm_internal.h"
+
+namespace gs {
+namespace {
+
+struct XgmiArgs {
+    char *peer[kXgmiMaxRanks];
+    int world, rank;
+    int64_t cap, n;
+    int nchunks;
+    float scale;
+    uint64_t timeout;
+    uint32_t *seq;        // [kXgmiMaxWG] exchanges completed per workgroup (this rank only)
+};
+
+// W1/b1 entries p..p+3 (p < oW2) of the flat gradient: the per-row-block partials summed in
+// row-block order (as k_clip_adam does on one GPU), 8 row blocks' loads in flight at a time
+__device__ __forceinline__ float4 fold_part1(const Part1Fold &f, int64_t p)
+{
+    const int64_t n1 = (int64_t)f.L.H1 * (f.L.D + 1);
+    int64_t u[4];
+    bool ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        ok[j] = p + j < f.L.oW2;
+        u[j] = ok[j] ? part1_index(f.L, p + j) : 0;
+    }
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int rb = 0;
+    for (; rb + 8 <= f.nrb; rb += 8) {
+        float t[8][4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[i][j] = ok[j] ? f.part1[(int64_t)(rb + i) * n1 + u[j]] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] += t[i][j];
+    }
+    for (; rb < f.nrb; ++rb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += ok[j] ? f.part1[(int64_t)rb * n1 + u[j]] : 0.f;
+    return make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+// this rank's gradient entries p..p+3 (zeros past n)
+__device__ __forceinline__ float4 own_values(const float *__restrict__ G, const Part1Fold &fold, int64_t n, int64_t p)
+{
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (fold.part1 && p < fold.L.oW2) {
+        v = fold_part1(fold, p);
+        if (p + 3 >= fold.L.oW2) {          // a 4-group straddling the end of b1
+            if (p + 1 >= fold.L.oW2 && p + 1 < n) v.y = G[p + 1];
+            if (p + 2 >= fold.L.oW2 && p + 2 < n) v.z = G[p + 2];
+            if (p + 3 >= fold.L.oW2 && p + 3 < n) v.w = G[p + 3];
+        }
+    } else if (p + 3 < n) {
+        v = *reinterpret_cast<const float4 *>(G + p);
+    } else {
+        if (p + 0 < n) v.x = G[p + 0];
+        if (p + 1 < n) v.y = G[p + 1];
+        if (p + 2 < n) v.z = G[p + 2];
+    }
+    return v;
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// 16-byte store with sc0 sc1 (system coherence): written through to the destination
+// memory whatever the MTYPE of the peer mapping is; completion is awaited by s_waitcnt.
+__device__ __forceinline__ void store_system(float *p, f4 v)
+{
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ float *slot(char *region, int par, int world, int src, int64_t cap)
+{
+    return reinterpret_cast<float *>(region + kXgmiOffData) + ((int64_t)par * world + src) * cap;
+}
+
+__global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Part1Fold fold, XgmiArgs xa,
+                                                       float *__restrict__ sumsq, int32_t *__restrict__ stop)
+{
+    __shared__ float s_red[4];
+    const int w = blockIdx.x, tid = threadIdx.x;
+    char *me = xa.peer[xa.rank];
+    uint32_t *err = reinterpret_cast<uint32_t *>(me + kXgmiOffErr);
+    const uint32_t seq = xa.seq[w] + 1u;     // local cached counter: issued with the gradient loads
+    const int par = (int)(seq & 1u);
+    const uint32_t mystop = (stop && *stop) ? 1u : 0u;
+
+    // 1. push this rank's chunks into slot [par][rank] of every peer's region (its own
+    //    contribution stays in G: step 3 re-reads it locally)
+    float4 first = make_float4(0.f, 0.f, 0.f, 0.f);     // own values of the first chunk, kept
+    for (int c = w; c < xa.nchunks; c += gridDim.x) {
+        const int64_t p = (int64_t)c * kXgmiChunk + tid * 4;
+        const float4 v = own_values(G, fold, xa.n, p);
+        if (c == w) first = v;
+        const f4 vv = {v.x, v.y, v.z, v.w};
+        for (int r = 0; r < xa.world; ++r)
+            if (r != xa.rank) store_system(slot(xa.peer[r], par, xa.world, xa.rank, xa.cap) + p, vv);
+    }
+    // every store of this workgroup acknowledged by its destination memory, then the flags.
+    // (No buffer_wbl2: the data never entered an L2, so a system-scope release, which writes
+    // back this GPU's whole dirty L2, would only cost time.)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid < xa.world && tid != xa.rank) {
+        uint32_t *f = reinterpret_cast<uint32_t *>(xa.peer[tid] + kXgmiOffFlags) + xa.rank * kXgmiMaxWG + w;
+        __hip_atomic_store(f, (seq << 1) | mystop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+
+    // 2. wait for every source's flag (bounded: a dead peer sets the sticky error instead)
+    int anystop = tid == xa.rank ? (int)mystop : 0;
+    if (tid < xa.world && tid != xa.rank) {
+        const uint32_t *f = reinterpret_cast<const uint32_t *>(me + kXgmiOffFlags) + tid * kXgmiMaxWG + w;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+        while (!failed) {
+            const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((v >> 1) >= seq) {
+                anystop = (int)(v & 1u);
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout) {
+                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                failed = true;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    anystop = __syncthreads_or(anystop);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // drop this CU's L1 lines; the region itself is uncached
+
+    // 3. fixed-order sum over sources, write back, sum of squares of the result
+    float ss = 0.0f;
+    for (int c = w; c < xa.nchunks; c += gridDim.x) {
+        const int64_t p = (int64_t)c * kXgmiChunk + tid * 4;
+        const float4 own = c == w ? first : own_values(G, fold, xa.n, p);
+        float4 a = xa.rank == 0 ? own : *reinterpret_cast<const float4 *>(slot(me, par, xa.world, 0, xa.cap) + p);
+        for (int r = 1; r < xa.world; ++r) {
+            const float4 b = r == xa.rank ? own : *reinterpret_cast<const float4 *>(slot(me, par, xa.world, r, xa.cap) + p);
+            a.x += b.x;
+            a.y += b.y;
+            a.z += b.z;
+            a.w += b.w;
+        }
+        a.x *= xa.scale;
+        a.y *= xa.scale;
+        a.z *= xa.scale;
+        a.w *= xa.scale;
+        if (p + 3 < xa.n) {
+            *reinterpret_cast<float4 *>(G + p) = a;
+        } else {
+            if (p + 0 < xa.n) G[p + 0] = a.x;
+            if (p + 1 < xa.n) G[p + 1] = a.y;
+            if (p + 2 < xa.n) G[p + 2] = a.z;
+        }
+        ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;   // lanes past n hold zeros
+    }
+    if (sumsq) {
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+        if ((tid & 63) == 0) s_red[tid >> 6] = ss;
+        __syncthreads();
+        if (tid == 0) sumsq[w] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    }
+    if (tid == 0) {
+        if (w == 0 && stop && anystop) *stop = 1;
+        xa.seq[w] = seq;
+    }
+}
+
+int nwg_of(const gs_comm *c) { return (int)std::min<int64_t>(c->cap / kXgmiChunk, kXgmiMaxWG); }
+
+}  // namespace
+
+int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
+                  float scale, hipStream_t s)
+{
+    GS_REQUIRE(c->connected, "xGMI communicator used before gs_comm_xgmi_connect");
+    GS_REQUIRE(n >= 0 && n <= c->cap, "exchange of %lld floats exceeds the communicator capacity %lld",
+               (long long)n, (long long)c->cap);
+    GS_REQUIRE(((uintptr_t)G & 15) == 0, "exchange buffer must be 16-byte aligned");
+    XgmiArgs xa{};
+    for (int r = 0; r < c->nranks; ++r) xa.peer[r] = c->peer[r];
+    xa.world = c->nranks;
+    xa.rank = c->rank;
+    xa.cap = c->cap;
+    xa.n = n;
+    xa.nchunks = (int)((n + kXgmiChunk - 1) / kXgmiChunk);
+    xa.scale = scale;
+    xa.timeout = c->timeout_ticks;
+    xa.seq = c->seq;
+    const int nwg = nwg_of(c);
+    hipLaunchKernelGGL(k_xgmi_exchange, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
+    GS_LAUNCH_CHECK("k_xgmi_exchange");
+    if (n_slots) *n_slots = nwg;
+    return GS_OK;
+}
+
+int comm_grad_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots,
+                       int32_t *stop, hipStream_t s, int *world)
+{
+    *world = c->nranks;
+    if (c->kind == kCommXgmi) return xgmi_exchange(c, G, n, fold, sumsq, n_slots, stop, 1.0f, s);
+    int rc;
+    if (fold.part1 && (rc = launch_reduce_part1(fold.part1, fold.L, fold.nrb, G, stop, s))) return rc;
+    if ((rc = comm_allreduce_sum(c, G, n, s, world, stop))) return rc;
+    constexpr int kNormBlocks = 64;
+    if ((rc = launch_sumsq_flat(G, n, sumsq, kNormBlocks, s))) return rc;
+    *n_slots = kNormBlocks;
+    return GS_OK;
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint8_t out_handle[64], gs_comm **out)
+{
+    GS_REQUIRE(out && out_handle, "gs_comm_xgmi_create: null output");
+    GS_REQUIRE(nranks >= 1 && nranks <= kXgmiMaxRanks && rank >= 0 && rank < nranks,
+               "gs_comm_xgmi_create: rank %d / nranks %d (at most %d ranks: one node)", rank, nranks, kXgmiMaxRanks);
+    GS_REQUIRE(max_count >= 1 && max_count <= ((int64_t)1 << 30), "gs_comm_xgmi_create: bad max_count %lld",
+               (long long)max_count);
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is 64 bytes");
+    const int64_t cap = (max_count + kXgmiChunk - 1) / kXgmiChunk * kXgmiChunk;
+    const size_t bytes = kXgmiOffData + sizeof(float) * 2 * (size_t)nranks * (size_t)cap;
+    void *p = nullptr;
+    GS_HIP(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
+    hipError_t e = hipMemset(p, 0, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    hipIpcMemHandle_t h;
+    if (e == hipSuccess) e = hipIpcGetMemHandle(&h, p);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return hip_fail(e, "xGMI exchange region setup", __FILE__, __LINE__);
+    }
+    memcpy(out_handle, &h, 64);
+    gs_comm *c = new gs_comm{};
+    c->kind = kCommXgmi;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->local = (char *)p;
+    c->region_bytes = bytes;
+    c->cap = cap;
+    c->peer[rank] = c->local;
+    void *sq = nullptr;
+    e = hipMalloc(&sq, sizeof(uint32_t) * kXgmiMaxWG);
+    if (e == hipSuccess) e = hipMemset(sq, 0, sizeof(uint32_t) * kXgmiMaxWG);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        delete c;
+        return hip_fail(e, "xGMI sequence counters", __FILE__, __LINE__);
+    }
+    c->seq = (uint32_t *)sq;
+    double secs = 120.0;
+    if (const char *env = getenv("GS_XGMI_TIMEOUT_S")) secs = atof(env);
+    c->timeout_ticks = (uint64_t)(secs > 0 ? secs * 1e8 : 1.2e10);   // s_memrealtime: 100 MHz
+    *out = c;
+    return GS_OK;
+}
+
+extern "C" int gs_comm_xgmi_connect(gs_comm *c, const uint8_t *handles)
+{
+    GS_REQUIRE(c && c->kind == kCommXgmi && handles, "gs_comm_xgmi_connect: not an xGMI communicator");
+    GS_REQUIRE(!c->connected, "gs_comm_xgmi_connect: already connected");
+    for (int r = 0; r < c->nranks; ++r) {
+        if (r == c->rank) continue;
+        hipIpcMemHandle_t h;
+        memcpy(&h, handles + 64 * (size_t)r, 64);
+        void *pp = nullptr;
+        GS_HIP(hipIpcOpenMemHandle(&pp, h, hipIpcMemLazyEnablePeerAccess));
+        c->peer[r] = (char *)pp;
+        c->opened[r] = true;
+    }
+    c->connected = true;
+    return GS_OK;
+}
+
+extern "C" int gs_comm_status(gs_comm *c)
+{
+    GS_REQUIRE(c, "gs_comm_status: null communicator");
+    if (c->kind != kCommXgmi) return GS_OK;
+    uint32_t err = 0;
+    GS_HIP(hipMemcpy(&err, c->local + kXgmiOffErr, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+        set_error("xGMI exchange timed out waiting for a peer (rank %d of %d)", c->rank, c->nranks);
+        return GS_E_COMM;
+    }
+    return GS_OK;
+}
+
+namespace gs {
+int xgmi_destroy(gs_comm *c)
+{
+    for (int r = 0; r < c->nranks; ++r)
+        if (c->opened[r]) (void)hipIpcCloseMemHandle(c->peer[r]);
+    if (c->seq) GS_HIP(hipFree(c->seq));
+    if (c->local) GS_HIP(hipFree(c->local));
+    return GS_OK;
+}
+}  // namespace gs

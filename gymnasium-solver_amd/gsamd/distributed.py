@@ -1,7 +1,10 @@
 """Multi-GPU plumbing for the device path: one process per GPU, envs sharded
-by rank, one RCCL communicator per process built from a unique id that rank 0 makes and
-torch.distributed broadcasts.  The communicator is handed to DevicePPOAgent(comm=...) and used
-inside the C-ABI for the per-minibatch gradient all-reduce; nothing else crosses GPUs."""
+by rank, one communicator per process handed to DevicePPOAgent(comm=...) and used inside the
+C-ABI for the per-minibatch gradient mean; nothing else crosses GPUs.
+
+Two transports: the one-shot xGMI exchange (init_xgmi_comm: IPC handles of
+each rank's exchange region all-gathered through torch.distributed; the default) and RCCL
+(init_device_comm: a unique id that rank 0 makes and torch.distributed broadcasts)."""
 from __future__ import annotations
 
 import ctypes
@@ -45,9 +48,112 @@ def init_device_comm(rank: int, world_size: int, device: Optional[torch.device] 
     return h.value
 
 
-def init_local_comm() -> int:
+XGMI_HANDLE_BYTES = 64
+
+
+def _all_gather_bytes(payload: bytes, device: Optional[torch.device] = None) -> bytes:
+    """Concatenate every rank's fixed-size payload in rank order over torch.distributed."""
+    import torch.distributed as dist
+    t = torch.frombuffer(bytearray(payload), dtype=torch.uint8).clone()
+    if dist.get_backend() == "nccl":
+        t = t.to(device if device is not None else torch.device("cuda", torch.cuda.current_device()))
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return b"".join(bytes(p.cpu().numpy().tobytes()) for p in parts)
+
+
+def xgmi_create(rank: int, world_size: int, max_count: int):
+    """Allocate and IPC-export this rank's exchange region: (handle, 64 handle bytes)."""
+    hb = (ctypes.c_uint8 * XGMI_HANDLE_BYTES)()
+    h = ctypes.c_void_p()
+    check(lib.gs_comm_xgmi_create(int(world_size), int(rank), int(max_count), ctypes.addressof(hb), ctypes.byref(h)),
+          "gs_comm_xgmi_create")
+    return h.value, bytes(hb)
+
+
+def xgmi_connect(handle: int, all_handles: bytes) -> None:
+    buf = (ctypes.c_uint8 * len(all_handles)).from_buffer_copy(all_handles)
+    check(lib.gs_comm_xgmi_connect(handle, ctypes.addressof(buf)), "gs_comm_xgmi_connect")
+
+
+def _agree(ok: bool, device: Optional[torch.device]) -> bool:
+    """True only if every rank passes ok=True."""
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    if dist.get_backend() == "nccl":
+        t = t.to(device if device is not None else torch.device("cuda", torch.cuda.current_device()))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def xgmi_self_test(handle: int, rank: int, world_size: int, n: int, device: torch.device, rounds: int = 3) -> bool:
+    """Exchange known vectors a few times and compare every element with the exact
+    fixed-order answer (also proves the peers' flags arrive)."""
+    import numpy as np
+    from ._lib import stream_handle
+    idx = np.arange(n, dtype=np.int64)
+    for it in range(rounds):
+        vals = [((r + 1) * (it + 3) + (idx * (r + 5) + it) % 11).astype(np.float32) for r in range(world_size)]
+        buf = torch.from_numpy(vals[rank]).to(device)
+        check(lib.gs_comm_allreduce_mean_f32(handle, buf.data_ptr(), n, stream_handle()), "gs_comm_allreduce_mean_f32")
+        acc = vals[0]
+        for r in range(1, world_size):
+            acc = acc + vals[r]
+        want = acc * np.float32(1.0 / world_size)
+        got = buf.cpu().numpy()
+        if lib.gs_comm_status(handle) != 0 or not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+            return False
+    return True
+
+
+def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[torch.device] = None,
+                   self_test: bool = True) -> int:
+    """One-shot xGMI communicator for exchanges of up to max_count floats (the policy's
+    parameter count): create, all-gather the handles, open the peers, barrier, then (by
+    default) a bit-exact self-test agreed on by every rank.  Raises RuntimeError on every
+    rank if any rank fails (the caller may then choose RCCL instead)."""
+    import torch.distributed as dist
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    h, ok, why = None, True, ""
+    try:
+        h, mine = xgmi_create(rank, world_size, max_count)
+    except RuntimeError as e:
+        ok, why = False, str(e)
+    handles = _all_gather_bytes(mine if ok else bytes(XGMI_HANDLE_BYTES), device)
+    if ok:
+        try:
+            xgmi_connect(h, handles)
+        except RuntimeError as e:
+            ok, why = False, str(e)
+    ok = _agree(ok, device)
+    dist.barrier()
+    if ok and self_test:
+        try:
+            ok = xgmi_self_test(h, rank, world_size, min(int(max_count), 1 << 16), dev)
+            why = "" if ok else "self-test mismatch or timeout"
+        except RuntimeError as e:
+            ok, why = False, str(e)
+        ok = _agree(ok, device)
+    if not ok:
+        if h:
+            destroy_comm(h)
+        raise RuntimeError(f"xGMI exchange unavailable on rank {rank}: {why or 'a peer failed'}")
+    return h
+
+
+def comm_status(handle: Optional[int]) -> None:
+    """Raise if an exchange on this communicator timed out waiting for a peer."""
+    if handle:
+        check(lib.gs_comm_status(handle), "gs_comm_status")
+
+
+def init_local_comm(transport: str = "rccl", max_count: int = 1 << 20) -> int:
     """A one-rank communicator (no torch.distributed needed): exercises the multi-GPU kernel
-    chain and the RCCL call on a single GPU."""
+    chain and the transport's call on a single GPU."""
+    if transport == "xgmi":
+        h, mine = xgmi_create(0, 1, max_count)
+        xgmi_connect(h, mine)
+        return h
     uid = (ctypes.c_uint8 * UNIQUE_ID_BYTES)()
     check(lib.gs_comm_unique_id(ctypes.addressof(uid)), "gs_comm_unique_id")
     h = ctypes.c_void_p()

@@ -281,11 +281,23 @@ int gs_atari_env_step(int32_t *state_dev, float *ep_ret_dev, uint8_t *stack_dev,
                       uint8_t *dones_row_dev, uint8_t *timeouts_row_dev, int32_t *ep_done_count_dev,
                       float *ep_ret_sum_dev, float *ep_len_sum_dev, void *stream);
 
-/* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI)
- * One process per GPU.  Rank 0 creates the 128-byte unique id, the launcher
- * broadcasts it (torch.distributed), every rank calls gs_comm_init. */
+/* ---------------------------------------------------------------- multi-GPU (xGMI / RCCL)
+ * One process per GPU; replaces the reference's single-process gradient step
+ * (agents/base_agent.py:331-355 manual_backward + optimizer.step) with a data-parallel
+ * mean over ranks.  Two transports behind the same handle:
+ *   RCCL: rank 0 creates the 128-byte unique id, the launcher broadcasts it
+ *         (torch.distributed), every rank calls gs_comm_init.
+ *   xGMI one-shot (default for the update): every rank calls gs_comm_xgmi_create (allocates
+ *         and IPC-exports its exchange region, max_count = largest exchange in floats),
+ *         the launcher all-gathers the 64-byte handles in rank order, every rank calls
+ *         gs_comm_xgmi_connect; after a barrier the communicator is ready.  A wait that
+ *         exceeds GS_XGMI_TIMEOUT_S (default 120 s) sets a sticky error that
+ *         gs_comm_status reports (GS_E_COMM); later exchanges then fail fast. */
 int gs_comm_unique_id(uint8_t out_id[128]);
 int gs_comm_init(const uint8_t id[128], int nranks, int rank, struct gs_comm **out);
+int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint8_t out_handle[64], struct gs_comm **out);
+int gs_comm_xgmi_connect(struct gs_comm *comm, const uint8_t *handles);
+int gs_comm_status(struct gs_comm *comm);
 int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
 int gs_comm_destroy(struct gs_comm *comm);
 

@@ -124,3 +124,71 @@ def dp_worker(rank, world, port, result_dir):
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------------------
+# GPU ranks (tests/test_gpu_xgmi.py): every rank on cuda:0 of the one-GPU box, exchanging
+# through IPC-mapped regions exactly as the ranks of a node do over xGMI.
+# --------------------------------------------------------------------------------------
+def exchange_values(rank, it, n):
+    """Deterministic per-(rank, iteration) payload with mixed magnitudes and signs."""
+    rng = np.random.default_rng(1 + 7919 * it + 104729 * rank)
+    return (rng.standard_normal(n) * np.exp(rng.uniform(-6, 6, n))).astype(np.float32)
+
+
+def xgmi_exchange_worker(rank, world, port, result_dir, n, iters):
+    """Back-to-back exchanges with no host sync in between (both parity slots reused many
+    times), then the device result of every iteration is saved for the parent."""
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd._lib import check, lib
+        from gsamd.distributed import comm_status, destroy_comm, init_xgmi_comm
+        torch.cuda.set_device(0)
+        h = init_xgmi_comm(rank, world, n)
+        bufs = [torch.from_numpy(exchange_values(rank, it, n)).cuda() for it in range(iters)]
+        torch.cuda.synchronize()
+        dist.barrier()
+        s = torch.cuda.current_stream()
+        for b in bufs:
+            check(lib.gs_comm_allreduce_mean_f32(h, b.data_ptr(), n, s.cuda_stream), "allreduce")
+        torch.cuda.synchronize()
+        comm_status(h)
+        np.save(os.path.join(result_dir, f"x{rank}.npy"), torch.stack(bufs).cpu().numpy())
+        dist.barrier()
+        destroy_comm(h)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def xgmi_ppo_worker(rank, world, port, result_dir, use_graph):
+    """Data-parallel PPO update over the xGMI transport: rank-sharded envs, one rollout and
+    2 epochs; every rank saves its final parameters and per-minibatch losses."""
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd.config import load_config
+        from gsamd.distributed import comm_status, destroy_comm, init_xgmi_comm
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        torch.manual_seed(42)
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=256, n_epochs=2))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=use_graph,
+                               track_stats=False)
+        agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
+        agent.train_epoch()
+        torch.cuda.synchronize()
+        comm_status(agent.comm)
+        np.save(os.path.join(result_dir, f"p{rank}.npy"), agent.policy_model.params.cpu().numpy())
+        np.save(os.path.join(result_dir, f"l{rank}.npy"), np.asarray(agent.minibatch_losses(), np.float32))
+        dist.barrier()
+        comm = agent.comm
+        del agent
+        destroy_comm(comm)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()

@@ -314,10 +314,12 @@ def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph
     np.testing.assert_allclose(m0, m1, rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("transport", ["rccl", "xgmi"])
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_comm_update_path_matches_single_gpu(cuda, use_graph):
-    """The multi-GPU kernel chain (dW1 partial reduce -> RCCL all-reduce (one-rank communicator)
-    -> flat-norm -> clip+Adam scaled by 1/G) gives the single-GPU update: identical losses for the
+def test_comm_update_path_matches_single_gpu(cuda, use_graph, transport):
+    """The multi-GPU kernel chain (dW1 partial fold -> exchange over a one-rank communicator
+    (RCCL all-reduce, or the xGMI exchange kernel) -> flat norm -> clip+Adam scaled by 1/G)
+    gives the single-GPU update: identical losses for the
     first minibatch, losses within 1e-4 and final params within 1e-5 relative L2 after one rollout
     x 2 epochs = 128 minibatch steps (the clip norm's summation order differs between the chains)."""
     from gsamd.config import load_config
@@ -325,7 +327,7 @@ def test_comm_update_path_matches_single_gpu(cuda, use_graph):
     from gsamd.ppo_agent import DevicePPOAgent
     out = []
     for with_comm in (False, True):
-        comm = init_local_comm() if with_comm else None
+        comm = init_local_comm(transport, 70_000) if with_comm else None
         torch.manual_seed(42)
         cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=512, n_epochs=2))
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False, comm=comm)
