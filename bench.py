@@ -52,13 +52,16 @@ def cnn_minibatch_flops(B, A):
     return 2.0 * B * (fwd + bwd)
 
 
-def stage_flops_bytes(D, H1, H2, A, B, P):
-    """Algorithmic work per launch of each minibatch-step kernel."""
+def stage_flops_bytes(D, H1, H2, A, B, P, fused=True):
+    """Algorithmic work per launch of each minibatch-step kernel; in the fused
+    chain k_bwd also computes the loss rows (no k_loss launch)."""
     A1 = A + 1
     fwd = 2.0 * B * (D * H1 + H1 * H2 + H2 * A1)
     loss = 2.0 * B * A1 * (H2 // 16) + 30.0 * B
     bwd = 2.0 * B * H2 * A1 + 2.0 * B * H1 * H2 * 2 + 2.0 * B * H1 * (D + 1) + 2.0 * B * H2 * A1 + B * H2
     adam_bytes = 4.0 * P * 7      # read p, g, m, v; write p, m, v
+    if fused:
+        return {"fwd": ("mfma", fwd), "bwd": ("mfma", bwd + loss), "adam": ("hbm", adam_bytes)}
     return {"fwd": ("mfma", fwd), "loss": ("mfma", loss), "bwd": ("mfma", bwd), "adam": ("hbm", adam_bytes)}
 
 
@@ -76,7 +79,11 @@ def time_stages(agent, reps: int):
                        agent.workspace.data_ptr(), torch.cuda.current_stream().cuda_stream)
     saved = [t.clone() for t in (pm.params, agent.grads, agent.adam_m, agent.adam_v)]
     out = {}
-    for st, name in enumerate(("fwd", "loss", "bwd", "adam")):
+    # the fused chain (what gs_ppo_update runs for the compile-time shapes): gather once,
+    # then k_fwd_hidden<fused>, k_bwd<fused> (loss rows inside), k_clip_adam
+    fused = lib.gs_ppo_stage(*args(6)) == 0
+    stages = ((4, "fwd"), (5, "bwd"), (3, "adam")) if fused else ((0, "fwd"), (1, "loss"), (2, "bwd"), (3, "adam"))
+    for st, name in stages:
         for _ in range(3):
             check(lib.gs_ppo_stage(*args(st)), "gs_ppo_stage")
         torch.cuda.synchronize()
@@ -94,7 +101,7 @@ def time_stages(agent, reps: int):
         del g
     for t, s in zip((pm.params, agent.grads, agent.adam_m, agent.adam_v), saved):
         t.copy_(s)
-    return out
+    return out, fused
 
 
 def time_exchange(comm, n: int, reps: int, device, barrier):
@@ -238,9 +245,9 @@ def main():
                     "kernel": "cnn minibatch step (rocBLAS sgemm + gs_cnn kernels)", "avg_us": round(mb_us, 3),
                     "work_per_launch": amount}
     else:
-        stage_us = time_stages(agent, args.stage_reps)
+        stage_us, fused = time_stages(agent, args.stage_reps)
         work = stage_flops_bytes(pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions, agent.batch_size,
-                                 pm.n_params)
+                                 pm.n_params, fused)
         dom = max(stage_us, key=stage_us.get)
         bound, amount = work[dom]
         if bound == "mfma":

@@ -312,11 +312,24 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
 {
     int rc = validate_update(dims, ro, batch, workspace);
     if (rc) return rc;
-    GS_REQUIRE(stage >= 0 && stage <= 3, "gs_ppo_stage: stage %d not in [0, 3]", stage);
+    GS_REQUIRE(stage >= 0 && stage <= 6, "gs_ppo_stage: stage %d not in [0, 6]", stage);
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
     const StepArgs sa = make_step_args(hp, L, batch, adam_step < 1 ? 1 : adam_step);
     hipStream_t s = (hipStream_t)stream;
+    if (stage >= 4) {     // the fused chain's kernels on minibatch 0 of a one-minibatch update
+        GS_REQUIRE(has_fused(L, batch), "gs_ppo_stage: no fused instantiation for this shape");
+        const FusedWs fw = carve_fused(workspace, L, batch, 1);
+        FusedFwd ff{};
+        ff.xg = fw.xg, ff.fa = fw.fa, ff.folp = fw.folp, ff.fov = fw.fov, ff.fadv = fw.fadv, ff.fret = fw.fret;
+        ff.mpart = fw.mpart;
+        ff.dz = ws.dz;
+        if (stage == 6)
+            return launch_gather_all(L, batch, 1, idx, ro.obs, ro.actions, ro.logprobs, ro.values, ro.advantages,
+                                     ro.returns, ro.T, ro.N, hp.normalize_adv, ff, metrics, s);
+        if (stage == 4) return launch_fwd_fused(params, L, batch, ff, sa.la, ws, nullptr, s);
+        return launch_bwd(params, L, batch, ws, grads, nullptr, s, &ff, &sa.la);
+    }
     switch (stage) {
     case 0: {
         const RowGather rg = gather_of(ro, ws);

@@ -170,9 +170,12 @@ int gs_ppo_minibatch_step(float *params_dev, float *grads_dev, float *adam_m_dev
 int gs_ppo_loss(const float *params_dev, gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout,
                 const int32_t *idx_dev, int64_t batch, float *metrics_dev, void *workspace_dev, void *stream);
 
-/* Enqueue ONE stage of a minibatch step on the current workspace (0 = k_fwd_hidden,
- * 1 = k_loss, 2 = k_bwd, 3 = k_clip_adam).  Used by bench.py to time each kernel
- * with events on the stream it is launched on (roofline measurement). */
+/* Enqueue ONE stage of a minibatch step on the current workspace.  Unfused chain:
+ * 0 = k_fwd_hidden, 1 = k_loss, 2 = k_bwd, 3 = k_clip_adam.  Fused chain (the one
+ * gs_ppo_update runs for the compile-time shapes): 6 = k_gather_all for a one-minibatch
+ * update (run once first), 4 = k_fwd_hidden<fused>, 5 = k_bwd<fused> (loss rows inside),
+ * then 3.  Used by bench.py to time each kernel with events on the stream it is launched
+ * on (roofline measurement). */
 int gs_ppo_stage(int stage, float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
                  gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout, const int32_t *idx_dev,
                  int64_t batch, int64_t adam_step, float *metrics_dev, void *workspace_dev, void *stream);

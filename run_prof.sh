@@ -1,9 +1,9 @@
 #!/bin/bash
 # GPU-box: default bench under rocprofv3 kernel-trace stats, then two separate PMC passes.
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r01
+TAG=${TAG:-r01}; mkdir -p gpurun_out/$TAG
 export TMPDIR=/tmp
-O=gpurun_out/r01
+O=gpurun_out/$TAG
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/stats -o bench --output-format csv -- python bench.py ${BENCH_ARGS} > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep '^{' $O/bench.log; tail -3 $O/bench.log
 rm -f $O/stats/bench_kernel_trace.csv; cut -c1-60,200-400 $O/stats/bench_kernel_stats.csv | head -8

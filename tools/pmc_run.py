@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Workload for the rocprofv3 --pmc passes (profiles/pmc_traffic.json): one C2 rollout, then
-`--reps` eager launches of each minibatch-step kernel through gs_ppo_stage (no hipGraph, so
+`--reps` eager launches of each fused-chain minibatch kernel through gs_ppo_stage (no hipGraph, so
 every dispatch is a separate counter record).  Run under
   rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d DIR -o pmc_fetch -- python tools/pmc_run.py
   rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d DIR -o pmc_write -- python tools/pmc_run.py
@@ -30,13 +30,16 @@ def main():
     agent.train_epoch()
     pm = agent.policy_model
     idx = agent.prefetcher.device_buf
-    for st in range(4):
+    def stage(st):
+        check(lib.gs_ppo_stage(st, pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                               agent.adam_v.data_ptr(), pm.dims, agent.hparams(),
+                               agent.get_rollout_collector("train").buffer.view(), idx.data_ptr(),
+                               agent.batch_size, 1, agent.metrics_buf.data_ptr(), agent.workspace.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream), "gs_ppo_stage")
+    stage(6)                     # the fused chain's per-update gather (what gs_ppo_update runs)
+    for st in (4, 5, 3):         # k_fwd_hidden<fused>, k_bwd<fused>, k_clip_adam
         for _ in range(a.reps):
-            check(lib.gs_ppo_stage(st, pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
-                                   agent.adam_v.data_ptr(), pm.dims, agent.hparams(),
-                                   agent.get_rollout_collector("train").buffer.view(), idx.data_ptr(),
-                                   agent.batch_size, 1, agent.metrics_buf.data_ptr(), agent.workspace.data_ptr(),
-                                   torch.cuda.current_stream().cuda_stream), "gs_ppo_stage")
+            stage(st)
     torch.cuda.synchronize()
     print("pmc_run done")
 
