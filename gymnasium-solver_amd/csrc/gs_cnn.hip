@@ -4,19 +4,19 @@
 // utils/policy_ops.py:44-75, MaskedCategorical utils/distributions.py:8-82, PPO losses
 // agents/ppo/ppo_agent.py:21-152, clip_grad_norm_ + Adam agents/base_agent.py:591-621.
 //
-// Layout: activations are NHWC so every convolution is one GEMM over an
-// im2col matrix whose rows are (sample, out_y, out_x) and whose columns run (ky, kx, c)
-// with c fastest (contiguous float4 gathers).  conv1 reads the u8 frame stack straight from
-// the rollout buffer (NCHW, the reference's order) through the minibatch index, so its
-// columns run (c, ky, kx) and its weight keeps torch's layout.  conv2 / conv3 / fc weights are
-// stored internally in (out, ky, kx, c) / (out, y, x, c) order; gsamd.cnn converts state_dicts.
+// Layout: activations are NHWC; every convolution is an implicit GEMM
+// (gs_gemm.hip) whose rows are (sample, out_y, out_x) and whose patch columns run
+// (ky, kx, c) with c fastest.  conv1 reads the u8 frame stack straight from the rollout buffer
+// (NCHW, the reference's order) through the minibatch index inside the GEMM's operand loader,
+// so its columns run (c, ky, kx) and its weight keeps torch's layout.  conv2 / conv3 / fc
+// weights are stored internally in (out, ky, kx, c) / (out, y, x, c) order; gsamd.cnn
+// converts state_dicts.
 //
-// GEMMs (conv fwd / dgrad / wgrad, fc) are rocBLAS sgemm calls in fp32 with atomics disabled
-// (deterministic); everything around them is hand-written here: im2col gathers (u8 -> /255
-// through an exact LUT), bias+ReLU, heads, the masked-categorical PPO loss with analytic
-// dlogits, ReLU-masked col2im, bias-gradient column sums, global-norm clip and Adam.
+// Every kernel is hand-written: the fp32 MFMA GEMM engine (conv forward with bias + ReLU in
+// the epilogue, split-K weight gradients with fixed-order partial sums, fc, heads, dgrad), the
+// masked-categorical PPO loss with analytic dlogits, ReLU-masked col2im, bias-gradient column
+// sums, global-norm clip and Adam.  All reductions run in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
 
 #include <float.h>
 #include <math.h>
@@ -25,6 +25,7 @@
 #include <unordered_map>
 
 #include "gs_comm_internal.h"
+#include "gs_gemm.h"
 
 namespace gs {
 
@@ -78,7 +79,7 @@ struct CnnLayout {
 };
 
 struct CnnWs {
-    float *cols1, *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dh, *da3, *da2, *da1;
+    float *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dh, *da3, *da2, *da1;
     int32_t *f_act;
     float *f_olp, *f_ov, *f_adv, *f_ret;
     double *norm_part;
@@ -88,8 +89,19 @@ struct CnnWs {
 };
 
 constexpr int kNormBlocks = 1024;
-constexpr int kSplitK = 32;     // weight-gradient GEMMs: K = B*positions split into 32 sample groups
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
+// split-K slices of the weight-gradient GEMMs (K = minibatch rows x positions): enough slices
+// that the small (Cout x patch) outputs still fill the chip
+constexpr int kSplitW1 = 128, kSplitW2 = 64, kSplitW3 = 64;
+
+// split-K slices for an (M x N x K) GEMM whose 64 x 64 tiles alone would not fill 256 CUs
+inline int splits_for(int64_t M, int64_t N, int64_t K)
+{
+    const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
+    int s = 1;
+    while (tiles * s < 512 && K / (2 * s) >= 128 && s < 16) s *= 2;
+    return s;
+}
 
 CnnWs carve(void *base, const CnnLayout &L, int64_t R)
 {
@@ -101,7 +113,6 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
         return q;
     };
     CnnWs w{};
-    w.cols1 = (float *)take(sizeof(float) * L.rows1(R) * L.K1);
     w.a1 = (float *)take(sizeof(float) * L.rows1(R) * L.c1);
     w.cols2 = (float *)take(sizeof(float) * L.rows2(R) * L.K2);
     w.a2 = (float *)take(sizeof(float) * L.rows2(R) * L.c2);
@@ -122,16 +133,19 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks);
     w.dhead_b = (float *)take(sizeof(float) * (L.A + 1));
     {
-        const int64_t wparts = (int64_t)kSplitK * std::max({(int64_t)L.c1 * L.K1, (int64_t)L.c2 * L.K2,
-                                                            (int64_t)L.c3 * L.K3});
+        const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * L.K2,
+                                         (int64_t)kSplitW3 * L.c3 * L.K3});
         const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
-        w.parts = (float *)take(sizeof(float) * std::max(wparts, cparts));
+        const int64_t gparts = std::max({(int64_t)splits_for(R, L.HID, L.F) * R * L.HID,
+                                         (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
+                                         (int64_t)splits_for(L.A + 1, L.HID, R) * (L.A + 1) * L.HID,
+                                         (int64_t)splits_for(L.HID, L.F, R) * L.HID * L.F});
+        w.parts = (float *)take(sizeof(float) * std::max({wparts, cparts, gparts}));
     }
     w.bytes = off;
     return w;
 }
 
-__constant__ float c_u8_to_f32[256];   // u / 255.0f, correctly rounded (the reference's obs / 255.0)
 
 __device__ __forceinline__ int64_t frame_row(const int32_t *idx, int64_t r, int64_t T, int64_t N)
 {
@@ -139,58 +153,6 @@ __device__ __forceinline__ int64_t frame_row(const int32_t *idx, int64_t r, int6
     const int64_t i = idx[r];
     const int64_t env = i / T, t = i - env * T;   // env-major sample index (rollout_buffer.py:11-13)
     return t * N + env;
-}
-
-// ---- conv1 im2col straight from the u8 frame stacks: one thread per (row, c, ky), 8 kx
-__global__ __launch_bounds__(256) void k_im2col1(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
-                                                 int64_t T, int64_t N, int64_t R, CnnLayout L,
-                                                 float *__restrict__ cols)
-{
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int per_row = L.C * L.k1;
-    const int64_t total = L.rows1(R) * per_row;
-    if (t >= total) return;
-    const int64_t m = t / per_row;
-    const int ck = (int)(t - m * per_row);
-    const int c = ck / L.k1, ky = ck - c * L.k1;
-    const int hw = L.h1 * L.w1;
-    const int64_t r = m / hw;
-    const int pos = (int)(m - r * hw);
-    const int oy = pos / L.w1, ox = pos - oy * L.w1;
-    const int64_t src = frame_row(idx, r, T, N);
-    const uint8_t *row = obs + ((src * L.C + c) * L.H + (oy * L.s1 + ky)) * (int64_t)L.W + ox * L.s1;
-    const uint32_t lo = *(const uint32_t *)row, hi = *(const uint32_t *)(row + 4);   // 4-B aligned (s1 = 4)
-    float4 v0, v1;
-    v0.x = c_u8_to_f32[lo & 255], v0.y = c_u8_to_f32[(lo >> 8) & 255];
-    v0.z = c_u8_to_f32[(lo >> 16) & 255], v0.w = c_u8_to_f32[lo >> 24];
-    v1.x = c_u8_to_f32[hi & 255], v1.y = c_u8_to_f32[(hi >> 8) & 255];
-    v1.z = c_u8_to_f32[(hi >> 16) & 255], v1.w = c_u8_to_f32[hi >> 24];
-    float4 *dst = (float4 *)(cols + m * L.K1 + (c * L.k1 + ky) * L.k1);
-    dst[0] = v0;
-    dst[1] = v1;
-}
-
-// ---- NHWC im2col: one thread per (row, ky, kx, c4)
-__global__ __launch_bounds__(256) void k_im2col_nhwc(const float *__restrict__ a, int64_t R, int Hin, int Win,
-                                                     int Cin, int k, int s, int Hout, int Wout,
-                                                     float *__restrict__ cols)
-{
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int c4n = Cin >> 2;
-    const int K = k * k * Cin;
-    const int per_row = k * k * c4n;
-    const int64_t total = R * Hout * Wout * per_row;
-    if (t >= total) return;
-    const int64_t m = t / per_row;
-    const int j = (int)(t - m * per_row);
-    const int kk = j / c4n, c4 = j - kk * c4n;
-    const int ky = kk / k, kx = kk - ky * k;
-    const int hw = Hout * Wout;
-    const int64_t r = m / hw;
-    const int pos = (int)(m - r * hw);
-    const int oy = pos / Wout, ox = pos - oy * Wout;
-    const float4 v = *(const float4 *)(a + ((r * Hin + oy * s + ky) * Win + ox * s + kx) * Cin + c4 * 4);
-    *(float4 *)(cols + m * K + kk * Cin + c4 * 4) = v;
 }
 
 // ---- ReLU-masked col2im (gather form, fixed summation order): dA[r,y,x,c] for stride s
@@ -231,21 +193,6 @@ __global__ __launch_bounds__(256) void k_col2im_relu(const float *__restrict__ d
     o.z = av.z > 0.f ? acc.z : 0.f;
     o.w = av.w > 0.f ? acc.w : 0.f;
     *(float4 *)(dA + e * Cin + c4 * 4) = o;
-}
-
-// ---- y = relu(y + b) over rows x C (C % 4 == 0)
-__global__ __launch_bounds__(256) void k_bias_relu(float *__restrict__ y, const float *__restrict__ b, int64_t rows,
-                                                   int C)
-{
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int c4n = C >> 2;
-    if (t >= rows * c4n) return;
-    const int c4 = (int)(t % c4n);
-    float4 v = ((float4 *)y)[t];
-    const float4 bb = *(const float4 *)(b + c4 * 4);
-    v.x = fmaxf(v.x + bb.x, 0.f), v.y = fmaxf(v.y + bb.y, 0.f);
-    v.z = fmaxf(v.z + bb.z, 0.f), v.w = fmaxf(v.w + bb.w, 0.f);
-    ((float4 *)y)[t] = v;
 }
 
 // ---- d = a > 0 ? d : 0
@@ -676,50 +623,6 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
-std::mutex g_blas_mu;
-std::unordered_map<int, rocblas_handle> g_blas;
-
-int blas_for(hipStream_t s, rocblas_handle *out)
-{
-    int dev = 0;
-    GS_HIP(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(g_blas_mu);
-    auto it = g_blas.find(dev);
-    if (it == g_blas.end()) {
-        rocblas_handle h;
-        if (rocblas_create_handle(&h) != rocblas_status_success) {
-            set_error("rocblas_create_handle failed");
-            return GS_E_HIP;
-        }
-        rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed);   // deterministic reductions
-        rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
-        it = g_blas.emplace(dev, h).first;
-    }
-    if (rocblas_set_stream(it->second, s) != rocblas_status_success) {
-        set_error("rocblas_set_stream failed");
-        return GS_E_HIP;
-    }
-    *out = it->second;
-    return GS_OK;
-}
-
-// Row-major C[M][N] = op(A) op(B) (+ beta C); ta: A stored K x M, tb: B stored N x K.
-int gemm_rm(rocblas_handle hb, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-            const float *B, int64_t ldb, float beta, float *C, int64_t ldc)
-{
-    const float one = 1.0f;
-    const rocblas_status st = rocblas_sgemm(hb, tb ? rocblas_operation_transpose : rocblas_operation_none,
-                                            ta ? rocblas_operation_transpose : rocblas_operation_none,
-                                            (rocblas_int)N, (rocblas_int)M, (rocblas_int)K, &one, B,
-                                            (rocblas_int)ldb, A, (rocblas_int)lda, &beta, C, (rocblas_int)ldc);
-    if (st != rocblas_status_success) {
-        set_error("rocblas_sgemm(%lld x %lld x %lld) failed: %s", (long long)M, (long long)N, (long long)K,
-                  rocblas_status_to_string(st));
-        return GS_E_HIP;
-    }
-    return GS_OK;
-}
-
 inline unsigned nblk(int64_t n);
 
 // bias grad: db[c] = sum over rows of X[rows][C] (two deterministic passes)
@@ -732,47 +635,7 @@ int colsum(const float *X, int64_t rows, int C, float *parts, float *db, hipStre
     return GS_OK;
 }
 
-// weight grad dW[Cout][K] = dY[M][Cout]^T cols[M][K] with M = B * positions: split over kSplitK
-// sample groups as one strided-batched GEMM into partials, then a fixed-order sum
-int wgrad(rocblas_handle hb, const float *dY, const float *cols, int64_t B, int64_t hw, int Cout, int K,
-          float *parts, float *dW, hipStream_t s)
-{
-    const int S = (B % kSplitK == 0) ? kSplitK : 1;
-    const int64_t Mc = B / S * hw;
-    const float one = 1.0f, zero = 0.0f;
-    const rocblas_status st = rocblas_sgemm_strided_batched(
-        hb, rocblas_operation_none, rocblas_operation_transpose, K, Cout, (rocblas_int)Mc, &one, cols, K,
-        (rocblas_stride)(Mc * K), dY, Cout, (rocblas_stride)(Mc * Cout), &zero, S == 1 ? dW : parts, K,
-        (rocblas_stride)((int64_t)Cout * K), S);
-    if (st != rocblas_status_success) {
-        set_error("rocblas_sgemm_strided_batched (wgrad) failed: %s", rocblas_status_to_string(st));
-        return GS_E_HIP;
-    }
-    if (S > 1) {
-        const int64_t n = (int64_t)Cout * K;
-        hipLaunchKernelGGL(k_sum_parts, dim3(nblk(n)), dim3(256), 0, s, parts, S, n, dW);
-        GS_LAUNCH_CHECK("k_sum_parts");
-    }
-    return GS_OK;
-}
-
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
-
-int lut_ready = 0;
-std::mutex g_lut_mu;
-
-int ensure_lut()
-{
-    std::lock_guard<std::mutex> lk(g_lut_mu);
-    int dev = 0;
-    GS_HIP(hipGetDevice(&dev));
-    if (lut_ready & (1 << dev)) return GS_OK;
-    float lut[256];
-    for (int u = 0; u < 256; ++u) lut[u] = (float)u / 255.0f;
-    GS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_u8_to_f32), lut, sizeof(lut)));
-    lut_ready |= 1 << dev;
-    return GS_OK;
-}
 
 int check_cnn(const gs_cnn_dims &d)
 {
@@ -785,68 +648,91 @@ int check_cnn(const gs_cnn_dims &d)
     return GS_OK;
 }
 
+// Convolution geometries of the trunk for R rows
+ConvGeom geom1(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.H, L.W, L.C, L.k1, L.s1, L.h1, L.w1, L.c1}; }
+ConvGeom geom2(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h1, L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, L.c2}; }
+ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.w2, L.c2, L.k3, L.s3, L.h3, L.w3, L.c3}; }
+
 // conv trunk + fc + heads for R rows: obs rows come from the u8 buffer through idx (or 0..R)
-int forward(const float *P, const CnnLayout &L, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
-            int64_t R, const CnnWs &w, rocblas_handle hb, hipStream_t s)
+int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s)
 {
     int rc;
-    const int64_t m1 = L.rows1(R), m2 = L.rows2(R), m3 = L.rows3(R);
-    hipLaunchKernelGGL(k_im2col1, dim3(nblk(m1 * L.C * L.k1)), dim3(256), 0, s, obs, idx, T, N, R, L, w.cols1);
-    GS_LAUNCH_CHECK("k_im2col1");
-    if ((rc = gemm_rm(hb, false, true, m1, L.c1, L.K1, w.cols1, L.K1, P + L.oW1, L.K1, 0.f, w.a1, L.c1))) return rc;
-    hipLaunchKernelGGL(k_bias_relu, dim3(nblk(m1 * L.c1 / 4)), dim3(256), 0, s, w.a1, P + L.ob1, m1, L.c1);
-    GS_LAUNCH_CHECK("k_bias_relu");
-    hipLaunchKernelGGL(k_im2col_nhwc, dim3(nblk(m2 * L.k2 * L.k2 * (L.c1 / 4))), dim3(256), 0, s, w.a1, R, L.h1,
-                       L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, w.cols2);
-    GS_LAUNCH_CHECK("k_im2col_nhwc");
-    if ((rc = gemm_rm(hb, false, true, m2, L.c2, L.K2, w.cols2, L.K2, P + L.oW2, L.K2, 0.f, w.a2, L.c2))) return rc;
-    hipLaunchKernelGGL(k_bias_relu, dim3(nblk(m2 * L.c2 / 4)), dim3(256), 0, s, w.a2, P + L.ob2, m2, L.c2);
-    hipLaunchKernelGGL(k_im2col_nhwc, dim3(nblk(m3 * L.k3 * L.k3 * (L.c2 / 4))), dim3(256), 0, s, w.a2, R, L.h2,
-                       L.w2, L.c2, L.k3, L.s3, L.h3, L.w3, w.cols3);
-    if ((rc = gemm_rm(hb, false, true, m3, L.c3, L.K3, w.cols3, L.K3, P + L.oW3, L.K3, 0.f, w.a3, L.c3))) return rc;
-    hipLaunchKernelGGL(k_bias_relu, dim3(nblk(m3 * L.c3 / 4)), dim3(256), 0, s, w.a3, P + L.ob3, m3, L.c3);
-    if ((rc = gemm_rm(hb, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, 0.f, w.h, L.HID))) return rc;
-    hipLaunchKernelGGL(k_bias_relu, dim3(nblk(R * L.HID / 4)), dim3(256), 0, s, w.h, P + L.obf, R, L.HID);
+    if ((rc = conv_fwd_u8(s, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) return rc;
+    if ((rc = conv_fwd_nhwc(s, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
+    if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) return rc;
+    // fc: h = relu(a3 Wf^T + bf), split-K partials summed with the bias + ReLU epilogue
+    const int sf = splits_for(R, L.HID, L.F);
+    if (sf == 1) {
+        if ((rc = gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf, true)))
+            return rc;
+    } else {
+        if ((rc = gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.parts, L.HID, 0.f, nullptr,
+                           false, sf, R * L.HID)))
+            return rc;
+        if ((rc = sum_parts(s, w.parts, sf, R * L.HID, w.h, P + L.obf, L.HID, true))) return rc;
+    }
     // heads: z[r][0:A] = h Wp^T, z[r][A] = h Wv^T (row stride A+1); biases are added where z is read
-    if ((rc = gemm_rm(hb, false, true, R, L.A, L.HID, w.h, L.HID, P + L.oWp, L.HID, 0.f, w.z, L.A + 1))) return rc;
-    if ((rc = gemm_rm(hb, false, true, R, 1, L.HID, w.h, L.HID, P + L.oWv, L.HID, 0.f, w.z + L.A, L.A + 1)))
-        return rc;
-    return GS_OK;
+    return heads_fwd(s, R, L.HID, L.A, w.h, P + L.oWp, P + L.oWv, w.z, w.parts, splits_for(R, L.A + 1, L.HID));
 }
 
-int backward(const float *P, const CnnLayout &L, int64_t B, const CnnWs &w, float *G, const int32_t *stop,
-             rocblas_handle hb, hipStream_t s)
+int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
+             const int32_t *stop, hipStream_t s)
 {
     int rc;
-    const int64_t m1 = L.rows1(B), m2 = L.rows2(B), m3 = L.rows3(B);
-    // head grads: dWp = dz[:, :A]^T h, dWv = dz[:, A]^T h, biases = column sums of dz
-    if ((rc = gemm_rm(hb, true, false, L.A, L.HID, B, w.dz, L.A + 1, w.h, L.HID, 0.f, G + L.oWp, L.HID))) return rc;
-    if ((rc = gemm_rm(hb, true, false, 1, L.HID, B, w.dz + L.A, L.A + 1, w.h, L.HID, 0.f, G + L.oWv, L.HID)))
-        return rc;
+    const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
+    // head grads: dW[a] = dz[:, a]^T h for a in [0, A] (policy rows, then the value row),
+    // split-K partials summed straight into the two parameter blocks; biases = column sums of dz
+    {
+        const int A1 = L.A + 1;
+        const int sh = splits_for(A1, L.HID, B);
+        const int64_t n = (int64_t)A1 * L.HID;
+        if ((rc = gemm_f32(s, true, false, A1, L.HID, B, w.dz, A1, w.h, L.HID, w.parts, L.HID, 0.f, nullptr, false, sh,
+                           n)))
+            return rc;
+        if ((rc = sum_parts(s, w.parts, sh, (int64_t)L.A * L.HID, G + L.oWp, nullptr, 1, false, n))) return rc;
+        if ((rc = sum_parts(s, w.parts + (int64_t)L.A * L.HID, sh, L.HID, G + L.oWv, nullptr, 1, false, n))) return rc;
+    }
     if ((rc = colsum(w.dz, B, L.A + 1, w.parts, w.dhead_b, s))) return rc;
     hipLaunchKernelGGL(k_scatter_head_bias, dim3(1), dim3(64), 0, s, w.dhead_b, L, G);
     hipLaunchKernelGGL(k_cnn_dh, dim3(nblk(B * L.HID)), dim3(256), 0, s, w.dz, P, L, w.h, B, w.dh, stop);
     // fc
     if ((rc = colsum(w.dh, B, L.HID, w.parts, G + L.obf, s))) return rc;
-    if ((rc = gemm_rm(hb, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, 0.f, G + L.oWf, L.F))) return rc;
-    if ((rc = gemm_rm(hb, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, 0.f, w.da3, L.F))) return rc;
+    {
+        const int sw = splits_for(L.HID, L.F, B);
+        if (sw == 1) {
+            if ((rc = gemm_f32(s, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, 0.f, nullptr,
+                               false)))
+                return rc;
+        } else {
+            if ((rc = gemm_f32(s, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, w.parts, L.F, 0.f, nullptr, false,
+                               sw, (int64_t)L.HID * L.F)))
+                return rc;
+            if ((rc = sum_parts(s, w.parts, sw, (int64_t)L.HID * L.F, G + L.oWf))) return rc;
+        }
+    }
+    if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr, false)))
+        return rc;
     hipLaunchKernelGGL(k_relu_mask, dim3(nblk(B * L.F / 4)), dim3(256), 0, s, w.da3, w.a3, B * L.F / 4);
     // conv3 (dY3 = da3 as [m3][c3])
     if ((rc = colsum(w.da3, m3, L.c3, w.parts, G + L.ob3, s))) return rc;
-    if ((rc = wgrad(hb, w.da3, w.cols3, B, (int64_t)L.h3 * L.w3, L.c3, L.K3, w.parts, G + L.oW3, s))) return rc;
-    if ((rc = gemm_rm(hb, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, 0.f, w.cols3, L.K3))) return rc;
+    if ((rc = conv_wgrad_nhwc(s, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3))) return rc;
+    if ((rc = gemm_f32(s, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, w.cols3, L.K3, 0.f, nullptr,
+                       false)))
+        return rc;
     hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(m2 * (L.c2 / 4))), dim3(256), 0, s, w.cols3, w.a2, B, L.h2, L.w2,
                        L.c2, L.k3, L.s3, L.h3, L.w3, w.da2);
     GS_LAUNCH_CHECK("k_col2im_relu");
     // conv2
     if ((rc = colsum(w.da2, m2, L.c2, w.parts, G + L.ob2, s))) return rc;
-    if ((rc = wgrad(hb, w.da2, w.cols2, B, (int64_t)L.h2 * L.w2, L.c2, L.K2, w.parts, G + L.oW2, s))) return rc;
-    if ((rc = gemm_rm(hb, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, 0.f, w.cols2, L.K2))) return rc;
-    hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(m1 * (L.c1 / 4))), dim3(256), 0, s, w.cols2, w.a1, B, L.h1, L.w1,
-                       L.c1, L.k2, L.s2, L.h2, L.w2, w.da1);
-    // conv1 (no input gradient)
-    if ((rc = colsum(w.da1, m1, L.c1, w.parts, G + L.ob1, s))) return rc;
-    return wgrad(hb, w.da1, w.cols1, B, (int64_t)L.h1 * L.w1, L.c1, L.K1, w.parts, G + L.oW1, s);
+    if ((rc = conv_wgrad_nhwc(s, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2))) return rc;
+    if ((rc = gemm_f32(s, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, w.cols2, L.K2, 0.f, nullptr,
+                       false)))
+        return rc;
+    hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(L.rows1(B) * (L.c1 / 4))), dim3(256), 0, s, w.cols2, w.a1, B, L.h1,
+                       L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, w.da1);
+    // conv1 (no input gradient): patches re-read from the u8 frames
+    if ((rc = colsum(w.da1, L.rows1(B), L.c1, w.parts, G + L.ob1, s))) return rc;
+    return conv_wgrad_u8(s, geom1(L, B), fs, w.da1, w.parts, kSplitW1, G + L.oW1);
 }
 
 AdamArgs adam_args(const gs_ppo_hparams &hp, int64_t t)
@@ -894,17 +780,16 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
              const gs_rollout_view_u8 &ro, const int32_t *idx, int64_t B, int64_t adam_step, float *metrics,
              int32_t *stop, const CnnWs &w, gs_comm *comm, hipStream_t s)
 {
-    rocblas_handle hb;
-    int rc = blas_for(s, &hb);
-    if (rc) return rc;
+    int rc;
+    const FrameSrc fs{ro.obs, idx, ro.T, ro.N};
     hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions, ro.logprobs,
                        ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
     GS_LAUNCH_CHECK("k_gather_fields");
-    if ((rc = forward(P, L, ro.obs, idx, ro.T, ro.N, B, w, hb, s))) return rc;
+    if ((rc = forward(P, L, fs, B, w, s))) return rc;
     hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, P, L, (int)B, w.f_act, w.f_olp, w.f_ov, w.f_adv,
                        w.f_ret, loss_args(hp), w.dz, metrics, stop);
     GS_LAUNCH_CHECK("k_cnn_loss");
-    if ((rc = backward(P, L, B, w, G, stop, hb, s))) return rc;
+    if ((rc = backward(P, L, fs, B, w, G, stop, s))) return rc;
     AdamArgs aa = adam_args(hp, adam_step);
     if (comm) {
         int world = 1;
@@ -947,12 +832,9 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     GS_REQUIRE(mode >= 0 && mode <= 2, "mode %d not in {0,1,2}", mode);
     GS_REQUIRE(actions || mode == 0 || !logp, "actions required for modes 1/2");
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = ensure_lut())) return rc;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, N);
-    rocblas_handle hb;
-    if ((rc = blas_for(s, &hb))) return rc;
-    if ((rc = forward(params, L, obs, nullptr, 1, N, N, w, hb, s))) return rc;
+    if ((rc = forward(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s))) return rc;
     hipLaunchKernelGGL(k_cnn_act, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed, rng_counter, actions,
                        logp, value);
     GS_LAUNCH_CHECK("k_cnn_act");
@@ -967,14 +849,11 @@ extern "C" int gs_cnn_ppo_loss(const float *params, gs_cnn_dims dims, gs_ppo_hpa
     if (rc) return rc;
     GS_REQUIRE(params && idx && metrics, "gs_cnn_ppo_loss: null buffer");
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = ensure_lut())) return rc;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
-    rocblas_handle hb;
-    if ((rc = blas_for(s, &hb))) return rc;
     hipLaunchKernelGGL(k_gather_fields, dim3(nblk(batch)), dim3(256), 0, s, idx, batch, ro.T, ro.N, ro.actions,
                        ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
-    if ((rc = forward(params, L, ro.obs, idx, ro.T, ro.N, batch, w, hb, s))) return rc;
+    if ((rc = forward(params, L, FrameSrc{ro.obs, idx, ro.T, ro.N}, batch, w, s))) return rc;
     hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, params, L, (int)batch, w.f_act, w.f_olp, w.f_ov, w.f_adv,
                        w.f_ret, loss_args(hp), dlogits_out ? dlogits_out : w.dz, metrics, nullptr);
     GS_LAUNCH_CHECK("k_cnn_loss");
@@ -992,7 +871,6 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     GS_REQUIRE(params && grads && adam_m && adam_v && idx && metrics, "gs_cnn_ppo_update: null buffer");
     GS_REQUIRE(ro.T * ro.N < ((int64_t)1 << 31), "rollout larger than 2^31 samples");
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = ensure_lut())) return rc;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
     for (int64_t k = 0; k < n_minibatches; ++k) {

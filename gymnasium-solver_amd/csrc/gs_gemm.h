@@ -1,0 +1,56 @@
+// gs_gemm.h — the fp32 MFMA GEMM engine of the NatureCNN path (gs_gemm.hip).
+//
+// One kernel template serves dense GEMMs and the convolutions as implicit GEMMs: the A and B
+// tiles are produced by operand loaders, so the conv1 patches are read straight from the u8
+// frame stacks of the rollout (through the minibatch index) and the conv2/conv3 patches from
+// the NHWC activations — no im2col matrix ever exists in HBM.
+#pragma once
+
+#include "gs_common.h"
+
+namespace gs {
+
+// Convolution geometry: input R x H x W x C (NHWC, or NCHW u8 frames for conv1), kernel k,
+// stride s, output R x OH x OW x Cout.
+struct ConvGeom {
+    int R, H, W, C, k, s, OH, OW, Cout;
+    int64_t rows() const { return (int64_t)R * OH * OW; }
+    int patch() const { return k * k * C; }
+};
+
+// u8 frame source of conv1: obs[(T*N) rows][C][H][W]; minibatch row r reads rollout row
+// idx[r] (env-major sample index, rollout_buffer.py:11-13) or r itself when idx == nullptr.
+struct FrameSrc {
+    const uint8_t *obs;
+    const int32_t *idx;
+    int64_t T, N;
+};
+
+// Dense row-major GEMM: C[M][N] = op(A) op(B) (+ beta C) (+ bias[n]) (ReLU), with
+// op(A)[m][k] = TA ? A[k*lda + m] : A[m*lda + k], op(B)[k][n] = TB ? B[n*ldb + k] : B[k*ldb + n].
+// splits > 1: K is cut into `splits` slices; slice z writes its partial product to
+// C + z*sC (beta/bias/relu must then be off) — the caller sums them in a fixed order.
+int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+             const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu,
+             int splits = 1, int64_t sC = 0);
+
+// out[r,oy,ox,co] = relu(bias[co] + sum_{c,ky,kx} W[co][c][ky][kx] * frame[c][oy*s+ky][ox*s+kx] / 255)
+int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out);
+// out[r,oy,ox,co] = relu(bias[co] + sum_{ky,kx,c} W[co][ky][kx][c] * in[r, oy*s+ky, ox*s+kx, c])
+int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out);
+// dW[co][patch] = sum over rows of dY[row][co] * patch(row): split over `splits` row slices
+// into parts (splits * Cout * patch floats), then summed in slice order into dW.
+int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
+                  float *dW);
+int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
+                    float *dW);
+// out[i] = (bias/relu epilogue of) sum_{p < np} parts[p*n + i], fixed order; C = row length
+// for the bias index (i % C)
+// (pstride: distance between consecutive partials, default n)
+int sum_parts(hipStream_t s, const float *parts, int np, int64_t n, float *out, const float *bias = nullptr,
+              int C = 1, bool relu = false, int64_t pstride = 0);
+// heads: z[r][a] = h[r] . Wp[a] (a < A), z[r][A] = h[r] . Wv — row stride A+1, no bias
+int heads_fwd(hipStream_t s, int64_t R, int HID, int A, const float *h, const float *Wp, const float *Wv, float *z,
+              float *parts, int splits);
+
+}  // namespace gs

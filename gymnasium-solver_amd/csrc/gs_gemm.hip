@@ -1,19 +1,18 @@
-// gs_gemm.hip — hand-written fp32 GEMM on the CDNA4 matrix cores for the NatureCNN path
-// (conv forward / dgrad / wgrad as GEMMs over im2col matrices, fc, heads).
+// gs_gemm.hip — hand-written fp32 GEMM engine on the CDNA4 matrix cores for the NatureCNN
+// path: dense GEMMs (fc, heads, conv dgrad) and the convolutions as IMPLICIT GEMMs whose
+// operand tiles are gathered on the fly (see gs_gemm.h).
 //
-// Row-major semantics: C[M][N] = op(A) op(B) (+ beta C) (+ bias[n], ReLU), with
-//   op(A)[m][k] = TA ? A[k * lda + m] : A[m * lda + k]
-//   op(B)[k][n] = TB ? B[n * ldb + k] : B[k * ldb + n]
-// and an optional batch (blockIdx.z) with element strides — the deterministic split-K of the
-// weight gradients runs as a batch of K-slices whose partials are summed in a fixed order.
-//
-// Tiling: 256 threads (4 waves of 64) own a BM x BN block tile; each wave a (BM/2) x (BN/2)
-// quarter made of 16 x 16 sub-tiles on v_mfma_f32_16x16x4_f32 (exact fp32 products and
-// sums, like the reference's fp32 torch ops).  K advances 16 at a time through two LDS buffers
-// stored k-major ([BK][BM + 4] / [BK][BN + 4]) so every MFMA operand is one ds_read_b32 per
-// lane; the next K tile's global loads (float4 where the layout is contiguous) are issued
-// before the current tile's MFMAs.
-#include "gs_common.h"
+// Kernel k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K>: 256 threads (4 waves of 64) own a BM x BN
+// block tile, arranged WGM x (4/WGM) waves, each wave a grid of 16 x 16 sub-tiles on
+// v_mfma_f32_16x16x4_f32 (exact fp32 products and sums, like the reference's fp32 torch ops).
+// K advances 16 at a time through two LDS buffers stored k-major ([16][BM + 16] /
+// [16][BN + 16]: the +16 pad puts the four k rows a wave reads at once in disjoint banks), so
+// every MFMA operand is one ds_read_b32 per lane; the next K tile's global loads are issued
+// before the current tile's MFMAs.  Operand loaders return 4 consecutive elements along
+// their contiguous dimension (A_K / B_K: that dimension is k), zero outside the problem.
+// Optional split-K (blockIdx.z = K slice, slices aligned to the 16-deep K tiles) writes
+// partial products that sum_parts() adds in slice order: deterministic reductions.
+#include "gs_gemm.h"
 
 namespace gs {
 namespace {
@@ -25,27 +24,126 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c)
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int BM, int BN, bool TA, bool TB>
-__global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const float *__restrict__ A, int lda,
-                                                  const float *__restrict__ B, int ldb, float *__restrict__ C,
-                                                  int ldc, float beta, const float *__restrict__ bias, int relu,
-                                                  int64_t sA, int64_t sB, int64_t sC, int vecA, int vecB)
+// n / d for 0 <= n < 2^31 by multiply-high (divisors are runtime layer geometry)
+struct FastDiv {
+    uint32_t d, m, s;
+    FastDiv() = default;
+    explicit FastDiv(uint32_t dv) : d(dv), m(0), s(0)
+    {
+        while ((1ull << s) < dv) ++s;
+        m = (uint32_t)((((1ull << 32) * ((1ull << s) - dv)) / dv) + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> s; }
+};
+
+// ---- operand loaders: load4(outer, inner) = elements [outer][inner .. inner+3]
+struct DenseOp {        // p[outer * ld + inner]
+    const float *p;
+    int64_t ld;
+    int n_outer, n_inner, vec;
+    __device__ __forceinline__ float4 load4(int o, int i) const
+    {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (o >= n_outer) return x;
+        const float *r = p + (int64_t)o * ld;
+        if (vec && i + 3 < n_inner) return *reinterpret_cast<const float4 *>(r + i);
+        x.x = i < n_inner ? r[i] : 0.f;
+        x.y = i + 1 < n_inner ? r[i + 1] : 0.f;
+        x.z = i + 2 < n_inner ? r[i + 2] : 0.f;
+        x.w = i + 3 < n_inner ? r[i + 3] : 0.f;
+        return x;
+    }
+};
+
+// rows [0, n_first) from p1, rows [n_first, n_outer) from p2 (the policy and value heads,
+// which are not adjacent in the flat parameter vector); inner contiguous
+struct RowsOp2 {
+    const float *p1, *p2;
+    int64_t ld1, ld2;
+    int n_first, n_outer, n_inner;
+    __device__ __forceinline__ float4 load4(int o, int i) const
+    {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (o >= n_outer) return x;
+        const float *r = o < n_first ? p1 + (int64_t)o * ld1 : p2 + (int64_t)(o - n_first) * ld2;
+        x.x = i < n_inner ? r[i] : 0.f;
+        x.y = i + 1 < n_inner ? r[i + 1] : 0.f;
+        x.z = i + 2 < n_inner ? r[i + 2] : 0.f;
+        x.w = i + 3 < n_inner ? r[i + 3] : 0.f;
+        return x;
+    }
+};
+
+// NHWC patches: outer = output row m = (r, oy, ox), inner = (ky, kx, c); C % 4 == 0
+struct NhwcPatchOp {
+    const float *a;
+    int n_rows, n_patch, H, W, C, s, OW, OHW, KC;
+    FastDiv d_ohw, d_ow, d_kc, d_c;
+    __device__ __forceinline__ float4 load4(int m, int kk) const
+    {
+        if (m >= n_rows || kk >= n_patch) return make_float4(0.f, 0.f, 0.f, 0.f);
+        const uint32_t r = d_ohw.div((uint32_t)m);
+        const int pos = m - (int)r * OHW;
+        const int oy = (int)d_ow.div((uint32_t)pos), ox = pos - oy * OW;
+        const int ky = (int)d_kc.div((uint32_t)kk);
+        const int rem = kk - ky * KC;
+        const int kx = (int)d_c.div((uint32_t)rem), c = rem - kx * C;
+        return *reinterpret_cast<const float4 *>(a + (((int64_t)r * H + oy * s + ky) * W + ox * s + kx) * C + c);
+    }
+};
+
+// conv1 patches straight from the u8 frame stacks: outer = m = (r, oy, ox), inner = (c, ky, kx)
+// (the reference's OIHW weight order); 4 consecutive kx are one aligned u32 (s % 4 == 0,
+// W % 4 == 0, k % 4 == 0), each byte / 255 correctly rounded (the reference's obs / 255.0)
+struct U8PatchOp {
+    const uint8_t *obs;
+    const int32_t *idx;
+    int64_t T, N;
+    int n_rows, n_patch, C, H, W, s, k, OW, OHW, KK;
+    FastDiv d_ohw, d_ow, d_kk, d_k, d_T;
+    __device__ __forceinline__ float4 load4(int m, int kk) const
+    {
+        if (m >= n_rows || kk >= n_patch) return make_float4(0.f, 0.f, 0.f, 0.f);
+        const uint32_t r = d_ohw.div((uint32_t)m);
+        const int pos = m - (int)r * OHW;
+        const int oy = (int)d_ow.div((uint32_t)pos), ox = pos - oy * OW;
+        const int c = (int)d_kk.div((uint32_t)kk);
+        const int rem = kk - c * KK;
+        const int ky = (int)d_k.div((uint32_t)rem), kx = rem - ky * k;
+        int64_t src = r;
+        if (idx) {                       // env-major sample index -> (t, env) row of the (T, N) buffer
+            const uint32_t i = (uint32_t)idx[r];
+            const uint32_t env = d_T.div(i), t = i - env * (uint32_t)T;
+            src = (int64_t)t * N + env;
+        }
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(
+            obs + ((src * C + c) * H + oy * s + ky) * (int64_t)W + ox * s + kx);
+        return make_float4((float)(v & 255u) / 255.0f, (float)((v >> 8) & 255u) / 255.0f,
+                           (float)((v >> 16) & 255u) / 255.0f, (float)(v >> 24) / 255.0f);
+    }
+};
+
+template <int BM, int BN, int WGM, class AOp, bool A_K, class BOp, bool B_K>
+__global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, int K, int kchunk,
+                                              float *__restrict__ C, int ldc, int64_t sC, float beta,
+                                              const float *__restrict__ bias, int relu)
 {
-    constexpr int LA = BM + 4, LB = BN + 4;
-    constexpr int WM = BM / 2, WN = BN / 2;          // per-wave quarter
+    constexpr int WGN = 4 / WGM;
+    constexpr int WM = BM / WGM, WN = BN / WGN;      // per-wave block
     constexpr int TM = WM / 16, TN = WN / 16;        // 16x16 sub-tiles per wave
-    // global -> register staging: the A tile is BM x BK, the B tile BK x BN
-    constexpr int NA4 = BM * BK / 4, NB4 = BK * BN / 4;   // float4 in the A / B tiles
-    constexpr int AV = (NA4 + 255) / 256, BV = (NB4 + 255) / 256;   // per thread
+    constexpr int LA = BM + 16, LB = BN + 16;
+    constexpr int NA4 = BM * BK / 4, NB4 = BK * BN / 4;
+    constexpr int AV = (NA4 + 255) / 256, BV = (NB4 + 255) / 256;
+    static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "bad tile");
     __shared__ float As[2][BK][LA];
     __shared__ float Bs[2][BK][LB];
 
-    A += (int64_t)blockIdx.z * sA;
-    B += (int64_t)blockIdx.z * sB;
+    const int kbeg = blockIdx.z * kchunk;
+    const int kend = min(K, kbeg + kchunk);
     C += (int64_t)blockIdx.z * sC;
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
+    const int wm = (wave / WGN) * WM, wn = (wave % WGN) * WN;
     const int li = lane & 15, lq = lane >> 4;
 
     float4 ra[AV], rb[BV];
@@ -53,89 +151,47 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
 #pragma unroll
         for (int v = 0; v < AV; ++v) {
             const int t = tid + 256 * v;
-            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (t >= NA4) {
-            } else if (!TA) {     // rows m, 4 contiguous k
-                const int m = t / (BK / 4), k4 = t % (BK / 4);
-                const int gm = m0 + m, gk = k0 + 4 * k4;
-                if (vecA && gm < M && gk + 3 < K) x = *reinterpret_cast<const float4 *>(A + (int64_t)gm * lda + gk);
-                else if (gm < M) {
-                    x.x = gk < K ? A[(int64_t)gm * lda + gk] : 0.f;
-                    x.y = gk + 1 < K ? A[(int64_t)gm * lda + gk + 1] : 0.f;
-                    x.z = gk + 2 < K ? A[(int64_t)gm * lda + gk + 2] : 0.f;
-                    x.w = gk + 3 < K ? A[(int64_t)gm * lda + gk + 3] : 0.f;
-                }
-            } else {              // rows k, 4 contiguous m
-                const int k = t / (BM / 4), m4 = t % (BM / 4);
-                const int gk = k0 + k, gm = m0 + 4 * m4;
-                if (vecA && gk < K && gm + 3 < M) x = *reinterpret_cast<const float4 *>(A + (int64_t)gk * lda + gm);
-                else if (gk < K) {
-                    x.x = gm < M ? A[(int64_t)gk * lda + gm] : 0.f;
-                    x.y = gm + 1 < M ? A[(int64_t)gk * lda + gm + 1] : 0.f;
-                    x.z = gm + 2 < M ? A[(int64_t)gk * lda + gm + 2] : 0.f;
-                    x.w = gm + 3 < M ? A[(int64_t)gk * lda + gm + 3] : 0.f;
-                }
+            if (t < NA4) {
+                if (A_K) ra[v] = aop.load4(m0 + t / (BK / 4), k0 + 4 * (t % (BK / 4)));
+                else ra[v] = aop.load4(k0 + t / (BM / 4), m0 + 4 * (t % (BM / 4)));
             }
-            ra[v] = x;
         }
 #pragma unroll
         for (int v = 0; v < BV; ++v) {
             const int t = tid + 256 * v;
-            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (t >= NB4) {
-            } else if (!TB) {     // rows k, 4 contiguous n
-                const int k = t / (BN / 4), n4 = t % (BN / 4);
-                const int gk = k0 + k, gn = n0 + 4 * n4;
-                if (vecB && gk < K && gn + 3 < N) x = *reinterpret_cast<const float4 *>(B + (int64_t)gk * ldb + gn);
-                else if (gk < K) {
-                    x.x = gn < N ? B[(int64_t)gk * ldb + gn] : 0.f;
-                    x.y = gn + 1 < N ? B[(int64_t)gk * ldb + gn + 1] : 0.f;
-                    x.z = gn + 2 < N ? B[(int64_t)gk * ldb + gn + 2] : 0.f;
-                    x.w = gn + 3 < N ? B[(int64_t)gk * ldb + gn + 3] : 0.f;
-                }
-            } else {              // rows n, 4 contiguous k
-                const int n = t / (BK / 4), k4 = t % (BK / 4);
-                const int gn = n0 + n, gk = k0 + 4 * k4;
-                if (vecB && gn < N && gk + 3 < K) x = *reinterpret_cast<const float4 *>(B + (int64_t)gn * ldb + gk);
-                else if (gn < N) {
-                    x.x = gk < K ? B[(int64_t)gn * ldb + gk] : 0.f;
-                    x.y = gk + 1 < K ? B[(int64_t)gn * ldb + gk + 1] : 0.f;
-                    x.z = gk + 2 < K ? B[(int64_t)gn * ldb + gk + 2] : 0.f;
-                    x.w = gk + 3 < K ? B[(int64_t)gn * ldb + gk + 3] : 0.f;
-                }
+            if (t < NB4) {
+                if (B_K) rb[v] = bop.load4(n0 + t / (BK / 4), k0 + 4 * (t % (BK / 4)));
+                else rb[v] = bop.load4(k0 + t / (BN / 4), n0 + 4 * (t % (BN / 4)));
             }
-            rb[v] = x;
         }
     };
     auto store = [&](int buf) {
 #pragma unroll
         for (int v = 0; v < AV; ++v) {
             const int t = tid + 256 * v;
-            if (t >= NA4) {
-            } else if (!TA) {
+            if (t >= NA4) continue;
+            if (A_K) {
                 const int m = t / (BK / 4), k4 = t % (BK / 4);
                 As[buf][4 * k4 + 0][m] = ra[v].x;
                 As[buf][4 * k4 + 1][m] = ra[v].y;
                 As[buf][4 * k4 + 2][m] = ra[v].z;
                 As[buf][4 * k4 + 3][m] = ra[v].w;
             } else {
-                const int k = t / (BM / 4), m4 = t % (BM / 4);
-                *reinterpret_cast<float4 *>(&As[buf][k][4 * m4]) = ra[v];
+                *reinterpret_cast<float4 *>(&As[buf][t / (BM / 4)][4 * (t % (BM / 4))]) = ra[v];
             }
         }
 #pragma unroll
         for (int v = 0; v < BV; ++v) {
             const int t = tid + 256 * v;
-            if (t >= NB4) {
-            } else if (!TB) {
-                const int k = t / (BN / 4), n4 = t % (BN / 4);
-                *reinterpret_cast<float4 *>(&Bs[buf][k][4 * n4]) = rb[v];
-            } else {
+            if (t >= NB4) continue;
+            if (B_K) {
                 const int n = t / (BK / 4), k4 = t % (BK / 4);
                 Bs[buf][4 * k4 + 0][n] = rb[v].x;
                 Bs[buf][4 * k4 + 1][n] = rb[v].y;
                 Bs[buf][4 * k4 + 2][n] = rb[v].z;
                 Bs[buf][4 * k4 + 3][n] = rb[v].w;
+            } else {
+                *reinterpret_cast<float4 *>(&Bs[buf][t / (BN / 4)][4 * (t % (BN / 4))]) = rb[v];
             }
         }
     };
@@ -146,13 +202,15 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = (K + BK - 1) / BK;
-    load(0);
-    store(0);
+    const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    if (nk > 0) {
+        load(kbeg);
+        store(0);
+    }
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) load((kt + 1) * BK);          // next tile in flight during the MFMAs
+        if (kt + 1 < nk) load(kbeg + (kt + 1) * BK);          // next tile in flight during the MFMAs
 #pragma unroll
         for (int k4 = 0; k4 < BK; k4 += 4) {
             float a[TM], b[TN];
@@ -189,38 +247,180 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int M, int N, int K, const flo
         }
 }
 
-template <int BM, int BN>
-int launch_tiles(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-                 const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu,
-                 int batch, int64_t sA, int64_t sB, int64_t sC)
+template <int BM, int BN, int WGM, bool A_K, bool B_K, class AOp, class BOp>
+int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
+           int64_t ldc, int64_t sC, float beta, const float *bias, bool relu)
 {
-    const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)batch);
-    // float4 global loads only where every row start of every batch slice is 16-B aligned
-    const int vecA = lda % 4 == 0 && sA % 4 == 0 && ((uintptr_t)A & 15) == 0;
-    const int vecB = ldb % 4 == 0 && sB % 4 == 0 && ((uintptr_t)B & 15) == 0;
-#define GS_GEMM_LAUNCH(TA_, TB_)                                                                                   \
-    hipLaunchKernelGGL((k_gemm_f32<BM, BN, TA_, TB_>), grid, dim3(256), 0, s, (int)M, (int)N, (int)K, A, (int)lda, \
-                       B, (int)ldb, C, (int)ldc, beta, bias, relu ? 1 : 0, sA, sB, sC, vecA, vecB)
-    if (!ta && !tb) GS_GEMM_LAUNCH(false, false);
-    else if (!ta && tb) GS_GEMM_LAUNCH(false, true);
-    else if (ta && !tb) GS_GEMM_LAUNCH(true, false);
-    else GS_GEMM_LAUNCH(true, true);
-#undef GS_GEMM_LAUNCH
-    GS_LAUNCH_CHECK("k_gemm_f32");
+    const int64_t per = (K + splits - 1) / splits;
+    const int64_t kchunk = (per + BK - 1) / BK * BK;
+    const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
+    hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K>), grid, dim3(256), 0, s, a, b, (int)M, (int)N, (int)K,
+                       (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0);
+    GS_LAUNCH_CHECK("k_gemm");
     return GS_OK;
+}
+
+// tile shape by output shape: skinny N (conv forward: 32 / 64 channels) takes tall tiles,
+// tiny M (weight gradients of 32 / 64 output channels) flat ones
+template <bool A_K, bool B_K, class AOp, class BOp>
+int dispatch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
+             int64_t ldc, int64_t sC, float beta, const float *bias, bool relu)
+{
+    if (N <= 32) return launch<256, 32, 4, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (M <= 32) return launch<32, 128, 1, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (N <= 64) return launch<128, 64, 2, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    const int64_t big_tiles = ((M + 127) / 128) * ((N + 127) / 128) * splits;
+    if (big_tiles >= 512) return launch<128, 128, 2, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    return launch<64, 64, 2, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+}
+
+DenseOp dense(const float *p, int64_t ld, int64_t n_outer, int64_t n_inner)
+{
+    const int vec = ld % 4 == 0 && ((uintptr_t)p & 15) == 0;
+    return DenseOp{p, ld, (int)n_outer, (int)n_inner, vec};
+}
+
+NhwcPatchOp nhwc_patches(const ConvGeom &g, const float *in)
+{
+    NhwcPatchOp o{};
+    o.a = in;
+    o.n_rows = (int)g.rows();
+    o.n_patch = g.patch();
+    o.H = g.H, o.W = g.W, o.C = g.C, o.s = g.s, o.OW = g.OW, o.OHW = g.OH * g.OW, o.KC = g.k * g.C;
+    o.d_ohw = FastDiv((uint32_t)o.OHW);
+    o.d_ow = FastDiv((uint32_t)g.OW);
+    o.d_kc = FastDiv((uint32_t)o.KC);
+    o.d_c = FastDiv((uint32_t)g.C);
+    return o;
+}
+
+U8PatchOp u8_patches(const ConvGeom &g, const FrameSrc &f)
+{
+    U8PatchOp o{};
+    o.obs = f.obs, o.idx = f.idx, o.T = f.T, o.N = f.N;
+    o.n_rows = (int)g.rows();
+    o.n_patch = g.patch();
+    o.C = g.C, o.H = g.H, o.W = g.W, o.s = g.s, o.k = g.k, o.OW = g.OW, o.OHW = g.OH * g.OW, o.KK = g.k * g.k;
+    o.d_ohw = FastDiv((uint32_t)o.OHW);
+    o.d_ow = FastDiv((uint32_t)g.OW);
+    o.d_kk = FastDiv((uint32_t)o.KK);
+    o.d_k = FastDiv((uint32_t)g.k);
+    o.d_T = FastDiv((uint32_t)(f.T > 0 ? f.T : 1));
+    return o;
+}
+
+int check_geom(const ConvGeom &g)
+{
+    GS_REQUIRE(g.R > 0 && g.OH > 0 && g.OW > 0 && g.Cout > 0, "conv: empty geometry");
+    GS_REQUIRE((g.OH - 1) * g.s + g.k <= g.H && (g.OW - 1) * g.s + g.k <= g.W, "conv: output exceeds input");
+    GS_REQUIRE(g.rows() < (1ll << 31) && (int64_t)g.patch() * g.Cout < (1ll << 31), "conv: problem too large");
+    return GS_OK;
+}
+
+__global__ __launch_bounds__(256) void k_sum_parts_ep(const float *__restrict__ parts, int np, int64_t n,
+                                                      int64_t pstride, float *__restrict__ out,
+                                                      const float *__restrict__ bias, int C, int relu)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int p = 0;
+    for (; p + 8 <= np; p += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += parts[(int64_t)(p + j) * pstride + i];
+    }
+    for (; p < np; ++p) a[0] += parts[(int64_t)p * pstride + i];
+    float v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    if (bias) v += bias[i % C];
+    if (relu) v = v > 0.f ? v : 0.f;
+    out[i] = v;
 }
 
 }  // namespace
 
-int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-             const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu, int batch,
-             int64_t sA, int64_t sB, int64_t sC)
+int sum_parts(hipStream_t s, const float *parts, int np, int64_t n, float *out, const float *bias, int C, bool relu,
+              int64_t pstride)
 {
-    GS_REQUIRE(M > 0 && N > 0 && K > 0 && batch > 0, "gemm_f32: empty problem");
+    GS_REQUIRE(np >= 1 && n >= 1 && C >= 1, "sum_parts: bad sizes");
+    if (pstride <= 0) pstride = n;
+    hipLaunchKernelGGL(k_sum_parts_ep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, parts, np, n, pstride, out,
+                       bias, C, relu ? 1 : 0);
+    GS_LAUNCH_CHECK("k_sum_parts_ep");
+    return GS_OK;
+}
+
+int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+             const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu, int splits,
+             int64_t sC)
+{
+    GS_REQUIRE(M > 0 && N > 0 && K > 0 && splits > 0, "gemm_f32: empty problem");
     GS_REQUIRE(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gemm_f32: dimension too large");
-    // skinny N (conv forward: 32 / 64 output channels) takes tall tiles, the rest 64 x 64
-    if (N <= 32) return launch_tiles<128, 32>(s, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, beta, bias, relu, batch, sA, sB, sC);
-    return launch_tiles<64, 64>(s, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, beta, bias, relu, batch, sA, sB, sC);
+    GS_REQUIRE(splits == 1 || (beta == 0.0f && !bias && !relu), "gemm_f32: split-K partials take no epilogue");
+    const DenseOp a = ta ? dense(A, lda, K, M) : dense(A, lda, M, K);
+    const DenseOp b = tb ? dense(B, ldb, N, K) : dense(B, ldb, K, N);
+    if (!ta && !tb) return dispatch<true, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (!ta && tb) return dispatch<true, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (ta && !tb) return dispatch<false, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    return dispatch<false, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+}
+
+int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out)
+{
+    int rc = check_geom(g);
+    if (rc) return rc;
+    GS_REQUIRE(g.k % 4 == 0 && g.s % 4 == 0 && g.W % 4 == 0, "conv_fwd_u8: needs k, s, W multiples of 4");
+    const int64_t M = g.rows(), K = g.patch();
+    return dispatch<true, true>(s, u8_patches(g, f), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0, 0.0f,
+                                bias, true);
+}
+
+int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out)
+{
+    int rc = check_geom(g);
+    if (rc) return rc;
+    GS_REQUIRE(g.C % 4 == 0 && ((uintptr_t)in & 15) == 0, "conv_fwd_nhwc: channels must be float4-aligned");
+    const int64_t M = g.rows(), K = g.patch();
+    return dispatch<true, true>(s, nhwc_patches(g, in), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0,
+                                0.0f, bias, true);
+}
+
+int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
+                  float *dW)
+{
+    int rc = check_geom(g);
+    if (rc) return rc;
+    GS_REQUIRE(g.k % 4 == 0 && g.s % 4 == 0 && g.W % 4 == 0, "conv_wgrad_u8: needs k, s, W multiples of 4");
+    const int64_t rows = g.rows(), P = g.patch(), n = (int64_t)g.Cout * P;
+    // dW (Cout x P) = dY^T (Cout x rows) . patches (rows x P): A stored [rows][Cout], B = patches
+    rc = dispatch<false, false>(s, dense(dY, g.Cout, rows, g.Cout), u8_patches(g, f), g.Cout, P, rows, splits,
+                                splits == 1 ? dW : parts, P, n, 0.0f, nullptr, false);
+    if (rc || splits == 1) return rc;
+    return sum_parts(s, parts, splits, n, dW);
+}
+
+int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
+                    float *dW)
+{
+    int rc = check_geom(g);
+    if (rc) return rc;
+    GS_REQUIRE(g.C % 4 == 0 && ((uintptr_t)in & 15) == 0, "conv_wgrad_nhwc: channels must be float4-aligned");
+    const int64_t rows = g.rows(), P = g.patch(), n = (int64_t)g.Cout * P;
+    rc = dispatch<false, false>(s, dense(dY, g.Cout, rows, g.Cout), nhwc_patches(g, in), g.Cout, P, rows, splits,
+                                splits == 1 ? dW : parts, P, n, 0.0f, nullptr, false);
+    if (rc || splits == 1) return rc;
+    return sum_parts(s, parts, splits, n, dW);
+}
+
+int heads_fwd(hipStream_t s, int64_t R, int HID, int A, const float *h, const float *Wp, const float *Wv, float *z,
+              float *parts, int splits)
+{
+    GS_REQUIRE(R > 0 && HID > 0 && A > 0 && splits >= 1, "heads_fwd: bad sizes");
+    const RowsOp2 b{Wp, Wv, HID, HID, A, A + 1, HID};
+    const int64_t n = R * (A + 1);
+    int rc = dispatch<true, true>(s, dense(h, HID, R, HID), b, R, A + 1, HID, splits, splits == 1 ? z : parts, A + 1,
+                                  n, 0.0f, nullptr, false);
+    if (rc || splits == 1) return rc;
+    return sum_parts(s, parts, splits, n, z);
 }
 
 }  // namespace gs
@@ -231,5 +431,5 @@ extern "C" int gs_gemm_f32(int ta, int tb, int64_t M, int64_t N, int64_t K, cons
 {
     GS_REQUIRE(A && B && C, "gs_gemm_f32: null operand");
     return gs::gemm_f32((hipStream_t)stream, ta != 0, tb != 0, M, N, K, A, lda, B, ldb, C, ldc, beta, bias,
-                        relu != 0, 1, 0, 0, 0);
+                        relu != 0);
 }
