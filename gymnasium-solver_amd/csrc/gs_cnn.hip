@@ -25,6 +25,7 @@
 #include <unordered_map>
 
 #include "gs_comm_internal.h"
+#include "gs_conv.h"
 #include "gs_gemm.h"
 
 namespace gs {
@@ -83,6 +84,7 @@ struct CnnWs {
     int32_t *f_act;
     float *f_olp, *f_ov, *f_adv, *f_ret;
     double *norm_part;
+    double *loss_part;     // kSums per loss row block
     float *dhead_b;        // column sums of dz (A policy biases + value bias)
     float *parts;          // split-K weight-gradient partials / bias column-sum partials
     size_t bytes;
@@ -131,10 +133,12 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks);
+    w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + 255) / 256));
     w.dhead_b = (float *)take(sizeof(float) * (L.A + 1));
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * L.K2,
-                                         (int64_t)kSplitW3 * L.c3 * L.K3});
+                                         (int64_t)kSplitW3 * L.c3 * L.K3,
+                                         (int64_t)kConv1WgradWG * (L.c1 * L.K1 + L.c1)});
         const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
         const int64_t gparts = std::max({(int64_t)splits_for(R, L.HID, L.F) * R * L.HID,
                                          (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
@@ -396,6 +400,8 @@ __device__ __forceinline__ void wg_reduce(T (&v)[NV], T *scratch)
 }
 
 constexpr int kSums = 13;
+constexpr int kLossRows = 256;   // loss rows per workgroup (one per thread)
+static_assert(kSums == 13, "carve() sizes loss_part for 13 sums");
 
 // ---- the PPO loss of one minibatch with (Masked)Categorical heads; one workgroup.
 __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
@@ -403,18 +409,11 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
                                                   const int32_t *__restrict__ f_act, const float *__restrict__ f_olp,
                                                   const float *__restrict__ f_ov, const float *__restrict__ f_adv,
                                                   const float *__restrict__ f_ret, LossArgs la, float *__restrict__ dz,
-                                                  float *__restrict__ metrics, int32_t *__restrict__ stop)
+                                                  double *__restrict__ part, const int32_t *__restrict__ stop)
 {
     __shared__ double sred[kSums * 256 + kSums * 16];
     const int tid = threadIdx.x;
-    if (stop && *stop) {
-        if (tid == 0) {
-            for (int k = 0; k < GS_NUM_METRICS; ++k) metrics[k] = 0.0f;
-            metrics[GS_M_SKIPPED] = 1.0f;
-            metrics[GS_M_KL_STOP] = 1.0f;
-        }
-        return;
-    }
+    if (stop && *stop) return;
     const int A = L.A, A1 = A + 1;
     const bool masked = L.valid != 0u;
     const float invB = 1.0f / (float)B;
@@ -436,7 +435,8 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
     double acc[kSums];
 #pragma unroll
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
-    for (int r = tid; r < B; r += 256) {
+    const int r_end = min(B, (int)(blockIdx.x + 1) * kLossRows);
+    for (int r = blockIdx.x * kLossRows + tid; r < r_end; r += 256) {
         float zr[kAMax + 1];
         for (int a = 0; a < A1; ++a) zr[a] = z[(int64_t)r * A1 + a] + (a < A ? P[L.obp + a] : P[L.obv]);
         const int act = f_act[r];
@@ -516,7 +516,28 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
         dzr[A] = (gv * hu) * (2.0f * du) + (gv * hc) * (2.0f * dc) * invc;
     }
     wg_reduce<kSums>(acc, sred);
-    if (tid == 0) {
+    if (tid == 0)
+        for (int q = 0; q < kSums; ++q) part[(int64_t)blockIdx.x * kSums + q] = acc[q];
+}
+
+// ---- loss metrics from the row-block partial sums (summed in block order) + KL early stop
+__global__ void k_cnn_loss_final(const double *__restrict__ part, int nb, int B, LossArgs la,
+                                 float *__restrict__ metrics, int32_t *__restrict__ stop)
+{
+    if (threadIdx.x != 0) return;
+    if (stop && *stop) {
+        for (int k = 0; k < GS_NUM_METRICS; ++k) metrics[k] = 0.0f;
+        metrics[GS_M_SKIPPED] = 1.0f;
+        metrics[GS_M_KL_STOP] = 1.0f;
+        return;
+    }
+    double acc[kSums];
+    for (int q = 0; q < kSums; ++q) {
+        double v = 0.0;
+        for (int b = 0; b < nb; ++b) v += part[(int64_t)b * kSums + q];
+        acc[q] = v;
+    }
+    {
         const double *t = acc;
         const double Bd = (double)B;
         const float pl = (float)(-t[0] / Bd);
@@ -657,7 +678,11 @@ ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.
 int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s)
 {
     int rc;
-    if ((rc = conv_fwd_u8(s, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) return rc;
+    if (conv1_lds_supported(L.C, L.H, L.W)) {
+        if ((rc = conv1_lds_fwd(s, (int)R, fs.obs, fs.idx, fs.T, fs.N, P + L.oW1, P + L.ob1, w.a1))) return rc;
+    } else if ((rc = conv_fwd_u8(s, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) {
+        return rc;
+    }
     if ((rc = conv_fwd_nhwc(s, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
     if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) return rc;
     // fc: h = relu(a3 Wf^T + bf), split-K partials summed with the bias + ReLU epilogue
@@ -731,6 +756,8 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
     hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(L.rows1(B) * (L.c1 / 4))), dim3(256), 0, s, w.cols2, w.a1, B, L.h1,
                        L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, w.da1);
     // conv1 (no input gradient): patches re-read from the u8 frames
+    if (conv1_lds_supported(L.C, L.H, L.W))
+        return conv1_lds_wgrad(s, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1);
     if ((rc = colsum(w.da1, L.rows1(B), L.c1, w.parts, G + L.ob1, s))) return rc;
     return conv_wgrad_u8(s, geom1(L, B), fs, w.da1, w.parts, kSplitW1, G + L.oW1);
 }
@@ -764,6 +791,18 @@ LossArgs loss_args(const gs_ppo_hparams &hp)
     return la;
 }
 
+// row-parallel masked-categorical PPO loss (dlogits into dz) + one metrics/KL-stop block
+int launch_cnn_loss(const float *z, const float *P, const CnnLayout &L, int64_t B, const CnnWs &w, const LossArgs &la,
+                    float *dz, float *metrics, int32_t *stop, hipStream_t s)
+{
+    const int nb = (int)((B + kLossRows - 1) / kLossRows);
+    hipLaunchKernelGGL(k_cnn_loss, dim3((unsigned)nb), dim3(256), 0, s, z, P, L, (int)B, w.f_act, w.f_olp, w.f_ov,
+                       w.f_adv, w.f_ret, la, dz, w.loss_part, stop);
+    hipLaunchKernelGGL(k_cnn_loss_final, dim3(1), dim3(64), 0, s, w.loss_part, nb, (int)B, la, metrics, stop);
+    GS_LAUNCH_CHECK("k_cnn_loss");
+    return GS_OK;
+}
+
 int validate_cnn_update(const gs_cnn_dims &dims, const gs_rollout_view_u8 &ro, int64_t B, const void *ws)
 {
     int rc = check_cnn(dims);
@@ -786,9 +825,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
                        ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
     GS_LAUNCH_CHECK("k_gather_fields");
     if ((rc = forward(P, L, fs, B, w, s))) return rc;
-    hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, P, L, (int)B, w.f_act, w.f_olp, w.f_ov, w.f_adv,
-                       w.f_ret, loss_args(hp), w.dz, metrics, stop);
-    GS_LAUNCH_CHECK("k_cnn_loss");
+    if ((rc = launch_cnn_loss(w.z, P, L, B, w, loss_args(hp), w.dz, metrics, stop, s))) return rc;
     if ((rc = backward(P, L, fs, B, w, G, stop, s))) return rc;
     AdamArgs aa = adam_args(hp, adam_step);
     if (comm) {
@@ -854,9 +891,9 @@ extern "C" int gs_cnn_ppo_loss(const float *params, gs_cnn_dims dims, gs_ppo_hpa
     hipLaunchKernelGGL(k_gather_fields, dim3(nblk(batch)), dim3(256), 0, s, idx, batch, ro.T, ro.N, ro.actions,
                        ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
     if ((rc = forward(params, L, FrameSrc{ro.obs, idx, ro.T, ro.N}, batch, w, s))) return rc;
-    hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(256), 0, s, w.z, params, L, (int)batch, w.f_act, w.f_olp, w.f_ov, w.f_adv,
-                       w.f_ret, loss_args(hp), dlogits_out ? dlogits_out : w.dz, metrics, nullptr);
-    GS_LAUNCH_CHECK("k_cnn_loss");
+    if ((rc = launch_cnn_loss(w.z, params, L, batch, w, loss_args(hp), dlogits_out ? dlogits_out : w.dz, metrics,
+                              nullptr, s)))
+        return rc;
     return GS_OK;
 }
 

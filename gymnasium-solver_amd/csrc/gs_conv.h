@@ -1,0 +1,19 @@
+// gs_conv.h — LDS-resident NatureCNN conv1 kernels (gs_conv.hip) for 4 x 84 x 84 u8 stacks.
+#pragma once
+
+#include "gs_common.h"
+
+namespace gs {
+
+constexpr int kConv1WgradWG = 256;     // workgroups (= partials) of the conv1 weight gradient
+
+bool conv1_lds_supported(int C, int H, int W);
+// out[r][oy][ox][co] = relu(b1[co] + sum W1[co][c][ky][kx] * frame(r)[c][4 oy + ky][4 ox + kx] / 255)
+int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N, const float *W1,
+                  const float *b1, float *out);
+// dW1 = sum_rows dA1^T . patches, db1 = column sums of dA1; parts: kConv1WgradWG x (32*256 + 32) floats
+int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
+                    const float *dA, float *parts, float *dW1, float *db1);
+int conv1_lds_wgrad_parts();
+
+}  // namespace gs

@@ -1,0 +1,321 @@
+// gs_conv.hip — NatureCNN conv1 (4 x 84 x 84 u8 frame stacks -> 20 x 20 x 32, kernel 8,
+// stride 4) as LDS-resident per-sample MFMA kernels.
+//
+// conv1 is the largest layer (3.3 M MAC per sample, 26 % of the network) and the only one
+// whose input is the u8 rollout buffer.  Instead of a GEMM over an im2col matrix (419 MB of
+// fp32 patches per B = 1024 minibatch), a workgroup stages one half of a sample's frame stack
+// (4 x 44 rows x 84 px, the receptive field of 10 output rows) into LDS as fp32 (x / 255,
+// correctly rounded, once per pixel), and the MFMA operands are read from that tile:
+//
+//   k_conv1_fwd   one workgroup per (sample, half): 200 positions x 32 filters x 256 taps on
+//                 v_mfma_f32_16x16x4_f32.  The filters live in registers (each lane holds the
+//                 64 taps it multiplies); the patch operand is one ds_read_b128 per 4 MFMAs
+//                 (a lane's 4 consecutive taps are 4 consecutive pixels).  Bias + ReLU in the
+//                 epilogue, NHWC fp32 output.
+//   k_conv1_wgrad 256 workgroups, each walking a fixed set of (sample, half) bands: dW1 (32 x
+//                 256) += dA1^T . patches with dA1 staged in LDS next to the frame tile, and
+//                 db1 from the same dA1 tile; one partial per workgroup, summed in workgroup
+//                 order by k_sum_partials (deterministic).
+// Frame rows come through the minibatch index exactly like the generic loader (env-major
+// sample index -> (t, env) row of the (T, N) rollout buffer).
+#include "gs_conv.h"
+
+namespace gs {
+namespace {
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int C_, int H_, int W_>
+struct C1 {
+    static constexpr int C = C_, H = H_, W = W_;
+    static constexpr int K = 8, S = 4, CO = 32;
+    static constexpr int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+    static constexpr int BOH = (OH + 1) / 2;              // output rows per band (2 bands per sample)
+    static constexpr int BIR = (BOH - 1) * S + K;         // input rows per band
+    static constexpr int BP = BOH * OW;                   // positions per (full) band
+    static constexpr int MT = (BP + 15) / 16;             // 16-position MFMA tiles per band
+    static constexpr int KK = C * K * K;                  // taps
+    static constexpr int KS = KK / 4;                     // MFMA k-steps
+    static constexpr int W4 = W / 4;
+    static constexpr int FRAME = C * BIR * W;             // floats of the staged band
+    static_assert(W % 4 == 0 && C == 4 && KK == 256, "conv1 kernels are written for 4-frame stacks");
+};
+
+__device__ __forceinline__ int64_t frame_src(const int32_t *idx, int64_t r, int64_t T, int64_t N)
+{
+    if (!idx) return r;
+    const int64_t i = idx[r];
+    const int64_t env = i / T, t = i - env * T;
+    return t * N + env;
+}
+
+// stage frame rows [y0, y0 + BIR) of sample r as fp32 [C][BIR][W] (rows past H are zero):
+// every thread issues all of its u32 loads before converting any (one memory latency)
+template <class G>
+__device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict__ obs, int64_t src, int y0)
+{
+    constexpr int NE = G::C * G::BIR * G::W4, PER = (NE + 255) / 256;
+    const uint8_t *base = obs + src * (int64_t)(G::C * G::H * G::W);
+    uint32_t v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int e = threadIdx.x + 256 * j;
+        const int c = e / (G::BIR * G::W4);
+        const int rem = e - c * (G::BIR * G::W4);
+        const int y = rem / G::W4, x4 = rem - y * G::W4;
+        v[j] = (e < NE && y0 + y < G::H)
+                   ? *reinterpret_cast<const uint32_t *>(base + ((int64_t)c * G::H + y0 + y) * G::W + 4 * x4)
+                   : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int e = threadIdx.x + 256 * j;
+        if (e < NE) {
+            const int c = e / (G::BIR * G::W4);
+            const int rem = e - c * (G::BIR * G::W4);
+            const int y = rem / G::W4, x4 = rem - y * G::W4;
+            const float4 f = make_float4((float)(v[j] & 255u) / 255.0f, (float)((v[j] >> 8) & 255u) / 255.0f,
+                                         (float)((v[j] >> 16) & 255u) / 255.0f, (float)(v[j] >> 24) / 255.0f);
+            *reinterpret_cast<float4 *>(fr + (c * G::BIR + y) * G::W + 4 * x4) = f;
+        }
+    }
+}
+
+// tap order of MFMA k-step s = 4g + j for lane quarter q: channel g / 4, row ky = 2 (g % 4) + q / 2,
+// column kx = 4 (q % 2) + j — a lane's 4 steps of a group are 4 adjacent pixels
+template <class G>
+__global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
+                                                   int64_t T, int64_t N, const float *__restrict__ W1,
+                                                   const float *__restrict__ b1, float *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) float fr[G::FRAME];
+    const int r = blockIdx.x >> 1, band = blockIdx.x & 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lq = lane >> 4;
+    const int oy0 = band * G::BOH;
+    const int rows = min(G::BOH, G::OH - oy0);
+    const int P = rows * G::OW;
+
+    // filters -> registers: b[g][nt] = W1[nt*16 + li][taps of group g for this lane quarter]
+    float4 b[G::KS / 4][2];
+#pragma unroll
+    for (int g = 0; g < G::KS / 4; ++g) {
+        const int c = g >> 2, ky = 2 * (g & 3) + (lq >> 1), kx0 = 4 * (lq & 1);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+            b[g][nt] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
+    }
+    stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S);
+    __syncthreads();
+
+    // m-tiles of this wave: wave, wave + 4, ... (13 tiles at 84 x 84: 4, 3, 3, 3)
+    constexpr int TMW = (G::MT + 3) / 4;
+    int abase[TMW];
+#pragma unroll
+    for (int t = 0; t < TMW; ++t) {
+        const int p = (wave + 4 * t) * 16 + li;
+        const int pc = p < P ? p : 0;
+        const int oy = pc / G::OW, ox = pc - oy * G::OW;
+        abase[t] = (oy * G::S + (lq >> 1)) * G::W + ox * G::S + 4 * (lq & 1);
+    }
+    f32x4 acc[TMW][2];
+#pragma unroll
+    for (int t = 0; t < TMW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < G::KS / 4; ++g) {
+        const int goff = ((g >> 2) * G::BIR + 2 * (g & 3)) * G::W;
+#pragma unroll
+        for (int t = 0; t < TMW; ++t) {
+            if (wave + 4 * t >= G::MT) break;
+            const float4 a = *reinterpret_cast<const float4 *>(fr + abase[t] + goff);
+            acc[t][0] = mfma(a.x, b[g][0].x, acc[t][0]);
+            acc[t][1] = mfma(a.x, b[g][1].x, acc[t][1]);
+            acc[t][0] = mfma(a.y, b[g][0].y, acc[t][0]);
+            acc[t][1] = mfma(a.y, b[g][1].y, acc[t][1]);
+            acc[t][0] = mfma(a.z, b[g][0].z, acc[t][0]);
+            acc[t][1] = mfma(a.z, b[g][1].z, acc[t][1]);
+            acc[t][0] = mfma(a.w, b[g][0].w, acc[t][0]);
+            acc[t][1] = mfma(a.w, b[g][1].w, acc[t][1]);
+        }
+    }
+    // epilogue: D row = lq * 4 + j (position), col = li (filter)
+    float *o = out + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
+#pragma unroll
+    for (int t = 0; t < TMW; ++t) {
+        if (wave + 4 * t >= G::MT) break;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const int co = nt * 16 + li;
+            const float bb = b1[co];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int p = (wave + 4 * t) * 16 + lq * 4 + j;
+                if (p < P) {
+                    const float v = acc[t][nt][j] + bb;
+                    o[(int64_t)p * G::CO + co] = v > 0.f ? v : 0.f;
+                }
+            }
+        }
+    }
+}
+
+// dW1[co][tap] and db1[co] partials of one workgroup over bands blockIdx.x, + gridDim.x, ...
+// parts layout: [workgroup][CO * KK + CO]
+template <class G>
+__global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
+                                                     int64_t T, int64_t N, int R, const float *__restrict__ dA,
+                                                     float *__restrict__ parts)
+{
+    constexpr int DS = 48;                      // dA row stride (floats): kq rows land 16 banks apart
+    constexpr int BPP = (G::BP + 3) / 4 * 4;    // positions padded to whole k-steps
+    __shared__ __attribute__((aligned(16))) float fr[G::FRAME];
+    __shared__ __attribute__((aligned(16))) float da[BPP * DS];
+    __shared__ float dbred[8][G::CO];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lq = lane >> 4;
+    // wave w owns taps [64 w, 64 w + 64): 4 n-tiles; both 16-filter m-tiles
+    int boff[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int tap = wave * 64 + nt * 16 + li;
+        const int c = tap / (G::K * G::K), rem = tap - c * (G::K * G::K);
+        const int ky = rem / G::K, kx = rem - ky * G::K;
+        boff[nt] = (c * G::BIR + ky) * G::W + kx;
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float db = 0.f;                              // thread (co = tid % 32, group tid / 32)
+
+    for (int bnd = blockIdx.x; bnd < 2 * R; bnd += gridDim.x) {
+        const int r = bnd >> 1, band = bnd & 1;
+        const int oy0 = band * G::BOH;
+        const int rows = min(G::BOH, G::OH - oy0);
+        const int P = rows * G::OW;
+        __syncthreads();                         // previous band's readers are done
+        stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S);
+        const float *src = dA + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
+        {
+            constexpr int NE = BPP * (G::CO / 4), PER = (NE + 255) / 256;
+            float4 v[PER];
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int e = tid + 256 * j;
+                const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
+                v[j] = (e < NE && p < P) ? *reinterpret_cast<const float4 *>(src + (int64_t)p * G::CO + 4 * c4)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int e = tid + 256 * j;
+                const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
+                if (e < NE) *reinterpret_cast<float4 *>(da + p * DS + 4 * c4) = v[j];
+            }
+        }
+        __syncthreads();
+        // bias partial: thread (co, grp) sums positions grp, grp + 8, ... in order
+        {
+            const int co = tid & 31, grp = tid >> 5;
+            for (int p = grp; p < P; p += 8) db += da[p * DS + co];
+        }
+        for (int s = 0; s < BPP / 4; ++s) {
+            const int p = 4 * s + lq;                         // this lane's position of the k-step
+            const int oy = p / G::OW, ox = p - oy * G::OW;
+            const int pof = (oy * G::S) * G::W + ox * G::S;
+            const float a0 = da[p * DS + li], a1 = da[p * DS + 16 + li];
+            float bv[4];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) bv[nt] = p < P ? fr[pof + boff[nt]] : 0.f;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                acc[0][nt] = mfma(a0, bv[nt], acc[0][nt]);
+                acc[1][nt] = mfma(a1, bv[nt], acc[1][nt]);
+            }
+        }
+    }
+    // partial out: D row = lq * 4 + j (filter within the m-tile), col = li (tap within the n-tile)
+    float *o = parts + (int64_t)blockIdx.x * (G::CO * G::KK + G::CO);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                o[(mt * 16 + lq * 4 + j) * G::KK + wave * 64 + nt * 16 + li] = acc[mt][nt][j];
+    dbred[tid >> 5][tid & 31] = db;
+    __syncthreads();
+    if (tid < G::CO) {
+        float t = 0.f;
+        for (int g = 0; g < 8; ++g) t += dbred[g][tid];
+        o[G::CO * G::KK + tid] = t;
+    }
+}
+
+// out[i] = sum over partials p of parts[p * stride + i] in order p = 0, 1, ... (four
+// interleaved chains per output, combined in a fixed tree): 64 outputs per workgroup
+__global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ parts, int np, int64_t stride, int n,
+                                                      float *__restrict__ out)
+{
+    __shared__ float red[4][64];
+    const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + j;
+    float a = 0.f;
+    if (i < n) {
+        int p = g;
+        for (; p + 28 < np; p += 32) {           // 8 loads in flight, added in order
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = parts[(int64_t)(p + 4 * u) * stride + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; p < np; p += 4) a += parts[(int64_t)p * stride + i];
+    }
+    red[g][j] = a;
+    __syncthreads();
+    if (g == 0 && i < n) out[i] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
+}
+
+using C1_84 = C1<4, 84, 84>;
+
+}  // namespace
+
+bool conv1_lds_supported(int C, int H, int W) { return C == 4 && H == 84 && W == 84; }
+
+int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N, const float *W1,
+                  const float *b1, float *out)
+{
+    GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
+    hipLaunchKernelGGL(k_conv1_fwd<C1_84>, dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1, out);
+    GS_LAUNCH_CHECK("k_conv1_fwd");
+    return GS_OK;
+}
+
+int conv1_lds_wgrad_parts() { return kConv1WgradWG; }
+
+int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
+                    const float *dA, float *parts, float *dW1, float *db1)
+{
+    GS_REQUIRE(R > 0 && obs && dA && parts && dW1 && db1, "conv1_lds_wgrad: bad argument");
+    constexpr int n = C1_84::CO * C1_84::KK, stride = n + C1_84::CO;
+    hipLaunchKernelGGL(k_conv1_wgrad<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
+    GS_LAUNCH_CHECK("k_conv1_wgrad");
+    if (db1 == dW1 + n) {      // the flat layout keeps conv1's bias right after its weight: one sum
+        hipLaunchKernelGGL(k_sum_partials, dim3((stride + 63) / 64), dim3(256), 0, s, parts, kConv1WgradWG,
+                           (int64_t)stride, stride, dW1);
+    } else {
+        hipLaunchKernelGGL(k_sum_partials, dim3((n + 63) / 64), dim3(256), 0, s, parts, kConv1WgradWG,
+                           (int64_t)stride, n, dW1);
+        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, parts + n, kConv1WgradWG, (int64_t)stride,
+                           C1_84::CO, db1);
+    }
+    GS_LAUNCH_CHECK("k_sum_partials");
+    return GS_OK;
+}
+
+}  // namespace gs
