@@ -3,12 +3,12 @@
 // operand tiles are gathered on the fly (see gs_gemm.h).
 //
 // Kernel k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K>: 256 threads (4 waves of 64) own a BM x BN
-// block tile, arranged WGM x (4/WGM) waves, each wave a grid of 16 x 16 sub-tiles on
-// v_mfma_f32_16x16x4_f32 (exact fp32 products and sums, like the reference's fp32 torch ops).
-// K advances 16 at a time through two LDS buffers stored k-major ([16][BM + 16] /
-// [16][BN + 16]: the +16 pad puts the four k rows a wave reads at once in disjoint banks), so
-// every MFMA operand is one ds_read_b32 per lane; the next K tile's global loads are issued
-// before the current tile's MFMAs.  Operand loaders return 4 consecutive elements along
+// block tile, arranged WGM x (4/WGM) waves, each wave a grid of 32 x 32 sub-tiles on
+// v_mfma_f32_32x32x2_f32 (exact fp32 products and sums, like the reference's fp32 torch ops;
+// half the operand reads per FLOP of the 16x16x4 form).  K advances 16 at a time through two
+// LDS buffers stored k-major, so every MFMA operand is one ds_read_b32 per lane and a half-wave
+// reads 32 consecutive floats of one k row (conflict-free); the next K tile's global loads are
+// issued before the current tile's MFMAs.  Operand loaders return 4 consecutive elements along
 // their contiguous dimension (A_K / B_K: that dimension is k), zero outside the problem.
 // Optional split-K (blockIdx.z = K slice, slices aligned to the 16-deep K tiles) writes
 // partial products that sum_parts() adds in slice order: deterministic reductions.
@@ -19,9 +19,11 @@ namespace {
 
 constexpr int BK = 16;
 
-__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c)
 {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
 // n / d for 0 <= n < 2^31 by multiply-high (divisors are runtime layer geometry)
@@ -130,11 +132,13 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
 {
     constexpr int WGN = 4 / WGM;
     constexpr int WM = BM / WGM, WN = BN / WGN;      // per-wave block
-    constexpr int TM = WM / 16, TN = WN / 16;        // 16x16 sub-tiles per wave
-    constexpr int LA = BM + 16, LB = BN + 16;
+    constexpr int TM = WM / 32, TN = WN / 32;        // 32x32 sub-tiles per wave
+    // k-major LDS rows; a transposing (scalar) store pads by 2 so the four k rows one
+    // ds_write_b32 lane group touches sit 8 banks apart, a float4 store by 4 (alignment)
+    constexpr int LA = A_K ? BM + 2 : BM + 4, LB = B_K ? BN + 2 : BN + 4;
     constexpr int NA4 = BM * BK / 4, NB4 = BK * BN / 4;
     constexpr int AV = (NA4 + 255) / 256, BV = (NB4 + 255) / 256;
-    static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "bad tile");
+    static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "bad tile");
     __shared__ float As[2][BK][LA];
     __shared__ float Bs[2][BK][LB];
 
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = (wave / WGN) * WM, wn = (wave % WGN) * WN;
-    const int li = lane & 15, lq = lane >> 4;
+    const int l32 = lane & 31, lh = lane >> 5;
 
     float4 ra[AV], rb[BV];
     auto load = [&](int k0) {
@@ -196,11 +200,13 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
         }
     };
 
-    f32x4 acc[TM][TN];
+    f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
     const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
     if (nk > 0) {
@@ -212,37 +218,37 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
         const int buf = kt & 1;
         if (kt + 1 < nk) load(kbeg + (kt + 1) * BK);          // next tile in flight during the MFMAs
 #pragma unroll
-        for (int k4 = 0; k4 < BK; k4 += 4) {
+        for (int k2 = 0; k2 < BK; k2 += 2) {
             float a[TM], b[TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) a[i] = As[buf][k4 + lq][wm + 16 * i + li];
+            for (int i = 0; i < TM; ++i) a[i] = As[buf][k2 + lh][wm + 32 * i + l32];
 #pragma unroll
-            for (int j = 0; j < TN; ++j) b[j] = Bs[buf][k4 + lq][wn + 16 * j + li];
+            for (int j = 0; j < TN; ++j) b[j] = Bs[buf][k2 + lh][wn + 32 * j + l32];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x4(a[i], b[j], acc[i][j]);
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x2(a[i], b[j], acc[i][j]);
         }
         if (kt + 1 < nk) store(buf ^ 1);
         __syncthreads();
     }
-    // epilogue: D row = (lane >> 4) * 4 + r, col = lane & 15 of each 16 x 16 sub-tile
+    // epilogue: D col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5) of each 32 x 32 sub-tile
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int gn = n0 + wn + 16 * j + li;
+            const int gn = n0 + wn + 32 * j + l32;
             if (gn >= N) continue;
             const float bn = bias ? bias[gn] : 0.0f;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int gm = m0 + wm + 16 * i + lq * 4 + r;
+            for (int v = 0; v < 16; ++v) {
+                const int gm = m0 + wm + 32 * i + (v & 3) + 8 * (v >> 2) + 4 * lh;
                 if (gm >= M) continue;
-                float v = acc[i][j][r];
-                if (beta != 0.0f) v += beta * C[(int64_t)gm * ldc + gn];
-                v += bn;
-                if (relu) v = v > 0.0f ? v : 0.0f;
-                C[(int64_t)gm * ldc + gn] = v;
+                float x = acc[i][j][v];
+                if (beta != 0.0f) x += beta * C[(int64_t)gm * ldc + gn];
+                x += bn;
+                if (relu) x = x > 0.0f ? x : 0.0f;
+                C[(int64_t)gm * ldc + gn] = x;
             }
         }
 }
