@@ -85,7 +85,6 @@ struct CnnWs {
     float *f_olp, *f_ov, *f_adv, *f_ret;
     double *norm_part;
     double *loss_part;     // kSums per loss row block
-    float *dhead_b;        // column sums of dz (A policy biases + value bias)
     float *parts;          // split-K weight-gradient partials / bias column-sum partials
     size_t bytes;
 };
@@ -134,16 +133,15 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_ret = (float *)take(sizeof(float) * R);
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks);
     w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + 255) / 256));
-    w.dhead_b = (float *)take(sizeof(float) * (L.A + 1));
     {
-        const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * L.K2,
-                                         (int64_t)kSplitW3 * L.c3 * L.K3,
+        const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
+                                         (int64_t)kSplitW3 * L.c3 * (L.K3 + 1),
                                          (int64_t)kConv1WgradWG * (L.c1 * L.K1 + L.c1)});
         const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
         const int64_t gparts = std::max({(int64_t)splits_for(R, L.HID, L.F) * R * L.HID,
                                          (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
-                                         (int64_t)splits_for(L.A + 1, L.HID, R) * (L.A + 1) * L.HID,
-                                         (int64_t)splits_for(L.HID, L.F, R) * L.HID * L.F});
+                                         (int64_t)splits_for(L.A + 1, L.HID + 1, R) * (L.A + 1) * (L.HID + 1),
+                                         (int64_t)splits_for(L.HID, L.F + 1, R) * L.HID * (L.F + 1)});
         w.parts = (float *)take(sizeof(float) * std::max({wparts, cparts, gparts}));
     }
     w.bytes = off;
@@ -252,12 +250,6 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float *__restrict__ X
     }
 }
 
-__global__ void k_scatter_head_bias(const float *__restrict__ db, CnnLayout L, float *__restrict__ G)
-{
-    const int a = threadIdx.x;
-    if (a < L.A) G[L.obp + a] = db[a];
-    else if (a == L.A) G[L.obv] = db[a];
-}
 
 // out[i] = sum_p parts[p][i] (fixed order)
 __global__ __launch_bounds__(256) void k_sum_parts(const float *__restrict__ parts, int np, int64_t n,
@@ -705,42 +697,30 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
 {
     int rc;
     const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
-    // head grads: dW[a] = dz[:, a]^T h for a in [0, A] (policy rows, then the value row),
-    // split-K partials summed straight into the two parameter blocks; biases = column sums of dz
+    // head grads: [dW | db][a] = dz[:, a]^T [h | 1] for a in [0, A] (policy rows, then the
+    // value row); split-K partials summed straight into the parameter blocks
     {
         const int A1 = L.A + 1;
-        const int sh = splits_for(A1, L.HID, B);
-        const int64_t n = (int64_t)A1 * L.HID;
-        if ((rc = gemm_f32(s, true, false, A1, L.HID, B, w.dz, A1, w.h, L.HID, w.parts, L.HID, 0.f, nullptr, false, sh,
-                           n)))
+        const int sh = splits_for(A1, L.HID + 1, B);
+        const int64_t pstride = (int64_t)A1 * (L.HID + 1);
+        if ((rc = gemm_wgrad_bias(s, A1, L.HID, B, w.dz, A1, w.h, L.HID, w.parts, sh))) return rc;
+        if ((rc = sum_parts_wb(s, w.parts, sh, pstride, L.A, L.HID, G + L.oWp, G + L.obp))) return rc;
+        if ((rc = sum_parts_wb(s, w.parts + (int64_t)L.A * (L.HID + 1), sh, pstride, 1, L.HID, G + L.oWv, G + L.obv)))
             return rc;
-        if ((rc = sum_parts(s, w.parts, sh, (int64_t)L.A * L.HID, G + L.oWp, nullptr, 1, false, n))) return rc;
-        if ((rc = sum_parts(s, w.parts + (int64_t)L.A * L.HID, sh, L.HID, G + L.oWv, nullptr, 1, false, n))) return rc;
     }
-    if ((rc = colsum(w.dz, B, L.A + 1, w.parts, w.dhead_b, s))) return rc;
-    hipLaunchKernelGGL(k_scatter_head_bias, dim3(1), dim3(64), 0, s, w.dhead_b, L, G);
     hipLaunchKernelGGL(k_cnn_dh, dim3(nblk(B * L.HID)), dim3(256), 0, s, w.dz, P, L, w.h, B, w.dh, stop);
-    // fc
-    if ((rc = colsum(w.dh, B, L.HID, w.parts, G + L.obf, s))) return rc;
+    // fc: [dWf | dbf] = dh^T [a3 | 1]
     {
-        const int sw = splits_for(L.HID, L.F, B);
-        if (sw == 1) {
-            if ((rc = gemm_f32(s, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, 0.f, nullptr,
-                               false)))
-                return rc;
-        } else {
-            if ((rc = gemm_f32(s, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, w.parts, L.F, 0.f, nullptr, false,
-                               sw, (int64_t)L.HID * L.F)))
-                return rc;
-            if ((rc = sum_parts(s, w.parts, sw, (int64_t)L.HID * L.F, G + L.oWf))) return rc;
-        }
+        const int sw = splits_for(L.HID, L.F + 1, B);
+        if ((rc = gemm_wgrad_bias(s, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, w.parts, sw))) return rc;
+        if ((rc = sum_parts_wb(s, w.parts, sw, (int64_t)L.HID * (L.F + 1), L.HID, L.F, G + L.oWf, G + L.obf)))
+            return rc;
     }
     if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr, false)))
         return rc;
     hipLaunchKernelGGL(k_relu_mask, dim3(nblk(B * L.F / 4)), dim3(256), 0, s, w.da3, w.a3, B * L.F / 4);
     // conv3 (dY3 = da3 as [m3][c3])
-    if ((rc = colsum(w.da3, m3, L.c3, w.parts, G + L.ob3, s))) return rc;
-    if ((rc = conv_wgrad_nhwc(s, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3))) return rc;
+    if ((rc = conv_wgrad_nhwc(s, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) return rc;
     if ((rc = gemm_f32(s, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, w.cols3, L.K3, 0.f, nullptr,
                        false)))
         return rc;
@@ -748,8 +728,7 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
                        L.c2, L.k3, L.s3, L.h3, L.w3, w.da2);
     GS_LAUNCH_CHECK("k_col2im_relu");
     // conv2
-    if ((rc = colsum(w.da2, m2, L.c2, w.parts, G + L.ob2, s))) return rc;
-    if ((rc = conv_wgrad_nhwc(s, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2))) return rc;
+    if ((rc = conv_wgrad_nhwc(s, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) return rc;
     if ((rc = gemm_f32(s, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, w.cols2, L.K2, 0.f, nullptr,
                        false)))
         return rc;

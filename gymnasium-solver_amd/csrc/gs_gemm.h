@@ -42,8 +42,16 @@ int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float
 // into parts (splits * Cout * patch floats), then summed in slice order into dW.
 int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
                   float *dW);
+// conv_wgrad_nhwc also produces db[co] (column sums of dY) through a ones column of the
+// patch operand; parts: splits * Cout * (patch + 1) floats
 int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
-                    float *dW);
+                    float *dW, float *db);
+// [dW | db] partials of a dense weight gradient: parts[z] (M x (N+1)) = dY[K x M]^T [X | 1][K x (N+1)]
+// over split z of K; then sum_parts_wb scatters column N of each row into db
+int gemm_wgrad_bias(hipStream_t s, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
+                    int64_t ldx, float *parts, int splits);
+int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int rows, int ncols, float *dW,
+                 float *db);
 // out[i] = (bias/relu epilogue of) sum_{p < np} parts[p*n + i], fixed order; C = row length
 // for the bias index (i % C)
 // (pstride: distance between consecutive partials, default n)

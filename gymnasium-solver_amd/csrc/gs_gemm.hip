@@ -125,6 +125,19 @@ struct U8PatchOp {
     }
 };
 
+// B operand [rows][n] of a weight-gradient GEMM with one extra column of ones at n == n_cols:
+// that output column is the bias gradient (column sums of dY) from the same MFMA pass
+template <class Base>
+struct OnesColOp {
+    Base base;
+    int n_rows, n_cols;
+    __device__ __forceinline__ float4 load4(int o, int i) const
+    {
+        if (i < n_cols) return base.load4(o, i);
+        return make_float4(i == n_cols && o < n_rows ? 1.f : 0.f, 0.f, 0.f, 0.f);
+    }
+};
+
 template <int BM, int BN, int WGM, class AOp, bool A_K, class BOp, bool B_K>
 __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, int K, int kchunk,
                                               float *__restrict__ C, int ldc, int64_t sC, float beta,
@@ -342,6 +355,27 @@ __global__ __launch_bounds__(256) void k_sum_parts_ep(const float *__restrict__ 
     out[i] = v;
 }
 
+// dW[co][j] / db[co] from partials laid out [p][co][ncols + 1] (column ncols = bias)
+__global__ __launch_bounds__(256) void k_sum_parts_wb(const float *__restrict__ parts, int np, int64_t pstride,
+                                                      int rows, int ncols, float *__restrict__ dW,
+                                                      float *__restrict__ db)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = (int64_t)rows * (ncols + 1);
+    if (i >= n) return;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int p = 0;
+    for (; p + 8 <= np; p += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += parts[(int64_t)(p + j) * pstride + i];
+    }
+    for (; p < np; ++p) a[0] += parts[(int64_t)p * pstride + i];
+    const float v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    const int co = (int)(i / (ncols + 1)), j = (int)(i - (int64_t)co * (ncols + 1));
+    if (j < ncols) dW[(int64_t)co * ncols + j] = v;
+    else db[co] = v;
+}
+
 }  // namespace
 
 int sum_parts(hipStream_t s, const float *parts, int np, int64_t n, float *out, const float *bias, int C, bool relu,
@@ -390,6 +424,26 @@ int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float
                                 0.0f, bias, true);
 }
 
+int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int rows, int ncols, float *dW,
+                 float *db)
+{
+    GS_REQUIRE(np >= 1 && rows >= 1 && ncols >= 1, "sum_parts_wb: bad sizes");
+    const int64_t n = (int64_t)rows * (ncols + 1);
+    hipLaunchKernelGGL(k_sum_parts_wb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, parts, np, pstride, rows,
+                       ncols, dW, db);
+    GS_LAUNCH_CHECK("k_sum_parts_wb");
+    return GS_OK;
+}
+
+int gemm_wgrad_bias(hipStream_t s, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
+                    int64_t ldx, float *parts, int splits)
+{
+    GS_REQUIRE(M > 0 && N > 0 && K > 0 && splits >= 1, "gemm_wgrad_bias: empty problem");
+    const OnesColOp<DenseOp> b{dense(X, ldx, K, N), (int)K, (int)N};
+    return dispatch<false, false>(s, dense(dY, lddy, K, M), b, M, N + 1, K, splits, parts, N + 1, M * (N + 1), 0.0f,
+                                  nullptr, false);
+}
+
 int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
                   float *dW)
 {
@@ -405,16 +459,19 @@ int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const flo
 }
 
 int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
-                    float *dW)
+                    float *dW, float *db)
 {
     int rc = check_geom(g);
     if (rc) return rc;
     GS_REQUIRE(g.C % 4 == 0 && ((uintptr_t)in & 15) == 0, "conv_wgrad_nhwc: channels must be float4-aligned");
-    const int64_t rows = g.rows(), P = g.patch(), n = (int64_t)g.Cout * P;
-    rc = dispatch<false, false>(s, dense(dY, g.Cout, rows, g.Cout), nhwc_patches(g, in), g.Cout, P, rows, splits,
-                                splits == 1 ? dW : parts, P, n, 0.0f, nullptr, false);
-    if (rc || splits == 1) return rc;
-    return sum_parts(s, parts, splits, n, dW);
+    GS_REQUIRE(splits >= 1 && db, "conv_wgrad_nhwc: needs the split partials and a bias output");
+    const int64_t rows = g.rows(), P = g.patch(), n = (int64_t)g.Cout * (P + 1);
+    // [dW | db] (Cout x (P+1)) = dY^T (Cout x rows) . [patches | 1] (rows x (P+1))
+    const OnesColOp<NhwcPatchOp> b{nhwc_patches(g, in), (int)rows, (int)P};
+    rc = dispatch<false, false>(s, dense(dY, g.Cout, rows, g.Cout), b, g.Cout, P + 1, rows, splits, parts, P + 1, n,
+                                0.0f, nullptr, false);
+    if (rc) return rc;
+    return sum_parts_wb(s, parts, splits, n, g.Cout, (int)P, dW, db);
 }
 
 int heads_fwd(hipStream_t s, int64_t R, int HID, int A, const float *h, const float *Wp, const float *Wv, float *z,
