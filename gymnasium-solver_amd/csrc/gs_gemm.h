@@ -42,11 +42,11 @@ int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float
 // into parts (splits * Cout * patch floats), then summed in slice order into dW.
 int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
                   float *dW);
-// conv_wgrad_nhwc also produces db[co] (column sums of dY) through a ones column of the
-// patch operand; parts: splits * Cout * (patch + 1) floats
+// conv_wgrad_nhwc also produces db[co] (column sums of dY, summed from the A tiles in LDS
+// by the n-block-0 workgroups); parts: splits * Cout * (patch + 1) floats
 int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
                     float *dW, float *db);
-// [dW | db] partials of a dense weight gradient: parts[z] (M x (N+1)) = dY[K x M]^T [X | 1][K x (N+1)]
+// [dW | db] partials of a dense weight gradient: parts[z] (M x (N+1)) = [dY^T X | rowsum dY^T]
 // over split z of K; then sum_parts_wb scatters column N of each row into db
 int gemm_wgrad_bias(hipStream_t s, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
                     int64_t ldx, float *parts, int splits);

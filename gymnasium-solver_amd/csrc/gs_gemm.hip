@@ -125,20 +125,7 @@ struct U8PatchOp {
     }
 };
 
-// B operand [rows][n] of a weight-gradient GEMM with one extra column of ones at n == n_cols:
-// that output column is the bias gradient (column sums of dY) from the same MFMA pass
-template <class Base>
-struct OnesColOp {
-    Base base;
-    int n_rows, n_cols;
-    __device__ __forceinline__ float4 load4(int o, int i) const
-    {
-        if (i < n_cols) return base.load4(o, i);
-        return make_float4(i == n_cols && o < n_rows ? 1.f : 0.f, 0.f, 0.f, 0.f);
-    }
-};
-
-template <int BM, int BN, int WGM, class AOp, bool A_K, class BOp, bool B_K>
+template <int BM, int BN, int WGM, class AOp, bool A_K, class BOp, bool B_K, bool ASUM = false>
 __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, int K, int kchunk,
                                               float *__restrict__ C, int ldc, int64_t sC, float beta,
                                               const float *__restrict__ bias, int relu)
@@ -222,6 +209,8 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
     const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    const bool do_asum = ASUM && blockIdx.x == 0 && tid < BM;
+    float asum = 0.f;
     if (nk > 0) {
         load(kbeg);
         store(0);
@@ -230,6 +219,10 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < nk) load(kbeg + (kt + 1) * BK);          // next tile in flight during the MFMAs
+        if (do_asum) {
+#pragma unroll
+            for (int k = 0; k < BK; ++k) asum += As[buf][k][tid];
+        }
 #pragma unroll
         for (int k2 = 0; k2 < BK; k2 += 2) {
             float a[TM], b[TN];
@@ -245,6 +238,7 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
         if (kt + 1 < nk) store(buf ^ 1);
         __syncthreads();
     }
+    if (do_asum && m0 + tid < M) C[(int64_t)(m0 + tid) * ldc + N] = asum;
     // epilogue: D col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5) of each 32 x 32 sub-tile
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -266,14 +260,14 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
         }
 }
 
-template <int BM, int BN, int WGM, bool A_K, bool B_K, class AOp, class BOp>
+template <int BM, int BN, int WGM, bool A_K, bool B_K, bool ASUM = false, class AOp, class BOp>
 int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
            int64_t ldc, int64_t sC, float beta, const float *bias, bool relu)
 {
     const int64_t per = (K + splits - 1) / splits;
     const int64_t kchunk = (per + BK - 1) / BK * BK;
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
-    hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K>), grid, dim3(256), 0, s, a, b, (int)M, (int)N, (int)K,
+    hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K, ASUM>), grid, dim3(256), 0, s, a, b, (int)M, (int)N, (int)K,
                        (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0);
     GS_LAUNCH_CHECK("k_gemm");
     return GS_OK;
@@ -281,16 +275,16 @@ int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int6
 
 // tile shape by output shape: skinny N (conv forward: 32 / 64 channels) takes tall tiles,
 // tiny M (weight gradients of 32 / 64 output channels) flat ones
-template <bool A_K, bool B_K, class AOp, class BOp>
+template <bool A_K, bool B_K, bool ASUM = false, class AOp, class BOp>
 int dispatch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
              int64_t ldc, int64_t sC, float beta, const float *bias, bool relu)
 {
-    if (N <= 32) return launch<256, 32, 4, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    if (M <= 32) return launch<32, 128, 1, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    if (N <= 64) return launch<128, 64, 2, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (N <= 32) return launch<256, 32, 4, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (M <= 32) return launch<32, 128, 1, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (N <= 64) return launch<128, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
     const int64_t big_tiles = ((M + 127) / 128) * ((N + 127) / 128) * splits;
-    if (big_tiles >= 512) return launch<128, 128, 2, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    return launch<64, 64, 2, A_K, B_K>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (big_tiles >= 512) return launch<128, 128, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    return launch<64, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
 }
 
 DenseOp dense(const float *p, int64_t ld, int64_t n_outer, int64_t n_inner)
@@ -439,9 +433,8 @@ int gemm_wgrad_bias(hipStream_t s, int64_t M, int64_t N, int64_t K, const float 
                     int64_t ldx, float *parts, int splits)
 {
     GS_REQUIRE(M > 0 && N > 0 && K > 0 && splits >= 1, "gemm_wgrad_bias: empty problem");
-    const OnesColOp<DenseOp> b{dense(X, ldx, K, N), (int)K, (int)N};
-    return dispatch<false, false>(s, dense(dY, lddy, K, M), b, M, N + 1, K, splits, parts, N + 1, M * (N + 1), 0.0f,
-                                  nullptr, false);
+    return dispatch<false, false, true>(s, dense(dY, lddy, K, M), dense(X, ldx, K, N), M, N, K, splits, parts, N + 1,
+                                        M * (N + 1), 0.0f, nullptr, false);
 }
 
 int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
@@ -466,10 +459,9 @@ int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const flo
     GS_REQUIRE(g.C % 4 == 0 && ((uintptr_t)in & 15) == 0, "conv_wgrad_nhwc: channels must be float4-aligned");
     GS_REQUIRE(splits >= 1 && db, "conv_wgrad_nhwc: needs the split partials and a bias output");
     const int64_t rows = g.rows(), P = g.patch(), n = (int64_t)g.Cout * (P + 1);
-    // [dW | db] (Cout x (P+1)) = dY^T (Cout x rows) . [patches | 1] (rows x (P+1))
-    const OnesColOp<NhwcPatchOp> b{nhwc_patches(g, in), (int)rows, (int)P};
-    rc = dispatch<false, false>(s, dense(dY, g.Cout, rows, g.Cout), b, g.Cout, P + 1, rows, splits, parts, P + 1, n,
-                                0.0f, nullptr, false);
+    // [dW | db] (Cout x (P+1)) = dY^T (Cout x rows) . patches, db = row sums of dY^T (ASUM)
+    rc = dispatch<false, false, true>(s, dense(dY, g.Cout, rows, g.Cout), nhwc_patches(g, in), g.Cout, P, rows, splits,
+                                      parts, P + 1, n, 0.0f, nullptr, false);
     if (rc) return rc;
     return sum_parts_wb(s, parts, splits, n, g.Cout, (int)P, dW, db);
 }
