@@ -242,7 +242,7 @@ def main():
         achieved = amount / (mb_us * 1e-6) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 6), "traffic": None,
-                    "kernel": "cnn minibatch step (rocBLAS sgemm + gs_cnn kernels)", "avg_us": round(mb_us, 3),
+                    "kernel": "cnn minibatch step (k_conv1_*, k_gemm, gs_cnn kernels)", "avg_us": round(mb_us, 3),
                     "work_per_launch": amount}
     else:
         stage_us, fused = time_stages(agent, args.stage_reps)
