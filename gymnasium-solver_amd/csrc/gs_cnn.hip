@@ -675,8 +675,16 @@ int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, c
     } else if ((rc = conv_fwd_u8(s, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) {
         return rc;
     }
-    if ((rc = conv_fwd_nhwc(s, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
-    if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) return rc;
+    if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
+        if ((rc = conv23_lds_fwd(s, 2, (int)R, w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
+    } else if ((rc = conv_fwd_nhwc(s, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) {
+        return rc;
+    }
+    if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
+        if ((rc = conv23_lds_fwd(s, 3, (int)R, w.a2, P + L.oW3, P + L.ob3, w.a3))) return rc;
+    } else if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
+        return rc;
+    }
     // fc: h = relu(a3 Wf^T + bf), split-K partials summed with the bias + ReLU epilogue
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {

@@ -15,5 +15,9 @@ int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, 
 int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
                     const float *dA, float *parts, float *dW1, float *db1);
 int conv1_lds_wgrad_parts();
+// conv2 (20x20x32 -> 9x9x64, k4 s2) / conv3 (9x9x64 -> 7x7x64, k3 s1) forward with bias + ReLU,
+// NHWC fp32, LDS-resident samples (layer = 2 or 3)
+bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cout);
+int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float *Wt, const float *bias, float *out);
 
 }  // namespace gs

@@ -281,6 +281,116 @@ __global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ 
     if (g == 0 && i < n) out[i] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
 }
 
+// ---- conv2 / conv3 forward (NHWC fp32 in, 64 filters) as LDS-resident per-sample kernels.
+// SPB samples' activations are staged into LDS with a padded position stride CS (CS * stride
+// = 8 mod 64 dwords: the 16 positions of a ds_read_b128 lane group start 8 banks apart); wave w
+// owns filters [16 w, 16 w + 16) with all their taps in registers; every wave walks every
+// position tile.  k-step group g = one (ky, kx) tap x 16 channels: lane quarter q takes
+// channels 4q .. 4q + 3 of the group, one ds_read_b128 feeding 4 MFMAs.
+template <int H_, int W_, int C_, int K_, int S_, int SPB_>
+struct CN {
+    static constexpr int H = H_, W = W_, C = C_, K = K_, S = S_, SPB = SPB_, CO = 64;
+    static constexpr int OH = (H - K) / S + 1, OW = (W - K) / S + 1, OHW = OH * OW;
+    static constexpr int CS = S == 2 ? C + 4 : C + 8;     // (S * CS) % 64 == 8 for C = 32 / 64
+    static constexpr int KK = K * K * C;                   // taps x channels
+    static constexpr int NG = KK / 16;                     // k-step groups of 4 MFMAs
+    static constexpr int M = SPB * OHW;                    // positions per workgroup
+    static constexpr int MT = (M + 15) / 16;
+    static_assert((S * CS) % 64 == 8 && C % 16 == 0, "padding / channel grouping");
+};
+
+template <class G>
+__global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, int R, const float *__restrict__ Wt,
+                                                  const float *__restrict__ bias, float *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) float xs[G::SPB * G::H * G::W * G::CS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lq = lane >> 4;
+    const int r0 = blockIdx.x * G::SPB;
+    const int nsamp = min(G::SPB, R - r0);
+
+    // this wave's 16 filters, all taps: b[g] = W[16 wave + li][16 g + 4 lq .. + 3]
+    float4 b[G::NG];
+#pragma unroll
+    for (int g = 0; g < G::NG; ++g)
+        b[g] = *reinterpret_cast<const float4 *>(Wt + (int64_t)(16 * wave + li) * G::KK + 16 * g + 4 * lq);
+
+    // stage: [sample][position][channel] with position stride CS, 8 float4 loads in flight
+    {
+        constexpr int C4 = G::C / 4, NE = G::SPB * G::H * G::W * C4, BATCH = 8;
+        const float *src = in + (int64_t)r0 * G::H * G::W * G::C;
+        for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
+            float4 v[BATCH];
+#pragma unroll
+            for (int j = 0; j < BATCH; ++j) {
+                const int e = e0 + tid + 256 * j;
+                const int q = e / (G::H * G::W * C4);
+                v[j] = (e < NE && q < nsamp) ? *reinterpret_cast<const float4 *>(src + 4 * (int64_t)e)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < BATCH; ++j) {
+                const int e = e0 + tid + 256 * j;
+                if (e < NE) {
+                    const int pos = e / C4, c4 = e - pos * C4;
+                    *reinterpret_cast<float4 *>(xs + pos * G::CS + 4 * c4) = v[j];
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    int abase[G::MT];
+#pragma unroll
+    for (int t = 0; t < G::MT; ++t) {
+        const int p = t * 16 + li;
+        const int pc = p < G::M ? p : 0;
+        const int q = pc / G::OHW, pos = pc - q * G::OHW;
+        const int oy = pos / G::OW, ox = pos - oy * G::OW;
+        abase[t] = (q * G::H * G::W + oy * G::S * G::W + ox * G::S) * G::CS + 4 * lq;
+    }
+    f32x4 acc[G::MT];
+#pragma unroll
+    for (int t = 0; t < G::MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < G::NG; ++g) {
+        constexpr int CG = G::C / 16;
+        const int tap = g / CG, cb = (g - tap * CG) * 16;
+        const int ky = tap / G::K, kx = tap - ky * G::K;
+        const int off = (ky * G::W + kx) * G::CS + cb;
+#pragma unroll
+        for (int t = 0; t < G::MT; t += 2) {
+            const float4 a0 = *reinterpret_cast<const float4 *>(xs + abase[t] + off);
+            const float4 a1 = t + 1 < G::MT ? *reinterpret_cast<const float4 *>(xs + abase[t + 1] + off) : a0;
+            acc[t] = mfma(a0.x, b[g].x, acc[t]);
+            if (t + 1 < G::MT) acc[t + 1] = mfma(a1.x, b[g].x, acc[t + 1]);
+            acc[t] = mfma(a0.y, b[g].y, acc[t]);
+            if (t + 1 < G::MT) acc[t + 1] = mfma(a1.y, b[g].y, acc[t + 1]);
+            acc[t] = mfma(a0.z, b[g].z, acc[t]);
+            if (t + 1 < G::MT) acc[t + 1] = mfma(a1.z, b[g].z, acc[t + 1]);
+            acc[t] = mfma(a0.w, b[g].w, acc[t]);
+            if (t + 1 < G::MT) acc[t + 1] = mfma(a1.w, b[g].w, acc[t + 1]);
+        }
+    }
+    // epilogue: D row = lq * 4 + j (position), col = li (filter 16 wave + li)
+    const int co = 16 * wave + li;
+    const float bb = bias[co];
+    float *o = out + (int64_t)r0 * G::OHW * G::CO;
+#pragma unroll
+    for (int t = 0; t < G::MT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = t * 16 + lq * 4 + j;
+            if (p < nsamp * G::OHW) {
+                const float v = acc[t][j] + bb;
+                o[(int64_t)p * G::CO + co] = v > 0.f ? v : 0.f;
+            }
+        }
+}
+
+using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
+using C3_84 = CN<9, 9, 64, 3, 1, 2>;      // conv3: 9x9x64 -> 7x7x64
+
 using C1_84 = C1<4, 84, 84>;
 
 }  // namespace
@@ -315,6 +425,26 @@ int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx
                            C1_84::CO, db1);
     }
     GS_LAUNCH_CHECK("k_sum_partials");
+    return GS_OK;
+}
+
+bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cout)
+{
+    if (layer == 2) return H == 20 && W == 20 && C == 32 && k == 4 && st == 2 && Cout == 64;
+    return H == 9 && W == 9 && C == 64 && k == 3 && st == 1 && Cout == 64;
+}
+
+int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float *Wt, const float *bias, float *out)
+{
+    GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
+    if (layer == 2) {
+        hipLaunchKernelGGL(k_conv_fwd<C2_84>, dim3((unsigned)((R + C2_84::SPB - 1) / C2_84::SPB)), dim3(256), 0, s, in,
+                           R, Wt, bias, out);
+    } else {
+        hipLaunchKernelGGL(k_conv_fwd<C3_84>, dim3((unsigned)((R + C3_84::SPB - 1) / C3_84::SPB)), dim3(256), 0, s, in,
+                           R, Wt, bias, out);
+    }
+    GS_LAUNCH_CHECK("k_conv_fwd");
     return GS_OK;
 }
 
