@@ -729,19 +729,27 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
     hipLaunchKernelGGL(k_relu_mask, dim3(nblk(B * L.F / 4)), dim3(256), 0, s, w.da3, w.a3, B * L.F / 4);
     // conv3 (dY3 = da3 as [m3][c3])
     if ((rc = conv_wgrad_nhwc(s, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) return rc;
-    if ((rc = gemm_f32(s, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, w.cols3, L.K3, 0.f, nullptr,
-                       false)))
-        return rc;
-    hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(m2 * (L.c2 / 4))), dim3(256), 0, s, w.cols3, w.a2, B, L.h2, L.w2,
-                       L.c2, L.k3, L.s3, L.h3, L.w3, w.da2);
-    GS_LAUNCH_CHECK("k_col2im_relu");
+    if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
+        if ((rc = conv23_lds_dgrad(s, 3, (int)B, w.da3, w.a2, P + L.oW3, w.da2))) return rc;
+    } else {
+        if ((rc = gemm_f32(s, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, w.cols3, L.K3, 0.f, nullptr,
+                           false)))
+            return rc;
+        hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(m2 * (L.c2 / 4))), dim3(256), 0, s, w.cols3, w.a2, B, L.h2, L.w2,
+                           L.c2, L.k3, L.s3, L.h3, L.w3, w.da2);
+        GS_LAUNCH_CHECK("k_col2im_relu");
+    }
     // conv2
     if ((rc = conv_wgrad_nhwc(s, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) return rc;
-    if ((rc = gemm_f32(s, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, w.cols2, L.K2, 0.f, nullptr,
-                       false)))
-        return rc;
-    hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(L.rows1(B) * (L.c1 / 4))), dim3(256), 0, s, w.cols2, w.a1, B, L.h1,
-                       L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, w.da1);
+    if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
+        if ((rc = conv23_lds_dgrad(s, 2, (int)B, w.da2, w.a1, P + L.oW2, w.da1))) return rc;
+    } else {
+        if ((rc = gemm_f32(s, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, w.cols2, L.K2, 0.f, nullptr,
+                           false)))
+            return rc;
+        hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(L.rows1(B) * (L.c1 / 4))), dim3(256), 0, s, w.cols2, w.a1, B,
+                           L.h1, L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, w.da1);
+    }
     // conv1 (no input gradient): patches re-read from the u8 frames
     if (conv1_lds_supported(L.C, L.H, L.W))
         return conv1_lds_wgrad(s, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1);

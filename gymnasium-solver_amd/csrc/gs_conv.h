@@ -19,5 +19,8 @@ int conv1_lds_wgrad_parts();
 // NHWC fp32, LDS-resident samples (layer = 2 or 3)
 bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cout);
 int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float *Wt, const float *bias, float *out);
+// input gradient of conv2 / conv3 masked by ReLU'(act) (act = the layer's input activation):
+// dX = (dY conv^T W) * (act > 0), NHWC fp32
+int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX);
 
 }  // namespace gs

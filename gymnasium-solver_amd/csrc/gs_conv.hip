@@ -388,6 +388,141 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
         }
 }
 
+// ---- conv2 / conv3 input gradient (transposed convolution) with the ReLU mask of the layer
+// input, LDS-resident per sample — no patch-gradient matrix, no col2im pass.  Output positions
+// split into S x S parity classes (y = S yy + py): in a class every position has the same
+// K/S x K/S taps (ky = py + S dky, oy = yy - dky), so each class is a dense MFMA problem
+// over (tap, out-channel).  dY is staged with a zero border, so taps that fall outside the
+// output grid read zeros.  Waves = classes x channel chunks; each wave keeps the weights of
+// its class / chunk in registers.
+template <int H_, int W_, int C_, int K_, int S_, int SPB_, int NNC_>
+struct CD {
+    static constexpr int H = H_, W = W_, C = C_, K = K_, S = S_, SPB = SPB_, CO = 64;
+    static constexpr int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+    static constexpr int NY = H / S, NX = W / S;             // positions per class per sample (per axis)
+    static constexpr int KT = K / S;                         // taps per axis per class
+    static constexpr int PAD = KT - 1;
+    static constexpr int PH = PAD + (NY > OH ? NY : OH), PW = PAD + (NX > OW ? NX : OW);
+    static constexpr int CS = CO + 8;                         // 72: 8 banks between positions
+    static constexpr int NCLS = S * S, NNC = NNC_;            // waves: classes x channel chunks
+    static constexpr int NTHR = 64 * NCLS * NNC;
+    static constexpr int CW = C / NNC;                        // channels per wave
+    static constexpr int NT = CW / 16;                        // n-tiles per wave
+    static constexpr int NGRP = KT * KT * (CO / 16);          // k-step groups of 4 MFMAs
+    static constexpr int M = SPB * NY * NX;                   // positions per wave
+    static constexpr int MT = (M + 15) / 16;
+    static_assert(H % S == 0 && W % S == 0 && K % S == 0 && NTHR <= 512 && CW % 16 == 0, "shape");
+};
+
+template <class G>
+__global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict__ dY, const float *__restrict__ act, int R,
+                                                    const float *__restrict__ Wt, float *__restrict__ dX)
+{
+    __shared__ __attribute__((aligned(16))) float ys[G::SPB * G::PH * G::PW * G::CS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lq = lane >> 4;
+    const int cls = wave / G::NNC, chunk = wave - cls * G::NNC;
+    const int py = cls / G::S, px = cls - py * G::S;
+    const int c0 = chunk * G::CW;
+    const int r0 = blockIdx.x * G::SPB;
+    const int nsamp = min(G::SPB, R - r0);
+
+    // this wave's weights: b[g][nt].j = W[co = cb + 4 lq + j][ky][kx][c0 + 16 nt + li]
+    float4 b[G::NGRP][G::NT];
+#pragma unroll
+    for (int g = 0; g < G::NGRP; ++g) {
+        const int tap = g / (G::CO / 16), cb = (g - tap * (G::CO / 16)) * 16;
+        const int dky = tap / G::KT, dkx = tap - dky * G::KT;
+        const int ky = py + G::S * dky, kx = px + G::S * dkx;
+#pragma unroll
+        for (int nt = 0; nt < G::NT; ++nt) {
+            const float *w = Wt + (((int64_t)(cb + 4 * lq) * G::K + ky) * G::K + kx) * G::C + c0 + 16 * nt + li;
+            constexpr int64_t st = (int64_t)G::K * G::K * G::C;     // next out-channel
+            b[g][nt] = make_float4(w[0], w[st], w[2 * st], w[3 * st]);
+        }
+    }
+    // stage dY with a zero border: padded [sample][PH][PW][CS], 8 float4 loads in flight
+    {
+        constexpr int C4 = G::CO / 4, NE = G::SPB * G::PH * G::PW * C4, BATCH = 8;
+        for (int e0 = 0; e0 < NE; e0 += G::NTHR * BATCH) {
+            float4 v[BATCH];
+#pragma unroll
+            for (int j = 0; j < BATCH; ++j) {
+                const int e = e0 + tid + G::NTHR * j;
+                const int q = e / (G::PH * G::PW * C4);
+                const int rem = e - q * (G::PH * G::PW * C4);
+                const int pos = rem / C4, c4 = rem - pos * C4;
+                const int oy = pos / G::PW - G::PAD, ox = pos % G::PW - G::PAD;
+                const bool in = e < NE && q < nsamp && oy >= 0 && oy < G::OH && ox >= 0 && ox < G::OW;
+                v[j] = in ? *reinterpret_cast<const float4 *>(
+                                dY + (((int64_t)(r0 + q) * G::OH + oy) * G::OW + ox) * G::CO + 4 * c4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < BATCH; ++j) {
+                const int e = e0 + tid + G::NTHR * j;
+                if (e < NE) {
+                    const int q = e / (G::PH * G::PW * C4);
+                    const int rem = e - q * (G::PH * G::PW * C4);
+                    const int pos = rem / C4, c4 = rem - pos * C4;
+                    *reinterpret_cast<float4 *>(ys + (q * G::PH * G::PW + pos) * G::CS + 4 * c4) = v[j];
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    int abase[G::MT];
+#pragma unroll
+    for (int t = 0; t < G::MT; ++t) {
+        const int p = t * 16 + li;
+        const int pc = p < G::M ? p : 0;
+        const int q = pc / (G::NY * G::NX), rem = pc - q * (G::NY * G::NX);
+        const int yy = rem / G::NX, xx = rem - yy * G::NX;
+        abase[t] = (q * G::PH * G::PW + (yy + G::PAD) * G::PW + xx + G::PAD) * G::CS + 4 * lq;
+    }
+    f32x4 acc[G::MT][G::NT];
+#pragma unroll
+    for (int t = 0; t < G::MT; ++t)
+#pragma unroll
+        for (int nt = 0; nt < G::NT; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < G::NGRP; ++g) {
+        const int tap = g / (G::CO / 16), cb = (g - tap * (G::CO / 16)) * 16;
+        const int dky = tap / G::KT, dkx = tap - dky * G::KT;
+        const int off = -(dky * G::PW + dkx) * G::CS + cb;
+#pragma unroll
+        for (int t = 0; t < G::MT; ++t) {
+            const float4 a = *reinterpret_cast<const float4 *>(ys + abase[t] + off);
+#pragma unroll
+            for (int nt = 0; nt < G::NT; ++nt) {
+                acc[t][nt] = mfma(a.x, b[g][nt].x, acc[t][nt]);
+                acc[t][nt] = mfma(a.y, b[g][nt].y, acc[t][nt]);
+                acc[t][nt] = mfma(a.z, b[g][nt].z, acc[t][nt]);
+                acc[t][nt] = mfma(a.w, b[g][nt].w, acc[t][nt]);
+            }
+        }
+    }
+    // epilogue: D row = lq * 4 + j (class position), col = li (channel); ReLU mask of the input
+#pragma unroll
+    for (int t = 0; t < G::MT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = t * 16 + lq * 4 + j;
+            const int q = p / (G::NY * G::NX), rem = p - q * (G::NY * G::NX);
+            if (p >= G::M || q >= nsamp) continue;
+            const int yy = rem / G::NX, xx = rem - yy * G::NX;
+            const int y = G::S * yy + py, x = G::S * xx + px;
+            const int64_t e = (((int64_t)(r0 + q) * G::H + y) * G::W + x) * G::C + c0 + li;
+#pragma unroll
+            for (int nt = 0; nt < G::NT; ++nt)
+                dX[e + 16 * nt] = act[e + 16 * nt] > 0.f ? acc[t][nt][j] : 0.f;
+        }
+}
+
+using D2_84 = CD<20, 20, 32, 4, 2, 1, 2>;    // conv2 input gradient: 9x9x64 -> 20x20x32 (8 waves)
+using D3_84 = CD<9, 9, 64, 3, 1, 1, 4>;      // conv3 input gradient: 7x7x64 -> 9x9x64
+
 using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
 using C3_84 = CN<9, 9, 64, 3, 1, 2>;      // conv3: 9x9x64 -> 7x7x64
 
@@ -445,6 +580,20 @@ int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float
                            R, Wt, bias, out);
     }
     GS_LAUNCH_CHECK("k_conv_fwd");
+    return GS_OK;
+}
+
+int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX)
+{
+    GS_REQUIRE(R > 0 && dY && act && Wt && dX, "conv23_lds_dgrad: bad argument");
+    if (layer == 2) {
+        hipLaunchKernelGGL(k_conv_dgrad<D2_84>, dim3((unsigned)((R + D2_84::SPB - 1) / D2_84::SPB)), dim3(D2_84::NTHR), 0, s,
+                           dY, act, R, Wt, dX);
+    } else {
+        hipLaunchKernelGGL(k_conv_dgrad<D3_84>, dim3((unsigned)((R + D3_84::SPB - 1) / D3_84::SPB)), dim3(D3_84::NTHR), 0, s,
+                           dY, act, R, Wt, dX);
+    }
+    GS_LAUNCH_CHECK("k_conv_dgrad");
     return GS_OK;
 }
 
