@@ -8,8 +8,9 @@
 // correctly rounded, once per pixel), and the MFMA operands are read from that tile:
 //
 //   k_conv1_fwd   one workgroup per (sample, half): 200 positions x 32 filters x 256 taps on
-//                 v_mfma_f32_16x16x4_f32.  The filters live in registers (each lane holds the
-//                 64 taps it multiplies); the patch operand is one ds_read_b128 per 4 MFMAs
+//                 v_mfma_f32_16x16x4_f32.  Each wave owns 16 filters and every other position
+//                 tile; its filters live in registers (each lane holds the 64 taps it
+//                 multiplies); the patch operand is one ds_read_b128 per 4 MFMAs
 //                 (a lane's 4 consecutive taps are 4 consecutive pixels).  Bias + ReLU in the
 //                 epilogue, NHWC fp32 output.
 //   k_conv1_wgrad 256 workgroups, each walking a fixed set of (sample, half) bands: dW1 (32 x
@@ -99,64 +100,62 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
     const int rows = min(G::BOH, G::OH - oy0);
     const int P = rows * G::OW;
 
-    // filters -> registers: b[g][nt] = W1[nt*16 + li][taps of group g for this lane quarter]
-    float4 b[G::KS / 4][2];
+    // wave w: filters [16 nt, 16 nt + 16) with nt = w / 2, position tiles w % 2, w % 2 + 2, ...
+    // (7 or 6 of the 13 per band: balanced to within one tile)
+    const int nt = wave >> 1, tpar = wave & 1;
+    float4 b[G::KS / 4];
 #pragma unroll
     for (int g = 0; g < G::KS / 4; ++g) {
         const int c = g >> 2, ky = 2 * (g & 3) + (lq >> 1), kx0 = 4 * (lq & 1);
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-            b[g][nt] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
+        b[g] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
     }
     stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S);
     __syncthreads();
 
-    // m-tiles of this wave: wave, wave + 4, ... (13 tiles at 84 x 84: 4, 3, 3, 3)
-    constexpr int TMW = (G::MT + 3) / 4;
+    constexpr int TMW = (G::MT + 1) / 2;
     int abase[TMW];
 #pragma unroll
     for (int t = 0; t < TMW; ++t) {
-        const int p = (wave + 4 * t) * 16 + li;
+        const int p = (tpar + 2 * t) * 16 + li;
         const int pc = p < P ? p : 0;
         const int oy = pc / G::OW, ox = pc - oy * G::OW;
         abase[t] = (oy * G::S + (lq >> 1)) * G::W + ox * G::S + 4 * (lq & 1);
     }
-    f32x4 acc[TMW][2];
+    f32x4 acc[TMW];
 #pragma unroll
-    for (int t = 0; t < TMW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < TMW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int g = 0; g < G::KS / 4; ++g) {
         const int goff = ((g >> 2) * G::BIR + 2 * (g & 3)) * G::W;
 #pragma unroll
-        for (int t = 0; t < TMW; ++t) {
-            if (wave + 4 * t >= G::MT) break;
-            const float4 a = *reinterpret_cast<const float4 *>(fr + abase[t] + goff);
-            acc[t][0] = mfma(a.x, b[g][0].x, acc[t][0]);
-            acc[t][1] = mfma(a.x, b[g][1].x, acc[t][1]);
-            acc[t][0] = mfma(a.y, b[g][0].y, acc[t][0]);
-            acc[t][1] = mfma(a.y, b[g][1].y, acc[t][1]);
-            acc[t][0] = mfma(a.z, b[g][0].z, acc[t][0]);
-            acc[t][1] = mfma(a.z, b[g][1].z, acc[t][1]);
-            acc[t][0] = mfma(a.w, b[g][0].w, acc[t][0]);
-            acc[t][1] = mfma(a.w, b[g][1].w, acc[t][1]);
+        for (int t = 0; t < TMW; t += 2) {
+            const bool two = t + 1 < TMW && tpar + 2 * (t + 1) < G::MT;
+            if (tpar + 2 * t >= G::MT) break;
+            const float4 a0 = *reinterpret_cast<const float4 *>(fr + abase[t] + goff);
+            const float4 a1 = two ? *reinterpret_cast<const float4 *>(fr + abase[t + 1] + goff) : a0;
+            acc[t] = mfma(a0.x, b[g].x, acc[t]);
+            if (two) acc[t + 1] = mfma(a1.x, b[g].x, acc[t + 1]);
+            acc[t] = mfma(a0.y, b[g].y, acc[t]);
+            if (two) acc[t + 1] = mfma(a1.y, b[g].y, acc[t + 1]);
+            acc[t] = mfma(a0.z, b[g].z, acc[t]);
+            if (two) acc[t + 1] = mfma(a1.z, b[g].z, acc[t + 1]);
+            acc[t] = mfma(a0.w, b[g].w, acc[t]);
+            if (two) acc[t + 1] = mfma(a1.w, b[g].w, acc[t + 1]);
         }
     }
     // epilogue: D row = lq * 4 + j (position), col = li (filter)
     float *o = out + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
+    const int co = nt * 16 + li;
+    const float bb = b1[co];
 #pragma unroll
     for (int t = 0; t < TMW; ++t) {
-        if (wave + 4 * t >= G::MT) break;
+        if (tpar + 2 * t >= G::MT) break;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-            const int co = nt * 16 + li;
-            const float bb = b1[co];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int p = (wave + 4 * t) * 16 + lq * 4 + j;
-                if (p < P) {
-                    const float v = acc[t][nt][j] + bb;
-                    o[(int64_t)p * G::CO + co] = v > 0.f ? v : 0.f;
-                }
+        for (int j = 0; j < 4; ++j) {
+            const int p = (tpar + 2 * t) * 16 + lq * 4 + j;
+            if (p < P) {
+                const float v = acc[t][j] + bb;
+                o[(int64_t)p * G::CO + co] = v > 0.f ? v : 0.f;
             }
         }
     }
