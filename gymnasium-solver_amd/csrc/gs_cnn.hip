@@ -136,7 +136,8 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
                                          (int64_t)kSplitW3 * L.c3 * (L.K3 + 1),
-                                         (int64_t)kConv1WgradWG * (L.c1 * L.K1 + L.c1)});
+                                         (int64_t)kConv1WgradWG * (L.c1 * L.K1 + L.c1),
+                                         (int64_t)kConvWgradWG * 64 * (std::max(L.K2, L.K3) + 1)});
         const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
         const int64_t gparts = std::max({(int64_t)splits_for(R, L.HID, L.F) * R * L.HID,
                                          (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
@@ -728,7 +729,11 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
         return rc;
     hipLaunchKernelGGL(k_relu_mask, dim3(nblk(B * L.F / 4)), dim3(256), 0, s, w.da3, w.a3, B * L.F / 4);
     // conv3 (dY3 = da3 as [m3][c3])
-    if ((rc = conv_wgrad_nhwc(s, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) return rc;
+    if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
+        if ((rc = conv23_lds_wgrad(s, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
+    } else if ((rc = conv_wgrad_nhwc(s, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) {
+        return rc;
+    }
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
         if ((rc = conv23_lds_dgrad(s, 3, (int)B, w.da3, w.a2, P + L.oW3, w.da2))) return rc;
     } else {
@@ -740,7 +745,11 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
         GS_LAUNCH_CHECK("k_col2im_relu");
     }
     // conv2
-    if ((rc = conv_wgrad_nhwc(s, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) return rc;
+    if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
+        if ((rc = conv23_lds_wgrad(s, 2, (int)B, w.a1, w.da2, w.parts, G + L.oW2, G + L.ob2))) return rc;
+    } else if ((rc = conv_wgrad_nhwc(s, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) {
+        return rc;
+    }
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
         if ((rc = conv23_lds_dgrad(s, 2, (int)B, w.da2, w.a1, P + L.oW2, w.da1))) return rc;
     } else {

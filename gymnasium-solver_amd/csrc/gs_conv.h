@@ -6,6 +6,7 @@
 namespace gs {
 
 constexpr int kConv1WgradWG = 256;     // workgroups (= partials) of the conv1 weight gradient
+constexpr int kConvWgradWG = 256;      // workgroups (= partials) of the conv2 / conv3 weight gradients
 
 bool conv1_lds_supported(int C, int H, int W);
 // out[r][oy][ox][co] = relu(b1[co] + sum W1[co][c][ky][kx] * frame(r)[c][4 oy + ky][4 ox + kx] / 255)
@@ -22,5 +23,8 @@ int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float
 // input gradient of conv2 / conv3 masked by ReLU'(act) (act = the layer's input activation):
 // dX = (dY conv^T W) * (act > 0), NHWC fp32
 int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX);
+// dW (64 x patch) and db (64) of conv2 / conv3; parts: kConvWgradWG x 64 x (patch + 1) floats
+int conv23_lds_wgrad(hipStream_t s, int layer, int R, const float *in, const float *dY, float *parts, float *dW,
+                     float *db);
 
 }  // namespace gs

@@ -20,6 +20,7 @@
 // Frame rows come through the minibatch index exactly like the generic loader (env-major
 // sample index -> (t, env) row of the (T, N) rollout buffer).
 #include "gs_conv.h"
+#include "gs_gemm.h"
 
 namespace gs {
 namespace {
@@ -522,6 +523,117 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
 using D2_84 = CD<20, 20, 32, 4, 2, 1, 2>;    // conv2 input gradient: 9x9x64 -> 20x20x32 (8 waves)
 using D3_84 = CD<9, 9, 64, 3, 1, 1, 4>;      // conv3 input gradient: 7x7x64 -> 9x9x64
 
+// ---- conv2 / conv3 weight + bias gradient, LDS-resident per sample: dW[co][tap, c] +=
+// dY^T . patches with dY (positions x 64) and the input activation staged in LDS, positions
+// as the MFMA reduction dimension (4 per k-step, zero-padded).  Wave w owns patch columns
+// [w KK/4, (w+1) KK/4) for all 64 filters; db from the same dY tile.  One partial
+// [64][KK + 1] per workgroup (db in column KK), summed in workgroup order by k_sum_parts_wb.
+template <class G>
+struct WG2 {
+    static constexpr int CSX = G::S == 2 ? G::C + 8 : G::C + 16;   // S * CSX = 16 mod 32
+    static constexpr int DS = G::CO + 16;                          // 80: 16 banks between positions
+    static constexpr int PP = (G::OHW + 3) / 4 * 4;                // positions padded to k-steps
+    static constexpr int NTW = G::KK / 16 / 4;                     // n-tiles per wave
+    static_assert((G::S * CSX) % 32 == 16, "padding");
+};
+
+template <class G>
+__global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in, const float *__restrict__ dY, int R,
+                                                    float *__restrict__ parts)
+{
+    using X = WG2<G>;
+    __shared__ __attribute__((aligned(16))) float xs[G::H * G::W * X::CSX];
+    __shared__ __attribute__((aligned(16))) float ds[X::PP * X::DS];
+    __shared__ float dbred[4][G::CO];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lq = lane >> 4;
+    // this lane's patch columns: kk = 16 (wave NTW + nt) + li -> (tap, c)
+    int boff[X::NTW];
+#pragma unroll
+    for (int nt = 0; nt < X::NTW; ++nt) {
+        const int kk = 16 * (wave * X::NTW + nt) + li;
+        const int tap = kk / G::C, c = kk - tap * G::C;
+        const int ky = tap / G::K, kx = tap - ky * G::K;
+        boff[nt] = (ky * G::W + kx) * X::CSX + c;
+    }
+    f32x4 acc[4][X::NTW];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < X::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float db = 0.f;
+
+    for (int r = blockIdx.x; r < R; r += gridDim.x) {
+        __syncthreads();
+        {   // input activation [pos][c] with stride CSX, dY [pos][co] with stride DS (zero rows past OHW)
+            constexpr int NX4 = G::H * G::W * G::C / 4, ND4 = X::PP * G::CO / 4;
+            constexpr int NE = NX4 + ND4, BATCH = 8;
+            const float *xin = in + (int64_t)r * G::H * G::W * G::C;
+            const float *dyin = dY + (int64_t)r * G::OHW * G::CO;
+            for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
+                float4 v[BATCH];
+#pragma unroll
+                for (int j = 0; j < BATCH; ++j) {
+                    const int e = e0 + tid + 256 * j;
+                    if (e < NX4) {
+                        v[j] = *reinterpret_cast<const float4 *>(xin + 4 * (int64_t)e);
+                    } else {
+                        const int d = e - NX4;
+                        const int p = d / (G::CO / 4);
+                        v[j] = (e < NE && p < G::OHW) ? *reinterpret_cast<const float4 *>(dyin + 4 * (int64_t)d)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < BATCH; ++j) {
+                    const int e = e0 + tid + 256 * j;
+                    if (e < NX4) {
+                        const int pos = e / (G::C / 4), c4 = e - pos * (G::C / 4);
+                        *reinterpret_cast<float4 *>(xs + pos * X::CSX + 4 * c4) = v[j];
+                    } else if (e < NE) {
+                        const int d = e - NX4;
+                        const int p = d / (G::CO / 4), c4 = d - p * (G::CO / 4);
+                        *reinterpret_cast<float4 *>(ds + p * X::DS + 4 * c4) = v[j];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        {   // bias partial: thread (co = tid % 64, group tid / 64) sums positions group, group + 4, ...
+            const int co = tid & 63, grp = tid >> 6;
+            for (int p = grp; p < G::OHW; p += 4) db += ds[p * X::DS + co];
+        }
+        for (int s = 0; s < X::PP / 4; ++s) {
+            const int p = 4 * s + lq;
+            const bool ok = p < G::OHW;
+            const int pc = ok ? p : 0;
+            const int oy = pc / G::OW, ox = pc - oy * G::OW;
+            const int pof = (oy * G::S * G::W + ox * G::S) * X::CSX;
+            float a[4], bv[X::NTW];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) a[mt] = ds[p * X::DS + 16 * mt + li];
+#pragma unroll
+            for (int nt = 0; nt < X::NTW; ++nt) bv[nt] = ok ? xs[pof + boff[nt]] : 0.f;
+#pragma unroll
+            for (int nt = 0; nt < X::NTW; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = mfma(a[mt], bv[nt], acc[mt][nt]);
+        }
+    }
+    // partial: D row = lq * 4 + j (filter in the m-tile), col = li (patch column in the n-tile)
+    float *o = parts + (int64_t)blockIdx.x * G::CO * (G::KK + 1);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < X::NTW; ++nt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                o[(int64_t)(16 * mt + lq * 4 + j) * (G::KK + 1) + 16 * (wave * X::NTW + nt) + li] = acc[mt][nt][j];
+    dbred[tid >> 6][tid & 63] = db;
+    __syncthreads();
+    if (tid < G::CO) o[(int64_t)tid * (G::KK + 1) + G::KK] = (dbred[0][tid] + dbred[1][tid]) + (dbred[2][tid] + dbred[3][tid]);
+}
+
 using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
 using C3_84 = CN<9, 9, 64, 3, 1, 2>;      // conv3: 9x9x64 -> 7x7x64
 
@@ -594,6 +706,23 @@ int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const flo
     }
     GS_LAUNCH_CHECK("k_conv_dgrad");
     return GS_OK;
+}
+
+int conv23_lds_wgrad(hipStream_t s, int layer, int R, const float *in, const float *dY, float *parts, float *dW,
+                     float *db)
+{
+    GS_REQUIRE(R > 0 && in && dY && parts && dW && db, "conv23_lds_wgrad: bad argument");
+    const int nwg = kConvWgradWG;
+    int KK;
+    if (layer == 2) {
+        KK = C2_84::KK;
+        hipLaunchKernelGGL(k_conv_wgrad<C2_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+    } else {
+        KK = C3_84::KK;
+        hipLaunchKernelGGL(k_conv_wgrad<C3_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+    }
+    GS_LAUNCH_CHECK("k_conv_wgrad");
+    return sum_parts_wb(s, parts, nwg, (int64_t)64 * (KK + 1), 64, KK, dW, db);
 }
 
 }  // namespace gs
