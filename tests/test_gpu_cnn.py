@@ -101,3 +101,50 @@ def test_cnn_policy_act_vs_oracle(cuda, tag):
     assert set(np.unique(a_s)) <= set(valid)
     ln_rep = np.tile(ln, (64, 1))
     np.testing.assert_allclose(lp_s.cpu().numpy(), ln_rep[np.arange(len(a_s)), a_s], atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize("in_shape,T", [((4, 84, 84), 3), ((4, 52, 48), 2)])
+def test_cnn_update_gathered_rows_and_generic_shapes(cuda, in_shape, T):
+    """The update reads its minibatch through the sampler's env-major indices into a (T, N)
+    rollout buffer (rollout_buffer.py:11-13).  (4, 84, 84) runs the LDS-resident conv kernels,
+    (4, 52, 48) the generic implicit-GEMM path (u8 patch loader, NHWC patches, split-K weight
+    gradients, dense dgrad + col2im); both against the oracle on the gathered rows.
+    Tolerances as in test_cnn_update_step_vs_oracle_and_reference."""
+    from oracle import cnn_case as K
+    from oracle import cnn_ref as C
+    from gsamd._lib import GS_NUM_METRICS, PPOHparams, RolloutViewU8, check, lib
+    from gsamd.cnn import DeviceCNNActorCritic
+    valid, clip, ent, lr, N = [0, 3, 4], 0.2, 0.01, 3e-4, 20
+    B = 32
+    obs, act, olp, ov, adv, ret = K.cnn_batch(11, T * N, valid, in_shape=in_shape)   # row = t * N + env
+    rng = np.random.default_rng(5)
+    idx = rng.permutation(T * N)[:B].astype(np.int32)                     # env-major i = env * T + t
+    src = (idx % T) * N + idx // T
+    batch = (obs[src], act[src], olp[src], ov[src], adv[src], ret[src])
+    shapes = C.cnn_param_shapes(in_shape)
+    p_ref = K.cnn_params(3, in_shape=in_shape)
+    loss, met, g, logits, values = C.loss_and_grads(p_ref, shapes, *batch, valid=valid, clip=clip, clip_vf=0.2,
+                                                    vf_coef=0.5, ent_coef=ent)
+    P = p_ref.size
+    p1, _, _, gc, total = C.clip_and_adam(p_ref, g, shapes, np.zeros(P, np.float32), np.zeros(P, np.float32), 1, lr)
+
+    pm = DeviceCNNActorCritic(in_shape=in_shape, valid_actions=valid, device=cuda, init=False)
+    pm.load_reference_flat(p_ref)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x)).to(cuda).contiguous()  # noqa: E731
+    bufs = [t(obs), t(act), t(olp), t(ov), t(adv), t(ret)]
+    view = RolloutViewU8(*(b.data_ptr() for b in bufs), T, N)
+    hp = PPOHparams(clip, 0.2, 0.5, ent, 0.5, lr, 0.9, 0.999, 1e-8, 0.0, 1, 0)
+    idx_d = torch.as_tensor(idx).to(cuda)
+    grads, m, v = (torch.zeros(pm.n_params, device=cuda) for _ in range(3))
+    ws = torch.empty(int(lib.gs_cnn_workspace_bytes(pm.dims, B)), dtype=torch.uint8, device=cuda)
+    met_d = torch.zeros(GS_NUM_METRICS, device=cuda)
+    stop = torch.zeros(1, dtype=torch.int32, device=cuda)
+    check(lib.gs_cnn_ppo_update(pm.params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), pm.dims, hp, view,
+                                idx_d.data_ptr(), B, 1, 0, met_d.data_ptr(), stop.data_ptr(), ws.data_ptr(), None,
+                                torch.cuda.current_stream().cuda_stream), "gs_cnn_ppo_update")
+    torch.cuda.synchronize()
+    rec = met_d.cpu().numpy()
+    assert abs(rec[0] - loss) < 1e-5 * max(1.0, abs(loss))
+    assert abs(rec[12] - total) < 1e-5 * total
+    np.testing.assert_allclose(pm.flat_to_reference(grads), gc, atol=2e-5 * np.abs(gc).max(), rtol=0)
+    _adam_close(pm.flat_to_reference(pm.params), p1, lr)
