@@ -13,10 +13,11 @@
 //                 multiplies); the patch operand is one ds_read_b128 per 4 MFMAs
 //                 (a lane's 4 consecutive taps are 4 consecutive pixels).  Bias + ReLU in the
 //                 epilogue, NHWC fp32 output.
-//   k_conv1_wgrad 256 workgroups, each walking a fixed set of (sample, half) bands: dW1 (32 x
-//                 256) += dA1^T . patches with dA1 staged in LDS next to the frame tile, and
-//                 db1 from the same dA1 tile; one partial per workgroup, summed in workgroup
-//                 order by k_sum_partials (deterministic).
+//   k_conv1_wgrad 256 workgroups, each walking a fixed set of 5-output-row units: dW1 (32 x
+//                 256) += dA1^T . patches with dA1 staged in LDS next to the frame tile (two
+//                 buffers: the next unit loads under this unit's MFMAs), and db1 from the same
+//                 dA1 tile; one partial per workgroup, summed in workgroup order by
+//                 k_sum_partials (deterministic).
 // Frame rows come through the minibatch index exactly like the generic loader (env-major
 // sample index -> (t, env) row of the (T, N) rollout buffer).
 #include "gs_conv.h"
@@ -162,17 +163,26 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
     }
 }
 
-// dW1[co][tap] and db1[co] partials of one workgroup over bands blockIdx.x, + gridDim.x, ...
-// parts layout: [workgroup][CO * KK + CO]
+// dW1[co][tap] and db1[co] partials of one workgroup over units blockIdx.x, + gridDim.x, ...
+// A unit is 5 output rows of one sample (4 per sample at 84 x 84): its 24-row frame band
+// (fp32) and 100 x 32 dA rows fit twice in LDS, so the next unit's global loads (held in
+// registers) run under the current unit's MFMAs.  parts layout: [workgroup][CO * KK + CO]
 template <class G>
 __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
                                                      int64_t T, int64_t N, int R, const float *__restrict__ dA,
                                                      float *__restrict__ parts)
 {
-    constexpr int DS = 48;                      // dA row stride (floats): kq rows land 16 banks apart
-    constexpr int BPP = (G::BP + 3) / 4 * 4;    // positions padded to whole k-steps
-    __shared__ __attribute__((aligned(16))) float fr[G::FRAME];
-    __shared__ __attribute__((aligned(16))) float da[BPP * DS];
+    constexpr int UR = 5;                               // output rows per unit
+    constexpr int NU = (G::OH + UR - 1) / UR;           // units per sample
+    constexpr int UIR = (UR - 1) * G::S + G::K;         // frame rows per unit
+    constexpr int UP = UR * G::OW;                      // positions per (full) unit
+    constexpr int UPP = (UP + 3) / 4 * 4;
+    constexpr int DS = 48;                              // dA row stride: k-step rows 16 banks apart
+    constexpr int NF = G::C * UIR * G::W4;              // u32 words of a frame band
+    constexpr int NDA = UPP * (G::CO / 4);              // float4 of a dA unit
+    constexpr int PF = (NF + 255) / 256, PD = (NDA + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float fr[2][G::C * UIR * G::W];
+    __shared__ __attribute__((aligned(16))) float da[2][UPP * DS];
     __shared__ float dbred[8][G::CO];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
         const int tap = wave * 64 + nt * 16 + li;
         const int c = tap / (G::K * G::K), rem = tap - c * (G::K * G::K);
         const int ky = rem / G::K, kx = rem - ky * G::K;
-        boff[nt] = (c * G::BIR + ky) * G::W + kx;
+        boff[nt] = (c * UIR + ky) * G::W + kx;
     }
     f32x4 acc[2][4];
 #pragma unroll
@@ -192,51 +202,87 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
         for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     float db = 0.f;                              // thread (co = tid % 32, group tid / 32)
 
-    for (int bnd = blockIdx.x; bnd < 2 * R; bnd += gridDim.x) {
-        const int r = bnd >> 1, band = bnd & 1;
-        const int oy0 = band * G::BOH;
-        const int rows = min(G::BOH, G::OH - oy0);
-        const int P = rows * G::OW;
-        __syncthreads();                         // previous band's readers are done
-        stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S);
+    uint32_t fv[PF];
+    float4 dv[PD];
+    auto rows_of = [&](int unit) { return min(UR, G::OH - (unit % NU) * UR); };
+    auto load = [&](int unit) {
+        const int r = unit / NU, oy0 = (unit % NU) * UR;
+        const int P = rows_of(unit) * G::OW;
+        const uint8_t *base = obs + frame_src(idx, r, T, N) * (int64_t)(G::C * G::H * G::W);
+        const int y0 = oy0 * G::S;
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            const int e = tid + 256 * j;
+            const int c = e / (UIR * G::W4), rem = e - c * (UIR * G::W4);
+            const int y = rem / G::W4, x4 = rem - y * G::W4;
+            fv[j] = (e < NF && y0 + y < G::H)
+                        ? *reinterpret_cast<const uint32_t *>(base + ((int64_t)c * G::H + y0 + y) * G::W + 4 * x4)
+                        : 0u;
+        }
         const float *src = dA + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
-        {
-            constexpr int NE = BPP * (G::CO / 4), PER = (NE + 255) / 256;
-            float4 v[PER];
 #pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const int e = tid + 256 * j;
-                const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
-                v[j] = (e < NE && p < P) ? *reinterpret_cast<const float4 *>(src + (int64_t)p * G::CO + 4 * c4)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+        for (int j = 0; j < PD; ++j) {
+            const int e = tid + 256 * j;
+            const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
+            dv[j] = (e < NDA && p < P) ? *reinterpret_cast<const float4 *>(src + (int64_t)p * G::CO + 4 * c4)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
 #pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const int e = tid + 256 * j;
-                const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
-                if (e < NE) *reinterpret_cast<float4 *>(da + p * DS + 4 * c4) = v[j];
+        for (int j = 0; j < PF; ++j) {
+            const int e = tid + 256 * j;
+            if (e < NF) {
+                const int c = e / (UIR * G::W4), rem = e - c * (UIR * G::W4);
+                const int y = rem / G::W4, x4 = rem - y * G::W4;
+                const uint32_t v = fv[j];
+                *reinterpret_cast<float4 *>(&fr[buf][(c * UIR + y) * G::W + 4 * x4]) =
+                    make_float4((float)(v & 255u) / 255.0f, (float)((v >> 8) & 255u) / 255.0f,
+                                (float)((v >> 16) & 255u) / 255.0f, (float)(v >> 24) / 255.0f);
             }
         }
-        __syncthreads();
-        // bias partial: thread (co, grp) sums positions grp, grp + 8, ... in order
-        {
+#pragma unroll
+        for (int j = 0; j < PD; ++j) {
+            const int e = tid + 256 * j;
+            if (e < NDA) {
+                const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
+                *reinterpret_cast<float4 *>(&da[buf][p * DS + 4 * c4]) = dv[j];
+            }
+        }
+    };
+
+    const int n_units = R * NU;
+    int unit = blockIdx.x;
+    if (unit < n_units) {
+        load(unit);
+        store(0);
+    }
+    __syncthreads();
+    for (int it = 0; unit < n_units; ++it, unit += gridDim.x) {
+        const int buf = it & 1;
+        const int next = unit + gridDim.x;
+        if (next < n_units) load(next);                  // in flight during this unit's MFMAs
+        const int P = rows_of(unit) * G::OW;
+        {   // bias partial: thread (co, grp) sums positions grp, grp + 8, ... in order
             const int co = tid & 31, grp = tid >> 5;
-            for (int p = grp; p < P; p += 8) db += da[p * DS + co];
+            for (int p = grp; p < P; p += 8) db += da[buf][p * DS + co];
         }
-        for (int s = 0; s < BPP / 4; ++s) {
+        for (int s = 0; s < UPP / 4; ++s) {
             const int p = 4 * s + lq;                         // this lane's position of the k-step
             const int oy = p / G::OW, ox = p - oy * G::OW;
             const int pof = (oy * G::S) * G::W + ox * G::S;
-            const float a0 = da[p * DS + li], a1 = da[p * DS + 16 + li];
+            const float a0 = da[buf][p * DS + li], a1 = da[buf][p * DS + 16 + li];
             float bv[4];
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) bv[nt] = p < P ? fr[pof + boff[nt]] : 0.f;
+            for (int nt = 0; nt < 4; ++nt) bv[nt] = p < P ? fr[buf][pof + boff[nt]] : 0.f;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
                 acc[0][nt] = mfma(a0, bv[nt], acc[0][nt]);
                 acc[1][nt] = mfma(a1, bv[nt], acc[1][nt]);
             }
         }
+        if (next < n_units) store(buf ^ 1);
+        __syncthreads();
     }
     // partial out: D row = lq * 4 + j (filter within the m-tile), col = li (tap within the n-tile)
     float *o = parts + (int64_t)blockIdx.x * (G::CO * G::KK + G::CO);
