@@ -649,6 +649,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
             const int co = tid & 63, grp = tid >> 6;
             for (int p = grp; p < G::OHW; p += 4) db += ds[p * X::DS + co];
         }
+#pragma unroll 3
         for (int s = 0; s < X::PP / 4; ++s) {
             const int p = 4 * s + lq;
             const bool ok = p < G::OHW;
