@@ -349,24 +349,35 @@ __global__ __launch_bounds__(256) void k_sum_parts_ep(const float *__restrict__ 
     out[i] = v;
 }
 
-// dW[co][j] / db[co] from partials laid out [p][co][ncols + 1] (column ncols = bias)
+// dW[co][j] / db[co] from partials laid out [p][co][ncols + 1] (column ncols = bias).  64
+// outputs per workgroup x 4 interleaved partial chains (p = g, g + 4, ...), 8 loads in flight
+// per chain, combined in a fixed tree: the same order on every call.
 __global__ __launch_bounds__(256) void k_sum_parts_wb(const float *__restrict__ parts, int np, int64_t pstride,
                                                       int rows, int ncols, float *__restrict__ dW,
                                                       float *__restrict__ db)
 {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ float red[4][64];
+    const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + j;
     const int64_t n = (int64_t)rows * (ncols + 1);
-    if (i >= n) return;
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int p = 0;
-    for (; p + 8 <= np; p += 8) {
+    float a = 0.f;
+    if (i < n) {
+        int p = g;
+        for (; p + 28 < np; p += 32) {
+            float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] += parts[(int64_t)(p + j) * pstride + i];
+            for (int u = 0; u < 8; ++u) v[u] = parts[(int64_t)(p + 4 * u) * pstride + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; p < np; p += 4) a += parts[(int64_t)p * pstride + i];
     }
-    for (; p < np; ++p) a[0] += parts[(int64_t)p * pstride + i];
-    const float v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-    const int co = (int)(i / (ncols + 1)), j = (int)(i - (int64_t)co * (ncols + 1));
-    if (j < ncols) dW[(int64_t)co * ncols + j] = v;
+    red[g][j] = a;
+    __syncthreads();
+    if (g != 0 || i >= n) return;
+    const float v = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
+    const int co = (int)(i / (ncols + 1)), c = (int)(i - (int64_t)co * (ncols + 1));
+    if (c < ncols) dW[(int64_t)co * ncols + c] = v;
     else db[co] = v;
 }
 
@@ -423,7 +434,7 @@ int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int
 {
     GS_REQUIRE(np >= 1 && rows >= 1 && ncols >= 1, "sum_parts_wb: bad sizes");
     const int64_t n = (int64_t)rows * (ncols + 1);
-    hipLaunchKernelGGL(k_sum_parts_wb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, parts, np, pstride, rows,
+    hipLaunchKernelGGL(k_sum_parts_wb, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, parts, np, pstride, rows,
                        ncols, dW, db);
     GS_LAUNCH_CHECK("k_sum_parts_wb");
     return GS_OK;
