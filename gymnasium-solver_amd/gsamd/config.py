@@ -60,13 +60,27 @@ class PPOConfig:
     episode_len: int = 200
     truncate_every: int = 0
     env_dynamics: str = "synthetic"   # "synthetic" (SURVEY §8d fixed-length episodes) | "cartpole" (f1)
+    # {param: {schedule, start_value, end_value, start, end, warmup}} (gsamd.schedules)
+    schedules: Dict[str, Dict[str, Any]] = field(default_factory=dict)
 
     def __post_init__(self):
+        self._resolve_schedules()
         self._resolve_numeric_strings()
         self._resolve_batch_size()
         self.validate()
 
     # --- reference-equivalent resolution -------------------------------------------
+    def _resolve_schedules(self):
+        """utils/config.py:626-655: dict-valued policy_lr / ent_coef start at their 'start'."""
+        from .schedules import parse_schedule_dict
+        self.schedules = dict(self.schedules or {})
+        for p in ("policy_lr", "ent_coef"):
+            v = getattr(self, p)
+            if isinstance(v, dict):
+                spec = parse_schedule_dict(v)
+                self.schedules[p] = spec
+                setattr(self, p, spec["start_value"])
+
     def _resolve_numeric_strings(self):
         for f in dataclasses.fields(self):
             v = getattr(self, f.name)
@@ -219,10 +233,14 @@ def from_reference_config(cfg: Any, **extras) -> PPOConfig:
     fields this path uses by name (enums are reduced to their ``value``)."""
     if isinstance(cfg, PPOConfig):
         return apply_overrides(cfg, extras) if extras else cfg
+    from .schedules import SCHEDULABLE, from_attributes
     kw: Dict[str, Any] = {}
     for name in _FIELDS:
-        if hasattr(cfg, name):
+        if hasattr(cfg, name) and name != "schedules":
             v = getattr(cfg, name)
             kw[name] = getattr(v, "value", v)
+    sched = {p: spec for p in SCHEDULABLE if (spec := from_attributes(cfg, p)) is not None}
+    if sched:
+        kw["schedules"] = sched
     kw.update(extras)
     return PPOConfig(**kw)

@@ -29,6 +29,7 @@ from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
+from .schedules import build_schedulers
 
 STAGES = ("train",)
 
@@ -55,8 +56,12 @@ class DevicePPOAgent:
         # schedulable hyper-parameters (base_agent.py:72-77)
         self.policy_lr = config.policy_lr
         self.clip_range = config.clip_range
+        self.clip_range_vf = config.clip_range_vf
         self.vf_coef = config.vf_coef
         self.ent_coef = config.ent_coef
+        # HyperparameterSchedulerCallback equivalents (schedule_resolver.py:54-124); positions
+        # in vector steps of the whole job (all ranks step in lockstep)
+        self.schedulers = build_schedulers(config.schedules, config.max_env_steps, config.n_envs * int(world_size))
         self.n_epochs = config.n_epochs
         self.current_epoch = 0
         self._early_stop_epoch = False
@@ -251,7 +256,7 @@ class DevicePPOAgent:
     def hparams(self) -> PPOHparams:
         c = self.config
         tkl = c.target_kl if c.target_kl is not None else 0.0
-        return PPOHparams(float(self.clip_range), float(c.clip_range_vf), float(self.vf_coef), float(self.ent_coef),
+        return PPOHparams(float(self.clip_range), float(self.clip_range_vf), float(self.vf_coef), float(self.ent_coef),
                           float(c.max_grad_norm if c.max_grad_norm is not None else 0.0), float(self.policy_lr),
                           0.9, 0.999, 1e-8, float(tkl), 1 if c.normalize_advantages == "batch" else 0, 0)
 
@@ -341,6 +346,22 @@ class DevicePPOAgent:
             ev[-1][2].record()
         self.adam_step += self.n_minibatches
         self.current_epoch += 1
+        self.on_train_epoch_end()
+
+    def set_hyperparameter(self, param: str, value: float) -> None:
+        """hyperparameter_mixin.py:105-114 (+ the policy_lr setter of callback_builder.py:108-113:
+        the next update's Adam step size is the attribute itself)."""
+        setattr(self, param, value)
+        if hasattr(self.config, param):
+            setattr(self.config, param, value)
+
+    def on_train_epoch_end(self) -> None:
+        """HyperparameterSchedulerCallback.on_train_epoch_end for every configured schedule."""
+        if not self.schedulers:
+            return
+        total = self.get_rollout_collector("train").total_vec_steps
+        for s in self.schedulers:
+            self.set_hyperparameter(s.parameter, s.value(total))
 
     def epoch_metrics(self) -> Dict[str, float]:
         """Reference metric keys (ppo_agent.py:131-146, torch.py:170-173), epoch means."""

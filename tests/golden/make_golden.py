@@ -446,6 +446,47 @@ def make_synth_env():
     print("synth_env.npz written")
 
 
+def make_schedules():
+    """Reference scheduler callback + position resolver on a grid of cases
+    (trainer_callbacks/hyperparameter_scheduler.py, utils/schedule_resolver.py)."""
+    from trainer_callbacks.hyperparameter_scheduler import HyperparameterSchedulerCallback
+    from utils.schedule_resolver import schedule_pos_to_vec_steps
+
+    class _Coll:
+        total_vec_steps = 0
+
+    class _Mod:
+        def __init__(self):
+            self.coll, self.got = _Coll(), None
+
+        def get_rollout_collector(self, stage):
+            return self.coll
+
+    steps = np.array([0, 5, 10, 37, 50, 64, 99, 100, 101, 150, 200, 250, 400], np.float64)
+    cases, values = [], []
+    for kind in ("linear", "cosine", "exponential"):
+        for warm in (0.0, 0.25):
+            for (sv, ev, s0, s1) in ((1e-3, 1e-4, 10.0, 200.0), (0.2, 0.05, 0.0, 100.0), (0.0, 0.01, 50.0, 50.0)):
+                cb = HyperparameterSchedulerCallback(schedule=kind, parameter="p", start_value=sv, end_value=ev,
+                                                     start_step=s0, end_step=s1, warmup_fraction=warm,
+                                                     set_value_fn=lambda m, v: setattr(m, "got", v))
+                mod, row = _Mod(), []
+                for t in steps:
+                    mod.coll.total_vec_steps = float(t)
+                    cb.on_train_epoch_end(None, mod)
+                    row.append(mod.got)
+                cases.append(f"{kind}|{warm}|{sv}|{ev}|{s0}|{s1}")
+                values.append(row)
+    pos = []
+    for raw, dmax, mx, n in ((None, False, 1e6, 8), (None, True, 1e6, 8), (0.5, False, 1e6, 8), (1.0, True, 2e5, 16),
+                             (4096.0, False, None, 8), (123456.0, True, 1e6, 32)):
+        pos.append([schedule_pos_to_vec_steps(raw, param="p", default_to_max=dmax, max_env_steps=mx, n_envs=n)])
+    out = {"cases": np.array(cases), "steps": steps, "values": np.array(values, np.float64),
+           "pos": np.array(pos, np.float64)}
+    np.savez_compressed(os.path.join(HERE, "schedules.npz"), **out)
+    print("schedules.npz written")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -459,3 +500,4 @@ if __name__ == "__main__":
     make_configs()
     make_synth_env()
     make_trajectory()
+    make_schedules()

@@ -86,3 +86,32 @@ def test_agent_trains_on_device_cartpole(cuda):
     assert np.isfinite(a.minibatch_losses()).all()
     m = a.get_rollout_collector("train").get_metrics()
     assert m["cnt/total_episodes"] > 0 and m["roll/ep_len/mean"] > 0
+
+
+def test_schedules_applied_between_epochs(cuda):
+    """A cosine policy_lr schedule and a linear ent_coef schedule move the next epoch's kernel
+    arguments exactly as HyperparameterSchedulerCallback.on_train_epoch_end would (SURVEY §8 a14);
+    a manual set_hyperparameter wins until the next epoch end."""
+    import torch
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    from gsamd.schedules import build_schedulers
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=8, n_epochs=1, max_env_steps=8 * 32 * 4))
+    cfg.schedules = {"policy_lr": {"schedule": "cosine", "start_value": 1e-3, "end_value": 1e-4, "start": 0.0,
+                                   "end": 1.0, "warmup": 0.0},
+                     "ent_coef": {"schedule": "linear", "start_value": 0.02, "end_value": 0.0, "start": 0.25,
+                                  "end": 0.75, "warmup": 0.0}}
+    agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
+    ref = {s.parameter: s for s in build_schedulers(cfg.schedules, cfg.max_env_steps, cfg.n_envs)}
+    for epoch in range(4):
+        agent.train_epoch()
+        t = agent.get_rollout_collector("train").total_vec_steps
+        assert t == 32 * (epoch + 1)
+        hp = agent.hparams()
+        assert hp.lr == float(np.float32(ref["policy_lr"].value(t)))          # kernel args are f32
+        assert hp.ent_coef == float(np.float32(ref["ent_coef"].value(t)))
+    assert abs(agent.policy_lr - 1e-4) < 1e-12            # the schedule's end
+    agent.set_hyperparameter("clip_range", 0.15)
+    assert abs(agent.hparams().clip_range - 0.15) < 1e-7 and cfg.clip_range == 0.15
+    assert np.isfinite(agent.minibatch_losses()).all()
