@@ -17,6 +17,27 @@ from ._lib import check, lib
 UNIQUE_ID_BYTES = 128
 
 
+def world_active() -> bool:
+    """True inside an initialised torch.distributed job of more than one rank."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def allreduce_sum_f64(values) -> "np.ndarray":
+    """Sum a small host vector over ranks (float64; per-epoch metric partial sums).
+    A no-op outside a multi-rank job."""
+    import numpy as np
+    v = np.asarray(values, dtype=np.float64)
+    if not world_active():
+        return v
+    import torch.distributed as dist
+    t = torch.from_numpy(v.copy())
+    if dist.get_backend() == "nccl":
+        t = t.to(torch.device("cuda", torch.cuda.current_device()))
+    dist.all_reduce(t)
+    return t.cpu().numpy()
+
+
 def env_offset(rank: int, n_envs_per_rank: int) -> int:
     """Global id of a rank's first env: rank g owns [g·N, (g+1)·N)."""
     return int(rank) * int(n_envs_per_rank)

@@ -29,6 +29,7 @@ from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
+from .distributed import allreduce_sum_f64, world_active
 from .schedules import build_schedulers
 
 STAGES = ("train",)
@@ -384,6 +385,10 @@ class DevicePPOAgent:
         if self.config.normalize_advantages == "batch":
             out["roll/adv/norm/mean"] = mean[M["adv_norm_mean"]]
             out["roll/adv/norm/std"] = mean[M["adv_norm_std"]]
+        if world_active():     # every rank ran the same number of minibatches: job mean = mean of means
+            keys = list(out)
+            vals = allreduce_sum_f64([out[k] for k in keys]) / float(self.world_size)
+            out = dict(zip(keys, vals))
         return {k: float(v) for k, v in out.items()}
 
     def minibatch_losses(self) -> np.ndarray:

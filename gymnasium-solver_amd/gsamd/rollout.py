@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from ._lib import check, lib, ptr, stream_handle
+from .distributed import allreduce_sum_f64
 from .rollout_stats import RollingWindow
 
 
@@ -392,8 +393,21 @@ class DeviceRolloutCollector:
              "cnt/total_rollouts": self.total_rollouts, "roll/env_steps": self.rollout_steps,
              "roll/vec_steps": self.rollout_vec_steps,
              "roll/fps": float(self.rollout_fpss.mean()) if self.rollout_fpss else 0.0}
+        # additive partial sums of every rank are summed before the means (one all-reduce of a
+        # small float64 vector per call in a multi-rank job): job-wide statistics
+        part = [self.rollout_steps]
         if self._stats is not None:
-            s = self._stats.cpu().numpy()
+            part += list(self._stats.cpu().numpy().astype(np.float64))
+        env = self.env
+        native = getattr(env, "device_native", False)
+        if native:
+            part += [float(env.ep_count.sum().item()), float(env.ep_ret_sum.sum().item()),
+                     float(env.ep_len_sum.sum().item())]
+        part = allreduce_sum_f64(part)
+        m["roll/env_steps"] = int(part[0])
+        m["cnt/total_env_steps"] = int(self.total_steps * (part[0] / max(self.rollout_steps, 1)))
+        if self._stats is not None:
+            s = part[1:11]
 
             def ms(sum_, sq, n):
                 mean = sum_ / max(n, 1)
@@ -402,12 +416,11 @@ class DeviceRolloutCollector:
             m["roll/reward/mean"], m["roll/reward/std"] = ms(s[3], s[4], s[9])
             m["roll/adv/mean"], m["roll/adv/std"] = ms(s[5], s[6], s[9])
             m["roll/return/mean"], m["roll/return/std"] = ms(s[7], s[8], s[9])
-        env = self.env
-        if getattr(env, "device_native", False):
-            cnt = env.ep_count.sum().item()
+        if native:
+            cnt, ret_sum, len_sum = part[-3:]
             if cnt > 0:
                 self.total_episodes = int(cnt)
-                m["roll/ep_rew/mean"] = float(env.ep_ret_sum.sum().item() / cnt)
-                m["roll/ep_len/mean"] = int(env.ep_len_sum.sum().item() / cnt)
+                m["roll/ep_rew/mean"] = float(ret_sum / cnt)
+                m["roll/ep_len/mean"] = int(len_sum / cnt)
         m["cnt/total_episodes"] = self.total_episodes
         return m

@@ -121,6 +121,13 @@ def dp_worker(rank, world, port, result_dir):
         ps = _gather(dist, p)
         assert all(np.array_equal(x.view(np.uint32), ps[0].view(np.uint32)) for x in ps), "replicas diverged"
         assert np.array_equal(p.view(np.uint32), p_loc.view(np.uint32)), "DP update != mean-gradient update"
+        # (5) per-epoch metric partial sums are summed over ranks (job-wide statistics)
+        from gsamd.distributed import allreduce_sum_f64, world_active
+        assert world_active()
+        part = np.array([rank + 1.0, 10.0 * (rank + 1), 0.5], np.float64)
+        tot = allreduce_sum_f64(part)
+        assert np.array_equal(tot, np.array([sum(r + 1.0 for r in range(world)),
+                                             sum(10.0 * (r + 1) for r in range(world)), 0.5 * world]))
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()
