@@ -138,7 +138,11 @@ def test_reference_init_reproduces_reference_weights(golden):
     torch.manual_seed(42)
     sd = reference_init(4, (256, 256), 2)
     flat = torch.cat([t.reshape(-1) for t in sd.values()]).numpy()
-    assert np.array_equal(flat, z["params0"])
+    # Same RNG consumption as utils/torch.py:204-258; the orthogonal factor comes from the
+    # host's LAPACK QR, whose last bits depend on the CPU model and thread count,
+    # so the trajectory parity tests start from the committed params0, and this check is 1e-5.
+    np.testing.assert_allclose(flat, z["params0"], rtol=0, atol=1e-5)
+    assert np.array_equal(flat == 0, z["params0"] == 0)
 
 
 def test_product_does_not_import_oracle():
