@@ -104,6 +104,45 @@ def time_stages(agent, reps: int):
     return out, fused
 
 
+def time_gae(agent, reps: int):
+    """Average device duration of the GAE scan (gs_gae_f32) on this workload's rollout buffer:
+    `reps` launches captured into a hipGraph, replayed between HIP events on the launch
+    stream; writes into scratch outputs (the inputs are the last rollout's)."""
+    from gsamd.rollout import compute_batched_gae_advantages_and_returns as gae
+    buf = agent.get_rollout_collector("train").buffer
+    coll = agent.get_rollout_collector("train")
+    adv, ret = torch.empty_like(buf.advantages), torch.empty_like(buf.returns)
+    args = (buf.values, buf.rewards, buf.dones, buf.timeouts, buf.last_values, buf.bootstrapped_values,
+            coll.gamma, coll.gae_lambda)
+    gae(*args, adv_out=adv, ret_out=ret)
+    torch.cuda.synchronize()
+    if not (torch.equal(adv, buf.advantages) and torch.equal(ret, buf.returns)):
+        raise RuntimeError("GAE replay differs from the rollout's own advantages")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        for _ in range(reps):
+            gae(*args, adv_out=adv, ret_out=ret)
+    g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    e1.synchronize()
+    T, N = buf.values.shape
+    return e0.elapsed_time(e1) / reps * 1e3, int(T), int(N)
+
+
+def roofline_entry(bound: str, amount: float, us: float, kernel: str) -> dict:
+    if bound == "mfma":
+        a = amount / (us * 1e-6) / 1e12
+        return {"bound": "mfma", "achieved": round(a, 4), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(a / PEAK_F32_MFMA_TFLOPS, 6), "kernel": kernel, "avg_us": round(us, 3),
+                "work_per_launch": amount}
+    a = amount / (us * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": round(a, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(a / PEAK_HBM_GBS, 6), "kernel": kernel, "avg_us": round(us, 3), "work_per_launch": amount}
+
+
 def time_exchange(comm, n: int, reps: int, device, barrier):
     """Average duration of one gradient exchange of n floats (all ranks replay a graph of
     `reps` exchanges together after a barrier; HIP events on this rank's stream)."""
@@ -234,6 +273,7 @@ def main():
     # ---- roofline of the dominant minibatch kernel (device time by events) ----
     pm = agent.policy_model
     stage_us = {}
+    rooflines = {}
     if pixel:
         # the update is a chain of GEMMs + fused kernels per minibatch: price the whole
         # minibatch step (events around the update phase of the timed region) against MFMA
@@ -249,18 +289,16 @@ def main():
         work = stage_flops_bytes(pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions, agent.batch_size,
                                  pm.n_params, fused)
         dom = max(stage_us, key=stage_us.get)
-        bound, amount = work[dom]
-        if bound == "mfma":
-            achieved = amount / (stage_us[dom] * 1e-6) / 1e12
-            roofline = {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32_MFMA_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 6), "traffic": None}
-        else:
-            achieved = amount / (stage_us[dom] * 1e-6) / 1e9
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(achieved / PEAK_HBM_GBS, 6), "traffic": None}
-        roofline["kernel"] = {"fwd": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}[dom]
-        roofline["avg_us"] = round(stage_us[dom], 3)
-        roofline["work_per_launch"] = amount
+        kname = {"fwd": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}
+        for st, us in stage_us.items():
+            rooflines[st] = roofline_entry(work[st][0], work[st][1], us, kname[st])
+        roofline = {k: v for k, v in rooflines[dom].items()}
+        roofline["traffic"] = None
+    # GAE scan on this workload's rollout buffer (HBM-bound; 22 B/element + 4 B/env)
+    gae_us, gT, gN = time_gae(agent, args.stage_reps)
+    rooflines["gae"] = roofline_entry("hbm", 22.0 * gT * gN + 4.0 * gN, gae_us,
+                                      "k_gae_staged" if gN % 4 == 0 else "k_gae_f32")
+    rooflines["gae"]["shape"] = [gT, gN]
     if comm is not None:       # every rank takes part (the exchange is collective)
         stage_us["exchange"] = time_exchange(comm, pm.n_params, args.stage_reps, device, barrier)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -313,6 +351,7 @@ def main():
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph,
                        "grad_exchange": args.comm if comm is not None else None},
             "roofline": roofline,
+            "rooflines": rooflines,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},
             "phases_ms": {"collect": round(collect_ms, 3), "update": round(update_ms, 3),
                           "update_us_per_minibatch": round(update_ms * 1e3 / agent.n_minibatches, 3)},

@@ -34,8 +34,13 @@ def test_gae_bit_exact_vs_reference_fixtures(golden, cuda):
         assert np.array_equal(ret.cpu().numpy().view(np.uint32), c["ret"].view(np.uint32)), n
 
 
-@pytest.mark.parametrize("T,N", [(32, 4096), (2048, 1024), (7, 3000), (1, 1)])
-def test_gae_bit_exact_vs_c_oracle_full_size(cuda, T, N):
+# staged kernel: EW 16 (N % 16 == 0), 8, 4 with full / partial / half chunks; per-lane
+# kernel: N % 4 != 0 (and forced through GS_GAE_KERNEL=lane below); with and without the
+# bootstrap buffer
+@pytest.mark.parametrize("T,N,boot", [(32, 4096, True), (2048, 1024, True), (7, 3000, True), (1, 1, True),
+                                      (130, 1028, True), (64, 16, True), (65, 32, False), (200, 4104, False),
+                                      (97, 4098, True), (40, 6, False)])
+def test_gae_bit_exact_vs_c_oracle_full_size(cuda, T, N, boot):
     import oracle
     from gsamd.rollout import compute_batched_gae_advantages_and_returns as gae
     rng = np.random.default_rng(T * 7 + N)
@@ -44,12 +49,33 @@ def test_gae_bit_exact_vs_c_oracle_full_size(cuda, T, N):
     d = (rng.random((T, N)) < 0.05).astype(np.uint8)
     to = (d.astype(bool) & (rng.random((T, N)) < 0.3)).astype(np.uint8)
     lv = rng.standard_normal(N).astype(np.float32)
-    b = rng.standard_normal((T, N)).astype(np.float32)
-    a_ref, r_ref = oracle.gae_c(v, r, d, to, lv, b, 0.99, 0.95)
-    adv, ret = gae(_dev(v, cuda), _dev(r, cuda), _dev(d, cuda), _dev(to, cuda), _dev(lv, cuda), _dev(b, cuda),
-                   0.99, 0.95)
+    b = rng.standard_normal((T, N)).astype(np.float32) if boot else None
+    a_ref, r_ref = oracle.gae_c(v, r, d, to, lv, b if boot else np.zeros((T, N), np.float32), 0.99, 0.95)
+    if not boot:   # without the buffer the reference's timeouts bootstrap from v[t+1] (oracle: b = v shifted)
+        nv = np.concatenate([v[1:], lv[None]], 0)
+        a_ref, r_ref = oracle.gae_c(v, r, d, to, lv, nv, 0.99, 0.95)
+    adv, ret = gae(_dev(v, cuda), _dev(r, cuda), _dev(d, cuda), _dev(to, cuda), _dev(lv, cuda),
+                   _dev(b, cuda) if boot else None, 0.99, 0.95)
     assert np.array_equal(adv.cpu().numpy().view(np.uint32), a_ref.view(np.uint32))
     assert np.array_equal(ret.cpu().numpy().view(np.uint32), r_ref.view(np.uint32))
+
+
+def test_gae_lane_and_staged_kernels_agree(cuda, monkeypatch):
+    """Both device kernels on the same inputs (the per-lane one forced): bitwise equal."""
+    from gsamd.rollout import compute_batched_gae_advantages_and_returns as gae
+    rng = np.random.default_rng(5)
+    T, N = 300, 2048
+    arrs = [rng.standard_normal((T, N)).astype(np.float32) for _ in range(3)]
+    d = (rng.random((T, N)) < 0.05).astype(np.uint8)
+    to = (d.astype(bool) & (rng.random((T, N)) < 0.5)).astype(np.uint8)
+    lv = rng.standard_normal(N).astype(np.float32)
+    args = [_dev(arrs[0], cuda), _dev(arrs[1], cuda), _dev(d, cuda), _dev(to, cuda), _dev(lv, cuda),
+            _dev(arrs[2], cuda), 0.98, 0.8]
+    a1, r1 = gae(*args)
+    monkeypatch.setenv("GS_GAE_KERNEL", "lane")
+    a2, r2 = gae(*args)
+    assert torch.equal(a1.view(torch.int32), a2.view(torch.int32))
+    assert torch.equal(r1.view(torch.int32), r2.view(torch.int32))
 
 
 def test_gae_empty_is_noop(cuda):
