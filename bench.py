@@ -302,12 +302,21 @@ def main():
     if comm is not None:       # every rank takes part (the exchange is collective)
         stage_us["exchange"] = time_exchange(comm, pm.n_params, args.stage_reps, device, barrier)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path) and args.workload == "C2":   # the committed PMC passes are C2-shaped
+    if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
-                roofline["traffic"] = json.load(f).get(roofline["kernel"], {}).get("hbm_bytes_per_launch")
+                pmc = json.load(f)
         except (OSError, ValueError):
-            pass
+            pmc = {}
+        if args.workload == "C2":   # the committed minibatch-kernel PMC passes are C2-shaped
+            roofline["traffic"] = pmc.get(roofline["kernel"], {}).get("hbm_bytes_per_launch")
+            for st, ent in rooflines.items():
+                if st != "gae":
+                    ent["traffic"] = pmc.get(ent["kernel"], {}).get("hbm_bytes_per_launch")
+        # the GAE passes are keyed by grid size (tools/pmc_run.py: C2 and C3 shapes)
+        ew = 16 if gN % 16 == 0 else 8 if gN % 8 == 0 else 4
+        grid = (gN // ew) * (8 if ew >= 8 else 4) * 64
+        rooflines["gae"]["traffic"] = pmc.get(f"k_gae_staged[grid={grid}]", {}).get("hbm_bytes_per_launch")
 
     # ---- CPU baseline (rank 0, N=1 only): oracle restatement on the host cores ----
     cpu = None

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Workload for the rocprofv3 --pmc passes (profiles/pmc_traffic.json): one C2 rollout, then
 `--reps` eager launches of each fused-chain minibatch kernel through gs_ppo_stage (no hipGraph, so
-every dispatch is a separate counter record).  Run under
+every dispatch is a separate counter record), then the GAE scan at the C2 and C3 shapes.  Run under
   rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d DIR -o pmc_fetch -- python tools/pmc_run.py
   rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d DIR -o pmc_write -- python tools/pmc_run.py
 and reduce with tools/pmc_summarize.py."""
@@ -40,6 +40,19 @@ def main():
     for st in (4, 5, 3):         # k_fwd_hidden<fused>, k_bwd<fused>, k_clip_adam
         for _ in range(a.reps):
             stage(st)
+    # the GAE scan on the C2 rollout buffer, and on a C3-shaped (2048 x 1024) random rollout
+    from gsamd.rollout import compute_batched_gae_advantages_and_returns as gae
+    buf = agent.get_rollout_collector("train").buffer
+    for _ in range(8):
+        gae(buf.values, buf.rewards, buf.dones, buf.timeouts, buf.last_values, buf.bootstrapped_values, 0.98, 0.8,
+            adv_out=torch.empty_like(buf.advantages), ret_out=torch.empty_like(buf.returns))
+    T, N = 2048, 1024
+    v, r, b = (torch.randn(T, N, device="cuda:0") for _ in range(3))
+    d = (torch.rand(T, N, device="cuda:0") < 0.05).to(torch.uint8)
+    to = (d.bool() & (torch.rand(T, N, device="cuda:0") < 0.3)).to(torch.uint8)
+    lv = torch.randn(N, device="cuda:0")
+    for _ in range(8):
+        gae(v, r, d, to, lv, b, 0.99, 0.95)
     torch.cuda.synchronize()
     print("pmc_run done")
 

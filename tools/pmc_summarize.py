@@ -11,8 +11,9 @@ import re
 import sys
 from collections import defaultdict
 
-SHORT = ("k_fwd_hidden", "k_loss", "k_bwd", "k_clip_adam", "k_heads_act", "k_gae_f32", "k_env_step",
+SHORT = ("k_fwd_hidden", "k_loss", "k_bwd", "k_clip_adam", "k_heads_act", "k_gae_f32", "k_gae_staged", "k_env_step",
          "k_reduce_part1", "k_sumsq_flat")
+BY_GRID = ("k_gae_staged", "k_gae_f32")   # one kernel at several shapes: keyed by grid size
 
 
 def short(name):
@@ -29,6 +30,8 @@ def load(path, counter):
             if row.get("Counter_Name") != counter:
                 continue
             k = short(row.get("Kernel_Name", ""))
+            if k in BY_GRID:
+                k = f"{k}[grid={row.get('Grid_Size', '?')}]"
             if k:
                 per[k].append(float(row["Counter_Value"]))
     return per
