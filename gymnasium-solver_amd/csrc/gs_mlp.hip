@@ -1139,7 +1139,10 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
 // k_clip_adam: grid ceil(P / 1024), 256 threads, 4 params per thread (strided).
 // ------------------------------------------------------------------------------------
 
-template <class S>
+// NRB > 0 (the C2 shapes: NRB row blocks, NU = ceil(H1*(D+1)/256) partial entries per
+// thread): the dW1|db1 partials go straight to registers with every load in flight at once,
+// are folded there in row-block order, and only the folded values pass through LDS.
+template <class S, int NRB, int NU>
 __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layout Lrt, float *__restrict__ G,
                                                    float *__restrict__ M, float *__restrict__ V,
                                                    const float *__restrict__ part1, const float *__restrict__ sumsq,
@@ -1186,11 +1189,45 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     extern __shared__ float stage[];
     double ss = 0.0;
     const int64_t npart = (int64_t)aa.nrb * n1;
-    if (aa.stage_lds) {
+    if constexpr (NRB > 0) {
+        copy_to_lds(stage, sumsq, aa.n_slots);
+        float t[NU][NRB];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            const int64_t u = tid + 256 * j;
+#pragma unroll
+            for (int rb = 0; rb < NRB; ++rb) t[j][rb] = u < n1 ? part1[(int64_t)rb * n1 + u] : 0.0f;
+        }
+        float *w1s = stage + round4(aa.n_slots);
+        float gsum[NU];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            const int64_t u = tid + 256 * j;
+            float g = 0.0f;
+#pragma unroll
+            for (int rb = 0; rb < NRB; ++rb) g += t[j][rb];
+            gsum[j] = g;
+            if (u < n1) w1s[u] = g;
+        }
+        __syncthreads();
+        GS_STAMP(0)
+        if (base < L.oW2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t p = base + j * 256 + tid;
+                if (p < L.oW2) gv[j] = w1s[part1_index(L, p)];
+            }
+        }
+        for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)stage[s0];
+#pragma unroll
+        for (int j = 0; j < NU; ++j)
+            if (tid + 256 * j < n1) ss += (double)gsum[j] * (double)gsum[j];
+    } else if (aa.stage_lds) {
         copy_to_lds(stage, sumsq, aa.n_slots);
         const int off = round4(aa.n_slots);
         if (npart > 0) copy_to_lds(stage + off, part1, (int)npart);
         __syncthreads();
+        GS_STAMP(0)
         if (aa.nrb > 0 && base < L.oW2) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1210,6 +1247,7 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
             ss += (double)g * (double)g;
         }
     } else {
+        GS_STAMP(0)
         for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)sumsq[s0];
         for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
             float g = 0.0f;
@@ -1217,10 +1255,10 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
             ss += (double)g * (double)g;
         }
     }
-    GS_STAMP(0)
+    GS_STAMP(1)
     double tt[1] = {ss};
     block_reduce<1>(tt, sred);
-    GS_STAMP(1)
+    GS_STAMP(2)
     if (tid == 0) {
         const double tot = tt[0];
         const float total = (float)sqrt(tot) * aa.grad_scale;
@@ -1251,7 +1289,7 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
         M[p] = m;
         V[p] = v;
     }
-    GS_STAMP_END(2)
+    GS_STAMP_END(3)
 }
 
 // sum of squares over a flat range (multi-GPU path: norm after the all-reduce)
@@ -1390,8 +1428,13 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
     aa.stage_lds = stage <= 65536 ? 1 : 0;
     const unsigned nblk = (unsigned)((L.P + 1023) / 1024);
     return with_shape(L, 0, [&](auto sh) {
-        hipLaunchKernelGGL(k_clip_adam<decltype(sh)>, dim3(nblk), dim3(256), aa.stage_lds ? stage : 0, s, P, L, G, M,
-                           V, part1, sumsq, aa, metrics, stop);
+        const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
+        if (aa.nrb == 8 && aa.stage_lds && (n1 + 255) / 256 == 5)   // C2 shapes: B = 256, H1 (D+1) = 1280
+            hipLaunchKernelGGL((k_clip_adam<decltype(sh), 8, 5>), dim3(nblk), dim3(256), stage, s, P, L, G, M, V,
+                               part1, sumsq, aa, metrics, stop);
+        else
+            hipLaunchKernelGGL((k_clip_adam<decltype(sh), 0, 0>), dim3(nblk), dim3(256), aa.stage_lds ? stage : 0, s,
+                               P, L, G, M, V, part1, sumsq, aa, metrics, stop);
         GS_LAUNCH_CHECK("k_clip_adam");
         return GS_OK;
     });

@@ -43,7 +43,7 @@ cnt = (cnt - cnt0).astype(np.float64)
 names = {0: ("k_fwd_hidden", ["load operands", "row gather", "h1", "mfma h2", "h2 out + heads"]),
          1: ("k_loss", ["inputs + adv norm", "per-row loss/grad", "reduce", "metrics"]),
          2: ("k_bwd roleA blk0", ["load tiles", "dh2", "mfma dW2", "store + sumsq + db2"]),
-         3: ("k_clip_adam blk0", ["loads + norm partial", "reduce", "adam"]),
+         3: ("k_clip_adam blk0", ["own loads + LDS staging", "W1 fold + norm loops", "reduce", "adam"]),
          4: ("k_bwd roleB blk0", ["load slab", "dh2", "mfma dh1", "dW1 partial"]),
          5: ("k_bwd roleC blk0", ["load", "reduce + store"])}
 for k, (n, phases) in names.items():
