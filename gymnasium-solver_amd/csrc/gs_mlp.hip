@@ -1139,10 +1139,13 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
 // k_clip_adam: grid ceil(P / 1024), 256 threads, 4 params per thread (strided).
 // ------------------------------------------------------------------------------------
 
-// NRB > 0 (the C2 shapes: NRB row blocks, NU = ceil(H1*(D+1)/256) partial entries per
-// thread): the dW1|db1 partials go straight to registers with every load in flight at once,
-// are folded there in row-block order, and only the folded values pass through LDS.
-template <class S, int NRB, int NU>
+// Vectorised variant for the C2 shapes (NRB > 0: NRB row blocks of dW1|db1 partials; NQ =
+// ceil(H1*(D+1)/1024) float4 partial columns per thread; oW2, H1*(D+1) multiples of 4 and
+// 16-B aligned buffers, checked by the launcher): each thread owns 4 consecutive parameters
+// (float4 loads / stores of p, g, m, v), the partials go straight to registers as float4
+// with every load in flight at once, are folded there in row-block order, and only the folded
+// values pass through LDS.  The generic variant (NRB == 0) stages the partials in LDS.
+template <class S, int NRB, int NQ>
 __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layout Lrt, float *__restrict__ G,
                                                    float *__restrict__ M, float *__restrict__ V,
                                                    const float *__restrict__ part1, const float *__restrict__ sumsq,
@@ -1158,101 +1161,136 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     const Layout L = S::lay(Lrt);
     const int tid = threadIdx.x;
     const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
-    // ---- this block's parameters and optimizer state: loads issued first
     const int64_t base = (int64_t)blockIdx.x * 1024;
-    float gv[4], mv[4], vv[4], pv[4];
-    // W1|b1 gradients come from the dW1|db1 partials: summed after they are staged in LDS
-    // (below) when staging is on, instead of 4 x nrb dependent global loads here
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int64_t p = base + j * 256 + tid;
-        const bool ok = p < L.P;
-        float g = 0.0f;
-        if (ok) {
-            if (aa.nrb > 0 && p < L.oW2) {
-                if (!aa.stage_lds) {
-                    const int64_t u = part1_index(L, p);
-#pragma unroll 4
-                    for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
-                }
-            } else {
-                g = G[p];
-            }
-        }
-        gv[j] = g;
-        mv[j] = ok ? M[p] : 0.0f;
-        vv[j] = ok ? V[p] : 0.0f;
-        pv[j] = ok ? Pm[p] : 0.0f;
-    }
-    // ---- global squared norm (same order in every workgroup -> identical coef).  The
-    //      per-tile sums and dW1/db1 partials are staged into LDS in one burst first.
     extern __shared__ float stage[];
     double ss = 0.0;
-    const int64_t npart = (int64_t)aa.nrb * n1;
+    float gv[4], mv[4], vv[4], pv[4];
+    // this thread's parameters: p0 + i (vectorised) or base + i*256 + tid (generic)
+    const int64_t p0 = base + 4 * tid;
+    auto pidx = [&](int i) -> int64_t { return NRB > 0 ? p0 + i : base + i * 256 + tid; };
     if constexpr (NRB > 0) {
+        const bool full = p0 + 3 < L.P;
+        if (full) {
+            const float4 g4 = p0 >= L.oW2 ? *reinterpret_cast<const float4 *>(G + p0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 m4 = *reinterpret_cast<const float4 *>(M + p0);
+            const float4 v4 = *reinterpret_cast<const float4 *>(V + p0);
+            const float4 q4 = *reinterpret_cast<const float4 *>(Pm + p0);
+            gv[0] = g4.x, gv[1] = g4.y, gv[2] = g4.z, gv[3] = g4.w;
+            mv[0] = m4.x, mv[1] = m4.y, mv[2] = m4.z, mv[3] = m4.w;
+            vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
+            pv[0] = q4.x, pv[1] = q4.y, pv[2] = q4.z, pv[3] = q4.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t p = p0 + i;
+                const bool ok = p < L.P;
+                gv[i] = ok && p >= L.oW2 ? G[p] : 0.0f;
+                mv[i] = ok ? M[p] : 0.0f;
+                vv[i] = ok ? V[p] : 0.0f;
+                pv[i] = ok ? Pm[p] : 0.0f;
+            }
+        }
         copy_to_lds(stage, sumsq, aa.n_slots);
-        float t[NU][NRB];
+        float4 t[NQ][NRB];
 #pragma unroll
-        for (int j = 0; j < NU; ++j) {
-            const int64_t u = tid + 256 * j;
+        for (int j = 0; j < NQ; ++j) {
+            const int64_t q = tid + 256 * j;
 #pragma unroll
-            for (int rb = 0; rb < NRB; ++rb) t[j][rb] = u < n1 ? part1[(int64_t)rb * n1 + u] : 0.0f;
+            for (int rb = 0; rb < NRB; ++rb)
+                t[j][rb] = 4 * q < n1 ? *reinterpret_cast<const float4 *>(part1 + (int64_t)rb * n1 + 4 * q)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         float *w1s = stage + round4(aa.n_slots);
-        float gsum[NU];
+        float4 gsum[NQ];
 #pragma unroll
-        for (int j = 0; j < NU; ++j) {
-            const int64_t u = tid + 256 * j;
-            float g = 0.0f;
+        for (int j = 0; j < NQ; ++j) {
+            const int64_t q = tid + 256 * j;
+            float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-            for (int rb = 0; rb < NRB; ++rb) g += t[j][rb];
+            for (int rb = 0; rb < NRB; ++rb) {
+                g.x += t[j][rb].x;
+                g.y += t[j][rb].y;
+                g.z += t[j][rb].z;
+                g.w += t[j][rb].w;
+            }
             gsum[j] = g;
-            if (u < n1) w1s[u] = g;
+            if (4 * q < n1) *reinterpret_cast<float4 *>(w1s + 4 * q) = g;
         }
         __syncthreads();
         GS_STAMP(0)
-        if (base < L.oW2) {
+        if (p0 < L.oW2) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t p = base + j * 256 + tid;
-                if (p < L.oW2) gv[j] = w1s[part1_index(L, p)];
-            }
+            for (int i = 0; i < 4; ++i) gv[i] = w1s[part1_index(L, p0 + i)];
         }
         for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)stage[s0];
 #pragma unroll
-        for (int j = 0; j < NU; ++j)
-            if (tid + 256 * j < n1) ss += (double)gsum[j] * (double)gsum[j];
-    } else if (aa.stage_lds) {
-        copy_to_lds(stage, sumsq, aa.n_slots);
-        const int off = round4(aa.n_slots);
-        if (npart > 0) copy_to_lds(stage + off, part1, (int)npart);
-        __syncthreads();
-        GS_STAMP(0)
-        if (aa.nrb > 0 && base < L.oW2) {
+        for (int j = 0; j < NQ; ++j)
+            if (4 * (tid + 256 * j) < n1) {
+                const float4 g = gsum[j];
+                ss += (double)g.x * (double)g.x;
+                ss += (double)g.y * (double)g.y;
+                ss += (double)g.z * (double)g.z;
+                ss += (double)g.w * (double)g.w;
+            }
+    } else {
+        // W1|b1 gradients come from the dW1|db1 partials: summed after they are staged in
+        // LDS (below) when staging is on, instead of 4 x nrb dependent global loads here
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t p = base + j * 256 + tid;
-                if (p < L.oW2) {
-                    const int64_t u = part1_index(L, p);
-                    float g = 0.0f;
-                    for (int rb = 0; rb < aa.nrb; ++rb) g += stage[off + rb * n1 + u];
-                    gv[j] = g;
+        for (int j = 0; j < 4; ++j) {
+            const int64_t p = pidx(j);
+            const bool ok = p < L.P;
+            float g = 0.0f;
+            if (ok) {
+                if (aa.nrb > 0 && p < L.oW2) {
+                    if (!aa.stage_lds) {
+                        const int64_t u = part1_index(L, p);
+#pragma unroll 4
+                        for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
+                    }
+                } else {
+                    g = G[p];
                 }
             }
+            gv[j] = g;
+            mv[j] = ok ? M[p] : 0.0f;
+            vv[j] = ok ? V[p] : 0.0f;
+            pv[j] = ok ? Pm[p] : 0.0f;
         }
-        for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)stage[s0];
-        for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
-            float g = 0.0f;
-            for (int rb = 0; rb < aa.nrb; ++rb) g += stage[off + rb * n1 + u];
-            ss += (double)g * (double)g;
-        }
-    } else {
-        GS_STAMP(0)
-        for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)sumsq[s0];
-        for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
-            float g = 0.0f;
-            for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
-            ss += (double)g * (double)g;
+        // global squared norm (same order in every workgroup -> identical coef); the
+        // per-tile sums and dW1/db1 partials are staged into LDS in one burst first
+        const int64_t npart = (int64_t)aa.nrb * n1;
+        if (aa.stage_lds) {
+            copy_to_lds(stage, sumsq, aa.n_slots);
+            const int off = round4(aa.n_slots);
+            if (npart > 0) copy_to_lds(stage + off, part1, (int)npart);
+            __syncthreads();
+            GS_STAMP(0)
+            if (aa.nrb > 0 && base < L.oW2) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t p = pidx(j);
+                    if (p < L.oW2) {
+                        const int64_t u = part1_index(L, p);
+                        float g = 0.0f;
+                        for (int rb = 0; rb < aa.nrb; ++rb) g += stage[off + rb * n1 + u];
+                        gv[j] = g;
+                    }
+                }
+            }
+            for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)stage[s0];
+            for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
+                float g = 0.0f;
+                for (int rb = 0; rb < aa.nrb; ++rb) g += stage[off + rb * n1 + u];
+                ss += (double)g * (double)g;
+            }
+        } else {
+            GS_STAMP(0)
+            for (int s0 = tid; s0 < aa.n_slots; s0 += 256) ss += (double)sumsq[s0];
+            for (int64_t u = tid; u < n1 && aa.nrb > 0; u += 256) {
+                float g = 0.0f;
+                for (int rb = 0; rb < aa.nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
+                ss += (double)g * (double)g;
+            }
         }
     }
     GS_STAMP(1)
@@ -1274,20 +1312,35 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     const float coef = s_coef * aa.grad_scale;
     const float neg_step = aa.sched ? aa.sched[2 * (aa.sched_idx + kb)] : aa.neg_step_size;
     const float bc2s = aa.sched ? aa.sched[2 * (aa.sched_idx + kb) + 1] : aa.bc2_sqrt;
+    float go[4], mo[4], vo[4], po[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int64_t p = base + j * 256 + tid;
-        if (p >= L.P) break;
         const float g = gv[j] * coef;
-        G[p] = g;
         float m = mv[j], v = vv[j];
         m = m + aa.one_minus_b1 * (g - m);            // exp_avg.lerp_(grad, 1 - beta1)
         v = v * aa.b2;                                // exp_avg_sq.mul_(beta2)
         v = v + (aa.one_minus_b2 * g) * g;            //   .addcmul_(grad, grad, 1 - beta2)
         const float denom = sqrtf(v) / bc2s + aa.eps;
-        Pm[p] = pv[j] + neg_step * (m / denom);
-        M[p] = m;
-        V[p] = v;
+        go[j] = g;
+        mo[j] = m;
+        vo[j] = v;
+        po[j] = pv[j] + neg_step * (m / denom);
+    }
+    if (NRB > 0 && p0 + 3 < L.P) {
+        *reinterpret_cast<float4 *>(G + p0) = make_float4(go[0], go[1], go[2], go[3]);
+        *reinterpret_cast<float4 *>(Pm + p0) = make_float4(po[0], po[1], po[2], po[3]);
+        *reinterpret_cast<float4 *>(M + p0) = make_float4(mo[0], mo[1], mo[2], mo[3]);
+        *reinterpret_cast<float4 *>(V + p0) = make_float4(vo[0], vo[1], vo[2], vo[3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t p = pidx(j);
+            if (p >= L.P) break;
+            G[p] = go[j];
+            Pm[p] = po[j];
+            M[p] = mo[j];
+            V[p] = vo[j];
+        }
     }
     GS_STAMP_END(3)
 }
@@ -1429,8 +1482,10 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
     const unsigned nblk = (unsigned)((L.P + 1023) / 1024);
     return with_shape(L, 0, [&](auto sh) {
         const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
-        if (aa.nrb == 8 && aa.stage_lds && (n1 + 255) / 256 == 5)   // C2 shapes: B = 256, H1 (D+1) = 1280
-            hipLaunchKernelGGL((k_clip_adam<decltype(sh), 8, 5>), dim3(nblk), dim3(256), stage, s, P, L, G, M, V,
+        const bool al = (((uintptr_t)P | (uintptr_t)G | (uintptr_t)M | (uintptr_t)V | (uintptr_t)part1) & 15) == 0;
+        if (aa.nrb == 8 && aa.stage_lds && n1 % 4 == 0 && L.oW2 % 4 == 0 && (n1 / 4 + 255) / 256 == 2 && al)
+            // C2 shapes: B = 256 (8 row blocks of 32), H1 (D+1) = 1280
+            hipLaunchKernelGGL((k_clip_adam<decltype(sh), 8, 2>), dim3(nblk), dim3(256), stage, s, P, L, G, M, V,
                                part1, sumsq, aa, metrics, stop);
         else
             hipLaunchKernelGGL((k_clip_adam<decltype(sh), 0, 0>), dim3(nblk), dim3(256), aa.stage_lds ? stage : 0, s,
