@@ -106,13 +106,13 @@ __host__ __device__ __forceinline__ int64_t part1_index(const Layout &L, int64_t
 // configs are instantiated this way.  ShapeR keeps them runtime (any other MLP shape).
 template <int D_, int H1_, int H2_, int A_, int B_>
 struct ShapeC {
-    static constexpr int AMAX = A_, AEX = A_, H1c = H1_;
+    static constexpr int AMAX = A_, AEX = A_, H1c = H1_, Bc = B_;
     __host__ __device__ static constexpr Layout lay(const Layout &) { return Layout::make(D_, H1_, H2_, A_); }
     __host__ __device__ static constexpr int batch(int b) { return B_ > 0 ? B_ : b; }
 };
 template <int AMAX_>
 struct ShapeR {
-    static constexpr int AMAX = AMAX_, AEX = 0, H1c = 0;
+    static constexpr int AMAX = AMAX_, AEX = 0, H1c = 0, Bc = 0;
     __host__ __device__ static Layout lay(const Layout &L) { return L; }
     __host__ __device__ static int batch(int b) { return b; }
 };

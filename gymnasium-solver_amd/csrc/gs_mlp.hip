@@ -724,7 +724,7 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
                           kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024 +
                           (int64_t)kRowsB * n_col_blocks(L.H2);
-    const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + A1 * 256;
+    const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + (A1 * 256 > 1024 ? A1 * 256 : 1024);
     int64_t m = roleA;
     if (roleB > m) m = roleB;
     if (roleC > m) m = roleC;
@@ -787,7 +787,6 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                                              const float *__restrict__ zpart, FusedFwd ff, LossArgs la,
                                              const uint16_t *__restrict__ h2mask)
 {
-    GS_STAMP_BEGIN(2)
     if (stop && *stop) return;
     extern __shared__ float lds[];
     __shared__ float sbuf[272];
@@ -806,6 +805,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         // ---------------- role A: dW2[n0:n0+16, k0:k0+16] = sum_b dh2[b,n] h1[b,k]
         const int nb = bid / sh.nkb, kb = bid - nb * sh.nkb;
         const int n0 = nb * kTile, k0 = kb * kTile;
+        GS_STAMP_BEGIN_IF(2, bid == 0)
         const int Bp = (B + 63) / 64 * 64;      // padded K (batch) for 4 waves x 16
         const int ld = Bp + 4;
         float *dzs = lds;                            // [B][A1]
@@ -935,7 +935,71 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         // (fused path): the loss math overlaps the loads instead of following them
         constexpr int kLd = FUSED ? 192 : 256;
         int *mkB = reinterpret_cast<int *>(kred + 1024);   // [32][ncb] relu'(h2) bits
-        if (!FUSED || tid < kLd) {
+        if constexpr (S::H1c > 0 && S::Bc > 0) {
+            // compile-time shapes: every operand load of the slab is issued before the first
+            // LDS write (one memory round trip instead of one per operand loop)
+            constexpr Layout Lc = S::lay(Layout{});
+            constexpr int cH1 = Lc.H1, cH2 = Lc.H2, cD = Lc.D, cA1 = Lc.A + 1, cB = S::Bc;
+            constexpr int cncb = (cH2 + kTile - 1) / kTile, cH2p = (cH2 + 63) / 64 * 64;
+            constexpr int NM = (kRowsB * cncb + kLd - 1) / kLd, NW = (cH2p * 4 + kLd - 1) / kLd;
+            constexpr int NH = (cA1 * cH2 + kLd - 1) / kLd, N1 = (kRowsB * 16 + kLd - 1) / kLd;
+            constexpr int NX = (kRowsB * cD + kLd - 1) / kLd;
+            if (tid < kLd) {
+                int mr[NM];
+                float4 wr[NW];
+                float hr[NH], h1r[N1], xr[NX];
+#pragma unroll
+                for (int j = 0; j < NM; ++j) {
+                    const int u = tid + j * kLd, i = u / cncb, c = u - i * cncb;
+                    mr[j] = (u < kRowsB * cncb && b0 + i < cB) ? (int)h2mask[(int64_t)(b0 + i) * cncb + c] : 0;
+                }
+#pragma unroll
+                for (int j = 0; j < NW; ++j) {
+                    const int u = tid + j * kLd, n = u >> 2, c4 = u & 3;
+                    wr[j] = (u < cH2p * 4 && n < cH2 && k0 + 4 * c4 < cH1)
+                                ? *reinterpret_cast<const float4 *>(P + Lc.oW2 + (int64_t)n * cH1 + k0 + 4 * c4)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    const int u = tid + j * kLd, a = u / cH2, n = u - a * cH2;
+                    hr[j] = u < cA1 * cH2 ? P[Lc.head_row(a) + n] : 0.0f;
+                }
+#pragma unroll
+                for (int j = 0; j < N1; ++j) {
+                    const int u = tid + j * kLd, i = u >> 4, jj = u & 15;
+                    h1r[j] = (u < kRowsB * 16 && b0 + i < cB && k0 + jj < cH1) ? h1[(int64_t)(b0 + i) * cH1 + k0 + jj]
+                                                                              : 0.0f;
+                }
+#pragma unroll
+                for (int j = 0; j < NX; ++j) {
+                    const int u = tid + j * kLd;
+                    xr[j] = (u < kRowsB * cD && b0 * cD + u < cB * cD) ? x[(int64_t)b0 * cD + u] : 0.0f;
+                }
+#pragma unroll
+                for (int j = 0; j < NM; ++j)
+                    if (tid + j * kLd < kRowsB * cncb) mkB[tid + j * kLd] = mr[j];
+#pragma unroll
+                for (int j = 0; j < NW; ++j) {
+                    const int u = tid + j * kLd, n = u >> 2, c4 = u & 3;
+                    if (u < cH2p * 4) {
+                        W2T[(4 * c4 + 0) * ld + n] = wr[j].x;
+                        W2T[(4 * c4 + 1) * ld + n] = wr[j].y;
+                        W2T[(4 * c4 + 2) * ld + n] = wr[j].z;
+                        W2T[(4 * c4 + 3) * ld + n] = wr[j].w;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < NH; ++j)
+                    if (tid + j * kLd < cA1 * cH2) whs[tid + j * kLd] = hr[j];
+#pragma unroll
+                for (int j = 0; j < N1; ++j)
+                    if (tid + j * kLd < kRowsB * 16) h1m[tid + j * kLd] = h1r[j];
+#pragma unroll
+                for (int j = 0; j < NX; ++j)
+                    if (tid + j * kLd < kRowsB * cD) xs[tid + j * kLd] = xr[j];
+            }
+        } else if (!FUSED || tid < kLd) {
             for (int u = tid; u < kRowsB * sh.ncb; u += kLd) {
                 const int i = u / sh.ncb, c = u - i * sh.ncb;
                 mkB[u] = b0 + i < B ? (int)h2mask[(int64_t)(b0 + i) * sh.ncb + c] : 0;
@@ -961,9 +1025,24 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
             for (int u = tid; u < kRowsB * D; u += kLd) xs[u] = b0 * D + u < B * D ? x[(int64_t)b0 * D + u] : 0.0f;
         }
+#ifdef GS_STAMPS
+        const unsigned long long t_rb0 = __builtin_amdgcn_s_memtime();
+        if (bid == 0 && tid == 0) {   // loader waves: issue + land of the slab operands
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            atomicAdd(&g_stamp_acc[6][0], __builtin_amdgcn_s_memtime() - t_rb0);
+            atomicAdd(&g_stamp_cnt[6], 1ull);
+        }
+#endif
         if constexpr (FUSED)      // the kb == 0 slab also keeps its rows' metric sums
             loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), b0, kRowsB,
                              dzs, kb == 0 ? reinterpret_cast<double *>(kred) : nullptr, kLd, 256 - kLd);
+#ifdef GS_STAMPS
+        if (bid == 0 && tid == 192) {   // loss wave: its rows' loss + gradient
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            atomicAdd(&g_stamp_acc[7][0], __builtin_amdgcn_s_memtime() - t_rb0);
+            atomicAdd(&g_stamp_cnt[7], 1ull);
+        }
+#endif
         else
             for (int u = tid; u < kRowsB * A1; u += 256)
                 dzs[u] = b0 * A1 + u < B * A1 ? dz[(int64_t)b0 * A1 + u] : 0.0f;
@@ -973,7 +1052,35 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             if (kb == 0)
                 store_metric_groups(reinterpret_cast<const double *>(kred), kRowsB, b0, B,
                                     ff.k_local + (ff.step_base ? *ff.step_base : 0), ff.mpart);
-        // dh2 = relu'(h2) * (dz . Wh), in place; thread owns hidden unit n, loops the rows
+        // dh2 = relu'(h2) * (dz . Wh), in place
+        if (A1 <= 5 && H2 <= 1024 && 1024 % H2 == 0) {
+            // thread owns 4 consecutive hidden units (4 mask bits of one word, one float4 store)
+            // and every (256/(H2/4))-th row; threads of one row read the same dz (broadcast)
+            const int nt = H2 >> 2, rstep = 256 / nt;
+            const int n0 = 4 * (tid % nt), nb = n0 >> 4, sh4 = n0 & 15;
+            float w[5][4];
+#pragma unroll
+            for (int a = 0; a < 5; ++a)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w[a][j] = a < A1 ? whs[a * H2 + n0 + j] : 0.0f;
+#pragma unroll 4
+            for (int i = tid / nt; i < kRowsB; i += rstep) {
+                const unsigned m = (unsigned)(mkB[i * sh.ncb + nb] >> sh4);
+                float dzr[5];
+#pragma unroll
+                for (int a = 0; a < 5; ++a) dzr[a] = a < A1 ? dzs[i * A1 + a] : 0.0f;
+                float o[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float sacc = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < 5; ++a) sacc = a < A1 ? fmaf(dzr[a], w[a][j], sacc) : sacc;
+                    o[j] = ((m >> j) & 1u) ? sacc : 0.0f;
+                }
+                *reinterpret_cast<float4 *>(dh2s + i * ld + n0) = make_float4(o[0], o[1], o[2], o[3]);
+            }
+        } else
+        // thread owns hidden unit n, loops the rows
         for (int n = tid; n < H2; n += 256) {
             float w[kMaxActions + 1];
 #pragma unroll
@@ -1089,26 +1196,62 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
         __syncthreads();
         GS_STAMP(0)
-        // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
         float *partC = dzs + Bp * A1;           // [A1*16][16]
         const int nout = kTile * A1;
-        for (int u = tid; u < nout * 16; u += 256) {
-            const int o = u >> 4, j = u & 15;
-            const int a = o >> 4, i = o & 15;
-            float s = 0.0f;
-            for (int b = j; b < Bp; b += 16) s = fmaf(dzs[b * A1 + a], hs[b * 17 + i], s);
-            partC[u] = s;
-        }
-        __syncthreads();
         float sq = 0.0f;
-        for (int o = tid; o < nout; o += 256) {
-            float s = 0.0f;
+        if (A1 <= kTile) {
+            // dWh[a, n0+j] = sum_b dz[b, a] h2[b, n0+j] as one 16x16 MFMA tile (rows = actions,
+            // padded) with K = the batch split over the 4 waves; the wave partials are summed
+            // in wave order through LDS
+            const int li = lane & 15, lq = lane >> 4;
+            const int nch = Bp / kTile;
+            const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+            for (int ch = ch0; ch < ch1; ++ch) {
+                const int b = ch * kTile + 4 * lq;
+                float av[4], bv[4];
 #pragma unroll
-            for (int m = 0; m < 16; ++m) s += partC[o * 16 + m];
-            const int a = o >> 4, i = o & 15;
-            if (n0 + i < H2) {
-                G[L.head_row(a) + n0 + i] = s;
-                sq += s * s;
+                for (int c = 0; c < 4; ++c) {
+                    av[c] = li < A1 ? dzs[(b + c) * A1 + li] : 0.0f;
+                    bv[c] = hs[(b + c) * 17 + li];
+                }
+                acc0 = mfma4(av[0], bv[0], acc0);
+                acc1 = mfma4(av[1], bv[1], acc1);
+                acc0 = mfma4(av[2], bv[2], acc0);
+                acc1 = mfma4(av[3], bv[3], acc1);
+            }
+            const f32x4 acc = acc0 + acc1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) partC[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
+            __syncthreads();
+            if (tid < nout) {
+                const int a = tid >> 4, i = tid & 15;
+                const float s = ((partC[tid] + partC[256 + tid]) + partC[512 + tid]) + partC[768 + tid];
+                if (n0 + i < H2) {
+                    G[L.head_row(a) + n0 + i] = s;
+                    sq = s * s;
+                }
+            }
+        } else {
+            // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
+            for (int u = tid; u < nout * 16; u += 256) {
+                const int o = u >> 4, j = u & 15;
+                const int a = o >> 4, i = o & 15;
+                float s = 0.0f;
+                for (int b = j; b < Bp; b += 16) s = fmaf(dzs[b * A1 + a], hs[b * 17 + i], s);
+                partC[u] = s;
+            }
+            __syncthreads();
+            for (int o = tid; o < nout; o += 256) {
+                float s = 0.0f;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) s += partC[o * 16 + m];
+                const int a = o >> 4, i = o & 15;
+                if (n0 + i < H2) {
+                    G[L.head_row(a) + n0 + i] = s;
+                    sq += s * s;
+                }
             }
         }
         block_sumsq_store(sq, sumsq + sh.nA + sh.ncb + nb, sbuf);

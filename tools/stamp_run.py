@@ -45,7 +45,9 @@ names = {0: ("k_fwd_hidden", ["load operands", "row gather", "h1", "mfma h2", "h
          2: ("k_bwd roleA blk0", ["load tiles", "dh2", "mfma dW2", "store + sumsq + db2"]),
          3: ("k_clip_adam blk0", ["own loads + LDS staging", "W1 fold + norm loops", "reduce", "adam"]),
          4: ("k_bwd roleB blk0", ["load slab", "dh2", "mfma dh1", "dW1 partial"]),
-         5: ("k_bwd roleC blk0", ["load", "reduce + store"])}
+         5: ("k_bwd roleC blk0", ["load", "reduce + store"]),
+         6: ("k_bwd roleB slab loads (wave 0, from role start)", ["landed"]),
+         7: ("k_bwd roleB loss rows (wave 3, from role start)", ["done"])}
 for k, (n, phases) in names.items():
     if cnt[k] == 0:
         continue
