@@ -406,6 +406,23 @@ __device__ __forceinline__ void gather_head_row(const float *__restrict__ zpart,
     if constexpr (AEX > 0) {
         constexpr int A1c = AEX + 1;
         const float *zp = zpart + r * ncb * A1c;
+        if (ncb == 16 && (16 * A1c) % 4 == 0 && ((uintptr_t)zp & 15) == 0) {
+            // the row's 16 x A1 partials as float4 loads (one burst), summed in column-block order
+            constexpr int NV = 16 * A1c / 4;
+            float buf[16 * A1c];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const float4 q = reinterpret_cast<const float4 *>(zp)[v];
+                buf[4 * v + 0] = q.x;
+                buf[4 * v + 1] = q.y;
+                buf[4 * v + 2] = q.z;
+                buf[4 * v + 3] = q.w;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+#pragma unroll
+                for (int a = 0; a < A1c; ++a) z[a] += buf[j * A1c + a];
+        } else
         for (int cb0 = 0; cb0 < ncb; cb0 += 16) {
             float buf[16][A1c];
 #pragma unroll
@@ -813,28 +830,75 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         float *dh2T = whs + round4(A1 * 16);         // [16][Bp+4]  (n, b): h2 first, then dh2
         float *h1T = dh2T + kTile * ld;              // [16][Bp+4]  (k, b)
         float *red = h1T + kTile * ld;               // [4][256]
-        if constexpr (FUSED)
-            loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
-                             nullptr);
-        else
-            copy_to_lds(dzs, dz, B * A1);
-        if (tid < A1 * kTile) {
-            const int a = tid >> 4, j = tid & 15;
-            whs[tid] = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
-        }
         // relu'(h2) bits of this n-block (one word per row) and the h1 column tile (16 contiguous
         // floats per row = 4 float4, transposed into LDS); dh2T is filled by the dh2 pass
         int *mkA = reinterpret_cast<int *>(red + 1024);   // [Bp]
-        for (int b = tid; b < Bp; b += 256) mkA[b] = b < B ? (int)h2mask[(int64_t)b * sh.ncb + nb] : 0;
+        if constexpr (S::H1c > 0 && S::Bc > 0) {
+            // compile-time shapes: the tile loads are issued before the loss rows, which
+            // then run while they are in flight; LDS writes follow
+            constexpr Layout Lc = S::lay(Layout{});
+            constexpr int cB = S::Bc, cBp = (cB + 63) / 64 * 64, cncb = (Lc.H2 + kTile - 1) / kTile;
+            constexpr int NMk = (cBp + 255) / 256, NH1 = (cBp * 4 + 255) / 256;
+            int mr[NMk];
+            float4 hr[NH1];
+            float wh = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NMk; ++j) {
+                const int b = tid + 256 * j;
+                mr[j] = b < cB ? (int)h2mask[(int64_t)b * cncb + nb] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < NH1; ++j) {
+                const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
+                hr[j] = (u < cBp * 4 && b < cB && k0 + 4 * c4 < Lc.H1)
+                            ? *reinterpret_cast<const float4 *>(h1 + (int64_t)b * Lc.H1 + k0 + 4 * c4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            if (tid < A1 * kTile) {
+                const int a = tid >> 4, j = tid & 15;
+                wh = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
+            }
+            if constexpr (FUSED)
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
+                                 nullptr);
+            else
+                copy_to_lds(dzs, dz, B * A1);
+            if (tid < A1 * kTile) whs[tid] = wh;
+#pragma unroll
+            for (int j = 0; j < NMk; ++j)
+                if (tid + 256 * j < cBp) mkA[tid + 256 * j] = mr[j];
+#pragma unroll
+            for (int j = 0; j < NH1; ++j) {
+                const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
+                if (u < cBp * 4) {
+                    h1T[(4 * c4 + 0) * ld + b] = hr[j].x;
+                    h1T[(4 * c4 + 1) * ld + b] = hr[j].y;
+                    h1T[(4 * c4 + 2) * ld + b] = hr[j].z;
+                    h1T[(4 * c4 + 3) * ld + b] = hr[j].w;
+                }
+            }
+        } else {
+            if constexpr (FUSED)
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
+                                 nullptr);
+            else
+                copy_to_lds(dzs, dz, B * A1);
+            if (tid < A1 * kTile) {
+                const int a = tid >> 4, j = tid & 15;
+                whs[tid] = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
+            }
+            for (int b = tid; b < Bp; b += 256) mkA[b] = b < B ? (int)h2mask[(int64_t)b * sh.ncb + nb] : 0;
 #pragma unroll 4
-        for (int u = tid; u < Bp * 4; u += 256) {
-            const int b = u >> 2, c4 = u & 3;
-            float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (b < B && k0 + 4 * c4 < H1) gv = *reinterpret_cast<const float4 *>(h1 + (int64_t)b * H1 + k0 + 4 * c4);
-            h1T[(4 * c4 + 0) * ld + b] = gv.x;
-            h1T[(4 * c4 + 1) * ld + b] = gv.y;
-            h1T[(4 * c4 + 2) * ld + b] = gv.z;
-            h1T[(4 * c4 + 3) * ld + b] = gv.w;
+            for (int u = tid; u < Bp * 4; u += 256) {
+                const int b = u >> 2, c4 = u & 3;
+                float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (b < B && k0 + 4 * c4 < H1)
+                    gv = *reinterpret_cast<const float4 *>(h1 + (int64_t)b * H1 + k0 + 4 * c4);
+                h1T[(4 * c4 + 0) * ld + b] = gv.x;
+                h1T[(4 * c4 + 1) * ld + b] = gv.y;
+                h1T[(4 * c4 + 2) * ld + b] = gv.z;
+                h1T[(4 * c4 + 3) * ld + b] = gv.w;
+            }
         }
         __syncthreads();
         GS_STAMP(0)
@@ -1179,21 +1243,50 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         GS_STAMP_BEGIN_IF(5, bid == 0)
         float *hs = lds;                    // [Bp][17]
         float *dzs = hs + Bp * 17;          // [Bp][A1]
+        auto loss_in = [&]() {
+            if constexpr (FUSED)
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, Bp, dzs,
+                                 nullptr);
+            else
+                for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
+        };
+        if constexpr (S::H1c > 0 && S::Bc > 0) {
+            // compile-time shapes: the h2 column tile is in flight while the loss rows run
+            constexpr Layout Lc = S::lay(Layout{});
+            constexpr int cB = S::Bc, cBp = (cB + 15) / 16 * 16, NH = (cBp * 4 + 255) / 256;
+            float4 hr[NH];
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
+                hr[j] = (u < cBp * 4 && b < cB && n0 + 4 * c4 < Lc.H2)
+                            ? *reinterpret_cast<const float4 *>(h2 + (int64_t)b * Lc.H2 + n0 + 4 * c4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            loss_in();
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
+                if (u < cBp * 4) {
+                    hs[b * 17 + 4 * c4 + 0] = hr[j].x;
+                    hs[b * 17 + 4 * c4 + 1] = hr[j].y;
+                    hs[b * 17 + 4 * c4 + 2] = hr[j].z;
+                    hs[b * 17 + 4 * c4 + 3] = hr[j].w;
+                }
+            }
+        } else {
 #pragma unroll 4
-        for (int u = tid; u < Bp * 4; u += 256) {
-            const int b = u >> 2, c4 = u & 3;
-            float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (b < B && n0 + 4 * c4 < H2) hv = *reinterpret_cast<const float4 *>(h2 + (int64_t)b * H2 + n0 + 4 * c4);
-            hs[b * 17 + 4 * c4 + 0] = hv.x;
-            hs[b * 17 + 4 * c4 + 1] = hv.y;
-            hs[b * 17 + 4 * c4 + 2] = hv.z;
-            hs[b * 17 + 4 * c4 + 3] = hv.w;
+            for (int u = tid; u < Bp * 4; u += 256) {
+                const int b = u >> 2, c4 = u & 3;
+                float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (b < B && n0 + 4 * c4 < H2)
+                    hv = *reinterpret_cast<const float4 *>(h2 + (int64_t)b * H2 + n0 + 4 * c4);
+                hs[b * 17 + 4 * c4 + 0] = hv.x;
+                hs[b * 17 + 4 * c4 + 1] = hv.y;
+                hs[b * 17 + 4 * c4 + 2] = hv.z;
+                hs[b * 17 + 4 * c4 + 3] = hv.w;
+            }
+            loss_in();
         }
-        if constexpr (FUSED)
-            loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, Bp, dzs,
-                             nullptr);
-        else
-            for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
         __syncthreads();
         GS_STAMP(0)
         float *partC = dzs + Bp * A1;           // [A1*16][16]
