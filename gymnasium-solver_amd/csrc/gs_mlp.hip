@@ -175,7 +175,45 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     // ---- phase 0: every operand of this workgroup, all loads in flight together.
     //      Threads 0..15 run the dependent idx -> row -> obs/fields chain while the rest
     //      of the block streams the weights into LDS.
-    if (FUSED) {
+    // compile-time shapes on the fused path: every phase-0 operand goes to registers first
+    // (one memory round trip), then to LDS
+    constexpr bool kStage0 = FUSED && S::H1c > 0 && (S::H1c * 4) % 4 == 0;
+    if constexpr (kStage0) {
+        constexpr Layout Lc = S::lay(Layout{});
+        constexpr int cD = Lc.D, cH1 = Lc.H1, cA1 = Lc.A + 1;
+        static_assert((cH1 * cD) % 4 == 0 && cH1 % 4 == 0, "float4 staging");
+        constexpr int NW1 = (cH1 * cD / 4 + 255) / 256, NB1 = (cH1 / 4 + 255) / 256;
+        float4 w1v[NW1], b1v[NB1];
+        float xv = 0.0f, b2v = 0.0f, whv = 0.0f;
+        if (tid < kTile * cD) {
+            const int i = tid / cD;
+            xv = r0 + i < rows ? ff.xg[(kstep * rows + r0) * cD + tid] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < NW1; ++j) {
+            const int u = tid + 256 * j;
+            w1v[j] = u < cH1 * cD / 4 ? reinterpret_cast<const float4 *>(P + Lc.oW1)[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < NB1; ++j) {
+            const int u = tid + 256 * j;
+            b1v[j] = u < cH1 / 4 ? reinterpret_cast<const float4 *>(P + Lc.ob1)[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (tid < kTile) b2v = c0 + tid < H2 ? P[Lc.ob2 + c0 + tid] : 0.0f;
+        if (tid < cA1 * kTile) {
+            const int a = tid >> 4, j = tid & 15;
+            whv = c0 + j < H2 ? P[Lc.head_row(a) + c0 + j] : 0.0f;
+        }
+        if (tid < kTile * cD) xs[tid] = xv;
+#pragma unroll
+        for (int j = 0; j < NW1; ++j)
+            if (tid + 256 * j < cH1 * cD / 4) reinterpret_cast<float4 *>(W1s)[tid + 256 * j] = w1v[j];
+#pragma unroll
+        for (int j = 0; j < NB1; ++j)
+            if (tid + 256 * j < cH1 / 4) reinterpret_cast<float4 *>(b1s)[tid + 256 * j] = b1v[j];
+        if (tid < kTile) b2s[tid] = b2v;
+        if (tid < cA1 * kTile) whs[tid] = whv;
+    } else if (FUSED) {
         if (tid < kTile * D) {
             const int i = tid / D;
             xs[tid] = r0 + i < rows ? ff.xg[(kstep * rows + r0) * D + tid] : 0.0f;
@@ -193,12 +231,14 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             rg.f_ret[r] = rg.returns[src];
         }
     }
-    copy_to_lds(W1s, P + L.oW1, H1 * D);
-    copy_to_lds(b1s, P + L.ob1, H1);
-    if (tid < kTile) b2s[tid] = c0 + tid < H2 ? P[L.ob2 + c0 + tid] : 0.0f;
-    if (tid < A1 * kTile) {
-        const int a = tid >> 4, j = tid & 15;
-        whs[tid] = c0 + j < H2 ? P[L.head_row(a) + c0 + j] : 0.0f;
+    if constexpr (!kStage0) {
+        copy_to_lds(W1s, P + L.oW1, H1 * D);
+        copy_to_lds(b1s, P + L.ob1, H1);
+        if (tid < kTile) b2s[tid] = c0 + tid < H2 ? P[L.ob2 + c0 + tid] : 0.0f;
+        if (tid < A1 * kTile) {
+            const int a = tid >> 4, j = tid & 15;
+            whs[tid] = c0 + j < H2 ? P[L.head_row(a) + c0 + j] : 0.0f;
+        }
     }
     // W2 tile: with compile-time shapes the loads go to registers AFTER the h1 operands, so the
     // barrier below waits only for those (in-order vmcnt) and h1 is computed while the 16 KB
@@ -406,8 +446,9 @@ __device__ __forceinline__ void gather_head_row(const float *__restrict__ zpart,
     if constexpr (AEX > 0) {
         constexpr int A1c = AEX + 1;
         const float *zp = zpart + r * ncb * A1c;
-        if (ncb == 16 && (16 * A1c) % 4 == 0 && ((uintptr_t)zp & 15) == 0) {
+        if (ncb == 16 && (16 * A1c) % 4 == 0) {
             // the row's 16 x A1 partials as float4 loads (one burst), summed in column-block order
+            // (zpart is 256-B aligned in the workspace and a row is 16 x A1 floats: 16-B aligned)
             constexpr int NV = 16 * A1c / 4;
             float buf[16 * A1c];
 #pragma unroll
@@ -769,10 +810,12 @@ __device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const
         for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
         if (r < B) {
             const int64_t o = k * B + r;
+            // the row's fields are loaded before the head partials: one memory round trip
+            const int fa = ff.fa[o];
+            const float folp = ff.folp[o], fov = ff.fov[o], fadv = ff.fadv[o], fret = ff.fret[o];
             float z[AMAX + 1];
             gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
-            loss_row<AMAX>(z, L.A, ff.fa[o], ff.folp[o], ff.fov[o], ff.fadv[o], ff.fret[o], la, 1.0f / (float)B,
-                           dzs + i * A1, acc);
+            loss_row<AMAX>(z, L.A, fa, folp, fov, fadv, fret, la, 1.0f / (float)B, dzs + i * A1, acc);
         } else {
             for (int a = 0; a < A1; ++a) dzs[i * A1 + a] = 0.0f;
         }
@@ -1426,7 +1469,11 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
                 pv[i] = ok ? Pm[p] : 0.0f;
             }
         }
-        copy_to_lds(stage, sumsq, aa.n_slots);
+        // every load before the first LDS write: one memory round trip
+        constexpr int NS = 2;   // sum-of-squares slots per thread (launcher: n_slots <= 512)
+        float sl[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) sl[j] = tid + 256 * j < aa.n_slots ? sumsq[tid + 256 * j] : 0.0f;
         float4 t[NQ][NRB];
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
@@ -1436,6 +1483,9 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
                 t[j][rb] = 4 * q < n1 ? *reinterpret_cast<const float4 *>(part1 + (int64_t)rb * n1 + 4 * q)
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+            if (tid + 256 * j < aa.n_slots) stage[tid + 256 * j] = sl[j];
         float *w1s = stage + round4(aa.n_slots);
         float4 gsum[NQ];
 #pragma unroll
@@ -1719,7 +1769,8 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
     return with_shape(L, 0, [&](auto sh) {
         const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
         const bool al = (((uintptr_t)P | (uintptr_t)G | (uintptr_t)M | (uintptr_t)V | (uintptr_t)part1) & 15) == 0;
-        if (aa.nrb == 8 && aa.stage_lds && n1 % 4 == 0 && L.oW2 % 4 == 0 && (n1 / 4 + 255) / 256 == 2 && al)
+        if (aa.nrb == 8 && aa.stage_lds && n1 % 4 == 0 && L.oW2 % 4 == 0 && (n1 / 4 + 255) / 256 == 2 && al &&
+            aa.n_slots <= 512)
             // C2 shapes: B = 256 (8 row blocks of 32), H1 (D+1) = 1280
             hipLaunchKernelGGL((k_clip_adam<decltype(sh), 8, 2>), dim3(nblk), dim3(256), stage, s, P, L, G, M, V,
                                part1, sumsq, aa, metrics, stop);

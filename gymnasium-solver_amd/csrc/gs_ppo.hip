@@ -100,6 +100,7 @@ extern "C" int gs_policy_act(const float *params, gs_mlp_dims dims, const float 
     GS_REQUIRE(N > 0, "gs_policy_act: N must be > 0");
     GS_REQUIRE(mode >= 0 && mode <= 2, "gs_policy_act: mode %d not in {0,1,2}", mode);
     GS_REQUIRE(params && obs && actions && logp && value && scratch, "gs_policy_act: null buffer");
+    GS_REQUIRE(((uintptr_t)scratch & 15) == 0, "gs_policy_act: scratch must be 16-byte aligned");
     const Layout L = layout_of(dims);
     hipStream_t s = (hipStream_t)stream;
     float *zpart = (float *)scratch;
@@ -115,6 +116,7 @@ extern "C" int gs_policy_value(const float *params, gs_mlp_dims dims, const floa
     int rc = check_dims(dims);
     if (rc) return rc;
     GS_REQUIRE(N > 0 && params && obs && value && scratch, "gs_policy_value: bad argument");
+    GS_REQUIRE(((uintptr_t)scratch & 15) == 0, "gs_policy_value: scratch must be 16-byte aligned");
     const Layout L = layout_of(dims);
     hipStream_t s = (hipStream_t)stream;
     float *zpart = (float *)scratch;
@@ -399,7 +401,8 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     // configured (its per-minibatch decision needs the full loss before the backward) and the
     // caller's workspace holds the per-update arrays
     const bool fused = has_fused(L, batch) && !(hp.target_kl > 0.0f) &&
-                       workspace_bytes >= carve_fused(nullptr, L, batch, n_minibatches).bytes;
+                       workspace_bytes >= carve_fused(nullptr, L, batch, n_minibatches).bytes &&
+                       (((uintptr_t)params | (uintptr_t)grads | (uintptr_t)adam_m | (uintptr_t)adam_v) & 15) == 0;
     FusedWs fw{};
     FusedFwd ff0{};
     if (fused) {

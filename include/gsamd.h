@@ -83,7 +83,7 @@ int64_t gs_mlp_param_count(gs_mlp_dims dims);
  * (rng_seed, rng_counter, env)), 1 = deterministic (argmax, first max wins),
  * 2 = replay: actions_dev is an INPUT (recorded actions).  Writes actions (int64),
  * logp, value (N) and, when obs_store_dev != NULL, copies obs into it (the rollout
- * buffer slot of this step).  scratch_dev: gs_policy_scratch_bytes(dims, N) bytes.
+ * buffer slot of this step).  scratch_dev: gs_policy_scratch_bytes(dims, N) bytes, 16-byte aligned.
  */
 size_t gs_policy_scratch_bytes(gs_mlp_dims dims, int64_t N);
 int gs_policy_act(const float *params_dev, gs_mlp_dims dims, const float *obs_dev, int64_t N, int mode,
@@ -194,7 +194,9 @@ int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float 
  * fused chain (the BASELINE configs' MLP shapes) this includes the per-update gathered
  * minibatch fields and normalised advantages, so the per-step chain reads x in one load and
  * the loss runs row-parallel with metrics reduced once after the update; a smaller workspace
- * (>= gs_ppo_workspace_bytes) selects the index-chasing chain with bit-identical parameters. */
+ * (>= gs_ppo_workspace_bytes) selects the index-chasing chain with bit-identical parameters.
+ * The fused chain also needs params/grads/adam_m/adam_v 16-byte aligned (every torch
+ * allocation is); unaligned buffers take the index-chasing chain. */
 size_t gs_ppo_update_workspace_bytes(gs_mlp_dims dims, int64_t batch, int64_t n_minibatches);
 
 /* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)
