@@ -1769,14 +1769,19 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
     return with_shape(L, 0, [&](auto sh) {
         const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
         const bool al = (((uintptr_t)P | (uintptr_t)G | (uintptr_t)M | (uintptr_t)V | (uintptr_t)part1) & 15) == 0;
-        if (aa.nrb == 8 && aa.stage_lds && n1 % 4 == 0 && L.oW2 % 4 == 0 && (n1 / 4 + 255) / 256 == 2 && al &&
-            aa.n_slots <= 512)
-            // C2 shapes: B = 256 (8 row blocks of 32), H1 (D+1) = 1280
-            hipLaunchKernelGGL((k_clip_adam<decltype(sh), 8, 2>), dim3(nblk), dim3(256), stage, s, P, L, G, M, V,
-                               part1, sumsq, aa, metrics, stop);
-        else
-            hipLaunchKernelGGL((k_clip_adam<decltype(sh), 0, 0>), dim3(nblk), dim3(256), aa.stage_lds ? stage : 0, s,
-                               P, L, G, M, V, part1, sumsq, aa, metrics, stop);
+        const int nq = (int)((n1 / 4 + 255) / 256);
+        const bool vec = aa.stage_lds && n1 % 4 == 0 && L.oW2 % 4 == 0 && al && aa.n_slots <= 512 && nq <= 2;
+        using Sh = decltype(sh);
+        const void *fn = nullptr;   // the fused shapes: C2 (B 256 -> 8 row blocks), C3 (B 64 -> 2)
+        if (vec && aa.nrb == 8) fn = nq == 2 ? (const void *)k_clip_adam<Sh, 8, 2> : (const void *)k_clip_adam<Sh, 8, 1>;
+        if (vec && aa.nrb == 2) fn = nq == 2 ? (const void *)k_clip_adam<Sh, 2, 2> : (const void *)k_clip_adam<Sh, 2, 1>;
+        if (fn) {
+            void *args[] = {&P, (void *)&L, &G, &M, &V, &part1, &sumsq, &aa, &metrics, &stop};
+            GS_HIP(hipLaunchKernel(fn, dim3(nblk), dim3(256), args, stage, s));
+        } else {
+            hipLaunchKernelGGL((k_clip_adam<Sh, 0, 0>), dim3(nblk), dim3(256), aa.stage_lds ? stage : 0, s, P, L, G,
+                               M, V, part1, sumsq, aa, metrics, stop);
+        }
         GS_LAUNCH_CHECK("k_clip_adam");
         return GS_OK;
     });
