@@ -355,19 +355,21 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         for (int c = 0; c < kTile; ++c) z = fmaf(h2s[row * 17 + c], whs[a * 16 + c], z);
         zpart[((int64_t)(r0 + row) * ncbz + cb) * A1 + a] = z;
     }
-    if (cb == 0) {
-        const int nrow = min(kTile, rows - r0);
+    const int nrow = min(kTile, rows - r0);
+    if (cb == 0)
         for (int u = tid; u < nrow * D; u += 256) {
             if (x_out) x_out[(int64_t)r0 * D + u] = xs[u];
             if (obs_copy) obs_copy[(int64_t)r0 * D + u] = xs[u];
         }
-        if (h1_out) {
-            const int k4n = H1 >> 2;
-            for (int u = tid; u < nrow * k4n; u += 256) {
-                const int i = u / k4n, k4 = u - i * k4n;
-                *reinterpret_cast<float4 *>(h1_out + (int64_t)(r0 + i) * H1 + 4 * k4) =
-                    *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
-            }
+    if (h1_out) {
+        // every column-block workgroup of this row block holds all of h1: the store is split
+        // between them (H1/16 units each) instead of falling on column block 0 alone
+        const int k4n = H1 >> 2, ncbw = gridDim.x;
+        const int kb0 = (cb * k4n) / ncbw, kb1 = ((cb + 1) * k4n) / ncbw, nk = kb1 - kb0;
+        for (int u = tid; u < nrow * nk; u += 256) {
+            const int i = u / nk, k4 = kb0 + (u - i * nk);
+            *reinterpret_cast<float4 *>(h1_out + (int64_t)(r0 + i) * H1 + 4 * k4) =
+                *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
         }
     }
     GS_STAMP_END(4)
@@ -747,7 +749,7 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
 // k_bwd: three roles by block range.
 //   role A: dW2 tile (n-block, k-block), K = batch     -> grads, db2 (k-block 0)
 //   role B: dh1 slab (64 rows, k-block), K = H2        -> dW1/db1 partial per 64 rows
-//   role C: head grads for an n-block (+ head biases in block 0)
+//   role C: head grads for an n-block; one extra block for the head biases
 // sum-of-squares slot map: [0, nA) dW2 tiles, [nA, nA+ncb) db2 blocks,
 //                          [nA+ncb, nA+2ncb) head weight blocks, nA+2ncb head biases.
 // ------------------------------------------------------------------------------------
@@ -768,7 +770,7 @@ struct BwdShape {
         s.nrbB = (B + kRowsB - 1) / kRowsB;
         s.nA = s.ncb * s.nkb;
         s.nB = s.nrbB * s.nkb;
-        s.nC = s.ncb;
+        s.nC = s.ncb + 1;   // + one block for the head-bias gradients
         return s;
     }
 };
@@ -1279,7 +1281,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
     }
     bid -= sh.nB;
     {
-        // ---------------- role C: head grads for hidden block nb (+ biases in block 0)
+        // ---------------- role C: head grads for hidden block nb (block ncb: head biases)
         const int nb = bid;
         const int n0 = nb * kTile;
         const int Bp = (B + 15) / 16 * 16;
@@ -1333,66 +1335,67 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         __syncthreads();
         GS_STAMP(0)
         float *partC = dzs + Bp * A1;           // [A1*16][16]
-        const int nout = kTile * A1;
-        float sq = 0.0f;
-        if (A1 <= kTile) {
-            // dWh[a, n0+j] = sum_b dz[b, a] h2[b, n0+j] as one 16x16 MFMA tile (rows = actions,
-            // padded) with K = the batch split over the 4 waves; the wave partials are summed
-            // in wave order through LDS
-            const int li = lane & 15, lq = lane >> 4;
-            const int nch = Bp / kTile;
-            const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-            for (int ch = ch0; ch < ch1; ++ch) {
-                const int b = ch * kTile + 4 * lq;
-                float av[4], bv[4];
+        if (nb < sh.ncb) {
+            const int nout = kTile * A1;
+            float sq = 0.0f;
+            if (A1 <= kTile) {
+                // dWh[a, n0+j] = sum_b dz[b, a] h2[b, n0+j] as one 16x16 MFMA tile (rows = actions,
+                // padded) with K = the batch split over the 4 waves; the wave partials are summed
+                // in wave order through LDS
+                const int li = lane & 15, lq = lane >> 4;
+                const int nch = Bp / kTile;
+                const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    #pragma unroll 2
+                for (int ch = ch0; ch < ch1; ++ch) {
+                    const int b = ch * kTile + 4 * lq;
+                    float av[4], bv[4];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    av[c] = li < A1 ? dzs[(b + c) * A1 + li] : 0.0f;
-                    bv[c] = hs[(b + c) * 17 + li];
+                    for (int c = 0; c < 4; ++c) {
+                        av[c] = li < A1 ? dzs[(b + c) * A1 + li] : 0.0f;
+                        bv[c] = hs[(b + c) * 17 + li];
+                    }
+                    acc0 = mfma4(av[0], bv[0], acc0);
+                    acc1 = mfma4(av[1], bv[1], acc1);
+                    acc0 = mfma4(av[2], bv[2], acc0);
+                    acc1 = mfma4(av[3], bv[3], acc1);
                 }
-                acc0 = mfma4(av[0], bv[0], acc0);
-                acc1 = mfma4(av[1], bv[1], acc1);
-                acc0 = mfma4(av[2], bv[2], acc0);
-                acc1 = mfma4(av[3], bv[3], acc1);
-            }
-            const f32x4 acc = acc0 + acc1;
+                const f32x4 acc = acc0 + acc1;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) partC[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
-            __syncthreads();
-            if (tid < nout) {
-                const int a = tid >> 4, i = tid & 15;
-                const float s = ((partC[tid] + partC[256 + tid]) + partC[512 + tid]) + partC[768 + tid];
-                if (n0 + i < H2) {
-                    G[L.head_row(a) + n0 + i] = s;
-                    sq = s * s;
+                for (int r = 0; r < 4; ++r) partC[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
+                __syncthreads();
+                if (tid < nout) {
+                    const int a = tid >> 4, i = tid & 15;
+                    const float s = ((partC[tid] + partC[256 + tid]) + partC[512 + tid]) + partC[768 + tid];
+                    if (n0 + i < H2) {
+                        G[L.head_row(a) + n0 + i] = s;
+                        sq = s * s;
+                    }
+                }
+            } else {
+                // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
+                for (int u = tid; u < nout * 16; u += 256) {
+                    const int o = u >> 4, j = u & 15;
+                    const int a = o >> 4, i = o & 15;
+                    float s = 0.0f;
+                    for (int b = j; b < Bp; b += 16) s = fmaf(dzs[b * A1 + a], hs[b * 17 + i], s);
+                    partC[u] = s;
+                }
+                __syncthreads();
+                for (int o = tid; o < nout; o += 256) {
+                    float s = 0.0f;
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) s += partC[o * 16 + m];
+                    const int a = o >> 4, i = o & 15;
+                    if (n0 + i < H2) {
+                        G[L.head_row(a) + n0 + i] = s;
+                        sq += s * s;
+                    }
                 }
             }
+            block_sumsq_store(sq, sumsq + sh.nA + sh.ncb + nb, sbuf);
         } else {
-            // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
-            for (int u = tid; u < nout * 16; u += 256) {
-                const int o = u >> 4, j = u & 15;
-                const int a = o >> 4, i = o & 15;
-                float s = 0.0f;
-                for (int b = j; b < Bp; b += 16) s = fmaf(dzs[b * A1 + a], hs[b * 17 + i], s);
-                partC[u] = s;
-            }
-            __syncthreads();
-            for (int o = tid; o < nout; o += 256) {
-                float s = 0.0f;
-#pragma unroll
-                for (int m = 0; m < 16; ++m) s += partC[o * 16 + m];
-                const int a = o >> 4, i = o & 15;
-                if (n0 + i < H2) {
-                    G[L.head_row(a) + n0 + i] = s;
-                    sq += s * s;
-                }
-            }
-        }
-        block_sumsq_store(sq, sumsq + sh.nA + sh.ncb + nb, sbuf);
-        if (nb == 0) {
-            __syncthreads();
+            // the extra block: head-bias gradients (sum of dz over the batch)
             for (int u = tid; u < A1 * 16; u += 256) {
                 const int a = u >> 4, j = u & 15;
                 float s = 0.0f;
