@@ -761,14 +761,18 @@ __device__ __forceinline__ void block_sumsq_store(float v, float *slot, float *s
 }
 
 struct BwdShape {
-    int ncb, nkb, nrbB, nA, nB, nC;
+    int ncb, nkb, nrbB, ka, nT, nA, nB, nC;
     __host__ __device__ static BwdShape make(const Layout &L, int B)
     {
         BwdShape s;
         s.ncb = (L.H2 + kTile - 1) / kTile;
         s.nkb = (L.H1 + kTile - 1) / kTile;
         s.nrbB = (B + kRowsB - 1) / kRowsB;
-        s.nA = s.ncb * s.nkb;
+        // role A: ka k-blocks of the same n-block per workgroup (the loss rows, the relu' mask
+        // and dh2 are computed once for them); keeps the grid near one workgroup per CU
+        s.ka = s.nkb % 2 == 0 ? 2 : 1;
+        s.nT = s.ncb * s.nkb;                   // dW2 tiles (sum-of-squares slots)
+        s.nA = s.ncb * (s.nkb / s.ka);
         s.nB = s.nrbB * s.nkb;
         s.nC = s.ncb + 1;   // + one block for the head-bias gradients
         return s;
@@ -780,7 +784,7 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     const int A1 = L.A + 1;
     const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
     const int64_t H2p = (L.H2 + 63) / 64 * 64;
-    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 2 * kTile * (Bp64 + 4) + 1024 + Bp64;
+    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 3 * kTile * (Bp64 + 4) + 3072 + Bp64 + 816;
     const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
                           kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024 +
                           (int64_t)kRowsB * n_col_blocks(L.H2);
@@ -864,26 +868,28 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
     else if (bid < sh.nB + sh.nA) bid -= sh.nB;
 
     if (bid < sh.nA) {
-        // ---------------- role A: dW2[n0:n0+16, k0:k0+16] = sum_b dh2[b,n] h1[b,k]
-        const int nb = bid / sh.nkb, kb = bid - nb * sh.nkb;
-        const int n0 = nb * kTile, k0 = kb * kTile;
+        // ---------------- role A: dW2[n0:n0+16, k0:k0+16*ka] = sum_b dh2[b,n] h1[b,k]
+        const int nkg = sh.nkb / sh.ka;
+        const int nb = bid / nkg, kb = (bid - nb * nkg) * sh.ka;   // first of the ka k-blocks
+        const int n0 = nb * kTile, k0 = kb * kTile, kw = kTile * sh.ka;
         GS_STAMP_BEGIN_IF(2, bid == 0)
         const int Bp = (B + 63) / 64 * 64;      // padded K (batch) for 4 waves x 16
         const int ld = Bp + 4;
         float *dzs = lds;                            // [B][A1]
         float *whs = dzs + round4(B * A1);           // [A1][16]
         float *dh2T = whs + round4(A1 * 16);         // [16][Bp+4]  (n, b): h2 first, then dh2
-        float *h1T = dh2T + kTile * ld;              // [16][Bp+4]  (k, b)
-        float *red = h1T + kTile * ld;               // [4][256]
+        float *h1T = dh2T + kTile * ld;              // [16*ka][Bp+4]  (k, b)
+        float *red = h1T + kw * ld;                  // [4][3][256]
         // relu'(h2) bits of this n-block (one word per row) and the h1 column tile (16 contiguous
         // floats per row = 4 float4, transposed into LDS); dh2T is filled by the dh2 pass
-        int *mkA = reinterpret_cast<int *>(red + 1024);   // [Bp]
+        int *mkA = reinterpret_cast<int *>(red + 3072);   // [Bp]
         if constexpr (S::H1c > 0 && S::Bc > 0) {
             // compile-time shapes: the tile loads are issued before the loss rows, which
             // then run while they are in flight; LDS writes follow
             constexpr Layout Lc = S::lay(Layout{});
             constexpr int cB = S::Bc, cBp = (cB + 63) / 64 * 64, cncb = (Lc.H2 + kTile - 1) / kTile;
-            constexpr int NMk = (cBp + 255) / 256, NH1 = (cBp * 4 + 255) / 256;
+            constexpr int cka = (Lc.H1 / kTile) % 2 == 0 ? 2 : 1, ckw = kTile * cka, cq = ckw / 4;
+            constexpr int NMk = (cBp + 255) / 256, NH1 = (cBp * cq + 255) / 256;
             int mr[NMk];
             float4 hr[NH1];
             float wh = 0.0f;
@@ -894,8 +900,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
 #pragma unroll
             for (int j = 0; j < NH1; ++j) {
-                const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
-                hr[j] = (u < cBp * 4 && b < cB && k0 + 4 * c4 < Lc.H1)
+                const int u = tid + 256 * j, b = u / cq, c4 = u % cq;
+                hr[j] = (u < cBp * cq && b < cB && k0 + 4 * c4 < Lc.H1)
                             ? *reinterpret_cast<const float4 *>(h1 + (int64_t)b * Lc.H1 + k0 + 4 * c4)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
             }
@@ -914,8 +920,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 if (tid + 256 * j < cBp) mkA[tid + 256 * j] = mr[j];
 #pragma unroll
             for (int j = 0; j < NH1; ++j) {
-                const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
-                if (u < cBp * 4) {
+                const int u = tid + 256 * j, b = u / cq, c4 = u % cq;
+                if (u < cBp * cq) {
                     h1T[(4 * c4 + 0) * ld + b] = hr[j].x;
                     h1T[(4 * c4 + 1) * ld + b] = hr[j].y;
                     h1T[(4 * c4 + 2) * ld + b] = hr[j].z;
@@ -933,9 +939,10 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 whs[tid] = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
             }
             for (int b = tid; b < Bp; b += 256) mkA[b] = b < B ? (int)h2mask[(int64_t)b * sh.ncb + nb] : 0;
+            const int q4 = kw / 4;
 #pragma unroll 4
-            for (int u = tid; u < Bp * 4; u += 256) {
-                const int b = u >> 2, c4 = u & 3;
+            for (int u = tid; u < Bp * q4; u += 256) {
+                const int b = u / q4, c4 = u - b * q4;
                 float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (b < B && k0 + 4 * c4 < H1)
                     gv = *reinterpret_cast<const float4 *>(h1 + (int64_t)b * H1 + k0 + 4 * c4);
@@ -977,48 +984,53 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         GS_STAMP(1)
         const int nch = Bp / kTile;
         const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        // t < ka: dW2 tiles; t == ka (k-block-0 workgroups only): db2[n] = sum_b dh2[b, n] as an
+        // MFMA against a ones operand (every output column equals db2)
+        const int nt = sh.ka + (kb == 0 ? 1 : 0);
+        for (int t = 0; t < nt; ++t) {
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+            const float *hb = h1T + t * kTile * ld;
+            const bool ones = t == sh.ka;
 #pragma unroll 4
-        for (int ch = ch0; ch < ch1; ++ch) {
-            const int b = ch * kTile + 4 * lq;
-            const float4 a = *reinterpret_cast<const float4 *>(dh2T + li * ld + b);
-            const float4 bb = *reinterpret_cast<const float4 *>(h1T + li * ld + b);
-            acc0 = mfma4(a.x, bb.x, acc0);
-            acc1 = mfma4(a.y, bb.y, acc1);
-            acc0 = mfma4(a.z, bb.z, acc0);
-            acc1 = mfma4(a.w, bb.w, acc1);
-        }
-        const f32x4 acc = acc0 + acc1;
+            for (int ch = ch0; ch < ch1; ++ch) {
+                const int b = ch * kTile + 4 * lq;
+                const float4 a = *reinterpret_cast<const float4 *>(dh2T + li * ld + b);
+                const float4 bb = ones ? make_float4(1.f, 1.f, 1.f, 1.f)
+                                       : *reinterpret_cast<const float4 *>(hb + li * ld + b);
+                acc0 = mfma4(a.x, bb.x, acc0);
+                acc1 = mfma4(a.y, bb.y, acc1);
+                acc0 = mfma4(a.z, bb.z, acc0);
+                acc1 = mfma4(a.w, bb.w, acc1);
+            }
+            const f32x4 acc = acc0 + acc1;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
+            for (int r = 0; r < 4; ++r) red[(wave * 3 + t) * 256 + (lq * 4 + r) * kTile + li] = acc[r];
+        }
         __syncthreads();
         GS_STAMP(2)
-        const int row = tid >> 4, col = tid & 15;
-        const float g = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
-        float sq = 0.0f;
-        if (n0 + row < H2 && k0 + col < H1) {
-            G[L.oW2 + (int64_t)(n0 + row) * H1 + k0 + col] = g;
-            sq = g * g;
-        }
-        block_sumsq_store(sq, sumsq + bid, sbuf);
-        if (kb == 0) {
-            // db2[n] = sum_b dh2[b, n]: 16 partial sums per n in LDS (red), then 16 lanes
-            const int i = tid >> 4, j = tid & 15;
-            float s = 0.0f;
-            for (int b = j; b < Bp; b += 16) s += dh2T[i * ld + b];
-            red[tid] = s;
-            __syncthreads();
-            float sq2 = 0.0f;
-            if (tid < kTile) {
-                float t = 0.0f;
-#pragma unroll
-                for (int m = 0; m < 16; ++m) t += red[tid * 16 + m];
-                if (n0 + tid < H2) {
-                    G[L.ob2 + n0 + tid] = t;
-                    sq2 = t * t;
+        {
+            // one sum-of-squares slot per dW2 tile (tile index nb*nkb + kb + t), one for db2
+            const int row = tid >> 4, col = tid & 15;
+            float sqt[3] = {0.0f, 0.0f, 0.0f};
+            for (int t = 0; t < nt; ++t) {
+                const float g = ((red[(0 + t) * 256 + tid] + red[(3 + t) * 256 + tid]) + red[(6 + t) * 256 + tid]) +
+                                red[(9 + t) * 256 + tid];
+                if (t < sh.ka) {
+                    const int kc = k0 + t * kTile + col;
+                    if (n0 + row < H2 && kc < H1) {
+                        G[L.oW2 + (int64_t)(n0 + row) * H1 + kc] = g;
+                        sqt[t] = g * g;
+                    }
+                } else if (col == 0 && n0 + row < H2) {
+                    G[L.ob2 + n0 + row] = g;
+                    sqt[2] = g * g;
                 }
             }
-            block_sumsq_store(sq2, sumsq + sh.nA + nb, sbuf);
+            block_reduce<3>(sqt, reinterpret_cast<float *>(mkA + Bp));   // 3 x (256 + 16) floats
+            if (tid == 0) {
+                for (int t = 0; t < sh.ka; ++t) sumsq[nb * sh.nkb + kb + t] = sqt[t];
+                if (kb == 0) sumsq[sh.nT + nb] = sqt[2];
+            }
         }
         GS_STAMP_END(3)
         return;
@@ -1393,7 +1405,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     }
                 }
             }
-            block_sumsq_store(sq, sumsq + sh.nA + sh.ncb + nb, sbuf);
+            block_sumsq_store(sq, sumsq + sh.nT + sh.ncb + nb, sbuf);
         } else {
             // the extra block: head-bias gradients (sum of dz over the batch)
             for (int u = tid; u < A1 * 16; u += 256) {
@@ -1411,7 +1423,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 G[L.head_bias(tid)] = s;
                 sqb = s * s;
             }
-            block_sumsq_store(sqb, sumsq + sh.nA + 2 * sh.ncb, sbuf);
+            block_sumsq_store(sqb, sumsq + sh.nT + 2 * sh.ncb, sbuf);
         }
         GS_STAMP_END(1)
     }
