@@ -278,23 +278,30 @@ struct MRow {
     float lse, m2, S;
 };
 
-__device__ __forceinline__ MRow mrow_stats(const float *z, const CnnLayout &L)
+// AM: compile-time bound on the action count, so every per-action array of the callers is
+// indexed statically and stays in registers (a runtime bound put them in scratch memory)
+template <int AM>
+__device__ __forceinline__ MRow mrow_stats(const float (&z)[AM + 1], const CnnLayout &L)
 {
     float m = -INFINITY;
-    for (int a = 0; a < L.A; ++a)
-        if (L.is_valid(a)) m = fmaxf(m, z[a]);
+#pragma unroll
+    for (int a = 0; a < AM; ++a)
+        if (a < L.A && L.is_valid(a)) m = fmaxf(m, z[a]);
     float se = 0.f;
-    for (int a = 0; a < L.A; ++a)
-        if (L.is_valid(a)) se += expf(z[a] - m);
+#pragma unroll
+    for (int a = 0; a < AM; ++a)
+        if (a < L.A && L.is_valid(a)) se += expf(z[a] - m);
     MRow h;
     h.lse = m + logf(se);
     float m2 = -INFINITY;
-    for (int a = 0; a < L.A; ++a)
-        if (L.is_valid(a)) m2 = fmaxf(m2, z[a] - h.lse);
+#pragma unroll
+    for (int a = 0; a < AM; ++a)
+        if (a < L.A && L.is_valid(a)) m2 = fmaxf(m2, z[a] - h.lse);
     h.m2 = m2;
     float S = 0.f;
-    for (int a = 0; a < L.A; ++a)
-        if (L.is_valid(a)) S += expf((z[a] - h.lse) - m2);
+#pragma unroll
+    for (int a = 0; a < AM; ++a)
+        if (a < L.A && L.is_valid(a)) S += expf((z[a] - h.lse) - m2);
     h.S = S;
     return h;
 }
@@ -308,6 +315,7 @@ __device__ __forceinline__ uint64_t mix64d(uint64_t x)
 }
 
 // ---- rollout: action select over the valid set, log_prob, value.  One thread per env.
+template <int AM>
 __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
                                                  int64_t R, int mode,
                                                  uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
@@ -316,18 +324,24 @@ __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, co
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= R) return;
     const int A1 = L.A + 1;
-    float zr[kAMax + 1];
-    for (int a = 0; a < A1; ++a) zr[a] = z[r * A1 + a] + (a < L.A ? P[L.obp + a] : P[L.obv]);
-    if (value) value[r] = zr[L.A];
+    float zr[AM + 1];
+    float v = 0.f;
+#pragma unroll
+    for (int a = 0; a < AM + 1; ++a) {
+        zr[a] = a < A1 ? z[r * A1 + a] + (a < L.A ? P[L.obp + a] : P[L.obv]) : 0.f;
+        if (a == L.A) v = zr[a];
+    }
+    if (value) value[r] = v;
     if (!actions) return;
-    const MRow h = mrow_stats(zr, L);
+    const MRow h = mrow_stats<AM>(zr, L);
     int act = -1;
     if (mode == 2) {
         act = (int)actions[r];
     } else if (mode == 1) {
         float best = -INFINITY;
-        for (int a = 0; a < L.A; ++a) {
-            if (!L.is_valid(a)) continue;
+#pragma unroll
+        for (int a = 0; a < AM; ++a) {
+            if (a >= L.A || !L.is_valid(a)) continue;
             const float p = expf((zr[a] - h.lse) - h.m2) / h.S;
             if (p > best) best = p, act = a;
         }
@@ -337,8 +351,9 @@ __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, co
         const float u = (float)(hh >> 40) * (1.0f / 16777216.0f);
         float c = 0.f;
         int last = 0;
-        for (int a = 0; a < L.A; ++a) {
-            if (!L.is_valid(a)) continue;
+#pragma unroll
+        for (int a = 0; a < AM; ++a) {
+            if (a >= L.A || !L.is_valid(a)) continue;
             last = a;
             c += expf((zr[a] - h.lse) - h.m2) / h.S;
             if (act < 0 && u < c) act = a;
@@ -346,7 +361,11 @@ __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, co
         if (act < 0) act = last;
         actions[r] = act;
     }
-    logp[r] = zr[act] - h.lse;
+    float za = 0.f;
+#pragma unroll
+    for (int a = 0; a < AM; ++a)
+        if (a == act) za = zr[a];
+    logp[r] = za - h.lse;
 }
 
 // ---- gather the 5 per-row rollout fields of the minibatch
@@ -397,6 +416,7 @@ constexpr int kLossRows = 256;   // loss rows per workgroup (one per thread)
 static_assert(kSums == 13, "carve() sizes loss_part for 13 sums");
 
 // ---- the PPO loss of one minibatch with (Masked)Categorical heads; one workgroup.
+template <int AM>
 __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
                                                   int B,
                                                   const int32_t *__restrict__ f_act, const float *__restrict__ f_olp,
@@ -430,17 +450,24 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
     const int r_end = min(B, (int)(blockIdx.x + 1) * kLossRows);
     for (int r = blockIdx.x * kLossRows + tid; r < r_end; r += 256) {
-        float zr[kAMax + 1];
-        for (int a = 0; a < A1; ++a) zr[a] = z[(int64_t)r * A1 + a] + (a < A ? P[L.obp + a] : P[L.obv]);
+        float zr[AM + 1];
+        float v = 0.f;
+#pragma unroll
+        for (int a = 0; a < AM + 1; ++a) {
+            zr[a] = a < A1 ? z[(int64_t)r * A1 + a] + (a < A ? P[L.obp + a] : P[L.obv]) : 0.f;
+            if (a == A) v = zr[a];
+        }
         const int act = f_act[r];
         const float olp = f_olp[r], ov = f_ov[r], ret = f_ret[r];
         float adv = f_adv[r];
-        const float v = zr[A];
-        const MRow h = mrow_stats(zr, L);
+        const MRow h = mrow_stats<AM>(zr, L);
         const float invS = 1.0f / h.S;
-        float ln[kAMax], p[kAMax], g[kAMax];
+        float ln[AM], p[AM], g[AM];
         float H = 0.f, lp = 0.f, pg = 0.f;
-        for (int a = 0; a < A; ++a) {
+#pragma unroll
+        for (int a = 0; a < AM; ++a) {
+            ln[a] = -INFINITY, p[a] = 0.f, g[a] = 0.f;
+            if (a >= A) continue;
             const bool va = L.is_valid(a);
             ln[a] = va ? zr[a] - h.lse : -INFINITY;
             p[a] = va ? expf(ln[a] - h.m2) * invS : 0.f;
@@ -491,7 +518,9 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
         const float dlp = dratio * ratio;
         const float dH = -la.ent_coef * invB;
         float *dzr = dz + (int64_t)r * A1;
-        for (int a = 0; a < A; ++a) {
+#pragma unroll
+        for (int a = 0; a < AM; ++a) {
+            if (a >= A) continue;
             if (!L.is_valid(a)) {
                 dzr[a] = 0.f;      // masked_fill blocks the gradient
                 continue;
@@ -800,8 +829,12 @@ int launch_cnn_loss(const float *z, const float *P, const CnnLayout &L, int64_t 
                     float *dz, float *metrics, int32_t *stop, hipStream_t s)
 {
     const int nb = (int)((B + kLossRows - 1) / kLossRows);
-    hipLaunchKernelGGL(k_cnn_loss, dim3((unsigned)nb), dim3(256), 0, s, z, P, L, (int)B, w.f_act, w.f_olp, w.f_ov,
-                       w.f_adv, w.f_ret, la, dz, w.loss_part, stop);
+    if (L.A <= 18)   // the Atari action set
+        hipLaunchKernelGGL(k_cnn_loss<18>, dim3((unsigned)nb), dim3(256), 0, s, z, P, L, (int)B, w.f_act, w.f_olp,
+                           w.f_ov, w.f_adv, w.f_ret, la, dz, w.loss_part, stop);
+    else
+        hipLaunchKernelGGL(k_cnn_loss<kAMax>, dim3((unsigned)nb), dim3(256), 0, s, z, P, L, (int)B, w.f_act, w.f_olp,
+                           w.f_ov, w.f_adv, w.f_ret, la, dz, w.loss_part, stop);
     hipLaunchKernelGGL(k_cnn_loss_final, dim3(1), dim3(64), 0, s, w.loss_part, nb, (int)B, la, metrics, stop);
     GS_LAUNCH_CHECK("k_cnn_loss");
     return GS_OK;
@@ -876,8 +909,12 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, N);
     if ((rc = forward(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s))) return rc;
-    hipLaunchKernelGGL(k_cnn_act, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed, rng_counter, actions,
-                       logp, value);
+    if (L.A <= 18)
+        hipLaunchKernelGGL(k_cnn_act<18>, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed,
+                           rng_counter, actions, logp, value);
+    else
+        hipLaunchKernelGGL(k_cnn_act<kAMax>, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed,
+                           rng_counter, actions, logp, value);
     GS_LAUNCH_CHECK("k_cnn_act");
     return GS_OK;
 }
