@@ -61,7 +61,8 @@ def stage_flops_bytes(D, H1, H2, A, B, P, fused=True):
     bwd = 2.0 * B * H2 * A1 + 2.0 * B * H1 * H2 * 2 + 2.0 * B * H1 * (D + 1) + 2.0 * B * H2 * A1 + B * H2
     adam_bytes = 4.0 * P * 7      # read p, g, m, v; write p, m, v
     if fused:
-        return {"fwd": ("mfma", fwd), "bwd": ("mfma", bwd + loss), "adam": ("hbm", adam_bytes)}
+        return {"fwd": ("mfma", fwd), "fwd_adam": ("mfma", fwd), "bwd": ("mfma", bwd + loss),
+                "adam": ("hbm", adam_bytes)}
     return {"fwd": ("mfma", fwd), "loss": ("mfma", loss), "bwd": ("mfma", bwd), "adam": ("hbm", adam_bytes)}
 
 
@@ -80,9 +81,17 @@ def time_stages(agent, reps: int):
     saved = [t.clone() for t in (pm.params, agent.grads, agent.adam_m, agent.adam_v)]
     out = {}
     # the fused chain (what gs_ppo_update runs for the compile-time shapes): gather once,
-    # then k_fwd_hidden<fused>, k_bwd<fused> (loss rows inside), k_clip_adam
+    # then k_fwd_hidden<fused>, k_bwd<fused> (loss rows inside), k_clip_adam.  On one GPU the
+    # clip + Adam step rides in the next minibatch's forward (stage 7, k_fwd_hidden<fused, adam>)
+    # and k_clip_adam runs once per update, so it is not a per-minibatch stage there.
     fused = lib.gs_ppo_stage(*args(6)) == 0
-    stages = ((4, "fwd"), (5, "bwd"), (3, "adam")) if fused else ((0, "fwd"), (1, "loss"), (2, "bwd"), (3, "adam"))
+    lagged = fused and agent.comm is None and lib.gs_ppo_stage(*args(7)) == 0
+    if lagged:
+        stages = ((7, "fwd_adam"), (5, "bwd"))
+    elif fused:
+        stages = ((4, "fwd"), (5, "bwd"), (3, "adam"))
+    else:
+        stages = ((0, "fwd"), (1, "loss"), (2, "bwd"), (3, "adam"))
     for st, name in stages:
         for _ in range(3):
             check(lib.gs_ppo_stage(*args(st)), "gs_ppo_stage")
@@ -289,7 +298,7 @@ def main():
         work = stage_flops_bytes(pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions, agent.batch_size,
                                  pm.n_params, fused)
         dom = max(stage_us, key=stage_us.get)
-        kname = {"fwd": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}
+        kname = {"fwd": "k_fwd_hidden", "fwd_adam": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}
         for st, us in stage_us.items():
             rooflines[st] = roofline_entry(work[st][0], work[st][1], us, kname[st])
         roofline = {k: v for k, v in rooflines[dom].items()}

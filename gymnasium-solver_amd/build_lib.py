@@ -19,7 +19,7 @@ ARCH = "gfx950"
 
 # per-file extra flags: the GAE scan must not contract mul+add into FMA (bit-exactness
 # with the reference's numpy float32 loop)
-EXTRA = {"gs_gae.hip": ["-ffp-contract=off"], "gs_atari.hip": ["-ffp-contract=off"],
+EXTRA = {"gs_gae.hip": ["-ffp-contract=off"], "gs_mlp.hip": ["-ffp-contract=off"], "gs_atari.hip": ["-ffp-contract=off"],
          "gs_cartpole.hip": ["-ffp-contract=off"]}
 
 

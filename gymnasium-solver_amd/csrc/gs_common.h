@@ -189,12 +189,26 @@ struct AdamArgs {
     int stage_lds;          // set by the launcher: stage slots + partials through LDS
 };
 
+// Lagged optimizer step of the single-GPU fused chain (gs_ppo_update): the forward of
+// minibatch k first applies minibatch k-1's clip + Adam step to the parameters it reads
+// (k_fwd_hidden<S, true, true>); the row-block-0 workgroups write the results into the other
+// parameter set, which the backward of k then reads.
+struct AdamFwd {
+    const float *Min, *Vin;            // moments of the set the kernel's P belongs to
+    const float *G, *part1, *sumsq;    // step k-1's head/W2 grads, dW1|db1 partials, per-tile sums
+    float *Pout, *Mout, *Vout;         // the other set
+    float *metrics;                    // the update's records (GS_M_GRAD_NORM of step k-1)
+    AdamArgs aa;                       // step k-1's schedule: aa.sched[2(k-1)] when set, else the scalars
+    int force;                         // apply at k = 0 too (gs_ppo_stage timing)
+};
+
 inline int n_col_blocks(int H) { return (H + kTile - 1) / kTile; }
 inline int n_sumsq_slots(const Layout &L) { return n_col_blocks(L.H2) * n_col_blocks(L.H1) + 2 * n_col_blocks(L.H2) + 1; }
 
 // kernels' launch helpers (gs_mlp.hip)
 int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
-                     const Workspace &ws, const int32_t *stop, hipStream_t s);
+                     const Workspace &ws, const int32_t *stop, hipStream_t s, const AdamFwd *af = nullptr);
+bool has_lagged(const Layout &L, int64_t B);
 int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx, const float *obs,
                       const int64_t *actions, const float *logprobs, const float *values, const float *advantages,
                       const float *returns, int64_t T, int64_t N, int normalize, const FusedFwd &ff, float *metrics,

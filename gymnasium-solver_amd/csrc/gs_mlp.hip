@@ -117,6 +117,31 @@ __device__ __forceinline__ void copy_to_lds(float *dst, const float *src, int n)
     }
 }
 
+// clip_grad_norm_'s coefficient (max_norm <= 0: no clip; agents/base_agent.py:591-621)
+__device__ __forceinline__ float clip_coef(float total, const AdamArgs &aa)
+{
+    float coef = 1.0f;
+    if (aa.max_norm > 0.0f) {
+        coef = aa.max_norm / (total + 1e-6f);
+        coef = fminf(coef, 1.0f);
+    }
+    return coef;
+}
+
+// One parameter of torch.optim.Adam (single-tensor path, amsgrad off) on the clipped gradient;
+// shared by k_clip_adam and the lagged step in k_fwd_hidden so both round identically.
+__device__ __forceinline__ float adam_param(float graw, float coef, float &m, float &v, float &p,
+                                            const AdamArgs &aa, float neg_step, float bc2s)
+{
+    const float g = graw * coef;
+    m = m + aa.one_minus_b1 * (g - m);            // exp_avg.lerp_(grad, 1 - beta1)
+    v = v * aa.b2;                                // exp_avg_sq.mul_(beta2)
+    v = v + (aa.one_minus_b2 * g) * g;            //   .addcmul_(grad, grad, 1 - beta2)
+    const float denom = sqrtf(v) / bc2s + aa.eps;
+    p = p + neg_step * (m / denom);
+    return g;
+}
+
 // ------------------------------------------------------------------------------------
 // k_fwd_hidden: grid (ceil(H2/16), ceil(rows/16)), 256 threads.
 // LDS (floats): srcs[16] W1s[H1*D] b1s[H1] W2s[16][H1+4] b2s[16] whs[A1][16] xs[16][D]
@@ -142,12 +167,12 @@ __device__ __forceinline__ void loss_row(const float (&z)[AMAX + 1], int A, int 
 // index -> row -> obs chain).  The head combine stays in the next launch (k_loss_rows): an
 // in-launch last-arriver combine costs a release + acquire fence pair (~1.7 us each on
 // gfx950) on top of the skew wait, more than the ~1.45 us kernel boundary it would remove.
-template <class S, bool FUSED>
+template <class S, bool FUSED, bool ADAM = false>
 __global__ __launch_bounds__(256) void k_fwd_hidden(
     const float *__restrict__ P, Layout Lrt, const float *__restrict__ obs, const int32_t *__restrict__ idx, int T,
     int N, int rows, float *__restrict__ x_out, float *__restrict__ h1_out, float *__restrict__ h2_out,
     float *__restrict__ zpart, float *__restrict__ obs_copy, const int32_t *__restrict__ stop, RowGather rg,
-    FusedFwd ff, LossArgs la, uint16_t *__restrict__ h2mask)
+    FusedFwd ff, LossArgs la, uint16_t *__restrict__ h2mask, AdamFwd af = AdamFwd{})
 {
     GS_STAMP_BEGIN(0)
     if (stop && *stop) return;
@@ -178,7 +203,170 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     // compile-time shapes on the fused path: every phase-0 operand goes to registers first
     // (one memory round trip), then to LDS
     constexpr bool kStage0 = FUSED && S::H1c > 0 && (S::H1c * 4) % 4 == 0;
-    if constexpr (kStage0) {
+    constexpr int kW2v = S::H1c > 0 ? kTile * S::H1c / 4 / 256 : 0;
+    float4 w2r[kW2v > 0 ? kW2v : 1];
+    static_assert(!ADAM || (kStage0 && kW2v > 0), "lagged Adam: compile-time fused shapes only");
+    if constexpr (ADAM) {
+        // ---- lagged optimizer step: minibatch k-1's clip + Adam (k_clip_adam<S, NRB, NQ>'s
+        //      norm order and per-parameter arithmetic, so the result is bit-identical) on the
+        //      parameters this workgroup reads: W1|b1, its 16 W2 rows, its b2 and head-weight
+        //      slices, and in workgroup (0,0) the head biases.  Every load is issued in one burst
+        //      with the forward's own; row block 0 writes the results into the other parameter
+        //      set (the rest of the grid still reads this one).
+        constexpr Layout Lc = S::lay(Layout{});
+        constexpr int cD = Lc.D, cH1 = Lc.H1, cA1 = Lc.A + 1, n1 = cH1 * (cD + 1), k4n = cH1 / 4;
+        constexpr int NQ = (n1 / 4 + 255) / 256, NRB = (S::Bc + kRowsB - 1) / kRowsB, NS = 2;
+        static_assert(Lc.oW1 == 0 && Lc.oW2 == n1 && (cH1 * cD) % 4 == 0 && cH1 % 4 == 0, "W1|b1: one float4 region");
+        static_assert(NRB >= 1 && NRB <= 8 && NQ <= 2 && n1 <= kTile * (cH1 + 4), "lagged-Adam register / LDS budget");
+        const AdamArgs &aa = af.aa;
+        const int64_t kprev = kstep - 1 + af.force;
+        const bool apply = kprev >= 0;
+        const bool own1 = apply && cb == 0 && rb == 0, own2 = apply && rb == 0;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 *P4 = reinterpret_cast<const float4 *>(P);
+        const float4 *M4 = reinterpret_cast<const float4 *>(af.Min);
+        const float4 *V4 = reinterpret_cast<const float4 *>(af.Vin);
+        const float4 *G4 = reinterpret_cast<const float4 *>(af.G);
+        const float neg_step = apply && aa.sched ? aa.sched[2 * kprev] : aa.neg_step_size;
+        const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.bc2_sqrt;
+        float xv = 0.0f;
+        if (tid < kTile * cD) {
+            const int i = tid / cD;
+            xv = r0 + i < rows ? ff.xg[(kstep * rows + r0) * cD + tid] : 0.0f;
+        }
+        float4 w1p[NQ], w1m[NQ], w1v[NQ], t[NQ][NRB];     // W1|b1 (param order), dW1|db1 partials
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            const int q = tid + 256 * j;
+            const bool ok = 4 * q < n1, okg = ok && apply;
+            w1p[j] = ok ? P4[q] : z4;
+            w1m[j] = okg ? M4[q] : z4;
+            w1v[j] = okg ? V4[q] : z4;
+#pragma unroll
+            for (int b = 0; b < NRB; ++b)
+                t[j][b] = okg ? reinterpret_cast<const float4 *>(af.part1 + (int64_t)b * n1)[q] : z4;
+        }
+        float4 w2m[kW2v], w2v[kW2v], w2g[kW2v];           // this workgroup's 16 W2 rows
+#pragma unroll
+        for (int j = 0; j < kW2v; ++j) {
+            const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+            const bool ok = c0 + i < H2, okg = ok && apply;
+            const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
+            w2r[j] = ok ? P4[q] : z4;
+            w2m[j] = okg ? M4[q] : z4;
+            w2v[j] = okg ? V4[q] : z4;
+            w2g[j] = okg ? G4[q] : z4;
+        }
+        // scalar slices {p, m, v, g}: b2 (threads < 16), head weights (< 16*A1), head biases ((0,0), < A1)
+        float sb[4] = {0.f, 0.f, 0.f, 0.f}, sw[4] = {0.f, 0.f, 0.f, 0.f}, shb[4] = {0.f, 0.f, 0.f, 0.f};
+        const int64_t ob = tid < kTile && c0 + tid < H2 ? Lc.ob2 + c0 + tid : -1;
+        const int64_t ow = tid < cA1 * kTile && c0 + (tid & 15) < H2 ? Lc.head_row(tid >> 4) + c0 + (tid & 15) : -1;
+        const int64_t oh = own1 && tid < cA1 ? Lc.head_bias(tid) : -1;
+        auto load_slice = [&](float (&e)[4], int64_t o) {
+            if (o < 0) return;
+            e[0] = P[o];
+            if (apply) {
+                e[1] = af.Min[o];
+                e[2] = af.Vin[o];
+                e[3] = af.G[o];
+            }
+        };
+        load_slice(sb, ob);
+        load_slice(sw, ow);
+        load_slice(shb, oh);
+        float sl[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) sl[j] = apply && tid + 256 * j < aa.n_slots ? af.sumsq[tid + 256 * j] : 0.0f;
+        if (tid < kTile * cD) xs[tid] = xv;
+        // global norm -> clip coefficient: the per-tile slots, then the folded dW1|db1 (k_clip_adam's order)
+        float coef = 0.0f;
+        float *w1g = h1s;      // folded dW1|db1 in part1 order (h1s is unused until phase 1)
+        if (apply) {
+            double ss = 0.0;
+#pragma unroll
+            for (int j = 0; j < NS; ++j)
+                if (tid + 256 * j < aa.n_slots) ss += (double)sl[j];
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                float4 g = z4;
+#pragma unroll
+                for (int b = 0; b < NRB; ++b) {
+                    g.x += t[j][b].x;
+                    g.y += t[j][b].y;
+                    g.z += t[j][b].z;
+                    g.w += t[j][b].w;
+                }
+                if (4 * (tid + 256 * j) < n1) {
+                    reinterpret_cast<float4 *>(w1g)[tid + 256 * j] = g;
+                    ss += (double)g.x * (double)g.x;
+                    ss += (double)g.y * (double)g.y;
+                    ss += (double)g.z * (double)g.z;
+                    ss += (double)g.w * (double)g.w;
+                }
+            }
+            double tt[1] = {ss};
+            block_reduce<1>(tt, reinterpret_cast<double *>(red));   // its barriers also publish w1g
+            const float total = (float)sqrt(tt[0]) * aa.grad_scale;
+            coef = clip_coef(total, aa) * aa.grad_scale;
+            if (own1 && tid == 0 && af.metrics) af.metrics[kprev * GS_NUM_METRICS + GS_M_GRAD_NORM] = total;
+        }
+        // Adam on the owned parameters: new values to LDS / registers, and from row block 0 to the other set
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            const int q = tid + 256 * j;
+            if (4 * q >= n1) continue;
+            float4 p4 = w1p[j];
+            if (apply) {
+                float p[4] = {p4.x, p4.y, p4.z, p4.w};
+                float m[4] = {w1m[j].x, w1m[j].y, w1m[j].z, w1m[j].w};
+                float v[4] = {w1v[j].x, w1v[j].y, w1v[j].z, w1v[j].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    adam_param(w1g[part1_index(Lc, 4 * q + e)], coef, m[e], v[e], p[e], aa, neg_step, bc2s);
+                p4 = make_float4(p[0], p[1], p[2], p[3]);
+                if (own1) {
+                    reinterpret_cast<float4 *>(af.Pout)[q] = p4;
+                    reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
+                    reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
+                }
+            }
+            reinterpret_cast<float4 *>(W1s)[q] = p4;
+        }
+        if (apply) {
+#pragma unroll
+            for (int j = 0; j < kW2v; ++j) {
+                const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+                if (c0 + i >= H2) continue;
+                float p[4] = {w2r[j].x, w2r[j].y, w2r[j].z, w2r[j].w};
+                float m[4] = {w2m[j].x, w2m[j].y, w2m[j].z, w2m[j].w};
+                float v[4] = {w2v[j].x, w2v[j].y, w2v[j].z, w2v[j].w};
+                const float g[4] = {w2g[j].x, w2g[j].y, w2g[j].z, w2g[j].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) adam_param(g[e], coef, m[e], v[e], p[e], aa, neg_step, bc2s);
+                w2r[j] = make_float4(p[0], p[1], p[2], p[3]);
+                if (own2) {
+                    const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
+                    reinterpret_cast<float4 *>(af.Pout)[q] = w2r[j];
+                    reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
+                    reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
+                }
+            }
+        }
+        auto step_slice = [&](float (&e)[4], int64_t o, bool own) {
+            if (o < 0 || !apply) return;
+            adam_param(e[3], coef, e[1], e[2], e[0], aa, neg_step, bc2s);
+            if (own) {
+                af.Pout[o] = e[0];
+                af.Mout[o] = e[1];
+                af.Vout[o] = e[2];
+            }
+        };
+        step_slice(sb, ob, own2);
+        step_slice(sw, ow, own2);
+        step_slice(shb, oh, own1);
+        if (tid < kTile) b2s[tid] = sb[0];
+        if (tid < cA1 * kTile) whs[tid] = sw[0];
+    } else if constexpr (kStage0) {
         constexpr Layout Lc = S::lay(Layout{});
         constexpr int cD = Lc.D, cH1 = Lc.H1, cA1 = Lc.A + 1;
         static_assert((cH1 * cD) % 4 == 0 && cH1 % 4 == 0, "float4 staging");
@@ -243,9 +431,9 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     // W2 tile: with compile-time shapes the loads go to registers AFTER the h1 operands, so the
     // barrier below waits only for those (in-order vmcnt) and h1 is computed while the 16 KB
     // tile is still in flight; it is written to LDS after h1.
-    constexpr int kW2v = S::H1c > 0 ? kTile * S::H1c / 4 / 256 : 0;
-    float4 w2r[kW2v > 0 ? kW2v : 1];
-    if constexpr (kW2v > 0) {
+    if constexpr (ADAM) {
+        // w2r holds the updated tile (written to LDS after h1, below)
+    } else if constexpr (kW2v > 0) {
         const int k4n = H1 >> 2;
 #pragma unroll
         for (int j = 0; j < kW2v; ++j) {
@@ -1601,12 +1789,7 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     if (tid == 0) {
         const double tot = tt[0];
         const float total = (float)sqrt(tot) * aa.grad_scale;
-        float coef = 1.0f;
-        if (aa.max_norm > 0.0f) {
-            coef = aa.max_norm / (total + 1e-6f);
-            coef = fminf(coef, 1.0f);
-        }
-        s_coef = coef;
+        s_coef = clip_coef(total, aa);
         if (blockIdx.x == 0 && metrics) metrics[GS_M_GRAD_NORM] = total;
     }
     __syncthreads();
@@ -1616,16 +1799,11 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     float go[4], mo[4], vo[4], po[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const float g = gv[j] * coef;
-        float m = mv[j], v = vv[j];
-        m = m + aa.one_minus_b1 * (g - m);            // exp_avg.lerp_(grad, 1 - beta1)
-        v = v * aa.b2;                                // exp_avg_sq.mul_(beta2)
-        v = v + (aa.one_minus_b2 * g) * g;            //   .addcmul_(grad, grad, 1 - beta2)
-        const float denom = sqrtf(v) / bc2s + aa.eps;
-        go[j] = g;
+        float m = mv[j], v = vv[j], p = pv[j];
+        go[j] = adam_param(gv[j], coef, m, v, p, aa, neg_step, bc2s);
         mo[j] = m;
         vo[j] = v;
-        po[j] = pv[j] + neg_step * (m / denom);
+        po[j] = p;
     }
     if (NRB > 0 && p0 + 3 < L.P) {
         *reinterpret_cast<float4 *>(G + p0) = make_float4(go[0], go[1], go[2], go[3]);
@@ -1906,8 +2084,32 @@ bool has_fused(const Layout &L, int64_t B)
     return ok;
 }
 
+// the lagged optimizer step needs the compile-time W1|b1 / W2-tile register layout
+template <class Sh>
+constexpr bool lagged_shape()
+{
+    if constexpr (Sh::AEX == 0 || Sh::H1c == 0 || Sh::Bc == 0) {
+        return false;
+    } else {
+        constexpr Layout Lc = Sh::lay(Layout{});
+        constexpr int n1 = Lc.H1 * (Lc.D + 1);
+        return (kTile * Lc.H1 / 4) % 256 == 0 && Lc.H1 % 4 == 0 && (Lc.H1 * Lc.D) % 4 == 0 &&
+               (Sh::Bc + kRowsB - 1) / kRowsB <= 8 && (n1 / 4 + 255) / 256 <= 2 && n1 <= kTile * (Lc.H1 + 4);
+    }
+}
+
+bool has_lagged(const Layout &L, int64_t B)
+{
+    bool ok = false;
+    with_shape(L, B, [&](auto sh) {
+        ok = lagged_shape<decltype(sh)>() && n_sumsq_slots(L) <= 512;
+        return GS_OK;
+    });
+    return ok && has_fused(L, B);
+}
+
 int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const FusedFwd &ff, const LossArgs &la,
-                     const Workspace &ws, const int32_t *stop, hipStream_t s)
+                     const Workspace &ws, const int32_t *stop, hipStream_t s, const AdamFwd *af)
 {
     const dim3 grid((unsigned)((L.H2 + kTile - 1) / kTile), (unsigned)((B + kTile - 1) / kTile));
     return with_shape(L, B, [&](auto sh) {
@@ -1915,6 +2117,18 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
         const float *no_obs = nullptr;
         const int32_t *no_idx = nullptr;
         float *no_copy = nullptr;
+        if (af) {   // forward carrying the previous minibatch's clip + Adam (dW1|db1 partials)
+            if constexpr (lagged_shape<Sh>()) {
+                GS_REQUIRE(af->aa.nrb > 0 && af->aa.n_slots <= 512, "lagged Adam: bad slot / partial counts");
+                hipLaunchKernelGGL((k_fwd_hidden<Sh, true, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L,
+                                   no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop,
+                                   RowGather{}, ff, la, ws.h2mask, *af);
+                GS_LAUNCH_CHECK("k_fwd_hidden<fused, adam>");
+                return GS_OK;
+            } else {
+                GS_REQUIRE(false, "lagged Adam: no compile-time instantiation for this shape");
+            }
+        }
         hipLaunchKernelGGL((k_fwd_hidden<Sh, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L, no_obs, no_idx,
                            0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la,
                            ws.h2mask);

@@ -7,6 +7,7 @@
 // Here the whole loop is enqueued from C++ on one stream (no per-minibatch host sync,
 // no .item() calls: metrics stay on device, one record per minibatch).
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <mutex>
 #include <unordered_map>
@@ -140,6 +141,7 @@ struct FusedWs {
     float *xg, *folp, *fov, *fadv, *fret;
     int32_t *fa;
     double *mpart;
+    float *p1, *m1, *v1;    // the lagged chain's second parameter set (params | adam_m | adam_v)
     size_t bytes;       // whole update workspace (step + fused)
 };
 
@@ -161,6 +163,9 @@ FusedWs carve_fused(void *base, const Layout &L, int64_t B, int64_t n)
     f.fadv = (float *)take(sizeof(float) * (size_t)(n * B));
     f.fret = (float *)take(sizeof(float) * (size_t)(n * B));
     f.mpart = (double *)take(sizeof(double) * (size_t)(n * (B / kTile) * 14));
+    f.p1 = (float *)take(sizeof(float) * (size_t)L.P);
+    f.m1 = (float *)take(sizeof(float) * (size_t)L.P);
+    f.v1 = (float *)take(sizeof(float) * (size_t)L.P);
     f.bytes = off;
     return f;
 }
@@ -257,6 +262,39 @@ int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, 
     return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s);
 }
 
+// The lagged optimizer step is opt-in (GS_LAGGED_ADAM=1): bit-identical, but measured slower
+// on MI355X (the forward carrying it runs 14.6 us instead of 4.8 + 4.0 us)
+bool lagged_enabled()
+{
+    const char *e = getenv("GS_LAGGED_ADAM");
+    return e && e[0] == '1';
+}
+
+// The lagged chain's two parameter sets: [0] the caller's params / adam_m / adam_v, [1] a
+// workspace copy.
+struct ParamSet {
+    float *P, *M, *V;
+};
+
+// Minibatch step k with the optimizer step lagged into the next forward (single GPU;
+// bit-identical to enqueue_step_fused): k_fwd_hidden<fused, adam> applies step k-1 (reads set
+// (k+1)&1, its row-block-0 workgroups write set k&1; nothing at k = 0), then k_bwd<fused> on
+// set k&1.  The update's last optimizer step is one k_clip_adam after the loop.
+int enqueue_step_lagged(const ParamSet (&ps)[2], float *G, const Layout &L, const StepArgs &sa_prev, int64_t B,
+                        const FusedFwd &ff, int64_t k, float *metrics, int32_t *stop, const Workspace &ws,
+                        hipStream_t s)
+{
+    const ParamSet &cur = ps[k & 1], &prev = ps[(k & 1) ^ 1];
+    AdamFwd af{};
+    af.Min = prev.M, af.Vin = prev.V, af.G = G, af.part1 = ws.part1, af.sumsq = ws.sumsq;
+    af.Pout = cur.P, af.Mout = cur.M, af.Vout = cur.V;
+    af.metrics = metrics;
+    af.aa = sa_prev.aa;
+    int rc = launch_fwd_fused(prev.P, L, B, ff, sa_prev.la, ws, stop, s, &af);
+    if (rc) return rc;
+    return launch_bwd(cur.P, L, B, ws, G, stop, s, &ff, &sa_prev.la);
+}
+
 int validate_update(const gs_mlp_dims &dims, const gs_rollout_view &ro, int64_t batch, const void *ws)
 {
     int rc = check_dims(dims);
@@ -314,7 +352,7 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
 {
     int rc = validate_update(dims, ro, batch, workspace);
     if (rc) return rc;
-    GS_REQUIRE(stage >= 0 && stage <= 6, "gs_ppo_stage: stage %d not in [0, 6]", stage);
+    GS_REQUIRE(stage >= 0 && stage <= 7, "gs_ppo_stage: stage %d not in [0, 7]", stage);
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
     const StepArgs sa = make_step_args(hp, L, batch, adam_step < 1 ? 1 : adam_step);
@@ -330,6 +368,16 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
             return launch_gather_all(L, batch, 1, idx, ro.obs, ro.actions, ro.logprobs, ro.values, ro.advantages,
                                      ro.returns, ro.T, ro.N, hp.normalize_adv, ff, metrics, s);
         if (stage == 4) return launch_fwd_fused(params, L, batch, ff, sa.la, ws, nullptr, s);
+        if (stage == 7) {   // the lagged forward: minibatch 0 with a clip + Adam step applied first
+            GS_REQUIRE(lagged_enabled() && has_lagged(L, batch), "gs_ppo_stage: no lagged optimizer step here");
+            AdamFwd af{};
+            af.Min = adam_m, af.Vin = adam_v, af.G = grads, af.part1 = ws.part1, af.sumsq = ws.sumsq;
+            af.Pout = fw.p1, af.Mout = fw.m1, af.Vout = fw.v1;
+            af.metrics = metrics;
+            af.aa = sa.aa;
+            af.force = 1;
+            return launch_fwd_fused(params, L, batch, ff, sa.la, ws, nullptr, s, &af);
+        }
         return launch_bwd(params, L, batch, ws, grads, nullptr, s, &ff, &sa.la);
     }
     switch (stage) {
@@ -414,6 +462,11 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
                                ro.advantages, ro.returns, ro.T, ro.N, hp.normalize_adv, ff0, metrics, s);
         if (rc) return rc;
     }
+    // one GPU: minibatch k's clip + Adam runs inside the forward of k+1 (enqueue_step_lagged);
+    // step 0's forward reads set 1, which starts as a copy of the caller's parameters
+    const bool lagged = fused && !comm && lagged_enabled() && has_lagged(L, batch);
+    const ParamSet ps[2] = {{params, adam_m, adam_v}, {fw.p1, fw.m1, fw.v1}};
+    if (lagged) GS_HIP(hipMemcpyAsync(fw.p1, params, sizeof(float) * (size_t)L.P, hipMemcpyDeviceToDevice, s));
     auto step_ff = [&](int64_t k_local, int64_t slot, const int64_t *base) {
         FusedFwd f = ff0;
         f.k_local = (int)k_local;
@@ -421,8 +474,27 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         (void)slot;
         return f;
     };
+    auto lag_step = [&](int64_t k, const int64_t *base, const float *sched, hipStream_t st) {
+        StepArgs sp = make_step_args(hp, L, batch, adam_step0 + k > 0 ? adam_step0 + k : 1);   // step k-1's
+        sp.aa.sched = sched;
+        return enqueue_step_lagged(ps, grads, L, sp, batch, step_ff(k, k, base), k, metrics, stop_flag, ws, st);
+    };
     auto finish = [&]() -> int {
         if (!fused) return GS_OK;
+        if (lagged) {   // the update's last optimizer step, and its result back into the caller's set
+            const int64_t k = n_minibatches - 1;
+            const ParamSet &q = ps[k & 1];
+            const StepArgs sl = make_step_args(hp, L, batch, adam_step0 + k + 1);
+            int rc2 = launch_clip_adam(q.P, L, grads, q.M, q.V, ws.part1, ws.sumsq, sl.aa,
+                                       metrics + k * GS_NUM_METRICS, stop_flag, s);
+            if (rc2) return rc2;
+            if (k & 1) {
+                const size_t nb = sizeof(float) * (size_t)L.P;
+                GS_HIP(hipMemcpyAsync(params, q.P, nb, hipMemcpyDeviceToDevice, s));
+                GS_HIP(hipMemcpyAsync(adam_m, q.M, nb, hipMemcpyDeviceToDevice, s));
+                GS_HIP(hipMemcpyAsync(adam_v, q.V, nb, hipMemcpyDeviceToDevice, s));
+            }
+        }
         StepArgs sa = make_step_args(hp, L, batch, 1);
         return launch_metrics_all(L, batch, n_minibatches, ff0, sa.la, metrics, s);
     };
@@ -433,10 +505,11 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     if (!use_graph) {
         for (int64_t k = 0; k < n_minibatches; ++k) {
             const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
-            rc = fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
-                                            metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
-                       : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
-                                      metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
+            rc = lagged  ? lag_step(k, nullptr, nullptr, s)
+                 : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
+                                              metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
+                         : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                                        metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
             if (rc) return rc;
         }
         return finish();
@@ -455,7 +528,8 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     key.n[1] = n_minibatches;
     key.n[2] = ((int64_t)dims.obs_dim << 48) ^ ((int64_t)dims.hidden1 << 32) ^ ((int64_t)dims.hidden2 << 16) ^ dims.n_actions;
     key.n[3] = (int64_t)(intptr_t)workspace;
-    key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1) ^ (fused ? 1 : 0);
+    key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1) ^ (fused ? 1 : 0) ^
+               ((int64_t)lagged << 62);
     key.n[5] = ro.T * 1000003 + ro.N;
     // host-side hyper-parameters are baked into the capture: include them in the key
     uint32_t hbits[12];
@@ -486,7 +560,9 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
             sa.aa.sched_idx = (int)k;
             sa.aa.step_base = ent.base;
             sa.la.step_base = ent.base;
-            if (fused) {
+            if (lagged) {
+                rc = lag_step(k, ent.base, ent.sched, cs);
+            } else if (fused) {
                 LossArgs la_f = sa.la;
                 la_f.step_base = nullptr;      // the fused fwd takes its base from FusedFwd
                 StepArgs saf = sa;
@@ -529,9 +605,10 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     }
     for (int64_t k = n_full * chunk; k < n_minibatches; ++k) {
         const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
-        rc = fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
-                                        metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
-                   : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+        rc = lagged  ? lag_step(k, nullptr, nullptr, s)
+             : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
+                                          metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
+                     : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
                                   metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
         if (rc) return rc;
     }

@@ -31,15 +31,18 @@ def main():
     pm = agent.policy_model
     idx = agent.prefetcher.device_buf
     def stage(st):
-        check(lib.gs_ppo_stage(st, pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
-                               agent.adam_v.data_ptr(), pm.dims, agent.hparams(),
-                               agent.get_rollout_collector("train").buffer.view(), idx.data_ptr(),
-                               agent.batch_size, 1, agent.metrics_buf.data_ptr(), agent.workspace.data_ptr(),
-                               torch.cuda.current_stream().cuda_stream), "gs_ppo_stage")
-    stage(6)                     # the fused chain's per-update gather (what gs_ppo_update runs)
-    for st in (4, 5, 3):         # k_fwd_hidden<fused>, k_bwd<fused>, k_clip_adam
+        return lib.gs_ppo_stage(st, pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                                agent.adam_v.data_ptr(), pm.dims, agent.hparams(),
+                                agent.get_rollout_collector("train").buffer.view(), idx.data_ptr(),
+                                agent.batch_size, 1, agent.metrics_buf.data_ptr(), agent.workspace.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
+    check(stage(6), "gs_ppo_stage")   # the fused chain's per-update gather (what gs_ppo_update runs)
+    # the forward carrying the previous step's clip + Adam (stage 7, what gs_ppo_update runs on
+    # one GPU) when available, else the plain fused forward (4); k_bwd<fused>; k_clip_adam
+    fwd = 7 if stage(7) == 0 else 4
+    for st in (fwd, 5, 3):
         for _ in range(a.reps):
-            stage(st)
+            check(stage(st), "gs_ppo_stage")
     # the GAE scan on the C2 rollout buffer, and on a C3-shaped (2048 x 1024) random rollout
     from gsamd.rollout import compute_batched_gae_advantages_and_returns as gae
     buf = agent.get_rollout_collector("train").buffer
