@@ -223,10 +223,14 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         const bool apply = kprev >= 0;
         const bool own1 = apply && cb == 0 && rb == 0, own2 = apply && rb == 0;
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 *P4 = reinterpret_cast<const float4 *>(P);
-        const float4 *M4 = reinterpret_cast<const float4 *>(af.Min);
-        const float4 *V4 = reinterpret_cast<const float4 *>(af.Vin);
-        const float4 *G4 = reinterpret_cast<const float4 *>(af.G);
+        // global-address-space float4 loads (the AdamFwd pointers would otherwise lower to flat,
+        // and a predicated float4 select to four dword loads); the moment / gradient buffers are
+        // valid memory at k = 0 too, so only the range conditions stay
+        auto ld4 = [](const float *base, int64_t q) {
+            const f32x4 v = *(const __attribute__((address_space(1))) f32x4 *)(base + 4 * q);
+            return make_float4(v[0], v[1], v[2], v[3]);
+        };
+        auto ld1 = [](const float *base, int64_t o) { return *(const __attribute__((address_space(1))) float *)(base + o); };
         const float neg_step = apply && aa.sched ? aa.sched[2 * kprev] : aa.neg_step_size;
         const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.bc2_sqrt;
         float xv = 0.0f;
@@ -239,12 +243,12 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         for (int j = 0; j < NQ; ++j) {
             const int q = tid + 256 * j;
             const bool ok = 4 * q < n1, okg = ok && apply;
-            w1p[j] = ok ? P4[q] : z4;
-            w1m[j] = okg ? M4[q] : z4;
-            w1v[j] = okg ? V4[q] : z4;
+            (void)okg;
+            w1p[j] = ok ? ld4(P, q) : z4;
+            w1m[j] = ok ? ld4(af.Min, q) : z4;
+            w1v[j] = ok ? ld4(af.Vin, q) : z4;
 #pragma unroll
-            for (int b = 0; b < NRB; ++b)
-                t[j][b] = okg ? reinterpret_cast<const float4 *>(af.part1 + (int64_t)b * n1)[q] : z4;
+            for (int b = 0; b < NRB; ++b) t[j][b] = ok ? ld4(af.part1 + (int64_t)b * n1, q) : z4;
         }
         float4 w2m[kW2v], w2v[kW2v], w2g[kW2v];           // this workgroup's 16 W2 rows
 #pragma unroll
@@ -252,10 +256,11 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
             const bool ok = c0 + i < H2, okg = ok && apply;
             const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
-            w2r[j] = ok ? P4[q] : z4;
-            w2m[j] = okg ? M4[q] : z4;
-            w2v[j] = okg ? V4[q] : z4;
-            w2g[j] = okg ? G4[q] : z4;
+            (void)okg;
+            w2r[j] = ok ? ld4(P, q) : z4;
+            w2m[j] = ok ? ld4(af.Min, q) : z4;
+            w2v[j] = ok ? ld4(af.Vin, q) : z4;
+            w2g[j] = ok ? ld4(af.G, q) : z4;
         }
         // scalar slices {p, m, v, g}: b2 (threads < 16), head weights (< 16*A1), head biases ((0,0), < A1)
         float sb[4] = {0.f, 0.f, 0.f, 0.f}, sw[4] = {0.f, 0.f, 0.f, 0.f}, shb[4] = {0.f, 0.f, 0.f, 0.f};
@@ -264,19 +269,17 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         const int64_t oh = own1 && tid < cA1 ? Lc.head_bias(tid) : -1;
         auto load_slice = [&](float (&e)[4], int64_t o) {
             if (o < 0) return;
-            e[0] = P[o];
-            if (apply) {
-                e[1] = af.Min[o];
-                e[2] = af.Vin[o];
-                e[3] = af.G[o];
-            }
+            e[0] = ld1(P, o);
+            e[1] = ld1(af.Min, o);
+            e[2] = ld1(af.Vin, o);
+            e[3] = ld1(af.G, o);
         };
         load_slice(sb, ob);
         load_slice(sw, ow);
         load_slice(shb, oh);
         float sl[NS];
 #pragma unroll
-        for (int j = 0; j < NS; ++j) sl[j] = apply && tid + 256 * j < aa.n_slots ? af.sumsq[tid + 256 * j] : 0.0f;
+        for (int j = 0; j < NS; ++j) sl[j] = tid + 256 * j < aa.n_slots ? ld1(af.sumsq, tid + 256 * j) : 0.0f;
         if (tid < kTile * cD) xs[tid] = xv;
         // global norm -> clip coefficient: the per-tile slots, then the folded dW1|db1 (k_clip_adam's order)
         float coef = 0.0f;

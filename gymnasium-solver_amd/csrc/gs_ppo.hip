@@ -262,8 +262,8 @@ int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, 
     return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s);
 }
 
-// The lagged optimizer step is opt-in (GS_LAGGED_ADAM=1): bit-identical, but measured slower
-// on MI355X (the forward carrying it runs 14.6 us instead of 4.8 + 4.0 us)
+// The lagged optimizer step is opt-in (GS_LAGGED_ADAM=1): bit-identical, but no faster on
+// MI355X (the forward carrying it runs 9.9 us instead of 4.7 + 4.1 us)
 bool lagged_enabled()
 {
     const char *e = getenv("GS_LAGGED_ADAM");

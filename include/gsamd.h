@@ -201,7 +201,7 @@ int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float 
  * allocation is); unaligned buffers take the index-chasing chain.  The workspace also holds a
  * second params | adam_m | adam_v set for the opt-in lagged chain (GS_LAGGED_ADAM=1 in the
  * environment, single GPU: each minibatch's clip + Adam runs inside the next forward kernel;
- * bit-identical results, measured slower on MI355X). */
+ * bit-identical results, no faster on MI355X). */
 size_t gs_ppo_update_workspace_bytes(gs_mlp_dims dims, int64_t batch, int64_t n_minibatches);
 
 /* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)
