@@ -174,8 +174,8 @@ int gs_ppo_loss(const float *params_dev, gs_mlp_dims dims, gs_ppo_hparams hp, gs
  * 0 = k_fwd_hidden, 1 = k_loss, 2 = k_bwd, 3 = k_clip_adam.  Fused chain (the one
  * gs_ppo_update runs for the compile-time shapes): 6 = k_gather_all for a one-minibatch
  * update (run once first), 4 = k_fwd_hidden<fused>, 5 = k_bwd<fused> (loss rows inside),
- * then 3; 7 = k_fwd_hidden<fused> carrying the previous minibatch's clip + Adam step (the opt-in
- * lagged chain, GS_LAGGED_ADAM=1; writes the update workspace's second parameter set, so the
+ * then 3; 7 = k_fwd_hidden<fused> carrying the previous minibatch's clip + Adam step (the
+ * lagged chain gs_ppo_update runs on one GPU; writes the update workspace's second parameter set, so the
  * workspace must be gs_ppo_update_workspace_bytes(dims, batch, n >= 1) large).  Used by bench.py
  * to time each kernel with events on the stream it is launched on (roofline measurement). */
 int gs_ppo_stage(int stage, float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
@@ -199,9 +199,9 @@ int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float 
  * (>= gs_ppo_workspace_bytes) selects the index-chasing chain with bit-identical parameters.
  * The fused chain also needs params/grads/adam_m/adam_v 16-byte aligned (every torch
  * allocation is); unaligned buffers take the index-chasing chain.  The workspace also holds a
- * second params | adam_m | adam_v set for the opt-in lagged chain (GS_LAGGED_ADAM=1 in the
- * environment, single GPU: each minibatch's clip + Adam runs inside the next forward kernel;
- * bit-identical results, no faster on MI355X). */
+ * second params | adam_m | adam_v set for the lagged chain (single GPU: each minibatch's clip +
+ * Adam runs inside the next forward kernel; bit-identical results; GS_LAGGED_ADAM=0 in the
+ * environment selects a separate clip/Adam launch instead). */
 size_t gs_ppo_update_workspace_bytes(gs_mlp_dims dims, int64_t batch, int64_t n_minibatches);
 
 /* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)

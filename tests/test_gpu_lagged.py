@@ -1,8 +1,8 @@
 """The fused chain's lagged optimizer step: on one GPU, minibatch k's clip +
 Adam runs inside the forward kernel of minibatch k+1, alternating between the caller's
 parameter set and a workspace copy.  It must give bit for bit the update of the chain with a
-separate k_clip_adam launch per minibatch.  The lagged chain is opt-in (GS_LAGGED_ADAM=1; it is
-measured no faster); these tests select each chain explicitly."""
+separate k_clip_adam launch per minibatch.  GS_LAGGED_ADAM=0 selects the separate launch; these tests select
+each chain explicitly."""
 import numpy as np
 import pytest
 import torch
