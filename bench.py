@@ -180,6 +180,63 @@ def time_exchange(comm, n: int, reps: int, device, barrier):
     return us
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def rank_environments(n: int, base: dict, port: int) -> list:
+    """The torch.distributed.run-style environment of each of n local ranks (rank r on GPU r)."""
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n: int, argv, script: str = None, poll_s: float = 0.2) -> int:
+    """`python bench.py --gpus N` without an external launcher: start N child processes of
+    `script` (this file) with argv, one rank per GPU, and wait for them.  The parent never
+    touches the GPU (children are fresh processes, not forks or execs of a GPU-initialised
+    one).  Rank 0's stdout — the JSON line — is inherited; the other ranks' stdout goes to
+    stderr.  If any rank fails, the rest are terminated (they would wait at a barrier) and
+    the first failing exit code is returned."""
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT") or 0) or _free_port()
+    cmd = [sys.executable, "-u", os.path.abspath(script or __file__), *argv]
+    procs = [subprocess.Popen(cmd, env=e, stdout=None if r == 0 else sys.stderr)
+             for r, e in enumerate(rank_environments(n, os.environ, port))]
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]      # poll every rank (no short-circuit)
+            if all(c is not None for c in codes):
+                break
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                _log(f"[bench] a rank exited with {rc}; stopping the others")
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,8 +260,15 @@ def main():
     ap.add_argument("--cpu-minibatches", type=int, default=2000,
                     help="minibatches in the bounded CPU-baseline sample (0 disables)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start one rank per GPU ourselves (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: they must agree")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev_index = 0 if args.same_device else local_rank
@@ -245,6 +309,12 @@ def main():
         else:
             comm = gd.init_device_comm(rank, world, device)
         agent.comm = comm
+    comm_info = None
+    if comm is not None:
+        from gsamd.distributed import comm_info as _comm_info
+        comm_info = _comm_info(comm)
+        if comm_info["nranks"] != world or comm_info["rank"] != rank:
+            raise RuntimeError(f"communicator reports {comm_info}, launcher says rank {rank} of {world}")
     N, T = cfg.n_envs, cfg.n_steps
 
     def barrier():
@@ -370,7 +440,8 @@ def main():
                                   f"{len(cfg.valid_actions or [])},1}}" if pixel else
                                   f"MLP {pm.obs_dim}-{pm.hidden_dims[0]}-{pm.hidden_dims[1]}-{{{pm.n_actions},1}}"),
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph,
-                       "grad_exchange": args.comm if comm is not None else None},
+                       "grad_exchange": args.comm if comm is not None else None,
+                       "comm": comm_info, "same_device": bool(args.same_device)},
             "roofline": roofline,
             "rooflines": rooflines,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},

@@ -78,6 +78,18 @@ extern "C" int gs_comm_allreduce_mean_f32(gs_comm *comm, float *buf, int64_t cou
     return GS_OK;
 }
 
+extern "C" int gs_comm_info(gs_comm *comm, int *nranks, int *rank, int *transport)
+{
+    if (!comm) {
+        gs::set_error("gs_comm_info: null communicator");
+        return GS_E_INVALID;
+    }
+    if (nranks) *nranks = comm->nranks;
+    if (rank) *rank = comm->rank;
+    if (transport) *transport = comm->kind == gs::kCommXgmi ? GS_COMM_XGMI : GS_COMM_RCCL;
+    return GS_OK;
+}
+
 extern "C" int gs_comm_destroy(gs_comm *comm)
 {
     if (!comm) return GS_OK;

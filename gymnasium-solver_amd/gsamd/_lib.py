@@ -106,6 +106,7 @@ def _load():
         "gs_comm_xgmi_connect": (ctypes.c_int, [vp, vp]),
         "gs_comm_status": (ctypes.c_int, [vp]),
         "gs_comm_allreduce_mean_f32": (ctypes.c_int, [vp, vp, i64, vp]),
+        "gs_comm_info": (ctypes.c_int, [vp, vp, vp, vp]),
         "gs_comm_destroy": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -122,7 +123,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status",
-            "gs_comm_allreduce_mean_f32", "gs_comm_destroy")
+            "gs_comm_allreduce_mean_f32", "gs_comm_info", "gs_comm_destroy")
 
 
 def check(rc: int, what: str = "") -> None:

@@ -182,6 +182,13 @@ def init_local_comm(transport: str = "rccl", max_count: int = 1 << 20) -> int:
     return h.value
 
 
+def comm_info(handle: int) -> dict:
+    """{"nranks", "rank", "transport"} as the communicator itself reports them."""
+    n, r, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib.gs_comm_info(handle, ctypes.byref(n), ctypes.byref(r), ctypes.byref(t)), "gs_comm_info")
+    return {"nranks": n.value, "rank": r.value, "transport": "xgmi" if t.value == 1 else "rccl"}
+
+
 def destroy_comm(handle: Optional[int]) -> None:
     if handle:
         check(lib.gs_comm_destroy(handle), "gs_comm_destroy")

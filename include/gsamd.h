@@ -309,6 +309,11 @@ int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint8_t out_han
 int gs_comm_xgmi_connect(struct gs_comm *comm, const uint8_t *handles);
 int gs_comm_status(struct gs_comm *comm);
 int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
+/* What a communicator is: its rank count, this process's rank and the transport
+ * (GS_COMM_RCCL / GS_COMM_XGMI).  Any out pointer may be NULL.  Host-only, no GPU call. */
+#define GS_COMM_RCCL 0
+#define GS_COMM_XGMI 1
+int gs_comm_info(struct gs_comm *comm, int *nranks, int *rank, int *transport);
 int gs_comm_destroy(struct gs_comm *comm);
 
 #ifdef __cplusplus
