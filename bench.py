@@ -81,11 +81,12 @@ def time_stages(agent, reps: int):
     saved = [t.clone() for t in (pm.params, agent.grads, agent.adam_m, agent.adam_v)]
     out = {}
     # the fused chain (what gs_ppo_update runs for the compile-time shapes): gather once,
-    # then k_fwd_hidden<fused>, k_bwd<fused> (loss rows inside), k_clip_adam.  On one GPU the
-    # clip + Adam step rides in the next minibatch's forward (stage 7, k_fwd_hidden<fused, adam>)
-    # and k_clip_adam runs once per update, so it is not a per-minibatch stage there.
+    # then k_fwd_hidden<fused>, k_bwd<fused> (loss rows inside), k_clip_adam.  The clip + Adam
+    # step rides in the next minibatch's forward (stage 7, k_fwd_hidden<fused, adam>; with a
+    # communicator after the exchange) and k_clip_adam runs once per update, so it is not a
+    # per-minibatch stage.
     fused = lib.gs_ppo_stage(*args(6)) == 0
-    lagged = fused and agent.comm is None and lib.gs_ppo_stage(*args(7)) == 0
+    lagged = fused and lib.gs_ppo_stage(*args(7)) == 0
     if lagged:
         stages = ((7, "fwd_adam"), (5, "bwd"))
     elif fused:

@@ -59,6 +59,8 @@ int comm_allreduce_sum(gs_comm *c, float *buf, int64_t n, hipStream_t s, int *wo
 // transport: reduce_part1 + ncclAllReduce + sumsq_flat, same outputs.
 int comm_grad_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots,
                        int32_t *stop, hipStream_t s, int *world);
+// how many sum-of-squares partials comm_grad_exchange writes (host-only)
+int comm_sumsq_slots(const gs_comm *c);
 // xGMI kernel launcher (gs_xgmi.hip)
 int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
                   float scale, hipStream_t s);

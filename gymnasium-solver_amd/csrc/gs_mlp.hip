@@ -221,6 +221,9 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         static_assert(Lc.oW1 == 0 && Lc.oW2 == n1 && (cH1 * cD) % 4 == 0 && cH1 % 4 == 0, "W1|b1: one float4 region");
         static_assert(NRB >= 1 && NRB <= 8 && NQ <= 2 && n1 <= kTile * (cH1 + 4), "lagged-Adam register / LDS budget");
         const AdamArgs &aa = af.aa;
+        // multi-GPU chain: the exchange has already folded dW1|db1 into G (parameter order) and
+        // its per-workgroup sums of squares cover the whole gradient (k_clip_adam<S, 0, 0>'s order)
+        const bool fold = af.part1 != nullptr;
         const int64_t kprev = kstep - 1 + af.force;
         const bool apply = kprev >= 0;
         const bool own1 = apply && cb == 0 && rb == 0, own2 = apply && rb == 0;
@@ -249,8 +252,14 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             w1p[j] = ok ? ld4(P, q) : z4;
             w1m[j] = ok ? ld4(af.Min, q) : z4;
             w1v[j] = ok ? ld4(af.Vin, q) : z4;
+            if (fold) {
 #pragma unroll
-            for (int b = 0; b < NRB; ++b) t[j][b] = ok ? ld4(af.part1 + (int64_t)b * n1, q) : z4;
+                for (int b = 0; b < NRB; ++b) t[j][b] = ok ? ld4(af.part1 + (int64_t)b * n1, q) : z4;
+            } else {
+                t[j][0] = ok ? ld4(af.G, q) : z4;
+#pragma unroll
+                for (int b = 1; b < NRB; ++b) t[j][b] = z4;
+            }
         }
         float4 w2m[kW2v], w2v[kW2v], w2g[kW2v];           // this workgroup's 16 W2 rows
 #pragma unroll
@@ -285,7 +294,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         if (tid < kTile * cD) xs[tid] = xv;
         // global norm -> clip coefficient: the per-tile slots, then the folded dW1|db1 (k_clip_adam's order)
         float coef = 0.0f;
-        float *w1g = h1s;      // folded dW1|db1 in part1 order (h1s is unused until phase 1)
+        float *w1g = h1s;      // dW1|db1: part1 order when folded here, else parameter order (h1s is unused until phase 1)
         if (apply) {
             double ss = 0.0;
 #pragma unroll
@@ -303,10 +312,12 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 }
                 if (4 * (tid + 256 * j) < n1) {
                     reinterpret_cast<float4 *>(w1g)[tid + 256 * j] = g;
-                    ss += (double)g.x * (double)g.x;
-                    ss += (double)g.y * (double)g.y;
-                    ss += (double)g.z * (double)g.z;
-                    ss += (double)g.w * (double)g.w;
+                    if (fold) {
+                        ss += (double)g.x * (double)g.x;
+                        ss += (double)g.y * (double)g.y;
+                        ss += (double)g.z * (double)g.z;
+                        ss += (double)g.w * (double)g.w;
+                    }
                 }
             }
             double tt[1] = {ss};
@@ -315,6 +326,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             coef = clip_coef(total, aa) * aa.grad_scale;
             if (own1 && tid == 0 && af.metrics) af.metrics[kprev * GS_NUM_METRICS + GS_M_GRAD_NORM] = total;
         }
+        GS_STAMP(0)
         // Adam on the owned parameters: new values to LDS / registers, and from row block 0 to the other set
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
@@ -327,7 +339,8 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 float v[4] = {w1v[j].x, w1v[j].y, w1v[j].z, w1v[j].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    adam_param(w1g[part1_index(Lc, 4 * q + e)], coef, m[e], v[e], p[e], aa, neg_step, bc2s);
+                    adam_param(w1g[fold ? part1_index(Lc, 4 * q + e) : 4 * q + e], coef, m[e], v[e], p[e], aa,
+                               neg_step, bc2s);
                 p4 = make_float4(p[0], p[1], p[2], p[3]);
                 if (own1) {
                     reinterpret_cast<float4 *>(af.Pout)[q] = p4;
@@ -371,6 +384,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         step_slice(shb, oh, own1);
         if (tid < kTile) b2s[tid] = sb[0];
         if (tid < cA1 * kTile) whs[tid] = sw[0];
+        GS_STAMP(1)
     } else if constexpr (kStage0) {
         constexpr Layout Lc = S::lay(Layout{});
         constexpr int cD = Lc.D, cH1 = Lc.H1, cA1 = Lc.A + 1;
@@ -457,8 +471,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         }
     }
     __syncthreads();
-    GS_STAMP(0)
-    GS_STAMP(1)
+    GS_STAMP(2)
     // ---- phase 1: h1 = relu(x W1^T + b1) out of LDS; one hidden unit per thread
     for (int k = tid; k < H1; k += 256) {
         float w[8];
@@ -497,7 +510,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         }
     }
     __syncthreads();
-    GS_STAMP(2)
+    GS_STAMP(3)
     // ---- phase 2: h2 tile = h1[16 x H1] . W2[c0:c0+16, :]^T, MFMA, K split over 4 waves
     {
         const int i = lane & 15, q = lane >> 4;
@@ -519,7 +532,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         for (int r = 0; r < 4; ++r) red[wave * 256 + (q * 4 + r) * kTile + i] = acc[r];
     }
     __syncthreads();
-    GS_STAMP(3)
+    GS_STAMP(4)
     {
         const int row = tid >> 4, col = tid & 15;
         const float s = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
@@ -565,7 +578,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
         }
     }
-    GS_STAMP_END(4)
+    GS_STAMP_END(5)
 }
 
 static int set_lds_limit(const void *fn, size_t bytes);
@@ -2124,7 +2137,8 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
         float *no_copy = nullptr;
         if (af) {   // forward carrying the previous minibatch's clip + Adam (dW1|db1 partials)
             if constexpr (lagged_shape<Sh>()) {
-                GS_REQUIRE(af->aa.nrb > 0 && af->aa.n_slots <= 512, "lagged Adam: bad slot / partial counts");
+                GS_REQUIRE((af->part1 ? af->aa.nrb > 0 : af->aa.nrb == 0) && af->aa.n_slots <= 512,
+                           "lagged Adam: bad slot / partial counts");
                 hipLaunchKernelGGL((k_fwd_hidden<Sh, true, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L,
                                    no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop,
                                    RowGather{}, ff, la, ws.h2mask, *af);

@@ -276,23 +276,41 @@ struct ParamSet {
     float *P, *M, *V;
 };
 
-// Minibatch step k with the optimizer step lagged into the next forward (single GPU;
-// bit-identical to enqueue_step_fused): k_fwd_hidden<fused, adam> applies step k-1 (reads set
-// (k+1)&1, its row-block-0 workgroups write set k&1; nothing at k = 0), then k_bwd<fused> on
-// set k&1.  The update's last optimizer step is one k_clip_adam after the loop.
+// The clip + Adam arguments of a step whose gradient went through the exchange: the gradient
+// is final in G (W1 partials folded), the norm comes from the exchange's partial sums, and the
+// sum over ranks is scaled by 1/world inside the norm and the update.
+AdamArgs exchanged_adam_args(const AdamArgs &aa_in, const gs_comm *comm)
+{
+    AdamArgs aa = aa_in;
+    aa.n_slots = comm_sumsq_slots(comm);
+    aa.nrb = 0;
+    aa.grad_scale = 1.0f / (float)comm->nranks;
+    return aa;
+}
+
+// Minibatch step k with the optimizer step lagged into the next forward (bit-identical to
+// enqueue_step_fused): k_fwd_hidden<fused, adam> applies step k-1 (reads set (k+1)&1, its
+// row-block-0 workgroups write set k&1; nothing at k = 0), then k_bwd<fused> on set k&1.
+// With a communicator the chain is fwd(+Adam of k-1) -> bwd -> exchange of k: the exchange is
+// the only seam the multi-GPU step adds.  The update's last optimizer step is one k_clip_adam
+// after the loop.
 int enqueue_step_lagged(const ParamSet (&ps)[2], float *G, const Layout &L, const StepArgs &sa_prev, int64_t B,
                         const FusedFwd &ff, int64_t k, float *metrics, int32_t *stop, const Workspace &ws,
-                        hipStream_t s)
+                        gs_comm *comm, hipStream_t s)
 {
     const ParamSet &cur = ps[k & 1], &prev = ps[(k & 1) ^ 1];
     AdamFwd af{};
-    af.Min = prev.M, af.Vin = prev.V, af.G = G, af.part1 = ws.part1, af.sumsq = ws.sumsq;
+    af.Min = prev.M, af.Vin = prev.V, af.G = G, af.part1 = comm ? nullptr : ws.part1, af.sumsq = ws.sumsq;
     af.Pout = cur.P, af.Mout = cur.M, af.Vout = cur.V;
     af.metrics = metrics;
-    af.aa = sa_prev.aa;
+    af.aa = comm ? exchanged_adam_args(sa_prev.aa, comm) : sa_prev.aa;
     int rc = launch_fwd_fused(prev.P, L, B, ff, sa_prev.la, ws, stop, s, &af);
     if (rc) return rc;
-    return launch_bwd(cur.P, L, B, ws, G, stop, s, &ff, &sa_prev.la);
+    rc = launch_bwd(cur.P, L, B, ws, G, stop, s, &ff, &sa_prev.la);
+    if (rc || !comm) return rc;
+    int world = 1, n_slots = 0;
+    return comm_grad_exchange(comm, G, L.P, Part1Fold{ws.part1, sa_prev.aa.nrb, L}, ws.sumsq, &n_slots, stop, s,
+                              &world);
 }
 
 int validate_update(const gs_mlp_dims &dims, const gs_rollout_view &ro, int64_t batch, const void *ws)
@@ -369,6 +387,8 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
                                      ro.returns, ro.T, ro.N, hp.normalize_adv, ff, metrics, s);
         if (stage == 4) return launch_fwd_fused(params, L, batch, ff, sa.la, ws, nullptr, s);
         if (stage == 7) {   // the lagged forward: minibatch 0 with a clip + Adam step applied first
+            // (the single-GPU form: dW1|db1 folded from the partials; the multi-GPU form reads the
+            // same bytes less the partials, so this is the upper of the two)
             GS_REQUIRE(lagged_enabled() && has_lagged(L, batch), "gs_ppo_stage: no lagged optimizer step here");
             AdamFwd af{};
             af.Min = adam_m, af.Vin = adam_v, af.G = grads, af.part1 = ws.part1, af.sumsq = ws.sumsq;
@@ -426,9 +446,22 @@ struct GraphEntry {
     int64_t *hbase;    // pinned host table r * chunk, the source of each replay's base copy
     float *hsched;     // pinned staging for the schedule table
     hipEvent_t sched_copied;   // the last copy out of hsched (hsched is rewritten after it)
+    uint32_t hbits[12];        // the hyper-parameters baked into exec's kernel arguments (lr excluded)
 };
 std::mutex g_graph_mu;
 std::unordered_map<GraphKey, GraphEntry, GraphKeyHash> g_graphs;
+int64_t g_graph_captures = 0;
+
+// The hyper-parameter bits a capture bakes in.  lr is left out: the graph reads the step size
+// only from the per-step schedule table, which every call refreshes, so an lr schedule replays
+// the same graph.  A change of any other field (a scheduled clip_range, ent_coef, ...)
+// re-captures into the same entry (the old exec is destroyed: no growth over a long run).
+void baked_hparam_bits(const gs_ppo_hparams &hp, uint32_t (&out)[12])
+{
+    gs_ppo_hparams h = hp;
+    h.lr = 0.0f;
+    memcpy(out, &h, sizeof(out));
+}
 
 }  // namespace
 
@@ -462,9 +495,10 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
                                ro.advantages, ro.returns, ro.T, ro.N, hp.normalize_adv, ff0, metrics, s);
         if (rc) return rc;
     }
-    // one GPU: minibatch k's clip + Adam runs inside the forward of k+1 (enqueue_step_lagged);
-    // step 0's forward reads set 1, which starts as a copy of the caller's parameters
-    const bool lagged = fused && !comm && lagged_enabled() && has_lagged(L, batch);
+    // minibatch k's clip + Adam runs inside the forward of k+1 (enqueue_step_lagged), with or
+    // without a communicator; step 0's forward reads set 1, which starts as a copy of the
+    // caller's parameters
+    const bool lagged = fused && lagged_enabled() && has_lagged(L, batch);
     const ParamSet ps[2] = {{params, adam_m, adam_v}, {fw.p1, fw.m1, fw.v1}};
     if (lagged) GS_HIP(hipMemcpyAsync(fw.p1, params, sizeof(float) * (size_t)L.P, hipMemcpyDeviceToDevice, s));
     auto step_ff = [&](int64_t k_local, int64_t slot, const int64_t *base) {
@@ -477,7 +511,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     auto lag_step = [&](int64_t k, const int64_t *base, const float *sched, hipStream_t st) {
         StepArgs sp = make_step_args(hp, L, batch, adam_step0 + k > 0 ? adam_step0 + k : 1);   // step k-1's
         sp.aa.sched = sched;
-        return enqueue_step_lagged(ps, grads, L, sp, batch, step_ff(k, k, base), k, metrics, stop_flag, ws, st);
+        return enqueue_step_lagged(ps, grads, L, sp, batch, step_ff(k, k, base), k, metrics, stop_flag, ws, comm, st);
     };
     auto finish = [&]() -> int {
         if (!fused) return GS_OK;
@@ -485,8 +519,11 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
             const int64_t k = n_minibatches - 1;
             const ParamSet &q = ps[k & 1];
             const StepArgs sl = make_step_args(hp, L, batch, adam_step0 + k + 1);
-            int rc2 = launch_clip_adam(q.P, L, grads, q.M, q.V, ws.part1, ws.sumsq, sl.aa,
-                                       metrics + k * GS_NUM_METRICS, stop_flag, s);
+            int rc2 = comm ? launch_clip_adam(q.P, L, grads, q.M, q.V, nullptr, ws.sumsq,
+                                              exchanged_adam_args(sl.aa, comm), metrics + k * GS_NUM_METRICS,
+                                              stop_flag, s)
+                           : launch_clip_adam(q.P, L, grads, q.M, q.V, ws.part1, ws.sumsq, sl.aa,
+                                              metrics + k * GS_NUM_METRICS, stop_flag, s);
             if (rc2) return rc2;
             if (k & 1) {
                 const size_t nb = sizeof(float) * (size_t)L.P;
@@ -531,23 +568,35 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1) ^ (fused ? 1 : 0) ^
                ((int64_t)lagged << 62);
     key.n[5] = ro.T * 1000003 + ro.N;
-    // host-side hyper-parameters are baked into the capture: include them in the key
     uint32_t hbits[12];
-    memcpy(hbits, &hp, sizeof(hbits));
-    for (int i = 0; i < 12; ++i) key.n[5] = key.n[5] * 31 + hbits[i];
+    baked_hparam_bits(hp, hbits);
     std::lock_guard<std::mutex> lk(g_graph_mu);
     auto it = g_graphs.find(key);
-    if (it == g_graphs.end()) {
+    const bool fresh = it == g_graphs.end();
+    if (!fresh && memcmp(it->second.hbits, hbits, sizeof(hbits)) != 0) {
+        // same buffers, new baked hyper-parameters: drop the old exec, re-capture below
+        GS_HIP(hipEventSynchronize(it->second.sched_copied));
+        GS_HIP(hipStreamSynchronize(s));    // the old exec may still be running on the caller's stream
+        GS_HIP(hipGraphExecDestroy(it->second.exec));
+        it->second.exec = nullptr;
+    }
+    if (fresh || it->second.exec == nullptr) {
         rc = prepare_kernels(L, batch);   // function attributes may not change inside a capture
         if (rc) return rc;
         GraphEntry ent{};
-        GS_HIP(hipMalloc(&ent.sched, sizeof(float) * 2 * (size_t)n_minibatches + 64));
-        ent.base = (int64_t *)((char *)ent.sched + sizeof(float) * 2 * (size_t)n_minibatches);
-        // pinned and never rewritten: an async copy may read it whenever it executes
-        GS_HIP(hipHostMalloc((void **)&ent.hbase, sizeof(int64_t) * (size_t)(n_full + 1), hipHostMallocDefault));
-        for (int64_t r = 0; r <= n_full; ++r) ent.hbase[r] = r * chunk;
-        GS_HIP(hipHostMalloc((void **)&ent.hsched, sizeof(float) * 2 * (size_t)n_minibatches, hipHostMallocDefault));
-        GS_HIP(hipEventCreateWithFlags(&ent.sched_copied, hipEventDisableTiming));
+        if (fresh) {
+            GS_HIP(hipMalloc(&ent.sched, sizeof(float) * 2 * (size_t)n_minibatches + 64));
+            ent.base = (int64_t *)((char *)ent.sched + sizeof(float) * 2 * (size_t)n_minibatches);
+            // pinned and never rewritten: an async copy may read it whenever it executes
+            GS_HIP(hipHostMalloc((void **)&ent.hbase, sizeof(int64_t) * (size_t)(n_full + 1), hipHostMallocDefault));
+            for (int64_t r = 0; r <= n_full; ++r) ent.hbase[r] = r * chunk;
+            GS_HIP(hipHostMalloc((void **)&ent.hsched, sizeof(float) * 2 * (size_t)n_minibatches,
+                                 hipHostMallocDefault));
+            GS_HIP(hipEventCreateWithFlags(&ent.sched_copied, hipEventDisableTiming));
+        } else {
+            ent = it->second;
+        }
+        memcpy(ent.hbits, hbits, sizeof(hbits));
         // capture on a private stream (the caller's may be the legacy NULL stream, which
         // cannot capture); the instantiated graph is then launched on the caller's stream
         hipStream_t cs;
@@ -577,6 +626,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(cs, &dummy);
                 (void)hipStreamDestroy(cs);
+                if (!fresh) g_graphs.erase(it);
                 (void)hipFree(ent.sched);
                 (void)hipHostFree(ent.hbase);
                 (void)hipHostFree(ent.hsched);
@@ -588,7 +638,11 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         GS_HIP(hipStreamDestroy(cs));
         GS_HIP(hipGraphInstantiate(&ent.exec, g, nullptr, nullptr, 0));
         GS_HIP(hipGraphDestroy(g));
-        it = g_graphs.emplace(key, ent).first;
+        ++g_graph_captures;
+        if (fresh)
+            it = g_graphs.emplace(key, ent).first;
+        else
+            it->second = ent;
     }
     GraphEntry &e = it->second;
     GS_HIP(hipEventSynchronize(e.sched_copied));   // the previous call's copy has read hsched
@@ -613,4 +667,12 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         if (rc) return rc;
     }
     return finish();
+}
+
+extern "C" int gs_ppo_graph_cache_info(int64_t *n_entries, int64_t *n_captures)
+{
+    std::lock_guard<std::mutex> lk(g_graph_mu);
+    if (n_entries) *n_entries = (int64_t)g_graphs.size();
+    if (n_captures) *n_captures = g_graph_captures;
+    return GS_OK;
 }

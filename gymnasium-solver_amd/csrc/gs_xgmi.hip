@@ -38,6 +38,7 @@ struct XgmiArgs {
     char *peer[kXgmiMaxRanks];
     int world, rank;
     int64_t cap, n;
+    int region_bytes;     // own region size (buffer descriptor range; < 2 GiB, checked at create)
     int nchunks;
     float scale;
     uint64_t timeout;
@@ -110,6 +111,18 @@ __device__ __forceinline__ float *slot(char *region, int par, int world, int src
     return reinterpret_cast<float *>(region + kXgmiOffData) + ((int64_t)par * world + src) * cap;
 }
 
+// 16-byte load of the own region at byte offset `off` with sc1 (L1 bypass; the uncached region
+// is never held by an L2 either): what a peer wrote through with sc0 sc1 stores, read without an
+// acquire fence (every load of the handed-off bytes is such a load, the writer drained its
+// stores before raising the flag, the flag is polled with a system-scope load: the guide's
+// flag hand-off with sc1 loads in place of the acquire)
+__device__ __forceinline__ float4 load_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+
 __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Part1Fold fold, XgmiArgs xa,
                                                        float *__restrict__ sumsq, int32_t *__restrict__ stop)
 {
@@ -162,16 +175,20 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Pa
         }
     }
     anystop = __syncthreads_or(anystop);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // drop this CU's L1 lines; the region itself is uncached
 
-    // 3. fixed-order sum over sources, write back, sum of squares of the result
+    // 3. fixed-order sum over sources (peers' slots through sc1 loads), write back, sum of
+    //    squares of the result
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(me, 0, xa.region_bytes, 0x00020000);
+    auto src_off = [&](int r, int64_t p) {
+        return (uint32_t)(kXgmiOffData + 4 * (((int64_t)par * xa.world + r) * xa.cap + p));
+    };
     float ss = 0.0f;
     for (int c = w; c < xa.nchunks; c += gridDim.x) {
         const int64_t p = (int64_t)c * kXgmiChunk + tid * 4;
         const float4 own = c == w ? first : own_values(G, fold, xa.n, p);
-        float4 a = xa.rank == 0 ? own : *reinterpret_cast<const float4 *>(slot(me, par, xa.world, 0, xa.cap) + p);
+        float4 a = xa.rank == 0 ? own : load_sc1(rs, src_off(0, p));
         for (int r = 1; r < xa.world; ++r) {
-            const float4 b = r == xa.rank ? own : *reinterpret_cast<const float4 *>(slot(me, par, xa.world, r, xa.cap) + p);
+            const float4 b = r == xa.rank ? own : load_sc1(rs, src_off(r, p));
             a.x += b.x;
             a.y += b.y;
             a.z += b.z;
@@ -202,9 +219,9 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Pa
     }
 }
 
-int nwg_of(const gs_comm *c) { return (int)std::min<int64_t>(c->cap / kXgmiChunk, kXgmiMaxWG); }
-
 }  // namespace
+
+static int nwg_of(const gs_comm *c) { return (int)std::min<int64_t>(c->cap / kXgmiChunk, kXgmiMaxWG); }
 
 int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
                   float scale, hipStream_t s)
@@ -218,6 +235,7 @@ int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float 
     xa.world = c->nranks;
     xa.rank = c->rank;
     xa.cap = c->cap;
+    xa.region_bytes = (int)c->region_bytes;
     xa.n = n;
     xa.nchunks = (int)((n + kXgmiChunk - 1) / kXgmiChunk);
     xa.scale = scale;
@@ -230,6 +248,10 @@ int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float 
     return GS_OK;
 }
 
+constexpr int kRcclNormBlocks = 64;   // k_sumsq_flat partials after an RCCL all-reduce
+
+int comm_sumsq_slots(const gs_comm *c) { return c->kind == kCommXgmi ? nwg_of(c) : kRcclNormBlocks; }
+
 int comm_grad_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots,
                        int32_t *stop, hipStream_t s, int *world)
 {
@@ -238,9 +260,8 @@ int comm_grad_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, f
     int rc;
     if (fold.part1 && (rc = launch_reduce_part1(fold.part1, fold.L, fold.nrb, G, stop, s))) return rc;
     if ((rc = comm_allreduce_sum(c, G, n, s, world, stop))) return rc;
-    constexpr int kNormBlocks = 64;
-    if ((rc = launch_sumsq_flat(G, n, sumsq, kNormBlocks, s))) return rc;
-    *n_slots = kNormBlocks;
+    if ((rc = launch_sumsq_flat(G, n, sumsq, kRcclNormBlocks, s))) return rc;
+    *n_slots = kRcclNormBlocks;
     return GS_OK;
 }
 
@@ -258,6 +279,8 @@ extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is 64 bytes");
     const int64_t cap = (max_count + kXgmiChunk - 1) / kXgmiChunk * kXgmiChunk;
     const size_t bytes = kXgmiOffData + sizeof(float) * 2 * (size_t)nranks * (size_t)cap;
+    GS_REQUIRE(bytes < ((size_t)1 << 31), "gs_comm_xgmi_create: %lld floats x %d ranks exceed the 2 GiB region limit",
+               (long long)max_count, nranks);
     void *p = nullptr;
     GS_HIP(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
     hipError_t e = hipMemset(p, 0, bytes);

@@ -85,6 +85,7 @@ def _load():
         "gs_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64, i64, vp,
                                          vp, vp, sz, vp, ctypes.c_int, vp]),
         "gs_ppo_update_workspace_bytes": (sz, [MlpDims, i64, i64]),
+        "gs_ppo_graph_cache_info": (ctypes.c_int, [vp, vp]),
         "gs_cnn_param_count": (i64, [CnnDims]),
         "gs_cnn_workspace_bytes": (sz, [CnnDims, i64]),
         "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp]),
@@ -120,6 +121,7 @@ lib = _load()
 EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_env_reset", "gs_env_step",
             "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_ppo_update_workspace_bytes",
+            "gs_ppo_graph_cache_info",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status",

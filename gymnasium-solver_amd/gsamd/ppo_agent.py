@@ -17,7 +17,6 @@ minibatch, SURVEY.md §3 Boundaries).
 """
 from __future__ import annotations
 
-import ctypes
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -30,7 +29,7 @@ from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
 from .distributed import allreduce_sum_f64, world_active
-from .schedules import build_schedulers
+from .schedules import SCHEDULABLE, build_schedulers
 
 STAGES = ("train",)
 
@@ -172,6 +171,8 @@ class DevicePPOAgent:
             "adam_step": int(self.adam_step), "run_id": None,
             "config": {k: (list(v) if isinstance(v, tuple) else v) for k, v in dataclasses.asdict(self.config).items()},
             "best_train_reward": float(coll._best_episode_reward),
+            # the schedulable hyper-parameters in effect (a resumed run continues from these)
+            "hyperparameters": {k: float(getattr(self, k)) for k in SCHEDULABLE},
             "rng_states": {"torch": torch.get_rng_state().tolist(),
                            "numpy": {"state_type": np_state[0], "state_keys": np_state[1].tolist(),
                                      "state_pos": int(np_state[2]), "state_has_gauss": int(np_state[3]),
@@ -211,6 +212,12 @@ class DevicePPOAgent:
             self.adam_v.copy_(vt.to(self.device))
             steps = {int(float(st[i]["step"])) for i in st}
             self.adam_step = int(state.get("adam_step", max(steps) if steps else 0))
+            groups = opt.get("param_groups") or []
+            if groups and "lr" in groups[0]:      # torch's Adam.load_state_dict restores lr too
+                self.set_hyperparameter("policy_lr", float(groups[0]["lr"]))
+        for k, v in (state.get("hyperparameters") or {}).items():
+            if k in SCHEDULABLE:
+                self.set_hyperparameter(k, float(v))
         self.current_epoch = int(state.get("epoch", 0))
         coll = self.get_rollout_collector("train")
         coll.total_steps = int(state.get("total_env_steps", 0))
@@ -422,5 +429,3 @@ def build_agent(config, *args, **kwargs):
         raise ValueError(f"device path implements algo_id 'ppo' only, got {algo!r}")
     return DevicePPOAgent(from_reference_config(config), *args, **kwargs)
 
-
-_ = ctypes

@@ -204,6 +204,11 @@ int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float 
  * environment selects a separate clip/Adam launch instead). */
 size_t gs_ppo_update_workspace_bytes(gs_mlp_dims dims, int64_t batch, int64_t n_minibatches);
 
+/* The update graphs gs_ppo_update keeps (one per distinct set of buffers and shapes) and the
+ * number of captures made so far.  lr never causes a re-capture (the graph reads the step size
+ * from a per-call table); a change of another hyper-parameter re-captures in place. */
+int gs_ppo_graph_cache_info(int64_t *n_entries_host, int64_t *n_captures_host);
+
 /* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)
  * Replaces CNNActorCritic (utils/models.py:347-455; conv 8x8s4 -> 4x4s2 -> 3x3s1 with 32/64/64
  * channels, ReLU, Linear F->hidden ReLU, policy/value heads), action masking

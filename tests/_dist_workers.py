@@ -170,10 +170,14 @@ def xgmi_exchange_worker(rank, world, port, result_dir, n, iters):
         dist.destroy_process_group()
 
 
-def xgmi_ppo_worker(rank, world, port, result_dir, use_graph):
+def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", workload="mlp"):
     """Data-parallel PPO update over the xGMI transport: rank-sharded envs, one rollout and
-    2 epochs; every rank saves its final parameters and per-minibatch losses."""
+    2 epochs; every rank saves its final parameters and per-minibatch losses.  lagged="0"
+    selects the chain with a separate clip + Adam launch after each exchange.  workload="cnn":
+    the C5 Breakout rgb_ppo shard (128 envs per rank, NatureCNN, B=1024, 4 epochs) over a
+    32-step rollout, so the 1.69 M-float gradient exchange runs 16 times."""
     os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    os.environ["GS_LAGGED_ADAM"] = lagged
     dist = _init(rank, world, port)
     try:
         import torch
@@ -183,7 +187,10 @@ def xgmi_ppo_worker(rank, world, port, result_dir, use_graph):
         torch.cuda.set_device(0)
         dev = torch.device("cuda:0")
         torch.manual_seed(42)
-        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=256, n_epochs=2))
+        if workload == "cnn":
+            cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(n_envs=128, n_steps=32))
+        else:
+            cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=256, n_epochs=2))
         agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=use_graph,
                                track_stats=False)
         agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)

@@ -22,6 +22,8 @@ def test_checkpoint_round_trip(cuda, tmp_path, env, variant):
     a = _agent(cuda, env, variant)
     a.train_epoch()
     torch.cuda.synchronize()
+    a.set_hyperparameter("policy_lr", 5e-4)        # e.g. where a schedule had moved it
+    a.set_hyperparameter("clip_range", 0.15)
     a.save_checkpoint(tmp_path)
     sd = torch.load(tmp_path / "model.pt", map_location="cpu", weights_only=True)
     assert list(sd) == [n for n, _ in a.policy_model.shapes()]
@@ -36,6 +38,7 @@ def test_checkpoint_round_trip(cuda, tmp_path, env, variant):
     for x, y in ((a.policy_model.params, b.policy_model.params), (a.adam_m, b.adam_m), (a.adam_v, b.adam_v)):
         assert torch.equal(x, y)
     assert b.adam_step == a.adam_step and b.current_epoch == a.current_epoch
+    assert b.policy_lr == 5e-4 and b.clip_range == 0.15      # resumed with the values in effect
     assert b.get_rollout_collector("train").total_steps == a.get_rollout_collector("train").total_steps
     # the state_dict is the reference's layout (the CNN stores conv2/3 and fc permuted inside)
     for n, t in b.policy_model.state_dict().items():
@@ -114,4 +117,43 @@ def test_schedules_applied_between_epochs(cuda):
     assert abs(agent.policy_lr - 1e-4) < 1e-12            # the schedule's end
     agent.set_hyperparameter("clip_range", 0.15)
     assert abs(agent.hparams().clip_range - 0.15) < 1e-7 and cfg.clip_range == 0.15
+    assert np.isfinite(agent.minibatch_losses()).all()
+
+
+def test_scheduled_lr_reuses_the_update_graph(cuda):
+    """a policy_lr schedule changes lr every epoch; the captured update graph must be
+    replayed (lr reaches it through the per-step table), not re-captured, and device memory must
+    not grow.  A scheduled clip_range re-captures in place (same entry count)."""
+    import ctypes
+    from gsamd._lib import lib
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+
+    def info():
+        n, c = ctypes.c_int64(), ctypes.c_int64()
+        assert lib.gs_ppo_graph_cache_info(ctypes.byref(n), ctypes.byref(c)) == 0
+        return n.value, c.value
+
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=64, n_epochs=1, max_env_steps=64 * 32 * 8))
+    cfg.schedules = {"policy_lr": {"schedule": "linear", "start_value": 1e-3, "end_value": 1e-4, "start": 0.0,
+                                   "end": 1.0, "warmup": 0.0}}
+    agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
+    agent.train_epoch()
+    torch.cuda.synchronize()
+    n0, c0 = info()
+    mem0 = torch.cuda.memory_allocated()
+    lrs = []
+    for _ in range(3):
+        lrs.append(agent.hparams().lr)
+        agent.train_epoch()
+    torch.cuda.synchronize()
+    assert len(set(lrs)) == 3                     # the schedule really moved lr
+    assert info() == (n0, c0)                     # no new entry, no re-capture
+    assert torch.cuda.memory_allocated() == mem0
+    # a baked hyper-parameter change re-captures into the same entry
+    agent.set_hyperparameter("clip_range", 0.15)
+    agent.train_epoch()
+    torch.cuda.synchronize()
+    assert info() == (n0, c0 + 1)
     assert np.isfinite(agent.minibatch_losses()).all()

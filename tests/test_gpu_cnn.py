@@ -148,3 +148,29 @@ def test_cnn_update_gathered_rows_and_generic_shapes(cuda, in_shape, T):
     assert abs(rec[12] - total) < 1e-5 * total
     np.testing.assert_allclose(pm.flat_to_reference(grads), gc, atol=2e-5 * np.abs(gc).max(), rtol=0)
     _adam_close(pm.flat_to_reference(pm.params), p1, lr)
+
+
+@pytest.mark.parametrize("transport", ["xgmi", "rccl"])
+def test_cnn_update_local_comm_equals_no_comm(cuda, transport):
+    """gs_cnn_ppo_update with a one-rank communicator (the multi-GPU chain: gradient sum over
+    ranks, 1/world scale in the norm and the update) gives bit for bit the single-GPU update on
+    a C5-shaped shard (Breakout rgb_ppo, NatureCNN, B=1024): parameters, moments, losses."""
+    from gsamd.config import load_config
+    from gsamd.distributed import destroy_comm, init_local_comm
+    from gsamd.ppo_agent import DevicePPOAgent
+    out = []
+    for with_comm in (False, True):
+        torch.manual_seed(42)
+        cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(n_envs=64, n_steps=32, n_epochs=2))
+        agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
+        comm = init_local_comm(transport, agent.policy_model.n_params) if with_comm else None
+        agent.comm = comm
+        agent.train_epoch()
+        torch.cuda.synchronize()
+        out.append([t.cpu().numpy() for t in (agent.policy_model.params, agent.adam_m, agent.adam_v)] +
+                   [agent.minibatch_losses()])
+        del agent
+        destroy_comm(comm)
+    assert np.isfinite(out[0][0]).all()
+    for name, x, y in zip(("params", "adam_m", "adam_v", "losses"), out[0], out[1]):
+        assert np.array_equal(np.ascontiguousarray(x).view(np.uint8), np.ascontiguousarray(y).view(np.uint8)), name

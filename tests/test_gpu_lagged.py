@@ -17,20 +17,25 @@ def _same(name, x, y):
 
 
 # eager; graph-replayed 512-step chunks + an eager tail with the last step landing in the
-# workspace set (768 minibatches: copied back) and in the caller's set (767)
-@pytest.mark.parametrize("use_graph,n_envs,n_epochs,drop", [(False, 512, 2, 1), (True, 2048, 3, 0),
-                                                             (True, 2048, 3, 1)])
-def test_lagged_adam_matches_separate_adam(cuda, monkeypatch, use_graph, n_envs, n_epochs, drop):
-    """Parameters, Adam moments, clipped gradients and metric records bit-identical."""
+# workspace set (768 minibatches: copied back) and in the caller's set (767); and the
+# multi-GPU chain (fwd(+Adam of k-1) -> bwd -> exchange of k) over a one-rank communicator
+@pytest.mark.parametrize("use_graph,n_envs,n_epochs,drop,transport", [
+    (False, 512, 2, 1, None), (True, 2048, 3, 0, None), (True, 2048, 3, 1, None),
+    (False, 512, 2, 1, "xgmi"), (True, 2048, 3, 1, "xgmi"), (True, 2048, 3, 0, "rccl")])
+def test_lagged_adam_matches_separate_adam(cuda, monkeypatch, use_graph, n_envs, n_epochs, drop, transport):
+    """Parameters, Adam moments, the last step's clipped gradients and metric records
+    bit-identical."""
     from gsamd._lib import check, lib
     from gsamd.config import load_config
+    from gsamd.distributed import destroy_comm, init_local_comm
     from gsamd.ppo_agent import DevicePPOAgent
     out = []
     for lag in ("1", "0"):
         monkeypatch.setenv("GS_LAGGED_ADAM", lag)
         torch.manual_seed(7)
         cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=n_envs, n_epochs=n_epochs))
-        agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
+        comm = init_local_comm(transport, 70_000) if transport else None
+        agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False, comm=comm)
         coll = agent.get_rollout_collector("train")
         coll.collect()
         idx = agent.prefetcher.upload(0)
@@ -38,12 +43,13 @@ def test_lagged_adam_matches_separate_adam(cuda, monkeypatch, use_graph, n_envs,
         check(lib.gs_ppo_update(agent.policy_model.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
                                 agent.adam_v.data_ptr(), agent.policy_model.dims, agent.hparams(), coll.buffer.view(),
                                 idx.data_ptr(), agent.batch_size, n, 3, agent.metrics_buf.data_ptr(),
-                                agent.stop_flag.data_ptr(), agent.workspace.data_ptr(), agent.workspace.numel(), None,
+                                agent.stop_flag.data_ptr(), agent.workspace.data_ptr(), agent.workspace.numel(), comm,
                                 1 if use_graph else 0, torch.cuda.current_stream().cuda_stream), "gs_ppo_update")
         torch.cuda.synchronize()
         out.append([t.cpu().numpy() for t in (agent.policy_model.params, agent.adam_m, agent.adam_v, agent.grads,
                                                agent.metrics_buf[:n])])
         del agent
+        destroy_comm(comm)
     assert np.isfinite(out[0][0]).all()
     for name, x, y in zip(("params", "adam_m", "adam_v", "grads", "metrics"), out[0], out[1]):
         _same(name, x, y)

@@ -40,10 +40,11 @@ def _run(target, world, tmp_path, *args, timeout=300):
     assert codes == [0] * world, codes
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_xgmi_exchange_bit_exact(tmp_path, world):
+# 67 651: an MLP-sized vector with an odd tail; 1 693 875: the NatureCNN's parameter count —
+# more chunks than the exchange has workgroups, so each workgroup loops over several chunks
+@pytest.mark.parametrize("world,n,iters", [(2, 67_651, 24), (4, 67_651, 24), (2, 1_693_875, 6)])
+def test_xgmi_exchange_bit_exact(tmp_path, world, n, iters):
     from _dist_workers import exchange_values, xgmi_exchange_worker
-    n, iters = 67_651, 24            # the CartPole MLP's parameter count (odd tail), 12 x each parity
     _run(xgmi_exchange_worker, world, tmp_path, n, iters)
     outs = [np.load(tmp_path / f"x{r}.npy") for r in range(world)]
     for it in range(iters):
@@ -65,3 +66,34 @@ def test_xgmi_data_parallel_ppo_replicas_identical(tmp_path, use_graph):
     assert np.isfinite(p[0]).all() and all(np.isfinite(l).all() for l in losses)
     assert np.array_equal(p[0].view(np.uint32), p[1].view(np.uint32)), "replicas diverged"
     assert not np.array_equal(losses[0], losses[1])      # the ranks trained on different env shards
+
+
+def test_xgmi_cnn_data_parallel_replicas_identical(tmp_path):
+    """C5's sharded path: 2 ranks, each with its own 128 Breakout envs, NatureCNN update with the
+    1.69 M-float gradient exchanged every minibatch; replicas end bitwise identical."""
+    from _dist_workers import xgmi_ppo_worker
+    world = 2
+    _run(xgmi_ppo_worker, world, tmp_path, False, "1", "cnn", timeout=400)
+    p = [np.load(tmp_path / f"p{r}.npy") for r in range(world)]
+    losses = [np.load(tmp_path / f"l{r}.npy") for r in range(world)]
+    assert p[0].size == 1_693_875 and np.isfinite(p[0]).all()
+    assert np.array_equal(p[0].view(np.uint32), p[1].view(np.uint32)), "replicas diverged"
+    assert not np.array_equal(losses[0], losses[1])
+
+
+def test_xgmi_lagged_chain_equals_separate_chain(tmp_path):
+    """2 ranks on the xGMI exchange: the lagged chain (each exchanged gradient's clip + Adam
+    inside the next forward) ends with the parameters and losses of the chain with a separate
+    clip + Adam launch, bit for bit, on every rank."""
+    from _dist_workers import xgmi_ppo_worker
+    world = 2
+    runs = {}
+    for lag in ("1", "0"):
+        d = tmp_path / f"lag{lag}"
+        d.mkdir()
+        _run(xgmi_ppo_worker, world, d, True, lag, timeout=400)
+        runs[lag] = [(np.load(d / f"p{r}.npy"), np.load(d / f"l{r}.npy")) for r in range(world)]
+    for r in range(world):
+        (p1, l1), (p0, l0) = runs["1"][r], runs["0"][r]
+        assert np.array_equal(p1.view(np.uint32), p0.view(np.uint32)), f"rank {r}: params differ"
+        assert np.array_equal(l1.view(np.uint32), l0.view(np.uint32)), f"rank {r}: losses differ"
