@@ -551,6 +551,7 @@ __global__ void k_cnn_loss_final(const double *__restrict__ part, int nb, int B,
         for (int k = 0; k < GS_NUM_METRICS; ++k) metrics[k] = 0.0f;
         metrics[GS_M_SKIPPED] = 1.0f;
         metrics[GS_M_KL_STOP] = 1.0f;
+        metrics[GS_M_UNEVALUATED] = 1.0f;
         return;
     }
     double acc[kSums];
@@ -586,7 +587,7 @@ __global__ void k_cnn_loss_final(const double *__restrict__ part, int nb, int B,
         metrics[GS_M_KL_STOP] = kl_stop ? 1.0f : 0.0f;
         metrics[GS_M_GRAD_NORM] = 0.0f;
         metrics[GS_M_SKIPPED] = kl_stop ? 1.0f : 0.0f;
-        metrics[GS_M_RES0] = 0.0f;
+        metrics[GS_M_UNEVALUATED] = 0.0f;
         metrics[GS_M_RES1] = 0.0f;
         if (kl_stop && stop) *stop = 1;
     }

@@ -72,7 +72,48 @@ __global__ __launch_bounds__(256) void k_env_step(int32_t *__restrict__ state, f
     for (int d = 0; d < D; ++d) obs[e * D + d] = synth_obs(seed, ge, step_count, (uint64_t)d);
 }
 
+// Completed-episode records of a rollout (the RecordEpisodeStatistics "episode" {r, l} the
+// reference reads per done env, utils/rollout_collector.py:223-240): one thread per env walks
+// its column t = 0..T-1 (coalesced row reads), carrying the running return / length across
+// rollouts in run_ret / run_len.  ep_ret / ep_len rows are written where done (elsewhere 0).
+__global__ __launch_bounds__(256) void k_episode_stats(const float *__restrict__ rewards,
+                                                       const uint8_t *__restrict__ dones, int64_t T, int64_t N,
+                                                       float *__restrict__ run_ret, int32_t *__restrict__ run_len,
+                                                       float *__restrict__ ep_ret, int32_t *__restrict__ ep_len)
+{
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= N) return;
+    float r = run_ret[e];
+    int32_t l = run_len[e];
+    for (int64_t t = 0; t < T; ++t) {
+        const int64_t o = t * N + e;
+        r += rewards[o];
+        l += 1;
+        const bool d = dones[o] != 0;
+        ep_ret[o] = d ? r : 0.0f;
+        ep_len[o] = d ? l : 0;
+        if (d) {
+            r = 0.0f;
+            l = 0;
+        }
+    }
+    run_ret[e] = r;
+    run_len[e] = l;
+}
+
 }  // namespace
+
+extern "C" int gs_episode_stats(const float *rewards, const uint8_t *dones, int64_t T, int64_t N, float *run_ret,
+                                int32_t *run_len, float *ep_ret, int32_t *ep_len, void *stream)
+{
+    GS_REQUIRE(T >= 0 && N >= 0, "gs_episode_stats: bad shape");
+    GS_REQUIRE(rewards && dones && run_ret && run_len && ep_ret && ep_len, "gs_episode_stats: null buffer");
+    if (T == 0 || N == 0) return GS_OK;
+    hipLaunchKernelGGL(k_episode_stats, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       rewards, dones, T, N, run_ret, run_len, ep_ret, ep_len);
+    GS_LAUNCH_CHECK("k_episode_stats");
+    return GS_OK;
+}
 
 extern "C" int gs_env_reset(int32_t *state, float *ep_ret, float *obs, int64_t N, int32_t obs_dim, int32_t episode_len,
                             uint64_t seed, int64_t env_offset, void *stream)

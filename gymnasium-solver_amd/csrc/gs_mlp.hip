@@ -875,7 +875,7 @@ __device__ __forceinline__ void write_metrics(const double *t, double Bd, const 
     }
     metrics[GS_M_KL_STOP] = kl_stop ? 1.0f : 0.0f;
     metrics[GS_M_SKIPPED] = kl_stop ? 1.0f : 0.0f;
-    metrics[GS_M_RES0] = 0.0f;
+    metrics[GS_M_UNEVALUATED] = 0.0f;
     metrics[GS_M_RES1] = 0.0f;
 }
 
@@ -904,6 +904,7 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
             for (int k = 0; k < GS_NUM_METRICS; ++k) metrics[k] = 0.0f;
             metrics[GS_M_SKIPPED] = 1.0f;
             metrics[GS_M_KL_STOP] = 1.0f;
+            metrics[GS_M_UNEVALUATED] = 1.0f;
         }
         return;
     }

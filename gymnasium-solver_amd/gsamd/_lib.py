@@ -20,7 +20,7 @@ GS_NUM_METRICS = 16
 METRIC_SLOTS = (
     "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
     "explained_var", "kl", "approx_kl", "adv_norm_mean", "adv_norm_std", "kl_stop", "grad_norm",
-    "skipped", "res0", "res1",
+    "skipped", "unevaluated", "res1",
 )
 M = {name: i for i, name in enumerate(METRIC_SLOTS)}
 
@@ -76,6 +76,7 @@ def _load():
         "gs_env_reset": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, u64, i64, vp]),
         "gs_env_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, f32, u64, i64, u64, vp, vp, vp, vp, vp,
                                        vp, vp]),
+        "gs_episode_stats": (ctypes.c_int, [vp, vp, i64, i64, vp, vp, vp, vp, vp]),
         "gs_ppo_workspace_bytes": (sz, [MlpDims, i64]),
         "gs_ppo_minibatch_step": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64,
                                                  vp, vp, vp, vp, vp]),
@@ -120,6 +121,7 @@ def _load():
 lib = _load()
 EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_env_reset", "gs_env_step",
+            "gs_episode_stats",
             "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_ppo_update_workspace_bytes",
             "gs_ppo_graph_cache_info",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",

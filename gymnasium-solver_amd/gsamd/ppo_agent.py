@@ -22,13 +22,14 @@ from typing import Any, Dict, Optional
 import numpy as np
 import torch
 
-from ._lib import GS_NUM_METRICS, M, PPOHparams, check, lib, ptr, stream_handle
+from ._lib import GS_NUM_METRICS, M, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
 from .atari_env import DeviceAtariVecEnv
 from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
 from .distributed import allreduce_sum_f64, world_active
+from .metrics import MetricsRecorder, ppo_keys, ppo_records
 from .schedules import SCHEDULABLE, build_schedulers
 
 STAGES = ("train",)
@@ -68,6 +69,8 @@ class DevicePPOAgent:
         self._envs: Dict[str, Any] = {}
         self._rollout_collectors: Dict[str, DeviceRolloutCollector] = {}
         self.metrics_history = []
+        self.metrics_recorder = MetricsRecorder()    # base_agent.py:85
+        self._staged = None                          # a tensor batch's T=1 rollout view (losses_for_batch)
         # optional per-epoch (start, update-start, end) events on the launch stream (bench.py)
         self.phase_events = None
         self.build_env("train", env)
@@ -129,7 +132,7 @@ class DevicePPOAgent:
             self._envs[stage] = env
             self._rollout_collectors[stage] = DeviceRolloutCollector(
                 env, self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
-                rng_seed=c.seed + 1000 + 7919 * self.rank, track_stats=False)
+                rng_seed=c.seed + 1000 + 7919 * self.rank, track_stats=True)
         return self._rollout_collectors[stage]
 
     # ---- checkpoints (agents/base_agent.py:658-885) -----------------------------------------
@@ -284,40 +287,90 @@ class DevicePPOAgent:
         if self.current_epoch > 0:
             self._trajectories = self.get_rollout_collector("train").collect()
 
-    def losses_for_batch(self, batch: MinibatchIndices, batch_idx: int):
-        """PPOAgent.losses_for_batch: loss + metrics of one minibatch (no optimizer step)."""
-        buf = self.get_rollout_collector("train").buffer
+    def _stage_batch(self, batch):
+        """A tensor batch (RolloutTrajectory or any object with observations / actions /
+        logprobs / values / advantages / returns, rollout_buffer.py:16-25; the reference's tests
+        pass SimpleNamespace) -> device copies laid out as a one-step rollout of B envs, so the
+        env-major indices 0..B-1 select the rows in order.  Returns (view, idx, B)."""
+        obs = torch.as_tensor(batch.observations)
+        B = int(obs.shape[0])
+        pix = self.is_pixel
+        st = self._staged
+        if st is None or st["B"] != B:
+            dev = self.device
+            st = {"B": B, "idx": torch.arange(B, dtype=torch.int32, device=dev),
+                  "obs": torch.empty((1, *obs.shape), dtype=torch.uint8 if pix else torch.float32, device=dev),
+                  "act": torch.empty(1, B, dtype=torch.int64, device=dev),
+                  **{k: torch.empty(1, B, dtype=torch.float32, device=dev) for k in ("lp", "v", "adv", "ret")}}
+            ws_need = int(lib.gs_cnn_workspace_bytes(self.policy_model.dims, B) if pix else
+                          lib.gs_ppo_workspace_bytes(self.policy_model.dims, B))
+            st["ws"] = self.workspace if ws_need <= self.workspace.numel() else \
+                torch.zeros(ws_need, dtype=torch.uint8, device=dev)
+            self._staged = st
+        st["obs"][0].copy_(obs.to(st["obs"].dtype).reshape(st["obs"].shape[1:]))
+        st["act"][0].copy_(torch.as_tensor(batch.actions).reshape(B).to(torch.int64))
+        for k, f in (("lp", "logprobs"), ("v", "values"), ("adv", "advantages"), ("ret", "returns")):
+            st[k][0].copy_(torch.as_tensor(getattr(batch, f)).reshape(B).to(torch.float32))
+        V = RolloutViewU8 if pix else RolloutView
+        view = V(ptr(st["obs"]), ptr(st["act"]), ptr(st["lp"]), ptr(st["v"]), ptr(st["adv"]), ptr(st["ret"]), 1, B)
+        return view, st["idx"], B, st["ws"]
+
+    def _batch_view(self, batch):
+        if isinstance(batch, MinibatchIndices):
+            return self.get_rollout_collector("train").buffer.view(), batch.idx, len(batch), self.workspace
+        return self._stage_batch(batch)
+
+    def _record_step(self, rec: torch.Tensor) -> np.ndarray:
+        """metrics_recorder.record("train", ...) with losses_for_batch's keys (ppo_agent.py:131-146)."""
+        row = rec.detach().cpu().numpy().reshape(1, GS_NUM_METRICS)
+        norm = self.config.normalize_advantages == "batch"
+        vals = ppo_records(row, float(self.vf_coef), float(self.ent_coef), norm)[0]
+        self.metrics_recorder.record("train", dict(zip(ppo_keys(norm), vals)))
+        return row[0]
+
+    def losses_for_batch(self, batch, batch_idx: int):
+        """PPOAgent.losses_for_batch (agents/ppo/ppo_agent.py:21-152): forward + loss + metrics of
+        one minibatch, no optimizer step.  `batch` is the reference's tensor batch or this
+        agent's MinibatchIndices.  Returns {loss: 0-d device tensor, early_stop_epoch: bool} and
+        records the metrics under "train"."""
+        view, idx, B, ws = self._batch_view(batch)
         if self.is_pixel:
-            check(lib.gs_cnn_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(),
-                                      buf.view(), ptr(batch.idx), len(batch), ptr(self._step_metrics), None,
-                                      ptr(self.workspace), stream_handle()), "gs_cnn_ppo_loss")
+            check(lib.gs_cnn_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(), view,
+                                      ptr(idx), B, ptr(self._step_metrics), None, ptr(ws), stream_handle()),
+                  "gs_cnn_ppo_loss")
         else:
-            check(lib.gs_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(), buf.view(),
-                                  ptr(batch.idx), len(batch), ptr(self._step_metrics), ptr(self.workspace),
-                                  stream_handle()), "gs_ppo_loss")
-        early = False
-        if self.config.target_kl is not None:
-            early = float(self._step_metrics[M["approx_kl"]].item()) > float(self.config.target_kl)
+            check(lib.gs_ppo_loss(ptr(self.policy_model.params), self.policy_model.dims, self.hparams(), view,
+                                  ptr(idx), B, ptr(self._step_metrics), ptr(ws), stream_handle()), "gs_ppo_loss")
+        row = self._record_step(self._step_metrics)
+        early = self.config.target_kl is not None and bool(row[M["kl_stop"]])
         return dict(loss=self._step_metrics[M["loss"]].clone(), early_stop_epoch=early)
 
-    def training_step(self, batch: MinibatchIndices, batch_idx: int):
-        """Forward, loss, backward, clip_grad_norm_(max_grad_norm), Adam.step — fused."""
+    def training_step(self, batch, batch_idx: int):
+        """BaseAgent.training_step (base_agent.py:330-366) fused: forward, loss, backward,
+        clip_grad_norm_(max_grad_norm), Adam.step.  The KL early stop is sticky as in the
+        reference: the minibatch that trips it takes no step, nor does any later one."""
         if self._early_stop_epoch:
             return None
-        buf = self.get_rollout_collector("train").buffer
+        view, idx, B, ws = self._batch_view(batch)
         self.adam_step += 1
         rec = self.metrics_buf[batch_idx % self.n_minibatches]
         if self.is_pixel:
             check(lib.gs_cnn_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
-                                        ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(),
-                                        ptr(batch.idx), len(batch), 1, self.adam_step - 1, ptr(rec),
-                                        ptr(self.stop_flag), ptr(self.workspace), self.comm, stream_handle()),
+                                        ptr(self.adam_v), self.policy_model.dims, self.hparams(), view,
+                                        ptr(idx), B, 1, self.adam_step - 1, ptr(rec),
+                                        ptr(self.stop_flag), ptr(ws), self.comm, stream_handle()),
                   "gs_cnn_ppo_update")
-            return None
-        check(lib.gs_ppo_minibatch_step(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
-                                        ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(),
-                                        ptr(batch.idx), len(batch), self.adam_step, ptr(rec), ptr(self.stop_flag),
-                                        ptr(self.workspace), self.comm, stream_handle()), "gs_ppo_minibatch_step")
+        else:
+            check(lib.gs_ppo_minibatch_step(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                            ptr(self.adam_v), self.policy_model.dims, self.hparams(), view,
+                                            ptr(idx), B, self.adam_step, ptr(rec), ptr(self.stop_flag),
+                                            ptr(ws), self.comm, stream_handle()), "gs_ppo_minibatch_step")
+        row = self._record_step(rec)
+        if self.config.target_kl is not None and row[M["kl_stop"]]:
+            self._early_stop_epoch = True
+            self.adam_step -= 1              # the tripping minibatch took no optimizer step
+        else:
+            self.metrics_recorder.record("train", {"opt/grads/norm/all": float(row[M["grad_norm"]])})
         return None
 
     # ---- fused epoch (the trainer's path) -------------------------------------------------------
@@ -352,7 +405,10 @@ class DevicePPOAgent:
                                     1 if self.use_graph else 0, stream_handle()), "gs_ppo_update")
         if ev is not None:
             ev[-1][2].record()
-        self.adam_step += self.n_minibatches
+        if self.config.target_kl is None:
+            self.adam_step += self.n_minibatches
+        else:       # minibatches from the sticky KL stop on took no optimizer step
+            self.adam_step += int((self.metrics_buf[:, M["skipped"]] == 0).sum().item())
         self.current_epoch += 1
         self.on_train_epoch_end()
 
@@ -371,29 +427,32 @@ class DevicePPOAgent:
         for s in self.schedulers:
             self.set_hyperparameter(s.parameter, s.value(total))
 
-    def epoch_metrics(self) -> Dict[str, float]:
-        """Reference metric keys (ppo_agent.py:131-146, torch.py:170-173), epoch means."""
+    def record_epoch_metrics(self) -> np.ndarray:
+        """Book the last update's per-minibatch records into metrics_recorder["train"] with
+        losses_for_batch's keys — only the minibatches whose loss was evaluated, as the
+        reference records them (the one that trips the KL stop included) — plus
+        opt/grads/norm/all of the minibatches that stepped (base_agent.py:607-608).  One D2H."""
         rec = self.metrics_buf.cpu().numpy()
-        live = rec[rec[:, M["skipped"]] == 0]
-        if len(live) == 0:
-            live = rec[:1] * 0
-        mean = live.mean(axis=0)
-        vf, ent = float(self.vf_coef), float(self.ent_coef)
-        out = {
-            "opt/loss/total": mean[M["loss"]], "opt/loss/policy": mean[M["policy_loss"]],
-            "opt/loss/entropy": -mean[M["entropy"]], "opt/policy/entropy": mean[M["entropy"]],
-            "opt/loss/entropy_scaled": -ent * mean[M["entropy"]], "opt/loss/value": mean[M["value_loss"]],
-            "opt/loss/value_scaled": vf * mean[M["value_loss"]], "opt/ppo/clip_fraction": mean[M["clip_fraction"]],
-            "opt/ppo/clip_fraction_vf": mean[M["clip_fraction_vf"]],
-            "opt/value/explained_var": mean[M["explained_var"]], "opt/ppo/kl": mean[M["kl"]],
-            "opt/ppo/approx_kl": mean[M["approx_kl"]], "opt/ppo/kl_stop_triggered": mean[M["kl_stop"]],
-            "opt/grads/norm/all": mean[M["grad_norm"]],
-        }
-        if self.config.normalize_advantages == "batch":
-            out["roll/adv/norm/mean"] = mean[M["adv_norm_mean"]]
-            out["roll/adv/norm/std"] = mean[M["adv_norm_std"]]
-        if world_active():     # every rank ran the same number of minibatches: job mean = mean of means
-            keys = list(out)
+        norm = self.config.normalize_advantages == "batch"
+        live = rec[rec[:, M["unevaluated"]] == 0]
+        self.metrics_recorder.record_rows("train", ppo_keys(norm),
+                                          ppo_records(live, float(self.vf_coef), float(self.ent_coef), norm))
+        stepped = rec[rec[:, M["skipped"]] == 0]
+        self.metrics_recorder.record_rows("train", ("opt/grads/norm/all",), stepped[:, M["grad_norm"]])
+        if self.config.target_kl is not None and (rec[:, M["kl_stop"]] != 0).any():
+            self._early_stop_epoch = True        # sticky, as BaseAgent._early_stop_epoch
+        return rec
+
+    def epoch_metrics(self) -> Dict[str, float]:
+        """The last update's epoch means under the reference's metric keys (ppo_agent.py:131-146,
+        torch.py:170-173, base_agent.py:607-608); the recorder's "train" namespace is reset
+        first, so this is exactly one update.  In a multi-rank job the means are averaged over
+        ranks (every rank evaluates the same number of minibatches)."""
+        self.metrics_recorder.reset_epoch("train")
+        self.record_epoch_metrics()
+        out = self.metrics_recorder.compute_epoch_means("train")
+        if world_active():
+            keys = sorted(out)
             vals = allreduce_sum_f64([out[k] for k in keys]) / float(self.world_size)
             out = dict(zip(keys, vals))
         return {k: float(v) for k, v in out.items()}
@@ -413,7 +472,9 @@ class DevicePPOAgent:
             self.train_epoch()
             epochs += 1
             if log is not None:
-                log({**self.get_rollout_collector("train").get_metrics(), **self.epoch_metrics()})
+                m = self.get_rollout_collector("train").get_metrics()
+                m.pop("action_dist", None)
+                log({**m, **self.epoch_metrics()})
 
     # ---- misc -----------------------------------------------------------------------------------
     def make_sampler(self) -> MultiPassRandomSampler:

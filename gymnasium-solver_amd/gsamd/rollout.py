@@ -224,13 +224,19 @@ class DeviceRolloutCollector:
         self.track_stats = bool(track_stats)
         self.total_rollouts = self.total_steps = self.total_vec_steps = self.total_episodes = 0
         self.rollout_steps = self.rollout_vec_steps = self.rollout_episodes = 0
+        self.stats_window_size = int(stats_window_size)
         self.rollout_fpss = RollingWindow(stats_window_size)
+        # finished-episode statistics in the reference's processing order (step, then env):
+        # rolling windows, best / last episode (utils/rollout_collector.py:93-98, 210-294)
+        self.episode_reward_deque = RollingWindow(stats_window_size)
+        self.episode_length_deque = RollingWindow(stats_window_size)
         self._best_episode_reward = -float("inf")
         self._last_episode_reward, self._last_episode_length = 0.0, 0
+        self._recent_episodes = []       # (env, return, length, timeout) since the last consumer
         self._buffer: Optional[DeviceRolloutBuffer] = None
         self._started = False
         self._stats = None
-        self._ep_seen = None
+        self._action_counts = None       # device int64 histogram of taken actions
 
     # ---- phases --------------------------------------------------------------------
     def _prepare(self):
@@ -247,7 +253,25 @@ class DeviceRolloutCollector:
             obs_shape = tuple(obs.shape[1:])
         self._buffer = DeviceRolloutBuffer(self.n_envs, obs_shape, self.n_steps, self.device, obs_dtype)
         self._obs_dev = torch.zeros(self.n_envs, *obs_shape, dtype=obs_dtype, device=self.device)
+        # running episode return / length per env (carried across rollouts) and this rollout's
+        # completed-episode rows (gs_episode_stats)
+        z = dict(device=self.device)
+        self._run_ret = torch.zeros(self.n_envs, dtype=torch.float32, **z)
+        self._run_len = torch.zeros(self.n_envs, dtype=torch.int32, **z)
+        self._ep_ret_rows = torch.zeros(self.n_steps, self.n_envs, dtype=torch.float32, **z)
+        self._ep_len_rows = torch.zeros(self.n_steps, self.n_envs, dtype=torch.int32, **z)
         self._started = True
+
+    def _reset_env(self):
+        """Fresh episodes on every env (evaluate_episodes; the reference sets obs = None)."""
+        self._prepare()
+        if getattr(self.env, "device_native", False):
+            self.env.reset()
+        else:
+            obs, _ = self.env.reset()
+            self._host_obs = np.asarray(obs, dtype=self._host_obs.dtype)
+        self._run_ret.zero_()
+        self._run_len.zero_()
 
     @property
     def buffer(self) -> DeviceRolloutBuffer:
@@ -264,6 +288,7 @@ class DeviceRolloutCollector:
         t0 = time.time()
         mode = 2 if replay_actions is not None else (1 if deterministic else 0)
         native = getattr(self.env, "device_native", False)
+        self.rollout_episodes = 0
         for t in range(T):
             if replay_actions is not None:
                 buf.actions[t].copy_(replay_actions[t])
@@ -282,7 +307,7 @@ class DeviceRolloutCollector:
                 buf.rewards[t].copy_(torch.from_numpy(np.asarray(rew, np.float32)))
                 buf.dones[t].copy_(torch.from_numpy(done.astype(np.uint8)))
                 buf.timeouts[t].copy_(torch.from_numpy(np.asarray(trunc).astype(np.uint8)))
-                self._host_episode_infos(done, infos)
+                self._host_episode_infos(done, np.asarray(trunc, bool), infos)
                 self._host_obs = np.asarray(next_obs, dtype=self._host_obs.dtype)
         last_obs = self.env.obs if native else self._obs_dev.copy_(torch.from_numpy(self._host_obs))
         pm.predict_values(last_obs, out=buf.last_values)
@@ -295,16 +320,45 @@ class DeviceRolloutCollector:
         self.total_rollouts += 1
         if self.track_stats:
             self._accumulate_stats()
+            if native:
+                self._episode_records()
+        if not native:
+            self.total_episodes += self.rollout_episodes
         self.rollout_fpss.append(N * T / max(time.time() - t0, 1e-9))
         return DeviceTrajectory(buf)
 
-    def _host_episode_infos(self, done, infos):
+    def _record_episode(self, env: int, ret: float, length: int, timeout: bool) -> None:
+        """One finished episode, as _process_done_infos books it (rollout_collector.py:242-294)."""
+        self.episode_reward_deque.append(ret)
+        self.episode_length_deque.append(length)
+        self._last_episode_reward, self._last_episode_length = ret, length
+        self._best_episode_reward = max(self._best_episode_reward, ret)
+        self._recent_episodes.append((env, ret, length, timeout))
+
+    def _episode_records(self):
+        """This rollout's finished episodes in the reference's order (step, then env), one D2H
+        of their (return, length, timeout) records."""
+        buf, N, T = self._buffer, self.n_envs, self.n_steps
+        check(lib.gs_episode_stats(ptr(buf.rewards), ptr(buf.dones), T, N, ptr(self._run_ret), ptr(self._run_len),
+                                   ptr(self._ep_ret_rows), ptr(self._ep_len_rows), stream_handle()),
+              "gs_episode_stats")
+        at = torch.nonzero(buf.dones.reshape(-1)).squeeze(1)        # time-major = (step, env) order
+        rec = torch.stack([at.double(), self._ep_ret_rows.reshape(-1)[at].double(),
+                           self._ep_len_rows.reshape(-1)[at].double(),
+                           buf.timeouts.reshape(-1)[at].double()]).cpu().numpy()
+        for pos, r, length, to in rec.T:
+            self._record_episode(int(pos) % N, float(np.float32(r)), int(length), bool(to))
+        self.rollout_episodes = rec.shape[1]
+        self.total_episodes += self.rollout_episodes
+
+    def _host_episode_infos(self, done, trunc, infos):
+        """A host env's RecordEpisodeStatistics infos (rollout_collector.py:210-294)."""
         ep, mask = infos.get("episode"), infos.get("_episode")
         for e in np.nonzero(done)[0]:
-            r = float(ep["r"][e]) if ep is not None and mask is not None and mask[e] else 0.0
-            self._best_episode_reward = max(self._best_episode_reward, r)
-            self._last_episode_reward = r
-            self.total_episodes += 1
+            ok = ep is not None and mask is not None and mask[e]
+            self._record_episode(int(e), float(ep["r"][e]) if ok else 0.0, int(ep["l"][e]) if ok else 0,
+                                 bool(trunc[e]))
+        self.rollout_episodes += int(np.count_nonzero(done))
 
     def _accumulate_stats(self):
         """Device-side RunningStats sums (utils/rollout_stats.py:34-67) for get_metrics."""
@@ -328,53 +382,51 @@ class DeviceRolloutCollector:
         s[7] += buf.returns.sum(dtype=torch.float64)
         s[8] += (buf.returns.double() ** 2).sum()
         s[9] += buf.rewards.numel()
+        # action histogram (rollout_collector.py:189-199), on device
+        n_act = int(getattr(self.policy_model, "n_actions", 0)) or int(buf.actions.max().item()) + 1
+        h = torch.bincount(buf.actions.reshape(-1), minlength=n_act)
+        if self._action_counts is None or self._action_counts.numel() < h.numel():
+            grown = torch.zeros(h.numel(), dtype=torch.int64, device=self.device)
+            if self._action_counts is not None:
+                grown[:self._action_counts.numel()] += self._action_counts
+            self._action_counts = grown
+        self._action_counts[:h.numel()] += h
 
     # ---- evaluation (utils/rollout_collector.py:570-655) -----------------------------
     def evaluate_episodes(self, *, n_episodes: int, deterministic: bool = True,
                           timeout_seconds: Optional[float] = None) -> dict:
-        """Run the policy (argmax when deterministic) on this collector's device env from a
-        fresh reset until every env finished its balanced share of n_episodes; episode return
-        and length come from the env's completed-episode counters (one small D2H per vector
-        step: evaluation is off the training hot path)."""
-        env = self.env
-        if not getattr(env, "device_native", False):
-            raise ValueError("evaluate_episodes needs a device env")
+        """The reference's protocol on this collector's env: fresh episodes on every env, whole
+        rollouts (deterministic: argmax actions) until every env finished its balanced share of
+        n_episodes; means over those episodes only, env steps counted per rollout."""
         N = self.n_envs
         base, rem = divmod(int(n_episodes), N)
-        targets = np.array([base + (1 if i < rem else 0) for i in range(N)], np.int64)
-        counts = np.zeros(N, np.int64)
-        rew_sum = len_sum = 0.0
-        env.reset()
-        dev = self.device
-        rew = torch.empty(N, dtype=torch.float32, device=dev)
-        done = torch.empty(N, dtype=torch.uint8, device=dev)
-        tout = torch.empty(N, dtype=torch.uint8, device=dev)
-        act = torch.empty(N, dtype=torch.int64, device=dev)
-        logp = torch.empty(N, dtype=torch.float32, device=dev)
-        val = torch.empty(N, dtype=torch.float32, device=dev)
-        prev_ret = env.ep_ret_sum.double().cpu().numpy()
-        prev_len = env.ep_len_sum.double().cpu().numpy()
-        steps = 0
+        targets = [base + (1 if i < rem else 0) for i in range(N)]
+        counts = [0] * N
+        rew_sum, len_sum, steps, vec_steps = 0.0, 0, 0, 0
+        self._reset_env()
+        self._recent_episodes = []
+        was_tracking, self.track_stats = self.track_stats, True    # episode records are needed
         t0 = time.time()
-        while (counts < targets).any():
-            self.policy_model.act(env.obs, mode=1 if deterministic else 0, rng_seed=self.rng_seed + 1,
-                                  rng_counter=steps, actions=act, logp=logp, values=val)
-            env.step_into(rew, done, tout, actions=act)
-            steps += 1
-            d = done.cpu().numpy().astype(bool)
-            if d.any():
-                r_now = env.ep_ret_sum.double().cpu().numpy()
-                l_now = env.ep_len_sum.double().cpu().numpy()
-                for e in np.nonzero(d)[0]:
-                    if counts[e] < targets[e]:
-                        rew_sum += r_now[e] - prev_ret[e]
-                        len_sum += l_now[e] - prev_len[e]
-                        counts[e] += 1
-                prev_ret, prev_len = r_now, l_now
-            if timeout_seconds is not None and time.time() - t0 >= float(timeout_seconds):
-                break
-        total = int(counts.sum())
-        m = {"cnt/total_episodes": total, "cnt/total_env_steps": int(steps * N), "cnt/total_vec_steps": int(steps)}
+        try:
+            while any(c < t for c, t in zip(counts, targets)):
+                self.collect(deterministic=deterministic)
+                steps += N * self.n_steps
+                vec_steps += self.rollout_vec_steps
+                recent, self._recent_episodes = self._recent_episodes, []
+                for env, r, length, _ in recent:
+                    if counts[env] >= targets[env]:
+                        continue
+                    rew_sum += float(r)
+                    len_sum += int(length)
+                    counts[env] += 1
+                if timeout_seconds is not None and time.time() - t0 >= float(timeout_seconds):
+                    break
+        finally:
+            self.track_stats = was_tracking
+        total = int(sum(counts))
+        m = self.get_metrics()
+        m.pop("action_dist", None)
+        m.update({"cnt/total_episodes": total, "cnt/total_env_steps": int(steps), "cnt/total_vec_steps": int(vec_steps)})
         if total > 0:
             m["roll/ep_rew/mean"] = float(rew_sum / total)
             m["roll/ep_len/mean"] = float(len_sum / total)
@@ -388,39 +440,72 @@ class DeviceRolloutCollector:
         return SimpleNamespace(**{f: getattr(trajectories, f)[idx] for f in DeviceTrajectory._FIELDS[:-1]})
 
     def get_metrics(self):
-        """Key-compatible subset of utils/rollout_collector.py:686-760 (one D2H)."""
-        m = {"cnt/total_env_steps": self.total_steps, "cnt/total_vec_steps": self.total_vec_steps,
-             "cnt/total_rollouts": self.total_rollouts, "roll/env_steps": self.rollout_steps,
-             "roll/vec_steps": self.rollout_vec_steps,
-             "roll/fps": float(self.rollout_fpss.mean()) if self.rollout_fpss else 0.0}
-        # additive partial sums of every rank are summed before the means (one all-reduce of a
-        # small float64 vector per call in a multi-rank job): job-wide statistics
-        part = [self.rollout_steps]
+        """utils/rollout_collector.py:686-760: counters, running obs / reward / return /
+        advantage statistics, the action histogram and its moments, baseline statistics (PPO's
+        GAE targets never update them: zeros), and — once an episode has finished — the rolling
+        window means, best and last episode.  In a multi-rank job the additive sums (steps,
+        episodes, statistics, action counts) are summed over ranks before the means; the rolling
+        window and best/last episode are this rank's."""
+        part = [self.rollout_steps, self.total_episodes, self.rollout_episodes]
+        n_stats = 0
         if self._stats is not None:
-            part += list(self._stats.cpu().numpy().astype(np.float64))
+            st = list(self._stats.cpu().numpy().astype(np.float64))
+            n_stats = len(st)
+            part += st
+        counts = self._action_counts.cpu().numpy() if self._action_counts is not None else np.zeros(0, np.int64)
+        part += list(counts.astype(np.float64))
         env = self.env
         native = getattr(env, "device_native", False)
-        if native:
+        dev_eps = native and not self.track_stats      # episode sums from the env's device counters
+        if dev_eps:
             part += [float(env.ep_count.sum().item()), float(env.ep_ret_sum.sum().item()),
                      float(env.ep_len_sum.sum().item())]
         part = allreduce_sum_f64(part)
-        m["roll/env_steps"] = int(part[0])
-        m["cnt/total_env_steps"] = int(self.total_steps * (part[0] / max(self.rollout_steps, 1)))
-        if self._stats is not None:
-            s = part[1:11]
+        scale = part[0] / max(self.rollout_steps, 1)
+        m = {"cnt/total_env_steps": int(round(self.total_steps * scale)), "cnt/total_vec_steps": self.total_vec_steps,
+             "cnt/total_episodes": int(part[1]), "cnt/total_rollouts": self.total_rollouts,
+             "roll/env_steps": int(part[0]), "roll/vec_steps": self.rollout_vec_steps,
+             "roll/episodes": int(part[2]), "roll/fps": float(self.rollout_fpss.mean()) if self.rollout_fpss else 0.0}
 
-            def ms(sum_, sq, n):
-                mean = sum_ / max(n, 1)
-                return float(mean), float(np.sqrt(max(0.0, sq / max(n, 1) - mean * mean)))
-            m["roll/obs/mean"], m["roll/obs/std"] = ms(s[1], s[2], s[0])
-            m["roll/reward/mean"], m["roll/reward/std"] = ms(s[3], s[4], s[9])
-            m["roll/adv/mean"], m["roll/adv/std"] = ms(s[5], s[6], s[9])
-            m["roll/return/mean"], m["roll/return/std"] = ms(s[7], s[8], s[9])
-        if native:
+        def mean_std(sum_, sq, n):      # RunningStats.mean / .std (rollout_stats.py:59-67)
+            if n <= 0:
+                return 0.0, 0.0
+            mean = sum_ / n
+            return float(mean), float(np.sqrt(max(0.0, sq / n - mean * mean)))
+        zero = (0.0, 0.0)
+        if n_stats:
+            s = part[3:3 + n_stats]
+            obs, rew, adv, ret = (mean_std(s[1], s[2], s[0]), mean_std(s[3], s[4], s[9]), mean_std(s[5], s[6], s[9]),
+                                  mean_std(s[7], s[8], s[9]))
+        else:
+            obs = rew = adv = ret = zero
+        m["roll/obs/mean"], m["roll/obs/std"] = obs
+        m["roll/reward/mean"], m["roll/reward/std"] = rew
+        m["roll/return/mean"], m["roll/return/std"] = ret
+        m["roll/adv/mean"], m["roll/adv/std"] = adv
+        hist = np.asarray(part[3 + n_stats:3 + n_stats + counts.size], np.int64)
+        nz = np.flatnonzero(hist)
+        if nz.size:     # the reference's histogram grows to the largest action seen
+            hist = hist[:nz[-1] + 1]
+            idxs = np.arange(hist.shape[0], dtype=np.float32)
+            total = float(hist.sum())
+            a_mean = float((idxs * hist).sum() / total)
+            a_var = float(((idxs - a_mean) ** 2 * hist).sum() / total)
+            m["roll/actions/mean"], m["roll/actions/std"] = a_mean, float(np.sqrt(max(0.0, a_var)))
+            m["action_dist"] = hist
+        else:
+            m["roll/actions/mean"], m["roll/actions/std"], m["action_dist"] = 0.0, 0.0, None
+        m["roll/baseline/mean"], m["roll/baseline/std"] = zero
+        if dev_eps:
             cnt, ret_sum, len_sum = part[-3:]
-            if cnt > 0:
-                self.total_episodes = int(cnt)
+            m["cnt/total_episodes"] = int(cnt)
+            if cnt > 0:     # cumulative means (track_stats=False keeps no per-episode records)
                 m["roll/ep_rew/mean"] = float(ret_sum / cnt)
                 m["roll/ep_len/mean"] = int(len_sum / cnt)
-        m["cnt/total_episodes"] = self.total_episodes
+        elif self.episode_reward_deque:
+            m["roll/ep_rew/mean"] = float(self.episode_reward_deque.mean())
+            m["roll/ep_len/mean"] = int(self.episode_length_deque.mean())
+            m["roll/ep_rew/best"] = float(self._best_episode_reward)
+            m["roll/ep_rew/last"] = float(self._last_episode_reward)
+            m["roll/ep_len/last"] = int(self._last_episode_length)
         return m

@@ -109,6 +109,14 @@ int gs_env_step(int32_t *state_dev, float *ep_ret_dev, float *obs_dev, int64_t N
                 uint8_t *timeouts_row_dev, int32_t *ep_done_count_dev, float *ep_ret_sum_dev,
                 float *ep_len_sum_dev, void *stream);
 
+/* Completed-episode records of a (T, N) rollout, for the collector's episode statistics
+ * (utils/rollout_collector.py:210-294 _process_done_infos, :686-760 get_metrics): per env the
+ * running return (f32, the rewards summed in step order) and length carry across rollouts in
+ * run_ret_dev / run_len_dev (N each, zero after a reset); ep_ret_dev / ep_len_dev (T, N) receive
+ * the finished episode's return and length where dones_dev is set, 0 elsewhere. */
+int gs_episode_stats(const float *rewards_dev, const uint8_t *dones_dev, int64_t T, int64_t N, float *run_ret_dev,
+                     int32_t *run_len_dev, float *ep_ret_dev, int32_t *ep_len_dev, void *stream);
+
 /* ---------------------------------------------------------------- PPO update
  * Replaces the minibatch loop: DataLoader(MultiPassRandomSampler) + collate
  * (utils/dataloaders.py:20-77, rollout_collector.py:657-682) + PPOAgent.losses_for_batch
@@ -130,12 +138,15 @@ typedef struct gs_ppo_hparams {
     int32_t pad;
 } gs_ppo_hparams;
 
-/* Per-minibatch metric record written by the loss kernel (floats, GS_NUM_METRICS each). */
+/* Per-minibatch metric record written by the loss kernel (floats, GS_NUM_METRICS each).
+ * KL early stop (agents/base_agent.py:330-366, sticky): the minibatch whose approx_kl exceeds
+ * target_kl keeps its loss metrics with KL_STOP = SKIPPED = 1 (no optimizer step); every later
+ * one is zeros with SKIPPED = KL_STOP = UNEVALUATED = 1 (its loss was never computed). */
 #define GS_NUM_METRICS 16
 enum gs_metric_slot {
     GS_M_LOSS = 0, GS_M_POLICY_LOSS, GS_M_VALUE_LOSS, GS_M_ENTROPY, GS_M_CLIP_FRAC,
     GS_M_CLIP_FRAC_VF, GS_M_EXPLAINED_VAR, GS_M_KL, GS_M_APPROX_KL, GS_M_ADV_NORM_MEAN,
-    GS_M_ADV_NORM_STD, GS_M_KL_STOP, GS_M_GRAD_NORM, GS_M_SKIPPED, GS_M_RES0, GS_M_RES1
+    GS_M_ADV_NORM_STD, GS_M_KL_STOP, GS_M_GRAD_NORM, GS_M_SKIPPED, GS_M_UNEVALUATED, GS_M_RES1
 };
 
 size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch);

@@ -28,7 +28,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     else:
-        print(json.dumps(line), file=sys.stderr, flush=True)
+        os.write(2, (json.dumps(line) + "\n").encode())   # one write: ranks share stderr
     dist.barrier()
     dist.destroy_process_group()
 

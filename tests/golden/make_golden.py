@@ -20,6 +20,11 @@ Fixtures written:
                    adv, ret, sampler order, per-minibatch losses, final params
   policy_fwd.npz   MLPActorCritic forward (utils/models.py:285-346) + Categorical log_prob/entropy
   configs.json     load_config(...) resolution for the BASELINE.json configs C1-C5
+  configs_full.json  every field of those Config objects (what agents.build_agent receives)
+  trajectory_kl.npz  the trajectory with target_kl set: the sticky KL early stop
+                   (agents/base_agent.py:330-366) fires in the second rollout's update
+  ref_ckpt/        model.pt / optimizer.pt / state.json written by BaseAgent.save_checkpoint
+                   (agents/base_agent.py:658-732) after the trajectory run
   synth_env.npz    the synthetic env's hashed observations (spec below, not a reference artefact)
 
 Usage:  python tests/golden/make_golden.py
@@ -217,6 +222,8 @@ def _flat_grads(model):
 
 
 def _agent(model, cfg):
+    """A PPOAgent with just the attributes losses_for_batch reads (as test_ppo.py:73-98 builds
+    one); metrics_recorder.record collects every record."""
     agent = object.__new__(PPOAgent)
     torch.nn.Module.__init__(agent)
     agent.config = types.SimpleNamespace(normalize_advantages=cfg["normalize"], target_kl=cfg.get("target_kl"))
@@ -354,8 +361,25 @@ class _RefVecEnvAdapter:
         return self._env.step(actions)
 
 
-def make_trajectory():
-    """CartPole-v1:ppo shapes (C1: N=8, T=32, B=256, E=20) for 3 rollouts."""
+# get_metrics() keys that are wall-clock or object-valued (compared separately or not at all)
+_METRIC_SKIP = ("roll/fps", "action_dist")
+
+
+def _metrics_arrays(dicts):
+    """A list of metric dicts with identical keys -> (sorted key names, values [n, K])."""
+    keys = sorted(k for k in dicts[0] if k not in _METRIC_SKIP)
+    return np.array(keys), np.array([[float(d[k]) for k in keys] for d in dicts], np.float64)
+
+
+def make_trajectory(target_kl=None, out_name="trajectory.npz"):
+    """CartPole-v1:ppo shapes (C1: N=8, T=32, B=256, E=20) for 3 rollouts, through the
+    reference's own training-step logic (agents/base_agent.py:330-366): the sticky KL early
+    stop (`_early_stop_epoch`, never reset) skips the triggering minibatch's optimizer step and
+    every minibatch after it.  Also records, per rollout, the collector's get_metrics()
+    (utils/rollout_collector.py:686-760), every metrics_recorder record of losses_for_batch
+    (agents/ppo/ppo_agent.py:131-146) and, for the plain run, evaluate_episodes
+    (rollout_collector.py:570-655) on a second collector and a checkpoint written by
+    BaseAgent.save_checkpoint (agents/base_agent.py:658-732)."""
     N, T, E, B, D, A = 8, 32, 20, 256, 4, 2
     set_random_seed(42)
     model = MLPActorCritic(input_shape=(D,), hidden_dims=(256, 256), output_shape=(A,), activation="relu")
@@ -363,31 +387,44 @@ def make_trajectory():
     env = SyntheticVecEnv(n_envs=N, obs_dim=D, n_actions=A, episode_len=20, seed=42, truncate_every=3)
     collector = RolloutCollector(_RefVecEnvAdapter(env), model, n_steps=T, gamma=0.98, gae_lambda=0.8,
                                  returns_type="gae:rtg", advantages_type="gae", normalize_advantages=False)
-    cfg = dict(normalize="batch", clip=0.1, clip_vf=0.2, vf_coef=0.5, ent_coef=0.0)
+    cfg = dict(normalize="batch", clip=0.1, clip_vf=0.2, vf_coef=0.5, ent_coef=0.0, target_kl=target_kl)
     agent, recs = _agent(model, cfg)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     traj_holder = {}
     from utils.random import get_global_torch_generator
     loader = None
     rec = {k: [] for k in ["actions", "logp", "values", "adv", "ret", "obs", "rewards", "dones", "order", "losses"]}
+    evaluated, stepped, roll_metrics, action_dist = [], [], [], []
+    early_stop = False                 # BaseAgent._early_stop_epoch: set once, never reset
     for epoch in range(3):
         traj = collector.collect()
         traj_holder["t"] = traj
+        m = collector.get_metrics()
+        roll_metrics.append(m)
+        action_dist.append(np.asarray(m["action_dist"], np.int64))
         if loader is None:
             loader = build_index_collate_loader_from_collector(
                 collector=collector, trajectories_getter=lambda: traj_holder["t"], batch_size=B,
                 num_passes=E, generator=get_global_torch_generator(42))
         loader.sampler.set_epoch(epoch)        # Lightning fit_loop._set_sampler_epoch
-        order = []
-        orig_collate = loader.collate_fn
         for bi, batch in enumerate(loader):
-            # recover the batch indices from the sampler stream for the fixture
+            if early_stop:                     # training_step returns before losses_for_batch
+                evaluated.append(0)
+                stepped.append(0)
+                rec["losses"].append(np.nan)
+                continue
             opt.zero_grad()
             res = agent.losses_for_batch(batch, bi)
+            evaluated.append(1)
+            rec["losses"].append(float(res["loss"].item()))
+            if res["early_stop_epoch"]:
+                early_stop = True
+                stepped.append(0)
+                continue
             res["loss"].backward()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
             opt.step()
-            rec["losses"].append(float(res["loss"].item()))
+            stepped.append(1)
         loader.sampler.set_epoch(epoch)
         order = np.asarray(list(iter(loader.sampler)), np.int64)
         rec["order"].append(order)
@@ -401,12 +438,80 @@ def make_trajectory():
         rec["dones"].append(traj.dones.numpy().astype(np.uint8))
     out = {k: np.asarray(v) for k, v in rec.items()}
     out["losses"] = np.asarray(rec["losses"], np.float64)
+    out["evaluated"] = np.asarray(evaluated, np.uint8)
+    out["stepped"] = np.asarray(stepped, np.uint8)
     out["params0"] = params0
     out["params_final"] = _flat_params(model)
     out["dims"] = np.array([N, T, E, B, D, A], np.int64)
     out["env"] = np.array([20, 42, 3], np.int64)
-    np.savez_compressed(os.path.join(HERE, "trajectory.npz"), **out)
-    print("trajectory.npz written: losses", len(rec["losses"]))
+    out["target_kl"] = np.float64(target_kl if target_kl is not None else 0.0)
+    out["roll_metric_names"], out["roll_metric_values"] = _metrics_arrays(roll_metrics)
+    out["action_dist"] = np.asarray(action_dist)
+    out["train_metric_names"], out["train_metric_values"] = _metrics_arrays(recs)
+    if target_kl is None:
+        # evaluate_episodes on a second collector (the device agent's "val" stage: same env
+        # shape, seed + 1000), deterministic, 20 episodes over 8 envs
+        eval_env = SyntheticVecEnv(n_envs=N, obs_dim=D, n_actions=A, episode_len=20, seed=42 + 1000,
+                                   truncate_every=3)
+        eval_coll = RolloutCollector(_RefVecEnvAdapter(eval_env), model, n_steps=T, gamma=0.98, gae_lambda=0.8,
+                                     returns_type="gae:rtg", advantages_type="gae", normalize_advantages=False)
+        ev = eval_coll.evaluate_episodes(n_episodes=20, deterministic=True)
+        out["eval_metric_names"], out["eval_metric_values"] = _metrics_arrays([ev])
+        _write_reference_checkpoint(model, opt, collector)
+    np.savez_compressed(os.path.join(HERE, out_name), **out)
+    print(f"{out_name} written: losses", int(out["evaluated"].sum()), "of", len(evaluated), "evaluated")
+    return out
+
+
+def _write_reference_checkpoint(model, opt, collector):
+    """BaseAgent.save_checkpoint (agents/base_agent.py:658-732) on the trained trajectory model:
+    model.pt, optimizer.pt, state.json written by the reference's own code into ref_ckpt/."""
+    from agents.base_agent import BaseAgent
+    d = os.path.join(HERE, "ref_ckpt")
+    os.makedirs(d, exist_ok=True)
+    this = types.SimpleNamespace(
+        policy_model=model, optimizers=lambda: opt, current_epoch=3, run=None,
+        config=load_config("CartPole-v1", "ppo"),
+        get_rollout_collector=lambda stage: collector if stage == "train" else types.SimpleNamespace(
+            _best_episode_reward=float("-inf")))
+    torch.manual_seed(1234)            # the RNG state the file records (any fixed state)
+    BaseAgent.save_checkpoint(this, d)
+    print("ref_ckpt/ written:", sorted(os.listdir(d)))
+
+
+def make_trajectory_kl():
+    """The trajectory with target_kl set so that the sticky early stop fires in the middle of
+    the second rollout's update: the threshold sits halfway between the first approx_kl that
+    exceeds it and the largest one before."""
+    base = np.load(os.path.join(HERE, "trajectory.npz"))
+    names = [str(x) for x in base["train_metric_names"]]
+    ak = base["train_metric_values"][:, names.index("opt/ppo/approx_kl")]
+    best = None
+    for first in range(20, 45):
+        lo, hi = float(ak[:first].max()), float(ak[first])
+        if hi > lo * 1.05:
+            best = (first, 0.5 * (lo + hi))
+            break
+    assert best is not None, "no clean early-stop threshold in 20..45"
+    out = make_trajectory(target_kl=best[1], out_name="trajectory_kl.npz")
+    assert int(out["evaluated"].sum()) == best[0] + 1, (out["evaluated"].sum(), best)
+
+
+def make_configs_full():
+    """Every field of the Config object the reference's load_config resolves for C1-C5
+    (utils/config.py:887-889; dataclasses.asdict, enums as their values): what
+    agents.build_agent receives from train.py."""
+    import dataclasses
+    out = {}
+    for env, var in [("CartPole-v1", "ppo"), ("LunarLander-v3", "ppo"), ("ALE-Pong-v5", "rgb_ppo"),
+                     ("ALE-Breakout-v5", "rgb_ppo")]:
+        c = load_config(env, var)
+        d = {k: getattr(v, "value", v) for k, v in dataclasses.asdict(c).items()}
+        d["algo_id"] = c.algo_id
+        out[f"{env}:{var}"] = json.loads(json.dumps(d, default=lambda o: getattr(o, "value", str(o))))
+    with open(os.path.join(HERE, "configs_full.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print("configs_full.json written")
 
 
 def make_configs():
@@ -500,4 +605,6 @@ if __name__ == "__main__":
     make_configs()
     make_synth_env()
     make_trajectory()
+    make_trajectory_kl()
+    make_configs_full()
     make_schedules()

@@ -1,0 +1,232 @@
+"""GPU: the drop-in plugin surface against the reference's own outputs.
+
+* losses_for_batch / training_step on the reference's tensor batch (agents/ppo/ppo_agent.py:21-152,
+  base_agent.py:330-366) with metrics_recorder.record("train", ...) (ppo_agent.py:131-146);
+* the rollout collector's get_metrics() after every rollout (utils/rollout_collector.py:686-760)
+  and evaluate_episodes (:570-655), against the reference collector driven by the same
+  synthetic env (tests/golden/trajectory.npz);
+* the sticky KL early stop (base_agent.py:60,330-366; tests/golden/trajectory_kl.npz);
+* a checkpoint written by the reference's BaseAgent.save_checkpoint (tests/golden/ref_ckpt/);
+* build_agent from the Config the reference's load_config resolves (tests/golden/configs_full.json).
+
+Tolerances: one-minibatch loss and metrics 2e-6 (+1e-5 relative); trajectory-level losses and
+per-minibatch metrics 1e-4 (the north-star bar); collector statistics 1e-5 relative where they
+depend only on the env / replayed actions, 1e-3 relative where they depend on the policy's
+values (the trained weights agree to ~1e-5 relative), counts exactly.
+"""
+import json
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _agent_for_step(cuda, tag):
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(42)
+    if tag == "cartpole":
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=8))
+    else:
+        cfg = load_config("LunarLander-v3", "ppo", overrides=dict(n_envs=1, n_steps=64, ent_coef=0.01))
+    return DevicePPOAgent(cfg, device=cuda, use_graph=False)
+
+
+@pytest.mark.parametrize("tag", ["cartpole", "lunar_ent"])
+def test_losses_for_batch_on_reference_tensor_batch(golden, cuda, tag):
+    """The reference's batch (CPU tensors in a SimpleNamespace, as its tests pass it) through
+    DevicePPOAgent.losses_for_batch: loss and every recorded metric equal the reference's
+    record; then training_step on the same batch gives the reference's clipped-Adam update."""
+    from gsamd.metrics import ppo_keys
+    z = golden("ppo_step.npz")
+    agent = _agent_for_step(cuda, tag)
+    agent.policy_model.load_flat(z[f"{tag}/params0"])
+    batch = SimpleNamespace(observations=torch.as_tensor(z[f"{tag}/obs"]),
+                            actions=torch.as_tensor(z[f"{tag}/actions"]),
+                            logprobs=torch.as_tensor(z[f"{tag}/old_logprobs"]),
+                            values=torch.as_tensor(z[f"{tag}/old_values"]),
+                            advantages=torch.as_tensor(z[f"{tag}/advantages"]),
+                            returns=torch.as_tensor(z[f"{tag}/returns"]))
+    agent.metrics_recorder.reset_epoch("train")
+    out = agent.losses_for_batch(batch, 0)
+    assert set(out) == {"loss", "early_stop_epoch"} and out["early_stop_epoch"] is False
+    assert out["loss"].dim() == 0 and out["loss"].is_cuda
+    np.testing.assert_allclose(float(out["loss"]), float(z[f"{tag}/loss"]), atol=2e-6, rtol=1e-5)
+    got = agent.metrics_recorder.compute_epoch_means("train")
+    ref = dict(zip([str(x) for x in z[f"{tag}/metric_names"]], z[f"{tag}/metric_values"]))
+    assert set(got) == set(ref) == set(ppo_keys(True))
+    for k in ref:
+        np.testing.assert_allclose(got[k], ref[k], atol=2e-6, rtol=1e-5, err_msg=k)
+    agent.training_step(batch, 0)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(agent.policy_model.params.cpu().numpy(), z[f"{tag}/params1"], atol=2e-6, rtol=0)
+    assert agent.adam_step == 1
+
+
+def _replay_trajectory(agent, z, cuda, check_metrics=True):
+    """Replay the fixture's three rollouts (recorded actions) and updates through the agent's
+    collector and gs_ppo_update; returns the per-minibatch device records."""
+    from gsamd._lib import check, lib
+    N, T, E, B, D, A = (int(x) for x in z["dims"])
+    coll = agent.get_rollout_collector("train")
+    names = [str(x) for x in z["roll_metric_names"]]
+    recs = []
+    for ep in range(3):
+        acts = torch.as_tensor(z["actions"][ep].reshape(N, T).T.copy()).to(cuda)
+        coll.collect(replay_actions=acts)
+        torch.cuda.synchronize()
+        if check_metrics:
+            m = coll.get_metrics()
+            assert set(names) <= set(m), set(names) - set(m)
+            np.testing.assert_array_equal(m["action_dist"], z["action_dist"][ep])
+            for j, k in enumerate(names):
+                want = z["roll_metric_values"][ep][j]
+                if k.startswith("cnt/") or k in ("roll/env_steps", "roll/vec_steps", "roll/episodes") or \
+                        k.startswith("roll/ep_") or k.startswith("roll/baseline"):
+                    assert m[k] == want, (ep, k, m[k], want)
+                elif k.startswith(("roll/adv", "roll/return")):
+                    np.testing.assert_allclose(m[k], want, rtol=1e-3, atol=1e-5, err_msg=f"{ep} {k}")
+                else:
+                    np.testing.assert_allclose(m[k], want, rtol=1e-5, atol=1e-6, err_msg=f"{ep} {k}")
+        idx = agent.prefetcher.upload(ep)
+        check(lib.gs_ppo_update(agent.policy_model.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                                agent.adam_v.data_ptr(), agent.policy_model.dims, agent.hparams(), coll.buffer.view(),
+                                idx.data_ptr(), B, agent.n_minibatches, agent.adam_step, agent.metrics_buf.data_ptr(),
+                                agent.stop_flag.data_ptr(), agent.workspace.data_ptr(), agent.workspace.numel(), None,
+                                0, torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        rec = agent.metrics_buf.cpu().numpy().copy()
+        agent.adam_step += int((rec[:, 13] == 0).sum())
+        recs.append(rec)
+    return np.concatenate(recs)
+
+
+def _trajectory_agent(cuda, z, **over):
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    N, T, E, B, D, A = (int(x) for x in z["dims"])
+    L, seed, trunc = (int(x) for x in z["env"])
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(episode_len=L, truncate_every=trunc, obs_dim=D,
+                                                           n_actions=A, **over))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False)
+    agent.policy_model.load_flat(z["params0"])
+    return agent
+
+
+def test_collector_metrics_and_evaluation_vs_reference(golden, cuda):
+    """get_metrics() after each of the three replayed rollouts (counters, running statistics,
+    action histogram, rolling episode window, best / last episode), the per-minibatch
+    metrics_recorder records of the update, and evaluate_episodes(20, deterministic) on the val
+    collector after training — all against the reference collector's own outputs."""
+    from gsamd.metrics import ppo_keys, ppo_records
+    z = golden("trajectory.npz")
+    agent = _trajectory_agent(cuda, z)
+    rec = _replay_trajectory(agent, z, cuda)
+    names = [str(x) for x in z["train_metric_names"]]
+    keys = list(ppo_keys(True))
+    dev = ppo_records(rec, 0.5, 0.0, True)
+    ref = z["train_metric_values"]
+    assert set(names) == set(keys) and dev.shape == ref.shape
+    for j, k in enumerate(keys):
+        np.testing.assert_allclose(dev[:, j], ref[:, names.index(k)], atol=1e-4, rtol=1e-4, err_msg=k)
+    ev = agent.get_rollout_collector("val").evaluate_episodes(n_episodes=20, deterministic=True)
+    en = [str(x) for x in z["eval_metric_names"]]
+    assert set(en) <= set(ev), set(en) - set(ev)
+    for j, k in enumerate(en):
+        want = z["eval_metric_values"][0][j]
+        if k.startswith(("roll/adv", "roll/return")):
+            np.testing.assert_allclose(ev[k], want, rtol=1e-3, atol=1e-5, err_msg=k)
+        else:
+            np.testing.assert_allclose(ev[k], want, rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_kl_early_stop_vs_reference(golden, cuda):
+    """target_kl set so the reference's sticky early stop fires in the second rollout's update
+    (minibatch 37 of 60): the same minibatches are evaluated, the same ones step, their losses
+    agree within 1e-4, and the final weights match."""
+    from gsamd._lib import M
+    z = golden("trajectory_kl.npz")
+    agent = _trajectory_agent(cuda, z, target_kl=float(z["target_kl"]))
+    rec = _replay_trajectory(agent, z, cuda, check_metrics=False)
+    evaluated = (rec[:, M["unevaluated"]] == 0).astype(np.uint8)
+    stepped = (rec[:, M["skipped"]] == 0).astype(np.uint8)
+    np.testing.assert_array_equal(evaluated, z["evaluated"])
+    np.testing.assert_array_equal(stepped, z["stepped"])
+    ev = z["evaluated"].astype(bool)
+    np.testing.assert_allclose(rec[ev, M["loss"]], z["losses"][ev], atol=1e-4, rtol=0)
+    p_dev = agent.policy_model.params.cpu().numpy().astype(np.float64)
+    p_ref = z["params_final"].astype(np.float64)
+    assert np.linalg.norm(p_dev - p_ref) / np.linalg.norm(p_ref) < 1e-4
+    # the recorder books the evaluated minibatches (the tripping one included), as the reference
+    agent.record_epoch_metrics()
+    assert agent._early_stop_epoch
+    assert agent.adam_step == int(z["stepped"].sum())
+
+
+def test_reference_checkpoint_resumes(cuda):
+    """model.pt / optimizer.pt / state.json written by the reference's BaseAgent.save_checkpoint
+    after the trajectory run: weights, Adam moments, step count, lr, counters load exactly,
+    and training continues from them."""
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    d = os.path.join(GOLDEN, "ref_ckpt")
+    sd = torch.load(os.path.join(d, "model.pt"), map_location="cpu", weights_only=True)
+    opt = torch.load(os.path.join(d, "optimizer.pt"), map_location="cpu", weights_only=True)
+    state = json.load(open(os.path.join(d, "state.json")))
+    torch.manual_seed(0)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=8, n_epochs=2))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
+    agent.load_checkpoint(d)
+    torch.cuda.synchronize()
+    flat = np.concatenate([t.reshape(-1).numpy() for t in sd.values()])
+    assert np.array_equal(agent.policy_model.params.cpu().numpy(), flat)
+    st = opt[0]["state"]
+    m = np.concatenate([st[i]["exp_avg"].reshape(-1).numpy() for i in sorted(st)])
+    v = np.concatenate([st[i]["exp_avg_sq"].reshape(-1).numpy() for i in sorted(st)])
+    assert np.array_equal(agent.adam_m.cpu().numpy(), m) and np.array_equal(agent.adam_v.cpu().numpy(), v)
+    assert agent.adam_step == int(float(st[0]["step"]))
+    assert agent.policy_lr == opt[0]["param_groups"][0]["lr"]
+    assert agent.current_epoch == state["epoch"]
+    coll = agent.get_rollout_collector("train")
+    assert coll.total_steps == state["total_env_steps"] and coll.total_vec_steps == state["total_vec_steps"]
+    assert coll._best_episode_reward == state["best_train_reward"]
+    agent.train_epoch()
+    torch.cuda.synchronize()
+    assert np.isfinite(agent.minibatch_losses()).all()
+    assert agent.adam_step == int(float(st[0]["step"])) + agent.n_minibatches
+
+
+@pytest.mark.parametrize("key", ["CartPole-v1:ppo", "ALE-Breakout-v5:rgb_ppo"])
+def test_build_agent_from_reference_config(cuda, key):
+    """agents.build_agent(config) with the Config object train.py would pass (every field the
+    reference's load_config resolved): the device agent's hyper-parameters are the reference's."""
+    from gsamd import build_agent
+    full = json.load(open(os.path.join(GOLDEN, "configs_full.json")))[key]
+    want = json.load(open(os.path.join(GOLDEN, "configs.json")))[key]
+    ref_cfg = SimpleNamespace(**full)
+    small = dict(n_envs=8, n_steps=128, batch_size=1024) if "ALE" in key else {}
+    torch.manual_seed(42)
+    agent = build_agent(ref_cfg, device=cuda, track_stats=False) if not small else None
+    if agent is None:
+        from gsamd.config import from_reference_config
+        from gsamd.ppo_agent import DevicePPOAgent
+        agent = DevicePPOAgent(from_reference_config(ref_cfg, **small), device=cuda, track_stats=False)
+    c = agent.config
+    for k in ("n_epochs", "gamma", "gae_lambda", "clip_range", "clip_range_vf", "ent_coef", "vf_coef",
+              "policy_lr", "max_grad_norm", "seed", "target_kl", "normalize_advantages", "model_id"):
+        assert getattr(c, k) == want[k], k
+    if not small:
+        assert (c.n_envs, c.n_steps, c.batch_size) == (want["n_envs"], want["n_steps"], want["batch_size"])
+    assert tuple(c.hidden_dims) == tuple(want["hidden_dims"])
+    hp = agent.hparams()
+    assert hp.clip_range == np.float32(want["clip_range"]) and hp.lr == np.float32(want["policy_lr"])
+    agent.train_epoch()
+    torch.cuda.synchronize()
+    assert np.isfinite(agent.minibatch_losses()).all()

@@ -153,3 +153,68 @@ def test_product_does_not_import_oracle():
                 src = open(os.path.join(dp, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle\b", src, re.M), f
                 assert "liboracle" not in src, f
+
+
+def test_reference_config_object_adapts_to_the_presets():
+    """build_agent receives the reference's Config object (every field its load_config resolved,
+    tests/golden/configs_full.json); from_reference_config must yield the hyper-parameters the
+    reference resolved (configs.json) for C1, C3, C4 and C5."""
+    import json
+    from types import SimpleNamespace
+    from gsamd.config import from_reference_config
+    full = json.load(open(os.path.join(ROOT, "tests", "golden", "configs_full.json")))
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+    assert set(full) == set(want)
+    for key, d in full.items():
+        c = from_reference_config(SimpleNamespace(**d))
+        r = want[key]
+        for f in ("n_envs", "n_steps", "batch_size", "n_epochs", "gamma", "gae_lambda", "clip_range",
+                  "clip_range_vf", "ent_coef", "vf_coef", "policy_lr", "max_grad_norm", "model_id", "seed",
+                  "normalize_advantages", "target_kl", "frame_stack"):
+            assert getattr(c, f) == r[f], (key, f)
+        assert list(c.hidden_dims) == r["hidden_dims"] and c.valid_actions == r["valid_actions"]
+        assert c.resolved_n_actions() == r["n_actions"] and c.obs_type == r["obs_type"]
+
+
+def test_rolling_window_matches_reference_arithmetic():
+    """The episode window's mean is formed by the same float operations as the reference's
+    RollingWindow (add; when full subtract the evicted value first): compare against a direct
+    restatement on values whose running sum rounds."""
+    from collections import deque
+    from gsamd.rollout_stats import RollingWindow
+    rng = np.random.default_rng(0)
+    vals = (rng.standard_normal(1000) * 10 ** rng.uniform(-3, 3, 1000)).tolist()
+    w = RollingWindow(100)
+    dq, total = deque(), 0.0
+    for v in vals:
+        if len(dq) == 100:
+            total -= float(dq.popleft())
+        dq.append(v)
+        total += float(v)
+        w.append(v)
+        assert w.mean() == total / len(dq) and len(w) == len(dq)
+    with pytest.raises(ValueError):
+        RollingWindow(0)
+
+
+def test_metrics_recorder_means_and_ppo_keys():
+    """record / record_rows / compute_epoch_means (utils/metrics_recorder.py surface) and the
+    device-record -> losses_for_batch key mapping (agents/ppo/ppo_agent.py:131-146)."""
+    import torch
+    from gsamd._lib import GS_NUM_METRICS, M
+    from gsamd.metrics import MetricsRecorder, ppo_keys, ppo_records
+    r = MetricsRecorder()
+    r.record("train", {"a": torch.tensor(1.0), "b": np.float32(2.0), "skip": np.zeros(3)})
+    r.record_rows("train", ("a", "b"), np.array([[3.0, 4.0], [5.0, 6.0]]))
+    assert r.compute_epoch_means("train") == {"a": 3.0, "b": 4.0}
+    with pytest.raises(AssertionError):
+        r.record("train", {"a": float("nan")})
+    r.reset_epoch("train")
+    assert r.compute_epoch_means("train") == {}
+    row = np.zeros((1, GS_NUM_METRICS), np.float32)
+    row[0, M["loss"]], row[0, M["entropy"]], row[0, M["value_loss"]] = 1.5, 0.6, 0.25
+    vals = dict(zip(ppo_keys(True), ppo_records(row, 0.5, 0.01, True)[0]))
+    assert vals["opt/loss/entropy"] == np.float32(-0.6) and vals["opt/policy/entropy"] == np.float32(0.6)
+    assert vals["opt/loss/value_scaled"] == np.float32(0.125)
+    assert vals["opt/loss/entropy_scaled"] == np.float32(0.01) * np.float32(-0.6)
+    assert len(ppo_keys(False)) == 13 and len(ppo_keys(True)) == 15
