@@ -33,6 +33,9 @@ import torch  # noqa: E402
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
+# CPU port vs the reference's own loop on the same 8-core container at C2 shapes
+# (5 646 / 2 814 env-steps/s)
+CPU_PORT_OVER_REFERENCE = round(5646.0 / 2814.0, 3)
 
 
 def _log(*a):
@@ -413,6 +416,8 @@ def main():
                "step_ms": round(r["step_s"] * 1e3, 3), "minibatch_ms": round(r["minibatch_s"] * 1e3, 3)}
     elif rank == 0 and world == 1 and args.cpu_minibatches > 0:
         from oracle.cpu_ppo import run_cpu_baseline
+        # the box's CPU share is 16 threads per GPU (os.sched_getaffinity shows the whole
+        # machine there): use at most that many, report both
         cores = min(len(os.sched_getaffinity(0)), 16)
         r = run_cpu_baseline(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,
                              obs_dim=pm.obs_dim, hidden=tuple(pm.hidden_dims), n_actions=pm.n_actions,
@@ -423,9 +428,14 @@ def main():
                           f"{r['minibatches_timed']} of {r['minibatches_per_rollout']} minibatch steps "
                           f"(torch-CPU fwd/bwd/clip/Adam), update extrapolated; wall {r['wall_s']:.1f}s"),
                "collect_s": round(r["collect_s"], 4), "minibatch_ms": round(r["minibatch_s"] * 1e3, 4),
-               "calibration": ("on the build container's 8 cores the port ran 5 646 env-steps/s vs 2 814 for the "
-                               "reference's own loop (SURVEY.md §6): the port omits Lightning/DataLoader/recorder "
-                               "overheads, so this baseline is ~2x conservative")}
+               "affinity_cores": len(os.sched_getaffinity(0)),
+               # measured in the build container, same 8 cores, same C2 shapes:
+               # port 5 646 env-steps/s vs the reference's own loop 2 814
+               "calibration_port_over_reference": CPU_PORT_OVER_REFERENCE,
+               "reference_equivalent_value": round(r["env_steps_per_s"] / CPU_PORT_OVER_REFERENCE, 2),
+               "calibration": ("the port omits the reference's Lightning training_step, DataLoader collate and "
+                               "metrics-recorder overheads; divided by the measured ratio it estimates the "
+                               "reference loop on these cores")}
 
     if rank == 0:
         line = {

@@ -179,11 +179,12 @@ struct AdamArgs {
     float one_minus_b2;     // f32(1 - beta2)
     float neg_step_size;    // f32(-lr / (1 - beta1^t))
     float bc2_sqrt;         // f32(sqrt(1 - beta2^t))
+    float inv_bc2_sqrt;     // f32(1 / sqrt(1 - beta2^t)) (MLP chain: a multiply instead of a division)
     float eps;
     float grad_scale;       // 1/world for all-reduced sums, else 1
     int n_slots;
     int nrb;                // dW1/db1 partial row blocks (0: grads already final in G)
-    const float *sched;     // optional device table {neg_step_size, bc2_sqrt} per step (graph replay)
+    const float *sched;     // optional device table {neg_step_size, inv_bc2_sqrt} per step (graph replay)
     int sched_idx;
     const int64_t *step_base;   // graph chunk replay: added to sched_idx and the metrics record
     int stage_lds;          // set by the launcher: stage slots + partials through LDS

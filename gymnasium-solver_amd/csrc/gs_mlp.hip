@@ -130,17 +130,20 @@ __device__ __forceinline__ float clip_coef(float total, const AdamArgs &aa)
 
 // One parameter of torch.optim.Adam (single-tensor path, amsgrad off) on the clipped gradient;
 // shared by k_clip_adam and the lagged step in k_fwd_hidden so both round identically.
+// inv_bc2s = f32(1 / sqrt(1 - beta2^t)) (host, double), so the bias correction is a multiply.
 __device__ __forceinline__ float adam_param(float graw, float coef, float &m, float &v, float &p,
-                                            const AdamArgs &aa, float neg_step, float bc2s)
+                                            const AdamArgs &aa, float neg_step, float inv_bc2s)
 {
     const float g = graw * coef;
     m = m + aa.one_minus_b1 * (g - m);            // exp_avg.lerp_(grad, 1 - beta1)
     v = v * aa.b2;                                // exp_avg_sq.mul_(beta2)
     v = v + (aa.one_minus_b2 * g) * g;            //   .addcmul_(grad, grad, 1 - beta2)
-    // hardware sqrt and reciprocal-based division (~1-2 ulp; the correctly rounded sequences
-    // cost ~4x the instructions and this runs 4-21 times per thread)
-    const float denom = __fdividef(__builtin_amdgcn_sqrtf(v), bc2s) + aa.eps;
-    p = p + neg_step * __fdividef(m, denom);
+    // hardware sqrt and reciprocal (v_sqrt_f32, v_rcp_f32: ~1 ulp each) instead of torch's
+    // correctly rounded divisions: IEEE division lowers to a v_div_scale / v_div_fmas /
+    // v_div_fixup sequence serialised through VCC, ~10x the latency, and this runs 4-21 times
+    // per thread on the minibatch chain's critical path
+    const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2s + aa.eps;
+    p = p + neg_step * (m * __builtin_amdgcn_rcpf(denom));
     return g;
 }
 
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         };
         auto ld1 = [](const float *base, int64_t o) { return *(const __attribute__((address_space(1))) float *)(base + o); };
         const float neg_step = apply && aa.sched ? aa.sched[2 * kprev] : aa.neg_step_size;
-        const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.bc2_sqrt;
+        const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.inv_bc2_sqrt;
         float xv = 0.0f;
         if (tid < kTile * cD) {
             const int i = tid / cD;
@@ -1814,7 +1817,7 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     __syncthreads();
     const float coef = s_coef * aa.grad_scale;
     const float neg_step = aa.sched ? aa.sched[2 * (aa.sched_idx + kb)] : aa.neg_step_size;
-    const float bc2s = aa.sched ? aa.sched[2 * (aa.sched_idx + kb) + 1] : aa.bc2_sqrt;
+    const float bc2s = aa.sched ? aa.sched[2 * (aa.sched_idx + kb) + 1] : aa.inv_bc2_sqrt;
     float go[4], mo[4], vo[4], po[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -206,6 +206,7 @@ StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, in
     const double bc2 = 1.0 - pow(b2, (double)t);
     a.aa.neg_step_size = (float)(-(double)hp.lr / bc1);
     a.aa.bc2_sqrt = (float)sqrt(bc2);
+    a.aa.inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
     a.aa.eps = hp.adam_eps;
     a.aa.grad_scale = 1.0f;
     a.aa.n_slots = n_sumsq_slots(L);
@@ -441,7 +442,7 @@ struct GraphKeyHash {
 };
 struct GraphEntry {
     hipGraphExec_t exec;
-    float *sched;      // per-step {neg_step_size, bc2_sqrt}, n_minibatches entries
+    float *sched;      // per-step {neg_step_size, inv_bc2_sqrt}, n_minibatches entries
     int64_t *base;     // first minibatch of the replayed chunk (device scalar)
     int64_t *hbase;    // pinned host table r * chunk, the source of each replay's base copy
     float *hsched;     // pinned staging for the schedule table
@@ -649,7 +650,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     for (int64_t k = 0; k < n_minibatches; ++k) {
         const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
         e.hsched[2 * k] = sa.aa.neg_step_size;
-        e.hsched[2 * k + 1] = sa.aa.bc2_sqrt;
+        e.hsched[2 * k + 1] = sa.aa.inv_bc2_sqrt;
     }
     GS_HIP(hipMemcpyAsync(e.sched, e.hsched, sizeof(float) * 2 * (size_t)n_minibatches, hipMemcpyHostToDevice, s));
     GS_HIP(hipEventRecord(e.sched_copied, s));

@@ -2,7 +2,7 @@
 
 Importable only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
 as the checker.  The product path (gymnasium-solver_amd/) never imports anything here;
-tests/test_product_isolation.py enforces that.
+tests/test_host_cpu.py::test_product_does_not_import_oracle enforces that.
 """
 import ctypes
 import os

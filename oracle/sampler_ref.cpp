@@ -1,4 +1,4 @@
-// ORACLE — test infrastructure only (see oracle/README.md): the checker for the
+// ORACLE — test infrastructure only (see oracle/__init__.py): the checker for the
 // product sampler, never linked into gymnasium-solver_amd/.
 //
 // Restatement of the reference's MultiPassRandomSampler index stream

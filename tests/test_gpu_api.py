@@ -79,8 +79,12 @@ def _replay_trajectory(agent, z, cuda, check_metrics=True):
     recs = []
     for ep in range(3):
         acts = torch.as_tensor(z["actions"][ep].reshape(N, T).T.copy()).to(cuda)
-        coll.collect(replay_actions=acts)
+        traj = coll.collect(replay_actions=acts)
         torch.cuda.synchronize()
+        np.testing.assert_array_equal(traj.observations.cpu().numpy(), z["obs"][ep])
+        np.testing.assert_array_equal(traj.dones.cpu().numpy().astype(np.uint8), z["dones"][ep])
+        np.testing.assert_allclose(traj.advantages.cpu().numpy(), z["adv"][ep], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(traj.returns.cpu().numpy(), z["ret"][ep], atol=1e-5, rtol=0)
         if check_metrics:
             m = coll.get_metrics()
             assert set(names) <= set(m), set(names) - set(m)
@@ -107,27 +111,34 @@ def _replay_trajectory(agent, z, cuda, check_metrics=True):
     return np.concatenate(recs)
 
 
-def _trajectory_agent(cuda, z, **over):
+def _trajectory_agent(cuda, z, host_env=False, **over):
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
+    from gsamd.synthetic_env import SyntheticVecEnv
     N, T, E, B, D, A = (int(x) for x in z["dims"])
     L, seed, trunc = (int(x) for x in z["env"])
     torch.manual_seed(42)
     cfg = load_config("CartPole-v1", "ppo", overrides=dict(episode_len=L, truncate_every=trunc, obs_dim=D,
                                                            n_actions=A, **over))
-    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False)
+    # host_env: a gymnasium-style host vector env (reset / 5-tuple step / RecordEpisodeStatistics
+    # infos) -> the collector's host branch: one H2D of obs and one D2H of actions per step
+    env = SyntheticVecEnv(n_envs=N, obs_dim=D, n_actions=A, episode_len=L, seed=seed, truncate_every=trunc) \
+        if host_env else None
+    agent = DevicePPOAgent(cfg, env=env, device=cuda, use_graph=False)
     agent.policy_model.load_flat(z["params0"])
     return agent
 
 
-def test_collector_metrics_and_evaluation_vs_reference(golden, cuda):
+@pytest.mark.parametrize("host_env", [False, True])
+def test_collector_metrics_and_evaluation_vs_reference(golden, cuda, host_env):
     """get_metrics() after each of the three replayed rollouts (counters, running statistics,
     action histogram, rolling episode window, best / last episode), the per-minibatch
     metrics_recorder records of the update, and evaluate_episodes(20, deterministic) on the val
-    collector after training — all against the reference collector's own outputs."""
+    collector after training — all against the reference collector's own outputs; with the
+    device env and with a host env (the collector's per-step H2D/D2H branch)."""
     from gsamd.metrics import ppo_keys, ppo_records
     z = golden("trajectory.npz")
-    agent = _trajectory_agent(cuda, z)
+    agent = _trajectory_agent(cuda, z, host_env=host_env)
     rec = _replay_trajectory(agent, z, cuda)
     names = [str(x) for x in z["train_metric_names"]]
     keys = list(ppo_keys(True))

@@ -305,6 +305,53 @@ def test_minibatch_step_vs_numpy_oracle(cuda, env, variant, n_envs):
     np.testing.assert_allclose(agent.policy_model.params.cpu().numpy(), p1, atol=5e-6, rtol=0)
 
 
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_update_first_minibatches_vs_numpy_oracle(cuda, use_graph):
+    """The default update chain at the full C2 size (4096 envs x 32 steps, the lagged fused
+    chain: each minibatch's clip + Adam inside the next forward) over the first 8 minibatches of
+    the sampler stream, against 8 sequential numpy-oracle steps on the same rows: every
+    minibatch loss within 1e-5 relative, the parameters after the 8th step within 1e-5
+    relative L2 (Adam turns last-bit gradient differences of near-zero-gradient weights into up
+    to lr-sized moves, hence the norm bar)."""
+    from oracle import ppo_ref as R
+    from gsamd._lib import check, lib
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
+    agent.train_dataloader()
+    traj = agent._trajectories
+    coll = agent.get_rollout_collector("train")
+    idx_dev = agent.prefetcher.upload(0)
+    pm = agent.policy_model
+    dims = (pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions)
+    p = pm.params.cpu().numpy()
+    n, B = 8, agent.batch_size
+    check(lib.gs_ppo_update(pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                            agent.adam_v.data_ptr(), pm.dims, agent.hparams(), coll.buffer.view(), idx_dev.data_ptr(),
+                            B, n, 0, agent.metrics_buf.data_ptr(), agent.stop_flag.data_ptr(),
+                            agent.workspace.data_ptr(), agent.workspace.numel(), None, 1 if use_graph else 0,
+                            torch.cuda.current_stream().cuda_stream), "gs_ppo_update")
+    torch.cuda.synchronize()
+    losses = agent.metrics_buf[:n, 0].cpu().numpy()
+    stream = idx_dev.cpu().numpy().astype(np.int64)
+    fields = [traj.observations.cpu().numpy(), traj.actions.cpu().numpy(), traj.logprobs.cpu().numpy(),
+              traj.values.cpu().numpy(), traj.advantages.cpu().numpy(), traj.returns.cpu().numpy()]
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    for k in range(n):
+        rows = stream[k * B:(k + 1) * B]
+        loss, _, g = R.ppo_loss_and_grads(p, dims, *(f[rows] for f in fields), clip=cfg.clip_range,
+                                          clip_vf=cfg.clip_range_vf, vf_coef=cfg.vf_coef, ent_coef=cfg.ent_coef)
+        np.testing.assert_allclose(losses[k], loss, rtol=1e-5, atol=1e-6, err_msg=f"minibatch {k}")
+        gc, _ = R.clip_grad_norm(g, dims, cfg.max_grad_norm)
+        p, m, v = R.adam_step(p, gc, m, v, k + 1, cfg.policy_lr)
+    p_dev = pm.params.cpu().numpy().astype(np.float64)
+    assert np.linalg.norm(p_dev - p) / np.linalg.norm(p) < 1e-5
+    assert np.abs(p_dev - p).max() < 1e-3
+
+
 @pytest.mark.parametrize("env,variant,n_envs", CASES)
 @pytest.mark.parametrize("use_graph", [False, True])
 def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph):
