@@ -47,10 +47,12 @@ __global__ __launch_bounds__(256) void k_atari_counters(int32_t *__restrict__ st
                                                         int64_t env_offset, uint64_t step_count,
                                                         float *__restrict__ rew_row, uint8_t *__restrict__ done_row,
                                                         uint8_t *__restrict__ to_row, int32_t *__restrict__ ep_cnt,
-                                                        float *__restrict__ ep_ret_sum, float *__restrict__ ep_len_sum)
+                                                        float *__restrict__ ep_ret_sum, float *__restrict__ ep_len_sum,
+                                                        const uint64_t *__restrict__ clock)
 {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= N) return;
+    if (clock) step_count += clock[1];      // rollout clock (graph replay)
     const uint64_t ge = (uint64_t)(env_offset + e);
     int k = state[4 * e + 0] + 1;
     int epi = state[4 * e + 1];
@@ -80,9 +82,11 @@ __global__ __launch_bounds__(256) void k_atari_counters(int32_t *__restrict__ st
 
 // ---- the frame source: raw RGB frames 2*step and 2*step+1 of every env, 8 bytes per thread
 __global__ __launch_bounds__(256) void k_atari_render(uint8_t *__restrict__ frames, int64_t N, uint64_t seed,
-                                                      int64_t env_offset, uint64_t step_count)
+                                                      int64_t env_offset, uint64_t step_count,
+                                                      const uint64_t *__restrict__ clock)
 {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (clock) step_count += clock[1];
     constexpr int per_env = 2 * kFrameBytes / 8;
     if (t >= N * per_env) return;
     const int64_t e = t / per_env;
@@ -213,7 +217,7 @@ extern "C" int gs_atari_render(uint8_t *frames, int64_t N, uint64_t seed, int64_
 {
     GS_REQUIRE(N > 0 && frames, "gs_atari_render: bad argument");
     hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, (hipStream_t)stream, frames,
-                       N, seed, env_offset, step_count);
+                       N, seed, env_offset, step_count, (const uint64_t *)nullptr);
     GS_LAUNCH_CHECK("k_atari_render");
     return GS_OK;
 }
@@ -238,7 +242,7 @@ extern "C" int gs_atari_env_reset(int32_t *state, float *ep_ret, uint8_t *stack,
     GS_HIP(hipStreamSynchronize(s));   // pageable source: keep it alive until copied
     GS_HIP(hipMemsetAsync(ep_ret, 0, sizeof(float) * N, s));
     hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
-                       env_offset, (uint64_t)0);
+                       env_offset, (uint64_t)0, (const uint64_t *)nullptr);
     hipLaunchKernelGGL(k_atari_stack, dim3(nblk(N * out_h * out_w)), dim3(256), 0, s, frames, (const uint8_t *)nullptr,
                        N, stack_n, out_h, out_w, stack);
     GS_LAUNCH_CHECK("k_atari_stack");
@@ -249,7 +253,7 @@ extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, 
                                  int32_t stack_n, int32_t out_h, int32_t out_w, int32_t episode_len,
                                  int32_t truncate_every, uint64_t seed, int64_t env_offset, uint64_t step_count,
                                  float *rewards_row, uint8_t *dones_row, uint8_t *timeouts_row, int32_t *ep_done_count,
-                                 float *ep_ret_sum, float *ep_len_sum, void *stream)
+                                 float *ep_ret_sum, float *ep_len_sum, const uint64_t *clock, void *stream)
 {
     GS_REQUIRE(N > 0 && state && ep_ret && stack && frames && stack_n >= 1 && episode_len > 0,
                "gs_atari_env_step: bad argument");
@@ -260,9 +264,9 @@ extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, 
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_atari_counters, dim3(nblk(N)), dim3(256), 0, s, state, ep_ret, N, episode_len, truncate_every,
                        seed, env_offset, step_count, rewards_row, dones_row, timeouts_row, ep_done_count, ep_ret_sum,
-                       ep_len_sum);
+                       ep_len_sum, clock);
     hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
-                       env_offset, step_count);
+                       env_offset, step_count, clock);
     hipLaunchKernelGGL(k_atari_stack, dim3(nblk(N * out_h * out_w)), dim3(256), 0, s, frames, dones_row, N, stack_n,
                        out_h, out_w, stack);
     GS_LAUNCH_CHECK("k_atari_stack");

@@ -319,7 +319,8 @@ template <int AM>
 __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
                                                  int64_t R, int mode,
                                                  uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
-                                                 float *__restrict__ logp, float *__restrict__ value)
+                                                 float *__restrict__ logp, float *__restrict__ value,
+                                                 const uint64_t *__restrict__ clock)
 {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= R) return;
@@ -347,7 +348,8 @@ __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, co
         }
         actions[r] = act;
     } else {
-        const uint64_t hh = mix64d(mix64d(mix64d(seed) ^ counter) ^ (uint64_t)r);
+        const uint64_t ctr = counter + (clock ? clock[0] : 0ull);   // rollout clock (graph replay)
+        const uint64_t hh = mix64d(mix64d(mix64d(seed) ^ ctr) ^ (uint64_t)r);
         const float u = (float)(hh >> 40) * (1.0f / 16777216.0f);
         float c = 0.f;
         int last = 0;
@@ -898,7 +900,7 @@ extern "C" size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows)
 
 extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const uint8_t *obs, int64_t N, int mode,
                                  uint64_t rng_seed, uint64_t rng_counter, int64_t *actions, float *logp, float *value,
-                                 void *workspace, void *stream)
+                                 void *workspace, const uint64_t *clock, void *stream)
 {
     int rc = check_cnn(dims);
     if (rc) return rc;
@@ -912,10 +914,10 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     if ((rc = forward(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s))) return rc;
     if (L.A <= 18)
         hipLaunchKernelGGL(k_cnn_act<18>, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed,
-                           rng_counter, actions, logp, value);
+                           rng_counter, actions, logp, value, clock);
     else
         hipLaunchKernelGGL(k_cnn_act<kAMax>, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed,
-                           rng_counter, actions, logp, value);
+                           rng_counter, actions, logp, value, clock);
     GS_LAUNCH_CHECK("k_cnn_act");
     return GS_OK;
 }

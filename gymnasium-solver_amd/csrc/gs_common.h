@@ -222,7 +222,8 @@ int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, co
                       float *zpart, float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s, uint16_t *h2mask = nullptr);
 size_t fwd_lds_bytes(const Layout &L);
 int launch_heads_act(const float *P, const Layout &L, const float *zpart, int64_t rows, int mode, uint64_t seed,
-                     uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s);
+                     uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s,
+                     const uint64_t *clock = nullptr);
 int launch_loss(const float *P, const Layout &L, int64_t B, const Workspace &ws, const LossArgs &la, float *metrics,
                 int32_t *stop, hipStream_t s);
 size_t bwd_lds_bytes(const Layout &L, int64_t B);

@@ -42,10 +42,12 @@ __global__ __launch_bounds__(256) void k_env_step(int32_t *__restrict__ state, f
                                                   float reward, uint64_t seed, int64_t env_offset, uint64_t step_count,
                                                   float *__restrict__ rew_row, uint8_t *__restrict__ done_row,
                                                   uint8_t *__restrict__ to_row, int32_t *__restrict__ ep_cnt,
-                                                  float *__restrict__ ep_ret_sum, float *__restrict__ ep_len_sum)
+                                                  float *__restrict__ ep_ret_sum, float *__restrict__ ep_len_sum,
+                                                  const uint64_t *__restrict__ clock)
 {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= N) return;
+    if (clock) step_count += clock[1];      // rollout clock (graph replay)
     int k = state[4 * e + 0] + 1;
     int epi = state[4 * e + 1];
     int len = state[4 * e + 2] + 1;
@@ -128,13 +130,14 @@ extern "C" int gs_env_reset(int32_t *state, float *ep_ret, float *obs, int64_t N
 extern "C" int gs_env_step(int32_t *state, float *ep_ret, float *obs, int64_t N, int32_t obs_dim, int32_t episode_len,
                            int32_t truncate_every, float reward, uint64_t seed, int64_t env_offset,
                            uint64_t step_count, float *rewards_row, uint8_t *dones_row, uint8_t *timeouts_row,
-                           int32_t *ep_done_count, float *ep_ret_sum, float *ep_len_sum, void *stream)
+                           int32_t *ep_done_count, float *ep_ret_sum, float *ep_len_sum, const uint64_t *clock,
+                           void *stream)
 {
     GS_REQUIRE(N > 0 && obs_dim > 0 && episode_len > 0, "gs_env_step: bad shape");
     GS_REQUIRE(rewards_row && dones_row && timeouts_row, "gs_env_step: null output row");
     hipLaunchKernelGGL(k_env_step, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, state,
                        ep_ret, obs, N, obs_dim, episode_len, truncate_every, reward, seed, env_offset, step_count,
-                       rewards_row, dones_row, timeouts_row, ep_done_count, ep_ret_sum, ep_len_sum);
+                       rewards_row, dones_row, timeouts_row, ep_done_count, ep_ret_sum, ep_len_sum, clock);
     GS_LAUNCH_CHECK("k_env_step");
     return GS_OK;
 }

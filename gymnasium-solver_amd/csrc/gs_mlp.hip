@@ -295,6 +295,11 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
 #pragma unroll
         for (int j = 0; j < NS; ++j) sl[j] = tid + 256 * j < aa.n_slots ? ld1(af.sumsq, tid + 256 * j) : 0.0f;
         if (tid < kTile * cD) xs[tid] = xv;
+#ifdef GS_STAMPS
+        __builtin_amdgcn_s_waitcnt(0);     // diagnostic build only: split "loads landed" from the norm
+        __syncthreads();
+#endif
+        GS_STAMP(0)
         // global norm -> clip coefficient: the per-tile slots, then the folded dW1|db1 (k_clip_adam's order)
         float coef = 0.0f;
         float *w1g = h1s;      // dW1|db1: part1 order when folded here, else parameter order (h1s is unused until phase 1)
@@ -329,7 +334,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             coef = clip_coef(total, aa) * aa.grad_scale;
             if (own1 && tid == 0 && af.metrics) af.metrics[kprev * GS_NUM_METRICS + GS_M_GRAD_NORM] = total;
         }
-        GS_STAMP(0)
+        GS_STAMP(1)
         // Adam on the owned parameters: new values to LDS / registers, and from row block 0 to the other set
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         step_slice(shb, oh, own1);
         if (tid < kTile) b2s[tid] = sb[0];
         if (tid < cA1 * kTile) whs[tid] = sw[0];
-        GS_STAMP(1)
+        GS_STAMP(2)
     } else if constexpr (kStage0) {
         constexpr Layout Lc = S::lay(Layout{});
         constexpr int cD = Lc.D, cH1 = Lc.H1, cA1 = Lc.A + 1;
@@ -474,7 +479,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         }
     }
     __syncthreads();
-    GS_STAMP(2)
+    GS_STAMP(3)
     // ---- phase 1: h1 = relu(x W1^T + b1) out of LDS; one hidden unit per thread
     for (int k = tid; k < H1; k += 256) {
         float w[8];
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         }
     }
     __syncthreads();
-    GS_STAMP(3)
+    GS_STAMP(4)
     // ---- phase 2: h2 tile = h1[16 x H1] . W2[c0:c0+16, :]^T, MFMA, K split over 4 waves
     {
         const int i = lane & 15, q = lane >> 4;
@@ -535,7 +540,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         for (int r = 0; r < 4; ++r) red[wave * 256 + (q * 4 + r) * kTile + i] = acc[r];
     }
     __syncthreads();
-    GS_STAMP(4)
+    GS_STAMP(5)
     {
         const int row = tid >> 4, col = tid & 15;
         const float s = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
@@ -581,7 +586,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
         }
     }
-    GS_STAMP_END(5)
+    GS_STAMP_END(6)
 }
 
 static int set_lds_limit(const void *fn, size_t bytes);
@@ -717,7 +722,8 @@ template <class S>
 __global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, Layout Lrt,
                                                    const float *__restrict__ zpart, int64_t rows, int mode,
                                                    uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
-                                                   float *__restrict__ logp, float *__restrict__ value)
+                                                   float *__restrict__ logp, float *__restrict__ value,
+                                                   const uint64_t *__restrict__ clock)
 {
     constexpr int AMAX = S::AMAX, AEX = S::AEX;
     const Layout L = S::lay(Lrt);
@@ -747,7 +753,8 @@ __global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, 
         }
         actions[r] = act;
     } else {                    // inverse-CDF sample with a counter-based uniform
-        const uint64_t hh = mix64(mix64(mix64(seed) ^ counter) ^ (uint64_t)r);
+        const uint64_t ctr = counter + (clock ? clock[0] : 0ull);   // rollout clock (graph replay)
+        const uint64_t hh = mix64(mix64(mix64(seed) ^ ctr) ^ (uint64_t)r);
         const float u = (float)(hh >> 40) * (1.0f / 16777216.0f);
         float c = 0.0f;
         act = -1;
@@ -1927,12 +1934,13 @@ int prepare_kernels(const Layout &L, int64_t B)
 }
 
 int launch_heads_act(const float *P, const Layout &L, const float *zpart, int64_t rows, int mode, uint64_t seed,
-                     uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s)
+                     uint64_t counter, int64_t *actions, float *logp, float *value, hipStream_t s,
+                     const uint64_t *clock)
 {
     const dim3 grid((unsigned)((rows + 255) / 256));
     return with_shape(L, 0, [&](auto sh) {
         hipLaunchKernelGGL(k_heads_act<decltype(sh)>, grid, dim3(256), 0, s, P, L, zpart, rows, mode, seed, counter,
-                           actions, logp, value);
+                           actions, logp, value, clock);
         GS_LAUNCH_CHECK("k_heads_act");
         return GS_OK;
     });

@@ -94,7 +94,7 @@ extern "C" size_t gs_policy_scratch_bytes(gs_mlp_dims dims, int64_t N)
 
 extern "C" int gs_policy_act(const float *params, gs_mlp_dims dims, const float *obs, int64_t N, int mode,
                              uint64_t rng_seed, uint64_t rng_counter, int64_t *actions, float *logp, float *value,
-                             float *obs_store, void *scratch, void *stream)
+                             float *obs_store, void *scratch, const uint64_t *clock, void *stream)
 {
     int rc = check_dims(dims);
     if (rc) return rc;
@@ -108,7 +108,7 @@ extern "C" int gs_policy_act(const float *params, gs_mlp_dims dims, const float 
     rc = launch_fwd_hidden(params, L, obs, nullptr, 1, N, N, nullptr, nullptr, nullptr, zpart, obs_store, nullptr,
                            nullptr, s);
     if (rc) return rc;
-    return launch_heads_act(params, L, zpart, N, mode, rng_seed, rng_counter, actions, logp, value, s);
+    return launch_heads_act(params, L, zpart, N, mode, rng_seed, rng_counter, actions, logp, value, s, clock);
 }
 
 extern "C" int gs_policy_value(const float *params, gs_mlp_dims dims, const float *obs, int64_t N, float *value,

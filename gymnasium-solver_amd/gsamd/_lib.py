@@ -71,11 +71,11 @@ def _load():
         "gs_sampler_stream_i32": (ctypes.c_int, [i64, i64, u64, vp, ctypes.c_int]),
         "gs_mlp_param_count": (i64, [MlpDims]),
         "gs_policy_scratch_bytes": (sz, [MlpDims, i64]),
-        "gs_policy_act": (ctypes.c_int, [vp, MlpDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp]),
+        "gs_policy_act": (ctypes.c_int, [vp, MlpDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp, vp]),
         "gs_policy_value": (ctypes.c_int, [vp, MlpDims, vp, i64, vp, vp, vp]),
         "gs_env_reset": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, u64, i64, vp]),
         "gs_env_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, f32, u64, i64, u64, vp, vp, vp, vp, vp,
-                                       vp, vp]),
+                                       vp, vp, vp]),
         "gs_episode_stats": (ctypes.c_int, [vp, vp, i64, i64, vp, vp, vp, vp, vp]),
         "gs_ppo_workspace_bytes": (sz, [MlpDims, i64]),
         "gs_ppo_minibatch_step": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64,
@@ -89,7 +89,7 @@ def _load():
         "gs_ppo_graph_cache_info": (ctypes.c_int, [vp, vp]),
         "gs_cnn_param_count": (i64, [CnnDims]),
         "gs_cnn_workspace_bytes": (sz, [CnnDims, i64]),
-        "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp]),
+        "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp]),
         "gs_cnn_ppo_loss": (ctypes.c_int, [vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, vp, vp, vp, vp]),
         "gs_cnn_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, i64, i64,
                                              vp, vp, vp, vp, vp]),
@@ -101,7 +101,7 @@ def _load():
         "gs_atari_render": (ctypes.c_int, [vp, i64, u64, i64, u64, vp]),
         "gs_atari_env_reset": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, i32, i32, u64, i64, vp]),
         "gs_atari_env_step": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, i32, i32, i32, u64, i64, u64, vp, vp, vp,
-                                             vp, vp, vp, vp]),
+                                             vp, vp, vp, vp, vp]),
         "gs_comm_unique_id": (ctypes.c_int, [vp]),
         "gs_comm_init": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
         "gs_comm_xgmi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, vp, ctypes.POINTER(vp)]),

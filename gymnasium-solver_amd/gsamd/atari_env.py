@@ -45,13 +45,16 @@ class DeviceAtariVecEnv:
                                      self.seed, self.env_offset, stream_handle()), "gs_atari_env_reset")
         return self.obs, {}
 
-    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None):
-        self.step_count += 1
+    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None, clock=None, step=None):
+        """One vector step; clock/step as DeviceSyntheticVecEnv.step_into (captured rollouts)."""
+        if clock is None:
+            self.step_count += 1
         check(lib.gs_atari_env_step(ptr(self.state), ptr(self.ep_ret), ptr(self.obs), ptr(self.frames),
                                     self.num_envs, self.frame_stack, self.out_h, self.out_w, self.episode_len,
-                                    self.truncate_every, self.seed, self.env_offset, self.step_count,
-                                    ptr(rewards_row), ptr(dones_row), ptr(timeouts_row), ptr(self.ep_count),
-                                    ptr(self.ep_ret_sum), ptr(self.ep_len_sum), stream_handle()), "gs_atari_env_step")
+                                    self.truncate_every, self.seed, self.env_offset,
+                                    self.step_count if clock is None else int(step), ptr(rewards_row),
+                                    ptr(dones_row), ptr(timeouts_row), ptr(self.ep_count), ptr(self.ep_ret_sum),
+                                    ptr(self.ep_len_sum), ptr(clock), stream_handle()), "gs_atari_env_step")
 
 
 def atari_preprocess(frames: torch.Tensor, out_hw=(84, 84)) -> torch.Tensor:

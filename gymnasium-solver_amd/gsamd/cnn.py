@@ -164,7 +164,7 @@ class DeviceCNNActorCritic:
 
     def act(self, obs: torch.Tensor, *, mode: int = 0, rng_seed: int = 0, rng_counter: int = 0,
             actions: torch.Tensor = None, logp: torch.Tensor = None, values: torch.Tensor = None,
-            obs_store: torch.Tensor = None):
+            obs_store: torch.Tensor = None, clock: torch.Tensor = None):
         """policy_act (utils/policy_ops.py:14-34) on u8 frame stacks (N, C, H, W); obs_store
         (the rollout row) receives a copy of the observation."""
         n = obs.shape[0]
@@ -180,7 +180,7 @@ class DeviceCNNActorCritic:
             values = torch.empty(n, dtype=torch.float32, device=self.device)
         check(lib.gs_cnn_policy_act(ptr(self.params), self.dims, ptr(obs), n, int(mode), int(rng_seed),
                                     int(rng_counter), ptr(actions), ptr(logp), ptr(values), ptr(self.workspace(n)),
-                                    stream_handle()), "gs_cnn_policy_act")
+                                    ptr(clock), stream_handle()), "gs_cnn_policy_act")
         return actions, logp, values
 
     def predict_values(self, obs: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
@@ -188,7 +188,7 @@ class DeviceCNNActorCritic:
         if out is None:
             out = torch.empty(n, dtype=torch.float32, device=self.device)
         check(lib.gs_cnn_policy_act(ptr(self.params), self.dims, ptr(obs), n, 0, 0, 0, None, None, ptr(out),
-                                    ptr(self.workspace(n)), stream_handle()), "gs_cnn_policy_act")
+                                    ptr(self.workspace(n)), None, stream_handle()), "gs_cnn_policy_act")
         return out
 
     def parameters(self):

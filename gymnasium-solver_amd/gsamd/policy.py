@@ -118,8 +118,9 @@ class DeviceMLPActorCritic:
 
     def act(self, obs: torch.Tensor, *, mode: int = 0, rng_seed: int = 0, rng_counter: int = 0,
             actions: torch.Tensor = None, logp: torch.Tensor = None, values: torch.Tensor = None,
-            obs_store: torch.Tensor = None):
-        """policy_act (utils/policy_ops.py:14-34): returns (actions int64, logp, values)."""
+            obs_store: torch.Tensor = None, clock: torch.Tensor = None):
+        """policy_act (utils/policy_ops.py:14-34): returns (actions int64, logp, values).  clock:
+        optional (2,) uint64 device tensor whose [0] is added to rng_counter on device."""
         n = obs.shape[0]
         assert obs.is_contiguous() and obs.dtype == torch.float32 and obs.device == self.device
         if actions is None:
@@ -130,7 +131,7 @@ class DeviceMLPActorCritic:
             values = torch.empty(n, dtype=torch.float32, device=self.device)
         check(lib.gs_policy_act(ptr(self.params), self.dims, ptr(obs), n, int(mode), int(rng_seed),
                                 int(rng_counter), ptr(actions), ptr(logp), ptr(values), ptr(obs_store),
-                                ptr(self.scratch(n)), stream_handle()), "gs_policy_act")
+                                ptr(self.scratch(n)), ptr(clock), stream_handle()), "gs_policy_act")
         return actions, logp, values
 
     def predict_values(self, obs: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:

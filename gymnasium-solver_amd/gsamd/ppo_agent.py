@@ -118,7 +118,7 @@ class DevicePPOAgent:
         c = self.config
         self._rollout_collectors[stage] = DeviceRolloutCollector(
             self.get_env(stage), self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
-            rng_seed=c.seed + 7919 * self.rank, track_stats=self.track_stats)
+            rng_seed=c.seed + 7919 * self.rank, track_stats=self.track_stats, use_graph=self.use_graph)
 
     def get_rollout_collector(self, stage: str) -> DeviceRolloutCollector:
         if stage not in self._rollout_collectors and stage in ("val", "test"):

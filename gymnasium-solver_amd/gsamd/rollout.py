@@ -61,13 +61,16 @@ class DeviceSyntheticVecEnv:
                                self.episode_len, self.seed, self.env_offset, stream_handle()), "gs_env_reset")
         return self.obs, {}
 
-    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None):
-        self.step_count += 1
+    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None, clock=None, step=None):
+        """One vector step into the rollout rows.  clock/step: inside a captured rollout the
+        step count is clock[1] (device) + step instead of the host counter."""
+        if clock is None:
+            self.step_count += 1
         check(lib.gs_env_step(ptr(self.state), ptr(self.ep_ret), ptr(self.obs), self.num_envs, self.obs_dim,
                               self.episode_len, self.truncate_every, self.reward, self.seed, self.env_offset,
-                              self.step_count, ptr(rewards_row), ptr(dones_row), ptr(timeouts_row),
-                              ptr(self.ep_count), ptr(self.ep_ret_sum), ptr(self.ep_len_sum), stream_handle()),
-              "gs_env_step")
+                              self.step_count if clock is None else int(step), ptr(rewards_row), ptr(dones_row),
+                              ptr(timeouts_row), ptr(self.ep_count), ptr(self.ep_ret_sum), ptr(self.ep_len_sum),
+                              ptr(clock), stream_handle()), "gs_env_step")
 
 
 class DeviceCartPoleVecEnv:
@@ -96,7 +99,7 @@ class DeviceCartPoleVecEnv:
                                     self.seed, self.env_offset, stream_handle()), "gs_cartpole_reset")
         return self.obs, {}
 
-    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None):
+    def step_into(self, rewards_row, dones_row, timeouts_row, actions=None, clock=None, step=None):
         if actions is None:
             raise ValueError("CartPole dynamics need the step's actions")
         check(lib.gs_cartpole_step(ptr(self.state), ptr(self.meta), ptr(self.ep_ret), ptr(self.obs), ptr(actions),
@@ -213,7 +216,8 @@ class DeviceRolloutCollector:
     """RolloutCollector (utils/rollout_collector.py:22-777) for the device path."""
 
     def __init__(self, env, policy_model, n_steps, *, gamma: float = 0.99, gae_lambda: float = 0.95,
-                 stats_window_size: int = 100, rng_seed: int = 42, track_stats: bool = True, **kwargs):
+                 stats_window_size: int = 100, rng_seed: int = 42, track_stats: bool = True,
+                 use_graph: bool = True, **kwargs):
         self.env = env
         self.policy_model = policy_model
         self.n_steps = int(n_steps)
@@ -222,6 +226,12 @@ class DeviceRolloutCollector:
         self.device = policy_model.device
         self.rng_seed = int(rng_seed)
         self.track_stats = bool(track_stats)
+        # device envs: the T-step loop (policy act + env step per vector step) is captured once
+        # per sampling mode into a hipGraph and replayed; the per-rollout counters reach the
+        # kernels through a 2-word device clock (include/gsamd.h "Rollout clock")
+        self.use_graph = bool(use_graph)
+        self._graphs = {}
+        self._clock = None
         self.total_rollouts = self.total_steps = self.total_vec_steps = self.total_episodes = 0
         self.rollout_steps = self.rollout_vec_steps = self.rollout_episodes = 0
         self.stats_window_size = int(stats_window_size)
@@ -289,6 +299,9 @@ class DeviceRolloutCollector:
         mode = 2 if replay_actions is not None else (1 if deterministic else 0)
         native = getattr(self.env, "device_native", False)
         self.rollout_episodes = 0
+        if native and replay_actions is None and self.use_graph:
+            self._collect_steps_graph(mode)
+            T = 0                               # the steps ran inside the graph
         for t in range(T):
             if replay_actions is not None:
                 buf.actions[t].copy_(replay_actions[t])
@@ -309,6 +322,7 @@ class DeviceRolloutCollector:
                 buf.timeouts[t].copy_(torch.from_numpy(np.asarray(trunc).astype(np.uint8)))
                 self._host_episode_infos(done, np.asarray(trunc, bool), infos)
                 self._host_obs = np.asarray(next_obs, dtype=self._host_obs.dtype)
+        T = self.n_steps
         last_obs = self.env.obs if native else self._obs_dev.copy_(torch.from_numpy(self._host_obs))
         pm.predict_values(last_obs, out=buf.last_values)
         compute_batched_gae_advantages_and_returns(buf.values, buf.rewards, buf.dones, buf.timeouts,
@@ -326,6 +340,41 @@ class DeviceRolloutCollector:
             self.total_episodes += self.rollout_episodes
         self.rollout_fpss.append(N * T / max(time.time() - t0, 1e-9))
         return DeviceTrajectory(buf)
+
+    def _steps_into_buffer(self, mode, clock=None):
+        """The rollout's T vector steps on a device env: policy act (writes the step's obs /
+        action / log-prob / value rows) then the env step (reward / done / timeout rows)."""
+        buf, pm, env = self._buffer, self.policy_model, self.env
+        for t in range(self.n_steps):
+            pm.act(env.obs, mode=mode, rng_seed=self.rng_seed, rng_counter=t if clock is not None else
+                   self.total_vec_steps + t, actions=buf.actions[t], logp=buf.logprobs[t], values=buf.values[t],
+                   obs_store=buf.obs[t], clock=clock)
+            env.step_into(buf.rewards[t], buf.dones[t], buf.timeouts[t], actions=buf.actions[t], clock=clock,
+                          step=t + 1)
+
+    def _collect_steps_graph(self, mode):
+        """Replay the captured T-step graph of this sampling mode (captured on the mode's second
+        rollout; the first runs eagerly and allocates every scratch buffer the steps use).  The
+        clock holds {rng counter, env step count} at the rollout start."""
+        env = self.env
+        if self._clock is None:
+            self._clock = torch.zeros(2, dtype=torch.int64, device=self.device)
+        step0 = int(getattr(env, "step_count", 0))
+        g = self._graphs.get(mode)
+        if g is None and (mode, "warm") not in self._graphs:
+            self._graphs[(mode, "warm")] = True
+            self._steps_into_buffer(mode)                       # eager, host counters
+            return
+        self._clock[0:1].fill_(self.total_vec_steps)
+        self._clock[1:2].fill_(step0)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._steps_into_buffer(mode, clock=self._clock)
+            self._graphs[mode] = g
+        g.replay()
+        if hasattr(env, "step_count"):
+            env.step_count = step0 + self.n_steps
 
     def _record_episode(self, env: int, ret: float, length: int, timeout: bool) -> None:
         """One finished episode, as _process_done_infos books it (rollout_collector.py:242-294)."""

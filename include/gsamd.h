@@ -77,6 +77,11 @@ typedef struct gs_mlp_dims {
 
 int64_t gs_mlp_param_count(gs_mlp_dims dims);
 
+/* Rollout clock (clock_dev, optional, 2 x uint64 in HBM): {rng counter base, env step base}.
+ * When non-NULL the kernels add clock_dev[0] to rng_counter and clock_dev[1] to step_count, so
+ * a captured T-step rollout graph replays with the next rollout's counters written into the
+ * clock (one 16-byte copy) instead of re-capturing; NULL = the counters as passed. */
+
 /* Policy forward for a rollout step — replaces utils/policy_ops.py:14-34 (policy_act)
  * on MLPActorCritic.forward (utils/models.py:328-346) + Categorical sample / mode /
  * log_prob.  obs_dev (N, D) f32.  mode: 0 = sample (counter-based RNG, key
@@ -88,7 +93,8 @@ int64_t gs_mlp_param_count(gs_mlp_dims dims);
 size_t gs_policy_scratch_bytes(gs_mlp_dims dims, int64_t N);
 int gs_policy_act(const float *params_dev, gs_mlp_dims dims, const float *obs_dev, int64_t N, int mode,
                   uint64_t rng_seed, uint64_t rng_counter, int64_t *actions_dev, float *logp_dev,
-                  float *value_dev, float *obs_store_dev, void *scratch_dev, void *stream);
+                  float *value_dev, float *obs_store_dev, void *scratch_dev, const uint64_t *clock_dev,
+                  void *stream);
 
 /* Value-only forward (utils/policy_ops.py:37-42 policy_predict_values), e.g. the
  * bootstrap value of the last observation (utils/rollout_collector.py:373). */
@@ -107,7 +113,7 @@ int gs_env_step(int32_t *state_dev, float *ep_ret_dev, float *obs_dev, int64_t N
                 int32_t episode_len, int32_t truncate_every, float reward, uint64_t seed,
                 int64_t env_offset, uint64_t step_count, float *rewards_row_dev, uint8_t *dones_row_dev,
                 uint8_t *timeouts_row_dev, int32_t *ep_done_count_dev, float *ep_ret_sum_dev,
-                float *ep_len_sum_dev, void *stream);
+                float *ep_len_sum_dev, const uint64_t *clock_dev, void *stream);
 
 /* Completed-episode records of a (T, N) rollout, for the collector's episode statistics
  * (utils/rollout_collector.py:210-294 _process_done_infos, :686-760 get_metrics): per env the
@@ -254,7 +260,7 @@ size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows);
  * 2 replay (as gs_policy_act); masked actions are never drawn. */
 int gs_cnn_policy_act(const float *params_dev, gs_cnn_dims dims, const uint8_t *obs_dev, int64_t N, int mode,
                       uint64_t rng_seed, uint64_t rng_counter, int64_t *actions_dev, float *logp_dev,
-                      float *value_dev, void *workspace_dev, void *stream);
+                      float *value_dev, void *workspace_dev, const uint64_t *clock_dev, void *stream);
 /* losses_for_batch on one minibatch: metrics record + (optional) dLoss/dlogits (B, A+1). */
 int gs_cnn_ppo_loss(const float *params_dev, gs_cnn_dims dims, gs_ppo_hparams hp, gs_rollout_view_u8 rollout,
                     const int32_t *idx_dev, int64_t batch, float *metrics_dev, float *dlogits_dev,
@@ -305,7 +311,7 @@ int gs_atari_env_step(int32_t *state_dev, float *ep_ret_dev, uint8_t *stack_dev,
                       int32_t stack_n, int32_t out_h, int32_t out_w, int32_t episode_len, int32_t truncate_every,
                       uint64_t seed, int64_t env_offset, uint64_t step_count, float *rewards_row_dev,
                       uint8_t *dones_row_dev, uint8_t *timeouts_row_dev, int32_t *ep_done_count_dev,
-                      float *ep_ret_sum_dev, float *ep_len_sum_dev, void *stream);
+                      float *ep_ret_sum_dev, float *ep_len_sum_dev, const uint64_t *clock_dev, void *stream);
 
 /* ---------------------------------------------------------------- multi-GPU (xGMI / RCCL)
  * One process per GPU; replaces the reference's single-process gradient step

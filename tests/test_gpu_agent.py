@@ -140,6 +140,7 @@ def test_scheduled_lr_reuses_the_update_graph(cuda):
                                    "end": 1.0, "warmup": 0.0}}
     agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
     agent.train_epoch()
+    agent.train_epoch()        # the rollout graph is captured on the second rollout
     torch.cuda.synchronize()
     n0, c0 = info()
     mem0 = torch.cuda.memory_allocated()
@@ -157,3 +158,42 @@ def test_scheduled_lr_reuses_the_update_graph(cuda):
     torch.cuda.synchronize()
     assert info() == (n0, c0 + 1)
     assert np.isfinite(agent.minibatch_losses()).all()
+
+
+@pytest.mark.parametrize("env,variant,over", [
+    ("CartPole-v1", "ppo", dict(n_envs=256)),
+    ("CartPole-v1", "ppo", dict(n_envs=128, env_dynamics="cartpole")),
+    ("LunarLander-v3", "ppo", dict(n_envs=64, n_steps=256, batch_size=64)),
+    ("ALE-Breakout-v5", "rgb_ppo", dict(n_envs=8, n_steps=16, batch_size=64, n_epochs=1))])
+def test_rollout_graph_equals_eager(cuda, env, variant, over):
+    """The captured T-step rollout (policy act + env step per vector step, replayed with the
+    rollout clock) writes bit for bit the rollout of the eager per-step launches — sampled and
+    deterministic actions, over several rollouts, between updates that move the weights."""
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    runs = []
+    for use_graph in (False, True):
+        torch.manual_seed(42)
+        cfg = load_config(env, variant, overrides=over)
+        agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=True)
+        coll = agent.get_rollout_collector("train")
+        rec = []
+        for k in range(4):
+            agent.train_epoch()
+            b = coll.buffer
+            rec.append([t.clone() for t in (b.obs, b.actions, b.logprobs, b.values, b.rewards, b.dones, b.timeouts,
+                                            b.advantages, b.returns)])
+        coll.collect(deterministic=True)
+        coll.collect(deterministic=True)
+        rec.append([coll.buffer.actions.clone(), coll.buffer.values.clone()])
+        torch.cuda.synchronize()
+        runs.append((rec, coll.get_metrics(), coll.total_vec_steps))
+        assert (coll._graphs.get(0) is not None) == use_graph
+        del agent
+    (r0, m0, n0), (r1, m1, n1) = runs
+    assert n0 == n1
+    for k, (a, b) in enumerate(zip(r0, r1)):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), k
+    assert m0["cnt/total_episodes"] == m1["cnt/total_episodes"]
+    assert m0.get("roll/ep_rew/mean") == m1.get("roll/ep_rew/mean")

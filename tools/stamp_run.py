@@ -40,8 +40,9 @@ cnt = np.zeros(8, np.uint64)
 _lib.lib.gs_debug_stamps(acc.ctypes.data, cnt.ctypes.data)
 acc = (acc - acc0).reshape(8, 16).astype(np.float64)
 cnt = (cnt - cnt0).astype(np.float64)
-names = {0: ("k_fwd_hidden<fused, adam> (0,0)", ["loads + W1 fold + norm", "adam (W1, W2 rows, slices)",
-                                                  "operands in LDS", "h1", "mfma h2", "h2 out + heads"]),
+names = {0: ("k_fwd_hidden<fused, adam> (0,0)", ["loads landed (waitcnt: stamp build only)", "W1 fold + norm",
+                                                  "adam (W1, W2 rows, slices)", "operands in LDS", "h1", "mfma h2",
+                                                  "h2 out + heads"]),
          1: ("k_loss", ["inputs + adv norm", "per-row loss/grad", "reduce", "metrics"]),
          2: ("k_bwd roleA blk0", ["load tiles", "dh2", "mfma dW2", "store + sumsq + db2"]),
          3: ("k_clip_adam blk0", ["own loads + LDS staging", "W1 fold + norm loops", "reduce", "adam"]),
