@@ -18,10 +18,13 @@ namespace gs {
 constexpr int kXgmiMaxRanks = 8;       // one node: 8 MI355X on xGMI
 constexpr int kXgmiMaxWG = 256;        // exchange workgroups: <= one per CU, all co-resident
 constexpr int kXgmiChunk = 1024;       // floats per workgroup chunk (4 per thread)
-// exchange region layout (bytes): flags[src][wg] | err | data[parity][src][cap]
+// exchange region layout (bytes): flags[src][wg] | flags2[src][wg] | err | data[parity][src][cap]
+// | res[parity][cap] | resq[parity][cap / kXgmiChunk]  (res / resq: the reduce-scatter +
+// all-gather form's owner results and per-chunk sums of squares)
 constexpr size_t kXgmiOffFlags = 0;
-constexpr size_t kXgmiOffErr = kXgmiOffFlags + sizeof(uint32_t) * kXgmiMaxRanks * kXgmiMaxWG;
-constexpr size_t kXgmiOffData = 16384;
+constexpr size_t kXgmiOffFlags2 = kXgmiOffFlags + sizeof(uint32_t) * kXgmiMaxRanks * kXgmiMaxWG;
+constexpr size_t kXgmiOffErr = kXgmiOffFlags2 + sizeof(uint32_t) * kXgmiMaxRanks * kXgmiMaxWG;
+constexpr size_t kXgmiOffData = kXgmiOffErr + 4096;
 
 enum CommKind { kCommRccl = 0, kCommXgmi = 1 };
 
@@ -47,6 +50,7 @@ struct gs_comm {
     bool connected;
     uint32_t *seq;                                // per-workgroup exchange counters (local, cached)
     uint64_t timeout_ticks;                       // spin limit, s_memrealtime ticks (100 MHz)
+    int rsag;                                     // 1: reduce-scatter + all-gather form (>= 4 ranks)
 };
 
 namespace gs {

@@ -487,7 +487,32 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
 #pragma unroll
         for (int d = 0; d < 8; ++d) w[d] = (small && d < D) ? W1s[k * D + d] : 0.0f;
         const float bk = b1s[k];
-        if (small) {
+        if (small && D % 4 == 0) {
+            // every x row first (float4 LDS reads; xs is 16-B aligned), then the 16 outputs: the
+            // h1s stores may alias xs as far as the compiler knows, so reads interleaved with them
+            // would each wait for the LDS round trip
+            float4 xq[kTile][2];
+#pragma unroll
+            for (int i = 0; i < kTile; ++i)
+#pragma unroll
+                for (int d4 = 0; d4 < 2; ++d4)
+                    xq[i][d4] = 4 * d4 < D ? reinterpret_cast<const float4 *>(xs + i * D)[d4]
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            float hv[kTile];
+#pragma unroll
+            for (int i = 0; i < kTile; ++i) {
+                const float xr[8] = {xq[i][0].x, xq[i][0].y, xq[i][0].z, xq[i][0].w,
+                                     xq[i][1].x, xq[i][1].y, xq[i][1].z, xq[i][1].w};
+                float acc = 0.0f;
+#pragma unroll
+                for (int d = 0; d < 8; ++d)
+                    if (d < D) acc = fmaf(xr[d], w[d], acc);
+                acc += bk;
+                hv[i] = acc > 0.0f ? acc : 0.0f;
+            }
+#pragma unroll
+            for (int i = 0; i < kTile; ++i) h1s[i * ldh + k] = hv[i];
+        } else if (small) {
 #pragma unroll
             for (int i = 0; i < kTile; ++i) {
                 float xr[8];

@@ -219,6 +219,147 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Pa
     }
 }
 
+// ---- the reduce-scatter + all-gather form (>= 4 ranks) --------------------------------
+// The one-shot form sends the whole gradient over every link (n floats per link); here chunk c
+// belongs to rank c mod world: every rank pushes its chunk c to that owner only (phase 1), the
+// owner sums the sources in rank order, forms the chunk's sum of squares and pushes the result to
+// every rank (phase 2), every rank then reads all results (phase 3) — 2n/world floats per link
+// for one more flag round trip.  Bitwise identical results on every rank; per-chunk sums of
+// squares are added in chunk order, so every rank also gets the same norm partials.
+
+__device__ __forceinline__ float *res_slot(char *region, int par, int world, int64_t cap)
+{
+    return reinterpret_cast<float *>(region + kXgmiOffData) + ((int64_t)2 * world + par) * cap;
+}
+
+__device__ __forceinline__ float *resq_slot(char *region, int par, int world, int64_t cap)
+{
+    return reinterpret_cast<float *>(region + kXgmiOffData) + (int64_t)2 * (world + 1) * cap +
+           (int64_t)par * (cap / kXgmiChunk);
+}
+
+// raise flag word `off`[src = rank][w] = value in every other rank's region (after this
+// workgroup's stores drained: the caller's s_waitcnt + barrier)
+__device__ __forceinline__ void raise_flags(const XgmiArgs &xa, size_t off, int w, uint32_t value)
+{
+    const int tid = threadIdx.x;
+    if (tid < xa.world && tid != xa.rank) {
+        uint32_t *f = reinterpret_cast<uint32_t *>(xa.peer[tid] + off) + xa.rank * kXgmiMaxWG + w;
+        __hip_atomic_store(f, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// wait until flag word `off`[src][w] of the own region reaches seq for every other src (bounded:
+// a dead peer sets the sticky error); returns the OR of the sources' stop bits (bit 0)
+__device__ __forceinline__ int wait_flags(const XgmiArgs &xa, size_t off, int w, uint32_t seq, uint32_t *err)
+{
+    const int tid = threadIdx.x;
+    int anystop = 0;
+    if (tid < xa.world && tid != xa.rank) {
+        const uint32_t *f = reinterpret_cast<const uint32_t *>(xa.peer[xa.rank] + off) + tid * kXgmiMaxWG + w;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+        while (!failed) {
+            const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((v >> 1) >= seq) {
+                anystop = (int)(v & 1u);
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout) {
+                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                failed = true;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return __syncthreads_or(anystop);
+}
+
+__global__ __launch_bounds__(256) void k_xgmi_rsag(float *__restrict__ G, Part1Fold fold, XgmiArgs xa,
+                                                   float *__restrict__ sumsq, int32_t *__restrict__ stop)
+{
+    __shared__ float s_red[4];
+    const int w = blockIdx.x, tid = threadIdx.x;
+    char *me = xa.peer[xa.rank];
+    uint32_t *err = reinterpret_cast<uint32_t *>(me + kXgmiOffErr);
+    const uint32_t seq = xa.seq[w] + 1u;
+    const int par = (int)(seq & 1u);
+    const uint32_t mystop = (stop && *stop) ? 1u : 0u;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(me, 0, xa.region_bytes, 0x00020000);
+    const uint32_t res0 = (uint32_t)((char *)res_slot(me, par, xa.world, xa.cap) - me);
+    const uint32_t resq0 = (uint32_t)((char *)resq_slot(me, par, xa.world, xa.cap) - me);
+
+    // 1. reduce-scatter: chunk c to its owner's slot [par][rank]
+    for (int c = w; c < xa.nchunks; c += gridDim.x) {
+        const int o = c % xa.world;
+        if (o == xa.rank) continue;
+        const int64_t p = (int64_t)c * kXgmiChunk + tid * 4;
+        const float4 v = own_values(G, fold, xa.n, p);
+        store_system(slot(xa.peer[o], par, xa.world, xa.rank, xa.cap) + p, f4{v.x, v.y, v.z, v.w});
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    raise_flags(xa, kXgmiOffFlags, w, (seq << 1) | mystop);
+    const int anystop = wait_flags(xa, kXgmiOffFlags, w, seq, err) | (int)mystop;
+
+    // 2. owned chunks: fixed-order sum, sum of squares, result to every rank (self included)
+    for (int c = w; c < xa.nchunks; c += gridDim.x) {
+        if (c % xa.world != xa.rank) continue;
+        const int64_t p = (int64_t)c * kXgmiChunk + tid * 4;
+        const float4 own = own_values(G, fold, xa.n, p);
+        float4 a = xa.rank == 0 ? own
+                                : load_sc1(rs, (uint32_t)(kXgmiOffData + 4 * ((int64_t)par * xa.world * xa.cap + p)));
+        for (int r = 1; r < xa.world; ++r) {
+            const float4 b = r == xa.rank ? own : load_sc1(rs, (uint32_t)(kXgmiOffData +
+                                                                          4 * (((int64_t)par * xa.world + r) * xa.cap + p)));
+            a.x += b.x;
+            a.y += b.y;
+            a.z += b.z;
+            a.w += b.w;
+        }
+        a.x *= xa.scale;
+        a.y *= xa.scale;
+        a.z *= xa.scale;
+        a.w *= xa.scale;
+        float ss = a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;     // lanes past n hold zeros
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+        if ((tid & 63) == 0) s_red[tid >> 6] = ss;
+        __syncthreads();
+        const float q = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        __syncthreads();
+        for (int r = 0; r < xa.world; ++r) {
+            store_system(res_slot(xa.peer[r], par, xa.world, xa.cap) + p, f4{a.x, a.y, a.z, a.w});
+            if (tid == 0)     // one word, written through (system-scope dword store)
+                __hip_atomic_store(reinterpret_cast<uint32_t *>(resq_slot(xa.peer[r], par, xa.world, xa.cap) + c),
+                                   __float_as_uint(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    raise_flags(xa, kXgmiOffFlags2, w, seq << 1);
+    (void)wait_flags(xa, kXgmiOffFlags2, w, seq, err);
+
+    // 3. all-gather: every chunk's result and sum of squares (in chunk order) from the own region
+    float ssum = 0.0f;
+    for (int c = w; c < xa.nchunks; c += gridDim.x) {
+        const int64_t p = (int64_t)c * kXgmiChunk + tid * 4;
+        const float4 a = load_sc1(rs, res0 + (uint32_t)(4 * p));
+        if (p + 3 < xa.n) {
+            *reinterpret_cast<float4 *>(G + p) = a;
+        } else {
+            if (p + 0 < xa.n) G[p + 0] = a.x;
+            if (p + 1 < xa.n) G[p + 1] = a.y;
+            if (p + 2 < xa.n) G[p + 2] = a.z;
+        }
+        if (tid == 0) ssum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(resq0 + 4 * c), 0, 16));
+    }
+    if (tid == 0) {
+        if (sumsq) sumsq[w] = ssum;
+        if (w == 0 && stop && anystop) *stop = 1;
+        xa.seq[w] = seq;
+    }
+}
+
 }  // namespace
 
 static int nwg_of(const gs_comm *c) { return (int)std::min<int64_t>(c->cap / kXgmiChunk, kXgmiMaxWG); }
@@ -242,8 +383,13 @@ int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float 
     xa.timeout = c->timeout_ticks;
     xa.seq = c->seq;
     const int nwg = nwg_of(c);
-    hipLaunchKernelGGL(k_xgmi_exchange, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
-    GS_LAUNCH_CHECK("k_xgmi_exchange");
+    if (c->rsag && c->nranks > 1) {
+        hipLaunchKernelGGL(k_xgmi_rsag, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
+        GS_LAUNCH_CHECK("k_xgmi_rsag");
+    } else {
+        hipLaunchKernelGGL(k_xgmi_exchange, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
+        GS_LAUNCH_CHECK("k_xgmi_exchange");
+    }
     if (n_slots) *n_slots = nwg;
     return GS_OK;
 }
@@ -278,7 +424,8 @@ extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint
                (long long)max_count);
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is 64 bytes");
     const int64_t cap = (max_count + kXgmiChunk - 1) / kXgmiChunk * kXgmiChunk;
-    const size_t bytes = kXgmiOffData + sizeof(float) * 2 * (size_t)nranks * (size_t)cap;
+    const size_t bytes = kXgmiOffData + sizeof(float) * (2 * (size_t)nranks * (size_t)cap + 2 * (size_t)cap +
+                                                         2 * (size_t)(cap / kXgmiChunk));
     GS_REQUIRE(bytes < ((size_t)1 << 31), "gs_comm_xgmi_create: %lld floats x %d ranks exceed the 2 GiB region limit",
                (long long)max_count, nranks);
     void *p = nullptr;
@@ -310,6 +457,10 @@ extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint
         return hip_fail(e, "xGMI sequence counters", __FILE__, __LINE__);
     }
     c->seq = (uint32_t *)sq;
+    // reduce-scatter + all-gather from 4 ranks on (2n/world floats per link instead of n, one more
+    // flag round trip); GS_XGMI_ALGO=oneshot|rsag overrides
+    c->rsag = nranks >= 4 ? 1 : 0;
+    if (const char *a = getenv("GS_XGMI_ALGO")) c->rsag = strcmp(a, "rsag") == 0 ? 1 : strcmp(a, "oneshot") == 0 ? 0 : c->rsag;
     double secs = 120.0;
     if (const char *env = getenv("GS_XGMI_TIMEOUT_S")) secs = atof(env);
     c->timeout_ticks = (uint64_t)(secs > 0 ? secs * 1e8 : 1.2e10);   // s_memrealtime: 100 MHz

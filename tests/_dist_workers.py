@@ -143,10 +143,13 @@ def exchange_values(rank, it, n):
     return (rng.standard_normal(n) * np.exp(rng.uniform(-6, 6, n))).astype(np.float32)
 
 
-def xgmi_exchange_worker(rank, world, port, result_dir, n, iters):
+def xgmi_exchange_worker(rank, world, port, result_dir, n, iters, algo=""):
     """Back-to-back exchanges with no host sync in between (both parity slots reused many
-    times), then the device result of every iteration is saved for the parent."""
+    times), then the device result of every iteration is saved for the parent.  algo forces
+    the exchange form (oneshot | rsag; default by rank count)."""
     os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    if algo:
+        os.environ["GS_XGMI_ALGO"] = algo
     dist = _init(rank, world, port)
     try:
         import torch
@@ -170,7 +173,7 @@ def xgmi_exchange_worker(rank, world, port, result_dir, n, iters):
         dist.destroy_process_group()
 
 
-def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", workload="mlp"):
+def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", workload="mlp", algo=""):
     """Data-parallel PPO update over the xGMI transport: rank-sharded envs, one rollout and
     2 epochs; every rank saves its final parameters and per-minibatch losses.  lagged="0"
     selects the chain with a separate clip + Adam launch after each exchange.  workload="cnn":
@@ -178,6 +181,8 @@ def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", worklo
     32-step rollout, so the 1.69 M-float gradient exchange runs 16 times."""
     os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
     os.environ["GS_LAGGED_ADAM"] = lagged
+    if algo:
+        os.environ["GS_XGMI_ALGO"] = algo
     dist = _init(rank, world, port)
     try:
         import torch

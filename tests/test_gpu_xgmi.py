@@ -1,4 +1,5 @@
-"""GPU: the one-shot xGMI gradient exchange (csrc/gs_xgmi.hip) with 2 and 4 ranks.  The box
+"""GPU: the xGMI gradient exchange (csrc/gs_xgmi.hip: one-shot and reduce-scatter + all-gather
+forms) with 2 to 4 ranks.  The box
 has one MI355X, so every rank runs on cuda:0 and the peers' regions are opened through the
 same IPC path the ranks of an 8-GPU node use; the cross-device link itself is
 exercised only by the driver's multi-GPU bench.
@@ -41,11 +42,15 @@ def _run(target, world, tmp_path, *args, timeout=300):
 
 
 # 67 651: an MLP-sized vector with an odd tail; 1 693 875: the NatureCNN's parameter count —
-# more chunks than the exchange has workgroups, so each workgroup loops over several chunks
-@pytest.mark.parametrize("world,n,iters", [(2, 67_651, 24), (4, 67_651, 24), (2, 1_693_875, 6)])
-def test_xgmi_exchange_bit_exact(tmp_path, world, n, iters):
+# more chunks than the exchange has workgroups, so each workgroup loops over several chunks.
+# algo: the one-shot form (default below 4 ranks) and the reduce-scatter + all-gather form
+# (default from 4 ranks), each at 2 and 4 ranks
+@pytest.mark.parametrize("world,n,iters,algo", [(2, 67_651, 24, ""), (4, 67_651, 24, ""), (2, 1_693_875, 6, ""),
+                                                 (2, 67_651, 24, "rsag"), (4, 67_651, 24, "oneshot"),
+                                                 (3, 1_693_875, 6, "rsag")])
+def test_xgmi_exchange_bit_exact(tmp_path, world, n, iters, algo):
     from _dist_workers import exchange_values, xgmi_exchange_worker
-    _run(xgmi_exchange_worker, world, tmp_path, n, iters)
+    _run(xgmi_exchange_worker, world, tmp_path, n, iters, algo)
     outs = [np.load(tmp_path / f"x{r}.npy") for r in range(world)]
     for it in range(iters):
         acc = exchange_values(0, it, n)
@@ -79,6 +84,18 @@ def test_xgmi_cnn_data_parallel_replicas_identical(tmp_path):
     assert p[0].size == 1_693_875 and np.isfinite(p[0]).all()
     assert np.array_equal(p[0].view(np.uint32), p[1].view(np.uint32)), "replicas diverged"
     assert not np.array_equal(losses[0], losses[1])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_rsag_ppo_replicas_identical(tmp_path, world):
+    """The reduce-scatter + all-gather exchange carrying the lagged data-parallel PPO update:
+    replicas end bitwise identical (2 ranks forced, 4 ranks by default)."""
+    from _dist_workers import xgmi_ppo_worker
+    _run(xgmi_ppo_worker, world, tmp_path, True, "1", "mlp", "rsag", timeout=400)
+    p = [np.load(tmp_path / f"p{r}.npy") for r in range(world)]
+    assert np.isfinite(p[0]).all()
+    for r in range(1, world):
+        assert np.array_equal(p[0].view(np.uint32), p[r].view(np.uint32)), f"rank {r} diverged"
 
 
 def test_xgmi_lagged_chain_equals_separate_chain(tmp_path):
