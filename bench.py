@@ -69,6 +69,17 @@ def stage_flops_bytes(D, H1, H2, A, B, P, fused=True):
     return {"fwd": ("mfma", fwd), "loss": ("mfma", loss), "bwd": ("mfma", bwd), "adam": ("hbm", adam_bytes)}
 
 
+def fwd_adam_hbm_bytes(D, H1, H2, A, B, P):
+    """Algorithmic HBM bytes of one lagged forward (k_fwd_hidden<fused, adam>): the clip + Adam
+    of the previous step (read p, g, m, v; write p, m, v: 28 B/param) + the dW1|db1 partials
+    folded on the way (8 row blocks x H1(D+1) floats) + this minibatch's x rows, and the
+    activations it writes for the backward (h1, h2, per-column-block head partials, relu' bits)."""
+    nrb = (B + 31) // 32
+    adam = 28.0 * P + 4.0 * nrb * H1 * (D + 1)
+    acts = 4.0 * B * D + 4.0 * B * (H1 + H2) + 4.0 * (H2 // 16) * B * (A + 1) + 2.0 * B * (H2 // 16)
+    return adam + acts
+
+
 def time_stages(agent, reps: int):
     """Average device duration of each minibatch-step kernel: `reps` launches of one stage
     captured into a hipGraph (no host launch gaps) and replayed between HIP events recorded on
@@ -375,6 +386,16 @@ def main():
         kname = {"fwd": "k_fwd_hidden", "fwd_adam": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}
         for st, us in stage_us.items():
             rooflines[st] = roofline_entry(work[st][0], work[st][1], us, kname[st])
+        if "fwd_adam" in rooflines:
+            # the lagged forward also streams the previous step's clip + Adam (28 B/param) and
+            # writes the activations the backward reads: its HBM term beside the MFMA one; the
+            # two fractions add (time shares of one launch)
+            hb = fwd_adam_hbm_bytes(pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions, agent.batch_size,
+                                    pm.n_params)
+            h = roofline_entry("hbm", hb, stage_us["fwd_adam"], "k_fwd_hidden")
+            e = rooflines["fwd_adam"]
+            e["hbm_term"] = {k: h[k] for k in ("achieved", "peak", "unit", "frac", "work_per_launch")}
+            e["combined_frac"] = round(e["frac"] + h["frac"], 6)
         roofline = {k: v for k, v in rooflines[dom].items()}
         roofline["traffic"] = None
     # GAE scan on this workload's rollout buffer (HBM-bound; 22 B/element + 4 B/env)

@@ -1281,7 +1281,18 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
     if (bid < sh.nB) {
         // ---------------- role B: dh1 slab rows b0..b0+64, cols k0..k0+16 (K = H2);
         //                  wave w owns rows b0+16w .. b0+16w+15 with the full K
-        const int rb = bid / sh.nkb, kb = bid - rb * sh.nkb;
+        // XCD-aware order (blocks b and b + 8 share an XCD): with 16 k-blocks and 8 role-A k-block
+        // pairs, the role-B workgroups of XCD x take k-blocks 2x, 2x+1 — the h1 columns the role-A
+        // workgroups on that XCD read — so each XCD's L2 fetches one h1 column slab, not two
+        int rb, kb;
+        if (sh.nkb == 16 && sh.ka == 2 && sh.nB % 8 == 0) {
+            const int x = bid & 7, i = bid >> 3;
+            kb = 2 * x + (i & 1);
+            rb = i >> 1;
+        } else {
+            rb = bid / sh.nkb;
+            kb = bid - rb * sh.nkb;
+        }
         const int b0 = rb * kRowsB, k0 = kb * kTile;
         GS_STAMP_BEGIN_IF(4, bid == 0)
         const int H2p = (H2 + 63) / 64 * 64;
