@@ -403,8 +403,14 @@ def main():
     rooflines["gae"] = roofline_entry("hbm", 22.0 * gT * gN + 4.0 * gN, gae_us,
                                       "k_gae_staged" if gN % 4 == 0 else "k_gae_f32")
     rooflines["gae"]["shape"] = [gT, gN]
+    in_bwd = None
     if comm is not None:       # every rank takes part (the exchange is collective)
-        stage_us["exchange"] = time_exchange(comm, pm.n_params, args.stage_reps, device, barrier)
+        if not pixel:
+            from gsamd.distributed import exchange_inside_bwd
+            in_bwd = exchange_inside_bwd(comm, pm.dims, cfg.batch_size)
+        # the exchange as its own launch (what the chain runs after k_bwd unless in_bwd)
+        stage_us["exchange_launch" if in_bwd else "exchange"] = time_exchange(comm, pm.n_params, args.stage_reps,
+                                                                               device, barrier)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
@@ -473,6 +479,7 @@ def main():
                                   f"MLP {pm.obs_dim}-{pm.hidden_dims[0]}-{pm.hidden_dims[1]}-{{{pm.n_actions},1}}"),
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph,
                        "grad_exchange": args.comm if comm is not None else None,
+                       "exchange_in_bwd": in_bwd,
                        "comm": comm_info, "same_device": bool(args.same_device)},
             "roofline": roofline,
             "rooflines": rooflines,

@@ -16,6 +16,7 @@
 namespace gs {
 
 constexpr int kXgmiMaxRanks = 8;       // one node: 8 MI355X on xGMI
+static_assert(kXgmiMaxRanks == kBwdXMaxRanks, "one rank limit for both exchanges");
 constexpr int kXgmiMaxWG = 256;        // exchange workgroups: <= one per CU, all co-resident
 constexpr int kXgmiChunk = 1024;       // floats per workgroup chunk (4 per thread)
 // exchange region layout (bytes): flags[src][wg] | flags2[src][wg] | err | data[parity][src][cap]
@@ -51,6 +52,12 @@ struct gs_comm {
     uint32_t *seq;                                // per-workgroup exchange counters (local, cached)
     uint64_t timeout_ticks;                       // spin limit, s_memrealtime ticks (100 MHz)
     int rsag;                                     // 1: reduce-scatter + all-gather form (>= 4 ranks)
+    // the exchange inside the MLP backward (nranks > 1): flags1 | flags2 | data | res at
+    // off_bwd of the region (gs_common.h BwdXchg), its own per-workgroup counters
+    size_t off_bwd;
+    uint32_t *seq_bwd;
+    bool bwd_xchg;                                // GS_XGMI_BWD=0 turns it off (separate exchange launch)
+    int colocated;                                // most ranks sharing one GPU (gs_comm_xgmi_set_colocation)
 };
 
 namespace gs {
@@ -65,6 +72,10 @@ int comm_grad_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, f
                        int32_t *stop, hipStream_t s, int *world);
 // how many sum-of-squares partials comm_grad_exchange writes (host-only)
 int comm_sumsq_slots(const gs_comm *c);
+// k_bwd's in-kernel exchange arguments for this communicator; false when it does not apply
+// (RCCL transport, not connected, or switched off), and the chain then exchanges after k_bwd
+bool xgmi_bwd_args(const gs_comm *c, BwdXchg *bx);
+
 // xGMI kernel launcher (gs_xgmi.hip)
 int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
                   float scale, hipStream_t s);

@@ -203,6 +203,24 @@ struct AdamFwd {
     int force;                         // apply at k = 0 too (gs_ppo_stage timing)
 };
 
+// Gradient exchange inside k_bwd (multi-GPU MLP chain over xGMI, gs_xgmi_dev.h): every
+// backward workgroup pushes its output values into its peers' exchange regions, waits for theirs
+// and keeps the rank-ordered mean, so the update's gradient leaves the backward already
+// exchanged (no exchange launch).  world <= 1: no exchange (the single-GPU kernel).
+constexpr int kBwdXMaxRanks = 8;       // one node
+constexpr int kBwdXMaxWG = 1024;       // backward workgroups with a flag / data slot
+constexpr int kBwdXSlot = 1024;        // floats per workgroup slot (4 per thread)
+struct BwdXchg {
+    char *peer[kBwdXMaxRanks];         // exchange region base per rank (peer[rank]: own)
+    uint32_t off_flags1, off_flags2;   // [src][kBwdXMaxWG] u32 flag words (seq << 1)
+    uint32_t off_data, off_res;        // data[parity][src][wg][slot], res[parity][wg][slot]
+    int world, rank, rsag, region_bytes;
+    float scale;                       // 1 / world
+    uint64_t timeout;                  // spin limit, s_memrealtime ticks
+    uint32_t *seq;                     // [kBwdXMaxWG] exchanges completed per workgroup (local)
+    uint32_t *err;                     // sticky error word of the own region
+};
+
 inline int n_col_blocks(int H) { return (H + kTile - 1) / kTile; }
 inline int n_sumsq_slots(const Layout &L) { return n_col_blocks(L.H2) * n_col_blocks(L.H1) + 2 * n_col_blocks(L.H2) + 1; }
 
@@ -229,7 +247,11 @@ int launch_loss(const float *P, const Layout &L, int64_t B, const Workspace &ws,
 size_t bwd_lds_bytes(const Layout &L, int64_t B);
 int prepare_kernels(const Layout &L, int64_t B);
 int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
-               hipStream_t s, const FusedFwd *ff = nullptr, const LossArgs *la = nullptr);
+               hipStream_t s, const FusedFwd *ff = nullptr, const LossArgs *la = nullptr,
+               const BwdXchg *bx = nullptr);
+// whether k_bwd's in-kernel exchange covers this shape (grid and per-workgroup slot limits, and
+// co-residency with `colocated` ranks sharing the GPU)
+bool bwd_xchg_fits(const Layout &L, int64_t B, int colocated = 1);
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
                      const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s);
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);

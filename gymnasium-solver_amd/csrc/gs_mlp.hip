@@ -39,6 +39,7 @@
 #include <unordered_map>
 
 #include "gs_common.h"
+#include "gs_xgmi_dev.h"
 
 namespace gs {
 
@@ -1093,9 +1094,13 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                                              float *__restrict__ G, float *__restrict__ part1,
                                              float *__restrict__ sumsq, const int32_t *__restrict__ stop,
                                              const float *__restrict__ zpart, FusedFwd ff, LossArgs la,
-                                             const uint16_t *__restrict__ h2mask)
+                                             const uint16_t *__restrict__ h2mask, BwdXchg bx)
 {
     if (stop && *stop) return;
+    // multi-GPU: every output value goes through bwd_exchange before it is stored (its
+    // counter is read here, off the epilogue's critical path)
+    const bool xchg = bx.world > 1;
+    const uint32_t xseq = xchg ? bx.seq[blockIdx.x] + 1u : 0u;
     extern __shared__ float lds[];
     __shared__ float sbuf[272];
     const Layout L = S::lay(Lrt);
@@ -1253,20 +1258,25 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         {
             // one sum-of-squares slot per dW2 tile (tile index nb*nkb + kb + t), one for db2
             const int row = tid >> 4, col = tid & 15;
-            float sqt[3] = {0.0f, 0.0f, 0.0f};
+            float gv[3] = {0.0f, 0.0f, 0.0f};
+            bool ok[3] = {false, false, false};
             for (int t = 0; t < nt; ++t) {
                 const float g = ((red[(0 + t) * 256 + tid] + red[(3 + t) * 256 + tid]) + red[(6 + t) * 256 + tid]) +
                                 red[(9 + t) * 256 + tid];
-                if (t < sh.ka) {
-                    const int kc = k0 + t * kTile + col;
-                    if (n0 + row < H2 && kc < H1) {
-                        G[L.oW2 + (int64_t)(n0 + row) * H1 + kc] = g;
-                        sqt[t] = g * g;
-                    }
-                } else if (col == 0 && n0 + row < H2) {
-                    G[L.ob2 + n0 + row] = g;
-                    sqt[2] = g * g;
-                }
+                const int j = t < sh.ka ? t : 2;
+                gv[j] = g;
+                ok[j] = t < sh.ka ? (n0 + row < H2 && k0 + t * kTile + col < H1) : (col == 0 && n0 + row < H2);
+            }
+            if (xchg) bwd_exchange<3>(bx, xseq, gv, ok);
+            float sqt[3] = {0.0f, 0.0f, 0.0f};
+            for (int t = 0; t < nt; ++t) {
+                const int j = t < sh.ka ? t : 2;
+                if (!ok[j]) continue;
+                if (t < sh.ka)
+                    G[L.oW2 + (int64_t)(n0 + row) * H1 + k0 + t * kTile + col] = gv[j];
+                else
+                    G[L.ob2 + n0 + row] = gv[j];
+                sqt[j] = gv[j] * gv[j];
             }
             block_reduce<3>(sqt, reinterpret_cast<float *>(mkA + Bp));   // 3 x (256 + 16) floats
             if (tid == 0) {
@@ -1533,6 +1543,26 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 pr[u] = s;
             }
             __syncthreads();
+            if (xchg) {      // nout <= 4 * 256 (bwd_xchg_fits)
+                float pv[4];
+                bool ok[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = tid + 256 * j, col = o / (D + 1);
+                    ok[j] = o < nout && k0 + col < H1;
+                    float t = 0.0f;
+                    if (o < nout)
+#pragma unroll
+                        for (int g = 0; g < ng; ++g) t += pr[g * nout + o];
+                    pv[j] = t;
+                }
+                bwd_exchange<4>(bx, xseq, pv, ok);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = tid + 256 * j, col = o / (D + 1), d = o - col * (D + 1);
+                    if (ok[j]) part1[((int64_t)rb * H1 + k0 + col) * (D + 1) + d] = pv[j];
+                }
+            } else
             for (int o = tid; o < nout; o += 256) {
                 const int col = o / (D + 1), d = o - col * (D + 1);
                 float t = 0.0f;
@@ -1629,13 +1659,14 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
 #pragma unroll
                 for (int r = 0; r < 4; ++r) partC[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
                 __syncthreads();
-                if (tid < nout) {
-                    const int a = tid >> 4, i = tid & 15;
-                    const float s = ((partC[tid] + partC[256 + tid]) + partC[512 + tid]) + partC[768 + tid];
-                    if (n0 + i < H2) {
-                        G[L.head_row(a) + n0 + i] = s;
-                        sq = s * s;
-                    }
+                const int a = tid >> 4, i = tid & 15;
+                float hv[1] = {tid < nout ? ((partC[tid] + partC[256 + tid]) + partC[512 + tid]) + partC[768 + tid]
+                                          : 0.0f};
+                bool ok[1] = {tid < nout && n0 + i < H2};
+                if (xchg) bwd_exchange<1>(bx, xseq, hv, ok);
+                if (ok[0]) {
+                    G[L.head_row(a) + n0 + i] = hv[0];
+                    sq = hv[0] * hv[0];
                 }
             } else {
                 // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
@@ -1647,14 +1678,26 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     partC[u] = s;
                 }
                 __syncthreads();
-                for (int o = tid; o < nout; o += 256) {
-                    float s = 0.0f;
+                // nout = A1 * 16 <= 4 * 256 (kMaxActions)
+                float hv[4];
+                bool ok[4];
 #pragma unroll
-                    for (int m = 0; m < 16; ++m) s += partC[o * 16 + m];
-                    const int a = o >> 4, i = o & 15;
-                    if (n0 + i < H2) {
-                        G[L.head_row(a) + n0 + i] = s;
-                        sq += s * s;
+                for (int j = 0; j < 4; ++j) {
+                    const int o = tid + 256 * j;
+                    float s = 0.0f;
+                    if (o < nout)
+#pragma unroll
+                        for (int m = 0; m < 16; ++m) s += partC[o * 16 + m];
+                    hv[j] = s;
+                    ok[j] = o < nout && n0 + (o & 15) < H2;
+                }
+                if (xchg) bwd_exchange<4>(bx, xseq, hv, ok);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = tid + 256 * j, a = o >> 4, i = o & 15;
+                    if (ok[j]) {
+                        G[L.head_row(a) + n0 + i] = hv[j];
+                        sq += hv[j] * hv[j];
                     }
                 }
             }
@@ -1669,12 +1712,15 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
             __syncthreads();
             float sqb = 0.0f;
-            if (tid < A1) {
-                float s = 0.0f;
+            float bv[1] = {0.0f};
+            bool ok[1] = {tid < A1};
+            if (tid < A1)
 #pragma unroll
-                for (int m = 0; m < 16; ++m) s += partC[tid * 16 + m];
-                G[L.head_bias(tid)] = s;
-                sqb = s * s;
+                for (int m = 0; m < 16; ++m) bv[0] += partC[tid * 16 + m];
+            if (xchg) bwd_exchange<1>(bx, xseq, bv, ok);
+            if (ok[0]) {
+                G[L.head_bias(tid)] = bv[0];
+                sqb = bv[0] * bv[0];
             }
             block_sumsq_store(sqb, sumsq + sh.nT + 2 * sh.ncb, sbuf);
         }
@@ -1993,25 +2039,57 @@ int launch_loss(const float *P, const Layout &L, int64_t B, const Workspace &ws,
     });
 }
 
+bool bwd_xchg_coresident(int64_t nblk, size_t lds_bytes, int colocated);
+
+bool bwd_xchg_fits(const Layout &L, int64_t B, int colocated)
+{
+    const BwdShape sh = BwdShape::make(L, (int)B);
+    const int64_t nblk = sh.nA + sh.nB + sh.nC;
+    return nblk <= kBwdXMaxWG && kTile * (L.D + 1) <= kBwdXSlot && (L.A + 1) * kTile <= kBwdXSlot &&
+           bwd_xchg_coresident(nblk, bwd_lds_bytes(L, B), colocated);
+}
+
+// Progress of the exchange inside k_bwd: workgroup w of a rank waits only for workgroup w of its
+// peers, and each rank's resident workgroups are a prefix of its grid (in-order dispatch), so
+// the exchange completes unless one rank has no resident workgroup while the others fill the GPU.
+// One rank per GPU never starves; c ranks on one GPU need (c - 1) grids to leave a free slot.
+bool bwd_xchg_coresident(int64_t nblk, size_t lds_bytes, int colocated)
+{
+    if (colocated <= 1) return true;
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    int64_t per_cu = (int64_t)(160 * 1024) / (int64_t)(lds_bytes > 0 ? lds_bytes : 1);
+    if (per_cu > 4) per_cu = 4;       // 16 waves per CU at k_bwd's register use
+    return (int64_t)(colocated - 1) * nblk < (int64_t)ncu * per_cu;
+}
+
 int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
-               hipStream_t s, const FusedFwd *ff, const LossArgs *la)
+               hipStream_t s, const FusedFwd *ff, const LossArgs *la, const BwdXchg *bxp)
 {
     const BwdShape sh0 = BwdShape::make(L, (int)B);
     const unsigned nblk = (unsigned)(sh0.nA + sh0.nB + sh0.nC);
     const size_t lds = bwd_lds_bytes(L, B);
+    BwdXchg bx{};
+    if (bxp && bxp->world > 1) {
+        GS_REQUIRE(bwd_xchg_fits(L, B), "k_bwd exchange: %u workgroups or their output slots exceed the limits",
+                   nblk);
+        bx = *bxp;
+    }
     return with_shape(L, B, [&](auto sh) {
         using Sh = decltype(sh);
         if (ff) {
             int rc = set_lds_limit((const void *)k_bwd<Sh, true>, lds);
             if (rc) return rc;
             hipLaunchKernelGGL((k_bwd<Sh, true>), dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2,
-                               ws.dz, G, ws.part1, ws.sumsq, stop, ws.zpart, *ff, *la, ws.h2mask);
+                               ws.dz, G, ws.part1, ws.sumsq, stop, ws.zpart, *ff, *la, ws.h2mask, bx);
         } else {
             int rc = set_lds_limit((const void *)k_bwd<Sh, false>, lds);
             if (rc) return rc;
             hipLaunchKernelGGL((k_bwd<Sh, false>), dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x, ws.h1, ws.h2,
                                ws.dz, G, ws.part1, ws.sumsq, stop, (const float *)nullptr, FusedFwd{}, LossArgs{},
-                               ws.h2mask);
+                               ws.h2mask, bx);
         }
         GS_LAUNCH_CHECK("k_bwd");
         return GS_OK;

@@ -248,6 +248,14 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
     return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s);
 }
 
+// The fused chains' exchange inside k_bwd (xGMI transport, shapes within its limits): the
+// gradient, the W1 partials and the per-tile sums of squares leave the backward as the mean
+// over ranks, and the rest of the step is the single-GPU one.  False: exchange after k_bwd.
+bool bwd_exchange_of(gs_comm *comm, const Layout &L, int64_t B, BwdXchg *bx)
+{
+    return comm && xgmi_bwd_args(comm, bx) && bwd_xchg_fits(L, B, comm->colocated);
+}
+
 // One minibatch step of the fused chain: k_fwd_hidden<fused> (pre-gathered x), k_bwd<fused>
 // (each workgroup computes the loss rows it needs from the partial heads: no loss launch,
 // no block reduction; metric sums per 16 rows), then the same clip/Adam tail as enqueue_step.
@@ -255,11 +263,13 @@ int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, 
                        const FusedFwd &ff, float *metrics, int32_t *stop, const Workspace &ws, gs_comm *comm,
                        hipStream_t s)
 {
+    BwdXchg bx;
+    const bool inbwd = bwd_exchange_of(comm, L, B, &bx);
     int rc = launch_fwd_fused(P, L, B, ff, sa.la, ws, stop, s);
     if (rc) return rc;
-    rc = launch_bwd(P, L, B, ws, G, stop, s, &ff, &sa.la);
+    rc = launch_bwd(P, L, B, ws, G, stop, s, &ff, &sa.la, inbwd ? &bx : nullptr);
     if (rc) return rc;
-    if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
+    if (!comm || inbwd) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
     return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s);
 }
 
@@ -292,23 +302,26 @@ AdamArgs exchanged_adam_args(const AdamArgs &aa_in, const gs_comm *comm)
 // Minibatch step k with the optimizer step lagged into the next forward (bit-identical to
 // enqueue_step_fused): k_fwd_hidden<fused, adam> applies step k-1 (reads set (k+1)&1, its
 // row-block-0 workgroups write set k&1; nothing at k = 0), then k_bwd<fused> on set k&1.
-// With a communicator the chain is fwd(+Adam of k-1) -> bwd -> exchange of k: the exchange is
-// the only seam the multi-GPU step adds.  The update's last optimizer step is one k_clip_adam
+// With an xGMI communicator k_bwd exchanges its outputs itself (bwd_exchange_of) and the chain
+// is the single-GPU one; with RCCL it is fwd(+Adam of k-1) -> bwd -> exchange of k.  The update's last optimizer step is one k_clip_adam
 // after the loop.
 int enqueue_step_lagged(const ParamSet (&ps)[2], float *G, const Layout &L, const StepArgs &sa_prev, int64_t B,
                         const FusedFwd &ff, int64_t k, float *metrics, int32_t *stop, const Workspace &ws,
                         gs_comm *comm, hipStream_t s)
 {
     const ParamSet &cur = ps[k & 1], &prev = ps[(k & 1) ^ 1];
+    BwdXchg bx;
+    const bool inbwd = bwd_exchange_of(comm, L, B, &bx);
+    const bool after = comm && !inbwd;     // exchange launch after the backward
     AdamFwd af{};
-    af.Min = prev.M, af.Vin = prev.V, af.G = G, af.part1 = comm ? nullptr : ws.part1, af.sumsq = ws.sumsq;
+    af.Min = prev.M, af.Vin = prev.V, af.G = G, af.part1 = after ? nullptr : ws.part1, af.sumsq = ws.sumsq;
     af.Pout = cur.P, af.Mout = cur.M, af.Vout = cur.V;
     af.metrics = metrics;
-    af.aa = comm ? exchanged_adam_args(sa_prev.aa, comm) : sa_prev.aa;
+    af.aa = after ? exchanged_adam_args(sa_prev.aa, comm) : sa_prev.aa;
     int rc = launch_fwd_fused(prev.P, L, B, ff, sa_prev.la, ws, stop, s, &af);
     if (rc) return rc;
-    rc = launch_bwd(cur.P, L, B, ws, G, stop, s, &ff, &sa_prev.la);
-    if (rc || !comm) return rc;
+    rc = launch_bwd(cur.P, L, B, ws, G, stop, s, &ff, &sa_prev.la, inbwd ? &bx : nullptr);
+    if (rc || !after) return rc;
     int world = 1, n_slots = 0;
     return comm_grad_exchange(comm, G, L.P, Part1Fold{ws.part1, sa_prev.aa.nrb, L}, ws.sumsq, &n_slots, stop, s,
                               &world);
@@ -520,7 +533,9 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
             const int64_t k = n_minibatches - 1;
             const ParamSet &q = ps[k & 1];
             const StepArgs sl = make_step_args(hp, L, batch, adam_step0 + k + 1);
-            int rc2 = comm ? launch_clip_adam(q.P, L, grads, q.M, q.V, nullptr, ws.sumsq,
+            BwdXchg bx;
+            const bool after = comm && !bwd_exchange_of(comm, L, batch, &bx);
+            int rc2 = after ? launch_clip_adam(q.P, L, grads, q.M, q.V, nullptr, ws.sumsq,
                                               exchanged_adam_args(sl.aa, comm), metrics + k * GS_NUM_METRICS,
                                               stop_flag, s)
                            : launch_clip_adam(q.P, L, grads, q.M, q.V, ws.part1, ws.sumsq, sl.aa,
@@ -675,5 +690,17 @@ extern "C" int gs_ppo_graph_cache_info(int64_t *n_entries, int64_t *n_captures)
     std::lock_guard<std::mutex> lk(g_graph_mu);
     if (n_entries) *n_entries = (int64_t)g_graphs.size();
     if (n_captures) *n_captures = g_graph_captures;
+    return GS_OK;
+}
+
+extern "C" int gs_ppo_exchange_inside_bwd(gs_comm *comm, gs_mlp_dims dims, int64_t batch, int *inside)
+{
+    GS_REQUIRE(comm && inside, "gs_ppo_exchange_inside_bwd: null argument");
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    GS_REQUIRE(batch >= 2 && batch <= 1024, "batch %lld outside [2, 1024]", (long long)batch);
+    const Layout L = layout_of(dims);
+    BwdXchg bx;
+    *inside = has_fused(L, batch) && bwd_exchange_of(comm, L, batch, &bx) ? 1 : 0;
     return GS_OK;
 }

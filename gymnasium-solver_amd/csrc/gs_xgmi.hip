@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include "gs_comm_internal.h"
+#include "gs_xgmi_dev.h"
 
 namespace gs {
 namespace {
@@ -97,30 +98,11 @@ __device__ __forceinline__ float4 own_values(const float *__restrict__ G, const 
     return v;
 }
 
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-// 16-byte store with sc0 sc1 (system coherence): written through to the destination
-// memory whatever the MTYPE of the peer mapping is; completion is awaited by s_waitcnt.
-__device__ __forceinline__ void store_system(float *p, f4 v)
-{
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-}
+typedef xf4 f4;
 
 __device__ __forceinline__ float *slot(char *region, int par, int world, int src, int64_t cap)
 {
     return reinterpret_cast<float *>(region + kXgmiOffData) + ((int64_t)par * world + src) * cap;
-}
-
-// 16-byte load of the own region at byte offset `off` with sc1 (L1 bypass; the uncached region
-// is never held by an L2 either): what a peer wrote through with sc0 sc1 stores, read without an
-// acquire fence (every load of the handed-off bytes is such a load, the writer drained its
-// stores before raising the flag, the flag is polled with a system-scope load: the guide's
-// flag hand-off with sc1 loads in place of the acquire)
-__device__ __forceinline__ float4 load_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off)
-{
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16);
-    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
 __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Part1Fold fold, XgmiArgs xa,
@@ -394,6 +376,28 @@ int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float 
     return GS_OK;
 }
 
+bool xgmi_bwd_args(const gs_comm *c, BwdXchg *bx)
+{
+    if (c->kind != kCommXgmi || !c->connected || !c->bwd_xchg) return false;
+    *bx = BwdXchg{};
+    bx->world = c->nranks;
+    bx->rank = c->rank;
+    if (c->nranks <= 1) return true;      // nothing to exchange: the single-GPU backward
+    for (int r = 0; r < c->nranks; ++r) bx->peer[r] = c->peer[r];
+    const size_t fl = sizeof(uint32_t) * kBwdXMaxRanks * kBwdXMaxWG;
+    bx->off_flags1 = (uint32_t)c->off_bwd;
+    bx->off_flags2 = (uint32_t)(c->off_bwd + fl);
+    bx->off_data = (uint32_t)(c->off_bwd + 2 * fl);
+    bx->off_res = (uint32_t)(c->off_bwd + 2 * fl + sizeof(float) * (size_t)kBwdXMaxWG * kBwdXSlot * 2 * c->nranks);
+    bx->rsag = c->rsag;
+    bx->region_bytes = (int)c->region_bytes;
+    bx->scale = 1.0f / (float)c->nranks;
+    bx->timeout = c->timeout_ticks;
+    bx->seq = c->seq_bwd;
+    bx->err = reinterpret_cast<uint32_t *>(c->local + kXgmiOffErr);
+    return true;
+}
+
 constexpr int kRcclNormBlocks = 64;   // k_sumsq_flat partials after an RCCL all-reduce
 
 int comm_sumsq_slots(const gs_comm *c) { return c->kind == kCommXgmi ? nwg_of(c) : kRcclNormBlocks; }
@@ -424,8 +428,13 @@ extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint
                (long long)max_count);
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is 64 bytes");
     const int64_t cap = (max_count + kXgmiChunk - 1) / kXgmiChunk * kXgmiChunk;
-    const size_t bytes = kXgmiOffData + sizeof(float) * (2 * (size_t)nranks * (size_t)cap + 2 * (size_t)cap +
-                                                         2 * (size_t)(cap / kXgmiChunk));
+    size_t bytes = kXgmiOffData + sizeof(float) * (2 * (size_t)nranks * (size_t)cap + 2 * (size_t)cap +
+                                                   2 * (size_t)(cap / kXgmiChunk));
+    // the backward's exchange area (more than one rank): flags1 | flags2 | data | res
+    const size_t off_bwd = (bytes + 4095) / 4096 * 4096;
+    if (nranks > 1)
+        bytes = off_bwd + 2 * sizeof(uint32_t) * kBwdXMaxRanks * kBwdXMaxWG +
+                sizeof(float) * (size_t)kBwdXMaxWG * kBwdXSlot * (2 * (size_t)nranks + 2);
     GS_REQUIRE(bytes < ((size_t)1 << 31), "gs_comm_xgmi_create: %lld floats x %d ranks exceed the 2 GiB region limit",
                (long long)max_count, nranks);
     void *p = nullptr;
@@ -457,6 +466,24 @@ extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint
         return hip_fail(e, "xGMI sequence counters", __FILE__, __LINE__);
     }
     c->seq = (uint32_t *)sq;
+    c->off_bwd = off_bwd;
+    if (nranks > 1) {
+        void *sb = nullptr;
+        e = hipMalloc(&sb, sizeof(uint32_t) * kBwdXMaxWG);
+        if (e == hipSuccess) e = hipMemset(sb, 0, sizeof(uint32_t) * kBwdXMaxWG);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            (void)hipFree(sq);
+            (void)hipFree(p);
+            delete c;
+            return hip_fail(e, "xGMI backward exchange counters", __FILE__, __LINE__);
+        }
+        c->seq_bwd = (uint32_t *)sb;
+    }
+    // the exchange inside the MLP backward; GS_XGMI_BWD=0 keeps a separate exchange launch
+    c->bwd_xchg = true;
+    c->colocated = 1;
+    if (const char *b = getenv("GS_XGMI_BWD")) c->bwd_xchg = b[0] != '0';
     // reduce-scatter + all-gather from 4 ranks on (2n/world floats per link instead of n, one more
     // flag round trip); GS_XGMI_ALGO=oneshot|rsag overrides
     c->rsag = nranks >= 4 ? 1 : 0;
@@ -485,6 +512,15 @@ extern "C" int gs_comm_xgmi_connect(gs_comm *c, const uint8_t *handles)
     return GS_OK;
 }
 
+extern "C" int gs_comm_xgmi_set_colocation(gs_comm *c, int ranks_per_device)
+{
+    GS_REQUIRE(c && c->kind == kCommXgmi, "gs_comm_xgmi_set_colocation: not an xGMI communicator");
+    GS_REQUIRE(ranks_per_device >= 1 && ranks_per_device <= c->nranks,
+               "gs_comm_xgmi_set_colocation: %d ranks per device with %d ranks", ranks_per_device, c->nranks);
+    c->colocated = ranks_per_device;
+    return GS_OK;
+}
+
 extern "C" int gs_comm_status(gs_comm *c)
 {
     GS_REQUIRE(c, "gs_comm_status: null communicator");
@@ -504,6 +540,7 @@ int xgmi_destroy(gs_comm *c)
     for (int r = 0; r < c->nranks; ++r)
         if (c->opened[r]) (void)hipIpcCloseMemHandle(c->peer[r]);
     if (c->seq) GS_HIP(hipFree(c->seq));
+    if (c->seq_bwd) GS_HIP(hipFree(c->seq_bwd));
     if (c->local) GS_HIP(hipFree(c->local));
     return GS_OK;
 }

@@ -87,6 +87,7 @@ def _load():
                                          vp, vp, sz, vp, ctypes.c_int, vp]),
         "gs_ppo_update_workspace_bytes": (sz, [MlpDims, i64, i64]),
         "gs_ppo_graph_cache_info": (ctypes.c_int, [vp, vp]),
+        "gs_ppo_exchange_inside_bwd": (ctypes.c_int, [vp, MlpDims, ctypes.c_int64, vp]),
         "gs_cnn_param_count": (i64, [CnnDims]),
         "gs_cnn_workspace_bytes": (sz, [CnnDims, i64]),
         "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp]),
@@ -107,6 +108,7 @@ def _load():
         "gs_comm_xgmi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, vp, ctypes.POINTER(vp)]),
         "gs_comm_xgmi_connect": (ctypes.c_int, [vp, vp]),
         "gs_comm_status": (ctypes.c_int, [vp]),
+        "gs_comm_xgmi_set_colocation": (ctypes.c_int, [vp, ctypes.c_int]),
         "gs_comm_allreduce_mean_f32": (ctypes.c_int, [vp, vp, i64, vp]),
         "gs_comm_info": (ctypes.c_int, [vp, vp, vp, vp]),
         "gs_comm_destroy": (ctypes.c_int, [vp]),
@@ -123,10 +125,11 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_env_reset", "gs_env_step",
             "gs_episode_stats",
             "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_ppo_update_workspace_bytes",
-            "gs_ppo_graph_cache_info",
+            "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status",
+            "gs_comm_xgmi_set_colocation",
             "gs_comm_allreduce_mean_f32", "gs_comm_info", "gs_comm_destroy")
 
 

@@ -147,6 +147,14 @@ def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[
         except RuntimeError as e:
             ok, why = False, str(e)
     ok = _agree(ok, device)
+    if ok:
+        # ranks sharing one GPU (same-device rehearsals): the exchange inside the backward
+        # needs the peers' workgroups resident together (include/gsamd.h)
+        pr = torch.cuda.get_device_properties(dev)
+        ident = f"{pr.pci_domain_id:08x}:{pr.pci_bus_id:04x}:{pr.pci_device_id:04x}".encode()
+        ids = _all_gather_bytes(ident.ljust(32, b"\0"), device)
+        ids = [ids[32 * r:32 * (r + 1)] for r in range(world_size)]
+        check(lib.gs_comm_xgmi_set_colocation(h, max(ids.count(i) for i in ids)), "gs_comm_xgmi_set_colocation")
     dist.barrier()
     if ok and self_test:
         try:
@@ -160,6 +168,14 @@ def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[
             destroy_comm(h)
         raise RuntimeError(f"xGMI exchange unavailable on rank {rank}: {why or 'a peer failed'}")
     return h
+
+
+def exchange_inside_bwd(handle: int, dims, batch: int) -> bool:
+    """Whether the fused MLP update exchanges gradients inside its backward kernel on this
+    communicator (include/gsamd.h gs_ppo_exchange_inside_bwd)."""
+    v = ctypes.c_int()
+    check(lib.gs_ppo_exchange_inside_bwd(handle, dims, int(batch), ctypes.byref(v)), "gs_ppo_exchange_inside_bwd")
+    return bool(v.value)
 
 
 def comm_status(handle: Optional[int]) -> None:

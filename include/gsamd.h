@@ -225,6 +225,12 @@ size_t gs_ppo_update_workspace_bytes(gs_mlp_dims dims, int64_t batch, int64_t n_
  * number of captures made so far.  lr never causes a re-capture (the graph reads the step size
  * from a per-call table); a change of another hyper-parameter re-captures in place. */
 int gs_ppo_graph_cache_info(int64_t *n_entries_host, int64_t *n_captures_host);
+/* Where the fused MLP update (gs_ppo_update without target_kl) exchanges gradients over
+ * `comm`: *inside_host = 1 when k_bwd exchanges its own outputs (xGMI transport, the shape
+ * within the in-kernel exchange's limits and co-residency, include the one-rank case where the
+ * exchange is empty), 0 when a separate exchange launch follows the backward (RCCL, or
+ * GS_XGMI_BWD=0).  Host query (reads device attributes, launches nothing). */
+int gs_ppo_exchange_inside_bwd(struct gs_comm *comm, gs_mlp_dims dims, int64_t batch, int *inside_host);
 
 /* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)
  * Replaces CNNActorCritic (utils/models.py:347-455; conv 8x8s4 -> 4x4s2 -> 3x3s1 with 32/64/64
@@ -330,6 +336,13 @@ int gs_comm_init(const uint8_t id[128], int nranks, int rank, struct gs_comm **o
 int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint8_t out_handle[64], struct gs_comm **out);
 int gs_comm_xgmi_connect(struct gs_comm *comm, const uint8_t *handles);
 int gs_comm_status(struct gs_comm *comm);
+/* The MLP update's exchange runs inside the backward kernel (every workgroup waits for the
+ * same workgroup of its peers), which needs the peers' workgroups to be resident together.
+ * That always holds with one rank per GPU (a node); with c ranks sharing a GPU it needs
+ * (c - 1) backward grids to leave a free workgroup slot.  The launcher reports the largest
+ * number of ranks sharing one GPU here (default 1); where the grids would not fit, the update
+ * exchanges with a separate launch after the backward instead.  Host-only, no GPU call. */
+int gs_comm_xgmi_set_colocation(struct gs_comm *comm, int ranks_per_device);
 int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
 /* What a communicator is: its rank count, this process's rank and the transport
  * (GS_COMM_RCCL / GS_COMM_XGMI).  Any out pointer may be NULL.  Host-only, no GPU call. */

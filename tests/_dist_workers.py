@@ -173,14 +173,19 @@ def xgmi_exchange_worker(rank, world, port, result_dir, n, iters, algo=""):
         dist.destroy_process_group()
 
 
-def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", workload="mlp", algo=""):
+def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", workload="mlp", algo="",
+                    identical=False, bwd="1"):
     """Data-parallel PPO update over the xGMI transport: rank-sharded envs, one rollout and
     2 epochs; every rank saves its final parameters and per-minibatch losses.  lagged="0"
     selects the chain with a separate clip + Adam launch after each exchange.  workload="cnn":
     the C5 Breakout rgb_ppo shard (128 envs per rank, NatureCNN, B=1024, 4 epochs) over a
-    32-step rollout, so the 1.69 M-float gradient exchange runs 16 times."""
+    32-step rollout, so the 1.69 M-float gradient exchange runs 16 times.  identical=True:
+    every rank trains on rank 0's shard (same envs, sampler and seeds), so the exchanged mean
+    of 2 ranks equals each rank's own gradient exactly.  bwd="0": the exchange runs as its
+    own launch after the backward instead of inside it (GS_XGMI_BWD)."""
     os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
     os.environ["GS_LAGGED_ADAM"] = lagged
+    os.environ["GS_XGMI_BWD"] = bwd
     if algo:
         os.environ["GS_XGMI_ALGO"] = algo
     dist = _init(rank, world, port)
@@ -194,11 +199,17 @@ def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", worklo
         torch.manual_seed(42)
         if workload == "cnn":
             cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(n_envs=128, n_steps=32))
+        elif workload == "lunar":     # C3's MLP shapes: a small backward grid (57 workgroups)
+            cfg = load_config("LunarLander-v3", "ppo", overrides=dict(n_envs=64, n_steps=128, n_epochs=2))
         else:
             cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=256, n_epochs=2))
-        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=use_graph,
-                               track_stats=False)
+        agent = DevicePPOAgent(cfg, device=dev, rank=0 if identical else rank, world_size=1 if identical else world,
+                               use_graph=use_graph, track_stats=False)
         agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
+        if workload != "cnn":      # which exchange the fused chain runs, for the parent's checks
+            from gsamd.distributed import exchange_inside_bwd
+            inside = exchange_inside_bwd(agent.comm, agent.policy_model.dims, agent.batch_size)
+            open(os.path.join(result_dir, f"inside{rank}"), "w").write(str(int(inside)))
         agent.train_epoch()
         torch.cuda.synchronize()
         comm_status(agent.comm)

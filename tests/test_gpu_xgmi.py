@@ -1,5 +1,5 @@
 """GPU: the xGMI gradient exchange (csrc/gs_xgmi.hip: one-shot and reduce-scatter + all-gather
-forms) with 2 to 4 ranks.  The box
+forms, as an exchange launch and inside the MLP backward, csrc/gs_xgmi_dev.h) with 2 to 4 ranks.  The box
 has one MI355X, so every rank runs on cuda:0 and the peers' regions are opened through the
 same IPC path the ranks of an 8-GPU node use; the cross-device link itself is
 exercised only by the driver's multi-GPU bench.
@@ -114,3 +114,45 @@ def test_xgmi_lagged_chain_equals_separate_chain(tmp_path):
         (p1, l1), (p0, l0) = runs["1"][r], runs["0"][r]
         assert np.array_equal(p1.view(np.uint32), p0.view(np.uint32)), f"rank {r}: params differ"
         assert np.array_equal(l1.view(np.uint32), l0.view(np.uint32)), f"rank {r}: losses differ"
+
+
+@pytest.mark.parametrize("algo", ["oneshot", "rsag"])
+def test_xgmi_bwd_exchange_identical_shards_equal_one_gpu(tmp_path, algo):
+    """The exchange inside k_bwd (default for the fused MLP chain): 2 ranks training on the same
+    shard exchange identical gradients, whose mean (g + g) * 0.5 is g exactly, so every rank must
+    end bit-identical to the one-rank run — any slot, flag, parity or ordering error shows."""
+    from _dist_workers import xgmi_ppo_worker
+    runs = {}
+    for world in (1, 2):
+        d = tmp_path / f"w{world}"
+        d.mkdir()
+        _run(xgmi_ppo_worker, world, d, True, "1", "mlp", algo, True, timeout=400)
+        runs[world] = [(np.load(d / f"p{r}.npy"), np.load(d / f"l{r}.npy")) for r in range(world)]
+        assert all((d / f"inside{r}").read_text() == "1" for r in range(world)), "exchange not inside k_bwd"
+    p1, l1 = runs[1][0]
+    for r in range(2):
+        p2, l2 = runs[2][r]
+        assert np.array_equal(p2.view(np.uint32), p1.view(np.uint32)), f"rank {r}: params differ from one rank"
+        assert np.array_equal(l2.view(np.uint32), l1.view(np.uint32)), f"rank {r}: losses differ from one rank"
+
+
+def test_xgmi_bwd_exchange_matches_exchange_launch(tmp_path):
+    """4 ranks on their own shards with C3's MLP shapes (a backward grid small enough for 4 ranks
+    to share the GPU's workgroup slots), reduce-scatter + all-gather form: the exchange inside
+    k_bwd and the separate exchange launch (GS_XGMI_BWD=0) compute the same mean gradient with
+    the W1 partials folded after (inside k_bwd) or before (launch) the rank sum, so the final
+    parameters agree to rounding; each run's replicas are bitwise identical."""
+    from _dist_workers import xgmi_ppo_worker
+    world = 4
+    res = {}
+    for bwd in ("1", "0"):
+        d = tmp_path / f"bwd{bwd}"
+        d.mkdir()
+        _run(xgmi_ppo_worker, world, d, True, "1", "lunar", "", False, bwd, timeout=400)
+        p = [np.load(d / f"p{r}.npy") for r in range(world)]
+        for r in range(1, world):
+            assert np.array_equal(p[0].view(np.uint32), p[r].view(np.uint32)), (bwd, r)
+        assert all((d / f"inside{r}").read_text() == bwd for r in range(world)), "unexpected exchange placement"
+        res[bwd] = p[0]
+    assert not np.array_equal(res["1"].view(np.uint32), res["0"].view(np.uint32))   # two distinct paths ran
+    np.testing.assert_allclose(res["1"], res["0"], rtol=1e-4, atol=1e-6)
