@@ -240,27 +240,29 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             return make_float4(v[0], v[1], v[2], v[3]);
         };
         auto ld1 = [](const float *base, int64_t o) { return *(const __attribute__((address_space(1))) float *)(base + o); };
-        const float neg_step = apply && aa.sched ? aa.sched[2 * kprev] : aa.neg_step_size;
-        const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.inv_bc2_sqrt;
-        float xv = 0.0f;
-        if (tid < kTile * cD) {
-            const int i = tid / cD;
-            xv = r0 + i < rows ? ff.xg[(kstep * rows + r0) * cD + tid] : 0.0f;
-        }
+        // Every vector load below is unconditional, at an index clamped into its array, and the
+        // lanes past an array's end discard what they loaded: a predicated load (`ok ? load : 0`)
+        // compiles to an exec-masked branch per load, and the register moves around those
+        // branches force s_waitcnt vmcnt stalls in the middle of the burst (one memory round trip
+        // per stall instead of one for the whole prologue)
+        constexpr int nq1 = n1 / 4;
         float4 w1p[NQ], w1m[NQ], w1v[NQ], t[NQ][NRB];     // W1|b1 (param order), dW1|db1 partials
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
-            const int q = tid + 256 * j;
-            const bool ok = 4 * q < n1, okg = ok && apply;
-            (void)okg;
-            w1p[j] = ok ? ld4(P, q) : z4;
-            w1m[j] = ok ? ld4(af.Min, q) : z4;
-            w1v[j] = ok ? ld4(af.Vin, q) : z4;
-            if (fold) {
+            const int q = min(tid + 256 * j, nq1 - 1);
+            w1p[j] = ld4(P, q);
+            w1m[j] = ld4(af.Min, q);
+            w1v[j] = ld4(af.Vin, q);
+        }
+        if (fold) {
 #pragma unroll
-                for (int b = 0; b < NRB; ++b) t[j][b] = ok ? ld4(af.part1 + (int64_t)b * n1, q) : z4;
-            } else {
-                t[j][0] = ok ? ld4(af.G, q) : z4;
+            for (int j = 0; j < NQ; ++j)
+#pragma unroll
+                for (int b = 0; b < NRB; ++b) t[j][b] = ld4(af.part1 + (int64_t)b * n1, min(tid + 256 * j, nq1 - 1));
+        } else {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                t[j][0] = ld4(af.G, min(tid + 256 * j, nq1 - 1));
 #pragma unroll
                 for (int b = 1; b < NRB; ++b) t[j][b] = z4;
             }
@@ -269,32 +271,44 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
 #pragma unroll
         for (int j = 0; j < kW2v; ++j) {
             const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
-            const bool ok = c0 + i < H2, okg = ok && apply;
-            const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
-            (void)okg;
-            w2r[j] = ok ? ld4(P, q) : z4;
-            w2m[j] = ok ? ld4(af.Min, q) : z4;
-            w2v[j] = ok ? ld4(af.Vin, q) : z4;
-            w2g[j] = ok ? ld4(af.G, q) : z4;
+            const int64_t q = (Lc.oW2 + (int64_t)min(c0 + i, H2 - 1) * cH1) / 4 + k4;
+            w2r[j] = ld4(P, q);
+            w2m[j] = ld4(af.Min, q);
+            w2v[j] = ld4(af.Vin, q);
+            w2g[j] = ld4(af.G, q);
         }
         // scalar slices {p, m, v, g}: b2 (threads < 16), head weights (< 16*A1), head biases ((0,0), < A1)
-        float sb[4] = {0.f, 0.f, 0.f, 0.f}, sw[4] = {0.f, 0.f, 0.f, 0.f}, shb[4] = {0.f, 0.f, 0.f, 0.f};
         const int64_t ob = tid < kTile && c0 + tid < H2 ? Lc.ob2 + c0 + tid : -1;
         const int64_t ow = tid < cA1 * kTile && c0 + (tid & 15) < H2 ? Lc.head_row(tid >> 4) + c0 + (tid & 15) : -1;
         const int64_t oh = own1 && tid < cA1 ? Lc.head_bias(tid) : -1;
+        float sb[4], sw[4], shb[4];
         auto load_slice = [&](float (&e)[4], int64_t o) {
-            if (o < 0) return;
-            e[0] = ld1(P, o);
-            e[1] = ld1(af.Min, o);
-            e[2] = ld1(af.Vin, o);
-            e[3] = ld1(af.G, o);
+            const int64_t oc = o < 0 ? 0 : o;
+            e[0] = ld1(P, oc);
+            e[1] = ld1(af.Min, oc);
+            e[2] = ld1(af.Vin, oc);
+            e[3] = ld1(af.G, oc);
         };
         load_slice(sb, ob);
         load_slice(sw, ow);
         load_slice(shb, oh);
         float sl[NS];
 #pragma unroll
-        for (int j = 0; j < NS; ++j) sl[j] = tid + 256 * j < aa.n_slots ? ld1(af.sumsq, tid + 256 * j) : 0.0f;
+        for (int j = 0; j < NS; ++j) sl[j] = ld1(af.sumsq, min(tid + 256 * j, aa.n_slots - 1));
+        // then the loads behind the graph replay's step base: this minibatch's x rows and step
+        // k-1's schedule entries
+        float xv = 0.0f;
+        {
+            const int i = min(tid / cD, kTile - 1);
+            const bool okx = tid < kTile * cD && r0 + i < rows;
+            xv = ff.xg[(kstep * rows + r0) * cD + (okx ? tid : 0)];
+            if (!okx) xv = 0.0f;
+        }
+        const float neg_step = apply && aa.sched ? aa.sched[2 * kprev] : aa.neg_step_size;
+        const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.inv_bc2_sqrt;
+#pragma unroll
+        for (int j = 0; j < NS; ++j)
+            if (tid + 256 * j >= aa.n_slots) sl[j] = 0.0f;
         if (tid < kTile * cD) xs[tid] = xv;
 #ifdef GS_STAMPS
         __builtin_amdgcn_s_waitcnt(0);     // diagnostic build only: split "loads landed" from the norm
@@ -391,8 +405,8 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         step_slice(sb, ob, own2);
         step_slice(sw, ow, own2);
         step_slice(shb, oh, own1);
-        if (tid < kTile) b2s[tid] = sb[0];
-        if (tid < cA1 * kTile) whs[tid] = sw[0];
+        if (tid < kTile) b2s[tid] = ob < 0 ? 0.0f : sb[0];
+        if (tid < cA1 * kTile) whs[tid] = ow < 0 ? 0.0f : sw[0];
         GS_STAMP(2)
     } else if constexpr (kStage0) {
         constexpr Layout Lc = S::lay(Layout{});
@@ -1057,16 +1071,21 @@ __device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const
         double acc[kNumSums];
 #pragma unroll
         for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
-        if (r < B) {
-            const int64_t o = k * B + r;
-            // the row's fields are loaded before the head partials: one memory round trip
-            const int fa = ff.fa[o];
-            const float folp = ff.folp[o], fov = ff.fov[o], fadv = ff.fadv[o], fret = ff.fret[o];
-            float z[AMAX + 1];
-            gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
-            loss_row<AMAX>(z, L.A, fa, folp, fov, fadv, fret, la, 1.0f / (float)B, dzs + i * A1, acc);
-        } else {
+        // rows past B (padding) load row B-1 unconditionally and discard the result: a predicated
+        // load burst would compile to branches with vmcnt stalls inside it
+        const bool live = r < B;
+        const int rc = live ? r : B - 1;
+        const int64_t o = k * B + rc;
+        // the row's fields are loaded before the head partials: one memory round trip
+        const int fa = ff.fa[o];
+        const float folp = ff.folp[o], fov = ff.fov[o], fadv = ff.fadv[o], fret = ff.fret[o];
+        float z[AMAX + 1];
+        gather_head_row<AMAX, AEX>(zpart, P, L, rc, z);
+        loss_row<AMAX>(z, L.A, fa, folp, fov, fadv, fret, la, 1.0f / (float)B, dzs + i * A1, acc);
+        if (!live) {
             for (int a = 0; a < A1; ++a) dzs[i * A1 + a] = 0.0f;
+#pragma unroll
+            for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
         }
         if (dscr)
 #pragma unroll
@@ -1140,39 +1159,41 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             int mr[NMk];
             float4 hr[NH1];
             float wh = 0.0f;
+            // unconditional loads at clamped indices, out-of-range lanes zeroed at the LDS stores
+            // (predicated loads would put vmcnt stalls inside the burst)
 #pragma unroll
             for (int j = 0; j < NMk; ++j) {
                 const int b = tid + 256 * j;
-                mr[j] = b < cB ? (int)h2mask[(int64_t)b * cncb + nb] : 0;
+                mr[j] = (int)h2mask[(int64_t)min(b, cB - 1) * cncb + nb];
             }
 #pragma unroll
             for (int j = 0; j < NH1; ++j) {
                 const int u = tid + 256 * j, b = u / cq, c4 = u % cq;
-                hr[j] = (u < cBp * cq && b < cB && k0 + 4 * c4 < Lc.H1)
-                            ? *reinterpret_cast<const float4 *>(h1 + (int64_t)b * Lc.H1 + k0 + 4 * c4)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                hr[j] = *reinterpret_cast<const float4 *>(h1 + (int64_t)min(b, cB - 1) * Lc.H1 +
+                                                          min(k0 + 4 * c4, Lc.H1 - 4));
             }
-            if (tid < A1 * kTile) {
-                const int a = tid >> 4, j = tid & 15;
-                wh = n0 + j < H2 ? P[L.head_row(a) + n0 + j] : 0.0f;
+            {
+                const int a = min(tid >> 4, A1 - 1), j = tid & 15;
+                wh = P[L.head_row(a) + min(n0 + j, H2 - 1)];
             }
             if constexpr (FUSED)
                 loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
                                  nullptr);
             else
                 copy_to_lds(dzs, dz, B * A1);
-            if (tid < A1 * kTile) whs[tid] = wh;
+            if (tid < A1 * kTile) whs[tid] = n0 + (tid & 15) < H2 ? wh : 0.0f;
 #pragma unroll
             for (int j = 0; j < NMk; ++j)
-                if (tid + 256 * j < cBp) mkA[tid + 256 * j] = mr[j];
+                if (tid + 256 * j < cBp) mkA[tid + 256 * j] = tid + 256 * j < cB ? mr[j] : 0;
 #pragma unroll
             for (int j = 0; j < NH1; ++j) {
                 const int u = tid + 256 * j, b = u / cq, c4 = u % cq;
                 if (u < cBp * cq) {
-                    h1T[(4 * c4 + 0) * ld + b] = hr[j].x;
-                    h1T[(4 * c4 + 1) * ld + b] = hr[j].y;
-                    h1T[(4 * c4 + 2) * ld + b] = hr[j].z;
-                    h1T[(4 * c4 + 3) * ld + b] = hr[j].w;
+                    const bool ok = b < cB && k0 + 4 * c4 < Lc.H1;
+                    h1T[(4 * c4 + 0) * ld + b] = ok ? hr[j].x : 0.0f;
+                    h1T[(4 * c4 + 1) * ld + b] = ok ? hr[j].y : 0.0f;
+                    h1T[(4 * c4 + 2) * ld + b] = ok ? hr[j].z : 0.0f;
+                    h1T[(4 * c4 + 3) * ld + b] = ok ? hr[j].w : 0.0f;
                 }
             }
         } else {
@@ -1332,56 +1353,61 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 int mr[NM];
                 float4 wr[NW];
                 float hr[NH], h1r[N1], xr[NX];
+                // unconditional loads at clamped indices; out-of-range lanes zeroed at the stores
 #pragma unroll
                 for (int j = 0; j < NM; ++j) {
-                    const int u = tid + j * kLd, i = u / cncb, c = u - i * cncb;
-                    mr[j] = (u < kRowsB * cncb && b0 + i < cB) ? (int)h2mask[(int64_t)(b0 + i) * cncb + c] : 0;
+                    const int u = min(tid + j * kLd, kRowsB * cncb - 1), i = u / cncb, c = u - i * cncb;
+                    mr[j] = (int)h2mask[(int64_t)min(b0 + i, cB - 1) * cncb + c];
                 }
 #pragma unroll
                 for (int j = 0; j < NW; ++j) {
-                    const int u = tid + j * kLd, n = u >> 2, c4 = u & 3;
-                    wr[j] = (u < cH2p * 4 && n < cH2 && k0 + 4 * c4 < cH1)
-                                ? *reinterpret_cast<const float4 *>(P + Lc.oW2 + (int64_t)n * cH1 + k0 + 4 * c4)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const int u = tid + j * kLd, n = min(u >> 2, cH2 - 1), c4 = u & 3;
+                    wr[j] = *reinterpret_cast<const float4 *>(P + Lc.oW2 + (int64_t)n * cH1 + min(k0 + 4 * c4, cH1 - 4));
                 }
 #pragma unroll
                 for (int j = 0; j < NH; ++j) {
-                    const int u = tid + j * kLd, a = u / cH2, n = u - a * cH2;
-                    hr[j] = u < cA1 * cH2 ? P[Lc.head_row(a) + n] : 0.0f;
+                    const int u = min(tid + j * kLd, cA1 * cH2 - 1), a = u / cH2, n = u - a * cH2;
+                    hr[j] = P[Lc.head_row(a) + n];
                 }
 #pragma unroll
                 for (int j = 0; j < N1; ++j) {
-                    const int u = tid + j * kLd, i = u >> 4, jj = u & 15;
-                    h1r[j] = (u < kRowsB * 16 && b0 + i < cB && k0 + jj < cH1) ? h1[(int64_t)(b0 + i) * cH1 + k0 + jj]
-                                                                              : 0.0f;
+                    const int u = tid + j * kLd, i = min(u >> 4, kRowsB - 1), jj = u & 15;
+                    h1r[j] = h1[(int64_t)min(b0 + i, cB - 1) * cH1 + min(k0 + jj, cH1 - 1)];
                 }
 #pragma unroll
                 for (int j = 0; j < NX; ++j) {
                     const int u = tid + j * kLd;
-                    xr[j] = (u < kRowsB * cD && b0 * cD + u < cB * cD) ? x[(int64_t)b0 * cD + u] : 0.0f;
+                    xr[j] = x[min((int64_t)b0 * cD + u, (int64_t)cB * cD - 1)];
                 }
 #pragma unroll
-                for (int j = 0; j < NM; ++j)
-                    if (tid + j * kLd < kRowsB * cncb) mkB[tid + j * kLd] = mr[j];
+                for (int j = 0; j < NM; ++j) {
+                    const int u = tid + j * kLd, i = u / cncb;
+                    if (u < kRowsB * cncb) mkB[u] = b0 + i < cB ? mr[j] : 0;
+                }
 #pragma unroll
                 for (int j = 0; j < NW; ++j) {
                     const int u = tid + j * kLd, n = u >> 2, c4 = u & 3;
                     if (u < cH2p * 4) {
-                        W2T[(4 * c4 + 0) * ld + n] = wr[j].x;
-                        W2T[(4 * c4 + 1) * ld + n] = wr[j].y;
-                        W2T[(4 * c4 + 2) * ld + n] = wr[j].z;
-                        W2T[(4 * c4 + 3) * ld + n] = wr[j].w;
+                        const bool ok = n < cH2 && k0 + 4 * c4 < cH1;
+                        W2T[(4 * c4 + 0) * ld + n] = ok ? wr[j].x : 0.0f;
+                        W2T[(4 * c4 + 1) * ld + n] = ok ? wr[j].y : 0.0f;
+                        W2T[(4 * c4 + 2) * ld + n] = ok ? wr[j].z : 0.0f;
+                        W2T[(4 * c4 + 3) * ld + n] = ok ? wr[j].w : 0.0f;
                     }
                 }
 #pragma unroll
                 for (int j = 0; j < NH; ++j)
                     if (tid + j * kLd < cA1 * cH2) whs[tid + j * kLd] = hr[j];
 #pragma unroll
-                for (int j = 0; j < N1; ++j)
-                    if (tid + j * kLd < kRowsB * 16) h1m[tid + j * kLd] = h1r[j];
+                for (int j = 0; j < N1; ++j) {
+                    const int u = tid + j * kLd, i = u >> 4, jj = u & 15;
+                    if (u < kRowsB * 16) h1m[u] = (b0 + i < cB && k0 + jj < cH1) ? h1r[j] : 0.0f;
+                }
 #pragma unroll
-                for (int j = 0; j < NX; ++j)
-                    if (tid + j * kLd < kRowsB * cD) xs[tid + j * kLd] = xr[j];
+                for (int j = 0; j < NX; ++j) {
+                    const int u = tid + j * kLd;
+                    if (u < kRowsB * cD) xs[u] = b0 * cD + u < cB * cD ? xr[j] : 0.0f;
+                }
             }
         } else if (!FUSED || tid < kLd) {
             for (int u = tid; u < kRowsB * sh.ncb; u += kLd) {
@@ -1596,21 +1622,21 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             constexpr int cB = S::Bc, cBp = (cB + 15) / 16 * 16, NH = (cBp * 4 + 255) / 256;
             float4 hr[NH];
 #pragma unroll
-            for (int j = 0; j < NH; ++j) {
+            for (int j = 0; j < NH; ++j) {      // clamped, unconditional; zeroed at the stores
                 const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
-                hr[j] = (u < cBp * 4 && b < cB && n0 + 4 * c4 < Lc.H2)
-                            ? *reinterpret_cast<const float4 *>(h2 + (int64_t)b * Lc.H2 + n0 + 4 * c4)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                hr[j] = *reinterpret_cast<const float4 *>(h2 + (int64_t)min(b, cB - 1) * Lc.H2 +
+                                                          min(n0 + 4 * c4, Lc.H2 - 4));
             }
             loss_in();
 #pragma unroll
             for (int j = 0; j < NH; ++j) {
                 const int u = tid + 256 * j, b = u >> 2, c4 = u & 3;
                 if (u < cBp * 4) {
-                    hs[b * 17 + 4 * c4 + 0] = hr[j].x;
-                    hs[b * 17 + 4 * c4 + 1] = hr[j].y;
-                    hs[b * 17 + 4 * c4 + 2] = hr[j].z;
-                    hs[b * 17 + 4 * c4 + 3] = hr[j].w;
+                    const bool ok = b < cB && n0 + 4 * c4 < Lc.H2;
+                    hs[b * 17 + 4 * c4 + 0] = ok ? hr[j].x : 0.0f;
+                    hs[b * 17 + 4 * c4 + 1] = ok ? hr[j].y : 0.0f;
+                    hs[b * 17 + 4 * c4 + 2] = ok ? hr[j].z : 0.0f;
+                    hs[b * 17 + 4 * c4 + 3] = ok ? hr[j].w : 0.0f;
                 }
             }
         } else {

@@ -498,6 +498,9 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     const bool fused = has_fused(L, batch) && !(hp.target_kl > 0.0f) &&
                        workspace_bytes >= carve_fused(nullptr, L, batch, n_minibatches).bytes &&
                        (((uintptr_t)params | (uintptr_t)grads | (uintptr_t)adam_m | (uintptr_t)adam_v) & 15) == 0;
+    // the fused chain has no KL early stop (target_kl unset): its kernels get no stop flag, so
+    // none of them starts with a dependent load of it
+    if (fused) stop_flag = nullptr;
     FusedWs fw{};
     FusedFwd ff0{};
     if (fused) {

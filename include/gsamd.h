@@ -202,7 +202,10 @@ int gs_ppo_stage(int stage, float *params_dev, float *grads_dev, float *adam_m_d
 /* The whole update phase of one rollout: n_minibatches consecutive steps over
  * idx_dev (n_minibatches * batch indices), metrics_dev gets n_minibatches records.
  * adam_step0 is the optimizer step count BEFORE the first of these steps.
- * use_graph != 0 replays chunks of 512 steps from a captured hipGraph. */
+ * use_graph != 0 replays chunks of 512 steps from a captured hipGraph.  stop_flag_dev is the
+ * KL early stop of hp.target_kl > 0 (sticky: set when a minibatch's approx_kl exceeds it, every
+ * later step skipped); with target_kl unset the update never reads or writes it (the fused
+ * chain's kernels then start without that dependent load). */
 int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
                   gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout, const int32_t *idx_dev,
                   int64_t batch, int64_t n_minibatches, int64_t adam_step0, float *metrics_dev,
