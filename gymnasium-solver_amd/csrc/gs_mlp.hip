@@ -46,6 +46,31 @@ namespace gs {
 #ifdef GS_STAMPS
 __device__ unsigned long long g_stamp_acc[8][16];
 __device__ unsigned long long g_stamp_cnt[8];
+// chain timeline (diagnostic build): per minibatch k < kSpanK and workgroup, the start (thread 0)
+// and each wave's end after its memory ops drained, low 32 bits of s_memrealtime (100 MHz, one
+// clock for the whole device); plain per-workgroup stores (atomics on shared words would
+// serialise and distort the timeline); kernel 0 = lagged forward, 1 = k_bwd
+constexpr int kSpanK = 2048, kSpanWG = 288;
+__device__ unsigned g_span[2][kSpanK][kSpanWG][5];
+__device__ __forceinline__ int span_wg() { return (int)(blockIdx.x + blockIdx.y * gridDim.x); }
+__device__ __forceinline__ void span_start(int kern, int64_t k, unsigned long long t0)
+{
+    if (threadIdx.x == 0 && k >= 0 && k < kSpanK && span_wg() < kSpanWG) g_span[kern][k][span_wg()][0] = (unsigned)t0;
+}
+__device__ __forceinline__ void span_end(int kern, int64_t k)
+{
+    if ((threadIdx.x & 63) == 0 && k >= 0 && k < kSpanK && span_wg() < kSpanWG) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        g_span[kern][k][span_wg()][1 + (threadIdx.x >> 6)] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    }
+}
+#define GS_SPAN_T0 const unsigned long long _sp_t0 = __builtin_amdgcn_s_memrealtime();
+#define GS_SPAN_START(slot, k) span_start(slot, k, _sp_t0);
+#define GS_SPAN_END(slot, k) span_end(slot, k);
+#else
+#define GS_SPAN_T0
+#define GS_SPAN_START(slot, k) ;
+#define GS_SPAN_END(slot, k) ;
 #endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c)
@@ -181,6 +206,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     FusedFwd ff, LossArgs la, uint16_t *__restrict__ h2mask, AdamFwd af = AdamFwd{})
 {
     GS_STAMP_BEGIN(0)
+    GS_SPAN_T0
     if (stop && *stop) return;
     extern __shared__ float lds[];
     const Layout L = S::lay(Lrt);
@@ -203,6 +229,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
 
     if (rg.step_base && idx) idx += *rg.step_base * rows;
     const int64_t kstep = FUSED ? ff.k_local + (ff.step_base ? *ff.step_base : 0) : 0;
+    if constexpr (ADAM) GS_SPAN_START(0, kstep)
     // ---- phase 0: every operand of this workgroup, all loads in flight together.
     //      Threads 0..15 run the dependent idx -> row -> obs/fields chain while the rest
     //      of the block streams the weights into LDS.
@@ -627,6 +654,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         }
     }
     GS_STAMP_END(6)
+    if constexpr (ADAM) GS_SPAN_END(0, kstep)
 }
 
 static int set_lds_limit(const void *fn, size_t bytes);
@@ -1004,9 +1032,10 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
 
 // ------------------------------------------------------------------------------------
 // k_bwd: three roles by block range.
-//   role A: dW2 tile (n-block, k-block), K = batch     -> grads, db2 (k-block 0)
-//   role B: dh1 slab (64 rows, k-block), K = H2        -> dW1/db1 partial per 64 rows
-//   role C: head grads for an n-block; one extra block for the head biases
+//   role A: dW2 tiles (n-block, ka k-blocks), K = batch -> grads
+//   role B: dh1 slab (32 rows, k-block), K = H2        -> dW1/db1 partial per 32 rows
+//   role C: head grads and db2 for an n-block, metric row groups; one extra block for the
+//           head biases
 // sum-of-squares slot map: [0, nA) dW2 tiles, [nA, nA+ncb) db2 blocks,
 //                          [nA+ncb, nA+2ncb) head weight blocks, nA+2ncb head biases.
 // ------------------------------------------------------------------------------------
@@ -1016,6 +1045,18 @@ __device__ __forceinline__ void block_sumsq_store(float v, float *slot, float *s
     block_reduce<1>(t, sbuf);      // sbuf: 272 floats
     if (threadIdx.x == 0) *slot = t[0];
 }
+
+// The role-A workgroup that stores metric row group g (16 rows) of a minibatch of G groups:
+// spread over the nA workgroups, off the k-block-0 ones (they also form db2) when there is room
+__host__ __device__ inline int metric_owner(int g, int G, int nA)
+{
+    if (G <= nA) {
+        const int stride = nA / G;
+        return g * stride + (stride > 1 ? 1 : 0);
+    }
+    return (int)(((int64_t)g * nA) / G);
+}
+__host__ __device__ inline int metric_groups_per_wg(int G, int nA) { return G <= nA ? 1 : (G + nA - 1) / nA; }
 
 struct BwdShape {
     int ncb, nkb, nrbB, ka, nT, nA, nB, nC;
@@ -1041,7 +1082,9 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     const int A1 = L.A + 1;
     const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
     const int64_t H2p = (L.H2 + 63) / 64 * 64;
-    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 3 * kTile * (Bp64 + 4) + 3072 + Bp64 + 816;
+    const BwdShape shp = BwdShape::make(L, (int)B);
+    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 3 * kTile * (Bp64 + 4) + 3072 + Bp64 + 816 + 2 +
+                          (int64_t)metric_groups_per_wg((int)B / kTile, shp.nA) * kTile * kNumSums * 2;
     const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
                           kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024 +
                           (int64_t)kRowsB * n_col_blocks(L.H2);
@@ -1054,13 +1097,15 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
 
 // Fused path: the loss rows a workgroup needs (dLoss/dlogits | dLoss/dvalue) are computed
 // from the forward's partial heads straight into LDS, so the chain has no separate loss
-// launch.  Threads [t0, t0 + nthr) take rows [r0, r0 + n); dscr != nullptr also keeps each
-// row's 14 metric sums (n x 14 doubles of LDS) for store_metric_groups after a barrier.
+// launch.  Threads [t0, t0 + nthr) take rows [r0, r0 + n); dscr != nullptr also keeps the 14
+// metric sums of the rows in [d0, d1) ((d1 - d0) x 14 doubles of LDS) for store_metric_groups
+// after a barrier.
 template <class S>
 __device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const Layout &L,
                                               const float *__restrict__ zpart, const FusedFwd &ff,
                                               const LossArgs &la, int B, int64_t k, int r0, int n, float *dzs,
-                                              double *dscr, int t0 = 0, int nthr = 256)
+                                              double *dscr, int t0 = 0, int nthr = 256, int d0 = 0,
+                                              int d1 = 1 << 30)
 {
     constexpr int AMAX = S::AMAX, AEX = S::AEX;
     const int A1 = L.A + 1;
@@ -1087,9 +1132,9 @@ __device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const
 #pragma unroll
             for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
         }
-        if (dscr)
+        if (dscr && r >= d0 && r < d1)      // rows of the metric window [d0, d1) only
 #pragma unroll
-            for (int q = 0; q < kNumSums; ++q) dscr[i * kNumSums + q] = acc[q];
+            for (int q = 0; q < kNumSums; ++q) dscr[(r - d0) * kNumSums + q] = acc[q];
     }
 }
 
@@ -1115,11 +1160,17 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                                              const float *__restrict__ zpart, FusedFwd ff, LossArgs la,
                                              const uint16_t *__restrict__ h2mask, BwdXchg bx)
 {
+    GS_SPAN_T0
     if (stop && *stop) return;
     // multi-GPU: every output value goes through bwd_exchange before it is stored (its
     // counter is read here, off the epilogue's critical path)
     const bool xchg = bx.world > 1;
     const uint32_t xseq = xchg ? bx.seq[blockIdx.x] + 1u : 0u;
+    // this minibatch's index in the update (graph replay: + the chunk's device step base), read
+    // once here: a later re-read (the metric-group stores come after LDS/global stores the
+    // compiler cannot order it against) would be a dependent round trip in the middle of a phase
+    const int64_t kstep = FUSED ? ff.k_local + (ff.step_base ? *ff.step_base : 0) : 0;
+    if constexpr (FUSED) GS_SPAN_START(1, kstep)
     extern __shared__ float lds[];
     __shared__ float sbuf[272];
     const Layout L = S::lay(Lrt);
@@ -1149,6 +1200,21 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         // relu'(h2) bits of this n-block (one word per row) and the h1 column tile (16 contiguous
         // floats per row = 4 float4, transposed into LDS); dh2T is filled by the dh2 pass
         int *mkA = reinterpret_cast<int *>(red + 3072);   // [Bp]
+        // metric row groups this workgroup stores (fused path): rows [16 gs, 16 ge), their 14 sums
+        // each in dscrA (after mkA and block_reduce's scratch)
+        int gs = 0, ge = 0;
+        if constexpr (FUSED) {
+            const int G = B / kTile;
+            gs = G;
+            for (int g = 0; g < G; ++g)
+                if (metric_owner(g, G, sh.nA) == bid) {
+                    gs = min(gs, g);
+                    ge = g + 1;
+                }
+            if (ge == 0) gs = 0;
+        }
+        double *dscrA = reinterpret_cast<double *>(
+            (reinterpret_cast<uintptr_t>(reinterpret_cast<float *>(mkA + Bp) + 816) + 7) & ~(uintptr_t)7);
         if constexpr (S::H1c > 0 && S::Bc > 0) {
             // compile-time shapes: the tile loads are issued before the loss rows, which
             // then run while they are in flight; LDS writes follow
@@ -1177,8 +1243,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 wh = P[L.head_row(a) + min(n0 + j, H2 - 1)];
             }
             if constexpr (FUSED)
-                loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
-                                 nullptr);
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, B, dzs, ge > gs ? dscrA : nullptr, 0, 256,
+                                 kTile * gs, kTile * ge);
             else
                 copy_to_lds(dzs, dz, B * A1);
             if (tid < A1 * kTile) whs[tid] = n0 + (tid & 15) < H2 ? wh : 0.0f;
@@ -1198,8 +1264,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
         } else {
             if constexpr (FUSED)
-                loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, B, dzs,
-                                 nullptr);
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, B, dzs, ge > gs ? dscrA : nullptr, 0, 256,
+                                 kTile * gs, kTile * ge);
             else
                 copy_to_lds(dzs, dz, B * A1);
             if (tid < A1 * kTile) {
@@ -1222,23 +1288,67 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         }
         __syncthreads();
         GS_STAMP(0)
-        // dh2 = relu'(h2) * (dz . Wh), in place; lane owns hidden unit i, rows stride 16
-        {
-            const int i = tid & 15;
-            float w[kMaxActions + 1];
+        const int nch = Bp / kTile;
+        const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
+        // the ka dW2 tiles; k-block-0 workgroups also form db2[n] = sum_b dh2[b, n]: from the A
+        // operands they already hold (fast path), or as an MFMA against a ones operand (t == ka)
+        const bool fast = A1 <= 5;
+        const int nt = sh.ka + (!fast && kb == 0 ? 1 : 0);
+        if constexpr (FUSED)      // this workgroup's metric row groups (rows' sums from the loss pass)
+            for (int g = gs; g < ge; ++g)
+                store_metric_groups(dscrA + (int64_t)(g - gs) * kTile * kNumSums, kTile, g * kTile, B, kstep,
+                                    ff.mpart);
+        if (fast) {
+            // dh2 = relu'(h2) * (dz . Wh) formed in registers as the MFMA's A operand (lane: hidden
+            // unit n0 + li, rows b..b+3 of its K chunk), with the two-phase path's arithmetic and
+            // order, so no dh2 tile goes through LDS and one barrier less; the chunk's operand
+            // feeds every tile of the workgroup
+            float w[5];
 #pragma unroll
-            for (int a = 0; a < kMaxActions + 1; ++a) w[a] = a < A1 ? whs[a * 16 + i] : 0.0f;
-            if (A1 <= 5) {
-                // branch-free body so the unrolled iterations' LDS reads issue together
-#pragma unroll 8
-                for (int b = tid >> 4; b < Bp; b += 16) {
-                    const bool on = (mkA[b] >> i) & 1;
-                    float s = 0.0f;
+            for (int a = 0; a < 5; ++a) w[a] = a < A1 ? whs[a * 16 + li] : 0.0f;
+            f32x4 acc[3][2];
 #pragma unroll
-                    for (int a = 0; a < 5; ++a) s = a < A1 ? fmaf(dzs[b * A1 + a], w[a], s) : s;
-                    dh2T[i * ld + b] = on ? s : 0.0f;
+            for (int t = 0; t < 3; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float dsum = 0.0f;      // db2 partial of this lane's rows (k-block 0)
+#pragma unroll 2
+            for (int ch = ch0; ch < ch1; ++ch) {
+                const int b = ch * kTile + 4 * lq;
+                float av[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    float sacc = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < 5; ++a) sacc = a < A1 ? fmaf(dzs[(b + c) * A1 + a], w[a], sacc) : sacc;
+                    av[c] = (mkA[b + c] >> li) & 1 ? sacc : 0.0f;
                 }
-            } else {
+                if (kb == 0) dsum = (((dsum + av[0]) + av[1]) + av[2]) + av[3];
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    if (t >= nt) break;
+                    const float4 bb = t == sh.ka ? make_float4(1.f, 1.f, 1.f, 1.f)
+                                                 : *reinterpret_cast<const float4 *>(h1T + (t * kTile + li) * ld + b);
+                    acc[t][0] = mfma4(av[0], bb.x, acc[t][0]);
+                    acc[t][1] = mfma4(av[1], bb.y, acc[t][1]);
+                    acc[t][0] = mfma4(av[2], bb.z, acc[t][0]);
+                    acc[t][1] = mfma4(av[3], bb.w, acc[t][1]);
+                }
+            }
+            GS_STAMP(1)
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                if (t >= nt) break;
+                const f32x4 at = acc[t][0] + acc[t][1];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[(wave * 3 + t) * 256 + (lq * 4 + r) * kTile + li] = at[r];
+            }
+            if (kb == 0) red[(wave * 3 + 2) * 256 + lq * kTile + li] = dsum;   // slab 2 is free (nt <= 2)
+        } else {
+            // dh2 = relu'(h2) * (dz . Wh), in place; lane owns hidden unit i, rows stride 16
+            {
+                const int i = tid & 15;
+                float w[kMaxActions + 1];
+#pragma unroll
+                for (int a = 0; a < kMaxActions + 1; ++a) w[a] = a < A1 ? whs[a * 16 + i] : 0.0f;
                 for (int b = tid >> 4; b < Bp; b += 16) {
                     const bool on = (mkA[b] >> i) & 1;
                     float s = 0.0f;
@@ -1247,32 +1357,27 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     dh2T[i * ld + b] = on ? s : 0.0f;
                 }
             }
-        }
-        __syncthreads();
-        GS_STAMP(1)
-        const int nch = Bp / kTile;
-        const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
-        // t < ka: dW2 tiles; t == ka (k-block-0 workgroups only): db2[n] = sum_b dh2[b, n] as an
-        // MFMA against a ones operand (every output column equals db2)
-        const int nt = sh.ka + (kb == 0 ? 1 : 0);
-        for (int t = 0; t < nt; ++t) {
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-            const float *hb = h1T + t * kTile * ld;
-            const bool ones = t == sh.ka;
+            __syncthreads();
+            GS_STAMP(1)
+            for (int t = 0; t < nt; ++t) {
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                const float *hb = h1T + t * kTile * ld;
+                const bool ones = t == sh.ka;
 #pragma unroll 4
-            for (int ch = ch0; ch < ch1; ++ch) {
-                const int b = ch * kTile + 4 * lq;
-                const float4 a = *reinterpret_cast<const float4 *>(dh2T + li * ld + b);
-                const float4 bb = ones ? make_float4(1.f, 1.f, 1.f, 1.f)
-                                       : *reinterpret_cast<const float4 *>(hb + li * ld + b);
-                acc0 = mfma4(a.x, bb.x, acc0);
-                acc1 = mfma4(a.y, bb.y, acc1);
-                acc0 = mfma4(a.z, bb.z, acc0);
-                acc1 = mfma4(a.w, bb.w, acc1);
-            }
-            const f32x4 acc = acc0 + acc1;
+                for (int ch = ch0; ch < ch1; ++ch) {
+                    const int b = ch * kTile + 4 * lq;
+                    const float4 a = *reinterpret_cast<const float4 *>(dh2T + li * ld + b);
+                    const float4 bb = ones ? make_float4(1.f, 1.f, 1.f, 1.f)
+                                           : *reinterpret_cast<const float4 *>(hb + li * ld + b);
+                    acc0 = mfma4(a.x, bb.x, acc0);
+                    acc1 = mfma4(a.y, bb.y, acc1);
+                    acc0 = mfma4(a.z, bb.z, acc0);
+                    acc1 = mfma4(a.w, bb.w, acc1);
+                }
+                const f32x4 acc = acc0 + acc1;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) red[(wave * 3 + t) * 256 + (lq * 4 + r) * kTile + li] = acc[r];
+                for (int r = 0; r < 4; ++r) red[(wave * 3 + t) * 256 + (lq * 4 + r) * kTile + li] = acc[r];
+            }
         }
         __syncthreads();
         GS_STAMP(2)
@@ -1288,16 +1393,28 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 gv[j] = g;
                 ok[j] = t < sh.ka ? (n0 + row < H2 && k0 + t * kTile + col < H1) : (col == 0 && n0 + row < H2);
             }
+            // db2 element of this thread: n0 + row (ones tile, col 0) or n0 + tid (fast path: the 16
+            // (wave, lane group) partials of column tid, in order)
+            int db2n = n0 + row;
+            if (fast && kb == 0) {
+                db2n = n0 + tid;
+                float d = 0.0f;
+                if (tid < kTile)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) d += red[((q >> 2) * 3 + 2) * 256 + (q & 3) * kTile + tid];
+                gv[2] = d;
+                ok[2] = tid < kTile && n0 + tid < H2;
+            }
             if (xchg) bwd_exchange<3>(bx, xseq, gv, ok);
             float sqt[3] = {0.0f, 0.0f, 0.0f};
-            for (int t = 0; t < nt; ++t) {
-                const int j = t < sh.ka ? t : 2;
-                if (!ok[j]) continue;
-                if (t < sh.ka)
-                    G[L.oW2 + (int64_t)(n0 + row) * H1 + k0 + t * kTile + col] = gv[j];
-                else
-                    G[L.ob2 + n0 + row] = gv[j];
-                sqt[j] = gv[j] * gv[j];
+            for (int t = 0; t < sh.ka; ++t) {
+                if (!ok[t]) continue;
+                G[L.oW2 + (int64_t)(n0 + row) * H1 + k0 + t * kTile + col] = gv[t];
+                sqt[t] = gv[t] * gv[t];
+            }
+            if (ok[2]) {
+                G[L.ob2 + db2n] = gv[2];
+                sqt[2] = gv[2] * gv[2];
             }
             block_reduce<3>(sqt, reinterpret_cast<float *>(mkA + Bp));   // 3 x (256 + 16) floats
             if (tid == 0) {
@@ -1306,6 +1423,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
         }
         GS_STAMP_END(3)
+        if constexpr (FUSED) GS_SPAN_END(1, kstep)
         return;
     }
     bid -= sh.nA;
@@ -1339,6 +1457,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         // waves 0-2 stream the slab's operands into LDS while wave 3 computes its loss rows
         // (fused path): the loss math overlaps the loads instead of following them
         constexpr int kLd = FUSED ? 192 : 256;
+        const bool dh2_regs = A1 <= 5 && H2 % 64 == 0;
         int *mkB = reinterpret_cast<int *>(kred + 1024);   // [32][ncb] relu'(h2) bits
         if constexpr (S::H1c > 0 && S::Bc > 0) {
             // compile-time shapes: every operand load of the slab is issued before the first
@@ -1444,8 +1563,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         }
 #endif
         if constexpr (FUSED)      // the kb == 0 slab also keeps its rows' metric sums
-            loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), b0, kRowsB,
-                             dzs, kb == 0 ? reinterpret_cast<double *>(kred) : nullptr, kLd, 256 - kLd);
+            loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, b0, kRowsB, dzs, nullptr, kLd, 256 - kLd);
 #ifdef GS_STAMPS
         if (bid == 0 && tid == 192) {   // loss wave: its rows' loss + gradient
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1458,10 +1576,47 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 dzs[u] = b0 * A1 + u < B * A1 ? dz[(int64_t)b0 * A1 + u] : 0.0f;
         __syncthreads();
         GS_STAMP(0)
-        if constexpr (FUSED)
-            if (kb == 0)
-                store_metric_groups(reinterpret_cast<const double *>(kred), kRowsB, b0, B,
-                                    ff.k_local + (ff.step_base ? *ff.step_base : 0), ff.mpart);
+        // 32 rows = 2 row tiles; waves (0,1) / (2,3) split K = H2 of tile 0 / 1 in halves
+        const int nchB = H2p / kTile;
+        const int rt = wave >> 1, half = wave & 1;
+        const int chb = half ? nchB / 2 : 0, che = half ? nchB : nchB / 2;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        if (dh2_regs) {
+            // dh2 = relu'(h2) * (dz . Wh) formed in registers as the MFMA's A operand (lane: slab
+            // row rt*16 + li, hidden units n..n+3 of its K chunk), with the two-phase path's
+            // arithmetic and order: no dh2 slab through LDS, one barrier less
+            const int row = rt * 16 + li;
+            float dzr[5];
+#pragma unroll
+            for (int a = 0; a < 5; ++a) dzr[a] = a < A1 ? dzs[row * A1 + a] : 0.0f;
+            const float *brow = W2T + li * ld;
+#pragma unroll 2
+            for (int ch = chb; ch < che; ++ch) {
+                const int n = ch * kTile + 4 * lq;
+                const unsigned m = (unsigned)(mkB[row * sh.ncb + ch] >> (4 * lq));
+                float4 wh[5];
+#pragma unroll
+                for (int a = 0; a < 5; ++a)
+                    wh[a] = a < A1 ? *reinterpret_cast<const float4 *>(whs + a * H2 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+                float av[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float sacc = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < 5; ++a) {
+                        const float wv = j == 0 ? wh[a].x : j == 1 ? wh[a].y : j == 2 ? wh[a].z : wh[a].w;
+                        sacc = a < A1 ? fmaf(dzr[a], wv, sacc) : sacc;
+                    }
+                    av[j] = ((m >> j) & 1u) ? sacc : 0.0f;
+                }
+                const float4 w = *reinterpret_cast<const float4 *>(brow + n);
+                acc0 = mfma4(av[0], w.x, acc0);
+                acc1 = mfma4(av[1], w.y, acc1);
+                acc0 = mfma4(av[2], w.z, acc0);
+                acc1 = mfma4(av[3], w.w, acc1);
+            }
+            GS_STAMP(1)
+        } else {
         // dh2 = relu'(h2) * (dz . Wh), in place
         if (A1 <= 5 && H2 <= 1024 && 1024 % H2 == 0) {
             // thread owns 4 consecutive hidden units (4 mask bits of one word, one float4 store)
@@ -1473,21 +1628,32 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             for (int a = 0; a < 5; ++a)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) w[a][j] = a < A1 ? whs[a * H2 + n0 + j] : 0.0f;
-#pragma unroll 4
-            for (int i = tid / nt; i < kRowsB; i += rstep) {
-                const unsigned m = (unsigned)(mkB[i * sh.ncb + nb] >> sh4);
-                float dzr[5];
+            // 8 rows at a time, all their LDS reads before their stores (the dh2s stores may
+            // alias mkB / dzs as far as the compiler knows)
+            for (int i0 = tid / nt; i0 < kRowsB; i0 += 8 * rstep) {
+                unsigned mm[8];
+                float dzr[8][5];
 #pragma unroll
-                for (int a = 0; a < 5; ++a) dzr[a] = a < A1 ? dzs[i * A1 + a] : 0.0f;
-                float o[4];
+                for (int c = 0; c < 8; ++c) {
+                    const int i = min(i0 + c * rstep, kRowsB - 1);
+                    mm[c] = (unsigned)(mkB[i * sh.ncb + nb] >> sh4);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float sacc = 0.0f;
-#pragma unroll
-                    for (int a = 0; a < 5; ++a) sacc = a < A1 ? fmaf(dzr[a], w[a][j], sacc) : sacc;
-                    o[j] = ((m >> j) & 1u) ? sacc : 0.0f;
+                    for (int a = 0; a < 5; ++a) dzr[c][a] = a < A1 ? dzs[i * A1 + a] : 0.0f;
                 }
-                *reinterpret_cast<float4 *>(dh2s + i * ld + n0) = make_float4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const int i = i0 + c * rstep;
+                    float o[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float sacc = 0.0f;
+#pragma unroll
+                        for (int a = 0; a < 5; ++a) sacc = a < A1 ? fmaf(dzr[c][a], w[a][j], sacc) : sacc;
+                        o[j] = ((mm[c] >> j) & 1u) ? sacc : 0.0f;
+                    }
+                    if (i < kRowsB)
+                        *reinterpret_cast<float4 *>(dh2s + i * ld + n0) = make_float4(o[0], o[1], o[2], o[3]);
+                }
             }
         } else
         // thread owns hidden unit n, loops the rows
@@ -1522,13 +1688,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         __syncthreads();
         GS_STAMP(1)
         {
-            // 32 rows = 2 row tiles; waves (0,1) / (2,3) split K = H2 of tile 0 / 1 in halves
-            const int nch = H2p / kTile;
-            const int rt = wave >> 1, half = wave & 1;
-            const int chb = half ? nch / 2 : 0, che = half ? nch : nch / 2;
             const float *arow = dh2s + (rt * 16 + li) * ld;
             const float *brow = W2T + li * ld;
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
             for (int ch = chb; ch < che; ++ch) {
                 const int n = ch * kTile + 4 * lq;
@@ -1539,6 +1700,9 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 acc0 = mfma4(a.z, w.z, acc0);
                 acc1 = mfma4(a.w, w.w, acc1);
             }
+        }
+        }
+        {
             const f32x4 acc = acc0 + acc1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) kred[wave * 256 + (lq * 4 + r) * kTile + li] = acc[r];
@@ -1598,6 +1762,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
         }
         GS_STAMP_END(3)
+        if constexpr (FUSED) GS_SPAN_END(1, kstep)
         return;
     }
     bid -= sh.nB;
@@ -1751,6 +1916,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             block_sumsq_store(sqb, sumsq + sh.nT + 2 * sh.ncb, sbuf);
         }
         GS_STAMP_END(1)
+        if constexpr (FUSED) GS_SPAN_END(1, kstep)
     }
 }
 
@@ -2351,6 +2517,21 @@ extern "C" int gs_debug_stamps(unsigned long long *acc_out, unsigned long long *
 {
     GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(g_stamp_acc), sizeof(unsigned long long) * 128));
     GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(g_stamp_cnt), sizeof(unsigned long long) * 8));
+    return GS_OK;
+}
+
+// chain timeline: zero / read the 2 x kSpanK x kSpanWG x 5 words
+extern "C" int gs_debug_span_reset()
+{
+    void *p = nullptr;
+    GS_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(g_span)));
+    GS_HIP(hipMemset(p, 0, sizeof(unsigned) * 2 * kSpanK * kSpanWG * 5));
+    GS_HIP(hipDeviceSynchronize());
+    return GS_OK;
+}
+extern "C" int gs_debug_span_read(unsigned *out)
+{
+    GS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_span), sizeof(unsigned) * 2 * kSpanK * kSpanWG * 5));
     return GS_OK;
 }
 #endif

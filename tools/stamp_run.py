@@ -33,8 +33,13 @@ torch.cuda.synchronize()
 acc0 = np.zeros(128, np.uint64)
 cnt0 = np.zeros(8, np.uint64)
 _lib.lib.gs_debug_stamps(acc0.ctypes.data, cnt0.ctypes.data)
+_lib.lib.gs_debug_span_reset.argtypes = []
+_lib.lib.gs_debug_span_read.argtypes = [ctypes.c_void_p]
+_lib.lib.gs_debug_span_reset()
 agent.train_epoch()
 torch.cuda.synchronize()
+span = np.zeros((2, 2048, 288, 5), np.uint32)
+_lib.lib.gs_debug_span_read(span.ctypes.data)
 acc = np.zeros(128, np.uint64)
 cnt = np.zeros(8, np.uint64)
 _lib.lib.gs_debug_stamps(acc.ctypes.data, cnt.ctypes.data)
@@ -58,3 +63,28 @@ for k, (n, phases) in names.items():
     print(f"{n:18s} launches {int(cnt[k]):6d}  total {tot:8.0f} cyc = {tot / 2.4e3:6.2f} us")
     for i, ph in enumerate(phases):
         print(f"    {ph:24s} {per[i]:8.0f} cyc  {per[i] / 2.4e3:6.2f} us")
+
+# chain timeline of the second update's first 2048 minibatches (100 MHz device clock -> us):
+# kernel spans from the first workgroup start to the last wave end, and the gaps between kernels
+n = min(agent.n_minibatches, 2048)
+sp = span[:, :n].astype(np.int64)
+ref = int(sp[0, 0, 0, 0])
+rel = ((sp - ref + 2**31) % 2**32 - 2**31).astype(np.float64) / 100.0   # wrap-safe, us
+live = span[:, :n, :, 0] != 0                                           # workgroups that ran
+st = np.where(live, rel[..., 0], np.inf).min(axis=2)                     # (2, n) first start
+en = np.where(live[..., None], rel[..., 1:], -np.inf).max(axis=(2, 3))   # (2, n) last wave end
+wg_end = np.where(live, rel[..., 1:].max(axis=3), np.nan)               # per-workgroup end
+pct = lambda x: f"mean {np.mean(x):6.2f}  p10 {np.percentile(x, 10):6.2f}  p50 {np.median(x):6.2f}  p90 {np.percentile(x, 90):6.2f}"
+print(f"chain timeline over {n} minibatches (us)")
+print("    fwd span (first WG start -> last wave end)", pct(en[0] - st[0]))
+print("    fwd end -> bwd first WG start             ", pct(st[1] - en[0]))
+print("    bwd span                                   ", pct(en[1] - st[1]))
+print("    bwd end -> next fwd first WG start         ", pct(st[0, 1:] - en[1, :-1]))
+print("    minibatch period (fwd start -> next)       ", pct(np.diff(st[0])))
+# which workgroups end last: per kernel, the mean (end - kernel start) of each workgroup
+for kern, name, nwg in ((0, "fwd", 256), (1, "bwd", 273)):
+    e = np.nanmean(wg_end[kern, :, :nwg] - st[kern][:, None], axis=0)
+    s0 = np.nanmean(rel[kern, :, :nwg, 0] - st[kern][:, None], axis=0)
+    order = np.argsort(-e)[:6]
+    print(f"    {name}: latest-ending workgroups " + ", ".join(f"#{w} start {s0[w]:.2f} end {e[w]:.2f}" for w in order))
+    print(f"    {name}: workgroup start spread p50 {np.median(s0):.2f} max {s0.max():.2f}; end p50 {np.median(e):.2f}")
