@@ -46,6 +46,8 @@ namespace gs {
 #ifdef GS_STAMPS
 __device__ unsigned long long g_stamp_acc[8][16];
 __device__ unsigned long long g_stamp_cnt[8];
+#endif
+#if defined(GS_STAMPS) || defined(GS_SPANS)
 // chain timeline (diagnostic build): per minibatch k < kSpanK and workgroup, the start (thread 0)
 // and each wave's end after its memory ops drained, low 32 bits of s_memrealtime (100 MHz, one
 // clock for the whole device); plain per-workgroup stores (atomics on shared words would
@@ -1046,17 +1048,10 @@ __device__ __forceinline__ void block_sumsq_store(float v, float *slot, float *s
     if (threadIdx.x == 0) *slot = t[0];
 }
 
-// The role-A workgroup that stores metric row group g (16 rows) of a minibatch of G groups:
-// spread over the nA workgroups, off the k-block-0 ones (they also form db2) when there is room
-__host__ __device__ inline int metric_owner(int g, int G, int nA)
-{
-    if (G <= nA) {
-        const int stride = nA / G;
-        return g * stride + (stride > 1 ? 1 : 0);
-    }
-    return (int)(((int64_t)g * nA) / G);
-}
-__host__ __device__ inline int metric_groups_per_wg(int G, int nA) { return G <= nA ? 1 : (G + nA - 1) / nA; }
+// The role-C workgroup that stores metric row group g (16 rows) of a minibatch of G groups: a
+// contiguous range of groups per workgroup
+__host__ __device__ inline int metric_owner(int g, int G, int nW) { return G <= nW ? g : (int)(((int64_t)g * nW) / G); }
+__host__ __device__ inline int metric_groups_per_wg(int G, int nW) { return G <= nW ? 1 : (G + nW - 1) / nW; }
 
 struct BwdShape {
     int ncb, nkb, nrbB, ka, nT, nA, nB, nC;
@@ -1083,12 +1078,12 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
     const int64_t H2p = (L.H2 + 63) / 64 * 64;
     const BwdShape shp = BwdShape::make(L, (int)B);
-    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 3 * kTile * (Bp64 + 4) + 3072 + Bp64 + 816 + 2 +
-                          (int64_t)metric_groups_per_wg((int)B / kTile, shp.nA) * kTile * kNumSums * 2;
+    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 3 * kTile * (Bp64 + 4) + 3072 + Bp64 + 816;
     const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
                           kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024 +
                           (int64_t)kRowsB * n_col_blocks(L.H2);
-    const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + (A1 * 256 > 1024 ? A1 * 256 : 1024);
+    const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + (A1 * 256 > 1024 ? A1 * 256 : 1024) + 2 +
+                          (int64_t)metric_groups_per_wg((int)B / kTile, shp.nC) * kTile * kNumSums * 2;
     int64_t m = roleA;
     if (roleB > m) m = roleB;
     if (roleC > m) m = roleC;
@@ -1200,21 +1195,6 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         // relu'(h2) bits of this n-block (one word per row) and the h1 column tile (16 contiguous
         // floats per row = 4 float4, transposed into LDS); dh2T is filled by the dh2 pass
         int *mkA = reinterpret_cast<int *>(red + 3072);   // [Bp]
-        // metric row groups this workgroup stores (fused path): rows [16 gs, 16 ge), their 14 sums
-        // each in dscrA (after mkA and block_reduce's scratch)
-        int gs = 0, ge = 0;
-        if constexpr (FUSED) {
-            const int G = B / kTile;
-            gs = G;
-            for (int g = 0; g < G; ++g)
-                if (metric_owner(g, G, sh.nA) == bid) {
-                    gs = min(gs, g);
-                    ge = g + 1;
-                }
-            if (ge == 0) gs = 0;
-        }
-        double *dscrA = reinterpret_cast<double *>(
-            (reinterpret_cast<uintptr_t>(reinterpret_cast<float *>(mkA + Bp) + 816) + 7) & ~(uintptr_t)7);
         if constexpr (S::H1c > 0 && S::Bc > 0) {
             // compile-time shapes: the tile loads are issued before the loss rows, which
             // then run while they are in flight; LDS writes follow
@@ -1243,8 +1223,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 wh = P[L.head_row(a) + min(n0 + j, H2 - 1)];
             }
             if constexpr (FUSED)
-                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, B, dzs, ge > gs ? dscrA : nullptr, 0, 256,
-                                 kTile * gs, kTile * ge);
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, B, dzs, nullptr);
             else
                 copy_to_lds(dzs, dz, B * A1);
             if (tid < A1 * kTile) whs[tid] = n0 + (tid & 15) < H2 ? wh : 0.0f;
@@ -1264,8 +1243,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
             }
         } else {
             if constexpr (FUSED)
-                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, B, dzs, ge > gs ? dscrA : nullptr, 0, 256,
-                                 kTile * gs, kTile * ge);
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, B, dzs, nullptr);
             else
                 copy_to_lds(dzs, dz, B * A1);
             if (tid < A1 * kTile) {
@@ -1294,10 +1272,6 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         // operands they already hold (fast path), or as an MFMA against a ones operand (t == ka)
         const bool fast = A1 <= 5;
         const int nt = sh.ka + (!fast && kb == 0 ? 1 : 0);
-        if constexpr (FUSED)      // this workgroup's metric row groups (rows' sums from the loss pass)
-            for (int g = gs; g < ge; ++g)
-                store_metric_groups(dscrA + (int64_t)(g - gs) * kTile * kNumSums, kTile, g * kTile, B, kstep,
-                                    ff.mpart);
         if (fast) {
             // dh2 = relu'(h2) * (dz . Wh) formed in registers as the MFMA's A operand (lane: hidden
             // unit n0 + li, rows b..b+3 of its K chunk), with the two-phase path's arithmetic and
@@ -1774,10 +1748,25 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         GS_STAMP_BEGIN_IF(5, bid == 0)
         float *hs = lds;                    // [Bp][17]
         float *dzs = hs + Bp * 17;          // [Bp][A1]
+        // metric row groups this workgroup stores (fused path): rows [16 gs, 16 ge), their 14 sums
+        // each in dscrC (after partC)
+        int gs = 0, ge = 0;
+        if constexpr (FUSED) {
+            const int G = B / kTile;
+            gs = G;
+            for (int g = 0; g < G; ++g)
+                if (metric_owner(g, G, sh.nC) == nb) {
+                    gs = min(gs, g);
+                    ge = g + 1;
+                }
+            if (ge == 0) gs = 0;
+        }
+        double *dscrC = reinterpret_cast<double *>(
+            (reinterpret_cast<uintptr_t>(dzs + Bp * A1 + (A1 * 256 > 1024 ? A1 * 256 : 1024)) + 7) & ~(uintptr_t)7);
         auto loss_in = [&]() {
             if constexpr (FUSED)
-                loss_rows_lds<S>(P, L, zpart, ff, la, B, ff.k_local + (ff.step_base ? *ff.step_base : 0), 0, Bp, dzs,
-                                 nullptr);
+                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, Bp, dzs, ge > gs ? dscrC : nullptr, 0, 256,
+                                 kTile * gs, kTile * ge);
             else
                 for (int u = tid; u < Bp * A1; u += 256) dzs[u] = u < B * A1 ? dz[u] : 0.0f;
         };
@@ -1820,6 +1809,10 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         }
         __syncthreads();
         GS_STAMP(0)
+        if constexpr (FUSED)      // this workgroup's metric row groups (rows' sums from the loss pass)
+            for (int g = gs; g < ge; ++g)
+                store_metric_groups(dscrC + (int64_t)(g - gs) * kTile * kNumSums, kTile, g * kTile, B, kstep,
+                                    ff.mpart);
         float *partC = dzs + Bp * A1;           // [A1*16][16]
         if (nb < sh.ncb) {
             const int nout = kTile * A1;
@@ -2520,6 +2513,9 @@ extern "C" int gs_debug_stamps(unsigned long long *acc_out, unsigned long long *
     return GS_OK;
 }
 
+#endif
+
+#if defined(GS_STAMPS) || defined(GS_SPANS)
 // chain timeline: zero / read the 2 x kSpanK x kSpanWG x 5 words
 extern "C" int gs_debug_span_reset()
 {

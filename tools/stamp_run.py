@@ -10,12 +10,17 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gymnasium-solver_amd")]
 VARIANT = os.path.join(ROOT, "tools", "libgsamd_stamps.so")
+SPANS = os.path.join(ROOT, "tools", "libgsamd_spans.so")     # timeline only: no per-phase atomics
+SPANS_ONLY = "--spans" in sys.argv
 
 if "--build" in sys.argv:
     import build_lib
     build_lib.build_variant(VARIANT, ["GS_STAMPS"])
-    print("built", VARIANT)
+    build_lib.build_variant(SPANS, ["GS_SPANS"])
+    print("built", VARIANT, SPANS)
     sys.exit(0)
+if SPANS_ONLY:
+    VARIANT = SPANS
 
 os.environ["GSAMD_LIB"] = VARIANT
 import numpy as np  # noqa: E402
@@ -24,7 +29,8 @@ from gsamd import _lib  # noqa: E402
 from gsamd.config import load_config  # noqa: E402
 from gsamd.ppo_agent import DevicePPOAgent  # noqa: E402
 
-_lib.lib.gs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+if not SPANS_ONLY:
+    _lib.lib.gs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 torch.manual_seed(42)
 cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
 agent = DevicePPOAgent(cfg, device="cuda:0", use_graph=True, track_stats=False)
@@ -32,7 +38,8 @@ agent.train_epoch()
 torch.cuda.synchronize()
 acc0 = np.zeros(128, np.uint64)
 cnt0 = np.zeros(8, np.uint64)
-_lib.lib.gs_debug_stamps(acc0.ctypes.data, cnt0.ctypes.data)
+if not SPANS_ONLY:
+    _lib.lib.gs_debug_stamps(acc0.ctypes.data, cnt0.ctypes.data)
 _lib.lib.gs_debug_span_reset.argtypes = []
 _lib.lib.gs_debug_span_read.argtypes = [ctypes.c_void_p]
 _lib.lib.gs_debug_span_reset()
@@ -42,7 +49,8 @@ span = np.zeros((2, 2048, 288, 5), np.uint32)
 _lib.lib.gs_debug_span_read(span.ctypes.data)
 acc = np.zeros(128, np.uint64)
 cnt = np.zeros(8, np.uint64)
-_lib.lib.gs_debug_stamps(acc.ctypes.data, cnt.ctypes.data)
+if not SPANS_ONLY:
+    _lib.lib.gs_debug_stamps(acc.ctypes.data, cnt.ctypes.data)
 acc = (acc - acc0).reshape(8, 16).astype(np.float64)
 cnt = (cnt - cnt0).astype(np.float64)
 names = {0: ("k_fwd_hidden<fused, adam> (0,0)", ["loads landed (waitcnt: stamp build only)", "W1 fold + norm",
@@ -88,3 +96,8 @@ for kern, name, nwg in ((0, "fwd", 256), (1, "bwd", 273)):
     order = np.argsort(-e)[:6]
     print(f"    {name}: latest-ending workgroups " + ", ".join(f"#{w} start {s0[w]:.2f} end {e[w]:.2f}" for w in order))
     print(f"    {name}: workgroup start spread p50 {np.median(s0):.2f} max {s0.max():.2f}; end p50 {np.median(e):.2f}")
+    if kern == 1:      # k_bwd dispatch order: role B, role A, role C (C2: 128 / 128 / 17 workgroups)
+        nBw = nAw = 128
+        for rname, lo, hi in (("B", 0, nBw), ("A", nBw, nBw + nAw), ("C", nBw + nAw, nwg)):
+            r = e[lo:hi]
+            print(f"    bwd role {rname}: end mean {r.mean():.2f} p90 {np.percentile(r, 90):.2f} max {r.max():.2f}")
