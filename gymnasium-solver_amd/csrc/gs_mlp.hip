@@ -170,8 +170,13 @@ __device__ __forceinline__ float adam_param(float graw, float coef, float &m, fl
     // correctly rounded divisions: IEEE division lowers to a v_div_scale / v_div_fmas /
     // v_div_fixup sequence serialised through VCC, ~10x the latency, and this runs 4-21 times
     // per thread on the minibatch chain's critical path
+#ifdef GS_EXP_NO_TRANS      // timing experiment only (wrong results): Adam without sqrt / rcp
+    const float denom = v * inv_bc2s + aa.eps;
+    p = p + neg_step * (m * denom);
+#else
     const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2s + aa.eps;
     p = p + neg_step * (m * __builtin_amdgcn_rcpf(denom));
+#endif
     return g;
 }
 
@@ -260,6 +265,18 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         const int64_t kprev = kstep - 1 + af.force;
         const bool apply = kprev >= 0;
         const bool own1 = apply && cb == 0 && rb == 0, own2 = apply && rb == 0;
+#ifdef GS_EXP_SPLIT_STORES
+        const int gy = (int)gridDim.y, gx = (int)gridDim.x;
+        const bool stW2[3] = {apply && rb == 0, apply && rb == 1 % gy, apply && rb == 2 % gy};
+        const bool stW1[3] = {apply && rb == 3 % gy && cb == 0, apply && rb == 3 % gy && cb == 1 % gx,
+                              apply && rb == 3 % gy && cb == 2 % gx};
+#elif defined(GS_EXP_NO_OWNER_STORES)      // timing experiment only: the new set is never stored
+        const bool stW2[3] = {false, false, false};
+        const bool stW1[3] = {false, false, false};
+#else
+        const bool stW2[3] = {own2, own2, own2};
+        const bool stW1[3] = {own1, own1, own1};
+#endif
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         // global-address-space float4 loads (the AdamFwd pointers would otherwise lower to flat,
         // and a predicated float4 select to four dword loads); the moment / gradient buffers are
@@ -287,7 +304,12 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
 #pragma unroll
             for (int j = 0; j < NQ; ++j)
 #pragma unroll
-                for (int b = 0; b < NRB; ++b) t[j][b] = ld4(af.part1 + (int64_t)b * n1, min(tid + 256 * j, nq1 - 1));
+                for (int b = 0; b < NRB; ++b)
+#ifdef GS_EXP_ONE_PARTIAL      // timing experiment only: one partial row block loaded
+                    t[j][b] = b == 0 ? ld4(af.part1, min(tid + 256 * j, nq1 - 1)) : z4;
+#else
+                    t[j][b] = ld4(af.part1 + (int64_t)b * n1, min(tid + 256 * j, nq1 - 1));
+#endif
         } else {
 #pragma unroll
             for (int j = 0; j < NQ; ++j) {
@@ -394,11 +416,11 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                     adam_param(w1g[fold ? part1_index(Lc, 4 * q + e) : 4 * q + e], coef, m[e], v[e], p[e], aa,
                                neg_step, bc2s);
                 p4 = make_float4(p[0], p[1], p[2], p[3]);
-                if (own1) {
-                    reinterpret_cast<float4 *>(af.Pout)[q] = p4;
-                    reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
-                    reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
-                }
+                // the new W1|b1 p / m / v are stored by three different workgroups of row block 3
+                // (workgroup-uniform choice: one workgroup storing all three drained last)
+                if (stW1[0]) reinterpret_cast<float4 *>(af.Pout)[q] = p4;
+                if (stW1[1]) reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
+                if (stW1[2]) reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
             }
             reinterpret_cast<float4 *>(W1s)[q] = p4;
         }
@@ -414,12 +436,11 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
 #pragma unroll
                 for (int e = 0; e < 4; ++e) adam_param(g[e], coef, m[e], v[e], p[e], aa, neg_step, bc2s);
                 w2r[j] = make_float4(p[0], p[1], p[2], p[3]);
-                if (own2) {
-                    const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
-                    reinterpret_cast<float4 *>(af.Pout)[q] = w2r[j];
-                    reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
-                    reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
-                }
+                // this column block's 16 new W2 rows: p by row block 0, m by 1, v by 2 (16 KB each)
+                const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
+                if (stW2[0]) reinterpret_cast<float4 *>(af.Pout)[q] = w2r[j];
+                if (stW2[1]) reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
+                if (stW2[2]) reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
             }
         }
         auto step_slice = [&](float (&e)[4], int64_t o, bool own) {

@@ -21,6 +21,8 @@ if "--build" in sys.argv:
     sys.exit(0)
 if SPANS_ONLY:
     VARIANT = SPANS
+if "--lib" in sys.argv:      # an experiment variant (tools/ab_build.py)
+    VARIANT = os.path.join(ROOT, sys.argv[sys.argv.index("--lib") + 1])
 
 os.environ["GSAMD_LIB"] = VARIANT
 import numpy as np  # noqa: E402
