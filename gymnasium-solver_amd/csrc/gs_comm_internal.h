@@ -56,7 +56,7 @@ struct gs_comm {
     // off_bwd of the region (gs_common.h BwdXchg), its own per-workgroup counters
     size_t off_bwd;
     uint32_t *seq_bwd;
-    bool bwd_xchg;                                // GS_XGMI_BWD=0 turns it off (separate exchange launch)
+    int bwd_xchg;                                 // 0 off (GS_XGMI_BWD=0), 1 one rank per GPU only, 2 also colocated
     int colocated;                                // most ranks sharing one GPU (gs_comm_xgmi_set_colocation)
 };
 

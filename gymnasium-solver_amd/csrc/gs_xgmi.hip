@@ -379,6 +379,11 @@ int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float 
 bool xgmi_bwd_args(const gs_comm *c, BwdXchg *bx)
 {
     if (c->kind != kCommXgmi || !c->connected || !c->bwd_xchg) return false;
+    // ranks sharing a GPU belong to different processes, whose workgroups the GPU does not keep
+    // resident together: a workgroup waiting for its peer can hold the CU until the scheduler
+    // time-slices the processes (ms per minibatch) — the exchange launch is used there unless
+    // GS_XGMI_BWD=1 asks for the in-backward form anyway
+    if (c->colocated > 1 && c->bwd_xchg != 2) return false;
     *bx = BwdXchg{};
     bx->world = c->nranks;
     bx->rank = c->rank;
@@ -480,10 +485,12 @@ extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint
         }
         c->seq_bwd = (uint32_t *)sb;
     }
-    // the exchange inside the MLP backward; GS_XGMI_BWD=0 keeps a separate exchange launch
-    c->bwd_xchg = true;
+    // the exchange inside the MLP backward: default on with one rank per GPU; GS_XGMI_BWD=0 keeps
+    // a separate exchange launch, GS_XGMI_BWD=1 also uses it for ranks sharing a GPU (tests: the
+    // ranks' kernels then rely on the GPU time-slicing the processes, correct but slow)
+    c->bwd_xchg = 1;
     c->colocated = 1;
-    if (const char *b = getenv("GS_XGMI_BWD")) c->bwd_xchg = b[0] != '0';
+    if (const char *b = getenv("GS_XGMI_BWD")) c->bwd_xchg = b[0] == '0' ? 0 : b[0] == '1' ? 2 : 1;
     // reduce-scatter + all-gather from 4 ranks on (2n/world floats per link instead of n, one more
     // flag round trip); GS_XGMI_ALGO=oneshot|rsag overrides
     c->rsag = nranks >= 4 ? 1 : 0;

@@ -342,9 +342,11 @@ int gs_comm_status(struct gs_comm *comm);
 /* The MLP update's exchange runs inside the backward kernel (every workgroup waits for the
  * same workgroup of its peers), which needs the peers' workgroups to be resident together.
  * That always holds with one rank per GPU (a node); with c ranks sharing a GPU it needs
- * (c - 1) backward grids to leave a free workgroup slot.  The launcher reports the largest
- * number of ranks sharing one GPU here (default 1); where the grids would not fit, the update
- * exchanges with a separate launch after the backward instead.  Host-only, no GPU call. */
+ * (c - 1) backward grids to leave a free workgroup slot, and even then the ranks are separate
+ * processes, which the GPU time-slices rather than co-schedules.  The launcher reports the
+ * largest number of ranks sharing one GPU here (default 1); from 2 the update exchanges with a
+ * separate launch after the backward (GS_XGMI_BWD=1 forces the in-backward form where the grids
+ * fit: correct, but paced by the time-slicing).  Host-only, no GPU call. */
 int gs_comm_xgmi_set_colocation(struct gs_comm *comm, int ranks_per_device);
 int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
 /* What a communicator is: its rank count, this process's rank and the transport
