@@ -438,9 +438,16 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 w2r[j] = make_float4(p[0], p[1], p[2], p[3]);
                 // this column block's 16 new W2 rows: p by row block 0, m by 1, v by 2 (16 KB each)
                 const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
+#ifdef GS_EXP_NT_STORES      // experiment: non-temporal stores for the new W2 rows
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                if (stW2[0]) __builtin_nontemporal_store(f4v{w2r[j].x, w2r[j].y, w2r[j].z, w2r[j].w}, reinterpret_cast<f4v *>(af.Pout) + q);
+                if (stW2[1]) __builtin_nontemporal_store(f4v{m[0], m[1], m[2], m[3]}, reinterpret_cast<f4v *>(af.Mout) + q);
+                if (stW2[2]) __builtin_nontemporal_store(f4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4v *>(af.Vout) + q);
+#else
                 if (stW2[0]) reinterpret_cast<float4 *>(af.Pout)[q] = w2r[j];
                 if (stW2[1]) reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
                 if (stW2[2]) reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
+#endif
             }
         }
         auto step_slice = [&](float (&e)[4], int64_t o, bool own) {
