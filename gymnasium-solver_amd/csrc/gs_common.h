@@ -221,6 +221,28 @@ struct BwdXchg {
     uint32_t *err;                     // sticky error word of the own region
 };
 
+// One-launch rollout of the synthetic env (gs_mlp.hip k_rollout_synth)
+struct SynthEnvArgs {
+    int32_t *state;                  // [N][4] {k, episode, len, -}
+    float *ep_ret, *obs;             // [N], [N][D]: running return, current observation
+    int32_t *ep_cnt;                 // [N] finished-episode counters (may be null)
+    float *ep_ret_sum, *ep_len_sum;
+    int L, trunc_every;
+    float reward;
+    uint64_t seed, step0;            // env seed, vector steps taken before this rollout
+    int64_t env_offset;
+};
+struct RolloutRows {                 // time-major (T, N) rows of the rollout buffer
+    float *obs;                      // (T, N, D)
+    int64_t *actions;                // replayed from (mode 2) or written
+    float *logp, *value, *reward;
+    uint8_t *done, *timeout;
+};
+
+bool rollout_synth_fits(const Layout &L);
+int launch_rollout_synth(const float *P, const Layout &L, int64_t N, int T, int mode, uint64_t rng_seed,
+                         uint64_t counter0, const SynthEnvArgs &ev, const RolloutRows &rw, hipStream_t s);
+
 inline int n_col_blocks(int H) { return (H + kTile - 1) / kTile; }
 inline int n_sumsq_slots(const Layout &L) { return n_col_blocks(L.H2) * n_col_blocks(L.H1) + 2 * n_col_blocks(L.H2) + 1; }
 

@@ -5,22 +5,11 @@
 // rows, so a rollout step never leaves HBM (the reference crosses host<->device three
 // times per step, utils/rollout_collector.py:476-534).
 #include "gs_common.h"
+#include "gs_synth_env.h"
 
 namespace {
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x)
-{
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-
-__device__ __forceinline__ float synth_obs(uint64_t seed, uint64_t env, uint64_t step, uint64_t dim)
-{
-    const uint64_t h = mix64(mix64(mix64(mix64(seed) ^ env) ^ step) ^ dim);
-    return (float)(uint32_t)(h >> 40) * 1.1920928955078125e-07f - 1.0f;   // * 2^-23 - 1, exact
-}
+using gs::synth_obs;
 
 __global__ __launch_bounds__(256) void k_env_reset(int32_t *__restrict__ state, float *__restrict__ ep_ret,
                                                    float *__restrict__ obs, int64_t N, int D, int L, uint64_t seed,
@@ -48,27 +37,17 @@ __global__ __launch_bounds__(256) void k_env_step(int32_t *__restrict__ state, f
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= N) return;
     if (clock) step_count += clock[1];      // rollout clock (graph replay)
-    int k = state[4 * e + 0] + 1;
-    int epi = state[4 * e + 1];
-    int len = state[4 * e + 2] + 1;
-    float er = ep_ret[e] + reward;
-    const bool done = k >= L;
-    const bool trunc_ep = trunc_every > 0 && (epi % trunc_every) == trunc_every - 1;
-    rew_row[e] = reward;
-    done_row[e] = done ? 1 : 0;
-    to_row[e] = (done && trunc_ep) ? 1 : 0;
-    if (done) {
-        if (ep_cnt) ep_cnt[e] += 1;
-        if (ep_ret_sum) ep_ret_sum[e] += er;
-        if (ep_len_sum) ep_len_sum[e] += (float)len;
-        k = 0;
-        epi += 1;
-        len = 0;
-        er = 0.0f;
-    }
-    state[4 * e + 0] = k;
-    state[4 * e + 1] = epi;
-    state[4 * e + 2] = len;
+    int32_t st[3] = {state[4 * e + 0], state[4 * e + 1], state[4 * e + 2]};
+    float er = ep_ret[e];
+    const gs::SynthStep o = gs::synth_env_step(st, er, L, trunc_every, reward, ep_cnt ? ep_cnt + e : nullptr,
+                                               ep_ret_sum ? ep_ret_sum + e : nullptr,
+                                               ep_len_sum ? ep_len_sum + e : nullptr);
+    rew_row[e] = o.reward;
+    done_row[e] = o.done ? 1 : 0;
+    to_row[e] = o.timeout ? 1 : 0;
+    state[4 * e + 0] = st[0];
+    state[4 * e + 1] = st[1];
+    state[4 * e + 2] = st[2];
     ep_ret[e] = er;
     const uint64_t ge = (uint64_t)(env_offset + e);
     for (int d = 0; d < D; ++d) obs[e * D + d] = synth_obs(seed, ge, step_count, (uint64_t)d);

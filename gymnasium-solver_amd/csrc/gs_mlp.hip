@@ -40,6 +40,7 @@
 
 #include "gs_common.h"
 #include "gs_xgmi_dev.h"
+#include "gs_synth_env.h"
 
 namespace gs {
 
@@ -816,30 +817,23 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x)
 // k_heads_act: rollout head — logits/value from partials, action select, log_prob.
 // one thread per env row.
 // ------------------------------------------------------------------------------------
-template <class S>
-__global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, Layout Lrt,
-                                                   const float *__restrict__ zpart, int64_t rows, int mode,
-                                                   uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
-                                                   float *__restrict__ logp, float *__restrict__ value,
-                                                   const uint64_t *__restrict__ clock)
+// value, action (sampled / argmax / replayed) and its log-prob of one env row from its raw
+// logits | value z; ctr = the rollout step's counter of the counter-based uniform
+template <int AMAX>
+__device__ __forceinline__ void head_act_row(const float (&z)[AMAX + 1], int A, int mode, uint64_t seed, uint64_t ctr,
+                                             int64_t r, int64_t *__restrict__ action, float *__restrict__ logp,
+                                             float *__restrict__ value)
 {
-    constexpr int AMAX = S::AMAX, AEX = S::AEX;
-    const Layout L = S::lay(Lrt);
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= rows) return;
-    const int A = L.A;
-    float z[AMAX + 1];
-    gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
     float v = 0.0f;
 #pragma unroll
     for (int a = 0; a < AMAX + 1; ++a)
         if (a == A) v = z[a];
-    if (value) value[r] = v;
-    if (!actions) return;
+    if (value) *value = v;
+    if (!action) return;
     const HeadRow h = head_stats<AMAX>(z, A);
     int act = 0;
     if (mode == 2) {            // replay recorded actions
-        act = (int)actions[r];
+        act = (int)*action;
     } else if (mode == 1) {     // Categorical.mode = probs.argmax(-1), first max wins
         float best = -INFINITY;
 #pragma unroll
@@ -849,9 +843,8 @@ __global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, 
                 if (p > best) { best = p; act = a; }
             }
         }
-        actions[r] = act;
+        *action = act;
     } else {                    // inverse-CDF sample with a counter-based uniform
-        const uint64_t ctr = counter + (clock ? clock[0] : 0ull);   // rollout clock (graph replay)
         const uint64_t hh = mix64(mix64(mix64(seed) ^ ctr) ^ (uint64_t)r);
         const float u = (float)(hh >> 40) * (1.0f / 16777216.0f);
         float c = 0.0f;
@@ -864,13 +857,240 @@ __global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, 
             }
         }
         if (act < 0) act = A - 1;
-        actions[r] = act;
+        *action = act;
     }
     float za = 0.0f;
 #pragma unroll
     for (int a = 0; a < AMAX; ++a)
         if (a == act) za = z[a];
-    logp[r] = za - h.lse;
+    *logp = za - h.lse;
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void k_heads_act(const float *__restrict__ P, Layout Lrt,
+                                                   const float *__restrict__ zpart, int64_t rows, int mode,
+                                                   uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
+                                                   float *__restrict__ logp, float *__restrict__ value,
+                                                   const uint64_t *__restrict__ clock)
+{
+    constexpr int AMAX = S::AMAX, AEX = S::AEX;
+    const Layout L = S::lay(Lrt);
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    float z[AMAX + 1];
+    gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
+    const uint64_t ctr = counter + (clock && mode == 0 ? clock[0] : 0ull);   // rollout clock (graph replay)
+    head_act_row<AMAX>(z, L.A, mode, seed, ctr, r, actions ? actions + r : nullptr, logp ? logp + r : nullptr,
+                       value ? value + r : nullptr);
+}
+
+// ------------------------------------------------------------------------------------
+// k_rollout_synth: a whole rollout of the synthetic env in one launch (C3-sized MLPs, whose
+// weights fit in LDS).  Workgroup = 16 envs (one MFMA row tile) for all T vector steps: the
+// policy's act with gs_policy_act's arithmetic in its order (h1 fmaf chain + bias; each h2
+// column block's 4 K-range MFMA partials summed in range order, as the 4 waves of
+// k_fwd_hidden do; partial heads per column block summed in block order as k_heads_act), so the
+// rows are bit-identical to the step-wise rollout; then the env step (gs_synth_env.h).  No
+// launch and no HBM round trip per step: the envs' observations stay in LDS.
+// LDS (floats): W1 [H1*D] b1 [H1] W2 [H2][H1+4] b2 [H2] Wh [A1][H2] bh [round4(A1)] x [16][D]
+//               h1 [16][H1+4] h2 [ncb][16][17] zp [16][ncb][A1]
+// ------------------------------------------------------------------------------------
+size_t rollout_synth_lds_bytes(const Layout &L)
+{
+    const int A1 = L.A + 1, ncb = (L.H2 + kTile - 1) / kTile;
+    const size_t n = round4(L.H1 * L.D) + round4(L.H1) + (size_t)L.H2 * (L.H1 + 4) + round4(L.H2) +
+                     round4(A1 * L.H2) + round4(A1) + round4(kTile * L.D) + kTile * (L.H1 + 4) + (size_t)ncb * kTile * 17 +
+                     round4(kTile * ncb * A1);
+    return n * sizeof(float);
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void k_rollout_synth(const float *__restrict__ P, Layout Lrt, int64_t N, int T,
+                                                       int mode, uint64_t rng_seed, uint64_t counter0, SynthEnvArgs ev,
+                                                       RolloutRows rw)
+{
+    constexpr int AMAX = S::AMAX;
+    const Layout L = S::lay(Lrt);
+    const int D = L.D, H1 = L.H1, H2 = L.H2, A = L.A, A1 = A + 1;
+    const int ncb = (H2 + kTile - 1) / kTile, nch = H1 / kTile, ldh = H1 + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lq = lane >> 4;
+    const int64_t e0 = (int64_t)blockIdx.x * kTile;
+    extern __shared__ float lds[];
+    float *W1s = lds;
+    float *b1s = W1s + round4(H1 * D);
+    float *W2s = b1s + round4(H1);
+    float *b2s = W2s + (size_t)H2 * ldh;
+    float *whs = b2s + round4(H2);
+    float *bhs = whs + round4(A1 * H2);
+    float *xs = bhs + round4(A1);
+    float *h1s = xs + round4(kTile * D);
+    float *h2s = h1s + kTile * ldh;
+    float *zps = h2s + ncb * kTile * 17;
+    // ---- the policy into LDS, once
+    for (int u = tid; u < H1 * D; u += 256) W1s[u] = P[L.oW1 + u];
+    for (int u = tid; u < H1; u += 256) b1s[u] = P[L.ob1 + u];
+    for (int u = tid; u < H2 * (H1 / 4); u += 256) {
+        const int n = u / (H1 / 4), k4 = u - n * (H1 / 4);
+        *reinterpret_cast<float4 *>(W2s + n * ldh + 4 * k4) =
+            *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)n * H1 + 4 * k4);
+    }
+    for (int u = tid; u < H2; u += 256) b2s[u] = P[L.ob2 + u];
+    for (int u = tid; u < A1 * H2; u += 256) {
+        const int a = u / H2, n = u - a * H2;
+        whs[u] = P[L.head_row(a) + n];
+    }
+    if (tid < A1) bhs[tid] = P[L.head_bias(tid)];
+    // ---- this workgroup's envs: state in registers of threads 0..15, observations in LDS
+    const int64_t me = e0 + (tid < kTile ? tid : 0);
+    const bool env_thread = tid < kTile && me < N;
+    int32_t st[3] = {0, 0, 0};
+    float er = 0.0f;
+    if (env_thread) {
+        st[0] = ev.state[4 * me + 0];
+        st[1] = ev.state[4 * me + 1];
+        st[2] = ev.state[4 * me + 2];
+        er = ev.ep_ret[me];
+    }
+    for (int u = tid; u < kTile * D; u += 256) {
+        const int i = u / D;
+        xs[u] = e0 + i < N ? ev.obs[(e0 + i) * D + (u - i * D)] : 0.0f;
+    }
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+        const int64_t row0 = (int64_t)t * N;
+        // obs row t of the buffer (the observation the action is taken on)
+        for (int u = tid; u < kTile * D; u += 256) {
+            const int i = u / D;
+            if (e0 + i < N) rw.obs[(row0 + e0 + i) * D + (u - i * D)] = xs[u];
+        }
+        // h1 = relu(x W1^T + b1): fmaf over d in order, then + b1 (k_fwd_hidden's order)
+        for (int u = tid; u < kTile * H1; u += 256) {
+            const int i = u / H1, k = u - i * H1;
+            float acc = 0.0f;
+            for (int d = 0; d < D; ++d) acc = fmaf(xs[i * D + d], W1s[k * D + d], acc);
+            acc += b1s[k];
+            h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
+        }
+        __syncthreads();
+        // h2 column blocks, one wave each: the 4 K-range partials (k_fwd_hidden's 4 waves) summed
+        // in range order, + b2, relu, into h2s[cb]
+        for (int cb = wave; cb < ncb; cb += 4) {
+            const int c0 = cb * kTile;
+            f32x4 part[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ch0 = (q * nch) / 4, ch1 = ((q + 1) * nch) / 4;
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                for (int ch = ch0; ch < ch1; ++ch) {
+                    const int k = ch * kTile + 4 * lq;
+                    const float4 a = *reinterpret_cast<const float4 *>(h1s + li * ldh + k);
+                    const float4 b = c0 + li < H2 ? *reinterpret_cast<const float4 *>(W2s + (c0 + li) * ldh + k)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+                    acc0 = mfma4(a.x, b.x, acc0);
+                    acc1 = mfma4(a.y, b.y, acc1);
+                    acc0 = mfma4(a.z, b.z, acc0);
+                    acc1 = mfma4(a.w, b.w, acc1);
+                }
+                part[q] = acc0 + acc1;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = lq * 4 + r;
+                const float s = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
+                float h = 0.0f;
+                if (c0 + li < H2) {
+                    h = s + b2s[c0 + li];
+                    h = h > 0.0f ? h : 0.0f;
+                }
+                h2s[(cb * kTile + row) * 17 + li] = h;
+            }
+        }
+        __syncthreads();
+        // partial heads per column block (fmaf over its 16 hidden units in order)
+        for (int u = tid; u < ncb * kTile * A1; u += 256) {
+            const int cb = u / (kTile * A1), rem = u - cb * kTile * A1, row = rem / A1, a = rem - row * A1;
+            float z = 0.0f;
+#pragma unroll
+            for (int c = 0; c < kTile; ++c) {
+                const float w = cb * kTile + c < H2 ? whs[a * H2 + cb * kTile + c] : 0.0f;
+                z = fmaf(h2s[(cb * kTile + row) * 17 + c], w, z);
+            }
+            zps[(row * ncb + cb) * A1 + a] = z;
+        }
+        __syncthreads();
+        // heads + action (threads 0..15, one env each), then the env step
+        if (env_thread) {
+            float z[AMAX + 1];
+#pragma unroll
+            for (int a = 0; a < AMAX + 1; ++a) z[a] = 0.0f;
+            if constexpr (S::AEX > 0) {     // gather_head_row's order: blocks of 16, zeros past ncb
+                for (int cbb = 0; cbb < ncb; cbb += 16)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j)
+#pragma unroll
+                        for (int a = 0; a < AMAX + 1; ++a)
+                            if (a < A1) z[a] += cbb + j < ncb ? zps[(tid * ncb + cbb + j) * A1 + a] : 0.0f;
+            } else {
+                for (int cb = 0; cb < ncb; ++cb)
+#pragma unroll
+                    for (int a = 0; a < AMAX + 1; ++a)
+                        if (a < A1) z[a] += zps[(tid * ncb + cb) * A1 + a];
+            }
+#pragma unroll
+            for (int a = 0; a < AMAX + 1; ++a)
+                if (a < A1) z[a] += bhs[a];
+            const int64_t o = row0 + me;
+            head_act_row<AMAX>(z, A, mode, rng_seed, counter0 + (uint64_t)t, me, rw.actions + o, rw.logp + o,
+                               rw.value + o);
+            const SynthStep so = synth_env_step(st, er, ev.L, ev.trunc_every, ev.reward,
+                                                ev.ep_cnt ? ev.ep_cnt + me : nullptr,
+                                                ev.ep_ret_sum ? ev.ep_ret_sum + me : nullptr,
+                                                ev.ep_len_sum ? ev.ep_len_sum + me : nullptr);
+            rw.reward[o] = so.reward;
+            rw.done[o] = so.done ? 1 : 0;
+            rw.timeout[o] = so.timeout ? 1 : 0;
+        }
+        // next observations (after step0 + t + 1 vector steps)
+        for (int u = tid; u < kTile * D; u += 256) {
+            const int i = u / D;
+            if (e0 + i < N)
+                xs[u] = synth_obs(ev.seed, (uint64_t)(ev.env_offset + e0 + i), ev.step0 + (uint64_t)t + 1,
+                                  (uint64_t)(u - i * D));
+        }
+        __syncthreads();
+    }
+    // ---- the envs' state and observations back
+    if (env_thread) {
+        ev.state[4 * me + 0] = st[0];
+        ev.state[4 * me + 1] = st[1];
+        ev.state[4 * me + 2] = st[2];
+        ev.ep_ret[me] = er;
+    }
+    for (int u = tid; u < kTile * D; u += 256) {
+        const int i = u / D;
+        if (e0 + i < N) ev.obs[(e0 + i) * D + (u - i * D)] = xs[u];
+    }
+}
+
+bool rollout_synth_fits(const Layout &L)
+{
+    return L.H1 % kTile == 0 && L.H1 >= kTile && rollout_synth_lds_bytes(L) <= 160 * 1024;
+}
+
+int launch_rollout_synth(const float *P, const Layout &L, int64_t N, int T, int mode, uint64_t rng_seed,
+                         uint64_t counter0, const SynthEnvArgs &ev, const RolloutRows &rw, hipStream_t s)
+{
+    GS_REQUIRE(rollout_synth_fits(L), "gs_rollout_synth: the policy does not fit in LDS");
+    const size_t lds = rollout_synth_lds_bytes(L);
+    const dim3 grid((unsigned)((N + kTile - 1) / kTile));
+    return with_shape(L, 0, [&](auto sh) {
+        int rc = set_lds_limit((const void *)k_rollout_synth<decltype(sh)>, lds);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_rollout_synth<decltype(sh)>, grid, dim3(256), lds, s, P, L, N, T, mode, rng_seed,
+                           counter0, ev, rw);
+        GS_LAUNCH_CHECK("k_rollout_synth");
+        return GS_OK;
+    });
 }
 
 // ------------------------------------------------------------------------------------

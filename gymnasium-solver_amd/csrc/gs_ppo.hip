@@ -111,6 +111,39 @@ extern "C" int gs_policy_act(const float *params, gs_mlp_dims dims, const float 
     return launch_heads_act(params, L, zpart, N, mode, rng_seed, rng_counter, actions, logp, value, s, clock);
 }
 
+extern "C" int gs_rollout_synth_supported(gs_mlp_dims dims, int *supported)
+{
+    GS_REQUIRE(supported, "gs_rollout_synth_supported: null output");
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    *supported = rollout_synth_fits(layout_of(dims)) ? 1 : 0;
+    return GS_OK;
+}
+
+extern "C" int gs_rollout_synth(const float *params, gs_mlp_dims dims, int64_t N, int64_t T, int mode,
+                                uint64_t rng_seed, uint64_t rng_counter0, int32_t *env_state, float *env_ep_ret,
+                                float *env_obs, int32_t episode_len, int32_t truncate_every, float reward,
+                                uint64_t env_seed, int64_t env_offset, uint64_t env_step0, int32_t *ep_done_count,
+                                float *ep_ret_sum, float *ep_len_sum, float *obs_rows, int64_t *action_rows,
+                                float *logp_rows, float *value_rows, float *reward_rows, uint8_t *done_rows,
+                                uint8_t *timeout_rows, void *stream)
+{
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    GS_REQUIRE(N > 0 && T >= 0 && T < (int64_t)1 << 31, "gs_rollout_synth: bad N / T");
+    GS_REQUIRE(mode >= 0 && mode <= 2, "gs_rollout_synth: mode %d not in {0,1,2}", mode);
+    GS_REQUIRE(episode_len > 0, "gs_rollout_synth: episode_len must be > 0");
+    GS_REQUIRE(params && env_state && env_ep_ret && env_obs && obs_rows && action_rows && logp_rows && value_rows &&
+                   reward_rows && done_rows && timeout_rows,
+               "gs_rollout_synth: null buffer");
+    if (T == 0) return GS_OK;
+    SynthEnvArgs ev{env_state, env_ep_ret, env_obs, ep_done_count, ep_ret_sum, ep_len_sum, episode_len,
+                    truncate_every, reward, env_seed, env_step0, env_offset};
+    RolloutRows rw{obs_rows, action_rows, logp_rows, value_rows, reward_rows, done_rows, timeout_rows};
+    return launch_rollout_synth(params, layout_of(dims), N, (int)T, mode, rng_seed, rng_counter0, ev, rw,
+                                (hipStream_t)stream);
+}
+
 extern "C" int gs_policy_value(const float *params, gs_mlp_dims dims, const float *obs, int64_t N, float *value,
                                void *scratch, void *stream)
 {

@@ -73,6 +73,9 @@ def _load():
         "gs_policy_scratch_bytes": (sz, [MlpDims, i64]),
         "gs_policy_act": (ctypes.c_int, [vp, MlpDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp, vp]),
         "gs_policy_value": (ctypes.c_int, [vp, MlpDims, vp, i64, vp, vp, vp]),
+        "gs_rollout_synth_supported": (ctypes.c_int, [MlpDims, vp]),
+        "gs_rollout_synth": (ctypes.c_int, [vp, MlpDims, i64, i64, ctypes.c_int, u64, u64, vp, vp, vp, i32, i32, f32,
+                                            u64, i64, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "gs_env_reset": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, u64, i64, vp]),
         "gs_env_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, f32, u64, i64, u64, vp, vp, vp, vp, vp,
                                        vp, vp, vp]),
@@ -122,7 +125,8 @@ def _load():
 
 lib = _load()
 EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
-            "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_env_reset", "gs_env_step",
+            "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_rollout_synth_supported",
+            "gs_rollout_synth", "gs_env_reset", "gs_env_step",
             "gs_episode_stats",
             "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_ppo_update_workspace_bytes",
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",

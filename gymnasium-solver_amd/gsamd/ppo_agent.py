@@ -48,11 +48,12 @@ class MinibatchIndices:
 
 class DevicePPOAgent:
     def __init__(self, config, env=None, device: Optional[str] = None, rank: int = 0, world_size: int = 1,
-                 comm=None, use_graph: bool = True, track_stats: bool = True):
+                 comm=None, use_graph: bool = True, track_stats: bool = True, one_launch: bool = True):
         self.config = config
         self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
         self.rank, self.world_size, self.comm = int(rank), int(world_size), comm
         self.use_graph = bool(use_graph)
+        self.one_launch = bool(one_launch)      # synthetic env + LDS-sized MLP: one-launch rollouts
         self.track_stats = bool(track_stats)
         # schedulable hyper-parameters (base_agent.py:72-77)
         self.policy_lr = config.policy_lr
@@ -118,7 +119,8 @@ class DevicePPOAgent:
         c = self.config
         self._rollout_collectors[stage] = DeviceRolloutCollector(
             self.get_env(stage), self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
-            rng_seed=c.seed + 7919 * self.rank, track_stats=self.track_stats, use_graph=self.use_graph)
+            rng_seed=c.seed + 7919 * self.rank, track_stats=self.track_stats, use_graph=self.use_graph,
+            one_launch=self.one_launch)
 
     def get_rollout_collector(self, stage: str) -> DeviceRolloutCollector:
         if stage not in self._rollout_collectors and stage in ("val", "test"):

@@ -23,6 +23,7 @@ device update reads the time-major buffers directly through sampler indices.
 """
 from __future__ import annotations
 
+import ctypes
 import time
 from typing import Optional
 
@@ -217,7 +218,7 @@ class DeviceRolloutCollector:
 
     def __init__(self, env, policy_model, n_steps, *, gamma: float = 0.99, gae_lambda: float = 0.95,
                  stats_window_size: int = 100, rng_seed: int = 42, track_stats: bool = True,
-                 use_graph: bool = True, **kwargs):
+                 use_graph: bool = True, one_launch: bool = True, **kwargs):
         self.env = env
         self.policy_model = policy_model
         self.n_steps = int(n_steps)
@@ -230,6 +231,10 @@ class DeviceRolloutCollector:
         # per sampling mode into a hipGraph and replayed; the per-rollout counters reach the
         # kernels through a 2-word device clock (include/gsamd.h "Rollout clock")
         self.use_graph = bool(use_graph)
+        # the synthetic device env with a policy that fits in LDS: the whole rollout is one
+        # launch (gs_rollout_synth, rows bit-identical to the step-wise loop)
+        self.one_launch = bool(one_launch) and isinstance(env, DeviceSyntheticVecEnv) and \
+            hasattr(policy_model, "dims") and self._synth_supported(policy_model)
         self._graphs = {}
         self._clock = None
         self.total_rollouts = self.total_steps = self.total_vec_steps = self.total_episodes = 0
@@ -299,7 +304,12 @@ class DeviceRolloutCollector:
         mode = 2 if replay_actions is not None else (1 if deterministic else 0)
         native = getattr(self.env, "device_native", False)
         self.rollout_episodes = 0
-        if native and replay_actions is None and self.use_graph:
+        if self.one_launch:
+            if replay_actions is not None:
+                buf.actions.copy_(replay_actions)
+            self._collect_one_launch(mode)
+            T = 0                               # the steps ran inside the launch
+        elif native and replay_actions is None and self.use_graph:
             self._collect_steps_graph(mode)
             T = 0                               # the steps ran inside the graph
         for t in range(T):
@@ -340,6 +350,25 @@ class DeviceRolloutCollector:
             self.total_episodes += self.rollout_episodes
         self.rollout_fpss.append(N * T / max(time.time() - t0, 1e-9))
         return DeviceTrajectory(buf)
+
+    @staticmethod
+    def _synth_supported(pm) -> bool:
+        v = ctypes.c_int()
+        check(lib.gs_rollout_synth_supported(pm.dims, ctypes.byref(v)), "gs_rollout_synth_supported")
+        return bool(v.value)
+
+    def _collect_one_launch(self, mode):
+        """The T vector steps as one gs_rollout_synth launch (policy act + env step per step,
+        envs resident in LDS); the env's host step counter advances by T."""
+        buf, pm, env = self._buffer, self.policy_model, self.env
+        check(lib.gs_rollout_synth(ptr(pm.params), pm.dims, self.n_envs, self.n_steps, int(mode), self.rng_seed,
+                                   self.total_vec_steps, ptr(env.state), ptr(env.ep_ret), ptr(env.obs),
+                                   env.episode_len, env.truncate_every, env.reward, env.seed, env.env_offset,
+                                   env.step_count, ptr(env.ep_count), ptr(env.ep_ret_sum), ptr(env.ep_len_sum),
+                                   ptr(buf.obs), ptr(buf.actions), ptr(buf.logprobs), ptr(buf.values),
+                                   ptr(buf.rewards), ptr(buf.dones), ptr(buf.timeouts), stream_handle()),
+              "gs_rollout_synth")
+        env.step_count += self.n_steps
 
     def _steps_into_buffer(self, mode, clock=None):
         """The rollout's T vector steps on a device env: policy act (writes the step's obs /

@@ -96,6 +96,22 @@ int gs_policy_act(const float *params_dev, gs_mlp_dims dims, const float *obs_de
                   float *value_dev, float *obs_store_dev, void *scratch_dev, const uint64_t *clock_dev,
                   void *stream);
 
+/* A whole rollout of the synthetic env (gs_env_*) in ONE launch, for MLP policies whose weights
+ * fit in LDS (gs_rollout_synth_supported; the C3 shapes do, C2's 256x256 W2 does not): per
+ * workgroup 16 envs for all T vector steps, the policy act with gs_policy_act's arithmetic in its
+ * order and the env step with gs_env_step's, so every row equals the step-wise rollout bit for
+ * bit (actions of mode 2 are read from action_rows).  Rows are time-major (T, N); the env state,
+ * running returns and observations are left after the last step, as T gs_env_step calls leave
+ * them; the rng counter of step t is rng_counter0 + t, the env step count env_step0 + t + 1.
+ * Replaces (with gs_env_step) the loop of utils/rollout_collector.py:459-567. */
+int gs_rollout_synth_supported(gs_mlp_dims dims, int *supported_host);
+int gs_rollout_synth(const float *params_dev, gs_mlp_dims dims, int64_t N, int64_t T, int mode, uint64_t rng_seed,
+                     uint64_t rng_counter0, int32_t *env_state_dev, float *env_ep_ret_dev, float *env_obs_dev,
+                     int32_t episode_len, int32_t truncate_every, float reward, uint64_t env_seed, int64_t env_offset,
+                     uint64_t env_step0, int32_t *ep_done_count_dev, float *ep_ret_sum_dev, float *ep_len_sum_dev,
+                     float *obs_rows_dev, int64_t *action_rows_dev, float *logp_rows_dev, float *value_rows_dev,
+                     float *reward_rows_dev, uint8_t *done_rows_dev, uint8_t *timeout_rows_dev, void *stream);
+
 /* Value-only forward (utils/policy_ops.py:37-42 policy_predict_values), e.g. the
  * bootstrap value of the last observation (utils/rollout_collector.py:373). */
 int gs_policy_value(const float *params_dev, gs_mlp_dims dims, const float *obs_dev, int64_t N,

@@ -175,7 +175,7 @@ def test_rollout_graph_equals_eager(cuda, env, variant, over):
     for use_graph in (False, True):
         torch.manual_seed(42)
         cfg = load_config(env, variant, overrides=over)
-        agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=True)
+        agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=True, one_launch=False)
         coll = agent.get_rollout_collector("train")
         rec = []
         for k in range(4):
@@ -197,3 +197,45 @@ def test_rollout_graph_equals_eager(cuda, env, variant, over):
             assert torch.equal(x, y), k
     assert m0["cnt/total_episodes"] == m1["cnt/total_episodes"]
     assert m0.get("roll/ep_rew/mean") == m1.get("roll/ep_rew/mean")
+
+
+@pytest.mark.parametrize("env,variant,over", [
+    ("LunarLander-v3", "ppo", dict(n_envs=72, n_steps=96, batch_size=64, n_epochs=2)),
+    ("CartPole-v1", "ppo", dict(n_envs=40, n_steps=64, batch_size=64, n_epochs=2, model_id="mlp_small"))])
+def test_one_launch_rollout_equals_step_loop(cuda, env, variant, over):
+    """gs_rollout_synth (the whole rollout in one launch, envs resident in LDS) writes bit for bit
+    the rows of the per-step loop (gs_policy_act + gs_env_step launches): sampled, deterministic
+    and replayed actions, over rollouts separated by updates, a ragged last workgroup (N % 16 != 0),
+    and leaves the same env state, observations and episode counters."""
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    runs = []
+    for one in (False, True):
+        torch.manual_seed(42)
+        cfg = load_config(env, variant, overrides=over)
+        agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=True, one_launch=one)
+        coll = agent.get_rollout_collector("train")
+        assert coll.one_launch == one
+        rec = []
+        for k in range(3):
+            agent.train_epoch()
+            b = coll.buffer
+            rec.append([t.clone() for t in (b.obs, b.actions, b.logprobs, b.values, b.rewards, b.dones, b.timeouts,
+                                            b.advantages, b.returns)])
+        coll.collect(deterministic=True)
+        rec.append([t.clone() for t in (coll.buffer.actions, coll.buffer.logprobs, coll.buffer.values)])
+        replay = torch.randint(0, coll.env.n_actions, coll.buffer.actions.shape, device=coll.buffer.actions.device,
+                               generator=torch.Generator(device=coll.buffer.actions.device).manual_seed(7))
+        coll.collect(replay_actions=replay)
+        rec.append([t.clone() for t in (coll.buffer.actions, coll.buffer.logprobs, coll.buffer.values)])
+        e = coll.env
+        rec.append([t.clone() for t in (e.state, e.ep_ret, e.obs, e.ep_count, e.ep_ret_sum, e.ep_len_sum)])
+        torch.cuda.synchronize()
+        runs.append((rec, coll.get_metrics(), coll.total_vec_steps, e.step_count))
+        del agent
+    (r0, m0, n0, s0), (r1, m1, n1, s1) = runs
+    assert (n0, s0) == (n1, s1)
+    for k, (a, b) in enumerate(zip(r0, r1)):
+        for j, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (k, j)
+    assert m0["cnt/total_episodes"] == m1["cnt/total_episodes"]
