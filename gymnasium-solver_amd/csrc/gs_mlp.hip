@@ -955,6 +955,16 @@ __global__ __launch_bounds__(256) void k_rollout_synth(const float *__restrict__
         const int i = u / D;
         xs[u] = e0 + i < N ? ev.obs[(e0 + i) * D + (u - i * D)] : 0.0f;
     }
+    constexpr int kW1Reg = 16;
+    const bool w1reg = H1 <= 256 && 256 % H1 == 0 && D <= kW1Reg;
+    float w1r[kW1Reg];
+    float b1r = 0.0f;
+    if (w1reg) {
+        const int k = tid % H1;
+#pragma unroll
+        for (int d = 0; d < kW1Reg; ++d) w1r[d] = d < D ? P[L.oW1 + (int64_t)k * D + d] : 0.0f;
+        b1r = P[L.ob1 + k];
+    }
     __syncthreads();
     for (int t = 0; t < T; ++t) {
         const int64_t row0 = (int64_t)t * N;
@@ -964,35 +974,53 @@ __global__ __launch_bounds__(256) void k_rollout_synth(const float *__restrict__
             if (e0 + i < N) rw.obs[(row0 + e0 + i) * D + (u - i * D)] = xs[u];
         }
         // h1 = relu(x W1^T + b1): fmaf over d in order, then + b1 (k_fwd_hidden's order)
-        for (int u = tid; u < kTile * H1; u += 256) {
-            const int i = u / H1, k = u - i * H1;
-            float acc = 0.0f;
-            for (int d = 0; d < D; ++d) acc = fmaf(xs[i * D + d], W1s[k * D + d], acc);
-            acc += b1s[k];
-            h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
+        if (w1reg) {       // this thread's hidden unit is fixed: its W1 row and bias in registers
+            const int k = tid % H1;
+            for (int i = tid / H1; i < kTile; i += 256 / H1) {
+                float acc = 0.0f;
+#pragma unroll
+                for (int d = 0; d < kW1Reg; ++d)
+                    if (d < D) acc = fmaf(xs[i * D + d], w1r[d], acc);
+                acc += b1r;
+                h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
+            }
+        } else {
+            for (int u = tid; u < kTile * H1; u += 256) {
+                const int i = u / H1, k = u - i * H1;
+                float acc = 0.0f;
+                for (int d = 0; d < D; ++d) acc = fmaf(xs[i * D + d], W1s[k * D + d], acc);
+                acc += b1s[k];
+                h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
+            }
         }
         __syncthreads();
         // h2 column blocks, one wave each: the 4 K-range partials (k_fwd_hidden's 4 waves) summed
         // in range order, + b2, relu, into h2s[cb]
         for (int cb = wave; cb < ncb; cb += 4) {
             const int c0 = cb * kTile;
-            f32x4 part[4];
+            // the 4 partials' MFMA chains interleaved (8 independent accumulators hide the MFMA
+            // latency); each partial keeps its own chunk order, so the sums are unchanged
+            f32x4 acc0[4], acc1[4], part[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int ch0 = (q * nch) / 4, ch1 = ((q + 1) * nch) / 4;
-                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-                for (int ch = ch0; ch < ch1; ++ch) {
+            for (int q = 0; q < 4; ++q) acc0[q] = acc1[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int nmax = (nch + 3) / 4;
+            for (int c = 0; c < nmax; ++c) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int ch = (q * nch) / 4 + c;
+                    if (ch >= ((q + 1) * nch) / 4) continue;
                     const int k = ch * kTile + 4 * lq;
                     const float4 a = *reinterpret_cast<const float4 *>(h1s + li * ldh + k);
                     const float4 b = c0 + li < H2 ? *reinterpret_cast<const float4 *>(W2s + (c0 + li) * ldh + k)
                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-                    acc0 = mfma4(a.x, b.x, acc0);
-                    acc1 = mfma4(a.y, b.y, acc1);
-                    acc0 = mfma4(a.z, b.z, acc0);
-                    acc1 = mfma4(a.w, b.w, acc1);
+                    acc0[q] = mfma4(a.x, b.x, acc0[q]);
+                    acc1[q] = mfma4(a.y, b.y, acc1[q]);
+                    acc0[q] = mfma4(a.z, b.z, acc0[q]);
+                    acc1[q] = mfma4(a.w, b.w, acc1[q]);
                 }
-                part[q] = acc0 + acc1;
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) part[q] = acc0[q] + acc1[q];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = lq * 4 + r;
