@@ -54,7 +54,7 @@ __device__ unsigned long long g_stamp_cnt[8];
 // clock for the whole device); plain per-workgroup stores (atomics on shared words would
 // serialise and distort the timeline); kernel 0 = lagged forward, 1 = k_bwd
 constexpr int kSpanK = 2048, kSpanWG = 288;
-__device__ unsigned g_span[2][kSpanK][kSpanWG][5];
+__device__ unsigned g_span[2][kSpanK][kSpanWG][9];   // start + up to 8 wave ends
 __device__ __forceinline__ int span_wg() { return (int)(blockIdx.x + blockIdx.y * gridDim.x); }
 __device__ __forceinline__ void span_start(int kern, int64_t k, unsigned long long t0)
 {
@@ -104,12 +104,15 @@ constexpr int kNumSums = 14;   // metric sums of one minibatch (loss_row)
 // Sum NV per-thread values over the 256-thread block in a fixed order (deterministic),
 // through LDS (two levels of 16) — __shfl would lower to ds_bpermute chains (~100+ cycles
 // per step).  Every thread returns the totals.  scratch: NV*(256+16) elements of T.
+// In a block wider than 256 threads only threads 0..255 contribute (the others only meet the
+// barriers and read the totals), so the sum order is the 256-thread one.
 template <int NV, typename T>
 __device__ __forceinline__ void block_reduce(T (&v)[NV], T *scratch)
 {
     const int tid = threadIdx.x;
+    if (tid < 256)
 #pragma unroll
-    for (int k = 0; k < NV; ++k) scratch[k * 256 + tid] = v[k];
+        for (int k = 0; k < NV; ++k) scratch[k * 256 + tid] = v[k];
     __syncthreads();
     T *part = scratch + NV * 256;
     if (tid < NV * 16) {
@@ -206,8 +209,20 @@ __device__ __forceinline__ void loss_row(const float (&z)[AMAX + 1], int A, int 
 // index -> row -> obs chain).  The head combine stays in the next launch (k_loss_rows): an
 // in-launch last-arriver combine costs a release + acquire fence pair (~1.7 us each on
 // gfx950) on top of the skew wait, more than the ~1.45 us kernel boundary it would remove.
+//
+// ADAM (the lagged chain's forward) runs 512 threads (kFwdAdamThreads): two waves per SIMD share
+// the Adam step on the workgroup's W1|b1 and W2 rows and the h1 rows, so the prologue's
+// per-thread arithmetic halves; the global norm keeps the 256-thread grouping (threads 0..255,
+// k_clip_adam's order) and the h2 MFMA stays on waves 0..3, so every value is bit-identical to
+// the 256-thread kernel.
+#ifndef GS_FWD_ADAM_NT
+#define GS_FWD_ADAM_NT 512
+#endif
+constexpr int kFwdAdamThreads = GS_FWD_ADAM_NT;
+static_assert(kFwdAdamThreads == 256 || kFwdAdamThreads == 512, "lagged forward: 256 or 512 threads");
+
 template <class S, bool FUSED, bool ADAM = false>
-__global__ __launch_bounds__(256) void k_fwd_hidden(
+__global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
     const float *__restrict__ P, Layout Lrt, const float *__restrict__ obs, const int32_t *__restrict__ idx, int T,
     int N, int rows, float *__restrict__ x_out, float *__restrict__ h1_out, float *__restrict__ h2_out,
     float *__restrict__ zpart, float *__restrict__ obs_copy, const int32_t *__restrict__ stop, RowGather rg,
@@ -223,6 +238,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     const int r0 = rb * kTile;
     const int c0 = cb * kTile;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NT = ADAM ? kFwdAdamThreads : 256;     // threads per workgroup
     const int ldh = H1 + 4;
     int *srcs = reinterpret_cast<int *>(lds);
     float *W1s = lds + 16;
@@ -244,7 +260,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     // compile-time shapes on the fused path: every phase-0 operand goes to registers first
     // (one memory round trip), then to LDS
     constexpr bool kStage0 = FUSED && S::H1c > 0 && (S::H1c * 4) % 4 == 0;
-    constexpr int kW2v = S::H1c > 0 ? kTile * S::H1c / 4 / 256 : 0;
+    constexpr int kW2v = S::H1c > 0 ? kTile * S::H1c / 4 / NT : 0;
     float4 w2r[kW2v > 0 ? kW2v : 1];
     static_assert(!ADAM || (kStage0 && kW2v > 0), "lagged Adam: compile-time fused shapes only");
     if constexpr (ADAM) {
@@ -293,15 +309,24 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         // branches force s_waitcnt vmcnt stalls in the middle of the burst (one memory round trip
         // per stall instead of one for the whole prologue)
         constexpr int nq1 = n1 / 4;
-        float4 w1p[NQ], w1m[NQ], w1v[NQ], t[NQ][NRB];     // W1|b1 (param order), dW1|db1 partials
+        // Adam: W1|b1 quad q = tid + NT*j; norm partials: threads 0..255, quad tid + 256*j (the
+        // 256-thread grouping of k_clip_adam, wave-uniform branch for the wider block)
+        constexpr int NQP = (nq1 + NT - 1) / NT;
+        const bool nrm = NT == 256 || tid < 256;
+        float4 w1p[NQP], w1m[NQP], w1v[NQP], t[NQ][NRB];  // W1|b1 (param order), dW1|db1 partials
 #pragma unroll
-        for (int j = 0; j < NQ; ++j) {
-            const int q = min(tid + 256 * j, nq1 - 1);
+        for (int j = 0; j < NQP; ++j) {
+            const int q = min(tid + NT * j, nq1 - 1);
             w1p[j] = ld4(P, q);
             w1m[j] = ld4(af.Min, q);
             w1v[j] = ld4(af.Vin, q);
         }
-        if (fold) {
+        if (!nrm) {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j)
+#pragma unroll
+                for (int b = 0; b < NRB; ++b) t[j][b] = z4;
+        } else if (fold) {
 #pragma unroll
             for (int j = 0; j < NQ; ++j)
 #pragma unroll
@@ -322,7 +347,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         float4 w2m[kW2v], w2v[kW2v], w2g[kW2v];           // this workgroup's 16 W2 rows
 #pragma unroll
         for (int j = 0; j < kW2v; ++j) {
-            const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+            const int u = tid + NT * j, i = u / k4n, k4 = u - i * k4n;
             const int64_t q = (Lc.oW2 + (int64_t)min(c0 + i, H2 - 1) * cH1) / 4 + k4;
             w2r[j] = ld4(P, q);
             w2m[j] = ld4(af.Min, q);
@@ -346,7 +371,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         load_slice(shb, oh);
         float sl[NS];
 #pragma unroll
-        for (int j = 0; j < NS; ++j) sl[j] = ld1(af.sumsq, min(tid + 256 * j, aa.n_slots - 1));
+        for (int j = 0; j < NS; ++j) sl[j] = nrm ? ld1(af.sumsq, min(tid + 256 * j, aa.n_slots - 1)) : 0.0f;
         // then the loads behind the graph replay's step base: this minibatch's x rows and step
         // k-1's schedule entries
         float xv = 0.0f;
@@ -360,7 +385,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.inv_bc2_sqrt;
 #pragma unroll
         for (int j = 0; j < NS; ++j)
-            if (tid + 256 * j >= aa.n_slots) sl[j] = 0.0f;
+            if (!nrm || tid + 256 * j >= aa.n_slots) sl[j] = 0.0f;
         if (tid < kTile * cD) xs[tid] = xv;
 #ifdef GS_STAMPS
         __builtin_amdgcn_s_waitcnt(0);     // diagnostic build only: split "loads landed" from the norm
@@ -377,6 +402,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 if (tid + 256 * j < aa.n_slots) ss += (double)sl[j];
 #pragma unroll
             for (int j = 0; j < NQ; ++j) {
+                if (!nrm) break;
                 float4 g = z4;
 #pragma unroll
                 for (int b = 0; b < NRB; ++b) {
@@ -404,8 +430,8 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         GS_STAMP(1)
         // Adam on the owned parameters: new values to LDS / registers, and from row block 0 to the other set
 #pragma unroll
-        for (int j = 0; j < NQ; ++j) {
-            const int q = tid + 256 * j;
+        for (int j = 0; j < NQP; ++j) {
+            const int q = tid + NT * j;
             if (4 * q >= n1) continue;
             float4 p4 = w1p[j];
             if (apply) {
@@ -428,7 +454,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         if (apply) {
 #pragma unroll
             for (int j = 0; j < kW2v; ++j) {
-                const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+                const int u = tid + NT * j, i = u / k4n, k4 = u - i * k4n;
                 if (c0 + i >= H2) continue;
                 float p[4] = {w2r[j].x, w2r[j].y, w2r[j].z, w2r[j].w};
                 float m[4] = {w2m[j].x, w2m[j].y, w2m[j].z, w2m[j].w};
@@ -537,7 +563,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         const int k4n = H1 >> 2;
 #pragma unroll
         for (int j = 0; j < kW2v; ++j) {
-            const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+            const int u = tid + NT * j, i = u / k4n, k4 = u - i * k4n;
             w2r[j] = c0 + i < H2 ? *reinterpret_cast<const float4 *>(P + L.oW2 + (int64_t)(c0 + i) * H1 + 4 * k4)
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -553,8 +579,11 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     }
     __syncthreads();
     GS_STAMP(3)
-    // ---- phase 1: h1 = relu(x W1^T + b1) out of LDS; one hidden unit per thread
-    for (int k = tid; k < H1; k += 256) {
+    // ---- phase 1: h1 = relu(x W1^T + b1) out of LDS; one hidden unit per thread, rows
+    //      [i0, i0 + RPT) of the tile (all 16 with 256 threads, 8 with 512)
+    constexpr int RPT = kTile * 256 / NT;
+    const int i0 = (tid >> 8) * RPT;
+    for (int k = tid & 255; k < H1; k += 256) {
         float w[8];
         const bool small = D <= 8;
 #pragma unroll
@@ -564,16 +593,16 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
             // every x row first (float4 LDS reads; xs is 16-B aligned), then the 16 outputs: the
             // h1s stores may alias xs as far as the compiler knows, so reads interleaved with them
             // would each wait for the LDS round trip
-            float4 xq[kTile][2];
+            float4 xq[RPT][2];
 #pragma unroll
-            for (int i = 0; i < kTile; ++i)
+            for (int i = 0; i < RPT; ++i)
 #pragma unroll
                 for (int d4 = 0; d4 < 2; ++d4)
-                    xq[i][d4] = 4 * d4 < D ? reinterpret_cast<const float4 *>(xs + i * D)[d4]
+                    xq[i][d4] = 4 * d4 < D ? reinterpret_cast<const float4 *>(xs + (i0 + i) * D)[d4]
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-            float hv[kTile];
+            float hv[RPT];
 #pragma unroll
-            for (int i = 0; i < kTile; ++i) {
+            for (int i = 0; i < RPT; ++i) {
                 const float xr[8] = {xq[i][0].x, xq[i][0].y, xq[i][0].z, xq[i][0].w,
                                      xq[i][1].x, xq[i][1].y, xq[i][1].z, xq[i][1].w};
                 float acc = 0.0f;
@@ -584,10 +613,10 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 hv[i] = acc > 0.0f ? acc : 0.0f;
             }
 #pragma unroll
-            for (int i = 0; i < kTile; ++i) h1s[i * ldh + k] = hv[i];
+            for (int i = 0; i < RPT; ++i) h1s[(i0 + i) * ldh + k] = hv[i];
         } else if (small) {
 #pragma unroll
-            for (int i = 0; i < kTile; ++i) {
+            for (int i = i0; i < i0 + RPT; ++i) {
                 float xr[8];
 #pragma unroll
                 for (int d = 0; d < 8; ++d) xr[d] = d < D ? xs[i * D + d] : 0.0f;
@@ -599,7 +628,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
                 h1s[i * ldh + k] = acc > 0.0f ? acc : 0.0f;
             }
         } else {
-            for (int i = 0; i < kTile; ++i) {
+            for (int i = i0; i < i0 + RPT; ++i) {
                 float acc = 0.0f;
                 for (int d = 0; d < D; ++d) acc = fmaf(xs[i * D + d], W1s[k * D + d], acc);
                 acc += bk;
@@ -611,14 +640,15 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         const int k4n = H1 >> 2;
 #pragma unroll
         for (int j = 0; j < kW2v; ++j) {
-            const int u = tid + 256 * j, i = u / k4n, k4 = u - i * k4n;
+            const int u = tid + NT * j, i = u / k4n, k4 = u - i * k4n;
             *reinterpret_cast<float4 *>(W2s + i * ldh + 4 * k4) = w2r[j];
         }
     }
     __syncthreads();
     GS_STAMP(4)
     // ---- phase 2: h2 tile = h1[16 x H1] . W2[c0:c0+16, :]^T, MFMA, K split over 4 waves
-    {
+    //      (waves 0..3 of a wider block: the K ranges and their sum order stay those of 4 waves)
+    if (wave < 4) {
         const int i = lane & 15, q = lane >> 4;
         const int nch = H1 / kTile;
         const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
@@ -639,7 +669,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     }
     __syncthreads();
     GS_STAMP(5)
-    {
+    if (tid < 256) {
         const int row = tid >> 4, col = tid & 15;
         const float s = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
         float h = 0.0f;
@@ -659,7 +689,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     }
     // ---- phase 3: partial head outputs over this tile's 16 hidden units
     const int ncbz = gridDim.x;
-    for (int u = tid; u < kTile * A1; u += 256) {
+    for (int u = tid; u < kTile * A1; u += NT) {
         const int row = u / A1, a = u - row * A1;
         if (r0 + row >= rows) continue;
         float z = 0.0f;
@@ -669,7 +699,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
     }
     const int nrow = min(kTile, rows - r0);
     if (cb == 0)
-        for (int u = tid; u < nrow * D; u += 256) {
+        for (int u = tid; u < nrow * D; u += NT) {
             if (x_out) x_out[(int64_t)r0 * D + u] = xs[u];
             if (obs_copy) obs_copy[(int64_t)r0 * D + u] = xs[u];
         }
@@ -678,7 +708,7 @@ __global__ __launch_bounds__(256) void k_fwd_hidden(
         // between them (H1/16 units each) instead of falling on column block 0 alone
         const int k4n = H1 >> 2, ncbw = gridDim.x;
         const int kb0 = (cb * k4n) / ncbw, kb1 = ((cb + 1) * k4n) / ncbw, nk = kb1 - kb0;
-        for (int u = tid; u < nrow * nk; u += 256) {
+        for (int u = tid; u < nrow * nk; u += NT) {
             const int i = u / nk, k4 = kb0 + (u - i * nk);
             *reinterpret_cast<float4 *>(h1_out + (int64_t)(r0 + i) * H1 + 4 * k4) =
                 *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
@@ -2698,7 +2728,7 @@ constexpr bool lagged_shape()
     } else {
         constexpr Layout Lc = Sh::lay(Layout{});
         constexpr int n1 = Lc.H1 * (Lc.D + 1);
-        return (kTile * Lc.H1 / 4) % 256 == 0 && Lc.H1 % 4 == 0 && (Lc.H1 * Lc.D) % 4 == 0 &&
+        return (kTile * Lc.H1 / 4) % kFwdAdamThreads == 0 && Lc.H1 % 4 == 0 && (Lc.H1 * Lc.D) % 4 == 0 &&
                (Sh::Bc + kRowsB - 1) / kRowsB <= 8 && (n1 / 4 + 255) / 256 <= 2 && n1 <= kTile * (Lc.H1 + 4);
     }
 }
@@ -2726,7 +2756,8 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
             if constexpr (lagged_shape<Sh>()) {
                 GS_REQUIRE((af->part1 ? af->aa.nrb > 0 : af->aa.nrb == 0) && af->aa.n_slots <= 512,
                            "lagged Adam: bad slot / partial counts");
-                hipLaunchKernelGGL((k_fwd_hidden<Sh, true, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L,
+                hipLaunchKernelGGL((k_fwd_hidden<Sh, true, true>), grid, dim3(kFwdAdamThreads), fwd_lds_bytes(L), s,
+                                   params, L,
                                    no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop,
                                    RowGather{}, ff, la, ws.h2mask, *af);
                 GS_LAUNCH_CHECK("k_fwd_hidden<fused, adam>");
@@ -2792,18 +2823,18 @@ extern "C" int gs_debug_stamps(unsigned long long *acc_out, unsigned long long *
 #endif
 
 #if defined(GS_STAMPS) || defined(GS_SPANS)
-// chain timeline: zero / read the 2 x kSpanK x kSpanWG x 5 words
+// chain timeline: zero / read the 2 x kSpanK x kSpanWG x 9 words
 extern "C" int gs_debug_span_reset()
 {
     void *p = nullptr;
     GS_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(g_span)));
-    GS_HIP(hipMemset(p, 0, sizeof(unsigned) * 2 * kSpanK * kSpanWG * 5));
+    GS_HIP(hipMemset(p, 0, sizeof(unsigned) * 2 * kSpanK * kSpanWG * 9));
     GS_HIP(hipDeviceSynchronize());
     return GS_OK;
 }
 extern "C" int gs_debug_span_read(unsigned *out)
 {
-    GS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_span), sizeof(unsigned) * 2 * kSpanK * kSpanWG * 5));
+    GS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_span), sizeof(unsigned) * 2 * kSpanK * kSpanWG * 9));
     return GS_OK;
 }
 #endif

@@ -47,7 +47,7 @@ _lib.lib.gs_debug_span_read.argtypes = [ctypes.c_void_p]
 _lib.lib.gs_debug_span_reset()
 agent.train_epoch()
 torch.cuda.synchronize()
-span = np.zeros((2, 2048, 288, 5), np.uint32)
+span = np.zeros((2, 2048, 288, 9), np.uint32)   # start + up to 8 wave ends (0 = no such wave)
 _lib.lib.gs_debug_span_read(span.ctypes.data)
 acc = np.zeros(128, np.uint64)
 cnt = np.zeros(8, np.uint64)
@@ -82,8 +82,9 @@ ref = int(sp[0, 0, 0, 0])
 rel = ((sp - ref + 2**31) % 2**32 - 2**31).astype(np.float64) / 100.0   # wrap-safe, us
 live = span[:, :n, :, 0] != 0                                           # workgroups that ran
 st = np.where(live, rel[..., 0], np.inf).min(axis=2)                     # (2, n) first start
-en = np.where(live[..., None], rel[..., 1:], -np.inf).max(axis=(2, 3))   # (2, n) last wave end
-wg_end = np.where(live, rel[..., 1:].max(axis=3), np.nan)               # per-workgroup end
+wlive = live[..., None] & (span[:, :n, :, 1:] != 0)                     # waves that exist
+en = np.where(wlive, rel[..., 1:], -np.inf).max(axis=(2, 3))            # (2, n) last wave end
+wg_end = np.where(live, np.where(wlive, rel[..., 1:], -np.inf).max(axis=3), np.nan)   # per-workgroup end
 pct = lambda x: f"mean {np.mean(x):6.2f}  p10 {np.percentile(x, 10):6.2f}  p50 {np.median(x):6.2f}  p90 {np.percentile(x, 90):6.2f}"
 print(f"chain timeline over {n} minibatches (us)")
 print("    fwd span (first WG start -> last wave end)", pct(en[0] - st[0]))
