@@ -54,7 +54,6 @@ class DevicePPOAgent:
         self.rank, self.world_size, self.comm = int(rank), int(world_size), comm
         self.use_graph = bool(use_graph)
         self.one_launch = bool(one_launch)      # synthetic env + LDS-sized MLP: one-launch rollouts
-        self._copy_stream = None                 # side stream of the index uploads
         self.track_stats = bool(track_stats)
         # schedulable hyper-parameters (base_agent.py:72-77)
         self.policy_lr = config.policy_lr
@@ -385,20 +384,19 @@ class DevicePPOAgent:
         if ev is not None:
             ev.append([torch.cuda.Event(enable_timing=True) for _ in range(3)])
             ev[-1][0].record()
-        # the epoch's minibatch indices go up on a side stream while the rollout runs (C3: 84 MB)
-        if self._copy_stream is None:
-            self._copy_stream = torch.cuda.Stream(device=self.device)
-        idx_ready = self.prefetcher.upload_async(epoch, self._copy_stream)
         if epoch == 0 and collector.total_rollouts == 0:
             self._trajectories = collector.collect()
         elif epoch > 0:
             self._trajectories = collector.collect()
-        idx = self.prefetcher.device_buf
+        # the epoch's minibatch indices go up on the update's own stream: a side-stream upload
+        # overlapping the rollout (tried: C3 collect -2 ms) made every minibatch step of the
+        # update that followed ~1.4 us slower (same-box A/B on C2: 16.8 vs 15.3 us), with the
+        # update waiting on the copy's event on the device or on the host alike
+        idx = self.prefetcher.upload(epoch)
         self.prefetcher.prefetch(epoch + 1)
         buf = collector.buffer
         if ev is not None:
             ev[-1][1].record()
-        torch.cuda.current_stream().wait_event(idx_ready)
         if self.is_pixel:
             check(lib.gs_cnn_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
                                         ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(), ptr(idx),

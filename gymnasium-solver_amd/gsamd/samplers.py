@@ -104,11 +104,3 @@ class IndexStreamPrefetcher:
             ev.record(s)
         self._events[slot] = ev
         return self.device_buf
-
-    def upload_async(self, epoch: int, side_stream) -> torch.cuda.Event:
-        """The same H2D on a side stream, after everything already on the current stream (the
-        previous update, the last reader of device_buf), so it overlaps the rollout enqueued next;
-        the caller makes the current stream wait for the returned event before the update."""
-        side_stream.wait_stream(torch.cuda.current_stream())
-        self.upload(epoch, stream=side_stream)
-        return self._events[epoch % 2]
