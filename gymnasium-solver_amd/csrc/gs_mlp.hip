@@ -646,6 +646,33 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
     }
     __syncthreads();
     GS_STAMP(4)
+    // x rows and this workgroup's share of h1 to HBM (read only xs / h1s, final from here on):
+    // in a 512-thread block waves 4..7 store them while waves 0..3 run the h2 MFMA
+    const int nrow = min(kTile, rows - r0);
+    auto store_x_h1 = [&](int t0, int stride) {
+        if (cb == 0)
+            for (int u = t0; u < nrow * D; u += stride) {
+                if (x_out) x_out[(int64_t)r0 * D + u] = xs[u];
+                if (obs_copy) obs_copy[(int64_t)r0 * D + u] = xs[u];
+            }
+        if (h1_out) {
+            // every column-block workgroup of this row block holds all of h1: the store is split
+            // between them (H1/16 units each) instead of falling on column block 0 alone
+            const int k4n = H1 >> 2, ncbw = gridDim.x;
+            const int kb0 = (cb * k4n) / ncbw, kb1 = ((cb + 1) * k4n) / ncbw, nk = kb1 - kb0;
+            for (int u = t0; u < nrow * nk; u += stride) {
+                const int i = u / nk, k4 = kb0 + (u - i * nk);
+                *reinterpret_cast<float4 *>(h1_out + (int64_t)(r0 + i) * H1 + 4 * k4) =
+                    *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
+            }
+        }
+    };
+#ifdef GS_EXP_LATE_X_H1      // timing experiment: the stores after the heads, as with 256 threads
+    constexpr bool kEarly = false;
+#else
+    constexpr bool kEarly = NT == 512;
+#endif
+    if (kEarly && wave >= 4) store_x_h1(tid - 256, 256);
     // ---- phase 2: h2 tile = h1[16 x H1] . W2[c0:c0+16, :]^T, MFMA, K split over 4 waves
     //      (waves 0..3 of a wider block: the K ranges and their sum order stay those of 4 waves)
     if (wave < 4) {
@@ -681,11 +708,13 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         h2s[row * 17 + col] = h;
     }
     __syncthreads();
-    if (h2mask && tid < kTile && r0 + tid < rows) {   // relu'(h2) bits of this row's 16 columns
+    // relu'(h2) bits of each row's 16 columns (a 512-thread block: on wave 4, beside the heads)
+    const int hm = tid - (NT == 512 ? 256 : 0);
+    if (h2mask && hm >= 0 && hm < kTile && r0 + hm < rows) {
         unsigned m = 0;
 #pragma unroll
-        for (int c = 0; c < kTile; ++c) m |= (h2s[tid * 17 + c] > 0.0f ? 1u : 0u) << c;
-        h2mask[(int64_t)(r0 + tid) * gridDim.x + cb] = (uint16_t)m;
+        for (int c = 0; c < kTile; ++c) m |= (h2s[hm * 17 + c] > 0.0f ? 1u : 0u) << c;
+        h2mask[(int64_t)(r0 + hm) * gridDim.x + cb] = (uint16_t)m;
     }
     // ---- phase 3: partial head outputs over this tile's 16 hidden units
     const int ncbz = gridDim.x;
@@ -697,23 +726,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         for (int c = 0; c < kTile; ++c) z = fmaf(h2s[row * 17 + c], whs[a * 16 + c], z);
         zpart[((int64_t)(r0 + row) * ncbz + cb) * A1 + a] = z;
     }
-    const int nrow = min(kTile, rows - r0);
-    if (cb == 0)
-        for (int u = tid; u < nrow * D; u += NT) {
-            if (x_out) x_out[(int64_t)r0 * D + u] = xs[u];
-            if (obs_copy) obs_copy[(int64_t)r0 * D + u] = xs[u];
-        }
-    if (h1_out) {
-        // every column-block workgroup of this row block holds all of h1: the store is split
-        // between them (H1/16 units each) instead of falling on column block 0 alone
-        const int k4n = H1 >> 2, ncbw = gridDim.x;
-        const int kb0 = (cb * k4n) / ncbw, kb1 = ((cb + 1) * k4n) / ncbw, nk = kb1 - kb0;
-        for (int u = tid; u < nrow * nk; u += NT) {
-            const int i = u / nk, k4 = kb0 + (u - i * nk);
-            *reinterpret_cast<float4 *>(h1_out + (int64_t)(r0 + i) * H1 + 4 * k4) =
-                *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
-        }
-    }
+    if (!kEarly) store_x_h1(tid, NT);
     GS_STAMP_END(6)
     if constexpr (ADAM) GS_SPAN_END(0, kstep)
 }
