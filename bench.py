@@ -36,6 +36,19 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
 # CPU port vs the reference's own loop on the same 8-core container at C2 shapes
 # (5 646 / 2 814 env-steps/s)
 CPU_PORT_OVER_REFERENCE = round(5646.0 / 2814.0, 3)
+CALIBRATION_PROVENANCE = ("build container, 8-core Intel Xeon (1 thread/core), torch 2.10 CPU at 8 threads, C2 shapes; "
+                          "reference loop: SURVEY.md §6 (2 814 env-steps/s), port: DESIGN.md §6b (5 646)")
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
 
 
 def _log(*a):
@@ -45,6 +58,32 @@ def _log(*a):
 # workload id -> (env id, variant, envs per GPU)  (BASELINE.json configs)
 WORKLOADS = {"C2": ("CartPole-v1", "ppo", 4096), "C3": ("LunarLander-v3", "ppo", 1024),
              "C4": ("ALE-Pong-v5", "rgb_ppo", 256), "C5": ("ALE-Breakout-v5", "rgb_ppo", 128)}
+# BASELINE.json's metric is quoted on C2; the other workloads are labelled as what they are
+METRICS = {"C2": "env steps/sec (rollout+PPO update), CartPole n_envs=4096, 1/2/4/8 MI355X",
+           "C3": "env steps/sec (rollout+PPO update), LunarLander-v3 shapes n_envs={n}/GPU, MI355X",
+           "C4": "env steps/sec (rollout+PPO update), ALE/Pong-v5 rgb_ppo NatureCNN n_envs={n}/GPU, MI355X",
+           "C5": "env steps/sec (rollout+PPO update), ALE/Breakout-v5 rgb_ppo NatureCNN n_envs={n}/GPU, MI355X"}
+
+
+def usable_cores() -> tuple:
+    """(threads to use, cores in the affinity mask, cgroup CPU quota in cores or None): a GPU
+    box shows the whole machine in sched_getaffinity while its cgroup grants a share of it, so
+    the CPU baseline runs one thread per core of the quota (SURVEY §8d asks for the cores the
+    process can use)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    use = min(aff, quota) if quota else aff
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:      # the box's per-GPU CPU share (16 on the GPU pool)
+        use = min(use, int(omp))
+    return use, aff, quota
 
 
 def cnn_minibatch_flops(B, A):
@@ -272,8 +311,8 @@ def main():
                     help="rehearsal on a one-GPU box: all ranks share cuda:0 (gloo process group, "
                          "xGMI exchange through same-device IPC); throughput is not meaningful")
     ap.add_argument("--stage-reps", type=int, default=200)
-    ap.add_argument("--cpu-minibatches", type=int, default=2000,
-                    help="minibatches in the bounded CPU-baseline sample (0 disables)")
+    ap.add_argument("--cpu-minibatches", type=int, default=-1,
+                    help="minibatches timed in the CPU baseline (-1: the whole update, 0: no CPU baseline)")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -302,9 +341,9 @@ def main():
     env_id, variant, n_default = WORKLOADS[args.workload]
     pixel = variant == "rgb_ppo"
     n_envs = args.n_envs or n_default
-    over = dict(n_envs=n_envs)
-    if not pixel and args.env_dynamics != "synthetic":
-        over["env_dynamics"] = args.env_dynamics
+    # the benchmark's env is chosen explicitly: SURVEY §8d synthetic fixed-length episodes (or the
+    # synthetic Atari frame source), or the device CartPole-v1 dynamics
+    over = dict(n_envs=n_envs, env_dynamics="synthetic" if pixel else args.env_dynamics)
     cfg = load_config(env_id, variant, overrides=over)
     agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world,
                            use_graph=not args.no_graph, track_stats=False)
@@ -411,13 +450,21 @@ def main():
         # the exchange as its own launch (what the chain runs after k_bwd unless in_bwd)
         stage_us["exchange_launch" if in_bwd else "exchange"] = time_exchange(comm, pm.n_params, args.stage_reps,
                                                                                device, barrier)
+    # PMC HBM traffic per launch (tools/pmc_run.py + tools/pmc_summarize.py), used only when it was
+    # recorded from the kernel sources this library is built from (gsamd.buildinfo.source_hash)
+    from gsamd.buildinfo import source_hash
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    pmc = {}
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
         except (OSError, ValueError):
             pmc = {}
+    traffic_src = {"file": "profiles/pmc_traffic.json", "recorded_source_hash": pmc.get("_source_hash"),
+                   "library_source_hash": source_hash()}
+    traffic_src["current"] = bool(pmc) and traffic_src["recorded_source_hash"] == traffic_src["library_source_hash"]
+    if traffic_src["current"]:
         if args.workload == "C2":   # the committed minibatch-kernel PMC passes are C2-shaped
             roofline["traffic"] = pmc.get(roofline["kernel"], {}).get("hbm_bytes_per_launch")
             for st, ent in rooflines.items():
@@ -427,12 +474,20 @@ def main():
         ew = 16 if gN % 16 == 0 else 8 if gN % 8 == 0 else 4
         grid = (gN // ew) * (8 if ew >= 8 else 4) * 64
         rooflines["gae"]["traffic"] = pmc.get(f"k_gae_staged[grid={grid}]", {}).get("hbm_bytes_per_launch")
+    roofline["traffic_source"] = traffic_src
 
     # ---- CPU baseline (rank 0, N=1 only): oracle restatement on the host cores ----
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_minibatches > 0 and pixel:
+    if rank == 0 and world == 1 and args.cpu_minibatches != 0:
+        import datetime
+        import platform
+        cores, aff, quota = usable_cores()
+        host = {"cores": cores, "affinity_cores": aff, "cgroup_quota_cores": quota,
+                "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": _cpu_model(),
+                "measured_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
+                "host": platform.node()}
+    if cpu is None and rank == 0 and world == 1 and args.cpu_minibatches != 0 and pixel:
         from oracle.cpu_ppo import run_cpu_baseline_cnn
-        cores = min(len(os.sched_getaffinity(0)), 16)
         r = run_cpu_baseline_cnn(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,
                                  in_shape=tuple(pm.in_shape), n_actions=pm.n_actions, valid=cfg.valid_actions,
                                  clip=cfg.clip_range, ent_coef=cfg.ent_coef, lr=cfg.policy_lr, threads=cores)
@@ -440,33 +495,40 @@ def main():
                "sample": (f"8 vector steps of the torch-CPU NatureCNN policy on {N} envs + 3 of "
                           f"{r['minibatches_per_rollout']} minibatch steps (B={cfg.batch_size}), extrapolated; env "
                           f"emulation excluded; wall {r['wall_s']:.1f}s"),
-               "step_ms": round(r["step_s"] * 1e3, 3), "minibatch_ms": round(r["minibatch_s"] * 1e3, 3)}
-    elif rank == 0 and world == 1 and args.cpu_minibatches > 0:
+               "step_ms": round(r["step_s"] * 1e3, 3), "minibatch_ms": round(r["minibatch_s"] * 1e3, 3), **host}
+    elif cpu is None and rank == 0 and world == 1 and args.cpu_minibatches != 0:
         from oracle.cpu_ppo import run_cpu_baseline
-        # the box's CPU share is 16 threads per GPU (os.sched_getaffinity shows the whole
-        # machine there): use at most that many, report both
-        cores = min(len(os.sched_getaffinity(0)), 16)
         r = run_cpu_baseline(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,
                              obs_dim=pm.obs_dim, hidden=tuple(pm.hidden_dims), n_actions=pm.n_actions,
                              gamma=cfg.gamma, lam=cfg.gae_lambda, clip=cfg.clip_range, lr=cfg.policy_lr,
-                             max_minibatches=args.cpu_minibatches, threads=cores)
+                             max_minibatches=args.cpu_minibatches if args.cpu_minibatches > 0 else None,
+                             threads=cores)
+        whole = r["minibatches_timed"] == r["minibatches_per_rollout"]
         cpu = {"value": round(r["env_steps_per_s"], 2), "unit": "env_steps/s", "cores": r["threads"], "kind": "port",
                "sample": (f"1 rollout of {N}x{T} env steps (torch-CPU policy, numpy synthetic env, numpy GAE) + "
-                          f"{r['minibatches_timed']} of {r['minibatches_per_rollout']} minibatch steps "
-                          f"(torch-CPU fwd/bwd/clip/Adam), update extrapolated; wall {r['wall_s']:.1f}s"),
+                          f"{'all ' if whole else ''}{r['minibatches_timed']} of {r['minibatches_per_rollout']} "
+                          f"minibatch steps (torch-CPU fwd/bwd/clip/Adam){'' if whole else ', update extrapolated'}; "
+                          f"wall {r['wall_s']:.1f}s"),
                "collect_s": round(r["collect_s"], 4), "minibatch_ms": round(r["minibatch_s"] * 1e3, 4),
-               "affinity_cores": len(os.sched_getaffinity(0)),
-               # measured in the build container, same 8 cores, same C2 shapes:
-               # port 5 646 env-steps/s vs the reference's own loop 2 814
+               # per-minibatch time of each tenth of the timed minibatches: their spread is how far an
+               # extrapolation from a shorter sample (or a noisy neighbour) could move the value
+               "window_minibatch_ms": [round(x * 1e3, 4) for x in r["window_minibatch_s"]],
+               **host,
+               # measured in the build container (8-core Intel Xeon, 8 threads, torch 2.10 CPU, round 1, C2
+               # shapes): port 5 646 env-steps/s vs the reference's own loop 2 814
                "calibration_port_over_reference": CPU_PORT_OVER_REFERENCE,
+               "calibration_provenance": CALIBRATION_PROVENANCE,
                "reference_equivalent_value": round(r["env_steps_per_s"] / CPU_PORT_OVER_REFERENCE, 2),
                "calibration": ("the port omits the reference's Lightning training_step, DataLoader collate and "
                                "metrics-recorder overheads; divided by the measured ratio it estimates the "
                                "reference loop on these cores")}
 
+    if comm is not None:       # a timed-out exchange never yields a bench line
+        from gsamd.distributed import comm_status
+        comm_status(comm)
     if rank == 0:
         line = {
-            "metric": "env steps/sec (rollout+PPO update), CartPole n_envs=4096, 1/2/4/8 MI355X",
+            "metric": METRICS[args.workload].format(n=N),
             "value": round(value, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -490,8 +552,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if comm is not None:
-        from gsamd.distributed import comm_status, destroy_comm
-        comm_status(comm)
+        from gsamd.distributed import destroy_comm
         del agent
         destroy_comm(comm)
     if world > 1:

@@ -31,11 +31,12 @@ def _obj(src):
     return os.path.join(BUILD, src + ".o")
 
 
-def _compile(src, build_dir=None, defines=()):
-    path = os.path.join(CSRC, src)
+def _compile(src, build_dir=None, defines=(), csrc=None):
+    csrc = csrc or CSRC
+    path = os.path.join(csrc, src)
     obj = os.path.join(build_dir, src + ".o") if build_dir else _obj(src)
     deps = [path, os.path.join(HERE, "..", "include", "gsamd.h")] + [
-        os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+        os.path.join(csrc, h) for h in os.listdir(csrc) if h.endswith(".h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return None
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-c", path, "-o", obj]
@@ -65,13 +66,31 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     return LIB
 
 
-def build_variant(out_path: str, defines, jobs: int = 8) -> str:
-    """Diagnostic variant (e.g. GS_STAMPS phase timers) built into its own directory."""
-    bdir = os.path.join(BUILD, "variant_" + "_".join(defines))
+def build_variant(out_path: str, defines, jobs: int = 8, patches=(), tag: str = "") -> str:
+    """Diagnostic variant (e.g. GS_STAMPS phase timers) built into its own directory.  patches:
+    (file, old, new) source substitutions applied to a copy of csrc/ (timing experiments live in
+    tools/ab_experiments.py, not in the product sources)."""
+    import shutil
+    bdir = os.path.join(BUILD, "variant_" + "_".join(list(defines) + ([tag] if tag else [])))
     os.makedirs(bdir, exist_ok=True)
+    csrc = None
+    if patches:
+        # bdir/src/csrc: its sources' "../../include/gsamd.h" resolves to bdir/include -> include/
+        csrc = os.path.join(bdir, "src", "csrc")
+        shutil.rmtree(os.path.dirname(csrc), ignore_errors=True)
+        shutil.copytree(CSRC, csrc)
+        inc = os.path.join(bdir, "include")
+        if not os.path.exists(inc):
+            os.symlink(os.path.join(HERE, "..", "include"), inc)
+        for f, old, new in patches:
+            fp = os.path.join(csrc, f)
+            text = open(fp).read()
+            if old not in text:
+                raise RuntimeError(f"experiment patch does not apply to {f}: {old[:60]!r}...")
+            open(fp, "w").write(text.replace(old, new))
     srcs = _sources()
     with ThreadPoolExecutor(max_workers=min(jobs, len(srcs))) as ex:
-        list(ex.map(lambda s: _compile(s, bdir, defines), srcs))
+        list(ex.map(lambda s: _compile(s, bdir, defines, csrc), srcs))
     objs = [os.path.join(bdir, s + ".o") for s in srcs]
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_path] + objs + [
         "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]

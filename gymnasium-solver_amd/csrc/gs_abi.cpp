@@ -25,6 +25,6 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line)
 
 }  // namespace gs
 
-extern "C" int gs_abi_version(void) { return 1; }
+extern "C" int gs_abi_version(void) { return GS_ABI_VERSION; }
 
 extern "C" const char *gs_last_error(void) { return gs::t_err; }

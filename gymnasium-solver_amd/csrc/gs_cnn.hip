@@ -634,7 +634,14 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
                                                         const double *__restrict__ part, int nparts, AdamArgs aa,
                                                         float *__restrict__ metrics, const int32_t *__restrict__ stop)
 {
-    if (stop && *stop) return;
+    if (stop && *stop) {
+        // a job-wide stop (the exchange ORs the ranks' stop bits): no step on any rank
+        if (metrics && blockIdx.x == 0 && threadIdx.x == 0) {
+            metrics[GS_M_SKIPPED] = 1.0f;
+            metrics[GS_M_KL_STOP] = 1.0f;
+        }
+        return;
+    }
     __shared__ double sred[256 + 16];
     __shared__ float s_coef;
     double s[1] = {0.0};

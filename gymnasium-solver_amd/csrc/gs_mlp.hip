@@ -174,13 +174,8 @@ __device__ __forceinline__ float adam_param(float graw, float coef, float &m, fl
     // correctly rounded divisions: IEEE division lowers to a v_div_scale / v_div_fmas /
     // v_div_fixup sequence serialised through VCC, ~10x the latency, and this runs 4-21 times
     // per thread on the minibatch chain's critical path
-#ifdef GS_EXP_NO_TRANS      // timing experiment only (wrong results): Adam without sqrt / rcp
-    const float denom = v * inv_bc2s + aa.eps;
-    p = p + neg_step * (m * denom);
-#else
     const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2s + aa.eps;
     p = p + neg_step * (m * __builtin_amdgcn_rcpf(denom));
-#endif
     return g;
 }
 
@@ -282,18 +277,8 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         const int64_t kprev = kstep - 1 + af.force;
         const bool apply = kprev >= 0;
         const bool own1 = apply && cb == 0 && rb == 0, own2 = apply && rb == 0;
-#ifdef GS_EXP_SPLIT_STORES
-        const int gy = (int)gridDim.y, gx = (int)gridDim.x;
-        const bool stW2[3] = {apply && rb == 0, apply && rb == 1 % gy, apply && rb == 2 % gy};
-        const bool stW1[3] = {apply && rb == 3 % gy && cb == 0, apply && rb == 3 % gy && cb == 1 % gx,
-                              apply && rb == 3 % gy && cb == 2 % gx};
-#elif defined(GS_EXP_NO_OWNER_STORES)      // timing experiment only: the new set is never stored
-        const bool stW2[3] = {false, false, false};
-        const bool stW1[3] = {false, false, false};
-#else
         const bool stW2[3] = {own2, own2, own2};
         const bool stW1[3] = {own1, own1, own1};
-#endif
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         // global-address-space float4 loads (the AdamFwd pointers would otherwise lower to flat,
         // and a predicated float4 select to four dword loads); the moment / gradient buffers are
@@ -331,11 +316,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             for (int j = 0; j < NQ; ++j)
 #pragma unroll
                 for (int b = 0; b < NRB; ++b)
-#ifdef GS_EXP_ONE_PARTIAL      // timing experiment only: one partial row block loaded
-                    t[j][b] = b == 0 ? ld4(af.part1, min(tid + 256 * j, nq1 - 1)) : z4;
-#else
                     t[j][b] = ld4(af.part1 + (int64_t)b * n1, min(tid + 256 * j, nq1 - 1));
-#endif
         } else {
 #pragma unroll
             for (int j = 0; j < NQ; ++j) {
@@ -465,16 +446,9 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
                 w2r[j] = make_float4(p[0], p[1], p[2], p[3]);
                 // this column block's 16 new W2 rows: p by row block 0, m by 1, v by 2 (16 KB each)
                 const int64_t q = (Lc.oW2 + (int64_t)(c0 + i) * cH1) / 4 + k4;
-#ifdef GS_EXP_NT_STORES      // experiment: non-temporal stores for the new W2 rows
-                typedef float f4v __attribute__((ext_vector_type(4)));
-                if (stW2[0]) __builtin_nontemporal_store(f4v{w2r[j].x, w2r[j].y, w2r[j].z, w2r[j].w}, reinterpret_cast<f4v *>(af.Pout) + q);
-                if (stW2[1]) __builtin_nontemporal_store(f4v{m[0], m[1], m[2], m[3]}, reinterpret_cast<f4v *>(af.Mout) + q);
-                if (stW2[2]) __builtin_nontemporal_store(f4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4v *>(af.Vout) + q);
-#else
                 if (stW2[0]) reinterpret_cast<float4 *>(af.Pout)[q] = w2r[j];
                 if (stW2[1]) reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);
                 if (stW2[2]) reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);
-#endif
             }
         }
         auto step_slice = [&](float (&e)[4], int64_t o, bool own) {
@@ -667,11 +641,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             }
         }
     };
-#ifdef GS_EXP_LATE_X_H1      // timing experiment: the stores after the heads, as with 256 threads
-    constexpr bool kEarly = false;
-#else
     constexpr bool kEarly = NT == 512;
-#endif
     if (kEarly && wave >= 4) store_x_h1(tid - 256, 256);
     // ---- phase 2: h2 tile = h1[16 x H1] . W2[c0:c0+16, :]^T, MFMA, K split over 4 waves
     //      (waves 0..3 of a wider block: the K ranges and their sum order stay those of 4 waves)
@@ -2249,7 +2219,16 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
                                                    AdamArgs aa, float *__restrict__ metrics,
                                                    const int32_t *__restrict__ stop)
 {
-    if (stop && *stop) return;
+    if (stop && *stop) {
+        // a job-wide stop (the exchange ORs the ranks' stop bits): this minibatch takes no step on
+        // any rank, also on one whose own approx_kl stayed under target_kl — its record says so
+        if (metrics && blockIdx.x == 0 && threadIdx.x == 0) {
+            float *m = metrics + (aa.step_base ? *aa.step_base : 0) * GS_NUM_METRICS;
+            m[GS_M_SKIPPED] = 1.0f;
+            m[GS_M_KL_STOP] = 1.0f;
+        }
+        return;
+    }
     GS_STAMP_BEGIN(3)
     const int64_t kb = aa.step_base ? *aa.step_base : 0;
     if (metrics) metrics += kb * GS_NUM_METRICS;

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Pa
                 break;
             }
             if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout) {
-                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                record_timeout(err, kWaitExchange, tid, w);
                 failed = true;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -248,7 +248,7 @@ __device__ __forceinline__ int wait_flags(const XgmiArgs &xa, size_t off, int w,
                 break;
             }
             if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout) {
-                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                record_timeout(err, off == kXgmiOffFlags ? kWaitRsagScatter : kWaitRsagGather, tid, w);
                 failed = true;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -381,9 +381,11 @@ bool xgmi_bwd_args(const gs_comm *c, BwdXchg *bx)
     if (c->kind != kCommXgmi || !c->connected || !c->bwd_xchg) return false;
     // ranks sharing a GPU belong to different processes, whose workgroups the GPU does not keep
     // resident together: a workgroup waiting for its peer can hold the CU until the scheduler
-    // time-slices the processes (ms per minibatch) — the exchange launch is used there unless
-    // GS_XGMI_BWD=1 asks for the in-backward form anyway
-    if (c->colocated > 1 && c->bwd_xchg != 2) return false;
+    // time-slices the processes (ms per minibatch) — the exchange launch is used there, and
+    // wherever the launcher has not reported one rank per GPU, unless GS_XGMI_BWD=1 asks for the
+    // in-backward form anyway
+    // colocation unknown (0: the launcher never called gs_comm_xgmi_set_colocation) counts as shared
+    if (c->colocated != 1 && c->bwd_xchg != 2) return false;
     *bx = BwdXchg{};
     bx->world = c->nranks;
     bx->rank = c->rank;
@@ -489,7 +491,7 @@ extern "C" int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint
     // a separate exchange launch, GS_XGMI_BWD=1 also uses it for ranks sharing a GPU (tests: the
     // ranks' kernels then rely on the GPU time-slicing the processes, correct but slow)
     c->bwd_xchg = 1;
-    c->colocated = 1;
+    c->colocated = nranks == 1 ? 1 : 0;      // unknown until the launcher reports it
     if (const char *b = getenv("GS_XGMI_BWD")) c->bwd_xchg = b[0] == '0' ? 0 : b[0] == '1' ? 2 : 1;
     // reduce-scatter + all-gather from 4 ranks on (2n/world floats per link instead of n, one more
     // flag round trip); GS_XGMI_ALGO=oneshot|rsag overrides
@@ -532,12 +534,29 @@ extern "C" int gs_comm_status(gs_comm *c)
 {
     GS_REQUIRE(c, "gs_comm_status: null communicator");
     if (c->kind != kCommXgmi) return GS_OK;
-    uint32_t err = 0;
-    GS_HIP(hipMemcpy(&err, c->local + kXgmiOffErr, sizeof(err), hipMemcpyDeviceToHost));
-    if (err) {
-        set_error("xGMI exchange timed out waiting for a peer (rank %d of %d)", c->rank, c->nranks);
+    uint32_t err[2] = {0u, 0u};
+    GS_HIP(hipMemcpy(err, c->local + kXgmiOffErr, sizeof(err), hipMemcpyDeviceToHost));
+    if (err[0]) {
+        static const char *const where[] = {"?", "exchange launch", "reduce-scatter", "all-gather",
+                                            "k_bwd exchange push", "k_bwd exchange result"};
+        const uint32_t site = err[1] >> 28, src = (err[1] >> 20) & 0xffu, wg = (err[1] & 0xfffffu);
+        set_error("xGMI exchange timed out waiting for a peer (rank %d of %d): workgroup %d waited for rank %u "
+                  "in the %s (GS_XGMI_TIMEOUT_S); the parameters of this update are not the exchanged mean",
+                  c->rank, c->nranks, (int)wg - 1, src, where[site <= 5 ? site : 0]);
         return GS_E_COMM;
     }
+    return GS_OK;
+}
+
+extern "C" int gs_comm_error_record(gs_comm *c, int *timed_out, int *workgroup, int *peer, int *site)
+{
+    GS_REQUIRE(c, "gs_comm_error_record: null communicator");
+    uint32_t err[2] = {0u, 0u};
+    if (c->kind == kCommXgmi) GS_HIP(hipMemcpy(err, c->local + kXgmiOffErr, sizeof(err), hipMemcpyDeviceToHost));
+    if (timed_out) *timed_out = err[0] ? 1 : 0;
+    if (workgroup) *workgroup = err[0] ? (int)(err[1] & 0xfffffu) - 1 : -1;
+    if (peer) *peer = err[0] ? (int)((err[1] >> 20) & 0xffu) : -1;
+    if (site) *site = err[0] ? (int)(err[1] >> 28) : 0;
     return GS_OK;
 }
 

@@ -37,6 +37,25 @@ __device__ __forceinline__ float load_sc1_f(__amdgpu_buffer_rsrc_t rs, uint32_t 
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 16));
 }
 
+// ---- timeout record -------------------------------------------------------------------
+// The sticky error area of a region: err[0] bit 0 = a wait timed out (every later wait then
+// gives up at once); err[1] = the first timeout's record, (where << 28) | (src << 20) | (wg + 1),
+// set once (compare-and-swap from 0), which gs_comm_status reports.
+enum XgmiWaitSite : uint32_t {
+    kWaitExchange = 1,     // k_xgmi_exchange
+    kWaitRsagScatter = 2,  // k_xgmi_rsag, reduce-scatter flags
+    kWaitRsagGather = 3,   // k_xgmi_rsag, all-gather flags
+    kWaitBwd1 = 4,         // k_bwd in-kernel exchange, push flags
+    kWaitBwd2 = 5,         // k_bwd in-kernel exchange (rsag form), owner result flags
+};
+__device__ __forceinline__ void record_timeout(uint32_t *err, uint32_t where, int src, int w)
+{
+    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t expect = 0u;
+    __hip_atomic_compare_exchange_strong(err + 1, &expect, (where << 28) | ((uint32_t)src << 20) | (uint32_t)(w + 1),
+                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- the exchange inside k_bwd --------------------------------------------------------
 
 // raise flag [rank][w] = seq << 1 at byte offset `off` of every rank in `mask` (after this
@@ -62,7 +81,7 @@ __device__ __forceinline__ void bx_wait(const BwdXchg &bx, uint32_t off, int w, 
         while (!failed) {
             if ((__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 1) >= seq) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > bx.timeout) {
-                __hip_atomic_fetch_or(bx.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                record_timeout(bx.err, off == bx.off_flags1 ? kWaitBwd1 : kWaitBwd2, tid, w);
                 failed = true;
             }
             __builtin_amdgcn_s_sleep(1);

@@ -16,6 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before the library)
 LIB_PATH = os.environ.get("GSAMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
 
 GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
+GS_ABI_VERSION = 2          # include/gsamd.h: the argument lists this binding declares
 GS_NUM_METRICS = 16
 METRIC_SLOTS = (
     "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
@@ -111,6 +112,7 @@ def _load():
         "gs_comm_xgmi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, vp, ctypes.POINTER(vp)]),
         "gs_comm_xgmi_connect": (ctypes.c_int, [vp, vp]),
         "gs_comm_status": (ctypes.c_int, [vp]),
+        "gs_comm_error_record": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "gs_comm_xgmi_set_colocation": (ctypes.c_int, [vp, ctypes.c_int]),
         "gs_comm_allreduce_mean_f32": (ctypes.c_int, [vp, vp, i64, vp]),
         "gs_comm_info": (ctypes.c_int, [vp, vp, vp, vp]),
@@ -120,6 +122,9 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if L.gs_abi_version() != GS_ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} implements C-ABI version {L.gs_abi_version()}, this binding version "
+                          f"{GS_ABI_VERSION}: rebuild the library (__graft_entry__.build())")
     return L
 
 
@@ -132,7 +137,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
-            "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status",
+            "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status", "gs_comm_error_record",
             "gs_comm_xgmi_set_colocation",
             "gs_comm_allreduce_mean_f32", "gs_comm_info", "gs_comm_destroy")
 

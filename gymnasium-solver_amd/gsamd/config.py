@@ -54,12 +54,26 @@ class PPOConfig:
     frame_stack: Optional[int] = None
     accelerator: str = "auto"
     spec: Dict[str, Any] = field(default_factory=dict)
+    # env construction fields the env choice depends on (utils/config.py:96-151, get_env_args :676-696)
+    max_episode_steps: Optional[int] = None
+    seed_train: int = 42
+    seed_val: int = 1042
+    seed_test: int = 2042
+    env_wrappers: List[Any] = field(default_factory=list)
+    env_kwargs: Dict[str, Any] = field(default_factory=dict)
+    normalize_obs: Any = False
     # device-path extras (not reference fields): synthetic env shape for bench / tests
     obs_dim: Optional[int] = None
     n_actions: Optional[int] = None
     episode_len: int = 200
     truncate_every: int = 0
-    env_dynamics: str = "synthetic"   # "synthetic" (SURVEY §8d fixed-length episodes) | "cartpole" (f1)
+    # which env the agent steps when the caller passes none (device_env_kind):
+    #   "auto"      the env_id's own dynamics where the device implements them (CartPole-v1),
+    #               otherwise the caller must pass the host VectorEnv (raises if not)
+    #   "synthetic" the fixed-length-episode synthetic env of SURVEY §8d (bench / tests), or the
+    #               synthetic Atari frame source for rgb configs
+    #   "cartpole"  device CartPole-v1 dynamics
+    env_dynamics: str = "auto"
     # {param: {schedule, start_value, end_value, start, end, warmup}} (gsamd.schedules)
     schedules: Dict[str, Dict[str, Any]] = field(default_factory=dict)
 
@@ -110,6 +124,8 @@ class PPOConfig:
                              f"rollout_size={rollout}, batch_size={self.batch_size}.")
         if self.normalize_advantages not in ("batch", "rollout", "off", False, None, ""):
             raise ValueError("normalize_advantages must be 'rollout', 'batch', or 'off'.")
+        if str(self.env_dynamics or "auto") not in ENV_DYNAMICS:
+            raise ValueError(f"env_dynamics must be one of {ENV_DYNAMICS}, got {self.env_dynamics!r}")
 
     # --- derived -----------------------------------------------------------------------
     @property
@@ -147,6 +163,32 @@ class PPOConfig:
 
 _FIELDS = {f.name for f in dataclasses.fields(PPOConfig)}
 _ALIASES = {"LunarLander-v2": "LunarLander-v3"}
+
+ENV_DYNAMICS = ("auto", "synthetic", "cartpole")
+# env ids whose dynamics the device implements, as BaseAgent.build_env would build them from a
+# config without wrappers / env kwargs / observation normalisation
+DEVICE_DYNAMICS = {"CartPole-v1": "cartpole"}
+
+
+def device_env_kind(cfg) -> Optional[str]:
+    """The device env a config trains on when the caller passes no env: "synthetic",
+    "cartpole", or None when the config names an env the device does not simulate — the
+    caller then passes the host VectorEnv the reference would build
+    (agents/base_agent.py:129-192 → utils/environment.py:421-425 build_env_from_config)."""
+    mode = str(getattr(cfg, "env_dynamics", None) or "auto")
+    if mode != "auto":
+        return mode
+    if str(getattr(cfg, "obs_type", "vector")) == "rgb":
+        return None
+    kind = DEVICE_DYNAMICS.get(str(getattr(cfg, "env_id", "")))
+    plain = (not getattr(cfg, "env_wrappers", None) and not getattr(cfg, "env_kwargs", None)
+             and not getattr(cfg, "normalize_obs", False) and getattr(cfg, "frame_stack", None) in (None, 0, 1))
+    return kind if plain else None
+
+
+def needs_host_env(cfg) -> bool:
+    """True when build_agent(cfg) needs env= (a gymnasium VectorEnv built on the host)."""
+    return device_env_kind(from_reference_config(cfg)) is None
 
 
 def _sanitize(name: str) -> str:

@@ -184,6 +184,14 @@ def comm_status(handle: Optional[int]) -> None:
         check(lib.gs_comm_status(handle), "gs_comm_status")
 
 
+def comm_error_record(handle: int) -> dict:
+    """The first exchange timeout's record (include/gsamd.h gs_comm_error_record)."""
+    t, w, p, site = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib.gs_comm_error_record(handle, ctypes.byref(t), ctypes.byref(w), ctypes.byref(p), ctypes.byref(site)),
+          "gs_comm_error_record")
+    return {"timed_out": bool(t.value), "workgroup": w.value, "peer": p.value, "site": site.value}
+
+
 def init_local_comm(transport: str = "rccl", max_count: int = 1 << 20) -> int:
     """A one-rank communicator (no torch.distributed needed): exercises the multi-GPU kernel
     chain and the transport's call on a single GPU."""

@@ -81,6 +81,12 @@ class MetricsRecorder:
         s, c = self._ns(namespace)
         return {k: s[k] / c[k] for k in s if c[k]}
 
+    def sums_counts(self, namespace: str, keys) -> np.ndarray:
+        """(2, len(keys)) float64: the sum and the record count of each key (zeros for a key with
+        no record) — a fixed-length vector a multi-rank job can all-reduce."""
+        s, c = self._ns(namespace)
+        return np.array([[s.get(k, 0.0) for k in keys], [float(c.get(k, 0)) for k in keys]], np.float64)
+
     def reset_epoch(self, namespace: str) -> None:
         s, c = self._ns(namespace)
         s.clear()

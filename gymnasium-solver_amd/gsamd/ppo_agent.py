@@ -24,11 +24,12 @@ import torch
 
 from ._lib import GS_NUM_METRICS, M, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
 from .atari_env import DeviceAtariVecEnv
+from .config import device_env_kind
 from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
-from .distributed import allreduce_sum_f64, world_active
+from .distributed import allreduce_sum_f64, comm_status, world_active
 from .metrics import MetricsRecorder, ppo_keys, ppo_records
 from .schedules import SCHEDULABLE, build_schedulers
 
@@ -48,8 +49,10 @@ class MinibatchIndices:
 
 class DevicePPOAgent:
     def __init__(self, config, env=None, device: Optional[str] = None, rank: int = 0, world_size: int = 1,
-                 comm=None, use_graph: bool = True, track_stats: bool = True, one_launch: bool = True):
+                 comm=None, use_graph: bool = True, track_stats: bool = True, one_launch: bool = True,
+                 env_factory=None):
         self.config = config
+        self.env_factory = env_factory       # stage -> host VectorEnv (configs without device dynamics)
         self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
         self.rank, self.world_size, self.comm = int(rank), int(world_size), comm
         self.use_graph = bool(use_graph)
@@ -81,20 +84,43 @@ class DevicePPOAgent:
 
     # ---- construction (base_agent.py:103-222) -------------------------------------------
     def build_env(self, stage: str, env=None):
+        """BaseAgent.build_env (base_agent.py:129-192): the env the config names.  A passed env
+        (the host VectorEnv build_env_from_config returns, or a device env) is used as is;
+        otherwise env_factory(stage) when given, otherwise the device dynamics of
+        config.device_env_kind — and a config naming an env the device does not simulate
+        raises instead of training on a stand-in."""
         c = self.config
-        if env is None and self.is_pixel:
-            env = DeviceAtariVecEnv(n_envs=c.n_envs, n_actions=c.resolved_n_actions(), episode_len=c.episode_len,
-                                    seed=c.seed, truncate_every=c.truncate_every, env_offset=self.rank * c.n_envs,
-                                    frame_stack=int(c.frame_stack or 4), device=self.device)
-        if env is None and str(getattr(c, "env_dynamics", "synthetic")) == "cartpole":
-            if c.resolved_obs_dim() != 4 or c.resolved_n_actions() != 2:
-                raise ValueError("env_dynamics='cartpole' needs obs_dim 4 and 2 actions")
-            env = DeviceCartPoleVecEnv(c.n_envs, seed=c.seed, env_offset=self.rank * c.n_envs, device=self.device)
+        if env is None and self.env_factory is not None and device_env_kind(c) is None:
+            env = self.env_factory(stage)
         if env is None:
-            env = DeviceSyntheticVecEnv(n_envs=c.n_envs, obs_dim=c.resolved_obs_dim(), n_actions=c.resolved_n_actions(),
-                                        episode_len=c.episode_len, seed=c.seed, truncate_every=c.truncate_every,
-                                        env_offset=self.rank * c.n_envs, device=self.device)
+            env = self._device_env(stage)
+        if int(getattr(env, "num_envs", c.n_envs)) != int(c.n_envs):
+            raise ValueError(f"env has {env.num_envs} envs, config.n_envs is {c.n_envs}")
         self._envs[stage] = env
+
+    def _device_env(self, stage: str):
+        c = self.config
+        kind = device_env_kind(c)
+        if kind is None:
+            raise ValueError(
+                f"env_id {c.env_id!r} (obs_type {c.obs_type!r}) has no device dynamics: pass env=<the gymnasium "
+                f"VectorEnv build_env_from_config(config, seed=config.seed_train) returns> (or env_factory=), or "
+                f"set env_dynamics='synthetic' for the fixed-length synthetic env of the benchmark")
+        off = self.rank * c.n_envs
+        train = stage == "train"
+        if kind == "cartpole":
+            if self.is_pixel or c.resolved_obs_dim() != 4 or c.resolved_n_actions() != 2:
+                raise ValueError("env_dynamics='cartpole' needs vector observations of dim 4 and 2 actions")
+            return DeviceCartPoleVecEnv(c.n_envs, seed=c.seed_train if train else c.seed_val, env_offset=off,
+                                        max_steps=int(c.max_episode_steps or 500), device=self.device)
+        seed = c.seed if train else c.seed + 1000
+        if self.is_pixel:
+            return DeviceAtariVecEnv(n_envs=c.n_envs, n_actions=c.resolved_n_actions(), episode_len=c.episode_len,
+                                     seed=seed, truncate_every=c.truncate_every, env_offset=off,
+                                     frame_stack=int(c.frame_stack or 4), device=self.device)
+        return DeviceSyntheticVecEnv(n_envs=c.n_envs, obs_dim=c.resolved_obs_dim(), n_actions=c.resolved_n_actions(),
+                                     episode_len=c.episode_len, seed=seed, truncate_every=c.truncate_every,
+                                     env_offset=off, device=self.device)
 
     def get_env(self, stage: str):
         return self._envs[stage]
@@ -104,16 +130,33 @@ class DevicePPOAgent:
         """rgb observations -> NatureCNN + Atari pipeline (C4/C5), else the MLP path."""
         return str(getattr(self.config, "obs_type", "vector")) == "rgb"
 
+    def _env_shapes(self):
+        """(observation shape, action count) of the train env: a device env's own attributes, a
+        host VectorEnv's single spaces (build_policy_from_env_and_config, policy_factory.py:79-130),
+        else the config's spec."""
+        c, env = self.config, self.get_env("train")
+        shape = getattr(env, "obs_shape", None)
+        n_act = getattr(env, "n_actions", None)
+        osp, asp = getattr(env, "single_observation_space", None), getattr(env, "single_action_space", None)
+        if shape is None and getattr(env, "obs_dim", None) is not None:
+            shape = (int(env.obs_dim),)
+        if shape is None and getattr(osp, "shape", None) is not None:
+            shape = tuple(int(x) for x in osp.shape)
+        if n_act is None and getattr(asp, "n", None) is not None:
+            n_act = int(asp.n)
+        shape = tuple(shape) if shape is not None else (c.resolved_obs_dim(),)
+        return shape, int(n_act if n_act is not None else c.resolved_n_actions())
+
     def build_models(self):
         c = self.config
+        shape, n_act = self._env_shapes()
         if self.is_pixel:
-            env = self.get_env("train")
-            self.policy_model = DeviceCNNActorCritic(in_shape=tuple(env.obs_shape), n_actions=c.resolved_n_actions(),
-                                                     hidden=int(c.hidden_dims[0]), valid_actions=c.valid_actions,
-                                                     device=self.device)
+            self.policy_model = DeviceCNNActorCritic(in_shape=shape, n_actions=n_act, hidden=int(c.hidden_dims[0]),
+                                                     valid_actions=c.valid_actions, device=self.device)
         else:
-            self.policy_model = DeviceMLPActorCritic(c.resolved_obs_dim(), c.hidden_dims, c.resolved_n_actions(),
-                                                     device=self.device)
+            if len(shape) != 1:
+                raise ValueError(f"the MLP policy needs flat observations, the env gives {shape}")
+            self.policy_model = DeviceMLPActorCritic(int(shape[0]), c.hidden_dims, n_act, device=self.device)
 
     def build_rollout_collector(self, stage: str):
         c = self.config
@@ -124,14 +167,10 @@ class DevicePPOAgent:
 
     def get_rollout_collector(self, stage: str) -> DeviceRolloutCollector:
         if stage not in self._rollout_collectors and stage in ("val", "test"):
-            # evaluation collector: its own env instance (offset seed), same policy
+            # evaluation collector: its own env instance (the stage's seed), same policy
             c = self.config
-            kw = dict(seed=c.seed + 1000, truncate_every=c.truncate_every, env_offset=self.rank * c.n_envs,
-                      episode_len=c.episode_len, device=self.device)
-            env = (DeviceAtariVecEnv(c.n_envs, n_actions=c.resolved_n_actions(), frame_stack=int(c.frame_stack or 4),
-                                     **kw) if self.is_pixel else
-                   DeviceSyntheticVecEnv(c.n_envs, c.resolved_obs_dim(), c.resolved_n_actions(), **kw))
-            self._envs[stage] = env
+            self.build_env(stage)
+            env = self._envs[stage]
             self._rollout_collectors[stage] = DeviceRolloutCollector(
                 env, self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
                 rng_seed=c.seed + 1000 + 7919 * self.rank, track_stats=True)
@@ -411,6 +450,11 @@ class DevicePPOAgent:
                                     1 if self.use_graph else 0, stream_handle()), "gs_ppo_update")
         if ev is not None:
             ev[-1][2].record()
+        if self.comm:
+            # the exchange's sticky timeout record, read once per epoch (one 8-byte D2H after the
+            # update): a peer that never arrived leaves this update on a non-mean gradient, so
+            # training stops here with the workgroup and peer that timed out
+            comm_status(self.comm)
         if self.config.target_kl is None:
             self.adam_step += self.n_minibatches
         else:       # minibatches from the sticky KL stop on took no optimizer step
@@ -449,19 +493,25 @@ class DevicePPOAgent:
             self._early_stop_epoch = True        # sticky, as BaseAgent._early_stop_epoch
         return rec
 
+    def epoch_metric_keys(self):
+        """The fixed key list of epoch_metrics (every rank sends the same vector)."""
+        norm = self.config.normalize_advantages == "batch"
+        return tuple(ppo_keys(norm)) + ("opt/grads/norm/all",)
+
     def epoch_metrics(self) -> Dict[str, float]:
         """The last update's epoch means under the reference's metric keys (ppo_agent.py:131-146,
         torch.py:170-173, base_agent.py:607-608); the recorder's "train" namespace is reset
-        first, so this is exactly one update.  In a multi-rank job the means are averaged over
-        ranks (every rank evaluates the same number of minibatches)."""
+        first, so this is exactly one update.  In a multi-rank job every rank all-reduces the same
+        fixed key list as (sum, count) pairs — a rank whose KL stop left a key without records adds
+        0 to both — and the means are pooled over all ranks' records."""
         self.metrics_recorder.reset_epoch("train")
         self.record_epoch_metrics()
-        out = self.metrics_recorder.compute_epoch_means("train")
-        if world_active():
-            keys = sorted(out)
-            vals = allreduce_sum_f64([out[k] for k in keys]) / float(self.world_size)
-            out = dict(zip(keys, vals))
-        return {k: float(v) for k, v in out.items()}
+        if not world_active():
+            out = self.metrics_recorder.compute_epoch_means("train")
+            return {k: float(v) for k, v in out.items()}
+        keys = self.epoch_metric_keys()
+        sc = allreduce_sum_f64(self.metrics_recorder.sums_counts("train", keys).reshape(-1)).reshape(2, -1)
+        return {k: float(sc[0, j] / sc[1, j]) for j, k in enumerate(keys) if sc[1, j] > 0}
 
     def minibatch_losses(self) -> np.ndarray:
         return self.metrics_buf[:, M["loss"]].cpu().numpy().astype(np.float64)
@@ -489,7 +539,11 @@ class DevicePPOAgent:
 
 def build_agent(config, *args, **kwargs):
     """agents/__init__.py:1-8 for the device path.  Accepts a gsamd PPOConfig or the
-    reference's own Config object (adapted by name, gsamd.config.from_reference_config)."""
+    reference's own Config object (adapted by name, gsamd.config.from_reference_config).
+    The env is the one the config names (DevicePPOAgent.build_env): CartPole-v1 steps on the
+    device CartPole dynamics; any other env_id needs env= / env_factory= (the host VectorEnv
+    the reference's build_env_from_config returns); the synthetic env only with
+    env_dynamics='synthetic'."""
     from .config import from_reference_config
     algo = getattr(getattr(config, "algo_id", None), "value", getattr(config, "algo_id", None))
     if algo != "ppo":

@@ -37,7 +37,12 @@ extern "C" {
 #define GS_E_HIP (-2)       /* HIP runtime error */
 #define GS_E_COMM (-3)      /* RCCL error */
 
-/* ---------------------------------------------------------------- misc */
+/* ---------------------------------------------------------------- misc
+ * gs_abi_version() returns GS_ABI_VERSION of the header the library was built with; a binding
+ * must refuse a library whose version differs (argument lists change between versions:
+ * version 2 added the rollout clock argument of gs_policy_act / gs_cnn_policy_act /
+ * gs_env_step / gs_atari_env_step and gs_comm_error_record). */
+#define GS_ABI_VERSION 2
 int gs_abi_version(void);
 const char *gs_last_error(void);
 
@@ -355,14 +360,21 @@ int gs_comm_init(const uint8_t id[128], int nranks, int rank, struct gs_comm **o
 int gs_comm_xgmi_create(int nranks, int rank, int64_t max_count, uint8_t out_handle[64], struct gs_comm **out);
 int gs_comm_xgmi_connect(struct gs_comm *comm, const uint8_t *handles);
 int gs_comm_status(struct gs_comm *comm);
+/* The first timeout's record (host-only read of the region, synchronous): *timed_out = 1 when a
+ * wait gave up; then *workgroup = the exchange workgroup that waited, *peer = the rank it waited
+ * for, *site = where (1 exchange launch, 2 / 3 reduce-scatter / all-gather flags of the rsag
+ * launch, 4 / 5 push / result flags of the exchange inside k_bwd); -1 / 0 when none.  Any out
+ * pointer may be NULL.  gs_comm_status's message carries the same record. */
+int gs_comm_error_record(struct gs_comm *comm, int *timed_out, int *workgroup, int *peer, int *site);
 /* The MLP update's exchange runs inside the backward kernel (every workgroup waits for the
  * same workgroup of its peers), which needs the peers' workgroups to be resident together.
  * That always holds with one rank per GPU (a node); with c ranks sharing a GPU it needs
  * (c - 1) backward grids to leave a free workgroup slot, and even then the ranks are separate
  * processes, which the GPU time-slices rather than co-schedules.  The launcher reports the
- * largest number of ranks sharing one GPU here (default 1); from 2 the update exchanges with a
- * separate launch after the backward (GS_XGMI_BWD=1 forces the in-backward form where the grids
- * fit: correct, but paced by the time-slicing).  Host-only, no GPU call. */
+ * largest number of ranks sharing one GPU here; until it does (more than one rank) the
+ * colocation counts as unknown and the update exchanges with a separate launch after the
+ * backward, as it does from 2 ranks per GPU (GS_XGMI_BWD=1 forces the in-backward form where the
+ * grids fit: correct, but paced by the time-slicing).  Host-only, no GPU call. */
 int gs_comm_xgmi_set_colocation(struct gs_comm *comm, int ranks_per_device);
 int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
 /* What a communicator is: its rank count, this process's rank and the transport

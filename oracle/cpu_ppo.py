@@ -83,9 +83,10 @@ def _losses(model, obs, actions, old_lp, old_v, adv, ret, clip, clip_vf, vf_coef
 
 
 def run_cpu_baseline(n_envs=4096, n_steps=32, batch=256, n_epochs=20, obs_dim=4, hidden=(256, 256), n_actions=2,
-                     gamma=0.98, lam=0.8, clip=0.1, lr=1e-3, max_minibatches=2000, threads=None, seed=42):
-    """Time one rollout + GAE + `max_minibatches` of the update; extrapolate to the full
-    update (n_envs*n_steps/batch*n_epochs minibatches).  Returns a dict."""
+                     gamma=0.98, lam=0.8, clip=0.1, lr=1e-3, max_minibatches=None, threads=None, seed=42):
+    """Time one rollout + GAE + the update (all n_envs*n_steps/batch*n_epochs minibatches, or the
+    first `max_minibatches` extrapolated).  Returns a dict; window_minibatch_s holds the mean
+    minibatch time of each tenth of the timed minibatches."""
     from gsamd.synthetic_env import SyntheticVecEnv     # shared env spec (host numpy twin)
     if threads:
         torch.set_num_threads(int(threads))
@@ -128,7 +129,9 @@ def run_cpu_baseline(n_envs=4096, n_steps=32, batch=256, n_epochs=20, obs_dim=4,
     order = torch.argsort(torch.rand((n_epochs, N * T), generator=g), dim=1).reshape(-1)
     t3 = time.perf_counter()
     n_total = N * T // batch * n_epochs
-    n_run = min(max_minibatches, n_total)
+    n_run = n_total if max_minibatches is None else min(int(max_minibatches), n_total)
+    marks = [time.perf_counter()]
+    edges = {int(round(n_run * j / 10)) for j in range(1, 11)}
     for k in range(n_run):
         idx = order[k * batch:(k + 1) * batch]
         # collate: the reference slices all 9 trajectory fields per minibatch
@@ -142,12 +145,17 @@ def run_cpu_baseline(n_envs=4096, n_steps=32, batch=256, n_epochs=20, obs_dim=4,
         _grad_norms(model)
         torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
         opt.step()
+        if k + 1 in edges:
+            marks.append(time.perf_counter())
     t4 = time.perf_counter()
     per_mb = (t4 - t3) / max(n_run, 1)
+    bounds = sorted(edges)
+    sizes = [b - a for a, b in zip([0] + bounds[:-1], bounds)]
+    windows = [(marks[j + 1] - marks[j]) / s for j, s in enumerate(sizes) if s > 0]
     rollout_s = (t1 - t0) + (t2 - t1) + (t3 - t2) + per_mb * n_total
     return dict(env_steps_per_s=N * T / rollout_s, collect_s=t1 - t0, gae_s=t2 - t1, sampler_s=t3 - t2,
                 minibatch_s=per_mb, minibatches_timed=n_run, minibatches_per_rollout=n_total,
-                wall_s=t4 - t0, threads=torch.get_num_threads())
+                window_minibatch_s=windows, wall_s=t4 - t0, threads=torch.get_num_threads())
 
 
 class _CNNActorCritic(nn.Module):

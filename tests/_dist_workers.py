@@ -198,11 +198,11 @@ def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", worklo
         dev = torch.device("cuda:0")
         torch.manual_seed(42)
         if workload == "cnn":
-            cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(n_envs=128, n_steps=32))
+            cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=128, n_steps=32))
         elif workload == "lunar":     # C3's MLP shapes: a small backward grid (57 workgroups)
-            cfg = load_config("LunarLander-v3", "ppo", overrides=dict(n_envs=64, n_steps=128, n_epochs=2))
+            cfg = load_config("LunarLander-v3", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, n_steps=128, n_epochs=2))
         else:
-            cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=256, n_epochs=2))
+            cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=256, n_epochs=2))
         agent = DevicePPOAgent(cfg, device=dev, rank=0 if identical else rank, world_size=1 if identical else world,
                                use_graph=use_graph, track_stats=False)
         agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
@@ -222,3 +222,99 @@ def xgmi_ppo_worker(rank, world, port, result_dir, use_graph, lagged="1", worklo
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()
+
+
+def xgmi_oracle_worker(rank, world, port, result_dir, transport="xgmi", algo="", bwd="1", n_steps=8):
+    """One rank of the data-parallel C2-shaped update on its OWN env shard (env_offset = rank x
+    256), for the parent's comparison with the numpy oracle's mean-gradient update: the fused
+    lagged chain's first n_steps minibatches (gs_ppo_update over n_steps, the exchange inside
+    k_bwd (bwd="1", forced also for ranks sharing the GPU) or as a launch after it (bwd="0"), or
+    RCCL).  Saves the initial parameters, the rollout's env-major fields, the index stream, the
+    per-minibatch losses and the final parameters."""
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    os.environ["GS_XGMI_BWD"] = bwd
+    if algo:
+        os.environ["GS_XGMI_ALGO"] = algo
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd._lib import check, lib
+        from gsamd.config import load_config
+        from gsamd.distributed import comm_status, destroy_comm, exchange_inside_bwd, init_device_comm, init_xgmi_comm
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        torch.manual_seed(42)
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=256, n_epochs=1))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        pm = agent.policy_model
+        comm = init_xgmi_comm(rank, world, pm.n_params) if transport == "xgmi" else init_device_comm(rank, world, dev)
+        inside = exchange_inside_bwd(comm, pm.dims, agent.batch_size)
+        agent.train_dataloader()
+        traj = agent._trajectories
+        idx = agent.prefetcher.upload(0)
+        p0 = pm.params.cpu().numpy()
+        torch.cuda.synchronize()
+        dist.barrier()
+        check(lib.gs_ppo_update(pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
+                                agent.adam_v.data_ptr(), pm.dims, agent.hparams(), agent.get_rollout_collector("train")
+                                .buffer.view(), idx.data_ptr(), agent.batch_size, n_steps, 0,
+                                agent.metrics_buf.data_ptr(), agent.stop_flag.data_ptr(), agent.workspace.data_ptr(),
+                                agent.workspace.numel(), comm, 0, torch.cuda.current_stream().cuda_stream),
+              "gs_ppo_update")
+        torch.cuda.synchronize()
+        comm_status(comm)
+        np.savez(os.path.join(result_dir, f"r{rank}.npz"), p0=p0, p1=pm.params.cpu().numpy(),
+                 losses=agent.metrics_buf[:n_steps, 0].cpu().numpy(),
+                 idx=idx[:n_steps * agent.batch_size].cpu().numpy(), obs=traj.observations.cpu().numpy(),
+                 actions=traj.actions.cpu().numpy(), logp=traj.logprobs.cpu().numpy(),
+                 values=traj.values.cpu().numpy(), adv=traj.advantages.cpu().numpy(),
+                 ret=traj.returns.cpu().numpy(), inside=np.int32(inside))
+        dist.barrier()
+        del agent
+        destroy_comm(comm)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def xgmi_timeout_worker(rank, world, port, result_dir):
+    """The designed failure: both ranks connect (self-test included), then rank 1 never runs its
+    update.  Rank 0's train_epoch must raise GsError (the exchange's bounded wait, 2 s) naming
+    the workgroup and the peer it waited for, and exit non-zero (3) — never return a trained
+    model.  Rank 1 waits for rank 0's verdict file and exits 0."""
+    import time
+    os.environ["GS_XGMI_TIMEOUT_S"] = "2"
+    dist = _init(rank, world, port)
+    done = os.path.join(result_dir, "rank0_done")
+    code = 0
+    try:
+        import torch
+        from gsamd._lib import GsError
+        from gsamd.config import load_config
+        from gsamd.distributed import comm_error_record, init_xgmi_comm
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        torch.manual_seed(42)
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, n_epochs=1))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
+        if rank == 1:
+            t0 = time.time()
+            while not os.path.exists(done) and time.time() - t0 < 90:
+                time.sleep(0.1)
+            return
+        try:
+            agent.train_epoch()
+            open(os.path.join(result_dir, "outcome"), "w").write("returned")
+        except GsError as e:
+            import json
+            rec = comm_error_record(agent.comm)
+            json.dump({"message": str(e), **rec}, open(os.path.join(result_dir, "outcome"), "w"))
+            code = 3
+        open(done, "w").write("done")
+    finally:
+        if rank == 0 and not os.path.exists(done):
+            open(done, "w").write("done")
+    os._exit(code)

@@ -13,7 +13,7 @@ def _agent(cuda, env="CartPole-v1", variant="ppo", seed=42, **over):
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(seed)
     base = dict(n_envs=64, n_epochs=2) if variant == "ppo" else dict(n_envs=8, n_steps=16, batch_size=64, n_epochs=1)
-    cfg = load_config(env, variant, overrides=dict(base, **over))
+    cfg = load_config(env, variant, overrides=dict(dict(base, env_dynamics="synthetic"), **over))
     return DevicePPOAgent(cfg, device=cuda, track_stats=False)
 
 
@@ -100,7 +100,7 @@ def test_schedules_applied_between_epochs(cuda):
     from gsamd.ppo_agent import DevicePPOAgent
     from gsamd.schedules import build_schedulers
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=8, n_epochs=1, max_env_steps=8 * 32 * 4))
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=8, n_epochs=1, max_env_steps=8 * 32 * 4))
     cfg.schedules = {"policy_lr": {"schedule": "cosine", "start_value": 1e-3, "end_value": 1e-4, "start": 0.0,
                                    "end": 1.0, "warmup": 0.0},
                      "ent_coef": {"schedule": "linear", "start_value": 0.02, "end_value": 0.0, "start": 0.25,
@@ -135,7 +135,7 @@ def test_scheduled_lr_reuses_the_update_graph(cuda):
         return n.value, c.value
 
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=64, n_epochs=1, max_env_steps=64 * 32 * 8))
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, n_epochs=1, max_env_steps=64 * 32 * 8))
     cfg.schedules = {"policy_lr": {"schedule": "linear", "start_value": 1e-3, "end_value": 1e-4, "start": 0.0,
                                    "end": 1.0, "warmup": 0.0}}
     agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
@@ -174,7 +174,7 @@ def test_rollout_graph_equals_eager(cuda, env, variant, over):
     runs = []
     for use_graph in (False, True):
         torch.manual_seed(42)
-        cfg = load_config(env, variant, overrides=over)
+        cfg = load_config(env, variant, overrides=dict({"env_dynamics": "synthetic"}, **over))
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=True, one_launch=False)
         coll = agent.get_rollout_collector("train")
         rec = []
@@ -212,7 +212,7 @@ def test_one_launch_rollout_equals_step_loop(cuda, env, variant, over):
     runs = []
     for one in (False, True):
         torch.manual_seed(42)
-        cfg = load_config(env, variant, overrides=over)
+        cfg = load_config(env, variant, overrides=dict({"env_dynamics": "synthetic"}, **over))
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=True, one_launch=one)
         coll = agent.get_rollout_collector("train")
         assert coll.one_launch == one

@@ -32,9 +32,9 @@ def _agent_for_step(cuda, tag):
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
     if tag == "cartpole":
-        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=8))
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=8))
     else:
-        cfg = load_config("LunarLander-v3", "ppo", overrides=dict(n_envs=1, n_steps=64, ent_coef=0.01))
+        cfg = load_config("LunarLander-v3", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=1, n_steps=64, ent_coef=0.01))
     return DevicePPOAgent(cfg, device=cuda, use_graph=False)
 
 
@@ -72,7 +72,7 @@ def test_losses_for_batch_on_reference_tensor_batch(golden, cuda, tag):
 def _replay_trajectory(agent, z, cuda, check_metrics=True):
     """Replay the fixture's three rollouts (recorded actions) and updates through the agent's
     collector and gs_ppo_update; returns the per-minibatch device records."""
-    from gsamd._lib import check, lib
+    from gsamd._lib import M, check, lib
     N, T, E, B, D, A = (int(x) for x in z["dims"])
     coll = agent.get_rollout_collector("train")
     names = [str(x) for x in z["roll_metric_names"]]
@@ -106,7 +106,7 @@ def _replay_trajectory(agent, z, cuda, check_metrics=True):
                                 0, torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
         rec = agent.metrics_buf.cpu().numpy().copy()
-        agent.adam_step += int((rec[:, 13] == 0).sum())
+        agent.adam_step += int((rec[:, M["skipped"]] == 0).sum())
         recs.append(rec)
     return np.concatenate(recs)
 
@@ -118,7 +118,7 @@ def _trajectory_agent(cuda, z, host_env=False, **over):
     N, T, E, B, D, A = (int(x) for x in z["dims"])
     L, seed, trunc = (int(x) for x in z["env"])
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(episode_len=L, truncate_every=trunc, obs_dim=D,
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", episode_len=L, truncate_every=trunc, obs_dim=D,
                                                            n_actions=A, **over))
     # host_env: a gymnasium-style host vector env (reset / 5-tuple step / RecordEpisodeStatistics
     # infos) -> the collector's host branch: one H2D of obs and one D2H of actions per step
@@ -192,7 +192,7 @@ def test_reference_checkpoint_resumes(cuda):
     opt = torch.load(os.path.join(d, "optimizer.pt"), map_location="cpu", weights_only=True)
     state = json.load(open(os.path.join(d, "state.json")))
     torch.manual_seed(0)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=8, n_epochs=2))
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=8, n_epochs=2))
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
     agent.load_checkpoint(d)
     torch.cuda.synchronize()
@@ -217,18 +217,25 @@ def test_reference_checkpoint_resumes(cuda):
 @pytest.mark.parametrize("key", ["CartPole-v1:ppo", "ALE-Breakout-v5:rgb_ppo"])
 def test_build_agent_from_reference_config(cuda, key):
     """agents.build_agent(config) with the Config object train.py would pass (every field the
-    reference's load_config resolved): the device agent's hyper-parameters are the reference's."""
+    reference's load_config resolved): the device agent's hyper-parameters are the reference's,
+    and the env is the one the config names — CartPole-v1 on the device CartPole dynamics; an
+    ALE config (no device emulator) only with an explicit env_dynamics='synthetic'."""
     from gsamd import build_agent
+    from gsamd.rollout import DeviceCartPoleVecEnv
     full = json.load(open(os.path.join(GOLDEN, "configs_full.json")))[key]
     want = json.load(open(os.path.join(GOLDEN, "configs.json")))[key]
     ref_cfg = SimpleNamespace(**full)
-    small = dict(n_envs=8, n_steps=128, batch_size=1024) if "ALE" in key else {}
+    small = dict(n_envs=8, n_steps=128, batch_size=1024, env_dynamics="synthetic") if "ALE" in key else {}
     torch.manual_seed(42)
     agent = build_agent(ref_cfg, device=cuda, track_stats=False) if not small else None
     if agent is None:
         from gsamd.config import from_reference_config
         from gsamd.ppo_agent import DevicePPOAgent
+        with pytest.raises(ValueError, match="no device dynamics"):
+            build_agent(ref_cfg, device=cuda, track_stats=False)
         agent = DevicePPOAgent(from_reference_config(ref_cfg, **small), device=cuda, track_stats=False)
+    else:
+        assert isinstance(agent.get_env("train"), DeviceCartPoleVecEnv)
     c = agent.config
     for k in ("n_epochs", "gamma", "gae_lambda", "clip_range", "clip_range_vf", "ent_coef", "vf_coef",
               "policy_lr", "max_grad_norm", "seed", "target_kl", "normalize_advantages", "model_id"):
@@ -241,3 +248,25 @@ def test_build_agent_from_reference_config(cuda, key):
     agent.train_epoch()
     torch.cuda.synchronize()
     assert np.isfinite(agent.minibatch_losses()).all()
+
+
+def test_build_agent_with_host_env_vs_reference_trajectory(golden, cuda):
+    """The drop-in's env hand-off: build_agent(reference Config, env=<host
+    VectorEnv>) — the env build_env_from_config would return, here the host twin of the synthetic
+    env the fixture's reference RolloutCollector stepped — runs the host-env branch of the
+    collector (one H2D of obs and one D2H of actions per step) and reproduces the reference's
+    trajectory.npz: rollout tensors, per-minibatch losses within 1e-4 (the north-star bar)."""
+    from gsamd import build_agent
+    from gsamd.synthetic_env import SyntheticVecEnv
+    z = golden("trajectory.npz")
+    N, T, E, B, D, A = (int(x) for x in z["dims"])
+    L, seed, trunc = (int(x) for x in z["env"])
+    full = json.load(open(os.path.join(GOLDEN, "configs_full.json")))["CartPole-v1:ppo"]
+    assert (full["n_envs"], full["n_steps"], full["batch_size"], full["n_epochs"]) == (N, T, B, E)
+    torch.manual_seed(42)
+    env = SyntheticVecEnv(n_envs=N, obs_dim=D, n_actions=A, episode_len=L, seed=seed, truncate_every=trunc)
+    agent = build_agent(SimpleNamespace(**full), env=env, device=cuda, use_graph=False)
+    assert agent.get_env("train") is env
+    agent.policy_model.load_flat(z["params0"])
+    recs = _replay_trajectory(agent, z, cuda, check_metrics=False)
+    np.testing.assert_allclose(recs[:, 0], z["losses"], atol=1e-4, rtol=0)

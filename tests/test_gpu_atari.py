@@ -47,7 +47,7 @@ def _pixel_agent(cuda, **over):
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
-    cfg = load_config("ALE-Pong-v5", "rgb_ppo", overrides=dict(dict(n_envs=8, n_steps=16, batch_size=64, n_epochs=2),
+    cfg = load_config("ALE-Pong-v5", "rgb_ppo", overrides=dict(dict(env_dynamics="synthetic", n_envs=8, n_steps=16, batch_size=64, n_epochs=2),
                                                                 **over))
     return cfg, DevicePPOAgent(cfg, device=cuda, track_stats=True)
 

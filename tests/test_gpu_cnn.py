@@ -161,7 +161,7 @@ def test_cnn_update_local_comm_equals_no_comm(cuda, transport):
     out = []
     for with_comm in (False, True):
         torch.manual_seed(42)
-        cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(n_envs=64, n_steps=32, n_epochs=2))
+        cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, n_steps=32, n_epochs=2))
         agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
         comm = init_local_comm(transport, agent.policy_model.n_params) if with_comm else None
         agent.comm = comm

@@ -33,7 +33,7 @@ def test_lagged_adam_matches_separate_adam(cuda, monkeypatch, use_graph, n_envs,
     for lag in ("1", "0"):
         monkeypatch.setenv("GS_LAGGED_ADAM", lag)
         torch.manual_seed(7)
-        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=n_envs, n_epochs=n_epochs))
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=n_envs, n_epochs=n_epochs))
         comm = init_local_comm(transport, 70_000) if transport else None
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False, comm=comm)
         coll = agent.get_rollout_collector("train")
@@ -63,7 +63,7 @@ def test_lagged_stage_writes_workspace_set_only(cuda, monkeypatch):
     from gsamd.ppo_agent import DevicePPOAgent
     monkeypatch.setenv("GS_LAGGED_ADAM", "1")
     torch.manual_seed(3)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=512, n_epochs=1))
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=512, n_epochs=1))
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
     agent.train_epoch()
     pm = agent.policy_model

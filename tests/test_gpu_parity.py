@@ -206,7 +206,7 @@ def test_trajectory_replay_vs_reference(golden, cuda):
     N, T, E, B, D, A = (int(x) for x in z["dims"])
     L, seed, trunc = (int(x) for x in z["env"])
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(episode_len=L, truncate_every=trunc, obs_dim=D,
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", episode_len=L, truncate_every=trunc, obs_dim=D,
                                                            n_actions=A))
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=False)
     # initial weights come from the fixture: orthogonal_ init goes through LAPACK QR, whose
@@ -260,7 +260,7 @@ def test_update_graph_equals_eager_and_is_deterministic(cuda, env, variant, n_en
     results = []
     for use_graph in (False, True, True):
         torch.manual_seed(42)
-        cfg = load_config(env, variant, overrides=dict(n_envs=n_envs))
+        cfg = load_config(env, variant, overrides=dict(env_dynamics="synthetic", n_envs=n_envs))
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
         agent.train_epoch()
         agent.train_epoch()
@@ -281,7 +281,7 @@ def test_minibatch_step_vs_numpy_oracle(cuda, env, variant, n_envs):
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
-    cfg = load_config(env, variant, overrides=dict(n_envs=n_envs))
+    cfg = load_config(env, variant, overrides=dict(env_dynamics="synthetic", n_envs=n_envs))
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
     batches = agent.train_dataloader()
     traj = agent._trajectories
@@ -318,7 +318,7 @@ def test_update_first_minibatches_vs_numpy_oracle(cuda, use_graph):
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=4096))
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
     agent.train_dataloader()
     traj = agent._trajectories
@@ -364,7 +364,7 @@ def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph
     out = []
     for fused in (True, False):
         torch.manual_seed(42)
-        cfg = load_config(env, variant, overrides=dict(n_envs=n_envs // 8 if env == "CartPole-v1" else n_envs,
+        cfg = load_config(env, variant, overrides=dict(env_dynamics="synthetic", n_envs=n_envs // 8 if env == "CartPole-v1" else n_envs,
                                                        n_epochs=2))
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False)
         coll = agent.get_rollout_collector("train")
@@ -405,7 +405,7 @@ def test_comm_update_path_matches_single_gpu(cuda, use_graph, transport):
     for with_comm in (False, True):
         comm = init_local_comm(transport, 70_000) if with_comm else None
         torch.manual_seed(42)
-        cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=512, n_epochs=2))
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=512, n_epochs=2))
         agent = DevicePPOAgent(cfg, device=cuda, use_graph=use_graph, track_stats=False, comm=comm)
         agent.train_epoch()
         torch.cuda.synchronize()

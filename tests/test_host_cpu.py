@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(_lib.lib, n), f"libgsamd.so does not export {n}"
     assert set(names) == set(_lib.EXPORTED)
-    assert _lib.lib.gs_abi_version() == 1
+    assert _lib.lib.gs_abi_version() == _lib.GS_ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -114,6 +114,55 @@ def test_yaml_drop_in_mode_matches_presets():
         for f in ("n_envs", "n_steps", "batch_size", "n_epochs", "gamma", "gae_lambda", "clip_range", "policy_lr",
                   "model_id", "max_env_steps"):
             assert getattr(a, f) == getattr(b, f), f
+
+
+def _bare_agent(cfg, **kw):
+    """A DevicePPOAgent with only what build_env reads (no device buffers: runs on CPU)."""
+    import torch
+    from gsamd.ppo_agent import DevicePPOAgent
+    a = object.__new__(DevicePPOAgent)
+    a.config, a.rank, a.device, a._envs = cfg, 0, torch.device("cpu"), {}
+    a.env_factory = kw.get("env_factory")
+    return a
+
+
+def test_env_follows_config_env_id():
+    """build_agent's env is the one the reference Config names (agents/base_agent.py:129-192):
+    CartPole-v1 -> the device CartPole dynamics (seed_train / seed_val per stage); an env_id the
+    device does not simulate raises unless the caller hands over the host VectorEnv (env= or
+    env_factory=); the synthetic env only on explicit request."""
+    import json
+    from types import SimpleNamespace
+    from gsamd import build_agent, needs_host_env
+    from gsamd.config import device_env_kind, from_reference_config
+    from gsamd.rollout import DeviceCartPoleVecEnv, DeviceSyntheticVecEnv
+    full = json.load(open(os.path.join(ROOT, "tests", "golden", "configs_full.json")))
+    cart = from_reference_config(SimpleNamespace(**full["CartPole-v1:ppo"]))
+    assert cart.env_dynamics == "auto" and device_env_kind(cart) == "cartpole"
+    assert not needs_host_env(SimpleNamespace(**full["CartPole-v1:ppo"]))
+    a = _bare_agent(cart)
+    a.build_env("train")
+    a.build_env("val")
+    assert isinstance(a.get_env("train"), DeviceCartPoleVecEnv) and a.get_env("train").seed == cart.seed_train
+    assert isinstance(a.get_env("val"), DeviceCartPoleVecEnv) and a.get_env("val").seed == cart.seed_val
+    # reward-shaped CartPole (env_wrappers) is not the plain dynamics: host env needed
+    shaped = from_reference_config(SimpleNamespace(**dict(full["CartPole-v1:ppo"], env_wrappers=[{"id": "X"}])))
+    assert device_env_kind(shaped) is None
+    for key in ("LunarLander-v3:ppo", "ALE-Pong-v5:rgb_ppo", "ALE-Breakout-v5:rgb_ppo"):
+        ref = SimpleNamespace(**full[key])
+        assert needs_host_env(ref), key
+        with pytest.raises(ValueError, match="no device dynamics"):
+            build_agent(ref, device="cpu")
+    lunar = from_reference_config(SimpleNamespace(**full["LunarLander-v3:ppo"]))
+    made = []
+    a = _bare_agent(lunar, env_factory=lambda stage: made.append(stage) or SimpleNamespace(num_envs=lunar.n_envs))
+    a.build_env("train")
+    assert made == ["train"]
+    a = _bare_agent(from_reference_config(SimpleNamespace(**full["LunarLander-v3:ppo"]), env_dynamics="synthetic"))
+    a.build_env("train")
+    assert isinstance(a.get_env("train"), DeviceSyntheticVecEnv)
+    with pytest.raises(ValueError):
+        from_reference_config(SimpleNamespace(**full["CartPole-v1:ppo"]), env_dynamics="mujoco")
 
 
 def test_synthetic_env_fixture(golden):

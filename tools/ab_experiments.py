@@ -1,0 +1,34 @@
+"""Timing-only experiments on the product kernels, as source substitutions applied to a copy of
+csrc/ by tools/ab_build.py (never compiled into libgsamd.so).  Several give WRONG results on
+purpose: they price one cost of the lagged forward by removing it."""
+
+ADAM_DENOM = ("gs_mlp.hip",
+              "    const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2s + aa.eps;\n"
+              "    p = p + neg_step * (m * __builtin_amdgcn_rcpf(denom));",
+              "    const float denom = v * inv_bc2s + aa.eps;\n"
+              "    p = p + neg_step * (m * denom);")
+
+EXPERIMENTS = {
+    # Adam without sqrt / rcp (wrong results): the transcendental cost of the lagged step
+    "no_trans": [ADAM_DENOM],
+    # new W2 / W1 set stored from three row blocks instead of one
+    "split_stores": [("gs_mlp.hip",
+                      "        const bool stW2[3] = {own2, own2, own2};\n"
+                      "        const bool stW1[3] = {own1, own1, own1};",
+                      "        const int gy = (int)gridDim.y, gx = (int)gridDim.x;\n"
+                      "        const bool stW2[3] = {apply && rb == 0, apply && rb == 1 % gy, apply && rb == 2 % gy};\n"
+                      "        const bool stW1[3] = {apply && rb == 3 % gy && cb == 0, apply && rb == 3 % gy && cb == 1 % gx,\n"
+                      "                              apply && rb == 3 % gy && cb == 2 % gx};")],
+    # the new set never stored (wrong results)
+    "no_owner_stores": [("gs_mlp.hip",
+                         "        const bool stW2[3] = {own2, own2, own2};\n"
+                         "        const bool stW1[3] = {own1, own1, own1};",
+                         "        const bool stW2[3] = {false, false, false};\n"
+                         "        const bool stW1[3] = {false, false, false};")],
+    # one of the 8 dW1|db1 row-block partials loaded (wrong results): the fold's price
+    "one_partial": [("gs_mlp.hip",
+                     "                    t[j][b] = ld4(af.part1 + (int64_t)b * n1, min(tid + 256 * j, nq1 - 1));",
+                     "                    t[j][b] = b == 0 ? ld4(af.part1, min(tid + 256 * j, nq1 - 1)) : z4;")],
+    # x / h1 stores after the heads, as with 256 threads
+    "late_x_h1": [("gs_mlp.hip", "    constexpr bool kEarly = NT == 512;", "    constexpr bool kEarly = false;")],
+}

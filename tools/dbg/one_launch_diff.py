@@ -8,7 +8,7 @@ from gsamd.ppo_agent import DevicePPOAgent
 out = []
 for one in (False, True):
     torch.manual_seed(42)
-    cfg = load_config("LunarLander-v3", "ppo", overrides=dict(n_envs=72, n_steps=96, batch_size=64, n_epochs=2))
+    cfg = load_config("LunarLander-v3", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=72, n_steps=96, batch_size=64, n_epochs=2))
     agent = DevicePPOAgent(cfg, device="cuda:0", use_graph=False, track_stats=True, one_launch=one)
     coll = agent.get_rollout_collector("train")
     coll.collect()

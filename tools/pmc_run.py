@@ -25,7 +25,7 @@ def main():
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
-    cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=a.n_envs, n_epochs=1))
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=a.n_envs, n_epochs=1))
     agent = DevicePPOAgent(cfg, device="cuda:0", use_graph=False, track_stats=False)
     agent.train_epoch()
     pm = agent.policy_model

@@ -7,9 +7,13 @@ counters come from separate passes (TCC slots: FETCH_SIZE costs 3, WRITE_SIZE 2)
   python tools/pmc_summarize.py FETCH.csv WRITE.csv > profiles/pmc_traffic.json"""
 import csv
 import json
+import os
 import re
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gymnasium-solver_amd"))
+from gsamd.buildinfo import source_hash  # noqa: E402
 
 SHORT = ("k_fwd_hidden", "k_loss", "k_bwd", "k_clip_adam", "k_heads_act", "k_gae_f32", "k_gae_staged", "k_env_step",
          "k_reduce_part1", "k_sumsq_flat")
@@ -41,7 +45,8 @@ def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
     out = {"_note": "HBM-side bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB->B, gfx950 FETCH_SIZE x2 "
-                    "correction per MI355X_MICROARCH.md); Infinity-Cache hits are included by the counters"}
+                    "correction per MI355X_MICROARCH.md); Infinity-Cache hits are included by the counters",
+           "_source_hash": source_hash()}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [])
         w = write.get(k, [])

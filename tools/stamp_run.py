@@ -34,7 +34,7 @@ from gsamd.ppo_agent import DevicePPOAgent  # noqa: E402
 if not SPANS_ONLY:
     _lib.lib.gs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 torch.manual_seed(42)
-cfg = load_config("CartPole-v1", "ppo", overrides=dict(n_envs=4096))
+cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=4096))
 agent = DevicePPOAgent(cfg, device="cuda:0", use_graph=True, track_stats=False)
 agent.train_epoch()
 torch.cuda.synchronize()
