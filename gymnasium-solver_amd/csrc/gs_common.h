@@ -133,6 +133,7 @@ struct Workspace {
     float *dz;       // (B, A+1)   dLoss/dlogits | dLoss/dvalue
     float *part1;    // (ceil(B/64), H1, D+1) dW1|db1 partials per 64-row block
     float *sumsq;    // (n_slots)  per-tile sum of squared gradients
+    float *kl4;      // (4)        global mode: the step's approx_kl share, exchanged in place
     int32_t *f_act;  // (B)        gathered minibatch fields (written by k_fwd_hidden)
     float *f_olp, *f_ov, *f_adv, *f_ret;
     int n_slots;
@@ -170,6 +171,14 @@ struct LossArgs {
     float target_kl;            // <= 0: None
     const int64_t *step_base;   // graph chunk replay: metrics record offset (null: 0)
     int normalize;
+    float inv_batch;            // f32(1 / batch_rows): the gradient of the loss's mean
+    int batch_rows;             // rows of the minibatch the loss averages over (global mode: all ranks')
+    // global mode (gs_ppo_update_global): rows whose action is < 0 are another rank's (padding:
+    // no loss, no gradient); the step's advantage statistics come from all ranks; this rank's raw
+    // loss sums are exported for the host to combine; the KL stop is decided on the global value
+    const float *adv_stats;     // per minibatch {mean, std} (f32) of the global minibatch's advantages
+    double *sums_out;           // per minibatch kNumSums raw loss sums of this rank's rows
+    float *kl_part;             // unfused chain: this rank's share of approx_kl (the exchange sums it)
 };
 
 struct AdamArgs {
@@ -253,7 +262,9 @@ bool has_lagged(const Layout &L, int64_t B);
 int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx, const float *obs,
                       const int64_t *actions, const float *logprobs, const float *values, const float *advantages,
                       const float *returns, int64_t T, int64_t N, int normalize, const FusedFwd &ff, float *metrics,
-                      hipStream_t s);
+                      hipStream_t s, const float *adv_stats = nullptr);
+int launch_kl_decide(const float *kl, float target_kl, int32_t *stop, float *metrics, const int64_t *step_base,
+                     hipStream_t s);
 int launch_metrics_all(const Layout &L, int64_t B, int64_t n, const FusedFwd &ff, const LossArgs &la, float *metrics,
                        hipStream_t s);
 bool has_fused(const Layout &L, int64_t B);

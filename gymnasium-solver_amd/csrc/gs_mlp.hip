@@ -508,7 +508,10 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         }
     } else if (tid < kTile) {
         const int r = r0 + tid;
-        const int src = r < rows ? (idx ? sample_row(idx[r], T, N) : r) : -1;
+        // a negative index is another rank's row of a global minibatch (gs_ppo_update_global):
+        // zero observation, action -1 (no loss, no gradient)
+        const int si = r < rows ? (idx ? idx[r] : r) : -1;
+        const int src = si >= 0 ? (idx ? sample_row(si, T, N) : si) : -1;
         srcs[tid] = src;
         for (int d = 0; d < D; ++d) xs[tid * D + d] = src >= 0 ? obs[(int64_t)src * D + d] : 0.0f;
         if (cb == 0 && rg.f_act && src >= 0) {
@@ -517,6 +520,9 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             rg.f_ov[r] = rg.values[src];
             rg.f_adv[r] = rg.advantages[src];
             rg.f_ret[r] = rg.returns[src];
+        } else if (cb == 0 && rg.f_act && r < rows) {
+            rg.f_act[r] = -1;
+            rg.f_olp[r] = rg.f_ov[r] = rg.f_adv[r] = rg.f_ret[r] = 0.0f;
         }
     }
     if constexpr (!kStage0) {
@@ -1278,11 +1284,15 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
         return;
     }
     const int A = L.A, A1 = A + 1;
-    const float invB = 1.0f / (float)B;
+    const float invB = la.inv_batch;
+    const int64_t kb = la.step_base ? *la.step_base : 0;
 
     // ---- batch advantage normalisation: (a - mean) / (std_unbiased + 1e-8)
     float meanf = 0.0f, stdf = 1.0f;
-    if (la.normalize) {
+    if (la.normalize && la.adv_stats) {      // global mode: the whole minibatch's statistics
+        meanf = la.adv_stats[2 * kb];
+        stdf = la.adv_stats[2 * kb + 1];
+    } else if (la.normalize) {
         double m1[1] = {0.0};
         for (int r = tid; r < B; r += 256) m1[0] += (double)f_adv[r];
         block_reduce<1>(m1, sred);
@@ -1305,18 +1315,31 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
         // every input of the row first (one round trip), then the math
         float z[AMAX + 1];
         gather_head_row<AMAX, AEX>(zpart, P, L, r, z);
+        const int act = f_act[r];
         float adv = f_adv[r];
         if (la.normalize) adv = (adv - meanf) / (stdf + 1e-8f);
-        loss_row<AMAX>(z, A, f_act[r], f_olp[r], f_ov[r], adv, f_ret[r], la, invB, dz + (int64_t)r * A1, acc);
+        if (act < 0) {      // another rank's row of a global minibatch
+            for (int a = 0; a < A1; ++a) dz[(int64_t)r * A1 + a] = 0.0f;
+            continue;
+        }
+        loss_row<AMAX>(z, A, act, f_olp[r], f_ov[r], adv, f_ret[r], la, invB, dz + (int64_t)r * A1, acc);
     }
     GS_STAMP(1)
     block_reduce<kNumSums>(acc, sred);     // fixed order -> deterministic
     GS_STAMP(2)
     if (tid == 0) {
-        write_metrics(acc, (double)B, la, metrics, true);
+        const double rows = (double)la.batch_rows;
+        write_metrics(acc, rows, la, metrics, true);
         metrics[GS_M_GRAD_NORM] = 0.0f;
-        const float approx_kl = (float)(acc[6] / (double)B);
-        if (la.target_kl > 0.0f && approx_kl > la.target_kl && stop) *stop = 1;
+        if (la.sums_out)
+            for (int q = 0; q < kNumSums; ++q) la.sums_out[kb * kNumSums + q] = acc[q];
+        if (la.kl_part) {           // global KL stop: decided after the exchange (k_kl_decide)
+            la.kl_part[0] = (float)(acc[6] * (double)invB);
+            metrics[GS_M_KL_STOP] = metrics[GS_M_SKIPPED] = 0.0f;
+        } else {
+            const float approx_kl = (float)(acc[6] / rows);
+            if (la.target_kl > 0.0f && approx_kl > la.target_kl && stop) *stop = 1;
+        }
     }
     GS_STAMP_END(3)
 }
@@ -1402,15 +1425,16 @@ __device__ __forceinline__ void loss_rows_lds(const float *__restrict__ P, const
         for (int q = 0; q < kNumSums; ++q) acc[q] = 0.0;
         // rows past B (padding) load row B-1 unconditionally and discard the result: a predicated
         // load burst would compile to branches with vmcnt stalls inside it
-        const bool live = r < B;
-        const int rc = live ? r : B - 1;
+        const int rc = r < B ? r : B - 1;
         const int64_t o = k * B + rc;
         // the row's fields are loaded before the head partials: one memory round trip
         const int fa = ff.fa[o];
         const float folp = ff.folp[o], fov = ff.fov[o], fadv = ff.fadv[o], fret = ff.fret[o];
         float z[AMAX + 1];
         gather_head_row<AMAX, AEX>(zpart, P, L, rc, z);
-        loss_row<AMAX>(z, L.A, fa, folp, fov, fadv, fret, la, 1.0f / (float)B, dzs + i * A1, acc);
+        // action < 0: another rank's row of a global minibatch (gs_ppo_update_global)
+        const bool live = r < B && fa >= 0;
+        loss_row<AMAX>(z, L.A, fa, folp, fov, fadv, fret, la, la.inv_batch, dzs + i * A1, acc);
         if (!live) {
             for (int a = 0; a < A1; ++a) dzs[i * A1 + a] = 0.0f;
 #pragma unroll
@@ -2619,7 +2643,8 @@ __global__ __launch_bounds__(256) void k_gather_all(const int32_t *__restrict__ 
                                                     const float *__restrict__ logprobs, const float *__restrict__ values,
                                                     const float *__restrict__ advantages,
                                                     const float *__restrict__ returns, int T, int N, int D,
-                                                    int normalize, FusedFwd ff, float *__restrict__ metrics)
+                                                    int normalize, FusedFwd ff, float *__restrict__ metrics,
+                                                    const float *__restrict__ adv_stats)
 {
     __shared__ double sred[2 * (256 + 16)];
     const int B = S::batch(Brt);
@@ -2627,22 +2652,42 @@ __global__ __launch_bounds__(256) void k_gather_all(const int32_t *__restrict__ 
     const int tid = threadIdx.x;
     constexpr int kMaxRows = 4;     // B <= 1024
     float adv[kMaxRows];
+    bool mine[kMaxRows];
     double m1[1] = {0.0};
 #pragma unroll
     for (int j = 0; j < kMaxRows; ++j) {
         const int r = tid + 256 * j;
         adv[j] = 0.0f;
+        mine[j] = false;
         if (r < B) {
-            const int src = sample_row(idx[k * B + r], T, N);
+            const int si = idx[k * B + r];
             const int64_t o = k * B + r;
+            if (si < 0) {      // another rank's row of a global minibatch: no loss, no gradient
+                for (int d = 0; d < D; ++d) const_cast<float *>(ff.xg)[o * D + d] = 0.0f;
+                const_cast<int32_t *>(ff.fa)[o] = -1;
+                const_cast<float *>(ff.folp)[o] = 0.0f;
+                const_cast<float *>(ff.fov)[o] = 0.0f;
+                const_cast<float *>(ff.fret)[o] = 0.0f;
+                continue;
+            }
+            const int src = sample_row(si, T, N);
             for (int d = 0; d < D; ++d) const_cast<float *>(ff.xg)[o * D + d] = obs[(int64_t)src * D + d];
             const_cast<int32_t *>(ff.fa)[o] = (int32_t)actions[src];
             const_cast<float *>(ff.folp)[o] = logprobs[src];
             const_cast<float *>(ff.fov)[o] = values[src];
             const_cast<float *>(ff.fret)[o] = returns[src];
             adv[j] = advantages[src];
+            mine[j] = true;
             m1[0] += (double)adv[j];
         }
+    }
+    if (normalize && adv_stats) {    // global mode: the whole minibatch's statistics (all ranks)
+        const float meanf = adv_stats[2 * k], stdf = adv_stats[2 * k + 1];
+#pragma unroll
+        for (int j = 0; j < kMaxRows; ++j)
+            if (tid + 256 * j < B)
+                const_cast<float *>(ff.fadv)[k * B + tid + 256 * j] = mine[j] ? (adv[j] - meanf) / (stdf + 1e-8f) : 0.0f;
+        return;     // ADV_NORM metrics: from the combined loss sums (host)
     }
     if (!normalize) {
 #pragma unroll
@@ -2697,7 +2742,35 @@ __global__ __launch_bounds__(256) void k_metrics_all(const double *__restrict__ 
     for (int rb = 0; rb < nrb; ++rb)
 #pragma unroll
         for (int q = 0; q < kNumSums; ++q) t[q] += mpart[(k * nrb + rb) * kNumSums + q];
-    write_metrics(t, (double)B, la, metrics + k * GS_NUM_METRICS, false);
+    write_metrics(t, (double)la.batch_rows, la, metrics + k * GS_NUM_METRICS, la.sums_out != nullptr);
+    if (la.sums_out)
+#pragma unroll
+        for (int q = 0; q < kNumSums; ++q) la.sums_out[k * kNumSums + q] = t[q];
+    (void)B;
+}
+
+// global mode, unfused chain: the KL early stop on the exchanged approx_kl of the whole minibatch
+// (sticky, agents/base_agent.py:330-366): the tripping minibatch keeps its loss record with
+// KL_STOP = SKIPPED = 1 and takes no optimizer step on any rank
+__global__ void k_kl_decide(const float *__restrict__ kl, float target_kl, int32_t *__restrict__ stop,
+                            float *__restrict__ metrics, const int64_t *__restrict__ step_base)
+{
+    if (threadIdx.x != 0 || (stop && *stop)) return;
+    float *m = metrics + (step_base ? *step_base : 0) * GS_NUM_METRICS;
+    m[GS_M_APPROX_KL] = kl[0];
+    if (target_kl > 0.0f && kl[0] > target_kl) {
+        if (stop) *stop = 1;
+        m[GS_M_KL_STOP] = 1.0f;
+        m[GS_M_SKIPPED] = 1.0f;
+    }
+}
+
+int launch_kl_decide(const float *kl, float target_kl, int32_t *stop, float *metrics, const int64_t *step_base,
+                     hipStream_t s)
+{
+    hipLaunchKernelGGL(k_kl_decide, dim3(1), dim3(64), 0, s, kl, target_kl, stop, metrics, step_base);
+    GS_LAUNCH_CHECK("k_kl_decide");
+    return GS_OK;
 }
 
 bool has_fused(const Layout &L, int64_t B)
@@ -2769,11 +2842,12 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
 int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx, const float *obs,
                       const int64_t *actions, const float *logprobs, const float *values, const float *advantages,
                       const float *returns, int64_t T, int64_t N, int normalize, const FusedFwd &ff, float *metrics,
-                      hipStream_t s)
+                      hipStream_t s, const float *adv_stats)
 {
     return with_shape(L, B, [&](auto sh) {
         hipLaunchKernelGGL(k_gather_all<decltype(sh)>, dim3((unsigned)n), dim3(256), 0, s, idx, (int)B, obs, actions,
-                           logprobs, values, advantages, returns, (int)T, (int)N, L.D, normalize, ff, metrics);
+                           logprobs, values, advantages, returns, (int)T, (int)N, L.D, normalize, ff, metrics,
+                           adv_stats);
         GS_LAUNCH_CHECK("k_gather_all");
         return GS_OK;
     });

@@ -46,6 +46,7 @@ Workspace carve_workspace(void *base, const Layout &L, int64_t B)
     w.n_slots = n_sumsq_slots(L);
     const int comm_slots = kXgmiMaxWG;   // the xGMI exchange writes one partial per workgroup
     w.sumsq = take((size_t)(w.n_slots > comm_slots ? w.n_slots : comm_slots));
+    w.kl4 = take(4);
     w.bytes = off;
     return w;
 }
@@ -168,6 +169,7 @@ extern "C" size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch)
 namespace {
 
 constexpr int64_t kChunk = 512;    // minibatch steps per captured graph
+constexpr int64_t kNumSumsHost = 14;   // raw loss sums per minibatch (gs_mlp.hip kNumSums)
 
 // The fused update path's per-update arrays, after the step workspace.
 struct FusedWs {
@@ -218,11 +220,21 @@ namespace {
 struct StepArgs {
     LossArgs la;
     AdamArgs aa;
+    bool sum_exchange;      // global mode: every rank's gradient is its share of the global mean (sum, no 1/world)
 };
 
-StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, int64_t t)
+// glob != nullptr: gs_ppo_update_global's global-minibatch mode (include/gsamd.h)
+StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, int64_t t,
+                        const gs_ppo_global *glob = nullptr)
 {
     StepArgs a{};
+    a.la.batch_rows = (int)(glob ? glob->batch_global : B);
+    a.la.inv_batch = 1.0f / (float)a.la.batch_rows;
+    if (glob) {
+        a.la.adv_stats = glob->adv_stats;
+        a.la.sums_out = glob->metric_sums;
+        a.sum_exchange = true;
+    }
     a.la.clip_lo = (float)(1.0 - (double)hp.clip_range);
     a.la.clip_hi = (float)(1.0 + (double)hp.clip_range);
     a.la.clip_vf = hp.clip_range_vf;
@@ -260,7 +272,7 @@ int exchange_and_adam(float *P, float *G, float *M, float *V, const Layout &L, c
     AdamArgs aa = sa.aa;
     aa.n_slots = n_slots;
     aa.nrb = 0;
-    aa.grad_scale = 1.0f / (float)world;
+    aa.grad_scale = sa.sum_exchange ? 1.0f : 1.0f / (float)world;
     return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
 }
 
@@ -275,6 +287,12 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
     if (rc) return rc;
     rc = launch_loss(P, L, B, ws, sa.la, metrics, stop, s);
     if (rc) return rc;
+    if (sa.la.kl_part) {    // global mode's KL stop: this rank's approx_kl share summed over ranks first
+        int world = 1;
+        if (comm && (rc = comm_allreduce_sum(comm, sa.la.kl_part, 1, s, &world))) return rc;
+        rc = launch_kl_decide(sa.la.kl_part, sa.la.target_kl, stop, metrics, sa.la.step_base, s);
+        if (rc) return rc;
+    }
     rc = launch_bwd(P, L, B, ws, G, stop, s);
     if (rc) return rc;
     if (!comm) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
@@ -284,9 +302,11 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
 // The fused chains' exchange inside k_bwd (xGMI transport, shapes within its limits): the
 // gradient, the W1 partials and the per-tile sums of squares leave the backward as the mean
 // over ranks, and the rest of the step is the single-GPU one.  False: exchange after k_bwd.
-bool bwd_exchange_of(gs_comm *comm, const Layout &L, int64_t B, BwdXchg *bx)
+bool bwd_exchange_of(gs_comm *comm, const Layout &L, int64_t B, BwdXchg *bx, bool sum_exchange = false)
 {
-    return comm && xgmi_bwd_args(comm, bx) && bwd_xchg_fits(L, B, comm->colocated);
+    if (!(comm && xgmi_bwd_args(comm, bx) && bwd_xchg_fits(L, B, comm->colocated))) return false;
+    if (sum_exchange) bx->scale = 1.0f;     // global mode: the ranks' shares add up to the mean
+    return true;
 }
 
 // One minibatch step of the fused chain: k_fwd_hidden<fused> (pre-gathered x), k_bwd<fused>
@@ -297,7 +317,7 @@ int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, 
                        hipStream_t s)
 {
     BwdXchg bx;
-    const bool inbwd = bwd_exchange_of(comm, L, B, &bx);
+    const bool inbwd = bwd_exchange_of(comm, L, B, &bx, sa.sum_exchange);
     int rc = launch_fwd_fused(P, L, B, ff, sa.la, ws, stop, s);
     if (rc) return rc;
     rc = launch_bwd(P, L, B, ws, G, stop, s, &ff, &sa.la, inbwd ? &bx : nullptr);
@@ -323,12 +343,12 @@ struct ParamSet {
 // The clip + Adam arguments of a step whose gradient went through the exchange: the gradient
 // is final in G (W1 partials folded), the norm comes from the exchange's partial sums, and the
 // sum over ranks is scaled by 1/world inside the norm and the update.
-AdamArgs exchanged_adam_args(const AdamArgs &aa_in, const gs_comm *comm)
+AdamArgs exchanged_adam_args(const AdamArgs &aa_in, const gs_comm *comm, bool sum_exchange = false)
 {
     AdamArgs aa = aa_in;
     aa.n_slots = comm_sumsq_slots(comm);
     aa.nrb = 0;
-    aa.grad_scale = 1.0f / (float)comm->nranks;
+    aa.grad_scale = sum_exchange ? 1.0f : 1.0f / (float)comm->nranks;
     return aa;
 }
 
@@ -344,13 +364,13 @@ int enqueue_step_lagged(const ParamSet (&ps)[2], float *G, const Layout &L, cons
 {
     const ParamSet &cur = ps[k & 1], &prev = ps[(k & 1) ^ 1];
     BwdXchg bx;
-    const bool inbwd = bwd_exchange_of(comm, L, B, &bx);
+    const bool inbwd = bwd_exchange_of(comm, L, B, &bx, sa_prev.sum_exchange);
     const bool after = comm && !inbwd;     // exchange launch after the backward
     AdamFwd af{};
     af.Min = prev.M, af.Vin = prev.V, af.G = G, af.part1 = after ? nullptr : ws.part1, af.sumsq = ws.sumsq;
     af.Pout = cur.P, af.Mout = cur.M, af.Vout = cur.V;
     af.metrics = metrics;
-    af.aa = after ? exchanged_adam_args(sa_prev.aa, comm) : sa_prev.aa;
+    af.aa = after ? exchanged_adam_args(sa_prev.aa, comm, sa_prev.sum_exchange) : sa_prev.aa;
     int rc = launch_fwd_fused(prev.P, L, B, ff, sa_prev.la, ws, stop, s, &af);
     if (rc) return rc;
     rc = launch_bwd(cur.P, L, B, ws, G, stop, s, &ff, &sa_prev.la, inbwd ? &bx : nullptr);
@@ -466,11 +486,11 @@ namespace {
 
 // A captured update phase: keyed by every pointer/shape baked into its nodes.
 struct GraphKey {
-    const void *p[12];
+    const void *p[14];
     int64_t n[6];
     bool operator==(const GraphKey &o) const
     {
-        for (int i = 0; i < 12; ++i)
+        for (int i = 0; i < 14; ++i)
             if (p[i] != o.p[i]) return false;
         for (int i = 0; i < 6; ++i)
             if (n[i] != o.n[i]) return false;
@@ -481,7 +501,7 @@ struct GraphKeyHash {
     size_t operator()(const GraphKey &k) const
     {
         size_t h = 1469598103934665603ull;
-        for (int i = 0; i < 12; ++i) h = (h ^ (size_t)k.p[i]) * 1099511628211ull;
+        for (int i = 0; i < 14; ++i) h = (h ^ (size_t)k.p[i]) * 1099511628211ull;
         for (int i = 0; i < 6; ++i) h = (h ^ (size_t)k.n[i]) * 1099511628211ull;
         return h;
     }
@@ -512,10 +532,11 @@ void baked_hparam_bits(const gs_ppo_hparams &hp, uint32_t (&out)[12])
 
 }  // namespace
 
-extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
-                             gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
-                             int64_t n_minibatches, int64_t adam_step0, float *metrics, int32_t *stop_flag,
-                             void *workspace, size_t workspace_bytes, gs_comm *comm, int use_graph, void *stream)
+static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
+                      gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
+                      int64_t n_minibatches, int64_t adam_step0, float *metrics, int32_t *stop_flag,
+                      void *workspace, size_t workspace_bytes, gs_comm *comm, int use_graph, void *stream,
+                      const gs_ppo_global *glob)
 {
     int rc = validate_update(dims, ro, batch, workspace);
     if (rc) return rc;
@@ -524,6 +545,19 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     if (n_minibatches == 0) return GS_OK;
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
+    // every StepArgs of this update (glob: the global-minibatch mode)
+    auto make_step_args = [&](const gs_ppo_hparams &h, const Layout &Lx, int64_t Bx, int64_t t) {
+        StepArgs a = ::make_step_args(h, Lx, Bx, t, glob);
+        if (glob && h.target_kl > 0.0f) a.la.kl_part = ws.kl4;
+        return a;
+    };
+    // the unfused chain's per-step loss reads / writes minibatch k's rows of the global-mode
+    // arrays (plus *step_base on device inside a replayed chunk, like its metrics record)
+    auto at_step = [](StepArgs a, int64_t k) {
+        if (a.la.adv_stats) a.la.adv_stats += 2 * k;
+        if (a.la.sums_out) a.la.sums_out += kNumSumsHost * k;
+        return a;
+    };
     hipStream_t s = (hipStream_t)stream;
     // fused chain when this shape has a compile-time instantiation, no KL early stop is
     // configured (its per-minibatch decision needs the full loss before the backward) and the
@@ -542,7 +576,8 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         ff0.mpart = fw.mpart;
         ff0.dz = ws.dz;
         rc = launch_gather_all(L, batch, n_minibatches, idx, ro.obs, ro.actions, ro.logprobs, ro.values,
-                               ro.advantages, ro.returns, ro.T, ro.N, hp.normalize_adv, ff0, metrics, s);
+                               ro.advantages, ro.returns, ro.T, ro.N, hp.normalize_adv, ff0, metrics, s,
+                               glob ? glob->adv_stats : nullptr);
         if (rc) return rc;
     }
     // minibatch k's clip + Adam runs inside the forward of k+1 (enqueue_step_lagged), with or
@@ -570,9 +605,10 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
             const ParamSet &q = ps[k & 1];
             const StepArgs sl = make_step_args(hp, L, batch, adam_step0 + k + 1);
             BwdXchg bx;
-            const bool after = comm && !bwd_exchange_of(comm, L, batch, &bx);
+            const bool after = comm && !bwd_exchange_of(comm, L, batch, &bx, sl.sum_exchange);
             int rc2 = after ? launch_clip_adam(q.P, L, grads, q.M, q.V, nullptr, ws.sumsq,
-                                              exchanged_adam_args(sl.aa, comm), metrics + k * GS_NUM_METRICS,
+                                              exchanged_adam_args(sl.aa, comm, sl.sum_exchange),
+                                              metrics + k * GS_NUM_METRICS,
                                               stop_flag, s)
                            : launch_clip_adam(q.P, L, grads, q.M, q.V, ws.part1, ws.sumsq, sl.aa,
                                               metrics + k * GS_NUM_METRICS, stop_flag, s);
@@ -597,7 +633,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
             rc = lagged  ? lag_step(k, nullptr, nullptr, s)
                  : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
                                               metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
-                         : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                         : enqueue_step(params, grads, adam_m, adam_v, L, at_step(sa, k), ro, idx + k * batch, batch,
                                         metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
             if (rc) return rc;
         }
@@ -610,16 +646,17 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
     const int64_t chunk = n_minibatches < kChunk ? n_minibatches : kChunk;
     const int64_t n_full = n_minibatches / chunk;
     GraphKey key{};
-    const void *ptrs[12] = {params, grads, adam_m, adam_v, ro.obs, ro.actions, ro.logprobs, ro.values,
-                            ro.advantages, ro.returns, idx, metrics};
-    for (int i = 0; i < 12; ++i) key.p[i] = ptrs[i];
+    const void *ptrs[14] = {params, grads, adam_m, adam_v, ro.obs, ro.actions, ro.logprobs, ro.values,
+                            ro.advantages, ro.returns, idx, metrics, glob ? glob->adv_stats : nullptr,
+                            glob ? glob->metric_sums : nullptr};
+    for (int i = 0; i < 14; ++i) key.p[i] = ptrs[i];
     key.n[0] = batch;
     key.n[1] = n_minibatches;
     key.n[2] = ((int64_t)dims.obs_dim << 48) ^ ((int64_t)dims.hidden1 << 32) ^ ((int64_t)dims.hidden2 << 16) ^ dims.n_actions;
     key.n[3] = (int64_t)(intptr_t)workspace;
     key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1) ^ (fused ? 1 : 0) ^
                ((int64_t)lagged << 62);
-    key.n[5] = ro.T * 1000003 + ro.N;
+    key.n[5] = ro.T * 1000003 + ro.N + (glob ? glob->batch_global << 40 : 0);
     uint32_t hbits[12];
     baked_hparam_bits(hp, hbits);
     std::lock_guard<std::mutex> lk(g_graph_mu);
@@ -671,7 +708,7 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
                 rc = enqueue_step_fused(params, grads, adam_m, adam_v, L, saf, batch, step_ff(k, k, ent.base),
                                         metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
             } else {
-                rc = enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                rc = enqueue_step(params, grads, adam_m, adam_v, L, at_step(sa, k), ro, idx + k * batch, batch,
                                   metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
             }
             if (rc) {
@@ -714,11 +751,33 @@ extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *
         rc = lagged  ? lag_step(k, nullptr, nullptr, s)
              : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
                                           metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
-                     : enqueue_step(params, grads, adam_m, adam_v, L, sa, ro, idx + k * batch, batch,
+                     : enqueue_step(params, grads, adam_m, adam_v, L, at_step(sa, k), ro, idx + k * batch, batch,
                                   metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
         if (rc) return rc;
     }
     return finish();
+}
+
+extern "C" int gs_ppo_update(float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
+                             gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
+                             int64_t n_minibatches, int64_t adam_step0, float *metrics, int32_t *stop_flag,
+                             void *workspace, size_t workspace_bytes, gs_comm *comm, int use_graph, void *stream)
+{
+    return ppo_update(params, grads, adam_m, adam_v, dims, hp, ro, idx, batch, n_minibatches, adam_step0, metrics,
+                      stop_flag, workspace, workspace_bytes, comm, use_graph, stream, nullptr);
+}
+
+extern "C" int gs_ppo_update_global(float *params, float *grads, float *adam_m, float *adam_v, gs_mlp_dims dims,
+                                    gs_ppo_hparams hp, gs_rollout_view ro, const int32_t *idx, int64_t batch,
+                                    int64_t n_minibatches, int64_t adam_step0, float *metrics, int32_t *stop_flag,
+                                    void *workspace, size_t workspace_bytes, gs_comm *comm, int use_graph,
+                                    const gs_ppo_global *glob, void *stream)
+{
+    GS_REQUIRE(glob && glob->batch_global >= 2 && glob->metric_sums, "gs_ppo_update_global: bad global arguments");
+    GS_REQUIRE(!hp.normalize_adv || glob->adv_stats, "gs_ppo_update_global: normalize_adv needs adv_stats");
+    GS_REQUIRE(glob->batch_global >= batch || !comm, "gs_ppo_update_global: batch_global < local rows");
+    return ppo_update(params, grads, adam_m, adam_v, dims, hp, ro, idx, batch, n_minibatches, adam_step0, metrics,
+                      stop_flag, workspace, workspace_bytes, comm, use_graph, stream, glob);
 }
 
 extern "C" int gs_ppo_graph_cache_info(int64_t *n_entries, int64_t *n_captures)

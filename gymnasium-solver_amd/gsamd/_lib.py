@@ -44,6 +44,11 @@ class RolloutView(ctypes.Structure):
                 ("T", ctypes.c_int64), ("N", ctypes.c_int64)]
 
 
+class PPOGlobal(ctypes.Structure):
+    """gs_ppo_global (include/gsamd.h): the global-minibatch mode's extra arguments."""
+    _fields_ = [("batch_global", ctypes.c_int64), ("adv_stats", ctypes.c_void_p), ("metric_sums", ctypes.c_void_p)]
+
+
 class CnnDims(ctypes.Structure):
     _fields_ = [("in_c", ctypes.c_int32), ("in_h", ctypes.c_int32), ("in_w", ctypes.c_int32),
                 ("n_actions", ctypes.c_int32), ("hidden", ctypes.c_int32), ("valid_mask", ctypes.c_uint32)]
@@ -89,6 +94,8 @@ def _load():
                                         i64, vp, vp, vp]),
         "gs_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64, i64, vp,
                                          vp, vp, sz, vp, ctypes.c_int, vp]),
+        "gs_ppo_update_global": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64, i64,
+                                                vp, vp, vp, sz, vp, ctypes.c_int, ctypes.POINTER(PPOGlobal), vp]),
         "gs_ppo_update_workspace_bytes": (sz, [MlpDims, i64, i64]),
         "gs_ppo_graph_cache_info": (ctypes.c_int, [vp, vp]),
         "gs_ppo_exchange_inside_bwd": (ctypes.c_int, [vp, MlpDims, ctypes.c_int64, vp]),
@@ -133,7 +140,8 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_rollout_synth_supported",
             "gs_rollout_synth", "gs_env_reset", "gs_env_step",
             "gs_episode_stats",
-            "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update", "gs_ppo_update_workspace_bytes",
+            "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update",
+            "gs_ppo_update_global", "gs_ppo_update_workspace_bytes",
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",

@@ -74,6 +74,11 @@ class PPOConfig:
     #               synthetic Atari frame source for rgb configs
     #   "cartpole"  device CartPole-v1 dynamics
     env_dynamics: str = "auto"
+    # data-parallel semantics of a multi-rank update:
+    #   "local"  every rank takes B-row minibatches of its own samples (weak scaling, global batch G·B)
+    #   "global" every rank takes its share of the reference's global minibatches (the single-GPU
+    #            math on G GPUs: global sampler, normalisation and KL stop; gs_ppo_update_global)
+    dp_mode: str = "local"
     # {param: {schedule, start_value, end_value, start, end, warmup}} (gsamd.schedules)
     schedules: Dict[str, Dict[str, Any]] = field(default_factory=dict)
 
@@ -124,6 +129,8 @@ class PPOConfig:
                              f"rollout_size={rollout}, batch_size={self.batch_size}.")
         if self.normalize_advantages not in ("batch", "rollout", "off", False, None, ""):
             raise ValueError("normalize_advantages must be 'rollout', 'batch', or 'off'.")
+        if self.dp_mode not in ("local", "global"):
+            raise ValueError(f"dp_mode must be 'local' or 'global', got {self.dp_mode!r}")
         if str(self.env_dynamics or "auto") not in ENV_DYNAMICS:
             raise ValueError(f"env_dynamics must be one of {ENV_DYNAMICS}, got {self.env_dynamics!r}")
 

@@ -40,6 +40,37 @@ def ppo_records(rows: np.ndarray, vf_coef: float, ent_coef: float, normalize_bat
     return np.stack(cols, axis=1).astype(np.float64)
 
 
+NUM_SUMS = 14      # raw loss sums per minibatch (include/gsamd.h gs_ppo_global.metric_sums)
+
+
+def records_from_sums(sums: np.ndarray, rows: int, vf_coef: float, ent_coef: float, normalize: bool) -> np.ndarray:
+    """(n, 14) raw loss sums of whole minibatches (every rank's added) -> the (n, 16) loss slots of
+    the device records, with the arithmetic of csrc/gs_mlp.hip write_metrics (f32 terms from
+    double sums; torch.var's unbiased variance for explained_var, utils/torch.py:97-99 statistics
+    for the normalised advantages).  The KL / skip / grad-norm slots are left at zero."""
+    t = np.asarray(sums, np.float64).reshape(-1, NUM_SUMS)
+    Bd = float(rows)
+    out = np.zeros((t.shape[0], 16), np.float32)
+    pl = (-t[:, 0] / Bd).astype(np.float32)
+    vl = (t[:, 1] / Bd).astype(np.float32)
+    ent = (t[:, 2] / Bd).astype(np.float32)
+    loss = (pl + np.float32(vf_coef) * vl) + np.float32(ent_coef) * (-ent)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        var_rv = (t[:, 8] - t[:, 7] * t[:, 7] / Bd) / (Bd - 1.0)
+        var_r = (t[:, 10] - t[:, 9] * t[:, 9] / Bd) / (Bd - 1.0)
+        out[:, M["explained_var"]] = (1.0 - var_rv / var_r).astype(np.float32)
+    out[:, M["loss"]], out[:, M["policy_loss"]], out[:, M["value_loss"]], out[:, M["entropy"]] = loss, pl, vl, ent
+    out[:, M["clip_fraction"]] = (t[:, 3] / Bd).astype(np.float32)
+    out[:, M["clip_fraction_vf"]] = (t[:, 4] / Bd).astype(np.float32)
+    out[:, M["kl"]] = (t[:, 5] / Bd).astype(np.float32)
+    out[:, M["approx_kl"]] = (t[:, 6] / Bd).astype(np.float32)
+    if normalize:
+        out[:, M["adv_norm_mean"]] = (t[:, 11] / Bd).astype(np.float32)
+        out[:, M["adv_norm_std"]] = np.sqrt(np.maximum(0.0, (t[:, 12] - t[:, 11] ** 2 / Bd) / (Bd - 1.0))
+                                            ).astype(np.float32)
+    return out
+
+
 def ppo_keys(normalize_batch: bool):
     return PPO_KEYS + (ADV_NORM_KEYS if normalize_batch else ())
 

@@ -22,15 +22,17 @@ from typing import Any, Dict, Optional
 import numpy as np
 import torch
 
-from ._lib import GS_NUM_METRICS, M, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
+import ctypes
+
+from ._lib import GS_NUM_METRICS, M, PPOGlobal, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
 from .atari_env import DeviceAtariVecEnv
 from .config import device_env_kind
 from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
-from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler
+from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler, index_stream, rank_share
 from .distributed import allreduce_sum_f64, comm_status, world_active
-from .metrics import MetricsRecorder, ppo_keys, ppo_records
+from .metrics import NUM_SUMS, MetricsRecorder, ppo_keys, ppo_records, records_from_sums
 from .schedules import SCHEDULABLE, build_schedulers
 
 STAGES = ("train",)
@@ -294,6 +296,18 @@ class DevicePPOAgent:
             raise ValueError(f"Batch size must divide rollout size exactly: data_len={self.data_len}, "
                              f"batch_size={self.batch_size}.")
         self.n_minibatches = self.data_len // self.batch_size * c.n_epochs
+        # global-minibatch mode (dp_mode "global"): every rank runs the reference's
+        # minibatches of the whole job's rollout, its own rows of each padded to B
+        self.global_mode = str(getattr(c, "dp_mode", "local")) == "global"
+        if self.global_mode:
+            if self.is_pixel:
+                raise ValueError("dp_mode 'global' is implemented for the MLP update (gs_ppo_update_global)")
+            self.n_minibatches = self.data_len * self.world_size // self.batch_size * c.n_epochs
+            z64 = dict(dtype=torch.float64, device=self.device)
+            self._gsums = torch.zeros(self.n_minibatches, NUM_SUMS, **z64)
+            self._adv_stats = torch.zeros(self.n_minibatches, 2, dtype=torch.float32, device=self.device)
+            self._gidx = torch.empty(self.n_minibatches * self.batch_size, dtype=torch.int32, device=self.device)
+        self._base_seed = int(torch.initial_seed())
         if self.is_pixel:
             ws = int(lib.gs_cnn_workspace_bytes(self.policy_model.dims, self.batch_size))
         else:   # the whole update's workspace (fused chain: per-update gathered minibatch fields)
@@ -319,6 +333,9 @@ class DevicePPOAgent:
         return self._epoch_batches(0)
 
     def _epoch_batches(self, epoch: int):
+        if self.global_mode:
+            raise NotImplementedError("dp_mode 'global' runs whole updates (train_epoch), not per-minibatch "
+                                      "training_step calls")
         idx = self.prefetcher.upload(epoch)
         self.prefetcher.prefetch(epoch + 1)
         B = self.batch_size
@@ -427,16 +444,27 @@ class DevicePPOAgent:
             self._trajectories = collector.collect()
         elif epoch > 0:
             self._trajectories = collector.collect()
+        self.update_phase(ev)
+
+    def update_phase(self, ev=None) -> None:
+        """The update half of an epoch on the train collector's current rollout (the n_epochs
+        passes of minibatch steps, then the epoch's bookkeeping) — train_epoch after its collect;
+        callers that collect themselves (e.g. a replayed rollout) call it directly."""
+        epoch = self.current_epoch
+        collector = self.get_rollout_collector("train")
         # the epoch's minibatch indices go up on the update's own stream: a side-stream upload
         # overlapping the rollout (tried: C3 collect -2 ms) made every minibatch step of the
         # update that followed ~1.4 us slower (same-box A/B on C2: 16.8 vs 15.3 us), with the
         # update waiting on the copy's event on the device or on the host alike
-        idx = self.prefetcher.upload(epoch)
-        self.prefetcher.prefetch(epoch + 1)
+        idx = None if self.global_mode else self.prefetcher.upload(epoch)
+        if not self.global_mode:
+            self.prefetcher.prefetch(epoch + 1)
         buf = collector.buffer
-        if ev is not None:
+        if ev:
             ev[-1][1].record()
-        if self.is_pixel:
+        if self.global_mode:
+            self._global_update(epoch, buf)
+        elif self.is_pixel:
             check(lib.gs_cnn_ppo_update(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
                                         ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(), ptr(idx),
                                         self.batch_size, self.n_minibatches, self.adam_step, ptr(self.metrics_buf),
@@ -448,7 +476,7 @@ class DevicePPOAgent:
                                     self.batch_size, self.n_minibatches, self.adam_step, ptr(self.metrics_buf),
                                     ptr(self.stop_flag), ptr(self.workspace), self.workspace.numel(), self.comm,
                                     1 if self.use_graph else 0, stream_handle()), "gs_ppo_update")
-        if ev is not None:
+        if ev:
             ev[-1][2].record()
         if self.comm:
             # the exchange's sticky timeout record, read once per epoch (one 8-byte D2H after the
@@ -461,6 +489,48 @@ class DevicePPOAgent:
             self.adam_step += int((self.metrics_buf[:, M["skipped"]] == 0).sum().item())
         self.current_epoch += 1
         self.on_train_epoch_end()
+
+    def global_shares(self, epoch: int) -> np.ndarray:
+        """This rank's rows of every global minibatch of `epoch` (padded with -1): the reference's
+        sampler over the whole job's rollout (utils/samplers.py:25-34, seed initial_seed + epoch,
+        global env g = rank * n_envs + local env)."""
+        stream = index_stream(self.data_len * self.world_size, self.config.n_epochs, self._base_seed + int(epoch))
+        return rank_share(stream, self.batch_size, self.rank, self.data_len)
+
+    def _global_update(self, epoch: int, buf) -> None:
+        """gs_ppo_update_global on this rank's shares of the global minibatches: the advantage
+        statistics of every global minibatch from all ranks' rows first (two host all-reduces of
+        n doubles), the update, then every rank's raw loss sums added and turned into the
+        minibatch records (gsamd.metrics.records_from_sums) — identical on every rank."""
+        c, B, n, T = self.config, self.batch_size, self.n_minibatches, self.config.n_steps
+        self._gidx.copy_(torch.from_numpy(self.global_shares(epoch)))
+        norm = c.normalize_advantages == "batch"
+        if norm:     # utils/torch.py:97-99 over the whole global minibatch
+            li = self._gidx.view(n, B).long()
+            mine = li >= 0
+            lc = li.clamp(min=0)
+            adv = torch.where(mine, buf.advantages[lc % T, lc // T].double(), torch.zeros((), dtype=torch.float64,
+                                                                                           device=self.device))
+            mean = allreduce_sum_f64(adv.sum(1).cpu().numpy()) / B
+            dev = torch.where(mine, adv - torch.from_numpy(mean).to(self.device)[:, None], 0.0)
+            std = np.sqrt(allreduce_sum_f64((dev * dev).sum(1).cpu().numpy()) / (B - 1))
+            self._adv_stats.copy_(torch.from_numpy(np.stack([mean, std], 1).astype(np.float32)))
+        glob = PPOGlobal(B, ptr(self._adv_stats) if norm else None, ptr(self._gsums))
+        check(lib.gs_ppo_update_global(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                       ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(),
+                                       ptr(self._gidx), B, n, self.adam_step, ptr(self.metrics_buf),
+                                       ptr(self.stop_flag), ptr(self.workspace), self.workspace.numel(), self.comm,
+                                       1 if self.use_graph else 0, ctypes.byref(glob), stream_handle()),
+              "gs_ppo_update_global")
+        sums = allreduce_sum_f64(self._gsums.cpu().numpy().reshape(-1)).reshape(n, NUM_SUMS)
+        rec = self.metrics_buf.cpu().numpy()
+        new = records_from_sums(sums, B, float(self.vf_coef), float(self.ent_coef), norm)
+        live = rec[:, M["unevaluated"]] == 0
+        cols = [M[k] for k in ("loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
+                               "explained_var", "kl", "approx_kl", "adv_norm_mean", "adv_norm_std")]
+        for j in cols:
+            rec[live, j] = new[live, j]
+        self.metrics_buf.copy_(torch.from_numpy(rec))
 
     def set_hyperparameter(self, param: str, value: float) -> None:
         """hyperparameter_mixin.py:105-114 (+ the policy_lr setter of callback_builder.py:108-113:

@@ -104,3 +104,16 @@ class IndexStreamPrefetcher:
             ev.record(s)
         self._events[slot] = ev
         return self.device_buf
+
+
+def rank_share(stream: np.ndarray, batch: int, rank: int, samples_per_rank: int) -> np.ndarray:
+    """Global-minibatch mode (include/gsamd.h gs_ppo_update_global): the global env-major index
+    stream (global env g = rank * n_envs + local env, index g * T + t) cut into minibatches of
+    `batch`; per minibatch, this rank's rows in stream order as local env-major indices, padded to
+    `batch` entries with -1.  (n_minibatches * batch,) int32."""
+    s = np.asarray(stream, np.int64).reshape(-1, int(batch))
+    mine = (s // int(samples_per_rank)) == int(rank)
+    order = np.argsort(~mine, axis=1, kind="stable")          # this rank's rows first, in order
+    rows = np.take_along_axis(s - int(rank) * int(samples_per_rank), order, axis=1)
+    keep = np.take_along_axis(mine, order, axis=1)
+    return np.where(keep, rows, -1).astype(np.int32).reshape(-1)

@@ -233,6 +233,31 @@ int gs_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float 
                   int32_t *stop_flag_dev, void *workspace_dev, size_t workspace_bytes, struct gs_comm *comm,
                   int use_graph, void *stream);
 
+/* Global-minibatch mode of a data-parallel update (SURVEY.md §8e "exact global" option): the
+ * reference's single-GPU math on G ranks.  Every rank runs the SAME n_minibatches global
+ * minibatches of batch_global rows, drawn from the reference's permutation of ALL ranks' samples
+ * (utils/samplers.py:25-34 over the global env-major index); idx_dev holds, per minibatch, this
+ * rank's rows (local env-major indices) padded to `batch` entries with -1 (another rank's row: no
+ * loss, no gradient).  The loss and its gradient are means over batch_global rows, so each rank's
+ * gradient is its share of the global one and the exchange SUMS them (no 1/G); the advantage
+ * normalisation uses the whole minibatch's statistics adv_stats (utils/torch.py:97-99, computed by
+ * the caller from all ranks' rows); with target_kl the KL early stop is decided on approx_kl summed
+ * over ranks (agents/ppo/ppo_agent.py:126-129), so every rank stops at the same minibatch.  This
+ * rank's raw loss sums per minibatch (14 doubles: sum of min-surrogate, clipped value loss,
+ * entropy, clip counts, kl, approx_kl, ret - v and its square, ret and its square, normalised adv
+ * and its square, one unused slot) go to metric_sums; the caller adds them over ranks and forms the records
+ * (gsamd.metrics.records_from_sums). */
+typedef struct gs_ppo_global {
+    int64_t batch_global;       /* rows of a global minibatch (all ranks) */
+    const float *adv_stats;     /* (n_minibatches, 2) f32 {mean, std} of each global minibatch's advantages */
+    double *metric_sums;        /* (n_minibatches, 14) out: this rank's raw loss sums */
+} gs_ppo_global;
+int gs_ppo_update_global(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
+                         gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout, const int32_t *idx_dev,
+                         int64_t batch, int64_t n_minibatches, int64_t adam_step0, float *metrics_dev,
+                         int32_t *stop_flag_dev, void *workspace_dev, size_t workspace_bytes, struct gs_comm *comm,
+                         int use_graph, const gs_ppo_global *glob, void *stream);
+
 /* Workspace for gs_ppo_update over n_minibatches steps.  When the shape has a compiled
  * fused chain (the BASELINE configs' MLP shapes) this includes the per-update gathered
  * minibatch fields and normalised advantages, so the per-step chain reads x in one load and

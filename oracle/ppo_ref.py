@@ -161,6 +161,41 @@ def ppo_loss_and_grads(flat, dims, obs, actions, old_logp, old_values, adv, ret,
     return float(loss), metrics, flatten(G, dims)
 
 
+def loss_sums(flat, dims, obs, actions, old_logp, old_values, adv, ret, *, clip, clip_vf, normalize="batch",
+              adv_stats=None):
+    """The 14 raw per-minibatch sums the device exports in the global-minibatch mode
+    (include/gsamd.h gs_ppo_global.metric_sums), over the given rows: sum of min-surrogate,
+    clipped value loss, entropy, ratio / value clip counts, kl, approx_kl (utils/torch.py:102-119),
+    ret - v and its square, ret and its square, normalised advantage and its square, and one
+    unused slot (agents/ppo/ppo_agent.py:53-146).  adv_stats: the (mean, std) to normalise with (a global
+    minibatch's); default the rows' own (utils/torch.py:97-99)."""
+    adv = np.asarray(adv, F32)
+    if normalize == "batch":
+        mu, sd = adv_stats if adv_stats is not None else (adv.mean(dtype=np.float64), adv.std(ddof=1, dtype=np.float64))
+        adv = ((adv - F32(mu)) / (F32(sd) + F32(1e-8))).astype(F32)
+    logits, value, _ = forward(flat, dims, obs)
+    ln = log_softmax(logits)
+    p = np.exp(ln).astype(F32)
+    n = obs.shape[0]
+    a = np.asarray(actions, np.int64)
+    new_lp = ln[np.arange(n), a]
+    ratio = np.exp(new_lp - old_logp).astype(F32)
+    rc = np.clip(ratio, F32(1 - clip), F32(1 + clip))
+    vdelta = value - old_values
+    vu = (value - ret) ** 2
+    vc = (old_values + np.clip(vdelta, -clip_vf, clip_vf) - ret) ** 2
+    H = -(p * ln).sum(axis=1)
+    r2 = np.exp(np.clip(new_lp - old_logp, -20.0, 20.0))
+    rv = (ret - value).astype(np.float64)
+    d = np.float64
+    return np.array([np.minimum(adv * ratio, adv * rc).sum(dtype=d), np.maximum(vu, vc).sum(dtype=d),
+                     H.sum(dtype=d), ((ratio < F32(1 - clip)) | (ratio > F32(1 + clip))).sum(dtype=d),
+                     ((vdelta < -clip_vf) | (vdelta > clip_vf)).sum(dtype=d), (old_logp - new_lp).sum(dtype=d),
+                     ((r2 - 1) - np.log(r2)).sum(dtype=d), rv.sum(), (rv * rv).sum(),
+                     np.asarray(ret, d).sum(), (np.asarray(ret, d) ** 2).sum(), adv.sum(dtype=d),
+                     (adv.astype(d) ** 2).sum(), 0.0])
+
+
 def clip_grad_norm(flat_grads, dims, max_norm):
     """torch.nn.utils.clip_grad_norm_: norm of per-parameter norms, coef clamped to 1."""
     P = unflatten(flat_grads, dims)

@@ -326,3 +326,55 @@ def xgmi_timeout_worker(rank, world, port, result_dir):
         if rank == 0 and not os.path.exists(done):
             open(done, "w").write("done")
     os._exit(code)
+
+
+def global_trajectory_worker(rank, world, port, result_dir, fixture, transport="xgmi", bwd="1"):
+    """dp_mode 'global' on the reference's trajectory fixture: the fixture's N envs split over
+    `world` ranks (rank g steps global envs [g N/world, (g+1) N/world) of the same synthetic env),
+    each replaying the reference's recorded actions of its envs; three rollouts + updates.  Saves
+    every minibatch record and the final parameters."""
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    os.environ["GS_XGMI_BWD"] = bwd
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd.config import load_config
+        from gsamd.distributed import comm_status, destroy_comm, init_device_comm, init_xgmi_comm
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        z = np.load(fixture)
+        N, T, E, B, D, A = (int(x) for x in z["dims"])
+        L, seed, trunc = (int(x) for x in z["env"])
+        n = N // world
+        torch.manual_seed(42)
+        over = dict(env_dynamics="synthetic", episode_len=L, truncate_every=trunc, obs_dim=D, n_actions=A, n_envs=n,
+                    dp_mode="global")
+        if "target_kl" in z.files and float(z["target_kl"]) > 0:
+            over["target_kl"] = float(z["target_kl"])
+        cfg = load_config("CartPole-v1", "ppo", overrides=over)
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        agent.policy_model.load_flat(z["params0"])
+        if world > 1:
+            agent.comm = (init_xgmi_comm(rank, world, agent.policy_model.n_params) if transport == "xgmi"
+                          else init_device_comm(rank, world, dev))
+        coll = agent.get_rollout_collector("train")
+        recs = []
+        for ep in range(3):
+            acts = torch.as_tensor(z["actions"][ep].reshape(N, T).T[:, rank * n:(rank + 1) * n].copy()).to(dev)
+            coll.collect(replay_actions=acts)
+            agent.update_phase()
+            recs.append(agent.metrics_buf.cpu().numpy().copy())
+        torch.cuda.synchronize()
+        np.savez(os.path.join(result_dir, f"g{rank}.npz"), rec=np.concatenate(recs),
+                 p=agent.policy_model.params.cpu().numpy(), adam_step=np.int64(agent.adam_step))
+        comm = agent.comm
+        if comm:
+            comm_status(comm)
+            dist.barrier()
+        del agent
+        if comm:
+            destroy_comm(comm)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()

@@ -241,3 +241,37 @@ def test_exchange_timeout_raises_from_train_epoch(tmp_path):
     out = json.load(open(tmp_path / "outcome"))
     assert out["timed_out"] and out["peer"] == 1 and out["workgroup"] >= 0 and out["site"] == 1, out
     assert "timed out" in out["message"] and "rank 1" in out["message"], out["message"]
+
+
+@pytest.mark.parametrize("fixture,world,bwd", [("trajectory.npz", 2, "1"), ("trajectory.npz", 2, "0"),
+                                               ("trajectory.npz", 1, "1"), ("trajectory_kl.npz", 2, "0")])
+def test_global_mode_reproduces_single_gpu_reference(tmp_path, fixture, world, bwd):
+    """dp_mode 'global' (SURVEY §8e exact-global option, gs_ppo_update_global): the reference
+    trajectory's 8 envs split 4 + 4 over 2 same-device ranks, each replaying the reference's
+    actions of its envs, reproduce the SINGLE-process reference run — the global sampler
+    (utils/samplers.py:25-34 over all ranks' samples), advantage normalisation over the whole
+    minibatch (utils/torch.py:97-99), the gradient as the sum of the ranks' shares (exchange inside
+    k_bwd, or as a launch), and with target_kl the KL stop decided on the all-rank approx_kl
+    (agents/ppo/ppo_agent.py:126-129): per-minibatch losses within 1e-4 of the fixture (the
+    north-star bar), the evaluated / stepped pattern exact, replicas bitwise identical."""
+    from _dist_workers import global_trajectory_worker
+    from gsamd._lib import M
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", fixture)
+    z = np.load(path)
+    _run(global_trajectory_worker, world, tmp_path, path, "xgmi", bwd, timeout=400)
+    runs = [np.load(tmp_path / f"g{r}.npz") for r in range(world)]
+    rec = runs[0]["rec"]
+    assert rec.shape[0] == z["losses"].shape[0]
+    if "evaluated" in z.files:
+        np.testing.assert_array_equal((rec[:, M["unevaluated"]] == 0).astype(np.uint8), z["evaluated"])
+        np.testing.assert_array_equal((rec[:, M["skipped"]] == 0).astype(np.uint8), z["stepped"])
+        ev = z["evaluated"].astype(bool)
+    else:
+        ev = np.ones(rec.shape[0], bool)
+    np.testing.assert_allclose(rec[ev, M["loss"]], z["losses"][ev], atol=1e-4, rtol=0)
+    p_ref = z["params_final"].astype(np.float64)
+    for r in range(world):
+        assert np.array_equal(runs[r]["p"].view(np.uint32), runs[0]["p"].view(np.uint32)), f"rank {r} diverged"
+        np.testing.assert_array_equal(runs[r]["rec"][:, M["loss"]], rec[:, M["loss"]])
+    p = runs[0]["p"].astype(np.float64)
+    assert np.linalg.norm(p - p_ref) / np.linalg.norm(p_ref) < 1e-4

@@ -267,3 +267,52 @@ def test_metrics_recorder_means_and_ppo_keys():
     assert vals["opt/loss/value_scaled"] == np.float32(0.125)
     assert vals["opt/loss/entropy_scaled"] == np.float32(0.01) * np.float32(-0.6)
     assert len(ppo_keys(False)) == 13 and len(ppo_keys(True)) == 15
+
+
+def test_global_mode_rank_shares_partition_the_reference_minibatches(golden):
+    """dp_mode 'global': every global minibatch of the reference's sampler stream (the fixture's
+    order over all envs) is split between the ranks that own its envs — each row exactly once, in
+    stream order, as the owner's local env-major index, padded with -1 to the batch size."""
+    from gsamd.samplers import rank_share
+    z = golden("trajectory.npz")
+    N, T, E, B, D, A = (int(x) for x in z["dims"])
+    stream = z["order"][0].astype(np.int64)
+    for world in (2, 4):
+        n = N // world
+        shares = [rank_share(stream, B, r, n * T).reshape(-1, B) for r in range(world)]
+        mb = stream.reshape(-1, B)
+        for k in range(mb.shape[0]):
+            got = []
+            for r, sh in enumerate(shares):
+                row = sh[k]
+                mine = row[row >= 0]
+                assert np.all(row[len(mine):] == -1)          # padding after this rank's rows
+                got.append(mine + r * n * T)
+            want_by_rank = [mb[k][(mb[k] // (n * T)) == r] for r in range(world)]
+            for g, w in zip(got, want_by_rank):
+                assert np.array_equal(g, w)                    # stream order kept
+            assert sorted(np.concatenate(got).tolist()) == sorted(mb[k].tolist())
+
+
+def test_records_from_sums_match_the_reference_record(golden):
+    """records_from_sums (the host half of the global mode's metrics) turns the 14 raw loss sums
+    of a minibatch into the reference's record: checked on the ppo_step fixture's batch, whose
+    sums the oracle computes row by row."""
+    from gsamd._lib import M
+    from gsamd.metrics import records_from_sums
+    from oracle import ppo_ref as R
+    z = golden("ppo_step.npz")
+    tag = "cartpole"
+    D, H1, H2, A, B = (int(x) for x in z[f"{tag}/dims"])
+    clip, cvf, vf, ent, lr = (float(x) for x in z[f"{tag}/hparams"])
+    sums = R.loss_sums(z[f"{tag}/params0"], (D, H1, H2, A), z[f"{tag}/obs"], z[f"{tag}/actions"],
+                       z[f"{tag}/old_logprobs"], z[f"{tag}/old_values"], z[f"{tag}/advantages"], z[f"{tag}/returns"],
+                       clip=clip, clip_vf=cvf)
+    rec = records_from_sums(sums[None], B, vf, ent, True)[0]
+    ref = dict(zip([str(x) for x in z[f"{tag}/metric_names"]], z[f"{tag}/metric_values"]))
+    np.testing.assert_allclose(rec[M["loss"]], float(z[f"{tag}/loss"]), rtol=1e-5, atol=1e-6)
+    for key, slot in [("opt/loss/policy", "policy_loss"), ("opt/loss/value", "value_loss"),
+                      ("opt/policy/entropy", "entropy"), ("opt/ppo/clip_fraction", "clip_fraction"),
+                      ("opt/value/explained_var", "explained_var"), ("opt/ppo/kl", "kl"),
+                      ("opt/ppo/approx_kl", "approx_kl"), ("roll/adv/norm/std", "adv_norm_std")]:
+        np.testing.assert_allclose(rec[M[slot]], ref[key], rtol=1e-5, atol=2e-6, err_msg=key)
