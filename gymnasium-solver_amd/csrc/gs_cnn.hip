@@ -131,7 +131,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_ov = (float *)take(sizeof(float) * R);
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
-    w.norm_part = (double *)take(sizeof(double) * kNormBlocks);
+    w.norm_part = (double *)take(sizeof(double) * kNormBlocks * 5);   // total + 4 component partials
     w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + 255) / 256));
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
@@ -614,18 +614,23 @@ __global__ __launch_bounds__(256) void k_cnn_dh(const float *__restrict__ dz, co
 
 
 // ---- global-norm partials (double) of the flat gradient
+// part[0 .. nb): the block partials of the whole gradient; part[nb (1 + c) + b]: component c's
+// (c = cnn trunk, mlp trunk, policy_head, value_head: flat ranges split at cut[0..2]) for the
+// per-component norms (utils/models.py:196-230)
 __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__ G, int64_t n, double *__restrict__ part,
-                                                       const int32_t *__restrict__ stop)
+                                                       const int32_t *__restrict__ stop, int64_t cut0, int64_t cut1,
+                                                       int64_t cut2)
 {
     if (stop && *stop) return;
-    __shared__ double sred[256 + 16];
-    double s[1] = {0.0};
+    __shared__ double sred[5 * (256 + 16)];
+    double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const double g = (double)G[i];
         s[0] += g * g;
+        s[1 + (i >= cut0) + (i >= cut1) + (i >= cut2)] += g * g;
     }
-    wg_reduce<1>(s, sred);
-    if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+    wg_reduce<5>(s, sred);
+    if (threadIdx.x < 5) part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s[threadIdx.x];
 }
 
 // ---- clip coefficient from the partials (every block, fixed order) + Adam (torch single-tensor)
@@ -647,6 +652,21 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     double s[1] = {0.0};
     for (int i = threadIdx.x; i < nparts; i += 256) s[0] += part[i];
     wg_reduce<1>(s, sred);
+    if (blockIdx.x == gridDim.x - 1 && metrics) {     // per-component norms (utils/models.py:196-230)
+        double c[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int i = threadIdx.x; i < nparts; i += 256)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c[k] += part[(int64_t)(1 + k) * nparts + i];
+        __shared__ double cred[4 * (256 + 16)];
+        wg_reduce<4>(c, cred);
+        if (threadIdx.x == 0) {
+            const float gs = aa.grad_scale;
+            metrics[GS_M_GN_BACKBONE] = (float)sqrt(c[0]) * gs;      // NatureCNN: the cnn trunk
+            metrics[GS_M_GN_MLP] = (float)sqrt(c[1]) * gs;
+            metrics[GS_M_GN_POLICY_HEAD] = (float)sqrt(c[2]) * gs;
+            metrics[GS_M_GN_VALUE_HEAD] = (float)sqrt(c[3]) * gs;
+        }
+    }
     if (threadIdx.x == 0) {
         const double ss = s[0] * (double)aa.grad_scale * (double)aa.grad_scale;
         const float total = (float)sqrt(ss);
@@ -880,7 +900,8 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         if ((rc = comm_allreduce_sum(comm, G, L.P, s, &world, stop))) return rc;
         aa.grad_scale = 1.0f / (float)world;
     }
-    hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop);
+    hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
+                       L.oWv);
     hipLaunchKernelGGL(k_clip_adam_flat, dim3(1024), dim3(256), 0, s, P, G, Mm, Vv, L.P, w.norm_part, kNormBlocks,
                        aa, metrics, stop);
     GS_LAUNCH_CHECK("k_clip_adam_flat");

@@ -133,6 +133,18 @@ __device__ __forceinline__ void block_reduce(T (&v)[NV], T *scratch)
     __syncthreads();
 }
 
+__device__ __forceinline__ void store_component_norms(double (&hq)[2], double total_sq, float gscale, float *rec,
+                                                      double *scratch)
+{
+    block_reduce<2>(hq, scratch);
+    if (threadIdx.x == 0 && rec) {
+        rec[GS_M_GN_POLICY_HEAD] = (float)sqrt(hq[0]) * gscale;
+        rec[GS_M_GN_VALUE_HEAD] = (float)sqrt(hq[1]) * gscale;
+        rec[GS_M_GN_BACKBONE] = (float)sqrt(fmax(0.0, total_sq - hq[0] - hq[1])) * gscale;
+        rec[GS_M_GN_MLP] = 0.0f;
+    }
+}
+
 // copy n floats global -> LDS, vectorised when both sides are 16-B aligned
 __device__ __forceinline__ void copy_to_lds(float *dst, const float *src, int n)
 {
@@ -158,6 +170,27 @@ __device__ __forceinline__ float clip_coef(float total, const AdamArgs &aa)
         coef = fminf(coef, 1.0f);
     }
     return coef;
+}
+
+// Per-component pre-clip gradient norms of one step (utils/models.py:196-230 compute_grad_norms,
+// recorded at agents/base_agent.py:607-608): policy_head and value_head from their gradients in G,
+// backbone as the rest of the step's squared total (every component of the MLP policy is one of
+// the three).  hq: this thread's {policy, value} sums of squares; every thread of the block calls
+// it (threads 0..255 contribute); scratch: 2 x (256 + 16) doubles; thread 0 writes the record.
+__device__ __forceinline__ void store_component_norms(double (&hq)[2], double total_sq, float gscale, float *rec,
+                                                      double *scratch);
+// head gradient u of the flat head index space: u < A1*H2 the weight rows (policy rows 0..A-1, then
+// the value row), past it the A1 biases; *value = whether it belongs to the value head
+__host__ __device__ inline int64_t head_grad_offset(const Layout &L, int u, bool *value)
+{
+    const int nw = (L.A + 1) * L.H2;
+    if (u < nw) {
+        const int a = u / L.H2;
+        *value = a == L.A;
+        return L.head_row(a) + (u - a * L.H2);
+    }
+    *value = u - nw == L.A;
+    return L.head_bias(u - nw);
 }
 
 // One parameter of torch.optim.Adam (single-tensor path, amsgrad off) on the clipped gradient;
@@ -353,6 +386,18 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         float sl[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) sl[j] = nrm ? ld1(af.sumsq, min(tid + 256 * j, aa.n_slots - 1)) : 0.0f;
+        // the grid's last workgroup (never a parameter owner while the grid has more than one row
+        // block) also records the per-component gradient norms: its head gradients join the burst
+        constexpr int nhg = cA1 * Lc.H2 + cA1, NHG = (nhg + 255) / 256;
+        const bool diag = apply && af.metrics && cb == (int)gridDim.x - 1 && rb == (int)gridDim.y - 1;
+        float hg[NHG];
+        bool hval[NHG];
+#pragma unroll
+        for (int j = 0; j < NHG; ++j) {
+            hg[j] = 0.0f;
+            hval[j] = false;
+            if (diag && nrm) hg[j] = ld1(af.G, head_grad_offset(Lc, min(tid + 256 * j, nhg - 1), &hval[j]));
+        }
         // then the loads behind the graph replay's step base: this minibatch's x rows and step
         // k-1's schedule entries
         float xv = 0.0f;
@@ -407,6 +452,15 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             const float total = (float)sqrt(tt[0]) * aa.grad_scale;
             coef = clip_coef(total, aa) * aa.grad_scale;
             if (own1 && tid == 0 && af.metrics) af.metrics[kprev * GS_NUM_METRICS + GS_M_GRAD_NORM] = total;
+            if (diag) {
+                double hq[2] = {0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j < NHG; ++j)
+                    if (nrm && tid + 256 * j < nhg) hq[hval[j] ? 1 : 0] += (double)hg[j] * (double)hg[j];
+                // scratch: red (1024 floats) and the h2 tile after it, both unused until phase 2
+                store_component_norms(hq, tt[0], aa.grad_scale, af.metrics + kprev * GS_NUM_METRICS,
+                                      reinterpret_cast<double *>(red));
+            }
         }
         GS_STAMP(1)
         // Adam on the owned parameters: new values to LDS / registers, and from row block 0 to the other set
@@ -2256,7 +2310,7 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
     GS_STAMP_BEGIN(3)
     const int64_t kb = aa.step_base ? *aa.step_base : 0;
     if (metrics) metrics += kb * GS_NUM_METRICS;
-    __shared__ double sred[272];
+    __shared__ double sred[2 * 272];
     __shared__ float s_coef;
     const Layout L = S::lay(Lrt);
     const int tid = threadIdx.x;
@@ -2409,6 +2463,16 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
         const float total = (float)sqrt(tot) * aa.grad_scale;
         s_coef = clip_coef(total, aa);
         if (blockIdx.x == 0 && metrics) metrics[GS_M_GRAD_NORM] = total;
+    }
+    if (metrics && blockIdx.x == gridDim.x - 1) {   // per-component norms (utils/models.py:196-230)
+        double hq[2] = {0.0, 0.0};
+        const int nhg = (L.A + 1) * (L.H2 + 1);
+        for (int u = tid; u < nhg; u += 256) {
+            bool val;
+            const double g = (double)G[head_grad_offset(L, u, &val)];
+            hq[val ? 1 : 0] += g * g;
+        }
+        store_component_norms(hq, tt[0], aa.grad_scale, metrics, sred);
     }
     __syncthreads();
     const float coef = s_coef * aa.grad_scale;

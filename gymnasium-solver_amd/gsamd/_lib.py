@@ -16,12 +16,14 @@ import torch  # noqa: F401  (load torch's HIP runtime before the library)
 LIB_PATH = os.environ.get("GSAMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
 
 GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
-GS_ABI_VERSION = 2          # include/gsamd.h: the argument lists this binding declares
-GS_NUM_METRICS = 16
+GS_ABI_VERSION = 3          # include/gsamd.h: the argument lists this binding declares
+GS_NUM_METRICS = 24
 METRIC_SLOTS = (
     "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
     "explained_var", "kl", "approx_kl", "adv_norm_mean", "adv_norm_std", "kl_stop", "grad_norm",
     "skipped", "unevaluated", "res1",
+    # pre-clip per-component gradient norms (utils/models.py:196-230)
+    "gn_backbone", "gn_policy_head", "gn_value_head", "gn_mlp", "res20", "res21", "res22", "res23",
 )
 M = {name: i for i, name in enumerate(METRIC_SLOTS)}
 

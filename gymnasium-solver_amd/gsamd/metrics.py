@@ -3,7 +3,7 @@
 appends one record, ``compute_epoch_means(namespace)`` averages every key over its records,
 ``reset_epoch(namespace)`` clears them.
 
-The device update writes one 16-float record per minibatch (include/gsamd.h GS_M_* slots) and
+The device update writes one 24-float record per minibatch (include/gsamd.h GS_M_* slots) and
 the host reads them once per epoch; ``ppo_records`` turns such records into the reference's
 ``losses_for_batch`` keys (agents/ppo/ppo_agent.py:131-146, utils/torch.py:170-173), and
 ``record_rows`` books a whole block of them at once (no per-minibatch Python on the fast path).
@@ -44,13 +44,13 @@ NUM_SUMS = 14      # raw loss sums per minibatch (include/gsamd.h gs_ppo_global.
 
 
 def records_from_sums(sums: np.ndarray, rows: int, vf_coef: float, ent_coef: float, normalize: bool) -> np.ndarray:
-    """(n, 14) raw loss sums of whole minibatches (every rank's added) -> the (n, 16) loss slots of
+    """(n, 14) raw loss sums of whole minibatches (every rank's added) -> the (n, 24) loss slots of
     the device records, with the arithmetic of csrc/gs_mlp.hip write_metrics (f32 terms from
     double sums; torch.var's unbiased variance for explained_var, utils/torch.py:97-99 statistics
     for the normalised advantages).  The KL / skip / grad-norm slots are left at zero."""
     t = np.asarray(sums, np.float64).reshape(-1, NUM_SUMS)
     Bd = float(rows)
-    out = np.zeros((t.shape[0], 16), np.float32)
+    out = np.zeros((t.shape[0], len(M)), np.float32)
     pl = (-t[:, 0] / Bd).astype(np.float32)
     vl = (t[:, 1] / Bd).astype(np.float32)
     ent = (t[:, 2] / Bd).astype(np.float32)

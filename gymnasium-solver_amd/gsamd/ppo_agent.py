@@ -11,7 +11,7 @@ agents/ppo/ppo_agent.py:10-152):
   get_rollout_collector(stage)                DeviceRolloutCollector
 and the fast path the trainer uses instead of per-minibatch Python:
   train_epoch()                               rollout + the whole update phase in one C-ABI call
-Metrics are kept on device, one 16-float record per minibatch, and converted to the
+Metrics are kept on device, one 24-float record per minibatch, and converted to the
 reference's metric keys once per epoch (the reference pays ~20 .item() syncs per
 minibatch, SURVEY.md §3 Boundaries).
 """
@@ -428,8 +428,18 @@ class DevicePPOAgent:
             self._early_stop_epoch = True
             self.adam_step -= 1              # the tripping minibatch took no optimizer step
         else:
-            self.metrics_recorder.record("train", {"opt/grads/norm/all": float(row[M["grad_norm"]])})
+            keys, slots = self.grad_norm_keys()
+            self.metrics_recorder.record("train", {k: float(row[j]) for k, j in zip(keys, slots)})
         return None
+
+    def grad_norm_keys(self):
+        """compute_grad_norms' keys (utils/models.py:196-230, base_agent.py:607-608) and their record
+        slots: "all", then the model's components in the reference's discovery order."""
+        comps = ("cnn", "mlp", "policy_head", "value_head") if self.is_pixel else ("backbone", "policy_head", "value_head")
+        slot = {"backbone": M["gn_backbone"], "cnn": M["gn_backbone"], "mlp": M["gn_mlp"],
+                "policy_head": M["gn_policy_head"], "value_head": M["gn_value_head"]}
+        return (("opt/grads/norm/all",) + tuple(f"opt/grads/norm/{c}" for c in comps),
+                [M["grad_norm"]] + [slot[c] for c in comps])
 
     # ---- fused epoch (the trainer's path) -------------------------------------------------------
     def train_epoch(self) -> None:
@@ -558,7 +568,8 @@ class DevicePPOAgent:
         self.metrics_recorder.record_rows("train", ppo_keys(norm),
                                           ppo_records(live, float(self.vf_coef), float(self.ent_coef), norm))
         stepped = rec[rec[:, M["skipped"]] == 0]
-        self.metrics_recorder.record_rows("train", ("opt/grads/norm/all",), stepped[:, M["grad_norm"]])
+        keys, slots = self.grad_norm_keys()
+        self.metrics_recorder.record_rows("train", keys, stepped[:, slots])
         if self.config.target_kl is not None and (rec[:, M["kl_stop"]] != 0).any():
             self._early_stop_epoch = True        # sticky, as BaseAgent._early_stop_epoch
         return rec
@@ -566,7 +577,7 @@ class DevicePPOAgent:
     def epoch_metric_keys(self):
         """The fixed key list of epoch_metrics (every rank sends the same vector)."""
         norm = self.config.normalize_advantages == "batch"
-        return tuple(ppo_keys(norm)) + ("opt/grads/norm/all",)
+        return tuple(ppo_keys(norm)) + self.grad_norm_keys()[0]
 
     def epoch_metrics(self) -> Dict[str, float]:
         """The last update's epoch means under the reference's metric keys (ppo_agent.py:131-146,

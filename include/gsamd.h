@@ -41,8 +41,9 @@ extern "C" {
  * gs_abi_version() returns GS_ABI_VERSION of the header the library was built with; a binding
  * must refuse a library whose version differs (argument lists change between versions:
  * version 2 added the rollout clock argument of gs_policy_act / gs_cnn_policy_act /
- * gs_env_step / gs_atari_env_step and gs_comm_error_record). */
-#define GS_ABI_VERSION 2
+ * gs_env_step / gs_atari_env_step and gs_comm_error_record; version 3 widened the metric record
+ * to 24 floats and added gs_ppo_update_global). */
+#define GS_ABI_VERSION 3
 int gs_abi_version(void);
 const char *gs_last_error(void);
 
@@ -169,11 +170,16 @@ typedef struct gs_ppo_hparams {
  * KL early stop (agents/base_agent.py:330-366, sticky): the minibatch whose approx_kl exceeds
  * target_kl keeps its loss metrics with KL_STOP = SKIPPED = 1 (no optimizer step); every later
  * one is zeros with SKIPPED = KL_STOP = UNEVALUATED = 1 (its loss was never computed). */
-#define GS_NUM_METRICS 16
+#define GS_NUM_METRICS 24
 enum gs_metric_slot {
     GS_M_LOSS = 0, GS_M_POLICY_LOSS, GS_M_VALUE_LOSS, GS_M_ENTROPY, GS_M_CLIP_FRAC,
     GS_M_CLIP_FRAC_VF, GS_M_EXPLAINED_VAR, GS_M_KL, GS_M_APPROX_KL, GS_M_ADV_NORM_MEAN,
-    GS_M_ADV_NORM_STD, GS_M_KL_STOP, GS_M_GRAD_NORM, GS_M_SKIPPED, GS_M_UNEVALUATED, GS_M_RES1
+    GS_M_ADV_NORM_STD, GS_M_KL_STOP, GS_M_GRAD_NORM, GS_M_SKIPPED, GS_M_UNEVALUATED, GS_M_RES1,
+    /* pre-clip gradient norms per component (utils/models.py:196-230 compute_grad_norms, recorded
+     * at agents/base_agent.py:607-608): MLP backbone | NatureCNN cnn trunk, policy_head,
+     * value_head, and the NatureCNN mlp (fc) trunk (0 for the MLP policy) */
+    GS_M_GN_BACKBONE, GS_M_GN_POLICY_HEAD, GS_M_GN_VALUE_HEAD, GS_M_GN_MLP,
+    GS_M_RES20, GS_M_RES21, GS_M_RES22, GS_M_RES23
 };
 
 size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch);

@@ -262,9 +262,13 @@ def make_ppo_step():
                                       advantages=adv, returns=ret)
         opt = torch.optim.Adam(model.parameters(), lr=1e-3 if tag == "cartpole" else 3e-4)
         opt.zero_grad()
+        model._track_activations = True          # BaseAgent.training_step (base_agent.py:336-347)
         res = agent.losses_for_batch(batch, 0)
+        acts = model.compute_activation_stats()
+        model._track_activations = False
         res["loss"].backward()
         g_raw = _flat_grads(model)
+        gnorms = model.compute_grad_norms()      # BaseAgent._backpropagate_and_step (base_agent.py:607-608)
         total = torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
         g_clip = _flat_grads(model)
         opt.step()
@@ -279,7 +283,11 @@ def make_ppo_step():
                     f"{tag}/dims": np.array([D, *H, A, B], np.int64),
                     f"{tag}/hparams": np.array([clip, 0.2, 0.5, ent, opt.param_groups[0]["lr"]], np.float64),
                     f"{tag}/metric_names": np.array(sorted(metrics)),
-                    f"{tag}/metric_values": np.array([metrics[k] for k in sorted(metrics)], np.float64)})
+                    f"{tag}/metric_values": np.array([metrics[k] for k in sorted(metrics)], np.float64),
+                    f"{tag}/grad_norm_names": np.array(sorted(gnorms)),
+                    f"{tag}/grad_norm_values": np.array([gnorms[k] for k in sorted(gnorms)], np.float64),
+                    f"{tag}/activation_names": np.array(sorted(acts)),
+                    f"{tag}/activation_values": np.array([acts[k] for k in sorted(acts)], np.float64)})
     np.savez_compressed(os.path.join(HERE, "ppo_step.npz"), **out)
     print("ppo_step.npz written")
 
@@ -311,9 +319,13 @@ def make_cnn_step():
             logits = dist.logits.numpy()
         opt = torch.optim.Adam(model.parameters(), lr=lr)
         opt.zero_grad()
+        model._track_activations = True          # BaseAgent.training_step (base_agent.py:336-347)
         res = agent.losses_for_batch(batch, 0)
+        acts = model.compute_activation_stats()
+        model._track_activations = False
         res["loss"].backward()
         g_raw = _flat_grads(model)
+        gnorms = model.compute_grad_norms()      # BaseAgent._backpropagate_and_step (base_agent.py:607-608)
         norms = np.array([p.grad.double().norm().item() for p in model.parameters()], np.float64)
         total = torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
         opt.step()
@@ -325,7 +337,11 @@ def make_cnn_step():
                     f"{tag}/grads_sel": g_raw[sel], f"{tag}/params1_sel": p1[sel],
                     f"{tag}/logits": logits, f"{tag}/values": v.numpy(),
                     f"{tag}/metric_names": np.array(sorted(metrics)),
-                    f"{tag}/metric_values": np.array([metrics[k] for k in sorted(metrics)], np.float64)})
+                    f"{tag}/metric_values": np.array([metrics[k] for k in sorted(metrics)], np.float64),
+                    f"{tag}/grad_norm_names": np.array(sorted(gnorms)),
+                    f"{tag}/grad_norm_values": np.array([gnorms[k] for k in sorted(gnorms)], np.float64),
+                    f"{tag}/activation_names": np.array(sorted(acts)),
+                    f"{tag}/activation_values": np.array([acts[k] for k in sorted(acts)], np.float64)})
     np.savez_compressed(os.path.join(HERE, "cnn_step.npz"), **out)
     print("cnn_step.npz written")
 

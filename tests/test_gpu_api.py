@@ -63,10 +63,18 @@ def test_losses_for_batch_on_reference_tensor_batch(golden, cuda, tag):
     assert set(got) == set(ref) == set(ppo_keys(True))
     for k in ref:
         np.testing.assert_allclose(got[k], ref[k], atol=2e-6, rtol=1e-5, err_msg=k)
+    agent.metrics_recorder.reset_epoch("train")
     agent.training_step(batch, 0)
     torch.cuda.synchronize()
     np.testing.assert_allclose(agent.policy_model.params.cpu().numpy(), z[f"{tag}/params1"], atol=2e-6, rtol=0)
     assert agent.adam_step == 1
+    # the pre-clip gradient norms the reference's compute_grad_norms records (utils/models.py:196-230,
+    # base_agent.py:607-608): all, backbone, policy_head, value_head
+    got = agent.metrics_recorder.compute_epoch_means("train")
+    gn = dict(zip([str(x) for x in z[f"{tag}/grad_norm_names"]], z[f"{tag}/grad_norm_values"]))
+    assert set(gn) <= set(got), set(gn) - set(got)
+    for k in gn:
+        np.testing.assert_allclose(got[k], gn[k], rtol=1e-5, err_msg=k)
 
 
 def _replay_trajectory(agent, z, cuda, check_metrics=True):

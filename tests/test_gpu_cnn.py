@@ -77,6 +77,14 @@ def test_cnn_update_step_vs_oracle_and_reference(golden, cuda, tag):
     for key, slot in (("opt/loss/policy", 1), ("opt/loss/value", 2), ("opt/policy/entropy", 3),
                       ("opt/ppo/clip_fraction", 4), ("opt/ppo/approx_kl", 8)):
         assert abs(rec[slot] - ref[key]) < 1e-5 * max(1.0, abs(ref[key])), key
+    # pre-clip gradient norms per component, as the reference's compute_grad_norms records them
+    # (utils/models.py:196-230: all, cnn, mlp, policy_head, value_head)
+    from gsamd._lib import M
+    gn = dict(zip([str(x) for x in z[f"{tag}/grad_norm_names"]], z[f"{tag}/grad_norm_values"]))
+    for key, slot in (("opt/grads/norm/all", "grad_norm"), ("opt/grads/norm/cnn", "gn_backbone"),
+                      ("opt/grads/norm/mlp", "gn_mlp"), ("opt/grads/norm/policy_head", "gn_policy_head"),
+                      ("opt/grads/norm/value_head", "gn_value_head")):
+        np.testing.assert_allclose(rec[M[slot]], gn[key], rtol=1e-5, err_msg=key)
 
 
 @pytest.mark.parametrize("tag", list(CASES))

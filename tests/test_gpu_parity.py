@@ -340,11 +340,22 @@ def test_update_first_minibatches_vs_numpy_oracle(cuda, use_graph):
               traj.values.cpu().numpy(), traj.advantages.cpu().numpy(), traj.returns.cpu().numpy()]
     m = np.zeros_like(p)
     v = np.zeros_like(p)
+    from gsamd._lib import M
+    rec = agent.metrics_buf[:n].cpu().numpy()
+    D_, H1, H2, A_ = dims
+    o_pol = H1 * D_ + H1 + H2 * H1 + H2
+    o_val = o_pol + A_ * H2 + A_
     for k in range(n):
         rows = stream[k * B:(k + 1) * B]
         loss, _, g = R.ppo_loss_and_grads(p, dims, *(f[rows] for f in fields), clip=cfg.clip_range,
                                           clip_vf=cfg.clip_range_vf, vf_coef=cfg.vf_coef, ent_coef=cfg.ent_coef)
         np.testing.assert_allclose(losses[k], loss, rtol=1e-5, atol=1e-6, err_msg=f"minibatch {k}")
+        # per-component pre-clip norms (utils/models.py:196-230), written by the next forward's
+        # lagged step (the last one by k_clip_adam)
+        g64 = g.astype(np.float64)
+        for slot, part in (("gn_backbone", g64[:o_pol]), ("gn_policy_head", g64[o_pol:o_val]),
+                           ("gn_value_head", g64[o_val:])):
+            np.testing.assert_allclose(rec[k, M[slot]], np.linalg.norm(part), rtol=2e-5, err_msg=f"{slot} {k}")
         gc, _ = R.clip_grad_norm(g, dims, cfg.max_grad_norm)
         p, m, v = R.adam_step(p, gc, m, v, k + 1, cfg.policy_lr)
     p_dev = pm.params.cpu().numpy().astype(np.float64)
