@@ -121,10 +121,12 @@ class PPOConfig:
         if not (0 < self.gamma <= 1):
             raise ValueError("gamma must be in (0, 1]")
         rollout = self.n_envs * self.n_steps
-        if self.batch_size > rollout:
+        if self.dp_mode == "global":
+            pass        # minibatches span every rank's rollout: DevicePPOAgent checks them with the world size
+        elif self.batch_size > rollout:
             raise ValueError(f"batch_size ({self.batch_size}) should not exceed n_envs ({self.n_envs}) * "
                              f"n_steps ({self.n_steps}).")
-        if rollout % self.batch_size != 0:
+        if self.dp_mode != "global" and rollout % self.batch_size != 0:
             raise ValueError("batch_size must divide (n_envs * n_steps) exactly to yield uniform minibatches: "
                              f"rollout_size={rollout}, batch_size={self.batch_size}.")
         if self.normalize_advantages not in ("batch", "rollout", "off", False, None, ""):

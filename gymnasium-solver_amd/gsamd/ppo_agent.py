@@ -292,7 +292,12 @@ class DevicePPOAgent:
         c = self.config
         self.batch_size = int(c.batch_size)
         self.data_len = c.n_envs * c.n_steps
-        if self.data_len % self.batch_size != 0:
+        if str(getattr(c, "dp_mode", "local")) == "global":
+            total = self.data_len * self.world_size
+            if self.batch_size > total or total % self.batch_size != 0:
+                raise ValueError(f"batch_size ({self.batch_size}) must divide the job's rollout of {total} samples "
+                                 f"({self.world_size} ranks x {c.n_envs} envs x {c.n_steps} steps) in global mode")
+        elif self.data_len % self.batch_size != 0:
             raise ValueError(f"Batch size must divide rollout size exactly: data_len={self.data_len}, "
                              f"batch_size={self.batch_size}.")
         self.n_minibatches = self.data_len // self.batch_size * c.n_epochs
