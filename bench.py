@@ -33,6 +33,7 @@ import torch  # noqa: E402
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 # CPU port vs the reference's own loop on the same 8-core container at C2 shapes
 # (5 646 / 2 814 env-steps/s)
 CPU_PORT_OVER_REFERENCE = round(5646.0 / 2814.0, 3)
@@ -234,6 +235,41 @@ def time_exchange(comm, n: int, reps: int, device, barrier):
     return us
 
 
+def bf16_deviation(agent) -> dict:
+    """Loss trajectory of one update (all its minibatches) in the fp32 parity path and in the bf16
+    mode, from the same parameters / Adam state on the same rollout and index stream."""
+    import numpy as np
+    from gsamd._lib import GS_HP_BF16, check, lib, ptr, stream_handle
+    pm, coll = agent.policy_model, agent.get_rollout_collector("train")
+    idx = agent.prefetcher.device_buf
+    state = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v)]
+    res = {}
+    for name, flags in (("fp32", 0), ("bf16", GS_HP_BF16)):
+        for t, s0 in zip((pm.params, agent.adam_m, agent.adam_v), state):
+            t.copy_(s0)
+        hp = agent.hparams()
+        hp.flags = flags
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
+                                    hp, coll.buffer.view(), ptr(idx), agent.batch_size, agent.n_minibatches,
+                                    agent.adam_step, ptr(agent.metrics_buf), ptr(agent.stop_flag),
+                                    ptr(agent.workspace), None, stream_handle()), "gs_cnn_ppo_update")
+        e1.record()
+        e1.synchronize()
+        res[name] = (agent.metrics_buf[:, 0].cpu().numpy().astype(np.float64), pm.params.cpu().numpy().astype(np.float64),
+                     e0.elapsed_time(e1))
+    for t, s0 in zip((pm.params, agent.adam_m, agent.adam_v), state):
+        t.copy_(s0)
+    (l32, p32, t32), (l16, p16, t16) = res["fp32"], res["bf16"]
+    scale = max(1.0, float(np.abs(l32).max()))
+    return {"minibatches": int(l32.size), "loss_max_abs_dev": float(np.abs(l16 - l32).max()),
+            "loss_max_dev_rel_to_scale": float(np.abs(l16 - l32).max() / scale),
+            "loss_mean_abs_dev": float(np.abs(l16 - l32).mean()),
+            "final_params_rel_l2": float(np.linalg.norm(p16 - p32) / np.linalg.norm(p32)),
+            "update_ms": {"fp32": round(t32, 3), "bf16": round(t16, 3)}}
+
+
 def _free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -310,6 +346,9 @@ def main():
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: all ranks share cuda:0 (gloo process group, "
                          "xGMI exchange through same-device IPC); throughput is not meaningful")
+    ap.add_argument("--dtype", choices=("f32", "bf16"), default="f32",
+                    help="f32: the fp32 parity path (default, the metric's line); bf16: bf16 MFMA operands in the "
+                         "NatureCNN update (C4/C5 only), reported as its own line with its deviation from fp32")
     ap.add_argument("--stage-reps", type=int, default=200)
     ap.add_argument("--cpu-minibatches", type=int, default=-1,
                     help="minibatches timed in the CPU baseline (-1: the whole update, 0: no CPU baseline)")
@@ -344,6 +383,10 @@ def main():
     # the benchmark's env is chosen explicitly: SURVEY §8d synthetic fixed-length episodes (or the
     # synthetic Atari frame source), or the device CartPole-v1 dynamics
     over = dict(n_envs=n_envs, env_dynamics="synthetic" if pixel else args.env_dynamics)
+    if args.dtype == "bf16":
+        if not pixel:
+            raise SystemExit("[bench] --dtype bf16 is implemented for the NatureCNN workloads (C4, C5)")
+        over["precision"] = "bf16"
     cfg = load_config(env_id, variant, overrides=over)
     agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world,
                            use_graph=not args.no_graph, track_stats=False)
@@ -413,8 +456,9 @@ def main():
         amount = cnn_minibatch_flops(agent.batch_size, pm.n_actions)
         mb_us = update_ms * 1e3 / agent.n_minibatches
         achieved = amount / (mb_us * 1e-6) / 1e12
-        roofline = {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 6), "traffic": None,
+        peak = PEAK_BF16_MFMA_TFLOPS if args.dtype == "bf16" else PEAK_F32_MFMA_TFLOPS
+        roofline = {"bound": "mfma", "achieved": round(achieved, 4), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 6), "traffic": None,
                     "kernel": "cnn minibatch step (k_conv1_*, k_gemm, gs_cnn kernels)", "avg_us": round(mb_us, 3),
                     "work_per_launch": amount}
     else:
@@ -476,6 +520,10 @@ def main():
         rooflines["gae"]["traffic"] = pmc.get(f"k_gae_staged[grid={grid}]", {}).get("hbm_bytes_per_launch")
     roofline["traffic_source"] = traffic_src
 
+    # ---- bf16 mode: one whole update in fp32 and in bf16 from the same state, rollout and
+    #      sampler order; the per-minibatch loss deviation is reported beside the line ----
+    bf16_dev = bf16_deviation(agent) if args.dtype == "bf16" and rank == 0 else None
+
     # ---- CPU baseline (rank 0, N=1 only): oracle restatement on the host cores ----
     cpu = None
     if rank == 0 and world == 1 and args.cpu_minibatches != 0:
@@ -531,7 +579,7 @@ def main():
             "metric": METRICS[args.workload].format(n=N),
             "value": round(value, 2), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic" if args.env_dynamics == "synthetic" else "device CartPole-v1 dynamics",
             "config": {"workload": (f"{env_id}:{variant} {args.workload} (rollout {N} envs x {T} steps + "
                                     f"{cfg.n_epochs}-epoch PPO update, B={cfg.batch_size})"),
@@ -550,6 +598,8 @@ def main():
                           "update_us_per_minibatch": round(update_ms * 1e3 / agent.n_minibatches, 3)},
             "cpu_baseline": cpu,
         }
+        if bf16_dev is not None:
+            line["bf16_vs_fp32"] = bf16_dev
         print(json.dumps(line), flush=True)
     if comm is not None:
         from gsamd.distributed import destroy_comm

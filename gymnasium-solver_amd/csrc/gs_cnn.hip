@@ -957,6 +957,7 @@ extern "C" int gs_cnn_ppo_loss(const float *params, gs_cnn_dims dims, gs_ppo_hpa
     int rc = validate_cnn_update(dims, ro, batch, workspace);
     if (rc) return rc;
     GS_REQUIRE(params && idx && metrics, "gs_cnn_ppo_loss: null buffer");
+    const Bf16Scope prec((hp.flags & GS_HP_BF16) != 0);
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
@@ -979,6 +980,8 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     GS_REQUIRE(n_minibatches >= 0 && adam_step0 >= 0, "bad n_minibatches/adam_step0");
     GS_REQUIRE(params && grads && adam_m && adam_v && idx && metrics, "gs_cnn_ppo_update: null buffer");
     GS_REQUIRE(ro.T * ro.N < ((int64_t)1 << 31), "rollout larger than 2^31 samples");
+    // GS_HP_BF16: bf16 MFMA operands in every convolution / GEMM launch of this update
+    const Bf16Scope prec((hp.flags & GS_HP_BF16) != 0);
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);

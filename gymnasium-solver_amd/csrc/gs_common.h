@@ -8,6 +8,7 @@
 #include "../../include/gsamd.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace gs {
 
@@ -289,5 +290,37 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
                      const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s);
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);
 int launch_sumsq_flat(const float *G, int64_t n, float *out, int nblocks, hipStream_t s);
+
+// ---- bf16 MFMA operands of the NatureCNN path (GS_HP_BF16 performance mode) ----------------
+// 8 fp32 values -> one bf16 fragment of v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16 (round to
+// nearest even: v_cvt_pk_bf16_f32); accumulation stays fp32
+__device__ __forceinline__ bf16x8 bf16_frag(float4 lo, float4 hi)
+{
+    bf16x8 r;
+    r[0] = (__bf16)lo.x, r[1] = (__bf16)lo.y, r[2] = (__bf16)lo.z, r[3] = (__bf16)lo.w;
+    r[4] = (__bf16)hi.x, r[5] = (__bf16)hi.y, r[6] = (__bf16)hi.z, r[7] = (__bf16)hi.w;
+    return r;
+}
+__device__ __forceinline__ bf16x8 bf16_frag(const float (&v)[8])
+{
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+    return r;
+}
+// 16x16 tile, K = 32: lane l holds A[l & 15][8 (l >> 4) + j] and B[8 (l >> 4) + j][l & 15];
+// C/D as the fp32 16x16x4 form (col = l & 15, row = 4 (l >> 4) + reg)
+__device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// host: the operand precision of this thread's NatureCNN launches (gs_cnn_ppo_update and
+// gs_cnn_policy_act set it from hp.flags for the duration of their enqueues)
+bool cnn_bf16();
+struct Bf16Scope {
+    bool prev;
+    explicit Bf16Scope(bool on);
+    ~Bf16Scope();
+};
 
 }  // namespace gs

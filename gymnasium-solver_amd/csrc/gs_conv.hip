@@ -89,7 +89,7 @@ __device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict_
 
 // tap order of MFMA k-step s = 4g + j for lane quarter q: channel g / 4, row ky = 2 (g % 4) + q / 2,
 // column kx = 4 (q % 2) + j — a lane's 4 steps of a group are 4 adjacent pixels
-template <class G>
+template <class G, bool BF = false>
 __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
                                                    int64_t T, int64_t N, const float *__restrict__ W1,
                                                    const float *__restrict__ b1, float *__restrict__ out)
@@ -126,6 +126,26 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
     f32x4 acc[TMW];
 #pragma unroll
     for (int t = 0; t < TMW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BF) {
+        // GS_HP_BF16: groups g, g + 1 as one 16x16x32 bf16 MFMA — element j of lane quarter q is
+        // tap (g, q, j) for j < 4 and (g + 1, q, j - 4) after, in the patch and filter operands alike
+        bf16x8 bw[G::KS / 8];
+#pragma unroll
+        for (int gp = 0; gp < G::KS / 8; ++gp) bw[gp] = bf16_frag(b[2 * gp], b[2 * gp + 1]);
+#pragma unroll
+        for (int gp = 0; gp < G::KS / 8; ++gp) {
+            const int g0 = 2 * gp, g1 = g0 + 1;
+            const int goff0 = ((g0 >> 2) * G::BIR + 2 * (g0 & 3)) * G::W;
+            const int goff1 = ((g1 >> 2) * G::BIR + 2 * (g1 & 3)) * G::W;
+#pragma unroll
+            for (int t = 0; t < TMW; ++t) {
+                if (tpar + 2 * t >= G::MT) break;
+                const bf16x8 a = bf16_frag(*reinterpret_cast<const float4 *>(fr + abase[t] + goff0),
+                                           *reinterpret_cast<const float4 *>(fr + abase[t] + goff1));
+                acc[t] = mfma16_bf16(a, bw[gp], acc[t]);
+            }
+        }
+    } else
 #pragma unroll
     for (int g = 0; g < G::KS / 4; ++g) {
         const int goff = ((g >> 2) * G::BIR + 2 * (g & 3)) * G::W;
@@ -167,7 +187,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
 // A unit is 5 output rows of one sample (4 per sample at 84 x 84): its 24-row frame band
 // (fp32) and 100 x 32 dA rows fit twice in LDS, so the next unit's global loads (held in
 // registers) run under the current unit's MFMAs.  parts layout: [workgroup][CO * KK + CO]
-template <class G>
+template <class G, bool BF = false>
 __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
                                                      int64_t T, int64_t N, int R, const float *__restrict__ dA,
                                                      float *__restrict__ parts)
@@ -267,6 +287,33 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
             const int co = tid & 31, grp = tid >> 5;
             for (int p = grp; p < P; p += 8) db += da[buf][p * DS + co];
         }
+        if constexpr (BF) {
+            // GS_HP_BF16: 8 k-steps per 16x16x32 bf16 MFMA — element j of lane quarter q is
+            // position 4 (s0 + j) + q in both operands; steps past the unit are zeros
+            constexpr int NS = UPP / 4;
+            for (int s0 = 0; s0 < NS; s0 += 8) {
+                float a0[8], a1[8], bv[4][8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int p = 4 * (s0 + j) + lq;
+                    const bool in = s0 + j < NS;
+                    const int pc = in ? p : 0;
+                    const int oy = pc / G::OW, ox = pc - oy * G::OW;
+                    const int pof = (oy * G::S) * G::W + ox * G::S;
+                    a0[j] = in ? da[buf][pc * DS + li] : 0.f;
+                    a1[j] = in ? da[buf][pc * DS + 16 + li] : 0.f;
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) bv[nt][j] = in && p < P ? fr[buf][pof + boff[nt]] : 0.f;
+                }
+                const bf16x8 f0 = bf16_frag(a0), f1 = bf16_frag(a1);
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    const bf16x8 fb = bf16_frag(bv[nt]);
+                    acc[0][nt] = mfma16_bf16(f0, fb, acc[0][nt]);
+                    acc[1][nt] = mfma16_bf16(f1, fb, acc[1][nt]);
+                }
+            }
+        } else
         for (int s = 0; s < UPP / 4; ++s) {
             const int p = 4 * s + lq;                         // this lane's position of the k-step
             const int oy = p / G::OW, ox = p - oy * G::OW;
@@ -345,7 +392,7 @@ struct CN {
     static_assert((S * CS) % 64 == 8 && C % 16 == 0, "padding / channel grouping");
 };
 
-template <class G>
+template <class G, bool BF = false>
 __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, int R, const float *__restrict__ Wt,
                                                   const float *__restrict__ bias, float *__restrict__ out)
 {
@@ -398,6 +445,28 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
     f32x4 acc[G::MT];
 #pragma unroll
     for (int t = 0; t < G::MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BF) {
+        // GS_HP_BF16: groups g, g + 1 as one 16x16x32 bf16 MFMA (element j < 4: channel 4q + j of
+        // group g, j >= 4: of group g + 1 — the same k order in both operands)
+        static_assert(G::NG % 2 == 0, "bf16: group pairs");
+        constexpr int CG = G::C / 16;
+        auto goff = [&](int g) {
+            const int tap = g / CG, cb = (g - tap * CG) * 16;
+            const int ky = tap / G::K, kx = tap - ky * G::K;
+            return (ky * G::W + kx) * G::CS + cb;
+        };
+#pragma unroll
+        for (int gp = 0; gp < G::NG / 2; ++gp) {
+            const bf16x8 bw = bf16_frag(b[2 * gp], b[2 * gp + 1]);
+            const int o0 = goff(2 * gp), o1 = goff(2 * gp + 1);
+#pragma unroll
+            for (int t = 0; t < G::MT; ++t) {
+                const bf16x8 a = bf16_frag(*reinterpret_cast<const float4 *>(xs + abase[t] + o0),
+                                           *reinterpret_cast<const float4 *>(xs + abase[t] + o1));
+                acc[t] = mfma16_bf16(a, bw, acc[t]);
+            }
+        }
+    } else
 #pragma unroll
     for (int g = 0; g < G::NG; ++g) {
         constexpr int CG = G::C / 16;
@@ -460,7 +529,7 @@ struct CD {
     static_assert(H % S == 0 && W % S == 0 && K % S == 0 && NTHR <= 512 && CW % 16 == 0, "shape");
 };
 
-template <class G>
+template <class G, bool BF = false>
 __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict__ dY, const float *__restrict__ act, int R,
                                                     const float *__restrict__ Wt, float *__restrict__ dX)
 {
@@ -532,6 +601,29 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
     for (int t = 0; t < G::MT; ++t)
 #pragma unroll
         for (int nt = 0; nt < G::NT; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BF) {
+        // GS_HP_BF16: groups g, g + 1 as one 16x16x32 bf16 MFMA (same k order in both operands)
+        static_assert(G::NGRP % 2 == 0, "bf16: group pairs");
+        auto goff = [&](int g) {
+            const int tap = g / (G::CO / 16), cb = (g - tap * (G::CO / 16)) * 16;
+            const int dky = tap / G::KT, dkx = tap - dky * G::KT;
+            return -(dky * G::PW + dkx) * G::CS + cb;
+        };
+#pragma unroll
+        for (int gp = 0; gp < G::NGRP / 2; ++gp) {
+            const int o0 = goff(2 * gp), o1 = goff(2 * gp + 1);
+            bf16x8 bw[G::NT];
+#pragma unroll
+            for (int nt = 0; nt < G::NT; ++nt) bw[nt] = bf16_frag(b[2 * gp][nt], b[2 * gp + 1][nt]);
+#pragma unroll
+            for (int t = 0; t < G::MT; ++t) {
+                const bf16x8 a = bf16_frag(*reinterpret_cast<const float4 *>(ys + abase[t] + o0),
+                                           *reinterpret_cast<const float4 *>(ys + abase[t] + o1));
+#pragma unroll
+                for (int nt = 0; nt < G::NT; ++nt) acc[t][nt] = mfma16_bf16(a, bw[nt], acc[t][nt]);
+            }
+        }
+    } else
 #pragma unroll
     for (int g = 0; g < G::NGRP; ++g) {
         const int tap = g / (G::CO / 16), cb = (g - tap * (G::CO / 16)) * 16;
@@ -583,7 +675,7 @@ struct WG2 {
     static_assert((G::S * CSX) % 32 == 16, "padding");
 };
 
-template <class G>
+template <class G, bool BF = false>
 __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in, const float *__restrict__ dY, int R,
                                                     float *__restrict__ parts)
 {
@@ -649,6 +741,38 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
             const int co = tid & 63, grp = tid >> 6;
             for (int p = grp; p < G::OHW; p += 4) db += ds[p * X::DS + co];
         }
+        if constexpr (BF) {
+            // GS_HP_BF16: 8 k-steps per 16x16x32 bf16 MFMA (element j of lane quarter q: position
+            // 4 (s0 + j) + q in both operands; positions past OHW are zeros)
+            constexpr int NS = X::PP / 4;
+            for (int s0 = 0; s0 < NS; s0 += 8) {
+                bf16x8 fa[4];
+                float bv[X::NTW][8];
+                {
+                    float a[4][8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int p = 4 * (s0 + j) + lq;
+                        const bool ok = s0 + j < NS && p < G::OHW;
+                        const int pc = ok ? p : 0;
+                        const int oy = pc / G::OW, ox = pc - oy * G::OW;
+                        const int pof = (oy * G::S * G::W + ox * G::S) * X::CSX;
+#pragma unroll
+                        for (int mt = 0; mt < 4; ++mt) a[mt][j] = ok ? ds[pc * X::DS + 16 * mt + li] : 0.f;
+#pragma unroll
+                        for (int nt = 0; nt < X::NTW; ++nt) bv[nt][j] = ok ? xs[pof + boff[nt]] : 0.f;
+                    }
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt) fa[mt] = bf16_frag(a[mt]);
+                }
+#pragma unroll
+                for (int nt = 0; nt < X::NTW; ++nt) {
+                    const bf16x8 fb = bf16_frag(bv[nt]);
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = mfma16_bf16(fa[mt], fb, acc[mt][nt]);
+                }
+            }
+        } else
 #pragma unroll 3
         for (int s = 0; s < X::PP / 4; ++s) {
             const int p = 4 * s + lq;
@@ -694,7 +818,11 @@ int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, 
                   const float *b1, float *out)
 {
     GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
-    hipLaunchKernelGGL(k_conv1_fwd<C1_84>, dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1, out);
+    if (cnn_bf16())
+        hipLaunchKernelGGL((k_conv1_fwd<C1_84, true>), dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1,
+                           out);
+    else
+        hipLaunchKernelGGL(k_conv1_fwd<C1_84>, dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1, out);
     GS_LAUNCH_CHECK("k_conv1_fwd");
     return GS_OK;
 }
@@ -706,7 +834,11 @@ int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx
 {
     GS_REQUIRE(R > 0 && obs && dA && parts && dW1 && db1, "conv1_lds_wgrad: bad argument");
     constexpr int n = C1_84::CO * C1_84::KK, stride = n + C1_84::CO;
-    hipLaunchKernelGGL(k_conv1_wgrad<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
+    if (cnn_bf16())
+        hipLaunchKernelGGL((k_conv1_wgrad<C1_84, true>), dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA,
+                           parts);
+    else
+        hipLaunchKernelGGL(k_conv1_wgrad<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
     GS_LAUNCH_CHECK("k_conv1_wgrad");
     if (db1 == dW1 + n) {      // the flat layout keeps conv1's bias right after its weight: one sum
         hipLaunchKernelGGL(k_sum_partials, dim3((stride + 63) / 64), dim3(256), 0, s, parts, kConv1WgradWG,
@@ -730,12 +862,15 @@ bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cou
 int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float *Wt, const float *bias, float *out)
 {
     GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
+    const bool bf = cnn_bf16();
     if (layer == 2) {
-        hipLaunchKernelGGL(k_conv_fwd<C2_84>, dim3((unsigned)((R + C2_84::SPB - 1) / C2_84::SPB)), dim3(256), 0, s, in,
-                           R, Wt, bias, out);
+        const dim3 grid((unsigned)((R + C2_84::SPB - 1) / C2_84::SPB));
+        if (bf) hipLaunchKernelGGL((k_conv_fwd<C2_84, true>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        else hipLaunchKernelGGL(k_conv_fwd<C2_84>, grid, dim3(256), 0, s, in, R, Wt, bias, out);
     } else {
-        hipLaunchKernelGGL(k_conv_fwd<C3_84>, dim3((unsigned)((R + C3_84::SPB - 1) / C3_84::SPB)), dim3(256), 0, s, in,
-                           R, Wt, bias, out);
+        const dim3 grid((unsigned)((R + C3_84::SPB - 1) / C3_84::SPB));
+        if (bf) hipLaunchKernelGGL((k_conv_fwd<C3_84, true>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        else hipLaunchKernelGGL(k_conv_fwd<C3_84>, grid, dim3(256), 0, s, in, R, Wt, bias, out);
     }
     GS_LAUNCH_CHECK("k_conv_fwd");
     return GS_OK;
@@ -744,12 +879,15 @@ int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float
 int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX)
 {
     GS_REQUIRE(R > 0 && dY && act && Wt && dX, "conv23_lds_dgrad: bad argument");
+    const bool bf = cnn_bf16();
     if (layer == 2) {
-        hipLaunchKernelGGL(k_conv_dgrad<D2_84>, dim3((unsigned)((R + D2_84::SPB - 1) / D2_84::SPB)), dim3(D2_84::NTHR), 0, s,
-                           dY, act, R, Wt, dX);
+        const dim3 grid((unsigned)((R + D2_84::SPB - 1) / D2_84::SPB));
+        if (bf) hipLaunchKernelGGL((k_conv_dgrad<D2_84, true>), grid, dim3(D2_84::NTHR), 0, s, dY, act, R, Wt, dX);
+        else hipLaunchKernelGGL(k_conv_dgrad<D2_84>, grid, dim3(D2_84::NTHR), 0, s, dY, act, R, Wt, dX);
     } else {
-        hipLaunchKernelGGL(k_conv_dgrad<D3_84>, dim3((unsigned)((R + D3_84::SPB - 1) / D3_84::SPB)), dim3(D3_84::NTHR), 0, s,
-                           dY, act, R, Wt, dX);
+        const dim3 grid((unsigned)((R + D3_84::SPB - 1) / D3_84::SPB));
+        if (bf) hipLaunchKernelGGL((k_conv_dgrad<D3_84, true>), grid, dim3(D3_84::NTHR), 0, s, dY, act, R, Wt, dX);
+        else hipLaunchKernelGGL(k_conv_dgrad<D3_84>, grid, dim3(D3_84::NTHR), 0, s, dY, act, R, Wt, dX);
     }
     GS_LAUNCH_CHECK("k_conv_dgrad");
     return GS_OK;
@@ -761,12 +899,15 @@ int conv23_lds_wgrad(hipStream_t s, int layer, int R, const float *in, const flo
     GS_REQUIRE(R > 0 && in && dY && parts && dW && db, "conv23_lds_wgrad: bad argument");
     const int nwg = kConvWgradWG;
     int KK;
+    const bool bf = cnn_bf16();
     if (layer == 2) {
         KK = C2_84::KK;
-        hipLaunchKernelGGL(k_conv_wgrad<C2_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+        if (bf) hipLaunchKernelGGL((k_conv_wgrad<C2_84, true>), dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+        else hipLaunchKernelGGL(k_conv_wgrad<C2_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
     } else {
         KK = C3_84::KK;
-        hipLaunchKernelGGL(k_conv_wgrad<C3_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+        if (bf) hipLaunchKernelGGL((k_conv_wgrad<C3_84, true>), dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+        else hipLaunchKernelGGL(k_conv_wgrad<C3_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
     }
     GS_LAUNCH_CHECK("k_conv_wgrad");
     return sum_parts_wb(s, parts, nwg, (int64_t)64 * (KK + 1), 64, KK, dW, db);

@@ -15,6 +15,12 @@
 #include "gs_gemm.h"
 
 namespace gs {
+
+static thread_local bool t_bf16 = false;
+bool cnn_bf16() { return t_bf16; }
+Bf16Scope::Bf16Scope(bool on) : prev(t_bf16) { t_bf16 = on; }
+Bf16Scope::~Bf16Scope() { t_bf16 = prev; }
+
 namespace {
 
 constexpr int BK = 16;
@@ -125,7 +131,7 @@ struct U8PatchOp {
     }
 };
 
-template <int BM, int BN, int WGM, class AOp, bool A_K, class BOp, bool B_K, bool ASUM = false>
+template <int BM, int BN, int WGM, class AOp, bool A_K, class BOp, bool B_K, bool ASUM = false, bool BF = false>
 __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, int K, int kchunk,
                                               float *__restrict__ C, int ldc, int64_t sC, float beta,
                                               const float *__restrict__ bias, int relu)
@@ -223,17 +229,43 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
 #pragma unroll
             for (int k = 0; k < BK; ++k) asum += As[buf][k][tid];
         }
+        if constexpr (BF) {
+            // GS_HP_BF16: the whole 16-deep K tile as one v_mfma_f32_32x32x16_bf16 per sub-tile;
+            // lane (r = l & 31, h = l >> 5) holds A[r][8 h + j], B[8 h + j][r] (the same LDS
+            // reads as the fp32 form's eight K = 2 steps, one MFMA instead of eight)
+            bf16x8 a[TM], b[TN];
 #pragma unroll
-        for (int k2 = 0; k2 < BK; k2 += 2) {
-            float a[TM], b[TN];
+            for (int i = 0; i < TM; ++i) {
+                float v[8];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) a[i] = As[buf][k2 + lh][wm + 32 * i + l32];
+                for (int j = 0; j < 8; ++j) v[j] = As[buf][8 * lh + j][wm + 32 * i + l32];
+                a[i] = bf16_frag(v);
+            }
 #pragma unroll
-            for (int j = 0; j < TN; ++j) b[j] = Bs[buf][k2 + lh][wn + 32 * j + l32];
+            for (int jn = 0; jn < TN; ++jn) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = Bs[buf][8 * lh + j][wn + 32 * jn + l32];
+                b[jn] = bf16_frag(v);
+            }
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x2(a[i], b[j], acc[i][j]);
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int k2 = 0; k2 < BK; k2 += 2) {
+                float a[TM], b[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) a[i] = As[buf][k2 + lh][wm + 32 * i + l32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) b[j] = Bs[buf][k2 + lh][wn + 32 * j + l32];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x2(a[i], b[j], acc[i][j]);
+            }
         }
         if (kt + 1 < nk) store(buf ^ 1);
         __syncthreads();
@@ -267,8 +299,12 @@ int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int6
     const int64_t per = (K + splits - 1) / splits;
     const int64_t kchunk = (per + BK - 1) / BK * BK;
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
-    hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K, ASUM>), grid, dim3(256), 0, s, a, b, (int)M, (int)N, (int)K,
-                       (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0);
+    if (cnn_bf16())
+        hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K, ASUM, true>), grid, dim3(256), 0, s, a, b, (int)M,
+                           (int)N, (int)K, (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0);
+    else
+        hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K, ASUM>), grid, dim3(256), 0, s, a, b, (int)M, (int)N,
+                           (int)K, (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0);
     GS_LAUNCH_CHECK("k_gemm");
     return GS_OK;
 }

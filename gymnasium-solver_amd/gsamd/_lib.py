@@ -37,7 +37,10 @@ class PPOHparams(ctypes.Structure):
     _fields_ = [("clip_range", ctypes.c_float), ("clip_range_vf", ctypes.c_float), ("vf_coef", ctypes.c_float),
                 ("ent_coef", ctypes.c_float), ("max_grad_norm", ctypes.c_float), ("lr", ctypes.c_float),
                 ("adam_beta1", ctypes.c_float), ("adam_beta2", ctypes.c_float), ("adam_eps", ctypes.c_float),
-                ("target_kl", ctypes.c_float), ("normalize_adv", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("target_kl", ctypes.c_float), ("normalize_adv", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+GS_HP_BF16 = 1      # include/gsamd.h: bf16 MFMA operands in the NatureCNN update
 
 
 class RolloutView(ctypes.Structure):

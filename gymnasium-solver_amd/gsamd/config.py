@@ -79,6 +79,9 @@ class PPOConfig:
     #   "global" every rank takes its share of the reference's global minibatches (the single-GPU
     #            math on G GPUs: global sampler, normalisation and KL stop; gs_ppo_update_global)
     dp_mode: str = "local"
+    # MFMA operand precision of the NatureCNN update (include/gsamd.h GS_HP_BF16): "fp32" (the
+    # parity path, default) or "bf16" (bf16 operands, fp32 accumulation / parameters / Adam)
+    precision: str = "fp32"
     # {param: {schedule, start_value, end_value, start, end, warmup}} (gsamd.schedules)
     schedules: Dict[str, Dict[str, Any]] = field(default_factory=dict)
 
@@ -131,6 +134,10 @@ class PPOConfig:
                              f"rollout_size={rollout}, batch_size={self.batch_size}.")
         if self.normalize_advantages not in ("batch", "rollout", "off", False, None, ""):
             raise ValueError("normalize_advantages must be 'rollout', 'batch', or 'off'.")
+        if self.precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {self.precision!r}")
+        if self.precision == "bf16" and self.obs_type != "rgb":
+            raise ValueError("precision 'bf16' is implemented for the NatureCNN (rgb) update; the MLP path is fp32")
         if self.dp_mode not in ("local", "global"):
             raise ValueError(f"dp_mode must be 'local' or 'global', got {self.dp_mode!r}")
         if str(self.env_dynamics or "auto") not in ENV_DYNAMICS:

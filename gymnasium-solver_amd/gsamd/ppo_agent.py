@@ -24,7 +24,7 @@ import torch
 
 import ctypes
 
-from ._lib import GS_NUM_METRICS, M, PPOGlobal, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
+from ._lib import GS_HP_BF16, GS_NUM_METRICS, M, PPOGlobal, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
 from .atari_env import DeviceAtariVecEnv
 from .config import device_env_kind
 from .cnn import DeviceCNNActorCritic
@@ -327,9 +327,10 @@ class DevicePPOAgent:
     def hparams(self) -> PPOHparams:
         c = self.config
         tkl = c.target_kl if c.target_kl is not None else 0.0
+        flags = GS_HP_BF16 if str(getattr(c, "precision", "fp32")) == "bf16" else 0
         return PPOHparams(float(self.clip_range), float(self.clip_range_vf), float(self.vf_coef), float(self.ent_coef),
                           float(c.max_grad_norm if c.max_grad_norm is not None else 0.0), float(self.policy_lr),
-                          0.9, 0.999, 1e-8, float(tkl), 1 if c.normalize_advantages == "batch" else 0, 0)
+                          0.9, 0.999, 1e-8, float(tkl), 1 if c.normalize_advantages == "batch" else 0, flags)
 
     # ---- Lightning-style hooks ------------------------------------------------------------
     def train_dataloader(self):

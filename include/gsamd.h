@@ -163,8 +163,12 @@ typedef struct gs_ppo_hparams {
     float adam_eps;
     float target_kl;          /* <= 0: None */
     int32_t normalize_adv;    /* 1 = "batch" (utils/torch.py:97-99), 0 = off */
-    int32_t pad;
+    int32_t flags;            /* GS_HP_* bits; 0 = the fp32 parity path */
 } gs_ppo_hparams;
+/* bf16 MFMA operands (fp32 accumulation, fp32 parameters / Adam / loss) in the NatureCNN update's
+ * convolutions and GEMMs — a performance mode beside the fp32 one (SURVEY.md Appendix A
+ * "Precision modes"); the MLP chain ignores it. */
+#define GS_HP_BF16 1
 
 /* Per-minibatch metric record written by the loss kernel (floats, GS_NUM_METRICS each).
  * KL early stop (agents/base_agent.py:330-366, sticky): the minibatch whose approx_kl exceeds

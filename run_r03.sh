@@ -14,7 +14,9 @@ fi
 step bench timeout -k 10 400 python bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err && cat $O/bench.json &&
 step cnn-stats timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/cnn_stats -o cnn -- python tools/cnn_kernel_run.py > $O/cnn_stats.log 2>&1 &&
 step cnn-fetch timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/cnn_fetch -o fetch -- python tools/cnn_kernel_run.py > $O/cnn_fetch.log 2>&1 &&
-step cnn-write timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/cnn_write -o write -- python tools/cnn_kernel_run.py > $O/cnn_write.log 2>&1
+step cnn-write timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/cnn_write -o write -- python tools/cnn_kernel_run.py > $O/cnn_write.log 2>&1 &&
+step c4-f32 timeout -k 10 400 python bench.py --workload C4 --steps 1 --warmup 1 --cpu-minibatches 0 > $O/bench_c4.json 2> $O/bench_c4.err && cat $O/bench_c4.json &&
+step c4-bf16 timeout -k 10 400 python bench.py --workload C4 --steps 1 --warmup 1 --cpu-minibatches 0 --dtype bf16 > $O/bench_c4_bf16.json 2> $O/bench_c4_bf16.err && cat $O/bench_c4_bf16.json
 rc=$?
 find $O -name "*.csv" | xargs ls -la
 exit $rc

@@ -182,3 +182,44 @@ def test_cnn_update_local_comm_equals_no_comm(cuda, transport):
     assert np.isfinite(out[0][0]).all()
     for name, x, y in zip(("params", "adam_m", "adam_v", "losses"), out[0], out[1]):
         assert np.array_equal(np.ascontiguousarray(x).view(np.uint8), np.ascontiguousarray(y).view(np.uint8)), name
+
+
+def test_cnn_bf16_mode_deviation_bounded(cuda):
+    """The bf16 performance mode (GS_HP_BF16: bf16 MFMA operands in every convolution / GEMM of
+    the NatureCNN update, fp32 accumulation, parameters, loss and Adam) run
+    beside the fp32 parity path from the same state on the same rollout and sampler order: the
+    first minibatch's gradient keeps its direction (cosine > 0.999, relative L2 < 3e-2) and the
+    per-minibatch losses of one update (C4 shapes, B = 1024, 8 minibatches) stay within 2e-3 of the
+    fp32 ones relative to their scale.  The fp32 path stays the default and the parity reference."""
+    from gsamd._lib import GS_HP_BF16, check, lib, ptr, stream_handle
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(42)
+    cfg = load_config("ALE-Pong-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=16, n_steps=128,
+                                                               n_epochs=4))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
+    coll = agent.get_rollout_collector("train")
+    coll.collect()
+    idx = agent.prefetcher.upload(0)
+    pm = agent.policy_model
+    state = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v)]
+    out = {}
+    for name, n in (("fp32", 1), ("bf16", 1), ("fp32", agent.n_minibatches), ("bf16", agent.n_minibatches)):
+        for t, s0 in zip((pm.params, agent.adam_m, agent.adam_v), state):
+            t.copy_(s0)
+        hp = agent.hparams()
+        hp.flags = GS_HP_BF16 if name == "bf16" else 0
+        check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
+                                    hp, coll.buffer.view(), ptr(idx), agent.batch_size, n, 0, ptr(agent.metrics_buf),
+                                    ptr(agent.stop_flag), ptr(agent.workspace), None, stream_handle()),
+              "gs_cnn_ppo_update")
+        torch.cuda.synchronize()
+        out[(name, n)] = (agent.grads.cpu().numpy().astype(np.float64), agent.metrics_buf[:n, 0].cpu().numpy())
+    g32, g16 = out[("fp32", 1)][0], out[("bf16", 1)][0]
+    cos = float(g32 @ g16 / (np.linalg.norm(g32) * np.linalg.norm(g16)))
+    rel = float(np.linalg.norm(g16 - g32) / np.linalg.norm(g32))
+    assert cos > 0.999 and rel < 3e-2 and rel > 0.0, (cos, rel)
+    l32, l16 = out[("fp32", agent.n_minibatches)][1], out[("bf16", agent.n_minibatches)][1]
+    assert agent.n_minibatches == 8 and np.isfinite(l16).all()
+    dev = np.abs(l16.astype(np.float64) - l32) / max(1.0, float(np.abs(l32).max()))
+    assert dev.max() < 2e-3, dev
