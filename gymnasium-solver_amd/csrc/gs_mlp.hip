@@ -2464,16 +2464,6 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
         s_coef = clip_coef(total, aa);
         if (blockIdx.x == 0 && metrics) metrics[GS_M_GRAD_NORM] = total;
     }
-    if (metrics && blockIdx.x == gridDim.x - 1) {   // per-component norms (utils/models.py:196-230)
-        double hq[2] = {0.0, 0.0};
-        const int nhg = (L.A + 1) * (L.H2 + 1);
-        for (int u = tid; u < nhg; u += 256) {
-            bool val;
-            const double g = (double)G[head_grad_offset(L, u, &val)];
-            hq[val ? 1 : 0] += g * g;
-        }
-        store_component_norms(hq, tt[0], aa.grad_scale, metrics, sred);
-    }
     __syncthreads();
     const float coef = s_coef * aa.grad_scale;
     const float neg_step = aa.sched ? aa.sched[2 * (aa.sched_idx + kb)] : aa.neg_step_size;
@@ -2667,10 +2657,48 @@ int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, 
     });
 }
 
+// Per-component pre-clip gradient norms of the step k_clip_adam is about to take (utils/models.py:
+// 196-230).  Its own kernel: k_clip_adam's workgroups overwrite G with the clipped gradients, so a
+// workgroup of it cannot read the raw head gradients of another one race-free.  Total squared norm
+// from the same slots + dW1|db1 partials k_clip_adam folds (double sums; order-only differences).
+__global__ __launch_bounds__(256) void k_component_norms(Layout L, const float *__restrict__ G,
+                                                         const float *__restrict__ part1,
+                                                         const float *__restrict__ sumsq, int n_slots, int nrb,
+                                                         float gscale, const int64_t *__restrict__ step_base,
+                                                         float *__restrict__ metrics,
+                                                         const int32_t *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    __shared__ double sred[2 * 272];
+    const int tid = threadIdx.x;
+    const int64_t n1 = (int64_t)L.H1 * (L.D + 1);
+    double tt[1] = {0.0};
+    for (int s0 = tid; s0 < n_slots; s0 += 256) tt[0] += (double)sumsq[s0];
+    for (int64_t u = tid; u < n1 && nrb > 0; u += 256) {
+        float g = 0.0f;
+        for (int rb = 0; rb < nrb; ++rb) g += part1[(int64_t)rb * n1 + u];
+        tt[0] += (double)g * (double)g;
+    }
+    block_reduce<1>(tt, sred);
+    double hq[2] = {0.0, 0.0};
+    const int nhg = (L.A + 1) * (L.H2 + 1);
+    for (int u = tid; u < nhg; u += 256) {
+        bool val;
+        const double g = (double)G[head_grad_offset(L, u, &val)];
+        hq[val ? 1 : 0] += g * g;
+    }
+    store_component_norms(hq, tt[0], gscale, metrics + (step_base ? *step_base : 0) * GS_NUM_METRICS, sred);
+}
+
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
                      const float *sumsq, const AdamArgs &aa_in, float *metrics, const int32_t *stop, hipStream_t s)
 {
     AdamArgs aa = aa_in;
+    if (metrics) {
+        hipLaunchKernelGGL(k_component_norms, dim3(1), dim3(256), 0, s, L, G, part1, sumsq, aa.n_slots, aa.nrb,
+                           aa.grad_scale, aa.step_base, metrics, stop);
+        GS_LAUNCH_CHECK("k_component_norms");
+    }
     const size_t stage = sizeof(float) * (round4(aa.n_slots) + (size_t)aa.nrb * L.H1 * (L.D + 1));
     aa.stage_lds = stage <= 65536 ? 1 : 0;
     const unsigned nblk = (unsigned)((L.P + 1023) / 1024);

@@ -78,13 +78,14 @@ def test_cnn_update_step_vs_oracle_and_reference(golden, cuda, tag):
                       ("opt/ppo/clip_fraction", 4), ("opt/ppo/approx_kl", 8)):
         assert abs(rec[slot] - ref[key]) < 1e-5 * max(1.0, abs(ref[key])), key
     # pre-clip gradient norms per component, as the reference's compute_grad_norms records them
-    # (utils/models.py:196-230: all, cnn, mlp, policy_head, value_head)
+    # (utils/models.py:196-230: all, cnn, mlp, policy_head, value_head).  1e-4: the reference sums
+    # 1.7 M fp32 squares in torch's order (rec[12] meets the f64 oracle's norm at 1e-5 above)
     from gsamd._lib import M
     gn = dict(zip([str(x) for x in z[f"{tag}/grad_norm_names"]], z[f"{tag}/grad_norm_values"]))
     for key, slot in (("opt/grads/norm/all", "grad_norm"), ("opt/grads/norm/cnn", "gn_backbone"),
                       ("opt/grads/norm/mlp", "gn_mlp"), ("opt/grads/norm/policy_head", "gn_policy_head"),
                       ("opt/grads/norm/value_head", "gn_value_head")):
-        np.testing.assert_allclose(rec[M[slot]], gn[key], rtol=1e-5, err_msg=key)
+        np.testing.assert_allclose(rec[M[slot]], gn[key], rtol=1e-4, err_msg=key)
 
 
 @pytest.mark.parametrize("tag", list(CASES))
