@@ -48,20 +48,70 @@ def unflatten(flat, shapes):
     return out
 
 
-def forward(params: dict, obs_u8, valid=None, spec=NATURE):
-    """-> (masked logits (B,A) with -inf for invalid actions, value (B,), hidden (B,512))."""
+def _bf(t):
+    """round-to-nearest-even to bf16 and back (v_cvt_pk_bf16_f32)."""
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+class _Bf16Conv(torch.autograd.Function):
+    """conv2d with bf16-rounded operands and fp32 accumulation in all three products (forward,
+    input gradient, weight gradient); the bias gradient sums the unrounded output gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride):
+        ctx.save_for_backward(x, w)
+        ctx.stride = stride
+        return F.conv2d(_bf(x), _bf(w), b, stride=stride)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        g = _bf(gy)
+        dx = torch.nn.grad.conv2d_input(x.shape, _bf(w), g, stride=ctx.stride) if ctx.needs_input_grad[0] else None
+        dw = torch.nn.grad.conv2d_weight(_bf(x), w.shape, g, stride=ctx.stride)
+        return dx, dw, gy.sum((0, 2, 3)), None
+
+
+class _Bf16Linear(torch.autograd.Function):
+    """linear with bf16-rounded operands; round_dx=False keeps the input gradient in fp32 (the
+    heads' dh, a plain fp32 kernel on the device)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, round_dx):
+        ctx.save_for_backward(x, w)
+        ctx.round_dx = round_dx
+        y = _bf(x) @ _bf(w).t()
+        return y + b if b is not None else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        g = _bf(gy)
+        dx = (g @ _bf(w)) if ctx.round_dx else (gy @ w)
+        return dx, g.t() @ _bf(x), gy.sum(0), None
+
+
+def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False):
+    """-> (masked logits (B,A) with -inf for invalid actions, value (B,), hidden (B,512)).
+
+    bf16=True: the device's GS_HP_BF16 mode (SURVEY.md Appendix A "Precision modes") — every
+    convolution / GEMM product takes bf16-rounded operands with fp32 accumulation, at the points
+    the HIP kernels round them (u8/255 frames, activations, weights, output gradients); biases,
+    ReLU, the loss, the heads' input gradient and Adam stay fp32."""
     x = torch.as_tensor(obs_u8)
     x = x.to(torch.float32) / 255.0 if x.dtype == torch.uint8 else x.to(torch.float32)
+    conv = (lambda x, w, b, s: _Bf16Conv.apply(x, w, b, s)) if bf16 else (lambda x, w, b, s: F.conv2d(x, w, b, stride=s))
+    lin = (lambda x, w, b, rd=True: _Bf16Linear.apply(x, w, b, rd)) if bf16 else (lambda x, w, b, rd=True: F.linear(x, w, b))
     for i, s in enumerate(spec["strides"]):
-        x = F.relu(F.conv2d(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], stride=s))
+        x = F.relu(conv(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], s))
     x = x.flatten(1)
-    h = F.relu(F.linear(x, params["mlp.0.weight"], params["mlp.0.bias"]))
-    logits = F.linear(h, params["policy_head.weight"], params["policy_head.bias"])
+    h = F.relu(lin(x, params["mlp.0.weight"], params["mlp.0.bias"]))
+    logits = lin(h, params["policy_head.weight"], params["policy_head.bias"], False)
     if valid is not None:
         mask = torch.ones_like(logits, dtype=torch.bool)
         mask[:, list(valid)] = False
         logits = logits.masked_fill(mask, float("-inf"))
-    value = F.linear(h, params["value_head.weight"], params["value_head.bias"]).squeeze(-1)
+    value = lin(h, params["value_head.weight"], params["value_head.bias"], False).squeeze(-1)
     return logits, value, h
 
 
@@ -80,8 +130,8 @@ def dist_terms(logits, actions, valid):
 
 
 def loss_and_grads(flat, shapes, obs_u8, actions, old_logp, old_values, adv, ret, *, valid, clip, clip_vf,
-                   vf_coef, ent_coef, normalize="batch"):
-    """(loss, metrics, flat grads, logits, values) of losses_for_batch + backward."""
+                   vf_coef, ent_coef, normalize="batch", bf16=False):
+    """(loss, metrics, flat grads, logits, values) of losses_for_batch + backward (bf16: see forward)."""
     params = {k: v.clone().requires_grad_(True) for k, v in unflatten(flat, shapes).items()}
     adv = torch.as_tensor(np.asarray(adv, np.float32))
     old_logp = torch.as_tensor(np.asarray(old_logp, np.float32))
@@ -94,7 +144,7 @@ def loss_and_grads(flat, shapes, obs_u8, actions, old_logp, old_values, adv, ret
         metrics["roll/adv/norm/std"] = float(adv_n.std())
     else:
         adv_n = adv
-    logits, value, _ = forward(params, obs_u8, valid)
+    logits, value, _ = forward(params, obs_u8, valid, bf16=bf16)
     new_lp, H = dist_terms(logits, actions, valid)
     ratio = torch.exp(new_lp - old_logp)
     pl = -torch.min(adv_n * ratio, adv_n * torch.clamp(ratio, 1.0 - clip, 1.0 + clip)).mean()
