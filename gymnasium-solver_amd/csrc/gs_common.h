@@ -160,6 +160,9 @@ struct FusedFwd {
     const int32_t *fa;         // (n, B) actions
     const float *folp, *fov, *fadv, *fret;   // (n, B) old logp, old value, normalised adv, return
     double *mpart;             // (n, B/16, 14) per-row-block metric sums
+    float *headsq;             // (n, H2/16 + 1, 2) per role-C workgroup {policy, value} head-gradient
+                               // sums of squares (k_metrics_all: per-component gradient norms)
+    double *normsq;            // (n) the steps' squared total norms (AdamArgs::normsq)
     float *dz;                 // (B, A+1) dLoss/dlogits | dLoss/dvalue of the current step
     const int64_t *step_base;
     int k_local;
@@ -198,6 +201,10 @@ struct AdamArgs {
     int sched_idx;
     const int64_t *step_base;   // graph chunk replay: added to sched_idx and the metrics record
     int stage_lds;          // set by the launcher: stage slots + partials through LDS
+    // fused update: the step's squared pre-clip norm x grad_scale^2 in double, for k_metrics_all's
+    // per-component norms.  Lagged forward: the update's array (indexed by the applied step);
+    // k_clip_adam: offset to its step like its metrics record (+ *step_base in a replay)
+    double *normsq;
 };
 
 // Lagged optimizer step of the single-GPU fused chain (gs_ppo_update): the forward of
@@ -286,8 +293,13 @@ int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, 
 // whether k_bwd's in-kernel exchange covers this shape (grid and per-workgroup slot limits, and
 // co-residency with `colocated` ranks sharing the GPU)
 bool bwd_xchg_fits(const Layout &L, int64_t B, int colocated = 1);
+// comp_norms: also record the step's per-component gradient norms (k_component_norms); the fused
+// update leaves them to k_metrics_all (role C's per-step head sums)
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
-                     const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s);
+                     const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s,
+                     bool comp_norms = true);
+// fused update, exchange launched behind k_bwd: step ff.k_local's head record from the exchanged G
+int launch_head_sq(const Layout &L, const float *G, float scale, const FusedFwd &ff, hipStream_t s);
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);
 int launch_sumsq_flat(const float *G, int64_t n, float *out, int nblocks, hipStream_t s);
 

@@ -386,18 +386,6 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         float sl[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) sl[j] = nrm ? ld1(af.sumsq, min(tid + 256 * j, aa.n_slots - 1)) : 0.0f;
-        // the grid's last workgroup (never a parameter owner while the grid has more than one row
-        // block) also records the per-component gradient norms: its head gradients join the burst
-        constexpr int nhg = cA1 * Lc.H2 + cA1, NHG = (nhg + 255) / 256;
-        const bool diag = apply && af.metrics && cb == (int)gridDim.x - 1 && rb == (int)gridDim.y - 1;
-        float hg[NHG];
-        bool hval[NHG];
-#pragma unroll
-        for (int j = 0; j < NHG; ++j) {
-            hg[j] = 0.0f;
-            hval[j] = false;
-            if (diag && nrm) hg[j] = ld1(af.G, head_grad_offset(Lc, min(tid + 256 * j, nhg - 1), &hval[j]));
-        }
         // then the loads behind the graph replay's step base: this minibatch's x rows and step
         // k-1's schedule entries
         float xv = 0.0f;
@@ -452,15 +440,8 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             const float total = (float)sqrt(tt[0]) * aa.grad_scale;
             coef = clip_coef(total, aa) * aa.grad_scale;
             if (own1 && tid == 0 && af.metrics) af.metrics[kprev * GS_NUM_METRICS + GS_M_GRAD_NORM] = total;
-            if (diag) {
-                double hq[2] = {0.0, 0.0};
-#pragma unroll
-                for (int j = 0; j < NHG; ++j)
-                    if (nrm && tid + 256 * j < nhg) hq[hval[j] ? 1 : 0] += (double)hg[j] * (double)hg[j];
-                // scratch: red (1024 floats) and the h2 tile after it, both unused until phase 2
-                store_component_norms(hq, tt[0], aa.grad_scale, af.metrics + kprev * GS_NUM_METRICS,
-                                      reinterpret_cast<double *>(red));
-            }
+            if (own1 && tid == 0 && aa.normsq)
+                aa.normsq[kprev] = tt[0] * (double)aa.grad_scale * (double)aa.grad_scale;
         }
         GS_STAMP(1)
         // Adam on the owned parameters: new values to LDS / registers, and from row block 0 to the other set
@@ -1414,6 +1395,26 @@ __device__ __forceinline__ void block_sumsq_store(float v, float *slot, float *s
     if (threadIdx.x == 0) *slot = t[0];
 }
 
+// role C's sum-of-squares slot, and with a fused update's per-step head record (headsq != null)
+// the {policy head, value head} split of the same values for the per-component gradient norms
+// (utils/models.py:196-230; k_metrics_all turns them into the record).  The slot's sum is the
+// first of the reduced values, so it is the same sum in the same order as block_sumsq_store's.
+__device__ __forceinline__ void store_head_sums(float sq, float sqp, float sqv, float *slot, float *headsq,
+                                                int64_t o, float *sbuf)
+{
+    if (!headsq) {
+        block_sumsq_store(sq, slot, sbuf);
+        return;
+    }
+    float t[3] = {sq, sqp, sqv};
+    block_reduce<3>(t, sbuf);      // sbuf: 3 x 272 floats
+    if (threadIdx.x == 0) {
+        *slot = t[0];
+        headsq[o] = t[1];
+        headsq[o + 1] = t[2];
+    }
+}
+
 // The role-C workgroup that stores metric row group g (16 rows) of a minibatch of G groups: a
 // contiguous range of groups per workgroup
 __host__ __device__ inline int metric_owner(int g, int G, int nW) { return G <= nW ? g : (int)(((int64_t)g * nW) / G); }
@@ -1534,7 +1535,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
     const int64_t kstep = FUSED ? ff.k_local + (ff.step_base ? *ff.step_base : 0) : 0;
     if constexpr (FUSED) GS_SPAN_START(1, kstep)
     extern __shared__ float lds[];
-    __shared__ float sbuf[272];
+    __shared__ float sbuf[FUSED ? 3 * 272 : 272];    // fused: role C's {slot, policy, value} sums
     const Layout L = S::lay(Lrt);
     const int B = S::batch(Brt);
     const int D = L.D, H1 = L.H1, H2 = L.H2, A = L.A, A1 = A + 1;
@@ -2183,7 +2184,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         float *partC = dzs + Bp * A1;           // [A1*16][16]
         if (nb < sh.ncb) {
             const int nout = kTile * A1;
-            float sq = 0.0f;
+            float sq = 0.0f, sqp = 0.0f, sqv = 0.0f;     // all head weights / policy rows / value row
             if (A1 <= kTile) {
                 // dWh[a, n0+j] = sum_b dz[b, a] h2[b, n0+j] as one 16x16 MFMA tile (rows = actions,
                 // padded) with K = the batch split over the 4 waves; the wave partials are summed
@@ -2218,6 +2219,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 if (ok[0]) {
                     G[L.head_row(a) + n0 + i] = hv[0];
                     sq = hv[0] * hv[0];
+                    sqp = a < A ? sq : 0.0f;
+                    sqv = a == A ? sq : 0.0f;
                 }
             } else {
                 // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
@@ -2249,10 +2252,13 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     if (ok[j]) {
                         G[L.head_row(a) + n0 + i] = hv[j];
                         sq += hv[j] * hv[j];
+                        if (a == A) sqv += hv[j] * hv[j];
+                        else sqp += hv[j] * hv[j];
                     }
                 }
             }
-            block_sumsq_store(sq, sumsq + sh.nT + sh.ncb + nb, sbuf);
+            store_head_sums(sq, sqp, sqv, sumsq + sh.nT + sh.ncb + nb, FUSED ? ff.headsq : nullptr,
+                            (kstep * (sh.ncb + 1) + nb) * 2, sbuf);
         } else {
             // the extra block: head-bias gradients (sum of dz over the batch)
             for (int u = tid; u < A1 * 16; u += 256) {
@@ -2273,7 +2279,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 G[L.head_bias(tid)] = bv[0];
                 sqb = bv[0] * bv[0];
             }
-            block_sumsq_store(sqb, sumsq + sh.nT + 2 * sh.ncb, sbuf);
+            store_head_sums(sqb, tid < A ? sqb : 0.0f, tid == A ? sqb : 0.0f, sumsq + sh.nT + 2 * sh.ncb, FUSED ? ff.headsq : nullptr,
+                            (kstep * (sh.ncb + 1) + sh.ncb) * 2, sbuf);
         }
         GS_STAMP_END(1)
         if constexpr (FUSED) GS_SPAN_END(1, kstep)
@@ -2463,6 +2470,7 @@ __global__ __launch_bounds__(256) void k_clip_adam(float *__restrict__ Pm, Layou
         const float total = (float)sqrt(tot) * aa.grad_scale;
         s_coef = clip_coef(total, aa);
         if (blockIdx.x == 0 && metrics) metrics[GS_M_GRAD_NORM] = total;
+        if (blockIdx.x == 0 && aa.normsq) aa.normsq[kb] = tot * (double)aa.grad_scale * (double)aa.grad_scale;
     }
     __syncthreads();
     const float coef = s_coef * aa.grad_scale;
@@ -2691,10 +2699,11 @@ __global__ __launch_bounds__(256) void k_component_norms(Layout L, const float *
 }
 
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
-                     const float *sumsq, const AdamArgs &aa_in, float *metrics, const int32_t *stop, hipStream_t s)
+                     const float *sumsq, const AdamArgs &aa_in, float *metrics, const int32_t *stop, hipStream_t s,
+                     bool comp_norms)
 {
     AdamArgs aa = aa_in;
-    if (metrics) {
+    if (metrics && comp_norms) {
         hipLaunchKernelGGL(k_component_norms, dim3(1), dim3(256), 0, s, L, G, part1, sumsq, aa.n_slots, aa.nrb,
                            aa.grad_scale, aa.step_base, metrics, stop);
         GS_LAUNCH_CHECK("k_component_norms");
@@ -2824,7 +2833,8 @@ __global__ __launch_bounds__(256) void k_gather_all(const int32_t *__restrict__ 
 // thread per minibatch: the row-block sums (fixed order) -> the metrics record
 __global__ __launch_bounds__(256) void k_metrics_all(const double *__restrict__ mpart, int nrb, int64_t n, int B,
                                                      LossArgs la, float *__restrict__ metrics,
-                                                     const int32_t *__restrict__ stop)
+                                                     const float *__restrict__ headsq, int nhw,
+                                                     const double *__restrict__ normsq)
 {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
@@ -2834,11 +2844,57 @@ __global__ __launch_bounds__(256) void k_metrics_all(const double *__restrict__ 
     for (int rb = 0; rb < nrb; ++rb)
 #pragma unroll
         for (int q = 0; q < kNumSums; ++q) t[q] += mpart[(k * nrb + rb) * kNumSums + q];
-    write_metrics(t, (double)la.batch_rows, la, metrics + k * GS_NUM_METRICS, la.sums_out != nullptr);
+    float *rec = metrics + k * GS_NUM_METRICS;
+    write_metrics(t, (double)la.batch_rows, la, rec, la.sums_out != nullptr);
     if (la.sums_out)
 #pragma unroll
         for (int q = 0; q < kNumSums; ++q) la.sums_out[k * kNumSums + q] = t[q];
     (void)B;
+    if (headsq) {
+        // per-component pre-clip norms (utils/models.py:196-230): the heads from role C's per-step
+        // sums (the exchanged, scaled gradient's), the backbone as the rest of the recorded total
+        double hq[2] = {0.0, 0.0};
+        for (int w = 0; w < nhw; ++w) {
+            hq[0] += (double)headsq[(k * nhw + w) * 2];
+            hq[1] += (double)headsq[(k * nhw + w) * 2 + 1];
+        }
+        rec[GS_M_GN_POLICY_HEAD] = (float)sqrt(hq[0]);
+        rec[GS_M_GN_VALUE_HEAD] = (float)sqrt(hq[1]);
+        rec[GS_M_GN_BACKBONE] = (float)sqrt(fmax(0.0, normsq[k] - hq[0] - hq[1]));
+        rec[GS_M_GN_MLP] = 0.0f;
+    }
+}
+
+// After an exchange launched behind k_bwd (RCCL, or the xGMI kernel): step k's head record from
+// the exchanged gradient in G (role C's sums were of this rank's own gradient), x scale (1/world)
+__global__ __launch_bounds__(256) void k_head_sq(Layout L, const float *__restrict__ G, float scale,
+                                                 const int64_t *__restrict__ step_base, int64_t k_local,
+                                                 float *__restrict__ headsq)
+{
+    __shared__ double sred[2 * 272];
+    const int tid = threadIdx.x;
+    double hq[2] = {0.0, 0.0};
+    const int nhg = (L.A + 1) * (L.H2 + 1);
+    for (int u = tid; u < nhg; u += 256) {
+        bool val;
+        const double g = (double)G[head_grad_offset(L, u, &val)] * (double)scale;
+        hq[val ? 1 : 0] += g * g;
+    }
+    block_reduce<2>(hq, sred);
+    if (tid == 0) {
+        const int nhw = (L.H2 + kTile - 1) / kTile + 1;
+        float *o = headsq + (k_local + (step_base ? *step_base : 0)) * nhw * 2;
+        o[0] = (float)hq[0];
+        o[1] = (float)hq[1];
+        for (int w = 1; w < nhw; ++w) o[2 * w] = o[2 * w + 1] = 0.0f;
+    }
+}
+
+int launch_head_sq(const Layout &L, const float *G, float scale, const FusedFwd &ff, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_head_sq, dim3(1), dim3(256), 0, s, L, G, scale, ff.step_base, (int64_t)ff.k_local, ff.headsq);
+    GS_LAUNCH_CHECK("k_head_sq");
+    return GS_OK;
 }
 
 // global mode, unfused chain: the KL early stop on the exchanged approx_kl of the whole minibatch
@@ -2948,9 +3004,9 @@ int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx,
 int launch_metrics_all(const Layout &L, int64_t B, int64_t n, const FusedFwd &ff, const LossArgs &la, float *metrics,
                        hipStream_t s)
 {
-    (void)L;
     hipLaunchKernelGGL(k_metrics_all, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ff.mpart,
-                       (int)(B / kTile), n, (int)B, la, metrics, nullptr);
+                       (int)(B / kTile), n, (int)B, la, metrics, ff.normsq ? ff.headsq : nullptr,
+                       (L.H2 + kTile - 1) / kTile + 1, ff.normsq);
     GS_LAUNCH_CHECK("k_metrics_all");
     return GS_OK;
 }

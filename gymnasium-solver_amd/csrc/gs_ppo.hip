@@ -176,6 +176,8 @@ struct FusedWs {
     float *xg, *folp, *fov, *fadv, *fret;
     int32_t *fa;
     double *mpart;
+    float *headsq;          // (n, H2/16 + 1, 2) role C's {policy, value} head sums of squares
+    double *normsq;         // (n) squared total norm per step
     float *p1, *m1, *v1;    // the lagged chain's second parameter set (params | adam_m | adam_v)
     size_t bytes;       // whole update workspace (step + fused)
 };
@@ -198,6 +200,8 @@ FusedWs carve_fused(void *base, const Layout &L, int64_t B, int64_t n)
     f.fadv = (float *)take(sizeof(float) * (size_t)(n * B));
     f.fret = (float *)take(sizeof(float) * (size_t)(n * B));
     f.mpart = (double *)take(sizeof(double) * (size_t)(n * (B / kTile) * 14));
+    f.headsq = (float *)take(sizeof(float) * (size_t)(n * ((L.H2 + kTile - 1) / kTile + 1) * 2));
+    f.normsq = (double *)take(sizeof(double) * (size_t)n);
     f.p1 = (float *)take(sizeof(float) * (size_t)L.P);
     f.m1 = (float *)take(sizeof(float) * (size_t)L.P);
     f.v1 = (float *)take(sizeof(float) * (size_t)L.P);
@@ -263,7 +267,7 @@ StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, in
 // over ranks (one xGMI exchange kernel, or reduce_part1 + RCCL + sumsq), then clip/Adam on
 // the mean (grad_scale 1/world) with the exchange's sum-of-squares partials.
 int exchange_and_adam(float *P, float *G, float *M, float *V, const Layout &L, const StepArgs &sa, float *metrics,
-                      int32_t *stop, const Workspace &ws, gs_comm *comm, hipStream_t s)
+                      int32_t *stop, const Workspace &ws, gs_comm *comm, hipStream_t s, const FusedFwd *ff = nullptr)
 {
     int world = 1, n_slots = 0;
     int rc = comm_grad_exchange(comm, G, L.P, Part1Fold{ws.part1, sa.aa.nrb, L}, ws.sumsq, &n_slots, stop, s,
@@ -273,7 +277,8 @@ int exchange_and_adam(float *P, float *G, float *M, float *V, const Layout &L, c
     aa.n_slots = n_slots;
     aa.nrb = 0;
     aa.grad_scale = sa.sum_exchange ? 1.0f : 1.0f / (float)world;
-    return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s);
+    if (ff && (rc = launch_head_sq(L, G, aa.grad_scale, *ff, s))) return rc;
+    return launch_clip_adam(P, L, G, M, V, nullptr, ws.sumsq, aa, metrics, stop, s, ff == nullptr);
 }
 
 int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const StepArgs &sa,
@@ -322,8 +327,8 @@ int enqueue_step_fused(float *P, float *G, float *M, float *V, const Layout &L, 
     if (rc) return rc;
     rc = launch_bwd(P, L, B, ws, G, stop, s, &ff, &sa.la, inbwd ? &bx : nullptr);
     if (rc) return rc;
-    if (!comm || inbwd) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s);
-    return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s);
+    if (!comm || inbwd) return launch_clip_adam(P, L, G, M, V, ws.part1, ws.sumsq, sa.aa, metrics, stop, s, false);
+    return exchange_and_adam(P, G, M, V, L, sa, metrics, stop, ws, comm, s, &ff);
 }
 
 // GS_LAGGED_ADAM=0 in the environment keeps a separate clip/Adam launch per minibatch (the
@@ -376,8 +381,9 @@ int enqueue_step_lagged(const ParamSet (&ps)[2], float *G, const Layout &L, cons
     rc = launch_bwd(cur.P, L, B, ws, G, stop, s, &ff, &sa_prev.la, inbwd ? &bx : nullptr);
     if (rc || !after) return rc;
     int world = 1, n_slots = 0;
-    return comm_grad_exchange(comm, G, L.P, Part1Fold{ws.part1, sa_prev.aa.nrb, L}, ws.sumsq, &n_slots, stop, s,
-                              &world);
+    rc = comm_grad_exchange(comm, G, L.P, Part1Fold{ws.part1, sa_prev.aa.nrb, L}, ws.sumsq, &n_slots, stop, s, &world);
+    if (rc) return rc;
+    return launch_head_sq(L, G, exchanged_adam_args(sa_prev.aa, comm, sa_prev.sum_exchange).grad_scale, ff, s);
 }
 
 int validate_update(const gs_mlp_dims &dims, const gs_rollout_view &ro, int64_t batch, const void *ws)
@@ -448,6 +454,7 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
         FusedFwd ff{};
         ff.xg = fw.xg, ff.fa = fw.fa, ff.folp = fw.folp, ff.fov = fw.fov, ff.fadv = fw.fadv, ff.fret = fw.fret;
         ff.mpart = fw.mpart;
+        ff.headsq = fw.headsq;
         ff.dz = ws.dz;
         if (stage == 6)
             return launch_gather_all(L, batch, 1, idx, ro.obs, ro.actions, ro.logprobs, ro.values, ro.advantages,
@@ -574,6 +581,8 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
         fw = carve_fused(workspace, L, batch, n_minibatches);
         ff0.xg = fw.xg, ff0.fa = fw.fa, ff0.folp = fw.folp, ff0.fov = fw.fov, ff0.fadv = fw.fadv, ff0.fret = fw.fret;
         ff0.mpart = fw.mpart;
+        ff0.headsq = fw.headsq;
+        ff0.normsq = fw.normsq;
         ff0.dz = ws.dz;
         rc = launch_gather_all(L, batch, n_minibatches, idx, ro.obs, ro.actions, ro.logprobs, ro.values,
                                ro.advantages, ro.returns, ro.T, ro.N, hp.normalize_adv, ff0, metrics, s,
@@ -596,22 +605,29 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
     auto lag_step = [&](int64_t k, const int64_t *base, const float *sched, hipStream_t st) {
         StepArgs sp = make_step_args(hp, L, batch, adam_step0 + k > 0 ? adam_step0 + k : 1);   // step k-1's
         sp.aa.sched = sched;
+        sp.aa.normsq = fw.normsq;      // the lagged forward indexes it by the applied step
         return enqueue_step_lagged(ps, grads, L, sp, batch, step_ff(k, k, base), k, metrics, stop_flag, ws, comm, st);
+    };
+    // the fused (non-lagged) chain's k_clip_adam of step k: its squared norm beside its record
+    auto with_norm = [&](StepArgs a, int64_t k) {
+        a.aa.normsq = fw.normsq ? fw.normsq + k : nullptr;
+        return a;
     };
     auto finish = [&]() -> int {
         if (!fused) return GS_OK;
         if (lagged) {   // the update's last optimizer step, and its result back into the caller's set
             const int64_t k = n_minibatches - 1;
             const ParamSet &q = ps[k & 1];
-            const StepArgs sl = make_step_args(hp, L, batch, adam_step0 + k + 1);
+            StepArgs sl = make_step_args(hp, L, batch, adam_step0 + k + 1);
+            sl.aa.normsq = fw.normsq + k;
             BwdXchg bx;
             const bool after = comm && !bwd_exchange_of(comm, L, batch, &bx, sl.sum_exchange);
             int rc2 = after ? launch_clip_adam(q.P, L, grads, q.M, q.V, nullptr, ws.sumsq,
                                               exchanged_adam_args(sl.aa, comm, sl.sum_exchange),
                                               metrics + k * GS_NUM_METRICS,
-                                              stop_flag, s)
+                                              stop_flag, s, false)
                            : launch_clip_adam(q.P, L, grads, q.M, q.V, ws.part1, ws.sumsq, sl.aa,
-                                              metrics + k * GS_NUM_METRICS, stop_flag, s);
+                                              metrics + k * GS_NUM_METRICS, stop_flag, s, false);
             if (rc2) return rc2;
             if (k & 1) {
                 const size_t nb = sizeof(float) * (size_t)L.P;
@@ -631,8 +647,9 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
         for (int64_t k = 0; k < n_minibatches; ++k) {
             const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
             rc = lagged  ? lag_step(k, nullptr, nullptr, s)
-                 : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
-                                              metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
+                 : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, with_norm(sa, k), batch,
+                                              step_ff(k, k, nullptr), metrics + k * GS_NUM_METRICS, stop_flag, ws,
+                                              comm, s)
                          : enqueue_step(params, grads, adam_m, adam_v, L, at_step(sa, k), ro, idx + k * batch, batch,
                                         metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
             if (rc) return rc;
@@ -705,7 +722,8 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
                 la_f.step_base = nullptr;      // the fused fwd takes its base from FusedFwd
                 StepArgs saf = sa;
                 saf.la = la_f;
-                rc = enqueue_step_fused(params, grads, adam_m, adam_v, L, saf, batch, step_ff(k, k, ent.base),
+                rc = enqueue_step_fused(params, grads, adam_m, adam_v, L, with_norm(saf, k), batch,
+                                        step_ff(k, k, ent.base),
                                         metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
             } else {
                 rc = enqueue_step(params, grads, adam_m, adam_v, L, at_step(sa, k), ro, idx + k * batch, batch,
@@ -749,8 +767,9 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
     for (int64_t k = n_full * chunk; k < n_minibatches; ++k) {
         const StepArgs sa = make_step_args(hp, L, batch, adam_step0 + k + 1);
         rc = lagged  ? lag_step(k, nullptr, nullptr, s)
-             : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, sa, batch, step_ff(k, k, nullptr),
-                                          metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s)
+             : fused ? enqueue_step_fused(params, grads, adam_m, adam_v, L, with_norm(sa, k), batch,
+                                          step_ff(k, k, nullptr), metrics + k * GS_NUM_METRICS, stop_flag, ws, comm,
+                                          s)
                      : enqueue_step(params, grads, adam_m, adam_v, L, at_step(sa, k), ro, idx + k * batch, batch,
                                   metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, s);
         if (rc) return rc;

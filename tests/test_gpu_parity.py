@@ -395,7 +395,14 @@ def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph
         del agent
     (p0, m0), (p1, m1) = out
     assert np.array_equal(p0.view(np.uint32), p1.view(np.uint32))
-    np.testing.assert_allclose(m0, m1, rtol=1e-6, atol=1e-7)
+    # per-component gradient norms: the fused chain sums role C's fp32 head sums per step, the
+    # 4-launch chain re-reads the head gradients in double (k_component_norms)
+    from gsamd._lib import M
+    gn = [M[k] for k in ("gn_backbone", "gn_policy_head", "gn_value_head")]
+    rest = [c for c in range(m0.shape[1]) if c not in gn]
+    np.testing.assert_allclose(m0[:, rest], m1[:, rest], rtol=1e-6, atol=1e-7)
+    bad = np.argwhere(~np.isclose(m0[:, gn], m1[:, gn], rtol=1e-4, atol=1e-7))
+    assert len(bad) == 0, [(int(r), gn[c], m0[r], m1[r]) for r, c in bad[:4]]
 
 
 @pytest.mark.parametrize("transport", ["rccl", "xgmi"])
