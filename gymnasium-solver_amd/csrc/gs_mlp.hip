@@ -1399,6 +1399,18 @@ __device__ __forceinline__ void block_sumsq_store(float v, float *slot, float *s
 // the {policy head, value head} split of the same values for the per-component gradient norms
 // (utils/models.py:196-230; k_metrics_all turns them into the record).  The slot's sum is the
 // first of the reduced values, so it is the same sum in the same order as block_sumsq_store's.
+// after block_sumsq_store: thread 0 splits the head values the reduction's LDS levels still hold
+// (v[a]: head row / bias a's share) into the step's {policy, value} record
+__device__ __forceinline__ void store_head_split(const float *v, int A, float *headsq, int64_t o)
+{
+    if (threadIdx.x == 0 && headsq) {
+        float p = 0.0f;
+        for (int a = 0; a < A; ++a) p += v[a];
+        headsq[o] = p;
+        headsq[o + 1] = v[A];
+    }
+}
+
 __device__ __forceinline__ void store_head_sums(float sq, float sqp, float sqv, float *slot, float *headsq,
                                                 int64_t o, float *sbuf)
 {
@@ -2219,8 +2231,6 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 if (ok[0]) {
                     G[L.head_row(a) + n0 + i] = hv[0];
                     sq = hv[0] * hv[0];
-                    sqp = a < A ? sq : 0.0f;
-                    sqv = a == A ? sq : 0.0f;
                 }
             } else {
                 // outputs (a, i): A1*16 of them; each summed over b by 16 threads into LDS partials
@@ -2257,8 +2267,14 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     }
                 }
             }
-            store_head_sums(sq, sqp, sqv, sumsq + sh.nT + sh.ncb + nb, FUSED ? ff.headsq : nullptr,
-                            (kstep * (sh.ncb + 1) + nb) * 2, sbuf);
+            if (A1 <= kTile) {
+                // the reduction's first level leaves the sum of each 16-thread group = head row a
+                block_sumsq_store(sq, sumsq + sh.nT + sh.ncb + nb, sbuf);
+                if constexpr (FUSED) store_head_split(sbuf + 256, A, ff.headsq, (kstep * (sh.ncb + 1) + nb) * 2);
+            } else {
+                store_head_sums(sq, sqp, sqv, sumsq + sh.nT + sh.ncb + nb, FUSED ? ff.headsq : nullptr,
+                                (kstep * (sh.ncb + 1) + nb) * 2, sbuf);
+            }
         } else {
             // the extra block: head-bias gradients (sum of dz over the batch)
             for (int u = tid; u < A1 * 16; u += 256) {
@@ -2279,8 +2295,9 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 G[L.head_bias(tid)] = bv[0];
                 sqb = bv[0] * bv[0];
             }
-            store_head_sums(sqb, tid < A ? sqb : 0.0f, tid == A ? sqb : 0.0f, sumsq + sh.nT + 2 * sh.ncb, FUSED ? ff.headsq : nullptr,
-                            (kstep * (sh.ncb + 1) + sh.ncb) * 2, sbuf);
+            block_sumsq_store(sqb, sumsq + sh.nT + 2 * sh.ncb, sbuf);
+            // the reduction's input level: thread a's square = head bias a
+            if constexpr (FUSED) store_head_split(sbuf, A, ff.headsq, (kstep * (sh.ncb + 1) + sh.ncb) * 2);
         }
         GS_STAMP_END(1)
         if constexpr (FUSED) GS_SPAN_END(1, kstep)
