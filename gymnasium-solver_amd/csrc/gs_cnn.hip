@@ -22,6 +22,7 @@
 #include <math.h>
 #include <algorithm>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "gs_comm_internal.h"
@@ -89,8 +90,10 @@ struct CnnWs {
     size_t bytes;
 };
 
-constexpr int kNormBlocks = 1024;
+constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block sums them)
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
+constexpr int kHeadRows = 8;    // minibatch rows per k_cnn_head_loss workgroup
+constexpr int kHeadSlices = 256 / kHeadRows;   // its z product's K slices (one thread per row x slice)
 // split-K slices of the weight-gradient GEMMs (K = minibatch rows x positions): enough slices
 // that the small (Cout x patch) outputs still fill the chip
 constexpr int kSplitW1 = 128, kSplitW2 = 64, kSplitW3 = 64;
@@ -132,7 +135,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks * 5);   // total + 4 component partials
-    w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + 255) / 256));
+    w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + kHeadRows - 1) / kHeadRows));
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
                                          (int64_t)kSplitW3 * L.c3 * (L.K3 + 1),
@@ -143,7 +146,8 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
                                          (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
                                          (int64_t)splits_for(L.A + 1, L.HID + 1, R) * (L.A + 1) * (L.HID + 1),
                                          (int64_t)splits_for(L.HID, L.F + 1, R) * L.HID * (L.F + 1)});
-        w.parts = (float *)take(sizeof(float) * std::max({wparts, cparts, gparts}));
+        const int64_t hparts = (R + kHeadRows - 1) / kHeadRows * (int64_t)(L.A + 1) * (L.HID + 1);
+        w.parts = (float *)take(sizeof(float) * std::max({wparts, cparts, gparts, hparts}));
     }
     w.bytes = off;
     return w;
@@ -157,6 +161,15 @@ __device__ __forceinline__ int64_t frame_row(const int32_t *idx, int64_t r, int6
     const int64_t env = i / T, t = i - env * T;   // env-major sample index (rollout_buffer.py:11-13)
     return t * N + env;
 }
+
+// the minibatch's rollout fields read in place through the sampler indices (the fused head + loss
+// kernel gathers its own rows; utils/rollout_collector.py:657-682)
+struct CnnFields {
+    const int32_t *idx;
+    int64_t T, N;
+    const int64_t *actions;
+    const float *logprobs, *values, *advantages, *returns;
+};
 
 // ---- ReLU-masked col2im (gather form, fixed summation order): dA[r,y,x,c] for stride s
 __global__ __launch_bounds__(256) void k_col2im_relu(const float *__restrict__ dcols, const float *__restrict__ act,
@@ -196,18 +209,6 @@ __global__ __launch_bounds__(256) void k_col2im_relu(const float *__restrict__ d
     o.z = av.z > 0.f ? acc.z : 0.f;
     o.w = av.w > 0.f ? acc.w : 0.f;
     *(float4 *)(dA + e * Cin + c4 * 4) = o;
-}
-
-// ---- d = a > 0 ? d : 0
-__global__ __launch_bounds__(256) void k_relu_mask(float *__restrict__ d, const float *__restrict__ a, int64_t n4)
-{
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= n4) return;
-    float4 v = ((float4 *)d)[t];
-    const float4 av = ((const float4 *)a)[t];
-    v.x = av.x > 0.f ? v.x : 0.f, v.y = av.y > 0.f ? v.y : 0.f;
-    v.z = av.z > 0.f ? v.z : 0.f, v.w = av.w > 0.f ? v.w : 0.f;
-    ((float4 *)d)[t] = v;
 }
 
 // ---- bias gradient: column sums of X[rows][C], deterministic two-pass.  Block p sums rows
@@ -283,25 +284,32 @@ struct MRow {
 template <int AM>
 __device__ __forceinline__ MRow mrow_stats(const float (&z)[AM + 1], const CnnLayout &L)
 {
+    // branch-free over the static action range (invalid lanes selected out, sums in action order):
+    // a uniform branch per action would serialise the independent exp chains
+    bool va[AM];
+#pragma unroll
+    for (int a = 0; a < AM; ++a) va[a] = a < L.A && L.is_valid(a);
     float m = -INFINITY;
 #pragma unroll
-    for (int a = 0; a < AM; ++a)
-        if (a < L.A && L.is_valid(a)) m = fmaxf(m, z[a]);
+    for (int a = 0; a < AM; ++a) m = fmaxf(m, va[a] ? z[a] : -INFINITY);
     float se = 0.f;
 #pragma unroll
-    for (int a = 0; a < AM; ++a)
-        if (a < L.A && L.is_valid(a)) se += expf(z[a] - m);
+    for (int a = 0; a < AM; ++a) {
+        const float e = expf(z[a] - m);
+        se += va[a] ? e : 0.f;
+    }
     MRow h;
     h.lse = m + logf(se);
     float m2 = -INFINITY;
 #pragma unroll
-    for (int a = 0; a < AM; ++a)
-        if (a < L.A && L.is_valid(a)) m2 = fmaxf(m2, z[a] - h.lse);
+    for (int a = 0; a < AM; ++a) m2 = fmaxf(m2, va[a] ? z[a] - h.lse : -INFINITY);
     h.m2 = m2;
     float S = 0.f;
 #pragma unroll
-    for (int a = 0; a < AM; ++a)
-        if (a < L.A && L.is_valid(a)) S += expf((z[a] - h.lse) - m2);
+    for (int a = 0; a < AM; ++a) {
+        const float e = expf((z[a] - h.lse) - m2);
+        S += va[a] ? e : 0.f;
+    }
     h.S = S;
     return h;
 }
@@ -417,6 +425,154 @@ constexpr int kSums = 13;
 constexpr int kLossRows = 256;   // loss rows per workgroup (one per thread)
 static_assert(kSums == 13, "carve() sizes loss_part for 13 sums");
 
+// One row of the PPO loss with (Masked)Categorical heads (agents/ppo/ppo_agent.py:21-152,
+// utils/distributions.py:8-82): zr = the row's logits | value with biases, adv raw (normalised
+// here when la.normalize); adds the row's 13 metric sums to acc and writes dLoss/dz to dzr.
+template <int AM>
+__device__ __forceinline__ void cnn_loss_row(const float (&zr)[AM + 1], float v, int act, float olp, float ov,
+                                             float adv, float ret, float meanf, float stdf, const LossArgs &la,
+                                             float invB, const CnnLayout &L, float *__restrict__ dzr,
+                                             double (&acc)[kSums])
+{
+    const int A = L.A;
+    const bool masked = L.valid != 0u;
+    const MRow h = mrow_stats<AM>(zr, L);
+    const float invS = 1.0f / h.S;
+    float ln[AM], p[AM], g[AM];
+    bool va[AM];
+    float H = 0.f, lp = 0.f, pg = 0.f;
+    // branch-free over the static action range (see mrow_stats); sums in action order
+#pragma unroll
+    for (int a = 0; a < AM; ++a) {
+        va[a] = a < A && L.is_valid(a);
+        const float lnr = zr[a] - h.lse;
+        ln[a] = va[a] ? lnr : -INFINITY;
+        const float pr = expf(lnr - h.m2) * invS;
+        p[a] = va[a] ? pr : 0.f;
+        if (masked) {
+            const float lq = logf(p[a] + 1e-8f);      // MaskedCategorical.entropy
+            g[a] = lq + p[a] / (p[a] + 1e-8f);         // -dH/dp_a
+            H += va[a] ? p[a] * lq : 0.f;
+            pg += va[a] ? p[a] * g[a] : 0.f;
+        } else {
+            g[a] = 0.f;
+            H += va[a] ? fmaxf(ln[a], -FLT_MAX) * p[a] : 0.f;    // Categorical.entropy
+        }
+        lp = (va[a] && a == act) ? ln[a] : lp;
+    }
+    H = -H;
+    if (la.normalize) adv = (adv - meanf) / (stdf + 1e-8f);
+    const float ratio = expf(lp - olp);
+    const float rc = fminf(fmaxf(ratio, la.clip_lo), la.clip_hi);
+    const float s1 = adv * ratio, s2 = adv * rc;
+    const float mn = fminf(s1, s2);
+    const float vdelta = v - ov;
+    const float du = v - ret;
+    const float vu = du * du;
+    const float vcl = ov + fminf(fmaxf(vdelta, -la.clip_vf), la.clip_vf);
+    const float dc = vcl - ret;
+    const float vc = dc * dc;
+    const float ldiff = fminf(fmaxf(lp - olp, -20.0f), 20.0f);
+    const float r2 = expf(ldiff);
+    const float rv = ret - v;
+    acc[0] += (double)mn;
+    acc[1] += (double)fmaxf(vu, vc);
+    acc[2] += (double)H;
+    acc[3] += (ratio < la.clip_lo || ratio > la.clip_hi) ? 1.0 : 0.0;
+    acc[4] += (vdelta < -la.clip_vf || vdelta > la.clip_vf) ? 1.0 : 0.0;
+    acc[5] += (double)(olp - lp);
+    acc[6] += (double)((r2 - 1.0f) - logf(r2));
+    acc[7] += (double)rv;
+    acc[8] += (double)rv * (double)rv;
+    acc[9] += (double)ret;
+    acc[10] += (double)ret * (double)ret;
+    acc[11] += (double)adv;
+    acc[12] += (double)adv * (double)adv;
+    const float ga = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+    const float gb = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+    const float inclip = (ratio >= la.clip_lo && ratio <= la.clip_hi) ? 1.0f : 0.0f;
+    const float g_mn = -invB;
+    const float dratio = adv * (g_mn * ga) + adv * (g_mn * gb) * inclip;
+    const float dlp = dratio * ratio;
+    const float dH = -la.ent_coef * invB;
+    float dzv[AM];
+#pragma unroll
+    for (int a = 0; a < AM; ++a) {
+        const float pe = expf(ln[a]);
+        float gg = dlp * ((a == act ? 1.0f : 0.0f) - pe);
+        if (masked) gg += dH * (p[a] * (pg - g[a]));
+        else gg += dH * (-p[a] * (ln[a] + H));
+        dzv[a] = va[a] ? gg : 0.f;      // masked_fill blocks the gradient of an invalid action
+    }
+#pragma unroll
+    for (int a = 0; a < AM; ++a)
+        if (a < A) dzr[a] = dzv[a];
+    const float hu = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+    const float hc = vc > vu ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+    const float invc = (vdelta >= -la.clip_vf && vdelta <= la.clip_vf) ? 1.0f : 0.0f;
+    const float gv = la.vf_coef * invB;
+    dzr[A] = (gv * hu) * (2.0f * du) + (gv * hc) * (2.0f * dc) * invc;
+}
+
+// batch advantage normalisation statistics (utils/torch.py:97-99): mean and unbiased std over the
+// minibatch in double, two passes; every thread of the (256-thread) workgroup calls it
+__device__ __forceinline__ void batch_adv_stats(const float *__restrict__ f_adv, int B, double *sred, float &meanf,
+                                                float &stdf)
+{
+    const int tid = threadIdx.x;
+    constexpr int NB = 8;       // loads of a batch all in flight before the sums
+    double m1[1] = {0.0};
+    for (int b0 = 0; b0 < B; b0 += 256 * NB) {
+        float t[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) t[j] = f_adv[min(b0 + tid + 256 * j, B - 1)];
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+            if (b0 + tid + 256 * j < B) m1[0] += (double)t[j];
+    }
+    wg_reduce<1>(m1, sred);
+    const double mean = m1[0] / (double)B;
+    double q[1] = {0.0};
+    for (int b0 = 0; b0 < B; b0 += 256 * NB) {
+        float t[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) t[j] = f_adv[min(b0 + tid + 256 * j, B - 1)];
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+            if (b0 + tid + 256 * j < B) {
+                const double dv = (double)t[j] - mean;
+                q[0] += dv * dv;
+            }
+    }
+    wg_reduce<1>(q, sred);
+    meanf = (float)mean;
+    stdf = (float)sqrt(q[0] / (double)(B - 1));
+}
+
+// the same from the minibatch's advantages already in registers (thread t holds rows t + 256 j)
+template <int NA>
+__device__ __forceinline__ void batch_adv_stats_regs(const float (&adv)[NA], int B, double *sred, float &meanf,
+                                                     float &stdf)
+{
+    const int tid = threadIdx.x;
+    double m1[1] = {0.0};
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+        if (tid + 256 * j < B) m1[0] += (double)adv[j];
+    wg_reduce<1>(m1, sred);
+    const double mean = m1[0] / (double)B;
+    double q[1] = {0.0};
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+        if (tid + 256 * j < B) {
+            const double dv = (double)adv[j] - mean;
+            q[0] += dv * dv;
+        }
+    wg_reduce<1>(q, sred);
+    meanf = (float)mean;
+    stdf = (float)sqrt(q[0] / (double)(B - 1));
+}
+
 // ---- the PPO loss of one minibatch with (Masked)Categorical heads; one workgroup.
 template <int AM>
 __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
@@ -430,23 +586,9 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
     const int tid = threadIdx.x;
     if (stop && *stop) return;
     const int A = L.A, A1 = A + 1;
-    const bool masked = L.valid != 0u;
     const float invB = 1.0f / (float)B;
     float meanf = 0.f, stdf = 1.f;
-    if (la.normalize) {
-        double m1[1] = {0.0};
-        for (int r = tid; r < B; r += 256) m1[0] += (double)f_adv[r];
-        wg_reduce<1>(m1, sred);
-        const double mean = m1[0] / (double)B;
-        double q[1] = {0.0};
-        for (int r = tid; r < B; r += 256) {
-            const double dv = (double)f_adv[r] - mean;
-            q[0] += dv * dv;
-        }
-        wg_reduce<1>(q, sred);
-        meanf = (float)mean;
-        stdf = (float)sqrt(q[0] / (double)(B - 1));
-    }
+    if (la.normalize) batch_adv_stats(f_adv, B, sred, meanf, stdf);
     double acc[kSums];
 #pragma unroll
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
@@ -461,83 +603,7 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
         }
         const int act = f_act[r];
         const float olp = f_olp[r], ov = f_ov[r], ret = f_ret[r];
-        float adv = f_adv[r];
-        const MRow h = mrow_stats<AM>(zr, L);
-        const float invS = 1.0f / h.S;
-        float ln[AM], p[AM], g[AM];
-        float H = 0.f, lp = 0.f, pg = 0.f;
-#pragma unroll
-        for (int a = 0; a < AM; ++a) {
-            ln[a] = -INFINITY, p[a] = 0.f, g[a] = 0.f;
-            if (a >= A) continue;
-            const bool va = L.is_valid(a);
-            ln[a] = va ? zr[a] - h.lse : -INFINITY;
-            p[a] = va ? expf(ln[a] - h.m2) * invS : 0.f;
-            if (!va) continue;
-            if (masked) {
-                const float lq = logf(p[a] + 1e-8f);      // MaskedCategorical.entropy
-                H += p[a] * lq;
-                g[a] = lq + p[a] / (p[a] + 1e-8f);         // -dH/dp_a
-                pg += p[a] * g[a];
-            } else {
-                H += fmaxf(ln[a], -FLT_MAX) * p[a];        // Categorical.entropy
-            }
-            if (a == act) lp = ln[a];
-        }
-        H = -H;
-        if (la.normalize) adv = (adv - meanf) / (stdf + 1e-8f);
-        const float ratio = expf(lp - olp);
-        const float rc = fminf(fmaxf(ratio, la.clip_lo), la.clip_hi);
-        const float s1 = adv * ratio, s2 = adv * rc;
-        const float mn = fminf(s1, s2);
-        const float vdelta = v - ov;
-        const float du = v - ret;
-        const float vu = du * du;
-        const float vcl = ov + fminf(fmaxf(vdelta, -la.clip_vf), la.clip_vf);
-        const float dc = vcl - ret;
-        const float vc = dc * dc;
-        const float ldiff = fminf(fmaxf(lp - olp, -20.0f), 20.0f);
-        const float r2 = expf(ldiff);
-        const float rv = ret - v;
-        acc[0] += (double)mn;
-        acc[1] += (double)fmaxf(vu, vc);
-        acc[2] += (double)H;
-        acc[3] += (ratio < la.clip_lo || ratio > la.clip_hi) ? 1.0 : 0.0;
-        acc[4] += (vdelta < -la.clip_vf || vdelta > la.clip_vf) ? 1.0 : 0.0;
-        acc[5] += (double)(olp - lp);
-        acc[6] += (double)((r2 - 1.0f) - logf(r2));
-        acc[7] += (double)rv;
-        acc[8] += (double)rv * (double)rv;
-        acc[9] += (double)ret;
-        acc[10] += (double)ret * (double)ret;
-        acc[11] += (double)adv;
-        acc[12] += (double)adv * (double)adv;
-        const float ga = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-        const float gb = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-        const float inclip = (ratio >= la.clip_lo && ratio <= la.clip_hi) ? 1.0f : 0.0f;
-        const float g_mn = -invB;
-        const float dratio = adv * (g_mn * ga) + adv * (g_mn * gb) * inclip;
-        const float dlp = dratio * ratio;
-        const float dH = -la.ent_coef * invB;
-        float *dzr = dz + (int64_t)r * A1;
-#pragma unroll
-        for (int a = 0; a < AM; ++a) {
-            if (a >= A) continue;
-            if (!L.is_valid(a)) {
-                dzr[a] = 0.f;      // masked_fill blocks the gradient
-                continue;
-            }
-            const float pe = expf(ln[a]);
-            float gg = dlp * ((a == act ? 1.0f : 0.0f) - pe);
-            if (masked) gg += dH * (p[a] * (pg - g[a]));
-            else gg += dH * (-p[a] * (ln[a] + H));
-            dzr[a] = gg;
-        }
-        const float hu = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
-        const float hc = vc > vu ? 1.0f : (vu == vc ? 0.5f : 0.0f);
-        const float invc = (vdelta >= -la.clip_vf && vdelta <= la.clip_vf) ? 1.0f : 0.0f;
-        const float gv = la.vf_coef * invB;
-        dzr[A] = (gv * hu) * (2.0f * du) + (gv * hc) * (2.0f * dc) * invc;
+        cnn_loss_row<AM>(zr, v, act, olp, ov, f_adv[r], ret, meanf, stdf, la, invB, L, dz + (int64_t)r * A1, acc);
     }
     wg_reduce<kSums>(acc, sred);
     if (tid == 0)
@@ -545,10 +611,11 @@ __global__ __launch_bounds__(256) void k_cnn_loss(const float *__restrict__ z, c
 }
 
 // ---- loss metrics from the row-block partial sums (summed in block order) + KL early stop
-__global__ void k_cnn_loss_final(const double *__restrict__ part, int nb, int B, LossArgs la,
-                                 float *__restrict__ metrics, int32_t *__restrict__ stop)
+// the minibatch record from the loss row-block partial sums (summed in block order) + the KL
+// early stop (agents/base_agent.py:330-366); one thread
+__device__ void cnn_write_metrics(const double *__restrict__ part, int nb, int B, const LossArgs &la,
+                                  float *__restrict__ metrics, int32_t *__restrict__ stop)
 {
-    if (threadIdx.x != 0) return;
     if (stop && *stop) {
         for (int k = 0; k < GS_NUM_METRICS; ++k) metrics[k] = 0.0f;
         metrics[GS_M_SKIPPED] = 1.0f;
@@ -556,42 +623,308 @@ __global__ void k_cnn_loss_final(const double *__restrict__ part, int nb, int B,
         metrics[GS_M_UNEVALUATED] = 1.0f;
         return;
     }
-    double acc[kSums];
+    double t[kSums];
     for (int q = 0; q < kSums; ++q) {
         double v = 0.0;
         for (int b = 0; b < nb; ++b) v += part[(int64_t)b * kSums + q];
-        acc[q] = v;
+        t[q] = v;
     }
+    const double Bd = (double)B;
+    const float pl = (float)(-t[0] / Bd);
+    const float vl = (float)(t[1] / Bd);
+    const float ent = (float)(t[2] / Bd);
+    const float loss = pl + la.vf_coef * vl + la.ent_coef * (-ent);
+    const double var_rv = (t[8] - t[7] * t[7] / Bd) / (Bd - 1.0);
+    const double var_r = (t[10] - t[9] * t[9] / Bd) / (Bd - 1.0);
+    const double amean = t[11] / Bd;
+    const double astd = sqrt(fmax(0.0, (t[12] - t[11] * t[11] / Bd) / (Bd - 1.0)));
+    const float approx_kl = (float)(t[6] / Bd);
+    const bool kl_stop = la.target_kl > 0.0f && approx_kl > la.target_kl;
+    metrics[GS_M_LOSS] = loss;
+    metrics[GS_M_POLICY_LOSS] = pl;
+    metrics[GS_M_VALUE_LOSS] = vl;
+    metrics[GS_M_ENTROPY] = ent;
+    metrics[GS_M_CLIP_FRAC] = (float)(t[3] / Bd);
+    metrics[GS_M_CLIP_FRAC_VF] = (float)(t[4] / Bd);
+    metrics[GS_M_EXPLAINED_VAR] = (float)(1.0 - var_rv / var_r);
+    metrics[GS_M_KL] = (float)(t[5] / Bd);
+    metrics[GS_M_APPROX_KL] = approx_kl;
+    metrics[GS_M_ADV_NORM_MEAN] = la.normalize ? (float)amean : 0.0f;
+    metrics[GS_M_ADV_NORM_STD] = la.normalize ? (float)astd : 0.0f;
+    metrics[GS_M_KL_STOP] = kl_stop ? 1.0f : 0.0f;
+    metrics[GS_M_GRAD_NORM] = 0.0f;
+    metrics[GS_M_SKIPPED] = kl_stop ? 1.0f : 0.0f;
+    metrics[GS_M_UNEVALUATED] = 0.0f;
+    metrics[GS_M_RES1] = 0.0f;
+    if (kl_stop && stop) *stop = 1;
+}
+
+__global__ void k_cnn_loss_final(const double *__restrict__ part, int nb, int B, LossArgs la,
+                                 float *__restrict__ metrics, int32_t *__restrict__ stop)
+{
+    if (threadIdx.x == 0) cnn_write_metrics(part, nb, B, la, metrics, stop);
+}
+
+// ---- the update's head + loss section as two launches (replacing heads GEMM + split-K sum,
+// loss rows + final, head weight-gradient GEMM + two sums and the dh kernel):
+// k_cnn_head_loss: kHeadRows minibatch rows per workgroup — z = h Wh^T (K split over 16 thread
+// slices, summed in slice order), the loss rows (cnn_loss_row), dz, dh = relu'(h) (dz Wh)
+// (policy rows, then the value row: k_cnn_dh's order) and the workgroup's [dWh | dbh] = dz^T [h | 1]
+// partial (its rows in order); k_cnn_head_wsum: the partials summed in workgroup order and, in its
+// last workgroup, the minibatch record.  BF (GS_HP_BF16): the z and
+// dWh products take bf16-rounded operands (fp32 accumulation), as the GEMM engine's bf16 form.
+__device__ __forceinline__ float bf16r(float x) { return (float)(__bf16)x; }
+
+// head rows of A1 values padded to a float4 multiple: LDS rows read as float4 (a row stride of
+// 4 (mod 64) banks x a multiple of 4 keeps 16 consecutive rows on distinct banks)
+__host__ __device__ constexpr int head_zs(int A1) { return (A1 + 3) & ~3; }
+
+size_t head_loss_lds(const CnnLayout &L)
+{
+    const int ZS = head_zs(L.A + 1);
+    return sizeof(float) * ((size_t)kHeadRows * (L.HID + kHeadSlices) + (size_t)L.HID * ZS +
+                            (size_t)kHeadSlices * kHeadRows * ZS + (size_t)kHeadRows * ZS);
+}
+
+// the head weights' gradient partials of one k_cnn_head_loss workgroup: [A1][HID + 1] (bias last)
+__host__ __device__ inline int64_t head_part_stride(const CnnLayout &L) { return (int64_t)(L.A + 1) * (L.HID + 1); }
+
+template <int AM, bool BF>
+__global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__ h, const float *__restrict__ P,
+                                                       CnnLayout L, int B, CnnFields fl, LossArgs la,
+                                                       float *__restrict__ dz, float *__restrict__ dh,
+                                                       float *__restrict__ wpart, double *__restrict__ part,
+                                                       const int32_t *__restrict__ stop, int dbg)
+{
+    constexpr int NZ = (AM + 1 + 3) / 4;               // float4 chunks of a padded head row
+    __shared__ double sred[kSums * 256 + kSums * 16];
+    extern __shared__ float lds[];
+    if (stop && *stop) return;
+    const int tid = threadIdx.x, A = L.A, A1 = A + 1, HID = L.HID, HS = HID + kHeadSlices, ZS = head_zs(A1);
+    const int r0 = blockIdx.x * kHeadRows;
+    float *hs = lds;                                  // [kHeadRows][HS] (kHeadSlices banks between rows)
+    float *wt = hs + kHeadRows * HS;                  // [HID][ZS]: Wh transposed (policy rows, then value)
+    float *zp = wt + HID * ZS;                        // [kHeadSlices][kHeadRows][ZS]
+    float *zs = zp + kHeadSlices * kHeadRows * ZS;    // [kHeadRows][ZS]: z, then dz
+    // staging: one burst of clamped, unconditional loads (h rows and Wp as float4, the value row,
+    // the minibatch's advantages for the normalisation and this workgroup's rows' fields, both
+    // through the sampler indices), then the LDS stores (Wh transposed).  head_fused() keeps the
+    // shapes within the slots: HID <= 512, A * HID <= 12288, B <= 2048
+    constexpr int NH = 8, NW = 12, NV = 4, NA = 8;
+    const int H4 = HID / 4, nh4 = kHeadRows * H4, np4 = A * HID / 4;
+    float adv_r[NA];
+    int my_act = 0;
+    float my_olp = 0.f, my_ov = 0.f, my_adv = 0.f, my_ret = 0.f;
     {
-        const double *t = acc;
-        const double Bd = (double)B;
-        const float pl = (float)(-t[0] / Bd);
-        const float vl = (float)(t[1] / Bd);
-        const float ent = (float)(t[2] / Bd);
-        const float loss = pl + la.vf_coef * vl + la.ent_coef * (-ent);
-        const double var_rv = (t[8] - t[7] * t[7] / Bd) / (Bd - 1.0);
-        const double var_r = (t[10] - t[9] * t[9] / Bd) / (Bd - 1.0);
-        const double amean = t[11] / Bd;
-        const double astd = sqrt(fmax(0.0, (t[12] - t[11] * t[11] / Bd) / (Bd - 1.0)));
-        const float approx_kl = (float)(t[6] / Bd);
-        const bool kl_stop = la.target_kl > 0.0f && approx_kl > la.target_kl;
-        metrics[GS_M_LOSS] = loss;
-        metrics[GS_M_POLICY_LOSS] = pl;
-        metrics[GS_M_VALUE_LOSS] = vl;
-        metrics[GS_M_ENTROPY] = ent;
-        metrics[GS_M_CLIP_FRAC] = (float)(t[3] / Bd);
-        metrics[GS_M_CLIP_FRAC_VF] = (float)(t[4] / Bd);
-        metrics[GS_M_EXPLAINED_VAR] = (float)(1.0 - var_rv / var_r);
-        metrics[GS_M_KL] = (float)(t[5] / Bd);
-        metrics[GS_M_APPROX_KL] = approx_kl;
-        metrics[GS_M_ADV_NORM_MEAN] = la.normalize ? (float)amean : 0.0f;
-        metrics[GS_M_ADV_NORM_STD] = la.normalize ? (float)astd : 0.0f;
-        metrics[GS_M_KL_STOP] = kl_stop ? 1.0f : 0.0f;
-        metrics[GS_M_GRAD_NORM] = 0.0f;
-        metrics[GS_M_SKIPPED] = kl_stop ? 1.0f : 0.0f;
-        metrics[GS_M_UNEVALUATED] = 0.0f;
-        metrics[GS_M_RES1] = 0.0f;
-        if (kl_stop && stop) *stop = 1;
+        float4 th[NH], tw[NW];
+        float tv[NV];
+        const float4 *wp4 = reinterpret_cast<const float4 *>(P + L.oWp);
+        int64_t src[NA];
+#pragma unroll
+        for (int j = 0; j < NA; ++j) src[j] = frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N);
+        const int64_t my_src = frame_row(fl.idx, min(r0 + (tid & (kHeadRows - 1)), B - 1), fl.T, fl.N);
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+            const int u = min(tid + 256 * j, nh4 - 1), r = u / H4, c4 = u - r * H4;
+            th[j] = *reinterpret_cast<const float4 *>(h + (int64_t)min(r0 + r, B - 1) * HID + 4 * c4);
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) tw[j] = wp4[min(tid + 256 * j, np4 - 1)];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) tv[j] = P[L.oWv + min(tid + 256 * j, HID - 1)];
+#pragma unroll
+        for (int j = 0; j < NA; ++j) adv_r[j] = fl.advantages[src[j]];
+        my_act = (int)fl.actions[my_src];
+        my_olp = fl.logprobs[my_src];
+        my_ov = fl.values[my_src];
+        my_adv = fl.advantages[my_src];
+        my_ret = fl.returns[my_src];
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+            const int u = tid + 256 * j, r = u / H4, c4 = u - r * H4;
+            if (u < nh4) *reinterpret_cast<float4 *>(hs + r * HS + 4 * c4) = r0 + r < B ? th[j]
+                                                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            const int u = tid + 256 * j;
+            if (u < np4) {
+                const int a = (4 * u) / HID, c = 4 * u - a * HID;     // 4 consecutive columns of row a
+                wt[(c + 0) * ZS + a] = tw[j].x;
+                wt[(c + 1) * ZS + a] = tw[j].y;
+                wt[(c + 2) * ZS + a] = tw[j].z;
+                wt[(c + 3) * ZS + a] = tw[j].w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int c = tid + 256 * j;
+            if (c < HID) {
+                wt[c * ZS + A] = tv[j];
+                for (int a = A1; a < ZS; ++a) wt[c * ZS + a] = 0.f;
+            }
+        }
+    }
+    float meanf = 0.f, stdf = 1.f;
+    if (la.normalize) batch_adv_stats_regs<NA>(adv_r, B, sred, meanf, stdf);    // its barriers cover the staging
+    else __syncthreads();
+    if (!(dbg & 1)) {   // z partials: thread (row r, slice q) over k = q, q + kHeadSlices, ...
+        const int r = tid / kHeadSlices, q = tid % kHeadSlices;
+        float acc[4 * NZ];
+#pragma unroll
+        for (int a = 0; a < 4 * NZ; ++a) acc[a] = 0.f;
+        for (int k = q; k < HID; k += kHeadSlices) {
+            const float hv = BF ? bf16r(hs[r * HS + k]) : hs[r * HS + k];
+#pragma unroll
+            for (int c = 0; c < NZ; ++c) {
+                if (4 * c >= ZS) break;
+                const float4 w = *reinterpret_cast<const float4 *>(wt + k * ZS + 4 * c);
+                acc[4 * c + 0] = fmaf(hv, BF ? bf16r(w.x) : w.x, acc[4 * c + 0]);
+                acc[4 * c + 1] = fmaf(hv, BF ? bf16r(w.y) : w.y, acc[4 * c + 1]);
+                acc[4 * c + 2] = fmaf(hv, BF ? bf16r(w.z) : w.z, acc[4 * c + 2]);
+                acc[4 * c + 3] = fmaf(hv, BF ? bf16r(w.w) : w.w, acc[4 * c + 3]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NZ; ++c)
+            if (4 * c < ZS)
+                *reinterpret_cast<float4 *>(zp + (q * kHeadRows + r) * ZS + 4 * c) =
+                    make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+    }
+    __syncthreads();
+    for (int o = tid; o < kHeadRows * A1; o += 256) {
+        const int r = o / A1, a = o - r * A1;
+        float z = 0.f;
+        for (int q = 0; q < kHeadSlices; ++q) z += zp[(q * kHeadRows + r) * ZS + a];
+        zs[r * ZS + a] = z + (a < A ? P[L.obp + a] : P[L.obv]);
+    }
+    __syncthreads();
+    double acc[kSums];
+#pragma unroll
+    for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
+    const float invB = 1.0f / (float)B;
+    if (tid < kHeadRows && r0 + tid < B && !(dbg & 2)) {
+        const int r = r0 + tid;
+        float zr[AM + 1];
+        float v = 0.f;
+#pragma unroll
+        for (int a = 0; a < AM + 1; ++a) {
+            zr[a] = a < A1 ? zs[tid * ZS + a] : 0.f;
+            if (a == A) v = zr[a];
+        }
+        float *dzr = zs + tid * ZS;     // the row's z (now in zr) is overwritten by its dz
+        cnn_loss_row<AM>(zr, v, my_act, my_olp, my_ov, my_adv, my_ret, meanf, stdf, la, invB, L, dzr, acc);
+        for (int a = 0; a < A1; ++a) dz[(int64_t)r * A1 + a] = dzr[a];
+        for (int a = A1; a < ZS; ++a) dzr[a] = 0.f;
+    } else if (tid < kHeadRows) {
+        for (int a = 0; a < ZS; ++a) zs[tid * ZS + a] = 0.f;
+    }
+    wg_reduce<kSums>(acc, sred);      // its barriers publish zs (now dz) too
+    if (tid == 0)
+        for (int q = 0; q < kSums; ++q) part[(int64_t)blockIdx.x * kSums + q] = acc[q];
+    float *wp = wpart + (int64_t)blockIdx.x * head_part_stride(L);
+    for (int j = tid; j < HID && !(dbg & 4); j += 256) {
+        float w[4 * NZ];
+#pragma unroll
+        for (int c = 0; c < NZ; ++c) {
+            const float4 t = 4 * c < ZS ? *reinterpret_cast<const float4 *>(wt + j * ZS + 4 * c)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            w[4 * c] = t.x, w[4 * c + 1] = t.y, w[4 * c + 2] = t.z, w[4 * c + 3] = t.w;
+        }
+        float g[4 * NZ];
+#pragma unroll
+        for (int a = 0; a < 4 * NZ; ++a) g[a] = 0.f;
+        for (int r = 0; r < kHeadRows; ++r) {
+            float d[4 * NZ];
+#pragma unroll
+            for (int c = 0; c < NZ; ++c) {
+                const float4 t = 4 * c < ZS ? *reinterpret_cast<const float4 *>(zs + r * ZS + 4 * c)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                d[4 * c] = t.x, d[4 * c + 1] = t.y, d[4 * c + 2] = t.z, d[4 * c + 3] = t.w;
+            }
+            const float hv = hs[r * HS + j];
+            // dh[r][j] = h > 0 ? sum_a dz[r][a] Wp[a][j] + dz[r][A] Wv[j] : 0 (fp32 weights; the
+            // padding lanes are zero)
+            float sacc = 0.f;
+#pragma unroll
+            for (int a = 0; a < AM; ++a)
+                if (a < A) sacc += d[a] * w[a];
+            float dA = 0.f, wA = 0.f;
+#pragma unroll
+            for (int a = 0; a < 4 * NZ; ++a)
+                if (a == A) dA = d[a], wA = w[a];
+            sacc += dA * wA;
+            if (r0 + r < B) dh[(int64_t)(r0 + r) * HID + j] = hv > 0.f ? sacc : 0.f;
+            // this workgroup's share of dWh[a][j] = sum_r dz[r][a] h[r][j] (rows in order)
+            const float hb = BF ? bf16r(hv) : hv;
+#pragma unroll
+            for (int a = 0; a < 4 * NZ; ++a) g[a] = fmaf(BF ? bf16r(d[a]) : d[a], hb, g[a]);
+        }
+#pragma unroll
+        for (int a = 0; a < 4 * NZ; ++a)
+            if (a < A1) wp[a * (HID + 1) + j] = g[a];
+    }
+    if (tid < A1) {     // the bias column: sum of the (unrounded) dz rows
+        float sb = 0.f;
+        for (int r = 0; r < kHeadRows; ++r) sb += zs[r * ZS + tid];
+        wp[tid * (HID + 1) + HID] = sb;
+    }
+}
+
+// [dWh | dbh] = the k_cnn_head_loss partials summed in workgroup order (64 outputs per workgroup,
+// 4 thread groups over contiguous partial ranges, combined in group order); the last workgroup
+// writes the minibatch record (and sets the KL stop)
+__global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__ wpart, int nparts, CnnLayout L,
+                                                       float *__restrict__ G, const double *__restrict__ part, int B,
+                                                       LossArgs la, float *__restrict__ metrics,
+                                                       int32_t *__restrict__ stop)
+{
+    __shared__ float red[4][64];
+    const int tid = threadIdx.x, HID = L.HID, A = L.A;
+    const int64_t nout = head_part_stride(L);
+    if ((int64_t)blockIdx.x * 64 >= nout) {
+        // the record: the 13 loss sums over the partials, 16 threads per sum (strided, in order),
+        // then the 16 in order; thread 0 writes it from a one-partial view of the totals
+        __shared__ double msum[kSums][16];
+        __shared__ double tot[kSums];
+        if (tid < kSums * 16) {
+            const int q = tid >> 4, j = tid & 15;
+            double v = 0.0;
+            for (int b = j; b < nparts; b += 16) v += part[(int64_t)b * kSums + q];
+            msum[q][j] = v;
+        }
+        __syncthreads();
+        if (tid < kSums) {
+            double v = 0.0;
+            for (int j = 0; j < 16; ++j) v += msum[tid][j];
+            tot[tid] = v;
+        }
+        __syncthreads();
+        if (tid == 0) cnn_write_metrics(tot, 1, B, la, metrics, stop);
+        return;
+    }
+    if (stop && *stop) return;
+    const int o = tid & 63, g = tid >> 6;
+    const int64_t out = (int64_t)blockIdx.x * 64 + o;
+    const int64_t oc = out < nout ? out : nout - 1;
+    const int w0 = (g * nparts) / 4, w1 = ((g + 1) * nparts) / 4;
+    float sacc = 0.f;
+    constexpr int NB = 8;
+    for (int w = w0; w < w1; w += NB) {
+        float t[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) t[j] = wpart[(int64_t)min(w + j, w1 - 1) * nout + oc];
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+            if (w + j < w1) sacc += t[j];
+    }
+    red[g][o] = sacc;
+    __syncthreads();
+    if (g == 0 && out < nout) {
+        const float v = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+        const int a = (int)(out / (HID + 1)), c = (int)(out - (int64_t)a * (HID + 1));
+        const int64_t dst = c < HID ? (a < A ? L.oWp + (int64_t)a * HID + c : L.oWv + c) : (a < A ? L.obp + a : L.obv);
+        G[dst] = v;
     }
 }
 
@@ -624,16 +957,48 @@ __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__
     if (stop && *stop) return;
     __shared__ double sred[5 * (256 + 16)];
     double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const double g = (double)G[i];
+    // float4 chunks (G is 256-B aligned), NB of them in flight per thread, then the scalar tail
+    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
+    constexpr int NB = 8;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += stride * NB) {
+        float4 t[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) t[j] = reinterpret_cast<const float4 *>(G)[min(i0 + stride * j, n4 - 1)];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int64_t i = i0 + stride * j;
+            if (i >= n4) continue;
+            const float e[4] = {t[j].x, t[j].y, t[j].z, t[j].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t k = 4 * i + q;
+                const double g = (double)e[q];
+                s[0] += g * g;
+                s[1 + (k >= cut0) + (k >= cut1) + (k >= cut2)] += g * g;
+            }
+        }
+    }
+    for (int64_t k = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) {
+        const double g = (double)G[k];
         s[0] += g * g;
-        s[1 + (i >= cut0) + (i >= cut1) + (i >= cut2)] += g * g;
+        s[1 + (k >= cut0) + (k >= cut1) + (k >= cut2)] += g * g;
     }
     wg_reduce<5>(s, sred);
     if (threadIdx.x < 5) part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s[threadIdx.x];
 }
 
-// ---- clip coefficient from the partials (every block, fixed order) + Adam (torch single-tensor)
+// one parameter of torch.optim.Adam's single-tensor step on the clipped gradient (IEEE sqrt and
+// divisions as torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step * m / denom)
+__device__ __forceinline__ float adam_flat(float g, float &m, float &v, float p, const AdamArgs &aa)
+{
+    m = m + aa.one_minus_b1 * (g - m);
+    v = v * aa.b2 + (aa.one_minus_b2 * g) * g;
+    const float denom = sqrtf(v) / aa.bc2_sqrt + aa.eps;
+    return p + aa.neg_step_size * (m / denom);
+}
+
+// ---- clip coefficient from the partials (every block, fixed order) + Adam (torch single-tensor):
+// one float4 of parameters per thread (grid = ceil(n / 1024)), the scalar tail by the last block
 __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, float *__restrict__ G,
                                                         float *__restrict__ M, float *__restrict__ V, int64_t n,
                                                         const double *__restrict__ part, int nparts, AdamArgs aa,
@@ -649,14 +1014,24 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     __shared__ double sred[256 + 16];
     __shared__ float s_coef;
+    const int64_t n4 = n / 4, i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // this thread's parameters first (clamped, unconditional), then the norm partials
+    const int64_t ic = i < n4 ? i : (n4 > 0 ? n4 - 1 : 0);
+    float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), m4 = g4, v4 = g4, p4 = g4;
+    if (n4 > 0) {
+        g4 = reinterpret_cast<const float4 *>(G)[ic];
+        m4 = reinterpret_cast<const float4 *>(M)[ic];
+        v4 = reinterpret_cast<const float4 *>(V)[ic];
+        p4 = reinterpret_cast<const float4 *>(Pm)[ic];
+    }
     double s[1] = {0.0};
-    for (int i = threadIdx.x; i < nparts; i += 256) s[0] += part[i];
+    for (int k = threadIdx.x; k < nparts; k += 256) s[0] += part[k];
     wg_reduce<1>(s, sred);
     if (blockIdx.x == gridDim.x - 1 && metrics) {     // per-component norms (utils/models.py:196-230)
         double c[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int i = threadIdx.x; i < nparts; i += 256)
+        for (int k = threadIdx.x; k < nparts; k += 256)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) c[k] += part[(int64_t)(1 + k) * nparts + i];
+            for (int q = 0; q < 4; ++q) c[q] += part[(int64_t)(1 + q) * nparts + k];
         __shared__ double cred[4 * (256 + 16)];
         wg_reduce<4>(c, cred);
         if (threadIdx.x == 0) {
@@ -680,17 +1055,25 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     __syncthreads();
     const float coef = s_coef;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const float g = G[i] * coef;
-        G[i] = g;
-        float m = M[i], v = V[i];
-        m = m + aa.one_minus_b1 * (g - m);
-        v = v * aa.b2 + (aa.one_minus_b2 * g) * g;
-        const float denom = sqrtf(v) / aa.bc2_sqrt + aa.eps;
-        Pm[i] = Pm[i] + aa.neg_step_size * (m / denom);
-        M[i] = m;
-        V[i] = v;
+    if (i < n4) {
+        float g[4] = {g4.x * coef, g4.y * coef, g4.z * coef, g4.w * coef};
+        float m[4] = {m4.x, m4.y, m4.z, m4.w}, v[4] = {v4.x, v4.y, v4.z, v4.w}, p[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = adam_flat(g[q], m[q], v[q], p[q], aa);
+        reinterpret_cast<float4 *>(G)[i] = make_float4(g[0], g[1], g[2], g[3]);
+        reinterpret_cast<float4 *>(M)[i] = make_float4(m[0], m[1], m[2], m[3]);
+        reinterpret_cast<float4 *>(V)[i] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4 *>(Pm)[i] = make_float4(p[0], p[1], p[2], p[3]);
     }
+    if (blockIdx.x == gridDim.x - 1)
+        for (int64_t k = 4 * n4 + threadIdx.x; k < n; k += 256) {
+            const float g = G[k] * coef;
+            G[k] = g;
+            float m = M[k], v = V[k];
+            Pm[k] = adam_flat(g, m, v, Pm[k], aa);
+            M[k] = m;
+            V[k] = v;
+        }
 }
 
 // ------------------------------------------------------------------------------------
@@ -726,8 +1109,8 @@ ConvGeom geom1(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.H, L.W
 ConvGeom geom2(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h1, L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, L.c2}; }
 ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.w2, L.c2, L.k3, L.s3, L.h3, L.w3, L.c3}; }
 
-// conv trunk + fc + heads for R rows: obs rows come from the u8 buffer through idx (or 0..R)
-int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s)
+// conv trunk + fc for R rows (h): obs rows come from the u8 buffer through idx (or 0..R)
+int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s)
 {
     int rc;
     if (conv1_lds_supported(L.C, L.H, L.W)) {
@@ -756,15 +1139,25 @@ int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, c
             return rc;
         if ((rc = sum_parts(s, w.parts, sf, R * L.HID, w.h, P + L.obf, L.HID, true))) return rc;
     }
-    // heads: z[r][0:A] = h Wp^T, z[r][A] = h Wv^T (row stride A+1); biases are added where z is read
+    return GS_OK;
+}
+
+// conv trunk + fc + heads: z[r][0:A] = h Wp^T, z[r][A] = h Wv^T (row stride A+1); the biases are
+// added where z is read
+int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s)
+{
+    int rc = forward_trunk(P, L, fs, R, w, s);
+    if (rc) return rc;
     return heads_fwd(s, R, L.HID, L.A, w.h, P + L.oWp, P + L.oWv, w.z, w.parts, splits_for(R, L.A + 1, L.HID));
 }
+
+int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
+                   const int32_t *stop, hipStream_t s);
 
 int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
              const int32_t *stop, hipStream_t s)
 {
     int rc;
-    const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
     // head grads: [dW | db][a] = dz[:, a]^T [h | 1] for a in [0, A] (policy rows, then the
     // value row); split-K partials summed straight into the parameter blocks
     {
@@ -777,6 +1170,16 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
             return rc;
     }
     hipLaunchKernelGGL(k_cnn_dh, dim3(nblk(B * L.HID)), dim3(256), 0, s, w.dz, P, L, w.h, B, w.dh, stop);
+    return backward_trunk(P, L, fs, B, w, G, stop, s);
+}
+
+// the trunk's backward from dh (fc, then the convolutions)
+int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
+                   const int32_t *stop, hipStream_t s)
+{
+    int rc;
+    (void)stop;
+    const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
     // fc: [dWf | dbf] = dh^T [a3 | 1]
     {
         const int sw = splits_for(L.HID, L.F + 1, B);
@@ -784,9 +1187,10 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
         if ((rc = sum_parts_wb(s, w.parts, sw, (int64_t)L.HID * (L.F + 1), L.HID, L.F, G + L.oWf, G + L.obf)))
             return rc;
     }
-    if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr, false)))
+    // da3 = (dh Wf) masked by relu'(a3) in the GEMM's epilogue
+    if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr, false,
+                       1, 0, w.a3)))
         return rc;
-    hipLaunchKernelGGL(k_relu_mask, dim3(nblk(B * L.F / 4)), dim3(256), 0, s, w.da3, w.a3, B * L.F / 4);
     // conv3 (dY3 = da3 as [m3][c3])
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
         if ((rc = conv23_lds_wgrad(s, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
@@ -870,6 +1274,47 @@ int launch_cnn_loss(const float *z, const float *P, const CnnLayout &L, int64_t 
     return GS_OK;
 }
 
+// the update's fused head + loss pair (k_cnn_head_loss, k_cnn_head_wsum) where its LDS fits
+bool head_fused(const CnnLayout &L, int64_t B)
+{
+    // the kernel's load slots (k_cnn_head_loss staging) and its LDS
+    return head_loss_lds(L) <= 100 * 1024 && L.HID % 4 == 0 && L.HID <= 512 && (int64_t)L.A * L.HID <= 12288 &&
+           B <= 2048 && kHeadRows <= 256;
+}
+
+int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFields &fl, const CnnWs &w,
+                     const LossArgs &la, float *G, float *metrics, int32_t *stop, hipStream_t s)
+{
+    const unsigned nb = (unsigned)((B + kHeadRows - 1) / kHeadRows);
+    const size_t l1 = head_loss_lds(L);
+    const bool bf = cnn_bf16();
+    auto go = [&](auto am, auto bfc) {
+        constexpr int AM = decltype(am)::value;
+        constexpr bool BF = decltype(bfc)::value;
+        static std::once_flag attrs;      // > 64 KB of dynamic LDS (the update is never graph-captured)
+        std::call_once(attrs, [] {
+            (void)hipFuncSetAttribute((const void *)k_cnn_head_loss<AM, BF>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
+        });
+        hipLaunchKernelGGL((k_cnn_head_loss<AM, BF>), dim3(nb), dim3(256), l1, s, w.h, P, L, (int)B, fl, la, w.dz,
+                           w.dh, w.parts, w.loss_part, stop,
+                           getenv("GS_HL_DBG") ? atoi(getenv("GS_HL_DBG")) : 0);
+        GS_LAUNCH_CHECK("k_cnn_head_loss");
+        return GS_OK;
+    };
+    using F = std::false_type;
+    using T = std::true_type;
+    int rc;
+    if (L.A <= 18) rc = bf ? go(std::integral_constant<int, 18>{}, T{}) : go(std::integral_constant<int, 18>{}, F{});
+    else rc = bf ? go(std::integral_constant<int, kAMax>{}, T{}) : go(std::integral_constant<int, kAMax>{}, F{});
+    if (rc) return rc;
+    const int64_t nout = head_part_stride(L);
+    hipLaunchKernelGGL(k_cnn_head_wsum, dim3((unsigned)((nout + 63) / 64 + 1)), dim3(256), 0, s, w.parts, (int)nb, L,
+                       G, w.loss_part, (int)B, la, metrics, stop);
+    GS_LAUNCH_CHECK("k_cnn_head_wsum");
+    return GS_OK;
+}
+
 int validate_cnn_update(const gs_cnn_dims &dims, const gs_rollout_view_u8 &ro, int64_t B, const void *ws)
 {
     int rc = check_cnn(dims);
@@ -888,12 +1333,20 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
 {
     int rc;
     const FrameSrc fs{ro.obs, idx, ro.T, ro.N};
-    hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions, ro.logprobs,
-                       ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
-    GS_LAUNCH_CHECK("k_gather_fields");
-    if ((rc = forward(P, L, fs, B, w, s))) return rc;
-    if ((rc = launch_cnn_loss(w.z, P, L, B, w, loss_args(hp), w.dz, metrics, stop, s))) return rc;
-    if ((rc = backward(P, L, fs, B, w, G, stop, s))) return rc;
+    if (head_fused(L, B)) {
+        const CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
+        if ((rc = forward_trunk(P, L, fs, B, w, s))) return rc;
+        if ((rc = launch_head_loss(P, L, B, fl, w, loss_args(hp), G, metrics, stop, s))) return rc;
+        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s))) return rc;
+    } else {
+        hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
+                           ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv,
+                           w.f_ret);
+        GS_LAUNCH_CHECK("k_gather_fields");
+        if ((rc = forward(P, L, fs, B, w, s))) return rc;
+        if ((rc = launch_cnn_loss(w.z, P, L, B, w, loss_args(hp), w.dz, metrics, stop, s))) return rc;
+        if ((rc = backward(P, L, fs, B, w, G, stop, s))) return rc;
+    }
     AdamArgs aa = adam_args(hp, adam_step);
     if (comm) {
         int world = 1;
@@ -902,8 +1355,8 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     }
     hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
                        L.oWv);
-    hipLaunchKernelGGL(k_clip_adam_flat, dim3(1024), dim3(256), 0, s, P, G, Mm, Vv, L.P, w.norm_part, kNormBlocks,
-                       aa, metrics, stop);
+    hipLaunchKernelGGL(k_clip_adam_flat, dim3((unsigned)((L.P / 4 + 255) / 256 + 1)), dim3(256), 0, s, P, G, Mm, Vv,
+                       L.P, w.norm_part, kNormBlocks, aa, metrics, stop);
     GS_LAUNCH_CHECK("k_clip_adam_flat");
     return GS_OK;
 }
@@ -979,6 +1432,8 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     if (rc) return rc;
     GS_REQUIRE(n_minibatches >= 0 && adam_step0 >= 0, "bad n_minibatches/adam_step0");
     GS_REQUIRE(params && grads && adam_m && adam_v && idx && metrics, "gs_cnn_ppo_update: null buffer");
+    GS_REQUIRE((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)adam_m | (uintptr_t)adam_v) & 15) == 0,
+               "gs_cnn_ppo_update: params / grads / adam_m / adam_v must be 16-byte aligned");
     GS_REQUIRE(ro.T * ro.N < ((int64_t)1 << 31), "rollout larger than 2^31 samples");
     // GS_HP_BF16: bf16 MFMA operands in every convolution / GEMM launch of this update
     const Bf16Scope prec((hp.flags & GS_HP_BF16) != 0);

@@ -29,10 +29,12 @@ struct FrameSrc {
 // Dense row-major GEMM: C[M][N] = op(A) op(B) (+ beta C) (+ bias[n]) (ReLU), with
 // op(A)[m][k] = TA ? A[k*lda + m] : A[m*lda + k], op(B)[k][n] = TB ? B[n*ldb + k] : B[k*ldb + n].
 // splits > 1: K is cut into `splits` slices; slice z writes its partial product to
-// C + z*sC (beta/bias/relu must then be off) — the caller sums them in a fixed order.
+// C + z*sC (beta/bias/relu/mask must then be off) — the caller sums them in a fixed order.
+// mask (leading dimension ldc): C[m][n] is kept only where mask[m][n] > 0 (relu' of the
+// activation the product is the gradient of), zero elsewhere.
 int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
              const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu,
-             int splits = 1, int64_t sC = 0);
+             int splits = 1, int64_t sC = 0, const float *mask = nullptr);
 
 // out[r,oy,ox,co] = relu(bias[co] + sum_{c,ky,kx} W[co][c][ky][kx] * frame[c][oy*s+ky][ox*s+kx] / 255)
 int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out);

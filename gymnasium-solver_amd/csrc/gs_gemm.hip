@@ -134,7 +134,8 @@ struct U8PatchOp {
 template <int BM, int BN, int WGM, class AOp, bool A_K, class BOp, bool B_K, bool ASUM = false, bool BF = false>
 __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, int K, int kchunk,
                                               float *__restrict__ C, int ldc, int64_t sC, float beta,
-                                              const float *__restrict__ bias, int relu)
+                                              const float *__restrict__ bias, int relu,
+                                              const float *__restrict__ mask)
 {
     constexpr int WGN = 4 / WGM;
     constexpr int WM = BM / WGM, WN = BN / WGN;      // per-wave block
@@ -287,6 +288,7 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
                 if (beta != 0.0f) x += beta * C[(int64_t)gm * ldc + gn];
                 x += bn;
                 if (relu) x = x > 0.0f ? x : 0.0f;
+                if (mask) x = mask[(int64_t)gm * ldc + gn] > 0.0f ? x : 0.0f;     // relu' of a stored activation
                 C[(int64_t)gm * ldc + gn] = x;
             }
         }
@@ -294,17 +296,17 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
 
 template <int BM, int BN, int WGM, bool A_K, bool B_K, bool ASUM = false, class AOp, class BOp>
 int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
-           int64_t ldc, int64_t sC, float beta, const float *bias, bool relu)
+           int64_t ldc, int64_t sC, float beta, const float *bias, bool relu, const float *mask)
 {
     const int64_t per = (K + splits - 1) / splits;
     const int64_t kchunk = (per + BK - 1) / BK * BK;
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
     if (cnn_bf16())
         hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K, ASUM, true>), grid, dim3(256), 0, s, a, b, (int)M,
-                           (int)N, (int)K, (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0);
+                           (int)N, (int)K, (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0, mask);
     else
         hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K, ASUM>), grid, dim3(256), 0, s, a, b, (int)M, (int)N,
-                           (int)K, (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0);
+                           (int)K, (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0, mask);
     GS_LAUNCH_CHECK("k_gemm");
     return GS_OK;
 }
@@ -313,14 +315,18 @@ int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int6
 // tiny M (weight gradients of 32 / 64 output channels) flat ones
 template <bool A_K, bool B_K, bool ASUM = false, class AOp, class BOp>
 int dispatch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
-             int64_t ldc, int64_t sC, float beta, const float *bias, bool relu)
+             int64_t ldc, int64_t sC, float beta, const float *bias, bool relu, const float *mask = nullptr)
 {
-    if (N <= 32) return launch<256, 32, 4, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    if (M <= 32) return launch<32, 128, 1, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    if (N <= 64) return launch<128, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (N <= 32)
+        return launch<256, 32, 4, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    if (M <= 32)
+        return launch<32, 128, 1, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    if (N <= 64)
+        return launch<128, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
     const int64_t big_tiles = ((M + 127) / 128) * ((N + 127) / 128) * splits;
-    if (big_tiles >= 512) return launch<128, 128, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    return launch<64, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (big_tiles >= 512)
+        return launch<128, 128, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    return launch<64, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
 }
 
 DenseOp dense(const float *p, int64_t ld, int64_t n_outer, int64_t n_inner)
@@ -432,17 +438,17 @@ int sum_parts(hipStream_t s, const float *parts, int np, int64_t n, float *out, 
 
 int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
              const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu, int splits,
-             int64_t sC)
+             int64_t sC, const float *mask)
 {
     GS_REQUIRE(M > 0 && N > 0 && K > 0 && splits > 0, "gemm_f32: empty problem");
     GS_REQUIRE(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gemm_f32: dimension too large");
-    GS_REQUIRE(splits == 1 || (beta == 0.0f && !bias && !relu), "gemm_f32: split-K partials take no epilogue");
+    GS_REQUIRE(splits == 1 || (beta == 0.0f && !bias && !relu && !mask), "gemm_f32: split-K partials take no epilogue");
     const DenseOp a = ta ? dense(A, lda, K, M) : dense(A, lda, M, K);
     const DenseOp b = tb ? dense(B, ldb, N, K) : dense(B, ldb, K, N);
-    if (!ta && !tb) return dispatch<true, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    if (!ta && tb) return dispatch<true, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    if (ta && !tb) return dispatch<false, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
-    return dispatch<false, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu);
+    if (!ta && !tb) return dispatch<true, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    if (!ta && tb) return dispatch<true, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    if (ta && !tb) return dispatch<false, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    return dispatch<false, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
 }
 
 int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out)

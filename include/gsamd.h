@@ -330,7 +330,8 @@ int gs_cnn_policy_act(const float *params_dev, gs_cnn_dims dims, const uint8_t *
 int gs_cnn_ppo_loss(const float *params_dev, gs_cnn_dims dims, gs_ppo_hparams hp, gs_rollout_view_u8 rollout,
                     const int32_t *idx_dev, int64_t batch, float *metrics_dev, float *dlogits_dev,
                     void *workspace_dev, void *stream);
-/* n_minibatches fused steps (forward, loss, backward, optional all-reduce, clip, Adam). */
+/* n_minibatches fused steps (forward, loss, backward, optional all-reduce, clip, Adam).
+ * params / grads / adam_m / adam_v: 16-byte aligned (the clip + Adam kernel moves float4s). */
 int gs_cnn_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev, gs_cnn_dims dims,
                       gs_ppo_hparams hp, gs_rollout_view_u8 rollout, const int32_t *idx_dev, int64_t batch,
                       int64_t n_minibatches, int64_t adam_step0, float *metrics_dev, int32_t *stop_flag_dev,

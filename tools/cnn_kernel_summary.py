@@ -27,8 +27,17 @@ PEAK_F32_MFMA = 157.3     # TFLOP/s, dense fp32 matrix (MI355X_MICROARCH.md)
 PEAK_BF16_MFMA = 2500.0   # TFLOP/s, dense bf16 matrix
 PEAK_HBM = 8000.0         # GB/s
 
-# position in the minibatch -> (label, expected kernel)
-SEQ = [("gather_fields", "k_gather_fields"), ("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"),
+# position in the minibatch -> (label, expected kernel): the fused head + loss pair (round 3)
+SEQ_FUSED = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"),
+             ("conv3_fwd", "k_conv_fwd"), ("fc_fwd", "k_gemm"), ("fc_fwd_splitk_sum", "k_sum_parts_ep"),
+             ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
+             ("fc_wgrad", "k_gemm"), ("fc_wgrad_splitk_sum", "k_sum_parts_wb"), ("fc_dgrad_relu_mask", "k_gemm"),
+             ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts_wb"),
+             ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
+             ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
+             ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
+# the separate heads GEMMs, loss and dh kernels (round-3 first build)
+SEQ_SPLIT = [("gather_fields", "k_gather_fields"), ("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"),
        ("conv3_fwd", "k_conv_fwd"), ("fc_fwd", "k_gemm"), ("fc_fwd_splitk_sum", "k_sum_parts_ep"),
        ("heads_fwd", "k_gemm"), ("heads_fwd_splitk_sum", "k_sum_parts_ep"), ("loss_rows", "k_cnn_loss"),
        ("loss_final", "k_cnn_loss_final"), ("heads_wgrad", "k_gemm"), ("heads_wgrad_sum_policy", "k_sum_parts_wb"),
@@ -38,6 +47,7 @@ SEQ = [("gather_fields", "k_gather_fields"), ("conv1_fwd", "k_conv1_fwd"), ("con
        ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"), ("conv2_dgrad", "k_conv_dgrad"),
        ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"), ("norm_partials", "k_norm_partials"),
        ("clip_adam", "k_clip_adam_flat")]
+SEQ = SEQ_FUSED
 
 
 def nature_work(B, A=18, C=4, H=84, W=84):
@@ -55,10 +65,11 @@ def nature_work(B, A=18, C=4, H=84, W=84):
     return {
         "conv1_fwd": (2 * m1, frames + W1 + a1), "conv2_fwd": (2 * m2, a1 + W2 + a2),
         "conv3_fwd": (2 * m3, a2 + W3 + a3), "fc_fwd": (2 * mf, a3 + Wf + hb), "heads_fwd": (2 * mh, hb + Wh + zb),
-        "heads_wgrad": (2 * mh, zb + hb + Wh), "fc_wgrad": (2 * mf, hb + a3 + Wf), "fc_dgrad": (2 * mf, hb + Wf + a3),
+        "heads_wgrad": (2 * mh, zb + hb + Wh), "fc_wgrad": (2 * mf, hb + a3 + Wf), "fc_dgrad": (2 * mf, hb + Wf + a3), "fc_dgrad_relu_mask": (2 * mf, hb + Wf + 2 * a3),
         "conv3_wgrad": (2 * m3, a2 + a3 + W3), "conv3_dgrad": (2 * m3, a3 + W3 + 2 * a2),   # + the ReLU mask read
         "conv2_wgrad": (2 * m2, a1 + a2 + W2), "conv2_dgrad": (2 * m2, a2 + W2 + 2 * a1),
         "conv1_wgrad": (2 * m1, frames + a1 + W1),
+        "head_loss": (4 * mh, hb + Wh + zb + hb),    # z = h Wh^T and the dWh partials (+ dh out)
     }
 
 
@@ -70,7 +81,7 @@ def short(name):
 def minibatches(rows):
     """rows (dicts) in dispatch order -> list of per-minibatch dispatch lists (gs kernels only)."""
     gs = [r for r in rows if short(r["Kernel_Name"]) is not None]
-    starts = [i for i, r in enumerate(gs) if short(r["Kernel_Name"]) == "k_gather_fields"]
+    starts = [i for i, r in enumerate(gs) if short(r["Kernel_Name"]) == SEQ[0][1]]
     out = []
     for a, b in zip(starts, starts[1:] + [len(gs)]):
         mb = gs[a:b]
@@ -112,7 +123,11 @@ def main():
     ap.add_argument("--bf16", action="store_true", help="the run used GS_HP_BF16 (bf16 MFMA peak)")
     ap.add_argument("--skip", type=int, default=1, help="warm minibatches to drop")
     a = ap.parse_args()
-    trace = minibatches(load_trace(one(os.path.join(a.dir, "cnn_stats", "**", "*kernel_trace.csv"))))[a.skip:]
+    global SEQ
+    rows = load_trace(one(os.path.join(a.dir, "cnn_stats", "**", "*kernel_trace.csv")))
+    names = [short(r["Kernel_Name"]) for r in rows if short(r["Kernel_Name"])]
+    SEQ = SEQ_FUSED if "k_cnn_head_loss" in names else SEQ_SPLIT
+    trace = minibatches(rows)[a.skip:]
     fetch = minibatches(load_pmc(one(os.path.join(a.dir, "cnn_fetch", "**", "*counter_collection.csv")),
                                  "FETCH_SIZE"))[a.skip:]
     write = minibatches(load_pmc(one(os.path.join(a.dir, "cnn_write", "**", "*counter_collection.csv")),
