@@ -694,7 +694,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
                                                        CnnLayout L, int B, CnnFields fl, LossArgs la,
                                                        float *__restrict__ dz, float *__restrict__ dh,
                                                        float *__restrict__ wpart, double *__restrict__ part,
-                                                       const int32_t *__restrict__ stop, int dbg)
+                                                       const int32_t *__restrict__ stop)
 {
     constexpr int NZ = (AM + 1 + 3) / 4;               // float4 chunks of a padded head row
     __shared__ double sred[kSums * 256 + kSums * 16];
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     float meanf = 0.f, stdf = 1.f;
     if (la.normalize) batch_adv_stats_regs<NA>(adv_r, B, sred, meanf, stdf);    // its barriers cover the staging
     else __syncthreads();
-    if (!(dbg & 1)) {   // z partials: thread (row r, slice q) over k = q, q + kHeadSlices, ...
+    {   // z partials: thread (row r, slice q) over k = q, q + kHeadSlices, ...
         const int r = tid / kHeadSlices, q = tid % kHeadSlices;
         float acc[4 * NZ];
 #pragma unroll
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 #pragma unroll
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
     const float invB = 1.0f / (float)B;
-    if (tid < kHeadRows && r0 + tid < B && !(dbg & 2)) {
+    if (tid < kHeadRows && r0 + tid < B) {
         const int r = r0 + tid;
         float zr[AM + 1];
         float v = 0.f;
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     if (tid == 0)
         for (int q = 0; q < kSums; ++q) part[(int64_t)blockIdx.x * kSums + q] = acc[q];
     float *wp = wpart + (int64_t)blockIdx.x * head_part_stride(L);
-    for (int j = tid; j < HID && !(dbg & 4); j += 256) {
+    for (int j = tid; j < HID; j += 256) {
         float w[4 * NZ];
 #pragma unroll
         for (int c = 0; c < NZ; ++c) {
@@ -1297,8 +1297,7 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
         });
         hipLaunchKernelGGL((k_cnn_head_loss<AM, BF>), dim3(nb), dim3(256), l1, s, w.h, P, L, (int)B, fl, la, w.dz,
-                           w.dh, w.parts, w.loss_part, stop,
-                           getenv("GS_HL_DBG") ? atoi(getenv("GS_HL_DBG")) : 0);
+                           w.dh, w.parts, w.loss_part, stop);
         GS_LAUNCH_CHECK("k_cnn_head_loss");
         return GS_OK;
     };
