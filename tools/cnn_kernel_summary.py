@@ -157,7 +157,7 @@ def main():
         tot_us += us
         tot_bytes += hbm
         kernels[label] = e
-    flops = sum(f for f, _ in work.values())
+    flops = sum(work[l][0] for l, _ in SEQ if l in work)
     out = {"_note": __doc__.split("\n\n")[1].replace("\n", " "),
            "_source_hash": source_hash(), "batch": a.batch, "operands": "bf16" if a.bf16 else "f32",
            "mfma_peak_TFLOPs": peak, "hbm_peak_GBps": PEAK_HBM, "minibatches_measured": len(trace),
