@@ -298,6 +298,10 @@ bool bwd_xchg_fits(const Layout &L, int64_t B, int colocated = 1);
 int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, const float *part1,
                      const float *sumsq, const AdamArgs &aa, float *metrics, const int32_t *stop, hipStream_t s,
                      bool comp_norms = true);
+// activation statistics parts of the MLP backbone (k_mlp_act_stats): ceil(R/16) x
+// 2 * (2 + max(H1, H2)) doubles
+int launch_act_stats(const float *P, const Layout &L, const float *obs, const int32_t *idx, int64_t T, int64_t N,
+                     int64_t R, double *part, hipStream_t s);
 // fused update, exchange launched behind k_bwd: step ff.k_local's head record from the exchanged G
 int launch_head_sq(const Layout &L, const float *G, float scale, const FusedFwd &ff, hipStream_t s);
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);

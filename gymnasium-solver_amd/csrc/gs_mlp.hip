@@ -2882,6 +2882,85 @@ __global__ __launch_bounds__(256) void k_metrics_all(const double *__restrict__ 
     }
 }
 
+// ---- activation statistics of the backbone's Linear outputs (utils/models.py:120-145: forward
+// hooks on backbone.0 and backbone.2, i.e. the pre-activation values z1 = W1 x + b1 and
+// z2 = W2 relu(z1) + b2; recorded by BaseAgent.training_step, base_agent.py:336-347) for rows
+// idx[0..R) of the rollout (idx null: rows 0..R).  One workgroup per 16 rows writes its part:
+// per layer {sum z, sum z^2} (double) and per neuron the count of |z| < 1e-6; the host adds the
+// parts (gsamd.metrics.activation_stats).  Diagnostics, off the minibatch chain: the agent
+// calls it once per epoch on the epoch's first minibatch with the parameters that minibatch uses.
+constexpr int kActRows = 16;
+__host__ __device__ inline int act_part_stride(const Layout &L) { return 2 * (2 + (L.H1 > L.H2 ? L.H1 : L.H2)); }
+
+__global__ __launch_bounds__(256) void k_mlp_act_stats(const float *__restrict__ P, Layout L,
+                                                       const float *__restrict__ obs, const int32_t *__restrict__ idx,
+                                                       int T, int N, int R, double *__restrict__ part)
+{
+    extern __shared__ float lds[];
+    __shared__ double sred[2 * 272];
+    const int tid = threadIdx.x, D = L.D, H1 = L.H1, H2 = L.H2;
+    const int r0 = blockIdx.x * kActRows, nr = min(kActRows, R - r0);
+    float *xs = lds;                      // [16][D]
+    float *h1s = xs + kActRows * D;       // [16][H1]
+    for (int u = tid; u < kActRows * D; u += 256) {
+        const int r = u / D, d = u - r * D;
+        const int src = r < nr ? (idx ? sample_row(idx[r0 + r], T, N) : r0 + r) : -1;
+        xs[u] = src >= 0 ? obs[(int64_t)src * D + d] : 0.0f;
+    }
+    __syncthreads();
+    double* out = part + (int64_t)blockIdx.x * act_part_stride(L);
+    const int HM = H1 > H2 ? H1 : H2;
+    double st[2] = {0.0, 0.0};
+    for (int n = tid; n < H1; n += 256) {
+        int cnt = 0;
+        for (int r = 0; r < nr; ++r) {
+            float z = P[L.ob1 + n];
+            for (int d = 0; d < D; ++d) z = fmaf(P[L.oW1 + (int64_t)n * D + d], xs[r * D + d], z);
+            st[0] += (double)z;
+            st[1] += (double)z * (double)z;
+            cnt += fabsf(z) < 1e-6f ? 1 : 0;
+            h1s[r * H1 + n] = z > 0.0f ? z : 0.0f;
+        }
+        out[2 + n] = (double)cnt;
+    }
+    block_reduce<2>(st, sred);       // its barriers also publish h1s
+    if (tid == 0) out[0] = st[0], out[1] = st[1];
+    double st2[2] = {0.0, 0.0};
+    for (int n = tid; n < H2; n += 256) {
+        float z[kActRows];
+        const float b = P[L.ob2 + n];
+#pragma unroll
+        for (int r = 0; r < kActRows; ++r) z[r] = b;
+        for (int k = 0; k < H1; ++k) {
+            const float w = P[L.oW2 + (int64_t)n * H1 + k];
+#pragma unroll
+            for (int r = 0; r < kActRows; ++r) z[r] = fmaf(w, h1s[r * H1 + k], z[r]);
+        }
+        int cnt = 0;
+#pragma unroll
+        for (int r = 0; r < kActRows; ++r)
+            if (r < nr) {
+                st2[0] += (double)z[r];
+                st2[1] += (double)z[r] * (double)z[r];
+                cnt += fabsf(z[r]) < 1e-6f ? 1 : 0;
+            }
+        out[2 + HM + 2 + n] = (double)cnt;
+    }
+    block_reduce<2>(st2, sred);
+    if (tid == 0) out[2 + HM] = st2[0], out[2 + HM + 1] = st2[1];
+}
+
+int launch_act_stats(const float *P, const Layout &L, const float *obs, const int32_t *idx, int64_t T, int64_t N,
+                     int64_t R, double *part, hipStream_t s)
+{
+    const size_t lds = sizeof(float) * (size_t)kActRows * (L.D + L.H1);
+    GS_REQUIRE(lds <= 64 * 1024, "activation stats: obs_dim + hidden1 too large");
+    const unsigned nb = (unsigned)((R + kActRows - 1) / kActRows);
+    hipLaunchKernelGGL(k_mlp_act_stats, dim3(nb), dim3(256), lds, s, P, L, obs, idx, (int)T, (int)N, (int)R, part);
+    GS_LAUNCH_CHECK("k_mlp_act_stats");
+    return GS_OK;
+}
+
 // After an exchange launched behind k_bwd (RCCL, or the xGMI kernel): step k's head record from
 // the exchanged gradient in G (role C's sums were of this rank's own gradient), x scale (1/world)
 __global__ __launch_bounds__(256) void k_head_sq(Layout L, const float *__restrict__ G, float scale,

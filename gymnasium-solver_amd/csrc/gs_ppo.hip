@@ -420,6 +420,16 @@ extern "C" int gs_ppo_minibatch_step(float *params, float *grads, float *adam_m,
                         (hipStream_t)stream);
 }
 
+extern "C" int gs_mlp_activation_stats(const float *params, gs_mlp_dims dims, gs_rollout_view ro, const int32_t *idx,
+                                       int64_t rows, double *part, void *stream)
+{
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    GS_REQUIRE(params && ro.obs && part && rows >= 1, "gs_mlp_activation_stats: null buffer or no rows");
+    GS_REQUIRE(idx || rows <= ro.T * ro.N, "gs_mlp_activation_stats: more rows than the rollout holds");
+    return launch_act_stats(params, layout_of(dims), ro.obs, idx, ro.T, ro.N, rows, part, (hipStream_t)stream);
+}
+
 extern "C" int gs_ppo_loss(const float *params, gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view ro,
                            const int32_t *idx, int64_t batch, float *metrics, void *workspace, void *stream)
 {

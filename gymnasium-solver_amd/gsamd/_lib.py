@@ -95,6 +95,7 @@ def _load():
         "gs_ppo_minibatch_step": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64,
                                                  vp, vp, vp, vp, vp]),
         "gs_ppo_loss": (ctypes.c_int, [vp, MlpDims, PPOHparams, RolloutView, vp, i64, vp, vp, vp]),
+        "gs_mlp_activation_stats": (ctypes.c_int, [vp, MlpDims, RolloutView, vp, i64, vp, vp]),
         "gs_ppo_stage": (ctypes.c_int, [ctypes.c_int, vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64,
                                         i64, vp, vp, vp]),
         "gs_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64, i64, vp,
@@ -145,7 +146,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_rollout_synth_supported",
             "gs_rollout_synth", "gs_env_reset", "gs_env_step",
             "gs_episode_stats",
-            "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_ppo_stage", "gs_ppo_update",
+            "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_mlp_activation_stats", "gs_ppo_stage", "gs_ppo_update",
             "gs_ppo_update_global", "gs_ppo_update_workspace_bytes",
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",

@@ -143,3 +143,24 @@ def _scalar(v):
     if a.size == 1 and a.dtype.kind in "biuf":
         return float(a.reshape(()).item())
     return None
+
+
+def activation_stats(parts: np.ndarray, rows: int, hidden: tuple, prefix: str = "backbone",
+                     layer_ids: tuple = (0, 2)) -> Dict[str, float]:
+    """gs_mlp_activation_stats parts (n_parts, 2 * (2 + max(H))) -> the reference's
+    ``opt/activations/<prefix>.<i>/{mean,std,dead_pct,dead_max}`` (utils/models.py:120-145,184-190:
+    mean and unbiased std over all of a Linear layer's outputs, dead_pct / dead_max the mean / max
+    over neurons of the fraction of rows with |z| < 1e-6)."""
+    p = np.asarray(parts, np.float64).reshape(parts.shape[0], 2, -1).sum(axis=0)
+    out: Dict[str, float] = {}
+    for layer, (lid, H) in enumerate(zip(layer_ids, hidden)):
+        n = float(rows) * H
+        s1, s2 = p[layer, 0], p[layer, 1]
+        dead = p[layer, 2:2 + H] / float(rows)
+        name = f"opt/activations/{prefix}.{lid}"
+        out[f"{name}/mean"] = s1 / n
+        out[f"{name}/std"] = math.sqrt(max(0.0, (s2 - s1 * s1 / n) / (n - 1.0)))
+        out[f"{name}/dead_pct"] = float(dead.mean())
+        out[f"{name}/dead_max"] = float(dead.max())
+    return out
+

@@ -32,7 +32,7 @@ from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler, index_stream, rank_share
 from .distributed import allreduce_sum_f64, comm_status, world_active
-from .metrics import NUM_SUMS, MetricsRecorder, ppo_keys, ppo_records, records_from_sums
+from .metrics import NUM_SUMS, MetricsRecorder, activation_stats, ppo_keys, ppo_records, records_from_sums
 from .schedules import SCHEDULABLE, build_schedulers
 
 STAGES = ("train",)
@@ -476,6 +476,7 @@ class DevicePPOAgent:
         if not self.global_mode:
             self.prefetcher.prefetch(epoch + 1)
         buf = collector.buffer
+        self._activation_stats_launch(buf, idx)
         if ev:
             ev[-1][1].record()
         if self.global_mode:
@@ -505,6 +506,29 @@ class DevicePPOAgent:
             self.adam_step += int((self.metrics_buf[:, M["skipped"]] == 0).sum().item())
         self.current_epoch += 1
         self.on_train_epoch_end()
+
+    def _activation_stats_launch(self, buf, idx) -> None:
+        """The reference records opt/activations/backbone.{0,2}/* on every training_step
+        (base_agent.py:336-347, utils/models.py:120-190); the device agent computes them once per
+        epoch, on the epoch's first minibatch with the parameters that minibatch's step reads,
+        on the update's stream ahead of it (gs_mlp_activation_stats; SURVEY §8b: diagnostics
+        may be computed per epoch).  MLP policies; off with track_stats=False."""
+        self._act_pending = False
+        if self.is_pixel or self.global_mode or not self.track_stats or idx is None:
+            return
+        dims = self.policy_model.dims
+        nparts = (self.batch_size + 15) // 16
+        width = 2 * (2 + max(int(dims.hidden1), int(dims.hidden2)))
+        if getattr(self, "_act_parts", None) is None or self._act_parts.numel() != nparts * width:
+            self._act_parts = torch.zeros(nparts * width, dtype=torch.float64, device=self.device)
+        check(lib.gs_mlp_activation_stats(ptr(self.policy_model.params), dims, buf.view(), ptr(idx), self.batch_size,
+                                          ptr(self._act_parts), stream_handle()), "gs_mlp_activation_stats")
+        self._act_pending = True
+
+    def activation_keys(self):
+        if self.is_pixel or self.global_mode or not self.track_stats:
+            return ()
+        return tuple(f"opt/activations/backbone.{i}/{k}" for i in (0, 2) for k in ("mean", "std", "dead_pct", "dead_max"))
 
     def global_shares(self, epoch: int) -> np.ndarray:
         """This rank's rows of every global minibatch of `epoch` (padded with -1): the reference's
@@ -576,6 +600,11 @@ class DevicePPOAgent:
         stepped = rec[rec[:, M["skipped"]] == 0]
         keys, slots = self.grad_norm_keys()
         self.metrics_recorder.record_rows("train", keys, stepped[:, slots])
+        if getattr(self, "_act_pending", False):
+            dims = self.policy_model.dims
+            parts = self._act_parts.cpu().numpy().reshape((self.batch_size + 15) // 16, -1)
+            self.metrics_recorder.record("train", activation_stats(parts, self.batch_size,
+                                                                   (int(dims.hidden1), int(dims.hidden2))))
         if self.config.target_kl is not None and (rec[:, M["kl_stop"]] != 0).any():
             self._early_stop_epoch = True        # sticky, as BaseAgent._early_stop_epoch
         return rec
@@ -583,7 +612,7 @@ class DevicePPOAgent:
     def epoch_metric_keys(self):
         """The fixed key list of epoch_metrics (every rank sends the same vector)."""
         norm = self.config.normalize_advantages == "batch"
-        return tuple(ppo_keys(norm)) + self.grad_norm_keys()[0]
+        return tuple(ppo_keys(norm)) + self.grad_norm_keys()[0] + self.activation_keys()
 
     def epoch_metrics(self) -> Dict[str, float]:
         """The last update's epoch means under the reference's metric keys (ppo_agent.py:131-146,

@@ -218,6 +218,15 @@ int gs_ppo_minibatch_step(float *params_dev, float *grads_dev, float *adam_m_dev
 int gs_ppo_loss(const float *params_dev, gs_mlp_dims dims, gs_ppo_hparams hp, gs_rollout_view rollout,
                 const int32_t *idx_dev, int64_t batch, float *metrics_dev, void *workspace_dev, void *stream);
 
+/* Activation statistics of the MLP backbone (utils/models.py:120-145: hooks on backbone.0 and
+ * backbone.2, i.e. the pre-activation outputs of the two Linear layers; recorded per
+ * training_step, base_agent.py:336-347) over rows idx_dev[0..rows) of the rollout (idx_dev null:
+ * rows 0..rows).  Writes ceil(rows/16) parts of 2 * (2 + max(hidden1, hidden2)) doubles: per layer
+ * {sum z, sum z^2, then per neuron the count of |z| < 1e-6}; the caller adds the parts
+ * (mean, unbiased std, dead_pct = mean over neurons of count / rows, dead_max = max). */
+int gs_mlp_activation_stats(const float *params_dev, gs_mlp_dims dims, gs_rollout_view rollout,
+                            const int32_t *idx_dev, int64_t rows, double *parts_dev, void *stream);
+
 /* Enqueue ONE stage of a minibatch step on the current workspace.  Unfused chain:
  * 0 = k_fwd_hidden, 1 = k_loss, 2 = k_bwd, 3 = k_clip_adam.  Fused chain (the one
  * gs_ppo_update runs for the compile-time shapes): 6 = k_gather_all for a one-minibatch

@@ -186,6 +186,19 @@ def test_ppo_step_vs_reference(golden, cuda, tag):
                       ("opt/ppo/kl", "kl"), ("opt/ppo/approx_kl", "approx_kl"),
                       ("roll/adv/norm/std", "adv_norm_std")]:
         np.testing.assert_allclose(mm[M[slot]], ref[key], atol=2e-6, rtol=1e-5, err_msg=key)
+    # the backbone's activation statistics (utils/models.py:120-190), as the reference's hooks
+    # recorded them on this batch (tests/golden/make_golden.py: compute_activation_stats)
+    from gsamd.metrics import activation_stats
+    nparts = (B + 15) // 16
+    parts = torch.zeros(nparts * 2 * (2 + max(H1, H2)), dtype=torch.float64, device=cuda)
+    check(lib.gs_mlp_activation_stats(params.data_ptr(), dims, view, idx.data_ptr(), B, parts.data_ptr(), s),
+          "gs_mlp_activation_stats")
+    torch.cuda.synchronize()
+    acts = activation_stats(parts.cpu().numpy().reshape(nparts, -1), B, (H1, H2))
+    aref = dict(zip([str(x) for x in z[f"{tag}/activation_names"]], z[f"{tag}/activation_values"]))
+    assert set(acts) == set(aref)
+    for key, val in aref.items():
+        np.testing.assert_allclose(acts[key], val, rtol=2e-5, atol=1e-7, err_msg=key)
     check(lib.gs_ppo_minibatch_step(params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), dims, hp, view,
                                     idx.data_ptr(), B, 1, met.data_ptr(), stop.data_ptr(), ws.data_ptr(), None, s))
     torch.cuda.synchronize()

@@ -316,3 +316,34 @@ def test_records_from_sums_match_the_reference_record(golden):
                       ("opt/value/explained_var", "explained_var"), ("opt/ppo/kl", "kl"),
                       ("opt/ppo/approx_kl", "approx_kl"), ("roll/adv/norm/std", "adv_norm_std")]:
         np.testing.assert_allclose(rec[M[slot]], ref[key], rtol=1e-5, atol=2e-6, err_msg=key)
+
+
+@pytest.mark.parametrize("tag", ["cartpole", "lunar_ent"])
+def test_activation_stats_reduction_matches_the_reference_hooks(golden, tag):
+    """gsamd.metrics.activation_stats (the host half of gs_mlp_activation_stats) on parts made from
+    the fixture batch's pre-activation outputs (numpy, f32 forward): the reference's hook values
+    (utils/models.py:120-190: mean, unbiased std, dead_pct / dead_max over neurons)."""
+    from gsamd.metrics import activation_stats
+    z = golden("ppo_step.npz")
+    D, H1, H2, A, B = (int(x) for x in z[f"{tag}/dims"])
+    p = z[f"{tag}/params0"].astype(np.float32)
+    o = 0
+    W1 = p[o:o + H1 * D].reshape(H1, D); o += H1 * D
+    b1 = p[o:o + H1]; o += H1
+    W2 = p[o:o + H2 * H1].reshape(H2, H1); o += H2 * H1
+    b2 = p[o:o + H2]
+    z1 = z[f"{tag}/obs"].astype(np.float32) @ W1.T + b1
+    z2 = np.maximum(z1, 0.0) @ W2.T + b2
+    HM = max(H1, H2)
+    part = np.zeros((1, 2 * (2 + HM)))
+    for layer, zz in enumerate((z1, z2)):
+        base = layer * (2 + HM)
+        zd = zz.astype(np.float64)
+        part[0, base] = zd.sum()
+        part[0, base + 1] = (zd * zd).sum()
+        part[0, base + 2:base + 2 + zz.shape[1]] = (np.abs(zz) < 1e-6).sum(axis=0)
+    acts = activation_stats(part, B, (H1, H2))
+    ref = dict(zip([str(x) for x in z[f"{tag}/activation_names"]], z[f"{tag}/activation_values"]))
+    assert set(acts) == set(ref)
+    for k, v in ref.items():
+        np.testing.assert_allclose(acts[k], v, rtol=2e-5, atol=1e-7, err_msg=k)

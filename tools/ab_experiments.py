@@ -31,4 +31,19 @@ EXPERIMENTS = {
                      "                    t[j][b] = b == 0 ? ld4(af.part1, min(tid + 256 * j, nq1 - 1)) : z4;")],
     # x / h1 stores after the heads, as with 256 threads
     "late_x_h1": [("gs_mlp.hip", "    constexpr bool kEarly = NT == 512;", "    constexpr bool kEarly = false;")],
+    # k_bwd grid padded to a multiple of 8 (the extra workgroups exit at once): every kernel of the
+    # chain then has a grid that is a multiple of the XCD count
+    "pad_bwd8": [("gs_mlp.hip",
+                  "    const unsigned nblk = (unsigned)(sh0.nA + sh0.nB + sh0.nC);",
+                  "    const unsigned nblk = (unsigned)((sh0.nA + sh0.nB + sh0.nC + 7) / 8 * 8);"),
+                 ("gs_mlp.hip",
+                  "    GS_SPAN_T0\n    if (stop && *stop) return;\n    // multi-GPU: every output value goes through bwd_exchange",
+                  "    {\n        const BwdShape s0 = BwdShape::make(S::lay(Lrt), S::batch(Brt));\n"
+                  "        if ((int)blockIdx.x >= s0.nA + s0.nB + s0.nC) return;\n    }\n"
+                  "    GS_SPAN_T0\n    if (stop && *stop) return;\n    // multi-GPU: every output value goes through bwd_exchange")],
+    # role A tile (n-block, k-group) by n-block fastest: the 8 workgroups of an n-block share an XCD
+    # with the forward workgroups that read their dW2 rows (with pad_bwd8)
+    "roleA_xcd": [("gs_mlp.hip",
+                   "        const int nb = bid / nkg, kb = (bid - nb * nkg) * sh.ka;   // first of the ka k-blocks",
+                   "        const int nb = bid % sh.ncb, kb = (bid / sh.ncb) * sh.ka;   // first of the ka k-blocks")],
 }
