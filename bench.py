@@ -519,6 +519,28 @@ def main():
         grid = (gN // ew) * (8 if ew >= 8 else 4) * 64
         rooflines["gae"]["traffic"] = pmc.get(f"k_gae_staged[grid={grid}]", {}).get("hbm_bytes_per_launch")
     roofline["traffic_source"] = traffic_src
+    if pixel and args.workload == "C4":
+        # the C4 minibatch's HBM bytes: the per-kernel PMC passes (tools/cnn_kernel_summary.py over
+        # tools/cnn_kernel_run.py, profiles/c4_kernels.json), again only from the current sources
+        kpath = os.path.join(ROOT, "profiles", "c4_kernels.json")
+        kern = {}
+        if os.path.exists(kpath):
+            try:
+                with open(kpath) as f:
+                    kern = json.load(f)
+            except (OSError, ValueError):
+                kern = {}
+        ksrc = {"file": "profiles/c4_kernels.json", "recorded_source_hash": kern.get("_source_hash"),
+                "library_source_hash": source_hash(), "operands": kern.get("operands")}
+        ksrc["current"] = bool(kern) and ksrc["recorded_source_hash"] == ksrc["library_source_hash"] and \
+            kern.get("operands") == ("bf16" if args.dtype == "bf16" else "f32")
+        if ksrc["current"]:
+            mb = kern.get("minibatch", {})
+            roofline["traffic"] = mb.get("hbm_bytes")
+            roofline["kernels"] = {k: {q: e.get(q) for q in ("avg_us", "mfma_frac", "hbm_frac", "traffic_over_alg")
+                                       if e.get(q) is not None}
+                                   for k, e in kern.get("kernels", {}).items()}
+        roofline["traffic_source"] = ksrc
 
     # ---- bf16 mode: one whole update in fp32 and in bf16 from the same state, rollout and
     #      sampler order; the per-minibatch loss deviation is reported beside the line ----

@@ -23,8 +23,9 @@ def main():
     ap.add_argument("--mb", type=int, default=6)
     ap.add_argument("--n-envs", type=int, default=256)
     ap.add_argument("--workload", default="ALE-Pong-v5")
+    ap.add_argument("--bf16", action="store_true", help="GS_HP_BF16 (bf16 MFMA operands)")
     a = ap.parse_args()
-    from gsamd._lib import check, lib, ptr, stream_handle
+    from gsamd._lib import GS_HP_BF16, check, lib, ptr, stream_handle
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(42)
@@ -34,9 +35,12 @@ def main():
     coll.collect()
     idx = agent.prefetcher.upload(0)
     pm = agent.policy_model
+    hp = agent.hparams()
+    if a.bf16:
+        hp.flags = GS_HP_BF16
     for n in (1, a.mb):     # one warm minibatch, then the measured ones
         check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
-                                    agent.hparams(), coll.buffer.view(), ptr(idx), agent.batch_size, n, 0,
+                                    hp, coll.buffer.view(), ptr(idx), agent.batch_size, n, 0,
                                     ptr(agent.metrics_buf), ptr(agent.stop_flag), ptr(agent.workspace), None,
                                     stream_handle()), "gs_cnn_ppo_update")
     torch.cuda.synchronize()

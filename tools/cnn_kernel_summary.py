@@ -122,15 +122,16 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--bf16", action="store_true", help="the run used GS_HP_BF16 (bf16 MFMA peak)")
     ap.add_argument("--skip", type=int, default=1, help="warm minibatches to drop")
+    ap.add_argument("--prefix", default="cnn", help="run directories <prefix>_stats / _fetch / _write")
     a = ap.parse_args()
     global SEQ
-    rows = load_trace(one(os.path.join(a.dir, "cnn_stats", "**", "*kernel_trace.csv")))
+    rows = load_trace(one(os.path.join(a.dir, a.prefix + "_stats", "**", "*kernel_trace.csv")))
     names = [short(r["Kernel_Name"]) for r in rows if short(r["Kernel_Name"])]
     SEQ = SEQ_FUSED if "k_cnn_head_loss" in names else SEQ_SPLIT
     trace = minibatches(rows)[a.skip:]
-    fetch = minibatches(load_pmc(one(os.path.join(a.dir, "cnn_fetch", "**", "*counter_collection.csv")),
+    fetch = minibatches(load_pmc(one(os.path.join(a.dir, a.prefix + "_fetch", "**", "*counter_collection.csv")),
                                  "FETCH_SIZE"))[a.skip:]
-    write = minibatches(load_pmc(one(os.path.join(a.dir, "cnn_write", "**", "*counter_collection.csv")),
+    write = minibatches(load_pmc(one(os.path.join(a.dir, a.prefix + "_write", "**", "*counter_collection.csv")),
                                  "WRITE_SIZE"))[a.skip:]
     for mb in trace + fetch + write:
         check_seq(mb)
