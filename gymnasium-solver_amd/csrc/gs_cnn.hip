@@ -687,7 +687,10 @@ size_t head_loss_lds(const CnnLayout &L)
 }
 
 // the head weights' gradient partials of one k_cnn_head_loss workgroup: [A1][HID + 1] (bias last)
-__host__ __device__ inline int64_t head_part_stride(const CnnLayout &L) { return (int64_t)(L.A + 1) * (L.HID + 1); }
+__host__ __device__ inline int64_t head_part_stride(const CnnLayout &L)
+{
+    return (int64_t)(L.A + 1) * (L.HID + 1) + L.HID;    // [dWh | dbh] rows, then dbf (column sums of dh)
+}
 
 template <int AM, bool BF>
 __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__ h, const float *__restrict__ P,
@@ -834,6 +837,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         float g[4 * NZ];
 #pragma unroll
         for (int a = 0; a < 4 * NZ; ++a) g[a] = 0.f;
+        float dbf = 0.f;      // this workgroup's rows of dbf[j] = sum_b dh[b][j] (the fc bias gradient)
         for (int r = 0; r < kHeadRows; ++r) {
             float d[4 * NZ];
 #pragma unroll
@@ -854,7 +858,11 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
             for (int a = 0; a < 4 * NZ; ++a)
                 if (a == A) dA = d[a], wA = w[a];
             sacc += dA * wA;
-            if (r0 + r < B) dh[(int64_t)(r0 + r) * HID + j] = hv > 0.f ? sacc : 0.f;
+            const float dhv = hv > 0.f ? sacc : 0.f;
+            if (r0 + r < B) {
+                dh[(int64_t)(r0 + r) * HID + j] = dhv;
+                dbf += dhv;
+            }
             // this workgroup's share of dWh[a][j] = sum_r dz[r][a] h[r][j] (rows in order)
             const float hb = BF ? bf16r(hv) : hv;
 #pragma unroll
@@ -863,6 +871,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 #pragma unroll
         for (int a = 0; a < 4 * NZ; ++a)
             if (a < A1) wp[a * (HID + 1) + j] = g[a];
+        wp[(int64_t)A1 * (HID + 1) + j] = dbf;
     }
     if (tid < A1) {     // the bias column: sum of the (unrounded) dz rows
         float sb = 0.f;
@@ -922,8 +931,10 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
     __syncthreads();
     if (g == 0 && out < nout) {
         const float v = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+        const int64_t nh = (int64_t)(A + 1) * (HID + 1);
         const int a = (int)(out / (HID + 1)), c = (int)(out - (int64_t)a * (HID + 1));
-        const int64_t dst = c < HID ? (a < A ? L.oWp + (int64_t)a * HID + c : L.oWv + c) : (a < A ? L.obp + a : L.obv);
+        const int64_t dst = out >= nh ? L.obf + (out - nh)
+                            : c < HID ? (a < A ? L.oWp + (int64_t)a * HID + c : L.oWv + c) : (a < A ? L.obp + a : L.obv);
         G[dst] = v;
     }
 }
@@ -1110,7 +1121,8 @@ ConvGeom geom2(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h1, L.
 ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.w2, L.c2, L.k3, L.s3, L.h3, L.w3, L.c3}; }
 
 // conv trunk + fc for R rows (h): obs rows come from the u8 buffer through idx (or 0..R)
-int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s)
+int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
+                  bool lib_fc = false)
 {
     int rc;
     if (conv1_lds_supported(L.C, L.H, L.W)) {
@@ -1128,7 +1140,10 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
     } else if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
         return rc;
     }
-    // fc: h = relu(a3 Wf^T + bf), split-K partials summed with the bias + ReLU epilogue
+    // fc: h = relu(a3 Wf^T + bf): hipBLASLt with its bias + ReLU epilogue (lib_fc: the update's
+    // fp32 path), else split-K partials summed with the bias + ReLU epilogue
+    if (lib_fc) return blaslt_gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf,
+                                       true);
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
         if ((rc = gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf, true)))
@@ -1152,7 +1167,7 @@ int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, c
 }
 
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s);
+                   const int32_t *stop, hipStream_t s, bool lib_fc = false);
 
 int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
              const int32_t *stop, hipStream_t s)
@@ -1175,13 +1190,17 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
 
 // the trunk's backward from dh (fc, then the convolutions)
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s)
+                   const int32_t *stop, hipStream_t s, bool lib_fc)
 {
     int rc;
     (void)stop;
     const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
-    // fc: [dWf | dbf] = dh^T [a3 | 1]
-    {
+    // fc: [dWf | dbf] = dh^T [a3 | 1]; lib_fc: dWf through hipBLASLt, dbf from the head kernels
+    if (lib_fc) {
+        if ((rc = blaslt_gemm_f32(s, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr,
+                                  false)))
+            return rc;
+    } else {
         const int sw = splits_for(L.HID, L.F + 1, B);
         if ((rc = gemm_wgrad_bias(s, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, w.parts, sw))) return rc;
         if ((rc = sum_parts_wb(s, w.parts, sw, (int64_t)L.HID * (L.F + 1), L.HID, L.F, G + L.oWf, G + L.obf)))
@@ -1334,9 +1353,12 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     const FrameSrc fs{ro.obs, idx, ro.T, ro.N};
     if (head_fused(L, B)) {
         const CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
-        if ((rc = forward_trunk(P, L, fs, B, w, s))) return rc;
+        // fp32: the fc layer's two plain GEMMs through hipBLASLt (dbf comes from the head kernels)
+        const bool lib_fc = !cnn_bf16() && blaslt_available(false, true, B, L.HID, L.F, L.F, L.F, L.HID, true, true) &&
+                            blaslt_available(true, false, L.HID, L.F, B, L.HID, L.F, L.F, false, false);
+        if ((rc = forward_trunk(P, L, fs, B, w, s, lib_fc))) return rc;
         if ((rc = launch_head_loss(P, L, B, fl, w, loss_args(hp), G, metrics, stop, s))) return rc;
-        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s))) return rc;
+        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, lib_fc))) return rc;
     } else {
         hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
                            ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv,

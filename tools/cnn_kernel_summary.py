@@ -47,6 +47,14 @@ SEQ_SPLIT = [("gather_fields", "k_gather_fields"), ("conv1_fwd", "k_conv1_fwd"),
        ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"), ("conv2_dgrad", "k_conv_dgrad"),
        ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"), ("norm_partials", "k_norm_partials"),
        ("clip_adam", "k_clip_adam_flat")]
+# the fp32 update with the fc layer's two plain GEMMs through hipBLASLt (dbf from the head kernels)
+SEQ_LIB = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd", "k_conv_fwd"),
+           ("fc_fwd", "blaslt"), ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
+           ("fc_wgrad", "blaslt"), ("fc_dgrad_relu_mask", "k_gemm"),
+           ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts_wb"),
+           ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
+           ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
+           ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
 SEQ = SEQ_FUSED
 
 
@@ -74,13 +82,32 @@ def nature_work(B, A=18, C=4, H=84, W=84):
 
 
 def short(name):
+    if "Cijk_" in name:     # hipBLASLt / Tensile GEMM kernels (the fc layer's fp32 GEMMs)
+        return "blaslt"
     m = re.search(r"\b(k_\w+)", name)
     return m.group(1) if m else None
 
 
+def merge_library_runs(rows):
+    """consecutive library kernels (a GEMM and its reduction kernels) become one dispatch: summed
+    duration (start of the first, end moved by the others' durations) and summed counter value"""
+    out = []
+    for r in rows:
+        if out and short(r["Kernel_Name"]) == "blaslt" and short(out[-1]["Kernel_Name"]) == "blaslt":
+            prev = dict(out[-1])
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            prev["End_Timestamp"] = str(int(prev["End_Timestamp"]) + dur)
+            if "Counter_Value" in r:
+                prev["Counter_Value"] = str(float(prev["Counter_Value"]) + float(r["Counter_Value"]))
+            out[-1] = prev
+        else:
+            out.append(r)
+    return out
+
+
 def minibatches(rows):
     """rows (dicts) in dispatch order -> list of per-minibatch dispatch lists (gs kernels only)."""
-    gs = [r for r in rows if short(r["Kernel_Name"]) is not None]
+    gs = merge_library_runs([r for r in rows if short(r["Kernel_Name"]) is not None])
     starts = [i for i, r in enumerate(gs) if short(r["Kernel_Name"]) == SEQ[0][1]]
     out = []
     for a, b in zip(starts, starts[1:] + [len(gs)]):
@@ -127,7 +154,7 @@ def main():
     global SEQ
     rows = load_trace(one(os.path.join(a.dir, a.prefix + "_stats", "**", "*kernel_trace.csv")))
     names = [short(r["Kernel_Name"]) for r in rows if short(r["Kernel_Name"])]
-    SEQ = SEQ_FUSED if "k_cnn_head_loss" in names else SEQ_SPLIT
+    SEQ = (SEQ_LIB if "blaslt" in names else SEQ_FUSED) if "k_cnn_head_loss" in names else SEQ_SPLIT
     trace = minibatches(rows)[a.skip:]
     fetch = minibatches(load_pmc(one(os.path.join(a.dir, a.prefix + "_fetch", "**", "*counter_collection.csv")),
                                  "FETCH_SIZE"))[a.skip:]
