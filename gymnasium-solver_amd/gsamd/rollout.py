@@ -346,6 +346,8 @@ class DeviceRolloutCollector:
             self._accumulate_stats()
             if native:
                 self._episode_records()
+        elif native:
+            self._episode_window()
         if not native:
             self.total_episodes += self.rollout_episodes
         self.rollout_fpss.append(N * T / max(time.time() - t0, 1e-9))
@@ -428,6 +430,54 @@ class DeviceRolloutCollector:
             self._record_episode(int(pos) % N, float(np.float32(r)), int(length), bool(to))
         self.rollout_episodes = rec.shape[1]
         self.total_episodes += self.rollout_episodes
+
+    def _episode_window(self):
+        """track_stats=False: the reference's rolling window (the last stats_window_size finished
+        episodes, rollout_collector.py:242-294, 753-758) kept on the device with no host sync —
+        this rollout's episodes in (step, env) order (gs_episode_stats) are merged behind the
+        previous window by index arithmetic; best / last episode and the count ride along."""
+        buf, N, T = self._buffer, self.n_envs, self.n_steps
+        W = int(self.stats_window_size)
+        check(lib.gs_episode_stats(ptr(buf.rewards), ptr(buf.dones), T, N, ptr(self._run_ret), ptr(self._run_len),
+                                   ptr(self._ep_ret_rows), ptr(self._ep_len_rows), stream_handle()),
+              "gs_episode_stats")
+        dev = self.device
+        if getattr(self, "_win", None) is None:
+            self._win = torch.zeros(2, W, dtype=torch.float64, device=dev)        # returns, lengths
+            self._win_meta = torch.zeros(3, dtype=torch.float64, device=dev)      # count, best, last valid
+            self._win_meta[1] = -float("inf")
+        done = buf.dones.reshape(-1).to(torch.int64)                   # time-major = (step, env)
+        pos = torch.cumsum(done, 0) - 1                                # episode number in the rollout
+        total = pos[-1] + 1
+        rets = self._ep_ret_rows.reshape(-1).double()
+        lens = self._ep_len_rows.reshape(-1).double()
+        # this rollout's last W episodes at slots W - total + pos (the rest go to a dump slot W)
+        slot = torch.where((done > 0) & (pos >= total - W), pos - (total - W), torch.full_like(pos, W))
+        last = torch.zeros(2, W + 1, dtype=torch.float64, device=dev)
+        last[0].scatter_(0, slot, rets)
+        last[1].scatter_(0, slot, lens)
+        i = torch.arange(W, device=dev)
+        keep_old = i + total < W
+        src = torch.clamp(i + total, max=W - 1)
+        self._win.copy_(torch.where(keep_old, self._win[:, src], last[:, :W]))
+        m = self._win_meta
+        m[0] += total.double()
+        best_now = torch.where(done > 0, rets, torch.full_like(rets, -float("inf"))).max()
+        m[1] = torch.maximum(m[1], best_now)
+        self.rollout_episodes_dev = total
+
+    def _window_metrics(self):
+        """roll/ep_rew/{mean,best,last} and roll/ep_len/{mean,last} from the device window (one D2H)."""
+        if getattr(self, "_win", None) is None:
+            return {}
+        w, meta = self._win.cpu().numpy(), self._win_meta.cpu().numpy()
+        n = int(min(meta[0], w.shape[1]))
+        if n <= 0:
+            return {}
+        r, ln = w[0, -n:], w[1, -n:]
+        return {"roll/ep_rew/mean": float(np.float32(r).mean()), "roll/ep_len/mean": int(ln.mean()),
+                "roll/ep_rew/best": float(meta[1]), "roll/ep_rew/last": float(np.float32(r[-1])),
+                "roll/ep_len/last": int(ln[-1])}
 
     def _host_episode_infos(self, done, trunc, infos):
         """A host env's RecordEpisodeStatistics infos (rollout_collector.py:210-294)."""
@@ -575,11 +625,9 @@ class DeviceRolloutCollector:
             m["roll/actions/mean"], m["roll/actions/std"], m["action_dist"] = 0.0, 0.0, None
         m["roll/baseline/mean"], m["roll/baseline/std"] = zero
         if dev_eps:
-            cnt, ret_sum, len_sum = part[-3:]
+            cnt = part[-3]
             m["cnt/total_episodes"] = int(cnt)
-            if cnt > 0:     # cumulative means (track_stats=False keeps no per-episode records)
-                m["roll/ep_rew/mean"] = float(ret_sum / cnt)
-                m["roll/ep_len/mean"] = int(len_sum / cnt)
+            m.update(self._window_metrics())      # this rank's rolling window, as the reference's deques
         elif self.episode_reward_deque:
             m["roll/ep_rew/mean"] = float(self.episode_reward_deque.mean())
             m["roll/ep_len/mean"] = int(self.episode_length_deque.mean())

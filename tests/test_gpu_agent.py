@@ -239,3 +239,31 @@ def test_one_launch_rollout_equals_step_loop(cuda, env, variant, over):
         for j, (x, y) in enumerate(zip(a, b)):
             assert torch.equal(x, y), (k, j)
     assert m0["cnt/total_episodes"] == m1["cnt/total_episodes"]
+
+
+@pytest.mark.parametrize("over", [dict(n_envs=256, episode_len=50), dict(n_envs=8, episode_len=7)])
+def test_untracked_collector_keeps_the_rolling_window(cuda, over):
+    """track_stats=False (the bench path) still reports the reference's rolling window
+    (rollout_collector.py:242-294, 753-758: the last 100 finished episodes, best and last episode),
+    kept on the device: equal to the tracked collector's host deques over several rollouts, with
+    many episodes per rollout (256 envs) and with fewer than the window per rollout (8 envs)."""
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    out = []
+    for track in (True, False):
+        torch.manual_seed(42)
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_epochs=1, **over))
+        agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=track)
+        coll = agent.get_rollout_collector("train")
+        ms = []
+        for _ in range(4):
+            agent.train_epoch()
+            ms.append(coll.get_metrics())
+        out.append(ms)
+        del agent
+    for mt, mu in zip(*out):
+        assert mt["cnt/total_episodes"] == mu["cnt/total_episodes"]
+        for k in ("roll/ep_rew/mean", "roll/ep_rew/best", "roll/ep_rew/last", "roll/ep_len/mean", "roll/ep_len/last"):
+            assert (k in mt) == (k in mu), k
+            if k in mt:
+                np.testing.assert_allclose(mu[k], mt[k], rtol=1e-6, atol=1e-6, err_msg=k)
