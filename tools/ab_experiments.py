@@ -46,4 +46,24 @@ EXPERIMENTS = {
     "roleA_xcd": [("gs_mlp.hip",
                    "        const int nb = bid / nkg, kb = (bid - nb * nkg) * sh.ka;   // first of the ka k-blocks",
                    "        const int nb = bid % sh.ncb, kb = (bid / sh.ncb) * sh.ka;   // first of the ka k-blocks")],
+    # every row block stores its share of the new set (row i of the column block by row block
+    # i mod gridDim.y; W1|b1 chunks q by row block q mod gridDim.y of column block 0)
+    "spread_stores": [("gs_mlp.hip",
+                       "                if (stW1[0]) reinterpret_cast<float4 *>(af.Pout)[q] = p4;\n"
+                       "                if (stW1[1]) reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);\n"
+                       "                if (stW1[2]) reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);",
+                       "                if (cb == 0 && q % (int)gridDim.y == rb) {\n"
+                       "                    reinterpret_cast<float4 *>(af.Pout)[q] = p4;\n"
+                       "                    reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);\n"
+                       "                    reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);\n"
+                       "                }"),
+                      ("gs_mlp.hip",
+                       "                if (stW2[0]) reinterpret_cast<float4 *>(af.Pout)[q] = w2r[j];\n"
+                       "                if (stW2[1]) reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);\n"
+                       "                if (stW2[2]) reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);",
+                       "                if (i % (int)gridDim.y == rb) {\n"
+                       "                    reinterpret_cast<float4 *>(af.Pout)[q] = w2r[j];\n"
+                       "                    reinterpret_cast<float4 *>(af.Mout)[q] = make_float4(m[0], m[1], m[2], m[3]);\n"
+                       "                    reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);\n"
+                       "                }")],
 }
