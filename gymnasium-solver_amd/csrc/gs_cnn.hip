@@ -1353,8 +1353,9 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     const FrameSrc fs{ro.obs, idx, ro.T, ro.N};
     if (head_fused(L, B)) {
         const CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
-        // fp32: the fc layer's two plain GEMMs through hipBLASLt (dbf comes from the head kernels)
-        const bool lib_fc = !cnn_bf16() && blaslt_available(false, true, B, L.HID, L.F, L.F, L.F, L.HID, true, true) &&
+        // the fc layer's forward and weight gradient through hipBLASLt in fp32 (dbf comes from the
+        // head kernels), also in the bf16 mode: faster there than the engine's bf16 form
+        const bool lib_fc = blaslt_available(false, true, B, L.HID, L.F, L.F, L.F, L.HID, true, true) &&
                             blaslt_available(true, false, L.HID, L.F, B, L.HID, L.F, L.F, false, false);
         if ((rc = forward_trunk(P, L, fs, B, w, s, lib_fc))) return rc;
         if ((rc = launch_head_loss(P, L, B, fl, w, loss_args(hp), G, metrics, stop, s))) return rc;

@@ -73,45 +73,49 @@ class _Bf16Conv(torch.autograd.Function):
 
 
 class _Bf16Linear(torch.autograd.Function):
-    """linear with bf16-rounded operands; round_dx=False keeps the input gradient in fp32 (the
-    heads' dh, a plain fp32 kernel on the device)."""
+    """linear with bf16-rounded operands in the products listed in `rounded` ("fwd", "dx", "dw"),
+    fp32 in the others: the heads round fwd + dw (their input gradient dh is a plain fp32 kernel);
+    the fc layer rounds only dx (its forward and weight gradient are hipBLASLt fp32 GEMMs, faster
+    than the bf16 form of the engine; its input gradient is the engine's bf16 GEMM)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, round_dx):
+    def forward(ctx, x, w, b, rounded):
         ctx.save_for_backward(x, w)
-        ctx.round_dx = round_dx
-        y = _bf(x) @ _bf(w).t()
+        ctx.rounded = rounded
+        y = (_bf(x) @ _bf(w).t()) if "fwd" in rounded else (x @ w.t())
         return y + b if b is not None else y
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        g = _bf(gy)
-        dx = (g @ _bf(w)) if ctx.round_dx else (gy @ w)
-        return dx, g.t() @ _bf(x), gy.sum(0), None
+        r = ctx.rounded
+        dx = (_bf(gy) @ _bf(w)) if "dx" in r else (gy @ w)
+        dw = (_bf(gy).t() @ _bf(x)) if "dw" in r else (gy.t() @ x)
+        return dx, dw, gy.sum(0), None
 
 
 def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False):
     """-> (masked logits (B,A) with -inf for invalid actions, value (B,), hidden (B,512)).
 
     bf16=True: the device's GS_HP_BF16 mode (SURVEY.md Appendix A "Precision modes") — every
-    convolution / GEMM product takes bf16-rounded operands with fp32 accumulation, at the points
-    the HIP kernels round them (u8/255 frames, activations, weights, output gradients); biases,
-    ReLU, the loss, the heads' input gradient and Adam stay fp32."""
+    convolution product and the heads' forward / weight gradient and the fc layer's input gradient
+    take bf16-rounded operands with fp32 accumulation, at the points the HIP kernels round them
+    (u8/255 frames, activations, weights, output gradients); the fc layer's forward and weight
+    gradient (hipBLASLt fp32), biases, ReLU, the loss, the heads' input gradient and Adam stay fp32."""
     x = torch.as_tensor(obs_u8)
     x = x.to(torch.float32) / 255.0 if x.dtype == torch.uint8 else x.to(torch.float32)
     conv = (lambda x, w, b, s: _Bf16Conv.apply(x, w, b, s)) if bf16 else (lambda x, w, b, s: F.conv2d(x, w, b, stride=s))
-    lin = (lambda x, w, b, rd=True: _Bf16Linear.apply(x, w, b, rd)) if bf16 else (lambda x, w, b, rd=True: F.linear(x, w, b))
+    lin = (lambda x, w, b, r: _Bf16Linear.apply(x, w, b, r)) if bf16 else (lambda x, w, b, r: F.linear(x, w, b))
     for i, s in enumerate(spec["strides"]):
         x = F.relu(conv(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], s))
     x = x.flatten(1)
-    h = F.relu(lin(x, params["mlp.0.weight"], params["mlp.0.bias"]))
-    logits = lin(h, params["policy_head.weight"], params["policy_head.bias"], False)
+    h = F.relu(lin(x, params["mlp.0.weight"], params["mlp.0.bias"], ("dx",)))
+    logits = lin(h, params["policy_head.weight"], params["policy_head.bias"], ("fwd", "dw"))
     if valid is not None:
         mask = torch.ones_like(logits, dtype=torch.bool)
         mask[:, list(valid)] = False
         logits = logits.masked_fill(mask, float("-inf"))
-    value = lin(h, params["value_head.weight"], params["value_head.bias"], False).squeeze(-1)
+    value = lin(h, params["value_head.weight"], params["value_head.bias"], ("fwd", "dw")).squeeze(-1)
     return logits, value, h
 
 
