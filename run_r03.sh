@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r03; mkdir -p $O
 export TMPDIR=/tmp
-step() { echo "== $1 $(date +%T)"; shift; "$@"; rc=$?; echo "rc=$rc"; return $rc; }
+step() { echo "== $1 $(date +%T)" >&2; shift; "$@"; rc=$?; echo "rc=$rc" >&2; return $rc; }
 if [ -n "$PYTEST_SEL" ]; then
   step pytest timeout -k 10 1000 python -u -m pytest $PYTEST_SEL -x -v -m gpu -p no:cacheprovider --timeout 300 \
       --timeout-method thread > $O/pytest.log 2>&1
