@@ -378,3 +378,42 @@ def global_trajectory_worker(rank, world, port, result_dir, fixture, transport="
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()
+
+
+def kl_one_rank_worker(rank, world, port, result_dir):
+    """Local data-parallel mode with target_kl set, where only rank 1's approx_kl trips the stop
+    (its rollout's old log-probs are shifted by +1, so ratio = e^-1 at minibatch 0): the exchange
+    ORs the stop bits, so rank 0 must skip the same optimizer steps, record them as skipped, and
+    count the same Adam steps (replicas would otherwise drift through bias correction)."""
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd._lib import M
+        from gsamd.config import load_config
+        from gsamd.distributed import comm_status, destroy_comm, init_xgmi_comm
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        torch.manual_seed(42)
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, n_epochs=2,
+                                                               target_kl=0.05))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
+        agent.train_dataloader()
+        if rank == 1:
+            agent.get_rollout_collector("train").buffer.logprobs.add_(1.0)
+        step0 = agent.adam_step
+        agent.update_phase()
+        torch.cuda.synchronize()
+        comm_status(agent.comm)
+        rec = agent.metrics_buf.cpu().numpy()
+        np.savez(os.path.join(result_dir, f"r{rank}.npz"), p=agent.policy_model.params.cpu().numpy(),
+                 steps=np.int64(agent.adam_step - step0), skipped=rec[:, M["skipped"]], kl_stop=rec[:, M["kl_stop"]])
+        dist.barrier()
+        comm = agent.comm
+        del agent
+        destroy_comm(comm)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()

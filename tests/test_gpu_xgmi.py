@@ -219,6 +219,19 @@ def test_multi_rank_update_vs_oracle_mean_gradient(tmp_path, transport, algo, bw
     assert np.linalg.norm(p_solo - p_ref) / np.linalg.norm(p_ref) > 1e-4
 
 
+def test_kl_stop_on_one_rank_skips_on_every_rank(tmp_path):
+    """Only rank 1's approx_kl trips target_kl (local mode): the exchange ORs the stop bits, so
+    both ranks skip the same optimizer steps — rank 0 records them as skipped too — count the same
+    Adam steps and end with bit-identical parameters."""
+    from _dist_workers import kl_one_rank_worker
+    _run(kl_one_rank_worker, 2, tmp_path, timeout=300)
+    r0, r1 = (dict(np.load(tmp_path / f"r{r}.npz")) for r in range(2))
+    assert r1["kl_stop"][0] == 1 and r1["skipped"][0] == 1          # rank 1 tripped at minibatch 0
+    assert r0["skipped"][0] == 1                                      # rank 0 took no step there either
+    assert int(r0["steps"]) == int(r1["steps"]) == 0                  # sticky: no step this epoch
+    assert np.array_equal(r0["p"].view(np.uint32), r1["p"].view(np.uint32))
+
+
 def test_exchange_timeout_raises_from_train_epoch(tmp_path):
     """A peer that connects and then never runs its update: rank 0's train_epoch raises GsError
     after the exchange's bounded wait (GS_XGMI_TIMEOUT_S=2) — the message and
