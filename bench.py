@@ -506,7 +506,7 @@ def main():
         except (OSError, ValueError):
             pmc = {}
     traffic_src = {"file": "profiles/pmc_traffic.json", "recorded_source_hash": pmc.get("_source_hash"),
-                   "library_source_hash": source_hash()}
+                   "library_source_hash": source_hash("mlp"), "sources": "mlp"}
     traffic_src["current"] = bool(pmc) and traffic_src["recorded_source_hash"] == traffic_src["library_source_hash"]
     if traffic_src["current"]:
         if args.workload == "C2":   # the committed minibatch-kernel PMC passes are C2-shaped
@@ -531,7 +531,7 @@ def main():
             except (OSError, ValueError):
                 kern = {}
         ksrc = {"file": "profiles/c4_kernels.json", "recorded_source_hash": kern.get("_source_hash"),
-                "library_source_hash": source_hash(), "operands": kern.get("operands")}
+                "library_source_hash": source_hash("cnn"), "sources": "cnn", "operands": kern.get("operands")}
         ksrc["current"] = bool(kern) and ksrc["recorded_source_hash"] == ksrc["library_source_hash"] and \
             kern.get("operands") == ("bf16" if args.dtype == "bf16" else "f32")
         if ksrc["current"]:

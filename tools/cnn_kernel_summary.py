@@ -187,7 +187,7 @@ def main():
         kernels[label] = e
     flops = sum(work[l][0] for l, _ in SEQ if l in work)
     out = {"_note": __doc__.split("\n\n")[1].replace("\n", " "),
-           "_source_hash": source_hash(), "batch": a.batch, "operands": "bf16" if a.bf16 else "f32",
+           "_source_hash": source_hash("cnn"), "batch": a.batch, "operands": "bf16" if a.bf16 else "f32",
            "mfma_peak_TFLOPs": peak, "hbm_peak_GBps": PEAK_HBM, "minibatches_measured": len(trace),
            "minibatch": {"sum_kernel_us": round(tot_us, 2), "flops": flops,
                          "TFLOPs_over_kernel_time": round(flops / tot_us / 1e6, 2),
