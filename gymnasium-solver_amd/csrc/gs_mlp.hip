@@ -145,6 +145,36 @@ __device__ __forceinline__ void store_component_norms(double (&hq)[2], double to
     }
 }
 
+// block_reduce's sums for thread 0 only (the others keep their own inputs): the same order and
+// the same two levels, without the broadcast level and its trailing barrier — for epilogues
+// whose single reader is thread 0 and which touch the scratch no more.
+template <int NV, typename T>
+__device__ __forceinline__ void block_reduce_t0(T (&v)[NV], T *scratch)
+{
+    const int tid = threadIdx.x;
+    if (tid < 256)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) scratch[k * 256 + tid] = v[k];
+    __syncthreads();
+    T *part = scratch + NV * 256;
+    if (tid < NV * 16) {
+        const int k = tid >> 4, j = tid & 15;
+        T acc = 0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc += scratch[k * 256 + j * 16 + m];
+        part[tid] = acc;
+    }
+    __syncthreads();
+    if (tid == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            T acc = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc += part[k * 16 + j];
+            v[k] = acc;
+        }
+}
+
 // copy n floats global -> LDS, vectorised when both sides are 16-B aligned
 __device__ __forceinline__ void copy_to_lds(float *dst, const float *src, int n)
 {
@@ -331,32 +361,31 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         // 256-thread grouping of k_clip_adam, wave-uniform branch for the wider block)
         constexpr int NQP = (nq1 + NT - 1) / NT;
         const bool nrm = NT == 256 || tid < 256;
+        // The lanes that take no part in the norm (waves 4..7 of a 512-thread block) load quad 0,
+        // and without the fold (G already holds dW1|db1) every partial slot re-reads G: no load
+        // sits in a branch, and no loaded register is merged with a constant at a join — either
+        // puts an s_waitcnt vmcnt(0) inside the burst, a memory round trip each.  The unused
+        // values are dropped where they are consumed.
+        // Issue order = the order the phases consume them (vmcnt counts in order): the norm's
+        // slots and partials first, so the fold + norm start while the Adam operands are in flight.
+        float sl[NS];     // slots past n_slots and the non-norm lanes are dropped in the norm
+#pragma unroll
+        for (int j = 0; j < NS; ++j) sl[j] = ld1(af.sumsq, nrm ? min(tid + 256 * j, aa.n_slots - 1) : 0);
         float4 w1p[NQP], w1m[NQP], w1v[NQP], t[NQ][NRB];  // W1|b1 (param order), dW1|db1 partials
+        const float *tsrc = fold ? af.part1 : af.G;
+        const int64_t tstride = fold ? (int64_t)n1 : 0;
+        const int nrb_used = fold ? NRB : 1;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j)
+#pragma unroll
+            for (int b = 0; b < NRB; ++b)
+                t[j][b] = ld4(tsrc + (int64_t)b * tstride, nrm ? min(tid + 256 * j, nq1 - 1) : 0);
 #pragma unroll
         for (int j = 0; j < NQP; ++j) {
             const int q = min(tid + NT * j, nq1 - 1);
             w1p[j] = ld4(P, q);
             w1m[j] = ld4(af.Min, q);
             w1v[j] = ld4(af.Vin, q);
-        }
-        if (!nrm) {
-#pragma unroll
-            for (int j = 0; j < NQ; ++j)
-#pragma unroll
-                for (int b = 0; b < NRB; ++b) t[j][b] = z4;
-        } else if (fold) {
-#pragma unroll
-            for (int j = 0; j < NQ; ++j)
-#pragma unroll
-                for (int b = 0; b < NRB; ++b)
-                    t[j][b] = ld4(af.part1 + (int64_t)b * n1, min(tid + 256 * j, nq1 - 1));
-        } else {
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) {
-                t[j][0] = ld4(af.G, min(tid + 256 * j, nq1 - 1));
-#pragma unroll
-                for (int b = 1; b < NRB; ++b) t[j][b] = z4;
-            }
         }
         float4 w2m[kW2v], w2v[kW2v], w2g[kW2v];           // this workgroup's 16 W2 rows
 #pragma unroll
@@ -383,24 +412,12 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         load_slice(sb, ob);
         load_slice(sw, ow);
         load_slice(shb, oh);
-        float sl[NS];
-#pragma unroll
-        for (int j = 0; j < NS; ++j) sl[j] = nrm ? ld1(af.sumsq, min(tid + 256 * j, aa.n_slots - 1)) : 0.0f;
-        // then the loads behind the graph replay's step base: this minibatch's x rows and step
-        // k-1's schedule entries
-        float xv = 0.0f;
-        {
-            const int i = min(tid / cD, kTile - 1);
-            const bool okx = tid < kTile * cD && r0 + i < rows;
-            xv = ff.xg[(kstep * rows + r0) * cD + (okx ? tid : 0)];
-            if (!okx) xv = 0.0f;
-        }
+        // then the loads behind the graph replay's step base: this minibatch's x rows (stored to
+        // LDS after the Adam step, where nothing waits for them) and step k-1's schedule entries
+        const bool okx = tid < kTile * cD && r0 + min(tid / cD, kTile - 1) < rows;
+        const float xv = ff.xg[(kstep * rows + r0) * cD + (okx ? tid : 0)];
         const float neg_step = apply && aa.sched ? aa.sched[2 * kprev] : aa.neg_step_size;
         const float bc2s = apply && aa.sched ? aa.sched[2 * kprev + 1] : aa.inv_bc2_sqrt;
-#pragma unroll
-        for (int j = 0; j < NS; ++j)
-            if (!nrm || tid + 256 * j >= aa.n_slots) sl[j] = 0.0f;
-        if (tid < kTile * cD) xs[tid] = xv;
 #ifdef GS_STAMPS
         __builtin_amdgcn_s_waitcnt(0);     // diagnostic build only: split "loads landed" from the norm
         __syncthreads();
@@ -413,13 +430,14 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             double ss = 0.0;
 #pragma unroll
             for (int j = 0; j < NS; ++j)
-                if (tid + 256 * j < aa.n_slots) ss += (double)sl[j];
+                if (nrm && tid + 256 * j < aa.n_slots) ss += (double)sl[j];
 #pragma unroll
             for (int j = 0; j < NQ; ++j) {
                 if (!nrm) break;
                 float4 g = z4;
 #pragma unroll
                 for (int b = 0; b < NRB; ++b) {
+                    if (b >= nrb_used) break;
                     g.x += t[j][b].x;
                     g.y += t[j][b].y;
                     g.z += t[j][b].z;
@@ -500,6 +518,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         step_slice(shb, oh, own1);
         if (tid < kTile) b2s[tid] = ob < 0 ? 0.0f : sb[0];
         if (tid < cA1 * kTile) whs[tid] = ow < 0 ? 0.0f : sw[0];
+        if (tid < kTile * cD) xs[tid] = okx ? xv : 0.0f;
         GS_STAMP(2)
     } else if constexpr (kStage0) {
         constexpr Layout Lc = S::lay(Layout{});
@@ -1391,7 +1410,7 @@ __global__ __launch_bounds__(256) void k_loss(const float *__restrict__ P, Layou
 __device__ __forceinline__ void block_sumsq_store(float v, float *slot, float *sbuf)
 {
     float t[1] = {v};
-    block_reduce<1>(t, sbuf);      // sbuf: 272 floats
+    block_reduce_t0<1>(t, sbuf);      // sbuf: 272 floats
     if (threadIdx.x == 0) *slot = t[0];
 }
 
@@ -1419,7 +1438,7 @@ __device__ __forceinline__ void store_head_sums(float sq, float sqp, float sqv, 
         return;
     }
     float t[3] = {sq, sqp, sqv};
-    block_reduce<3>(t, sbuf);      // sbuf: 3 x 272 floats
+    block_reduce_t0<3>(t, sbuf);      // sbuf: 3 x 272 floats
     if (threadIdx.x == 0) {
         *slot = t[0];
         headsq[o] = t[1];
@@ -1457,8 +1476,15 @@ size_t bwd_lds_bytes(const Layout &L, int64_t B)
     const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
     const int64_t H2p = (L.H2 + 63) / 64 * 64;
     const BwdShape shp = BwdShape::make(L, (int)B);
-    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + 3 * kTile * (Bp64 + 4) + 3072 + Bp64 + 816;
-    const int64_t roleB = (int64_t)kRowsB * (H2p + 4) + kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
+    // the fast paths (A1 <= 5) form dh2 in registers: role A has no dh2 tile (and its block
+    // reduction reuses the h1 tile after the MFMA loop), role B only the dW1 partial scratch in
+    // place of its dh2 slab — role A's 49 KB (+ 3 KB static) keep three workgroups per CU, so
+    // ranks sharing a GPU find room for each other's grids
+    const bool fastA = A1 <= 5, regsB = A1 <= 5 && L.H2 % 64 == 0;
+    const int64_t roleA = round4((int)B * A1) + round4(A1 * 16) + ((fastA ? 0 : 1) + 2) * kTile * (Bp64 + 4) + 3072 +
+                          Bp64 + (fastA ? 0 : 816);
+    const int64_t roleB = (regsB ? (int64_t)round4(kRowsB / 16 * 16 * (L.D + 1)) : (int64_t)kRowsB * (H2p + 4)) +
+                          kTile * (H2p + 4) + round4(A1 * L.H2) + round4(kRowsB * A1) +
                           kRowsB * 16 + round4(kRowsB * L.D) + kRowsB * 17 + 1024 +
                           (int64_t)kRowsB * n_col_blocks(L.H2);
     const int64_t roleC = Bp16 * 17 + round4((int)Bp16 * A1) + (A1 * 256 > 1024 ? A1 * 256 : 1024) + 2 +
@@ -1567,10 +1593,11 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         GS_STAMP_BEGIN_IF(2, bid == 0)
         const int Bp = (B + 63) / 64 * 64;      // padded K (batch) for 4 waves x 16
         const int ld = Bp + 4;
+        const bool fast = A1 <= 5;                   // dh2 in registers (no dh2 tile)
         float *dzs = lds;                            // [B][A1]
         float *whs = dzs + round4(B * A1);           // [A1][16]
-        float *dh2T = whs + round4(A1 * 16);         // [16][Bp+4]  (n, b): h2 first, then dh2
-        float *h1T = dh2T + kTile * ld;              // [16*ka][Bp+4]  (k, b)
+        float *dh2T = whs + round4(A1 * 16);         // [16][Bp+4]  (n, b): h2 first, then dh2 (!fast)
+        float *h1T = dh2T + (fast ? 0 : kTile * ld); // [16*ka][Bp+4]  (k, b)
         float *red = h1T + kw * ld;                  // [4][3][256]
         // relu'(h2) bits of this n-block (one word per row) and the h1 column tile (16 contiguous
         // floats per row = 4 float4, transposed into LDS); dh2T is filled by the dh2 pass
@@ -1650,7 +1677,6 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
         // the ka dW2 tiles; k-block-0 workgroups also form db2[n] = sum_b dh2[b, n]: from the A
         // operands they already hold (fast path), or as an MFMA against a ones operand (t == ka)
-        const bool fast = A1 <= 5;
         const int nt = sh.ka + (!fast && kb == 0 ? 1 : 0);
         if (fast) {
             // dh2 = relu'(h2) * (dz . Wh) formed in registers as the MFMA's A operand (lane: hidden
@@ -1770,7 +1796,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 G[L.ob2 + db2n] = gv[2];
                 sqt[2] = gv[2] * gv[2];
             }
-            block_reduce<3>(sqt, reinterpret_cast<float *>(mkA + Bp));   // 3 x (256 + 16) floats
+            // 3 x (256 + 16) floats: the h1 tile, dead after the barrier above (fast path)
+            block_reduce_t0<3>(sqt, fast ? h1T : reinterpret_cast<float *>(mkA + Bp));
             if (tid == 0) {
                 for (int t = 0; t < sh.ka; ++t) sumsq[nb * sh.nkb + kb + t] = sqt[t];
                 if (kb == 0) sumsq[sh.nT + nb] = sqt[2];
@@ -1800,8 +1827,9 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         GS_STAMP_BEGIN_IF(4, bid == 0)
         const int H2p = (H2 + 63) / 64 * 64;
         const int ld = H2p + 4;
-        float *dh2s = lds;                          // [64][H2p+4]  h2 rows, then dh2
-        float *W2T = dh2s + kRowsB * ld;            // [16][H2p+4]  W2[n][k0+j] -> (j, n)
+        const bool dh2_regs = A1 <= 5 && H2 % 64 == 0;   // dh2 formed in registers, no dh2 slab
+        float *dh2s = lds;                          // [32][H2p+4]  dh2 (!dh2_regs); dW1 partial scratch
+        float *W2T = dh2s + (dh2_regs ? round4(kRowsB / 16 * 16 * (D + 1)) : kRowsB * ld);   // [16][H2p+4]
         float *whs = W2T + kTile * ld;              // [A1][H2]
         float *dzs = whs + round4(A1 * H2);         // [64][A1]
         float *h1m = dzs + round4(kRowsB * A1);     // [64][16]
@@ -1811,7 +1839,6 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         // waves 0-2 stream the slab's operands into LDS while wave 3 computes its loss rows
         // (fused path): the loss math overlaps the loads instead of following them
         constexpr int kLd = FUSED ? 192 : 256;
-        const bool dh2_regs = A1 <= 5 && H2 % 64 == 0;
         int *mkB = reinterpret_cast<int *>(kred + 1024);   // [32][ncb] relu'(h2) bits
         if constexpr (S::H1c > 0 && S::Bc > 0) {
             // compile-time shapes: every operand load of the slab is issued before the first

@@ -168,7 +168,11 @@ extern "C" size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch)
 
 namespace {
 
-constexpr int64_t kChunk = 512;    // minibatch steps per captured graph
+constexpr int64_t kChunk = 512;    // minibatch steps per captured graph (chunked replay)
+// Updates of up to this many minibatch steps are captured whole, every kernel with its absolute
+// step index as an argument: no kernel of the chain then starts with a dependent load of the
+// replay's step base (a scalar memory round trip ahead of every operand load of k_bwd).
+constexpr int64_t kWholeCapture = 16384;
 constexpr int64_t kNumSumsHost = 14;   // raw loss sums per minibatch (gs_mlp.hip kNumSums)
 
 // The fused update path's per-update arrays, after the step workspace.
@@ -670,8 +674,9 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
     // with the chunk's first minibatch index in a device scalar (step_base) that the
     // kernels add to their index-stream, metrics and Adam-schedule offsets.  The tail
     // (n % kChunk steps) runs eagerly.  Graph size stays bounded for C3's 327 680 steps.
-    const int64_t chunk = n_minibatches < kChunk ? n_minibatches : kChunk;
+    const int64_t chunk = n_minibatches <= kWholeCapture ? n_minibatches : kChunk;
     const int64_t n_full = n_minibatches / chunk;
+    const bool whole = chunk == n_minibatches;      // absolute step indices, no device step base
     GraphKey key{};
     const void *ptrs[14] = {params, grads, adam_m, adam_v, ro.obs, ro.actions, ro.logprobs, ro.values,
                             ro.advantages, ro.returns, idx, metrics, glob ? glob->adv_stats : nullptr,
@@ -719,21 +724,22 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
         GS_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
         hipGraph_t g;
         GS_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+        const int64_t *base = whole ? nullptr : ent.base;
         for (int64_t k = 0; k < chunk; ++k) {
             StepArgs sa = make_step_args(hp, L, batch, 1);
             sa.aa.sched = ent.sched;
             sa.aa.sched_idx = (int)k;
-            sa.aa.step_base = ent.base;
-            sa.la.step_base = ent.base;
+            sa.aa.step_base = base;
+            sa.la.step_base = base;
             if (lagged) {
-                rc = lag_step(k, ent.base, ent.sched, cs);
+                rc = lag_step(k, base, ent.sched, cs);
             } else if (fused) {
                 LossArgs la_f = sa.la;
                 la_f.step_base = nullptr;      // the fused fwd takes its base from FusedFwd
                 StepArgs saf = sa;
                 saf.la = la_f;
                 rc = enqueue_step_fused(params, grads, adam_m, adam_v, L, with_norm(saf, k), batch,
-                                        step_ff(k, k, ent.base),
+                                        step_ff(k, k, base),
                                         metrics + k * GS_NUM_METRICS, stop_flag, ws, comm, cs);
             } else {
                 rc = enqueue_step(params, grads, adam_m, adam_v, L, at_step(sa, k), ro, idx + k * batch, batch,

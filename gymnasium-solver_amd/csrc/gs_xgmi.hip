@@ -344,7 +344,17 @@ __global__ __launch_bounds__(256) void k_xgmi_rsag(float *__restrict__ G, Part1F
 
 }  // namespace
 
-static int nwg_of(const gs_comm *c) { return (int)std::min<int64_t>(c->cap / kXgmiChunk, kXgmiMaxWG); }
+// Exchange-launch grid.  Its workgroups spin on their peers' flags.  Ranks that share a GPU
+// (or whose colocation is unknown) are separate processes: a full 256-workgroup grid of spinners
+// can hold every CU while the peer's own kernels ahead of its exchange (the NatureCNN convolutions
+// take a whole CU's LDS) wait for one, until the timeout.  Sharing, the grid is capped so that
+// all ranks' spinners together leave half the CUs free.
+static int nwg_of(const gs_comm *c)
+{
+    int64_t n = std::min<int64_t>(c->cap / kXgmiChunk, kXgmiMaxWG);
+    if (c->colocated != 1 && c->nranks > 1) n = std::min<int64_t>(n, std::max(8, 128 / c->nranks));
+    return (int)std::max<int64_t>(n, 1);
+}
 
 int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
                   float scale, hipStream_t s)

@@ -8,7 +8,35 @@ ADAM_DENOM = ("gs_mlp.hip",
               "    const float denom = v * inv_bc2s + aa.eps;\n"
               "    p = p + neg_step * (m * denom);")
 
+def _zero_loss(call):
+    """a loss_rows_lds call replaced by a constant dz fill of the same rows (wrong results)"""
+    return ("gs_mlp.hip", call, "for (int u = threadIdx.x; u < 256 * 3; u += 256) dzs[u] = 1e-3f;")
+
+
 EXPERIMENTS = {
+    # role A / B / C without their loss rows (wrong results): what the redundant loss costs each role
+    "no_loss_A": [_zero_loss("loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, B, dzs, nullptr);")],
+    "no_loss_B": [("gs_mlp.hip",
+                   "            loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, b0, kRowsB, dzs, nullptr, kLd, 256 - kLd);",
+                   "            for (int u = threadIdx.x; u < kRowsB * 3; u += 256) dzs[u] = 1e-3f;")],
+    "no_loss_C": [("gs_mlp.hip",
+                   "                loss_rows_lds<S>(P, L, zpart, ff, la, B, kstep, 0, Bp, dzs, ge > gs ? dscrC : nullptr, 0, 256,\n"
+                   "                                 kTile * gs, kTile * ge);",
+                   "                for (int u = threadIdx.x; u < Bp * 3; u += 256) dzs[u] = 1e-3f;")],
+    # role B on 64-row slabs (4 dW1|db1 partials instead of 8; correct results, other rounding):
+    # each wave takes one 16-row tile over the whole K = H2 instead of half of it
+    "rows64": [("gs_common.h", "constexpr int kRowsB = 32;", "constexpr int kRowsB = 64;"),
+               ("gs_mlp.hip", "        const int rt = wave >> 1, half = wave & 1;\n"
+                              "        const int chb = half ? nchB / 2 : 0, che = half ? nchB : nchB / 2;",
+                "        const int rt = wave;\n        const int chb = 0, che = nchB;"),
+               ("gs_mlp.hip",
+                "            const float g = kred[(2 * t) * 256 + rr * kTile + col] + kred[(2 * t + 1) * 256 + rr * kTile + col];",
+                "            const float g = kred[t * 256 + rr * kTile + col];")],
+    # the lagged forward without the W2 rows' Adam-state loads (m, v, g copied from p: wrong
+    # results): the price of the 48 KB per workgroup
+    "no_w2_state": [("gs_mlp.hip",
+                     "            w2m[j] = ld4(af.Min, q);\n            w2v[j] = ld4(af.Vin, q);\n            w2g[j] = ld4(af.G, q);",
+                     "            w2m[j] = w2r[j];\n            w2v[j] = w2r[j];\n            w2g[j] = w2r[j];")],
     # Adam without sqrt / rcp (wrong results): the transcendental cost of the lagged step
     "no_trans": [ADAM_DENOM],
     # new W2 / W1 set stored from three row blocks instead of one
@@ -27,8 +55,8 @@ EXPERIMENTS = {
                          "        const bool stW1[3] = {false, false, false};")],
     # one of the 8 dW1|db1 row-block partials loaded (wrong results): the fold's price
     "one_partial": [("gs_mlp.hip",
-                     "                    t[j][b] = ld4(af.part1 + (int64_t)b * n1, min(tid + 256 * j, nq1 - 1));",
-                     "                    t[j][b] = b == 0 ? ld4(af.part1, min(tid + 256 * j, nq1 - 1)) : z4;")],
+                     "                t[j][b] = ld4(tsrc + (int64_t)b * tstride, nrm ? min(tid + 256 * j, nq1 - 1) : 0);",
+                     "                t[j][b] = b == 0 ? ld4(tsrc, nrm ? min(tid + 256 * j, nq1 - 1) : 0) : z4;")],
     # x / h1 stores after the heads, as with 256 threads
     "late_x_h1": [("gs_mlp.hip", "    constexpr bool kEarly = NT == 512;", "    constexpr bool kEarly = false;")],
     # k_bwd grid padded to a multiple of 8 (the extra workgroups exit at once): every kernel of the
