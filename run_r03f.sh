@@ -19,3 +19,7 @@ for i in 1 2; do
     echo "$v run $i: $(grep -E 'minibatch period|fwd span|bwd span' $O/ab/$v.$i.log | awk '{printf "%s %s %s | ", $1, $2, $(NF-6)}')"
   done
 done
+if [ -n "$STAMPS" ]; then
+  timeout -k 10 120 python tools/stamp_run.py > $O/stamps.log 2>&1 || exit 1
+  grep -v amdgpu.ids $O/stamps.log | head -40
+fi

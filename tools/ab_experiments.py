@@ -95,3 +95,23 @@ EXPERIMENTS = {
                        "                    reinterpret_cast<float4 *>(af.Vout)[q] = make_float4(v[0], v[1], v[2], v[3]);\n"
                        "                }")],
 }
+
+# the lagged forward's h2 MFMA on all 8 waves (2 of the 16 K chunks each) instead of waves 0..3
+# (4 each), the x / h1 stores of waves 4..7 after their chunks: timing only (the 8 partials are
+# summed in another order than the 256-thread kernel's 4)
+EXPERIMENTS["mfma8"] = [
+    ("gs_mlp.hip", "               round4(kTile * L.D) + kTile * (L.H1 + 4) + 1024 + kTile * 17;",
+                   "               round4(kTile * L.D) + kTile * (L.H1 + 4) + 2048 + kTile * 17;"),
+    ("gs_mlp.hip", "    float *h2s = red + 1024;", "    float *h2s = red + 2048;"),
+    ("gs_mlp.hip", "    if (kEarly && wave >= 4) store_x_h1(tid - 256, 256);\n", ""),
+    ("gs_mlp.hip", "    if (wave < 4) {\n        const int i = lane & 15, q = lane >> 4;\n        const int nch = H1 / kTile;\n"
+                   "        const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;",
+                   "    {\n        const int i = lane & 15, q = lane >> 4;\n        const int nch = H1 / kTile;\n"
+                   "        const int ch0 = (wave * nch) / (NT / 64), ch1 = ((wave + 1) * nch) / (NT / 64);"),
+    ("gs_mlp.hip", "        for (int r = 0; r < 4; ++r) red[wave * 256 + (q * 4 + r) * kTile + i] = acc[r];\n    }\n    __syncthreads();\n    GS_STAMP(5)",
+                   "        for (int r = 0; r < 4; ++r) red[wave * 256 + (q * 4 + r) * kTile + i] = acc[r];\n    }\n"
+                   "    if (kEarly && wave >= 4) store_x_h1(tid - 256, 256);\n    __syncthreads();\n    GS_STAMP(5)"),
+    ("gs_mlp.hip", "        const float s = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];",
+                   "        float s = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];\n"
+                   "        if (NT == 512) s = (((s + red[1024 + tid]) + red[1280 + tid]) + red[1536 + tid]) + red[1792 + tid];"),
+]
