@@ -115,3 +115,11 @@ EXPERIMENTS["mfma8"] = [
                    "        float s = ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];\n"
                    "        if (NT == 512) s = (((s + red[1024 + tid]) + red[1280 + tid]) + red[1536 + tid]) + red[1792 + tid];"),
 ]
+
+# role C's n-blocks paired per XCD (n-blocks 2m, 2m+1 — one 128-B line of each h2 row — on XCD m):
+# correct results, half the h2 column-tile fetch from memory
+EXPERIMENTS["roleC_pair"] = [
+    ("gs_mlp.hip", "        const int nb = bid;\n        const int n0 = nb * kTile;\n        const int Bp = (B + 15) / 16 * 16;",
+                   "        const int nb = (sh.ncb == 16 && bid < 16) ? 2 * (bid & 7) + (bid >> 3) : bid;\n"
+                   "        const int n0 = nb * kTile;\n        const int Bp = (B + 15) / 16 * 16;"),
+]
