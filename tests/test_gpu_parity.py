@@ -120,6 +120,47 @@ def test_policy_sampling_follows_probs(cuda):
     assert np.abs(freq - probs).max() < 0.01, (freq, probs)
 
 
+def _mix64(x):
+    """SplitMix64 finaliser on uint64 numpy arrays (csrc/gs_mlp.hip mix64), wrapping arithmetic"""
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def test_policy_sampling_inverse_cdf_rows(cuda):
+    """Row-exact check of the default sampling path: every row's action is the first a with
+    u < cdf[a], u = the row's counter-based uniform (host restatement of the kernel's SplitMix64
+    draw) and cdf the running sum of that row's probabilities (from the replay path's log-probs).
+    Rows whose u lies within 2e-5 of a CDF boundary are left out (the host's exp(logp) and the
+    kernel's softmax differ in the last bits); near-tie rows — two actions with probabilities
+    within 1e-3 of each other — are generated on purpose and must be checked like the others."""
+    from gsamd.policy import DeviceMLPActorCritic
+    torch.manual_seed(5)
+    pm = DeviceMLPActorCritic(8, (128, 128), 4, device=cuda)
+    n = 8192
+    obs = (torch.rand(n, 8, device=cuda) * 4 - 2).contiguous()
+    seed, ctr = 1234, 7
+    a, _, _ = pm.act(obs, mode=0, rng_seed=seed, rng_counter=ctr)
+    a = a.cpu().numpy()
+    lp = np.zeros((n, 4), np.float32)
+    for act in range(4):
+        _, lpa, _ = pm.act(obs, mode=2, actions=torch.full((n,), act, device=cuda, dtype=torch.int64))
+        lp[:, act] = lpa.cpu().numpy()
+    probs = np.exp(lp.astype(np.float64))
+    cdf = np.cumsum(probs, axis=1)
+    with np.errstate(over="ignore"):
+        h = _mix64(_mix64(_mix64(np.uint64(seed)) ^ np.uint64(ctr)) ^ np.arange(n, dtype=np.uint64))
+    u = (h >> np.uint64(40)).astype(np.float64) / 16777216.0
+    want = np.minimum((u[:, None] >= cdf).sum(axis=1), 3)
+    clear = np.abs(u[:, None] - cdf[:, :3]).min(axis=1) > 2e-5
+    assert clear.sum() > n - 16, clear.sum()
+    np.testing.assert_array_equal(a[clear], want[clear])
+    srt = np.sort(probs, axis=1)
+    ties = (np.diff(srt, axis=1) < 1e-3).any(axis=1) & clear
+    assert ties.sum() >= 8, ties.sum()       # near-tie rows were checked above
+
+
 # ------------------------------------------------------------------------------- synthetic env
 def test_device_env_matches_host_env(cuda):
     from gsamd.rollout import DeviceSyntheticVecEnv
