@@ -140,7 +140,11 @@ struct Workspace {
     int n_slots;
     size_t bytes;
 };
-constexpr int kRowsB = 32;       // rows per dh1 workgroup in k_bwd (2 row tiles x 2 K halves over 4 waves)
+// rows per dh1 workgroup in k_bwd (2 row tiles x 2 K halves over 4 waves).  64 rows (one tile per
+// wave over the whole K) halve the dW1|db1 partials the next forward folds: C2 0.08 us faster per
+// minibatch, but C3 (B = 64: 8 role-B workgroups instead of 16) 9 % slower — kept at 32
+// (profiles/r03_ab_chain.txt)
+constexpr int kRowsB = 32;
 
 // Minibatch field gather done by the forward kernel (utils/rollout_collector.py:657-682).
 struct RowGather {

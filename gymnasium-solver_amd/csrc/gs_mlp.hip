@@ -2149,7 +2149,9 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
     bid -= sh.nB;
     {
         // ---------------- role C: head grads for hidden block nb (block ncb: head biases)
-        const int nb = bid;
+        // with 16 n-blocks the n-blocks 2m, 2m+1 (one 128-B line of every h2 row) go to workgroups m,
+        // m + 8 — one XCD (the grid before role C is a multiple of 8), so each h2 line is fetched once
+        const int nb = (sh.ncb == 16 && bid < 16) ? 2 * (bid & 7) + (bid >> 3) : bid;
         const int n0 = nb * kTile;
         const int Bp = (B + 15) / 16 * 16;
         GS_STAMP_BEGIN_IF(5, bid == 0)
