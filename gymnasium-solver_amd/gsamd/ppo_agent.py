@@ -633,10 +633,20 @@ class DevicePPOAgent:
         return self.metrics_buf[:, M["loss"]].cpu().numpy().astype(np.float64)
 
     def learn(self, max_epochs: Optional[int] = None, log=None) -> None:
-        """Lightning-free fit loop: max_env_steps guard (base_agent.py:306-320) + epochs."""
+        """Lightning-free fit loop: max_env_steps guard (base_agent.py:306-320) + epochs.
+        The run is bounded as the reference's Trainer bounds it (utils/trainer_factory.py:33:
+        `max_epochs=config.max_epochs`, -1 = unbounded when None): training stops once
+        current_epoch reaches config.max_epochs (Lightning counts epochs from the run's start, a
+        resumed run included).  An explicit `max_epochs` runs at most that many more epochs in
+        this call, inside the config's bound."""
         c = self.config
+        cap = getattr(c, "max_epochs", None)
+        if cap is not None and int(cap) < 0:
+            cap = None
         epochs = 0
         while max_epochs is None or epochs < max_epochs:
+            if cap is not None and self.current_epoch >= int(cap):
+                break
             if c.max_env_steps is not None:
                 done = self.get_rollout_collector("train").total_steps
                 if done + c.n_envs * c.n_steps * self.world_size > c.max_env_steps:

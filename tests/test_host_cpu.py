@@ -165,6 +165,36 @@ def test_env_follows_config_env_id():
         from_reference_config(SimpleNamespace(**full["CartPole-v1:ppo"]), env_dynamics="mujoco")
 
 
+def test_learn_stops_at_config_max_epochs():
+    """learn() is bounded as the reference's Trainer (utils/trainer_factory.py:33: max_epochs =
+    config.max_epochs, -1 when None): with max_epochs set and no max_env_steps it stops, counting
+    from the run's current epoch (a resumed run continues to the same bound); an explicit
+    learn(max_epochs=k) runs at most k more epochs within the config's bound."""
+    from types import SimpleNamespace
+    from gsamd.config import PPOConfig
+    from gsamd.ppo_agent import DevicePPOAgent
+
+    def run(cfg, start=0, **kw):
+        a = _bare_agent(cfg)
+        a.world_size, a.current_epoch = 1, start
+        coll = SimpleNamespace(total_steps=0)
+        a.get_rollout_collector = lambda stage: coll
+
+        def epoch():
+            a.current_epoch += 1
+            coll.total_steps += cfg.n_envs * cfg.n_steps
+        a.train_epoch = epoch
+        DevicePPOAgent.learn(a, **kw)
+        return a.current_epoch
+
+    assert run(PPOConfig(n_envs=4, n_steps=8, batch_size=8, max_epochs=5)) == 5
+    assert run(PPOConfig(n_envs=4, n_steps=8, batch_size=8, max_epochs=5), start=3) == 5        # resumed run
+    assert run(PPOConfig(n_envs=4, n_steps=8, batch_size=8, max_epochs=5), max_epochs=2) == 2
+    assert run(PPOConfig(n_envs=4, n_steps=8, batch_size=8, max_epochs=5, max_env_steps=64)) == 2
+    assert run(PPOConfig(n_envs=4, n_steps=8, batch_size=8, max_epochs=None, max_env_steps=96)) == 3
+    assert run(PPOConfig(n_envs=4, n_steps=8, batch_size=8, max_epochs=-1), max_epochs=4) == 4
+
+
 def test_synthetic_env_fixture(golden):
     from gsamd.synthetic_env import SyntheticVecEnv, synth_obs
     z = golden("synth_env.npz")

@@ -2,7 +2,7 @@
 # GPU-box: the xGMI test file (colocated exchange-launch grid cap), the C2 bench line + rocprof stats
 # (run_r03d.sh), then the same-box pricing A/B of timing-only variants (tools/run_ab.sh, 2 rounds).
 cd "$GRAFT_REPO_ROOT" || exit 1
-PYTEST_SEL=${PYTEST_SEL:-tests/test_gpu_xgmi.py} bash run_r03d.sh || exit 1
+PYTEST_SEL=${PYTEST_SEL:-tests/test_gpu_xgmi.py} bash tools/gpu/run_r03d.sh || exit 1
 [ -n "$AB" ] || exit 0
 mkdir -p gpurun_out/ab
 for i in 1 2; do
