@@ -196,11 +196,14 @@ def time_gae(agent, reps: int):
     return e0.elapsed_time(e1) / reps * 1e3, int(T), int(N)
 
 
-def roofline_entry(bound: str, amount: float, us: float, kernel: str) -> dict:
+def roofline_entry(bound: str, amount: float, us: float, kernel: str, mfma_peak: float = None) -> dict:
+    """mfma_peak: the dense MFMA peak of the operand type (f32 by default; the bf16 mode's lines use
+    the bf16 peak)."""
     if bound == "mfma":
+        pk = mfma_peak or PEAK_F32_MFMA_TFLOPS
         a = amount / (us * 1e-6) / 1e12
-        return {"bound": "mfma", "achieved": round(a, 4), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(a / PEAK_F32_MFMA_TFLOPS, 6), "kernel": kernel, "avg_us": round(us, 3),
+        return {"bound": "mfma", "achieved": round(a, 4), "peak": pk, "unit": "TFLOP/s",
+                "frac": round(a / pk, 6), "kernel": kernel, "avg_us": round(us, 3),
                 "work_per_launch": amount}
     a = amount / (us * 1e-6) / 1e9
     return {"bound": "hbm", "achieved": round(a, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -251,10 +254,18 @@ def bf16_deviation(agent) -> dict:
         hp.flags = flags
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
+        if agent.is_pixel:
+            check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v),
+                                        pm.dims, hp, coll.buffer.view(), ptr(idx), agent.batch_size,
+                                        agent.n_minibatches, agent.adam_step, ptr(agent.metrics_buf),
+                                        ptr(agent.stop_flag), ptr(agent.workspace), None, stream_handle()),
+                  "gs_cnn_ppo_update")
+        else:     # the MLP's fused chain (the update the bench line times), eager launches
+            check(lib.gs_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
                                     hp, coll.buffer.view(), ptr(idx), agent.batch_size, agent.n_minibatches,
                                     agent.adam_step, ptr(agent.metrics_buf), ptr(agent.stop_flag),
-                                    ptr(agent.workspace), None, stream_handle()), "gs_cnn_ppo_update")
+                                    ptr(agent.workspace), agent.workspace.numel(), None, 1, stream_handle()),
+                  "gs_ppo_update")
         e1.record()
         e1.synchronize()
         res[name] = (agent.metrics_buf[:, 0].cpu().numpy().astype(np.float64), pm.params.cpu().numpy().astype(np.float64),
@@ -348,7 +359,8 @@ def main():
                          "xGMI exchange through same-device IPC); throughput is not meaningful")
     ap.add_argument("--dtype", choices=("f32", "bf16"), default="f32",
                     help="f32: the fp32 parity path (default, the metric's line); bf16: bf16 MFMA operands in the "
-                         "NatureCNN update (C4/C5 only), reported as its own line with its deviation from fp32")
+                         "update (the MLP's fused chain, the NatureCNN's convolutions / GEMMs), reported as its own "
+                         "line with its deviation from fp32 over one whole update")
     ap.add_argument("--stage-reps", type=int, default=200)
     ap.add_argument("--cpu-minibatches", type=int, default=-1,
                     help="minibatches timed in the CPU baseline (-1: the whole update, 0: no CPU baseline)")
@@ -384,8 +396,6 @@ def main():
     # synthetic Atari frame source), or the device CartPole-v1 dynamics
     over = dict(n_envs=n_envs, env_dynamics="synthetic" if pixel else args.env_dynamics)
     if args.dtype == "bf16":
-        if not pixel:
-            raise SystemExit("[bench] --dtype bf16 is implemented for the NatureCNN workloads (C4, C5)")
         over["precision"] = "bf16"
     cfg = load_config(env_id, variant, overrides=over)
     agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world,
@@ -398,7 +408,9 @@ def main():
             comm = gd.init_local_comm(args.comm, n_params)
         elif args.comm == "xgmi":
             try:
-                comm = gd.init_xgmi_comm(rank, world, n_params, device)
+                # MLP: the in-backward exchange is checked on this job's shapes before the timed run
+                comm = gd.init_xgmi_comm(rank, world, n_params, device,
+                                         verify_shapes=None if pixel else (agent.policy_model.dims, cfg.batch_size))
             except RuntimeError as e:     # every rank raises together: switch transport together
                 _log(f"[bench] {e}; using RCCL for the gradient exchange")
                 args.comm = "rccl (xgmi unavailable)"
@@ -407,6 +419,7 @@ def main():
             comm = gd.init_device_comm(rank, world, device)
         agent.comm = comm
     comm_info = None
+    from gsamd.distributed import LAST_SELF_TEST as gd_self_test
     if comm is not None:
         from gsamd.distributed import comm_info as _comm_info
         comm_info = _comm_info(comm)
@@ -467,8 +480,9 @@ def main():
                                  pm.n_params, fused)
         dom = max(stage_us, key=stage_us.get)
         kname = {"fwd": "k_fwd_hidden", "fwd_adam": "k_fwd_hidden", "loss": "k_loss", "bwd": "k_bwd", "adam": "k_clip_adam"}
+        mpk = PEAK_BF16_MFMA_TFLOPS if args.dtype == "bf16" else PEAK_F32_MFMA_TFLOPS
         for st, us in stage_us.items():
-            rooflines[st] = roofline_entry(work[st][0], work[st][1], us, kname[st])
+            rooflines[st] = roofline_entry(work[st][0], work[st][1], us, kname[st], mpk)
         if "fwd_adam" in rooflines:
             # the lagged forward also streams the previous step's clip + Adam (28 B/param) and
             # writes the activations the backward reads: its HBM term beside the MFMA one; the
@@ -612,6 +626,7 @@ def main():
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.no_graph,
                        "grad_exchange": args.comm if comm is not None else None,
                        "exchange_in_bwd": in_bwd,
+                       "exchange_self_test": dict(gd_self_test) if comm is not None else None,
                        "comm": comm_info, "same_device": bool(args.same_device)},
             "roofline": roofline,
             "rooflines": rooflines,

@@ -150,6 +150,131 @@ __global__ __launch_bounds__(256) void k_atari_stack(const uint8_t *__restrict__
     st[(int64_t)(S - 1) * hw] = preprocess_px(f0, f0 + kFrameBytes, p / OW, p - (p / OW) * OW);
 }
 
+// ---- the 210x160 -> 84x84 pipeline at HBM rate.  One workgroup per (env, band of 12 output
+// rows); a band's output rows cover exactly input rows [30 b, 30 b + 30) (2.5 input rows per
+// output row), one contiguous 14 400-B run of each raw frame.  Per workgroup:
+//   1. every load issued up front: the stack slots 1..S-1 of the band (the shift's sources,
+//      16-B loads, first so that their data has landed before any store of this workgroup) and
+//      both frames' runs as 300 pixel-aligned 48-B chunks (16 pixels = three 16-B loads);
+//   2. grayscale + max-pool once per input pixel, 16 gray bytes per ds_write_b128 into LDS;
+//   3. the shifted slots stored (zeros after a done: FrameStackObservation's zero padding);
+//   4. the area resize from LDS in preprocess_px's order (row sums over ix, then total over iy,
+//      taps beyond a pixel's count weighted 0.0f: exact, every partial sum is >= 0), four
+//      consecutive output pixels per thread (21 threads per output row), one 4-B store each.
+// Algorithmic bytes per env step: 201 600 read + 7 056 written; the shift adds (S-1)·7 056 read
+// + (S-1)·7 056 written, all 16-B vector moves.
+constexpr int kOut84 = 84, kBandOut = 12, kBandIn = 30, kBands = kOut84 / kBandOut;
+constexpr int kRowBytes = kFW * kFC;                          // 480
+constexpr int kBandChunks = kBandIn * kFW / 16;               // 300 chunks of 16 pixels
+constexpr int kBandOutBytes = kBandOut * kOut84;              // 1 008 = 63 x 16 B
+constexpr int kMaxStackFast = 5;                              // (S-1) x 63 shift chunks <= 256 threads
+static_assert(kBandIn * kBands == kFH && 2 * kBandIn == 5 * kBandOut, "band geometry");
+
+__device__ __forceinline__ uint32_t gray16_word(const uint32_t (&a)[12], const uint32_t (&b)[12], int q)
+{
+    // pixels 4q..4q+3 of the 16 in a 48-B chunk: bytes 12q .. 12q+11 of each frame's chunk
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int byte = 12 * q + 3 * k;
+        int rgb0[3], rgb1[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int bb = byte + c;
+            rgb0[c] = (int)((a[bb >> 2] >> (8 * (bb & 3))) & 0xffu);
+            rgb1[c] = (int)((b[bb >> 2] >> (8 * (bb & 3))) & 0xffu);
+        }
+        const int g0 = (rgb0[0] * 4899 + rgb0[1] * 9617 + rgb0[2] * 1868 + (1 << 13)) >> 14;
+        const int g1 = (rgb1[0] * 4899 + rgb1[1] * 9617 + rgb1[2] * 1868 + (1 << 13)) >> 14;
+        out |= (uint32_t)max(g0, g1) << (8 * k);
+    }
+    return out;
+}
+
+__global__ __launch_bounds__(256) void k_atari_stack84(const uint8_t *__restrict__ frames,
+                                                       const uint8_t *__restrict__ done_row, int64_t N, int S,
+                                                       uint8_t *__restrict__ stack)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t g[kBandIn * kFW];     // 4 800 B of max-pooled gray
+    const int64_t e = blockIdx.x / kBands;
+    const int band = (int)(blockIdx.x - e * kBands);
+    const int tid = threadIdx.x;
+    constexpr int hw = kOut84 * kOut84;
+    uint8_t *st = stack + e * (int64_t)S * hw + band * kBandOutBytes;
+    // 1. loads: the shift's sources first, then the two frames' chunks (clamped, unconditional)
+    const int nshift = 63 * (S - 1);
+    const int sj = min(tid, max(nshift - 1, 0));
+    uint4 moved = make_uint4(0u, 0u, 0u, 0u);
+    if (nshift > 0) moved = *reinterpret_cast<const uint4 *>(st + (int64_t)(1 + sj / 63) * hw + 16 * (sj % 63));
+    const uint8_t *fa = frames + e * 2 * (int64_t)kFrameBytes + band * kBandIn * kRowBytes;
+    const uint8_t *fb = fa + kFrameBytes;
+    uint32_t a0[12], b0[12], a1[12], b1[12];
+    const int c0 = tid, c1 = min(tid + 256, kBandChunks - 1);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(fa + 48 * c0 + 16 * w);
+        const uint4 y = *reinterpret_cast<const uint4 *>(fb + 48 * c0 + 16 * w);
+        const uint4 u = *reinterpret_cast<const uint4 *>(fa + 48 * c1 + 16 * w);
+        const uint4 v = *reinterpret_cast<const uint4 *>(fb + 48 * c1 + 16 * w);
+        a0[4 * w] = x.x, a0[4 * w + 1] = x.y, a0[4 * w + 2] = x.z, a0[4 * w + 3] = x.w;
+        b0[4 * w] = y.x, b0[4 * w + 1] = y.y, b0[4 * w + 2] = y.z, b0[4 * w + 3] = y.w;
+        a1[4 * w] = u.x, a1[4 * w + 1] = u.y, a1[4 * w + 2] = u.z, a1[4 * w + 3] = u.w;
+        b1[4 * w] = v.x, b1[4 * w + 1] = v.y, b1[4 * w + 2] = v.z, b1[4 * w + 3] = v.w;
+    }
+    // the resize's coverage tables for this thread's row and four columns (L1-resident)
+    const int oyl = tid / 21, ox0 = 4 * (tid - 21 * (tid / 21));
+    const int orow = min(band * kBandOut + oyl, kOut84 - 1);
+    const int y0 = c_area.y0[orow] - band * kBandIn, ny = c_area.ny[orow];
+    float wy[3], wx[4][3];
+    int x0[4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) wy[i] = i < ny ? c_area.wy[orow][i] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int ox = min(ox0 + q, kOut84 - 1);
+        x0[q] = c_area.x0[ox];
+        const int nx = c_area.nx[ox];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) wx[q][i] = i < nx ? c_area.wx[ox][i] : 0.0f;
+    }
+    const bool reset = done_row ? done_row[e] != 0 : true;
+    // 2. grayscale + max-pool into LDS
+    if (c0 < kBandChunks)
+        *reinterpret_cast<uint4 *>(g + 16 * c0) = make_uint4(gray16_word(a0, b0, 0), gray16_word(a0, b0, 1),
+                                                             gray16_word(a0, b0, 2), gray16_word(a0, b0, 3));
+    if (tid + 256 < kBandChunks)
+        *reinterpret_cast<uint4 *>(g + 16 * c1) = make_uint4(gray16_word(a1, b1, 0), gray16_word(a1, b1, 1),
+                                                             gray16_word(a1, b1, 2), gray16_word(a1, b1, 3));
+    __syncthreads();
+    // 3. the shift (every source load of this workgroup has landed: the gray bytes above waited
+    //    for the younger frame loads)
+    if (tid < nshift)
+        *reinterpret_cast<uint4 *>(st + (int64_t)(tid / 63) * hw + 16 * (tid % 63)) =
+            reset ? make_uint4(0u, 0u, 0u, 0u) : moved;
+    // 4. area resize of four output pixels
+    if (tid < kBandOut * 21) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float total = 0.0f;
+#pragma unroll
+            for (int iy = 0; iy < 3; ++iy) {
+                const int yy = min(y0 + iy, kBandIn - 1);
+                float row = 0.0f;
+#pragma unroll
+                for (int ix = 0; ix < 3; ++ix) {
+                    const int xx = min(x0[q] + ix, kFW - 1);
+                    row = row + wx[q][ix] * (float)g[yy * kFW + xx];
+                }
+                total = total + wy[iy] * row;
+            }
+            const float v = rintf(total * c_area.inv_area);
+            packed |= (uint32_t)fminf(fmaxf(v, 0.0f), 255.0f) << (8 * q);
+        }
+        *reinterpret_cast<uint32_t *>(st + (int64_t)(S - 1) * hw + oyl * kOut84 + ox0) = packed;
+    }
+}
+
 std::mutex g_tab_mu;
 int g_tab_dev_mask = 0;
 int g_tab_oh = 0, g_tab_ow = 0;
@@ -196,6 +321,22 @@ int check_out(int OH, int OW)
 
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+// the stack update (and, with S = 1, the plain preprocess) on the HBM-rate band kernel where
+// the shape is the 84x84 pipeline, the per-pixel kernel for other targets
+int launch_stack(const uint8_t *frames, const uint8_t *done_row, int64_t N, int S, int OH, int OW, uint8_t *stack,
+                 hipStream_t s)
+{
+    if (OH == kOut84 && OW == kOut84 && S >= 1 && S <= kMaxStackFast) {
+        GS_REQUIRE(N * kBands < ((int64_t)1 << 31), "gs_atari: %lld envs exceed the launch grid", (long long)N);
+        hipLaunchKernelGGL(k_atari_stack84, dim3((unsigned)(N * kBands)), dim3(256), 0, s, frames, done_row, N, S, stack);
+        GS_LAUNCH_CHECK("k_atari_stack84");
+        return GS_OK;
+    }
+    hipLaunchKernelGGL(k_atari_stack, dim3(nblk(N * OH * OW)), dim3(256), 0, s, frames, done_row, N, S, OH, OW, stack);
+    GS_LAUNCH_CHECK("k_atari_stack");
+    return GS_OK;
+}
+
 }  // namespace
 
 extern "C" int gs_atari_preprocess(const uint8_t *frames, int64_t N, int32_t out_h, int32_t out_w, uint8_t *out,
@@ -206,6 +347,8 @@ extern "C" int gs_atari_preprocess(const uint8_t *frames, int64_t N, int32_t out
     if (rc) return rc;
     if ((rc = ensure_tables(out_h, out_w))) return rc;
     if (N == 0) return GS_OK;
+    if (out_h == kOut84 && out_w == kOut84)       // one frame per env: a stack of 1
+        return launch_stack(frames, nullptr, N, 1, out_h, out_w, out, (hipStream_t)stream);
     hipLaunchKernelGGL(k_atari_preprocess, dim3(nblk(N * out_h * out_w)), dim3(256), 0, (hipStream_t)stream, frames, N,
                        out_h, out_w, out);
     GS_LAUNCH_CHECK("k_atari_preprocess");
@@ -243,10 +386,7 @@ extern "C" int gs_atari_env_reset(int32_t *state, float *ep_ret, uint8_t *stack,
     GS_HIP(hipMemsetAsync(ep_ret, 0, sizeof(float) * N, s));
     hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
                        env_offset, (uint64_t)0, (const uint64_t *)nullptr);
-    hipLaunchKernelGGL(k_atari_stack, dim3(nblk(N * out_h * out_w)), dim3(256), 0, s, frames, (const uint8_t *)nullptr,
-                       N, stack_n, out_h, out_w, stack);
-    GS_LAUNCH_CHECK("k_atari_stack");
-    return GS_OK;
+    return launch_stack(frames, nullptr, N, stack_n, out_h, out_w, stack, s);
 }
 
 extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, uint8_t *frames, int64_t N,
@@ -267,8 +407,5 @@ extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, 
                        ep_len_sum, clock);
     hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
                        env_offset, step_count, clock);
-    hipLaunchKernelGGL(k_atari_stack, dim3(nblk(N * out_h * out_w)), dim3(256), 0, s, frames, dones_row, N, stack_n,
-                       out_h, out_w, stack);
-    GS_LAUNCH_CHECK("k_atari_stack");
-    return GS_OK;
+    return launch_stack(frames, dones_row, N, stack_n, out_h, out_w, stack, s);
 }

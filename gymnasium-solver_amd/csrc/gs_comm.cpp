@@ -78,6 +78,29 @@ extern "C" int gs_comm_allreduce_mean_f32(gs_comm *comm, float *buf, int64_t cou
     return GS_OK;
 }
 
+extern "C" int gs_comm_allreduce_sum_f64(gs_comm *comm, double *buf, int64_t count, void *stream)
+{
+    if (!comm || (!buf && count > 0) || count < 0 || ((uintptr_t)buf & 15)) {
+        gs::set_error("gs_comm_allreduce_sum_f64: bad argument (16-byte aligned buffer of count >= 0 doubles)");
+        return GS_E_INVALID;
+    }
+    if (count == 0) return GS_OK;
+    if (comm->kind == gs::kCommXgmi) {
+        // pieces of at most the communicator's capacity (cap floats = cap / 2 doubles), each one
+        // exchange on the same workgroups / flags / parity slots as the gradient exchange
+        const int64_t per = comm->cap / 2;
+        for (int64_t o = 0; o < count; o += per) {
+            const int64_t m = count - o < per ? count - o : per;
+            const int rc = gs::xgmi_exchange(comm, reinterpret_cast<float *>(buf + o), 2 * m, gs::Part1Fold{}, nullptr,
+                                             nullptr, nullptr, 1.0f, (hipStream_t)stream, true);
+            if (rc) return rc;
+        }
+        return GS_OK;
+    }
+    GS_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, (ncclComm_t)comm->nccl, (hipStream_t)stream));
+    return GS_OK;
+}
+
 extern "C" int gs_comm_info(gs_comm *comm, int *nranks, int *rank, int *transport)
 {
     if (!comm) {

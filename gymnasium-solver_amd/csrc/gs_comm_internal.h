@@ -77,6 +77,7 @@ int comm_sumsq_slots(const gs_comm *c);
 bool xgmi_bwd_args(const gs_comm *c, BwdXchg *bx);
 
 // xGMI kernel launcher (gs_xgmi.hip)
+// f64: G holds n / 2 doubles, summed in double in the same rank order (no fold, no sumsq)
 int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
-                  float scale, hipStream_t s);
+                  float scale, hipStream_t s, bool f64 = false);
 }  // namespace gs

@@ -108,14 +108,24 @@ __host__ __device__ __forceinline__ int64_t part1_index(const Layout &L, int64_t
 template <int D_, int H1_, int H2_, int A_, int B_>
 struct ShapeC {
     static constexpr int AMAX = A_, AEX = A_, H1c = H1_, Bc = B_;
+    static constexpr bool BF = false;     // bf16 MFMA operands (Bf16Shape)
     __host__ __device__ static constexpr Layout lay(const Layout &) { return Layout::make(D_, H1_, H2_, A_); }
     __host__ __device__ static constexpr int batch(int b) { return B_ > 0 ? B_ : b; }
 };
 template <int AMAX_>
 struct ShapeR {
     static constexpr int AMAX = AMAX_, AEX = 0, H1c = 0, Bc = 0;
+    static constexpr bool BF = false;
     __host__ __device__ static Layout lay(const Layout &L) { return L; }
     __host__ __device__ static int batch(int b) { return b; }
+};
+
+// The MLP update chain's bf16 mode (GS_HP_BF16, precision: bf16): the same compile-time shape with
+// bf16 MFMA operands in the fused forward / backward (fp32 accumulation, parameters, moments,
+// loss, clip and Adam)
+template <class S>
+struct Bf16Shape : S {
+    static constexpr bool BF = true;
 };
 
 constexpr int kTile = 16;        // MFMA 16x16x4 f32 output tile
@@ -187,6 +197,7 @@ struct LossArgs {
     const float *adv_stats;     // per minibatch {mean, std} (f32) of the global minibatch's advantages
     double *sums_out;           // per minibatch kNumSums raw loss sums of this rank's rows
     float *kl_part;             // unfused chain: this rank's share of approx_kl (the exchange sums it)
+    int bf16;                   // GS_HP_BF16: the fused MLP chain's MFMA operands in bf16
 };
 
 struct AdamArgs {
@@ -280,6 +291,7 @@ int launch_kl_decide(const float *kl, float target_kl, int32_t *stop, float *met
 int launch_metrics_all(const Layout &L, int64_t B, int64_t n, const FusedFwd &ff, const LossArgs &la, float *metrics,
                        hipStream_t s);
 bool has_fused(const Layout &L, int64_t B);
+bool has_bf16_chain(const Layout &L, int64_t B);     // the fused chain's bf16 instantiation exists
 int launch_fwd_hidden(const float *params, const Layout &L, const float *obs, const int32_t *idx,
                       int64_t T, int64_t N, int64_t rows, float *x_out, float *h1_out, float *h2_out,
                       float *zpart, float *obs_copy, const int32_t *stop_flag, const RowGather *rg, hipStream_t s, uint16_t *h2mask = nullptr);
@@ -309,6 +321,11 @@ int launch_act_stats(const float *P, const Layout &L, const float *obs, const in
 // fused update, exchange launched behind k_bwd: step ff.k_local's head record from the exchanged G
 int launch_head_sq(const Layout &L, const float *G, float scale, const FusedFwd &ff, hipStream_t s);
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);
+// global-minibatch mode around the update (gs_ppo_global_adv_stats / gs_ppo_global_records)
+int launch_global_adv_sums(const int32_t *idx, int64_t n, int64_t B, const float *adv, int64_t T, int64_t N,
+                           double *sums, hipStream_t s);
+int launch_global_adv_stats(const double *sums, int64_t n, int64_t Bg, float *stats, hipStream_t s);
+int launch_global_records(const double *sums, int64_t n, const LossArgs &la, float *metrics, hipStream_t s);
 int launch_sumsq_flat(const float *G, int64_t n, float *out, int nblocks, hipStream_t s);
 
 // ---- bf16 MFMA operands of the NatureCNN path (GS_HP_BF16 performance mode) ----------------

@@ -81,6 +81,15 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c)
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// bf16 mode: two K-chunks of 16 (lane quarter q's k = 4q..4q+3 of each chunk, the fp32 chain's
+// operand layout) as one v_mfma_f32_16x16x32_bf16 — elements 0..3 from chunk c, 4..7 from chunk
+// c + 1, the same order in both operands, so the product sums all 32 k; fp32 accumulation
+__device__ __forceinline__ f32x4 mfma_bf16_pair(float4 a0, float4 a1, float4 b0, float4 b1, f32x4 c)
+{
+    return mfma16_bf16(bf16_frag(a0, a1), bf16_frag(b0, b1), c);
+}
+__device__ __forceinline__ float4 f4(const float (&v)[4]) { return make_float4(v[0], v[1], v[2], v[3]); }
+
 // env-major sample index (utils/rollout_buffer.py:11-13) -> time-major buffer row
 __device__ __forceinline__ int sample_row(int s, int T, int N)
 {
@@ -710,6 +719,19 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         const int nch = H1 / kTile;
         const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (S::BF) {
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+            for (int ch = ch0; ch < ch1; ch += 2) {
+                const int k = ch * kTile + 4 * q;
+                const bool two = ch + 1 < ch1;
+                const float4 a0 = *reinterpret_cast<const float4 *>(h1s + i * ldh + k);
+                const float4 b0 = *reinterpret_cast<const float4 *>(W2s + i * ldh + k);
+                const float4 a1 = two ? *reinterpret_cast<const float4 *>(h1s + i * ldh + k + kTile) : z4;
+                const float4 b1 = two ? *reinterpret_cast<const float4 *>(W2s + i * ldh + k + kTile) : z4;
+                acc0 = mfma_bf16_pair(a0, a1, b0, b1, acc0);
+            }
+        } else {
 #pragma unroll 4
         for (int ch = ch0; ch < ch1; ++ch) {
             const int k = ch * kTile + 4 * q;
@@ -719,6 +741,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             acc1 = mfma4(a.y, b.y, acc1);
             acc0 = mfma4(a.z, b.z, acc0);
             acc1 = mfma4(a.w, b.w, acc1);
+        }
         }
         const f32x4 acc = acc0 + acc1;
 #pragma unroll
@@ -1690,10 +1713,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
 #pragma unroll
             for (int t = 0; t < 3; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
             float dsum = 0.0f;      // db2 partial of this lane's rows (k-block 0)
-#pragma unroll 2
-            for (int ch = ch0; ch < ch1; ++ch) {
-                const int b = ch * kTile + 4 * lq;
-                float av[4];
+            // lane's dh2 operand of rows b..b+3
+            auto dh2_rows = [&](int b, float (&av)[4]) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     float sacc = 0.0f;
@@ -1701,6 +1722,36 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     for (int a = 0; a < 5; ++a) sacc = a < A1 ? fmaf(dzs[(b + c) * A1 + a], w[a], sacc) : sacc;
                     av[c] = (mkA[b + c] >> li) & 1 ? sacc : 0.0f;
                 }
+            };
+            if constexpr (S::BF) {
+                // bf16 mode: chunk pairs (the fast path only has the ka dW2 tiles, no ones tile)
+                const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+                for (int ch = ch0; ch < ch1; ch += 2) {
+                    const int b = ch * kTile + 4 * lq;
+                    const bool two = ch + 1 < ch1;
+                    float av0[4], av1[4] = {0.f, 0.f, 0.f, 0.f};
+                    dh2_rows(b, av0);
+                    if (two) dh2_rows(b + kTile, av1);
+                    if (kb == 0) {
+                        dsum = (((dsum + av0[0]) + av0[1]) + av0[2]) + av0[3];
+                        dsum = (((dsum + av1[0]) + av1[1]) + av1[2]) + av1[3];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        if (t >= nt) break;
+                        const float *hb = h1T + (t * kTile + li) * ld + b;
+                        const float4 bb0 = *reinterpret_cast<const float4 *>(hb);
+                        const float4 bb1 = two ? *reinterpret_cast<const float4 *>(hb + kTile) : z4;
+                        acc[t][0] = mfma_bf16_pair(f4(av0), f4(av1), bb0, bb1, acc[t][0]);
+                    }
+                }
+            } else {
+#pragma unroll 2
+            for (int ch = ch0; ch < ch1; ++ch) {
+                const int b = ch * kTile + 4 * lq;
+                float av[4];
+                dh2_rows(b, av);
                 if (kb == 0) dsum = (((dsum + av[0]) + av[1]) + av[2]) + av[3];
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
@@ -1712,6 +1763,7 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     acc[t][0] = mfma4(av[2], bb.z, acc[t][0]);
                     acc[t][1] = mfma4(av[3], bb.w, acc[t][1]);
                 }
+            }
             }
             GS_STAMP(1)
 #pragma unroll
@@ -1971,15 +2023,14 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
 #pragma unroll
             for (int a = 0; a < 5; ++a) dzr[a] = a < A1 ? dzs[row * A1 + a] : 0.0f;
             const float *brow = W2T + li * ld;
-#pragma unroll 2
-            for (int ch = chb; ch < che; ++ch) {
+            // the lane's dh2 operand of hidden units n..n+3 (chunk ch)
+            auto dh2_cols = [&](int ch, float (&av)[4]) {
                 const int n = ch * kTile + 4 * lq;
                 const unsigned m = (unsigned)(mkB[row * sh.ncb + ch] >> (4 * lq));
                 float4 wh[5];
 #pragma unroll
                 for (int a = 0; a < 5; ++a)
                     wh[a] = a < A1 ? *reinterpret_cast<const float4 *>(whs + a * H2 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-                float av[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float sacc = 0.0f;
@@ -1990,11 +2041,32 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                     }
                     av[j] = ((m >> j) & 1u) ? sacc : 0.0f;
                 }
+            };
+            if constexpr (S::BF) {
+                const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+                for (int ch = chb; ch < che; ch += 2) {
+                    const int n = ch * kTile + 4 * lq;
+                    const bool two = ch + 1 < che;
+                    float av0[4], av1[4] = {0.f, 0.f, 0.f, 0.f};
+                    dh2_cols(ch, av0);
+                    if (two) dh2_cols(ch + 1, av1);
+                    const float4 w0 = *reinterpret_cast<const float4 *>(brow + n);
+                    const float4 w1 = two ? *reinterpret_cast<const float4 *>(brow + n + kTile) : z4;
+                    acc0 = mfma_bf16_pair(f4(av0), f4(av1), w0, w1, acc0);
+                }
+            } else {
+#pragma unroll 2
+            for (int ch = chb; ch < che; ++ch) {
+                const int n = ch * kTile + 4 * lq;
+                float av[4];
+                dh2_cols(ch, av);
                 const float4 w = *reinterpret_cast<const float4 *>(brow + n);
                 acc0 = mfma4(av[0], w.x, acc0);
                 acc1 = mfma4(av[1], w.y, acc1);
                 acc0 = mfma4(av[2], w.z, acc0);
                 acc1 = mfma4(av[3], w.w, acc1);
+            }
             }
             GS_STAMP(1)
         } else {
@@ -2234,19 +2306,33 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 const int nch = Bp / kTile;
                 const int ch0 = (wave * nch) / 4, ch1 = ((wave + 1) * nch) / 4;
                 f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    #pragma unroll 2
-                for (int ch = ch0; ch < ch1; ++ch) {
-                    const int b = ch * kTile + 4 * lq;
-                    float av[4], bv[4];
+                auto chunk = [&](int b, float (&av)[4], float (&bv)[4]) {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
                         av[c] = li < A1 ? dzs[(b + c) * A1 + li] : 0.0f;
                         bv[c] = hs[(b + c) * 17 + li];
                     }
+                };
+                if constexpr (S::BF) {
+#pragma unroll 2
+                    for (int ch = ch0; ch < ch1; ch += 2) {
+                        const int b = ch * kTile + 4 * lq;
+                        float av0[4], bv0[4], av1[4] = {0.f, 0.f, 0.f, 0.f}, bv1[4] = {0.f, 0.f, 0.f, 0.f};
+                        chunk(b, av0, bv0);
+                        if (ch + 1 < ch1) chunk(b + kTile, av1, bv1);
+                        acc0 = mfma_bf16_pair(f4(av0), f4(av1), f4(bv0), f4(bv1), acc0);
+                    }
+                } else {
+    #pragma unroll 2
+                for (int ch = ch0; ch < ch1; ++ch) {
+                    const int b = ch * kTile + 4 * lq;
+                    float av[4], bv[4];
+                    chunk(b, av, bv);
                     acc0 = mfma4(av[0], bv[0], acc0);
                     acc1 = mfma4(av[1], bv[1], acc1);
                     acc0 = mfma4(av[2], bv[2], acc0);
                     acc1 = mfma4(av[3], bv[3], acc1);
+                }
                 }
                 const f32x4 acc = acc0 + acc1;
 #pragma unroll
@@ -2608,8 +2694,40 @@ static int set_lds_limit(const void *fn, size_t bytes)
     return GS_OK;
 }
 
+// the bf16 mode's instantiations: compile-time shapes whose backward forms dh2 in registers
+// (the fast role-A / role-B paths carry the bf16 operand pairs)
+template <class Sh>
+constexpr bool bf16_shape()
+{
+    if constexpr (Sh::AEX == 0 || Sh::H1c == 0 || Sh::Bc == 0) {
+        return false;
+    } else {
+        constexpr Layout Lc = Sh::lay(Layout{});
+        return Lc.A + 1 <= 5 && Lc.H2 % 64 == 0;
+    }
+}
+
+bool has_bf16_chain(const Layout &L, int64_t B)
+{
+    bool ok = false;
+    with_shape(L, B, [&](auto sh) {
+        ok = bf16_shape<decltype(sh)>();
+        return GS_OK;
+    });
+    return ok && has_fused(L, B);
+}
+
 int prepare_kernels(const Layout &L, int64_t B)
 {
+    if (has_bf16_chain(L, B)) {
+        const int rc = with_shape(L, B, [&](auto sh) {
+            using Sh = decltype(sh);
+            if constexpr (bf16_shape<Sh>())
+                return set_lds_limit((const void *)k_bwd<Bf16Shape<Sh>, true>, bwd_lds_bytes(L, B));
+            return GS_OK;
+        });
+        if (rc) return rc;
+    }
     int rc = with_shape(L, B, [&](auto sh) {
         return set_lds_limit((const void *)k_bwd<decltype(sh), false>, bwd_lds_bytes(L, B));
     });
@@ -2694,6 +2812,18 @@ int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, 
     }
     return with_shape(L, B, [&](auto sh) {
         using Sh = decltype(sh);
+        if (ff && la && la->bf16) {      // the bf16 mode (GS_HP_BF16)
+            if constexpr (bf16_shape<Sh>()) {
+                int rc = set_lds_limit((const void *)k_bwd<Bf16Shape<Sh>, true>, lds);
+                if (rc) return rc;
+                hipLaunchKernelGGL((k_bwd<Bf16Shape<Sh>, true>), dim3(nblk), dim3(256), lds, s, P, L, (int)B, ws.x,
+                                   ws.h1, ws.h2, ws.dz, G, ws.part1, ws.sumsq, stop, ws.zpart, *ff, *la, ws.h2mask, bx);
+                GS_LAUNCH_CHECK("k_bwd<bf16>");
+                return GS_OK;
+            } else {
+                GS_REQUIRE(false, "precision bf16: no bf16 instantiation of the MLP chain for this shape");
+            }
+        }
         if (ff) {
             int rc = set_lds_limit((const void *)k_bwd<Sh, true>, lds);
             if (rc) return rc;
@@ -2874,6 +3004,83 @@ __global__ __launch_bounds__(256) void k_gather_all(const int32_t *__restrict__ 
         metrics[k * GS_NUM_METRICS + GS_M_ADV_NORM_STD] =
             (float)sqrt(fmax(0.0, (st[1] - st[0] * st[0] / Bd) / (Bd - 1.0)));
     }
+}
+
+// ---- global-minibatch mode (gs_ppo_global_adv_stats / gs_ppo_global_records): everything the
+// mode adds around the update stays on the device — the per-minibatch advantage sums of this
+// rank's rows (k_global_adv_sums) and, after the communicator's f64 sum over ranks, the whole
+// minibatch's mean / unbiased std (k_global_adv_stats, utils/torch.py:97-99; the one-pass double
+// form of k_gather_all's two-pass statistics); after the update, the ranks' summed loss sums
+// turned into every evaluated minibatch's record (k_global_records: write_metrics, the
+// arithmetic of k_metrics_all over the whole global minibatch).
+__global__ __launch_bounds__(256) void k_global_adv_sums(const int32_t *__restrict__ idx, int B,
+                                                         const float *__restrict__ advantages, int T, int N,
+                                                         double *__restrict__ sums)
+{
+    __shared__ double sred[2 * (256 + 16)];
+    const int64_t k = blockIdx.x;
+    double st[2] = {0.0, 0.0};
+    for (int r = threadIdx.x; r < B; r += 256) {
+        const int si = idx[k * B + r];
+        if (si < 0) continue;       // another rank's row
+        const double a = (double)advantages[sample_row(si, T, N)];
+        st[0] += a;
+        st[1] += a * a;
+    }
+    block_reduce<2>(st, sred);
+    if (threadIdx.x == 0) {
+        sums[2 * k] = st[0];
+        sums[2 * k + 1] = st[1];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_global_adv_stats(const double *__restrict__ sums, int64_t n, int Bg,
+                                                          float *__restrict__ stats)
+{
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    const double Bd = (double)Bg, s1 = sums[2 * k], s2 = sums[2 * k + 1];
+    const double mean = s1 / Bd;
+    stats[2 * k] = (float)mean;
+    stats[2 * k + 1] = (float)sqrt(fmax(0.0, (s2 - s1 * mean) / (Bd - 1.0)));
+}
+
+__global__ __launch_bounds__(256) void k_global_records(const double *__restrict__ sums, int64_t n, LossArgs la,
+                                                        float *__restrict__ metrics)
+{
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    float *rec = metrics + k * GS_NUM_METRICS;
+    if (rec[GS_M_UNEVALUATED] != 0.0f) return;     // after the KL stop: never evaluated
+    float tmp[GS_NUM_METRICS];
+    write_metrics(sums + k * kNumSums, (double)la.batch_rows, la, tmp, true);
+    const int cols[] = {GS_M_LOSS, GS_M_POLICY_LOSS, GS_M_VALUE_LOSS, GS_M_ENTROPY, GS_M_CLIP_FRAC,
+                        GS_M_CLIP_FRAC_VF, GS_M_EXPLAINED_VAR, GS_M_KL, GS_M_APPROX_KL, GS_M_ADV_NORM_MEAN,
+                        GS_M_ADV_NORM_STD};
+#pragma unroll
+    for (int c : cols) rec[c] = tmp[c];
+}
+
+int launch_global_adv_sums(const int32_t *idx, int64_t n, int64_t B, const float *adv, int64_t T, int64_t N,
+                           double *sums, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_global_adv_sums, dim3((unsigned)n), dim3(256), 0, s, idx, (int)B, adv, (int)T, (int)N, sums);
+    GS_LAUNCH_CHECK("k_global_adv_sums");
+    return GS_OK;
+}
+
+int launch_global_adv_stats(const double *sums, int64_t n, int64_t Bg, float *stats, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_global_adv_stats, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sums, n, (int)Bg, stats);
+    GS_LAUNCH_CHECK("k_global_adv_stats");
+    return GS_OK;
+}
+
+int launch_global_records(const double *sums, int64_t n, const LossArgs &la, float *metrics, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_global_records, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sums, n, la, metrics);
+    GS_LAUNCH_CHECK("k_global_records");
+    return GS_OK;
 }
 
 // thread per minibatch: the row-block sums (fixed order) -> the metrics record
@@ -3090,6 +3297,26 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
         const float *no_obs = nullptr;
         const int32_t *no_idx = nullptr;
         float *no_copy = nullptr;
+        if (la.bf16) {      // the bf16 mode (GS_HP_BF16)
+            if constexpr (bf16_shape<Sh>() && lagged_shape<Sh>()) {
+                using Sb = Bf16Shape<Sh>;
+                if (af) {
+                    GS_REQUIRE((af->part1 ? af->aa.nrb > 0 : af->aa.nrb == 0) && af->aa.n_slots <= 512,
+                               "lagged Adam: bad slot / partial counts");
+                    hipLaunchKernelGGL((k_fwd_hidden<Sb, true, true>), grid, dim3(kFwdAdamThreads), fwd_lds_bytes(L),
+                                       s, params, L, no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart,
+                                       no_copy, stop, RowGather{}, ff, la, ws.h2mask, *af);
+                } else {
+                    hipLaunchKernelGGL((k_fwd_hidden<Sb, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L,
+                                       no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop,
+                                       RowGather{}, ff, la, ws.h2mask);
+                }
+                GS_LAUNCH_CHECK("k_fwd_hidden<fused, bf16>");
+                return GS_OK;
+            } else {
+                GS_REQUIRE(false, "precision bf16: no bf16 instantiation of the MLP chain for this shape");
+            }
+        }
         if (af) {   // forward carrying the previous minibatch's clip + Adam (dW1|db1 partials)
             if constexpr (lagged_shape<Sh>()) {
                 GS_REQUIRE((af->part1 ? af->aa.nrb > 0 : af->aa.nrb == 0) && af->aa.n_slots <= 512,

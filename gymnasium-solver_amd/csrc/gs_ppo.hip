@@ -250,6 +250,7 @@ StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, in
     a.la.ent_coef = hp.ent_coef;
     a.la.target_kl = hp.target_kl;
     a.la.normalize = hp.normalize_adv;
+    a.la.bf16 = (hp.flags & GS_HP_BF16) ? 1 : 0;
     const double b1 = hp.adam_beta1, b2 = hp.adam_beta2;
     a.aa.max_norm = hp.max_grad_norm;
     a.aa.one_minus_b1 = (float)(1.0 - b1);
@@ -586,6 +587,11 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
     const bool fused = has_fused(L, batch) && !(hp.target_kl > 0.0f) &&
                        workspace_bytes >= carve_fused(nullptr, L, batch, n_minibatches).bytes &&
                        (((uintptr_t)params | (uintptr_t)grads | (uintptr_t)adam_m | (uintptr_t)adam_v) & 15) == 0;
+    // precision bf16 (GS_HP_BF16) is a mode of the fused chain only (its kernels carry the bf16
+    // operand pairs): no silent fp32 fallback for a configuration the chain does not run
+    GS_REQUIRE(!(hp.flags & GS_HP_BF16) || (fused && has_bf16_chain(L, batch)),
+               "precision bf16: the MLP update's bf16 mode runs on the fused chain of the compile-time shapes "
+               "(CartPole 4-256-256-2 / LunarLander 8-128-128-4, B %% 16 == 0, no target_kl)");
     // the fused chain has no KL early stop (target_kl unset): its kernels get no stop flag, so
     // none of them starts with a dependent load of it
     if (fused) stop_flag = nullptr;
@@ -686,8 +692,11 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
     key.n[1] = n_minibatches;
     key.n[2] = ((int64_t)dims.obs_dim << 48) ^ ((int64_t)dims.hidden1 << 32) ^ ((int64_t)dims.hidden2 << 16) ^ dims.n_actions;
     key.n[3] = (int64_t)(intptr_t)workspace;
+    // the communicator's exchange placement is baked into the capture (gs_comm_xgmi_set_bwd_exchange)
+    BwdXchg bx_key;
+    const bool in_bwd = comm && bwd_exchange_of(comm, L, batch, &bx_key);
     key.n[4] = (int64_t)(intptr_t)stop_flag ^ ((int64_t)(intptr_t)comm << 1) ^ (fused ? 1 : 0) ^
-               ((int64_t)lagged << 62);
+               ((int64_t)lagged << 62) ^ ((int64_t)in_bwd << 61);
     key.n[5] = ro.T * 1000003 + ro.N + (glob ? glob->batch_global << 40 : 0);
     uint32_t hbits[12];
     baked_hparam_bits(hp, hbits);
@@ -813,6 +822,34 @@ extern "C" int gs_ppo_update_global(float *params, float *grads, float *adam_m, 
     GS_REQUIRE(glob->batch_global >= batch || !comm, "gs_ppo_update_global: batch_global < local rows");
     return ppo_update(params, grads, adam_m, adam_v, dims, hp, ro, idx, batch, n_minibatches, adam_step0, metrics,
                       stop_flag, workspace, workspace_bytes, comm, use_graph, stream, glob);
+}
+
+extern "C" int gs_ppo_global_adv_stats(const int32_t *idx, int64_t n_minibatches, int64_t batch, int64_t batch_global,
+                                       const float *advantages, int64_t T, int64_t N, gs_comm *comm, double *sums,
+                                       float *adv_stats, void *stream)
+{
+    GS_REQUIRE(idx && advantages && sums && adv_stats, "gs_ppo_global_adv_stats: null buffer");
+    GS_REQUIRE(n_minibatches >= 0 && batch >= 1 && batch <= 1 << 20 && batch_global >= 2 && T > 0 && N > 0,
+               "gs_ppo_global_adv_stats: bad sizes");
+    if (n_minibatches == 0) return GS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = launch_global_adv_sums(idx, n_minibatches, batch, advantages, T, N, sums, s);
+    if (rc) return rc;
+    if (comm && (rc = gs_comm_allreduce_sum_f64(comm, sums, 2 * n_minibatches, stream))) return rc;
+    return launch_global_adv_stats(sums, n_minibatches, batch_global, adv_stats, s);
+}
+
+extern "C" int gs_ppo_global_records(const gs_ppo_hparams *hp, int64_t n_minibatches, int64_t batch_global,
+                                     gs_comm *comm, double *metric_sums, float *metrics, void *stream)
+{
+    GS_REQUIRE(hp && metric_sums && metrics && n_minibatches >= 0 && batch_global >= 2,
+               "gs_ppo_global_records: bad argument");
+    if (n_minibatches == 0) return GS_OK;
+    int rc;
+    if (comm && (rc = gs_comm_allreduce_sum_f64(comm, metric_sums, kNumSumsHost * n_minibatches, stream))) return rc;
+    gs_ppo_global g{batch_global, nullptr, metric_sums};
+    const StepArgs sa = make_step_args(*hp, Layout{}, batch_global, 1, &g);
+    return launch_global_records(metric_sums, n_minibatches, sa.la, metrics, (hipStream_t)stream);
 }
 
 extern "C" int gs_ppo_graph_cache_info(int64_t *n_entries, int64_t *n_captures)

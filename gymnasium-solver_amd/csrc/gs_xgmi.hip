@@ -100,11 +100,48 @@ __device__ __forceinline__ float4 own_values(const float *__restrict__ G, const 
 
 typedef xf4 f4;
 
+// acc += b over one 16-B group: four floats, or (F64: the f64 sum exchange) two doubles
+template <bool F64>
+__device__ __forceinline__ void add_group(float4 &a, const float4 &b)
+{
+    if constexpr (F64) {
+        double2 x = *reinterpret_cast<const double2 *>(&a);
+        const double2 y = *reinterpret_cast<const double2 *>(&b);
+        x.x += y.x;
+        x.y += y.y;
+        a = *reinterpret_cast<const float4 *>(&x);
+    } else {
+        a.x += b.x;
+        a.y += b.y;
+        a.z += b.z;
+        a.w += b.w;
+    }
+}
+
+template <bool F64>
+__device__ __forceinline__ void scale_group(float4 &a, float scale)
+{
+    if constexpr (F64) {
+        double2 x = *reinterpret_cast<const double2 *>(&a);
+        x.x *= (double)scale;
+        x.y *= (double)scale;
+        a = *reinterpret_cast<const float4 *>(&x);
+    } else {
+        a.x *= scale;
+        a.y *= scale;
+        a.z *= scale;
+        a.w *= scale;
+    }
+}
+
 __device__ __forceinline__ float *slot(char *region, int par, int world, int src, int64_t cap)
 {
     return reinterpret_cast<float *>(region + kXgmiOffData) + ((int64_t)par * world + src) * cap;
 }
 
+// F64: the buffer holds doubles (xa.n = 2 x their count, fold off, no sum of squares): the same
+// transport and flags, the fixed rank-order sum taken in double (gs_comm_allreduce_sum_f64)
+template <bool F64>
 __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Part1Fold fold, XgmiArgs xa,
                                                        float *__restrict__ sumsq, int32_t *__restrict__ stop)
 {
@@ -171,15 +208,9 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Pa
         float4 a = xa.rank == 0 ? own : load_sc1(rs, src_off(0, p));
         for (int r = 1; r < xa.world; ++r) {
             const float4 b = r == xa.rank ? own : load_sc1(rs, src_off(r, p));
-            a.x += b.x;
-            a.y += b.y;
-            a.z += b.z;
-            a.w += b.w;
+            add_group<F64>(a, b);
         }
-        a.x *= xa.scale;
-        a.y *= xa.scale;
-        a.z *= xa.scale;
-        a.w *= xa.scale;
+        scale_group<F64>(a, xa.scale);
         if (p + 3 < xa.n) {
             *reinterpret_cast<float4 *>(G + p) = a;
         } else {
@@ -187,9 +218,9 @@ __global__ __launch_bounds__(256) void k_xgmi_exchange(float *__restrict__ G, Pa
             if (p + 1 < xa.n) G[p + 1] = a.y;
             if (p + 2 < xa.n) G[p + 2] = a.z;
         }
-        ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;   // lanes past n hold zeros
+        if constexpr (!F64) ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;   // lanes past n hold zeros
     }
-    if (sumsq) {
+    if (!F64 && sumsq) {
         for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
         if ((tid & 63) == 0) s_red[tid >> 6] = ss;
         __syncthreads();
@@ -257,6 +288,7 @@ __device__ __forceinline__ int wait_flags(const XgmiArgs &xa, size_t off, int w,
     return __syncthreads_or(anystop);
 }
 
+template <bool F64>
 __global__ __launch_bounds__(256) void k_xgmi_rsag(float *__restrict__ G, Part1Fold fold, XgmiArgs xa,
                                                    float *__restrict__ sumsq, int32_t *__restrict__ stop)
 {
@@ -294,16 +326,10 @@ __global__ __launch_bounds__(256) void k_xgmi_rsag(float *__restrict__ G, Part1F
         for (int r = 1; r < xa.world; ++r) {
             const float4 b = r == xa.rank ? own : load_sc1(rs, (uint32_t)(kXgmiOffData +
                                                                           4 * (((int64_t)par * xa.world + r) * xa.cap + p)));
-            a.x += b.x;
-            a.y += b.y;
-            a.z += b.z;
-            a.w += b.w;
+            add_group<F64>(a, b);
         }
-        a.x *= xa.scale;
-        a.y *= xa.scale;
-        a.z *= xa.scale;
-        a.w *= xa.scale;
-        float ss = a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;     // lanes past n hold zeros
+        scale_group<F64>(a, xa.scale);
+        float ss = F64 ? 0.0f : a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;     // lanes past n hold zeros
         for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
         if ((tid & 63) == 0) s_red[tid >> 6] = ss;
         __syncthreads();
@@ -357,8 +383,9 @@ static int nwg_of(const gs_comm *c)
 }
 
 int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float *sumsq, int *n_slots, int32_t *stop,
-                  float scale, hipStream_t s)
+                  float scale, hipStream_t s, bool f64)
 {
+    GS_REQUIRE(!f64 || (!fold.part1 && !sumsq && n % 2 == 0), "f64 exchange: no fold / sum of squares, whole doubles");
     GS_REQUIRE(c->connected, "xGMI communicator used before gs_comm_xgmi_connect");
     GS_REQUIRE(n >= 0 && n <= c->cap, "exchange of %lld floats exceeds the communicator capacity %lld",
                (long long)n, (long long)c->cap);
@@ -376,10 +403,12 @@ int xgmi_exchange(gs_comm *c, float *G, int64_t n, const Part1Fold &fold, float 
     xa.seq = c->seq;
     const int nwg = nwg_of(c);
     if (c->rsag && c->nranks > 1) {
-        hipLaunchKernelGGL(k_xgmi_rsag, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
+        if (f64) hipLaunchKernelGGL(k_xgmi_rsag<true>, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
+        else hipLaunchKernelGGL(k_xgmi_rsag<false>, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
         GS_LAUNCH_CHECK("k_xgmi_rsag");
     } else {
-        hipLaunchKernelGGL(k_xgmi_exchange, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
+        if (f64) hipLaunchKernelGGL(k_xgmi_exchange<true>, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
+        else hipLaunchKernelGGL(k_xgmi_exchange<false>, dim3((unsigned)nwg), dim3(256), 0, s, G, fold, xa, sumsq, stop);
         GS_LAUNCH_CHECK("k_xgmi_exchange");
     }
     if (n_slots) *n_slots = nwg;
@@ -537,6 +566,14 @@ extern "C" int gs_comm_xgmi_set_colocation(gs_comm *c, int ranks_per_device)
     GS_REQUIRE(ranks_per_device >= 1 && ranks_per_device <= c->nranks,
                "gs_comm_xgmi_set_colocation: %d ranks per device with %d ranks", ranks_per_device, c->nranks);
     c->colocated = ranks_per_device;
+    return GS_OK;
+}
+
+extern "C" int gs_comm_xgmi_set_bwd_exchange(gs_comm *c, int mode)
+{
+    GS_REQUIRE(c && c->kind == kCommXgmi, "gs_comm_xgmi_set_bwd_exchange: not an xGMI communicator");
+    GS_REQUIRE(mode >= 0 && mode <= 2, "gs_comm_xgmi_set_bwd_exchange: mode %d (0 launch, 1 auto, 2 forced)", mode);
+    c->bwd_xchg = mode;
     return GS_OK;
 }
 

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before the library)
 LIB_PATH = os.environ.get("GSAMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
 
 GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
-GS_ABI_VERSION = 3          # include/gsamd.h: the argument lists this binding declares
+GS_ABI_VERSION = 4          # include/gsamd.h: the argument lists this binding declares
 GS_NUM_METRICS = 24
 METRIC_SLOTS = (
     "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
@@ -127,7 +127,11 @@ def _load():
         "gs_comm_status": (ctypes.c_int, [vp]),
         "gs_comm_error_record": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "gs_comm_xgmi_set_colocation": (ctypes.c_int, [vp, ctypes.c_int]),
+        "gs_comm_xgmi_set_bwd_exchange": (ctypes.c_int, [vp, ctypes.c_int]),
         "gs_comm_allreduce_mean_f32": (ctypes.c_int, [vp, vp, i64, vp]),
+        "gs_comm_allreduce_sum_f64": (ctypes.c_int, [vp, vp, i64, vp]),
+        "gs_ppo_global_adv_stats": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, i64, vp, vp, vp, vp]),
+        "gs_ppo_global_records": (ctypes.c_int, [ctypes.POINTER(PPOHparams), i64, i64, vp, vp, vp, vp]),
         "gs_comm_info": (ctypes.c_int, [vp, vp, vp, vp]),
         "gs_comm_destroy": (ctypes.c_int, [vp]),
     }
@@ -152,8 +156,9 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status", "gs_comm_error_record",
-            "gs_comm_xgmi_set_colocation",
-            "gs_comm_allreduce_mean_f32", "gs_comm_info", "gs_comm_destroy")
+            "gs_comm_xgmi_set_colocation", "gs_comm_xgmi_set_bwd_exchange",
+            "gs_comm_allreduce_mean_f32", "gs_comm_allreduce_sum_f64", "gs_ppo_global_adv_stats",
+            "gs_ppo_global_records", "gs_comm_info", "gs_comm_destroy")
 
 
 def check(rc: int, what: str = "") -> None:

@@ -136,8 +136,9 @@ class PPOConfig:
             raise ValueError("normalize_advantages must be 'rollout', 'batch', or 'off'.")
         if self.precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {self.precision!r}")
-        if self.precision == "bf16" and self.obs_type != "rgb":
-            raise ValueError("precision 'bf16' is implemented for the NatureCNN (rgb) update; the MLP path is fp32")
+        if self.precision == "bf16" and self.obs_type != "rgb" and self.target_kl is not None:
+            raise ValueError("precision 'bf16' of the MLP update runs on its fused chain, which has no KL early "
+                             "stop: unset target_kl or use precision 'fp32'")
         if self.dp_mode not in ("local", "global"):
             raise ValueError(f"dp_mode must be 'local' or 'global', got {self.dp_mode!r}")
         if str(self.env_dynamics or "auto") not in ENV_DYNAMICS:

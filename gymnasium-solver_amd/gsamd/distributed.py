@@ -38,6 +38,19 @@ def allreduce_sum_f64(values) -> "np.ndarray":
     return t.cpu().numpy()
 
 
+def broadcast_int(value: int, src: int = 0) -> int:
+    """Rank src's integer on every rank (int64 over torch.distributed); the value itself
+    outside a multi-rank job."""
+    if not world_active():
+        return int(value)
+    import torch.distributed as dist
+    t = torch.tensor([int(value)], dtype=torch.int64)
+    if dist.get_backend() == "nccl":
+        t = t.to(torch.device("cuda", torch.cuda.current_device()))
+    dist.broadcast(t, src)
+    return int(t.item())
+
+
 def env_offset(rank: int, n_envs_per_rank: int) -> int:
     """Global id of a rank's first env: rank g owns [g·N, (g+1)·N)."""
     return int(rank) * int(n_envs_per_rank)
@@ -127,12 +140,117 @@ def xgmi_self_test(handle: int, rank: int, world_size: int, n: int, device: torc
     return True
 
 
+def _digest(t: torch.Tensor) -> bytes:
+    import hashlib
+    return hashlib.sha256(t.detach().cpu().numpy().tobytes()).digest()
+
+
+def _chain_run(handle: int, rank: int, dims, batch: int, steps: int, device: torch.device) -> torch.Tensor:
+    """One fused-chain update of `steps` minibatches through gs_ppo_update on `handle`, from a
+    fixed parameter state (identical on every rank) and a rank-specific synthetic batch set:
+    the exchange the job's own update runs, on the job's shapes.  Returns the new parameters."""
+    import numpy as np
+    from ._lib import PPOHparams, RolloutView, GS_NUM_METRICS, stream_handle
+    D, H1, H2, A = int(dims.obs_dim), int(dims.hidden1), int(dims.hidden2), int(dims.n_actions)
+    P = H1 * D + H1 + H2 * H1 + H2 + A * H2 + A + H2 + 1
+    g = np.random.default_rng(20240917)
+    p = torch.from_numpy((g.standard_normal(P) * 0.05).astype(np.float32)).to(device)
+    r = np.random.default_rng(1009 + 7919 * int(rank))
+    N = 2 * int(batch)                      # T = 1: sample index i is env i
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device)  # noqa: E731
+    obs = f32(r.uniform(-1, 1, (1, N, D)))
+    act = torch.from_numpy(r.integers(0, A, (1, N))).to(device)
+    lp, val = f32(-r.uniform(0.1, 2.0, (1, N))), f32(r.standard_normal((1, N)))
+    adv, ret = f32(r.standard_normal((1, N))), f32(r.standard_normal((1, N)))
+    idx = torch.from_numpy(np.concatenate([r.permutation(N)[:batch] for _ in range(steps)]).astype(np.int32)).to(device)
+    z = dict(dtype=torch.float32, device=device)
+    grads, m, v = torch.zeros(P, **z), torch.zeros(P, **z), torch.zeros(P, **z)
+    metrics = torch.zeros(steps, GS_NUM_METRICS, **z)
+    stop = torch.zeros(1, dtype=torch.int32, device=device)
+    ws = torch.zeros(int(lib.gs_ppo_update_workspace_bytes(dims, int(batch), steps)), dtype=torch.uint8, device=device)
+    hp = PPOHparams(0.2, 0.2, 0.5, 0.01, 0.5, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, 0)
+    view = RolloutView(obs.data_ptr(), act.data_ptr(), lp.data_ptr(), val.data_ptr(), adv.data_ptr(), ret.data_ptr(), 1, N)
+    check(lib.gs_ppo_update(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), dims, hp, view, idx.data_ptr(),
+                            int(batch), steps, 0, metrics.data_ptr(), stop.data_ptr(), ws.data_ptr(), ws.numel(),
+                            handle, 0, stream_handle()), "gs_ppo_update (exchange self-test)")
+    torch.cuda.current_stream().synchronize()
+    check(lib.gs_comm_status(handle), "gs_comm_status (exchange self-test)")
+    if not bool(torch.isfinite(p).all()):
+        raise RuntimeError("non-finite parameters after the exchange self-test chain")
+    return p
+
+
+# what the last init_xgmi_comm's self-tests found (bench.py reports it beside its line)
+LAST_SELF_TEST: dict = {}
+
+
+def bwd_exchange_self_test(handle: int, rank: int, world_size: int, dims, batch: int,
+                           device: Optional[torch.device] = None, steps: int = 4) -> dict:
+    """The in-backward exchange (the fused MLP chain's default with one rank per GPU,
+    csrc/gs_xgmi_dev.h bwd_exchange) checked on the job's own shapes before the job trains:
+    `steps` fused-chain minibatches from a fixed state, each rank on its own synthetic rows,
+    (1) with the exchange inside k_bwd — every rank must end with the same parameter bits —
+    and (2) with the separate exchange launch (the form init_xgmi_comm's vector self-test
+    proved) — the two must agree to the rounding of their different W1-partial fold order
+    (relative L2 < 1e-4, the bar of test_xgmi_bwd_exchange_matches_exchange_launch), and the
+    launch form's replicas must be bit-identical too.  A stale or torn slot read on any rank
+    breaks (1) or (2).  If the in-backward form fails, every rank switches to the launch form
+    (gs_comm_xgmi_set_bwd_exchange(0)) together; if the launch form fails as well this raises
+    on every rank (the caller falls back to RCCL).  Collective: every rank calls it together.
+    Returns {"in_bwd_checked", "in_bwd_ok", "launch_ok", "rel_l2", "steps"}."""
+    import sys
+    import numpy as np
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    out = {"in_bwd_checked": False, "in_bwd_ok": None, "launch_ok": None, "rel_l2": None, "steps": int(steps)}
+    if world_size <= 1 or not exchange_inside_bwd(handle, dims, batch):
+        return out
+    out["in_bwd_checked"] = True
+    ok_b, why = True, ""
+    try:
+        pb = _chain_run(handle, rank, dims, batch, steps, dev)
+        digests = _all_gather_bytes(_digest(pb), device)
+        ok_b = len(set(digests[32 * r:32 * (r + 1)] for r in range(world_size))) == 1
+        why = "" if ok_b else "replicas differ after the in-backward exchange"
+    except RuntimeError as e:
+        pb, ok_b, why = None, False, str(e)
+    check(lib.gs_comm_xgmi_set_bwd_exchange(handle, 0), "gs_comm_xgmi_set_bwd_exchange")
+    ok_l = True
+    try:
+        pl = _chain_run(handle, rank, dims, batch, steps, dev)
+        digests = _all_gather_bytes(_digest(pl), device)
+        ok_l = len(set(digests[32 * r:32 * (r + 1)] for r in range(world_size))) == 1
+    except RuntimeError as e:
+        pl, ok_l, why = None, False, why or str(e)
+    if ok_b and ok_l:
+        a, b = pb.double().cpu().numpy(), pl.double().cpu().numpy()
+        out["rel_l2"] = float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+        if not out["rel_l2"] < 1e-4:
+            ok_b, why = False, f"in-backward vs launch relative L2 {out['rel_l2']:.3e}"
+    ok_b, ok_l = _agree(ok_b, device), _agree(ok_l, device)
+    out["in_bwd_ok"], out["launch_ok"] = ok_b, ok_l
+    if not ok_l:
+        raise RuntimeError(f"xGMI exchange self-test: the exchange launch failed on the job's shapes: {why}")
+    # restore the placement the job asked for (1: one rank per GPU; 2 where 1 would not place it
+    # inside, i.e. GS_XGMI_BWD=1 on a shared GPU), or keep the launch form after a failure
+    check(lib.gs_comm_xgmi_set_bwd_exchange(handle, 1 if ok_b else 0), "gs_comm_xgmi_set_bwd_exchange")
+    if ok_b and not exchange_inside_bwd(handle, dims, batch):
+        check(lib.gs_comm_xgmi_set_bwd_exchange(handle, 2), "gs_comm_xgmi_set_bwd_exchange")
+    if rank == 0:
+        print(f"[gsamd] xGMI in-backward exchange self-test ({world_size} ranks, {steps} minibatches, "
+              f"dims {int(dims.obs_dim)}-{int(dims.hidden1)}-{int(dims.hidden2)}-{int(dims.n_actions)}, B={batch}): "
+              + ("replicas bit-identical, vs exchange launch rel L2 %.2e" % out["rel_l2"] if ok_b else
+                 f"FAILED ({why or 'a peer failed'}); every rank uses the exchange launch"), file=sys.stderr, flush=True)
+    return out
+
+
 def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[torch.device] = None,
-                   self_test: bool = True) -> int:
+                   self_test: bool = True, verify_shapes=None) -> int:
     """One-shot xGMI communicator for exchanges of up to max_count floats (the policy's
     parameter count): create, all-gather the handles, open the peers, barrier, then (by
     default) a bit-exact self-test agreed on by every rank.  Raises RuntimeError on every
-    rank if any rank fails (the caller may then choose RCCL instead)."""
+    rank if any rank fails (the caller may then choose RCCL instead).  verify_shapes =
+    (gs_mlp_dims, batch): also check the in-backward exchange on those shapes
+    (bwd_exchange_self_test; it drops every rank to the exchange launch if that form fails)."""
     import torch.distributed as dist
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     h, ok, why = None, True, ""
@@ -163,11 +281,50 @@ def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[
         except RuntimeError as e:
             ok, why = False, str(e)
         ok = _agree(ok, device)
+    LAST_SELF_TEST.clear()
+    LAST_SELF_TEST["exchange_launch_ok"] = bool(ok) if self_test else None
+    if ok and self_test and verify_shapes is not None:
+        try:
+            LAST_SELF_TEST.update(bwd_exchange_self_test(h, rank, world_size, verify_shapes[0], int(verify_shapes[1]),
+                                                         dev))
+        except RuntimeError as e:
+            ok, why = False, str(e)
     if not ok:
         if h:
             destroy_comm(h)
         raise RuntimeError(f"xGMI exchange unavailable on rank {rank}: {why or 'a peer failed'}")
     return h
+
+
+def replica_checksum(params: torch.Tensor) -> torch.Tensor:
+    """Two float64 checksums of a flat parameter vector on its device: the plain sum and a
+    position-weighted sum (a swapped or shifted element changes the second)."""
+    p = params.detach().double()
+    w = (torch.arange(p.numel(), device=p.device, dtype=torch.float64) % 1021) + 1.0
+    return torch.stack([p.sum(), (p * w).sum()])
+
+
+def check_replicas(params: torch.Tensor, what: str = "parameters") -> None:
+    """Every rank's parameters must be bit-identical after an update (the exchange gives every
+    rank the same mean gradient and every rank runs the same clip + Adam,
+    agents/base_agent.py:591-621).  The checksums are all-reduced as MIN and MAX; any
+    difference raises GsError on every rank, so a stale-but-finite exchange can never yield a
+    trained model or a bench number.  A no-op outside a multi-rank job."""
+    if not world_active():
+        return
+    import torch.distributed as dist
+    from ._lib import GsError
+    cs = replica_checksum(params)
+    if dist.get_backend() != "nccl":
+        cs = cs.cpu()
+    lo, hi = cs.clone(), cs.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    lo, hi, mine = lo.cpu().numpy(), hi.cpu().numpy(), cs.cpu().numpy()
+    if not (lo == hi).all():
+        raise GsError(f"replica check failed on rank {dist.get_rank()}: the ranks' {what} differ after the update "
+                      f"(checksums min {lo.tolist()}, max {hi.tolist()}, this rank {mine.tolist()}); the gradient "
+                      f"exchange delivered different data to different ranks")
 
 
 def exchange_inside_bwd(handle: int, dims, batch: int) -> bool:
@@ -179,8 +336,12 @@ def exchange_inside_bwd(handle: int, dims, batch: int) -> bool:
 
 
 def comm_status(handle: Optional[int]) -> None:
-    """Raise if an exchange on this communicator timed out waiting for a peer."""
+    """Raise if an exchange on this communicator timed out waiting for a peer.  The current
+    stream (the one the update ran on) is synchronised first: gs_comm_status reads the sticky
+    error word with a host copy, which must come after the update's exchanges ran."""
     if handle:
+        if torch.cuda.is_available():
+            torch.cuda.current_stream().synchronize()
         check(lib.gs_comm_status(handle), "gs_comm_status")
 
 

@@ -31,8 +31,8 @@ from .cnn import DeviceCNNActorCritic
 from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler, index_stream, rank_share
-from .distributed import allreduce_sum_f64, comm_status, world_active
-from .metrics import NUM_SUMS, MetricsRecorder, activation_stats, ppo_keys, ppo_records, records_from_sums
+from .distributed import allreduce_sum_f64, broadcast_int, check_replicas, comm_status, world_active
+from .metrics import NUM_SUMS, MetricsRecorder, activation_stats, ppo_keys, ppo_records
 from .schedules import SCHEDULABLE, build_schedulers
 
 STAGES = ("train",)
@@ -311,8 +311,19 @@ class DevicePPOAgent:
             z64 = dict(dtype=torch.float64, device=self.device)
             self._gsums = torch.zeros(self.n_minibatches, NUM_SUMS, **z64)
             self._adv_stats = torch.zeros(self.n_minibatches, 2, dtype=torch.float32, device=self.device)
+            self._adv_sums = torch.zeros(self.n_minibatches, 2, **z64)
             self._gidx = torch.empty(self.n_minibatches * self.batch_size, dtype=torch.int32, device=self.device)
         self._base_seed = int(torch.initial_seed())
+        if self.global_mode and self.world_size > 1 and world_active():
+            # every rank must cut its shares from the SAME global permutation (samplers.py:25-34,
+            # seed initial_seed + epoch): launchers often seed ranks differently (seed + rank), so
+            # rank 0's seed is the job's sampler seed
+            seed0 = broadcast_int(self._base_seed, 0)
+            if seed0 != self._base_seed:
+                import warnings
+                warnings.warn(f"dp_mode 'global': rank {self.rank} was seeded {self._base_seed}, using rank 0's "
+                              f"sampler seed {seed0} so every rank draws the same global minibatches")
+            self._base_seed = seed0
         if self.is_pixel:
             ws = int(lib.gs_cnn_workspace_bytes(self.policy_model.dims, self.batch_size))
         else:   # the whole update's workspace (fused chain: per-update gathered minibatch fields)
@@ -500,6 +511,12 @@ class DevicePPOAgent:
             # update): a peer that never arrived leaves this update on a non-mean gradient, so
             # training stops here with the workgroup and peer that timed out
             comm_status(self.comm)
+            # replica check: every rank must hold the same parameter bits after the update (the
+            # exchange is the only thing that keeps them equal; a stale-but-finite slot would let
+            # them drift silently) — two float64 checksums all-reduced as min / max, GsError on
+            # a mismatch (DESIGN §5 Failure surfacing)
+            if self.world_size > 1:
+                check_replicas(self.policy_model.params)
         if self.config.target_kl is None:
             self.adam_step += self.n_minibatches
         else:       # minibatches from the sticky KL stop on took no optimizer step
@@ -538,39 +555,31 @@ class DevicePPOAgent:
         return rank_share(stream, self.batch_size, self.rank, self.data_len)
 
     def _global_update(self, epoch: int, buf) -> None:
-        """gs_ppo_update_global on this rank's shares of the global minibatches: the advantage
-        statistics of every global minibatch from all ranks' rows first (two host all-reduces of
-        n doubles), the update, then every rank's raw loss sums added and turned into the
-        minibatch records (gsamd.metrics.records_from_sums) — identical on every rank."""
+        """gs_ppo_update_global on this rank's shares of the global minibatches, with the mode's
+        statistics kept on the device: gs_ppo_global_adv_stats (this rank's per-minibatch advantage
+        sums, one f64 sum over ranks through the communicator, the whole minibatch's mean / std),
+        the update, then gs_ppo_global_records (the ranks' raw loss sums added through the
+        communicator, every evaluated record rewritten from them) — identical on every rank, no
+        host round trip."""
         c, B, n, T = self.config, self.batch_size, self.n_minibatches, self.config.n_steps
         self._gidx.copy_(torch.from_numpy(self.global_shares(epoch)))
         norm = c.normalize_advantages == "batch"
+        Bg = B   # batch_size is the global minibatch size
+        comm = self.comm if self.world_size > 1 else None
+        st = stream_handle()
         if norm:     # utils/torch.py:97-99 over the whole global minibatch
-            li = self._gidx.view(n, B).long()
-            mine = li >= 0
-            lc = li.clamp(min=0)
-            adv = torch.where(mine, buf.advantages[lc % T, lc // T].double(), torch.zeros((), dtype=torch.float64,
-                                                                                           device=self.device))
-            mean = allreduce_sum_f64(adv.sum(1).cpu().numpy()) / B
-            dev = torch.where(mine, adv - torch.from_numpy(mean).to(self.device)[:, None], 0.0)
-            std = np.sqrt(allreduce_sum_f64((dev * dev).sum(1).cpu().numpy()) / (B - 1))
-            self._adv_stats.copy_(torch.from_numpy(np.stack([mean, std], 1).astype(np.float32)))
-        glob = PPOGlobal(B, ptr(self._adv_stats) if norm else None, ptr(self._gsums))
+            check(lib.gs_ppo_global_adv_stats(ptr(self._gidx), n, B, Bg, ptr(buf.advantages), T, c.n_envs, comm,
+                                              ptr(self._adv_sums), ptr(self._adv_stats), st), "gs_ppo_global_adv_stats")
+        glob = PPOGlobal(Bg, ptr(self._adv_stats) if norm else None, ptr(self._gsums))
+        hp = self.hparams()
         check(lib.gs_ppo_update_global(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
-                                       ptr(self.adam_v), self.policy_model.dims, self.hparams(), buf.view(),
+                                       ptr(self.adam_v), self.policy_model.dims, hp, buf.view(),
                                        ptr(self._gidx), B, n, self.adam_step, ptr(self.metrics_buf),
                                        ptr(self.stop_flag), ptr(self.workspace), self.workspace.numel(), self.comm,
-                                       1 if self.use_graph else 0, ctypes.byref(glob), stream_handle()),
+                                       1 if self.use_graph else 0, ctypes.byref(glob), st),
               "gs_ppo_update_global")
-        sums = allreduce_sum_f64(self._gsums.cpu().numpy().reshape(-1)).reshape(n, NUM_SUMS)
-        rec = self.metrics_buf.cpu().numpy()
-        new = records_from_sums(sums, B, float(self.vf_coef), float(self.ent_coef), norm)
-        live = rec[:, M["unevaluated"]] == 0
-        cols = [M[k] for k in ("loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
-                               "explained_var", "kl", "approx_kl", "adv_norm_mean", "adv_norm_std")]
-        for j in cols:
-            rec[live, j] = new[live, j]
-        self.metrics_buf.copy_(torch.from_numpy(rec))
+        check(lib.gs_ppo_global_records(ctypes.byref(hp), n, Bg, comm, ptr(self._gsums), ptr(self.metrics_buf), st),
+              "gs_ppo_global_records")
 
     def set_hyperparameter(self, param: str, value: float) -> None:
         """hyperparameter_mixin.py:105-114 (+ the policy_lr setter of callback_builder.py:108-113:

@@ -42,8 +42,9 @@ extern "C" {
  * must refuse a library whose version differs (argument lists change between versions:
  * version 2 added the rollout clock argument of gs_policy_act / gs_cnn_policy_act /
  * gs_env_step / gs_atari_env_step and gs_comm_error_record; version 3 widened the metric record
- * to 24 floats and added gs_ppo_update_global). */
-#define GS_ABI_VERSION 3
+ * to 24 floats and added gs_ppo_update_global; version 4 added gs_comm_xgmi_set_bwd_exchange, gs_comm_allreduce_sum_f64,
+ * gs_ppo_global_adv_stats and gs_ppo_global_records). */
+#define GS_ABI_VERSION 4
 int gs_abi_version(void);
 const char *gs_last_error(void);
 
@@ -165,9 +166,12 @@ typedef struct gs_ppo_hparams {
     int32_t normalize_adv;    /* 1 = "batch" (utils/torch.py:97-99), 0 = off */
     int32_t flags;            /* GS_HP_* bits; 0 = the fp32 parity path */
 } gs_ppo_hparams;
-/* bf16 MFMA operands (fp32 accumulation, fp32 parameters / Adam / loss) in the NatureCNN update's
- * convolutions and GEMMs — a performance mode beside the fp32 one (SURVEY.md Appendix A
- * "Precision modes"); the MLP chain ignores it. */
+/* bf16 MFMA operands (fp32 accumulation, fp32 parameters / Adam / loss) — a performance mode
+ * beside the fp32 one (SURVEY.md Appendix A "Precision modes"): the NatureCNN update's
+ * convolutions and GEMMs, and the MLP update's fused chain (gs_ppo_update: the h2 product, the
+ * dW2 / dh1 products and the head-weight gradient; compile-time shapes only, GS_E_INVALID
+ * elsewhere).  The single-step MLP entries (gs_ppo_minibatch_step, gs_ppo_loss, gs_ppo_stage)
+ * stay fp32. */
 #define GS_HP_BF16 1
 
 /* Per-minibatch metric record written by the loss kernel (floats, GS_NUM_METRICS each).
@@ -299,6 +303,21 @@ int gs_ppo_graph_cache_info(int64_t *n_entries_host, int64_t *n_captures_host);
  * exchange is empty), 0 when a separate exchange launch follows the backward (RCCL, or
  * GS_XGMI_BWD=0).  Host query (reads device attributes, launches nothing). */
 int gs_ppo_exchange_inside_bwd(struct gs_comm *comm, gs_mlp_dims dims, int64_t batch, int *inside_host);
+/* Global-minibatch mode, the device half around gs_ppo_update_global (no host round trip):
+ * gs_ppo_global_adv_stats: Sum adv and Sum adv^2 (double) of this rank's rows (idx >= 0) of every
+ * global minibatch, summed over ranks through `comm` (gs_comm_allreduce_sum_f64; comm NULL: one
+ * rank), then the whole minibatch's mean and unbiased std into adv_stats[k][2] (f32) for
+ * gs_ppo_global.adv_stats — utils/torch.py:97-99 over all G ranks' rows.  sums: 2 x n doubles of
+ * workspace (16-B aligned).  gs_ppo_global_records: after the update, the ranks' raw loss sums
+ * (gs_ppo_global.metric_sums, 14 doubles per minibatch) summed over ranks in place and every
+ * evaluated minibatch's record rewritten from them (loss, policy / value loss, entropy, clip
+ * fractions, explained variance, kl, approx_kl, normalised-advantage mean / std) — identical on
+ * every rank.  Both are stream-ordered and graph-capturable. */
+int gs_ppo_global_adv_stats(const int32_t *idx_dev, int64_t n_minibatches, int64_t batch, int64_t batch_global,
+                            const float *advantages_dev, int64_t T, int64_t N, struct gs_comm *comm, double *sums_dev,
+                            float *adv_stats_dev, void *stream);
+int gs_ppo_global_records(const gs_ppo_hparams *hp, int64_t n_minibatches, int64_t batch_global, struct gs_comm *comm,
+                          double *metric_sums_dev, float *metrics_dev, void *stream);
 
 /* ---------------------------------------------------------------- NatureCNN actor-critic (C4/C5)
  * Replaces CNNActorCritic (utils/models.py:347-455; conv 8x8s4 -> 4x4s2 -> 3x3s1 with 32/64/64
@@ -421,7 +440,18 @@ int gs_comm_error_record(struct gs_comm *comm, int *timed_out, int *workgroup, i
  * backward, as it does from 2 ranks per GPU (GS_XGMI_BWD=1 forces the in-backward form where the
  * grids fit: correct, but paced by the time-slicing).  Host-only, no GPU call. */
 int gs_comm_xgmi_set_colocation(struct gs_comm *comm, int ranks_per_device);
+/* Where the MLP update exchanges on this communicator: mode 0 = always a separate exchange
+ * launch after the backward, 1 = inside the backward where one rank runs per GPU (the default),
+ * 2 = inside the backward also for ranks sharing a GPU (GS_XGMI_BWD=1).  The launcher's
+ * connect-time self-test (gsamd.distributed.init_xgmi_comm) runs the in-backward form on the
+ * job's shapes and sets mode 0 on every rank when it fails.  Every rank must set the same mode
+ * before its next update; captured update graphs are keyed by it.  Host-only, no GPU call. */
+int gs_comm_xgmi_set_bwd_exchange(struct gs_comm *comm, int mode);
 int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
+/* Sum of `count` doubles over ranks, in place (16-B aligned buffer), the same result bits on every
+ * rank: xGMI sums the sources in rank order in double (pieces of the communicator's capacity),
+ * RCCL runs ncclAllReduce(ncclFloat64, ncclSum).  Stream-ordered. */
+int gs_comm_allreduce_sum_f64(struct gs_comm *comm, double *buf_dev, int64_t count, void *stream);
 /* What a communicator is: its rank count, this process's rank and the transport
  * (GS_COMM_RCCL / GS_COMM_XGMI).  Any out pointer may be NULL.  Host-only, no GPU call. */
 #define GS_COMM_RCCL 0

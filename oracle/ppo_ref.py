@@ -48,13 +48,28 @@ def flatten(d, dims):
     return np.concatenate([np.asarray(d[n], F32).reshape(-1) for n, _ in param_shapes(dims)])
 
 
-def forward(flat, dims, obs):
+def bf16_round(x):
+    """float32 -> nearest bfloat16 (ties to even) -> float32: the device's v_cvt_pk_bf16_f32 on
+    finite values (the bf16 mode's MFMA operands)."""
+    u = np.ascontiguousarray(x, F32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(F32).reshape(np.shape(x))
+
+
+def forward(flat, dims, obs, bf16=False):
+    """bf16: the MLP chain's bf16 mode (GS_HP_BF16) — the hidden-to-hidden product takes bf16
+    operands with fp32 accumulation (h2 = relu(bf16(h1) bf16(W2)^T + b2)); the first layer and
+    the heads stay fp32 (VALU on the device)."""
     P = unflatten(flat, dims)
     nh = len(dims) - 2
     x = np.asarray(obs, F32)
     acts = [x]
     for i in range(nh):
-        x = np.maximum(x @ P[f"backbone.{2 * i}.weight"].T + P[f"backbone.{2 * i}.bias"], F32(0))
+        W = P[f"backbone.{2 * i}.weight"]
+        if bf16 and i > 0:
+            x = np.maximum((bf16_round(x) @ bf16_round(W).T).astype(F32) + P[f"backbone.{2 * i}.bias"], F32(0))
+        else:
+            x = np.maximum(x @ W.T + P[f"backbone.{2 * i}.bias"], F32(0))
         acts.append(x)
     logits = x @ P["policy_head.weight"].T + P["policy_head.bias"]
     value = (x @ P["value_head.weight"].T + P["value_head.bias"])[:, 0]
@@ -82,12 +97,18 @@ def _max_grads(a, b):
 
 
 def ppo_loss_and_grads(flat, dims, obs, actions, old_logp, old_values, adv, ret, *, clip, clip_vf,
-                       vf_coef, ent_coef, normalize="batch"):
-    """Return (loss, metrics, flat_grads) of PPOAgent.losses_for_batch + backward."""
+                       vf_coef, ent_coef, normalize="batch", bf16=False):
+    """Return (loss, metrics, flat_grads) of PPOAgent.losses_for_batch + backward.  bf16: the
+    device MLP chain's bf16 mode — bf16-rounded operands (fp32 accumulation) in the hidden-to-
+    hidden product, the head-weight gradient (bf16(dz)^T bf16(h2)), the hidden weight gradient
+    (bf16(dh2)^T bf16(h1)) and the hidden input gradient (bf16(dh2) bf16(W2)); biases, the first
+    layer and everything else fp32."""
     B = obs.shape[0]
     P = unflatten(flat, dims)
     nh = len(dims) - 2
-    logits, value, acts = forward(flat, dims, obs)
+    assert not bf16 or nh == 2, "bf16 emulation: the two-hidden-layer MLP of the device chain"
+    bq = bf16_round if bf16 else (lambda v: v)
+    logits, value, acts = forward(flat, dims, obs, bf16=bf16)
     adv = np.asarray(adv, F32)
     metrics = {}
     if normalize == "batch":
@@ -131,17 +152,25 @@ def ppo_loss_and_grads(flat, dims, obs, actions, old_logp, old_values, adv, ret,
 
     G = {}
     x = acts[-1]
-    G["policy_head.weight"] = dlogits.T @ x
+    if bf16:
+        G["policy_head.weight"] = (bq(dlogits.astype(F32)).T @ bq(x)).astype(F32)
+        G["value_head.weight"] = (bq(dvalue.astype(F32))[None, :] @ bq(x)).astype(F32)
+    else:
+        G["policy_head.weight"] = dlogits.T @ x
+        G["value_head.weight"] = (dvalue[:, None] * x).sum(0)[None, :]
     G["policy_head.bias"] = dlogits.sum(0)
-    G["value_head.weight"] = (dvalue[:, None] * x).sum(0)[None, :]
     G["value_head.bias"] = np.array([dvalue.sum()], F32)
     dx = dlogits @ P["policy_head.weight"] + dvalue[:, None] * P["value_head.weight"]
     for i in reversed(range(nh)):
         dx = dx * (acts[i + 1] > 0)
-        G[f"backbone.{2 * i}.weight"] = dx.T @ acts[i]
+        if bf16 and i > 0:
+            G[f"backbone.{2 * i}.weight"] = (bq(dx.astype(F32)).T @ bq(acts[i])).astype(F32)
+        else:
+            G[f"backbone.{2 * i}.weight"] = dx.T @ acts[i]
         G[f"backbone.{2 * i}.bias"] = dx.sum(0)
         if i > 0:
-            dx = dx @ P[f"backbone.{2 * i}.weight"]
+            W = P[f"backbone.{2 * i}.weight"]
+            dx = (bq(dx.astype(F32)) @ bq(W)).astype(F32) if bf16 else dx @ W
 
     with np.errstate(over="ignore"):
         clipfrac = ((ratio < 1 - clip) | (ratio > 1 + clip)).mean()

@@ -143,10 +143,12 @@ def exchange_values(rank, it, n):
     return (rng.standard_normal(n) * np.exp(rng.uniform(-6, 6, n))).astype(np.float32)
 
 
-def xgmi_exchange_worker(rank, world, port, result_dir, n, iters, algo=""):
+def xgmi_exchange_worker(rank, world, port, result_dir, n, iters, algo="", f64=False):
     """Back-to-back exchanges with no host sync in between (both parity slots reused many
     times), then the device result of every iteration is saved for the parent.  algo forces
-    the exchange form (oneshot | rsag; default by rank count)."""
+    the exchange form (oneshot | rsag; default by rank count).  f64: gs_comm_allreduce_sum_f64
+    on doubles (a communicator sized for n floats: n doubles take two pieces), interleaved with
+    f32 mean exchanges on the same communicator."""
     os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
     if algo:
         os.environ["GS_XGMI_ALGO"] = algo
@@ -157,12 +159,19 @@ def xgmi_exchange_worker(rank, world, port, result_dir, n, iters, algo=""):
         from gsamd.distributed import comm_status, destroy_comm, init_xgmi_comm
         torch.cuda.set_device(0)
         h = init_xgmi_comm(rank, world, n)
-        bufs = [torch.from_numpy(exchange_values(rank, it, n)).cuda() for it in range(iters)]
+        dt = np.float64 if f64 else np.float32
+        bufs = [torch.from_numpy(exchange_values(rank, it, n).astype(dt) * (1.0 + 1e-9 * it) if f64 else
+                                 exchange_values(rank, it, n)).cuda() for it in range(iters)]
         torch.cuda.synchronize()
         dist.barrier()
         s = torch.cuda.current_stream()
         for b in bufs:
-            check(lib.gs_comm_allreduce_mean_f32(h, b.data_ptr(), n, s.cuda_stream), "allreduce")
+            if f64:
+                check(lib.gs_comm_allreduce_sum_f64(h, b.data_ptr(), n, s.cuda_stream), "allreduce f64")
+                t = torch.ones(1000, device=b.device)      # an f32 mean exchange in between
+                check(lib.gs_comm_allreduce_mean_f32(h, t.data_ptr(), 1000, s.cuda_stream), "allreduce")
+            else:
+                check(lib.gs_comm_allreduce_mean_f32(h, b.data_ptr(), n, s.cuda_stream), "allreduce")
         torch.cuda.synchronize()
         comm_status(h)
         np.save(os.path.join(result_dir, f"x{rank}.npy"), torch.stack(bufs).cpu().numpy())
@@ -414,6 +423,56 @@ def kl_one_rank_worker(rank, world, port, result_dir):
         comm = agent.comm
         del agent
         destroy_comm(comm)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def guard_worker(rank, world, port, result_dir, bwd="1"):
+    """The multi-GPU guards (DESIGN §5 Failure surfacing): init_xgmi_comm with the job's MLP
+    shapes runs the in-backward exchange self-test (GS_XGMI_BWD=1 forces that form for ranks
+    sharing the one GPU; "" leaves it off there), then one update passes the per-epoch replica
+    check, then rank 1 perturbs one parameter and the next train_epoch must raise GsError on
+    EVERY rank.  Saves the self-test record and each rank's outcome."""
+    import json
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    if bwd:
+        os.environ["GS_XGMI_BWD"] = bwd
+    else:
+        os.environ.pop("GS_XGMI_BWD", None)
+    dist = _init(rank, world, port)
+    out = {}
+    try:
+        import torch
+        from gsamd._lib import GsError
+        from gsamd.config import load_config
+        from gsamd import distributed as gd
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        torch.manual_seed(42)
+        cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, n_epochs=1))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        pm = agent.policy_model
+        agent.comm = gd.init_xgmi_comm(rank, world, pm.n_params, dev, verify_shapes=(pm.dims, agent.batch_size))
+        out["self_test"] = dict(gd.LAST_SELF_TEST)
+        out["inside"] = bool(gd.exchange_inside_bwd(agent.comm, pm.dims, agent.batch_size))
+        agent.train_epoch()
+        out["first_epoch"] = "ok"
+        if rank == 1:
+            with torch.no_grad():
+                pm.params[123] += 1e-3
+        try:
+            agent.train_epoch()
+            out["second_epoch"] = "returned"
+        except GsError as e:
+            out["second_epoch"] = "GsError"
+            out["message"] = str(e)
+        json.dump(out, open(os.path.join(result_dir, f"guard{rank}.json"), "w"))
+        dist.barrier()
+        comm = agent.comm
+        del agent
+        gd.destroy_comm(comm)
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()

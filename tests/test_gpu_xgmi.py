@@ -61,6 +61,26 @@ def test_xgmi_exchange_bit_exact(tmp_path, world, n, iters, algo):
             assert np.array_equal(outs[r][it].view(np.uint32), want.view(np.uint32)), (world, it, r)
 
 
+@pytest.mark.parametrize("world,algo", [(2, ""), (3, "rsag")])
+def test_xgmi_sum_f64_bit_exact(tmp_path, world, algo):
+    """gs_comm_allreduce_sum_f64 (the global mode's statistics exchange): doubles summed in rank
+    order in double on both transport forms, in pieces of the communicator's capacity (n doubles
+    on a communicator sized for n floats), interleaved with f32 exchanges: every element equals
+    numpy's ((x0 + x1) + x2) in float64."""
+    from _dist_workers import exchange_values, xgmi_exchange_worker
+    n, iters = 5_000, 6
+    _run(xgmi_exchange_worker, world, tmp_path, n, iters, algo, True)
+    outs = [np.load(tmp_path / f"x{r}.npy") for r in range(world)]
+    for it in range(iters):
+        vals = [exchange_values(r, it, n).astype(np.float64) * (1.0 + 1e-9 * it) for r in range(world)]
+        acc = vals[0]
+        for r in range(1, world):
+            acc = acc + vals[r]
+        for r in range(world):
+            assert outs[r].dtype == np.float64
+            assert np.array_equal(outs[r][it].view(np.uint64), acc.view(np.uint64)), (world, it, r)
+
+
 @pytest.mark.parametrize("use_graph", [False, True])
 def test_xgmi_data_parallel_ppo_replicas_identical(tmp_path, use_graph):
     from _dist_workers import xgmi_ppo_worker
@@ -291,3 +311,30 @@ def test_global_mode_reproduces_single_gpu_reference(tmp_path, fixture, world, b
         np.testing.assert_array_equal(runs[r]["rec"][:, M["loss"]], rec[:, M["loss"]])
     p = runs[0]["p"].astype(np.float64)
     assert np.linalg.norm(p - p_ref) / np.linalg.norm(p_ref) < 1e-4
+
+
+@pytest.mark.parametrize("bwd", ["1", ""])
+def test_exchange_guards_self_test_and_replica_check(tmp_path, bwd):
+    """Guards of the default multi-GPU path: (a) init_xgmi_comm(verify_shapes=…)
+    runs the in-backward exchange itself on the job's shapes (fused-chain minibatches, replicas
+    bit-identical, within rounding of the exchange launch) whenever the update would use it —
+    forced here for ranks sharing the GPU (GS_XGMI_BWD=1); with the placement off (shared GPU, no
+    force) it is skipped and the launch form is what runs; (b) train_epoch's per-epoch replica
+    check passes on a clean update and raises GsError on every rank once one rank's parameters
+    differ (a stand-in for a stale-but-finite exchange)."""
+    import json
+    from _dist_workers import guard_worker
+    _run(guard_worker, 2, tmp_path, bwd, timeout=400)
+    outs = [json.load(open(tmp_path / f"guard{r}.json")) for r in range(2)]
+    for o in outs:
+        st = o["self_test"]
+        assert st["exchange_launch_ok"] is True
+        if bwd == "1":
+            assert st["in_bwd_checked"] and st["in_bwd_ok"] and st["launch_ok"], st
+            assert 0.0 < st["rel_l2"] < 1e-4, st          # two distinct forms ran and agree to rounding
+            assert o["inside"] is True                      # the checked form stays the job's form
+        else:
+            assert not st["in_bwd_checked"] and o["inside"] is False, st
+        assert o["first_epoch"] == "ok"
+        assert o["second_epoch"] == "GsError", o
+        assert "replica check failed" in o["message"]
