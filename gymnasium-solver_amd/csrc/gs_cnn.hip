@@ -154,10 +154,11 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
 }
 
 
-__device__ __forceinline__ int64_t frame_row(const int32_t *idx, int64_t r, int64_t T, int64_t N)
+__device__ __forceinline__ int64_t frame_row(const int32_t *idx, int64_t r, int64_t T, int64_t N, bool clamp = false)
 {
     if (!idx) return r;
-    const int64_t i = idx[r];
+    int64_t i = idx[r];
+    if (clamp && i < 0) i = 0;       // global mode: another rank's row reads sample 0 (and is dead)
     const int64_t env = i / T, t = i - env * T;   // env-major sample index (rollout_buffer.py:11-13)
     return t * N + env;
 }
@@ -422,6 +423,7 @@ __device__ __forceinline__ void wg_reduce(T (&v)[NV], T *scratch)
 }
 
 constexpr int kSums = 13;
+constexpr int kNumSumsGlobal = 14;     // gs_ppo_global.metric_sums per minibatch (the MLP's 14: slot 13 unused)
 constexpr int kLossRows = 256;   // loss rows per workgroup (one per thread)
 static_assert(kSums == 13, "carve() sizes loss_part for 13 sums");
 
@@ -718,14 +720,19 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     float adv_r[NA];
     int my_act = 0;
     float my_olp = 0.f, my_ov = 0.f, my_adv = 0.f, my_ret = 0.f;
+    // global-minibatch mode (gs_cnn_ppo_update_global, la.sums_out set): a negative index is another
+    // rank's row — it reads row 0's fields, takes no loss and no gradient (dz = 0, so every weight
+    // gradient gets exact zeros from it), and the advantage statistics are the whole minibatch's
+    const bool gmode = la.sums_out != nullptr;
+    const bool my_live = !gmode || fl.idx[min(r0 + (tid & (kHeadRows - 1)), B - 1)] >= 0;
     {
         float4 th[NH], tw[NW];
         float tv[NV];
         const float4 *wp4 = reinterpret_cast<const float4 *>(P + L.oWp);
         int64_t src[NA];
 #pragma unroll
-        for (int j = 0; j < NA; ++j) src[j] = frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N);
-        const int64_t my_src = frame_row(fl.idx, min(r0 + (tid & (kHeadRows - 1)), B - 1), fl.T, fl.N);
+        for (int j = 0; j < NA; ++j) src[j] = frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N, gmode);
+        const int64_t my_src = frame_row(fl.idx, min(r0 + (tid & (kHeadRows - 1)), B - 1), fl.T, fl.N, gmode);
 #pragma unroll
         for (int j = 0; j < NH; ++j) {
             const int u = min(tid + 256 * j, nh4 - 1), r = u / H4, c4 = u - r * H4;
@@ -769,8 +776,15 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         }
     }
     float meanf = 0.f, stdf = 1.f;
-    if (la.normalize) batch_adv_stats_regs<NA>(adv_r, B, sred, meanf, stdf);    // its barriers cover the staging
-    else __syncthreads();
+    if (la.normalize && gmode) {     // the global minibatch's statistics (gs_ppo_global_adv_stats)
+        meanf = la.adv_stats[0];
+        stdf = la.adv_stats[1];
+        __syncthreads();
+    } else if (la.normalize) {
+        batch_adv_stats_regs<NA>(adv_r, B, sred, meanf, stdf);    // its barriers cover the staging
+    } else {
+        __syncthreads();
+    }
     {   // z partials: thread (row r, slice q) over k = q, q + kHeadSlices, ...
         const int r = tid / kHeadSlices, q = tid % kHeadSlices;
         float acc[4 * NZ];
@@ -805,8 +819,8 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     double acc[kSums];
 #pragma unroll
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
-    const float invB = 1.0f / (float)B;
-    if (tid < kHeadRows && r0 + tid < B) {
+    const float invB = gmode ? la.inv_batch : 1.0f / (float)B;
+    if (tid < kHeadRows && r0 + tid < B && my_live) {
         const int r = r0 + tid;
         float zr[AM + 1];
         float v = 0.f;
@@ -821,6 +835,8 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         for (int a = A1; a < ZS; ++a) dzr[a] = 0.f;
     } else if (tid < kHeadRows) {
         for (int a = 0; a < ZS; ++a) zs[tid * ZS + a] = 0.f;
+        if (r0 + tid < B)     // another rank's row (global mode): no gradient
+            for (int a = 0; a < A1; ++a) dz[(int64_t)(r0 + tid) * A1 + a] = 0.f;
     }
     wg_reduce<kSums>(acc, sred);      // its barriers publish zs (now dz) too
     if (tid == 0)
@@ -909,7 +925,13 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
             tot[tid] = v;
         }
         __syncthreads();
-        if (tid == 0) cnn_write_metrics(tot, 1, B, la, metrics, stop);
+        if (tid == 0) {
+            cnn_write_metrics(tot, 1, B, la, metrics, stop);
+            if (la.sums_out) {      // global mode: this rank's raw sums (gs_ppo_global_records' layout)
+                for (int q = 0; q < kSums; ++q) la.sums_out[q] = tot[q];
+                for (int q = kSums; q < kNumSumsGlobal; ++q) la.sums_out[q] = 0.0;
+            }
+        }
         return;
     }
     if (stop && *stop) return;
@@ -1345,20 +1367,37 @@ int validate_cnn_update(const gs_cnn_dims &dims, const gs_rollout_view_u8 &ro, i
     return GS_OK;
 }
 
+// global-minibatch mode of one minibatch (gs_cnn_ppo_update_global): its rows' frame indices
+// (another rank's rows clamped to sample 0), its global statistics and sums slots
+struct CnnGlobalStep {
+    const int32_t *frame_idx;
+    const float *adv_stats;     // {mean, std} of the global minibatch
+    double *sums;               // kNumSumsGlobal raw loss sums of this rank's rows
+    int64_t batch_global;
+};
+
 int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const gs_ppo_hparams &hp,
              const gs_rollout_view_u8 &ro, const int32_t *idx, int64_t B, int64_t adam_step, float *metrics,
-             int32_t *stop, const CnnWs &w, gs_comm *comm, hipStream_t s)
+             int32_t *stop, const CnnWs &w, gs_comm *comm, hipStream_t s, const CnnGlobalStep *gl = nullptr)
 {
     int rc;
-    const FrameSrc fs{ro.obs, idx, ro.T, ro.N};
+    const FrameSrc fs{ro.obs, gl ? gl->frame_idx : idx, ro.T, ro.N};
+    GS_REQUIRE(!gl || head_fused(L, B), "global mode: the fused head + loss kernels do not fit this shape");
     if (head_fused(L, B)) {
         const CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
+        LossArgs la = loss_args(hp);
+        if (gl) {
+            la.adv_stats = gl->adv_stats;
+            la.sums_out = gl->sums;
+            la.batch_rows = (int)gl->batch_global;
+            la.inv_batch = 1.0f / (float)gl->batch_global;
+        }
         // the fc layer's forward and weight gradient through hipBLASLt in fp32 (dbf comes from the
         // head kernels), also in the bf16 mode: faster there than the engine's bf16 form
         const bool lib_fc = blaslt_available(false, true, B, L.HID, L.F, L.F, L.F, L.HID, true, true) &&
                             blaslt_available(true, false, L.HID, L.F, B, L.HID, L.F, L.F, false, false);
         if ((rc = forward_trunk(P, L, fs, B, w, s, lib_fc))) return rc;
-        if ((rc = launch_head_loss(P, L, B, fl, w, loss_args(hp), G, metrics, stop, s))) return rc;
+        if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s))) return rc;
         if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, lib_fc))) return rc;
     } else {
         hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
@@ -1373,7 +1412,9 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     if (comm) {
         int world = 1;
         if ((rc = comm_allreduce_sum(comm, G, L.P, s, &world, stop))) return rc;
-        aa.grad_scale = 1.0f / (float)world;
+        // global mode: each rank's gradient is its share of the global minibatch's mean (the loss
+        // divides by batch_global), so the sum over ranks is the gradient itself
+        aa.grad_scale = gl ? 1.0f : 1.0f / (float)world;
     }
     hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
                        L.oWv);
@@ -1442,6 +1483,38 @@ extern "C" int gs_cnn_ppo_loss(const float *params, gs_cnn_dims dims, gs_ppo_hpa
     if ((rc = launch_cnn_loss(w.z, params, L, batch, w, loss_args(hp), dlogits_out ? dlogits_out : w.dz, metrics,
                               nullptr, s)))
         return rc;
+    return GS_OK;
+}
+
+extern "C" int gs_cnn_ppo_update_global(float *params, float *grads, float *adam_m, float *adam_v, gs_cnn_dims dims,
+                                        gs_ppo_hparams hp, gs_rollout_view_u8 ro, const int32_t *idx,
+                                        const int32_t *frame_idx, int64_t batch, int64_t n_minibatches,
+                                        int64_t adam_step0, float *metrics, int32_t *stop_flag, void *workspace,
+                                        gs_comm *comm, const gs_ppo_global *glob, void *stream)
+{
+    int rc = validate_cnn_update(dims, ro, batch, workspace);
+    if (rc) return rc;
+    GS_REQUIRE(n_minibatches >= 0 && adam_step0 >= 0, "bad n_minibatches/adam_step0");
+    GS_REQUIRE(params && grads && adam_m && adam_v && idx && frame_idx && metrics,
+               "gs_cnn_ppo_update_global: null buffer");
+    GS_REQUIRE(glob && glob->batch_global >= 2 && glob->metric_sums && (!hp.normalize_adv || glob->adv_stats),
+               "gs_cnn_ppo_update_global: bad global arguments");
+    GS_REQUIRE(!(hp.target_kl > 0.0f), "gs_cnn_ppo_update_global: the NatureCNN global mode has no KL early stop "
+                                       "(target_kl must be unset)");
+    GS_REQUIRE((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)adam_m | (uintptr_t)adam_v) & 15) == 0,
+               "gs_cnn_ppo_update_global: params / grads / adam_m / adam_v must be 16-byte aligned");
+    GS_REQUIRE(ro.T * ro.N < ((int64_t)1 << 31), "rollout larger than 2^31 samples");
+    const Bf16Scope prec((hp.flags & GS_HP_BF16) != 0);
+    hipStream_t s = (hipStream_t)stream;
+    const CnnLayout L = CnnLayout::make(dims);
+    const CnnWs w = carve(workspace, L, batch);
+    for (int64_t k = 0; k < n_minibatches; ++k) {
+        const CnnGlobalStep gl{frame_idx + k * batch, glob->adv_stats ? glob->adv_stats + 2 * k : nullptr,
+                               glob->metric_sums + kNumSumsGlobal * k, glob->batch_global};
+        rc = cnn_step(params, grads, adam_m, adam_v, L, hp, ro, idx + k * batch, batch, adam_step0 + k + 1,
+                      metrics + k * GS_NUM_METRICS, stop_flag, w, comm, s, &gl);
+        if (rc) return rc;
+    }
     return GS_OK;
 }
 

@@ -111,6 +111,8 @@ def _load():
         "gs_cnn_ppo_loss": (ctypes.c_int, [vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, vp, vp, vp, vp]),
         "gs_cnn_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, i64, i64,
                                              vp, vp, vp, vp, vp]),
+        "gs_cnn_ppo_update_global": (ctypes.c_int, [vp, vp, vp, vp, CnnDims, PPOHparams, RolloutViewU8, vp, vp, i64, i64,
+                                                    i64, vp, vp, vp, vp, ctypes.POINTER(PPOGlobal), vp]),
         "gs_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64,
                                        f32, vp, ctypes.c_int, vp]),
         "gs_cartpole_reset": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, vp]),
@@ -154,6 +156,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_ppo_update_global", "gs_ppo_update_workspace_bytes",
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
+            "gs_cnn_ppo_update_global",
             "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status", "gs_comm_error_record",
             "gs_comm_xgmi_set_colocation", "gs_comm_xgmi_set_bwd_exchange",

@@ -305,14 +305,16 @@ class DevicePPOAgent:
         # minibatches of the whole job's rollout, its own rows of each padded to B
         self.global_mode = str(getattr(c, "dp_mode", "local")) == "global"
         if self.global_mode:
-            if self.is_pixel:
-                raise ValueError("dp_mode 'global' is implemented for the MLP update (gs_ppo_update_global)")
+            if self.is_pixel and c.target_kl is not None:
+                raise ValueError("dp_mode 'global' of the NatureCNN update has no KL early stop: unset target_kl")
             self.n_minibatches = self.data_len * self.world_size // self.batch_size * c.n_epochs
             z64 = dict(dtype=torch.float64, device=self.device)
             self._gsums = torch.zeros(self.n_minibatches, NUM_SUMS, **z64)
             self._adv_stats = torch.zeros(self.n_minibatches, 2, dtype=torch.float32, device=self.device)
             self._adv_sums = torch.zeros(self.n_minibatches, 2, **z64)
             self._gidx = torch.empty(self.n_minibatches * self.batch_size, dtype=torch.int32, device=self.device)
+            if self.is_pixel:     # frame reads of another rank's rows go to sample 0 (dead rows)
+                self._fidx = torch.empty_like(self._gidx)
         self._base_seed = int(torch.initial_seed())
         if self.global_mode and self.world_size > 1 and world_active():
             # every rank must cut its shares from the SAME global permutation (samplers.py:25-34,
@@ -555,7 +557,8 @@ class DevicePPOAgent:
         return rank_share(stream, self.batch_size, self.rank, self.data_len)
 
     def _global_update(self, epoch: int, buf) -> None:
-        """gs_ppo_update_global on this rank's shares of the global minibatches, with the mode's
+        """gs_ppo_update_global (MLP) / gs_cnn_ppo_update_global (NatureCNN) on this rank's shares
+        of the global minibatches, with the mode's
         statistics kept on the device: gs_ppo_global_adv_stats (this rank's per-minibatch advantage
         sums, one f64 sum over ranks through the communicator, the whole minibatch's mean / std),
         the update, then gs_ppo_global_records (the ranks' raw loss sums added through the
@@ -572,12 +575,20 @@ class DevicePPOAgent:
                                               ptr(self._adv_sums), ptr(self._adv_stats), st), "gs_ppo_global_adv_stats")
         glob = PPOGlobal(Bg, ptr(self._adv_stats) if norm else None, ptr(self._gsums))
         hp = self.hparams()
-        check(lib.gs_ppo_update_global(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
-                                       ptr(self.adam_v), self.policy_model.dims, hp, buf.view(),
-                                       ptr(self._gidx), B, n, self.adam_step, ptr(self.metrics_buf),
-                                       ptr(self.stop_flag), ptr(self.workspace), self.workspace.numel(), self.comm,
-                                       1 if self.use_graph else 0, ctypes.byref(glob), st),
-              "gs_ppo_update_global")
+        if self.is_pixel:
+            torch.clamp(self._gidx, min=0, out=self._fidx)
+            check(lib.gs_cnn_ppo_update_global(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                               ptr(self.adam_v), self.policy_model.dims, hp, buf.view(),
+                                               ptr(self._gidx), ptr(self._fidx), B, n, self.adam_step,
+                                               ptr(self.metrics_buf), ptr(self.stop_flag), ptr(self.workspace),
+                                               self.comm, ctypes.byref(glob), st), "gs_cnn_ppo_update_global")
+        else:
+            check(lib.gs_ppo_update_global(ptr(self.policy_model.params), ptr(self.grads), ptr(self.adam_m),
+                                           ptr(self.adam_v), self.policy_model.dims, hp, buf.view(),
+                                           ptr(self._gidx), B, n, self.adam_step, ptr(self.metrics_buf),
+                                           ptr(self.stop_flag), ptr(self.workspace), self.workspace.numel(),
+                                           self.comm, 1 if self.use_graph else 0, ctypes.byref(glob), st),
+                  "gs_ppo_update_global")
         check(lib.gs_ppo_global_records(ctypes.byref(hp), n, Bg, comm, ptr(self._gsums), ptr(self.metrics_buf), st),
               "gs_ppo_global_records")
 

@@ -43,7 +43,7 @@ extern "C" {
  * version 2 added the rollout clock argument of gs_policy_act / gs_cnn_policy_act /
  * gs_env_step / gs_atari_env_step and gs_comm_error_record; version 3 widened the metric record
  * to 24 floats and added gs_ppo_update_global; version 4 added gs_comm_xgmi_set_bwd_exchange, gs_comm_allreduce_sum_f64,
- * gs_ppo_global_adv_stats and gs_ppo_global_records). */
+ * gs_ppo_global_adv_stats, gs_ppo_global_records and gs_cnn_ppo_update_global). */
 #define GS_ABI_VERSION 4
 int gs_abi_version(void);
 const char *gs_last_error(void);
@@ -364,6 +364,20 @@ int gs_cnn_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, fl
                       gs_ppo_hparams hp, gs_rollout_view_u8 rollout, const int32_t *idx_dev, int64_t batch,
                       int64_t n_minibatches, int64_t adam_step0, float *metrics_dev, int32_t *stop_flag_dev,
                       void *workspace_dev, struct gs_comm *comm, void *stream);
+/* Global-minibatch mode of the NatureCNN update (dp_mode "global", the MLP's gs_ppo_update_global
+ * for NatureCNN): idx = this rank's rows of every global minibatch (-1 = another rank's row),
+ * frame_idx = the same with -1 replaced by a valid sample (those rows are read but dead: zero
+ * dLoss/dz, so every gradient gets exact zeros from them); advantage statistics from
+ * glob->adv_stats (gs_ppo_global_adv_stats), the loss averaged over glob->batch_global rows, the
+ * exchange summing the ranks' shares (no 1/world), and this rank's raw loss sums in
+ * glob->metric_sums (14 per minibatch, slot 13 zero) for gs_ppo_global_records.  No KL early
+ * stop (target_kl must be unset).  Replaces agents/base_agent.py:591-621 over the reference's
+ * single-process minibatches (utils/samplers.py:25-34, utils/torch.py:97-99). */
+int gs_cnn_ppo_update_global(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev,
+                             gs_cnn_dims dims, gs_ppo_hparams hp, gs_rollout_view_u8 rollout, const int32_t *idx_dev,
+                             const int32_t *frame_idx_dev, int64_t batch, int64_t n_minibatches, int64_t adam_step0,
+                             float *metrics_dev, int32_t *stop_flag_dev, void *workspace_dev, struct gs_comm *comm,
+                             const gs_ppo_global *glob, void *stream);
 
 /* ---------------------------------------------------------------- CartPole-v1 dynamics (f1)
  * gymnasium 1.x CartPoleEnv.step restated on device (double-precision state, Euler, tau 0.02,

@@ -476,3 +476,46 @@ def guard_worker(rank, world, port, result_dir, bwd="1"):
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()
+
+
+def cnn_global_worker(rank, world, port, result_dir, ref_path):
+    """dp_mode 'global' for NatureCNN (gs_cnn_ppo_update_global): the single-process run's 8
+    Breakout envs split 4 + 4 over 2 same-device ranks, each replaying that run's actions of its
+    envs for two rollouts + updates.  Saves every minibatch record and the final parameters."""
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd.config import load_config
+        from gsamd.distributed import comm_status, destroy_comm, init_xgmi_comm
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        z = np.load(ref_path)
+        N, T = (int(x) for x in z["NT"])
+        n = N // world
+        torch.manual_seed(42 + rank)        # the sampler seed comes from rank 0 (ADVICE r3)
+        cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(
+            env_dynamics="synthetic", n_envs=n, n_steps=T, batch_size=int(z["B"]), n_epochs=int(z["E"]),
+            dp_mode="global"))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        agent.policy_model.params.copy_(torch.from_numpy(z["p0"]).to(dev))
+        agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
+        coll = agent.get_rollout_collector("train")
+        recs = []
+        for ep in range(z["actions"].shape[0]):
+            acts = torch.as_tensor(z["actions"][ep][:, rank * n:(rank + 1) * n].copy()).to(dev)
+            coll.collect(replay_actions=acts)
+            agent.update_phase()
+            recs.append(agent.metrics_buf.cpu().numpy().copy())
+        torch.cuda.synchronize()
+        comm_status(agent.comm)
+        np.savez(os.path.join(result_dir, f"c{rank}.npz"), rec=np.concatenate(recs),
+                 p=agent.policy_model.params.cpu().numpy())
+        dist.barrier()
+        comm = agent.comm
+        del agent
+        destroy_comm(comm)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()

@@ -338,3 +338,50 @@ def test_exchange_guards_self_test_and_replica_check(tmp_path, bwd):
         assert o["first_epoch"] == "ok"
         assert o["second_epoch"] == "GsError", o
         assert "replica check failed" in o["message"]
+
+
+def test_cnn_global_mode_reproduces_single_gpu_run(tmp_path, cuda):
+    """dp_mode 'global' for NatureCNN: a single-process Breakout rgb_ppo run (8
+    envs x 32 steps, B = 64, 2 epochs, the local fused head + loss path: the reference's own
+    single-process math, utils/samplers.py:25-34 + utils/torch.py:97-99) against the same run as 2
+    ranks x 4 envs in global mode — global sampler order, whole-minibatch advantage statistics
+    and loss mean, the ranks' gradient shares summed, the records rebuilt from the summed loss sums
+    (all on the device), replaying the single run's actions.  Per-minibatch losses within 1e-4
+    (north_star's bar), every other record field within 1e-4 of its scale, final parameters within
+    1e-3 relative L2 (the ranks' partial sums reassociate the gradient; Adam turns that into
+    lr-sized moves on near-zero-gradient weights), replicas bitwise identical."""
+    import torch
+    from gsamd._lib import M
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    from _dist_workers import cnn_global_worker
+    N, T, B, E, epochs = 8, 32, 64, 2, 2
+    torch.manual_seed(42)
+    cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=N, n_steps=T,
+                                                                   batch_size=B, n_epochs=E))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
+    p0 = agent.policy_model.params.cpu().numpy()
+    coll = agent.get_rollout_collector("train")
+    acts, recs = [], []
+    for _ in range(epochs):
+        coll.collect()
+        acts.append(coll.buffer.actions.cpu().numpy().copy())
+        agent.update_phase()
+        recs.append(agent.metrics_buf.cpu().numpy().copy())
+    torch.cuda.synchronize()
+    rec1, p1 = np.concatenate(recs), agent.policy_model.params.cpu().numpy().astype(np.float64)
+    del agent
+    ref = tmp_path / "ref.npz"
+    np.savez(ref, NT=np.array([N, T]), B=np.int64(B), E=np.int64(E), p0=p0, actions=np.stack(acts))
+    _run(cnn_global_worker, 2, tmp_path, str(ref), timeout=400)
+    runs = [np.load(tmp_path / f"c{r}.npz") for r in range(2)]
+    assert np.array_equal(runs[0]["p"].view(np.uint32), runs[1]["p"].view(np.uint32)), "replicas diverged"
+    rec2 = runs[0]["rec"]
+    assert rec2.shape == rec1.shape
+    np.testing.assert_allclose(rec2[:, M["loss"]], rec1[:, M["loss"]], atol=1e-4, rtol=0)
+    for k in ("policy_loss", "value_loss", "entropy", "clip_fraction", "approx_kl", "adv_norm_mean", "adv_norm_std"):
+        scale = max(1.0, float(np.abs(rec1[:, M[k]]).max()))
+        np.testing.assert_allclose(rec2[:, M[k]], rec1[:, M[k]], atol=1e-4 * scale, rtol=0, err_msg=k)
+    p2 = runs[0]["p"].astype(np.float64)
+    rel = np.linalg.norm(p2 - p1) / np.linalg.norm(p1)
+    assert rel < 1e-3, rel
