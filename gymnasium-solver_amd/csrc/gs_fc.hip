@@ -1,0 +1,296 @@
+// gs_fc.hip — the NatureCNN fc layer's three GEMMs on hand-written CDNA4 MFMA kernels (no vendor
+// library): utils/models.py:56-110, h = relu(a3 Wf^T + bf) (3136 -> 512) and its backward.
+//
+//   fwd   h[B][HID]   = relu(a3[B][F] . Wf[HID][F]^T + bf)     both operands K-contiguous
+//   wgrad dWf[HID][F] = dh[B][HID]^T . a3[B][F]                  both operands K-strided (K = B)
+//   dgrad da3[B][F]   = (dh[B][HID] . Wf[HID][F]) * (a3 > 0)     A K-contiguous, B K-strided
+//
+// k_fc<BM, BN, WGM, KS, BF, AK, BKC, EPI>: 256 threads = 4 waves arranged WGM x WGN x KS; a wave
+// owns (BM/WGM) x (BN/WGN) of the output as 32 x 32 MFMA sub-tiles and, with KS > 1, every KS-th
+// k-group of each K tile (the KS partial tiles are added in ks order through LDS at the end:
+// deterministic).  Both operands are staged global -> registers -> LDS as [row][k] with k
+// contiguous (a K-strided source is transposed in registers from 4 x 4 blocks on the way), so an
+// MFMA operand is one ds_read_b128 per lane:
+//   fp32 (v_mfma_f32_32x32x2_f32, exact fp32): lane (r, q) reads k0 + 4q .. k0 + 4q + 3 of its row
+//        and MFMA j takes element j — the four MFMAs of a k-group cover k0 .. k0 + 7 once each, the
+//        same k in both operands;
+//   bf16 (GS_HP_BF16, v_mfma_f32_32x32x16_bf16): the tile is converted to bf16 (round to nearest
+//        even) as it is staged; lane (r, q) reads 8 bf16 at k0 + 8q: one MFMA per 16-k group.
+// A K tile is 128 B of every row (32 fp32 / 64 bf16) plus a 16-B pad (row stride 144 B: the 16
+// rows a ds_read_b128 lane group reads start 36 dwords apart -> distinct banks), two buffers, the
+// next tile's global loads in flight during the current tile's MFMAs, one barrier per tile.
+// Tile shapes are chosen so each launch fills the chip without split-K: fwd 32 x 64 (256
+// workgroups, KS = 2), wgrad / dgrad 64 x 64 (392 / 784 workgroups, two resident per CU).
+#include "gs_gemm.h"
+
+namespace gs {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum FcEpi { kEpiStore = 0, kEpiBiasRelu = 1, kEpiMask = 2 };
+
+constexpr int kRowBytes = 144;          // one staged K tile row: 128 B of data + 16 B pad
+
+template <bool BF>
+struct FcK {
+    static constexpr int KE = BF ? 64 : 32;     // K elements per tile
+    static constexpr int GK = BF ? 16 : 8;      // K elements per k-group (one ds_read_b128 per lane)
+    static constexpr int NG = KE / GK;          // k-groups per tile (4)
+};
+
+// 4 fp32 -> 4 bf16 (8 bytes)
+__device__ __forceinline__ uint2 pack_bf16x4(float4 v)
+{
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 r;
+    r[0] = (__bf16)v.x, r[1] = (__bf16)v.y, r[2] = (__bf16)v.z, r[3] = (__bf16)v.w;
+    return *reinterpret_cast<uint2 *>(&r);
+}
+
+// staging of one operand's K tile: ROWS rows (m or n) x KE k.  KC: source element (row, k) at
+// p[row * ld + k] (K-contiguous), else at p[k * ld + row].  Rows past n_rows load clamped and are
+// zeroed at the store.
+template <int ROWS, bool BF, bool KC>
+struct Stage {
+    static constexpr int KE = FcK<BF>::KE;
+    // K-contiguous: one float4 (4 k of one row) per unit; K-strided: a 4 x 4 block per unit
+    static constexpr int UNITS = KC ? ROWS * KE / 4 : ROWS * KE / 16;
+    static constexpr int PER = (UNITS + 255) / 256;
+    static constexpr int NV = KC ? 1 : 4;
+    float4 r[PER][NV];
+
+    __device__ __forceinline__ void load(const float *__restrict__ p, int64_t ld, int row0, int n_rows, int k0)
+    {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int u = min((int)threadIdx.x + 256 * j, UNITS - 1);
+            if constexpr (KC) {
+                const int row = u / (KE / 4), k4 = u - row * (KE / 4);
+                const int gr = min(row0 + row, n_rows - 1);
+                r[j][0] = *reinterpret_cast<const float4 *>(p + (int64_t)gr * ld + k0 + 4 * k4);
+            } else {
+                const int kb = u / (ROWS / 4), rb = u - kb * (ROWS / 4);
+                const int gr = min(row0 + 4 * rb, n_rows - 4);     // n_rows % 4 == 0 (host check)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    r[j][v] = *reinterpret_cast<const float4 *>(p + (int64_t)(k0 + 4 * kb + v) * ld + gr);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void store(char *lds, int row0, int n_rows) const
+    {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int u = (int)threadIdx.x + 256 * j;
+            if (u >= UNITS) continue;
+            if constexpr (KC) {
+                const int row = u / (KE / 4), k4 = u - row * (KE / 4);
+                const bool ok = row0 + row < n_rows;
+                const float4 v = ok ? r[j][0] : make_float4(0.f, 0.f, 0.f, 0.f);
+                char *dst = lds + row * kRowBytes;
+                if constexpr (BF) *reinterpret_cast<uint2 *>(dst + 8 * k4) = pack_bf16x4(v);
+                else *reinterpret_cast<float4 *>(dst + 16 * k4) = v;
+            } else {
+                const int kb = u / (ROWS / 4), rb = u - kb * (ROWS / 4);
+                const bool ok = row0 + 4 * rb < n_rows;
+                // r[j][v] = rows 4 rb .. 4 rb + 3 at k = 4 kb + v: column c is row 4 rb + c's 4 k
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 v = ok ? make_float4(c == 0 ? r[j][0].x : c == 1 ? r[j][0].y : c == 2 ? r[j][0].z : r[j][0].w,
+                                                      c == 0 ? r[j][1].x : c == 1 ? r[j][1].y : c == 2 ? r[j][1].z : r[j][1].w,
+                                                      c == 0 ? r[j][2].x : c == 1 ? r[j][2].y : c == 2 ? r[j][2].z : r[j][2].w,
+                                                      c == 0 ? r[j][3].x : c == 1 ? r[j][3].y : c == 2 ? r[j][3].z : r[j][3].w)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+                    char *dst = lds + (4 * rb + c) * kRowBytes;
+                    if constexpr (BF) *reinterpret_cast<uint2 *>(dst + 8 * kb) = pack_bf16x4(v);
+                    else *reinterpret_cast<float4 *>(dst + 16 * kb) = v;
+                }
+            }
+        }
+    }
+};
+
+template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int64_t lda, const float *__restrict__ Bm,
+                                               int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
+                                               const float *__restrict__ aux)
+{
+    constexpr int WGN = 4 / (WGM * KS);
+    static_assert(WGM * WGN * KS == 4, "4 waves");
+    constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
+    static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "32 x 32 sub-tiles");
+    constexpr int KE = FcK<BF>::KE, NG = FcK<BF>::NG;
+    static_assert(NG % KS == 0, "k-groups split evenly over KS");
+    constexpr int TILE = (BM + BN) * kRowBytes;
+    __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
+
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ks = wave % KS, wmn = wave / KS;
+    const int wm = (wmn / WGN) * WM, wn = (wmn % WGN) * WN;
+    const int l32 = lane & 31, lh = lane >> 5;
+
+    Stage<BM, BF, AK> sa;
+    Stage<BN, BF, BKC> sb;
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+    const int nk = K / KE;
+    sa.load(A, lda, m0, M, 0);
+    sb.load(Bm, ldb, n0, N, 0);
+    sa.store(lds, m0, M);
+    sb.store(lds + BM * kRowBytes, n0, N);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const char *buf = lds + (kt & 1) * TILE;
+        if (kt + 1 < nk) {          // the next tile's loads in flight during this tile's MFMAs
+            sa.load(A, lda, m0, M, (kt + 1) * KE);
+            sb.load(Bm, ldb, n0, N, (kt + 1) * KE);
+        }
+#pragma unroll
+        for (int g = ks; g < NG; g += KS) {
+            // lane (l32, lh): 16 B of its row at k-group g, half lh
+            float4 a[TM], b[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = *reinterpret_cast<const float4 *>(buf + (wm + 32 * i + l32) * kRowBytes + 32 * g + 16 * lh);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                b[j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 32 * j + l32) * kRowBytes + 32 * g + 16 * lh);
+            if constexpr (BF) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8 *>(&a[i]),
+                                                                            *reinterpret_cast<const bf16x8 *>(&b[j]),
+                                                                            acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            const float av = e == 0 ? a[i].x : e == 1 ? a[i].y : e == 2 ? a[i].z : a[i].w;
+                            const float bv = e == 0 ? b[j].x : e == 1 ? b[j].y : e == 2 ? b[j].z : b[j].w;
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+                        }
+            }
+        }
+        if (kt + 1 < nk) {
+            char *nb = lds + ((kt + 1) & 1) * TILE;
+            sa.store(nb, m0, M);
+            sb.store(nb + BM * kRowBytes, n0, N);
+        }
+        __syncthreads();
+    }
+    if constexpr (KS > 1) {
+        // the KS k-group partials of each wave tile, added in ks order (LDS is free after the loop)
+        float *red = reinterpret_cast<float *>(lds);
+        constexpr int PW = TM * TN * 16 * 64;      // floats per wave's partial tile
+        static_assert((KS - 1) * (4 / KS) * PW * 4 <= 2 * TILE, "KS reduction fits the LDS tiles");
+        if (ks > 0)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v)
+                        red[(((ks - 1) * (4 / KS) + wmn) * TM * TN + i * TN + j) * 16 * 64 + v * 64 + lane] = acc[i][j][v];
+        __syncthreads();
+        if (ks > 0) return;
+        for (int q = 1; q < KS; ++q)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v)
+                        acc[i][j][v] += red[(((q - 1) * (4 / KS) + wmn) * TM * TN + i * TN + j) * 16 * 64 + v * 64 + lane];
+    }
+    // epilogue: D col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5) of each 32 x 32 sub-tile
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int gn = n0 + wn + 32 * j + l32;
+            if (gn >= N) continue;
+            const float bn = EPI == kEpiBiasRelu ? aux[gn] : 0.0f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int gm = m0 + wm + 32 * i + (v & 3) + 8 * (v >> 2) + 4 * lh;
+                if (gm >= M) continue;
+                float x = acc[i][j][v];
+                if constexpr (EPI == kEpiBiasRelu) {
+                    x += bn;
+                    x = x > 0.0f ? x : 0.0f;
+                }
+                if constexpr (EPI == kEpiMask) x = aux[(int64_t)gm * ldc + gn] > 0.0f ? x : 0.0f;
+                C[(int64_t)gm * ldc + gn] = x;
+            }
+        }
+}
+
+template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI>
+int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
+              int64_t M, int64_t N, int64_t K, const float *aux)
+{
+    const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM));
+    if (bf)
+        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
+                           (int)M, (int)N, (int)K, aux);
+    else
+        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
+                           (int)M, (int)N, (int)K, aux);
+    GS_LAUNCH_CHECK("k_fc");
+    return GS_OK;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc)
+{
+    // K tiles of 64 (bf16) / 32 (fp32) with no tail; 16-B rows; K-strided operands in 4-row blocks
+    if (M < 4 || N < 4 || K < 64 || K % 64 != 0 || lda % 4 || ldb % 4 || ldc < N) return false;
+    if (M > (1 << 20) || N > (1 << 20) || K > (1 << 20)) return false;
+    if (op == 1) return M % 4 == 0 && N % 4 == 0;     // wgrad: both operands K-strided
+    if (op == 2) return N % 4 == 0;                   // dgrad: B K-strided
+    return true;
+}
+
+int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux)
+{
+    GS_REQUIRE(op >= 0 && op <= 2, "fc_gemm: op %d", op);
+    GS_REQUIRE(fc_supported(op, M, N, K, lda, ldb, ldc), "fc_gemm: shape %lld x %lld x %lld (op %d) not supported",
+               (long long)M, (long long)N, (long long)K, op);
+    GS_REQUIRE(aligned16(A) && aligned16(B) && (op == 1 || aux), "fc_gemm: 16-B aligned operands (and the epilogue "
+               "operand) required");
+    if (op == 0)     // fwd: C = relu(A B^T + bias), both K-contiguous
+        return launch_fc<32, 64, 1, 2, true, true, kEpiBiasRelu>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux);
+    if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]
+        return launch_fc<64, 64, 2, 1, false, false, kEpiStore>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr);
+    // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
+    return launch_fc<64, 64, 2, 1, true, false, kEpiMask>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux);
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" int gs_fc_gemm(int op, int bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+                          const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, void *stream)
+{
+    GS_REQUIRE(A && B && C, "gs_fc_gemm: null operand");
+    return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux);
+}

@@ -36,6 +36,14 @@ int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, c
              const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu,
              int splits = 1, int64_t sC = 0, const float *mask = nullptr);
 
+// The NatureCNN fc layer's GEMMs on the hand-written MFMA kernels of gs_fc.hip (fp32, or bf16
+// operands with fp32 accumulation): op 0 C = relu(A B^T + aux[n]) (A [M][K], B [N][K]); op 1
+// C = A^T B (A [K][M], B [K][N]); op 2 C = (A B) * (aux > 0) (A [M][K], B [K][N], aux like C).
+// fc_supported: the shapes they take (K % 64 == 0, 16-B rows, K-strided operands in 4-row blocks).
+bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux);
+
 // The same row-major product through hipBLASLt (fp32, plain library GEMMs: the NatureCNN fc layer),
 // no split-K; bias (+ ReLU) applied by hipBLASLt's epilogue.  gs_blaslt.cpp.
 int blaslt_gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,

@@ -601,7 +601,14 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
     // barrier below waits only for those (in-order vmcnt) and h1 is computed while the 16 KB
     // tile is still in flight; it is written to LDS after h1.
     if constexpr (ADAM) {
-        // w2r holds the updated tile (written to LDS after h1, below)
+        // w2r holds the updated tile: to LDS now, under the barrier below (the lagged forward forms
+        // h1 in registers inside the MFMA loop, so there is no h1 phase to overlap it with)
+        const int k4n = H1 >> 2;
+#pragma unroll
+        for (int j = 0; j < kW2v; ++j) {
+            const int u = tid + NT * j, i = u / k4n, k4 = u - i * k4n;
+            *reinterpret_cast<float4 *>(W2s + i * ldh + 4 * k4) = w2r[j];
+        }
     } else if constexpr (kW2v > 0) {
         const int k4n = H1 >> 2;
 #pragma unroll
@@ -626,6 +633,10 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
     //      [i0, i0 + RPT) of the tile (all 16 with 256 threads, 8 with 512)
     constexpr int RPT = kTile * 256 / NT;
     const int i0 = (tid >> 8) * RPT;
+    // the lagged forward (ADAM) has no h1 phase: h1 = relu(x W1^T + b1) is formed in registers,
+    // as the h2 MFMA's A operand on waves 0..3 and for the h1 store share on waves 4..7, with this
+    // loop's arithmetic and order (bit-identical values; no h1 tile, one barrier less)
+    if constexpr (!ADAM)
     for (int k = tid & 255; k < H1; k += 256) {
         float w[8];
         const bool small = D <= 8;
@@ -679,7 +690,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             }
         }
     }
-    if constexpr (kW2v > 0) {
+    if constexpr (kW2v > 0 && !ADAM) {
         const int k4n = H1 >> 2;
 #pragma unroll
         for (int j = 0; j < kW2v; ++j) {
@@ -687,8 +698,41 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             *reinterpret_cast<float4 *>(W2s + i * ldh + 4 * k4) = w2r[j];
         }
     }
-    __syncthreads();
+    if constexpr (!ADAM) __syncthreads();
     GS_STAMP(4)
+    // h1[i][k..k+3] from the LDS x row and W1 / b1 (ADAM path): phase 1's fmaf order over d,
+    // then + b1, then relu
+    auto h1_quad = [&](int i, int k) {
+        static_assert(!ADAM || (S::lay(Layout{}).D % 4 == 0 && S::lay(Layout{}).D <= 8), "h1 in registers: D = 4 or 8");
+        constexpr int cD = ADAM ? S::lay(Layout{}).D : 4;
+        float xr[8];
+#pragma unroll
+        for (int d4 = 0; d4 < 2; ++d4) {
+            const float4 v = 4 * d4 < cD ? *reinterpret_cast<const float4 *>(xs + i * cD + 4 * d4)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+            xr[4 * d4] = v.x, xr[4 * d4 + 1] = v.y, xr[4 * d4 + 2] = v.z, xr[4 * d4 + 3] = v.w;
+        }
+        const float4 bq = *reinterpret_cast<const float4 *>(b1s + k);
+        const float bk[4] = {bq.x, bq.y, bq.z, bq.w};
+        float h[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float w[8];
+#pragma unroll
+            for (int d4 = 0; d4 < 2; ++d4) {
+                const float4 v = 4 * d4 < cD ? *reinterpret_cast<const float4 *>(W1s + (k + j) * cD + 4 * d4)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                w[4 * d4] = v.x, w[4 * d4 + 1] = v.y, w[4 * d4 + 2] = v.z, w[4 * d4 + 3] = v.w;
+            }
+            float acc = 0.0f;
+#pragma unroll
+            for (int d = 0; d < 8; ++d)
+                if (d < cD) acc = fmaf(xr[d], w[d], acc);
+            acc += bk[j];
+            h[j] = acc > 0.0f ? acc : 0.0f;
+        }
+        return make_float4(h[0], h[1], h[2], h[3]);
+    };
     // x rows and this workgroup's share of h1 to HBM (read only xs / h1s, final from here on):
     // in a 512-thread block waves 4..7 store them while waves 0..3 run the h2 MFMA
     const int nrow = min(kTile, rows - r0);
@@ -706,7 +750,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             for (int u = t0; u < nrow * nk; u += stride) {
                 const int i = u / nk, k4 = kb0 + (u - i * nk);
                 *reinterpret_cast<float4 *>(h1_out + (int64_t)(r0 + i) * H1 + 4 * k4) =
-                    *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
+                    ADAM ? h1_quad(i, 4 * k4) : *reinterpret_cast<const float4 *>(h1s + i * ldh + 4 * k4);
             }
         }
     };
@@ -725,9 +769,10 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
             for (int ch = ch0; ch < ch1; ch += 2) {
                 const int k = ch * kTile + 4 * q;
                 const bool two = ch + 1 < ch1;
-                const float4 a0 = *reinterpret_cast<const float4 *>(h1s + i * ldh + k);
+                const float4 a0 = ADAM ? h1_quad(i, k) : *reinterpret_cast<const float4 *>(h1s + i * ldh + k);
                 const float4 b0 = *reinterpret_cast<const float4 *>(W2s + i * ldh + k);
-                const float4 a1 = two ? *reinterpret_cast<const float4 *>(h1s + i * ldh + k + kTile) : z4;
+                const float4 a1 = !two ? z4 : ADAM ? h1_quad(i, k + kTile)
+                                                   : *reinterpret_cast<const float4 *>(h1s + i * ldh + k + kTile);
                 const float4 b1 = two ? *reinterpret_cast<const float4 *>(W2s + i * ldh + k + kTile) : z4;
                 acc0 = mfma_bf16_pair(a0, a1, b0, b1, acc0);
             }
@@ -735,7 +780,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
 #pragma unroll 4
         for (int ch = ch0; ch < ch1; ++ch) {
             const int k = ch * kTile + 4 * q;
-            const float4 a = *reinterpret_cast<const float4 *>(h1s + i * ldh + k);
+            const float4 a = ADAM ? h1_quad(i, k) : *reinterpret_cast<const float4 *>(h1s + i * ldh + k);
             const float4 b = *reinterpret_cast<const float4 *>(W2s + i * ldh + k);
             acc0 = mfma4(a.x, b.x, acc0);
             acc1 = mfma4(a.y, b.y, acc1);

@@ -115,6 +115,7 @@ def _load():
                                                     i64, vp, vp, vp, vp, ctypes.POINTER(PPOGlobal), vp]),
         "gs_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64,
                                        f32, vp, ctypes.c_int, vp]),
+        "gs_fc_gemm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp]),
         "gs_cartpole_reset": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, vp]),
         "gs_cartpole_step": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, u64, i64, vp, vp, vp, vp, vp, vp, vp]),
         "gs_atari_preprocess": (ctypes.c_int, [vp, i64, i32, i32, vp, vp]),
@@ -157,7 +158,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",
             "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_cnn_ppo_update_global",
-            "gs_gemm_f32", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
+            "gs_gemm_f32", "gs_fc_gemm", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status", "gs_comm_error_record",
             "gs_comm_xgmi_set_colocation", "gs_comm_xgmi_set_bwd_exchange",
             "gs_comm_allreduce_mean_f32", "gs_comm_allreduce_sum_f64", "gs_ppo_global_adv_stats",

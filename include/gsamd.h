@@ -43,7 +43,7 @@ extern "C" {
  * version 2 added the rollout clock argument of gs_policy_act / gs_cnn_policy_act /
  * gs_env_step / gs_atari_env_step and gs_comm_error_record; version 3 widened the metric record
  * to 24 floats and added gs_ppo_update_global; version 4 added gs_comm_xgmi_set_bwd_exchange, gs_comm_allreduce_sum_f64,
- * gs_ppo_global_adv_stats, gs_ppo_global_records and gs_cnn_ppo_update_global). */
+ * gs_ppo_global_adv_stats, gs_ppo_global_records, gs_cnn_ppo_update_global and gs_fc_gemm). */
 #define GS_ABI_VERSION 4
 int gs_abi_version(void);
 const char *gs_last_error(void);
@@ -398,6 +398,14 @@ int gs_cartpole_step(double *state_dev, int32_t *meta_dev, float *ep_ret_dev, fl
 int gs_gemm_f32(int ta, int tb, int64_t M, int64_t N, int64_t K, const float *A_dev, int64_t lda,
                 const float *B_dev, int64_t ldb, float *C_dev, int64_t ldc, float beta, const float *bias_dev,
                 int relu, void *stream);
+/* The NatureCNN fc layer's three GEMMs (utils/models.py:56-110: h = relu(a3 Wf^T + bf) and its
+ * backward) on the hand-written MFMA kernels the update runs (csrc/gs_fc.hip), exposed for
+ * parity tests: op 0 C[M][N] = relu(A[M][K] B[N][K]^T + aux[N]); op 1 C = A^T B with A [K][M],
+ * B [K][N]; op 2 C = (A B) .* (aux > 0) with A [M][K], B [K][N], aux [M][ldc].  bf16 != 0: bf16
+ * operands (round to nearest even), fp32 accumulation.  GS_E_INVALID for shapes outside
+ * K % 64 == 0, 16-B aligned rows (and M, N % 4 == 0 for K-strided operands). */
+int gs_fc_gemm(int op, int bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda, const float *B,
+               int64_t ldb, float *C, int64_t ldc, const float *aux, void *stream);
 
 /* ---------------------------------------------------------------- Atari pixel path (a13)
  * The observation pipeline of ale-py's AtariVectorEnv / gymnasium AtariPreprocessing +

@@ -44,3 +44,56 @@ def test_gemm_epilogue_and_unaligned_ld(cuda):
     _check(cuda, False, True, 300, 64, 576, bias=True, relu=True)
     _check(cuda, True, False, 18, 512, 100, lda_pad=1)          # lda = 19 (the heads' dz rows)
     _check(cuda, False, False, 77, 45, 33, beta=1.0, ldb_pad=3)
+
+
+def _fc_case(cuda, op, bf16, M, N, K, seed=0):
+    """gs_fc_gemm (csrc/gs_fc.hip, the NatureCNN fc layer's kernels) against a float64 reference
+    on the same operands (bf16: the operands rounded to bf16 first, as the kernel rounds them;
+    fp32 accumulation either way).  Bar: 2e-6 x the |A||B| scale (x sqrt(K)/8 for long K)."""
+    from gsamd._lib import check, lib
+    g = torch.Generator(device="cpu").manual_seed(seed + 131 * op + 7 * M + N + K)
+    if op == 0:
+        A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+        aux = torch.randn(N, generator=g)
+        opA, opB = A, B.t()
+    elif op == 1:
+        A, B = torch.randn(K, M, generator=g), torch.randn(K, N, generator=g)
+        aux, opA, opB = None, A.t(), B
+    else:
+        A, B = torch.randn(M, K, generator=g), torch.randn(K, N, generator=g)
+        aux = torch.randn(M, N, generator=g)
+        opA, opB = A, B
+    rd = (lambda t: t.to(torch.bfloat16).double()) if bf16 else (lambda t: t.double())
+    ref = rd(opA) @ rd(opB)
+    if op == 0:
+        ref = (ref + aux.double()).clamp_min(0)
+    elif op == 2:
+        ref = torch.where(aux.double() > 0, ref, torch.zeros_like(ref))
+    out = torch.full((M, N), float("nan"), device=cuda)
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    auxd = aux.to(cuda) if aux is not None else None
+    check(lib.gs_fc_gemm(op, int(bf16), M, N, K, Ad.data_ptr(), Ad.shape[1], Bd.data_ptr(), Bd.shape[1],
+                         out.data_ptr(), N, auxd.data_ptr() if auxd is not None else None,
+                         torch.cuda.current_stream().cuda_stream), "gs_fc_gemm")
+    torch.cuda.synchronize()
+    scale = (rd(opA).abs() @ rd(opB).abs()).max().item() + 1.0
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-6 * scale * max(1.0, K ** 0.5 / 8), (op, bf16, M, N, K, err, scale)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("op,M,N,K", [(0, 1024, 512, 3136), (1, 512, 3136, 1024), (2, 1024, 3136, 512),
+                                      (0, 100, 72, 192), (1, 36, 100, 128), (2, 68, 92, 64), (0, 4, 4, 64)])
+def test_fc_gemm_matches_fp64_reference(cuda, op, M, N, K, bf16):
+    """The NatureCNN fc GEMMs at the C4/C5 shapes (B = 1024, HID = 512, F = 3136: forward with the
+    bias + ReLU epilogue, weight gradient, input gradient with the relu' mask) and ragged M / N
+    tiles, fp32 and bf16 operands."""
+    _fc_case(cuda, op, bf16, M, N, K)
+
+
+def test_fc_gemm_refuses_unsupported_shapes(cuda):
+    from gsamd._lib import check, lib
+    A = torch.zeros(64, 100, device=cuda)
+    with pytest.raises(ValueError):     # K % 64 != 0
+        check(lib.gs_fc_gemm(0, 0, 64, 64, 100, A.data_ptr(), 100, A.data_ptr(), 100, A.data_ptr(), 64, A.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream), "gs_fc_gemm")

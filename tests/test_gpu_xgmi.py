@@ -341,8 +341,8 @@ def test_exchange_guards_self_test_and_replica_check(tmp_path, bwd):
 
 
 def test_cnn_global_mode_reproduces_single_gpu_run(tmp_path, cuda):
-    """dp_mode 'global' for NatureCNN: a single-process Breakout rgb_ppo run (8
-    envs x 32 steps, B = 64, 2 epochs, the local fused head + loss path: the reference's own
+    """dp_mode 'global' for NatureCNN: a single-process Breakout rgb_ppo update (8
+    envs x 32 steps, B = 64, 4 epochs = 16 minibatches, the local fused head + loss path: the reference's own
     single-process math, utils/samplers.py:25-34 + utils/torch.py:97-99) against the same run as 2
     ranks x 4 envs in global mode — global sampler order, whole-minibatch advantage statistics
     and loss mean, the ranks' gradient shares summed, the records rebuilt from the summed loss sums
@@ -355,7 +355,10 @@ def test_cnn_global_mode_reproduces_single_gpu_run(tmp_path, cuda):
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     from _dist_workers import cnn_global_worker
-    N, T, B, E, epochs = 8, 32, 64, 2, 2
+    # one rollout, then 16 minibatch steps: the update's math from identical inputs (a second
+    # rollout would start from parameters that already differ at the reassociation level, which
+    # Adam's sign-like first steps amplify on near-zero-gradient weights: measured 1e-3 loss drift)
+    N, T, B, E, epochs = 8, 32, 64, 4, 1
     torch.manual_seed(42)
     cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=N, n_steps=T,
                                                                    batch_size=B, n_epochs=E))

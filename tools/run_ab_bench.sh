@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/abb
 for i in 1 2 3; do
   for v in intree "$@"; do
-    if [ "$v" = intree ]; then lib=""; else lib="tools/libgsamd_$v.so"; fi
+    if [ "$v" = intree ]; then lib=""; else lib="ab_libs/libgsamd_$v.so"; [ -f "$lib" ] || lib="tools/libgsamd_$v.so"; fi
     GSAMD_LIB=$lib timeout -k 10 200 python bench.py --cpu-minibatches 0 ${BENCH_ARGS} > "gpurun_out/abb/$v.$i.json" 2> "gpurun_out/abb/$v.$i.err" || exit 1
     python -c "
 import json, sys
