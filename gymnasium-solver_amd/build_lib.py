@@ -57,7 +57,7 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     objs = [_obj(s) for s in srcs]
     if done or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [
-            "-L/opt/rocm/lib", "-lrccl", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -93,7 +93,7 @@ def build_variant(out_path: str, defines, jobs: int = 8, patches=(), tag: str = 
         list(ex.map(lambda s: _compile(s, bdir, defines, csrc), srcs))
     objs = [os.path.join(bdir, s + ".o") for s in srcs]
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_path] + objs + [
-        "-L/opt/rocm/lib", "-lrccl", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+        "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -1162,10 +1162,9 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
     } else if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
         return rc;
     }
-    // fc: h = relu(a3 Wf^T + bf): hipBLASLt with its bias + ReLU epilogue (lib_fc: the update's
-    // fp32 path), else split-K partials summed with the bias + ReLU epilogue
-    if (lib_fc) return blaslt_gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf,
-                                       true);
+    // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
+    // update), else the engine's split-K partials summed with the bias + ReLU epilogue
+    if (lib_fc) return fc_gemm(s, 0, cnn_bf16(), R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf);
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
         if ((rc = gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf, true)))
@@ -1217,10 +1216,9 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     int rc;
     (void)stop;
     const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
-    // fc: [dWf | dbf] = dh^T [a3 | 1]; lib_fc: dWf through hipBLASLt, dbf from the head kernels
+    // fc: [dWf | dbf] = dh^T [a3 | 1]; lib_fc: dWf on the fc kernels, dbf from the head kernels
     if (lib_fc) {
-        if ((rc = blaslt_gemm_f32(s, true, false, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr,
-                                  false)))
+        if ((rc = fc_gemm(s, 1, cnn_bf16(), L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr)))
             return rc;
     } else {
         const int sw = splits_for(L.HID, L.F + 1, B);
@@ -1229,9 +1227,12 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
             return rc;
     }
     // da3 = (dh Wf) masked by relu'(a3) in the GEMM's epilogue
-    if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr, false,
-                       1, 0, w.a3)))
+    if (lib_fc) {
+        if ((rc = fc_gemm(s, 2, cnn_bf16(), B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, w.a3))) return rc;
+    } else if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr,
+                              false, 1, 0, w.a3))) {
         return rc;
+    }
     // conv3 (dY3 = da3 as [m3][c3])
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
         if ((rc = conv23_lds_wgrad(s, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
@@ -1392,10 +1393,11 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
             la.batch_rows = (int)gl->batch_global;
             la.inv_batch = 1.0f / (float)gl->batch_global;
         }
-        // the fc layer's forward and weight gradient through hipBLASLt in fp32 (dbf comes from the
-        // head kernels), also in the bf16 mode: faster there than the engine's bf16 form
-        const bool lib_fc = blaslt_available(false, true, B, L.HID, L.F, L.F, L.F, L.HID, true, true) &&
-                            blaslt_available(true, false, L.HID, L.F, B, L.HID, L.F, L.F, false, false);
+        // the fc layer's forward, weight and input gradients on the fc kernels (gs_fc.hip; dbf comes
+        // from the head kernels), in the operand precision of the update
+        const bool lib_fc = fc_supported(0, B, L.HID, L.F, L.F, L.F, L.HID) &&
+                            fc_supported(1, L.HID, L.F, B, L.HID, L.F, L.F) &&
+                            fc_supported(2, B, L.F, L.HID, L.HID, L.F, L.F);
         if ((rc = forward_trunk(P, L, fs, B, w, s, lib_fc))) return rc;
         if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s))) return rc;
         if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, lib_fc))) return rc;

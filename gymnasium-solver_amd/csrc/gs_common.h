@@ -105,9 +105,10 @@ __host__ __device__ __forceinline__ int64_t part1_index(const Layout &L, int64_t
 // into the kernel, so every loop bound and parameter offset is a compile-time constant
 // (fully unrolled, no integer division, no guard chains); the benchmarked / reference
 // configs are instantiated this way.  ShapeR keeps them runtime (any other MLP shape).
-template <int D_, int H1_, int H2_, int A_, int B_>
+template <int D_, int H1_, int H2_, int A_, int B_, int RB_ = 32>
 struct ShapeC {
     static constexpr int AMAX = A_, AEX = A_, H1c = H1_, Bc = B_;
+    static constexpr int RB = RB_;        // rows of a k_bwd role-B slab (one dW1|db1 partial each)
     static constexpr bool BF = false;     // bf16 MFMA operands (Bf16Shape)
     __host__ __device__ static constexpr Layout lay(const Layout &) { return Layout::make(D_, H1_, H2_, A_); }
     __host__ __device__ static constexpr int batch(int b) { return B_ > 0 ? B_ : b; }
@@ -115,6 +116,7 @@ struct ShapeC {
 template <int AMAX_>
 struct ShapeR {
     static constexpr int AMAX = AMAX_, AEX = 0, H1c = 0, Bc = 0;
+    static constexpr int RB = 32;
     static constexpr bool BF = false;
     __host__ __device__ static Layout lay(const Layout &L) { return L; }
     __host__ __device__ static int batch(int b) { return b; }
@@ -155,6 +157,9 @@ struct Workspace {
 // minibatch, but C3 (B = 64: 8 role-B workgroups instead of 16) 9 % slower — kept at 32
 // (profiles/r03_ab_chain.txt)
 constexpr int kRowsB = 32;
+// the role-B slab height of a shape (its S::RB; 32 for the runtime shapes): the dW1|db1 partial count
+// is ceil(B / rows_b)
+int rows_b(const Layout &L, int64_t B);
 
 // Minibatch field gather done by the forward kernel (utils/rollout_collector.py:657-682).
 struct RowGather {

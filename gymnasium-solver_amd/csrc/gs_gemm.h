@@ -44,12 +44,6 @@ bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
             const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux);
 
-// The same row-major product through hipBLASLt (fp32, plain library GEMMs: the NatureCNN fc layer),
-// no split-K; bias (+ ReLU) applied by hipBLASLt's epilogue.  gs_blaslt.cpp.
-int blaslt_gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-                    const float *B, int64_t ldb, float *C, int64_t ldc, const float *bias, bool relu);
-bool blaslt_available(bool ta, bool tb, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
-                      bool bias, bool relu);
 
 // out[r,oy,ox,co] = relu(bias[co] + sum_{c,ky,kx} W[co][c][ky][kx] * frame[c][oy*s+ky][ox*s+kx] / 255)
 int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out);

@@ -339,7 +339,7 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         //      set (the rest of the grid still reads this one).
         constexpr Layout Lc = S::lay(Layout{});
         constexpr int cD = Lc.D, cH1 = Lc.H1, cA1 = Lc.A + 1, n1 = cH1 * (cD + 1), k4n = cH1 / 4;
-        constexpr int NQ = (n1 / 4 + 255) / 256, NRB = (S::Bc + kRowsB - 1) / kRowsB, NS = 2;
+        constexpr int NQ = (n1 / 4 + 255) / 256, NRB = (S::Bc + S::RB - 1) / S::RB, NS = 2;
         static_assert(Lc.oW1 == 0 && Lc.oW2 == n1 && (cH1 * cD) % 4 == 0 && cH1 % 4 == 0, "W1|b1: one float4 region");
         static_assert(NRB >= 1 && NRB <= 8 && NQ <= 2 && n1 <= kTile * (cH1 + 4), "lagged-Adam register / LDS budget");
         const AdamArgs &aa = af.aa;
@@ -1521,8 +1521,9 @@ __host__ __device__ inline int metric_groups_per_wg(int G, int nW) { return G <=
 
 struct BwdShape {
     int ncb, nkb, nrbB, ka, nT, nA, nB, nC;
-    __host__ __device__ static BwdShape make(const Layout &L, int B)
+    __host__ __device__ static BwdShape make(const Layout &L, int B, int rb)
     {
+        const int kRowsB = rb;
         BwdShape s;
         s.ncb = (L.H2 + kTile - 1) / kTile;
         s.nkb = (L.H1 + kTile - 1) / kTile;
@@ -1540,10 +1541,11 @@ struct BwdShape {
 
 size_t bwd_lds_bytes(const Layout &L, int64_t B)
 {
+    const int kRowsB = rows_b(L, B);
     const int A1 = L.A + 1;
     const int64_t Bp64 = (B + 63) / 64 * 64, Bp16 = (B + 15) / 16 * 16;
     const int64_t H2p = (L.H2 + 63) / 64 * 64;
-    const BwdShape shp = BwdShape::make(L, (int)B);
+    const BwdShape shp = BwdShape::make(L, (int)B, kRowsB);
     // the fast paths (A1 <= 5) form dh2 in registers: role A has no dh2 tile (and its block
     // reduction reuses the h1 tile after the MFMA loop), role B only the dW1 partial scratch in
     // place of its dh2 slab — role A's 49 KB (+ 3 KB static) keep three workgroups per CU, so
@@ -1645,7 +1647,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
     const Layout L = S::lay(Lrt);
     const int B = S::batch(Brt);
     const int D = L.D, H1 = L.H1, H2 = L.H2, A = L.A, A1 = A + 1;
-    const BwdShape sh = BwdShape::make(L, B);
+    constexpr int kRowsB = S::RB;      // this shape's role-B slab height (shadows the default)
+    const BwdShape sh = BwdShape::make(L, B, kRowsB);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
     // dispatch order: role B (the longest) first, then A, then C; bid keeps the A, B, C numbering
@@ -2054,10 +2057,12 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
                 dzs[u] = b0 * A1 + u < B * A1 ? dz[(int64_t)b0 * A1 + u] : 0.0f;
         __syncthreads();
         GS_STAMP(0)
-        // 32 rows = 2 row tiles; waves (0,1) / (2,3) split K = H2 of tile 0 / 1 in halves
+        // 32 rows = 2 row tiles; waves (0,1) / (2,3) split K = H2 of tile 0 / 1 in halves; 64 rows =
+        // 4 row tiles, one per wave over the whole K
+        static_assert(kRowsB == 32 || kRowsB == 64, "role-B slabs of 32 or 64 rows");
         const int nchB = H2p / kTile;
-        const int rt = wave >> 1, half = wave & 1;
-        const int chb = half ? nchB / 2 : 0, che = half ? nchB : nchB / 2;
+        const int rt = kRowsB == 64 ? wave : wave >> 1, half = kRowsB == 64 ? 0 : wave & 1;
+        const int chb = half ? nchB / 2 : 0, che = (half || kRowsB == 64) ? nchB : nchB / 2;
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
         if (dh2_regs) {
             // dh2 = relu'(h2) * (dz . Wh) formed in registers as the MFMA's A operand (lane: slab
@@ -2209,7 +2214,8 @@ __global__ __launch_bounds__(256) void k_bwd(const float *__restrict__ P, Layout
         for (int u = tid; u < kRowsB * kTile; u += 256) {
             const int row = u >> 4, col = u & 15;
             const int t = row >> 4, rr = row & 15;
-            const float g = kred[(2 * t) * 256 + rr * kTile + col] + kred[(2 * t + 1) * 256 + rr * kTile + col];
+            const float g = kRowsB == 64 ? kred[t * 256 + rr * kTile + col]
+                                         : kred[(2 * t) * 256 + rr * kTile + col] + kred[(2 * t + 1) * 256 + rr * kTile + col];
             tile[row * 17 + col] = h1m[row * 16 + col] > 0.0f ? g : 0.0f;   // relu'(h1)
         }
         __syncthreads();
@@ -2713,7 +2719,7 @@ template <class F>
 static int with_shape(const Layout &L, int64_t B, F &&f)
 {
     if (L.D == 4 && L.H1 == 256 && L.H2 == 256 && L.A == 2) {        // CartPole-v1:ppo (mlp_medium)
-        if (B == 256) return f(ShapeC<4, 256, 256, 2, 256>{});
+        if (B == 256) return f(ShapeC<4, 256, 256, 2, 256, 64>{});      // 64-row role-B slabs: 4 partials
         return f(ShapeC<4, 256, 256, 2, 0>{});
     }
     if (L.D == 8 && L.H1 == 128 && L.H2 == 128 && L.A == 4) {        // LunarLander-v3:ppo (mlp_small)
@@ -2722,6 +2728,16 @@ static int with_shape(const Layout &L, int64_t B, F &&f)
     }
     if (L.A <= 4) return f(ShapeR<4>{});
     return f(ShapeR<kMaxActions>{});
+}
+
+int rows_b(const Layout &L, int64_t B)
+{
+    int rb = kRowsB;
+    with_shape(L, B, [&](auto sh) {
+        rb = decltype(sh)::RB;
+        return GS_OK;
+    });
+    return rb;
 }
 
 // Raise a kernel's dynamic-LDS limit once (never inside a stream capture: the first
@@ -2821,7 +2837,7 @@ bool bwd_xchg_coresident(int64_t nblk, size_t lds_bytes, int colocated);
 
 bool bwd_xchg_fits(const Layout &L, int64_t B, int colocated)
 {
-    const BwdShape sh = BwdShape::make(L, (int)B);
+    const BwdShape sh = BwdShape::make(L, (int)B, rows_b(L, B));
     const int64_t nblk = sh.nA + sh.nB + sh.nC;
     return nblk <= kBwdXMaxWG && kTile * (L.D + 1) <= kBwdXSlot && (L.A + 1) * kTile <= kBwdXSlot &&
            bwd_xchg_coresident(nblk, bwd_lds_bytes(L, B), colocated);
@@ -2846,7 +2862,7 @@ bool bwd_xchg_coresident(int64_t nblk, size_t lds_bytes, int colocated)
 int launch_bwd(const float *P, const Layout &L, int64_t B, const Workspace &ws, float *G, const int32_t *stop,
                hipStream_t s, const FusedFwd *ff, const LossArgs *la, const BwdXchg *bxp)
 {
-    const BwdShape sh0 = BwdShape::make(L, (int)B);
+    const BwdShape sh0 = BwdShape::make(L, (int)B, rows_b(L, B));
     const unsigned nblk = (unsigned)(sh0.nA + sh0.nB + sh0.nC);
     const size_t lds = bwd_lds_bytes(L, B);
     BwdXchg bx{};
@@ -2940,6 +2956,7 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
         using Sh = decltype(sh);
         const void *fn = nullptr;   // the fused shapes: C2 (B 256 -> 8 row blocks), C3 (B 64 -> 2)
         if (vec && aa.nrb == 8) fn = nq == 2 ? (const void *)k_clip_adam<Sh, 8, 2> : (const void *)k_clip_adam<Sh, 8, 1>;
+        if (vec && aa.nrb == 4) fn = nq == 2 ? (const void *)k_clip_adam<Sh, 4, 2> : (const void *)k_clip_adam<Sh, 4, 1>;
         if (vec && aa.nrb == 2) fn = nq == 2 ? (const void *)k_clip_adam<Sh, 2, 2> : (const void *)k_clip_adam<Sh, 2, 1>;
         if (fn) {
             void *args[] = {&P, (void *)&L, &G, &M, &V, &part1, &sumsq, &aa, &metrics, &stop};
@@ -3319,7 +3336,7 @@ constexpr bool lagged_shape()
         constexpr Layout Lc = Sh::lay(Layout{});
         constexpr int n1 = Lc.H1 * (Lc.D + 1);
         return (kTile * Lc.H1 / 4) % kFwdAdamThreads == 0 && Lc.H1 % 4 == 0 && (Lc.H1 * Lc.D) % 4 == 0 &&
-               (Sh::Bc + kRowsB - 1) / kRowsB <= 8 && (n1 / 4 + 255) / 256 <= 2 && n1 <= kTile * (Lc.H1 + 4);
+               (Sh::Bc + Sh::RB - 1) / Sh::RB <= 8 && (n1 / 4 + 255) / 256 <= 2 && n1 <= kTile * (Lc.H1 + 4);
     }
 }
 

@@ -30,7 +30,7 @@ Workspace carve_workspace(void *base, const Layout &L, int64_t B)
         return r;
     };
     const int A1 = L.A + 1;
-    const int64_t nrb = (B + kRowsB - 1) / kRowsB;
+    const int64_t nrb = (B + rows_b(L, B) - 1) / rows_b(L, B);
     w.x = take((size_t)B * L.D);
     w.h1 = take((size_t)B * L.H1);
     w.h2 = take((size_t)B * L.H2);
@@ -264,7 +264,7 @@ StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, in
     a.aa.eps = hp.adam_eps;
     a.aa.grad_scale = 1.0f;
     a.aa.n_slots = n_sumsq_slots(L);
-    a.aa.nrb = (int)((B + kRowsB - 1) / kRowsB);
+    a.aa.nrb = (int)((B + rows_b(L, B) - 1) / rows_b(L, B));
     return a;
 }
 

@@ -75,8 +75,8 @@ class _Bf16Conv(torch.autograd.Function):
 class _Bf16Linear(torch.autograd.Function):
     """linear with bf16-rounded operands in the products listed in `rounded` ("fwd", "dx", "dw"),
     fp32 in the others: the heads round fwd + dw (their input gradient dh is a plain fp32 kernel);
-    the fc layer rounds only dx (its forward and weight gradient are hipBLASLt fp32 GEMMs, faster
-    than the bf16 form of the engine; its input gradient is the engine's bf16 GEMM)."""
+    the fc layer rounds all three (csrc/gs_fc.hip's bf16 kernels: forward, weight gradient, input
+    gradient)."""
 
     @staticmethod
     def forward(ctx, x, w, b, rounded):
@@ -98,10 +98,10 @@ def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False):
     """-> (masked logits (B,A) with -inf for invalid actions, value (B,), hidden (B,512)).
 
     bf16=True: the device's GS_HP_BF16 mode (SURVEY.md Appendix A "Precision modes") — every
-    convolution product and the heads' forward / weight gradient and the fc layer's input gradient
+    convolution product, the fc layer's three products and the heads' forward / weight gradient
     take bf16-rounded operands with fp32 accumulation, at the points the HIP kernels round them
-    (u8/255 frames, activations, weights, output gradients); the fc layer's forward and weight
-    gradient (hipBLASLt fp32), biases, ReLU, the loss, the heads' input gradient and Adam stay fp32."""
+    (u8/255 frames, activations, weights, output gradients); biases, ReLU, the loss, the heads'
+    input gradient and Adam stay fp32."""
     x = torch.as_tensor(obs_u8)
     x = x.to(torch.float32) / 255.0 if x.dtype == torch.uint8 else x.to(torch.float32)
     conv = (lambda x, w, b, s: _Bf16Conv.apply(x, w, b, s)) if bf16 else (lambda x, w, b, s: F.conv2d(x, w, b, stride=s))
@@ -109,7 +109,7 @@ def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False):
     for i, s in enumerate(spec["strides"]):
         x = F.relu(conv(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], s))
     x = x.flatten(1)
-    h = F.relu(lin(x, params["mlp.0.weight"], params["mlp.0.bias"], ("dx",)))
+    h = F.relu(lin(x, params["mlp.0.weight"], params["mlp.0.bias"], ("fwd", "dx", "dw")))
     logits = lin(h, params["policy_head.weight"], params["policy_head.bias"], ("fwd", "dw"))
     if valid is not None:
         mask = torch.ones_like(logits, dtype=torch.bool)

@@ -497,7 +497,7 @@ def cnn_global_worker(rank, world, port, result_dir, ref_path):
         torch.manual_seed(42 + rank)        # the sampler seed comes from rank 0
         cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(
             env_dynamics="synthetic", n_envs=n, n_steps=T, batch_size=int(z["B"]), n_epochs=int(z["E"]),
-            dp_mode="global"))
+            dp_mode="global", clip_range=10.0, clip_range_vf=10.0))
         agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
         agent.policy_model.params.copy_(torch.from_numpy(z["p0"]).to(dev))
         agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)

@@ -28,6 +28,6 @@ with ThreadPoolExecutor(8) as ex:
 os.makedirs(os.path.join(ROOT, "ab_libs"), exist_ok=True)
 out = os.path.join(ROOT, "ab_libs", f"libgsamd_{name}.so")
 cmd = [build_lib.HIPCC, f"--offload-arch={build_lib.ARCH}", "-shared", "-fPIC", "-o", out] + \
-    [os.path.join(bdir, s + ".o") for s in srcs] + ["-L/opt/rocm/lib", "-lrccl", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+    [os.path.join(bdir, s + ".o") for s in srcs] + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 subprocess.run(cmd, check=True)
 print("built", out)
