@@ -15,7 +15,7 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 # passes, tools/pmc_run.py) and the NatureCNN update (C4 per-kernel passes, tools/cnn_kernel_run.py)
 PATH_SOURCES = {
     "mlp": ("gs_mlp.hip", "gs_ppo.hip", "gs_gae.hip", "gs_common.h", "gs_xgmi_dev.h", "gs_synth_env.h"),
-    "cnn": ("gs_cnn.hip", "gs_conv.hip", "gs_gemm.hip", "gs_blaslt.cpp", "gs_common.h", "gs_conv.h", "gs_gemm.h"),
+    "cnn": ("gs_cnn.hip", "gs_conv.hip", "gs_gemm.hip", "gs_fc.hip", "gs_common.h", "gs_conv.h", "gs_gemm.h"),
 }
 
 

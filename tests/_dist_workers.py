@@ -519,3 +519,33 @@ def cnn_global_worker(rank, world, port, result_dir, ref_path):
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
     finally:
         dist.destroy_process_group()
+
+
+def replica_check_cpu_worker(rank, world, port, result_dir):
+    """CPU (gloo) half of the multi-GPU guards: check_replicas passes on identical parameters and
+    raises GsError on EVERY rank once one rank's parameters differ in one element (also a swap of
+    two elements, which keeps the plain sum); broadcast_int hands rank 0's sampler seed to all."""
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd._lib import GsError
+        from gsamd.distributed import broadcast_int, check_replicas
+        assert broadcast_int(42 + rank) == 42
+        p = torch.linspace(-1.0, 1.0, 1001, dtype=torch.float32)
+        check_replicas(p)
+        outcomes = []
+        for change in ("one", "swap"):
+            q = p.clone()
+            if rank == 1 and change == "one":
+                q[500] += 1e-6
+            if rank == 1 and change == "swap":
+                q[[3, 7]] = q[[7, 3]]
+            try:
+                check_replicas(q)
+                outcomes.append("passed")
+            except GsError as e:
+                outcomes.append("GsError" if "replica check failed" in str(e) else "other")
+        open(os.path.join(result_dir, f"rc{rank}"), "w").write(",".join(outcomes))
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()

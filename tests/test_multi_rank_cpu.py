@@ -30,3 +30,23 @@ def test_data_parallel_protocol_gloo(tmp_path, world):
     codes = [p.exitcode for p in procs]
     assert codes == [0] * world, codes
     assert sorted(os.listdir(tmp_path)) == [f"ok{r}" for r in range(world)]
+
+
+def test_replica_check_and_seed_broadcast_gloo(tmp_path):
+    """The per-epoch replica check of train_epoch (gsamd.distributed.check_replicas, DESIGN §5
+    guards) and the global mode's sampler-seed agreement, on CPU ranks: identical parameters
+    pass, one changed element or two swapped elements raise GsError on every rank."""
+    from _dist_workers import replica_check_cpu_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=replica_check_cpu_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert [p.exitcode for p in procs] == [0, 0]
+    for r in range(2):
+        assert (tmp_path / f"rc{r}").read_text() == "GsError,GsError"

@@ -55,7 +55,15 @@ SEQ_LIB = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fw
            ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
            ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
            ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
-SEQ = SEQ_FUSED
+# round 4: the fc layer's three GEMMs on the hand-written k_fc kernels (csrc/gs_fc.hip)
+SEQ_FC = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd", "k_conv_fwd"),
+          ("fc_fwd", "k_fc"), ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
+          ("fc_wgrad", "k_fc"), ("fc_dgrad_relu_mask", "k_fc"),
+          ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts_wb"),
+          ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
+          ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
+          ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
+SEQ = SEQ_FC
 
 
 def nature_work(B, A=18, C=4, H=84, W=84):
@@ -154,7 +162,10 @@ def main():
     global SEQ
     rows = load_trace(one(os.path.join(a.dir, a.prefix + "_stats", "**", "*kernel_trace.csv")))
     names = [short(r["Kernel_Name"]) for r in rows if short(r["Kernel_Name"])]
-    SEQ = (SEQ_LIB if "blaslt" in names else SEQ_FUSED) if "k_cnn_head_loss" in names else SEQ_SPLIT
+    if "k_cnn_head_loss" not in names:
+        SEQ = SEQ_SPLIT
+    else:
+        SEQ = SEQ_FC if "k_fc" in names else SEQ_LIB if "blaslt" in names else SEQ_FUSED
     trace = minibatches(rows)[a.skip:]
     fetch = minibatches(load_pmc(one(os.path.join(a.dir, a.prefix + "_fetch", "**", "*counter_collection.csv")),
                                  "FETCH_SIZE"))[a.skip:]
