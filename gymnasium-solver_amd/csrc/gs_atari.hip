@@ -80,22 +80,32 @@ __global__ __launch_bounds__(256) void k_atari_counters(int32_t *__restrict__ st
     ep_ret[e] = er;
 }
 
-// ---- the frame source: raw RGB frames 2*step and 2*step+1 of every env, 8 bytes per thread
+// ---- the frame source: raw RGB frames 2*step and 2*step+1 of every env.  Word w of frame j of
+// env e is mix64(mix64(mix64(mix64(seed) ^ e) ^ (2 step + j)) ^ w): blockIdx.y = (env, frame), so
+// the three leading mixes are one per thread, and each thread writes kRenderWords words of it
+// (256-word strides: every wave store is 2 KB contiguous)
+constexpr int kFrameWords = kFrameBytes / 8;       // 12 600
+constexpr int kRenderWords = 4;
+constexpr int kRenderChunks = (kFrameWords + 256 * kRenderWords - 1) / (256 * kRenderWords);
+
 __global__ __launch_bounds__(256) void k_atari_render(uint8_t *__restrict__ frames, int64_t N, uint64_t seed,
                                                       int64_t env_offset, uint64_t step_count,
                                                       const uint64_t *__restrict__ clock)
 {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (clock) step_count += clock[1];
-    constexpr int per_env = 2 * kFrameBytes / 8;
-    if (t >= N * per_env) return;
-    const int64_t e = t / per_env;
-    const int w = (int)(t - e * per_env);
-    const int j = w / (kFrameBytes / 8);
-    const int word = w - j * (kFrameBytes / 8);
+    const int64_t ej = blockIdx.y;              // env * 2 + frame
+    const int64_t e = ej >> 1;
+    const int j = (int)(ej & 1);
     const uint64_t ge = (uint64_t)(env_offset + e);
-    const uint64_t h = mix64(mix64(mix64(mix64(seed) ^ ge) ^ (2 * step_count + (uint64_t)j)) ^ (uint64_t)word);
-    ((uint64_t *)frames)[t] = h;
+    const uint64_t hf = mix64(mix64(mix64(seed) ^ ge) ^ (2 * step_count + (uint64_t)j));
+    uint64_t *out = (uint64_t *)frames + ej * kFrameWords;
+    const int w0 = blockIdx.x * 256 * kRenderWords + threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < kRenderWords; ++q) {
+        const int w = w0 + 256 * q;
+        if (w < kFrameWords) out[w] = mix64(hf ^ (uint64_t)w);
+    }
+    (void)N;
 }
 
 __device__ __forceinline__ int gray_at(const uint8_t *f, int y, int x)
@@ -320,6 +330,8 @@ int check_out(int OH, int OW)
 }
 
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+inline dim3 render_grid(int64_t N) { return dim3((unsigned)kRenderChunks, (unsigned)(2 * N)); }
+constexpr int64_t kMaxAtariEnvs = 32767;       // render_grid's y extent (2 frames per env) < 65536
 
 // the stack update (and, with S = 1, the plain preprocess) on the HBM-rate band kernel where
 // the shape is the 84x84 pipeline, the per-pixel kernel for other targets
@@ -358,8 +370,8 @@ extern "C" int gs_atari_preprocess(const uint8_t *frames, int64_t N, int32_t out
 extern "C" int gs_atari_render(uint8_t *frames, int64_t N, uint64_t seed, int64_t env_offset, uint64_t step_count,
                                void *stream)
 {
-    GS_REQUIRE(N > 0 && frames, "gs_atari_render: bad argument");
-    hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, (hipStream_t)stream, frames,
+    GS_REQUIRE(N > 0 && N <= kMaxAtariEnvs && frames, "gs_atari_render: bad argument");
+    hipLaunchKernelGGL(k_atari_render, render_grid(N), dim3(256), 0, (hipStream_t)stream, frames,
                        N, seed, env_offset, step_count, (const uint64_t *)nullptr);
     GS_LAUNCH_CHECK("k_atari_render");
     return GS_OK;
@@ -369,7 +381,7 @@ extern "C" int gs_atari_env_reset(int32_t *state, float *ep_ret, uint8_t *stack,
                                   int32_t stack_n, int32_t out_h, int32_t out_w, int32_t episode_len, uint64_t seed,
                                   int64_t env_offset, void *stream)
 {
-    GS_REQUIRE(N > 0 && state && ep_ret && stack && frames && stack_n >= 1 && episode_len > 0,
+    GS_REQUIRE(N > 0 && N <= kMaxAtariEnvs && state && ep_ret && stack && frames && stack_n >= 1 && episode_len > 0,
                "gs_atari_env_reset: bad argument");
     int rc = check_out(out_h, out_w);
     if (rc) return rc;
@@ -384,7 +396,7 @@ extern "C" int gs_atari_env_reset(int32_t *state, float *ep_ret, uint8_t *stack,
     GS_HIP(hipMemcpyAsync(state, st.data(), st.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
     GS_HIP(hipStreamSynchronize(s));   // pageable source: keep it alive until copied
     GS_HIP(hipMemsetAsync(ep_ret, 0, sizeof(float) * N, s));
-    hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
+    hipLaunchKernelGGL(k_atari_render, render_grid(N), dim3(256), 0, s, frames, N, seed,
                        env_offset, (uint64_t)0, (const uint64_t *)nullptr);
     return launch_stack(frames, nullptr, N, stack_n, out_h, out_w, stack, s);
 }
@@ -395,7 +407,7 @@ extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, 
                                  float *rewards_row, uint8_t *dones_row, uint8_t *timeouts_row, int32_t *ep_done_count,
                                  float *ep_ret_sum, float *ep_len_sum, const uint64_t *clock, void *stream)
 {
-    GS_REQUIRE(N > 0 && state && ep_ret && stack && frames && stack_n >= 1 && episode_len > 0,
+    GS_REQUIRE(N > 0 && N <= kMaxAtariEnvs && state && ep_ret && stack && frames && stack_n >= 1 && episode_len > 0,
                "gs_atari_env_step: bad argument");
     GS_REQUIRE(rewards_row && dones_row && timeouts_row, "gs_atari_env_step: null output row");
     int rc = check_out(out_h, out_w);
@@ -405,7 +417,7 @@ extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, 
     hipLaunchKernelGGL(k_atari_counters, dim3(nblk(N)), dim3(256), 0, s, state, ep_ret, N, episode_len, truncate_every,
                        seed, env_offset, step_count, rewards_row, dones_row, timeouts_row, ep_done_count, ep_ret_sum,
                        ep_len_sum, clock);
-    hipLaunchKernelGGL(k_atari_render, dim3(nblk(N * 2 * kFrameBytes / 8)), dim3(256), 0, s, frames, N, seed,
+    hipLaunchKernelGGL(k_atari_render, render_grid(N), dim3(256), 0, s, frames, N, seed,
                        env_offset, step_count, clock);
     return launch_stack(frames, dones_row, N, stack_n, out_h, out_w, stack, s);
 }
