@@ -1,3 +1,4 @@
+#include <math.h>
 // Synthetic fixed-length-episode vector env on the device — the twin of
 // gsamd/synthetic_env.py: hashed observations, constant reward,
 // episodes of length L starting e mod L steps in, every `truncate_every`-th episode
@@ -93,6 +94,81 @@ extern "C" int gs_episode_stats(const float *rewards, const uint8_t *dones, int6
     hipLaunchKernelGGL(k_episode_stats, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        rewards, dones, T, N, run_ret, run_len, ep_ret, ep_len);
     GS_LAUNCH_CHECK("k_episode_stats");
+    return GS_OK;
+}
+
+// ---- the reference's rolling episode window (rollout_collector.py:242-294, 753-758) for
+// track_stats=False, one launch of one 1024-thread workgroup: this rollout's finished episodes in
+// (step, env) order (ep_ret / ep_len rows of gs_episode_stats, dones time-major) are numbered by a
+// block scan of per-thread done counts; the last W of them go to the window's tail slots in order
+// and the previous window shifts left by their count; meta = {episodes so far, best return, -}.
+constexpr int kWinThreads = 1024;
+
+__global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *__restrict__ dones,
+                                                                const float *__restrict__ ep_ret,
+                                                                const int32_t *__restrict__ ep_len, int64_t n, int W,
+                                                                double *__restrict__ win, double *__restrict__ meta,
+                                                                int64_t *__restrict__ total_out)
+{
+    __shared__ int64_t scan[kWinThreads];
+    __shared__ double sbest[kWinThreads];
+    extern __shared__ double old[];           // [2][W]
+    const int tid = threadIdx.x;
+    const int64_t per = (n + kWinThreads - 1) / kWinThreads;
+    const int64_t a = min((int64_t)tid * per, n), b = min(a + per, n);
+    int64_t cnt = 0;
+    double best = -INFINITY;
+    for (int64_t i = a; i < b; ++i)
+        if (dones[i]) {
+            ++cnt;
+            best = fmax(best, (double)ep_ret[i]);
+        }
+    for (int i = tid; i < 2 * W; i += kWinThreads) old[i] = win[i];
+    scan[tid] = cnt;
+    sbest[tid] = best;
+    __syncthreads();
+    // inclusive scan of the counts (Hillis-Steele), max of the bests
+    for (int off = 1; off < kWinThreads; off <<= 1) {
+        const int64_t v = tid >= off ? scan[tid - off] : 0;
+        const double bv = tid >= off ? sbest[tid - off] : -INFINITY;
+        __syncthreads();
+        scan[tid] += v;
+        sbest[tid] = fmax(sbest[tid], bv);
+        __syncthreads();
+    }
+    const int64_t total = scan[kWinThreads - 1];
+    // the previous window shifted left by this rollout's episode count
+    for (int i = tid; i < W; i += kWinThreads)
+        if (i + total < W) {
+            win[i] = old[i + total];
+            win[W + i] = old[W + i + total];
+        }
+    // this rollout's last W episodes at their slots
+    int64_t pos = scan[tid] - cnt;            // episodes before this thread's chunk
+    for (int64_t i = a; i < b; ++i)
+        if (dones[i]) {
+            const int64_t slot = pos - (total - W);
+            if (slot >= 0) {
+                win[slot] = (double)ep_ret[i];
+                win[W + slot] = (double)ep_len[i];
+            }
+            ++pos;
+        }
+    if (tid == 0) {
+        meta[0] += (double)total;
+        meta[1] = fmax(meta[1], sbest[kWinThreads - 1]);
+        if (total_out) *total_out = total;
+    }
+}
+
+extern "C" int gs_episode_window(const uint8_t *dones, const float *ep_ret, const int32_t *ep_len, int64_t T,
+                                 int64_t N, int64_t W, double *window, double *meta, int64_t *total_out, void *stream)
+{
+    GS_REQUIRE(T >= 0 && N >= 0 && W >= 1 && W <= 2048, "gs_episode_window: bad shape (W in [1, 2048])");
+    GS_REQUIRE(dones && ep_ret && ep_len && window && meta, "gs_episode_window: null buffer");
+    hipLaunchKernelGGL(k_episode_window, dim3(1), dim3(kWinThreads), sizeof(double) * 2 * W, (hipStream_t)stream,
+                       dones, ep_ret, ep_len, T * N, (int)W, window, meta, total_out);
+    GS_LAUNCH_CHECK("k_episode_window");
     return GS_OK;
 }
 

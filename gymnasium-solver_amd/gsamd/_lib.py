@@ -91,6 +91,7 @@ def _load():
         "gs_env_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, f32, u64, i64, u64, vp, vp, vp, vp, vp,
                                        vp, vp, vp]),
         "gs_episode_stats": (ctypes.c_int, [vp, vp, i64, i64, vp, vp, vp, vp, vp]),
+        "gs_episode_window": (ctypes.c_int, [vp, vp, vp, i64, i64, i64, vp, vp, vp, vp]),
         "gs_ppo_workspace_bytes": (sz, [MlpDims, i64]),
         "gs_ppo_minibatch_step": (ctypes.c_int, [vp, vp, vp, vp, MlpDims, PPOHparams, RolloutView, vp, i64, i64,
                                                  vp, vp, vp, vp, vp]),
@@ -152,7 +153,7 @@ lib = _load()
 EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_rollout_synth_supported",
             "gs_rollout_synth", "gs_env_reset", "gs_env_step",
-            "gs_episode_stats",
+            "gs_episode_stats", "gs_episode_window",
             "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_mlp_activation_stats", "gs_ppo_stage", "gs_ppo_update",
             "gs_ppo_update_global", "gs_ppo_update_workspace_bytes",
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",

@@ -444,27 +444,14 @@ class DeviceRolloutCollector:
         dev = self.device
         if getattr(self, "_win", None) is None:
             self._win = torch.zeros(2, W, dtype=torch.float64, device=dev)        # returns, lengths
-            self._win_meta = torch.zeros(3, dtype=torch.float64, device=dev)      # count, best, last valid
+            self._win_meta = torch.zeros(3, dtype=torch.float64, device=dev)      # count, best, -
             self._win_meta[1] = -float("inf")
-        done = buf.dones.reshape(-1).to(torch.int64)                   # time-major = (step, env)
-        pos = torch.cumsum(done, 0) - 1                                # episode number in the rollout
-        total = pos[-1] + 1
-        rets = self._ep_ret_rows.reshape(-1).double()
-        lens = self._ep_len_rows.reshape(-1).double()
-        # this rollout's last W episodes at slots W - total + pos (the rest go to a dump slot W)
-        slot = torch.where((done > 0) & (pos >= total - W), pos - (total - W), torch.full_like(pos, W))
-        last = torch.zeros(2, W + 1, dtype=torch.float64, device=dev)
-        last[0].scatter_(0, slot, rets)
-        last[1].scatter_(0, slot, lens)
-        i = torch.arange(W, device=dev)
-        keep_old = i + total < W
-        src = torch.clamp(i + total, max=W - 1)
-        self._win.copy_(torch.where(keep_old, self._win[:, src], last[:, :W]))
-        m = self._win_meta
-        m[0] += total.double()
-        best_now = torch.where(done > 0, rets, torch.full_like(rets, -float("inf"))).max()
-        m[1] = torch.maximum(m[1], best_now)
-        self.rollout_episodes_dev = total
+            self.rollout_episodes_dev = torch.zeros((), dtype=torch.int64, device=dev)
+        # one launch (gs_episode_window): the block scan numbers this rollout's episodes in (step,
+        # env) order, the last W land behind the shifted previous window
+        check(lib.gs_episode_window(ptr(buf.dones), ptr(self._ep_ret_rows), ptr(self._ep_len_rows), T, N, W,
+                                    ptr(self._win), ptr(self._win_meta), ptr(self.rollout_episodes_dev),
+                                    stream_handle()), "gs_episode_window")
 
     def _window_metrics(self):
         """roll/ep_rew/{mean,best,last} and roll/ep_len/{mean,last} from the device window (one D2H)."""

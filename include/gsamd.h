@@ -43,7 +43,8 @@ extern "C" {
  * version 2 added the rollout clock argument of gs_policy_act / gs_cnn_policy_act /
  * gs_env_step / gs_atari_env_step and gs_comm_error_record; version 3 widened the metric record
  * to 24 floats and added gs_ppo_update_global; version 4 added gs_comm_xgmi_set_bwd_exchange, gs_comm_allreduce_sum_f64,
- * gs_ppo_global_adv_stats, gs_ppo_global_records, gs_cnn_ppo_update_global and gs_fc_gemm). */
+ * gs_ppo_global_adv_stats, gs_ppo_global_records, gs_cnn_ppo_update_global, gs_fc_gemm and
+ * gs_episode_window). */
 #define GS_ABI_VERSION 4
 int gs_abi_version(void);
 const char *gs_last_error(void);
@@ -145,6 +146,15 @@ int gs_env_step(int32_t *state_dev, float *ep_ret_dev, float *obs_dev, int64_t N
  * the finished episode's return and length where dones_dev is set, 0 elsewhere. */
 int gs_episode_stats(const float *rewards_dev, const uint8_t *dones_dev, int64_t T, int64_t N, float *run_ret_dev,
                      int32_t *run_len_dev, float *ep_ret_dev, int32_t *ep_len_dev, void *stream);
+/* The reference's rolling window of the last W finished episodes (rollout_collector.py:242-294,
+ * 753-758; track_stats=False keeps it on the device): this rollout's episodes in (step, env) order
+ * — dones (T, N) time-major and gs_episode_stats' ep_ret / ep_len rows — appended behind the
+ * previous window (2 x W doubles: returns, then lengths; the oldest first), meta[0] += their count,
+ * meta[1] = max(meta[1], their best return), *total_out = their count (may be NULL).  One launch,
+ * no host round trip. */
+int gs_episode_window(const uint8_t *dones_dev, const float *ep_ret_dev, const int32_t *ep_len_dev, int64_t T,
+                      int64_t N, int64_t W, double *window_dev, double *meta_dev, int64_t *total_out_dev,
+                      void *stream);
 
 /* ---------------------------------------------------------------- PPO update
  * Replaces the minibatch loop: DataLoader(MultiPassRandomSampler) + collate
