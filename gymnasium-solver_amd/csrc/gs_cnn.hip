@@ -1144,7 +1144,7 @@ ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.
 
 // conv trunk + fc for R rows (h): obs rows come from the u8 buffer through idx (or 0..R)
 int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  bool lib_fc = false)
+                  bool lib_fc = false, const int32_t *stop = nullptr)
 {
     int rc;
     if (conv1_lds_supported(L.C, L.H, L.W)) {
@@ -1164,7 +1164,7 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
     }
     // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
     // update), else the engine's split-K partials summed with the bias + ReLU epilogue
-    if (lib_fc) return fc_gemm(s, 0, cnn_bf16(), R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf);
+    if (lib_fc) return fc_gemm(s, 0, cnn_bf16(), R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop);
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
         if ((rc = gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf, true)))
@@ -1214,11 +1214,10 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
                    const int32_t *stop, hipStream_t s, bool lib_fc)
 {
     int rc;
-    (void)stop;
     const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
     // fc: [dWf | dbf] = dh^T [a3 | 1]; lib_fc: dWf on the fc kernels, dbf from the head kernels
     if (lib_fc) {
-        if ((rc = fc_gemm(s, 1, cnn_bf16(), L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr)))
+        if ((rc = fc_gemm(s, 1, cnn_bf16(), L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr, stop)))
             return rc;
     } else {
         const int sw = splits_for(L.HID, L.F + 1, B);
@@ -1228,7 +1227,7 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // da3 = (dh Wf) masked by relu'(a3) in the GEMM's epilogue
     if (lib_fc) {
-        if ((rc = fc_gemm(s, 2, cnn_bf16(), B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, w.a3))) return rc;
+        if ((rc = fc_gemm(s, 2, cnn_bf16(), B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, w.a3, stop))) return rc;
     } else if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr,
                               false, 1, 0, w.a3))) {
         return rc;
@@ -1398,7 +1397,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         const bool lib_fc = fc_supported(0, B, L.HID, L.F, L.F, L.F, L.HID) &&
                             fc_supported(1, L.HID, L.F, B, L.HID, L.F, L.F) &&
                             fc_supported(2, B, L.F, L.HID, L.HID, L.F, L.F);
-        if ((rc = forward_trunk(P, L, fs, B, w, s, lib_fc))) return rc;
+        if ((rc = forward_trunk(P, L, fs, B, w, s, lib_fc, stop))) return rc;
         if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s))) return rc;
         if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, lib_fc))) return rc;
     } else {

@@ -115,8 +115,9 @@ struct Stage {
 template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI>
 __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int64_t lda, const float *__restrict__ Bm,
                                                int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
-                                               const float *__restrict__ aux)
+                                               const float *__restrict__ aux, const int32_t *__restrict__ stop)
 {
+    if (stop && *stop) return;      // KL early stop: the minibatch's product is never used
     constexpr int WGN = 4 / (WGM * KS);
     static_assert(WGM * WGN * KS == 4, "4 waves");
     constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
@@ -241,15 +242,15 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
 
 template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI>
 int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
-              int64_t M, int64_t N, int64_t K, const float *aux)
+              int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop)
 {
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM));
     if (bf)
         hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
-                           (int)M, (int)N, (int)K, aux);
+                           (int)M, (int)N, (int)K, aux, stop);
     else
         hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
-                           (int)M, (int)N, (int)K, aux);
+                           (int)M, (int)N, (int)K, aux, stop);
     GS_LAUNCH_CHECK("k_fc");
     return GS_OK;
 }
@@ -269,7 +270,7 @@ bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
 }
 
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux)
+            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop)
 {
     GS_REQUIRE(op >= 0 && op <= 2, "fc_gemm: op %d", op);
     GS_REQUIRE(fc_supported(op, M, N, K, lda, ldb, ldc), "fc_gemm: shape %lld x %lld x %lld (op %d) not supported",
@@ -277,11 +278,11 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
     GS_REQUIRE(aligned16(A) && aligned16(B) && (op == 1 || aux), "fc_gemm: 16-B aligned operands (and the epilogue "
                "operand) required");
     if (op == 0)     // fwd: C = relu(A B^T + bias), both K-contiguous
-        return launch_fc<32, 64, 1, 2, true, true, kEpiBiasRelu>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux);
+        return launch_fc<32, 64, 1, 2, true, true, kEpiBiasRelu>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
     if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]
-        return launch_fc<64, 64, 2, 1, false, false, kEpiStore>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr);
+        return launch_fc<64, 64, 2, 1, false, false, kEpiStore>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr, stop);
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
-    return launch_fc<64, 64, 2, 1, true, false, kEpiMask>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux);
+    return launch_fc<64, 64, 2, 1, true, false, kEpiMask>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
 }
 
 }  // namespace gs
@@ -292,5 +293,5 @@ extern "C" int gs_fc_gemm(int op, int bf16, int64_t M, int64_t N, int64_t K, con
                           const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, void *stream)
 {
     GS_REQUIRE(A && B && C, "gs_fc_gemm: null operand");
-    return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux);
+    return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux, nullptr);
 }

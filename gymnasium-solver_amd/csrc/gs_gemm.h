@@ -42,7 +42,7 @@ int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, c
 // fc_supported: the shapes they take (K % 64 == 0, 16-B rows, K-strided operands in 4-row blocks).
 bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux);
+            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop = nullptr);
 
 
 // out[r,oy,ox,co] = relu(bias[co] + sum_{c,ky,kx} W[co][c][ky][kx] * frame[c][oy*s+ky][ox*s+kx] / 255)
