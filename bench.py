@@ -361,6 +361,9 @@ def main():
                     help="f32: the fp32 parity path (default, the metric's line); bf16: bf16 MFMA operands in the "
                          "update (the MLP's fused chain, the NatureCNN's convolutions / GEMMs), reported as its own "
                          "line with its deviation from fp32 over one whole update")
+    ap.add_argument("--dp-mode", choices=("local", "global"), default="local",
+                    help="N>1: local (each rank's own minibatches, gradients averaged: the default) or global (the "
+                         "reference's exact global minibatches split over the ranks, sums exchanged)")
     ap.add_argument("--stage-reps", type=int, default=200)
     ap.add_argument("--cpu-minibatches", type=int, default=-1,
                     help="minibatches timed in the CPU baseline (-1: the whole update, 0: no CPU baseline)")
@@ -397,6 +400,8 @@ def main():
     over = dict(n_envs=n_envs, env_dynamics="synthetic" if pixel else args.env_dynamics)
     if args.dtype == "bf16":
         over["precision"] = "bf16"
+    if args.dp_mode == "global":
+        over["dp_mode"] = "global"
     cfg = load_config(env_id, variant, overrides=over)
     agent = DevicePPOAgent(cfg, device=device, rank=rank, world_size=world,
                            use_graph=not args.no_graph, track_stats=False)
@@ -627,7 +632,8 @@ def main():
                        "grad_exchange": args.comm if comm is not None else None,
                        "exchange_in_bwd": in_bwd,
                        "exchange_self_test": dict(gd_self_test) if comm is not None else None,
-                       "comm": comm_info, "same_device": bool(args.same_device)},
+                       "comm": comm_info, "same_device": bool(args.same_device),
+                       "dp_mode": args.dp_mode},
             "roofline": roofline,
             "rooflines": rooflines,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},

@@ -82,11 +82,13 @@ __global__ __launch_bounds__(256) void k_atari_counters(int32_t *__restrict__ st
 
 // ---- the frame source: raw RGB frames 2*step and 2*step+1 of every env.  Word w of frame j of
 // env e is mix64(mix64(mix64(mix64(seed) ^ e) ^ (2 step + j)) ^ w): blockIdx.y = (env, frame), so
-// the three leading mixes are one per thread, and each thread writes kRenderWords words of it
-// (256-word strides: every wave store is 2 KB contiguous)
+// the three leading mixes are one per thread, and each thread writes kRenderPairs 16-B pairs of
+// words (256-pair strides: every wave store is 1 KB contiguous)
 constexpr int kFrameWords = kFrameBytes / 8;       // 12 600
-constexpr int kRenderWords = 4;
-constexpr int kRenderChunks = (kFrameWords + 256 * kRenderWords - 1) / (256 * kRenderWords);
+constexpr int kFramePairs = kFrameWords / 2;       // 6 300
+constexpr int kRenderPairs = 2;
+constexpr int kRenderChunks = (kFramePairs + 256 * kRenderPairs - 1) / (256 * kRenderPairs);
+static_assert(kFrameWords % 2 == 0 && kFrameBytes % 16 == 0, "16-B frame pairs");
 
 __global__ __launch_bounds__(256) void k_atari_render(uint8_t *__restrict__ frames, int64_t N, uint64_t seed,
                                                       int64_t env_offset, uint64_t step_count,
@@ -98,12 +100,17 @@ __global__ __launch_bounds__(256) void k_atari_render(uint8_t *__restrict__ fram
     const int j = (int)(ej & 1);
     const uint64_t ge = (uint64_t)(env_offset + e);
     const uint64_t hf = mix64(mix64(mix64(seed) ^ ge) ^ (2 * step_count + (uint64_t)j));
-    uint64_t *out = (uint64_t *)frames + ej * kFrameWords;
-    const int w0 = blockIdx.x * 256 * kRenderWords + threadIdx.x;
+    ulonglong2 *out = reinterpret_cast<ulonglong2 *>(frames + ej * (int64_t)kFrameBytes);
+    const int p0 = blockIdx.x * 256 * kRenderPairs + threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < kRenderWords; ++q) {
-        const int w = w0 + 256 * q;
-        if (w < kFrameWords) out[w] = mix64(hf ^ (uint64_t)w);
+    for (int q = 0; q < kRenderPairs; ++q) {
+        const int p = p0 + 256 * q;
+        if (p < kFramePairs) {
+            ulonglong2 v;
+            v.x = mix64(hf ^ (uint64_t)(2 * p));
+            v.y = mix64(hf ^ (uint64_t)(2 * p + 1));
+            out[p] = v;
+        }
     }
     (void)N;
 }
@@ -165,8 +172,9 @@ __global__ __launch_bounds__(256) void k_atari_stack(const uint8_t *__restrict__
 // output row), one contiguous 14 400-B run of each raw frame.  Per workgroup:
 //   1. every load issued up front: the stack slots 1..S-1 of the band (the shift's sources,
 //      16-B loads, first so that their data has landed before any store of this workgroup) and
-//      both frames' runs as 300 pixel-aligned 48-B chunks (16 pixels = three 16-B loads);
-//   2. grayscale + max-pool once per input pixel, 16 gray bytes per ds_write_b128 into LDS;
+//      both frames' runs as 1 200 pixel-aligned 12-B units (4 pixels, one dwordx3 load: a wave's
+//      load instruction covers 768 contiguous bytes);
+//   2. grayscale + max-pool once per input pixel, 4 gray bytes per ds_write_b32 into LDS;
 //   3. the shifted slots stored (zeros after a done: FrameStackObservation's zero padding);
 //   4. the area resize from LDS in preprocess_px's order (row sums over ix, then total over iy,
 //      taps beyond a pixel's count weighted 0.0f: exact, every partial sum is >= 0), four
@@ -175,24 +183,25 @@ __global__ __launch_bounds__(256) void k_atari_stack(const uint8_t *__restrict__
 // + (S-1)·7 056 written, all 16-B vector moves.
 constexpr int kOut84 = 84, kBandOut = 12, kBandIn = 30, kBands = kOut84 / kBandOut;
 constexpr int kRowBytes = kFW * kFC;                          // 480
-constexpr int kBandChunks = kBandIn * kFW / 16;               // 300 chunks of 16 pixels
+constexpr int kBandUnits = kBandIn * kFW / 4;                 // 1 200 units of 4 pixels (12 B)
+constexpr int kBandUnitsPer = (kBandUnits + 255) / 256;       // 5 per thread
 constexpr int kBandOutBytes = kBandOut * kOut84;              // 1 008 = 63 x 16 B
 constexpr int kMaxStackFast = 5;                              // (S-1) x 63 shift chunks <= 256 threads
 static_assert(kBandIn * kBands == kFH && 2 * kBandIn == 5 * kBandOut, "band geometry");
 
-__device__ __forceinline__ uint32_t gray16_word(const uint32_t (&a)[12], const uint32_t (&b)[12], int q)
+// four max-pooled gray pixels from 12 bytes (4 RGB pixels) of each frame
+__device__ __forceinline__ uint32_t gray4(uint3 a, uint3 b)
 {
-    // pixels 4q..4q+3 of the 16 in a 48-B chunk: bytes 12q .. 12q+11 of each frame's chunk
+    const uint32_t wa[3] = {a.x, a.y, a.z}, wb[3] = {b.x, b.y, b.z};
     uint32_t out = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int byte = 12 * q + 3 * k;
         int rgb0[3], rgb1[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const int bb = byte + c;
-            rgb0[c] = (int)((a[bb >> 2] >> (8 * (bb & 3))) & 0xffu);
-            rgb1[c] = (int)((b[bb >> 2] >> (8 * (bb & 3))) & 0xffu);
+            const int bb = 3 * k + c;
+            rgb0[c] = (int)((wa[bb >> 2] >> (8 * (bb & 3))) & 0xffu);
+            rgb1[c] = (int)((wb[bb >> 2] >> (8 * (bb & 3))) & 0xffu);
         }
         const int g0 = (rgb0[0] * 4899 + rgb0[1] * 9617 + rgb0[2] * 1868 + (1 << 13)) >> 14;
         const int g1 = (rgb1[0] * 4899 + rgb1[1] * 9617 + rgb1[2] * 1868 + (1 << 13)) >> 14;
@@ -205,31 +214,27 @@ __global__ __launch_bounds__(256) void k_atari_stack84(const uint8_t *__restrict
                                                        const uint8_t *__restrict__ done_row, int64_t N, int S,
                                                        uint8_t *__restrict__ stack)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t g[kBandIn * kFW];     // 4 800 B of max-pooled gray
+    __shared__ __attribute__((aligned(16))) uint32_t g[kBandIn * kFW / 4];     // 4 800 B of max-pooled gray
     const int64_t e = blockIdx.x / kBands;
     const int band = (int)(blockIdx.x - e * kBands);
     const int tid = threadIdx.x;
     constexpr int hw = kOut84 * kOut84;
     uint8_t *st = stack + e * (int64_t)S * hw + band * kBandOutBytes;
-    // 1. loads: the shift's sources first, then the two frames' chunks (clamped, unconditional)
+    // 1. loads: the shift's sources first, then the two frames' runs as 12-B units (4 pixels):
+    //    lane i of a wave reads bytes 12 i .. 12 i + 11, so every dwordx3 load instruction covers
+    //    768 contiguous bytes (clamped, unconditional)
     const int nshift = 63 * (S - 1);
     const int sj = min(tid, max(nshift - 1, 0));
     uint4 moved = make_uint4(0u, 0u, 0u, 0u);
     if (nshift > 0) moved = *reinterpret_cast<const uint4 *>(st + (int64_t)(1 + sj / 63) * hw + 16 * (sj % 63));
     const uint8_t *fa = frames + e * 2 * (int64_t)kFrameBytes + band * kBandIn * kRowBytes;
     const uint8_t *fb = fa + kFrameBytes;
-    uint32_t a0[12], b0[12], a1[12], b1[12];
-    const int c0 = tid, c1 = min(tid + 256, kBandChunks - 1);
+    uint3 ra[kBandUnitsPer], rb[kBandUnitsPer];
 #pragma unroll
-    for (int w = 0; w < 3; ++w) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(fa + 48 * c0 + 16 * w);
-        const uint4 y = *reinterpret_cast<const uint4 *>(fb + 48 * c0 + 16 * w);
-        const uint4 u = *reinterpret_cast<const uint4 *>(fa + 48 * c1 + 16 * w);
-        const uint4 v = *reinterpret_cast<const uint4 *>(fb + 48 * c1 + 16 * w);
-        a0[4 * w] = x.x, a0[4 * w + 1] = x.y, a0[4 * w + 2] = x.z, a0[4 * w + 3] = x.w;
-        b0[4 * w] = y.x, b0[4 * w + 1] = y.y, b0[4 * w + 2] = y.z, b0[4 * w + 3] = y.w;
-        a1[4 * w] = u.x, a1[4 * w + 1] = u.y, a1[4 * w + 2] = u.z, a1[4 * w + 3] = u.w;
-        b1[4 * w] = v.x, b1[4 * w + 1] = v.y, b1[4 * w + 2] = v.z, b1[4 * w + 3] = v.w;
+    for (int j = 0; j < kBandUnitsPer; ++j) {
+        const int u = min(tid + 256 * j, kBandUnits - 1);
+        ra[j] = *reinterpret_cast<const uint3 *>(fa + 12 * u);
+        rb[j] = *reinterpret_cast<const uint3 *>(fb + 12 * u);
     }
     // the resize's coverage tables for this thread's row and four columns (L1-resident)
     const int oyl = tid / 21, ox0 = 4 * (tid - 21 * (tid / 21));
@@ -248,13 +253,10 @@ __global__ __launch_bounds__(256) void k_atari_stack84(const uint8_t *__restrict
         for (int i = 0; i < 3; ++i) wx[q][i] = i < nx ? c_area.wx[ox][i] : 0.0f;
     }
     const bool reset = done_row ? done_row[e] != 0 : true;
-    // 2. grayscale + max-pool into LDS
-    if (c0 < kBandChunks)
-        *reinterpret_cast<uint4 *>(g + 16 * c0) = make_uint4(gray16_word(a0, b0, 0), gray16_word(a0, b0, 1),
-                                                             gray16_word(a0, b0, 2), gray16_word(a0, b0, 3));
-    if (tid + 256 < kBandChunks)
-        *reinterpret_cast<uint4 *>(g + 16 * c1) = make_uint4(gray16_word(a1, b1, 0), gray16_word(a1, b1, 1),
-                                                             gray16_word(a1, b1, 2), gray16_word(a1, b1, 3));
+    // 2. grayscale + max-pool into LDS, one word of 4 pixels per unit
+#pragma unroll
+    for (int j = 0; j < kBandUnitsPer; ++j)
+        if (tid + 256 * j < kBandUnits) g[tid + 256 * j] = gray4(ra[j], rb[j]);
     __syncthreads();
     // 3. the shift (every source load of this workgroup has landed: the gray bytes above waited
     //    for the younger frame loads)
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(256) void k_atari_stack84(const uint8_t *__restrict
 #pragma unroll
                 for (int ix = 0; ix < 3; ++ix) {
                     const int xx = min(x0[q] + ix, kFW - 1);
-                    row = row + wx[q][ix] * (float)g[yy * kFW + xx];
+                    row = row + wx[q][ix] * (float)reinterpret_cast<const uint8_t *>(g)[yy * kFW + xx];
                 }
                 total = total + wy[iy] * row;
             }

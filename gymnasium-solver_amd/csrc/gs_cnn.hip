@@ -323,24 +323,14 @@ __device__ __forceinline__ uint64_t mix64d(uint64_t x)
     return x ^ (x >> 31);
 }
 
-// ---- rollout: action select over the valid set, log_prob, value.  One thread per env.
+// ---- rollout: action select over the valid set, log_prob, value of row r from its head outputs
+// zr (biases added; zr[A] = the value)
 template <int AM>
-__global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, const float *__restrict__ P, CnnLayout L,
-                                                 int64_t R, int mode,
-                                                 uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
-                                                 float *__restrict__ logp, float *__restrict__ value,
-                                                 const uint64_t *__restrict__ clock)
+__device__ __forceinline__ void act_select(const float (&zr)[AM + 1], float v, int64_t r, const CnnLayout &L, int mode,
+                                           uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
+                                           float *__restrict__ logp, float *__restrict__ value,
+                                           const uint64_t *__restrict__ clock)
 {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= R) return;
-    const int A1 = L.A + 1;
-    float zr[AM + 1];
-    float v = 0.f;
-#pragma unroll
-    for (int a = 0; a < AM + 1; ++a) {
-        zr[a] = a < A1 ? z[r * A1 + a] + (a < L.A ? P[L.obp + a] : P[L.obv]) : 0.f;
-        if (a == L.A) v = zr[a];
-    }
     if (value) value[r] = v;
     if (!actions) return;
     const MRow h = mrow_stats<AM>(zr, L);
@@ -377,6 +367,69 @@ __global__ __launch_bounds__(256) void k_cnn_act(const float *__restrict__ z, co
     for (int a = 0; a < AM; ++a)
         if (a == act) za = zr[a];
     logp[r] = za - h.lse;
+}
+
+// ---- the rollout's fc epilogue + heads + action select in one launch (one workgroup per env):
+// h[j] = relu(bf[j] + the fc's split-K partials summed in k_sum_parts_ep's order), kept in
+// registers; z = h [Wp; Wv]^T as per-thread partials over j = tid, tid + 256, ... reduced in a
+// fixed tree (32 consecutive threads, then the 8 groups in order); thread 0 adds the biases and
+// selects the action.  Replaces the heads GEMM, its split-K sum, the fc sum and a per-env act
+// kernel.
+template <int AM>
+__global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ parts, int np, int64_t pstride,
+                                                      const float *__restrict__ P, CnnLayout L, int mode,
+                                                      uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
+                                                      float *__restrict__ logp, float *__restrict__ value,
+                                                      const uint64_t *__restrict__ clock)
+{
+    __shared__ float red[(AM + 1) * 256];
+    const int64_t r = blockIdx.x;
+    const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
+    float acc[AM + 1];
+#pragma unroll
+    for (int a = 0; a < AM + 1; ++a) acc[a] = 0.f;
+    for (int j = tid; j < HID; j += 256) {
+        const int64_t i = r * HID + j;
+        float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int p = 0;
+        for (; p + 8 <= np; p += 8) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t[q] += parts[(int64_t)(p + q) * pstride + i];
+        }
+        for (; p < np; ++p) t[0] += parts[(int64_t)p * pstride + i];
+        float hv = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+        hv += P[L.obf + j];
+        hv = hv > 0.f ? hv : 0.f;
+#pragma unroll
+        for (int a = 0; a < AM + 1; ++a) {
+            if (a < A) acc[a] = fmaf(hv, P[L.oWp + (int64_t)a * HID + j], acc[a]);
+            else if (a == A) acc[a] = fmaf(hv, P[L.oWv + j], acc[a]);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < AM + 1; ++a) red[a * 256 + tid] = acc[a];
+    __syncthreads();
+    float g = 0.f;
+    if (tid < A1 * 8) {
+        const int a = tid >> 3, q = tid & 7;
+        for (int m = 0; m < 32; ++m) g += red[a * 256 + q * 32 + m];
+    }
+    __syncthreads();
+    if (tid < A1 * 8) red[tid] = g;
+    __syncthreads();
+    if (tid == 0) {
+        float zr[AM + 1];
+        float v = 0.f;
+#pragma unroll
+        for (int a = 0; a < AM + 1; ++a) {
+            float z = 0.f;
+            if (a < A1)
+                for (int q = 0; q < 8; ++q) z += red[a * 8 + q];
+            zr[a] = a < A1 ? z + (a < A ? P[L.obp + a] : P[L.obv]) : 0.f;
+            if (a == A) v = zr[a];
+        }
+        act_select<AM>(zr, v, r, L, mode, seed, counter, actions, logp, value, clock);
+    }
 }
 
 // ---- gather the 5 per-row rollout fields of the minibatch
@@ -1142,15 +1195,19 @@ ConvGeom geom1(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.H, L.W
 ConvGeom geom2(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h1, L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, L.c2}; }
 ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.w2, L.c2, L.k3, L.s3, L.h3, L.w3, L.c3}; }
 
-// conv trunk + fc for R rows (h): obs rows come from the u8 buffer through idx (or 0..R)
-int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  bool lib_fc = false, const int32_t *stop = nullptr)
+// the conv trunk for R rows (a3): obs rows come from the u8 buffer through idx (or 0..R)
+// (obs_copy: the rollout's obs row, written by conv1 from the frames it loads anyway)
+int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
+                  uint8_t *obs_copy = nullptr)
 {
     int rc;
     if (conv1_lds_supported(L.C, L.H, L.W)) {
-        if ((rc = conv1_lds_fwd(s, (int)R, fs.obs, fs.idx, fs.T, fs.N, P + L.oW1, P + L.ob1, w.a1))) return rc;
-    } else if ((rc = conv_fwd_u8(s, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) {
-        return rc;
+        if ((rc = conv1_lds_fwd(s, (int)R, fs.obs, fs.idx, fs.T, fs.N, P + L.oW1, P + L.ob1, w.a1, obs_copy)))
+            return rc;
+    } else {
+        if (obs_copy && obs_copy != fs.obs)
+            GS_HIP(hipMemcpyAsync(obs_copy, fs.obs, (size_t)R * L.C * L.H * L.W, hipMemcpyDeviceToDevice, s));
+        if ((rc = conv_fwd_u8(s, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) return rc;
     }
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
         if ((rc = conv23_lds_fwd(s, 2, (int)R, w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
@@ -1162,6 +1219,15 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
     } else if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
         return rc;
     }
+    return GS_OK;
+}
+
+// conv trunk + fc for R rows (h)
+int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
+                  bool lib_fc = false, const int32_t *stop = nullptr)
+{
+    int rc = forward_convs(P, L, fs, R, w, s);
+    if (rc) return rc;
     // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
     // update), else the engine's split-K partials summed with the bias + ReLU epilogue
     if (lib_fc) return fc_gemm(s, 0, cnn_bf16(), R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop);
@@ -1445,7 +1511,7 @@ extern "C" size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows)
 
 extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const uint8_t *obs, int64_t N, int mode,
                                  uint64_t rng_seed, uint64_t rng_counter, int64_t *actions, float *logp, float *value,
-                                 void *workspace, const uint64_t *clock, void *stream)
+                                 uint8_t *obs_store, void *workspace, const uint64_t *clock, void *stream)
 {
     int rc = check_cnn(dims);
     if (rc) return rc;
@@ -1456,14 +1522,21 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, N);
-    if ((rc = forward(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s))) return rc;
+    // the conv trunk, the fc product as split-K partials (no epilogue), then one launch for the
+    // fc epilogue + heads + action select
+    if ((rc = forward_convs(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s, obs_store))) return rc;
+    const int sf = splits_for(N, L.HID, L.F);
+    if ((rc = gemm_f32(s, false, true, N, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.parts, L.HID, 0.f, nullptr,
+                       false, sf, N * L.HID)))
+        return rc;
+    GS_REQUIRE(N < ((int64_t)1 << 31), "gs_cnn_policy_act: %lld envs exceed the launch grid", (long long)N);
     if (L.A <= 18)
-        hipLaunchKernelGGL(k_cnn_act<18>, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed,
-                           rng_counter, actions, logp, value, clock);
+        hipLaunchKernelGGL(k_cnn_head_act<18>, dim3((unsigned)N), dim3(256), 0, s, w.parts, sf, N * L.HID, params, L,
+                           mode, rng_seed, rng_counter, actions, logp, value, clock);
     else
-        hipLaunchKernelGGL(k_cnn_act<kAMax>, dim3(nblk(N)), dim3(256), 0, s, w.z, params, L, N, mode, rng_seed,
-                           rng_counter, actions, logp, value, clock);
-    GS_LAUNCH_CHECK("k_cnn_act");
+        hipLaunchKernelGGL(k_cnn_head_act<kAMax>, dim3((unsigned)N), dim3(256), 0, s, w.parts, sf, N * L.HID, params,
+                           L, mode, rng_seed, rng_counter, actions, logp, value, clock);
+    GS_LAUNCH_CHECK("k_cnn_head_act");
     return GS_OK;
 }
 

@@ -11,7 +11,7 @@ constexpr int kConvWgradWG = 256;      // workgroups (= partials) of the conv2 /
 bool conv1_lds_supported(int C, int H, int W);
 // out[r][oy][ox][co] = relu(b1[co] + sum W1[co][c][ky][kx] * frame(r)[c][4 oy + ky][4 ox + kx] / 255)
 int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N, const float *W1,
-                  const float *b1, float *out);
+                  const float *b1, float *out, uint8_t *obs_copy = nullptr);
 // dW1 = sum_rows dA1^T . patches, db1 = column sums of dA1; parts: kConv1WgradWG x (32*256 + 32) floats
 int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
                     const float *dA, float *parts, float *dW1, float *db1);

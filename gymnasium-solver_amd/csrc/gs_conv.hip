@@ -56,9 +56,12 @@ __device__ __forceinline__ int64_t frame_src(const int32_t *idx, int64_t r, int6
 }
 
 // stage frame rows [y0, y0 + BIR) of sample r as fp32 [C][BIR][W] (rows past H are zero):
-// every thread issues all of its u32 loads before converting any (one memory latency)
+// every thread issues all of its u32 loads before converting any (one memory latency).  copy:
+// the sample's u8 stack elsewhere (the rollout row), rows [ylo, yhi) of it written from the same
+// loaded words
 template <class G>
-__device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict__ obs, int64_t src, int y0)
+__device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict__ obs, int64_t src, int y0,
+                                           uint8_t *__restrict__ copy = nullptr, int ylo = 0, int yhi = 0)
 {
     constexpr int NE = G::C * G::BIR * G::W4, PER = (NE + 255) / 256;
     const uint8_t *base = obs + src * (int64_t)(G::C * G::H * G::W);
@@ -83,6 +86,8 @@ __device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict_
             const float4 f = make_float4((float)(v[j] & 255u) / 255.0f, (float)((v[j] >> 8) & 255u) / 255.0f,
                                          (float)((v[j] >> 16) & 255u) / 255.0f, (float)(v[j] >> 24) / 255.0f);
             *reinterpret_cast<float4 *>(fr + (c * G::BIR + y) * G::W + 4 * x4) = f;
+            if (copy && y0 + y >= ylo && y0 + y < yhi)
+                *reinterpret_cast<uint32_t *>(copy + ((int64_t)c * G::H + y0 + y) * G::W + 4 * x4) = v[j];
         }
     }
 }
@@ -92,8 +97,11 @@ __device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict_
 template <class G, bool BF = false>
 __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
                                                    int64_t T, int64_t N, const float *__restrict__ W1,
-                                                   const float *__restrict__ b1, float *__restrict__ out)
+                                                   const float *__restrict__ b1, float *__restrict__ out,
+                                                   uint8_t *__restrict__ obs_copy)
 {
+    // obs_copy (the rollout's obs row, idx == nullptr): band 0 copies rows [0, H/2), band 1 the rest
+    static_assert(G::BIR >= G::H / 2 && G::BOH * G::S <= G::H / 2, "the two bands cover the halves");
     __shared__ __attribute__((aligned(16))) float fr[G::FRAME];
     const int r = blockIdx.x >> 1, band = blockIdx.x & 1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -111,7 +119,9 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
         const int c = g >> 2, ky = 2 * (g & 3) + (lq >> 1), kx0 = 4 * (lq & 1);
         b[g] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
     }
-    stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S);
+    stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S,
+                  obs_copy ? obs_copy + (int64_t)r * (G::C * G::H * G::W) : nullptr, band * (G::H / 2),
+                  band ? G::H : G::H / 2);
     __syncthreads();
 
     constexpr int TMW = (G::MT + 1) / 2;
@@ -815,14 +825,16 @@ using C1_84 = C1<4, 84, 84>;
 bool conv1_lds_supported(int C, int H, int W) { return C == 4 && H == 84 && W == 84; }
 
 int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N, const float *W1,
-                  const float *b1, float *out)
+                  const float *b1, float *out, uint8_t *obs_copy)
 {
     GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
+    GS_REQUIRE(!obs_copy || !idx, "conv1_lds_fwd: the obs copy is for the rollout's own rows");
     if (cnn_bf16())
         hipLaunchKernelGGL((k_conv1_fwd<C1_84, true>), dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1,
-                           out);
+                           out, obs_copy);
     else
-        hipLaunchKernelGGL(k_conv1_fwd<C1_84>, dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1, out);
+        hipLaunchKernelGGL(k_conv1_fwd<C1_84>, dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
+                           obs_copy);
     GS_LAUNCH_CHECK("k_conv1_fwd");
     return GS_OK;
 }

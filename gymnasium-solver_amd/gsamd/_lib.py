@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before the library)
 LIB_PATH = os.environ.get("GSAMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
 
 GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
-GS_ABI_VERSION = 4          # include/gsamd.h: the argument lists this binding declares
+GS_ABI_VERSION = 5          # include/gsamd.h: the argument lists this binding declares
 GS_NUM_METRICS = 24
 METRIC_SLOTS = (
     "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
@@ -108,7 +108,7 @@ def _load():
         "gs_ppo_exchange_inside_bwd": (ctypes.c_int, [vp, MlpDims, ctypes.c_int64, vp]),
         "gs_cnn_param_count": (i64, [CnnDims]),
         "gs_cnn_workspace_bytes": (sz, [CnnDims, i64]),
-        "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp]),
+        "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp, vp]),
         "gs_cnn_ppo_loss": (ctypes.c_int, [vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, vp, vp, vp, vp]),
         "gs_cnn_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, i64, i64,
                                              vp, vp, vp, vp, vp]),

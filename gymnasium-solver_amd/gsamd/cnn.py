@@ -166,12 +166,13 @@ class DeviceCNNActorCritic:
             actions: torch.Tensor = None, logp: torch.Tensor = None, values: torch.Tensor = None,
             obs_store: torch.Tensor = None, clock: torch.Tensor = None):
         """policy_act (utils/policy_ops.py:14-34) on u8 frame stacks (N, C, H, W); obs_store
-        (the rollout row) receives a copy of the observation."""
+        (the rollout row) receives a copy of the observation (written by the first convolution)."""
         n = obs.shape[0]
         if not (obs.is_contiguous() and obs.dtype == torch.uint8 and obs.device == self.device):
             raise ValueError("obs must be a contiguous uint8 device tensor (N, C, H, W)")
-        if obs_store is not None:
-            obs_store.copy_(obs)
+        if obs_store is not None and not (obs_store.is_contiguous() and obs_store.dtype == torch.uint8
+                                          and obs_store.shape == obs.shape and obs_store.device == obs.device):
+            raise ValueError("obs_store must be a contiguous uint8 device tensor shaped like obs")
         if actions is None:
             actions = torch.empty(n, dtype=torch.int64, device=self.device)
         if logp is None:
@@ -179,7 +180,8 @@ class DeviceCNNActorCritic:
         if values is None:
             values = torch.empty(n, dtype=torch.float32, device=self.device)
         check(lib.gs_cnn_policy_act(ptr(self.params), self.dims, ptr(obs), n, int(mode), int(rng_seed),
-                                    int(rng_counter), ptr(actions), ptr(logp), ptr(values), ptr(self.workspace(n)),
+                                    int(rng_counter), ptr(actions), ptr(logp), ptr(values),
+                                    ptr(obs_store) if obs_store is not None else None, ptr(self.workspace(n)),
                                     ptr(clock), stream_handle()), "gs_cnn_policy_act")
         return actions, logp, values
 
@@ -187,7 +189,7 @@ class DeviceCNNActorCritic:
         n = obs.shape[0]
         if out is None:
             out = torch.empty(n, dtype=torch.float32, device=self.device)
-        check(lib.gs_cnn_policy_act(ptr(self.params), self.dims, ptr(obs), n, 0, 0, 0, None, None, ptr(out),
+        check(lib.gs_cnn_policy_act(ptr(self.params), self.dims, ptr(obs), n, 0, 0, 0, None, None, ptr(out), None,
                                     ptr(self.workspace(n)), None, stream_handle()), "gs_cnn_policy_act")
         return out
 

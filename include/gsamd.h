@@ -44,8 +44,8 @@ extern "C" {
  * gs_env_step / gs_atari_env_step and gs_comm_error_record; version 3 widened the metric record
  * to 24 floats and added gs_ppo_update_global; version 4 added gs_comm_xgmi_set_bwd_exchange, gs_comm_allreduce_sum_f64,
  * gs_ppo_global_adv_stats, gs_ppo_global_records, gs_cnn_ppo_update_global, gs_fc_gemm and
- * gs_episode_window). */
-#define GS_ABI_VERSION 4
+ * gs_episode_window; version 5 added the obs_store argument of gs_cnn_policy_act). */
+#define GS_ABI_VERSION 5
 int gs_abi_version(void);
 const char *gs_last_error(void);
 
@@ -360,10 +360,13 @@ int64_t gs_cnn_param_count(gs_cnn_dims dims);
 /* scratch for `rows` rows (the minibatch B for updates, N envs for gs_cnn_policy_act) */
 size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows);
 /* policy_act on N frame stacks obs_dev (N, in_c, in_h, in_w): mode 0 sample / 1 argmax /
- * 2 replay (as gs_policy_act); masked actions are never drawn. */
+ * 2 replay (as gs_policy_act); masked actions are never drawn.  obs_store_dev (may be NULL): the
+ * rollout buffer's obs row, receives a copy of obs_dev (written by the first convolution from the
+ * frames it loads, no separate copy launch). */
 int gs_cnn_policy_act(const float *params_dev, gs_cnn_dims dims, const uint8_t *obs_dev, int64_t N, int mode,
                       uint64_t rng_seed, uint64_t rng_counter, int64_t *actions_dev, float *logp_dev,
-                      float *value_dev, void *workspace_dev, const uint64_t *clock_dev, void *stream);
+                      float *value_dev, uint8_t *obs_store_dev, void *workspace_dev, const uint64_t *clock_dev,
+                      void *stream);
 /* losses_for_batch on one minibatch: metrics record + (optional) dLoss/dlogits (B, A+1). */
 int gs_cnn_ppo_loss(const float *params_dev, gs_cnn_dims dims, gs_ppo_hparams hp, gs_rollout_view_u8 rollout,
                     const int32_t *idx_dev, int64_t batch, float *metrics_dev, float *dlogits_dev,

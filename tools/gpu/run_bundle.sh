@@ -13,6 +13,11 @@ step atari-prof timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/atari -
 step c5-collect-prof timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/c5c -o c5c --output-format csv \
     -- python tools/collect_run.py C5 3 > $O/c5c.log 2>&1 && grep "collect" $O/c5c.log || exit 1
 step fc-bench timeout -k 10 120 python tools/fc_bench.py > $O/fc_bench.log 2>&1 && cat $O/fc_bench.log || exit 1
+if [ -n "$CNNK" ]; then
+  step cnn-trace timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/cnn_stats -o cnn --output-format csv \
+      -- python tools/cnn_kernel_run.py ${CNNK_ARGS} > $O/cnn_trace.log 2>&1 || exit 1
+fi
+[ -n "$C4B" ] || { rm -f $O/*/*kernel_trace.csv; exit 0; }
 step bench-c4 timeout -k 10 300 python bench.py --workload C4 --steps 2 --warmup 1 --cpu-minibatches 0 \
     > $O/bench_c4.json 2> $O/bench_c4.err && tail -c 600 $O/bench_c4.json || exit 1
 step bench-c4bf16 timeout -k 10 300 python bench.py --workload C4 --dtype bf16 --steps 2 --warmup 1 --cpu-minibatches 0 \
