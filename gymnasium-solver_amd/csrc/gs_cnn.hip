@@ -143,6 +143,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
                                          (int64_t)kConvWgradWG * 64 * (std::max(L.K2, L.K3) + 1)});
         const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
         const int64_t gparts = std::max({(int64_t)splits_for(R, L.HID, L.F) * R * L.HID,
+                                         (int64_t)fc_fwd_splits(R, L.HID, L.F) * R * L.HID,
                                          (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
                                          (int64_t)splits_for(L.A + 1, L.HID + 1, R) * (L.A + 1) * (L.HID + 1),
                                          (int64_t)splits_for(L.HID, L.F + 1, R) * L.HID * (L.F + 1)});
@@ -369,35 +370,31 @@ __device__ __forceinline__ void act_select(const float (&zr)[AM + 1], float v, i
     logp[r] = za - h.lse;
 }
 
-// ---- the rollout's fc epilogue + heads + action select in one launch (one workgroup per env):
-// h[j] = relu(bf[j] + the fc's split-K partials summed in k_sum_parts_ep's order), kept in
-// registers; z = h [Wp; Wv]^T as per-thread partials over j = tid, tid + 256, ... reduced in a
-// fixed tree (32 consecutive threads, then the 8 groups in order); thread 0 adds the biases and
-// selects the action.  Replaces the heads GEMM, its split-K sum, the fc sum and a per-env act
-// kernel.
+// ---- the rollout's fc epilogue + heads + action select in one launch, one wave per env (4 per
+// workgroup, no barrier): lane l takes j = l, l + 64, ... of the row: h[j] = relu(bf[j] + the
+// fc's split-K partials summed in slice order) and its share of z = h [Wp; Wv]^T; the lanes'
+// shares are added by a fixed xor butterfly; lane 0 adds the biases and selects the action.
+// Replaces the heads GEMM, its split-K sum, the fc sum and a per-env act kernel.
+constexpr int kActRowsPerWG = 4;
+
 template <int AM>
 __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ parts, int np, int64_t pstride,
-                                                      const float *__restrict__ P, CnnLayout L, int mode,
+                                                      int64_t R, const float *__restrict__ P, CnnLayout L, int mode,
                                                       uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
                                                       float *__restrict__ logp, float *__restrict__ value,
                                                       const uint64_t *__restrict__ clock)
 {
-    __shared__ float red[(AM + 1) * 256];
-    const int64_t r = blockIdx.x;
-    const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * kActRowsPerWG + (threadIdx.x >> 6);
+    if (r >= R) return;                               // wave-uniform
+    const int HID = L.HID, A = L.A;
     float acc[AM + 1];
 #pragma unroll
     for (int a = 0; a < AM + 1; ++a) acc[a] = 0.f;
-    for (int j = tid; j < HID; j += 256) {
+    for (int j = lane; j < HID; j += 64) {
         const int64_t i = r * HID + j;
-        float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        int p = 0;
-        for (; p + 8 <= np; p += 8) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) t[q] += parts[(int64_t)(p + q) * pstride + i];
-        }
-        for (; p < np; ++p) t[0] += parts[(int64_t)p * pstride + i];
-        float hv = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+        float hv = 0.f;
+        for (int p = 0; p < np; ++p) hv += parts[(int64_t)p * pstride + i];
         hv += P[L.obf + j];
         hv = hv > 0.f ? hv : 0.f;
 #pragma unroll
@@ -407,25 +404,15 @@ __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ 
         }
     }
 #pragma unroll
-    for (int a = 0; a < AM + 1; ++a) red[a * 256 + tid] = acc[a];
-    __syncthreads();
-    float g = 0.f;
-    if (tid < A1 * 8) {
-        const int a = tid >> 3, q = tid & 7;
-        for (int m = 0; m < 32; ++m) g += red[a * 256 + q * 32 + m];
-    }
-    __syncthreads();
-    if (tid < A1 * 8) red[tid] = g;
-    __syncthreads();
-    if (tid == 0) {
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int a = 0; a < AM + 1; ++a) acc[a] += __shfl_xor(acc[a], off);
+    if (lane == 0) {
         float zr[AM + 1];
         float v = 0.f;
 #pragma unroll
         for (int a = 0; a < AM + 1; ++a) {
-            float z = 0.f;
-            if (a < A1)
-                for (int q = 0; q < 8; ++q) z += red[a * 8 + q];
-            zr[a] = a < A1 ? z + (a < A ? P[L.obp + a] : P[L.obv]) : 0.f;
+            zr[a] = a <= A ? acc[a] + (a < A ? P[L.obp + a] : P[L.obv]) : 0.f;
             if (a == A) v = zr[a];
         }
         act_select<AM>(zr, v, r, L, mode, seed, counter, actions, logp, value, clock);
@@ -1525,17 +1512,23 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     // the conv trunk, the fc product as split-K partials (no epilogue), then one launch for the
     // fc epilogue + heads + action select
     if ((rc = forward_convs(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s, obs_store))) return rc;
-    const int sf = splits_for(N, L.HID, L.F);
-    if ((rc = gemm_f32(s, false, true, N, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.parts, L.HID, 0.f, nullptr,
-                       false, sf, N * L.HID)))
-        return rc;
-    GS_REQUIRE(N < ((int64_t)1 << 31), "gs_cnn_policy_act: %lld envs exceed the launch grid", (long long)N);
+    int sf = 1;
+    if (fc_supported(0, N, L.HID, L.F, L.F, L.F, L.HID)) {      // the fc kernels, split-K partials
+        sf = fc_fwd_splits(N, L.HID, L.F);
+        if ((rc = fc_fwd_partials(s, sf, N, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.parts, L.HID))) return rc;
+    } else {
+        sf = splits_for(N, L.HID, L.F);
+        if ((rc = gemm_f32(s, false, true, N, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.parts, L.HID, 0.f,
+                           nullptr, false, sf, N * L.HID)))
+            return rc;
+    }
+    const dim3 grid((unsigned)((N + kActRowsPerWG - 1) / kActRowsPerWG));
     if (L.A <= 18)
-        hipLaunchKernelGGL(k_cnn_head_act<18>, dim3((unsigned)N), dim3(256), 0, s, w.parts, sf, N * L.HID, params, L,
-                           mode, rng_seed, rng_counter, actions, logp, value, clock);
+        hipLaunchKernelGGL(k_cnn_head_act<18>, grid, dim3(256), 0, s, w.parts, sf, N * L.HID, N, params, L, mode,
+                           rng_seed, rng_counter, actions, logp, value, clock);
     else
-        hipLaunchKernelGGL(k_cnn_head_act<kAMax>, dim3((unsigned)N), dim3(256), 0, s, w.parts, sf, N * L.HID, params,
-                           L, mode, rng_seed, rng_counter, actions, logp, value, clock);
+        hipLaunchKernelGGL(k_cnn_head_act<kAMax>, grid, dim3(256), 0, s, w.parts, sf, N * L.HID, N, params, L, mode,
+                           rng_seed, rng_counter, actions, logp, value, clock);
     GS_LAUNCH_CHECK("k_cnn_head_act");
     return GS_OK;
 }

@@ -31,12 +31,12 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c)
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int C_, int H_, int W_>
+template <int C_, int H_, int W_, int NB_ = 2>
 struct C1 {
-    static constexpr int C = C_, H = H_, W = W_;
+    static constexpr int C = C_, H = H_, W = W_, NB = NB_;
     static constexpr int K = 8, S = 4, CO = 32;
     static constexpr int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
-    static constexpr int BOH = (OH + 1) / 2;              // output rows per band (2 bands per sample)
+    static constexpr int BOH = (OH + NB - 1) / NB;        // output rows per band (NB bands per sample)
     static constexpr int BIR = (BOH - 1) * S + K;         // input rows per band
     static constexpr int BP = BOH * OW;                   // positions per (full) band
     static constexpr int MT = (BP + 15) / 16;             // 16-position MFMA tiles per band
@@ -45,6 +45,14 @@ struct C1 {
     static constexpr int W4 = W / 4;
     static constexpr int FRAME = C * BIR * W;             // floats of the staged band
     static_assert(W % 4 == 0 && C == 4 && KK == 256, "conv1 kernels are written for 4-frame stacks");
+    // band b's input rows [b BOH S, b BOH S + BIR) cover [b H / NB, (b + 1) H / NB): the rows the
+    // rollout's obs copy takes from it
+    static constexpr bool bands_cover()
+    {
+        for (int b = 0; b < NB; ++b)
+            if (b * BOH * S > b * (H / NB) || b * BOH * S + BIR < (b + 1) * (H / NB)) return false;
+        return H % NB == 0;
+    }
 };
 
 __device__ __forceinline__ int64_t frame_src(const int32_t *idx, int64_t r, int64_t T, int64_t N)
@@ -100,10 +108,10 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
                                                    const float *__restrict__ b1, float *__restrict__ out,
                                                    uint8_t *__restrict__ obs_copy)
 {
-    // obs_copy (the rollout's obs row, idx == nullptr): band 0 copies rows [0, H/2), band 1 the rest
-    static_assert(G::BIR >= G::H / 2 && G::BOH * G::S <= G::H / 2, "the two bands cover the halves");
+    // obs_copy (the rollout's obs row, idx == nullptr): band b copies rows [b H / NB, (b + 1) H / NB)
+    static_assert(G::bands_cover(), "the bands cover the obs copy's row ranges");
     __shared__ __attribute__((aligned(16))) float fr[G::FRAME];
-    const int r = blockIdx.x >> 1, band = blockIdx.x & 1;
+    const int r = blockIdx.x / G::NB, band = blockIdx.x - r * G::NB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
     const int oy0 = band * G::BOH;
@@ -120,8 +128,8 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
         b[g] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
     }
     stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S,
-                  obs_copy ? obs_copy + (int64_t)r * (G::C * G::H * G::W) : nullptr, band * (G::H / 2),
-                  band ? G::H : G::H / 2);
+                  obs_copy ? obs_copy + (int64_t)r * (G::C * G::H * G::W) : nullptr, band * (G::H / G::NB),
+                  (band + 1) * (G::H / G::NB));
     __syncthreads();
 
     constexpr int TMW = (G::MT + 1) / 2;
@@ -402,21 +410,34 @@ struct CN {
     static_assert((S * CS) % 64 == 8 && C % 16 == 0, "padding / channel grouping");
 };
 
-template <class G, bool BF = false>
+// FS > 1 (the rollout's small batches, where one workgroup per sample leaves most CUs idle):
+// FS workgroups per sample group, each owning 4 / FS filter blocks of 16, and the waves of a
+// filter block splitting the k-step groups into FS contiguous ranges; the ranges' partial tiles
+// are added in range order through LDS (deterministic), then the bias + ReLU epilogue.
+template <class G, bool BF = false, int FS = 1>
 __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, int R, const float *__restrict__ Wt,
                                                   const float *__restrict__ bias, float *__restrict__ out)
 {
+    static_assert(FS == 1 || FS == 2 || FS == 4, "filter split");
+    constexpr int NFB = 4 / FS;                    // filter blocks per workgroup
+    constexpr int NGW = G::NG / FS;                // k-step groups per wave
+    static_assert(G::NG % FS == 0 && (!BF || NGW % 2 == 0), "k-step groups split evenly (bf16: in pairs)");
+    static_assert(FS == 1 || (FS - 1) * NFB * G::MT * 4 * 64 <= G::SPB * G::H * G::W * G::CS,
+                  "the k-range partials fit the staging tile");
     __shared__ __attribute__((aligned(16))) float xs[G::SPB * G::H * G::W * G::CS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
-    const int r0 = blockIdx.x * G::SPB;
+    const int sg = FS == 1 ? blockIdx.x : blockIdx.x / FS, fpart = FS == 1 ? 0 : blockIdx.x - sg * FS;
+    const int fb = fpart * NFB + wave % NFB, kr = wave / NFB;     // filter block, k-step range
+    const int g0 = kr * NGW;
+    const int r0 = sg * G::SPB;
     const int nsamp = min(G::SPB, R - r0);
 
-    // this wave's 16 filters, all taps: b[g] = W[16 wave + li][16 g + 4 lq .. + 3]
-    float4 b[G::NG];
+    // this wave's 16 filters, its k-step groups: b[g] = W[16 fb + li][16 (g0 + g) + 4 lq .. + 3]
+    float4 b[NGW];
 #pragma unroll
-    for (int g = 0; g < G::NG; ++g)
-        b[g] = *reinterpret_cast<const float4 *>(Wt + (int64_t)(16 * wave + li) * G::KK + 16 * g + 4 * lq);
+    for (int g = 0; g < NGW; ++g)
+        b[g] = *reinterpret_cast<const float4 *>(Wt + (int64_t)(16 * fb + li) * G::KK + 16 * (g0 + g) + 4 * lq);
 
     // stage: [sample][position][channel] with position stride CS, 8 float4 loads in flight
     {
@@ -455,20 +476,19 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
     f32x4 acc[G::MT];
 #pragma unroll
     for (int t = 0; t < G::MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int CG = G::C / 16;
+    auto goff = [&](int g) {       // LDS offset of k-step group g (one tap x 16 channels)
+        const int tap = g / CG, cb = (g - tap * CG) * 16;
+        const int ky = tap / G::K, kx = tap - ky * G::K;
+        return (ky * G::W + kx) * G::CS + cb;
+    };
     if constexpr (BF) {
         // GS_HP_BF16: groups g, g + 1 as one 16x16x32 bf16 MFMA (element j < 4: channel 4q + j of
         // group g, j >= 4: of group g + 1 — the same k order in both operands)
-        static_assert(G::NG % 2 == 0, "bf16: group pairs");
-        constexpr int CG = G::C / 16;
-        auto goff = [&](int g) {
-            const int tap = g / CG, cb = (g - tap * CG) * 16;
-            const int ky = tap / G::K, kx = tap - ky * G::K;
-            return (ky * G::W + kx) * G::CS + cb;
-        };
 #pragma unroll
-        for (int gp = 0; gp < G::NG / 2; ++gp) {
+        for (int gp = 0; gp < NGW / 2; ++gp) {
             const bf16x8 bw = bf16_frag(b[2 * gp], b[2 * gp + 1]);
-            const int o0 = goff(2 * gp), o1 = goff(2 * gp + 1);
+            const int o0 = goff(g0 + 2 * gp), o1 = goff(g0 + 2 * gp + 1);
 #pragma unroll
             for (int t = 0; t < G::MT; ++t) {
                 const bf16x8 a = bf16_frag(*reinterpret_cast<const float4 *>(xs + abase[t] + o0),
@@ -478,11 +498,8 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
         }
     } else
 #pragma unroll
-    for (int g = 0; g < G::NG; ++g) {
-        constexpr int CG = G::C / 16;
-        const int tap = g / CG, cb = (g - tap * CG) * 16;
-        const int ky = tap / G::K, kx = tap - ky * G::K;
-        const int off = (ky * G::W + kx) * G::CS + cb;
+    for (int g = 0; g < NGW; ++g) {
+        const int off = goff(g0 + g);
 #pragma unroll
         for (int t = 0; t < G::MT; t += 2) {
             const float4 a0 = *reinterpret_cast<const float4 *>(xs + abase[t] + off);
@@ -497,8 +514,28 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
             if (t + 1 < G::MT) acc[t + 1] = mfma(a1.w, b[g].w, acc[t + 1]);
         }
     }
-    // epilogue: D row = lq * 4 + j (position), col = li (filter 16 wave + li)
-    const int co = 16 * wave + li;
+    if constexpr (FS > 1) {
+        // the k ranges 1 .. FS-1 of each filter block through LDS (the staging tile is free once
+        // every wave has passed the barrier), added to range 0 in range order
+        __syncthreads();
+        float *red = xs;
+        if (kr > 0)
+#pragma unroll
+            for (int t = 0; t < G::MT; ++t)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    red[((((kr - 1) * NFB + wave % NFB) * G::MT + t) * 4 + j) * 64 + lane] = acc[t][j];
+        __syncthreads();
+        if (kr > 0) return;
+        for (int q = 1; q < FS; ++q)
+#pragma unroll
+            for (int t = 0; t < G::MT; ++t)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[t][j] += red[((((q - 1) * NFB + wave % NFB) * G::MT + t) * 4 + j) * 64 + lane];
+    }
+    // epilogue: D row = lq * 4 + j (position), col = li (filter 16 fb + li)
+    const int co = 16 * fb + li;
     const float bb = bias[co];
     float *o = out + (int64_t)r0 * G::OHW * G::CO;
 #pragma unroll
@@ -817,8 +854,11 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
 
 using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
 using C3_84 = CN<9, 9, 64, 3, 1, 2>;      // conv3: 9x9x64 -> 7x7x64
+using C3_84s = CN<9, 9, 64, 3, 1, 1>;     // conv3, one sample per workgroup (small batches)
+constexpr int kConvFwdSmallWG = 1024;     // FS = 2 up to this many workgroups (R <= 512)
 
 using C1_84 = C1<4, 84, 84>;
+using C1_84q = C1<4, 84, 84, 4>;          // 4 bands per sample (small batches)
 
 }  // namespace
 
@@ -829,12 +869,20 @@ int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, 
 {
     GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
     GS_REQUIRE(!obs_copy || !idx, "conv1_lds_fwd: the obs copy is for the rollout's own rows");
-    if (cnn_bf16())
-        hipLaunchKernelGGL((k_conv1_fwd<C1_84, true>), dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1,
-                           out, obs_copy);
-    else
-        hipLaunchKernelGGL(k_conv1_fwd<C1_84>, dim3((unsigned)(2 * R)), dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
-                           obs_copy);
+    // small batches (the rollout's policy act): 4 bands of 5 output rows per sample, so R = 128
+    // rows launch 512 workgroups; the update's minibatches keep 2 bands (fewer padded tiles)
+    const bool bf = cnn_bf16();
+    if ((int64_t)R * 2 <= kConvFwdSmallWG) {
+        const dim3 grid((unsigned)(C1_84q::NB * R));
+        if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84q, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
+                                   obs_copy);
+        else hipLaunchKernelGGL((k_conv1_fwd<C1_84q>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out, obs_copy);
+    } else {
+        const dim3 grid((unsigned)(C1_84::NB * R));
+        if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
+                                   obs_copy);
+        else hipLaunchKernelGGL((k_conv1_fwd<C1_84>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out, obs_copy);
+    }
     GS_LAUNCH_CHECK("k_conv1_fwd");
     return GS_OK;
 }
@@ -871,21 +919,30 @@ bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cou
     return H == 9 && W == 9 && C == 64 && k == 3 && st == 1 && Cout == 64;
 }
 
+// small batches (the rollout's policy act): one sample per workgroup group and FS = 2 filter
+// splits, so R = 128 rows still launch 256 workgroups; the update's minibatches keep FS = 1
+template <class G, class G1>
+int launch_conv_fwd(hipStream_t s, int R, const float *in, const float *Wt, const float *bias, float *out, bool bf)
+{
+    if ((int64_t)R * 2 <= kConvFwdSmallWG) {
+        const dim3 grid((unsigned)(2 * R));
+        if (bf) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        else hipLaunchKernelGGL((k_conv_fwd<G1, false, 2>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+    } else {
+        const dim3 grid((unsigned)((R + G::SPB - 1) / G::SPB));
+        if (bf) hipLaunchKernelGGL((k_conv_fwd<G, true>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        else hipLaunchKernelGGL((k_conv_fwd<G>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+    }
+    GS_LAUNCH_CHECK("k_conv_fwd");
+    return GS_OK;
+}
+
 int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float *Wt, const float *bias, float *out)
 {
     GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
     const bool bf = cnn_bf16();
-    if (layer == 2) {
-        const dim3 grid((unsigned)((R + C2_84::SPB - 1) / C2_84::SPB));
-        if (bf) hipLaunchKernelGGL((k_conv_fwd<C2_84, true>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
-        else hipLaunchKernelGGL(k_conv_fwd<C2_84>, grid, dim3(256), 0, s, in, R, Wt, bias, out);
-    } else {
-        const dim3 grid((unsigned)((R + C3_84::SPB - 1) / C3_84::SPB));
-        if (bf) hipLaunchKernelGGL((k_conv_fwd<C3_84, true>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
-        else hipLaunchKernelGGL(k_conv_fwd<C3_84>, grid, dim3(256), 0, s, in, R, Wt, bias, out);
-    }
-    GS_LAUNCH_CHECK("k_conv_fwd");
-    return GS_OK;
+    if (layer == 2) return launch_conv_fwd<C2_84, C2_84>(s, R, in, Wt, bias, out, bf);
+    return launch_conv_fwd<C3_84, C3_84s>(s, R, in, Wt, bias, out, bf);
 }
 
 int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX)

@@ -21,6 +21,8 @@
 // next tile's global loads in flight during the current tile's MFMAs, one barrier per tile.
 // Tile shapes are chosen so each launch fills the chip without split-K: fwd 32 x 64 (256
 // workgroups, KS = 2), wgrad / dgrad 64 x 64 (392 / 784 workgroups, two resident per CU).
+#include <type_traits>
+
 #include "gs_gemm.h"
 
 namespace gs {
@@ -31,6 +33,26 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 enum FcEpi { kEpiStore = 0, kEpiBiasRelu = 1, kEpiMask = 2 };
 
 constexpr int kRowBytes = 144;          // one staged K tile row: 128 B of data + 16 B pad
+
+// register prefetch depth (K tiles in flight) per launch shape and operand precision
+#ifndef FC_PD_FWD32
+#define FC_PD_FWD32 4
+#endif
+#ifndef FC_PD_FWD16
+#define FC_PD_FWD16 3
+#endif
+#ifndef FC_PD_WG32
+#define FC_PD_WG32 3
+#endif
+#ifndef FC_PD_WG16
+#define FC_PD_WG16 2
+#endif
+#ifndef FC_PD_DG32
+#define FC_PD_DG32 3
+#endif
+#ifndef FC_PD_DG16
+#define FC_PD_DG16 2
+#endif
 
 template <bool BF>
 struct FcK {
@@ -112,18 +134,33 @@ struct Stage {
     }
 };
 
-template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI>
+// f(integral_constant<I>) for I = B .. E-1 in order while it returns true (compile-time indices)
+template <int I, int E, class F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    if constexpr (I < E) {
+        if (f(std::integral_constant<int, I>{})) static_for<I + 1, E>(f);
+    }
+}
+
+template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, int PD>
 __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int64_t lda, const float *__restrict__ Bm,
                                                int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
-                                               const float *__restrict__ aux, const int32_t *__restrict__ stop)
+                                               const float *__restrict__ aux, const int32_t *__restrict__ stop,
+                                               int64_t sC)
 {
     if (stop && *stop) return;      // KL early stop: the minibatch's product is never used
+    // split-K (gridDim.z slices of K each, partial products at C + z sC; no epilogue)
+    A += (AK ? 1 : lda) * (int64_t)blockIdx.z * K;
+    Bm += (BKC ? 1 : ldb) * (int64_t)blockIdx.z * K;
+    C += (int64_t)blockIdx.z * sC;
     constexpr int WGN = 4 / (WGM * KS);
     static_assert(WGM * WGN * KS == 4, "4 waves");
     constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
     static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "32 x 32 sub-tiles");
     constexpr int KE = FcK<BF>::KE, NG = FcK<BF>::NG;
     static_assert(NG % KS == 0, "k-groups split evenly over KS");
+    static_assert(PD >= 1, "register prefetch depth");
     constexpr int TILE = (BM + BN) * kRowBytes;
     __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
 
@@ -133,8 +170,10 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
     const int wm = (wmn / WGN) * WM, wn = (wmn % WGN) * WN;
     const int l32 = lane & 31, lh = lane >> 5;
 
-    Stage<BM, BF, AK> sa;
-    Stage<BN, BF, BKC> sb;
+    // PD register sets: tile j is loaded into set j % PD, PD tiles before its LDS store, so a tile's
+    // global latency hides under PD tiles of MFMAs (one tile alone is too short to cover it)
+    Stage<BM, BF, AK> sa[PD];
+    Stage<BN, BF, BKC> sb[PD];
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -144,54 +183,70 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
     const int nk = K / KE;
-    sa.load(A, lda, m0, M, 0);
-    sb.load(Bm, ldb, n0, N, 0);
-    sa.store(lds, m0, M);
-    sb.store(lds + BM * kRowBytes, n0, N);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const char *buf = lds + (kt & 1) * TILE;
-        if (kt + 1 < nk) {          // the next tile's loads in flight during this tile's MFMAs
-            sa.load(A, lda, m0, M, (kt + 1) * KE);
-            sb.load(Bm, ldb, n0, N, (kt + 1) * KE);
+#pragma unroll
+    for (int u = 0; u < PD; ++u)
+        if (u < nk) {
+            sa[u].load(A, lda, m0, M, u * KE);
+            sb[u].load(Bm, ldb, n0, N, u * KE);
         }
+    sa[0].store(lds, m0, M);
+    sb[0].store(lds + BM * kRowBytes, n0, N);
+    __syncthreads();
+    if (PD < nk) {
+        sa[0].load(A, lda, m0, M, PD * KE);
+        sb[0].load(Bm, ldb, n0, N, PD * KE);
+    }
+    for (int kt0 = 0; kt0 < nk; kt0 += PD) {
+        static_for<0, PD>([&](auto uc) -> bool {
+            constexpr int u = decltype(uc)::value;
+            const int kt = kt0 + u;
+            if (kt >= nk) return false;
+            const char *buf = lds + (kt & 1) * TILE;
 #pragma unroll
-        for (int g = ks; g < NG; g += KS) {
-            // lane (l32, lh): 16 B of its row at k-group g, half lh
-            float4 a[TM], b[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-                a[i] = *reinterpret_cast<const float4 *>(buf + (wm + 32 * i + l32) * kRowBytes + 32 * g + 16 * lh);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                b[j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 32 * j + l32) * kRowBytes + 32 * g + 16 * lh);
-            if constexpr (BF) {
+            for (int g = ks; g < NG; g += KS) {
+                // lane (l32, lh): 16 B of its row at k-group g, half lh
+                float4 a[TM], b[TN];
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
+                    a[i] = *reinterpret_cast<const float4 *>(buf + (wm + 32 * i + l32) * kRowBytes + 32 * g + 16 * lh);
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8 *>(&a[i]),
-                                                                            *reinterpret_cast<const bf16x8 *>(&b[j]),
-                                                                            acc[i][j], 0, 0, 0);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
+                for (int j = 0; j < TN; ++j)
+                    b[j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 32 * j + l32) * kRowBytes + 32 * g +
+                                                             16 * lh);
+                if constexpr (BF) {
 #pragma unroll
                     for (int i = 0; i < TM; ++i)
 #pragma unroll
-                        for (int j = 0; j < TN; ++j) {
-                            const float av = e == 0 ? a[i].x : e == 1 ? a[i].y : e == 2 ? a[i].z : a[i].w;
-                            const float bv = e == 0 ? b[j].x : e == 1 ? b[j].y : e == 2 ? b[j].z : b[j].w;
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-                        }
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                *reinterpret_cast<const bf16x8 *>(&a[i]), *reinterpret_cast<const bf16x8 *>(&b[j]),
+                                acc[i][j], 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int i = 0; i < TM; ++i)
+#pragma unroll
+                            for (int j = 0; j < TN; ++j) {
+                                const float av = e == 0 ? a[i].x : e == 1 ? a[i].y : e == 2 ? a[i].z : a[i].w;
+                                const float bv = e == 0 ? b[j].x : e == 1 ? b[j].y : e == 2 ? b[j].z : b[j].w;
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+                            }
+                }
             }
-        }
-        if (kt + 1 < nk) {
-            char *nb = lds + ((kt + 1) & 1) * TILE;
-            sa.store(nb, m0, M);
-            sb.store(nb + BM * kRowBytes, n0, N);
-        }
-        __syncthreads();
+            constexpr int nv = (u + 1) % PD;     // the set holding tile kt + 1
+            if (kt + 1 < nk) {
+                char *nb = lds + ((kt + 1) & 1) * TILE;
+                sa[nv].store(nb, m0, M);
+                sb[nv].store(nb + BM * kRowBytes, n0, N);
+            }
+            __syncthreads();
+            if (kt + 1 + PD < nk) {
+                sa[nv].load(A, lda, m0, M, (kt + 1 + PD) * KE);
+                sb[nv].load(Bm, ldb, n0, N, (kt + 1 + PD) * KE);
+            }
+            return true;
+        });
     }
     if constexpr (KS > 1) {
         // the KS k-group partials of each wave tile, added in ks order (LDS is free after the loop)
@@ -240,17 +295,18 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
         }
 }
 
-template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI>
+template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16>
 int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
-              int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop)
+              int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop, int splits = 1, int64_t sC = 0)
 {
-    const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM));
+    const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
+    K /= splits;
     if (bf)
-        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
-                           (int)M, (int)N, (int)K, aux, stop);
+        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
+                           (int)M, (int)N, (int)K, aux, stop, sC);
     else
-        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
-                           (int)M, (int)N, (int)K, aux, stop);
+        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
+                           (int)M, (int)N, (int)K, aux, stop, sC);
     GS_LAUNCH_CHECK("k_fc");
     return GS_OK;
 }
@@ -269,6 +325,28 @@ bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
     return true;
 }
 
+int fc_fwd_splits(int64_t M, int64_t N, int64_t K)
+{
+    // the largest split of K into 64-multiples that keeps the 32 x 64 tiles x splits within 512
+    // workgroups (at most 16 slices)
+    const int64_t tiles = ((M + 31) / 32) * ((N + 63) / 64);
+    int best = 1;
+    for (int sp = 2; sp <= 16; ++sp)
+        if (K % (64 * sp) == 0 && tiles * sp <= 512) best = sp;
+    return best;
+}
+
+int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+                    const float *B, int64_t ldb, float *C, int64_t ldc)
+{
+    GS_REQUIRE(splits >= 1 && K % (64 * splits) == 0 && fc_supported(0, M, N, K / splits, lda, ldb, ldc),
+               "fc_fwd_partials: shape %lld x %lld x %lld / %d not supported", (long long)M, (long long)N,
+               (long long)K, splits);
+    GS_REQUIRE(aligned16(A) && aligned16(B), "fc_fwd_partials: 16-B aligned operands required");
+    return launch_fc<32, 64, 1, 2, true, true, kEpiStore, FC_PD_FWD32, FC_PD_FWD16>(
+        s, false, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, splits, M * ldc);
+}
+
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
             const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop)
 {
@@ -278,11 +356,11 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
     GS_REQUIRE(aligned16(A) && aligned16(B) && (op == 1 || aux), "fc_gemm: 16-B aligned operands (and the epilogue "
                "operand) required");
     if (op == 0)     // fwd: C = relu(A B^T + bias), both K-contiguous
-        return launch_fc<32, 64, 1, 2, true, true, kEpiBiasRelu>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
+        return launch_fc<32, 64, 1, 2, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
     if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]
-        return launch_fc<64, 64, 2, 1, false, false, kEpiStore>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr, stop);
+        return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr, stop);
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
-    return launch_fc<64, 64, 2, 1, true, false, kEpiMask>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
+    return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
 }
 
 }  // namespace gs

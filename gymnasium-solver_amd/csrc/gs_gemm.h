@@ -43,6 +43,12 @@ int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, c
 bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
             const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop = nullptr);
+// the fc forward product as split-K fp32 partials (no epilogue) for small row counts (the
+// rollout): C + z M ldc = A[:, z K/splits ..] B[:, z K/splits ..]^T for z < splits;
+// fc_fwd_splits picks the split (1 when the plain tiles already fill the chip)
+int fc_fwd_splits(int64_t M, int64_t N, int64_t K);
+int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+                    const float *B, int64_t ldb, float *C, int64_t ldc);
 
 
 // out[r,oy,ox,co] = relu(bias[co] + sum_{c,ky,kx} W[co][c][ky][kx] * frame[c][oy*s+ky][ox*s+kx] / 255)
