@@ -33,6 +33,15 @@ namespace gs {
 
 namespace {
 
+#ifdef GS_STAMPS
+// this file's own stamp slots (device globals do not link across translation units): the stamp
+// macros' names are mapped onto them
+#define g_stamp_acc g_cnn_stamp_acc
+#define g_stamp_cnt g_cnn_stamp_cnt
+__device__ unsigned long long g_cnn_stamp_acc[8][16];
+__device__ unsigned long long g_cnn_stamp_cnt[8];
+#endif
+
 constexpr int kAMax = 32;
 
 struct CnnLayout {
@@ -370,12 +379,14 @@ __device__ __forceinline__ void act_select(const float (&zr)[AM + 1], float v, i
     logp[r] = za - h.lse;
 }
 
-// ---- the rollout's fc epilogue + heads + action select in one launch, one wave per env (4 per
-// workgroup, no barrier): lane l takes j = l, l + 64, ... of the row: h[j] = relu(bf[j] + the
-// fc's split-K partials summed in slice order) and its share of z = h [Wp; Wv]^T; the lanes'
-// shares are added by a fixed xor butterfly; lane 0 adds the biases and selects the action.
-// Replaces the heads GEMM, its split-K sum, the fc sum and a per-env act kernel.
-constexpr int kActRowsPerWG = 4;
+// ---- the rollout's fc epilogue + heads + action select in one launch, one workgroup per env:
+// thread t takes j = t, t + 256 (HID <= 512): h[j] = relu(bf[j] + the fc's split-K partials
+// summed in slice order) and its products with the A + 1 head rows — every load of a thread is
+// issued before the first is used (one memory latency); the per-thread products are added in a
+// fixed tree through LDS (32 consecutive threads, then the 8 groups in order); thread 0 adds the
+// biases and selects the action.  Replaces the heads GEMM, its split-K sum, the fc sum and a
+// per-env act kernel.
+constexpr int kActMaxSplits = 16, kActMaxHid = 512;
 
 template <int AM>
 __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ parts, int np, int64_t pstride,
@@ -384,35 +395,63 @@ __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ 
                                                       float *__restrict__ logp, float *__restrict__ value,
                                                       const uint64_t *__restrict__ clock)
 {
-    const int lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * kActRowsPerWG + (threadIdx.x >> 6);
-    if (r >= R) return;                               // wave-uniform
-    const int HID = L.HID, A = L.A;
+    constexpr int NJ = kActMaxHid / 256;
+    __shared__ __attribute__((aligned(16))) float red[(AM + 1) * 256];
+    __shared__ __attribute__((aligned(16))) float red2[(AM + 1) * 8];
+    const int64_t r = blockIdx.x;
+    const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
+    float t[NJ][kActMaxSplits], bfv[NJ], w[NJ][AM + 1];
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) {
+        const int j = min(tid + 256 * u, HID - 1);
+#pragma unroll
+        for (int p = 0; p < kActMaxSplits; ++p) t[u][p] = p < np ? parts[(int64_t)p * pstride + r * HID + j] : 0.f;
+        bfv[u] = P[L.obf + j];
+#pragma unroll
+        for (int a = 0; a < AM + 1; ++a)
+            w[u][a] = a < A ? P[L.oWp + (int64_t)a * HID + j] : a == A ? P[L.oWv + j] : 0.f;
+    }
     float acc[AM + 1];
 #pragma unroll
     for (int a = 0; a < AM + 1; ++a) acc[a] = 0.f;
-    for (int j = lane; j < HID; j += 64) {
-        const int64_t i = r * HID + j;
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) {
+        if (tid + 256 * u >= HID) break;
         float hv = 0.f;
-        for (int p = 0; p < np; ++p) hv += parts[(int64_t)p * pstride + i];
-        hv += P[L.obf + j];
+#pragma unroll
+        for (int p = 0; p < kActMaxSplits; ++p)
+            if (p < np) hv += t[u][p];
+        hv += bfv[u];
         hv = hv > 0.f ? hv : 0.f;
 #pragma unroll
-        for (int a = 0; a < AM + 1; ++a) {
-            if (a < A) acc[a] = fmaf(hv, P[L.oWp + (int64_t)a * HID + j], acc[a]);
-            else if (a == A) acc[a] = fmaf(hv, P[L.oWv + j], acc[a]);
-        }
+        for (int a = 0; a < AM + 1; ++a) acc[a] = fmaf(hv, w[u][a], acc[a]);
     }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1)
+    for (int a = 0; a < AM + 1; ++a) red[a * 256 + tid] = acc[a];
+    __syncthreads();
+    if (tid < A1 * 8) {
+        const int a = tid >> 3, q = tid & 7;
+        const float4 *src = reinterpret_cast<const float4 *>(red + a * 256 + q * 32);
+        float4 v[8];
 #pragma unroll
-        for (int a = 0; a < AM + 1; ++a) acc[a] += __shfl_xor(acc[a], off);
-    if (lane == 0) {
+        for (int m = 0; m < 8; ++m) v[m] = src[m];
+        float g = 0.f;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) g = (((g + v[m].x) + v[m].y) + v[m].z) + v[m].w;
+        red2[tid] = g;
+    }
+    __syncthreads();
+    if (tid == 0) {
         float zr[AM + 1];
         float v = 0.f;
 #pragma unroll
         for (int a = 0; a < AM + 1; ++a) {
-            zr[a] = a <= A ? acc[a] + (a < A ? P[L.obp + a] : P[L.obv]) : 0.f;
+            float z = 0.f;
+            if (a < A1) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) z += red2[a * 8 + q];
+            }
+            zr[a] = a < A1 ? z + (a < A ? P[L.obp + a] : P[L.obv]) : 0.f;
             if (a == A) v = zr[a];
         }
         act_select<AM>(zr, v, r, L, mode, seed, counter, actions, logp, value, clock);
@@ -745,6 +784,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     __shared__ double sred[kSums * 256 + kSums * 16];
     extern __shared__ float lds[];
     if (stop && *stop) return;
+    GS_STAMP_BEGIN(0)
     const int tid = threadIdx.x, A = L.A, A1 = A + 1, HID = L.HID, HS = HID + kHeadSlices, ZS = head_zs(A1);
     const int r0 = blockIdx.x * kHeadRows;
     float *hs = lds;                                  // [kHeadRows][HS] (kHeadSlices banks between rows)
@@ -815,6 +855,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
             }
         }
     }
+    GS_STAMP(0)
     float meanf = 0.f, stdf = 1.f;
     if (la.normalize && gmode) {     // the global minibatch's statistics (gs_ppo_global_adv_stats)
         meanf = la.adv_stats[0];
@@ -825,6 +866,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     } else {
         __syncthreads();
     }
+    GS_STAMP(1)
     {   // z partials: thread (row r, slice q) over k = q, q + kHeadSlices, ...
         const int r = tid / kHeadSlices, q = tid % kHeadSlices;
         float acc[4 * NZ];
@@ -849,6 +891,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
                     make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
     }
     __syncthreads();
+    GS_STAMP(2)
     for (int o = tid; o < kHeadRows * A1; o += 256) {
         const int r = o / A1, a = o - r * A1;
         float z = 0.f;
@@ -856,6 +899,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         zs[r * ZS + a] = z + (a < A ? P[L.obp + a] : P[L.obv]);
     }
     __syncthreads();
+    GS_STAMP(3)
     double acc[kSums];
 #pragma unroll
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
@@ -878,7 +922,9 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         if (r0 + tid < B)     // another rank's row (global mode): no gradient
             for (int a = 0; a < A1; ++a) dz[(int64_t)(r0 + tid) * A1 + a] = 0.f;
     }
+    GS_STAMP(4)
     wg_reduce<kSums>(acc, sred);      // its barriers publish zs (now dz) too
+    GS_STAMP(5)
     if (tid == 0)
         for (int q = 0; q < kSums; ++q) part[(int64_t)blockIdx.x * kSums + q] = acc[q];
     float *wp = wpart + (int64_t)blockIdx.x * head_part_stride(L);
@@ -929,11 +975,13 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
             if (a < A1) wp[a * (HID + 1) + j] = g[a];
         wp[(int64_t)A1 * (HID + 1) + j] = dbf;
     }
+    GS_STAMP(6)
     if (tid < A1) {     // the bias column: sum of the (unrounded) dz rows
         float sb = 0.f;
         for (int r = 0; r < kHeadRows; ++r) sb += zs[r * ZS + tid];
         wp[tid * (HID + 1) + HID] = sb;
     }
+    GS_STAMP_END(7)
 }
 
 // [dWh | dbh] = the k_cnn_head_loss partials summed in workgroup order (64 outputs per workgroup,
@@ -1496,6 +1544,15 @@ extern "C" size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows)
     return carve(nullptr, CnnLayout::make(dims), rows).bytes;
 }
 
+#ifdef GS_STAMPS
+extern "C" int gs_debug_cnn_stamps(unsigned long long *acc_out, unsigned long long *cnt_out)
+{
+    GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(g_cnn_stamp_acc), sizeof(unsigned long long) * 128));
+    GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(g_cnn_stamp_cnt), sizeof(unsigned long long) * 8));
+    return GS_OK;
+}
+#endif
+
 extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const uint8_t *obs, int64_t N, int mode,
                                  uint64_t rng_seed, uint64_t rng_counter, int64_t *actions, float *logp, float *value,
                                  uint8_t *obs_store, void *workspace, const uint64_t *clock, void *stream)
@@ -1522,7 +1579,9 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
                            nullptr, false, sf, N * L.HID)))
             return rc;
     }
-    const dim3 grid((unsigned)((N + kActRowsPerWG - 1) / kActRowsPerWG));
+    GS_REQUIRE(sf <= kActMaxSplits && L.HID <= kActMaxHid, "gs_cnn_policy_act: fc splits %d / hidden %d exceed "
+               "the act kernel's %d / %d", sf, L.HID, kActMaxSplits, kActMaxHid);
+    const dim3 grid((unsigned)N);
     if (L.A <= 18)
         hipLaunchKernelGGL(k_cnn_head_act<18>, grid, dim3(256), 0, s, w.parts, sf, N * L.HID, N, params, L, mode,
                            rng_seed, rng_counter, actions, logp, value, clock);

@@ -856,6 +856,7 @@ using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
 using C3_84 = CN<9, 9, 64, 3, 1, 2>;      // conv3: 9x9x64 -> 7x7x64
 using C3_84s = CN<9, 9, 64, 3, 1, 1>;     // conv3, one sample per workgroup (small batches)
 constexpr int kConvFwdSmallWG = 1024;     // FS = 2 up to this many workgroups (R <= 512)
+constexpr int kConv1Bands4Below = 256;    // conv1 in 4 bands below this many 2-band workgroups
 
 using C1_84 = C1<4, 84, 84>;
 using C1_84q = C1<4, 84, 84, 4>;          // 4 bands per sample (small batches)
@@ -869,10 +870,11 @@ int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, 
 {
     GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
     GS_REQUIRE(!obs_copy || !idx, "conv1_lds_fwd: the obs copy is for the rollout's own rows");
-    // small batches (the rollout's policy act): 4 bands of 5 output rows per sample, so R = 128
-    // rows launch 512 workgroups; the update's minibatches keep 2 bands (fewer padded tiles)
+    // very small batches: 4 bands of 5 output rows per sample, so R < 128 rows still launch at
+    // least 256 workgroups; otherwise 2 bands (fewer padded tiles: at R = 128 the 2-band form
+    // already fills the chip and ran 16.7 us vs 21.6 us for 4 bands)
     const bool bf = cnn_bf16();
-    if ((int64_t)R * 2 <= kConvFwdSmallWG) {
+    if ((int64_t)R * 2 < kConv1Bands4Below) {
         const dim3 grid((unsigned)(C1_84q::NB * R));
         if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84q, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
                                    obs_copy);

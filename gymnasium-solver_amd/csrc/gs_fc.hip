@@ -5,9 +5,9 @@
 //   wgrad dWf[HID][F] = dh[B][HID]^T . a3[B][F]                  both operands K-strided (K = B)
 //   dgrad da3[B][F]   = (dh[B][HID] . Wf[HID][F]) * (a3 > 0)     A K-contiguous, B K-strided
 //
-// k_fc<BM, BN, WGM, KS, BF, AK, BKC, EPI>: 256 threads = 4 waves arranged WGM x WGN x KS; a wave
-// owns (BM/WGM) x (BN/WGN) of the output as 32 x 32 MFMA sub-tiles and, with KS > 1, every KS-th
-// k-group of each K tile (the KS partial tiles are added in ks order through LDS at the end:
+// k_fc<BM, BN, WGM, KS, BF, AK, BKC, EPI, PD, KT>: 256 threads = 4 waves arranged WGM x WGN x KS;
+// a wave owns (BM/WGM) x (BN/WGN) of the output as 32 x 32 MFMA sub-tiles and, with KS > 1, every
+// KS-th k-group of each K tile (the KS partial tiles are added in ks order through LDS at the end:
 // deterministic).  Both operands are staged global -> registers -> LDS as [row][k] with k
 // contiguous (a K-strided source is transposed in registers from 4 x 4 blocks on the way), so an
 // MFMA operand is one ds_read_b128 per lane:
@@ -16,11 +16,10 @@
 //        same k in both operands;
 //   bf16 (GS_HP_BF16, v_mfma_f32_32x32x16_bf16): the tile is converted to bf16 (round to nearest
 //        even) as it is staged; lane (r, q) reads 8 bf16 at k0 + 8q: one MFMA per 16-k group.
-// A K tile is 128 B of every row (32 fp32 / 64 bf16) plus a 16-B pad (row stride 144 B: the 16
-// rows a ds_read_b128 lane group reads start 36 dwords apart -> distinct banks), two buffers, the
-// next tile's global loads in flight during the current tile's MFMAs, one barrier per tile.
-// Tile shapes are chosen so each launch fills the chip without split-K: fwd 32 x 64 (256
-// workgroups, KS = 2), wgrad / dgrad 64 x 64 (392 / 784 workgroups, two resident per CU).
+// A K tile is KT x 128 B of every row plus a 16-B pad, two LDS buffers, PD register sets of
+// tiles in flight, one barrier per tile.  Launch shapes: fwd 64 x 32 with the 4 waves splitting
+// the k-groups (KS = 4: 256 workgroups, each wave two 32 x 32 accumulators), wgrad / dgrad
+// 64 x 64 (392 / 784 workgroups, two resident per CU); fp32 tiles are 64 deep (KT = 2).
 #include <type_traits>
 
 #include "gs_gemm.h"
@@ -32,34 +31,36 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum FcEpi { kEpiStore = 0, kEpiBiasRelu = 1, kEpiMask = 2 };
 
-constexpr int kRowBytes = 144;          // one staged K tile row: 128 B of data + 16 B pad
+// One K tile holds KT 128-B chunks of every staged row (32 KT fp32 or 64 KT bf16 elements) plus a
+// 16-B pad: a row stride of 4 (mod 64) dwords puts the 16 rows a ds_read_b128 lane group reads on
+// distinct banks.
+template <bool BF, int KT>
+struct FcK {
+    static constexpr int KE = (BF ? 64 : 32) * KT;   // K elements per tile
+    static constexpr int GK = BF ? 16 : 8;           // K elements per k-group (one ds_read_b128 per lane)
+    static constexpr int NG = KE / GK;               // k-groups per tile (4 KT)
+    static constexpr int RB = 128 * KT + 16;         // LDS bytes per staged row
+};
 
 // register prefetch depth (K tiles in flight) per launch shape and operand precision
 #ifndef FC_PD_FWD32
-#define FC_PD_FWD32 4
+#define FC_PD_FWD32 3
 #endif
 #ifndef FC_PD_FWD16
-#define FC_PD_FWD16 3
+#define FC_PD_FWD16 2
 #endif
 #ifndef FC_PD_WG32
-#define FC_PD_WG32 3
+#define FC_PD_WG32 2
 #endif
 #ifndef FC_PD_WG16
 #define FC_PD_WG16 2
 #endif
 #ifndef FC_PD_DG32
-#define FC_PD_DG32 3
+#define FC_PD_DG32 2
 #endif
 #ifndef FC_PD_DG16
 #define FC_PD_DG16 2
 #endif
-
-template <bool BF>
-struct FcK {
-    static constexpr int KE = BF ? 64 : 32;     // K elements per tile
-    static constexpr int GK = BF ? 16 : 8;      // K elements per k-group (one ds_read_b128 per lane)
-    static constexpr int NG = KE / GK;          // k-groups per tile (4)
-};
 
 // 4 fp32 -> 4 bf16 (8 bytes)
 __device__ __forceinline__ uint2 pack_bf16x4(float4 v)
@@ -70,15 +71,22 @@ __device__ __forceinline__ uint2 pack_bf16x4(float4 v)
     return *reinterpret_cast<uint2 *>(&r);
 }
 
+__device__ __forceinline__ float f4at(const float4 &v, int c)
+{
+    return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+
 // staging of one operand's K tile: ROWS rows (m or n) x KE k.  KC: source element (row, k) at
-// p[row * ld + k] (K-contiguous), else at p[k * ld + row].  Rows past n_rows load clamped and are
-// zeroed at the store.
-template <int ROWS, bool BF, bool KC>
+// p[row * ld + k] (K-contiguous), else at p[k * ld + row].  Every thread moves the same number of
+// units (no divergent branches, so the waitcnt counts stay exact); rows past n_rows load clamped
+// and are zeroed at the store.
+template <int ROWS, bool BF, bool KC, int KT>
 struct Stage {
-    static constexpr int KE = FcK<BF>::KE;
+    static constexpr int KE = FcK<BF, KT>::KE, RB = FcK<BF, KT>::RB;
     // K-contiguous: one float4 (4 k of one row) per unit; K-strided: a 4 x 4 block per unit
     static constexpr int UNITS = KC ? ROWS * KE / 4 : ROWS * KE / 16;
-    static constexpr int PER = (UNITS + 255) / 256;
+    static constexpr int PER = UNITS / 256;
+    static_assert(UNITS % 256 == 0, "whole units per thread");
     static constexpr int NV = KC ? 1 : 4;
     float4 r[PER][NV];
 
@@ -86,7 +94,7 @@ struct Stage {
     {
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const int u = min((int)threadIdx.x + 256 * j, UNITS - 1);
+            const int u = (int)threadIdx.x + 256 * j;
             if constexpr (KC) {
                 const int row = u / (KE / 4), k4 = u - row * (KE / 4);
                 const int gr = min(row0 + row, n_rows - 1);
@@ -106,12 +114,11 @@ struct Stage {
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int u = (int)threadIdx.x + 256 * j;
-            if (u >= UNITS) continue;
             if constexpr (KC) {
                 const int row = u / (KE / 4), k4 = u - row * (KE / 4);
                 const bool ok = row0 + row < n_rows;
                 const float4 v = ok ? r[j][0] : make_float4(0.f, 0.f, 0.f, 0.f);
-                char *dst = lds + row * kRowBytes;
+                char *dst = lds + row * RB;
                 if constexpr (BF) *reinterpret_cast<uint2 *>(dst + 8 * k4) = pack_bf16x4(v);
                 else *reinterpret_cast<float4 *>(dst + 16 * k4) = v;
             } else {
@@ -120,12 +127,10 @@ struct Stage {
                 // r[j][v] = rows 4 rb .. 4 rb + 3 at k = 4 kb + v: column c is row 4 rb + c's 4 k
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const float4 v = ok ? make_float4(c == 0 ? r[j][0].x : c == 1 ? r[j][0].y : c == 2 ? r[j][0].z : r[j][0].w,
-                                                      c == 0 ? r[j][1].x : c == 1 ? r[j][1].y : c == 2 ? r[j][1].z : r[j][1].w,
-                                                      c == 0 ? r[j][2].x : c == 1 ? r[j][2].y : c == 2 ? r[j][2].z : r[j][2].w,
-                                                      c == 0 ? r[j][3].x : c == 1 ? r[j][3].y : c == 2 ? r[j][3].z : r[j][3].w)
+                    const float4 v = ok ? make_float4(f4at(r[j][0], c), f4at(r[j][1], c), f4at(r[j][2], c),
+                                                      f4at(r[j][3], c))
                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-                    char *dst = lds + (4 * rb + c) * kRowBytes;
+                    char *dst = lds + (4 * rb + c) * RB;
                     if constexpr (BF) *reinterpret_cast<uint2 *>(dst + 8 * kb) = pack_bf16x4(v);
                     else *reinterpret_cast<float4 *>(dst + 16 * kb) = v;
                 }
@@ -143,7 +148,14 @@ __device__ __forceinline__ void static_for(F &&f)
     }
 }
 
-template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, int PD>
+// k_fc: 256 threads = 4 waves arranged WGM x WGN x KS; a wave owns (BM/WGM) x (BN/WGN) outputs as
+// 32 x 32 sub-tiles and, with KS > 1, every KS-th k-group of each tile (the KS partial tiles are
+// added in ks order through LDS at the end: deterministic).  Per tile a wave first issues every
+// LDS operand read of its k-groups, then the MFMAs; the next tile's registers go to the other LDS
+// buffer; one barrier per tile; tile kt + 1 + PD is loaded right after (tile j lives in register
+// set j % PD, so its global latency hides under PD tiles of MFMAs).  Loads and stores are
+// unconditional (the last tiles re-load a clamped tile) so the compiler's wait counts stay exact.
+template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, int PD, int KT>
 __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int64_t lda, const float *__restrict__ Bm,
                                                int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
                                                const float *__restrict__ aux, const int32_t *__restrict__ stop,
@@ -158,10 +170,11 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
     static_assert(WGM * WGN * KS == 4, "4 waves");
     constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
     static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "32 x 32 sub-tiles");
-    constexpr int KE = FcK<BF>::KE, NG = FcK<BF>::NG;
+    using K_ = FcK<BF, KT>;
+    constexpr int KE = K_::KE, NG = K_::NG, RB = K_::RB, NGW = NG / KS;
     static_assert(NG % KS == 0, "k-groups split evenly over KS");
     static_assert(PD >= 1, "register prefetch depth");
-    constexpr int TILE = (BM + BN) * kRowBytes;
+    constexpr int TILE = (BM + BN) * RB;
     __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
 
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
@@ -170,10 +183,8 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
     const int wm = (wmn / WGN) * WM, wn = (wmn % WGN) * WN;
     const int l32 = lane & 31, lh = lane >> 5;
 
-    // PD register sets: tile j is loaded into set j % PD, PD tiles before its LDS store, so a tile's
-    // global latency hides under PD tiles of MFMAs (one tile alone is too short to cover it)
-    Stage<BM, BF, AK> sa[PD];
-    Stage<BN, BF, BKC> sb[PD];
+    Stage<BM, BF, AK, KT> sa[PD];
+    Stage<BN, BF, BKC, KT> sb[PD];
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -183,43 +194,44 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
     const int nk = K / KE;
+    auto kof = [&](int t) { return min(t, nk - 1) * KE; };
 #pragma unroll
-    for (int u = 0; u < PD; ++u)
-        if (u < nk) {
-            sa[u].load(A, lda, m0, M, u * KE);
-            sb[u].load(Bm, ldb, n0, N, u * KE);
-        }
-    sa[0].store(lds, m0, M);
-    sb[0].store(lds + BM * kRowBytes, n0, N);
-    __syncthreads();
-    if (PD < nk) {
-        sa[0].load(A, lda, m0, M, PD * KE);
-        sb[0].load(Bm, ldb, n0, N, PD * KE);
+    for (int u = 0; u < PD; ++u) {
+        sa[u].load(A, lda, m0, M, kof(u));
+        sb[u].load(Bm, ldb, n0, N, kof(u));
     }
+    sa[0].store(lds, m0, M);
+    sb[0].store(lds + BM * RB, n0, N);
+    __syncthreads();
+    sa[0].load(A, lda, m0, M, kof(PD));
+    sb[0].load(Bm, ldb, n0, N, kof(PD));
     for (int kt0 = 0; kt0 < nk; kt0 += PD) {
         static_for<0, PD>([&](auto uc) -> bool {
             constexpr int u = decltype(uc)::value;
             const int kt = kt0 + u;
             if (kt >= nk) return false;
             const char *buf = lds + (kt & 1) * TILE;
+            // every operand read of this wave's k-groups first, then the MFMAs
+            float4 a[NGW][TM], b[NGW][TN];
 #pragma unroll
-            for (int g = ks; g < NG; g += KS) {
-                // lane (l32, lh): 16 B of its row at k-group g, half lh
-                float4 a[TM], b[TN];
+            for (int q = 0; q < NGW; ++q) {
+                const int g = ks + KS * q;
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
-                    a[i] = *reinterpret_cast<const float4 *>(buf + (wm + 32 * i + l32) * kRowBytes + 32 * g + 16 * lh);
+                    a[q][i] = *reinterpret_cast<const float4 *>(buf + (wm + 32 * i + l32) * RB + 32 * g + 16 * lh);
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    b[j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 32 * j + l32) * kRowBytes + 32 * g +
-                                                             16 * lh);
+                    b[q][j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 32 * j + l32) * RB + 32 * g + 16 * lh);
+            }
+#pragma unroll
+            for (int q = 0; q < NGW; ++q) {
                 if constexpr (BF) {
 #pragma unroll
                     for (int i = 0; i < TM; ++i)
 #pragma unroll
                         for (int j = 0; j < TN; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                                *reinterpret_cast<const bf16x8 *>(&a[i]), *reinterpret_cast<const bf16x8 *>(&b[j]),
+                                *reinterpret_cast<const bf16x8 *>(&a[q][i]), *reinterpret_cast<const bf16x8 *>(&b[q][j]),
                                 acc[i][j], 0, 0, 0);
                 } else {
 #pragma unroll
@@ -227,24 +239,18 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
 #pragma unroll
-                            for (int j = 0; j < TN; ++j) {
-                                const float av = e == 0 ? a[i].x : e == 1 ? a[i].y : e == 2 ? a[i].z : a[i].w;
-                                const float bv = e == 0 ? b[j].x : e == 1 ? b[j].y : e == 2 ? b[j].z : b[j].w;
-                                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-                            }
+                            for (int j = 0; j < TN; ++j)
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[q][i], e), f4at(b[q][j], e),
+                                                                                 acc[i][j], 0, 0, 0);
                 }
             }
             constexpr int nv = (u + 1) % PD;     // the set holding tile kt + 1
-            if (kt + 1 < nk) {
-                char *nb = lds + ((kt + 1) & 1) * TILE;
-                sa[nv].store(nb, m0, M);
-                sb[nv].store(nb + BM * kRowBytes, n0, N);
-            }
+            char *nb = lds + ((kt + 1) & 1) * TILE;
+            sa[nv].store(nb, m0, M);             // (past the last tile: a clamped copy, never read)
+            sb[nv].store(nb + BM * RB, n0, N);
             __syncthreads();
-            if (kt + 1 + PD < nk) {
-                sa[nv].load(A, lda, m0, M, (kt + 1 + PD) * KE);
-                sb[nv].load(Bm, ldb, n0, N, (kt + 1 + PD) * KE);
-            }
+            sa[nv].load(A, lda, m0, M, kof(kt + 1 + PD));
+            sb[nv].load(Bm, ldb, n0, N, kof(kt + 1 + PD));
             return true;
         });
     }
@@ -295,18 +301,18 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
         }
 }
 
-template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16>
+template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16, int KT32, int KT16>
 int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
               int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop, int splits = 1, int64_t sC = 0)
 {
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
     K /= splits;
     if (bf)
-        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
-                           (int)M, (int)N, (int)K, aux, stop, sC);
+        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16>), grid, dim3(256), 0, s, A, lda, B,
+                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC);
     else
-        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc,
-                           (int)M, (int)N, (int)K, aux, stop, sC);
+        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32>), grid, dim3(256), 0, s, A, lda, B,
+                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC);
     GS_LAUNCH_CHECK("k_fc");
     return GS_OK;
 }
@@ -327,9 +333,9 @@ bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
 
 int fc_fwd_splits(int64_t M, int64_t N, int64_t K)
 {
-    // the largest split of K into 64-multiples that keeps the 32 x 64 tiles x splits within 512
+    // the largest split of K into 64-multiples that keeps the 64 x 32 tiles x splits within 512
     // workgroups (at most 16 slices)
-    const int64_t tiles = ((M + 31) / 32) * ((N + 63) / 64);
+    const int64_t tiles = ((M + 63) / 64) * ((N + 31) / 32);
     int best = 1;
     for (int sp = 2; sp <= 16; ++sp)
         if (K % (64 * sp) == 0 && tiles * sp <= 512) best = sp;
@@ -343,7 +349,7 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
                "fc_fwd_partials: shape %lld x %lld x %lld / %d not supported", (long long)M, (long long)N,
                (long long)K, splits);
     GS_REQUIRE(aligned16(A) && aligned16(B), "fc_fwd_partials: 16-B aligned operands required");
-    return launch_fc<32, 64, 1, 2, true, true, kEpiStore, FC_PD_FWD32, FC_PD_FWD16>(
+    return launch_fc<64, 32, 1, 4, true, true, kEpiStore, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(
         s, false, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, splits, M * ldc);
 }
 
@@ -356,11 +362,14 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
     GS_REQUIRE(aligned16(A) && aligned16(B) && (op == 1 || aux), "fc_gemm: 16-B aligned operands (and the epilogue "
                "operand) required");
     if (op == 0)     // fwd: C = relu(A B^T + bias), both K-contiguous
-        return launch_fc<32, 64, 1, 2, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
+        return launch_fc<64, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
+                                                                                           ldc, M, N, K, aux, stop);
     if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]
-        return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr, stop);
+        return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1>(s, bf16, A, lda, B, ldb, C,
+                                                                                            ldc, M, N, K, nullptr, stop);
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
-    return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16>(s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop);
+    return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1>(s, bf16, A, lda, B, ldb, C, ldc,
+                                                                                          M, N, K, aux, stop);
 }
 
 }  // namespace gs

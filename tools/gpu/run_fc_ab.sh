@@ -13,6 +13,22 @@ for v in intree $FCV; do
   echo "-- $v"
   GSAMD_LIB=$lib step fc-$v timeout -k 10 120 python tools/fc_bench.py > $O/fc_$v.log 2>&1 && cat $O/fc_$v.log || exit 1
 done
+if [ -n "$C5C" ]; then
+  step c5-collect-prof timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/c5c -o c5c --output-format csv \
+      -- python tools/collect_run.py C5 3 > $O/c5c.log 2>&1 && grep "collect" $O/c5c.log || exit 1
+  rm -f $O/c5c/*kernel_trace.csv
+fi
+if [ -n "$STAMPS" ]; then
+  step cnn-stamps timeout -k 10 200 python tools/cnn_stamp_run.py > $O/stamps.log 2>&1 &&
+  step cnn-stamps-bf16 timeout -k 10 200 python tools/cnn_stamp_run.py --bf16 >> $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
+  grep -v "^W20" $O/stamps.log
+fi
+if [ -n "$C4B" ]; then
+  step bench-c4 timeout -k 10 300 python bench.py --workload C4 --steps 2 --warmup 1 --cpu-minibatches 0 \
+      > $O/bench_c4.json 2> $O/bench_c4.err && tail -c 400 $O/bench_c4.json || exit 1
+  step bench-c4bf16 timeout -k 10 300 python bench.py --workload C4 --dtype bf16 --steps 2 --warmup 1 --cpu-minibatches 0 \
+      > $O/bench_c4_bf16.json 2> $O/bench_c4_bf16.err && tail -c 400 $O/bench_c4_bf16.json || exit 1
+fi
 if [ -n "$AB" ]; then
   step ab timeout -k 10 600 bash tools/run_ab_bench.sh $AB > $O/ab.log 2>&1; rc=$?; cat $O/ab.log; [ $rc -eq 0 ] || exit $rc
 fi
