@@ -210,23 +210,44 @@ __device__ __forceinline__ uint32_t gray4(uint3 a, uint3 b)
     return out;
 }
 
+template <bool HAS_DONE>
 __global__ __launch_bounds__(256) void k_atari_stack84(const uint8_t *__restrict__ frames,
                                                        const uint8_t *__restrict__ done_row, int64_t N, int S,
                                                        uint8_t *__restrict__ stack)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t g[kBandIn * kFW / 4];     // 4 800 B of max-pooled gray
+    // 4 800 B of max-pooled gray (+ the words of the clamped units past the band, never read)
+    __shared__ __attribute__((aligned(16))) uint32_t g[256 * kBandUnitsPer];
     const int64_t e = blockIdx.x / kBands;
     const int band = (int)(blockIdx.x - e * kBands);
     const int tid = threadIdx.x;
     constexpr int hw = kOut84 * kOut84;
     uint8_t *st = stack + e * (int64_t)S * hw + band * kBandOutBytes;
-    // 1. loads: the shift's sources first, then the two frames' runs as 12-B units (4 pixels):
-    //    lane i of a wave reads bytes 12 i .. 12 i + 11, so every dwordx3 load instruction covers
-    //    768 contiguous bytes (clamped, unconditional)
+    // 1. loads, all unconditional (a predicated load compiles to a branch whose register merge
+    //    puts an s_waitcnt in the middle of the burst) and in the order they are consumed: the
+    //    done flag and the resize's coverage tables for this thread's row and four columns
+    //    (L1/L2-resident; taps past a pixel's count are weighted 0 below), the shift's sources,
+    //    then the two frames' runs as 12-B units (4 pixels): lane i of a wave reads bytes
+    //    12 i .. 12 i + 11, so every dwordx3 load instruction covers 768 contiguous bytes
+    const uint8_t done_flag = HAS_DONE ? done_row[e] : 1;     // no done row: a reset
+    const int oyl = tid / 21, ox0 = 4 * (tid - 21 * (tid / 21));
+    const int orow = min(band * kBandOut + oyl, kOut84 - 1);
+    const int y0 = c_area.y0[orow] - band * kBandIn, ny = c_area.ny[orow];
+    float wy[3], wx[4][3];
+    int x0[4], nx[4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) wy[i] = c_area.wy[orow][i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int ox = min(ox0 + q, kOut84 - 1);
+        x0[q] = c_area.x0[ox];
+        nx[q] = c_area.nx[ox];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) wx[q][i] = c_area.wx[ox][i];
+    }
     const int nshift = 63 * (S - 1);
     const int sj = min(tid, max(nshift - 1, 0));
-    uint4 moved = make_uint4(0u, 0u, 0u, 0u);
-    if (nshift > 0) moved = *reinterpret_cast<const uint4 *>(st + (int64_t)(1 + sj / 63) * hw + 16 * (sj % 63));
+    const uint4 moved = *reinterpret_cast<const uint4 *>(st + (int64_t)(1 + min(sj / 63, max(S - 2, 0))) * hw +
+                                                         16 * (sj % 63));
     const uint8_t *fa = frames + e * 2 * (int64_t)kFrameBytes + band * kBandIn * kRowBytes;
     const uint8_t *fb = fa + kFrameBytes;
     uint3 ra[kBandUnitsPer], rb[kBandUnitsPer];
@@ -236,33 +257,28 @@ __global__ __launch_bounds__(256) void k_atari_stack84(const uint8_t *__restrict
         ra[j] = *reinterpret_cast<const uint3 *>(fa + 12 * u);
         rb[j] = *reinterpret_cast<const uint3 *>(fb + 12 * u);
     }
-    // the resize's coverage tables for this thread's row and four columns (L1-resident)
-    const int oyl = tid / 21, ox0 = 4 * (tid - 21 * (tid / 21));
-    const int orow = min(band * kBandOut + oyl, kOut84 - 1);
-    const int y0 = c_area.y0[orow] - band * kBandIn, ny = c_area.ny[orow];
-    float wy[3], wx[4][3];
-    int x0[4];
+    // (weights times 0 / 1 rather than a select, which the compiler turns back into a branch
+    // around the load; the weights are >= 0, so the products are exact)
 #pragma unroll
-    for (int i = 0; i < 3; ++i) wy[i] = i < ny ? c_area.wy[orow][i] : 0.0f;
+    for (int i = 0; i < 3; ++i) wy[i] *= (float)(i < ny);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int ox = min(ox0 + q, kOut84 - 1);
-        x0[q] = c_area.x0[ox];
-        const int nx = c_area.nx[ox];
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) wx[q][i] = i < nx ? c_area.wx[ox][i] : 0.0f;
-    }
-    const bool reset = done_row ? done_row[e] != 0 : true;
-    // 2. grayscale + max-pool into LDS, one word of 4 pixels per unit
+        for (int i = 0; i < 3; ++i) wx[q][i] *= (float)(i < nx[q]);
+    // the shifted slot value, settled before the barrier (the empty asm keeps the compiler from
+    // sinking the done-flag and slot loads into the shift's branch, a memory round trip after it)
+    const uint4 shifted = done_flag != 0 ? make_uint4(0u, 0u, 0u, 0u) : moved;
+    asm volatile("" ::"v"(shifted.x), "v"(shifted.y), "v"(shifted.z), "v"(shifted.w));
+    // 2. grayscale + max-pool into LDS, one word of 4 pixels per unit (every unit stored, so no
+    //    load is sunk into a branch)
 #pragma unroll
-    for (int j = 0; j < kBandUnitsPer; ++j)
-        if (tid + 256 * j < kBandUnits) g[tid + 256 * j] = gray4(ra[j], rb[j]);
+    for (int j = 0; j < kBandUnitsPer; ++j) g[tid + 256 * j] = gray4(ra[j], rb[j]);
     __syncthreads();
     // 3. the shift (every source load of this workgroup has landed: the gray bytes above waited
     //    for the younger frame loads)
     if (tid < nshift)
         *reinterpret_cast<uint4 *>(st + (int64_t)(tid / 63) * hw + 16 * (tid % 63)) =
-            reset ? make_uint4(0u, 0u, 0u, 0u) : moved;
+            shifted;
     // 4. area resize of four output pixels
     if (tid < kBandOut * 21) {
         uint32_t packed = 0;
@@ -342,7 +358,12 @@ int launch_stack(const uint8_t *frames, const uint8_t *done_row, int64_t N, int 
 {
     if (OH == kOut84 && OW == kOut84 && S >= 1 && S <= kMaxStackFast) {
         GS_REQUIRE(N * kBands < ((int64_t)1 << 31), "gs_atari: %lld envs exceed the launch grid", (long long)N);
-        hipLaunchKernelGGL(k_atari_stack84, dim3((unsigned)(N * kBands)), dim3(256), 0, s, frames, done_row, N, S, stack);
+        if (done_row)
+            hipLaunchKernelGGL(k_atari_stack84<true>, dim3((unsigned)(N * kBands)), dim3(256), 0, s, frames, done_row, N, S,
+                               stack);
+        else
+            hipLaunchKernelGGL(k_atari_stack84<false>, dim3((unsigned)(N * kBands)), dim3(256), 0, s, frames, done_row, N,
+                               S, stack);
         GS_LAUNCH_CHECK("k_atari_stack84");
         return GS_OK;
     }

@@ -100,6 +100,7 @@ struct CnnWs {
 };
 
 constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block sums them)
+constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
 constexpr int kHeadRows = 8;    // minibatch rows per k_cnn_head_loss workgroup
 constexpr int kHeadSlices = 256 / kHeadRows;   // its z product's K slices (one thread per row x slice)
@@ -404,27 +405,27 @@ __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ 
 #pragma unroll
     for (int u = 0; u < NJ; ++u) {
         const int j = min(tid + 256 * u, HID - 1);
+        // every load unconditional, at clamped indices: a predicated load would be a branch whose
+        // register merge stalls the burst (slices past np, rows past A and j past HID are zeroed
+        // by the factors below: exact)
 #pragma unroll
-        for (int p = 0; p < kActMaxSplits; ++p) t[u][p] = p < np ? parts[(int64_t)p * pstride + r * HID + j] : 0.f;
+        for (int p = 0; p < kActMaxSplits; ++p) t[u][p] = parts[(int64_t)min(p, np - 1) * pstride + r * HID + j];
         bfv[u] = P[L.obf + j];
 #pragma unroll
-        for (int a = 0; a < AM + 1; ++a)
-            w[u][a] = a < A ? P[L.oWp + (int64_t)a * HID + j] : a == A ? P[L.oWv + j] : 0.f;
+        for (int a = 0; a < AM + 1; ++a) w[u][a] = a < A ? P[L.oWp + (int64_t)a * HID + j] : P[L.oWv + j];
     }
     float acc[AM + 1];
 #pragma unroll
     for (int a = 0; a < AM + 1; ++a) acc[a] = 0.f;
 #pragma unroll
     for (int u = 0; u < NJ; ++u) {
-        if (tid + 256 * u >= HID) break;
         float hv = 0.f;
 #pragma unroll
-        for (int p = 0; p < kActMaxSplits; ++p)
-            if (p < np) hv += t[u][p];
+        for (int p = 0; p < kActMaxSplits; ++p) hv += t[u][p] * (float)(p < np);
         hv += bfv[u];
-        hv = hv > 0.f ? hv : 0.f;
+        hv = (hv > 0.f ? hv : 0.f) * (float)(tid + 256 * u < HID);
 #pragma unroll
-        for (int a = 0; a < AM + 1; ++a) acc[a] = fmaf(hv, w[u][a], acc[a]);
+        for (int a = 0; a < AM + 1; ++a) acc[a] = fmaf(hv, w[u][a] * (float)(a <= A), acc[a]);
     }
 #pragma unroll
     for (int a = 0; a < AM + 1; ++a) red[a * 256 + tid] = acc[a];
@@ -1067,6 +1068,17 @@ __global__ __launch_bounds__(256) void k_cnn_dh(const float *__restrict__ dz, co
 }
 
 
+// s[0] += g2 and s[1 + c] += g2 with selects (a runtime index into the register array would put
+// it in scratch memory); adding +0.0 to the other components leaves their sums unchanged
+__device__ __forceinline__ void add_sq(double (&s)[5], double g2, int c)
+{
+    s[0] += g2;
+    s[1] += c == 0 ? g2 : 0.0;
+    s[2] += c == 1 ? g2 : 0.0;
+    s[3] += c == 2 ? g2 : 0.0;
+    s[4] += c == 3 ? g2 : 0.0;
+}
+
 // ---- global-norm partials (double) of the flat gradient
 // part[0 .. nb): the block partials of the whole gradient; part[nb (1 + c) + b]: component c's
 // (c = cnn trunk, mlp trunk, policy_head, value_head: flat ranges split at cut[0..2]) for the
@@ -1094,15 +1106,13 @@ __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__
             for (int q = 0; q < 4; ++q) {
                 const int64_t k = 4 * i + q;
                 const double g = (double)e[q];
-                s[0] += g * g;
-                s[1 + (k >= cut0) + (k >= cut1) + (k >= cut2)] += g * g;
+                add_sq(s, g * g, (k >= cut0) + (k >= cut1) + (k >= cut2));
             }
         }
     }
     for (int64_t k = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) {
         const double g = (double)G[k];
-        s[0] += g * g;
-        s[1 + (k >= cut0) + (k >= cut1) + (k >= cut2)] += g * g;
+        add_sq(s, g * g, (k >= cut0) + (k >= cut1) + (k >= cut2));
     }
     wg_reduce<5>(s, sred);
     if (threadIdx.x < 5) part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s[threadIdx.x];
@@ -1119,7 +1129,8 @@ __device__ __forceinline__ float adam_flat(float g, float &m, float &v, float p,
 }
 
 // ---- clip coefficient from the partials (every block, fixed order) + Adam (torch single-tensor):
-// one float4 of parameters per thread (grid = ceil(n / 1024)), the scalar tail by the last block
+// kAdamQuads float4 of parameters per thread, all loaded before the norm reduction (grid =
+// ceil(n / (1024 kAdamQuads)) + 1), the scalar tail by the last block
 __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, float *__restrict__ G,
                                                         float *__restrict__ M, float *__restrict__ V, int64_t n,
                                                         const double *__restrict__ part, int nparts, AdamArgs aa,
@@ -1135,15 +1146,21 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     __shared__ double sred[256 + 16];
     __shared__ float s_coef;
-    const int64_t n4 = n / 4, i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    constexpr int U = kAdamQuads;
+    const int64_t n4 = n / 4;
     // this thread's parameters first (clamped, unconditional), then the norm partials
-    const int64_t ic = i < n4 ? i : (n4 > 0 ? n4 - 1 : 0);
-    float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), m4 = g4, v4 = g4, p4 = g4;
-    if (n4 > 0) {
-        g4 = reinterpret_cast<const float4 *>(G)[ic];
-        m4 = reinterpret_cast<const float4 *>(M)[ic];
-        v4 = reinterpret_cast<const float4 *>(V)[ic];
-        p4 = reinterpret_cast<const float4 *>(Pm)[ic];
+    float4 g4[U], m4[U], v4[U], p4[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = ((int64_t)blockIdx.x * U + u) * 256 + threadIdx.x;
+        const int64_t ic = i < n4 ? i : (n4 > 0 ? n4 - 1 : 0);
+        g4[u] = m4[u] = v4[u] = p4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n4 > 0) {
+            g4[u] = reinterpret_cast<const float4 *>(G)[ic];
+            m4[u] = reinterpret_cast<const float4 *>(M)[ic];
+            v4[u] = reinterpret_cast<const float4 *>(V)[ic];
+            p4[u] = reinterpret_cast<const float4 *>(Pm)[ic];
+        }
     }
     double s[1] = {0.0};
     for (int k = threadIdx.x; k < nparts; k += 256) s[0] += part[k];
@@ -1176,9 +1193,13 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     __syncthreads();
     const float coef = s_coef;
-    if (i < n4) {
-        float g[4] = {g4.x * coef, g4.y * coef, g4.z * coef, g4.w * coef};
-        float m[4] = {m4.x, m4.y, m4.z, m4.w}, v[4] = {v4.x, v4.y, v4.z, v4.w}, p[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = ((int64_t)blockIdx.x * U + u) * 256 + threadIdx.x;
+        if (i >= n4) break;
+        float g[4] = {g4[u].x * coef, g4[u].y * coef, g4[u].z * coef, g4[u].w * coef};
+        float m[4] = {m4[u].x, m4[u].y, m4[u].z, m4[u].w}, v[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
+        float p[4] = {p4[u].x, p4[u].y, p4[u].z, p4[u].w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) p[q] = adam_flat(g[q], m[q], v[q], p[q], aa);
         reinterpret_cast<float4 *>(G)[i] = make_float4(g[0], g[1], g[2], g[3]);
@@ -1520,7 +1541,8 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     }
     hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
                        L.oWv);
-    hipLaunchKernelGGL(k_clip_adam_flat, dim3((unsigned)((L.P / 4 + 255) / 256 + 1)), dim3(256), 0, s, P, G, Mm, Vv,
+    hipLaunchKernelGGL(k_clip_adam_flat, dim3((unsigned)((L.P / 4 + 256 * kAdamQuads - 1) / (256 * kAdamQuads) + 1)),
+                       dim3(256), 0, s, P, G, Mm, Vv,
                        L.P, w.norm_part, kNormBlocks, aa, metrics, stop);
     GS_LAUNCH_CHECK("k_clip_adam_flat");
     return GS_OK;

@@ -42,6 +42,10 @@ struct FcK {
     static constexpr int RB = 128 * KT + 16;         // LDS bytes per staged row
 };
 
+#ifndef FC_XCD
+#define FC_XCD 1            // XCD-aware tile order (0: plain blockIdx order, for A/B runs)
+#endif
+
 // register prefetch depth (K tiles in flight) per launch shape and operand precision
 #ifndef FC_PD_FWD32
 #define FC_PD_FWD32 3
@@ -159,7 +163,7 @@ template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, 
 __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int64_t lda, const float *__restrict__ Bm,
                                                int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
                                                const float *__restrict__ aux, const int32_t *__restrict__ stop,
-                                               int64_t sC)
+                                               int64_t sC, int gm)
 {
     if (stop && *stop) return;      // KL early stop: the minibatch's product is never used
     // split-K (gridDim.z slices of K each, partial products at C + z sC; no epilogue)
@@ -177,7 +181,23 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
     constexpr int TILE = (BM + BN) * RB;
     __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
 
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    // XCD-aware tile order: workgroup b runs on XCD b % 8 (round-robin dispatch), so XCD x is
+    // given the contiguous run [x T/8, (x+1) T/8) of a grouped order (gm m-blocks per group, m
+    // fastest within it): its L2 then holds a band of A rows and a band of B rows instead of
+    // every XCD streaming all of A (T = tiles per split, a multiple of 8)
+    int bx = blockIdx.x, by = blockIdx.y;
+    {
+        const int nbx = gridDim.x, nby = gridDim.y, T = nbx * nby;
+        if (FC_XCD && T % 8 == 0 && gm > 0) {
+            const int b = by * nbx + bx;
+            const int t = (b & 7) * (T >> 3) + (b >> 3);
+            const int gsize = gm * nbx, grp = t / gsize, first = grp * gm, gcnt = min(nby - first, gm);
+            const int within = t - grp * gsize;
+            by = first + within % gcnt;
+            bx = within / gcnt;
+        }
+    }
+    const int m0 = by * BM, n0 = bx * BN;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ks = wave % KS, wmn = wave / KS;
     const int wm = (wmn / WGN) * WM, wn = (wmn % WGN) * WN;
@@ -303,16 +323,17 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
 
 template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16, int KT32, int KT16>
 int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
-              int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop, int splits = 1, int64_t sC = 0)
+              int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop, int gm, int splits = 1,
+              int64_t sC = 0)
 {
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
     K /= splits;
     if (bf)
         hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16>), grid, dim3(256), 0, s, A, lda, B,
-                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC);
+                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
     else
         hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32>), grid, dim3(256), 0, s, A, lda, B,
-                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC);
+                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
     GS_LAUNCH_CHECK("k_fc");
     return GS_OK;
 }
@@ -350,7 +371,7 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
                (long long)K, splits);
     GS_REQUIRE(aligned16(A) && aligned16(B), "fc_fwd_partials: 16-B aligned operands required");
     return launch_fc<64, 32, 1, 4, true, true, kEpiStore, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(
-        s, false, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, splits, M * ldc);
+        s, false, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 4, splits, M * ldc);
 }
 
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
@@ -363,13 +384,13 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
                "operand) required");
     if (op == 0)     // fwd: C = relu(A B^T + bias), both K-contiguous
         return launch_fc<64, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
-                                                                                           ldc, M, N, K, aux, stop);
+                                                                                           ldc, M, N, K, aux, stop, 4);
     if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]
         return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1>(s, bf16, A, lda, B, ldb, C,
-                                                                                            ldc, M, N, K, nullptr, stop);
+                                                                                            ldc, M, N, K, nullptr, stop, 8);
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
     return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1>(s, bf16, A, lda, B, ldb, C, ldc,
-                                                                                          M, N, K, aux, stop);
+                                                                                          M, N, K, aux, stop, 16);
 }
 
 }  // namespace gs

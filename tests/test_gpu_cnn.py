@@ -110,6 +110,24 @@ def test_cnn_policy_act_vs_oracle(cuda, tag):
     assert set(np.unique(a_s)) <= set(valid)
     ln_rep = np.tile(ln, (64, 1))
     np.testing.assert_allclose(lp_s.cpu().numpy(), ln_rep[np.arange(len(a_s)), a_s], atol=1e-5, rtol=0)
+    # the rollout row's obs copy (written by the first convolution from the frames it loads) and
+    # the values at the small-batch kernel shapes (conv1 in 4 bands below 128 rows, conv2 / conv3
+    # split over 2 workgroups per sample up to 512, the fc forward as split-K partials) and the
+    # update-sized ones above
+    g = torch.Generator().manual_seed(5)
+    P = C.unflatten(p_ref, C.cnn_param_shapes())
+    for n in (8, 128, 600):
+        o = torch.randint(0, 256, (n,) + tuple(obs.shape[1:]), generator=g, dtype=torch.uint8)
+        od = o.to(cuda)
+        store = torch.zeros_like(od)
+        a_n, lp_n, v_n = pm.act(od, mode=1, obs_store=store)
+        torch.cuda.synchronize()
+        assert torch.equal(store, od), n
+        lg, vals, _ = C.forward(P, o, valid)
+        ln_n = (lg - torch.logsumexp(lg, -1, keepdim=True)).numpy()
+        np.testing.assert_allclose(v_n.cpu().numpy(), vals.numpy(), atol=1e-5, rtol=0, err_msg=str(n))
+        a_n = a_n.cpu().numpy()
+        np.testing.assert_allclose(lp_n.cpu().numpy(), ln_n[np.arange(n), a_n], atol=1e-5, rtol=0, err_msg=str(n))
 
 
 @pytest.mark.parametrize("in_shape,T", [((4, 84, 84), 3), ((4, 52, 48), 2)])

@@ -13,6 +13,17 @@ for v in intree $FCV; do
   echo "-- $v"
   GSAMD_LIB=$lib step fc-$v timeout -k 10 120 python tools/fc_bench.py > $O/fc_$v.log 2>&1 && cat $O/fc_$v.log || exit 1
 done
+if [ -n "$ATARI" ]; then
+  step atari-prof timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/atari -o atari --output-format csv \
+      -- python tools/atari_run.py 256 > $O/atari.log 2>&1 && grep "env step" $O/atari.log || exit 1
+  rm -f $O/atari/*kernel_trace.csv
+fi
+if [ -n "$FCPMC" ]; then
+  step fc-fetch timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fc_fetch -o pmc \
+      -- python tools/fc_bench.py > $O/fc_fetch.log 2>&1 &&
+  step fc-write timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/fc_write -o pmc \
+      -- python tools/fc_bench.py > $O/fc_write.log 2>&1 || exit 1
+fi
 if [ -n "$C5C" ]; then
   step c5-collect-prof timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/c5c -o c5c --output-format csv \
       -- python tools/collect_run.py C5 3 > $O/c5c.log 2>&1 && grep "collect" $O/c5c.log || exit 1
