@@ -747,6 +747,112 @@ __global__ void k_cnn_loss_final(const double *__restrict__ part, int nb, int B,
     if (threadIdx.x == 0) cnn_write_metrics(part, nb, B, la, metrics, stop);
 }
 
+// ---- one minibatch row's masked-categorical PPO loss on a 32-lane segment of a wave (lane a =
+// action a; A <= 32): the same arithmetic as cnn_loss_row with the action sums as fixed xor trees
+// (lane 0's result broadcast, so every lane holds the same value) instead of one thread walking
+// the actions in order — a short instruction stream for the whole workgroup instead of an
+// unrolled per-action chain on 8 threads.  za: this lane's head output (biases added), v the
+// value; the lane's dLoss/dz goes to dzr[a] (a < A), lane 0 also writes dzr[A]; the 13 sums are
+// added to acc on lane 0 only (live: the row exists and is this rank's).
+__device__ __forceinline__ float seg_max(float x)
+{
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) x = fmaxf(x, __shfl_xor(x, off, 32));
+    return x;
+}
+__device__ __forceinline__ float seg_sum(float x)
+{
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) x += __shfl_xor(x, off, 32);
+    return __shfl(x, 0, 32);
+}
+
+__device__ __forceinline__ void cnn_loss_lanes(float za, float v, int act, float olp, float ov, float adv, float ret,
+                                               float meanf, float stdf, const LossArgs &la, float invB,
+                                               const CnnLayout &L, bool live, float *__restrict__ dzr,
+                                               float *__restrict__ dz_global, double (&acc)[kSums])
+{
+    const int a = threadIdx.x & 31, A = L.A;
+    const bool masked = L.valid != 0u;
+    const bool va = a < A && L.is_valid(a);
+    const float m = seg_max(va ? za : -INFINITY);
+    const float se = seg_sum(va ? expf(za - m) : 0.f);
+    const float lse = m + logf(se);
+    const float lnr = za - lse;
+    const float m2 = seg_max(va ? lnr : -INFINITY);
+    const float S = seg_sum(va ? expf(lnr - m2) : 0.f);
+    const float invS = 1.0f / S;
+    const float ln = va ? lnr : -INFINITY;
+    const float pr = expf(lnr - m2) * invS;
+    const float p = va ? pr : 0.f;
+    float g = 0.f, Hc, pgc = 0.f;
+    if (masked) {
+        const float lq = logf(p + 1e-8f);      // MaskedCategorical.entropy
+        g = lq + p / (p + 1e-8f);               // -dH/dp_a
+        Hc = va ? p * lq : 0.f;
+        pgc = va ? p * g : 0.f;
+    } else {
+        Hc = va ? fmaxf(ln, -FLT_MAX) * p : 0.f;    // Categorical.entropy
+    }
+    const float H = -seg_sum(Hc);
+    const float pg = masked ? seg_sum(pgc) : 0.f;
+    const float lp = __shfl(va ? ln : 0.f, min(max(act, 0), 31), 32) * (float)(act >= 0 && act < 32);
+    if (la.normalize) adv = (adv - meanf) / (stdf + 1e-8f);
+    const float ratio = expf(lp - olp);
+    const float rc = fminf(fmaxf(ratio, la.clip_lo), la.clip_hi);
+    const float s1 = adv * ratio, s2 = adv * rc;
+    const float mn = fminf(s1, s2);
+    const float vdelta = v - ov;
+    const float du = v - ret;
+    const float vu = du * du;
+    const float vcl = ov + fminf(fmaxf(vdelta, -la.clip_vf), la.clip_vf);
+    const float dc = vcl - ret;
+    const float vc = dc * dc;
+    if (a == 0 && live) {
+        const float ldiff = fminf(fmaxf(lp - olp, -20.0f), 20.0f);
+        const float r2 = expf(ldiff);
+        const float rv = ret - v;
+        acc[0] += (double)mn;
+        acc[1] += (double)fmaxf(vu, vc);
+        acc[2] += (double)H;
+        acc[3] += (ratio < la.clip_lo || ratio > la.clip_hi) ? 1.0 : 0.0;
+        acc[4] += (vdelta < -la.clip_vf || vdelta > la.clip_vf) ? 1.0 : 0.0;
+        acc[5] += (double)(olp - lp);
+        acc[6] += (double)((r2 - 1.0f) - logf(r2));
+        acc[7] += (double)rv;
+        acc[8] += (double)rv * (double)rv;
+        acc[9] += (double)ret;
+        acc[10] += (double)ret * (double)ret;
+        acc[11] += (double)adv;
+        acc[12] += (double)adv * (double)adv;
+    }
+    const float ga = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+    const float gb = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+    const float inclip = (ratio >= la.clip_lo && ratio <= la.clip_hi) ? 1.0f : 0.0f;
+    const float g_mn = -invB;
+    const float dratio = adv * (g_mn * ga) + adv * (g_mn * gb) * inclip;
+    const float dlp = dratio * ratio;
+    const float dH = -la.ent_coef * invB;
+    const float pe = expf(ln);
+    float gg = dlp * ((a == act ? 1.0f : 0.0f) - pe);
+    if (masked) gg += dH * (p * (pg - g));
+    else gg += dH * (-p * (ln + H));
+    const float dza = (va && live) ? gg : 0.f;     // masked_fill blocks the gradient of an invalid action
+    if (a < A) {
+        dzr[a] = dza;
+        if (dz_global) dz_global[a] = dza;
+    }
+    if (a == 0) {
+        const float hu = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+        const float hc = vc > vu ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+        const float invc = (vdelta >= -la.clip_vf && vdelta <= la.clip_vf) ? 1.0f : 0.0f;
+        const float gv = la.vf_coef * invB;
+        const float dzv = live ? (gv * hu) * (2.0f * du) + (gv * hc) * (2.0f * dc) * invc : 0.f;
+        dzr[A] = dzv;
+        if (dz_global) dz_global[A] = dzv;
+    }
+}
+
 // ---- the update's head + loss section as two launches (replacing heads GEMM + split-K sum,
 // loss rows + final, head weight-gradient GEMM + two sums and the dh kernel):
 // k_cnn_head_loss: kHeadRows minibatch rows per workgroup — z = h Wh^T (K split over 16 thread
@@ -805,7 +911,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     // rank's row — it reads row 0's fields, takes no loss and no gradient (dz = 0, so every weight
     // gradient gets exact zeros from it), and the advantage statistics are the whole minibatch's
     const bool gmode = la.sums_out != nullptr;
-    const bool my_live = !gmode || fl.idx[min(r0 + (tid & (kHeadRows - 1)), B - 1)] >= 0;
+    const bool my_live = !gmode || fl.idx[min(r0 + (tid >> 5), B - 1)] >= 0;     // row tid >> 5
     {
         float4 th[NH], tw[NW];
         float tv[NV];
@@ -813,7 +919,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         int64_t src[NA];
 #pragma unroll
         for (int j = 0; j < NA; ++j) src[j] = frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N, gmode);
-        const int64_t my_src = frame_row(fl.idx, min(r0 + (tid & (kHeadRows - 1)), B - 1), fl.T, fl.N, gmode);
+        const int64_t my_src = frame_row(fl.idx, min(r0 + (tid >> 5), B - 1), fl.T, fl.N, gmode);
 #pragma unroll
         for (int j = 0; j < NH; ++j) {
             const int u = min(tid + 256 * j, nh4 - 1), r = u / H4, c4 = u - r * H4;
@@ -905,23 +1011,18 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 #pragma unroll
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
     const float invB = gmode ? la.inv_batch : 1.0f / (float)B;
-    if (tid < kHeadRows && r0 + tid < B && my_live) {
-        const int r = r0 + tid;
-        float zr[AM + 1];
-        float v = 0.f;
-#pragma unroll
-        for (int a = 0; a < AM + 1; ++a) {
-            zr[a] = a < A1 ? zs[tid * ZS + a] : 0.f;
-            if (a == A) v = zr[a];
-        }
-        float *dzr = zs + tid * ZS;     // the row's z (now in zr) is overwritten by its dz
-        cnn_loss_row<AM>(zr, v, my_act, my_olp, my_ov, my_adv, my_ret, meanf, stdf, la, invB, L, dzr, acc);
-        for (int a = 0; a < A1; ++a) dz[(int64_t)r * A1 + a] = dzr[a];
-        for (int a = A1; a < ZS; ++a) dzr[a] = 0.f;
-    } else if (tid < kHeadRows) {
-        for (int a = 0; a < ZS; ++a) zs[tid * ZS + a] = 0.f;
-        if (r0 + tid < B)     // another rank's row (global mode): no gradient
-            for (int a = 0; a < A1; ++a) dz[(int64_t)(r0 + tid) * A1 + a] = 0.f;
+    {   // the loss rows: row tid >> 5 on a 32-lane segment of a wave, lane a = action a
+        static_assert(kHeadRows * 32 == 256, "one 32-lane segment per row");
+        const int row = tid >> 5, a = tid & 31;
+        const bool exists = r0 + row < B;
+        float *dzr = zs + row * ZS;             // the row's z, overwritten by its dz
+        const float za = a < A1 ? dzr[a] : 0.f;
+        const float v = dzr[A];
+        // another rank's row (global mode, !my_live) takes no loss and gets a zero gradient
+        cnn_loss_lanes(za, v, my_act, my_olp, my_ov, my_adv, my_ret, meanf, stdf, la, invB, L, exists && my_live, dzr,
+                       exists ? dz + (int64_t)(r0 + row) * A1 : nullptr, acc);
+        if (a == 0)
+            for (int c = A1; c < ZS; ++c) dzr[c] = 0.f;
     }
     GS_STAMP(4)
     wg_reduce<kSums>(acc, sred);      // its barriers publish zs (now dz) too
@@ -941,7 +1042,8 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 #pragma unroll
         for (int a = 0; a < 4 * NZ; ++a) g[a] = 0.f;
         float dbf = 0.f;      // this workgroup's rows of dbf[j] = sum_b dh[b][j] (the fc bias gradient)
-        for (int r = 0; r < kHeadRows; ++r) {
+#pragma unroll 1
+        for (int r = 0; r < kHeadRows; ++r) {      // rolled: a short instruction stream (cold i-cache)
             float d[4 * NZ];
 #pragma unroll
             for (int c = 0; c < NZ; ++c) {

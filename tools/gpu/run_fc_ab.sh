@@ -24,6 +24,11 @@ if [ -n "$FCPMC" ]; then
   step fc-write timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/fc_write -o pmc \
       -- python tools/fc_bench.py > $O/fc_write.log 2>&1 || exit 1
 fi
+if [ -n "$SQPMC" ]; then
+  step fc-sq timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+      SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv -d $O/fc_sq -o pmc \
+      -- python tools/fc_bench.py > $O/fc_sq.log 2>&1 || exit 1
+fi
 if [ -n "$C5C" ]; then
   step c5-collect-prof timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/c5c -o c5c --output-format csv \
       -- python tools/collect_run.py C5 3 > $O/c5c.log 2>&1 && grep "collect" $O/c5c.log || exit 1
