@@ -117,6 +117,22 @@ inline int splits_for(int64_t M, int64_t N, int64_t K)
     return s;
 }
 
+// the head weights' gradient partials of one k_cnn_head_loss workgroup: [rows][HID + 1] (bias
+// last; rows = the kernel's float4-padded head width, rows past A1 zero and never summed), then
+// dbf (column sums of dh); head_part_out: the A1 (HID + 1) + HID outputs k_cnn_head_wsum sums
+__host__ __device__ inline int head_part_rows(const CnnLayout &L)
+{
+    return 4 * (((L.A <= 18 ? 18 : kAMax) + 4) / 4);
+}
+__host__ __device__ inline int64_t head_part_stride(const CnnLayout &L)
+{
+    return (int64_t)head_part_rows(L) * (L.HID + 1) + L.HID;
+}
+__host__ __device__ inline int64_t head_part_out(const CnnLayout &L)
+{
+    return (int64_t)(L.A + 1) * (L.HID + 1) + L.HID;
+}
+
 CnnWs carve(void *base, const CnnLayout &L, int64_t R)
 {
     char *p = (char *)base;
@@ -157,7 +173,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
                                          (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
                                          (int64_t)splits_for(L.A + 1, L.HID + 1, R) * (L.A + 1) * (L.HID + 1),
                                          (int64_t)splits_for(L.HID, L.F + 1, R) * L.HID * (L.F + 1)});
-        const int64_t hparts = (R + kHeadRows - 1) / kHeadRows * (int64_t)(L.A + 1) * (L.HID + 1);
+        const int64_t hparts = (R + kHeadRows - 1) / kHeadRows * head_part_stride(L);
         w.parts = (float *)take(sizeof(float) * std::max({wparts, cparts, gparts, hparts}));
     }
     w.bytes = off;
@@ -874,11 +890,6 @@ size_t head_loss_lds(const CnnLayout &L)
                             (size_t)kHeadSlices * kHeadRows * ZS + (size_t)kHeadRows * ZS);
 }
 
-// the head weights' gradient partials of one k_cnn_head_loss workgroup: [A1][HID + 1] (bias last)
-__host__ __device__ inline int64_t head_part_stride(const CnnLayout &L)
-{
-    return (int64_t)(L.A + 1) * (L.HID + 1) + L.HID;    // [dWh | dbh] rows, then dbf (column sums of dh)
-}
 
 template <int AM, bool BF>
 __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__ h, const float *__restrict__ P,
@@ -1052,17 +1063,11 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
                 d[4 * c] = t.x, d[4 * c + 1] = t.y, d[4 * c + 2] = t.z, d[4 * c + 3] = t.w;
             }
             const float hv = hs[r * HS + j];
-            // dh[r][j] = h > 0 ? sum_a dz[r][a] Wp[a][j] + dz[r][A] Wv[j] : 0 (fp32 weights; the
-            // padding lanes are zero)
+            // dh[r][j] = h > 0 ? sum_a dz[r][a] [Wp; Wv][a][j] : 0 over the padded head width, in
+            // column order (fp32 weights; the value row sits at column A, the padding is zero)
             float sacc = 0.f;
 #pragma unroll
-            for (int a = 0; a < AM; ++a)
-                if (a < A) sacc += d[a] * w[a];
-            float dA = 0.f, wA = 0.f;
-#pragma unroll
-            for (int a = 0; a < 4 * NZ; ++a)
-                if (a == A) dA = d[a], wA = w[a];
-            sacc += dA * wA;
+            for (int a = 0; a < 4 * NZ; ++a) sacc += d[a] * w[a];
             const float dhv = hv > 0.f ? sacc : 0.f;
             if (r0 + r < B) {
                 dh[(int64_t)(r0 + r) * HID + j] = dhv;
@@ -1073,10 +1078,11 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 #pragma unroll
             for (int a = 0; a < 4 * NZ; ++a) g[a] = fmaf(BF ? bf16r(d[a]) : d[a], hb, g[a]);
         }
+        // every padded row stored (rows past A1 are zeros, never summed): no per-row branches
+        static_assert(4 * NZ == 4 * (((AM <= 18 ? 18 : kAMax) + 4) / 4), "head_part_rows");
 #pragma unroll
-        for (int a = 0; a < 4 * NZ; ++a)
-            if (a < A1) wp[a * (HID + 1) + j] = g[a];
-        wp[(int64_t)A1 * (HID + 1) + j] = dbf;
+        for (int a = 0; a < 4 * NZ; ++a) wp[a * (HID + 1) + j] = g[a];
+        wp[(int64_t)(4 * NZ) * (HID + 1) + j] = dbf;
     }
     GS_STAMP(6)
     if (tid < A1) {     // the bias column: sum of the (unrounded) dz rows
@@ -1097,7 +1103,8 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
 {
     __shared__ float red[4][64];
     const int tid = threadIdx.x, HID = L.HID, A = L.A;
-    const int64_t nout = head_part_stride(L);
+    const int64_t nout = head_part_out(L), pstride = head_part_stride(L);
+    const int64_t pad = (int64_t)(head_part_rows(L) - (A + 1)) * (HID + 1);     // the zero rows skipped
     if ((int64_t)blockIdx.x * 64 >= nout) {
         // the record: the 13 loss sums over the partials, 16 threads per sum (strided, in order),
         // then the 16 in order; thread 0 writes it from a one-partial view of the totals
@@ -1128,14 +1135,15 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
     if (stop && *stop) return;
     const int o = tid & 63, g = tid >> 6;
     const int64_t out = (int64_t)blockIdx.x * 64 + o;
-    const int64_t oc = out < nout ? out : nout - 1;
+    const int64_t oc0 = out < nout ? out : nout - 1;
+    const int64_t oc = oc0 < (int64_t)(A + 1) * (HID + 1) ? oc0 : oc0 + pad;     // its partial column
     const int w0 = (g * nparts) / 4, w1 = ((g + 1) * nparts) / 4;
     float sacc = 0.f;
     constexpr int NB = 8;
     for (int w = w0; w < w1; w += NB) {
         float t[NB];
 #pragma unroll
-        for (int j = 0; j < NB; ++j) t[j] = wpart[(int64_t)min(w + j, w1 - 1) * nout + oc];
+        for (int j = 0; j < NB; ++j) t[j] = wpart[(int64_t)min(w + j, w1 - 1) * pstride + oc];
 #pragma unroll
         for (int j = 0; j < NB; ++j)
             if (w + j < w1) sacc += t[j];
@@ -1572,7 +1580,7 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
     if (L.A <= 18) rc = bf ? go(std::integral_constant<int, 18>{}, T{}) : go(std::integral_constant<int, 18>{}, F{});
     else rc = bf ? go(std::integral_constant<int, kAMax>{}, T{}) : go(std::integral_constant<int, kAMax>{}, F{});
     if (rc) return rc;
-    const int64_t nout = head_part_stride(L);
+    const int64_t nout = head_part_out(L);
     hipLaunchKernelGGL(k_cnn_head_wsum, dim3((unsigned)((nout + 63) / 64 + 1)), dim3(256), 0, s, w.parts, (int)nb, L,
                        G, w.loss_part, (int)B, la, metrics, stop);
     GS_LAUNCH_CHECK("k_cnn_head_wsum");
