@@ -96,6 +96,8 @@ struct CnnWs {
     double *norm_part;
     double *loss_part;     // kSums per loss row block
     float *parts;          // split-K weight-gradient partials / bias column-sum partials
+    float *pre;            // [2][5][R]: a minibatch's gathered fields (act bits, olp, ov, adv, ret), by parity
+    float *pre_stats;      // [2][2]: its advantage mean / std
     size_t bytes;
 };
 
@@ -161,6 +163,8 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks * 5);   // total + 4 component partials
+    w.pre = (float *)take(sizeof(float) * 2 * 5 * R);
+    w.pre_stats = (float *)take(sizeof(float) * 4);
     w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + kHeadRows - 1) / kHeadRows));
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
@@ -197,6 +201,10 @@ struct CnnFields {
     int64_t T, N;
     const int64_t *actions;
     const float *logprobs, *values, *advantages, *returns;
+    // the minibatch's fields gathered ahead of time (k_cnn_prefetch / the previous step's clip +
+    // Adam launch): [5][B] (act bits, olp, ov, adv, ret) and {adv mean, std}; nullptr: gather here
+    const float *pre = nullptr;
+    const float *pre_stats = nullptr;
 };
 
 // ---- ReLU-masked col2im (gather form, fixed summation order): dA[r,y,x,c] for stride s
@@ -922,15 +930,24 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     // rank's row — it reads row 0's fields, takes no loss and no gradient (dz = 0, so every weight
     // gradient gets exact zeros from it), and the advantage statistics are the whole minibatch's
     const bool gmode = la.sums_out != nullptr;
-    const bool my_live = !gmode || fl.idx[min(r0 + (tid >> 5), B - 1)] >= 0;     // row tid >> 5
+    const bool pre = fl.pre != nullptr && !gmode;     // fields gathered ahead: contiguous, one round trip
+    const int my_row = min(r0 + (tid >> 5), B - 1);  // row tid >> 5 (its 32-lane segment)
+    const bool my_live = !gmode || fl.idx[my_row] >= 0;
     {
         float4 th[NH], tw[NW];
         float tv[NV];
         const float4 *wp4 = reinterpret_cast<const float4 *>(P + L.oWp);
         int64_t src[NA];
+        if (pre) {
+            my_act = __float_as_int(fl.pre[my_row]);
+            my_olp = fl.pre[B + my_row];
+            my_ov = fl.pre[2 * B + my_row];
+            my_adv = fl.pre[3 * B + my_row];
+            my_ret = fl.pre[4 * B + my_row];
+        }
 #pragma unroll
-        for (int j = 0; j < NA; ++j) src[j] = frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N, gmode);
-        const int64_t my_src = frame_row(fl.idx, min(r0 + (tid >> 5), B - 1), fl.T, fl.N, gmode);
+        for (int j = 0; j < NA; ++j) src[j] = pre ? 0 : frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N, gmode);
+        const int64_t my_src = pre ? 0 : frame_row(fl.idx, my_row, fl.T, fl.N, gmode);
 #pragma unroll
         for (int j = 0; j < NH; ++j) {
             const int u = min(tid + 256 * j, nh4 - 1), r = u / H4, c4 = u - r * H4;
@@ -940,13 +957,15 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         for (int j = 0; j < NW; ++j) tw[j] = wp4[min(tid + 256 * j, np4 - 1)];
 #pragma unroll
         for (int j = 0; j < NV; ++j) tv[j] = P[L.oWv + min(tid + 256 * j, HID - 1)];
+        if (!pre) {
 #pragma unroll
-        for (int j = 0; j < NA; ++j) adv_r[j] = fl.advantages[src[j]];
-        my_act = (int)fl.actions[my_src];
-        my_olp = fl.logprobs[my_src];
-        my_ov = fl.values[my_src];
-        my_adv = fl.advantages[my_src];
-        my_ret = fl.returns[my_src];
+            for (int j = 0; j < NA; ++j) adv_r[j] = fl.advantages[src[j]];
+            my_act = (int)fl.actions[my_src];
+            my_olp = fl.logprobs[my_src];
+            my_ov = fl.values[my_src];
+            my_adv = fl.advantages[my_src];
+            my_ret = fl.returns[my_src];
+        }
 #pragma unroll
         for (int j = 0; j < NH; ++j) {
             const int u = tid + 256 * j, r = u / H4, c4 = u - r * H4;
@@ -975,9 +994,10 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     }
     GS_STAMP(0)
     float meanf = 0.f, stdf = 1.f;
-    if (la.normalize && gmode) {     // the global minibatch's statistics (gs_ppo_global_adv_stats)
-        meanf = la.adv_stats[0];
-        stdf = la.adv_stats[1];
+    if (la.normalize && (gmode || pre)) {
+        // the global minibatch's statistics (gs_ppo_global_adv_stats) or the prefetched ones
+        meanf = gmode ? la.adv_stats[0] : fl.pre_stats[0];
+        stdf = gmode ? la.adv_stats[1] : fl.pre_stats[1];
         __syncthreads();
     } else if (la.normalize) {
         batch_adv_stats_regs<NA>(adv_r, B, sred, meanf, stdf);    // its barriers cover the staging
@@ -1228,6 +1248,53 @@ __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__
     if (threadIdx.x < 5) part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s[threadIdx.x];
 }
 
+// ---- a minibatch's rollout fields through the sampler indices into pre ([5][B]: act bits, olp,
+// ov, adv, ret) and its advantage statistics into pre_stats (batch_adv_stats_regs: the same
+// values k_cnn_head_loss computes from the gathered advantages); one 256-thread workgroup
+__device__ __forceinline__ void prefetch_fields(const CnnFields &fl, int B, bool normalize, float *__restrict__ pre,
+                                                float *__restrict__ pre_stats, double *sred)
+{
+    constexpr int NA = 8;     // B <= 2048 (head_fused)
+    const int tid = threadIdx.x;
+    float adv_r[NA];
+    int64_t src[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) src[j] = frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N);
+    int act[NA];
+    float olp[NA], ov[NA], ret[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        act[j] = (int)fl.actions[src[j]];
+        olp[j] = fl.logprobs[src[j]];
+        ov[j] = fl.values[src[j]];
+        adv_r[j] = fl.advantages[src[j]];
+        ret[j] = fl.returns[src[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        const int r = tid + 256 * j;
+        if (r < B) {
+            pre[r] = __int_as_float(act[j]);
+            pre[B + r] = olp[j];
+            pre[2 * B + r] = ov[j];
+            pre[3 * B + r] = adv_r[j];
+            pre[4 * B + r] = ret[j];
+        }
+    }
+    if (normalize) {
+        float meanf, stdf;
+        batch_adv_stats_regs<NA>(adv_r, B, sred, meanf, stdf);
+        if (tid == 0) pre_stats[0] = meanf, pre_stats[1] = stdf;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cnn_prefetch(CnnFields fl, int B, int normalize, float *__restrict__ pre,
+                                                      float *__restrict__ pre_stats)
+{
+    __shared__ double sred[256 + 16];
+    prefetch_fields(fl, B, normalize != 0, pre, pre_stats, sred);
+}
+
 // one parameter of torch.optim.Adam's single-tensor step on the clipped gradient (IEEE sqrt and
 // divisions as torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step * m / denom)
 __device__ __forceinline__ float adam_flat(float g, float &m, float &v, float p, const AdamArgs &aa)
@@ -1244,7 +1311,9 @@ __device__ __forceinline__ float adam_flat(float g, float &m, float &v, float p,
 __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, float *__restrict__ G,
                                                         float *__restrict__ M, float *__restrict__ V, int64_t n,
                                                         const double *__restrict__ part, int nparts, AdamArgs aa,
-                                                        float *__restrict__ metrics, const int32_t *__restrict__ stop)
+                                                        float *__restrict__ metrics, const int32_t *__restrict__ stop,
+                                                        CnnFields next, int next_B, int next_norm,
+                                                        float *__restrict__ next_pre, float *__restrict__ next_stats)
 {
     if (stop && *stop) {
         // a job-wide stop (the exchange ORs the ranks' stop bits): no step on any rank
@@ -1256,6 +1325,13 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     __shared__ double sred[256 + 16];
     __shared__ float s_coef;
+    // next.idx set: the last block gathers the next minibatch's fields for its head + loss kernel
+    // (off the critical path, beside this launch's Adam blocks); the scalar tail moves one block up
+    const int last = gridDim.x - 1 - (next.idx ? 1 : 0);
+    if (next.idx && (int)blockIdx.x == gridDim.x - 1) {
+        prefetch_fields(next, next_B, next_norm != 0, next_pre, next_stats, sred);
+        return;
+    }
     constexpr int U = kAdamQuads;
     const int64_t n4 = n / 4;
     // this thread's parameters first (clamped, unconditional), then the norm partials
@@ -1275,7 +1351,7 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     double s[1] = {0.0};
     for (int k = threadIdx.x; k < nparts; k += 256) s[0] += part[k];
     wg_reduce<1>(s, sred);
-    if (blockIdx.x == gridDim.x - 1 && metrics) {     // per-component norms (utils/models.py:196-230)
+    if ((int)blockIdx.x == last && metrics) {     // per-component norms (utils/models.py:196-230)
         double c[4] = {0.0, 0.0, 0.0, 0.0};
         for (int k = threadIdx.x; k < nparts; k += 256)
 #pragma unroll
@@ -1317,7 +1393,7 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
         reinterpret_cast<float4 *>(V)[i] = make_float4(v[0], v[1], v[2], v[3]);
         reinterpret_cast<float4 *>(Pm)[i] = make_float4(p[0], p[1], p[2], p[3]);
     }
-    if (blockIdx.x == gridDim.x - 1)
+    if ((int)blockIdx.x == last)
         for (int64_t k = 4 * n4 + threadIdx.x; k < n; k += 256) {
             const float g = G[k] * coef;
             G[k] = g;
@@ -1608,15 +1684,27 @@ struct CnnGlobalStep {
     int64_t batch_global;
 };
 
+// k >= 0 (the local update's fused path): this step's fields were gathered into parity k & 1 of
+// the prefetch buffers, and this step's clip + Adam launch gathers next_idx's (the next
+// minibatch's) into the other parity
 int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const gs_ppo_hparams &hp,
              const gs_rollout_view_u8 &ro, const int32_t *idx, int64_t B, int64_t adam_step, float *metrics,
-             int32_t *stop, const CnnWs &w, gs_comm *comm, hipStream_t s, const CnnGlobalStep *gl = nullptr)
+             int32_t *stop, const CnnWs &w, gs_comm *comm, hipStream_t s, const CnnGlobalStep *gl = nullptr,
+             int64_t k = -1, const int32_t *next_idx = nullptr)
 {
     int rc;
+    const bool pf = k >= 0 && !gl && head_fused(L, B);
+    CnnFields next{};
+    if (pf && next_idx)
+        next = CnnFields{next_idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
     const FrameSrc fs{ro.obs, gl ? gl->frame_idx : idx, ro.T, ro.N};
     GS_REQUIRE(!gl || head_fused(L, B), "global mode: the fused head + loss kernels do not fit this shape");
     if (head_fused(L, B)) {
-        const CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
+        CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
+        if (pf) {
+            fl.pre = w.pre + (k & 1) * 5 * B;
+            fl.pre_stats = w.pre_stats + (k & 1) * 2;
+        }
         LossArgs la = loss_args(hp);
         if (gl) {
             la.adv_stats = gl->adv_stats;
@@ -1651,9 +1739,10 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     }
     hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
                        L.oWv);
-    hipLaunchKernelGGL(k_clip_adam_flat, dim3((unsigned)((L.P / 4 + 256 * kAdamQuads - 1) / (256 * kAdamQuads) + 1)),
-                       dim3(256), 0, s, P, G, Mm, Vv,
-                       L.P, w.norm_part, kNormBlocks, aa, metrics, stop);
+    const unsigned nadam = (unsigned)((L.P / 4 + 256 * kAdamQuads - 1) / (256 * kAdamQuads) + 1 + (next.idx ? 1 : 0));
+    hipLaunchKernelGGL(k_clip_adam_flat, dim3(nadam), dim3(256), 0, s, P, G, Mm, Vv, L.P, w.norm_part, kNormBlocks, aa,
+                       metrics, stop, next, (int)B, hp.normalize_adv ? 1 : 0, w.pre + ((k + 1) & 1) * 5 * B,
+                       w.pre_stats + ((k + 1) & 1) * 2);
     GS_LAUNCH_CHECK("k_clip_adam_flat");
     return GS_OK;
 }
@@ -1793,9 +1882,17 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
+    // the first minibatch's fields gathered up front; each step's clip + Adam launch gathers the next
+    if (n_minibatches > 0 && head_fused(L, batch)) {
+        const CnnFields f0{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
+        hipLaunchKernelGGL(k_cnn_prefetch, dim3(1), dim3(256), 0, s, f0, (int)batch, hp.normalize_adv ? 1 : 0, w.pre,
+                           w.pre_stats);
+        GS_LAUNCH_CHECK("k_cnn_prefetch");
+    }
     for (int64_t k = 0; k < n_minibatches; ++k) {
         rc = cnn_step(params, grads, adam_m, adam_v, L, hp, ro, idx + k * batch, batch, adam_step0 + k + 1,
-                      metrics + k * GS_NUM_METRICS, stop_flag, w, comm, s);
+                      metrics + k * GS_NUM_METRICS, stop_flag, w, comm, s, nullptr, k,
+                      k + 1 < n_minibatches ? idx + (k + 1) * batch : nullptr);
         if (rc) return rc;
     }
     return GS_OK;
