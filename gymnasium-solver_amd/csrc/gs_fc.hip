@@ -42,6 +42,9 @@ struct FcK {
     static constexpr int RB = 128 * KT + 16;         // LDS bytes per staged row
 };
 
+#ifndef FC_MI16
+#define FC_MI16 1           // fp32 on v_mfma_f32_16x16x4_f32 (0: the 32 x 32 x 2 form, for A/B runs)
+#endif
 #ifndef FC_XCD
 #define FC_XCD 1            // XCD-aware tile order (0: plain blockIdx order, for A/B runs)
 #endif
@@ -321,6 +324,153 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
         }
 }
 
+// k_fc16: the fp32 form on v_mfma_f32_16x16x4_f32 (exact fp32) — a wave's (BM/WGM) x (BN/WGN)
+// outputs as 16 x 16 blocks (more independent accumulators per wave than the 32 x 32 form, the
+// shape the vendor library picks for these GEMMs).  Same staging, buffers, tile order and KS split
+// as k_fc; a 16-k chunk c of a tile: lane (r = lane & 15, q = lane >> 4) reads the 16 B at
+// k = 16 c + 4 q .. + 3 of its row, and MFMA e takes element e — the four MFMAs of a chunk cover
+// its 16 k once each, the same k in both operands.
+template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD, int KT>
+__global__ __launch_bounds__(256, 2) void k_fc16(const float *__restrict__ A, int64_t lda, const float *__restrict__ Bm,
+                                                 int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
+                                                 const float *__restrict__ aux, const int32_t *__restrict__ stop,
+                                                 int64_t sC, int gm)
+{
+    if (stop && *stop) return;      // KL early stop: the minibatch's product is never used
+    A += (AK ? 1 : lda) * (int64_t)blockIdx.z * K;
+    Bm += (BKC ? 1 : ldb) * (int64_t)blockIdx.z * K;
+    C += (int64_t)blockIdx.z * sC;
+    constexpr int WGN = 4 / (WGM * KS);
+    static_assert(WGM * WGN * KS == 4, "4 waves");
+    constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+    static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "16 x 16 blocks");
+    using K_ = FcK<false, KT>;
+    constexpr int KE = K_::KE, RB = K_::RB, NC = KE / 16, NCW = NC / KS;
+    static_assert(NC % KS == 0, "16-k chunks split evenly over KS");
+    constexpr int TILE = (BM + BN) * RB;
+    __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
+
+    int bx = blockIdx.x, by = blockIdx.y;
+    {
+        const int nbx = gridDim.x, nby = gridDim.y, T = nbx * nby;
+        if (FC_XCD && T % 8 == 0 && gm > 0) {
+            const int b = by * nbx + bx;
+            const int t = (b & 7) * (T >> 3) + (b >> 3);
+            const int gsize = gm * nbx, grp = t / gsize, first = grp * gm, gcnt = min(nby - first, gm);
+            const int within = t - grp * gsize;
+            by = first + within % gcnt;
+            bx = within / gcnt;
+        }
+    }
+    const int m0 = by * BM, n0 = bx * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ks = wave % KS, wmn = wave / KS;
+    const int wm = (wmn / WGN) * WM, wn = (wmn % WGN) * WN;
+    const int r16 = lane & 15, q4 = lane >> 4;
+
+    Stage<BM, false, AK, KT> sa[PD];
+    Stage<BN, false, BKC, KT> sb[PD];
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / KE;
+    auto kof = [&](int t) { return min(t, nk - 1) * KE; };
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+        sa[u].load(A, lda, m0, M, kof(u));
+        sb[u].load(Bm, ldb, n0, N, kof(u));
+    }
+    sa[0].store(lds, m0, M);
+    sb[0].store(lds + BM * RB, n0, N);
+    __syncthreads();
+    sa[0].load(A, lda, m0, M, kof(PD));
+    sb[0].load(Bm, ldb, n0, N, kof(PD));
+    for (int kt0 = 0; kt0 < nk; kt0 += PD) {
+        static_for<0, PD>([&](auto uc) -> bool {
+            constexpr int u = decltype(uc)::value;
+            const int kt = kt0 + u;
+            if (kt >= nk) return false;
+            const char *buf = lds + (kt & 1) * TILE;
+            float4 a[NCW][TM], b[NCW][TN];
+#pragma unroll
+            for (int q = 0; q < NCW; ++q) {
+                const int c = ks + KS * q;
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    a[q][i] = *reinterpret_cast<const float4 *>(buf + (wm + 16 * i + r16) * RB + 64 * c + 16 * q4);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    b[q][j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 16 * j + r16) * RB + 64 * c + 16 * q4);
+            }
+#pragma unroll
+            for (int q = 0; q < NCW; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4at(a[q][i], e), f4at(b[q][j], e),
+                                                                             acc[i][j], 0, 0, 0);
+            constexpr int nv = (u + 1) % PD;
+            char *nb = lds + ((kt + 1) & 1) * TILE;
+            sa[nv].store(nb, m0, M);
+            sb[nv].store(nb + BM * RB, n0, N);
+            __syncthreads();
+            sa[nv].load(A, lda, m0, M, kof(kt + 1 + PD));
+            sb[nv].load(Bm, ldb, n0, N, kof(kt + 1 + PD));
+            return true;
+        });
+    }
+    if constexpr (KS > 1) {
+        float *red = reinterpret_cast<float *>(lds);
+        constexpr int PW = TM * TN * 4 * 64;
+        static_assert((KS - 1) * (4 / KS) * PW * 4 <= 2 * TILE, "KS reduction fits the LDS tiles");
+        if (ks > 0)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        red[(((ks - 1) * (4 / KS) + wmn) * TM * TN + i * TN + j) * 4 * 64 + v * 64 + lane] = acc[i][j][v];
+        __syncthreads();
+        if (ks > 0) return;
+        for (int q = 1; q < KS; ++q)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        acc[i][j][v] += red[(((q - 1) * (4 / KS) + wmn) * TM * TN + i * TN + j) * 4 * 64 + v * 64 + lane];
+    }
+    // epilogue: D col = lane & 15, row = 4 (lane >> 4) + v of each 16 x 16 block
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int gn = n0 + wn + 16 * j + r16;
+            if (gn >= N) continue;
+            const float bn = EPI == kEpiBiasRelu ? aux[gn] : 0.0f;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int gmr = m0 + wm + 16 * i + 4 * q4 + v;
+                if (gmr >= M) continue;
+                float x = acc[i][j][v];
+                if constexpr (EPI == kEpiBiasRelu) {
+                    x += bn;
+                    x = x > 0.0f ? x : 0.0f;
+                }
+                if constexpr (EPI == kEpiMask) x = aux[(int64_t)gmr * ldc + gn] > 0.0f ? x : 0.0f;
+                C[(int64_t)gmr * ldc + gn] = x;
+            }
+        }
+}
+
 template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16, int KT32, int KT16>
 int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
               int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop, int gm, int splits = 1,
@@ -331,6 +481,9 @@ int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *
     if (bf)
         hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16>), grid, dim3(256), 0, s, A, lda, B,
                            ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+    else if (FC_MI16)
+        hipLaunchKernelGGL((k_fc16<BM, BN, WGM, KS, AK, BKC, EPI, PD32, KT32>), grid, dim3(256), 0, s, A, lda, B, ldb, C,
+                           ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
     else
         hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32>), grid, dim3(256), 0, s, A, lda, B,
                            ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
