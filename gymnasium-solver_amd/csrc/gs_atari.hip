@@ -42,17 +42,27 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x)
 }
 
 // ---- per-env counters, rewards, dones (fixed-length episodes starting e mod L steps in)
-__global__ __launch_bounds__(256) void k_atari_counters(int32_t *__restrict__ state, float *__restrict__ ep_ret,
-                                                        int64_t N, int L, int trunc_every, uint64_t seed,
-                                                        int64_t env_offset, uint64_t step_count,
-                                                        float *__restrict__ rew_row, uint8_t *__restrict__ done_row,
-                                                        uint8_t *__restrict__ to_row, int32_t *__restrict__ ep_cnt,
-                                                        float *__restrict__ ep_ret_sum, float *__restrict__ ep_len_sum,
-                                                        const uint64_t *__restrict__ clock)
+struct AtariCounters {
+    int32_t *state;
+    float *ep_ret;
+    int L, trunc_every;
+    float *rew_row;
+    uint8_t *done_row, *to_row;
+    int32_t *ep_cnt;
+    float *ep_ret_sum, *ep_len_sum;
+};
+
+// env e's step (step_count already includes the rollout clock)
+__device__ __forceinline__ void atari_counters(int64_t e, const AtariCounters &c, uint64_t seed, int64_t env_offset,
+                                               uint64_t step_count)
 {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= N) return;
-    if (clock) step_count += clock[1];      // rollout clock (graph replay)
+    int32_t *__restrict__ state = c.state;
+    float *__restrict__ ep_ret = c.ep_ret;
+    const int L = c.L, trunc_every = c.trunc_every;
+    float *__restrict__ rew_row = c.rew_row;
+    uint8_t *__restrict__ done_row = c.done_row, *__restrict__ to_row = c.to_row;
+    int32_t *__restrict__ ep_cnt = c.ep_cnt;
+    float *__restrict__ ep_ret_sum = c.ep_ret_sum, *__restrict__ ep_len_sum = c.ep_len_sum;
     const uint64_t ge = (uint64_t)(env_offset + e);
     int k = state[4 * e + 0] + 1;
     int epi = state[4 * e + 1];
@@ -90,14 +100,18 @@ constexpr int kRenderPairs = 2;
 constexpr int kRenderChunks = (kFramePairs + 256 * kRenderPairs - 1) / (256 * kRenderPairs);
 static_assert(kFrameWords % 2 == 0 && kFrameBytes % 16 == 0, "16-B frame pairs");
 
+// COUNTERS: the env step's counters ride along — env e's on thread 0 of workgroup (0, 2e) (one
+// launch less per step; the counters and the frames read nothing of each other)
+template <bool COUNTERS>
 __global__ __launch_bounds__(256) void k_atari_render(uint8_t *__restrict__ frames, int64_t N, uint64_t seed,
                                                       int64_t env_offset, uint64_t step_count,
-                                                      const uint64_t *__restrict__ clock)
+                                                      const uint64_t *__restrict__ clock, AtariCounters cnt)
 {
     if (clock) step_count += clock[1];
     const int64_t ej = blockIdx.y;              // env * 2 + frame
     const int64_t e = ej >> 1;
     const int j = (int)(ej & 1);
+    if (COUNTERS && blockIdx.x == 0 && j == 0 && threadIdx.x == 0) atari_counters(e, cnt, seed, env_offset, step_count);
     const uint64_t ge = (uint64_t)(env_offset + e);
     const uint64_t hf = mix64(mix64(mix64(seed) ^ ge) ^ (2 * step_count + (uint64_t)j));
     ulonglong2 *out = reinterpret_cast<ulonglong2 *>(frames + ej * (int64_t)kFrameBytes);
@@ -394,8 +408,8 @@ extern "C" int gs_atari_render(uint8_t *frames, int64_t N, uint64_t seed, int64_
                                void *stream)
 {
     GS_REQUIRE(N > 0 && N <= kMaxAtariEnvs && frames, "gs_atari_render: bad argument");
-    hipLaunchKernelGGL(k_atari_render, render_grid(N), dim3(256), 0, (hipStream_t)stream, frames,
-                       N, seed, env_offset, step_count, (const uint64_t *)nullptr);
+    hipLaunchKernelGGL(k_atari_render<false>, render_grid(N), dim3(256), 0, (hipStream_t)stream, frames,
+                       N, seed, env_offset, step_count, (const uint64_t *)nullptr, AtariCounters{});
     GS_LAUNCH_CHECK("k_atari_render");
     return GS_OK;
 }
@@ -419,8 +433,8 @@ extern "C" int gs_atari_env_reset(int32_t *state, float *ep_ret, uint8_t *stack,
     GS_HIP(hipMemcpyAsync(state, st.data(), st.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
     GS_HIP(hipStreamSynchronize(s));   // pageable source: keep it alive until copied
     GS_HIP(hipMemsetAsync(ep_ret, 0, sizeof(float) * N, s));
-    hipLaunchKernelGGL(k_atari_render, render_grid(N), dim3(256), 0, s, frames, N, seed,
-                       env_offset, (uint64_t)0, (const uint64_t *)nullptr);
+    hipLaunchKernelGGL(k_atari_render<false>, render_grid(N), dim3(256), 0, s, frames, N, seed,
+                       env_offset, (uint64_t)0, (const uint64_t *)nullptr, AtariCounters{});
     return launch_stack(frames, nullptr, N, stack_n, out_h, out_w, stack, s);
 }
 
@@ -437,10 +451,10 @@ extern "C" int gs_atari_env_step(int32_t *state, float *ep_ret, uint8_t *stack, 
     if (rc) return rc;
     if ((rc = ensure_tables(out_h, out_w))) return rc;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_atari_counters, dim3(nblk(N)), dim3(256), 0, s, state, ep_ret, N, episode_len, truncate_every,
-                       seed, env_offset, step_count, rewards_row, dones_row, timeouts_row, ep_done_count, ep_ret_sum,
-                       ep_len_sum, clock);
-    hipLaunchKernelGGL(k_atari_render, render_grid(N), dim3(256), 0, s, frames, N, seed,
-                       env_offset, step_count, clock);
+    // counters (rewards, dones, episode records) inside the render launch; the stack reads the done row
+    const AtariCounters cnt{state, ep_ret, episode_len, truncate_every, rewards_row, dones_row, timeouts_row,
+                            ep_done_count, ep_ret_sum, ep_len_sum};
+    hipLaunchKernelGGL(k_atari_render<true>, render_grid(N), dim3(256), 0, s, frames, N, seed, env_offset, step_count,
+                       clock, cnt);
     return launch_stack(frames, dones_row, N, stack_n, out_h, out_w, stack, s);
 }

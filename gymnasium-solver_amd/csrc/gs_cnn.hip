@@ -404,6 +404,83 @@ __device__ __forceinline__ void act_select(const float (&zr)[AM + 1], float v, i
     logp[r] = za - h.lse;
 }
 
+// ---- act_select on one wave (lane a = action a, A + 1 <= 64): each lane's head output from the
+// slice sums zsum[a][8] (in slice order) + its bias; the row statistics as fixed xor trees over the
+// wave (lane 0's value broadcast); lane 0 then walks the probabilities in action order for the
+// argmax / inverse-CDF draw exactly as act_select does (the cumulative sum stays sequential)
+__device__ __forceinline__ float wave_max(float x)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x = fmaxf(x, __shfl_xor(x, off));
+    return x;
+}
+__device__ __forceinline__ float wave_sum(float x)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+    return __shfl(x, 0);
+}
+
+__device__ __forceinline__ void act_select_wave(const float *__restrict__ zsum, int64_t r, const float *__restrict__ P,
+                                                const CnnLayout &L, int mode, uint64_t seed, uint64_t counter,
+                                                int64_t *__restrict__ actions, float *__restrict__ logp,
+                                                float *__restrict__ value, const uint64_t *__restrict__ clock)
+{
+    __shared__ float pz[64];
+    const int a = threadIdx.x & 63, A = L.A;
+    float z = 0.f;
+    if (a <= A) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) z += zsum[a * 8 + q];
+        z += a < A ? P[L.obp + a] : P[L.obv];
+    }
+    const float v = __shfl(z, A);
+    if (a == 0 && value) value[r] = v;
+    if (!actions) return;
+    const bool va = a < A && L.is_valid(a);
+    const float m = wave_max(va ? z : -INFINITY);
+    const float se = wave_sum(va ? expf(z - m) : 0.f);
+    const float lse = m + logf(se);
+    const float m2 = wave_max(va ? z - lse : -INFINITY);
+    const float S = wave_sum(va ? expf((z - lse) - m2) : 0.f);
+    pz[a] = va ? expf((z - lse) - m2) / S : -1.0f;     // -1: not a valid action
+    const float zl = z - lse;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int act = -1;
+    if (a == 0) {
+        if (mode == 2) {
+            act = (int)actions[r];
+        } else if (mode == 1) {
+            float best = -INFINITY;
+            for (int b = 0; b < A; ++b) {
+                const float p = pz[b];
+                if (p >= 0.f && p > best) best = p, act = b;
+            }
+            actions[r] = act;
+        } else {
+            const uint64_t ctr = counter + (clock ? clock[0] : 0ull);   // rollout clock (graph replay)
+            const uint64_t hh = mix64d(mix64d(mix64d(seed) ^ ctr) ^ (uint64_t)r);
+            const float u = (float)(hh >> 40) * (1.0f / 16777216.0f);
+            float c = 0.f;
+            int last = 0;
+            for (int b = 0; b < A; ++b) {
+                const float p = pz[b];
+                if (p < 0.f) continue;
+                last = b;
+                c += p;
+                if (act < 0 && u < c) act = b;
+            }
+            if (act < 0) act = last;
+            actions[r] = act;
+        }
+    }
+    act = __shfl(act, 0);
+    const float za = __shfl(zl, min(max(act, 0), 63));
+    if (a == 0) logp[r] = za;
+}
+
 // ---- the rollout's fc epilogue + heads + action select in one launch, one workgroup per env:
 // thread t takes j = t, t + 256 (HID <= 512): h[j] = relu(bf[j] + the fc's split-K partials
 // summed in slice order) and its products with the A + 1 head rows — every load of a thread is
@@ -466,21 +543,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ 
         red2[tid] = g;
     }
     __syncthreads();
-    if (tid == 0) {
-        float zr[AM + 1];
-        float v = 0.f;
-#pragma unroll
-        for (int a = 0; a < AM + 1; ++a) {
-            float z = 0.f;
-            if (a < A1) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) z += red2[a * 8 + q];
-            }
-            zr[a] = a < A1 ? z + (a < A ? P[L.obp + a] : P[L.obv]) : 0.f;
-            if (a == A) v = zr[a];
-        }
-        act_select<AM>(zr, v, r, L, mode, seed, counter, actions, logp, value, clock);
-    }
+    if (tid < 64) act_select_wave(red2, r, P, L, mode, seed, counter, actions, logp, value, clock);
 }
 
 // ---- gather the 5 per-row rollout fields of the minibatch
