@@ -17,9 +17,10 @@
 //   bf16 (GS_HP_BF16, v_mfma_f32_32x32x16_bf16): the tile is converted to bf16 (round to nearest
 //        even) as it is staged; lane (r, q) reads 8 bf16 at k0 + 8q: one MFMA per 16-k group.
 // A K tile is KT x 128 B of every row plus a 16-B pad, two LDS buffers, PD register sets of
-// tiles in flight, one barrier per tile.  Launch shapes: fwd 64 x 32 with the 4 waves splitting
-// the k-groups (KS = 4: 256 workgroups, each wave two 32 x 32 accumulators), wgrad / dgrad
-// 64 x 64 (392 / 784 workgroups, two resident per CU); fp32 tiles are 64 deep (KT = 2).
+// tiles in flight, one barrier per tile.  Launch shapes (same-box fc_bench sweeps):
+// fwd 32 x 32 with the 4 waves splitting the k-groups (KS = 4: 512 workgroups, two per CU);
+// wgrad 64 x 64 on 32x32x2 MFMAs and dgrad 64 x 64 on 16x16x4 blocks (k_fc16) in fp32 (392 / 784
+// workgroups); fp32 tiles are 64 deep (KT = 2).
 #include <type_traits>
 
 #include "gs_gemm.h"
@@ -471,7 +472,8 @@ __global__ __launch_bounds__(256, 2) void k_fc16(const float *__restrict__ A, in
         }
 }
 
-template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16, int KT32, int KT16>
+template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16, int KT32, int KT16,
+          bool MI16 = false>
 int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
               int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop, int gm, int splits = 1,
               int64_t sC = 0)
@@ -481,7 +483,7 @@ int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *
     if (bf)
         hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16>), grid, dim3(256), 0, s, A, lda, B,
                            ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
-    else if (FC_MI16)
+    else if (MI16 && FC_MI16)
         hipLaunchKernelGGL((k_fc16<BM, BN, WGM, KS, AK, BKC, EPI, PD32, KT32>), grid, dim3(256), 0, s, A, lda, B, ldb, C,
                            ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
     else
@@ -507,9 +509,9 @@ bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
 
 int fc_fwd_splits(int64_t M, int64_t N, int64_t K)
 {
-    // the largest split of K into 64-multiples that keeps the 64 x 32 tiles x splits within 512
+    // the largest split of K into 64-multiples that keeps the 32 x 32 tiles x splits within 512
     // workgroups (at most 16 slices)
-    const int64_t tiles = ((M + 63) / 64) * ((N + 31) / 32);
+    const int64_t tiles = ((M + 31) / 32) * ((N + 31) / 32);
     int best = 1;
     for (int sp = 2; sp <= 16; ++sp)
         if (K % (64 * sp) == 0 && tiles * sp <= 512) best = sp;
@@ -523,7 +525,7 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
                "fc_fwd_partials: shape %lld x %lld x %lld / %d not supported", (long long)M, (long long)N,
                (long long)K, splits);
     GS_REQUIRE(aligned16(A) && aligned16(B), "fc_fwd_partials: 16-B aligned operands required");
-    return launch_fc<64, 32, 1, 4, true, true, kEpiStore, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(
+    return launch_fc<32, 32, 1, 4, true, true, kEpiStore, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(
         s, false, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 4, splits, M * ldc);
 }
 
@@ -536,14 +538,14 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
     GS_REQUIRE(aligned16(A) && aligned16(B) && (op == 1 || aux), "fc_gemm: 16-B aligned operands (and the epilogue "
                "operand) required");
     if (op == 0)     // fwd: C = relu(A B^T + bias), both K-contiguous
-        return launch_fc<64, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
+        return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
                                                                                            ldc, M, N, K, aux, stop, 4);
     if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]
         return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1>(s, bf16, A, lda, B, ldb, C,
                                                                                             ldc, M, N, K, nullptr, stop, 8);
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
-    return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1>(s, bf16, A, lda, B, ldb, C, ldc,
-                                                                                          M, N, K, aux, stop, 16);
+    return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1, true>(s, bf16, A, lda, B, ldb, C,
+                                                                                                ldc, M, N, K, aux, stop, 16);
 }
 
 }  // namespace gs
