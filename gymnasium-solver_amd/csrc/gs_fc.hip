@@ -43,6 +43,9 @@ struct FcK {
     static constexpr int RB = 128 * KT + 16;         // LDS bytes per staged row
 };
 
+#ifndef FC_SWZ
+#define FC_SWZ 1            // LDS chunk swizzle (0: plain chunk order, for A/B runs)
+#endif
 #ifndef FC_MI16
 #define FC_MI16 1           // fp32 on v_mfma_f32_16x16x4_f32 (0: the 32 x 32 x 2 form, for A/B runs)
 #endif
@@ -78,6 +81,13 @@ __device__ __forceinline__ uint2 pack_bf16x4(float4 v)
     r[0] = (__bf16)v.x, r[1] = (__bf16)v.y, r[2] = (__bf16)v.z, r[3] = (__bf16)v.w;
     return *reinterpret_cast<uint2 *>(&r);
 }
+
+// LDS chunk swizzle: the 16-B chunk c of staged row r lives at chunk c ^ swz(r).  A K-strided
+// staging store writes rows 4 apart from consecutive lanes (row stride 4 (mod 64) dwords, so 16
+// (mod 64) every 4 rows: 4-way bank conflicts without it); XOR-ing the chunk with bits 4-5 of the
+// row spreads those lanes over all banks, and the operand reads (16 consecutive rows, one swizzle
+// value per 16-row group) stay conflict-free
+__device__ __forceinline__ int swz(int row) { return FC_SWZ ? (row >> 4) & 3 : 0; }
 
 __device__ __forceinline__ float f4at(const float4 &v, int c)
 {
@@ -127,8 +137,9 @@ struct Stage {
                 const bool ok = row0 + row < n_rows;
                 const float4 v = ok ? r[j][0] : make_float4(0.f, 0.f, 0.f, 0.f);
                 char *dst = lds + row * RB;
-                if constexpr (BF) *reinterpret_cast<uint2 *>(dst + 8 * k4) = pack_bf16x4(v);
-                else *reinterpret_cast<float4 *>(dst + 16 * k4) = v;
+                if constexpr (BF)
+                    *reinterpret_cast<uint2 *>(dst + 16 * ((k4 >> 1) ^ swz(row)) + 8 * (k4 & 1)) = pack_bf16x4(v);
+                else *reinterpret_cast<float4 *>(dst + 16 * (k4 ^ swz(row))) = v;
             } else {
                 const int kb = u / (ROWS / 4), rb = u - kb * (ROWS / 4);
                 const bool ok = row0 + 4 * rb < n_rows;
@@ -139,8 +150,10 @@ struct Stage {
                                                       f4at(r[j][3], c))
                                         : make_float4(0.f, 0.f, 0.f, 0.f);
                     char *dst = lds + (4 * rb + c) * RB;
-                    if constexpr (BF) *reinterpret_cast<uint2 *>(dst + 8 * kb) = pack_bf16x4(v);
-                    else *reinterpret_cast<float4 *>(dst + 16 * kb) = v;
+                    const int sr = swz(4 * rb + c);
+                    if constexpr (BF)
+                        *reinterpret_cast<uint2 *>(dst + 16 * ((kb >> 1) ^ sr) + 8 * (kb & 1)) = pack_bf16x4(v);
+                    else *reinterpret_cast<float4 *>(dst + 16 * (kb ^ sr)) = v;
                 }
             }
         }
@@ -242,10 +255,12 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
                 const int g = ks + KS * q;
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
-                    a[q][i] = *reinterpret_cast<const float4 *>(buf + (wm + 32 * i + l32) * RB + 32 * g + 16 * lh);
+                    a[q][i] = *reinterpret_cast<const float4 *>(buf + (wm + 32 * i + l32) * RB +
+                                                                16 * ((2 * g + lh) ^ swz(wm + 32 * i + l32)));
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    b[q][j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 32 * j + l32) * RB + 32 * g + 16 * lh);
+                    b[q][j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 32 * j + l32) * RB +
+                                                                16 * ((2 * g + lh) ^ swz(wn + 32 * j + l32)));
             }
 #pragma unroll
             for (int q = 0; q < NGW; ++q) {
@@ -401,10 +416,12 @@ __global__ __launch_bounds__(256, 2) void k_fc16(const float *__restrict__ A, in
                 const int c = ks + KS * q;
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
-                    a[q][i] = *reinterpret_cast<const float4 *>(buf + (wm + 16 * i + r16) * RB + 64 * c + 16 * q4);
+                    a[q][i] = *reinterpret_cast<const float4 *>(buf + (wm + 16 * i + r16) * RB +
+                                                                16 * ((4 * c + q4) ^ swz(wm + 16 * i + r16)));
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    b[q][j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 16 * j + r16) * RB + 64 * c + 16 * q4);
+                    b[q][j] = *reinterpret_cast<const float4 *>(buf + (BM + wn + 16 * j + r16) * RB +
+                                                                16 * ((4 * c + q4) ^ swz(wn + 16 * j + r16)));
             }
 #pragma unroll
             for (int q = 0; q < NCW; ++q)
