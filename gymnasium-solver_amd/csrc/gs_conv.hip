@@ -20,6 +20,8 @@
 //                 k_sum_partials (deterministic).
 // Frame rows come through the minibatch index exactly like the generic loader (env-major
 // sample index -> (t, env) row of the (T, N) rollout buffer).
+#include <type_traits>
+
 #include "gs_conv.h"
 #include "gs_gemm.h"
 
@@ -67,8 +69,8 @@ __device__ __forceinline__ int64_t frame_src(const int32_t *idx, int64_t r, int6
 // every thread issues all of its u32 loads before converting any (one memory latency).  copy:
 // the sample's u8 stack elsewhere (the rollout row), rows [ylo, yhi) of it written from the same
 // loaded words
-template <class G>
-__device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict__ obs, int64_t src, int y0,
+template <class G, typename FT = float>
+__device__ __forceinline__ void stage_band(FT *fr, const uint8_t *__restrict__ obs, int64_t src, int y0,
                                            uint8_t *__restrict__ copy = nullptr, int ylo = 0, int yhi = 0)
 {
     constexpr int NE = G::C * G::BIR * G::W4, PER = (NE + 255) / 256;
@@ -93,7 +95,14 @@ __device__ __forceinline__ void stage_band(float *fr, const uint8_t *__restrict_
             const int y = rem / G::W4, x4 = rem - y * G::W4;
             const float4 f = make_float4((float)(v[j] & 255u) / 255.0f, (float)((v[j] >> 8) & 255u) / 255.0f,
                                          (float)((v[j] >> 16) & 255u) / 255.0f, (float)(v[j] >> 24) / 255.0f);
-            *reinterpret_cast<float4 *>(fr + (c * G::BIR + y) * G::W + 4 * x4) = f;
+            if constexpr (sizeof(FT) == 2) {      // bf16 staging (GS_HP_BF16): rounded once here
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                bf16x4 h;
+                h[0] = (__bf16)f.x, h[1] = (__bf16)f.y, h[2] = (__bf16)f.z, h[3] = (__bf16)f.w;
+                *reinterpret_cast<bf16x4 *>(fr + (c * G::BIR + y) * G::W + 4 * x4) = h;
+            } else {
+                *reinterpret_cast<float4 *>(fr + (c * G::BIR + y) * G::W + 4 * x4) = f;
+            }
             if (copy && y0 + y >= ylo && y0 + y < yhi)
                 *reinterpret_cast<uint32_t *>(copy + ((int64_t)c * G::H + y0 + y) * G::W + 4 * x4) = v[j];
         }
@@ -110,7 +119,9 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
 {
     // obs_copy (the rollout's obs row, idx == nullptr): band b copies rows [b H / NB, (b + 1) H / NB)
     static_assert(G::bands_cover(), "the bands cover the obs copy's row ranges");
-    __shared__ __attribute__((aligned(16))) float fr[G::FRAME];
+    // BF: the band staged as bf16 (u8 / 255 rounded once; half the LDS, more workgroups per CU)
+    using FT = typename std::conditional<BF, uint16_t, float>::type;
+    __shared__ __attribute__((aligned(16))) FT fr[G::FRAME];
     const int r = blockIdx.x / G::NB, band = blockIdx.x - r * G::NB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
@@ -127,7 +138,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
         const int c = g >> 2, ky = 2 * (g & 3) + (lq >> 1), kx0 = 4 * (lq & 1);
         b[g] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
     }
-    stage_band<G>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S,
+    stage_band<G, FT>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S,
                   obs_copy ? obs_copy + (int64_t)r * (G::C * G::H * G::W) : nullptr, band * (G::H / G::NB),
                   (band + 1) * (G::H / G::NB));
     __syncthreads();
@@ -158,21 +169,23 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
 #pragma unroll
             for (int t = 0; t < TMW; ++t) {
                 if (tpar + 2 * t >= G::MT) break;
-                const bf16x8 a = bf16_frag(*reinterpret_cast<const float4 *>(fr + abase[t] + goff0),
-                                           *reinterpret_cast<const float4 *>(fr + abase[t] + goff1));
-                acc[t] = mfma16_bf16(a, bw[gp], acc[t]);
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                const bf16x4 lo = *reinterpret_cast<const bf16x4 *>(fr + abase[t] + goff0);
+                const bf16x4 hi = *reinterpret_cast<const bf16x4 *>(fr + abase[t] + goff1);
+                acc[t] = mfma16_bf16(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), bw[gp], acc[t]);
             }
         }
     } else
 #pragma unroll
     for (int g = 0; g < G::KS / 4; ++g) {
         const int goff = ((g >> 2) * G::BIR + 2 * (g & 3)) * G::W;
+        const float *ff = reinterpret_cast<const float *>(fr);
 #pragma unroll
         for (int t = 0; t < TMW; t += 2) {
             const bool two = t + 1 < TMW && tpar + 2 * (t + 1) < G::MT;
             if (tpar + 2 * t >= G::MT) break;
-            const float4 a0 = *reinterpret_cast<const float4 *>(fr + abase[t] + goff);
-            const float4 a1 = two ? *reinterpret_cast<const float4 *>(fr + abase[t + 1] + goff) : a0;
+            const float4 a0 = *reinterpret_cast<const float4 *>(ff + abase[t] + goff);
+            const float4 a1 = two ? *reinterpret_cast<const float4 *>(ff + abase[t + 1] + goff) : a0;
             acc[t] = mfma(a0.x, b[g].x, acc[t]);
             if (two) acc[t + 1] = mfma(a1.x, b[g].x, acc[t + 1]);
             acc[t] = mfma(a0.y, b[g].y, acc[t]);
@@ -422,9 +435,15 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
     constexpr int NFB = 4 / FS;                    // filter blocks per workgroup
     constexpr int NGW = G::NG / FS;                // k-step groups per wave
     static_assert(G::NG % FS == 0 && (!BF || NGW % 2 == 0), "k-step groups split evenly (bf16: in pairs)");
-    static_assert(FS == 1 || (FS - 1) * NFB * G::MT * 4 * 64 <= G::SPB * G::H * G::W * G::CS,
+    // BF (GS_HP_BF16): the tile is staged as bf16 (rounded once, at the store — the same value
+    // the fp32 tile gave at each operand read), half the LDS bytes and reads; the position
+    // stride CS stays in elements, so a position is S CS / 2 = 36 (mod 64) dwords from the next
+    // and the 16 positions of an 8-B operand read land on distinct banks
+    using XT = typename std::conditional<BF, uint16_t, float>::type;
+    constexpr int XS = G::SPB * G::H * G::W * G::CS;
+    static_assert(FS == 1 || (FS - 1) * NFB * G::MT * 4 * 64 * 4 <= XS * (int)sizeof(XT),
                   "the k-range partials fit the staging tile");
-    __shared__ __attribute__((aligned(16))) float xs[G::SPB * G::H * G::W * G::CS];
+    __shared__ __attribute__((aligned(16))) XT xs[XS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
     const int sg = FS == 1 ? blockIdx.x : blockIdx.x / FS, fpart = FS == 1 ? 0 : blockIdx.x - sg * FS;
@@ -457,7 +476,14 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
                 const int e = e0 + tid + 256 * j;
                 if (e < NE) {
                     const int pos = e / C4, c4 = e - pos * C4;
-                    *reinterpret_cast<float4 *>(xs + pos * G::CS + 4 * c4) = v[j];
+                    if constexpr (BF) {
+                        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                        bf16x4 h;
+                        h[0] = (__bf16)v[j].x, h[1] = (__bf16)v[j].y, h[2] = (__bf16)v[j].z, h[3] = (__bf16)v[j].w;
+                        *reinterpret_cast<bf16x4 *>(xs + pos * G::CS + 4 * c4) = h;
+                    } else {
+                        *reinterpret_cast<float4 *>(xs + pos * G::CS + 4 * c4) = v[j];
+                    }
                 }
             }
         }
@@ -491,8 +517,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
             const int o0 = goff(g0 + 2 * gp), o1 = goff(g0 + 2 * gp + 1);
 #pragma unroll
             for (int t = 0; t < G::MT; ++t) {
-                const bf16x8 a = bf16_frag(*reinterpret_cast<const float4 *>(xs + abase[t] + o0),
-                                           *reinterpret_cast<const float4 *>(xs + abase[t] + o1));
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                const bf16x4 lo = *reinterpret_cast<const bf16x4 *>(xs + abase[t] + o0);
+                const bf16x4 hi = *reinterpret_cast<const bf16x4 *>(xs + abase[t] + o1);
+                const bf16x8 a = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
                 acc[t] = mfma16_bf16(a, bw, acc[t]);
             }
         }
@@ -500,10 +528,11 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
 #pragma unroll
     for (int g = 0; g < NGW; ++g) {
         const int off = goff(g0 + g);
+        const float *xf = reinterpret_cast<const float *>(xs);
 #pragma unroll
         for (int t = 0; t < G::MT; t += 2) {
-            const float4 a0 = *reinterpret_cast<const float4 *>(xs + abase[t] + off);
-            const float4 a1 = t + 1 < G::MT ? *reinterpret_cast<const float4 *>(xs + abase[t + 1] + off) : a0;
+            const float4 a0 = *reinterpret_cast<const float4 *>(xf + abase[t] + off);
+            const float4 a1 = t + 1 < G::MT ? *reinterpret_cast<const float4 *>(xf + abase[t + 1] + off) : a0;
             acc[t] = mfma(a0.x, b[g].x, acc[t]);
             if (t + 1 < G::MT) acc[t + 1] = mfma(a1.x, b[g].x, acc[t + 1]);
             acc[t] = mfma(a0.y, b[g].y, acc[t]);
@@ -518,7 +547,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
         // the k ranges 1 .. FS-1 of each filter block through LDS (the staging tile is free once
         // every wave has passed the barrier), added to range 0 in range order
         __syncthreads();
-        float *red = xs;
+        float *red = reinterpret_cast<float *>(xs);
         if (kr > 0)
 #pragma unroll
             for (int t = 0; t < G::MT; ++t)
@@ -580,7 +609,10 @@ template <class G, bool BF = false>
 __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict__ dY, const float *__restrict__ act, int R,
                                                     const float *__restrict__ Wt, float *__restrict__ dX)
 {
-    __shared__ __attribute__((aligned(16))) float ys[G::SPB * G::PH * G::PW * G::CS];
+    // BF: dY staged as bf16 (rounded once at the store; CS = 72 elements = 36 dwords between
+    // positions: the 8-B operand reads of 16 positions stay on distinct banks)
+    using YT = typename std::conditional<BF, uint16_t, float>::type;
+    __shared__ __attribute__((aligned(16))) YT ys[G::SPB * G::PH * G::PW * G::CS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
     const int cls = wave / G::NNC, chunk = wave - cls * G::NNC;
@@ -627,7 +659,15 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
                     const int q = e / (G::PH * G::PW * C4);
                     const int rem = e - q * (G::PH * G::PW * C4);
                     const int pos = rem / C4, c4 = rem - pos * C4;
-                    *reinterpret_cast<float4 *>(ys + (q * G::PH * G::PW + pos) * G::CS + 4 * c4) = v[j];
+                    YT *dst = ys + (q * G::PH * G::PW + pos) * G::CS + 4 * c4;
+                    if constexpr (BF) {
+                        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                        bf16x4 h;
+                        h[0] = (__bf16)v[j].x, h[1] = (__bf16)v[j].y, h[2] = (__bf16)v[j].z, h[3] = (__bf16)v[j].w;
+                        *reinterpret_cast<bf16x4 *>(dst) = h;
+                    } else {
+                        *reinterpret_cast<float4 *>(dst) = v[j];
+                    }
                 }
             }
         }
@@ -664,8 +704,10 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
             for (int nt = 0; nt < G::NT; ++nt) bw[nt] = bf16_frag(b[2 * gp][nt], b[2 * gp + 1][nt]);
 #pragma unroll
             for (int t = 0; t < G::MT; ++t) {
-                const bf16x8 a = bf16_frag(*reinterpret_cast<const float4 *>(ys + abase[t] + o0),
-                                           *reinterpret_cast<const float4 *>(ys + abase[t] + o1));
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                const bf16x4 lo = *reinterpret_cast<const bf16x4 *>(ys + abase[t] + o0);
+                const bf16x4 hi = *reinterpret_cast<const bf16x4 *>(ys + abase[t] + o1);
+                const bf16x8 a = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
                 for (int nt = 0; nt < G::NT; ++nt) acc[t][nt] = mfma16_bf16(a, bw[nt], acc[t][nt]);
             }
@@ -676,9 +718,10 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
         const int tap = g / (G::CO / 16), cb = (g - tap * (G::CO / 16)) * 16;
         const int dky = tap / G::KT, dkx = tap - dky * G::KT;
         const int off = -(dky * G::PW + dkx) * G::CS + cb;
+        const float *yf = reinterpret_cast<const float *>(ys);
 #pragma unroll
         for (int t = 0; t < G::MT; ++t) {
-            const float4 a = *reinterpret_cast<const float4 *>(ys + abase[t] + off);
+            const float4 a = *reinterpret_cast<const float4 *>(yf + abase[t] + off);
 #pragma unroll
             for (int nt = 0; nt < G::NT; ++nt) {
                 acc[t][nt] = mfma(a.x, b[g][nt].x, acc[t][nt]);
