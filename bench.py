@@ -541,7 +541,8 @@ def main():
     if pixel and args.workload == "C4":
         # the C4 minibatch's HBM bytes: the per-kernel PMC passes (tools/cnn_kernel_summary.py over
         # tools/cnn_kernel_run.py, profiles/c4_kernels.json), again only from the current sources
-        kpath = os.path.join(ROOT, "profiles", "c4_kernels.json")
+        kname = "c4_kernels_bf16.json" if args.dtype == "bf16" else "c4_kernels.json"
+        kpath = os.path.join(ROOT, "profiles", kname)
         kern = {}
         if os.path.exists(kpath):
             try:
@@ -549,7 +550,7 @@ def main():
                     kern = json.load(f)
             except (OSError, ValueError):
                 kern = {}
-        ksrc = {"file": "profiles/c4_kernels.json", "recorded_source_hash": kern.get("_source_hash"),
+        ksrc = {"file": "profiles/" + kname, "recorded_source_hash": kern.get("_source_hash"),
                 "library_source_hash": source_hash("cnn"), "sources": "cnn", "operands": kern.get("operands")}
         ksrc["current"] = bool(kern) and ksrc["recorded_source_hash"] == ksrc["library_source_hash"] and \
             kern.get("operands") == ("bf16" if args.dtype == "bf16" else "f32")
