@@ -27,6 +27,7 @@
 
 #include "gs_comm_internal.h"
 #include "gs_conv.h"
+#include "gs_fields.h"
 #include "gs_gemm.h"
 
 namespace gs {
@@ -96,13 +97,14 @@ struct CnnWs {
     double *norm_part;
     double *loss_part;     // kSums per loss row block
     float *parts;          // split-K weight-gradient partials / bias column-sum partials
-    float *pre;            // [2][5][R]: a minibatch's gathered fields (act bits, olp, ov, adv, ret), by parity
-    float *pre_stats;      // [2][2]: its advantage mean / std
+    float *pre;            // [kPreChunk][5][R]: minibatches' gathered fields (act bits, olp, ov, adv, ret)
+    float *pre_stats;      // [kPreChunk][2]: their advantage mean / std
     size_t bytes;
 };
 
 constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block sums them)
 constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
+constexpr int kPreChunk = 16;      // minibatches per ahead-of-time fields gather (k_cnn_gather_chunk)
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
 constexpr int kHeadRows = 8;    // minibatch rows per k_cnn_head_loss workgroup
 constexpr int kHeadSlices = 256 / kHeadRows;   // its z product's K slices (one thread per row x slice)
@@ -163,8 +165,8 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks * 5);   // total + 4 component partials
-    w.pre = (float *)take(sizeof(float) * 2 * 5 * R);
-    w.pre_stats = (float *)take(sizeof(float) * 4);
+    w.pre = (float *)take(sizeof(float) * kPreChunk * 5 * R);
+    w.pre_stats = (float *)take(sizeof(float) * kPreChunk * 2);
     w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + kHeadRows - 1) / kHeadRows));
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
@@ -184,28 +186,6 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     return w;
 }
 
-
-__device__ __forceinline__ int64_t frame_row(const int32_t *idx, int64_t r, int64_t T, int64_t N, bool clamp = false)
-{
-    if (!idx) return r;
-    int64_t i = idx[r];
-    if (clamp && i < 0) i = 0;       // global mode: another rank's row reads sample 0 (and is dead)
-    const int64_t env = i / T, t = i - env * T;   // env-major sample index (rollout_buffer.py:11-13)
-    return t * N + env;
-}
-
-// the minibatch's rollout fields read in place through the sampler indices (the fused head + loss
-// kernel gathers its own rows; utils/rollout_collector.py:657-682)
-struct CnnFields {
-    const int32_t *idx;
-    int64_t T, N;
-    const int64_t *actions;
-    const float *logprobs, *values, *advantages, *returns;
-    // the minibatch's fields gathered ahead of time (k_cnn_prefetch / the previous step's clip +
-    // Adam launch): [5][B] (act bits, olp, ov, adv, ret) and {adv mean, std}; nullptr: gather here
-    const float *pre = nullptr;
-    const float *pre_stats = nullptr;
-};
 
 // ---- ReLU-masked col2im (gather form, fixed summation order): dA[r,y,x,c] for stride s
 __global__ __launch_bounds__(256) void k_col2im_relu(const float *__restrict__ dcols, const float *__restrict__ act,
@@ -565,30 +545,6 @@ __global__ __launch_bounds__(256) void k_gather_fields(const int32_t *__restrict
     f_ret[r] = returns[src];
 }
 
-template <int NV, typename T>
-__device__ __forceinline__ void wg_reduce(T (&v)[NV], T *scratch)
-{
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) scratch[k * 256 + tid] = v[k];
-    __syncthreads();
-    T *part = scratch + NV * 256;
-    if (tid < NV * 16) {
-        const int k = tid >> 4, j = tid & 15;
-        T acc = 0;
-        for (int m = 0; m < 16; ++m) acc += scratch[k * 256 + j * 16 + m];
-        part[tid] = acc;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        T acc = 0;
-        for (int j = 0; j < 16; ++j) acc += part[k * 16 + j];
-        v[k] = acc;
-    }
-    __syncthreads();
-}
-
 constexpr int kSums = 13;
 constexpr int kNumSumsGlobal = 14;     // gs_ppo_global.metric_sums per minibatch (the MLP's 14: slot 13 unused)
 constexpr int kLossRows = 256;   // loss rows per workgroup (one per thread)
@@ -713,30 +669,6 @@ __device__ __forceinline__ void batch_adv_stats(const float *__restrict__ f_adv,
                 q[0] += dv * dv;
             }
     }
-    wg_reduce<1>(q, sred);
-    meanf = (float)mean;
-    stdf = (float)sqrt(q[0] / (double)(B - 1));
-}
-
-// the same from the minibatch's advantages already in registers (thread t holds rows t + 256 j)
-template <int NA>
-__device__ __forceinline__ void batch_adv_stats_regs(const float (&adv)[NA], int B, double *sred, float &meanf,
-                                                     float &stdf)
-{
-    const int tid = threadIdx.x;
-    double m1[1] = {0.0};
-#pragma unroll
-    for (int j = 0; j < NA; ++j)
-        if (tid + 256 * j < B) m1[0] += (double)adv[j];
-    wg_reduce<1>(m1, sred);
-    const double mean = m1[0] / (double)B;
-    double q[1] = {0.0};
-#pragma unroll
-    for (int j = 0; j < NA; ++j)
-        if (tid + 256 * j < B) {
-            const double dv = (double)adv[j] - mean;
-            q[0] += dv * dv;
-        }
     wg_reduce<1>(q, sred);
     meanf = (float)mean;
     stdf = (float)sqrt(q[0] / (double)(B - 1));
@@ -1058,7 +990,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     GS_STAMP(0)
     float meanf = 0.f, stdf = 1.f;
     if (la.normalize && (gmode || pre)) {
-        // the global minibatch's statistics (gs_ppo_global_adv_stats) or the prefetched ones
+        // the global minibatch's statistics (gs_ppo_global_adv_stats) or the gathered ones
         meanf = gmode ? la.adv_stats[0] : fl.pre_stats[0];
         stdf = gmode ? la.adv_stats[1] : fl.pre_stats[1];
         __syncthreads();
@@ -1311,51 +1243,16 @@ __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__
     if (threadIdx.x < 5) part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s[threadIdx.x];
 }
 
-// ---- a minibatch's rollout fields through the sampler indices into pre ([5][B]: act bits, olp,
-// ov, adv, ret) and its advantage statistics into pre_stats (batch_adv_stats_regs: the same
-// values k_cnn_head_loss computes from the gathered advantages); one 256-thread workgroup
-__device__ __forceinline__ void prefetch_fields(const CnnFields &fl, int B, bool normalize, float *__restrict__ pre,
-                                                float *__restrict__ pre_stats, double *sred)
-{
-    constexpr int NA = 8;     // B <= 2048 (head_fused)
-    const int tid = threadIdx.x;
-    float adv_r[NA];
-    int64_t src[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) src[j] = frame_row(fl.idx, min(tid + 256 * j, B - 1), fl.T, fl.N);
-    int act[NA];
-    float olp[NA], ov[NA], ret[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        act[j] = (int)fl.actions[src[j]];
-        olp[j] = fl.logprobs[src[j]];
-        ov[j] = fl.values[src[j]];
-        adv_r[j] = fl.advantages[src[j]];
-        ret[j] = fl.returns[src[j]];
-    }
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        const int r = tid + 256 * j;
-        if (r < B) {
-            pre[r] = __int_as_float(act[j]);
-            pre[B + r] = olp[j];
-            pre[2 * B + r] = ov[j];
-            pre[3 * B + r] = adv_r[j];
-            pre[4 * B + r] = ret[j];
-        }
-    }
-    if (normalize) {
-        float meanf, stdf;
-        batch_adv_stats_regs<NA>(adv_r, B, sred, meanf, stdf);
-        if (tid == 0) pre_stats[0] = meanf, pre_stats[1] = stdf;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_cnn_prefetch(CnnFields fl, int B, int normalize, float *__restrict__ pre,
-                                                      float *__restrict__ pre_stats)
+// ---- the fields and advantage statistics of gridDim.x consecutive minibatches (workgroup k: sampler
+// rows idx + k B) into pre + k 5 B / pre_stats + 2 k, ahead of their steps (one launch per
+// kPreChunk minibatches: off the critical path, where a per-step gather sat in it)
+__global__ __launch_bounds__(256) void k_cnn_gather_chunk(CnnFields fl, int B, int normalize, float *__restrict__ pre,
+                                                          float *__restrict__ pre_stats)
 {
     __shared__ double sred[256 + 16];
-    prefetch_fields(fl, B, normalize != 0, pre, pre_stats, sred);
+    const int k = blockIdx.x;
+    fl.idx += (int64_t)k * B;
+    gather_fields(fl, B, normalize != 0, pre + (int64_t)k * 5 * B, pre_stats + 2 * k, sred);
 }
 
 // one parameter of torch.optim.Adam's single-tensor step on the clipped gradient (IEEE sqrt and
@@ -1374,9 +1271,7 @@ __device__ __forceinline__ float adam_flat(float g, float &m, float &v, float p,
 __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, float *__restrict__ G,
                                                         float *__restrict__ M, float *__restrict__ V, int64_t n,
                                                         const double *__restrict__ part, int nparts, AdamArgs aa,
-                                                        float *__restrict__ metrics, const int32_t *__restrict__ stop,
-                                                        CnnFields next, int next_B, int next_norm,
-                                                        float *__restrict__ next_pre, float *__restrict__ next_stats)
+                                                        float *__restrict__ metrics, const int32_t *__restrict__ stop)
 {
     if (stop && *stop) {
         // a job-wide stop (the exchange ORs the ranks' stop bits): no step on any rank
@@ -1388,13 +1283,7 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     __shared__ double sred[256 + 16];
     __shared__ float s_coef;
-    // next.idx set: the last block gathers the next minibatch's fields for its head + loss kernel
-    // (off the critical path, beside this launch's Adam blocks); the scalar tail moves one block up
-    const int last = gridDim.x - 1 - (next.idx ? 1 : 0);
-    if (next.idx && (int)blockIdx.x == gridDim.x - 1) {
-        prefetch_fields(next, next_B, next_norm != 0, next_pre, next_stats, sred);
-        return;
-    }
+    const int last = gridDim.x - 1;
     constexpr int U = kAdamQuads;
     const int64_t n4 = n / 4;
     // this thread's parameters first (clamped, unconditional), then the norm partials
@@ -1747,26 +1636,21 @@ struct CnnGlobalStep {
     int64_t batch_global;
 };
 
-// k >= 0 (the local update's fused path): this step's fields were gathered into parity k & 1 of
-// the prefetch buffers, and this step's clip + Adam launch gathers next_idx's (the next
-// minibatch's) into the other parity
+// pre / pre_stats (the local update's fused path): this minibatch's fields and advantage
+// statistics, gathered ahead by k_cnn_gather_chunk; the head + loss kernel reads them contiguously
 int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const gs_ppo_hparams &hp,
              const gs_rollout_view_u8 &ro, const int32_t *idx, int64_t B, int64_t adam_step, float *metrics,
              int32_t *stop, const CnnWs &w, gs_comm *comm, hipStream_t s, const CnnGlobalStep *gl = nullptr,
-             int64_t k = -1, const int32_t *next_idx = nullptr)
+             const float *pre = nullptr, const float *pre_stats = nullptr)
 {
     int rc;
-    const bool pf = k >= 0 && !gl && head_fused(L, B);
-    CnnFields next{};
-    if (pf && next_idx)
-        next = CnnFields{next_idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
     const FrameSrc fs{ro.obs, gl ? gl->frame_idx : idx, ro.T, ro.N};
     GS_REQUIRE(!gl || head_fused(L, B), "global mode: the fused head + loss kernels do not fit this shape");
     if (head_fused(L, B)) {
         CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
-        if (pf) {
-            fl.pre = w.pre + (k & 1) * 5 * B;
-            fl.pre_stats = w.pre_stats + (k & 1) * 2;
+        if (pre && !gl) {
+            fl.pre = pre;
+            fl.pre_stats = pre_stats;
         }
         LossArgs la = loss_args(hp);
         if (gl) {
@@ -1802,10 +1686,9 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     }
     hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
                        L.oWv);
-    const unsigned nadam = (unsigned)((L.P / 4 + 256 * kAdamQuads - 1) / (256 * kAdamQuads) + 1 + (next.idx ? 1 : 0));
+    const unsigned nadam = (unsigned)((L.P / 4 + 256 * kAdamQuads - 1) / (256 * kAdamQuads) + 1);
     hipLaunchKernelGGL(k_clip_adam_flat, dim3(nadam), dim3(256), 0, s, P, G, Mm, Vv, L.P, w.norm_part, kNormBlocks, aa,
-                       metrics, stop, next, (int)B, hp.normalize_adv ? 1 : 0, w.pre + ((k + 1) & 1) * 5 * B,
-                       w.pre_stats + ((k + 1) & 1) * 2);
+                       metrics, stop);
     GS_LAUNCH_CHECK("k_clip_adam_flat");
     return GS_OK;
 }
@@ -1945,17 +1828,21 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
-    // the first minibatch's fields gathered up front; each step's clip + Adam launch gathers the next
-    if (n_minibatches > 0 && head_fused(L, batch)) {
-        const CnnFields f0{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
-        hipLaunchKernelGGL(k_cnn_prefetch, dim3(1), dim3(256), 0, s, f0, (int)batch, hp.normalize_adv ? 1 : 0, w.pre,
-                           w.pre_stats);
-        GS_LAUNCH_CHECK("k_cnn_prefetch");
-    }
+    // the fused head + loss path reads each minibatch's fields gathered ahead (kPreChunk at a time)
+    const bool pre = head_fused(L, batch);
     for (int64_t k = 0; k < n_minibatches; ++k) {
+        const int64_t slot = k % kPreChunk;
+        if (pre && slot == 0) {
+            const CnnFields fk{idx + k * batch, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages,
+                               ro.returns};
+            const unsigned nk = (unsigned)std::min<int64_t>(kPreChunk, n_minibatches - k);
+            hipLaunchKernelGGL(k_cnn_gather_chunk, dim3(nk), dim3(256), 0, s, fk, (int)batch,
+                               hp.normalize_adv ? 1 : 0, w.pre, w.pre_stats);
+            GS_LAUNCH_CHECK("k_cnn_gather_chunk");
+        }
         rc = cnn_step(params, grads, adam_m, adam_v, L, hp, ro, idx + k * batch, batch, adam_step0 + k + 1,
-                      metrics + k * GS_NUM_METRICS, stop_flag, w, comm, s, nullptr, k,
-                      k + 1 < n_minibatches ? idx + (k + 1) * batch : nullptr);
+                      metrics + k * GS_NUM_METRICS, stop_flag, w, comm, s, nullptr,
+                      pre ? w.pre + slot * 5 * batch : nullptr, pre ? w.pre_stats + 2 * slot : nullptr);
         if (rc) return rc;
     }
     return GS_OK;

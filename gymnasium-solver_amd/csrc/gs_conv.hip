@@ -65,6 +65,21 @@ __device__ __forceinline__ int64_t frame_src(const int32_t *idx, int64_t r, int6
     return t * N + env;
 }
 
+// bf16(u8 / 255) for the bf16 modes: the product with fl(1/255) rounds to the same bf16 as the
+// correctly rounded quotient for all 256 bytes (checked exhaustively: the fp32 values differ in
+// 126 cases, never across a bf16 rounding boundary), one multiply instead of an IEEE division
+__device__ __forceinline__ __bf16 u8_bf16(uint32_t byte) { return (__bf16)((float)byte * (1.0f / 255.0f)); }
+
+// u8 / 255 correctly rounded (the fp32 modes): q = b fl(1/255) corrected by one fma residual step
+// equals the IEEE quotient for all 256 bytes (checked exhaustively), 3 instructions instead of the
+// division's scale / reciprocal / fixup sequence
+__device__ __forceinline__ float u8_f32(uint32_t byte)
+{
+    const float b = (float)byte, c = 1.0f / 255.0f;
+    const float q = b * c;
+    return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, b), c, q);
+}
+
 // stage frame rows [y0, y0 + BIR) of sample r as fp32 [C][BIR][W] (rows past H are zero):
 // every thread issues all of its u32 loads before converting any (one memory latency).  copy:
 // the sample's u8 stack elsewhere (the rollout row), rows [ylo, yhi) of it written from the same
@@ -93,14 +108,15 @@ __device__ __forceinline__ void stage_band(FT *fr, const uint8_t *__restrict__ o
             const int c = e / (G::BIR * G::W4);
             const int rem = e - c * (G::BIR * G::W4);
             const int y = rem / G::W4, x4 = rem - y * G::W4;
-            const float4 f = make_float4((float)(v[j] & 255u) / 255.0f, (float)((v[j] >> 8) & 255u) / 255.0f,
-                                         (float)((v[j] >> 16) & 255u) / 255.0f, (float)(v[j] >> 24) / 255.0f);
             if constexpr (sizeof(FT) == 2) {      // bf16 staging (GS_HP_BF16): rounded once here
                 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
                 bf16x4 h;
-                h[0] = (__bf16)f.x, h[1] = (__bf16)f.y, h[2] = (__bf16)f.z, h[3] = (__bf16)f.w;
+                h[0] = u8_bf16(v[j] & 255u), h[1] = u8_bf16((v[j] >> 8) & 255u);
+                h[2] = u8_bf16((v[j] >> 16) & 255u), h[3] = u8_bf16(v[j] >> 24);
                 *reinterpret_cast<bf16x4 *>(fr + (c * G::BIR + y) * G::W + 4 * x4) = h;
             } else {
+                const float4 f = make_float4(u8_f32(v[j] & 255u), u8_f32((v[j] >> 8) & 255u),
+                                             u8_f32((v[j] >> 16) & 255u), u8_f32(v[j] >> 24));
                 *reinterpret_cast<float4 *>(fr + (c * G::BIR + y) * G::W + 4 * x4) = f;
             }
             if (copy && y0 + y >= ylo && y0 + y < yhi)
@@ -123,6 +139,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
     using FT = typename std::conditional<BF, uint16_t, float>::type;
     __shared__ __attribute__((aligned(16))) FT fr[G::FRAME];
     const int r = blockIdx.x / G::NB, band = blockIdx.x - r * G::NB;
+    const int64_t src = frame_src(idx, r, T, N);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
     const int oy0 = band * G::BOH;
@@ -138,7 +155,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
         const int c = g >> 2, ky = 2 * (g & 3) + (lq >> 1), kx0 = 4 * (lq & 1);
         b[g] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
     }
-    stage_band<G, FT>(fr, obs, frame_src(idx, r, T, N), oy0 * G::S,
+    stage_band<G, FT>(fr, obs, src, oy0 * G::S,
                   obs_copy ? obs_copy + (int64_t)r * (G::C * G::H * G::W) : nullptr, band * (G::H / G::NB),
                   (band + 1) * (G::H / G::NB));
     __syncthreads();
@@ -288,8 +305,7 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
                 const int y = rem / G::W4, x4 = rem - y * G::W4;
                 const uint32_t v = fv[j];
                 *reinterpret_cast<float4 *>(&fr[buf][(c * UIR + y) * G::W + 4 * x4]) =
-                    make_float4((float)(v & 255u) / 255.0f, (float)((v >> 8) & 255u) / 255.0f,
-                                (float)((v >> 16) & 255u) / 255.0f, (float)(v >> 24) / 255.0f);
+                    make_float4(u8_f32(v & 255u), u8_f32((v >> 8) & 255u), u8_f32((v >> 16) & 255u), u8_f32(v >> 24));
             }
         }
 #pragma unroll
@@ -376,6 +392,175 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
     if (tid < G::CO) {
         float t = 0.f;
         for (int g = 0; g < 8; ++g) t += dbred[g][tid];
+        o[G::CO * G::KK + tid] = t;
+    }
+}
+
+// bf16 mode (GS_HP_BF16) of the conv1 weight gradient.  A lane's 8 k values of a 16x16x32 MFMA
+// are 8 consecutive output positions of one output row (lane quarter q of k-block m: position
+// group 4 m + q, groups of 8 positions, 3 per 20-position row, the last half padding), so both
+// operands are one 16-B LDS read: dA staged transposed as bf16 [filter][slot], the frame band as
+// bf16 "sub-rows" [c][y][kx][X] holding pixel 4 X + kx (a tap's 8 pixels at stride 4 become 8
+// adjacent elements).  Row strides: 16 filter rows 4 banks apart (136 slots), the 16 taps of an
+// n-tile (2 ky x 8 kx sub-rows of 12 dwords, ky 96 dwords apart) on 16 distinct 4-bank chunks.
+// db from the fp32 dA registers (the products' operands are rounded, the bias sum is not).
+// Same parts layout as k_conv1_wgrad.
+template <class G>
+__global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restrict__ obs,
+                                                        const int32_t *__restrict__ idx, int64_t T, int64_t N, int R,
+                                                        const float *__restrict__ dA, float *__restrict__ parts)
+{
+    constexpr int UR = 5;                               // output rows per unit
+    constexpr int NU = (G::OH + UR - 1) / UR;           // units per sample
+    constexpr int UIR = (UR - 1) * G::S + G::K;         // frame rows per unit
+    constexpr int GPR = (G::OW + 7) / 8;                // 8-position groups per output row
+    constexpr int NGRP = UR * GPR;                      // groups per unit
+    constexpr int NBLK = (NGRP + 3) / 4;                // MFMA k-blocks per unit
+    constexpr int DTS = NBLK * 32 + 8;                  // dA^T row stride (bf16)
+    constexpr int XS = 8 * GPR;                         // sub-row length (X)
+    constexpr int FBN = G::C * UIR * G::K * XS;         // bf16 of a frame band
+    constexpr int NF = G::C * UIR * G::W4;              // u32 words of a frame band
+    constexpr int UP = UR * G::OW;                      // positions per unit
+    constexpr int NDA = UP * (G::CO / 4);               // float4 of a dA unit
+    constexpr int PF = (NF + 255) / 256, PD = (NDA + 255) / 256;
+    static_assert(G::OH % UR == 0, "full units only");
+    static_assert(G::S == 4 && G::K == 8 && G::CO == 32 && G::C == 4, "written for NatureCNN conv1");
+    static_assert(4 * (XS - 1) + G::K - 1 >= G::W - 1, "sub-rows cover the row");
+    static_assert(XS - 1 >= G::OW, "a sub-row's last element is a padding position");
+    static_assert((DTS / 2) % 64 == 4 && (G::K * XS / 2) % 64 == 32 && (XS / 2) % 4 == 0, "bank layout");
+    __shared__ __attribute__((aligned(16))) __bf16 fb[2][FBN];
+    __shared__ __attribute__((aligned(16))) __bf16 dat[2][G::CO * DTS];
+    __shared__ float4 dbred[256];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lq = lane >> 4;
+    // zero both buffers once: sub-row elements past the row and padding slots are never written
+    {
+        constexpr int Z = (2 * FBN + 2 * G::CO * DTS) * 2 / 16;
+        uint4 *z0 = reinterpret_cast<uint4 *>(&fb[0][0]);
+        uint4 *z1 = reinterpret_cast<uint4 *>(&dat[0][0]);
+        constexpr int ZF = 2 * FBN * 2 / 16;
+        for (int i = tid; i < Z; i += 256) {
+            if (i < ZF) z0[i] = make_uint4(0u, 0u, 0u, 0u);
+            else z1[i - ZF] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    // wave w: taps of channel w (64 = 8 ky x 8 kx); n-tile nt: ky = 2 nt + li / 8, kx = li % 8
+    int bo[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bo[nt] = ((wave * UIR + 2 * nt + (li >> 3)) * G::K + (li & 7)) * XS;
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);     // channels 4 (tid % 8) .. + 3
+
+    uint32_t fv[PF];
+    float4 dv[PD];
+    auto load = [&](int unit) {
+        const int r = unit / NU, oy0 = (unit % NU) * UR;
+        const uint8_t *base = obs + frame_src(idx, r, T, N) * (int64_t)(G::C * G::H * G::W);
+        const int y0 = oy0 * G::S;
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            const int e = min(tid + 256 * j, NF - 1);
+            const int c = e / (UIR * G::W4), rem = e - c * (UIR * G::W4);
+            const int y = rem / G::W4, x4 = rem - y * G::W4;
+            fv[j] = *reinterpret_cast<const uint32_t *>(base + ((int64_t)c * G::H + y0 + y) * G::W + 4 * x4);
+        }
+        const float *src = dA + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
+#pragma unroll
+        for (int j = 0; j < PD; ++j) {
+            const int e = min(tid + 256 * j, NDA - 1);
+            dv[j] = *reinterpret_cast<const float4 *>(src + 4 * (int64_t)e);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            const int e = tid + 256 * j;
+            if (e < NF) {
+                const int c = e / (UIR * G::W4), rem = e - c * (UIR * G::W4);
+                const int y = rem / G::W4, w = rem - y * G::W4;
+                __bf16 *row = &fb[buf][(c * UIR + y) * G::K * XS];
+                const uint32_t v = fv[j];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const __bf16 h = u8_bf16((v >> (8 * b)) & 255u);
+                    row[b * XS + w] = h;                          // pixel 4 w + b: sub-row b, X = w
+                    // sub-row b + 4, X = w - 1; w = 0 writes the previous sub-row's last element,
+                    // a padding position whose dA slots are zero (unconditional: no branch)
+                    row[(b + 4) * XS + w - 1] = h;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PD; ++j) {
+            const int e = tid + 256 * j;
+            if (e < NDA) {
+                const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
+                const int oy = p / G::OW, ox = p - oy * G::OW;
+                const int slot = (oy * GPR + (ox >> 3)) * 8 + (ox & 7);
+                const float4 d = dv[j];
+                dat[buf][(4 * c4 + 0) * DTS + slot] = (__bf16)d.x;
+                dat[buf][(4 * c4 + 1) * DTS + slot] = (__bf16)d.y;
+                dat[buf][(4 * c4 + 2) * DTS + slot] = (__bf16)d.z;
+                dat[buf][(4 * c4 + 3) * DTS + slot] = (__bf16)d.w;
+                dbacc.x += d.x, dbacc.y += d.y, dbacc.z += d.z, dbacc.w += d.w;
+            }
+        }
+    };
+
+    const int n_units = R * NU;
+    int unit = blockIdx.x;
+    __syncthreads();                                    // the zero fill before the first stores
+    if (unit < n_units) {
+        load(unit);
+        store(0);
+    }
+    __syncthreads();
+    for (int it = 0; unit < n_units; ++it, unit += gridDim.x) {
+        const int buf = it & 1;
+        const int next = unit + gridDim.x;
+        if (next < n_units) load(next);                  // in flight during this unit's MFMAs
+#pragma unroll
+        for (int m = 0; m < NBLK; ++m) {
+            const int gi = 4 * m + lq;
+            const int oyl = min(gi / GPR, UR - 1), ox0 = 8 * (gi - (gi / GPR) * GPR);
+            const bf16x8 a0 = *reinterpret_cast<const bf16x8 *>(&dat[buf][li * DTS + 8 * gi]);
+            const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(&dat[buf][(16 + li) * DTS + 8 * gi]);
+            bf16x8 bv[4];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+                bv[nt] = *reinterpret_cast<const bf16x8 *>(&fb[buf][bo[nt] + oyl * G::S * G::K * XS + ox0]);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                acc[0][nt] = mfma16_bf16(a0, bv[nt], acc[0][nt]);
+                acc[1][nt] = mfma16_bf16(a1, bv[nt], acc[1][nt]);
+            }
+        }
+        if (next < n_units) store(buf ^ 1);
+        __syncthreads();
+    }
+    // partial out: D row = lq * 4 + j (filter within the m-tile), col = li (tap within the n-tile)
+    float *o = parts + (int64_t)blockIdx.x * (G::CO * G::KK + G::CO);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                o[(mt * 16 + lq * 4 + j) * G::KK + wave * 64 + nt * 16 + li] = acc[mt][nt][j];
+    // db: the 32 threads of each channel quad (tid % 8) summed in thread order
+    dbred[tid] = dbacc;
+    __syncthreads();
+    if (tid < G::CO) {
+        const int c4 = tid >> 2, k = tid & 3;
+        float t = 0.f;
+        for (int g = 0; g < 32; ++g) {
+            const float4 v = dbred[g * 8 + c4];
+            t += k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+        }
         o[G::CO * G::KK + tid] = t;
     }
 }
@@ -898,6 +1083,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
 using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
 using C3_84 = CN<9, 9, 64, 3, 1, 2>;      // conv3: 9x9x64 -> 7x7x64
 using C3_84s = CN<9, 9, 64, 3, 1, 1>;     // conv3, one sample per workgroup (small batches)
+using C2_84b = CN<20, 20, 32, 4, 2, 1>;   // bf16 update batches
+using C3_84b = CN<9, 9, 64, 3, 1, 2>;
+constexpr int kConv2BfFS = 1;
 constexpr int kConvFwdSmallWG = 1024;     // FS = 2 up to this many workgroups (R <= 512)
 constexpr int kConv1Bands4Below = 256;    // conv1 in 4 bands below this many 2-band workgroups
 
@@ -940,8 +1128,7 @@ int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx
     GS_REQUIRE(R > 0 && obs && dA && parts && dW1 && db1, "conv1_lds_wgrad: bad argument");
     constexpr int n = C1_84::CO * C1_84::KK, stride = n + C1_84::CO;
     if (cnn_bf16())
-        hipLaunchKernelGGL((k_conv1_wgrad<C1_84, true>), dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA,
-                           parts);
+        hipLaunchKernelGGL(k_conv1_wgrad_bf<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
     else
         hipLaunchKernelGGL(k_conv1_wgrad<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
     GS_LAUNCH_CHECK("k_conv1_wgrad");
@@ -966,17 +1153,20 @@ bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cou
 
 // small batches (the rollout's policy act): one sample per workgroup group and FS = 2 filter
 // splits, so R = 128 rows still launch 256 workgroups; the update's minibatches keep FS = 1
-template <class G, class G1>
+// G: fp32 update batches, GB: bf16 update batches, G1: small batches (FS = 2)
+template <class G, class G1, class GB, int FSB = 1>
 int launch_conv_fwd(hipStream_t s, int R, const float *in, const float *Wt, const float *bias, float *out, bool bf)
 {
     if ((int64_t)R * 2 <= kConvFwdSmallWG) {
         const dim3 grid((unsigned)(2 * R));
         if (bf) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
         else hipLaunchKernelGGL((k_conv_fwd<G1, false, 2>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+    } else if (bf) {
+        const dim3 grid((unsigned)((R + GB::SPB - 1) / GB::SPB * FSB));
+        hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
     } else {
         const dim3 grid((unsigned)((R + G::SPB - 1) / G::SPB));
-        if (bf) hipLaunchKernelGGL((k_conv_fwd<G, true>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
-        else hipLaunchKernelGGL((k_conv_fwd<G>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        hipLaunchKernelGGL((k_conv_fwd<G>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
     }
     GS_LAUNCH_CHECK("k_conv_fwd");
     return GS_OK;
@@ -986,8 +1176,8 @@ int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float
 {
     GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
     const bool bf = cnn_bf16();
-    if (layer == 2) return launch_conv_fwd<C2_84, C2_84>(s, R, in, Wt, bias, out, bf);
-    return launch_conv_fwd<C3_84, C3_84s>(s, R, in, Wt, bias, out, bf);
+    if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS>(s, R, in, Wt, bias, out, bf);
+    return launch_conv_fwd<C3_84, C3_84s, C3_84b>(s, R, in, Wt, bias, out, bf);
 }
 
 int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX)

@@ -377,3 +377,26 @@ def test_activation_stats_reduction_matches_the_reference_hooks(golden, tag):
     assert set(acts) == set(ref)
     for k, v in ref.items():
         np.testing.assert_allclose(acts[k], v, rtol=2e-5, atol=1e-7, err_msg=k)
+
+
+def test_u8_scale_shortcuts_exact():
+    """csrc/gs_conv.hip replaces the IEEE division u8 / 255 by (fp32) b fl(1/255) + one fma residual
+    correction and (bf16 modes) by the bare product: both must give the division's value for every
+    byte (the fp32 one bit for bit, the bf16 one after rounding to bf16)."""
+    from fractions import Fraction
+
+    def bf16_bits(x):
+        u = np.array([x], np.float32).view(np.uint32).astype(np.uint64)[0]
+        return int(((u + 0x7FFF + ((u >> 16) & 1)) >> 16) & 0xFFFF)
+
+    def f32(fr):       # exact rational -> nearest float32 (magnitudes here are far from subnormal)
+        return np.float32(float(fr))
+
+    c = np.float32(1) / np.float32(255)
+    for b in range(256):
+        ieee = np.float32(b) / np.float32(255)
+        q = np.float32(np.float32(b) * c)
+        r = f32(Fraction(b) - 255 * Fraction(float(q)))                 # fma(-q, 255, b)
+        fixed = f32(Fraction(float(r)) * Fraction(float(c)) + Fraction(float(q)))   # fma(r, c, q)
+        assert fixed == ieee, b
+        assert bf16_bits(q) == bf16_bits(ieee), b

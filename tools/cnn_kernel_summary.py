@@ -93,6 +93,8 @@ def short(name):
     if "Cijk_" in name:     # hipBLASLt / Tensile GEMM kernels (the fc layer's fp32 GEMMs)
         return "blaslt"
     m = re.search(r"\b(k_\w+)", name)
+    if m and m.group(1) == "k_conv1_wgrad_bf":    # the bf16 conv1 weight gradient (same position)
+        return "k_conv1_wgrad"
     if m and m.group(1) == "k_fc16":      # the fp32 fc kernels on 16x16x4 MFMA blocks (same positions)
         return "k_fc"
     return m.group(1) if m else None
