@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
 // A unit is 5 output rows of one sample (4 per sample at 84 x 84): its 24-row frame band
 // (fp32) and 100 x 32 dA rows fit twice in LDS, so the next unit's global loads (held in
 // registers) run under the current unit's MFMAs.  parts layout: [workgroup][CO * KK + CO]
-template <class G, bool BF = false>
+template <class G>
 __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
                                                      int64_t T, int64_t N, int R, const float *__restrict__ dA,
                                                      float *__restrict__ parts)
@@ -334,33 +334,6 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
             const int co = tid & 31, grp = tid >> 5;
             for (int p = grp; p < P; p += 8) db += da[buf][p * DS + co];
         }
-        if constexpr (BF) {
-            // GS_HP_BF16: 8 k-steps per 16x16x32 bf16 MFMA — element j of lane quarter q is
-            // position 4 (s0 + j) + q in both operands; steps past the unit are zeros
-            constexpr int NS = UPP / 4;
-            for (int s0 = 0; s0 < NS; s0 += 8) {
-                float a0[8], a1[8], bv[4][8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int p = 4 * (s0 + j) + lq;
-                    const bool in = s0 + j < NS;
-                    const int pc = in ? p : 0;
-                    const int oy = pc / G::OW, ox = pc - oy * G::OW;
-                    const int pof = (oy * G::S) * G::W + ox * G::S;
-                    a0[j] = in ? da[buf][pc * DS + li] : 0.f;
-                    a1[j] = in ? da[buf][pc * DS + 16 + li] : 0.f;
-#pragma unroll
-                    for (int nt = 0; nt < 4; ++nt) bv[nt][j] = in && p < P ? fr[buf][pof + boff[nt]] : 0.f;
-                }
-                const bf16x8 f0 = bf16_frag(a0), f1 = bf16_frag(a1);
-#pragma unroll
-                for (int nt = 0; nt < 4; ++nt) {
-                    const bf16x8 fb = bf16_frag(bv[nt]);
-                    acc[0][nt] = mfma16_bf16(f0, fb, acc[0][nt]);
-                    acc[1][nt] = mfma16_bf16(f1, fb, acc[1][nt]);
-                }
-            }
-        } else
         for (int s = 0; s < UPP / 4; ++s) {
             const int p = 4 * s + lq;                         // this lane's position of the k-step
             const int oy = p / G::OW, ox = p - oy * G::OW;
@@ -1083,9 +1056,13 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
 using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
 using C3_84 = CN<9, 9, 64, 3, 1, 2>;      // conv3: 9x9x64 -> 7x7x64
 using C3_84s = CN<9, 9, 64, 3, 1, 1>;     // conv3, one sample per workgroup (small batches)
-using C2_84b = CN<20, 20, 32, 4, 2, 1>;   // bf16 update batches
+// bf16 update batches: conv2 two samples per workgroup (the filter registers loaded once for both:
+// 44.9 -> 39.0 us per C4 minibatch; fp32 keeps one, its two-sample tile would not leave room for
+// a second workgroup per CU); conv3 as fp32 (4 or 1 samples per workgroup ran slower).  Same-box
+// sweep, profiles/r04_conv_fwd_bf16_sweep.txt
+using C2_84b = CN<20, 20, 32, 4, 2, 2>;
 using C3_84b = CN<9, 9, 64, 3, 1, 2>;
-constexpr int kConv2BfFS = 1;
+constexpr int kConv2BfFS = 1;              // 2 (filter blocks split over two workgroups): 52.2 us
 constexpr int kConvFwdSmallWG = 1024;     // FS = 2 up to this many workgroups (R <= 512)
 constexpr int kConv1Bands4Below = 256;    // conv1 in 4 bands below this many 2-band workgroups
 
