@@ -977,6 +977,7 @@ struct WG2 {
     static_assert((G::S * CSX) % 32 == 16, "padding");
 };
 
+constexpr int kWgradBurstMax = 24;      // float4 per thread of one staging burst (conv2: 18, conv3: 9)
 template <class G, bool BF = false>
 __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in, const float *__restrict__ dY, int R,
                                                     float *__restrict__ parts)
@@ -1006,8 +1007,10 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
     for (int r = blockIdx.x; r < R; r += gridDim.x) {
         __syncthreads();
         {   // input activation [pos][c] with stride CSX, dY [pos][co] with stride DS (zero rows past OHW)
+            // every load of the sample in one burst (one memory latency per sample; 8 per burst
+            // took 2 - 3 round trips)
             constexpr int NX4 = G::H * G::W * G::C / 4, ND4 = X::PP * G::CO / 4;
-            constexpr int NE = NX4 + ND4, BATCH = 8;
+            constexpr int NE = NX4 + ND4, BATCH = (NE + 255) / 256 <= kWgradBurstMax ? (NE + 255) / 256 : 8;
             const float *xin = in + (int64_t)r * G::H * G::W * G::C;
             const float *dyin = dY + (int64_t)r * G::OHW * G::CO;
             for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
