@@ -635,6 +635,7 @@ struct CN {
     static_assert((S * CS) % 64 == 8 && C % 16 == 0, "padding / channel grouping");
 };
 
+constexpr int kConvFwdBurst = 16;      // float4 loads per thread per staging burst of k_conv_fwd
 // FS > 1 (the rollout's small batches, where one workgroup per sample leaves most CUs idle):
 // FS workgroups per sample group, each owning 4 / FS filter blocks of 16, and the waves of a
 // filter block splitting the k-step groups into FS contiguous ranges; the ranges' partial tiles
@@ -672,7 +673,11 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
 
     // stage: [sample][position][channel] with position stride CS, 8 float4 loads in flight
     {
-        constexpr int C4 = G::C / 4, NE = G::SPB * G::H * G::W * C4, BATCH = 8;
+        constexpr int C4 = G::C / 4, NE = G::SPB * G::H * G::W * C4;
+        // one burst where the tile fits 16 loads per thread (conv2 fp32 65.7 vs 66.6 us with 8); the
+        // bf16 two-sample conv2 tile keeps bursts of 8 (16 cost it registers: 50.4 vs 39.1 us)
+        constexpr int BURST = (BF && NE > 256 * kConvFwdBurst) ? 8 : kConvFwdBurst;
+        constexpr int BATCH = (NE + 255) / 256 <= BURST ? (NE + 255) / 256 : BURST;
         const float *src = in + (int64_t)r0 * G::H * G::W * G::C;
         for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
             float4 v[BATCH];
