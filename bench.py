@@ -415,7 +415,8 @@ def main():
             try:
                 # MLP: the in-backward exchange is checked on this job's shapes before the timed run
                 comm = gd.init_xgmi_comm(rank, world, n_params, device,
-                                         verify_shapes=None if pixel else (agent.policy_model.dims, cfg.batch_size))
+                                         verify_shapes=None if pixel else (agent.policy_model.dims, cfg.batch_size,
+                                                                           int(agent.hparams().flags)))
             except RuntimeError as e:     # every rank raises together: switch transport together
                 _log(f"[bench] {e}; using RCCL for the gradient exchange")
                 args.comm = "rccl (xgmi unavailable)"

@@ -31,18 +31,40 @@ def _obj(src):
     return os.path.join(BUILD, src + ".o")
 
 
-def _compile(src, build_dir=None, defines=(), csrc=None):
+def _source_hashes(csrc=None):
+    """gsamd/buildinfo.source_hash of the measured paths, embedded into gs_abi.cpp
+    (gs_build_source_hash) so a measurement can be tied to the loaded binary."""
+    sys.path.insert(0, os.path.join(HERE, "gsamd"))
+    try:
+        import buildinfo
+    finally:
+        sys.path.pop(0)
+    kw = {"csrc": csrc} if csrc else {}
+    return {"MLP": buildinfo.source_hash("mlp", **kw), "CNN": buildinfo.source_hash("cnn", **kw),
+            "ALL": buildinfo.source_hash(None, **kw)}
+
+
+def _compile(src, build_dir=None, defines=(), csrc=None, hashes=None):
     csrc = csrc or CSRC
     path = os.path.join(csrc, src)
     obj = os.path.join(build_dir, src + ".o") if build_dir else _obj(src)
     deps = [path, os.path.join(HERE, "..", "include", "gsamd.h")] + [
         os.path.join(csrc, h) for h in os.listdir(csrc) if h.endswith(".h")]
+    hdefs = []
+    if src == "gs_abi.cpp" and hashes:
+        hdefs = [f'-DGS_SRC_HASH_{k}="{v}"' for k, v in sorted(hashes.items())]
+        stamp = obj + ".hash"
+        if not os.path.exists(stamp) or open(stamp).read() != " ".join(hdefs):
+            if os.path.exists(obj):
+                os.remove(obj)
+            with open(stamp, "w") as f:
+                f.write(" ".join(hdefs))
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return None
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-c", path, "-o", obj]
     if src.endswith(".hip"):
         cmd[1:1] = [f"--offload-arch={ARCH}", "-x", "hip"]
-    cmd += EXTRA.get(src, []) + [f"-D{d}" for d in defines]
+    cmd += EXTRA.get(src, []) + [f"-D{d}" for d in defines] + hdefs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -52,8 +74,9 @@ def _compile(src, build_dir=None, defines=(), csrc=None):
 def build(verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = _sources()
+    hashes = _source_hashes()
     with ThreadPoolExecutor(max_workers=min(jobs, len(srcs))) as ex:
-        done = [s for s in ex.map(_compile, srcs) if s]
+        done = [s for s in ex.map(lambda s: _compile(s, hashes=hashes), srcs) if s]
     objs = [_obj(s) for s in srcs]
     if done or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [
@@ -90,7 +113,7 @@ def build_variant(out_path: str, defines, jobs: int = 8, patches=(), tag: str = 
             open(fp, "w").write(text.replace(old, new))
     srcs = _sources()
     with ThreadPoolExecutor(max_workers=min(jobs, len(srcs))) as ex:
-        list(ex.map(lambda s: _compile(s, bdir, defines, csrc), srcs))
+        list(ex.map(lambda s: _compile(s, bdir, defines, csrc, hashes=_source_hashes(csrc)), srcs))
     objs = [os.path.join(bdir, s + ".o") for s in srcs]
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_path] + objs + [
         "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]

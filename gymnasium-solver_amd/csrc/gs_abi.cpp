@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "../../include/gsamd.h"
 
@@ -28,3 +29,23 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line)
 extern "C" int gs_abi_version(void) { return GS_ABI_VERSION; }
 
 extern "C" const char *gs_last_error(void) { return gs::t_err; }
+
+// the kernel sources' hashes, computed by build_lib.py (gsamd/buildinfo.source_hash) when this file
+// is compiled; build_lib.py recompiles it whenever a hash changes
+#ifndef GS_SRC_HASH_MLP
+#define GS_SRC_HASH_MLP "unknown"
+#endif
+#ifndef GS_SRC_HASH_CNN
+#define GS_SRC_HASH_CNN "unknown"
+#endif
+#ifndef GS_SRC_HASH_ALL
+#define GS_SRC_HASH_ALL "unknown"
+#endif
+
+extern "C" const char *gs_build_source_hash(const char *path)
+{
+    if (!path || !*path) return GS_SRC_HASH_ALL;
+    if (!strcmp(path, "mlp")) return GS_SRC_HASH_MLP;
+    if (!strcmp(path, "cnn")) return GS_SRC_HASH_CNN;
+    return nullptr;
+}

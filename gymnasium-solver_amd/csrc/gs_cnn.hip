@@ -1615,6 +1615,87 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
     return GS_OK;
 }
 
+
+// ---- activation statistics (utils/models.py:121-147, registered on cnn.0 / cnn.2 / cnn.4 /
+// mlp.0 at :419-422, recorded per training step at agents/base_agent.py:335-347): each layer's
+// pre-activation output z as a (rows x cols) matrix (a sample's NHWC block is its flattened
+// output; per-neuron statistics do not depend on the neuron order).  One thread per neuron
+// (column) walks the rows: sum and sum of squares in double, the count of |z| < 1e-6; with
+// relu_inplace the column is rewritten as relu(z), the next layer's input.  Partials per
+// workgroup: {sum, sumsq, dead count sum, dead count max}.
+__global__ __launch_bounds__(256) void k_act_stats_cols(float *__restrict__ x, int rows, int cols,
+                                                        double *__restrict__ part, int relu_inplace)
+{
+    __shared__ double sred[2 * (256 + 16)];
+    __shared__ int smax[256];
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    double v2[2] = {0.0, 0.0};
+    int dead = 0;
+    if (j < cols) {
+        int r = 0;
+        for (; r + 4 <= rows; r += 4) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = x[(int64_t)(r + u) * cols + j];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v2[0] += (double)v[u];
+                v2[1] += (double)v[u] * (double)v[u];
+                dead += fabsf(v[u]) < 1e-6f ? 1 : 0;
+                if (relu_inplace) x[(int64_t)(r + u) * cols + j] = v[u] > 0.0f ? v[u] : 0.0f;
+            }
+        }
+        for (; r < rows; ++r) {
+            const float v = x[(int64_t)r * cols + j];
+            v2[0] += (double)v;
+            v2[1] += (double)v * (double)v;
+            dead += fabsf(v) < 1e-6f ? 1 : 0;
+            if (relu_inplace) x[(int64_t)r * cols + j] = v > 0.0f ? v : 0.0f;
+        }
+    }
+    smax[threadIdx.x] = dead;
+    double c[1] = {(double)dead};
+    wg_reduce<2>(v2, sred);
+    wg_reduce<1>(c, sred);
+    if (threadIdx.x == 0) {
+        int m = 0;
+        for (int t = 0; t < 256; ++t) m = smax[t] > m ? smax[t] : m;
+        part[4 * blockIdx.x + 0] = v2[0];
+        part[4 * blockIdx.x + 1] = v2[1];
+        part[4 * blockIdx.x + 2] = c[0];
+        part[4 * blockIdx.x + 3] = (double)m;
+    }
+}
+
+struct ActStatLayers {
+    int nblk[4];
+    int cols[4];
+    int off[4];      // first partial of each layer
+};
+
+// the 4 layers' {mean, unbiased std, dead_pct (mean over neurons), dead_max} from the partials,
+// summed in workgroup order
+__global__ __launch_bounds__(64) void k_act_stats_final(const double *__restrict__ part, ActStatLayers ls, int rows,
+                                                        double *__restrict__ out)
+{
+    const int l = threadIdx.x;
+    if (l >= 4) return;
+    double s = 0.0, q = 0.0, c = 0.0, m = 0.0;
+    for (int b = 0; b < ls.nblk[l]; ++b) {
+        const double *p = part + 4 * (ls.off[l] + b);
+        s += p[0];
+        q += p[1];
+        c += p[2];
+        m = p[3] > m ? p[3] : m;
+    }
+    const double n = (double)rows * (double)ls.cols[l];
+    const double var = (q - s * s / n) / (n - 1.0);
+    out[4 * l + 0] = s / n;
+    out[4 * l + 1] = sqrt(var > 0.0 ? var : 0.0);
+    out[4 * l + 2] = c / n;
+    out[4 * l + 3] = m / (double)rows;
+}
+
 int validate_cnn_update(const gs_cnn_dims &dims, const gs_rollout_view_u8 &ro, int64_t B, const void *ws)
 {
     int rc = check_cnn(dims);
@@ -1845,5 +1926,49 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
                       pre ? w.pre + slot * 5 * batch : nullptr, pre ? w.pre_stats + 2 * slot : nullptr);
         if (rc) return rc;
     }
+    return GS_OK;
+}
+
+extern "C" int gs_cnn_activation_stats(const float *params, gs_cnn_dims dims, gs_rollout_view_u8 ro, const int32_t *idx,
+                                       int64_t batch, double *stats_out, void *workspace, void *stream)
+{
+    int rc = validate_cnn_update(dims, ro, batch, workspace);
+    if (rc) return rc;
+    GS_REQUIRE(params && idx && stats_out, "gs_cnn_activation_stats: null buffer");
+    GS_REQUIRE(batch <= (1 << 30), "gs_cnn_activation_stats: batch too large");
+    hipStream_t s = (hipStream_t)stream;
+    const CnnLayout L = CnnLayout::make(dims);
+    const CnnWs w = carve(workspace, L, batch);
+    const FrameSrc fs{ro.obs, idx, ro.T, ro.N};
+    // the trunk on the generic fp32 engine without the ReLU epilogues: each layer's output is its
+    // pre-activation (what the reference's Conv2d / Linear hooks see); the statistics kernel then
+    // applies the ReLU in place for the next layer
+    const int rows = (int)batch;
+    const int cols[4] = {L.h1 * L.w1 * L.c1, L.h2 * L.w2 * L.c2, L.F, L.HID};
+    ActStatLayers ls{};
+    int off = 0;
+    for (int l = 0; l < 4; ++l) {
+        ls.cols[l] = cols[l];
+        ls.nblk[l] = (cols[l] + 255) / 256;
+        ls.off[l] = off;
+        off += ls.nblk[l];
+    }
+    double *part = (double *)w.parts;
+    float *outs[4] = {w.a1, w.a2, w.a3, w.h};
+    if ((rc = conv_fwd_u8(s, geom1(L, batch), fs, params + L.oW1, params + L.ob1, w.a1, false))) return rc;
+    for (int l = 0; l < 4; ++l) {
+        if (l == 1 && (rc = conv_fwd_nhwc(s, geom2(L, batch), w.a1, params + L.oW2, params + L.ob2, w.a2, false)))
+            return rc;
+        if (l == 2 && (rc = conv_fwd_nhwc(s, geom3(L, batch), w.a2, params + L.oW3, params + L.ob3, w.a3, false)))
+            return rc;
+        if (l == 3 && (rc = gemm_f32(s, false, true, batch, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.h, L.HID,
+                                     0.f, params + L.obf, false)))
+            return rc;
+        hipLaunchKernelGGL(k_act_stats_cols, dim3((unsigned)ls.nblk[l]), dim3(256), 0, s, outs[l], rows, cols[l],
+                           part + 4 * ls.off[l], l < 3 ? 1 : 0);
+        GS_LAUNCH_CHECK("k_act_stats_cols");
+    }
+    hipLaunchKernelGGL(k_act_stats_final, dim3(1), dim3(64), 0, s, part, ls, rows, stats_out);
+    GS_LAUNCH_CHECK("k_act_stats_final");
     return GS_OK;
 }

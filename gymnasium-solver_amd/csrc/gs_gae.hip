@@ -16,6 +16,8 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "gs_common.h"
 
 namespace {
@@ -405,6 +407,147 @@ int launch_staged(bool boot, const float *values, const float *rewards, const ui
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
+
+// ---- rollout-level advantage normalisation (utils/returns_advantages.py:61-64, applied by
+// utils/rollout_collector.py:441-442 when normalize_advantages == "rollout"):
+// adv = (adv - mean) / (std + eps) over every element of the rollout, bit for bit as numpy computes
+// it on the float32 array.  numpy's float32 sum (np.add.reduce, the mean's and std's reduction) is
+// sequential over 8192-element buffer chunks, each chunk summed by pairwise_sum
+// (numpy/_core/src/umath/loops_utils.h.src): n < 8 a plain loop from 0; n <= 128 eight strided
+// accumulators combined ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the n % 8 rest;
+// larger n split at n2 = n / 2 - (n / 2) % 8.  mean = sum / n, std = sqrt(sum((a - mean)^2) / n),
+// all float32 (oracle/ppo_ref.py numpy_f32_sum restates this model; tests/test_oracle_golden.py
+// pins it against numpy itself).
+// k_pw_chunks: one wave per chunk; leaves (64..128 elements when the chunk exceeds 128) are found
+// by descending the split tree from the chunk root, so every leaf has one owner lane (the lane of
+// the first multiple of 64 inside it); internal nodes are then summed level by level in LDS in
+// heap order (node i has children 2i, 2i + 1).
+constexpr int kPwChunk = 8192;        // numpy's default ufunc buffer size
+constexpr int kPwIds = 256;           // heap ids of one chunk's tree (depth <= 7)
+
+// node `id` of the split tree of m0 elements: its (offset, size); false when an ancestor is a leaf
+__device__ __forceinline__ bool pw_node(int m0, int id, int &off, int &m)
+{
+    const int depth = 31 - __clz(id);
+    off = 0;
+    m = m0;
+    for (int d = depth - 1; d >= 0; --d) {
+        if (m <= 128) return false;
+        int n2 = m / 2;
+        n2 -= n2 % 8;
+        if ((id >> d) & 1) {
+            off += n2;
+            m -= n2;
+        } else {
+            m = n2;
+        }
+    }
+    return true;
+}
+
+// MODE 0: x itself; MODE 1: (x - mean)^2 in float32
+template <int MODE>
+__device__ __forceinline__ float pw_val(const float *__restrict__ x, int64_t i, float mean)
+{
+    const float v = x[i];
+    if (MODE == 0) return v;
+    const float d = v - mean;
+    return d * d;
+}
+
+template <int MODE>
+__device__ float pw_leaf(const float *__restrict__ x, int64_t base, int n, float mean)
+{
+    if (n < 8) {
+        float r = 0.0f;
+        for (int i = 0; i < n; ++i) r += pw_val<MODE>(x, base + i, mean);
+        return r;
+    }
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = pw_val<MODE>(x, base + j, mean);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += pw_val<MODE>(x, base + i + j, mean);
+    }
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += pw_val<MODE>(x, base + i, mean);
+    return res;
+}
+
+// numpy's float32 total from the chunk sums: ((0 + c0) + c1) + ...
+__device__ __forceinline__ float pw_total(const float *__restrict__ chunk, int nchunks)
+{
+    float s = 0.0f;
+    for (int c = 0; c < nchunks; ++c) s += chunk[c];
+    return s;
+}
+
+// MODE 1 needs the mean: every workgroup forms it from the MODE-0 chunk sums (scratch[0..nchunks))
+template <int MODE>
+__global__ __launch_bounds__(64) void k_pw_chunks(const float *__restrict__ x, int64_t n, float *__restrict__ scratch)
+{
+    __shared__ float node[kPwIds];
+    __shared__ float s_mean;
+    const int nchunks = (int)((n + kPwChunk - 1) / kPwChunk);
+    const int lane = threadIdx.x;
+    if (MODE == 1 && lane == 0) s_mean = pw_total(scratch, nchunks) / (float)n;
+    __syncthreads();
+    const float mean = MODE == 1 ? s_mean : 0.0f;
+    const int64_t c0 = (int64_t)blockIdx.x * kPwChunk;
+    const int m0 = (int)(n - c0 < kPwChunk ? n - c0 : kPwChunk);
+    // leaves
+    for (int k = lane; k * 64 < m0; k += 64) {
+        const int j = 64 * k;
+        int off = 0, m = m0, id = 1;
+        while (m > 128) {
+            int n2 = m / 2;
+            n2 -= n2 % 8;
+            if (j < off + n2) {
+                m = n2;
+                id = 2 * id;
+            } else {
+                off += n2;
+                m -= n2;
+                id = 2 * id + 1;
+            }
+        }
+        if ((off + 63) / 64 * 64 == j) node[id] = pw_leaf<MODE>(x, c0 + off, m, mean);
+    }
+    __syncthreads();
+    // internal nodes, deepest level first
+    for (int d = 6; d >= 0; --d) {
+        const int id = (1 << d) + lane;
+        if (lane < (1 << d)) {
+            int off, m;
+            if (pw_node(m0, id, off, m) && m > 128) node[id] = node[2 * id] + node[2 * id + 1];
+        }
+        __syncthreads();
+    }
+    if (lane == 0) scratch[(MODE == 0 ? 0 : nchunks) + blockIdx.x] = node[1];
+}
+
+__global__ __launch_bounds__(256) void k_adv_apply(float *__restrict__ x, int64_t n, const float *__restrict__ scratch,
+                                                   float eps, float *__restrict__ mean_std)
+{
+    __shared__ float s_ms[2];
+    const int nchunks = (int)((n + kPwChunk - 1) / kPwChunk);
+    if (threadIdx.x == 0) {
+        s_ms[0] = pw_total(scratch, nchunks) / (float)n;
+        s_ms[1] = sqrtf(pw_total(scratch + nchunks, nchunks) / (float)n);
+        if (mean_std && blockIdx.x == 0) {
+            mean_std[0] = s_ms[0];
+            mean_std[1] = s_ms[1];
+        }
+    }
+    __syncthreads();
+    const float m = s_ms[0];
+    const float den = s_ms[1] + eps;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        x[i] = (x[i] - m) / den;
+}
+
 }  // namespace
 
 extern "C" int gs_gae_f32(const float *values, const float *rewards, const uint8_t *dones,
@@ -458,6 +601,26 @@ extern "C" int gs_gae_f32(const float *values, const float *rewards, const uint8
                                bootstrap, last_values, T, N, c1, c2, adv, ret);
     }
     GS_LAUNCH_CHECK("k_gae_f32");
+    return GS_OK;
+}
+
+extern "C" size_t gs_normalize_advantages_scratch_bytes(int64_t n)
+{
+    return n < 1 ? 0 : sizeof(float) * 2 * (size_t)((n + kPwChunk - 1) / kPwChunk);
+}
+
+extern "C" int gs_normalize_advantages(float *adv, int64_t n, float eps, float *scratch, float *mean_std_out,
+                                       void *stream)
+{
+    GS_REQUIRE(adv && scratch, "gs_normalize_advantages: null buffer");
+    GS_REQUIRE(n >= 1 && n < ((int64_t)1 << 31), "gs_normalize_advantages: n = %lld outside [1, 2^31)", (long long)n);
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned nchunks = (unsigned)((n + kPwChunk - 1) / kPwChunk);
+    hipLaunchKernelGGL(k_pw_chunks<0>, dim3(nchunks), dim3(64), 0, s, adv, n, scratch);
+    hipLaunchKernelGGL(k_pw_chunks<1>, dim3(nchunks), dim3(64), 0, s, adv, n, scratch);
+    const int64_t nb = std::min<int64_t>((n + 1023) / 1024, 2048);
+    hipLaunchKernelGGL(k_adv_apply, dim3((unsigned)nb), dim3(256), 0, s, adv, n, scratch, eps, mean_std_out);
+    GS_LAUNCH_CHECK("k_adv_apply");
     return GS_OK;
 }
 

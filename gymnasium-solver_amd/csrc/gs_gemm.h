@@ -52,9 +52,12 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
 
 
 // out[r,oy,ox,co] = relu(bias[co] + sum_{c,ky,kx} W[co][c][ky][kx] * frame[c][oy*s+ky][ox*s+kx] / 255)
-int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out);
+// (relu = false: the pre-activation, for the activation statistics)
+int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out,
+                bool relu = true);
 // out[r,oy,ox,co] = relu(bias[co] + sum_{ky,kx,c} W[co][ky][kx][c] * in[r, oy*s+ky, ox*s+kx, c])
-int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out);
+int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out,
+                  bool relu = true);
 // dW[co][patch] = sum over rows of dY[row][co] * patch(row): split over `splits` row slices
 // into parts (splits * Cout * patch floats), then summed in slice order into dW.
 int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,

@@ -451,24 +451,26 @@ int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, c
     return dispatch<false, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
 }
 
-int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out)
+int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out,
+                bool relu)
 {
     int rc = check_geom(g);
     if (rc) return rc;
     GS_REQUIRE(g.k % 4 == 0 && g.s % 4 == 0 && g.W % 4 == 0, "conv_fwd_u8: needs k, s, W multiples of 4");
     const int64_t M = g.rows(), K = g.patch();
     return dispatch<true, true>(s, u8_patches(g, f), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0, 0.0f,
-                                bias, true);
+                                bias, relu);
 }
 
-int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out)
+int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out,
+                  bool relu)
 {
     int rc = check_geom(g);
     if (rc) return rc;
     GS_REQUIRE(g.C % 4 == 0 && ((uintptr_t)in & 15) == 0, "conv_fwd_nhwc: channels must be float4-aligned");
     const int64_t M = g.rows(), K = g.patch();
     return dispatch<true, true>(s, nhwc_patches(g, in), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0,
-                                0.0f, bias, true);
+                                0.0f, bias, relu);
 }
 
 int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int rows, int ncols, float *dW,

@@ -418,6 +418,8 @@ extern "C" int gs_ppo_minibatch_step(float *params, float *grads, float *adam_m,
     if (rc) return rc;
     GS_REQUIRE(adam_step >= 1, "adam_step is 1-based");
     GS_REQUIRE(params && grads && adam_m && adam_v && idx && metrics, "gs_ppo_minibatch_step: null buffer");
+    GS_REQUIRE(!(hp.flags & GS_HP_BF16), "gs_ppo_minibatch_step: precision bf16 is a mode of the fused chain "
+                                         "(gs_ppo_update) only; the single-step entries are fp32");
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
     const StepArgs sa = make_step_args(hp, L, batch, adam_step);
@@ -441,6 +443,8 @@ extern "C" int gs_ppo_loss(const float *params, gs_mlp_dims dims, gs_ppo_hparams
     int rc = validate_update(dims, ro, batch, workspace);
     if (rc) return rc;
     GS_REQUIRE(params && idx && metrics, "gs_ppo_loss: null buffer");
+    GS_REQUIRE(!(hp.flags & GS_HP_BF16), "gs_ppo_loss: precision bf16 is a mode of the fused chain "
+                                         "(gs_ppo_update) only; the single-step entries are fp32");
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
     const StepArgs sa = make_step_args(hp, L, batch, 1);
@@ -459,6 +463,8 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
     int rc = validate_update(dims, ro, batch, workspace);
     if (rc) return rc;
     GS_REQUIRE(stage >= 0 && stage <= 7, "gs_ppo_stage: stage %d not in [0, 7]", stage);
+    GS_REQUIRE(!(hp.flags & GS_HP_BF16), "gs_ppo_stage: precision bf16 is a mode of the fused chain "
+                                         "(gs_ppo_update) only; the single-step entries are fp32");
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
     const StepArgs sa = make_step_args(hp, L, batch, adam_step < 1 ? 1 : adam_step);

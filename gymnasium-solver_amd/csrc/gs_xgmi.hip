@@ -577,6 +577,21 @@ extern "C" int gs_comm_xgmi_set_bwd_exchange(gs_comm *c, int mode)
     return GS_OK;
 }
 
+extern "C" int gs_comm_xgmi_reset(gs_comm *c)
+{
+    GS_REQUIRE(c && c->kind == kCommXgmi, "gs_comm_xgmi_reset: not an xGMI communicator");
+    // every rank's flag banks, sticky error and sequence counters back to the connect-time state;
+    // the caller brackets this with host barriers after every rank's device work drained
+    // (gsamd.distributed.xgmi_reset), so no peer store is in flight
+    GS_HIP(hipDeviceSynchronize());
+    GS_HIP(hipMemset(c->local, 0, kXgmiOffData));
+    if (c->nranks > 1) GS_HIP(hipMemset(c->local + c->off_bwd, 0, 2 * sizeof(uint32_t) * kBwdXMaxRanks * kBwdXMaxWG));
+    GS_HIP(hipMemset(c->seq, 0, sizeof(uint32_t) * kXgmiMaxWG));
+    if (c->seq_bwd) GS_HIP(hipMemset(c->seq_bwd, 0, sizeof(uint32_t) * kBwdXMaxWG));
+    GS_HIP(hipDeviceSynchronize());
+    return GS_OK;
+}
+
 extern "C" int gs_comm_status(gs_comm *c)
 {
     GS_REQUIRE(c, "gs_comm_status: null communicator");

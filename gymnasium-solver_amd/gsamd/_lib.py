@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before the library)
 LIB_PATH = os.environ.get("GSAMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
 
 GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
-GS_ABI_VERSION = 5          # include/gsamd.h: the argument lists this binding declares
+GS_ABI_VERSION = 6          # include/gsamd.h: the argument lists this binding declares
 GS_NUM_METRICS = 24
 METRIC_SLOTS = (
     "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
@@ -78,6 +78,10 @@ def _load():
     sig = {
         "gs_abi_version": (ctypes.c_int, []),
         "gs_last_error": (ctypes.c_char_p, []),
+        "gs_build_source_hash": (ctypes.c_char_p, [ctypes.c_char_p]),
+        "gs_normalize_advantages_scratch_bytes": (sz, [i64]),
+        "gs_normalize_advantages": (ctypes.c_int, [vp, i64, f32, vp, vp, vp]),
+        "gs_cnn_activation_stats": (ctypes.c_int, [vp, CnnDims, RolloutViewU8, vp, i64, vp, vp, vp]),
         "gs_gae_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i64, f64, f64, vp, vp, vp]),
         "gs_sampler_stream_i32": (ctypes.c_int, [i64, i64, u64, vp, ctypes.c_int]),
         "gs_mlp_param_count": (i64, [MlpDims]),
@@ -132,6 +136,7 @@ def _load():
         "gs_comm_error_record": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "gs_comm_xgmi_set_colocation": (ctypes.c_int, [vp, ctypes.c_int]),
         "gs_comm_xgmi_set_bwd_exchange": (ctypes.c_int, [vp, ctypes.c_int]),
+        "gs_comm_xgmi_reset": (ctypes.c_int, [vp]),
         "gs_comm_allreduce_mean_f32": (ctypes.c_int, [vp, vp, i64, vp]),
         "gs_comm_allreduce_sum_f64": (ctypes.c_int, [vp, vp, i64, vp]),
         "gs_ppo_global_adv_stats": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, i64, vp, vp, vp, vp]),
@@ -150,7 +155,8 @@ def _load():
 
 
 lib = _load()
-EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
+EXPORTED = ("gs_abi_version", "gs_last_error", "gs_build_source_hash", "gs_normalize_advantages_scratch_bytes", "gs_normalize_advantages",
+            "gs_cnn_activation_stats", "gs_gae_f32", "gs_sampler_stream_i32", "gs_mlp_param_count",
             "gs_policy_scratch_bytes", "gs_policy_act", "gs_policy_value", "gs_rollout_synth_supported",
             "gs_rollout_synth", "gs_env_reset", "gs_env_step",
             "gs_episode_stats", "gs_episode_window",
@@ -161,7 +167,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_gae_f32", "gs_sampler_stream_
             "gs_cnn_ppo_update_global",
             "gs_gemm_f32", "gs_fc_gemm", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status", "gs_comm_error_record",
-            "gs_comm_xgmi_set_colocation", "gs_comm_xgmi_set_bwd_exchange",
+            "gs_comm_xgmi_set_colocation", "gs_comm_xgmi_set_bwd_exchange", "gs_comm_xgmi_reset",
             "gs_comm_allreduce_mean_f32", "gs_comm_allreduce_sum_f64", "gs_ppo_global_adv_stats",
             "gs_ppo_global_records", "gs_comm_info", "gs_comm_destroy")
 

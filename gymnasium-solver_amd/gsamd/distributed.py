@@ -120,24 +120,43 @@ def _agree(ok: bool, device: Optional[torch.device]) -> bool:
     return bool(t.item())
 
 
-def xgmi_self_test(handle: int, rank: int, world_size: int, n: int, device: torch.device, rounds: int = 3) -> bool:
-    """Exchange known vectors a few times and compare every element with the exact
-    fixed-order answer (also proves the peers' flags arrive)."""
-    import numpy as np
+def _pattern(rank: int, it: int, n: int, device) -> torch.Tensor:
+    """Rank `rank`'s exchange test vector of round `it`: small integers (exact in float32), a
+    different value in every round and rank, so a stale slot from an earlier round shows."""
+    idx = torch.arange(n, dtype=torch.int64, device=device)
+    return ((rank + 1) * (it + 3) + (idx * (rank + 5) + it) % 11).to(torch.float32)
+
+
+def xgmi_self_test(handle: int, rank: int, world_size: int, n: int, device: torch.device, rounds: int = 3,
+                   salt: int = 0) -> bool:
+    """Exchange known vectors `rounds` times through gs_comm_allreduce_mean_f32 and compare every
+    element with the exact fixed-order answer ((x0 + x1) + ...) * f32(1 / world), computed on the
+    device (also proves the peers' flags arrive).  n: the communicator's full capacity is what
+    covers every exchange workgroup and chunk the job's gradient uses."""
     from ._lib import stream_handle
-    idx = np.arange(n, dtype=np.int64)
     for it in range(rounds):
-        vals = [((r + 1) * (it + 3) + (idx * (r + 5) + it) % 11).astype(np.float32) for r in range(world_size)]
-        buf = torch.from_numpy(vals[rank]).to(device)
+        r_it = it + 7 * int(salt)
+        buf = _pattern(rank, r_it, n, device)
         check(lib.gs_comm_allreduce_mean_f32(handle, buf.data_ptr(), n, stream_handle()), "gs_comm_allreduce_mean_f32")
-        acc = vals[0]
+        acc = _pattern(0, r_it, n, device)
         for r in range(1, world_size):
-            acc = acc + vals[r]
-        want = acc * np.float32(1.0 / world_size)
-        got = buf.cpu().numpy()
-        if lib.gs_comm_status(handle) != 0 or not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+            acc = acc + _pattern(r, r_it, n, device)
+        want = acc * torch.tensor(1.0 / world_size, dtype=torch.float32, device=device)
+        same = torch.equal(buf.view(torch.int32), want.view(torch.int32))
+        if lib.gs_comm_status(handle) != 0 or not same:
             return False
     return True
+
+
+def xgmi_reset(handle: int, device: Optional[torch.device] = None) -> None:
+    """Every rank back to the connect-time exchange state after a failed or timed-out exchange
+    (gs_comm_xgmi_reset between two host barriers, after each rank's device work drained).
+    Collective."""
+    import torch.distributed as dist
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    check(lib.gs_comm_xgmi_reset(handle), "gs_comm_xgmi_reset")
+    dist.barrier()
 
 
 def _digest(t: torch.Tensor) -> bytes:
@@ -145,10 +164,16 @@ def _digest(t: torch.Tensor) -> bytes:
     return hashlib.sha256(t.detach().cpu().numpy().tobytes()).digest()
 
 
-def _chain_run(handle: int, rank: int, dims, batch: int, steps: int, device: torch.device) -> torch.Tensor:
+_FAILED_DIGEST = bytes(32)          # sent by a rank whose chain raised: no real digest is all zeros
+
+
+def _chain_run(handle: int, rank: int, dims, batch: int, steps: int, device: torch.device,
+               flags: int = 0) -> torch.Tensor:
     """One fused-chain update of `steps` minibatches through gs_ppo_update on `handle`, from a
     fixed parameter state (identical on every rank) and a rank-specific synthetic batch set:
-    the exchange the job's own update runs, on the job's shapes.  Returns the new parameters."""
+    the exchange the job's own update runs, on the job's shapes and precision (flags = the job's
+    gs_ppo_hparams.flags: the bf16 chain exchanges from its own k_bwd instantiation).  Returns the
+    new parameters."""
     import numpy as np
     from ._lib import PPOHparams, RolloutView, GS_NUM_METRICS, stream_handle
     D, H1, H2, A = int(dims.obs_dim), int(dims.hidden1), int(dims.hidden2), int(dims.n_actions)
@@ -168,7 +193,7 @@ def _chain_run(handle: int, rank: int, dims, batch: int, steps: int, device: tor
     metrics = torch.zeros(steps, GS_NUM_METRICS, **z)
     stop = torch.zeros(1, dtype=torch.int32, device=device)
     ws = torch.zeros(int(lib.gs_ppo_update_workspace_bytes(dims, int(batch), steps)), dtype=torch.uint8, device=device)
-    hp = PPOHparams(0.2, 0.2, 0.5, 0.01, 0.5, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, 0)
+    hp = PPOHparams(0.2, 0.2, 0.5, 0.01, 0.5, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, int(flags))
     view = RolloutView(obs.data_ptr(), act.data_ptr(), lp.data_ptr(), val.data_ptr(), adv.data_ptr(), ret.data_ptr(), 1, N)
     check(lib.gs_ppo_update(p.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr(), dims, hp, view, idx.data_ptr(),
                             int(batch), steps, 0, metrics.data_ptr(), stop.data_ptr(), ws.data_ptr(), ws.numel(),
@@ -180,47 +205,58 @@ def _chain_run(handle: int, rank: int, dims, batch: int, steps: int, device: tor
     return p
 
 
+def _chain_agreed(handle, rank, world_size, dims, batch, steps, dev, device, flags):
+    """Run the chain, then ALWAYS all-gather a digest (a failing rank sends _FAILED_DIGEST), so every
+    rank runs the same collective sequence whatever failed where.  -> (params or None, ok, why)."""
+    try:
+        p, why = _chain_run(handle, rank, dims, batch, steps, dev, flags), ""
+    except RuntimeError as e:
+        p, why = None, str(e)
+    digests = _all_gather_bytes(_digest(p) if p is not None else _FAILED_DIGEST, device)
+    parts = {digests[32 * r:32 * (r + 1)] for r in range(world_size)}
+    ok = p is not None and len(parts) == 1 and _FAILED_DIGEST not in parts
+    if p is not None and not ok:
+        why = "a peer's chain failed" if _FAILED_DIGEST in parts else "replicas differ after the exchange"
+    return p, ok, why
+
+
 # what the last init_xgmi_comm's self-tests found (bench.py reports it beside its line)
 LAST_SELF_TEST: dict = {}
+# (handle, dims, batch, flags) whose in-backward exchange a self-test already verified
+_VERIFIED: set = set()
 
 
 def bwd_exchange_self_test(handle: int, rank: int, world_size: int, dims, batch: int,
-                           device: Optional[torch.device] = None, steps: int = 4) -> dict:
+                           device: Optional[torch.device] = None, steps: int = 4, flags: int = 0) -> dict:
     """The in-backward exchange (the fused MLP chain's default with one rank per GPU,
-    csrc/gs_xgmi_dev.h bwd_exchange) checked on the job's own shapes before the job trains:
-    `steps` fused-chain minibatches from a fixed state, each rank on its own synthetic rows,
+    csrc/gs_xgmi_dev.h bwd_exchange) checked on the job's own shapes and precision before the job
+    trains: `steps` fused-chain minibatches from a fixed state, each rank on its own synthetic rows,
     (1) with the exchange inside k_bwd — every rank must end with the same parameter bits —
     and (2) with the separate exchange launch (the form init_xgmi_comm's vector self-test
     proved) — the two must agree to the rounding of their different W1-partial fold order
     (relative L2 < 1e-4, the bar of test_xgmi_bwd_exchange_matches_exchange_launch), and the
     launch form's replicas must be bit-identical too.  A stale or torn slot read on any rank
-    breaks (1) or (2).  If the in-backward form fails, every rank switches to the launch form
-    (gs_comm_xgmi_set_bwd_exchange(0)) together; if the launch form fails as well this raises
-    on every rank (the caller falls back to RCCL).  Collective: every rank calls it together.
-    Returns {"in_bwd_checked", "in_bwd_ok", "launch_ok", "rel_l2", "steps"}."""
+    breaks (1) or (2).  Every rank runs the same collectives whatever fails (a failing rank sends a
+    sentinel digest); after a failure of (1) every rank resets the communicator (xgmi_reset: flags,
+    sticky error, sequence counters) before (2) and then uses the launch form
+    (gs_comm_xgmi_set_bwd_exchange(0)); if the launch form fails as well this raises on every rank
+    (the caller falls back to RCCL).  Collective: every rank calls it together.
+    Returns {"in_bwd_checked", "in_bwd_ok", "launch_ok", "rel_l2", "steps", "flags"}."""
     import sys
     import numpy as np
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    out = {"in_bwd_checked": False, "in_bwd_ok": None, "launch_ok": None, "rel_l2": None, "steps": int(steps)}
+    out = {"in_bwd_checked": False, "in_bwd_ok": None, "launch_ok": None, "rel_l2": None, "steps": int(steps),
+           "flags": int(flags)}
     if world_size <= 1 or not exchange_inside_bwd(handle, dims, batch):
         return out
     out["in_bwd_checked"] = True
-    ok_b, why = True, ""
-    try:
-        pb = _chain_run(handle, rank, dims, batch, steps, dev)
-        digests = _all_gather_bytes(_digest(pb), device)
-        ok_b = len(set(digests[32 * r:32 * (r + 1)] for r in range(world_size))) == 1
-        why = "" if ok_b else "replicas differ after the in-backward exchange"
-    except RuntimeError as e:
-        pb, ok_b, why = None, False, str(e)
+    pb, ok_b, why = _chain_agreed(handle, rank, world_size, dims, batch, steps, dev, device, flags)
+    ok_b = _agree(ok_b, device)
+    if not ok_b:
+        xgmi_reset(handle, dev)          # a timed-out wait leaves flags / counters / the error word behind
     check(lib.gs_comm_xgmi_set_bwd_exchange(handle, 0), "gs_comm_xgmi_set_bwd_exchange")
-    ok_l = True
-    try:
-        pl = _chain_run(handle, rank, dims, batch, steps, dev)
-        digests = _all_gather_bytes(_digest(pl), device)
-        ok_l = len(set(digests[32 * r:32 * (r + 1)] for r in range(world_size))) == 1
-    except RuntimeError as e:
-        pl, ok_l, why = None, False, why or str(e)
+    pl, ok_l, why_l = _chain_agreed(handle, rank, world_size, dims, batch, steps, dev, device, flags)
+    why = why or why_l
     if ok_b and ok_l:
         a, b = pb.double().cpu().numpy(), pl.double().cpu().numpy()
         out["rel_l2"] = float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
@@ -235,22 +271,38 @@ def bwd_exchange_self_test(handle: int, rank: int, world_size: int, dims, batch:
     check(lib.gs_comm_xgmi_set_bwd_exchange(handle, 1 if ok_b else 0), "gs_comm_xgmi_set_bwd_exchange")
     if ok_b and not exchange_inside_bwd(handle, dims, batch):
         check(lib.gs_comm_xgmi_set_bwd_exchange(handle, 2), "gs_comm_xgmi_set_bwd_exchange")
+    if ok_b:
+        _VERIFIED.add(_verify_key(handle, dims, batch, flags))
     if rank == 0:
         print(f"[gsamd] xGMI in-backward exchange self-test ({world_size} ranks, {steps} minibatches, "
-              f"dims {int(dims.obs_dim)}-{int(dims.hidden1)}-{int(dims.hidden2)}-{int(dims.n_actions)}, B={batch}): "
+              f"dims {int(dims.obs_dim)}-{int(dims.hidden1)}-{int(dims.hidden2)}-{int(dims.n_actions)}, B={batch}, "
+              f"flags {int(flags)}): "
               + ("replicas bit-identical, vs exchange launch rel L2 %.2e" % out["rel_l2"] if ok_b else
                  f"FAILED ({why or 'a peer failed'}); every rank uses the exchange launch"), file=sys.stderr, flush=True)
     return out
+
+
+def _verify_key(handle, dims, batch, flags):
+    return (int(handle), int(dims.obs_dim), int(dims.hidden1), int(dims.hidden2), int(dims.n_actions), int(batch),
+            int(flags))
+
+
+def verified(handle, dims, batch, flags) -> bool:
+    """Whether bwd_exchange_self_test already verified this communicator on these shapes / flags."""
+    return _verify_key(handle, dims, batch, flags) in _VERIFIED
 
 
 def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[torch.device] = None,
                    self_test: bool = True, verify_shapes=None) -> int:
     """One-shot xGMI communicator for exchanges of up to max_count floats (the policy's
     parameter count): create, all-gather the handles, open the peers, barrier, then (by
-    default) a bit-exact self-test agreed on by every rank.  Raises RuntimeError on every
-    rank if any rank fails (the caller may then choose RCCL instead).  verify_shapes =
-    (gs_mlp_dims, batch): also check the in-backward exchange on those shapes
-    (bwd_exchange_self_test; it drops every rank to the exchange launch if that form fails)."""
+    default) a bit-exact self-test agreed on by every rank over the FULL max_count (every exchange
+    workgroup and chunk the job's gradient will use: the NatureCNN's 1.69 M floats included).
+    Raises RuntimeError on every rank if any rank fails (the caller may then choose RCCL
+    instead).  verify_shapes = (gs_mlp_dims, batch[, flags]): also check the in-backward exchange
+    on those shapes and that precision (bwd_exchange_self_test; it drops every rank to the exchange
+    launch if that form fails).  DevicePPOAgent runs the same check itself on its first update with
+    a communicator attached, so a launcher that passes no verify_shapes is still covered."""
     import torch.distributed as dist
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     h, ok, why = None, True, ""
@@ -276,7 +328,7 @@ def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[
     dist.barrier()
     if ok and self_test:
         try:
-            ok = xgmi_self_test(h, rank, world_size, min(int(max_count), 1 << 16), dev)
+            ok = xgmi_self_test(h, rank, world_size, int(max_count), dev)
             why = "" if ok else "self-test mismatch or timeout"
         except RuntimeError as e:
             ok, why = False, str(e)
@@ -285,8 +337,9 @@ def init_xgmi_comm(rank: int, world_size: int, max_count: int, device: Optional[
     LAST_SELF_TEST["exchange_launch_ok"] = bool(ok) if self_test else None
     if ok and self_test and verify_shapes is not None:
         try:
+            flags = int(verify_shapes[2]) if len(verify_shapes) > 2 else 0
             LAST_SELF_TEST.update(bwd_exchange_self_test(h, rank, world_size, verify_shapes[0], int(verify_shapes[1]),
-                                                         dev))
+                                                         dev, flags=flags))
         except RuntimeError as e:
             ok, why = False, str(e)
     if not ok:

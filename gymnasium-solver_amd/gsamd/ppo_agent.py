@@ -32,6 +32,7 @@ from .policy import DeviceMLPActorCritic
 from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSyntheticVecEnv
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler, index_stream, rank_share
 from .distributed import allreduce_sum_f64, broadcast_int, check_replicas, comm_status, world_active
+from . import distributed as _dist
 from .metrics import NUM_SUMS, MetricsRecorder, activation_stats, ppo_keys, ppo_records
 from .schedules import SCHEDULABLE, build_schedulers
 
@@ -165,7 +166,13 @@ class DevicePPOAgent:
         self._rollout_collectors[stage] = DeviceRolloutCollector(
             self.get_env(stage), self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
             rng_seed=c.seed + 7919 * self.rank, track_stats=self.track_stats, use_graph=self.use_graph,
-            one_launch=self.one_launch)
+            one_launch=self.one_launch, normalize_advantages=self._rollout_adv_norm())
+
+    def _rollout_adv_norm(self) -> bool:
+        """normalize_advantages == "rollout": the collector normalises each rollout's advantages
+        (utils/config.py:709-710 hands the collector that flag); "batch" is the loss's own
+        per-minibatch normalisation (hparams().normalize_adv), "off" neither."""
+        return str(getattr(self.config, "normalize_advantages", "batch")) == "rollout"
 
     def get_rollout_collector(self, stage: str) -> DeviceRolloutCollector:
         if stage not in self._rollout_collectors and stage in ("val", "test"):
@@ -175,7 +182,8 @@ class DevicePPOAgent:
             env = self._envs[stage]
             self._rollout_collectors[stage] = DeviceRolloutCollector(
                 env, self.policy_model, c.n_steps, gamma=c.gamma, gae_lambda=c.gae_lambda,
-                rng_seed=c.seed + 1000 + 7919 * self.rank, track_stats=True)
+                rng_seed=c.seed + 1000 + 7919 * self.rank, track_stats=True,
+                normalize_advantages=self._rollout_adv_norm())
         return self._rollout_collectors[stage]
 
     # ---- checkpoints (agents/base_agent.py:658-885) -----------------------------------------
@@ -307,6 +315,11 @@ class DevicePPOAgent:
         if self.global_mode:
             if self.is_pixel and c.target_kl is not None:
                 raise ValueError("dp_mode 'global' of the NatureCNN update has no KL early stop: unset target_kl")
+            if self._rollout_adv_norm() and self.world_size > 1:
+                # the reference normalises over the single process's whole rollout; each rank here
+                # holds a share of it, and the statistics are not summed over ranks
+                raise ValueError("dp_mode 'global' with normalize_advantages='rollout' is not supported over "
+                                 "several ranks: use 'batch' (whole-global-minibatch statistics) or dp_mode 'local'")
             self.n_minibatches = self.data_len * self.world_size // self.batch_size * c.n_epochs
             z64 = dict(dtype=torch.float64, device=self.device)
             self._gsums = torch.zeros(self.n_minibatches, NUM_SUMS, **z64)
@@ -489,6 +502,14 @@ class DevicePPOAgent:
         if not self.global_mode:
             self.prefetcher.prefetch(epoch + 1)
         buf = collector.buffer
+        if self.world_size > 1:
+            if self.global_mode and not self.comm:
+                # the mode's advantage statistics, loss records and gradient are sums over ranks:
+                # without a communicator each rank would train on its own rows' share only
+                raise ValueError("dp_mode 'global' with world_size > 1 needs a communicator (agent.comm = "
+                                 "init_xgmi_comm(...) or init_device_comm(...))")
+            if self.comm:
+                self._verify_exchange()
         self._activation_stats_launch(buf, idx)
         if ev:
             ev[-1][1].record()
@@ -519,6 +540,7 @@ class DevicePPOAgent:
             # a mismatch (DESIGN §5 Failure surfacing)
             if self.world_size > 1:
                 check_replicas(self.policy_model.params)
+                self._exchange_canary()
         if self.config.target_kl is None:
             self.adam_step += self.n_minibatches
         else:       # minibatches from the sticky KL stop on took no optimizer step
@@ -526,14 +548,60 @@ class DevicePPOAgent:
         self.current_epoch += 1
         self.on_train_epoch_end()
 
+    def _verify_exchange(self) -> None:
+        """Before the first update with an xGMI communicator attached (every rank reaches it
+        together): the in-backward exchange of the MLP chain is self-tested on THIS job's shapes and
+        precision (gsamd.distributed.bwd_exchange_self_test: replicas bit-identical, agreement
+        with the exchange launch; on failure every rank switches to the launch form together),
+        unless the launcher's init_xgmi_comm(verify_shapes=...) already did; the result is kept in
+        self.exchange_self_test.  The NatureCNN update exchanges with a launch only, which
+        init_xgmi_comm's full-capacity vector self-test covers."""
+        if getattr(self, "_exchange_checked", False):
+            return
+        self._exchange_checked = True
+        self.exchange_self_test = None
+        if _dist.comm_info(self.comm)["transport"] != "xgmi" or self.is_pixel:
+            return
+        dims, flags = self.policy_model.dims, int(self.hparams().flags)
+        if _dist.verified(self.comm, dims, self.batch_size, flags):
+            self.exchange_self_test = dict(_dist.LAST_SELF_TEST)
+            return
+        self.exchange_self_test = _dist.bwd_exchange_self_test(self.comm, self.rank, self.world_size, dims,
+                                                               self.batch_size, self.device, flags=flags)
+
+    def _exchange_canary(self) -> None:
+        """Once per epoch, after the replica check: one exchange of a known, epoch-dependent
+        pattern over the whole parameter count through the job's xGMI communicator, compared bit
+        for bit on every rank with the exact rank-order answer.  The replica check sees only
+        asymmetric faults; a slot read stale identically on every rank keeps the replicas equal
+        but fails this.  GsError on every rank on a mismatch."""
+        if _dist.comm_info(self.comm)["transport"] != "xgmi":
+            return
+        self._canary_round = getattr(self, "_canary_round", 0) + 1
+        ok = _dist.xgmi_self_test(self.comm, self.rank, self.world_size, self.policy_model.n_params, self.device,
+                                  rounds=1, salt=self._canary_round)
+        if not _dist._agree(ok, self.device):
+            from ._lib import GsError
+            raise GsError(f"exchange canary failed on epoch {self.current_epoch} (rank {self.rank}): a known "
+                          f"vector did not come back as its exact rank-order mean through the xGMI exchange")
+
     def _activation_stats_launch(self, buf, idx) -> None:
-        """The reference records opt/activations/backbone.{0,2}/* on every training_step
-        (base_agent.py:336-347, utils/models.py:120-190); the device agent computes them once per
-        epoch, on the epoch's first minibatch with the parameters that minibatch's step reads,
-        on the update's stream ahead of it (gs_mlp_activation_stats; SURVEY §8b: diagnostics
-        may be computed per epoch).  MLP policies; off with track_stats=False."""
+        """The reference records opt/activations/<layer>/* on every training_step
+        (base_agent.py:336-347, utils/models.py:120-190; MLP: backbone.{0,2}, NatureCNN: cnn.{0,2,4}
+        and mlp.0, models.py:419-422); the device agent computes them once per epoch, on the
+        epoch's first minibatch with the parameters that minibatch's step reads, on the update's
+        stream ahead of it (gs_mlp_activation_stats / gs_cnn_activation_stats; SURVEY §8b:
+        diagnostics may be computed per epoch).  Off with track_stats=False."""
         self._act_pending = False
-        if self.is_pixel or self.global_mode or not self.track_stats or idx is None:
+        if self.global_mode or not self.track_stats or idx is None:
+            return
+        if self.is_pixel:
+            if getattr(self, "_act_stats", None) is None:
+                self._act_stats = torch.zeros(16, dtype=torch.float64, device=self.device)
+            check(lib.gs_cnn_activation_stats(ptr(self.policy_model.params), self.policy_model.dims, buf.view(),
+                                              ptr(idx), self.batch_size, ptr(self._act_stats), ptr(self.workspace),
+                                              stream_handle()), "gs_cnn_activation_stats")
+            self._act_pending = True
             return
         dims = self.policy_model.dims
         nparts = (self.batch_size + 15) // 16
@@ -544,10 +612,13 @@ class DevicePPOAgent:
                                           ptr(self._act_parts), stream_handle()), "gs_mlp_activation_stats")
         self._act_pending = True
 
+    CNN_ACTIVATION_LAYERS = ("cnn.0", "cnn.2", "cnn.4", "mlp.0")
+
     def activation_keys(self):
-        if self.is_pixel or self.global_mode or not self.track_stats:
+        if self.global_mode or not self.track_stats:
             return ()
-        return tuple(f"opt/activations/backbone.{i}/{k}" for i in (0, 2) for k in ("mean", "std", "dead_pct", "dead_max"))
+        layers = self.CNN_ACTIVATION_LAYERS if self.is_pixel else ("backbone.0", "backbone.2")
+        return tuple(f"opt/activations/{n}/{k}" for n in layers for k in ("mean", "std", "dead_pct", "dead_max"))
 
     def global_shares(self, epoch: int) -> np.ndarray:
         """This rank's rows of every global minibatch of `epoch` (padded with -1): the reference's
@@ -620,7 +691,10 @@ class DevicePPOAgent:
         stepped = rec[rec[:, M["skipped"]] == 0]
         keys, slots = self.grad_norm_keys()
         self.metrics_recorder.record_rows("train", keys, stepped[:, slots])
-        if getattr(self, "_act_pending", False):
+        if getattr(self, "_act_pending", False) and self.is_pixel:
+            self.metrics_recorder.record("train", dict(zip(self.activation_keys(),
+                                                           self._act_stats.cpu().numpy().tolist())))
+        elif getattr(self, "_act_pending", False):
             dims = self.policy_model.dims
             parts = self._act_parts.cpu().numpy().reshape((self.batch_size + 15) // 16, -1)
             self.metrics_recorder.record("train", activation_stats(parts, self.batch_size,

@@ -218,7 +218,7 @@ class DeviceRolloutCollector:
 
     def __init__(self, env, policy_model, n_steps, *, gamma: float = 0.99, gae_lambda: float = 0.95,
                  stats_window_size: int = 100, rng_seed: int = 42, track_stats: bool = True,
-                 use_graph: bool = True, one_launch: bool = True, **kwargs):
+                 use_graph: bool = True, one_launch: bool = True, normalize_advantages: bool = False, **kwargs):
         self.env = env
         self.policy_model = policy_model
         self.n_steps = int(n_steps)
@@ -227,6 +227,10 @@ class DeviceRolloutCollector:
         self.device = policy_model.device
         self.rng_seed = int(rng_seed)
         self.track_stats = bool(track_stats)
+        # the rollout-level advantage normalisation (normalize_advantages == "rollout":
+        # utils/rollout_collector.py:441-442 with returns_advantages.py:61-64), after GAE on the device
+        self.normalize_advantages = bool(normalize_advantages)
+        self._adv_scratch = None
         # device envs: the T-step loop (policy act + env step per vector step) is captured once
         # per sampling mode into a hipGraph and replayed; the per-rollout counters reach the
         # kernels through a 2-word device clock (include/gsamd.h "Rollout clock")
@@ -348,6 +352,8 @@ class DeviceRolloutCollector:
                 self._episode_records()
         elif native:
             self._episode_window()
+        if self.normalize_advantages:
+            self._normalize_rollout_advantages()
         if not native:
             self.total_episodes += self.rollout_episodes
         self.rollout_fpss.append(N * T / max(time.time() - t0, 1e-9))
@@ -475,11 +481,30 @@ class DeviceRolloutCollector:
                                  bool(trunc[e]))
         self.rollout_episodes += int(np.count_nonzero(done))
 
+    def _normalize_rollout_advantages(self):
+        """adv = (adv - mean) / (std + 1e-8) over the whole rollout in place
+        (gs_normalize_advantages; utils/returns_advantages.py:61-64), after the pre-normalisation
+        advantage statistics were taken; with track_stats the normalised advantages feed the
+        roll/adv_norm/* running statistics (utils/rollout_collector.py:441-448)."""
+        buf = self._buffer
+        if self._adv_scratch is None:
+            nb = int(lib.gs_normalize_advantages_scratch_bytes(buf.advantages.numel()))
+            self._adv_scratch = torch.zeros(max(1, nb // 4), dtype=torch.float32, device=self.device)
+            self.adv_mean_std = torch.zeros(2, dtype=torch.float32, device=self.device)
+        check(lib.gs_normalize_advantages(ptr(buf.advantages), buf.advantages.numel(), 1e-8, ptr(self._adv_scratch),
+                                          ptr(self.adv_mean_std), stream_handle()), "gs_normalize_advantages")
+        if self.track_stats:
+            s = self._stats
+            s[10] += buf.advantages.sum(dtype=torch.float64)
+            s[11] += (buf.advantages.double() ** 2).sum()
+            s[12] += buf.advantages.numel()
+
     def _accumulate_stats(self):
-        """Device-side RunningStats sums (utils/rollout_stats.py:34-67) for get_metrics."""
+        """Device-side RunningStats sums (utils/rollout_stats.py:34-67) for get_metrics (slots 10-12:
+        the normalised advantages, filled by _normalize_rollout_advantages)."""
         buf = self._buffer
         if self._stats is None:
-            self._stats = torch.zeros(10, dtype=torch.float64, device=self.device)
+            self._stats = torch.zeros(13, dtype=torch.float64, device=self.device)
         s = self._stats
         s[0] += buf.obs.numel()
         if buf.obs.dtype == torch.uint8:     # exact, without a float copy of the frames
@@ -611,6 +636,8 @@ class DeviceRolloutCollector:
         else:
             m["roll/actions/mean"], m["roll/actions/std"], m["action_dist"] = 0.0, 0.0, None
         m["roll/baseline/mean"], m["roll/baseline/std"] = zero
+        if self.normalize_advantages and n_stats and s[12] > 0:      # rollout_collector.py:748-750
+            m["roll/adv_norm/mean"], m["roll/adv_norm/std"] = mean_std(s[10], s[11], s[12])
         if dev_eps:
             cnt = part[-3]
             m["cnt/total_episodes"] = int(cnt)

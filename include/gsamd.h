@@ -44,10 +44,16 @@ extern "C" {
  * gs_env_step / gs_atari_env_step and gs_comm_error_record; version 3 widened the metric record
  * to 24 floats and added gs_ppo_update_global; version 4 added gs_comm_xgmi_set_bwd_exchange, gs_comm_allreduce_sum_f64,
  * gs_ppo_global_adv_stats, gs_ppo_global_records, gs_cnn_ppo_update_global, gs_fc_gemm and
- * gs_episode_window; version 5 added the obs_store argument of gs_cnn_policy_act). */
-#define GS_ABI_VERSION 5
+ * gs_episode_window; version 5 added the obs_store argument of gs_cnn_policy_act; version 6 added
+ * gs_normalize_advantages(_scratch_bytes), gs_cnn_activation_stats, gs_build_source_hash and
+ * gs_comm_xgmi_reset). */
+#define GS_ABI_VERSION 6
 int gs_abi_version(void);
 const char *gs_last_error(void);
+/* sha256 prefix (16 hex digits) of the kernel sources this library was compiled from: path "mlp"
+ * (the MLP chain + GAE), "cnn" (the NatureCNN update) or "" (every csrc/ file) — the key under
+ * which measured PMC traffic (profiles/) is attributed to a build; NULL for an unknown path. */
+const char *gs_build_source_hash(const char *path);
 
 /* ---------------------------------------------------------------- GAE
  * Replaces utils/returns_advantages.py:115-155
@@ -60,6 +66,16 @@ int gs_gae_f32(const float *values_dev, const float *rewards_dev, const uint8_t 
                const uint8_t *timeouts_dev, const float *bootstrap_dev, const float *last_values_dev,
                int64_t T, int64_t N, double gamma, double gae_lambda, float *adv_dev, float *ret_dev,
                void *stream);
+/* Rollout-level advantage normalisation, in place over all n elements: replaces
+ * utils/returns_advantages.py:61-64 (_normalize_advantages: (a - mean) / (std + eps), std biased),
+ * applied by utils/rollout_collector.py:441-442 when normalize_advantages == "rollout".  Bit-exact
+ * with numpy on the float32 array: the mean's and std's sums are numpy's float32 pairwise sums over
+ * its 8192-element buffer chunks, the statistics and the elementwise pass float32.  scratch_dev:
+ * gs_normalize_advantages_scratch_bytes(n) bytes; mean_std_out_dev (2 floats: the mean and std
+ * applied) may be NULL.  1 <= n < 2^31. */
+size_t gs_normalize_advantages_scratch_bytes(int64_t n);
+int gs_normalize_advantages(float *adv_dev, int64_t n, float eps, float *scratch_dev, float *mean_std_out_dev,
+                            void *stream);
 
 /* ---------------------------------------------------------------- sampler (host)
  * Replaces utils/samplers.py:25-34 (MultiPassRandomSampler.set_epoch + __iter__):
@@ -371,6 +387,16 @@ int gs_cnn_policy_act(const float *params_dev, gs_cnn_dims dims, const uint8_t *
 int gs_cnn_ppo_loss(const float *params_dev, gs_cnn_dims dims, gs_ppo_hparams hp, gs_rollout_view_u8 rollout,
                     const int32_t *idx_dev, int64_t batch, float *metrics_dev, float *dlogits_dev,
                     void *workspace_dev, void *stream);
+/* Activation statistics of the NatureCNN on one minibatch (the reference's forward hooks,
+ * utils/models.py:121-147, registered on cnn.0 / cnn.2 / cnn.4 / mlp.0 at :419-422 and recorded
+ * per training step at agents/base_agent.py:335-347): stats_out_dev receives 16 doubles, per
+ * layer in that order {mean, std (unbiased), dead_pct, dead_max} of the layer's pre-activation
+ * output over the batch rows (dead: |z| < 1e-6, per-neuron fraction of rows; dead_pct its mean
+ * over neurons, dead_max its max).  fp32 (the reference's precision) whatever the update's mode;
+ * uses the update's workspace (gs_cnn_workspace_bytes(dims, batch)). */
+int gs_cnn_activation_stats(const float *params_dev, gs_cnn_dims dims, gs_rollout_view_u8 rollout,
+                            const int32_t *idx_dev, int64_t batch, double *stats_out_dev, void *workspace_dev,
+                            void *stream);
 /* n_minibatches fused steps (forward, loss, backward, optional all-reduce, clip, Adam).
  * params / grads / adam_m / adam_v: 16-byte aligned (the clip + Adam kernel moves float4s). */
 int gs_cnn_ppo_update(float *params_dev, float *grads_dev, float *adam_m_dev, float *adam_v_dev, gs_cnn_dims dims,
@@ -482,6 +508,11 @@ int gs_comm_xgmi_set_colocation(struct gs_comm *comm, int ranks_per_device);
  * job's shapes and sets mode 0 on every rank when it fails.  Every rank must set the same mode
  * before its next update; captured update graphs are keyed by it.  Host-only, no GPU call. */
 int gs_comm_xgmi_set_bwd_exchange(struct gs_comm *comm, int mode);
+/* Back to the connect-time protocol state after a failed or timed-out exchange: this rank's flag
+ * banks, sticky error word and sequence counters are zeroed (synchronous).  Collective in the
+ * caller's protocol: every rank drains its device work, meets the others at a host barrier, calls
+ * this, and meets them again before the next exchange (gsamd.distributed.xgmi_reset). */
+int gs_comm_xgmi_reset(struct gs_comm *comm);
 int gs_comm_allreduce_mean_f32(struct gs_comm *comm, float *buf_dev, int64_t count, void *stream);
 /* Sum of `count` doubles over ranks, in place (16-B aligned buffer), the same result bits on every
  * rank: xGMI sums the sources in rank order in double (pieces of the communicator's capacity),

@@ -265,3 +265,58 @@ def gae_numpy(values, rewards, dones, timeouts, last_values, bootstrap, gamma, l
         gae = delta + (c2 * gae) * nt[t]
         adv[t] = gae
     return adv, adv + values
+
+
+def numpy_f32_sum(a) -> np.float32:
+    """numpy's float32 np.add.reduce of a contiguous array, restated (what gs_normalize_advantages
+    reproduces on the device): sequential over 8192-element buffer chunks from 0, each chunk by
+    pairwise_sum (numpy/_core/src/umath/loops_utils.h.src): n < 8 a plain loop from 0; n <= 128 eight
+    strided accumulators, ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the n % 8 rest;
+    else split at n2 = n // 2 - (n // 2) % 8.  Pinned against numpy itself in
+    tests/test_oracle_golden.py."""
+    a = np.ascontiguousarray(a, F32).reshape(-1)
+
+    def pw(x):
+        n = x.size
+        if n < 8:
+            r = F32(0)
+            for v in x:
+                r = F32(r + v)
+            return r
+        if n <= 128:
+            r = x[:8].copy()
+            m = n - n % 8
+            for i in range(8, m, 8):
+                r = (r + x[i:i + 8]).astype(F32)
+            res = F32(F32(F32(r[0] + r[1]) + F32(r[2] + r[3])) + F32(F32(r[4] + r[5]) + F32(r[6] + r[7])))
+            for i in range(m, n):
+                res = F32(res + x[i])
+            return res
+        n2 = n // 2
+        n2 -= n2 % 8
+        return F32(pw(x[:n2]) + pw(x[n2:]))
+
+    total = F32(0)
+    for c in range(0, a.size, 8192):
+        total = F32(total + pw(a[c:c + 8192]))
+    return total
+
+
+def normalize_advantages_rollout(adv, eps: float = 1e-8) -> np.ndarray:
+    """utils/returns_advantages.py:61-64 (_normalize_advantages), the rollout-level normalisation
+    of utils/rollout_collector.py:441-442: (a - mean) / (std + eps) over every element, numpy
+    float32 statistics (std biased)."""
+    a = np.asarray(adv, F32)
+    flat = a.reshape(-1)
+    return (a - flat.mean()) / (flat.std() + float(eps))
+
+
+def normalize_advantages_model(adv, eps: float = 1e-8) -> np.ndarray:
+    """normalize_advantages_rollout written out with numpy_f32_sum (the device kernel's steps):
+    mean = S / n, std = sqrt(S((a - mean)^2) / n), all float32."""
+    a = np.asarray(adv, F32)
+    n = F32(a.size)
+    mean = F32(numpy_f32_sum(a) / n)
+    d = (a - mean).astype(F32)
+    std = np.sqrt(F32(numpy_f32_sum((d * d).astype(F32)) / n)).astype(F32)
+    return ((a - mean) / F32(std + F32(eps))).astype(F32)

@@ -478,49 +478,6 @@ def guard_worker(rank, world, port, result_dir, bwd="1"):
         dist.destroy_process_group()
 
 
-def cnn_global_worker(rank, world, port, result_dir, ref_path):
-    """dp_mode 'global' for NatureCNN (gs_cnn_ppo_update_global): the single-process run's 8
-    Breakout envs split 4 + 4 over 2 same-device ranks, each replaying that run's actions of its
-    envs for two rollouts + updates.  Saves every minibatch record and the final parameters."""
-    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
-    dist = _init(rank, world, port)
-    try:
-        import torch
-        from gsamd.config import load_config
-        from gsamd.distributed import comm_status, destroy_comm, init_xgmi_comm
-        from gsamd.ppo_agent import DevicePPOAgent
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda:0")
-        z = np.load(ref_path)
-        N, T = (int(x) for x in z["NT"])
-        n = N // world
-        torch.manual_seed(42 + rank)        # the sampler seed comes from rank 0 (ADVICE r3)
-        cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(
-            env_dynamics="synthetic", n_envs=n, n_steps=T, batch_size=int(z["B"]), n_epochs=int(z["E"]),
-            dp_mode="global", clip_range=10.0, clip_range_vf=10.0))
-        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
-        agent.policy_model.params.copy_(torch.from_numpy(z["p0"]).to(dev))
-        agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
-        coll = agent.get_rollout_collector("train")
-        recs = []
-        for ep in range(z["actions"].shape[0]):
-            acts = torch.as_tensor(z["actions"][ep][:, rank * n:(rank + 1) * n].copy()).to(dev)
-            coll.collect(replay_actions=acts)
-            agent.update_phase()
-            recs.append(agent.metrics_buf.cpu().numpy().copy())
-        torch.cuda.synchronize()
-        comm_status(agent.comm)
-        np.savez(os.path.join(result_dir, f"c{rank}.npz"), rec=np.concatenate(recs),
-                 p=agent.policy_model.params.cpu().numpy())
-        dist.barrier()
-        comm = agent.comm
-        del agent
-        destroy_comm(comm)
-        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
-    finally:
-        dist.destroy_process_group()
-
-
 def replica_check_cpu_worker(rank, world, port, result_dir):
     """CPU (gloo) half of the multi-GPU guards: check_replicas passes on identical parameters and
     raises GsError on EVERY rank once one rank's parameters differ in one element (also a swap of
@@ -547,5 +504,144 @@ def replica_check_cpu_worker(rank, world, port, result_dir):
                 outcomes.append("GsError" if "replica check failed" in str(e) else "other")
         open(os.path.join(result_dir, f"rc{rank}"), "w").write(",".join(outcomes))
         open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def cnn_global_tf_worker(rank, world, port, result_dir, ref_path, states_path):
+    """Teacher-forced dp_mode 'global' for NatureCNN: the single-process run's envs split over
+    `world` same-device ranks, replaying that run's actions; then, for every global minibatch k,
+    every rank restarts from the single run's (params, adam_m, adam_v) before step k and runs that
+    ONE minibatch through gs_cnn_ppo_update_global (its share of the rows, global advantage
+    statistics, the ranks' gradient shares summed over xGMI), so each step's arithmetic is compared
+    without Adam carrying earlier differences forward.  Rank 0 saves every step's clipped gradient
+    and new parameters; every rank saves a digest of them (replicas must agree bit for bit); the
+    records come from gs_ppo_global_records over all steps."""
+    import ctypes
+    import hashlib
+    os.environ.setdefault("GS_XGMI_TIMEOUT_S", "60")
+    dist = _init(rank, world, port)
+    try:
+        import torch
+        from gsamd._lib import PPOGlobal, check, lib, ptr, stream_handle
+        from gsamd.config import load_config
+        from gsamd.distributed import comm_status, destroy_comm, init_xgmi_comm
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        z = np.load(ref_path)
+        with np.load(states_path) as f:
+            st = {k: f[k] for k in ("p", "m", "v")}
+        N, T = (int(x) for x in z["NT"])
+        n = N // world
+        torch.manual_seed(42 + rank)
+        cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(
+            env_dynamics="synthetic", n_envs=n, n_steps=T, batch_size=int(z["B"]), n_epochs=int(z["E"]),
+            dp_mode="global"))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
+        coll = agent.get_rollout_collector("train")
+        acts = torch.as_tensor(z["actions"][0][:, rank * n:(rank + 1) * n].copy()).to(dev)
+        coll.collect(replay_actions=acts)
+        pm, B, K = agent.policy_model, agent.batch_size, agent.n_minibatches
+        buf = coll.buffer
+        agent._gidx.copy_(torch.from_numpy(agent.global_shares(0)))
+        torch.clamp(agent._gidx, min=0, out=agent._fidx)
+        s = stream_handle()
+        comm = agent.comm
+        check(lib.gs_ppo_global_adv_stats(ptr(agent._gidx), K, B, B, ptr(buf.advantages), T, n, comm,
+                                          ptr(agent._adv_sums), ptr(agent._adv_stats), s), "gs_ppo_global_adv_stats")
+        hp = agent.hparams()
+        grads, params, digests = [], [], []
+        for k in range(K):
+            for t, name in ((pm.params, "p"), (agent.adam_m, "m"), (agent.adam_v, "v")):
+                t.copy_(torch.from_numpy(np.ascontiguousarray(st[name][k])).to(dev))
+            glob = PPOGlobal(B, ptr(agent._adv_stats[k]), ptr(agent._gsums[k]))
+            check(lib.gs_cnn_ppo_update_global(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v),
+                                               pm.dims, hp, buf.view(), ptr(agent._gidx[k * B:]),
+                                               ptr(agent._fidx[k * B:]), B, 1, k, ptr(agent.metrics_buf[k]),
+                                               ptr(agent.stop_flag), ptr(agent.workspace), comm, ctypes.byref(glob), s),
+                  "gs_cnn_ppo_update_global")
+            g_k, p_k = agent.grads.cpu().numpy(), pm.params.cpu().numpy()
+            digests.append(hashlib.sha256(g_k.tobytes() + p_k.tobytes()).hexdigest())
+            if rank == 0:
+                grads.append(g_k)
+                params.append(p_k)
+        check(lib.gs_ppo_global_records(ctypes.byref(hp), K, B, comm, ptr(agent._gsums), ptr(agent.metrics_buf), s),
+              "gs_ppo_global_records")
+        torch.cuda.synchronize()
+        comm_status(comm)
+        out = dict(rec=agent.metrics_buf.cpu().numpy(), digests=np.array(digests))
+        if rank == 0:
+            out.update(g=np.stack(grads), p=np.stack(params))
+        np.savez(os.path.join(result_dir, f"tf{rank}.npz"), **out)
+        dist.barrier()
+        del agent
+        destroy_comm(comm)
+    finally:
+        dist.destroy_process_group()
+
+
+def agent_selftest_worker(rank, world, port, result_dir, mode):
+    """The agent's own exchange guards on ranks sharing the box's GPU (GS_XGMI_BWD=1 forces the
+    in-backward form):
+      mode "mlp":    init_xgmi_comm WITHOUT verify_shapes (the documented recipe may omit it): the
+                     agent's first update runs bwd_exchange_self_test itself on its dims / batch /
+                     flags; then two epochs pass the replica check and the per-epoch canary;
+      mode "inject": as "mlp", but rank 1's first self-test chain raises before it exchanges
+                     (a stand-in for a failed launch): rank 0's in-backward wait times out, every
+                     rank still runs the same collectives (sentinel digest), resets the
+                     communicator and switches to the exchange launch together, and training
+                     continues on the launch form;
+      mode "cnn":    a NatureCNN-sized communicator (1 693 875 floats): the vector self-test covers
+                     the whole capacity, and a Breakout epoch passes the canary.
+    Saves each rank's record."""
+    import json
+    os.environ["GS_XGMI_TIMEOUT_S"] = "5" if mode == "inject" else "60"
+    os.environ["GS_XGMI_BWD"] = "1"
+    dist = _init(rank, world, port)
+    out = {}
+    try:
+        import torch
+        from gsamd.config import load_config
+        from gsamd import distributed as gd
+        from gsamd.ppo_agent import DevicePPOAgent
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        torch.manual_seed(42)
+        if mode == "cnn":
+            cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=8,
+                                                                           n_steps=32, batch_size=64, n_epochs=1))
+        else:
+            cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, n_epochs=1))
+        agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
+        pm = agent.policy_model
+        if mode == "inject" and rank == 1:
+            real = gd._chain_run
+            calls = {"n": 0}
+
+            def failing(*a, **k):
+                calls["n"] += 1
+                if calls["n"] == 1:
+                    raise RuntimeError("injected failure before the exchange")
+                return real(*a, **k)
+            gd._chain_run = failing
+        agent.comm = gd.init_xgmi_comm(rank, world, pm.n_params, dev)
+        out["connect_self_test"] = dict(gd.LAST_SELF_TEST)
+        out["n_params"] = int(pm.n_params)
+        for ep in range(2):
+            agent.train_epoch()
+        torch.cuda.synchronize()
+        out["epochs"] = "ok"
+        out["agent_self_test"] = agent.exchange_self_test
+        out["canary_rounds"] = int(getattr(agent, "_canary_round", 0))
+        if not agent.is_pixel:
+            out["inside"] = bool(gd.exchange_inside_bwd(agent.comm, pm.dims, agent.batch_size))
+        out["params_sha"] = __import__("hashlib").sha256(pm.params.cpu().numpy().tobytes()).hexdigest()
+        json.dump(out, open(os.path.join(result_dir, f"ast{rank}.json"), "w"))
+        dist.barrier()
+        comm = agent.comm
+        del agent
+        gd.destroy_comm(comm)
     finally:
         dist.destroy_process_group()

@@ -26,6 +26,11 @@ Fixtures written:
   ref_ckpt/        model.pt / optimizer.pt / state.json written by BaseAgent.save_checkpoint
                    (agents/base_agent.py:658-732) after the trajectory run
   synth_env.npz    the synthetic env's hashed observations (spec below, not a reference artefact)
+  adv_norm.npz     _normalize_advantages (utils/returns_advantages.py:61-64) on a few arrays,
+                   the rollout-level advantage normalisation (normalize_advantages "rollout")
+  trajectory_rollnorm.npz  the trajectory with normalize_advantages "rollout": the collector
+                   normalises each rollout's advantages (utils/rollout_collector.py:441-448) and
+                   losses_for_batch does not (utils/torch.py:148-173)
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -116,6 +121,7 @@ _pl.Trainer = object
 sys.modules["pytorch_lightning"] = _pl
 
 from utils.returns_advantages import compute_batched_gae_advantages_and_returns  # noqa: E402
+from utils.returns_advantages import _normalize_advantages  # noqa: E402
 from utils.samplers import MultiPassRandomSampler  # noqa: E402
 from utils.models import MLPActorCritic, CNNActorCritic  # noqa: E402
 from utils.rollout_collector import RolloutCollector  # noqa: E402
@@ -387,7 +393,33 @@ def _metrics_arrays(dicts):
     return np.array(keys), np.array([[float(d[k]) for k in keys] for d in dicts], np.float64)
 
 
-def make_trajectory(target_kl=None, out_name="trajectory.npz"):
+def make_adv_norm():
+    """_normalize_advantages on (T, N) float32 arrays: the C2 shape's scale, a (64, 256) normal
+    case, a large common offset (cancellation in the mean), a constant array (std 0: the result is
+    (a - mean) / 1e-8 = 0) and a single element."""
+    rng = np.random.default_rng(7)
+    cases = {
+        "normal": (rng.standard_normal((64, 256)) * 2.0 + 0.3).astype(np.float32),
+        "offset": (1000.0 + rng.standard_normal((32, 64)) * 0.01).astype(np.float32),
+        "skewed": np.exp(rng.standard_normal((48, 40)) * 1.5).astype(np.float32),
+        "constant": np.full((4, 8), 1.5, np.float32),
+        "single": np.array([[3.25]], np.float32),
+    }
+    out = {}
+    for k, a in cases.items():
+        flat = a.reshape(-1)
+        out[f"{k}/in"] = a
+        out[f"{k}/out"] = _normalize_advantages(a)
+        out[f"{k}/mean_std"] = np.array([flat.mean(), flat.std()], np.float32)
+    np.savez_compressed(os.path.join(HERE, "adv_norm.npz"), **out)
+    print("adv_norm.npz written")
+
+
+def make_trajectory_rollnorm():
+    make_trajectory(out_name="trajectory_rollnorm.npz", normalize="rollout")
+
+
+def make_trajectory(target_kl=None, out_name="trajectory.npz", normalize="batch"):
     """CartPole-v1:ppo shapes (C1: N=8, T=32, B=256, E=20) for 3 rollouts, through the
     reference's own training-step logic (agents/base_agent.py:330-366): the sticky KL early
     stop (`_early_stop_epoch`, never reset) skips the triggering minibatch's optimizer step and
@@ -402,8 +434,9 @@ def make_trajectory(target_kl=None, out_name="trajectory.npz"):
     params0 = _flat_params(model)
     env = SyntheticVecEnv(n_envs=N, obs_dim=D, n_actions=A, episode_len=20, seed=42, truncate_every=3)
     collector = RolloutCollector(_RefVecEnvAdapter(env), model, n_steps=T, gamma=0.98, gae_lambda=0.8,
-                                 returns_type="gae:rtg", advantages_type="gae", normalize_advantages=False)
-    cfg = dict(normalize="batch", clip=0.1, clip_vf=0.2, vf_coef=0.5, ent_coef=0.0, target_kl=target_kl)
+                                 returns_type="gae:rtg", advantages_type="gae",
+                                 normalize_advantages=normalize == "rollout")
+    cfg = dict(normalize=normalize, clip=0.1, clip_vf=0.2, vf_coef=0.5, ent_coef=0.0, target_kl=target_kl)
     agent, recs = _agent(model, cfg)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     traj_holder = {}
@@ -464,7 +497,7 @@ def make_trajectory(target_kl=None, out_name="trajectory.npz"):
     out["roll_metric_names"], out["roll_metric_values"] = _metrics_arrays(roll_metrics)
     out["action_dist"] = np.asarray(action_dist)
     out["train_metric_names"], out["train_metric_values"] = _metrics_arrays(recs)
-    if target_kl is None:
+    if target_kl is None and normalize == "batch":
         # evaluate_episodes on a second collector (the device agent's "val" stage: same env
         # shape, seed + 1000), deterministic, 20 episodes over 8 envs
         eval_env = SyntheticVecEnv(n_envs=N, obs_dim=D, n_actions=A, episode_len=20, seed=42 + 1000,
@@ -624,3 +657,5 @@ if __name__ == "__main__":
     make_trajectory_kl()
     make_configs_full()
     make_schedules()
+    make_adv_norm()
+    make_trajectory_rollnorm()

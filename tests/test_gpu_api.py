@@ -278,3 +278,66 @@ def test_build_agent_with_host_env_vs_reference_trajectory(golden, cuda):
     agent.policy_model.load_flat(z["params0"])
     recs = _replay_trajectory(agent, z, cuda, check_metrics=False)
     np.testing.assert_allclose(recs[:, 0], z["losses"], atol=1e-4, rtol=0)
+
+
+def test_rollout_advantage_normalisation_vs_reference(golden, cuda):
+    """normalize_advantages: rollout (utils/rollout_collector.py:441-448 with
+    utils/returns_advantages.py:61-64): the collector normalises every rollout's advantages over
+    the whole (T, N) buffer after GAE (gs_normalize_advantages) and the loss takes them as they
+    are (no per-minibatch normalisation, utils/torch.py:148-173).  Replays trajectory_rollnorm.npz
+    (the reference collector + losses_for_batch with that setting): the normalised advantages
+    1e-5, get_metrics incl. roll/adv_norm/{mean,std}, every minibatch record with losses_for_batch's
+    keys for that mode, per-minibatch losses 1e-4 (the north-star bar) and the final weights."""
+    from gsamd.metrics import ppo_keys, ppo_records
+    z = golden("trajectory_rollnorm.npz")
+    agent = _trajectory_agent(cuda, z, normalize_advantages="rollout")
+    assert agent.hparams().normalize_adv == 0
+    assert agent.get_rollout_collector("train").normalize_advantages
+    rec = _replay_trajectory(agent, z, cuda)
+    names = [str(x) for x in z["train_metric_names"]]
+    keys = list(ppo_keys(False))
+    dev = ppo_records(rec, 0.5, 0.0, False)
+    ref = z["train_metric_values"]
+    assert set(names) == set(keys) and dev.shape == ref.shape
+    for j, k in enumerate(keys):
+        np.testing.assert_allclose(dev[:, j], ref[:, names.index(k)], atol=1e-4, rtol=1e-4, err_msg=k)
+    np.testing.assert_allclose(rec[:, 0], z["losses"], atol=1e-4, rtol=0)
+    p = agent.policy_model.params.cpu().numpy().astype(np.float64)
+    p_ref = z["params_final"].astype(np.float64)
+    assert np.linalg.norm(p - p_ref) / np.linalg.norm(p_ref) < 1e-4
+
+
+@pytest.mark.parametrize("case", ["normal", "offset", "skewed", "constant", "single"])
+def test_normalize_advantages_kernel_vs_reference(golden, cuda, case):
+    """gs_normalize_advantages against the reference's _normalize_advantages outputs
+    (adv_norm.npz), bit-exact: the kernel reproduces numpy's float32 pairwise sums over its
+    8192-element chunks, so the applied mean / std and every normalised element are numpy's bits —
+    also for the large-offset case, where numpy's float32 mean is 6e-5 off the exact one and a
+    double-precision normalisation would differ by 6e-3.  The std = 0 cases give 0 as numpy's
+    (a - mean) / 1e-8.  Plus a C2-sized (32 x 4096 = 16 chunks) and a ragged 3-chunk array against
+    numpy directly."""
+    from gsamd._lib import check, lib, ptr, stream_handle
+    from oracle.ppo_ref import normalize_advantages_rollout
+
+    def run(arr):
+        x = torch.as_tensor(arr).to(cuda).contiguous()
+        scratch = torch.zeros(int(lib.gs_normalize_advantages_scratch_bytes(x.numel())) // 4, dtype=torch.float32,
+                              device=cuda)
+        ms = torch.zeros(2, dtype=torch.float32, device=cuda)
+        check(lib.gs_normalize_advantages(ptr(x), x.numel(), 1e-8, ptr(scratch), ptr(ms), stream_handle()),
+              "gs_normalize_advantages")
+        torch.cuda.synchronize()
+        return x.cpu().numpy(), ms.cpu().numpy()
+
+    z = golden("adv_norm.npz")
+    y, ms = run(z[f"{case}/in"])
+    assert np.array_equal(ms.view(np.uint32), z[f"{case}/mean_std"].view(np.uint32)), (ms, z[f"{case}/mean_std"])
+    assert np.array_equal(y.view(np.uint32), z[f"{case}/out"].view(np.uint32))
+    if case in ("constant", "single"):
+        assert (y == 0).all()
+    if case == "offset":
+        rng = np.random.default_rng(3)
+        for shape in ((32, 4096), (3, 6000)):
+            a = (rng.standard_normal(shape) * 1.5 + 4.0).astype(np.float32)
+            y, _ = run(a)
+            assert np.array_equal(y.view(np.uint32), normalize_advantages_rollout(a).view(np.uint32)), shape

@@ -294,3 +294,182 @@ def test_cnn_bf16_update_step_vs_bf16_oracle(cuda, tag):
     assert abs(rec[0] - loss16) < 1e-4 * max(1.0, abs(loss16))
     assert all(r < 5e-3 for n, r in per if "head" in n), per
     assert r_emu < 2e-2 and r_emu < 0.5 * r_f32, (r_emu, r_f32, per)
+
+
+def _oracle_minibatches(p0, rows, K, B, kw, lr, bf16=False):
+    """K sequential reference minibatch steps (losses_for_batch + backward + clip_grad_norm_ + Adam,
+    agents/base_agent.py:591-621) on the gathered rows: per-minibatch loss, pre-clip component norms
+    (utils/models.py:196-230: all, cnn, mlp, policy_head, value_head) and the final parameters."""
+    from oracle import cnn_ref as C
+    shapes = C.cnn_param_shapes()
+    p = p0.copy()
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    losses, norms = [], []
+    for k in range(K):
+        sl = slice(k * B, (k + 1) * B)
+        loss, _, g, _, _ = C.loss_and_grads(p, shapes, *(x[sl] for x in rows), bf16=bf16, **kw)
+        comp = {"cnn": 0.0, "mlp": 0.0, "policy_head": 0.0, "value_head": 0.0}
+        o = 0
+        for n, s in shapes:
+            n_el = int(np.prod(s))
+            comp[n.split(".")[0]] += float(np.sum(g[o:o + n_el].astype(np.float64) ** 2))
+            o += n_el
+        norms.append([np.sqrt(sum(comp.values()))] + [np.sqrt(comp[c]) for c in ("cnn", "mlp", "policy_head",
+                                                                                  "value_head")])
+        p, m, v, _, _ = C.clip_and_adam(p, g, shapes, m, v, k + 1, lr)
+        losses.append(loss)
+    return np.array(losses), np.array(norms), p
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
+    """The production NatureCNN update at its production batch, against the oracle over many
+    minibatches (the counterpart of test_gpu_parity.py::test_update_first_minibatches_vs_numpy_oracle):
+    Pong rgb_ppo shapes, 32 envs x 256 steps, B = 1024 -> 8 minibatches of one gs_cnn_ppo_update
+    call, so the fc kernels at K = 1024, the 16-ahead field gather (k_cnn_gather_chunk), the
+    256-workgroup conv weight-gradient walks over 1024 samples and Adam steps 2..8 all run.  The
+    oracle takes the same gathered rows (sampler indices -> env-major -> time-major rows,
+    rollout_buffer.py:105-173) through 8 sequential reference steps.  The update is also captured
+    whole into a graph and replayed from the same state: bit-identical to the eager run.
+    Bars (fp32): per-minibatch losses 1e-5 relative, component grad norms 1e-4 relative, final
+    parameters 1e-5 relative L2.  bf16 (against the bf16 emulation, oracle/cnn_ref.py bf16=True;
+    the bars of test_cnn_bf16_update_step_vs_bf16_oracle carried over 8 steps): losses 1e-4 of
+    their scale, the final parameters closer to the emulation than half the mode's distance to
+    the fp32 oracle."""
+    from gsamd._lib import GS_HP_BF16, M, check, lib, ptr
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(3)
+    cfg = load_config("ALE-Pong-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=32, n_steps=256,
+                                                               n_epochs=1))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
+    coll = agent.get_rollout_collector("train")
+    coll.collect()
+    B, K = agent.batch_size, agent.n_minibatches
+    assert (B, K) == (1024, 8)
+    idx = agent.prefetcher.upload(0)
+    pm = agent.policy_model
+    p0 = pm.flat_to_reference(pm.params)
+    state = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v)]
+    hp = agent.hparams()
+    hp.flags = GS_HP_BF16 if prec == "bf16" else 0
+    buf = coll.buffer
+    s = torch.cuda.Stream(device=cuda)
+
+    def run():
+        check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
+                                    hp, buf.view(), ptr(idx), B, K, 0, ptr(agent.metrics_buf), ptr(agent.stop_flag),
+                                    ptr(agent.workspace), None, s.cuda_stream), "gs_cnn_ppo_update")
+
+    def restore():
+        for t, s0 in zip((pm.params, agent.adam_m, agent.adam_v), state):
+            t.copy_(s0)
+        agent.metrics_buf.zero_()
+        agent.stop_flag.zero_()
+
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        run()
+    torch.cuda.synchronize()
+    eager = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v, agent.metrics_buf)]
+    # graph capture of the whole update (the first, eager call above set every kernel attribute)
+    restore()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        run()
+    restore()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    for name, a, b in zip(("params", "adam_m", "adam_v", "records"), eager,
+                          (pm.params, agent.adam_m, agent.adam_v, agent.metrics_buf)):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), f"graph replay != eager: {name}"
+    rec = eager[3].cpu().numpy()
+    p_dev = pm.flat_to_reference(eager[0])
+
+    # the same rows on the host: env-major sample i = env * T + t -> row (t, env)
+    T, N = cfg.n_steps, cfg.n_envs
+    ii = idx.cpu().numpy().astype(np.int64)[:K * B]
+    src = (ii % T) * N + ii // T
+    flat = lambda x: x.reshape(T * N, *x.shape[2:]).cpu().numpy()  # noqa: E731
+    rows = tuple(flat(x)[src] for x in (buf.obs, buf.actions, buf.logprobs, buf.values, buf.advantages, buf.returns))
+    kw = dict(valid=cfg.valid_actions, clip=float(hp.clip_range), clip_vf=float(hp.clip_range_vf),
+              vf_coef=float(hp.vf_coef), ent_coef=float(hp.ent_coef))
+    lr = float(hp.lr)
+    slots = [M[k] for k in ("grad_norm", "gn_backbone", "gn_mlp", "gn_policy_head", "gn_value_head")]
+    rl = lambda a, b: float(np.linalg.norm(a.astype(np.float64) - b) / np.linalg.norm(b))  # noqa: E731
+    if prec == "fp32":
+        losses, norms, p_or = _oracle_minibatches(p0, rows, K, B, kw, lr)
+        dl = np.abs(rec[:K, M["loss"]] - losses) / np.maximum(1.0, np.abs(losses))
+        dn = np.abs(rec[:K][:, slots] - norms) / norms
+        dp = rl(p_dev, p_or)
+        print(f"fp32: loss dev {dl.max():.2e}, norm dev {dn.max():.2e}, params rel L2 {dp:.2e}")
+        assert (rec[:K, M["skipped"]] == 0).all()
+        assert dl.max() < 1e-5, dl
+        assert dn.max() < 1e-4, dn
+        assert dp < 1e-5, dp
+    else:
+        losses, norms, p_or = _oracle_minibatches(p0, rows, K, B, kw, lr, bf16=True)
+        _, _, p32 = _oracle_minibatches(p0, rows, K, B, kw, lr)
+        dl = np.abs(rec[:K, M["loss"]] - losses) / max(1.0, float(np.abs(losses).max()))
+        d_emu, d_f32 = rl(p_dev, p_or), rl(p_dev, p32)
+        print(f"bf16: loss dev {dl.max():.2e}, params vs emulation {d_emu:.2e}, vs fp32 {d_f32:.2e}")
+        assert dl.max() < 1e-4, dl
+        assert d_emu < 0.5 * d_f32, (d_emu, d_f32)
+
+
+@pytest.mark.parametrize("tag", list(CASES))
+def test_cnn_activation_stats_vs_reference(golden, cuda, tag):
+    """gs_cnn_activation_stats against the reference's forward hooks on the same case
+    (cnn_step.npz activation_names / values: utils/models.py:121-147 on cnn.0, cnn.2, cnn.4, mlp.0,
+    the pre-activation outputs of each Conv2d / Linear): mean and std within 1e-5 of the layer's
+    std, dead_pct / dead_max within one row (1 / B).  Also through the agent: the keys the
+    reference records (opt/activations/<layer>/{mean,std,dead_pct,dead_max})."""
+    from gsamd._lib import check, lib, ptr, stream_handle
+    valid, clip, ent, lr, B, _, _ = CASES[tag]
+    pm, p_ref, bufs, view, hp, idx, batch = _setup(cuda, tag)
+    ws = torch.empty(int(lib.gs_cnn_workspace_bytes(pm.dims, B)), dtype=torch.uint8, device=cuda)
+    out = torch.zeros(16, dtype=torch.float64, device=cuda)
+    check(lib.gs_cnn_activation_stats(ptr(pm.params), pm.dims, view, ptr(idx), B, ptr(out), ptr(ws), stream_handle()),
+          "gs_cnn_activation_stats")
+    torch.cuda.synchronize()
+    dev = out.cpu().numpy()
+    z = golden("cnn_step.npz")
+    ref = dict(zip([str(x) for x in z[f"{tag}/activation_names"]], z[f"{tag}/activation_values"]))
+    layers = ("cnn.0", "cnn.2", "cnn.4", "mlp.0")
+    assert set(ref) == {f"opt/activations/{n}/{k}" for n in layers for k in ("mean", "std", "dead_pct", "dead_max")}
+    for li, n in enumerate(layers):
+        sd = ref[f"opt/activations/{n}/std"]
+        for ki, k in enumerate(("mean", "std", "dead_pct", "dead_max")):
+            want, got = ref[f"opt/activations/{n}/{k}"], dev[4 * li + ki]
+            tol = 1e-5 * sd if k in ("mean", "std") else 1.0 / B + 1e-9
+            assert abs(got - want) <= tol, (n, k, got, want)
+
+
+def test_cnn_agent_records_activation_stats(cuda):
+    """The pixel agent records the NatureCNN's activation statistics once per epoch under the
+    reference's keys (base_agent.py:335-347 -> opt/activations/{cnn.0,cnn.2,cnn.4,mlp.0}/*), taken
+    on the epoch's first minibatch before its step: equal to gs_cnn_activation_stats on that
+    minibatch with the pre-update parameters."""
+    from gsamd._lib import check, lib, ptr, stream_handle
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(0)
+    cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=8, n_steps=32,
+                                                                   batch_size=64, n_epochs=1))
+    agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=True)
+    p0 = agent.policy_model.params.clone()
+    agent.train_epoch()
+    m = agent.epoch_metrics()
+    keys = [f"opt/activations/{n}/{k}" for n in ("cnn.0", "cnn.2", "cnn.4", "mlp.0")
+            for k in ("mean", "std", "dead_pct", "dead_max")]
+    assert set(keys) <= set(m), set(keys) - set(m)
+    idx = agent.prefetcher.upload(0)
+    ws = torch.empty(int(lib.gs_cnn_workspace_bytes(agent.policy_model.dims, 64)), dtype=torch.uint8, device=cuda)
+    out = torch.zeros(16, dtype=torch.float64, device=cuda)
+    check(lib.gs_cnn_activation_stats(ptr(p0), agent.policy_model.dims, agent.get_rollout_collector("train").buffer.view(),
+                                      ptr(idx), 64, ptr(out), ptr(ws), stream_handle()), "gs_cnn_activation_stats")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(np.array([m[k] for k in keys]), out.cpu().numpy())

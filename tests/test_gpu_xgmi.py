@@ -340,57 +340,124 @@ def test_exchange_guards_self_test_and_replica_check(tmp_path, bwd):
         assert "replica check failed" in o["message"]
 
 
-def test_cnn_global_mode_reproduces_single_gpu_run(tmp_path, cuda):
-    """dp_mode 'global' for NatureCNN: a single-process Breakout rgb_ppo update (8
-    envs x 32 steps, B = 64, 2 epochs = 8 minibatches, the local fused head + loss path: the reference's own
-    single-process math, utils/samplers.py:25-34 + utils/torch.py:97-99) against the same run as 2
-    ranks x 4 envs in global mode — global sampler order, whole-minibatch advantage statistics
-    and loss mean, the ranks' gradient shares summed, the records rebuilt from the summed loss sums
-    (all on the device), replaying the single run's actions.  Per-minibatch losses within 1e-4
-    (north_star's bar), every other record field within 1e-4 of its scale, final parameters within
-    1e-3 relative L2 (the ranks' partial sums reassociate the gradient; Adam turns that into
-    lr-sized moves on near-zero-gradient weights), replicas bitwise identical."""
+def test_cnn_global_mode_teacher_forced_vs_single_run_and_oracle(tmp_path, cuda):
+    """dp_mode 'global' for NatureCNN (gs_cnn_ppo_update_global), teacher-forced at the production
+    clip (Breakout rgb_ppo: clip 0.1, clip_vf 0.2): a single-process update of 8 envs x 32 steps,
+    B = 64, 4 epochs = 16 minibatches (the local fused head + loss path: the reference's own
+    single-process math, utils/samplers.py:25-34 + utils/torch.py:97-99) is stepped one minibatch
+    at a time and its (params, adam_m, adam_v) kept before every step.  2 ranks x 4 envs in global
+    mode replay its actions and, for every minibatch k, restart from the single run's state before
+    k and run that one global minibatch (their row shares, the whole minibatch's advantage
+    statistics and loss mean, the gradient shares summed over xGMI, the records rebuilt on the
+    device from the ranks' summed loss sums).  So each step's arithmetic is compared on its own,
+    without Adam carrying a reassociation-level difference into later steps.  Per step:
+      * the global run against the single run: loss 1e-5 relative, every record field 1e-5 of its
+        scale (the clip fractions at most one row apart), clipped gradient 1e-5 relative L2;
+      * both against the oracle (oracle/cnn_ref.py on the whole global minibatch's rows from the
+        same state, clip + Adam at step k + 1): loss 1e-5 relative, clipped gradient within
+        2e-5 x max|g| (test_gpu_cnn.py's bar);
+      * replicas bitwise identical (gradient + parameters digest per step).
+    The clip must actually fire: some minibatch has clip_fraction > 0."""
     import torch
-    from gsamd._lib import M
+    from gsamd._lib import M, check, lib, ptr, stream_handle
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
-    from _dist_workers import cnn_global_worker
-    # one rollout, then 16 minibatch steps: the update's math from identical inputs, with the PPO
-    # clip ranges opened (10): a sample whose ratio sits at 1 +- clip flips its clip decision on a
-    # reassociation-level parameter difference, a discrete change of the gradient that the
-    # following steps carry (measured with clip 0.1: losses equal to 1e-5 for 13 minibatches, then
-    # 2e-2 apart) — the mode's arithmetic is what this test pins, not PPO's sensitivity.  Even with
-    # the clips opened the two runs' reassociated gradient sums drift apart chaotically through
-    # Adam's sign-like steps on near-zero gradients (measured on the round-4 kernels: losses within
-    # 4e-6 for the first 10 minibatches, 2e-3 apart at the 16th), so the run stops at 8
-    N, T, B, E, epochs = 8, 32, 64, 2, 1
-    opened = dict(clip_range=10.0, clip_range_vf=10.0)
+    from oracle import cnn_ref as C
+    from _dist_workers import cnn_global_tf_worker
+    N, T, B, E = 8, 32, 64, 4
     torch.manual_seed(42)
     cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=N, n_steps=T,
-                                                                   batch_size=B, n_epochs=E, **opened))
+                                                                   batch_size=B, n_epochs=E))
+    assert cfg.clip_range == 0.1
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=False)
-    p0 = agent.policy_model.params.cpu().numpy()
+    pm = agent.policy_model
     coll = agent.get_rollout_collector("train")
-    acts, recs = [], []
-    for _ in range(epochs):
-        coll.collect()
-        acts.append(coll.buffer.actions.cpu().numpy().copy())
-        agent.update_phase()
-        recs.append(agent.metrics_buf.cpu().numpy().copy())
+    coll.collect()
+    buf = coll.buffer
+    K = agent.n_minibatches
+    assert K == 16
+    idx = agent.prefetcher.upload(0)
+    hp = agent.hparams()
+    st = {"p": [], "m": [], "v": []}
+    g1, p1 = [], []
+    for k in range(K):
+        for key, t in (("p", pm.params), ("m", agent.adam_m), ("v", agent.adam_v)):
+            st[key].append(t.cpu().numpy())
+        check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
+                                    hp, buf.view(), ptr(idx[k * B:]), B, 1, k, ptr(agent.metrics_buf[k]),
+                                    ptr(agent.stop_flag), ptr(agent.workspace), None, stream_handle()),
+              "gs_cnn_ppo_update")
+        g1.append(agent.grads.cpu().numpy())
+        p1.append(pm.params.cpu().numpy())
     torch.cuda.synchronize()
-    rec1, p1 = np.concatenate(recs), agent.policy_model.params.cpu().numpy().astype(np.float64)
-    del agent
+    rec1 = agent.metrics_buf.cpu().numpy()
+    ii = idx.cpu().numpy().astype(np.int64)[:K * B]
+    src = (ii % T) * N + ii // T
+    flat = lambda x: x.reshape(T * N, *x.shape[2:]).cpu().numpy()  # noqa: E731
+    rows = tuple(flat(x)[src] for x in (buf.obs, buf.actions, buf.logprobs, buf.values, buf.advantages, buf.returns))
+    to_ref = lambda a: pm.flat_to_reference(torch.as_tensor(a))  # noqa: E731
     ref = tmp_path / "ref.npz"
-    np.savez(ref, NT=np.array([N, T]), B=np.int64(B), E=np.int64(E), p0=p0, actions=np.stack(acts))
-    _run(cnn_global_worker, 2, tmp_path, str(ref), timeout=400)
-    runs = [np.load(tmp_path / f"c{r}.npz") for r in range(2)]
-    assert np.array_equal(runs[0]["p"].view(np.uint32), runs[1]["p"].view(np.uint32)), "replicas diverged"
-    rec2 = runs[0]["rec"]
+    states = tmp_path / "states.npz"
+    np.savez(ref, NT=np.array([N, T]), B=np.int64(B), E=np.int64(E), actions=buf.actions.cpu().numpy()[None])
+    np.savez(states, **{k: np.stack(v) for k, v in st.items()})
+    del agent
+    _run(cnn_global_tf_worker, 2, tmp_path, str(ref), str(states), timeout=400)
+    runs = [np.load(tmp_path / f"tf{r}.npz") for r in range(2)]
+    np.testing.assert_array_equal(runs[0]["digests"], runs[1]["digests"])
+    rec2, g2 = runs[0]["rec"], runs[0]["g"]
     assert rec2.shape == rec1.shape
-    np.testing.assert_allclose(rec2[:, M["loss"]], rec1[:, M["loss"]], atol=1e-4, rtol=0)
-    for k in ("policy_loss", "value_loss", "entropy", "clip_fraction", "approx_kl", "adv_norm_mean", "adv_norm_std"):
-        scale = max(1.0, float(np.abs(rec1[:, M[k]]).max()))
-        np.testing.assert_allclose(rec2[:, M[k]], rec1[:, M[k]], atol=1e-4 * scale, rtol=0, err_msg=k)
-    p2 = runs[0]["p"].astype(np.float64)
-    rel = np.linalg.norm(p2 - p1) / np.linalg.norm(p1)
-    assert rel < 1e-3, rel
+    shapes = C.cnn_param_shapes()
+    kw = dict(valid=cfg.valid_actions, clip=float(hp.clip_range), clip_vf=float(hp.clip_range_vf),
+              vf_coef=float(hp.vf_coef), ent_coef=float(hp.ent_coef))
+    rl = lambda a, b: float(np.linalg.norm(a.astype(np.float64) - b) / np.linalg.norm(b))  # noqa: E731
+    worst = {}
+    for k in range(K):
+        sl = slice(k * B, (k + 1) * B)
+        p_ref = to_ref(st["p"][k])
+        loss, _, g, _, _ = C.loss_and_grads(p_ref, shapes, *(x[sl] for x in rows), **kw)
+        _, _, _, gc, _ = C.clip_and_adam(p_ref, g, shapes, to_ref(st["m"][k]), to_ref(st["v"][k]), k + 1, float(hp.lr))
+        for tag, rec, gd in (("single", rec1, g1[k]), ("global", rec2, g2[k])):
+            dl = abs(rec[k, M["loss"]] - loss) / max(1.0, abs(loss))
+            assert dl < 1e-5, (tag, k, rec[k, M["loss"]], loss)
+            gr = to_ref(gd)
+            np.testing.assert_allclose(gr, gc, atol=2e-5 * np.abs(gc).max(), rtol=0, err_msg=f"{tag} step {k}")
+            worst[tag] = max(worst.get(tag, 0.0), rl(gr, gc))
+        worst["g_vs_s"] = max(worst.get("g_vs_s", 0.0), rl(g2[k], g1[k].astype(np.float64)))
+        assert rl(g2[k], g1[k].astype(np.float64)) < 1e-5, k
+    print(f"teacher-forced global mode: worst clipped-gradient rel L2 {worst}")
+    np.testing.assert_allclose(rec2[:, M["loss"]], rec1[:, M["loss"]], atol=1e-5, rtol=1e-5)
+    for key in ("policy_loss", "value_loss", "entropy", "approx_kl", "kl", "adv_norm_mean", "adv_norm_std",
+                "explained_var"):
+        scale = max(1.0, float(np.abs(rec1[:, M[key]]).max()))
+        np.testing.assert_allclose(rec2[:, M[key]], rec1[:, M[key]], atol=1e-5 * scale, rtol=0, err_msg=key)
+    for key in ("clip_fraction", "clip_fraction_vf"):
+        assert np.abs(rec2[:, M[key]] - rec1[:, M[key]]).max() <= 1.0 / B + 1e-7, key
+    assert (rec1[:, M["clip_fraction"]] > 0).any(), rec1[:, M["clip_fraction"]]
+
+
+@pytest.mark.parametrize("mode", ["mlp", "inject", "cnn"])
+def test_agent_attached_comm_self_tested(tmp_path, mode):
+    """Multi-GPU guards run by the agent itself: with init_xgmi_comm
+    called WITHOUT verify_shapes, the agent's first update self-tests the in-backward exchange on
+    its own dims / batch / precision; every epoch passes the replica check and an exchange canary
+    over the whole parameter count; a failure injected on one rank before its first self-test
+    exchange leaves every rank in the same collective sequence, resets the communicator and moves
+    every rank to the exchange launch, and training continues; the NatureCNN-sized communicator's
+    vector self-test covers all 1 693 875 floats.  Replicas end bit-identical in every mode."""
+    import json
+    from _dist_workers import agent_selftest_worker
+    _run(agent_selftest_worker, 2, tmp_path, mode, timeout=400)
+    outs = [json.load(open(tmp_path / f"ast{r}.json")) for r in range(2)]
+    assert outs[0]["params_sha"] == outs[1]["params_sha"]
+    for o in outs:
+        assert o["epochs"] == "ok" and o["canary_rounds"] == 2, o
+        assert o["connect_self_test"]["exchange_launch_ok"] is True
+        st = o["agent_self_test"]
+        if mode == "cnn":
+            assert o["n_params"] == 1_693_875 and st is None, o
+            continue
+        assert st["in_bwd_checked"] and st["launch_ok"] is True and st["flags"] == 0, st
+        if mode == "mlp":
+            assert st["in_bwd_ok"] is True and 0.0 < st["rel_l2"] < 1e-4 and o["inside"] is True, st
+        else:
+            assert st["in_bwd_ok"] is False and o["inside"] is False, st

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(_lib.lib, n), f"libgsamd.so does not export {n}"
     assert set(names) == set(_lib.EXPORTED)
-    assert _lib.lib.gs_abi_version() == _lib.GS_ABI_VERSION == 5
+    assert _lib.lib.gs_abi_version() == _lib.GS_ABI_VERSION == 6
 
 
 def test_library_is_gfx950_code_object():
@@ -400,3 +400,42 @@ def test_u8_scale_shortcuts_exact():
         fixed = f32(Fraction(float(r)) * Fraction(float(c)) + Fraction(float(q)))   # fma(r, c, q)
         assert fixed == ieee, b
         assert bf16_bits(q) == bf16_bits(ieee), b
+
+
+def test_pairwise_sum_kernel_tree_indexing():
+    """The leaf / node indexing of k_pw_chunks (csrc/gs_gae.hip), simulated for every chunk size
+    1..8192: each leaf of numpy's pairwise split tree gets exactly one owner lane (the lane of the
+    first multiple of 64 inside it), every heap id stays below the kernel's 256 LDS slots, every
+    internal node sits at depth <= 6 (the kernel's level loop), and summing leaves up the heap in
+    that order gives the recursion's tree."""
+    def split(m):
+        n2 = m // 2
+        return n2 - n2 % 8
+
+    def tree(off, m, ident, leaves, internal, depth):
+        if m <= 128:
+            leaves[ident] = (off, m)
+            return
+        internal[ident] = depth
+        n2 = split(m)
+        tree(off, n2, 2 * ident, leaves, internal, depth + 1)
+        tree(off + n2, m - n2, 2 * ident + 1, leaves, internal, depth + 1)
+
+    for m0 in range(1, 8193):
+        leaves, internal = {}, {}
+        tree(0, m0, 1, leaves, internal, 0)
+        owners = {}
+        for k in range((m0 + 63) // 64):
+            j, off, m, ident = 64 * k, 0, m0, 1
+            while m > 128:
+                n2 = split(m)
+                if j < off + n2:
+                    m, ident = n2, 2 * ident
+                else:
+                    off, m, ident = off + n2, m - n2, 2 * ident + 1
+            if (off + 63) // 64 * 64 == j:
+                assert ident not in owners
+                owners[ident] = (off, m)
+        assert owners == leaves, m0
+        assert max(list(leaves) + list(internal)) < 256, m0
+        assert not internal or max(internal.values()) <= 6, m0

@@ -145,3 +145,27 @@ def test_atari_oracle_known_answers():
     for _ in range(5):
         r, d, _ = env.step()
         assert r.min() >= -1 and r.max() < 1
+
+
+@pytest.mark.parametrize("case", ["normal", "offset", "skewed", "constant", "single"])
+def test_rollout_adv_norm_oracle_vs_reference(golden, case):
+    """oracle/ppo_ref.py normalize_advantages_rollout and its written-out model (numpy_f32_sum: the
+    steps gs_normalize_advantages takes on the device) against the reference's own
+    _normalize_advantages outputs (adv_norm.npz), bit for bit."""
+    from oracle.ppo_ref import normalize_advantages_model, normalize_advantages_rollout
+    z = golden("adv_norm.npz")
+    a, want = z[f"{case}/in"], z[f"{case}/out"]
+    for f in (normalize_advantages_rollout, normalize_advantages_model):
+        assert np.array_equal(f(a).view(np.uint32), want.view(np.uint32)), f.__name__
+
+
+def test_numpy_f32_sum_model_matches_numpy():
+    """The device's summation model (numpy's float32 pairwise sums over 8192-element buffer chunks)
+    equals np.add.reduce bit for bit, at sizes around every boundary of the model (8, 128, the
+    chunk) and at the C2 / C3 rollout sizes, on data with a large common offset (where the order of
+    the additions shows in the result)."""
+    from oracle.ppo_ref import numpy_f32_sum
+    rng = np.random.default_rng(0)
+    for n in (1, 7, 8, 9, 127, 128, 129, 136, 143, 255, 257, 1000, 8191, 8192, 8193, 20001, 131072, 2 ** 21 + 5):
+        a = (rng.standard_normal(n) * 3.0 + 100.0).astype(np.float32)
+        assert numpy_f32_sum(a) == np.add.reduce(a), n
