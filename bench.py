@@ -240,14 +240,16 @@ def time_exchange(comm, n: int, reps: int, device, barrier):
 
 def bf16_deviation(agent) -> dict:
     """Loss trajectory of one update (all its minibatches) in the fp32 parity path and in the bf16
-    mode, from the same parameters / Adam state on the same rollout and index stream."""
+    mode, from the same parameters / Adam state on the same rollout and index stream.  Each mode runs
+    twice from that state and the second run is timed (`update_ms`): the MLP chain's update graph is
+    then captured already (gs_ppo_update caches it), as in the bench line's own timed steps."""
     import numpy as np
     from gsamd._lib import GS_HP_BF16, check, lib, ptr, stream_handle
     pm, coll = agent.policy_model, agent.get_rollout_collector("train")
     idx = agent.prefetcher.device_buf
     state = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v)]
     res = {}
-    for name, flags in (("fp32", 0), ("bf16", GS_HP_BF16)):
+    for name, flags, rep in (("fp32", 0, 0), ("fp32", 0, 1), ("bf16", GS_HP_BF16, 0), ("bf16", GS_HP_BF16, 1)):
         for t, s0 in zip((pm.params, agent.adam_m, agent.adam_v), state):
             t.copy_(s0)
         hp = agent.hparams()
@@ -260,7 +262,7 @@ def bf16_deviation(agent) -> dict:
                                         agent.n_minibatches, agent.adam_step, ptr(agent.metrics_buf),
                                         ptr(agent.stop_flag), ptr(agent.workspace), None, stream_handle()),
                   "gs_cnn_ppo_update")
-        else:     # the MLP's fused chain (the update the bench line times), eager launches
+        else:     # the MLP's fused chain (the update the bench line times), as one captured graph
             check(lib.gs_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
                                     hp, coll.buffer.view(), ptr(idx), agent.batch_size, agent.n_minibatches,
                                     agent.adam_step, ptr(agent.metrics_buf), ptr(agent.stop_flag),
@@ -268,6 +270,8 @@ def bf16_deviation(agent) -> dict:
                   "gs_ppo_update")
         e1.record()
         e1.synchronize()
+        if rep == 0:      # warm-up: the graph capture (MLP) and first-touch costs
+            continue
         res[name] = (agent.metrics_buf[:, 0].cpu().numpy().astype(np.float64), pm.params.cpu().numpy().astype(np.float64),
                      e0.elapsed_time(e1))
     for t, s0 in zip((pm.params, agent.adam_m, agent.adam_v), state):
@@ -515,8 +519,16 @@ def main():
         stage_us["exchange_launch" if in_bwd else "exchange"] = time_exchange(comm, pm.n_params, args.stage_reps,
                                                                                device, barrier)
     # PMC HBM traffic per launch (tools/pmc_run.py + tools/pmc_summarize.py), used only when it was
-    # recorded from the kernel sources this library is built from (gsamd.buildinfo.source_hash)
-    from gsamd.buildinfo import source_hash
+    # recorded from the kernel sources the LOADED library was compiled from: the library carries
+    # its sources' hash (gs_build_source_hash, embedded by build_lib.py), and the sources on disk
+    # must still hash to it (a stale prebuilt library is never labelled current)
+    from gsamd.buildinfo import source_hash as _disk_hash
+    from gsamd._lib import lib as _lib
+
+    def source_hash(path):
+        h = _lib.gs_build_source_hash(path.encode())
+        h = h.decode() if h else None
+        return h if h == _disk_hash(path) else f"{h} (library) != {_disk_hash(path)} (sources on disk)"
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     pmc = {}
     if os.path.exists(pmc_path):

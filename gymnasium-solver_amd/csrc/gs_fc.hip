@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
     static_assert(NG % KS == 0, "k-groups split evenly over KS");
     static_assert(PD >= 1, "register prefetch depth");
     constexpr int TILE = (BM + BN) * RB;
-    __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
+    extern __shared__ __attribute__((aligned(16))) char lds[];     // 2 TILE bytes (launch_fc)
 
     // XCD-aware tile order: workgroup b runs on XCD b % 8 (round-robin dispatch), so XCD x is
     // given the contiguous run [x T/8, (x+1) T/8) of a grouped order (gm m-blocks per group, m
@@ -297,7 +297,8 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
         // the KS k-group partials of each wave tile, added in ks order (LDS is free after the loop)
         float *red = reinterpret_cast<float *>(lds);
         constexpr int PW = TM * TN * 16 * 64;      // floats per wave's partial tile
-        static_assert((KS - 1) * (4 / KS) * PW * 4 <= 2 * TILE, "KS reduction fits the LDS tiles");
+        static_assert(PW == WM * WN, "a wave's partial tile");     // launch_fc sizes the LDS for it
+        __syncthreads();      // every wave's last operand reads of the K tiles are done
         if (ks > 0)
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(256, 2) void k_fc16(const float *__restrict__ A, in
     constexpr int KE = K_::KE, RB = K_::RB, NC = KE / 16, NCW = NC / KS;
     static_assert(NC % KS == 0, "16-k chunks split evenly over KS");
     constexpr int TILE = (BM + BN) * RB;
-    __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
+    extern __shared__ __attribute__((aligned(16))) char lds[];     // 2 TILE bytes (launch_fc)
 
     int bx = blockIdx.x, by = blockIdx.y;
     {
@@ -446,7 +447,8 @@ __global__ __launch_bounds__(256, 2) void k_fc16(const float *__restrict__ A, in
     if constexpr (KS > 1) {
         float *red = reinterpret_cast<float *>(lds);
         constexpr int PW = TM * TN * 4 * 64;
-        static_assert((KS - 1) * (4 / KS) * PW * 4 <= 2 * TILE, "KS reduction fits the LDS tiles");
+        static_assert(PW == WM * WN, "a wave's partial tile");     // launch_fc sizes the LDS for it
+        __syncthreads();
         if (ks > 0)
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -489,6 +491,28 @@ __global__ __launch_bounds__(256, 2) void k_fc16(const float *__restrict__ A, in
         }
 }
 
+// a kernel's dynamic LDS above the 64 KB default: the attribute is set once per instantiation
+// (before any capture: the first call of a shape is eager)
+template <class KF>
+void lds_attr(KF k, size_t bytes)
+{
+    if (bytes <= 65536) return;
+    static bool done = false;
+    if (!done) {
+        (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        done = true;
+    }
+}
+
+// two staged K tiles, or the KS partial tiles of the in-workgroup k split if larger
+template <int BM, int BN, int WGM, int KS, bool BF, int KT>
+constexpr size_t fc_lds_bytes()
+{
+    const size_t tiles = 2 * (size_t)(BM + BN) * FcK<BF, KT>::RB;
+    const size_t red = (size_t)(KS - 1) * (4 / KS) * (BM / WGM) * (BN / (4 / (WGM * KS))) * 4;
+    return tiles > red ? tiles : red;
+}
+
 template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16, int KT32, int KT16,
           bool MI16 = false>
 int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
@@ -497,16 +521,65 @@ int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *
 {
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
     K /= splits;
-    if (bf)
-        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16>), grid, dim3(256), 0, s, A, lda, B,
-                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
-    else if (MI16 && FC_MI16)
-        hipLaunchKernelGGL((k_fc16<BM, BN, WGM, KS, AK, BKC, EPI, PD32, KT32>), grid, dim3(256), 0, s, A, lda, B, ldb, C,
-                           ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
-    else
-        hipLaunchKernelGGL((k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32>), grid, dim3(256), 0, s, A, lda, B,
-                           ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+    if (bf) {
+        constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, true, KT16>();
+        auto k = k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16>;
+        lds_attr(k, L);
+        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+    } else if (MI16 && FC_MI16) {
+        constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, false, KT32>();
+        auto k = k_fc16<BM, BN, WGM, KS, AK, BKC, EPI, PD32, KT32>;
+        lds_attr(k, L);
+        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+    } else {
+        constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, false, KT32>();
+        auto k = k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32>;
+        lds_attr(k, L);
+        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+    }
     GS_LAUNCH_CHECK("k_fc");
+    return GS_OK;
+}
+
+// split-K partials [S][M][ldp] summed in slice order, then the product's epilogue (bias + ReLU of
+// the forward, the relu' mask of the input gradient, none for the weight gradient); 4 columns per
+// thread (N % 4 == 0)
+template <int EPI>
+__global__ __launch_bounds__(256) void k_fc_sum(const float *__restrict__ parts, int S, int64_t sP, int M, int N,
+                                                int ldp, float *__restrict__ C, int64_t ldc,
+                                                const float *__restrict__ aux, const int32_t *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    const int n4 = N / 4;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)M * n4) return;
+    const int row = (int)(i / n4), c = 4 * (int)(i - (int64_t)row * n4);
+    const float *p = parts + (int64_t)row * ldp + c;
+    float4 acc = *reinterpret_cast<const float4 *>(p);
+    for (int z = 1; z < S; ++z) {
+        const float4 v = *reinterpret_cast<const float4 *>(p + z * sP);
+        acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+    }
+    float x[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if constexpr (EPI == kEpiBiasRelu) {
+            x[q] += aux[c + q];
+            x[q] = x[q] > 0.0f ? x[q] : 0.0f;
+        }
+        if constexpr (EPI == kEpiMask) x[q] = aux[(int64_t)row * ldc + c + q] > 0.0f ? x[q] : 0.0f;
+    }
+    *reinterpret_cast<float4 *>(C + (int64_t)row * ldc + c) = make_float4(x[0], x[1], x[2], x[3]);
+}
+
+template <int EPI>
+int fc_sum(hipStream_t s, const float *parts, int S, int64_t M, int64_t N, float *C, int64_t ldc, const float *aux,
+           const int32_t *stop)
+{
+    const int64_t n = M * (N / 4);
+    hipLaunchKernelGGL(k_fc_sum<EPI>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, parts, S, M * N, (int)M,
+                       (int)N, (int)N, C, ldc, aux, stop);
+    GS_LAUNCH_CHECK("k_fc_sum");
     return GS_OK;
 }
 
@@ -575,3 +648,62 @@ extern "C" int gs_fc_gemm(int op, int bf16, int64_t M, int64_t N, int64_t K, con
     GS_REQUIRE(A && B && C, "gs_fc_gemm: null operand");
     return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux, nullptr);
 }
+
+#ifdef GS_FC_SWEEP
+// Launch-shape sweep of the fc products for tools/fc_sweep.py (diagnostic builds only,
+// build_lib.build_variant with GS_FC_SWEEP): variant v of product op, fp32 / bf16 operands; split-K
+// variants write partials to `parts` (splits x M x N floats) and sum them in slice order.
+// Returns GS_E_INVALID for a variant this op does not have.
+extern "C" int gs_debug_fc_variant(int op, int v, int bf16, int64_t M, int64_t N, int64_t K, const float *A,
+                                   int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux,
+                                   float *parts, void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    const bool bf = bf16 != 0;
+    auto split = [&](auto launch, int S, auto epi) -> int {
+        constexpr int E = decltype(epi)::value;
+        int rc = launch(S);
+        if (rc) return rc;
+        return fc_sum<E>(s, parts, S, M, N, C, ldc, aux, nullptr);
+    };
+    using EBR = std::integral_constant<int, kEpiBiasRelu>;
+    using EST = std::integral_constant<int, kEpiStore>;
+    if (op == 0) {
+        switch (v) {
+        case 0: return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, 3, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 4);
+        case 1: return launch_fc<64, 32, 1, 4, true, true, kEpiBiasRelu, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 4);
+        case 2: return launch_fc<32, 64, 1, 4, true, true, kEpiBiasRelu, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 4);
+        case 3: return launch_fc<64, 32, 1, 4, true, true, kEpiBiasRelu, 2, 2, 4, 2>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 4);
+        case 4: return split([&](int S) { return launch_fc<128, 64, 2, 2, true, true, kEpiStore, 2, 2, 1, 1>(
+                                 s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 7, EBR{});
+        case 5: return split([&](int S) { return launch_fc<64, 64, 2, 2, true, true, kEpiStore, 2, 2, 1, 1>(
+                                 s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 2, EBR{});
+        case 6: return launch_fc<64, 32, 1, 4, true, true, kEpiBiasRelu, 3, 3, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 4);
+        default: break;
+        }
+    } else if (op == 1) {
+        switch (v) {
+        case 0: return launch_fc<64, 64, 2, 1, false, false, kEpiStore, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 8);
+        case 1: return launch_fc<64, 64, 1, 4, false, false, kEpiStore, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 8);
+        case 2: return launch_fc<128, 64, 2, 2, false, false, kEpiStore, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 4);
+        case 3: return split([&](int S) { return launch_fc<128, 64, 2, 2, false, false, kEpiStore, 2, 2, 2, 1>(
+                                 s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 2, EST{});
+        case 4: return launch_fc<64, 64, 1, 4, false, false, kEpiStore, 2, 2, 4, 2>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 8);
+        case 5: return launch_fc<64, 64, 2, 1, false, false, kEpiStore, 2, 2, 2, 1, true>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 8);
+        default: break;
+        }
+    } else if (op == 2) {
+        switch (v) {
+        case 0: return launch_fc<64, 64, 2, 1, true, false, kEpiMask, 2, 2, 2, 1, true>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 16);
+        case 1: return launch_fc<64, 64, 1, 4, true, false, kEpiMask, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 16);
+        case 2: return launch_fc<128, 64, 2, 2, true, false, kEpiMask, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 8);
+        case 3: return launch_fc<128, 64, 2, 2, true, false, kEpiMask, 2, 2, 2, 1, true>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 8);
+        case 4: return launch_fc<64, 64, 1, 4, true, false, kEpiMask, 2, 2, 2, 1, true>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 16);
+        case 5: return launch_fc<64, 64, 2, 1, true, false, kEpiMask, 2, 2, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 16);
+        default: break;
+        }
+    }
+    GS_REQUIRE(false, "gs_debug_fc_variant: op %d has no variant %d", op, v);
+    return GS_E_INVALID;
+}
+#endif

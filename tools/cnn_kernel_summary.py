@@ -27,35 +27,9 @@ PEAK_F32_MFMA = 157.3     # TFLOP/s, dense fp32 matrix (MI355X_MICROARCH.md)
 PEAK_BF16_MFMA = 2500.0   # TFLOP/s, dense bf16 matrix
 PEAK_HBM = 8000.0         # GB/s
 
-# position in the minibatch -> (label, expected kernel): the fused head + loss pair (round 3)
-SEQ_FUSED = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"),
-             ("conv3_fwd", "k_conv_fwd"), ("fc_fwd", "k_gemm"), ("fc_fwd_splitk_sum", "k_sum_parts_ep"),
-             ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
-             ("fc_wgrad", "k_gemm"), ("fc_wgrad_splitk_sum", "k_sum_parts_wb"), ("fc_dgrad_relu_mask", "k_gemm"),
-             ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts_wb"),
-             ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
-             ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
-             ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
-# the separate heads GEMMs, loss and dh kernels (round-3 first build)
-SEQ_SPLIT = [("gather_fields", "k_gather_fields"), ("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"),
-       ("conv3_fwd", "k_conv_fwd"), ("fc_fwd", "k_gemm"), ("fc_fwd_splitk_sum", "k_sum_parts_ep"),
-       ("heads_fwd", "k_gemm"), ("heads_fwd_splitk_sum", "k_sum_parts_ep"), ("loss_rows", "k_cnn_loss"),
-       ("loss_final", "k_cnn_loss_final"), ("heads_wgrad", "k_gemm"), ("heads_wgrad_sum_policy", "k_sum_parts_wb"),
-       ("heads_wgrad_sum_value", "k_sum_parts_wb"), ("heads_dgrad_dh", "k_cnn_dh"), ("fc_wgrad", "k_gemm"),
-       ("fc_wgrad_splitk_sum", "k_sum_parts_wb"), ("fc_dgrad", "k_gemm"), ("fc_relu_mask", "k_relu_mask"),
-       ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts_wb"), ("conv3_dgrad", "k_conv_dgrad"),
-       ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"), ("conv2_dgrad", "k_conv_dgrad"),
-       ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"), ("norm_partials", "k_norm_partials"),
-       ("clip_adam", "k_clip_adam_flat")]
-# the fp32 update with the fc layer's two plain GEMMs through hipBLASLt (dbf from the head kernels)
-SEQ_LIB = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd", "k_conv_fwd"),
-           ("fc_fwd", "blaslt"), ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
-           ("fc_wgrad", "blaslt"), ("fc_dgrad_relu_mask", "k_gemm"),
-           ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts_wb"),
-           ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
-           ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
-           ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
-# round 4: the fc layer's three GEMMs on the hand-written k_fc kernels (csrc/gs_fc.hip)
+# position in the minibatch -> (label, expected kernel): the update's dispatch sequence
+# (gs_cnn.hip cnn_step): the fc layer's three products on the hand-written k_fc kernels
+# (csrc/gs_fc.hip), the fused head + loss pair, the LDS-resident conv kernels
 SEQ_FC = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd", "k_conv_fwd"),
           ("fc_fwd", "k_fc"), ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
           ("fc_wgrad", "k_fc"), ("fc_dgrad_relu_mask", "k_fc"),
@@ -90,8 +64,6 @@ def nature_work(B, A=18, C=4, H=84, W=84):
 
 
 def short(name):
-    if "Cijk_" in name:     # hipBLASLt / Tensile GEMM kernels (the fc layer's fp32 GEMMs)
-        return "blaslt"
     m = re.search(r"\b(k_\w+)", name)
     if m and m.group(1) == "k_conv1_wgrad_bf":    # the bf16 conv1 weight gradient (same position)
         return "k_conv1_wgrad"
@@ -100,26 +72,9 @@ def short(name):
     return m.group(1) if m else None
 
 
-def merge_library_runs(rows):
-    """consecutive library kernels (a GEMM and its reduction kernels) become one dispatch: summed
-    duration (start of the first, end moved by the others' durations) and summed counter value"""
-    out = []
-    for r in rows:
-        if out and short(r["Kernel_Name"]) == "blaslt" and short(out[-1]["Kernel_Name"]) == "blaslt":
-            prev = dict(out[-1])
-            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            prev["End_Timestamp"] = str(int(prev["End_Timestamp"]) + dur)
-            if "Counter_Value" in r:
-                prev["Counter_Value"] = str(float(prev["Counter_Value"]) + float(r["Counter_Value"]))
-            out[-1] = prev
-        else:
-            out.append(r)
-    return out
-
-
 def minibatches(rows):
     """rows (dicts) in dispatch order -> list of per-minibatch dispatch lists (gs kernels only)."""
-    gs = merge_library_runs([r for r in rows if short(r["Kernel_Name"]) is not None])
+    gs = [r for r in rows if short(r["Kernel_Name"]) is not None]
     starts = [i for i, r in enumerate(gs) if short(r["Kernel_Name"]) == SEQ[0][1]]
     out = []
     for a, b in zip(starts, starts[1:] + [len(gs)]):
@@ -163,13 +118,7 @@ def main():
     ap.add_argument("--skip", type=int, default=1, help="warm minibatches to drop")
     ap.add_argument("--prefix", default="cnn", help="run directories <prefix>_stats / _fetch / _write")
     a = ap.parse_args()
-    global SEQ
     rows = load_trace(one(os.path.join(a.dir, a.prefix + "_stats", "**", "*kernel_trace.csv")))
-    names = [short(r["Kernel_Name"]) for r in rows if short(r["Kernel_Name"])]
-    if "k_cnn_head_loss" not in names:
-        SEQ = SEQ_SPLIT
-    else:
-        SEQ = SEQ_FC if "k_fc" in names else SEQ_LIB if "blaslt" in names else SEQ_FUSED
     trace = minibatches(rows)[a.skip:]
     fetch = minibatches(load_pmc(one(os.path.join(a.dir, a.prefix + "_fetch", "**", "*counter_collection.csv")),
                                  "FETCH_SIZE"))[a.skip:]
