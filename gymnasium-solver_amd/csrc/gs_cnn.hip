@@ -1392,25 +1392,25 @@ ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.
 // the conv trunk for R rows (a3): obs rows come from the u8 buffer through idx (or 0..R)
 // (obs_copy: the rollout's obs row, written by conv1 from the frames it loads anyway)
 int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  uint8_t *obs_copy = nullptr)
+                  bool bf, uint8_t *obs_copy = nullptr)
 {
     int rc;
     if (conv1_lds_supported(L.C, L.H, L.W)) {
-        if ((rc = conv1_lds_fwd(s, (int)R, fs.obs, fs.idx, fs.T, fs.N, P + L.oW1, P + L.ob1, w.a1, obs_copy)))
+        if ((rc = conv1_lds_fwd(s, bf, (int)R, fs.obs, fs.idx, fs.T, fs.N, P + L.oW1, P + L.ob1, w.a1, obs_copy)))
             return rc;
     } else {
         if (obs_copy && obs_copy != fs.obs)
             GS_HIP(hipMemcpyAsync(obs_copy, fs.obs, (size_t)R * L.C * L.H * L.W, hipMemcpyDeviceToDevice, s));
-        if ((rc = conv_fwd_u8(s, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) return rc;
+        if ((rc = conv_fwd_u8(s, bf, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) return rc;
     }
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_fwd(s, 2, (int)R, w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
-    } else if ((rc = conv_fwd_nhwc(s, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) {
+        if ((rc = conv23_lds_fwd(s, bf, 2, (int)R, w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
+    } else if ((rc = conv_fwd_nhwc(s, bf, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) {
         return rc;
     }
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_fwd(s, 3, (int)R, w.a2, P + L.oW3, P + L.ob3, w.a3))) return rc;
-    } else if ((rc = conv_fwd_nhwc(s, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
+        if ((rc = conv23_lds_fwd(s, bf, 3, (int)R, w.a2, P + L.oW3, P + L.ob3, w.a3))) return rc;
+    } else if ((rc = conv_fwd_nhwc(s, bf, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
         return rc;
     }
     return GS_OK;
@@ -1418,19 +1418,20 @@ int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
 
 // conv trunk + fc for R rows (h)
 int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  bool lib_fc = false, const int32_t *stop = nullptr)
+                  bool bf, bool lib_fc = false, const int32_t *stop = nullptr)
 {
-    int rc = forward_convs(P, L, fs, R, w, s);
+    int rc = forward_convs(P, L, fs, R, w, s, bf);
     if (rc) return rc;
     // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
     // update), else the engine's split-K partials summed with the bias + ReLU epilogue
-    if (lib_fc) return fc_gemm(s, 0, cnn_bf16(), R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop);
+    if (lib_fc) return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop);
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
-        if ((rc = gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf, true)))
+        if ((rc = gemm_f32(s, bf, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf,
+                           true)))
             return rc;
     } else {
-        if ((rc = gemm_f32(s, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.parts, L.HID, 0.f, nullptr,
+        if ((rc = gemm_f32(s, bf, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.parts, L.HID, 0.f, nullptr,
                            false, sf, R * L.HID)))
             return rc;
         if ((rc = sum_parts(s, w.parts, sf, R * L.HID, w.h, P + L.obf, L.HID, true))) return rc;
@@ -1440,18 +1441,18 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
 
 // conv trunk + fc + heads: z[r][0:A] = h Wp^T, z[r][A] = h Wv^T (row stride A+1); the biases are
 // added where z is read
-int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s)
+int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s, bool bf)
 {
-    int rc = forward_trunk(P, L, fs, R, w, s);
+    int rc = forward_trunk(P, L, fs, R, w, s, bf);
     if (rc) return rc;
-    return heads_fwd(s, R, L.HID, L.A, w.h, P + L.oWp, P + L.oWv, w.z, w.parts, splits_for(R, L.A + 1, L.HID));
+    return heads_fwd(s, bf, R, L.HID, L.A, w.h, P + L.oWp, P + L.oWv, w.z, w.parts, splits_for(R, L.A + 1, L.HID));
 }
 
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s, bool lib_fc = false);
+                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc = false);
 
 int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-             const int32_t *stop, hipStream_t s)
+             const int32_t *stop, hipStream_t s, bool bf)
 {
     int rc;
     // head grads: [dW | db][a] = dz[:, a]^T [h | 1] for a in [0, A] (policy rows, then the
@@ -1460,48 +1461,48 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
         const int A1 = L.A + 1;
         const int sh = splits_for(A1, L.HID + 1, B);
         const int64_t pstride = (int64_t)A1 * (L.HID + 1);
-        if ((rc = gemm_wgrad_bias(s, A1, L.HID, B, w.dz, A1, w.h, L.HID, w.parts, sh))) return rc;
+        if ((rc = gemm_wgrad_bias(s, bf, A1, L.HID, B, w.dz, A1, w.h, L.HID, w.parts, sh))) return rc;
         if ((rc = sum_parts_wb(s, w.parts, sh, pstride, L.A, L.HID, G + L.oWp, G + L.obp))) return rc;
         if ((rc = sum_parts_wb(s, w.parts + (int64_t)L.A * (L.HID + 1), sh, pstride, 1, L.HID, G + L.oWv, G + L.obv)))
             return rc;
     }
     hipLaunchKernelGGL(k_cnn_dh, dim3(nblk(B * L.HID)), dim3(256), 0, s, w.dz, P, L, w.h, B, w.dh, stop);
-    return backward_trunk(P, L, fs, B, w, G, stop, s);
+    return backward_trunk(P, L, fs, B, w, G, stop, s, bf);
 }
 
 // the trunk's backward from dh (fc, then the convolutions)
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s, bool lib_fc)
+                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc)
 {
     int rc;
     const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
     // fc: [dWf | dbf] = dh^T [a3 | 1]; lib_fc: dWf on the fc kernels, dbf from the head kernels
     if (lib_fc) {
-        if ((rc = fc_gemm(s, 1, cnn_bf16(), L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr, stop)))
+        if ((rc = fc_gemm(s, 1, bf, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr, stop)))
             return rc;
     } else {
         const int sw = splits_for(L.HID, L.F + 1, B);
-        if ((rc = gemm_wgrad_bias(s, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, w.parts, sw))) return rc;
+        if ((rc = gemm_wgrad_bias(s, bf, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, w.parts, sw))) return rc;
         if ((rc = sum_parts_wb(s, w.parts, sw, (int64_t)L.HID * (L.F + 1), L.HID, L.F, G + L.oWf, G + L.obf)))
             return rc;
     }
     // da3 = (dh Wf) masked by relu'(a3) in the GEMM's epilogue
     if (lib_fc) {
-        if ((rc = fc_gemm(s, 2, cnn_bf16(), B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, w.a3, stop))) return rc;
-    } else if ((rc = gemm_f32(s, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr,
+        if ((rc = fc_gemm(s, 2, bf, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, w.a3, stop))) return rc;
+    } else if ((rc = gemm_f32(s, bf, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr,
                               false, 1, 0, w.a3))) {
         return rc;
     }
     // conv3 (dY3 = da3 as [m3][c3])
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_wgrad(s, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
-    } else if ((rc = conv_wgrad_nhwc(s, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) {
+        if ((rc = conv23_lds_wgrad(s, bf, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
+    } else if ((rc = conv_wgrad_nhwc(s, bf, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) {
         return rc;
     }
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_dgrad(s, 3, (int)B, w.da3, w.a2, P + L.oW3, w.da2))) return rc;
+        if ((rc = conv23_lds_dgrad(s, bf, 3, (int)B, w.da3, w.a2, P + L.oW3, w.da2))) return rc;
     } else {
-        if ((rc = gemm_f32(s, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, w.cols3, L.K3, 0.f, nullptr,
+        if ((rc = gemm_f32(s, bf, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, w.cols3, L.K3, 0.f, nullptr,
                            false)))
             return rc;
         hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(m2 * (L.c2 / 4))), dim3(256), 0, s, w.cols3, w.a2, B, L.h2, L.w2,
@@ -1510,14 +1511,14 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // conv2
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_wgrad(s, 2, (int)B, w.a1, w.da2, w.parts, G + L.oW2, G + L.ob2))) return rc;
-    } else if ((rc = conv_wgrad_nhwc(s, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) {
+        if ((rc = conv23_lds_wgrad(s, bf, 2, (int)B, w.a1, w.da2, w.parts, G + L.oW2, G + L.ob2))) return rc;
+    } else if ((rc = conv_wgrad_nhwc(s, bf, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) {
         return rc;
     }
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_dgrad(s, 2, (int)B, w.da2, w.a1, P + L.oW2, w.da1))) return rc;
+        if ((rc = conv23_lds_dgrad(s, bf, 2, (int)B, w.da2, w.a1, P + L.oW2, w.da1))) return rc;
     } else {
-        if ((rc = gemm_f32(s, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, w.cols2, L.K2, 0.f, nullptr,
+        if ((rc = gemm_f32(s, bf, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, w.cols2, L.K2, 0.f, nullptr,
                            false)))
             return rc;
         hipLaunchKernelGGL(k_col2im_relu, dim3(nblk(L.rows1(B) * (L.c1 / 4))), dim3(256), 0, s, w.cols2, w.a1, B,
@@ -1525,9 +1526,9 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // conv1 (no input gradient): patches re-read from the u8 frames
     if (conv1_lds_supported(L.C, L.H, L.W))
-        return conv1_lds_wgrad(s, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1);
+        return conv1_lds_wgrad(s, bf, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1);
     if ((rc = colsum(w.da1, L.rows1(B), L.c1, w.parts, G + L.ob1, s))) return rc;
-    return conv_wgrad_u8(s, geom1(L, B), fs, w.da1, w.parts, kSplitW1, G + L.oW1);
+    return conv_wgrad_u8(s, bf, geom1(L, B), fs, w.da1, w.parts, kSplitW1, G + L.oW1);
 }
 
 AdamArgs adam_args(const gs_ppo_hparams &hp, int64_t t)
@@ -1584,11 +1585,10 @@ bool head_fused(const CnnLayout &L, int64_t B)
 }
 
 int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFields &fl, const CnnWs &w,
-                     const LossArgs &la, float *G, float *metrics, int32_t *stop, hipStream_t s)
+                     const LossArgs &la, float *G, float *metrics, int32_t *stop, hipStream_t s, bool bf)
 {
     const unsigned nb = (unsigned)((B + kHeadRows - 1) / kHeadRows);
     const size_t l1 = head_loss_lds(L);
-    const bool bf = cnn_bf16();
     auto go = [&](auto am, auto bfc) {
         constexpr int AM = decltype(am)::value;
         constexpr bool BF = decltype(bfc)::value;
@@ -1726,6 +1726,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
 {
     int rc;
     const FrameSrc fs{ro.obs, gl ? gl->frame_idx : idx, ro.T, ro.N};
+    const bool bf = (hp.flags & GS_HP_BF16) != 0;     // the operand precision of every product
     GS_REQUIRE(!gl || head_fused(L, B), "global mode: the fused head + loss kernels do not fit this shape");
     if (head_fused(L, B)) {
         CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
@@ -1745,17 +1746,17 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         const bool lib_fc = fc_supported(0, B, L.HID, L.F, L.F, L.F, L.HID) &&
                             fc_supported(1, L.HID, L.F, B, L.HID, L.F, L.F) &&
                             fc_supported(2, B, L.F, L.HID, L.HID, L.F, L.F);
-        if ((rc = forward_trunk(P, L, fs, B, w, s, lib_fc, stop))) return rc;
-        if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s))) return rc;
-        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, lib_fc))) return rc;
+        if ((rc = forward_trunk(P, L, fs, B, w, s, bf, lib_fc, stop))) return rc;
+        if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s, bf))) return rc;
+        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc))) return rc;
     } else {
         hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
                            ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv,
                            w.f_ret);
         GS_LAUNCH_CHECK("k_gather_fields");
-        if ((rc = forward(P, L, fs, B, w, s))) return rc;
+        if ((rc = forward(P, L, fs, B, w, s, bf))) return rc;
         if ((rc = launch_cnn_loss(w.z, P, L, B, w, loss_args(hp), w.dz, metrics, stop, s))) return rc;
-        if ((rc = backward(P, L, fs, B, w, G, stop, s))) return rc;
+        if ((rc = backward(P, L, fs, B, w, G, stop, s, bf))) return rc;
     }
     AdamArgs aa = adam_args(hp, adam_step);
     if (comm) {
@@ -1816,14 +1817,15 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     const CnnWs w = carve(workspace, L, N);
     // the conv trunk, the fc product as split-K partials (no epilogue), then one launch for the
     // fc epilogue + heads + action select
-    if ((rc = forward_convs(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s, obs_store))) return rc;
+    // the rollout's act runs the fp32 trunk (the update's precision mode is a mode of the update)
+    if ((rc = forward_convs(params, L, FrameSrc{obs, nullptr, 1, N}, N, w, s, false, obs_store))) return rc;
     int sf = 1;
     if (fc_supported(0, N, L.HID, L.F, L.F, L.F, L.HID)) {      // the fc kernels, split-K partials
         sf = fc_fwd_splits(N, L.HID, L.F);
         if ((rc = fc_fwd_partials(s, sf, N, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.parts, L.HID))) return rc;
     } else {
         sf = splits_for(N, L.HID, L.F);
-        if ((rc = gemm_f32(s, false, true, N, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.parts, L.HID, 0.f,
+        if ((rc = gemm_f32(s, false, false, true, N, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.parts, L.HID, 0.f,
                            nullptr, false, sf, N * L.HID)))
             return rc;
     }
@@ -1847,13 +1849,13 @@ extern "C" int gs_cnn_ppo_loss(const float *params, gs_cnn_dims dims, gs_ppo_hpa
     int rc = validate_cnn_update(dims, ro, batch, workspace);
     if (rc) return rc;
     GS_REQUIRE(params && idx && metrics, "gs_cnn_ppo_loss: null buffer");
-    const Bf16Scope prec((hp.flags & GS_HP_BF16) != 0);
+    const bool bf = (hp.flags & GS_HP_BF16) != 0;
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
     hipLaunchKernelGGL(k_gather_fields, dim3(nblk(batch)), dim3(256), 0, s, idx, batch, ro.T, ro.N, ro.actions,
                        ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv, w.f_ret);
-    if ((rc = forward(params, L, FrameSrc{ro.obs, idx, ro.T, ro.N}, batch, w, s))) return rc;
+    if ((rc = forward(params, L, FrameSrc{ro.obs, idx, ro.T, ro.N}, batch, w, s, bf))) return rc;
     if ((rc = launch_cnn_loss(w.z, params, L, batch, w, loss_args(hp), dlogits_out ? dlogits_out : w.dz, metrics,
                               nullptr, s)))
         return rc;
@@ -1878,7 +1880,6 @@ extern "C" int gs_cnn_ppo_update_global(float *params, float *grads, float *adam
     GS_REQUIRE((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)adam_m | (uintptr_t)adam_v) & 15) == 0,
                "gs_cnn_ppo_update_global: params / grads / adam_m / adam_v must be 16-byte aligned");
     GS_REQUIRE(ro.T * ro.N < ((int64_t)1 << 31), "rollout larger than 2^31 samples");
-    const Bf16Scope prec((hp.flags & GS_HP_BF16) != 0);
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
@@ -1904,8 +1905,8 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     GS_REQUIRE((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)adam_m | (uintptr_t)adam_v) & 15) == 0,
                "gs_cnn_ppo_update: params / grads / adam_m / adam_v must be 16-byte aligned");
     GS_REQUIRE(ro.T * ro.N < ((int64_t)1 << 31), "rollout larger than 2^31 samples");
-    // GS_HP_BF16: bf16 MFMA operands in every convolution / GEMM launch of this update
-    const Bf16Scope prec((hp.flags & GS_HP_BF16) != 0);
+    // GS_HP_BF16: bf16 MFMA operands in every convolution / GEMM launch of this update (cnn_step
+    // passes the precision to every product as an argument)
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
@@ -1955,13 +1956,13 @@ extern "C" int gs_cnn_activation_stats(const float *params, gs_cnn_dims dims, gs
     }
     double *part = (double *)w.parts;
     float *outs[4] = {w.a1, w.a2, w.a3, w.h};
-    if ((rc = conv_fwd_u8(s, geom1(L, batch), fs, params + L.oW1, params + L.ob1, w.a1, false))) return rc;
+    if ((rc = conv_fwd_u8(s, false, geom1(L, batch), fs, params + L.oW1, params + L.ob1, w.a1, false))) return rc;
     for (int l = 0; l < 4; ++l) {
-        if (l == 1 && (rc = conv_fwd_nhwc(s, geom2(L, batch), w.a1, params + L.oW2, params + L.ob2, w.a2, false)))
+        if (l == 1 && (rc = conv_fwd_nhwc(s, false, geom2(L, batch), w.a1, params + L.oW2, params + L.ob2, w.a2, false)))
             return rc;
-        if (l == 2 && (rc = conv_fwd_nhwc(s, geom3(L, batch), w.a2, params + L.oW3, params + L.ob3, w.a3, false)))
+        if (l == 2 && (rc = conv_fwd_nhwc(s, false, geom3(L, batch), w.a2, params + L.oW3, params + L.ob3, w.a3, false)))
             return rc;
-        if (l == 3 && (rc = gemm_f32(s, false, true, batch, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.h, L.HID,
+        if (l == 3 && (rc = gemm_f32(s, false, false, true, batch, L.HID, L.F, w.a3, L.F, params + L.oWf, L.F, w.h, L.HID,
                                      0.f, params + L.obf, false)))
             return rc;
         hipLaunchKernelGGL(k_act_stats_cols, dim3((unsigned)ls.nblk[l]), dim3(256), 0, s, outs[l], rows, cols[l],

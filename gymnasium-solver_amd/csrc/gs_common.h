@@ -356,13 +356,5 @@ __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c)
 {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-// host: the operand precision of this thread's NatureCNN launches (gs_cnn_ppo_update and
-// gs_cnn_policy_act set it from hp.flags for the duration of their enqueues)
-bool cnn_bf16();
-struct Bf16Scope {
-    bool prev;
-    explicit Bf16Scope(bool on);
-    ~Bf16Scope();
-};
 
 }  // namespace gs

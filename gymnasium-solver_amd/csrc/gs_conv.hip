@@ -1137,15 +1137,14 @@ using C1_84q = C1<4, 84, 84, 4>;          // 4 bands per sample (small batches)
 
 bool conv1_lds_supported(int C, int H, int W) { return C == 4 && H == 84 && W == 84; }
 
-int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N, const float *W1,
-                  const float *b1, float *out, uint8_t *obs_copy)
+int conv1_lds_fwd(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
+                  const float *W1, const float *b1, float *out, uint8_t *obs_copy)
 {
     GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
     GS_REQUIRE(!obs_copy || !idx, "conv1_lds_fwd: the obs copy is for the rollout's own rows");
     // very small batches: 4 bands of 5 output rows per sample, so R < 128 rows still launch at
     // least 256 workgroups; otherwise 2 bands (fewer padded tiles: at R = 128 the 2-band form
     // already fills the chip and ran 16.7 us vs 21.6 us for 4 bands)
-    const bool bf = cnn_bf16();
     if ((int64_t)R * 2 < kConv1Bands4Below) {
         const dim3 grid((unsigned)(C1_84q::NB * R));
         if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84q, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
@@ -1168,12 +1167,12 @@ int conv1_lds_fwd(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, 
 
 int conv1_lds_wgrad_parts() { return kConv1WgradWG; }
 
-int conv1_lds_wgrad(hipStream_t s, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
+int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
                     const float *dA, float *parts, float *dW1, float *db1)
 {
     GS_REQUIRE(R > 0 && obs && dA && parts && dW1 && db1, "conv1_lds_wgrad: bad argument");
     constexpr int n = C1_84::CO * C1_84::KK, stride = n + C1_84::CO;
-    if (cnn_bf16())
+    if (bf)
         hipLaunchKernelGGL(k_conv1_wgrad_bf<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
     else
         hipLaunchKernelGGL(k_conv1_wgrad<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
@@ -1218,18 +1217,18 @@ int launch_conv_fwd(hipStream_t s, int R, const float *in, const float *Wt, cons
     return GS_OK;
 }
 
-int conv23_lds_fwd(hipStream_t s, int layer, int R, const float *in, const float *Wt, const float *bias, float *out)
+int conv23_lds_fwd(hipStream_t s, bool bf, int layer, int R, const float *in, const float *Wt, const float *bias,
+                   float *out)
 {
     GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
-    const bool bf = cnn_bf16();
     if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS>(s, R, in, Wt, bias, out, bf);
     return launch_conv_fwd<C3_84, C3_84s, C3_84b>(s, R, in, Wt, bias, out, bf);
 }
 
-int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX)
+int conv23_lds_dgrad(hipStream_t s, bool bf, int layer, int R, const float *dY, const float *act, const float *Wt,
+                     float *dX)
 {
     GS_REQUIRE(R > 0 && dY && act && Wt && dX, "conv23_lds_dgrad: bad argument");
-    const bool bf = cnn_bf16();
     if (layer == 2) {
         const dim3 grid((unsigned)((R + D2_84::SPB - 1) / D2_84::SPB));
         if (bf) hipLaunchKernelGGL((k_conv_dgrad<D2_84, true>), grid, dim3(D2_84::NTHR), 0, s, dY, act, R, Wt, dX);
@@ -1243,13 +1242,12 @@ int conv23_lds_dgrad(hipStream_t s, int layer, int R, const float *dY, const flo
     return GS_OK;
 }
 
-int conv23_lds_wgrad(hipStream_t s, int layer, int R, const float *in, const float *dY, float *parts, float *dW,
-                     float *db)
+int conv23_lds_wgrad(hipStream_t s, bool bf, int layer, int R, const float *in, const float *dY, float *parts,
+                     float *dW, float *db)
 {
     GS_REQUIRE(R > 0 && in && dY && parts && dW && db, "conv23_lds_wgrad: bad argument");
     const int nwg = kConvWgradWG;
     int KK;
-    const bool bf = cnn_bf16();
     if (layer == 2) {
         KK = C2_84::KK;
         if (bf) hipLaunchKernelGGL((k_conv_wgrad<C2_84, true>), dim3(nwg), dim3(256), 0, s, in, dY, R, parts);

@@ -26,13 +26,16 @@ struct FrameSrc {
     int64_t T, N;
 };
 
+// Every NatureCNN product takes its operand precision as an argument (bf16: GS_HP_BF16, bf16
+// MFMA operands with fp32 accumulation; false: the fp32 parity path).
+//
 // Dense row-major GEMM: C[M][N] = op(A) op(B) (+ beta C) (+ bias[n]) (ReLU), with
 // op(A)[m][k] = TA ? A[k*lda + m] : A[m*lda + k], op(B)[k][n] = TB ? B[n*ldb + k] : B[k*ldb + n].
 // splits > 1: K is cut into `splits` slices; slice z writes its partial product to
 // C + z*sC (beta/bias/relu/mask must then be off) — the caller sums them in a fixed order.
 // mask (leading dimension ldc): C[m][n] is kept only where mask[m][n] > 0 (relu' of the
 // activation the product is the gradient of), zero elsewhere.
-int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+int gemm_f32(hipStream_t s, bool bf16, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
              const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu,
              int splits = 1, int64_t sC = 0, const float *mask = nullptr);
 
@@ -53,22 +56,22 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
 
 // out[r,oy,ox,co] = relu(bias[co] + sum_{c,ky,kx} W[co][c][ky][kx] * frame[c][oy*s+ky][ox*s+kx] / 255)
 // (relu = false: the pre-activation, for the activation statistics)
-int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out,
+int conv_fwd_u8(hipStream_t s, bool bf16, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out,
                 bool relu = true);
 // out[r,oy,ox,co] = relu(bias[co] + sum_{ky,kx,c} W[co][ky][kx][c] * in[r, oy*s+ky, ox*s+kx, c])
-int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out,
+int conv_fwd_nhwc(hipStream_t s, bool bf16, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out,
                   bool relu = true);
 // dW[co][patch] = sum over rows of dY[row][co] * patch(row): split over `splits` row slices
 // into parts (splits * Cout * patch floats), then summed in slice order into dW.
-int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
+int conv_wgrad_u8(hipStream_t s, bool bf16, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
                   float *dW);
 // conv_wgrad_nhwc also produces db[co] (column sums of dY, summed from the A tiles in LDS
 // by the n-block-0 workgroups); parts: splits * Cout * (patch + 1) floats
-int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
+int conv_wgrad_nhwc(hipStream_t s, bool bf16, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
                     float *dW, float *db);
 // [dW | db] partials of a dense weight gradient: parts[z] (M x (N+1)) = [dY^T X | rowsum dY^T]
 // over split z of K; then sum_parts_wb scatters column N of each row into db
-int gemm_wgrad_bias(hipStream_t s, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
+int gemm_wgrad_bias(hipStream_t s, bool bf16, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
                     int64_t ldx, float *parts, int splits);
 int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int rows, int ncols, float *dW,
                  float *db);
@@ -78,7 +81,7 @@ int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int
 int sum_parts(hipStream_t s, const float *parts, int np, int64_t n, float *out, const float *bias = nullptr,
               int C = 1, bool relu = false, int64_t pstride = 0);
 // heads: z[r][a] = h[r] . Wp[a] (a < A), z[r][A] = h[r] . Wv — row stride A+1, no bias
-int heads_fwd(hipStream_t s, int64_t R, int HID, int A, const float *h, const float *Wp, const float *Wv, float *z,
+int heads_fwd(hipStream_t s, bool bf16, int64_t R, int HID, int A, const float *h, const float *Wp, const float *Wv, float *z,
               float *parts, int splits);
 
 }  // namespace gs

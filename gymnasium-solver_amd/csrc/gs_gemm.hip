@@ -16,10 +16,7 @@
 
 namespace gs {
 
-static thread_local bool t_bf16 = false;
-bool cnn_bf16() { return t_bf16; }
-Bf16Scope::Bf16Scope(bool on) : prev(t_bf16) { t_bf16 = on; }
-Bf16Scope::~Bf16Scope() { t_bf16 = prev; }
+
 
 namespace {
 
@@ -295,13 +292,13 @@ __global__ __launch_bounds__(256) void k_gemm(AOp aop, BOp bop, int M, int N, in
 }
 
 template <int BM, int BN, int WGM, bool A_K, bool B_K, bool ASUM = false, class AOp, class BOp>
-int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
+int launch(hipStream_t s, bool bf16, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
            int64_t ldc, int64_t sC, float beta, const float *bias, bool relu, const float *mask)
 {
     const int64_t per = (K + splits - 1) / splits;
     const int64_t kchunk = (per + BK - 1) / BK * BK;
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
-    if (cnn_bf16())
+    if (bf16)
         hipLaunchKernelGGL((k_gemm<BM, BN, WGM, AOp, A_K, BOp, B_K, ASUM, true>), grid, dim3(256), 0, s, a, b, (int)M,
                            (int)N, (int)K, (int)kchunk, C, (int)ldc, sC, beta, bias, relu ? 1 : 0, mask);
     else
@@ -314,19 +311,19 @@ int launch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int6
 // tile shape by output shape: skinny N (conv forward: 32 / 64 channels) takes tall tiles,
 // tiny M (weight gradients of 32 / 64 output channels) flat ones
 template <bool A_K, bool B_K, bool ASUM = false, class AOp, class BOp>
-int dispatch(hipStream_t s, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
+int dispatch(hipStream_t s, bool bf16, const AOp &a, const BOp &b, int64_t M, int64_t N, int64_t K, int splits, float *C,
              int64_t ldc, int64_t sC, float beta, const float *bias, bool relu, const float *mask = nullptr)
 {
     if (N <= 32)
-        return launch<256, 32, 4, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+        return launch<256, 32, 4, A_K, B_K, ASUM>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
     if (M <= 32)
-        return launch<32, 128, 1, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+        return launch<32, 128, 1, A_K, B_K, ASUM>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
     if (N <= 64)
-        return launch<128, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+        return launch<128, 64, 2, A_K, B_K, ASUM>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
     const int64_t big_tiles = ((M + 127) / 128) * ((N + 127) / 128) * splits;
     if (big_tiles >= 512)
-        return launch<128, 128, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
-    return launch<64, 64, 2, A_K, B_K, ASUM>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+        return launch<128, 128, 2, A_K, B_K, ASUM>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    return launch<64, 64, 2, A_K, B_K, ASUM>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
 }
 
 DenseOp dense(const float *p, int64_t ld, int64_t n_outer, int64_t n_inner)
@@ -436,7 +433,7 @@ int sum_parts(hipStream_t s, const float *parts, int np, int64_t n, float *out, 
     return GS_OK;
 }
 
-int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
+int gemm_f32(hipStream_t s, bool bf16, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
              const float *B, int64_t ldb, float *C, int64_t ldc, float beta, const float *bias, bool relu, int splits,
              int64_t sC, const float *mask)
 {
@@ -445,31 +442,31 @@ int gemm_f32(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, c
     GS_REQUIRE(splits == 1 || (beta == 0.0f && !bias && !relu && !mask), "gemm_f32: split-K partials take no epilogue");
     const DenseOp a = ta ? dense(A, lda, K, M) : dense(A, lda, M, K);
     const DenseOp b = tb ? dense(B, ldb, N, K) : dense(B, ldb, K, N);
-    if (!ta && !tb) return dispatch<true, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
-    if (!ta && tb) return dispatch<true, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
-    if (ta && !tb) return dispatch<false, false>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
-    return dispatch<false, true>(s, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    if (!ta && !tb) return dispatch<true, false>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    if (!ta && tb) return dispatch<true, true>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    if (ta && !tb) return dispatch<false, false>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
+    return dispatch<false, true>(s, bf16, a, b, M, N, K, splits, C, ldc, sC, beta, bias, relu, mask);
 }
 
-int conv_fwd_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out,
+int conv_fwd_u8(hipStream_t s, bool bf16, const ConvGeom &g, const FrameSrc &f, const float *Wt, const float *bias, float *out,
                 bool relu)
 {
     int rc = check_geom(g);
     if (rc) return rc;
     GS_REQUIRE(g.k % 4 == 0 && g.s % 4 == 0 && g.W % 4 == 0, "conv_fwd_u8: needs k, s, W multiples of 4");
     const int64_t M = g.rows(), K = g.patch();
-    return dispatch<true, true>(s, u8_patches(g, f), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0, 0.0f,
+    return dispatch<true, true>(s, bf16, u8_patches(g, f), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0, 0.0f,
                                 bias, relu);
 }
 
-int conv_fwd_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out,
+int conv_fwd_nhwc(hipStream_t s, bool bf16, const ConvGeom &g, const float *in, const float *Wt, const float *bias, float *out,
                   bool relu)
 {
     int rc = check_geom(g);
     if (rc) return rc;
     GS_REQUIRE(g.C % 4 == 0 && ((uintptr_t)in & 15) == 0, "conv_fwd_nhwc: channels must be float4-aligned");
     const int64_t M = g.rows(), K = g.patch();
-    return dispatch<true, true>(s, nhwc_patches(g, in), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0,
+    return dispatch<true, true>(s, bf16, nhwc_patches(g, in), dense(Wt, K, g.Cout, K), M, g.Cout, K, 1, out, g.Cout, 0,
                                 0.0f, bias, relu);
 }
 
@@ -484,15 +481,15 @@ int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int
     return GS_OK;
 }
 
-int gemm_wgrad_bias(hipStream_t s, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
+int gemm_wgrad_bias(hipStream_t s, bool bf16, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
                     int64_t ldx, float *parts, int splits)
 {
     GS_REQUIRE(M > 0 && N > 0 && K > 0 && splits >= 1, "gemm_wgrad_bias: empty problem");
-    return dispatch<false, false, true>(s, dense(dY, lddy, K, M), dense(X, ldx, K, N), M, N, K, splits, parts, N + 1,
+    return dispatch<false, false, true>(s, bf16, dense(dY, lddy, K, M), dense(X, ldx, K, N), M, N, K, splits, parts, N + 1,
                                         M * (N + 1), 0.0f, nullptr, false);
 }
 
-int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
+int conv_wgrad_u8(hipStream_t s, bool bf16, const ConvGeom &g, const FrameSrc &f, const float *dY, float *parts, int splits,
                   float *dW)
 {
     int rc = check_geom(g);
@@ -500,13 +497,13 @@ int conv_wgrad_u8(hipStream_t s, const ConvGeom &g, const FrameSrc &f, const flo
     GS_REQUIRE(g.k % 4 == 0 && g.s % 4 == 0 && g.W % 4 == 0, "conv_wgrad_u8: needs k, s, W multiples of 4");
     const int64_t rows = g.rows(), P = g.patch(), n = (int64_t)g.Cout * P;
     // dW (Cout x P) = dY^T (Cout x rows) . patches (rows x P): A stored [rows][Cout], B = patches
-    rc = dispatch<false, false>(s, dense(dY, g.Cout, rows, g.Cout), u8_patches(g, f), g.Cout, P, rows, splits,
+    rc = dispatch<false, false>(s, bf16, dense(dY, g.Cout, rows, g.Cout), u8_patches(g, f), g.Cout, P, rows, splits,
                                 splits == 1 ? dW : parts, P, n, 0.0f, nullptr, false);
     if (rc || splits == 1) return rc;
     return sum_parts(s, parts, splits, n, dW);
 }
 
-int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
+int conv_wgrad_nhwc(hipStream_t s, bool bf16, const ConvGeom &g, const float *in, const float *dY, float *parts, int splits,
                     float *dW, float *db)
 {
     int rc = check_geom(g);
@@ -515,19 +512,19 @@ int conv_wgrad_nhwc(hipStream_t s, const ConvGeom &g, const float *in, const flo
     GS_REQUIRE(splits >= 1 && db, "conv_wgrad_nhwc: needs the split partials and a bias output");
     const int64_t rows = g.rows(), P = g.patch(), n = (int64_t)g.Cout * (P + 1);
     // [dW | db] (Cout x (P+1)) = dY^T (Cout x rows) . patches, db = row sums of dY^T (ASUM)
-    rc = dispatch<false, false, true>(s, dense(dY, g.Cout, rows, g.Cout), nhwc_patches(g, in), g.Cout, P, rows, splits,
+    rc = dispatch<false, false, true>(s, bf16, dense(dY, g.Cout, rows, g.Cout), nhwc_patches(g, in), g.Cout, P, rows, splits,
                                       parts, P + 1, n, 0.0f, nullptr, false);
     if (rc) return rc;
     return sum_parts_wb(s, parts, splits, n, g.Cout, (int)P, dW, db);
 }
 
-int heads_fwd(hipStream_t s, int64_t R, int HID, int A, const float *h, const float *Wp, const float *Wv, float *z,
+int heads_fwd(hipStream_t s, bool bf16, int64_t R, int HID, int A, const float *h, const float *Wp, const float *Wv, float *z,
               float *parts, int splits)
 {
     GS_REQUIRE(R > 0 && HID > 0 && A > 0 && splits >= 1, "heads_fwd: bad sizes");
     const RowsOp2 b{Wp, Wv, HID, HID, A, A + 1, HID};
     const int64_t n = R * (A + 1);
-    int rc = dispatch<true, true>(s, dense(h, HID, R, HID), b, R, A + 1, HID, splits, splits == 1 ? z : parts, A + 1,
+    int rc = dispatch<true, true>(s, bf16, dense(h, HID, R, HID), b, R, A + 1, HID, splits, splits == 1 ? z : parts, A + 1,
                                   n, 0.0f, nullptr, false);
     if (rc || splits == 1) return rc;
     return sum_parts(s, parts, splits, n, z);
@@ -540,6 +537,6 @@ extern "C" int gs_gemm_f32(int ta, int tb, int64_t M, int64_t N, int64_t K, cons
                            int relu, void *stream)
 {
     GS_REQUIRE(A && B && C, "gs_gemm_f32: null operand");
-    return gs::gemm_f32((hipStream_t)stream, ta != 0, tb != 0, M, N, K, A, lda, B, ldb, C, ldc, beta, bias,
+    return gs::gemm_f32((hipStream_t)stream, false, ta != 0, tb != 0, M, N, K, A, lda, B, ldb, C, ldc, beta, bias,
                         relu != 0);
 }
