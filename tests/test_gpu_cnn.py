@@ -296,50 +296,36 @@ def test_cnn_bf16_update_step_vs_bf16_oracle(cuda, tag):
     assert r_emu < 2e-2 and r_emu < 0.5 * r_f32, (r_emu, r_f32, per)
 
 
-def _oracle_minibatches(p0, rows, K, B, kw, lr, bf16=False):
-    """K sequential reference minibatch steps (losses_for_batch + backward + clip_grad_norm_ + Adam,
-    agents/base_agent.py:591-621) on the gathered rows: per-minibatch loss, pre-clip component norms
-    (utils/models.py:196-230: all, cnn, mlp, policy_head, value_head) and the final parameters."""
-    from oracle import cnn_ref as C
-    shapes = C.cnn_param_shapes()
-    p = p0.copy()
-    m = np.zeros_like(p)
-    v = np.zeros_like(p)
-    losses, norms = [], []
-    for k in range(K):
-        sl = slice(k * B, (k + 1) * B)
-        loss, _, g, _, _ = C.loss_and_grads(p, shapes, *(x[sl] for x in rows), bf16=bf16, **kw)
-        comp = {"cnn": 0.0, "mlp": 0.0, "policy_head": 0.0, "value_head": 0.0}
-        o = 0
-        for n, s in shapes:
-            n_el = int(np.prod(s))
-            comp[n.split(".")[0]] += float(np.sum(g[o:o + n_el].astype(np.float64) ** 2))
-            o += n_el
-        norms.append([np.sqrt(sum(comp.values()))] + [np.sqrt(comp[c]) for c in ("cnn", "mlp", "policy_head",
-                                                                                  "value_head")])
-        p, m, v, _, _ = C.clip_and_adam(p, g, shapes, m, v, k + 1, lr)
-        losses.append(loss)
-    return np.array(losses), np.array(norms), p
-
-
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
     """The production NatureCNN update at its production batch, against the oracle over many
     minibatches (the counterpart of test_gpu_parity.py::test_update_first_minibatches_vs_numpy_oracle):
     Pong rgb_ppo shapes, 32 envs x 256 steps, B = 1024 -> 8 minibatches of one gs_cnn_ppo_update
     call, so the fc kernels at K = 1024, the 16-ahead field gather (k_cnn_gather_chunk), the
-    256-workgroup conv weight-gradient walks over 1024 samples and Adam steps 2..8 all run.  The
-    oracle takes the same gathered rows (sampler indices -> env-major -> time-major rows,
-    rollout_buffer.py:105-173) through 8 sequential reference steps.  The update is also captured
-    whole into a graph and replayed from the same state: bit-identical to the eager run.
-    Bars (fp32): per-minibatch losses 1e-5 relative, component grad norms 1e-4 relative, final
-    parameters 1e-5 relative L2.  bf16 (against the bf16 emulation, oracle/cnn_ref.py bf16=True;
-    the bars of test_cnn_bf16_update_step_vs_bf16_oracle carried over 8 steps): losses 1e-4 of
-    their scale, the final parameters closer to the emulation than half the mode's distance to
-    the fp32 oracle."""
+    256-workgroup conv weight-gradient walks over 1024 samples and Adam steps 2..8 all run, on the
+    rows the sampler picks (env-major indices -> (t, env) rows, rollout_buffer.py:105-173).
+
+    * The update is captured whole into a graph and replayed from the same state: bit-identical to
+      the eager run.  Runs of the same call with n = 1..8 minibatches end on that run's states
+      after 1..8 steps, bit for bit (the update is deterministic), which gives the device's state
+      before every step of the production 8-minibatch run.
+    * Teacher-forced oracle, step by step: from the device's state before minibatch k, the oracle
+      (oracle/cnn_ref.py, reference steps agents/base_agent.py:591-621) computes that minibatch's
+      loss, pre-clip component norms and clip + Adam (step k + 1).  fp32 bars: loss 1e-5 relative,
+      norms 1e-4 relative, the new parameters within 2e-6 except where Adam's sign-like step on a
+      noise-level gradient moves a weight (at most 1e-4 of the weights, never more than 2 lr), and
+      within 2e-5 relative L2; the step's clipped gradient within 2e-5 x max|g|.  bf16 (against the
+      bf16 emulation, oracle/cnn_ref.py bf16=True): loss 1e-4 of its scale, every step's clipped
+      gradient within 2e-2 of the emulation's and under half its distance to the fp32 oracle's
+      (the bars of test_cnn_bf16_update_step_vs_bf16_oracle, at every one of the 8 steps).
+    * Free-running (oracle and device each on their own trajectory, measured 1e-4 loss and 8.5e-5
+      parameter deviation after 8 fp32 steps on the first GPU run — Adam amplifies reassociation-level
+      gradient differences of near-zero-gradient weights): fp32 losses within 5e-4 relative,
+      parameters within 5e-4 relative L2."""
     from gsamd._lib import GS_HP_BF16, M, check, lib, ptr
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
+    from oracle import cnn_ref as C
     torch.manual_seed(3)
     cfg = load_config("ALE-Pong-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=32, n_steps=256,
                                                                n_epochs=1))
@@ -350,16 +336,15 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
     assert (B, K) == (1024, 8)
     idx = agent.prefetcher.upload(0)
     pm = agent.policy_model
-    p0 = pm.flat_to_reference(pm.params)
     state = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v)]
     hp = agent.hparams()
     hp.flags = GS_HP_BF16 if prec == "bf16" else 0
     buf = coll.buffer
     s = torch.cuda.Stream(device=cuda)
 
-    def run():
+    def run(n):
         check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
-                                    hp, buf.view(), ptr(idx), B, K, 0, ptr(agent.metrics_buf), ptr(agent.stop_flag),
+                                    hp, buf.view(), ptr(idx), B, n, 0, ptr(agent.metrics_buf), ptr(agent.stop_flag),
                                     ptr(agent.workspace), None, s.cuda_stream), "gs_cnn_ppo_update")
 
     def restore():
@@ -370,7 +355,7 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
 
     torch.cuda.synchronize()
     with torch.cuda.stream(s):
-        run()
+        run(K)
     torch.cuda.synchronize()
     eager = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v, agent.metrics_buf)]
     # graph capture of the whole update (the first, eager call above set every kernel attribute)
@@ -378,7 +363,7 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        run()
+        run(K)
     restore()
     torch.cuda.synchronize()
     g.replay()
@@ -387,7 +372,18 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
                           (pm.params, agent.adam_m, agent.adam_v, agent.metrics_buf)):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32)), f"graph replay != eager: {name}"
     rec = eager[3].cpu().numpy()
-    p_dev = pm.flat_to_reference(eager[0])
+    # the device's state after n = 0..K steps of the same call (prefix runs)
+    to_ref = lambda t: pm.flat_to_reference(t).astype(np.float32)  # noqa: E731
+    states, grads = [tuple(to_ref(t) for t in state)], [None]
+    for n in range(1, K + 1):
+        restore()
+        with torch.cuda.stream(s):
+            run(n)
+        torch.cuda.synchronize()
+        states.append(tuple(to_ref(t) for t in (pm.params, agent.adam_m, agent.adam_v)))
+        grads.append(to_ref(agent.grads))      # step n's clipped gradient
+        assert np.array_equal(agent.metrics_buf[:n].cpu().numpy().view(np.uint32), rec[:n].view(np.uint32)), n
+    assert np.array_equal(states[K][0].view(np.uint32), to_ref(eager[0]).view(np.uint32))
 
     # the same rows on the host: env-major sample i = env * T + t -> row (t, env)
     T, N = cfg.n_steps, cfg.n_envs
@@ -398,26 +394,61 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
     kw = dict(valid=cfg.valid_actions, clip=float(hp.clip_range), clip_vf=float(hp.clip_range_vf),
               vf_coef=float(hp.vf_coef), ent_coef=float(hp.ent_coef))
     lr = float(hp.lr)
+    shapes = C.cnn_param_shapes()
     slots = [M[k] for k in ("grad_norm", "gn_backbone", "gn_mlp", "gn_policy_head", "gn_value_head")]
     rl = lambda a, b: float(np.linalg.norm(a.astype(np.float64) - b) / np.linalg.norm(b))  # noqa: E731
-    if prec == "fp32":
-        losses, norms, p_or = _oracle_minibatches(p0, rows, K, B, kw, lr)
-        dl = np.abs(rec[:K, M["loss"]] - losses) / np.maximum(1.0, np.abs(losses))
-        dn = np.abs(rec[:K][:, slots] - norms) / norms
-        dp = rl(p_dev, p_or)
-        print(f"fp32: loss dev {dl.max():.2e}, norm dev {dn.max():.2e}, params rel L2 {dp:.2e}")
-        assert (rec[:K, M["skipped"]] == 0).all()
-        assert dl.max() < 1e-5, dl
-        assert dn.max() < 1e-4, dn
-        assert dp < 1e-5, dp
-    else:
-        losses, norms, p_or = _oracle_minibatches(p0, rows, K, B, kw, lr, bf16=True)
-        _, _, p32 = _oracle_minibatches(p0, rows, K, B, kw, lr)
-        dl = np.abs(rec[:K, M["loss"]] - losses) / max(1.0, float(np.abs(losses).max()))
-        d_emu, d_f32 = rl(p_dev, p_or), rl(p_dev, p32)
-        print(f"bf16: loss dev {dl.max():.2e}, params vs emulation {d_emu:.2e}, vs fp32 {d_f32:.2e}")
-        assert dl.max() < 1e-4, dl
-        assert d_emu < 0.5 * d_f32, (d_emu, d_f32)
+    worst = {"loss": 0.0, "norm": 0.0, "p_rel": 0.0, "p_off": 0, "p_max": 0.0, "emu_vs_f32": []}
+    for k in range(K):
+        sl = slice(k * B, (k + 1) * B)
+        p, m, v = states[k]
+        bf = prec == "bf16"
+        loss, _, g, _, _ = C.loss_and_grads(p, shapes, *(x[sl] for x in rows), bf16=bf, **kw)
+        p1, _, _, gc, _ = C.clip_and_adam(p, g, shapes, m, v, k + 1, lr)
+        d_loss = abs(rec[k, M["loss"]] - loss) / max(1.0, abs(loss))
+        p_dev, g_dev = states[k + 1][0], grads[k + 1]
+        worst["loss"] = max(worst["loss"], d_loss)
+        if bf:
+            _, _, g32, _, _ = C.loss_and_grads(p, shapes, *(x[sl] for x in rows), **kw)
+            _, _, _, gc32, _ = C.clip_and_adam(p, g32, shapes, m, v, k + 1, lr)
+            worst["emu_vs_f32"].append((round(rl(g_dev, gc), 5), round(rl(g_dev, gc32), 5)))
+            assert d_loss < 1e-4, (k, rec[k, M["loss"]], loss)
+            continue
+        np.testing.assert_allclose(g_dev, gc, atol=2e-5 * np.abs(gc).max(), rtol=0, err_msg=f"step {k}")
+        comp = {"cnn": 0.0, "mlp": 0.0, "policy_head": 0.0, "value_head": 0.0}
+        o = 0
+        for n_, sh in shapes:
+            n_el = int(np.prod(sh))
+            comp[n_.split(".")[0]] += float(np.sum(g[o:o + n_el].astype(np.float64) ** 2))
+            o += n_el
+        norms = np.array([np.sqrt(sum(comp.values()))] + [np.sqrt(comp[c]) for c in ("cnn", "mlp", "policy_head",
+                                                                                      "value_head")])
+        d_norm = float(np.max(np.abs(rec[k, slots] - norms) / norms))
+        d = np.abs(p_dev.astype(np.float64) - p1)
+        worst["norm"] = max(worst["norm"], d_norm)
+        worst["p_rel"] = max(worst["p_rel"], rl(p_dev, p1))
+        worst["p_off"] = max(worst["p_off"], int((d > 2e-6).sum()))
+        worst["p_max"] = max(worst["p_max"], float(d.max()))
+        assert d_loss < 1e-5, (k, rec[k, M["loss"]], loss)
+        assert d_norm < 1e-4, (k, rec[k, slots], norms)
+        assert (d > 2e-6).sum() <= max(1, int(1e-4 * d.size)) and d.max() <= 2 * lr, (k, (d > 2e-6).sum(), d.max())
+        assert rl(p_dev, p1) < 2e-5, k
+    print(f"{prec} teacher-forced: {worst}")
+    if prec == "bf16":
+        # each step's clipped gradient within 2e-2 of the emulation's and under half its distance
+        # to the fp32 oracle's (test_cnn_bf16_update_step_vs_bf16_oracle's bars)
+        assert all(e < 2e-2 and e < 0.5 * f for e, f in worst["emu_vs_f32"]), worst["emu_vs_f32"]
+        return
+    # free-running: the oracle on its own trajectory from the same start
+    p, m, v = states[0]
+    losses = []
+    for k in range(K):
+        sl = slice(k * B, (k + 1) * B)
+        loss, _, g, _, _ = C.loss_and_grads(p, shapes, *(x[sl] for x in rows), **kw)
+        p, m, v, _, _ = C.clip_and_adam(p, g, shapes, m, v, k + 1, lr)
+        losses.append(loss)
+    dl = np.abs(rec[:K, M["loss"]] - np.array(losses)) / np.maximum(1.0, np.abs(losses))
+    print(f"fp32 free-running: loss dev {dl.max():.2e}, params rel L2 {rl(states[K][0], p):.2e}")
+    assert dl.max() < 5e-4 and rl(states[K][0], p) < 5e-4
 
 
 @pytest.mark.parametrize("tag", list(CASES))

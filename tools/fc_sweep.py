@@ -3,7 +3,7 @@ GS_FC_SWEEP diagnostic build) at the C4 / C5 shapes (B = 1024, HID = 512, F = 31
 checked against a float64 reference (the bar of tests/test_gpu_gemm.py::_fc_case), then timed over
 50 back-to-back launches between HIP events.  Prints one JSON object per (op, precision, variant).
 
-  GSAMD_LIB=tools/sweep/libgsamd_fcsweep.so python tools/fc_sweep.py"""
+  GSAMD_LIB=sweeplibs/libgsamd_fcsweep.so python tools/fc_sweep.py"""
 import ctypes
 import json
 import os
