@@ -175,6 +175,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
                                          (int64_t)kConvWgradWG * 64 * (std::max(L.K2, L.K3) + 1)});
         const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
         const int64_t gparts = std::max({(int64_t)splits_for(R, L.HID, L.F) * R * L.HID,
+                                         (int64_t)2 * R * L.HID,      // the fp32 fc forward's two K halves
                                          (int64_t)fc_fwd_splits(R, L.HID, L.F) * R * L.HID,
                                          (int64_t)splits_for(R, L.A + 1, L.HID) * R * (L.A + 1),
                                          (int64_t)splits_for(L.A + 1, L.HID + 1, R) * (L.A + 1) * (L.HID + 1),
@@ -1424,7 +1425,8 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
     if (rc) return rc;
     // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
     // update), else the engine's split-K partials summed with the bias + ReLU epilogue
-    if (lib_fc) return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop);
+    if (lib_fc)
+        return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop, w.parts);
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
         if ((rc = gemm_f32(s, bf, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf,

@@ -620,19 +620,30 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
 }
 
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop)
+            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop, float *parts)
 {
     GS_REQUIRE(op >= 0 && op <= 2, "fc_gemm: op %d", op);
     GS_REQUIRE(fc_supported(op, M, N, K, lda, ldb, ldc), "fc_gemm: shape %lld x %lld x %lld (op %d) not supported",
                (long long)M, (long long)N, (long long)K, op);
     GS_REQUIRE(aligned16(A) && aligned16(B) && (op == 1 || aux), "fc_gemm: 16-B aligned operands (and the epilogue "
                "operand) required");
-    if (op == 0)     // fwd: C = relu(A B^T + bias), both K-contiguous
+    if (op == 0) {   // fwd: C = relu(A B^T + bias), both K-contiguous
+        // fp32 with a partials buffer: 64 x 64 tiles (waves 2 x 1 x KS 2, 32 x 64 each) over two K
+        // halves, summed in slice order with the bias + ReLU epilogue (tools/fc_sweep.py, round 5:
+        // 42.95 vs 47.16 us at the C4 shape; K/2 must be whole 32-deep tiles)
+        if (!bf16 && parts && K % 64 == 0 && N % 4 == 0 && ldc == N) {
+            int rc = launch_fc<64, 64, 2, 2, true, true, kEpiStore, 2, 2, 1, 1>(s, false, A, lda, B, ldb, parts, N, M, N,
+                                                                               K, nullptr, stop, 4, 2, M * N);
+            if (rc) return rc;
+            return fc_sum<kEpiBiasRelu>(s, parts, 2, M, N, C, ldc, aux, stop);
+        }
         return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
                                                                                            ldc, M, N, K, aux, stop, 4);
-    if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]
-        return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1>(s, bf16, A, lda, B, ldb, C,
-                                                                                            ldc, M, N, K, nullptr, stop, 8);
+    }
+    if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]; fp32 on 16x16x4 blocks (round-5 sweep:
+                     // 46.2 vs 47.9 us with the 32x32x2 form), bf16 on 32x32x16
+        return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1, true>(
+            s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr, stop, 8);
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
     return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1, true>(s, bf16, A, lda, B, ldb, C,
                                                                                                 ldc, M, N, K, aux, stop, 16);
@@ -643,10 +654,11 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
 using namespace gs;
 
 extern "C" int gs_fc_gemm(int op, int bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-                          const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, void *stream)
+                          const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, float *parts,
+                          void *stream)
 {
     GS_REQUIRE(A && B && C, "gs_fc_gemm: null operand");
-    return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux, nullptr);
+    return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux, nullptr, parts);
 }
 
 #ifdef GS_FC_SWEEP

@@ -120,7 +120,8 @@ def _load():
                                                     i64, vp, vp, vp, vp, ctypes.POINTER(PPOGlobal), vp]),
         "gs_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64,
                                        f32, vp, ctypes.c_int, vp]),
-        "gs_fc_gemm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp]),
+        "gs_fc_gemm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, vp,
+                                      vp]),
         "gs_cartpole_reset": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, vp]),
         "gs_cartpole_step": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, u64, i64, vp, vp, vp, vp, vp, vp, vp]),
         "gs_atari_preprocess": (ctypes.c_int, [vp, i64, i32, i32, vp, vp]),

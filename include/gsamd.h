@@ -45,8 +45,8 @@ extern "C" {
  * to 24 floats and added gs_ppo_update_global; version 4 added gs_comm_xgmi_set_bwd_exchange, gs_comm_allreduce_sum_f64,
  * gs_ppo_global_adv_stats, gs_ppo_global_records, gs_cnn_ppo_update_global, gs_fc_gemm and
  * gs_episode_window; version 5 added the obs_store argument of gs_cnn_policy_act; version 6 added
- * gs_normalize_advantages(_scratch_bytes), gs_cnn_activation_stats, gs_build_source_hash and
- * gs_comm_xgmi_reset). */
+ * gs_normalize_advantages(_scratch_bytes), gs_cnn_activation_stats, gs_build_source_hash,
+ * gs_comm_xgmi_reset and the parts argument of gs_fc_gemm). */
 #define GS_ABI_VERSION 6
 int gs_abi_version(void);
 const char *gs_last_error(void);
@@ -442,9 +442,11 @@ int gs_gemm_f32(int ta, int tb, int64_t M, int64_t N, int64_t K, const float *A_
  * parity tests: op 0 C[M][N] = relu(A[M][K] B[N][K]^T + aux[N]); op 1 C = A^T B with A [K][M],
  * B [K][N]; op 2 C = (A B) .* (aux > 0) with A [M][K], B [K][N], aux [M][ldc].  bf16 != 0: bf16
  * operands (round to nearest even), fp32 accumulation.  GS_E_INVALID for shapes outside
- * K % 64 == 0, 16-B aligned rows (and M, N % 4 == 0 for K-strided operands). */
+ * K % 64 == 0, 16-B aligned rows (and M, N % 4 == 0 for K-strided operands).  parts_dev (may be NULL;
+ * 2 M N floats): with it the fp32 forward runs the update's split-K form (two K halves summed in
+ * order, then the bias + ReLU epilogue), without it the single-pass form (ABI 6 added it). */
 int gs_fc_gemm(int op, int bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda, const float *B,
-               int64_t ldb, float *C, int64_t ldc, const float *aux, void *stream);
+               int64_t ldb, float *C, int64_t ldc, const float *aux, float *parts_dev, void *stream);
 
 /* ---------------------------------------------------------------- Atari pixel path (a13)
  * The observation pipeline of ale-py's AtariVectorEnv / gymnasium AtariPreprocessing +

@@ -46,7 +46,7 @@ def test_gemm_epilogue_and_unaligned_ld(cuda):
     _check(cuda, False, False, 77, 45, 33, beta=1.0, ldb_pad=3)
 
 
-def _fc_case(cuda, op, bf16, M, N, K, seed=0):
+def _fc_case(cuda, op, bf16, M, N, K, seed=0, split=False):
     """gs_fc_gemm (csrc/gs_fc.hip, the NatureCNN fc layer's kernels) against a float64 reference
     on the same operands (bf16: the operands rounded to bf16 first, as the kernel rounds them;
     fp32 accumulation either way).  Bar: 2e-6 x the |A||B| scale (x sqrt(K)/8 for long K)."""
@@ -72,9 +72,10 @@ def _fc_case(cuda, op, bf16, M, N, K, seed=0):
     out = torch.full((M, N), float("nan"), device=cuda)
     Ad, Bd = A.to(cuda), B.to(cuda)
     auxd = aux.to(cuda) if aux is not None else None
+    parts = torch.full((2 * M * N,), float("nan"), device=cuda) if split else None
     check(lib.gs_fc_gemm(op, int(bf16), M, N, K, Ad.data_ptr(), Ad.shape[1], Bd.data_ptr(), Bd.shape[1],
                          out.data_ptr(), N, auxd.data_ptr() if auxd is not None else None,
-                         torch.cuda.current_stream().cuda_stream), "gs_fc_gemm")
+                         parts.data_ptr() if split else None, torch.cuda.current_stream().cuda_stream), "gs_fc_gemm")
     torch.cuda.synchronize()
     scale = (rd(opA).abs() @ rd(opB).abs()).max().item() + 1.0
     err = (out.cpu().double() - ref).abs().max().item()
@@ -91,9 +92,17 @@ def test_fc_gemm_matches_fp64_reference(cuda, op, M, N, K, bf16):
     _fc_case(cuda, op, bf16, M, N, K)
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 512, 3136), (100, 72, 192), (4, 4, 64), (68, 92, 128)])
+def test_fc_forward_split_form_matches_fp64_reference(cuda, M, N, K):
+    """The fp32 fc forward's split-K form (what the update runs when it hands the fc kernels a
+    partials buffer: 64 x 64 tiles over two K halves, summed in order, bias + ReLU after) against
+    the same float64 reference and bar, ragged tiles included."""
+    _fc_case(cuda, 0, False, M, N, K, split=True)
+
+
 def test_fc_gemm_refuses_unsupported_shapes(cuda):
     from gsamd._lib import check, lib
     A = torch.zeros(64, 100, device=cuda)
     with pytest.raises(ValueError):     # K % 64 != 0
         check(lib.gs_fc_gemm(0, 0, 64, 64, 100, A.data_ptr(), 100, A.data_ptr(), 100, A.data_ptr(), 64, A.data_ptr(),
-                             torch.cuda.current_stream().cuda_stream), "gs_fc_gemm")
+                             None, torch.cuda.current_stream().cuda_stream), "gs_fc_gemm")

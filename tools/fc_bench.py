@@ -23,6 +23,7 @@ def main():
     h = torch.empty(B, HID, device=dev)
     dW = torch.empty(HID, F, device=dev)
     da3 = torch.empty(B, F, device=dev)
+    parts = torch.empty(2 * B * F, device=dev)     # the fp32 forward's split-K partials (as the update)
     cases = {"fwd": (0, B, HID, F, a3, F, Wf, F, h, HID, bf), "wgrad": (1, HID, F, B, dh, HID, a3, F, dW, F, None),
              "dgrad": (2, B, F, HID, dh, HID, Wf, F, da3, F, a3)}
     st = torch.cuda.current_stream()
@@ -30,7 +31,7 @@ def main():
         for name, (op, M, N, K, A, lda, Bm, ldb, C, ldc, aux) in cases.items():
             run = lambda: check(lib.gs_fc_gemm(op, bf16, M, N, K, A.data_ptr(), lda, Bm.data_ptr(), ldb,  # noqa: E731
                                                C.data_ptr(), ldc, aux.data_ptr() if aux is not None else None,
-                                               st.cuda_stream), "gs_fc_gemm")
+                                               parts.data_ptr(), st.cuda_stream), "gs_fc_gemm")
             for _ in range(3):
                 run()
             torch.cuda.synchronize()
