@@ -540,6 +540,8 @@ def cnn_global_tf_worker(rank, world, port, result_dir, ref_path, states_path):
             dp_mode="global"))
         agent = DevicePPOAgent(cfg, device=dev, rank=rank, world_size=world, use_graph=False, track_stats=False)
         agent.comm = init_xgmi_comm(rank, world, agent.policy_model.n_params)
+        # the rollout's log-probs / values come from the single run's initial policy
+        agent.policy_model.params.copy_(torch.from_numpy(np.ascontiguousarray(st["p"][0])).to(dev))
         coll = agent.get_rollout_collector("train")
         acts = torch.as_tensor(z["actions"][0][:, rank * n:(rank + 1) * n].copy()).to(dev)
         coll.collect(replay_actions=acts)
