@@ -463,8 +463,12 @@ extern "C" int gs_ppo_stage(int stage, float *params, float *grads, float *adam_
     int rc = validate_update(dims, ro, batch, workspace);
     if (rc) return rc;
     GS_REQUIRE(stage >= 0 && stage <= 7, "gs_ppo_stage: stage %d not in [0, 7]", stage);
-    GS_REQUIRE(!(hp.flags & GS_HP_BF16), "gs_ppo_stage: precision bf16 is a mode of the fused chain "
-                                         "(gs_ppo_update) only; the single-step entries are fp32");
+    const Layout L0 = layout_of(dims);
+    // bf16 is a mode of the fused chain: its stages (4..7) run the chain's bf16 kernels where the
+    // shape has them; the unfused stages are fp32 and refuse it instead of running fp32 silently
+    GS_REQUIRE(!(hp.flags & GS_HP_BF16) || (stage >= 4 && has_bf16_chain(L0, batch)),
+               "gs_ppo_stage: precision bf16 runs only on the fused chain's stages (4..7) of a shape with a bf16 "
+               "instantiation; stage %d is fp32", stage);
     const Layout L = layout_of(dims);
     const Workspace ws = carve_workspace(workspace, L, batch);
     const StepArgs sa = make_step_args(hp, L, batch, adam_step < 1 ? 1 : adam_step);

@@ -103,3 +103,33 @@ def test_mlp_bf16_refuses_unsupported_chain(cuda):
     agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
     with pytest.raises(ValueError, match="bf16"):
         agent.train_epoch()
+
+
+def test_mlp_bf16_refuses_single_step_entries(cuda):
+    """The single-step entries (training_step -> gs_ppo_minibatch_step, losses_for_batch ->
+    gs_ppo_loss, the unfused gs_ppo_stage stages) run fp32 kernels: with precision bf16 they raise
+    ValueError instead of training in fp32 silently; the fused chain's stages keep the
+    bf16 mode (bench.py times them)."""
+    from gsamd._lib import check, lib, ptr, stream_handle
+    from gsamd.config import load_config
+    from gsamd.ppo_agent import DevicePPOAgent
+    torch.manual_seed(42)
+    cfg = load_config("CartPole-v1", "ppo", overrides=dict(env_dynamics="synthetic", n_envs=64, precision="bf16"))
+    agent = DevicePPOAgent(cfg, device=cuda, track_stats=False)
+    batches = agent.train_dataloader()
+    with pytest.raises(ValueError, match="bf16"):
+        agent.training_step(batches[0], 0)
+    with pytest.raises(ValueError, match="bf16"):
+        agent.losses_for_batch(batches[0], 0)
+    pm, hp = agent.policy_model, agent.hparams()
+    view = agent.get_rollout_collector("train").buffer.view()
+    idx = batches[0].idx
+
+    def stage(k):
+        return lib.gs_ppo_stage(k, ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims, hp,
+                                view, ptr(idx), agent.batch_size, 1, ptr(agent.metrics_buf), ptr(agent.workspace),
+                                stream_handle())
+    with pytest.raises(ValueError, match="bf16"):
+        check(stage(0), "gs_ppo_stage")
+    check(stage(6), "gs_ppo_stage")      # the fused chain's gather stage accepts the mode
+    torch.cuda.synchronize()
