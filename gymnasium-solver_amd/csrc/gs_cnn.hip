@@ -1425,8 +1425,9 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
     if (rc) return rc;
     // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
     // update), else the engine's split-K partials summed with the bias + ReLU epilogue
-    if (lib_fc)
-        return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop, w.parts);
+    // (the split-K form of the fp32 forward, fc_gemm's parts argument, was faster in the launch
+    // sweep but slower inside the update: 43.6 + 5.0 us vs 46.0, round 5 — not used here)
+    if (lib_fc) return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop);
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
         if ((rc = gemm_f32(s, bf, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf,

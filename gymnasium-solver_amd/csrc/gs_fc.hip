@@ -630,7 +630,8 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
     if (op == 0) {   // fwd: C = relu(A B^T + bias), both K-contiguous
         // fp32 with a partials buffer: 64 x 64 tiles (waves 2 x 1 x KS 2, 32 x 64 each) over two K
         // halves, summed in slice order with the bias + ReLU epilogue (tools/fc_sweep.py, round 5:
-        // 42.95 vs 47.16 us at the C4 shape; K/2 must be whole 32-deep tiles)
+        // 42.95 vs 47.16 us back to back at the C4 shape, but 43.6 + 5.0 vs 46.0 us inside the
+        // update, which therefore passes no partials buffer); K/2 must be whole 32-deep tiles
         if (!bf16 && parts && K % 64 == 0 && N % 4 == 0 && ldc == N) {
             int rc = launch_fc<64, 64, 2, 2, true, true, kEpiStore, 2, 2, 1, 1>(s, false, A, lda, B, ldb, parts, N, M, N,
                                                                                K, nullptr, stop, 4, 2, M * N);
@@ -640,10 +641,10 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
         return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
                                                                                            ldc, M, N, K, aux, stop, 4);
     }
-    if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N]; fp32 on 16x16x4 blocks (round-5 sweep:
-                     // 46.2 vs 47.9 us with the 32x32x2 form), bf16 on 32x32x16
-        return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1, true>(
-            s, bf16, A, lda, B, ldb, C, ldc, M, N, K, nullptr, stop, 8);
+    if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N] (the round-5 sweep's 16x16x4 form: 46.2
+                     // vs 47.9 us back to back, 46.9 vs 46.7 inside the update — kept on 32x32x2)
+        return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1>(s, bf16, A, lda, B, ldb, C,
+                                                                                            ldc, M, N, K, nullptr, stop, 8);
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
     return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1, true>(s, bf16, A, lda, B, ldb, C,
                                                                                                 ldc, M, N, K, aux, stop, 16);

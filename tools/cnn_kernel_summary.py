@@ -37,6 +37,8 @@ SEQ_FC = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd
           ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
           ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
           ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
+# the fp32 update (round 5): the fc forward as two K halves + k_fc_sum (the bias + ReLU epilogue)
+SEQ_FC_SPLIT = SEQ_FC[:4] + [("fc_fwd_splitk_sum", "k_fc_sum")] + SEQ_FC[4:]
 SEQ = SEQ_FC
 
 
@@ -118,7 +120,10 @@ def main():
     ap.add_argument("--skip", type=int, default=1, help="warm minibatches to drop")
     ap.add_argument("--prefix", default="cnn", help="run directories <prefix>_stats / _fetch / _write")
     a = ap.parse_args()
+    global SEQ
     rows = load_trace(one(os.path.join(a.dir, a.prefix + "_stats", "**", "*kernel_trace.csv")))
+    if any(short(r["Kernel_Name"]) == "k_fc_sum" for r in rows):
+        SEQ = SEQ_FC_SPLIT
     trace = minibatches(rows)[a.skip:]
     fetch = minibatches(load_pmc(one(os.path.join(a.dir, a.prefix + "_fetch", "**", "*counter_collection.csv")),
                                  "FETCH_SIZE"))[a.skip:]
