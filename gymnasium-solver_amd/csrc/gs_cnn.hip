@@ -99,6 +99,8 @@ struct CnnWs {
     float *parts;          // split-K weight-gradient partials / bias column-sum partials
     float *pre;            // [kPreChunk][5][R]: minibatches' gathered fields (act bits, olp, ov, adv, ret)
     float *pre_stats;      // [kPreChunk][2]: their advantage mean / std
+    uint16_t *pbf;         // [P]: the parameters as bf16, the weight operands of a bf16 update
+                           // with bf16 trunk storage (act16_trunk), refreshed by every Adam step
     size_t bytes;
 };
 
@@ -106,7 +108,12 @@ constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block
 constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
 constexpr int kPreChunk = 16;      // minibatches per ahead-of-time fields gather (k_cnn_gather_chunk)
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
-constexpr int kHeadRows = 8;    // minibatch rows per k_cnn_head_loss workgroup
+#ifndef GS_HEAD_ROWS
+#define GS_HEAD_ROWS 4
+#endif
+// minibatch rows per k_cnn_head_loss workgroup (4 or 8).  4 (round 5): 256 workgroups at B = 1024
+// fill the CUs — head + loss 23.6 -> 20.0 us, the partial sums 5.1 -> 7.4 (fp32; bf16 alike)
+constexpr int kHeadRows = GS_HEAD_ROWS;
 constexpr int kHeadSlices = 256 / kHeadRows;   // its z product's K slices (one thread per row x slice)
 // split-K slices of the weight-gradient GEMMs (K = minibatch rows x positions): enough slices
 // that the small (Cout x patch) outputs still fill the chip
@@ -167,6 +174,11 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.norm_part = (double *)take(sizeof(double) * kNormBlocks * 5);   // total + 4 component partials
     w.pre = (float *)take(sizeof(float) * kPreChunk * 5 * R);
     w.pre_stats = (float *)take(sizeof(float) * kPreChunk * 2);
+    {   // shifted so Wf's rows start on 128-B lines (the fc kernels stream them in 128-B chunks; a
+        // 64-B offset put every chunk across two lines: fc forward 28.0 -> 35.5 us); 8-B aligned
+        uint16_t *pb = (uint16_t *)take(sizeof(uint16_t) * (L.P + 64));
+        w.pbf = pb ? pb + (64 - L.oWf % 64) % 64 : nullptr;
+    }
     w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + kHeadRows - 1) / kHeadRows));
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
@@ -895,13 +907,16 @@ size_t head_loss_lds(const CnnLayout &L)
 }
 
 
-template <int AM, bool BF>
+// DH16 (bf16 trunk storage): dh stored as bf16 (round to nearest even: the fc products' operand);
+// dbf sums the unrounded values
+template <int AM, bool BF, bool DH16 = false>
 __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__ h, const float *__restrict__ P,
                                                        CnnLayout L, int B, CnnFields fl, LossArgs la,
-                                                       float *__restrict__ dz, float *__restrict__ dh,
+                                                       float *__restrict__ dz, void *__restrict__ dhv,
                                                        float *__restrict__ wpart, double *__restrict__ part,
                                                        const int32_t *__restrict__ stop)
 {
+    static_assert(!DH16 || BF, "bf16 dh storage: bf16 operands only");
     constexpr int NZ = (AM + 1 + 3) / 4;               // float4 chunks of a padded head row
     __shared__ double sred[kSums * 256 + kSums * 16];
     extern __shared__ float lds[];
@@ -1038,8 +1053,10 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 #pragma unroll
     for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
     const float invB = gmode ? la.inv_batch : 1.0f / (float)B;
-    {   // the loss rows: row tid >> 5 on a 32-lane segment of a wave, lane a = action a
-        static_assert(kHeadRows * 32 == 256, "one 32-lane segment per row");
+    // the loss rows: row tid >> 5 on a 32-lane segment of a wave, lane a = action a (segments past
+    // kHeadRows: whole idle waves)
+    static_assert(kHeadRows * 32 <= 256 && (kHeadRows * 32) % 64 == 0, "32-lane segments in whole waves");
+    if ((tid >> 5) < kHeadRows) {
         const int row = tid >> 5, a = tid & 31;
         const bool exists = r0 + row < B;
         float *dzr = zs + row * ZS;             // the row's z, overwritten by its dz
@@ -1084,10 +1101,12 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
             float sacc = 0.f;
 #pragma unroll
             for (int a = 0; a < 4 * NZ; ++a) sacc += d[a] * w[a];
-            const float dhv = hv > 0.f ? sacc : 0.f;
+            const float dhj = hv > 0.f ? sacc : 0.f;
             if (r0 + r < B) {
-                dh[(int64_t)(r0 + r) * HID + j] = dhv;
-                dbf += dhv;
+                if constexpr (DH16)
+                    static_cast<uint16_t *>(dhv)[(int64_t)(r0 + r) * HID + j] = __builtin_bit_cast(uint16_t, (__bf16)dhj);
+                else static_cast<float *>(dhv)[(int64_t)(r0 + r) * HID + j] = dhj;
+                dbf += dhj;
             }
             // this workgroup's share of dWh[a][j] = sum_r dz[r][a] h[r][j] (rows in order)
             const float hb = BF ? bf16r(hv) : hv;
@@ -1256,6 +1275,14 @@ __global__ __launch_bounds__(256) void k_cnn_gather_chunk(CnnFields fl, int B, i
     gather_fields(fl, B, normalize != 0, pre + (int64_t)k * 5 * B, pre_stats + 2 * k, sred);
 }
 
+// 4 fp32 -> 4 bf16 (round to nearest even), element 0 in the low half
+__device__ __forceinline__ uint2 bf16x4_rne(const float (&p)[4])
+{
+    const uint32_t b0 = __builtin_bit_cast(uint16_t, (__bf16)p[0]), b1 = __builtin_bit_cast(uint16_t, (__bf16)p[1]);
+    const uint32_t b2 = __builtin_bit_cast(uint16_t, (__bf16)p[2]), b3 = __builtin_bit_cast(uint16_t, (__bf16)p[3]);
+    return make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
+}
+
 // one parameter of torch.optim.Adam's single-tensor step on the clipped gradient (IEEE sqrt and
 // divisions as torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step * m / denom)
 __device__ __forceinline__ float adam_flat(float g, float &m, float &v, float p, const AdamArgs &aa)
@@ -1269,10 +1296,13 @@ __device__ __forceinline__ float adam_flat(float g, float &m, float &v, float p,
 // ---- clip coefficient from the partials (every block, fixed order) + Adam (torch single-tensor):
 // kAdamQuads float4 of parameters per thread, all loaded before the norm reduction (grid =
 // ceil(n / (1024 kAdamQuads)) + 1), the scalar tail by the last block
+// Pbf (bf16 trunk storage): the new parameters' bf16 copy (round to nearest even), the next
+// minibatch's weight operands
 __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, float *__restrict__ G,
                                                         float *__restrict__ M, float *__restrict__ V, int64_t n,
                                                         const double *__restrict__ part, int nparts, AdamArgs aa,
-                                                        float *__restrict__ metrics, const int32_t *__restrict__ stop)
+                                                        float *__restrict__ metrics, const int32_t *__restrict__ stop,
+                                                        uint16_t *__restrict__ Pbf)
 {
     if (stop && *stop) {
         // a job-wide stop (the exchange ORs the ranks' stop bits): no step on any rank
@@ -1345,6 +1375,7 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
         reinterpret_cast<float4 *>(M)[i] = make_float4(m[0], m[1], m[2], m[3]);
         reinterpret_cast<float4 *>(V)[i] = make_float4(v[0], v[1], v[2], v[3]);
         reinterpret_cast<float4 *>(Pm)[i] = make_float4(p[0], p[1], p[2], p[3]);
+        if (Pbf) reinterpret_cast<uint2 *>(Pbf)[i] = bf16x4_rne(p);
     }
     if ((int)blockIdx.x == last)
         for (int64_t k = 4 * n4 + threadIdx.x; k < n; k += 256) {
@@ -1354,7 +1385,21 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
             Pm[k] = adam_flat(g, m, v, Pm[k], aa);
             M[k] = m;
             V[k] = v;
+            if (Pbf) Pbf[k] = __builtin_bit_cast(uint16_t, (__bf16)Pm[k]);
         }
+}
+
+// the parameters' bf16 copy at the start of a bf16 update (k_clip_adam_flat keeps it current)
+__global__ __launch_bounds__(256) void k_params_bf16(const float *__restrict__ Pm, int64_t n, uint16_t *__restrict__ Pbf)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (4 * i + 3 < n) {
+        const float4 v = reinterpret_cast<const float4 *>(Pm)[i];
+        const float p[4] = {v.x, v.y, v.z, v.w};
+        reinterpret_cast<uint2 *>(Pbf)[i] = bf16x4_rne(p);
+    } else {
+        for (int64_t k = 4 * i; k < n; ++k) Pbf[k] = __builtin_bit_cast(uint16_t, (__bf16)Pm[k]);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1390,14 +1435,32 @@ ConvGeom geom1(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.H, L.W
 ConvGeom geom2(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h1, L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, L.c2}; }
 ConvGeom geom3(const CnnLayout &L, int64_t R) { return ConvGeom{(int)R, L.h2, L.w2, L.c2, L.k3, L.s3, L.h3, L.w3, L.c3}; }
 
+// the trunk's bf16 activation storage (gs_common.h act_bf16): a bf16 update whose every reader
+// of a1 / a2 / a3 is an LDS / fc kernel that takes them stored as bf16
+bool act16_trunk(const CnnLayout &L, bool bf, bool lib_fc)
+{
+    return bf && lib_fc && conv1_lds_supported(L.C, L.H, L.W) &&
+           conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2) &&
+           conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3);
+}
+
+// a weight operand of the trunk: the fp32 parameters, or (xh) their bf16 copy
+inline const void *wop(const float *P, const CnnWs &w, int64_t off, bool xh)
+{
+    return xh ? (const void *)(w.pbf + off) : (const void *)(P + off);
+}
+
 // the conv trunk for R rows (a3): obs rows come from the u8 buffer through idx (or 0..R)
-// (obs_copy: the rollout's obs row, written by conv1 from the frames it loads anyway)
+// (obs_copy: the rollout's obs row, written by conv1 from the frames it loads anyway; xh: a1 / a2
+// / a3 stored as bf16, act16_trunk)
 int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  bool bf, uint8_t *obs_copy = nullptr)
+                  bool bf, uint8_t *obs_copy = nullptr, bool xh = false)
 {
     int rc;
+    GS_REQUIRE(!xh || act16_trunk(L, bf, true), "bf16 activation storage: LDS trunk kernels only");
     if (conv1_lds_supported(L.C, L.H, L.W)) {
-        if ((rc = conv1_lds_fwd(s, bf, (int)R, fs.obs, fs.idx, fs.T, fs.N, P + L.oW1, P + L.ob1, w.a1, obs_copy)))
+        if ((rc = conv1_lds_fwd(s, bf, xh, (int)R, fs.obs, fs.idx, fs.T, fs.N, wop(P, w, L.oW1, xh), P + L.ob1, w.a1,
+                                obs_copy)))
             return rc;
     } else {
         if (obs_copy && obs_copy != fs.obs)
@@ -1405,12 +1468,12 @@ int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
         if ((rc = conv_fwd_u8(s, bf, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) return rc;
     }
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_fwd(s, bf, 2, (int)R, w.a1, P + L.oW2, P + L.ob2, w.a2))) return rc;
+        if ((rc = conv23_lds_fwd(s, bf, xh, 2, (int)R, w.a1, wop(P, w, L.oW2, xh), P + L.ob2, w.a2))) return rc;
     } else if ((rc = conv_fwd_nhwc(s, bf, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) {
         return rc;
     }
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_fwd(s, bf, 3, (int)R, w.a2, P + L.oW3, P + L.ob3, w.a3))) return rc;
+        if ((rc = conv23_lds_fwd(s, bf, xh, 3, (int)R, w.a2, wop(P, w, L.oW3, xh), P + L.ob3, w.a3))) return rc;
     } else if ((rc = conv_fwd_nhwc(s, bf, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
         return rc;
     }
@@ -1419,15 +1482,17 @@ int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
 
 // conv trunk + fc for R rows (h)
 int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  bool bf, bool lib_fc = false, const int32_t *stop = nullptr)
+                  bool bf, bool lib_fc = false, const int32_t *stop = nullptr, bool xh = false)
 {
-    int rc = forward_convs(P, L, fs, R, w, s, bf);
+    int rc = forward_convs(P, L, fs, R, w, s, bf, nullptr, xh);
     if (rc) return rc;
     // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
     // update), else the engine's split-K partials summed with the bias + ReLU epilogue
     // (the split-K form of the fp32 forward, fc_gemm's parts argument, was faster in the launch
     // sweep but slower inside the update: 43.6 + 5.0 us vs 46.0, round 5 — not used here)
-    if (lib_fc) return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, P + L.obf, stop);
+    if (lib_fc)
+        return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, wop(P, w, L.oWf, xh), L.F, w.h, L.HID, P + L.obf, stop,
+                       nullptr, xh);
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
         if ((rc = gemm_f32(s, bf, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf,
@@ -1452,7 +1517,7 @@ int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, c
 }
 
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc = false);
+                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc = false, bool xh = false);
 
 int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
              const int32_t *stop, hipStream_t s, bool bf)
@@ -1475,13 +1540,13 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
 
 // the trunk's backward from dh (fc, then the convolutions)
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc)
+                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc, bool xh)
 {
     int rc;
     const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
     // fc: [dWf | dbf] = dh^T [a3 | 1]; lib_fc: dWf on the fc kernels, dbf from the head kernels
     if (lib_fc) {
-        if ((rc = fc_gemm(s, 1, bf, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr, stop)))
+        if ((rc = fc_gemm(s, 1, bf, L.HID, L.F, B, w.dh, L.HID, w.a3, L.F, G + L.oWf, L.F, nullptr, stop, nullptr, xh)))
             return rc;
     } else {
         const int sw = splits_for(L.HID, L.F + 1, B);
@@ -1491,19 +1556,21 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // da3 = (dh Wf) masked by relu'(a3) in the GEMM's epilogue
     if (lib_fc) {
-        if ((rc = fc_gemm(s, 2, bf, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, w.a3, stop))) return rc;
+        if ((rc = fc_gemm(s, 2, bf, B, L.F, L.HID, w.dh, L.HID, wop(P, w, L.oWf, xh), L.F, w.da3, L.F, w.a3, stop,
+                          nullptr, xh)))
+            return rc;
     } else if ((rc = gemm_f32(s, bf, false, false, B, L.F, L.HID, w.dh, L.HID, P + L.oWf, L.F, w.da3, L.F, 0.f, nullptr,
                               false, 1, 0, w.a3))) {
         return rc;
     }
     // conv3 (dY3 = da3 as [m3][c3])
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_wgrad(s, bf, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
+        if ((rc = conv23_lds_wgrad(s, bf, xh, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
     } else if ((rc = conv_wgrad_nhwc(s, bf, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) {
         return rc;
     }
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_dgrad(s, bf, 3, (int)B, w.da3, w.a2, P + L.oW3, w.da2))) return rc;
+        if ((rc = conv23_lds_dgrad(s, bf, xh, 3, (int)B, w.da3, w.a2, wop(P, w, L.oW3, xh), w.da2))) return rc;
     } else {
         if ((rc = gemm_f32(s, bf, false, false, m3, L.K3, L.c3, w.da3, L.c3, P + L.oW3, L.K3, w.cols3, L.K3, 0.f, nullptr,
                            false)))
@@ -1514,12 +1581,12 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // conv2
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_wgrad(s, bf, 2, (int)B, w.a1, w.da2, w.parts, G + L.oW2, G + L.ob2))) return rc;
+        if ((rc = conv23_lds_wgrad(s, bf, xh, 2, (int)B, w.a1, w.da2, w.parts, G + L.oW2, G + L.ob2))) return rc;
     } else if ((rc = conv_wgrad_nhwc(s, bf, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) {
         return rc;
     }
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_dgrad(s, bf, 2, (int)B, w.da2, w.a1, P + L.oW2, w.da1))) return rc;
+        if ((rc = conv23_lds_dgrad(s, bf, xh, 2, (int)B, w.da2, w.a1, wop(P, w, L.oW2, xh), w.da1))) return rc;
     } else {
         if ((rc = gemm_f32(s, bf, false, false, m2, L.K2, L.c2, w.da2, L.c2, P + L.oW2, L.K2, w.cols2, L.K2, 0.f, nullptr,
                            false)))
@@ -1588,28 +1655,28 @@ bool head_fused(const CnnLayout &L, int64_t B)
 }
 
 int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFields &fl, const CnnWs &w,
-                     const LossArgs &la, float *G, float *metrics, int32_t *stop, hipStream_t s, bool bf)
+                     const LossArgs &la, float *G, float *metrics, int32_t *stop, hipStream_t s, bool bf, bool dh16)
 {
     const unsigned nb = (unsigned)((B + kHeadRows - 1) / kHeadRows);
     const size_t l1 = head_loss_lds(L);
-    auto go = [&](auto am, auto bfc) {
+    GS_REQUIRE(!dh16 || bf, "launch_head_loss: bf16 dh storage needs bf16 operands");
+    auto go = [&](auto am, auto bfc, auto dhc) {
         constexpr int AM = decltype(am)::value;
-        constexpr bool BF = decltype(bfc)::value;
+        constexpr bool BF = decltype(bfc)::value, DH16 = decltype(dhc)::value;
         static std::once_flag attrs;      // > 64 KB of dynamic LDS (the update is never graph-captured)
         std::call_once(attrs, [] {
-            (void)hipFuncSetAttribute((const void *)k_cnn_head_loss<AM, BF>,
+            (void)hipFuncSetAttribute((const void *)k_cnn_head_loss<AM, BF, DH16>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
         });
-        hipLaunchKernelGGL((k_cnn_head_loss<AM, BF>), dim3(nb), dim3(256), l1, s, w.h, P, L, (int)B, fl, la, w.dz,
-                           w.dh, w.parts, w.loss_part, stop);
+        hipLaunchKernelGGL((k_cnn_head_loss<AM, BF, DH16>), dim3(nb), dim3(256), l1, s, w.h, P, L, (int)B, fl, la,
+                           w.dz, (void *)w.dh, w.parts, w.loss_part, stop);
         GS_LAUNCH_CHECK("k_cnn_head_loss");
         return GS_OK;
     };
     using F = std::false_type;
     using T = std::true_type;
-    int rc;
-    if (L.A <= 18) rc = bf ? go(std::integral_constant<int, 18>{}, T{}) : go(std::integral_constant<int, 18>{}, F{});
-    else rc = bf ? go(std::integral_constant<int, kAMax>{}, T{}) : go(std::integral_constant<int, kAMax>{}, F{});
+    auto by_prec = [&](auto am) { return dh16 ? go(am, T{}, T{}) : bf ? go(am, T{}, F{}) : go(am, F{}, F{}); };
+    const int rc = L.A <= 18 ? by_prec(std::integral_constant<int, 18>{}) : by_prec(std::integral_constant<int, kAMax>{});
     if (rc) return rc;
     const int64_t nout = head_part_out(L);
     hipLaunchKernelGGL(k_cnn_head_wsum, dim3((unsigned)((nout + 63) / 64 + 1)), dim3(256), 0, s, w.parts, (int)nb, L,
@@ -1720,6 +1787,32 @@ struct CnnGlobalStep {
     int64_t batch_global;
 };
 
+// the update's fc products on the fc kernels (gs_fc.hip)
+bool fc_path(const CnnLayout &L, int64_t B)
+{
+    return fc_supported(0, B, L.HID, L.F, L.F, L.F, L.HID) && fc_supported(1, L.HID, L.F, B, L.HID, L.F, L.F) &&
+           fc_supported(2, B, L.F, L.HID, L.HID, L.F, L.F);
+}
+
+// a bf16 update on the fused path whose trunk kernels all take bf16 storage
+bool trunk_bf16_storage(const CnnLayout &L, const gs_ppo_hparams &hp, int64_t B)
+{
+    return (hp.flags & GS_HP_BF16) != 0 && head_fused(L, B) && act16_trunk(L, true, fc_path(L, B));
+}
+
+// the bf16 parameter copy at the start of an update that reads it
+int refresh_params_bf16(const float *P, const CnnLayout &L, const gs_ppo_hparams &hp, int64_t B, const CnnWs &w,
+                        hipStream_t s)
+{
+    if (!trunk_bf16_storage(L, hp, B)) return GS_OK;
+    GS_REQUIRE(((uintptr_t)w.pbf & 7) == 0 && ((uintptr_t)(w.pbf + L.oWf) & 127) == 0,
+               "the bf16 parameter copy is misaligned");
+    const int64_t n4 = (L.P + 3) / 4;
+    hipLaunchKernelGGL(k_params_bf16, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, P, L.P, w.pbf);
+    GS_LAUNCH_CHECK("k_params_bf16");
+    return GS_OK;
+}
+
 // pre / pre_stats (the local update's fused path): this minibatch's fields and advantage
 // statistics, gathered ahead by k_cnn_gather_chunk; the head + loss kernel reads them contiguously
 int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const gs_ppo_hparams &hp,
@@ -1730,6 +1823,10 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     int rc;
     const FrameSrc fs{ro.obs, gl ? gl->frame_idx : idx, ro.T, ro.N};
     const bool bf = (hp.flags & GS_HP_BF16) != 0;     // the operand precision of every product
+    // bf16 trunk storage (the update entry has made w.pbf current): the activations, dh and the
+    // weight operands stored as bf16 between the kernels — half the bytes, the same operand values
+    // and ReLU signs
+    const bool xh = trunk_bf16_storage(L, hp, B);
     GS_REQUIRE(!gl || head_fused(L, B), "global mode: the fused head + loss kernels do not fit this shape");
     if (head_fused(L, B)) {
         CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
@@ -1746,12 +1843,10 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         }
         // the fc layer's forward, weight and input gradients on the fc kernels (gs_fc.hip; dbf comes
         // from the head kernels), in the operand precision of the update
-        const bool lib_fc = fc_supported(0, B, L.HID, L.F, L.F, L.F, L.HID) &&
-                            fc_supported(1, L.HID, L.F, B, L.HID, L.F, L.F) &&
-                            fc_supported(2, B, L.F, L.HID, L.HID, L.F, L.F);
-        if ((rc = forward_trunk(P, L, fs, B, w, s, bf, lib_fc, stop))) return rc;
-        if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s, bf))) return rc;
-        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc))) return rc;
+        const bool lib_fc = fc_path(L, B);
+        if ((rc = forward_trunk(P, L, fs, B, w, s, bf, lib_fc, stop, xh))) return rc;
+        if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s, bf, xh))) return rc;
+        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc, xh))) return rc;
     } else {
         hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
                            ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv,
@@ -1773,7 +1868,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
                        L.oWv);
     const unsigned nadam = (unsigned)((L.P / 4 + 256 * kAdamQuads - 1) / (256 * kAdamQuads) + 1);
     hipLaunchKernelGGL(k_clip_adam_flat, dim3(nadam), dim3(256), 0, s, P, G, Mm, Vv, L.P, w.norm_part, kNormBlocks, aa,
-                       metrics, stop);
+                       metrics, stop, xh ? w.pbf : nullptr);
     GS_LAUNCH_CHECK("k_clip_adam_flat");
     return GS_OK;
 }
@@ -1886,6 +1981,7 @@ extern "C" int gs_cnn_ppo_update_global(float *params, float *grads, float *adam
     hipStream_t s = (hipStream_t)stream;
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
+    if ((rc = refresh_params_bf16(params, L, hp, batch, w, s))) return rc;
     for (int64_t k = 0; k < n_minibatches; ++k) {
         const CnnGlobalStep gl{frame_idx + k * batch, glob->adv_stats ? glob->adv_stats + 2 * k : nullptr,
                                glob->metric_sums + kNumSumsGlobal * k, glob->batch_global};
@@ -1915,6 +2011,7 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     const CnnWs w = carve(workspace, L, batch);
     // the fused head + loss path reads each minibatch's fields gathered ahead (kPreChunk at a time)
     const bool pre = head_fused(L, batch);
+    if ((rc = refresh_params_bf16(params, L, hp, batch, w, s))) return rc;
     for (int64_t k = 0; k < n_minibatches; ++k) {
         const int64_t slot = k % kPreChunk;
         if (pre && slot == 0) {

@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string>
+#include <type_traits>
 
 #include "../../include/gsamd.h"
 
@@ -355,6 +356,46 @@ __device__ __forceinline__ bf16x8 bf16_frag(const float (&v)[8])
 __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c)
 {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---- bf16 activation storage (GS_HP_BF16 updates on the NatureCNN trunk's LDS kernels) -------
+// The trunk's ReLU outputs a1 / a2 / a3 are only ever read as bf16 MFMA operands (rounded to
+// nearest even at every read) and as ReLU masks (their sign), so in the bf16 mode the forward
+// stores them rounded once: the same operand bits at half the bytes.  A positive value whose
+// rounding would be zero (below 2^-134) is stored as the smallest subnormal so the mask keeps
+// its sign.
+__device__ __forceinline__ uint16_t act_bf16(float v)
+{
+    const uint16_t u = __builtin_bit_cast(uint16_t, (__bf16)v);
+    return (v > 0.f && u == 0) ? (uint16_t)1 : u;
+}
+__device__ __forceinline__ float bf16_f32(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
+// 4 stored bf16 (8 bytes, element 0 in the low half) -> 4 fp32, exactly
+__device__ __forceinline__ float4 bf16x4_f32(uint2 u)
+{
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+}
+// the activation type of a trunk kernel: fp32, or bf16 storage (XH)
+template <bool XH>
+using act_t = typename std::conditional<XH, uint16_t, float>::type;
+template <bool XH>
+__device__ __forceinline__ float act_ld(const act_t<XH> *p, int64_t i)
+{
+    if constexpr (XH) return bf16_f32(p[i]);
+    else return p[i];
+}
+template <bool XH>
+__device__ __forceinline__ float4 act_ld4(const act_t<XH> *p, int64_t i)
+{
+    if constexpr (XH) return bf16x4_f32(*reinterpret_cast<const uint2 *>(p + i));
+    else return *reinterpret_cast<const float4 *>(p + i);
+}
+template <bool XH>
+__device__ __forceinline__ void act_st(act_t<XH> *p, int64_t i, float v)
+{
+    if constexpr (XH) p[i] = act_bf16(v);
+    else p[i] = v;
 }
 
 }  // namespace gs

@@ -10,22 +10,28 @@ constexpr int kConvWgradWG = 256;      // workgroups (= partials) of the conv2 /
 
 bool conv1_lds_supported(int C, int H, int W);
 // out[r][oy][ox][co] = relu(b1[co] + sum W1[co][c][ky][kx] * frame(r)[c][4 oy + ky][4 ox + kx] / 255)
-// bf: bf16 MFMA operands (GS_HP_BF16), fp32 accumulation; false: the fp32 parity path
-int conv1_lds_fwd(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N, const float *W1,
-                  const float *b1, float *out, uint8_t *obs_copy = nullptr);
+// bf: bf16 MFMA operands (GS_HP_BF16), fp32 accumulation; false: the fp32 parity path.
+// xh (needs bf): the activations a1 / a2 / a3 this file's kernels write and read are stored as
+// bf16 (gs_common.h act_bf16: the operand bits the bf16 mode rounds to anyway) and the forward /
+// input-gradient filters come from the update's bf16 weight copy, so those pointers are void:
+// fp32 or bf16 elements by xh (biases stay fp32)
+int conv1_lds_fwd(hipStream_t s, bool bf, bool xh, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
+                  const void *W1, const float *b1, void *out, uint8_t *obs_copy = nullptr);
 // dW1 = sum_rows dA1^T . patches, db1 = column sums of dA1; parts: kConv1WgradWG x (32*256 + 32) floats
 int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
                     const float *dA, float *parts, float *dW1, float *db1);
 int conv1_lds_wgrad_parts();
 // conv2 (20x20x32 -> 9x9x64, k4 s2) / conv3 (9x9x64 -> 7x7x64, k3 s1) forward with bias + ReLU,
-// NHWC fp32, LDS-resident samples (layer = 2 or 3)
+// NHWC, LDS-resident samples (layer = 2 or 3)
 bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cout);
-int conv23_lds_fwd(hipStream_t s, bool bf, int layer, int R, const float *in, const float *Wt, const float *bias, float *out);
+int conv23_lds_fwd(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const void *Wt,
+                   const float *bias, void *out);
 // input gradient of conv2 / conv3 masked by ReLU'(act) (act = the layer's input activation):
 // dX = (dY conv^T W) * (act > 0), NHWC fp32
-int conv23_lds_dgrad(hipStream_t s, bool bf, int layer, int R, const float *dY, const float *act, const float *Wt, float *dX);
+int conv23_lds_dgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const float *dY, const void *act,
+                     const void *Wt, float *dX);
 // dW (64 x patch) and db (64) of conv2 / conv3; parts: kConvWgradWG x 64 x (patch + 1) floats
-int conv23_lds_wgrad(hipStream_t s, bool bf, int layer, int R, const float *in, const float *dY, float *parts, float *dW,
-                     float *db);
+int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const float *dY, float *parts,
+                     float *dW, float *db);
 
 }  // namespace gs

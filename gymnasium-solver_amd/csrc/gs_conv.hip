@@ -167,13 +167,16 @@ __device__ __forceinline__ void stage_bands_bf16(uint16_t *fr, const uint8_t *__
 // column kx = 4 (q % 2) + j — a lane's 4 steps of a group are 4 adjacent pixels
 // SPB > 1 (bf16 update batches): the same band of SPB samples per workgroup, the filter registers
 // loaded once for all of them
-template <class G, bool BF = false, int SPB = 1>
+// XH: a1 stored as bf16 and W1 read from the update's bf16 weight copy (bf16 updates,
+// gs_common.h act_bf16)
+template <class G, bool BF = false, int SPB = 1, bool XH = false>
 __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
-                                                   int64_t T, int64_t N, const float *__restrict__ W1,
-                                                   const float *__restrict__ b1, float *__restrict__ out,
+                                                   int64_t T, int64_t N, const act_t<XH> *__restrict__ W1,
+                                                   const float *__restrict__ b1, act_t<XH> *__restrict__ out,
                                                    uint8_t *__restrict__ obs_copy, int R)
 {
     static_assert(SPB == 1 || BF, "several samples per workgroup: bf16 staging only");
+    static_assert(!XH || BF, "bf16 activation storage: bf16 operands only");
     // obs_copy (the rollout's obs row, idx == nullptr): band b copies rows [b H / NB, (b + 1) H / NB)
     static_assert(G::bands_cover(), "the bands cover the obs copy's row ranges");
     // BF: the band staged as bf16 (u8 / 255 rounded once; half the LDS, more workgroups per CU)
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
 #pragma unroll
     for (int g = 0; g < G::KS / 4; ++g) {
         const int c = g >> 2, ky = 2 * (g & 3) + (lq >> 1), kx0 = 4 * (lq & 1);
-        b[g] = *reinterpret_cast<const float4 *>(W1 + (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
+        b[g] = act_ld4<XH>(W1, (nt * 16 + li) * G::KK + (c * G::K + ky) * G::K + kx0);
     }
     if constexpr (SPB == 1) {
         stage_band<G, FT>(fr, obs, frame_src(idx, r0, T, N), oy0 * G::S,
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
             }
         }
         // epilogue: D row = lq * 4 + j (position), col = li (filter)
-        float *o = out + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
+        act_t<XH> *o = out + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
         const int co = nt * 16 + li;
         const float bb = b1[co];
     #pragma unroll
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
                 const int p = (tpar + 2 * t) * 16 + lq * 4 + j;
                 if (p < P) {
                     const float v = acc[t][j] + bb;
-                    o[(int64_t)p * G::CO + co] = v > 0.f ? v : 0.f;
+                    act_st<XH>(o, (int64_t)p * G::CO + co, v > 0.f ? v : 0.f);
                 }
             }
         }
@@ -640,11 +643,15 @@ constexpr int kConvFwdBurst = 16;      // float4 loads per thread per staging bu
 // FS workgroups per sample group, each owning 4 / FS filter blocks of 16, and the waves of a
 // filter block splitting the k-step groups into FS contiguous ranges; the ranges' partial tiles
 // are added in range order through LDS (deterministic), then the bias + ReLU epilogue.
-template <class G, bool BF = false, int FS = 1>
-__global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, int R, const float *__restrict__ Wt,
-                                                  const float *__restrict__ bias, float *__restrict__ out)
+// XH (bf16 updates): input and output activations stored as bf16 (gs_common.h act_bf16: the
+// staging copies the stored operand bits, the epilogue rounds once) and the filters read from the
+// update's bf16 weight copy
+template <class G, bool BF = false, int FS = 1, bool XH = false>
+__global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ in, int R, const act_t<XH> *__restrict__ Wt,
+                                                  const float *__restrict__ bias, act_t<XH> *__restrict__ out)
 {
     static_assert(FS == 1 || FS == 2 || FS == 4, "filter split");
+    static_assert(!XH || BF, "bf16 activation storage: bf16 operands only");
     constexpr int NFB = 4 / FS;                    // filter blocks per workgroup
     constexpr int NGW = G::NG / FS;                // k-step groups per wave
     static_assert(G::NG % FS == 0 && (!BF || NGW % 2 == 0), "k-step groups split evenly (bf16: in pairs)");
@@ -669,7 +676,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
     float4 b[NGW];
 #pragma unroll
     for (int g = 0; g < NGW; ++g)
-        b[g] = *reinterpret_cast<const float4 *>(Wt + (int64_t)(16 * fb + li) * G::KK + 16 * (g0 + g) + 4 * lq);
+        b[g] = act_ld4<XH>(Wt, (int64_t)(16 * fb + li) * G::KK + 16 * (g0 + g) + 4 * lq);
 
     // stage: [sample][position][channel] with position stride CS, 8 float4 loads in flight
     {
@@ -678,7 +685,28 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
         // bf16 two-sample conv2 tile keeps bursts of 8 (16 cost it registers: 50.4 vs 39.1 us)
         constexpr int BURST = (BF && NE > 256 * kConvFwdBurst) ? 8 : kConvFwdBurst;
         constexpr int BATCH = (NE + 255) / 256 <= BURST ? (NE + 255) / 256 : BURST;
-        const float *src = in + (int64_t)r0 * G::H * G::W * G::C;
+        const act_t<XH> *src = in + (int64_t)r0 * G::H * G::W * G::C;
+        if constexpr (XH) {
+            // stored bf16: 4 channels per 8-B load, copied as they are
+            for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
+                uint2 v[BATCH];
+#pragma unroll
+                for (int j = 0; j < BATCH; ++j) {
+                    const int e = e0 + tid + 256 * j;
+                    const int q = e / (G::H * G::W * C4);
+                    v[j] = (e < NE && q < nsamp) ? *reinterpret_cast<const uint2 *>(src + 4 * (int64_t)e)
+                                                 : make_uint2(0u, 0u);
+                }
+#pragma unroll
+                for (int j = 0; j < BATCH; ++j) {
+                    const int e = e0 + tid + 256 * j;
+                    if (e < NE) {
+                        const int pos = e / C4, c4 = e - pos * C4;
+                        *reinterpret_cast<uint2 *>(xs + pos * G::CS + 4 * c4) = v[j];
+                    }
+                }
+            }
+        } else
         for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
             float4 v[BATCH];
 #pragma unroll
@@ -783,7 +811,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
     // epilogue: D row = lq * 4 + j (position), col = li (filter 16 fb + li)
     const int co = 16 * fb + li;
     const float bb = bias[co];
-    float *o = out + (int64_t)r0 * G::OHW * G::CO;
+    act_t<XH> *o = out + (int64_t)r0 * G::OHW * G::CO;
 #pragma unroll
     for (int t = 0; t < G::MT; ++t)
 #pragma unroll
@@ -791,7 +819,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const float *__restrict__ in, 
             const int p = t * 16 + lq * 4 + j;
             if (p < nsamp * G::OHW) {
                 const float v = acc[t][j] + bb;
-                o[(int64_t)p * G::CO + co] = v > 0.f ? v : 0.f;
+                act_st<XH>(o, (int64_t)p * G::CO + co, v > 0.f ? v : 0.f);
             }
         }
 }
@@ -822,9 +850,10 @@ struct CD {
     static_assert(H % S == 0 && W % S == 0 && K % S == 0 && NTHR <= 512 && CW % 16 == 0, "shape");
 };
 
-template <class G, bool BF = false>
-__global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict__ dY, const float *__restrict__ act, int R,
-                                                    const float *__restrict__ Wt, float *__restrict__ dX)
+// XH: the mask's activation stored as bf16, the filters read from the update's bf16 weight copy
+template <class G, bool BF = false, bool XH = false>
+__global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict__ dY, const act_t<XH> *__restrict__ act,
+                                                    int R, const act_t<XH> *__restrict__ Wt, float *__restrict__ dX)
 {
     // BF: dY staged as bf16 (rounded once at the store; CS = 72 elements = 36 dwords between
     // positions: the 8-B operand reads of 16 positions stay on distinct banks)
@@ -847,9 +876,10 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
         const int ky = py + G::S * dky, kx = px + G::S * dkx;
 #pragma unroll
         for (int nt = 0; nt < G::NT; ++nt) {
-            const float *w = Wt + (((int64_t)(cb + 4 * lq) * G::K + ky) * G::K + kx) * G::C + c0 + 16 * nt + li;
+            const int64_t w = (((int64_t)(cb + 4 * lq) * G::K + ky) * G::K + kx) * G::C + c0 + 16 * nt + li;
             constexpr int64_t st = (int64_t)G::K * G::K * G::C;     // next out-channel
-            b[g][nt] = make_float4(w[0], w[st], w[2 * st], w[3 * st]);
+            b[g][nt] = make_float4(act_ld<XH>(Wt, w), act_ld<XH>(Wt, w + st), act_ld<XH>(Wt, w + 2 * st),
+                                   act_ld<XH>(Wt, w + 3 * st));
         }
     }
     // stage dY with a zero border: padded [sample][PH][PW][CS], 8 float4 loads in flight
@@ -961,7 +991,7 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
             const int64_t e = (((int64_t)(r0 + q) * G::H + y) * G::W + x) * G::C + c0 + li;
 #pragma unroll
             for (int nt = 0; nt < G::NT; ++nt)
-                dX[e + 16 * nt] = act[e + 16 * nt] > 0.f ? acc[t][nt][j] : 0.f;
+                dX[e + 16 * nt] = act_ld<XH>(act, e + 16 * nt) > 0.f ? acc[t][nt][j] : 0.f;
         }
 }
 
@@ -983,8 +1013,9 @@ struct WG2 {
 };
 
 constexpr int kWgradBurstMax = 24;      // float4 per thread of one staging burst (conv2: 18, conv3: 9)
-template <class G, bool BF = false>
-__global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in, const float *__restrict__ dY, int R,
+// XH: the input activation stored as bf16 (staged to LDS as its exact fp32 value)
+template <class G, bool BF = false, bool XH = false>
+__global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict__ in, const float *__restrict__ dY, int R,
                                                     float *__restrict__ parts)
 {
     using X = WG2<G>;
@@ -1014,19 +1045,23 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
         {   // input activation [pos][c] with stride CSX, dY [pos][co] with stride DS (zero rows past OHW)
             // every load of the sample in one burst (one memory latency per sample; 8 per burst
             // took 2 - 3 round trips)
-            constexpr int NX4 = G::H * G::W * G::C / 4, ND4 = X::PP * G::CO / 4;
-            constexpr int NE = NX4 + ND4, BATCH = (NE + 255) / 256 <= kWgradBurstMax ? (NE + 255) / 256 : 8;
-            const float *xin = in + (int64_t)r * G::H * G::W * G::C;
+            // XH: the bf16 input in 16-B units of 8 channels (every load of the burst 16 B wide, so
+            // the two kinds share registers without a merge that would wait on each load)
+            constexpr int XU = XH ? 8 : 4;     // input elements per 16-B unit
+            constexpr int NXU = G::H * G::W * G::C / XU, ND4 = X::PP * G::CO / 4;
+            constexpr int NE = NXU + ND4, BATCH = (NE + 255) / 256 <= kWgradBurstMax ? (NE + 255) / 256 : 8;
+            static_assert(G::C % XU == 0, "whole units per position");
+            const act_t<XH> *xin = in + (int64_t)r * G::H * G::W * G::C;
             const float *dyin = dY + (int64_t)r * G::OHW * G::CO;
             for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
                 float4 v[BATCH];
 #pragma unroll
                 for (int j = 0; j < BATCH; ++j) {
                     const int e = e0 + tid + 256 * j;
-                    if (e < NX4) {
-                        v[j] = *reinterpret_cast<const float4 *>(xin + 4 * (int64_t)e);
+                    if (e < NXU) {
+                        v[j] = *reinterpret_cast<const float4 *>(xin + XU * (int64_t)e);
                     } else {
-                        const int d = e - NX4;
+                        const int d = e - NXU;
                         const int p = d / (G::CO / 4);
                         v[j] = (e < NE && p < G::OHW) ? *reinterpret_cast<const float4 *>(dyin + 4 * (int64_t)d)
                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1035,11 +1070,19 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const float *__restrict__ in
 #pragma unroll
                 for (int j = 0; j < BATCH; ++j) {
                     const int e = e0 + tid + 256 * j;
-                    if (e < NX4) {
-                        const int pos = e / (G::C / 4), c4 = e - pos * (G::C / 4);
-                        *reinterpret_cast<float4 *>(xs + pos * X::CSX + 4 * c4) = v[j];
+                    if (e < NXU) {
+                        const int pos = e / (G::C / XU), cu = e - pos * (G::C / XU);
+                        float *dst = xs + pos * X::CSX + XU * cu;
+                        if constexpr (XH) {     // 8 stored bf16 -> their exact fp32 values
+                            const uint4 h = make_uint4(__float_as_uint(v[j].x), __float_as_uint(v[j].y),
+                                                       __float_as_uint(v[j].z), __float_as_uint(v[j].w));
+                            *reinterpret_cast<float4 *>(dst) = bf16x4_f32(make_uint2(h.x, h.y));
+                            *reinterpret_cast<float4 *>(dst + 4) = bf16x4_f32(make_uint2(h.z, h.w));
+                        } else {
+                            *reinterpret_cast<float4 *>(dst) = v[j];
+                        }
                     } else if (e < NE) {
-                        const int d = e - NX4;
+                        const int d = e - NXU;
                         const int p = d / (G::CO / 4), c4 = d - p * (G::CO / 4);
                         *reinterpret_cast<float4 *>(ds + p * X::DS + 4 * c4) = v[j];
                     }
@@ -1137,29 +1180,40 @@ using C1_84q = C1<4, 84, 84, 4>;          // 4 bands per sample (small batches)
 
 bool conv1_lds_supported(int C, int H, int W) { return C == 4 && H == 84 && W == 84; }
 
-int conv1_lds_fwd(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
-                  const float *W1, const float *b1, float *out, uint8_t *obs_copy)
+int conv1_lds_fwd(hipStream_t s, bool bf, bool xh, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
+                  const void *W1v, const float *b1, void *out, uint8_t *obs_copy)
 {
+    const float *W1 = static_cast<const float *>(W1v);
+    const uint16_t *W1h = static_cast<const uint16_t *>(W1v);
     GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
     GS_REQUIRE(!obs_copy || !idx, "conv1_lds_fwd: the obs copy is for the rollout's own rows");
+    GS_REQUIRE(!xh || bf, "conv1_lds_fwd: bf16 activation storage needs bf16 operands");
+    float *o32 = static_cast<float *>(out);
+    uint16_t *o16 = static_cast<uint16_t *>(out);
     // very small batches: 4 bands of 5 output rows per sample, so R < 128 rows still launch at
     // least 256 workgroups; otherwise 2 bands (fewer padded tiles: at R = 128 the 2-band form
     // already fills the chip and ran 16.7 us vs 21.6 us for 4 bands)
     if ((int64_t)R * 2 < kConv1Bands4Below) {
         const dim3 grid((unsigned)(C1_84q::NB * R));
-        if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84q, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
-                                   obs_copy, R);
-        else hipLaunchKernelGGL((k_conv1_fwd<C1_84q>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out, obs_copy, R);
+        if (xh) hipLaunchKernelGGL((k_conv1_fwd<C1_84q, true, 1, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1h, b1,
+                                   o16, obs_copy, R);
+        else if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84q, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, o32,
+                                        obs_copy, R);
+        else hipLaunchKernelGGL((k_conv1_fwd<C1_84q>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, o32, obs_copy, R);
     } else if (bf && !obs_copy && R >= kConv1PairsFrom) {
         // bf16 update batches: kConv1Spb samples per workgroup (36.7 -> 32.4 us per C4 minibatch with 2)
         const dim3 grid((unsigned)(C1_84::NB * ((R + kConv1Spb - 1) / kConv1Spb)));
-        hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, kConv1Spb>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
-                           obs_copy, R);
+        if (xh) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, kConv1Spb, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1h,
+                                   b1, o16, obs_copy, R);
+        else hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, kConv1Spb>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1,
+                                o32, obs_copy, R);
     } else {
         const dim3 grid((unsigned)(C1_84::NB * R));
-        if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out,
-                                   obs_copy, R);
-        else hipLaunchKernelGGL((k_conv1_fwd<C1_84>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, out, obs_copy, R);
+        if (xh) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, 1, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1h, b1,
+                                   o16, obs_copy, R);
+        else if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, o32,
+                                        obs_copy, R);
+        else hipLaunchKernelGGL((k_conv1_fwd<C1_84>), grid, dim3(256), 0, s, obs, idx, T, N, W1, b1, o32, obs_copy, R);
     }
     GS_LAUNCH_CHECK("k_conv1_fwd");
     return GS_OK;
@@ -1200,62 +1254,89 @@ bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cou
 // splits, so R = 128 rows still launch 256 workgroups; the update's minibatches keep FS = 1
 // G: fp32 update batches, GB: bf16 update batches, G1: small batches (FS = 2)
 template <class G, class G1, class GB, int FSB = 1>
-int launch_conv_fwd(hipStream_t s, int R, const float *in, const float *Wt, const float *bias, float *out, bool bf)
+int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const float *bias, void *out, bool bf, bool xh)
 {
+    const float *Wt = static_cast<const float *>(Wv);
+    const uint16_t *Wh = static_cast<const uint16_t *>(Wv);
+    const float *i32 = static_cast<const float *>(in);
+    const uint16_t *i16 = static_cast<const uint16_t *>(in);
+    float *o32 = static_cast<float *>(out);
+    uint16_t *o16 = static_cast<uint16_t *>(out);
     if ((int64_t)R * 2 <= kConvFwdSmallWG) {
         const dim3 grid((unsigned)(2 * R));
-        if (bf) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
-        else hipLaunchKernelGGL((k_conv_fwd<G1, false, 2>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        if (xh) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16);
+        else if (bf) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
+        else hipLaunchKernelGGL((k_conv_fwd<G1, false, 2>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
     } else if (bf) {
         const dim3 grid((unsigned)((R + GB::SPB - 1) / GB::SPB * FSB));
-        hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        if (xh) hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16);
+        else hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
     } else {
         const dim3 grid((unsigned)((R + G::SPB - 1) / G::SPB));
-        hipLaunchKernelGGL((k_conv_fwd<G>), grid, dim3(256), 0, s, in, R, Wt, bias, out);
+        hipLaunchKernelGGL((k_conv_fwd<G>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
     }
     GS_LAUNCH_CHECK("k_conv_fwd");
     return GS_OK;
 }
 
-int conv23_lds_fwd(hipStream_t s, bool bf, int layer, int R, const float *in, const float *Wt, const float *bias,
-                   float *out)
+int conv23_lds_fwd(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const void *Wt,
+                   const float *bias, void *out)
 {
     GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
-    if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS>(s, R, in, Wt, bias, out, bf);
-    return launch_conv_fwd<C3_84, C3_84s, C3_84b>(s, R, in, Wt, bias, out, bf);
+    GS_REQUIRE(!xh || bf, "conv23_lds_fwd: bf16 activation storage needs bf16 operands");
+    if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS>(s, R, in, Wt, bias, out, bf, xh);
+    return launch_conv_fwd<C3_84, C3_84s, C3_84b>(s, R, in, Wt, bias, out, bf, xh);
 }
 
-int conv23_lds_dgrad(hipStream_t s, bool bf, int layer, int R, const float *dY, const float *act, const float *Wt,
-                     float *dX)
+template <class G>
+void launch_conv_dgrad(hipStream_t s, bool bf, bool xh, int R, const float *dY, const void *act, const void *Wv,
+                       float *dX)
+{
+    const dim3 grid((unsigned)((R + G::SPB - 1) / G::SPB));
+    const float *a32 = static_cast<const float *>(act);
+    const float *Wt = static_cast<const float *>(Wv);
+    if (xh)
+        hipLaunchKernelGGL((k_conv_dgrad<G, true, true>), grid, dim3(G::NTHR), 0, s, dY,
+                           static_cast<const uint16_t *>(act), R, static_cast<const uint16_t *>(Wv), dX);
+    else if (bf) hipLaunchKernelGGL((k_conv_dgrad<G, true>), grid, dim3(G::NTHR), 0, s, dY, a32, R, Wt, dX);
+    else hipLaunchKernelGGL(k_conv_dgrad<G>, grid, dim3(G::NTHR), 0, s, dY, a32, R, Wt, dX);
+}
+
+int conv23_lds_dgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const float *dY, const void *act,
+                     const void *Wt, float *dX)
 {
     GS_REQUIRE(R > 0 && dY && act && Wt && dX, "conv23_lds_dgrad: bad argument");
-    if (layer == 2) {
-        const dim3 grid((unsigned)((R + D2_84::SPB - 1) / D2_84::SPB));
-        if (bf) hipLaunchKernelGGL((k_conv_dgrad<D2_84, true>), grid, dim3(D2_84::NTHR), 0, s, dY, act, R, Wt, dX);
-        else hipLaunchKernelGGL(k_conv_dgrad<D2_84>, grid, dim3(D2_84::NTHR), 0, s, dY, act, R, Wt, dX);
-    } else {
-        const dim3 grid((unsigned)((R + D3_84::SPB - 1) / D3_84::SPB));
-        if (bf) hipLaunchKernelGGL((k_conv_dgrad<D3_84, true>), grid, dim3(D3_84::NTHR), 0, s, dY, act, R, Wt, dX);
-        else hipLaunchKernelGGL(k_conv_dgrad<D3_84>, grid, dim3(D3_84::NTHR), 0, s, dY, act, R, Wt, dX);
-    }
+    GS_REQUIRE(!xh || bf, "conv23_lds_dgrad: bf16 activation storage needs bf16 operands");
+    if (layer == 2) launch_conv_dgrad<D2_84>(s, bf, xh, R, dY, act, Wt, dX);
+    else launch_conv_dgrad<D3_84>(s, bf, xh, R, dY, act, Wt, dX);
     GS_LAUNCH_CHECK("k_conv_dgrad");
     return GS_OK;
 }
 
-int conv23_lds_wgrad(hipStream_t s, bool bf, int layer, int R, const float *in, const float *dY, float *parts,
+template <class G>
+void launch_conv_wgrad(hipStream_t s, bool bf, bool xh, int nwg, int R, const void *in, const float *dY, float *parts)
+{
+    const float *i32 = static_cast<const float *>(in);
+    if (xh)
+        hipLaunchKernelGGL((k_conv_wgrad<G, true, true>), dim3(nwg), dim3(256), 0, s,
+                           static_cast<const uint16_t *>(in), dY, R, parts);
+    else if (bf) hipLaunchKernelGGL((k_conv_wgrad<G, true>), dim3(nwg), dim3(256), 0, s, i32, dY, R, parts);
+    else hipLaunchKernelGGL(k_conv_wgrad<G>, dim3(nwg), dim3(256), 0, s, i32, dY, R, parts);
+}
+
+int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const float *dY, float *parts,
                      float *dW, float *db)
 {
     GS_REQUIRE(R > 0 && in && dY && parts && dW && db, "conv23_lds_wgrad: bad argument");
+    GS_REQUIRE(!xh || bf, "conv23_lds_wgrad: bf16 activation storage needs bf16 operands");
     const int nwg = kConvWgradWG;
     int KK;
     if (layer == 2) {
         KK = C2_84::KK;
-        if (bf) hipLaunchKernelGGL((k_conv_wgrad<C2_84, true>), dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
-        else hipLaunchKernelGGL(k_conv_wgrad<C2_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+        launch_conv_wgrad<C2_84>(s, bf, xh, nwg, R, in, dY, parts);
     } else {
         KK = C3_84::KK;
-        if (bf) hipLaunchKernelGGL((k_conv_wgrad<C3_84, true>), dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
-        else hipLaunchKernelGGL(k_conv_wgrad<C3_84>, dim3(nwg), dim3(256), 0, s, in, dY, R, parts);
+        launch_conv_wgrad<C3_84>(s, bf, xh, nwg, R, in, dY, parts);
     }
     GS_LAUNCH_CHECK("k_conv_wgrad");
     return sum_parts_wb(s, parts, nwg, (int64_t)64 * (KK + 1), 64, KK, dW, db);

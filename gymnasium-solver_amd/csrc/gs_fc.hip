@@ -97,18 +97,24 @@ __device__ __forceinline__ float f4at(const float4 &v, int c)
 // staging of one operand's K tile: ROWS rows (m or n) x KE k.  KC: source element (row, k) at
 // p[row * ld + k] (K-contiguous), else at p[k * ld + row].  Every thread moves the same number of
 // units (no divergent branches, so the waitcnt counts stay exact); rows past n_rows load clamped
-// and are zeroed at the store.
-template <int ROWS, bool BF, bool KC, int KT>
+// and are zeroed at the store.  SH (bf16 operands only): the source holds bf16 (a bf16-stored
+// activation / weight copy), 4 elements per 8-B load kept as raw bits until the store writes them
+// (expanding them at the load made the compiler wait for each tile's loads as soon as they were
+// issued: the fc forward ran 28 -> 36 us)
+template <int ROWS, bool BF, bool KC, int KT, bool SH = false>
 struct Stage {
+    static_assert(!SH || BF, "bf16 source: bf16 staging");
     static constexpr int KE = FcK<BF, KT>::KE, RB = FcK<BF, KT>::RB;
     // K-contiguous: one float4 (4 k of one row) per unit; K-strided: a 4 x 4 block per unit
     static constexpr int UNITS = KC ? ROWS * KE / 4 : ROWS * KE / 16;
     static constexpr int PER = UNITS / 256;
     static_assert(UNITS % 256 == 0, "whole units per thread");
     static constexpr int NV = KC ? 1 : 4;
-    float4 r[PER][NV];
+    using RT = typename std::conditional<SH, uint2, float4>::type;
+    using ST = typename std::conditional<SH, uint16_t, float>::type;
+    RT r[PER][NV];
 
-    __device__ __forceinline__ void load(const float *__restrict__ p, int64_t ld, int row0, int n_rows, int k0)
+    __device__ __forceinline__ void load(const ST *__restrict__ p, int64_t ld, int row0, int n_rows, int k0)
     {
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
@@ -116,15 +122,21 @@ struct Stage {
             if constexpr (KC) {
                 const int row = u / (KE / 4), k4 = u - row * (KE / 4);
                 const int gr = min(row0 + row, n_rows - 1);
-                r[j][0] = *reinterpret_cast<const float4 *>(p + (int64_t)gr * ld + k0 + 4 * k4);
+                r[j][0] = *reinterpret_cast<const RT *>(p + (int64_t)gr * ld + k0 + 4 * k4);
             } else {
                 const int kb = u / (ROWS / 4), rb = u - kb * (ROWS / 4);
                 const int gr = min(row0 + 4 * rb, n_rows - 4);     // n_rows % 4 == 0 (host check)
 #pragma unroll
                 for (int v = 0; v < 4; ++v)
-                    r[j][v] = *reinterpret_cast<const float4 *>(p + (int64_t)(k0 + 4 * kb + v) * ld + gr);
+                    r[j][v] = *reinterpret_cast<const RT *>(p + (int64_t)(k0 + 4 * kb + v) * ld + gr);
             }
         }
+    }
+
+    // bf16 bits of element c of a raw 4-element unit
+    static __device__ __forceinline__ uint32_t h16(const uint2 &u, int c)
+    {
+        return ((c < 2 ? u.x : u.y) >> (16 * (c & 1))) & 0xffffu;
     }
 
     __device__ __forceinline__ void store(char *lds, int row0, int n_rows) const
@@ -135,25 +147,37 @@ struct Stage {
             if constexpr (KC) {
                 const int row = u / (KE / 4), k4 = u - row * (KE / 4);
                 const bool ok = row0 + row < n_rows;
-                const float4 v = ok ? r[j][0] : make_float4(0.f, 0.f, 0.f, 0.f);
                 char *dst = lds + row * RB;
-                if constexpr (BF)
-                    *reinterpret_cast<uint2 *>(dst + 16 * ((k4 >> 1) ^ swz(row)) + 8 * (k4 & 1)) = pack_bf16x4(v);
-                else *reinterpret_cast<float4 *>(dst + 16 * (k4 ^ swz(row))) = v;
+                if constexpr (SH) {
+                    *reinterpret_cast<uint2 *>(dst + 16 * ((k4 >> 1) ^ swz(row)) + 8 * (k4 & 1)) =
+                        ok ? r[j][0] : make_uint2(0u, 0u);
+                } else {
+                    const float4 v = ok ? r[j][0] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    if constexpr (BF)
+                        *reinterpret_cast<uint2 *>(dst + 16 * ((k4 >> 1) ^ swz(row)) + 8 * (k4 & 1)) = pack_bf16x4(v);
+                    else *reinterpret_cast<float4 *>(dst + 16 * (k4 ^ swz(row))) = v;
+                }
             } else {
                 const int kb = u / (ROWS / 4), rb = u - kb * (ROWS / 4);
                 const bool ok = row0 + 4 * rb < n_rows;
                 // r[j][v] = rows 4 rb .. 4 rb + 3 at k = 4 kb + v: column c is row 4 rb + c's 4 k
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const float4 v = ok ? make_float4(f4at(r[j][0], c), f4at(r[j][1], c), f4at(r[j][2], c),
-                                                      f4at(r[j][3], c))
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
                     char *dst = lds + (4 * rb + c) * RB;
                     const int sr = swz(4 * rb + c);
-                    if constexpr (BF)
-                        *reinterpret_cast<uint2 *>(dst + 16 * ((kb >> 1) ^ sr) + 8 * (kb & 1)) = pack_bf16x4(v);
-                    else *reinterpret_cast<float4 *>(dst + 16 * (kb ^ sr)) = v;
+                    if constexpr (SH) {
+                        const uint2 w = ok ? make_uint2(h16(r[j][0], c) | (h16(r[j][1], c) << 16),
+                                                        h16(r[j][2], c) | (h16(r[j][3], c) << 16))
+                                           : make_uint2(0u, 0u);
+                        *reinterpret_cast<uint2 *>(dst + 16 * ((kb >> 1) ^ sr) + 8 * (kb & 1)) = w;
+                    } else {
+                        const float4 v = ok ? make_float4(f4at(r[j][0], c), f4at(r[j][1], c), f4at(r[j][2], c),
+                                                          f4at(r[j][3], c))
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                        if constexpr (BF)
+                            *reinterpret_cast<uint2 *>(dst + 16 * ((kb >> 1) ^ sr) + 8 * (kb & 1)) = pack_bf16x4(v);
+                        else *reinterpret_cast<float4 *>(dst + 16 * (kb ^ sr)) = v;
+                    }
                 }
             }
         }
@@ -176,12 +200,22 @@ __device__ __forceinline__ void static_for(F &&f)
 // buffer; one barrier per tile; tile kt + 1 + PD is loaded right after (tile j lives in register
 // set j % PD, so its global latency hides under PD tiles of MFMAs).  Loads and stores are
 // unconditional (the last tiles re-load a clamped tile) so the compiler's wait counts stay exact.
-template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, int PD, int KT>
-__global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int64_t lda, const float *__restrict__ Bm,
+// H16 (bf16 updates): bit 1 — A, bit 2 — B, bit 4 — the mask operand aux are bf16-stored
+// activations (gs_common.h act_bf16), 2 B per element
+template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, int PD, int KT, int H16 = 0>
+__global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int64_t lda, const void *__restrict__ Bv,
                                                int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
-                                               const float *__restrict__ aux, const int32_t *__restrict__ stop,
+                                               const void *__restrict__ auxv, const int32_t *__restrict__ stop,
                                                int64_t sC, int gm)
 {
+    static_assert(H16 == 0 || BF, "bf16 operand storage: bf16 MFMA operands only");
+    static_assert(!(H16 & 4) || EPI == kEpiMask, "a bf16 aux is the mask operand");
+    using AT = typename std::conditional<(H16 & 1) != 0, uint16_t, float>::type;
+    using BT = typename std::conditional<(H16 & 2) != 0, uint16_t, float>::type;
+    using XT = typename std::conditional<(H16 & 4) != 0, uint16_t, float>::type;
+    const AT *A = static_cast<const AT *>(Av);
+    const BT *Bm = static_cast<const BT *>(Bv);
+    const XT *aux = static_cast<const XT *>(auxv);
     if (stop && *stop) return;      // KL early stop: the minibatch's product is never used
     // split-K (gridDim.z slices of K each, partial products at C + z sC; no epilogue)
     A += (AK ? 1 : lda) * (int64_t)blockIdx.z * K;
@@ -220,8 +254,8 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
     const int wm = (wmn / WGN) * WM, wn = (wmn % WGN) * WN;
     const int l32 = lane & 31, lh = lane >> 5;
 
-    Stage<BM, BF, AK, KT> sa[PD];
-    Stage<BN, BF, BKC, KT> sb[PD];
+    Stage<BM, BF, AK, KT, (H16 & 1) != 0> sa[PD];
+    Stage<BN, BF, BKC, KT, (H16 & 2) != 0> sb[PD];
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -325,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
         for (int j = 0; j < TN; ++j) {
             const int gn = n0 + wn + 32 * j + l32;
             if (gn >= N) continue;
-            const float bn = EPI == kEpiBiasRelu ? aux[gn] : 0.0f;
+            const float bn = EPI == kEpiBiasRelu ? act_ld<(H16 & 4) != 0>(aux, gn) : 0.0f;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int gm = m0 + wm + 32 * i + (v & 3) + 8 * (v >> 2) + 4 * lh;
@@ -335,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void k_fc(const float *__restrict__ A, int6
                     x += bn;
                     x = x > 0.0f ? x : 0.0f;
                 }
-                if constexpr (EPI == kEpiMask) x = aux[(int64_t)gm * ldc + gn] > 0.0f ? x : 0.0f;
+                if constexpr (EPI == kEpiMask) x = act_ld<(H16 & 4) != 0>(aux, (int64_t)gm * ldc + gn) > 0.0f ? x : 0.0f;
                 C[(int64_t)gm * ldc + gn] = x;
             }
         }
@@ -514,23 +548,25 @@ constexpr size_t fc_lds_bytes()
 }
 
 template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32, int PD16, int KT32, int KT16,
-          bool MI16 = false>
-int launch_fc(hipStream_t s, bool bf, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
-              int64_t M, int64_t N, int64_t K, const float *aux, const int32_t *stop, int gm, int splits = 1,
+          bool MI16 = false, int H16 = 0>
+int launch_fc(hipStream_t s, bool bf, const void *A, int64_t lda, const void *B, int64_t ldb, float *C, int64_t ldc,
+              int64_t M, int64_t N, int64_t K, const void *aux, const int32_t *stop, int gm, int splits = 1,
               int64_t sC = 0)
 {
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
+    GS_REQUIRE(H16 == 0 || (bf && splits == 1), "k_fc: bf16 operand storage needs bf16 operands, no K split");
     K /= splits;
     if (bf) {
         constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, true, KT16>();
-        auto k = k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16>;
+        auto k = k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16, H16>;
         lds_attr(k, L);
         hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
     } else if (MI16 && FC_MI16) {
         constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, false, KT32>();
         auto k = k_fc16<BM, BN, WGM, KS, AK, BKC, EPI, PD32, KT32>;
         lds_attr(k, L);
-        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+        hipLaunchKernelGGL(k, grid, dim3(256), L, s, static_cast<const float *>(A), lda, static_cast<const float *>(B),
+                           ldb, C, ldc, (int)M, (int)N, (int)K, static_cast<const float *>(aux), stop, sC, gm);
     } else {
         constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, false, KT32>();
         auto k = k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32>;
@@ -619,14 +655,16 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
         s, false, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 4, splits, M * ldc);
 }
 
-int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop, float *parts)
+int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const void *A, int64_t lda,
+            const void *B, int64_t ldb, float *C, int64_t ldc, const void *aux, const int32_t *stop, float *parts,
+            bool act16)
 {
     GS_REQUIRE(op >= 0 && op <= 2, "fc_gemm: op %d", op);
     GS_REQUIRE(fc_supported(op, M, N, K, lda, ldb, ldc), "fc_gemm: shape %lld x %lld x %lld (op %d) not supported",
                (long long)M, (long long)N, (long long)K, op);
     GS_REQUIRE(aligned16(A) && aligned16(B) && (op == 1 || aux), "fc_gemm: 16-B aligned operands (and the epilogue "
                "operand) required");
+    GS_REQUIRE(!act16 || (bf16 && !parts), "fc_gemm: bf16 activation storage needs bf16 operands, no partials");
     if (op == 0) {   // fwd: C = relu(A B^T + bias), both K-contiguous
         // fp32 with a partials buffer: 64 x 64 tiles (waves 2 x 1 x KS 2, 32 x 64 each) over two K
         // halves, summed in slice order with the bias + ReLU epilogue (tools/fc_sweep.py, round 5:
@@ -636,16 +674,27 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
             int rc = launch_fc<64, 64, 2, 2, true, true, kEpiStore, 2, 2, 1, 1>(s, false, A, lda, B, ldb, parts, N, M, N,
                                                                                K, nullptr, stop, 4, 2, M * N);
             if (rc) return rc;
-            return fc_sum<kEpiBiasRelu>(s, parts, 2, M, N, C, ldc, aux, stop);
+            return fc_sum<kEpiBiasRelu>(s, static_cast<float *>(parts), 2, M, N, C, ldc,
+                                        static_cast<const float *>(aux), stop);
         }
+        if (act16)      // A = a3, B = Wf: bf16 storage
+            return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1, false, 3>(
+                s, true, A, lda, B, ldb, C, ldc, M, N, K, aux, stop, 4);
         return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
                                                                                            ldc, M, N, K, aux, stop, 4);
     }
-    if (op == 1)     // wgrad: C = A^T B with A [K][M], B [K][N] (the round-5 sweep's 16x16x4 form: 46.2
+    if (op == 1) {   // wgrad: C = A^T B with A [K][M], B [K][N] (the round-5 sweep's 16x16x4 form: 46.2
                      // vs 47.9 us back to back, 46.9 vs 46.7 inside the update — kept on 32x32x2)
+        if (act16)      // A = dh, B = a3: bf16 storage
+            return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1, false, 3>(
+                s, true, A, lda, B, ldb, C, ldc, M, N, K, nullptr, stop, 8);
         return launch_fc<64, 64, 2, 1, false, false, kEpiStore, FC_PD_WG32, FC_PD_WG16, 2, 1>(s, bf16, A, lda, B, ldb, C,
                                                                                             ldc, M, N, K, nullptr, stop, 8);
+    }
     // dgrad: C = (A B) * (aux > 0) with A [M][K], B [K][N]
+    if (act16)          // A = dh, B = Wf, aux = a3: bf16 storage
+        return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1, true, 7>(
+            s, true, A, lda, B, ldb, C, ldc, M, N, K, aux, stop, 16);
     return launch_fc<64, 64, 2, 1, true, false, kEpiMask, FC_PD_DG32, FC_PD_DG16, 2, 1, true>(s, bf16, A, lda, B, ldb, C,
                                                                                                 ldc, M, N, K, aux, stop, 16);
 }

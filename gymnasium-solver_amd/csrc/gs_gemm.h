@@ -44,10 +44,13 @@ int gemm_f32(hipStream_t s, bool bf16, bool ta, bool tb, int64_t M, int64_t N, i
 // C = A^T B (A [K][M], B [K][N]); op 2 C = (A B) * (aux > 0) (A [M][K], B [K][N], aux like C).
 // fc_supported: the shapes they take (K % 64 == 0, 16-B rows, K-strided operands in 4-row blocks).
 bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
-// parts (optional, 2 M N floats): the fp32 forward's split-K partials (faster at the C4 shape)
-int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const float *A, int64_t lda,
-            const float *B, int64_t ldb, float *C, int64_t ldc, const float *aux, const int32_t *stop = nullptr,
-            float *parts = nullptr);
+// parts (optional, 2 M N floats): the fp32 forward's split-K partials (faster at the C4 shape).
+// act16 (needs bf16): every operand but the bias is stored as bf16 — a3 (op 0's A, op 1's B, op
+// 2's aux, gs_common.h act_bf16), dh (op 1's and op 2's A) and Wf (op 0's and op 2's B, the
+// update's bf16 weight copy) — so the operand pointers are void
+int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const void *A, int64_t lda,
+            const void *B, int64_t ldb, float *C, int64_t ldc, const void *aux, const int32_t *stop = nullptr,
+            float *parts = nullptr, bool act16 = false);
 // the fc forward product as split-K fp32 partials (no epilogue) for small row counts (the
 // rollout): C + z M ldc = A[:, z K/splits ..] B[:, z K/splits ..]^T for z < splits;
 // fc_fwd_splits picks the split (1 when the plain tiles already fill the chip)
