@@ -33,6 +33,15 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c)
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// f(integral_constant<I>) for I = B .. E-1 in order while it returns true (compile-time indices)
+template <int I, int E, class F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    if constexpr (I < E) {
+        if (f(std::integral_constant<int, I>{})) static_for<I + 1, E>(f);
+    }
+}
+
 template <int C_, int H_, int W_, int NB_ = 2>
 struct C1 {
     static constexpr int C = C_, H = H_, W = W_, NB = NB_;
@@ -434,8 +443,10 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
 // adjacent elements).  Row strides: 16 filter rows 4 banks apart (136 slots), the 16 taps of an
 // n-tile (2 ky x 8 kx sub-rows of 12 dwords, ky 96 dwords apart) on 16 distinct 4-bank chunks.
 // db from the fp32 dA registers (the products' operands are rounded, the bias sum is not).
-// Same parts layout as k_conv1_wgrad.
-template <class G>
+// Same parts layout as k_conv1_wgrad.  D units' loads in flight (register sets, unit i in set
+// i % D; the two LDS buffers as before): one workgroup per CU at one wave per SIMD, so the loads
+// of the next unit alone left each unit waiting out a memory latency.
+template <class G, int D = 1>
 __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restrict__ obs,
                                                         const int32_t *__restrict__ idx, int64_t T, int64_t N, int R,
                                                         const float *__restrict__ dA, float *__restrict__ parts)
@@ -485,9 +496,10 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
         for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);     // channels 4 (tid % 8) .. + 3
 
-    uint32_t fv[PF];
-    float4 dv[PD];
-    auto load = [&](int unit) {
+    uint32_t fv[D][PF];
+    float4 dv[D][PD];
+    auto load = [&](auto sc, int unit) {
+        constexpr int S = decltype(sc)::value;
         const int r = unit / NU, oy0 = (unit % NU) * UR;
         const uint8_t *base = obs + frame_src(idx, r, T, N) * (int64_t)(G::C * G::H * G::W);
         const int y0 = oy0 * G::S;
@@ -496,16 +508,17 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
             const int e = min(tid + 256 * j, NF - 1);
             const int c = e / (UIR * G::W4), rem = e - c * (UIR * G::W4);
             const int y = rem / G::W4, x4 = rem - y * G::W4;
-            fv[j] = *reinterpret_cast<const uint32_t *>(base + ((int64_t)c * G::H + y0 + y) * G::W + 4 * x4);
+            fv[S][j] = *reinterpret_cast<const uint32_t *>(base + ((int64_t)c * G::H + y0 + y) * G::W + 4 * x4);
         }
         const float *src = dA + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
 #pragma unroll
         for (int j = 0; j < PD; ++j) {
             const int e = min(tid + 256 * j, NDA - 1);
-            dv[j] = *reinterpret_cast<const float4 *>(src + 4 * (int64_t)e);
+            dv[S][j] = *reinterpret_cast<const float4 *>(src + 4 * (int64_t)e);
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](auto sc, int buf) {
+        constexpr int S = decltype(sc)::value;
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
             const int e = tid + 256 * j;
@@ -513,7 +526,7 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
                 const int c = e / (UIR * G::W4), rem = e - c * (UIR * G::W4);
                 const int y = rem / G::W4, w = rem - y * G::W4;
                 __bf16 *row = &fb[buf][(c * UIR + y) * G::K * XS];
-                const uint32_t v = fv[j];
+                const uint32_t v = fv[S][j];
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
                     const __bf16 h = u8_bf16((v >> (8 * b)) & 255u);
@@ -531,7 +544,7 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
                 const int p = e / (G::CO / 4), c4 = e - p * (G::CO / 4);
                 const int oy = p / G::OW, ox = p - oy * G::OW;
                 const int slot = (oy * GPR + (ox >> 3)) * 8 + (ox & 7);
-                const float4 d = dv[j];
+                const float4 d = dv[S][j];
                 dat[buf][(4 * c4 + 0) * DTS + slot] = (__bf16)d.x;
                 dat[buf][(4 * c4 + 1) * DTS + slot] = (__bf16)d.y;
                 dat[buf][(4 * c4 + 2) * DTS + slot] = (__bf16)d.z;
@@ -542,17 +555,23 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
     };
 
     const int n_units = R * NU;
-    int unit = blockIdx.x;
+    auto U = [&](int it) { return (int)blockIdx.x + it * (int)gridDim.x; };     // this workgroup's it-th unit
+    using I0 = std::integral_constant<int, 0>;
+    // units 0 .. D-1 in flight, unit 0 stored; then unit D into its set
+    static_for<0, D>([&](auto sc) -> bool {
+        if (U(decltype(sc)::value) < n_units) load(sc, U(decltype(sc)::value));
+        return true;
+    });
     __syncthreads();                                    // the zero fill before the first stores
-    if (unit < n_units) {
-        load(unit);
-        store(0);
-    }
+    if (U(0) < n_units) store(I0{}, 0);
     __syncthreads();
-    for (int it = 0; unit < n_units; ++it, unit += gridDim.x) {
+    if (U(D) < n_units) load(I0{}, U(D));
+    for (int it0 = 0; U(it0) < n_units; it0 += D) {
+      static_for<0, D>([&](auto uc) -> bool {
+        constexpr int u = decltype(uc)::value;
+        const int it = it0 + u;
+        if (U(it) >= n_units) return false;
         const int buf = it & 1;
-        const int next = unit + gridDim.x;
-        if (next < n_units) load(next);                  // in flight during this unit's MFMAs
 #pragma unroll
         for (int m = 0; m < NBLK; ++m) {
             const int gi = 4 * m + lq;
@@ -569,8 +588,12 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
                 acc[1][nt] = mfma16_bf16(a1, bv[nt], acc[1][nt]);
             }
         }
-        if (next < n_units) store(buf ^ 1);
+        constexpr int nv = (u + 1) % D;                 // the set holding unit it + 1
+        if (U(it + 1) < n_units) store(std::integral_constant<int, nv>{}, buf ^ 1);
         __syncthreads();
+        if (U(it + 1 + D) < n_units) load(std::integral_constant<int, nv>{}, U(it + 1 + D));
+        return true;
+      });
     }
     // partial out: D row = lq * 4 + j (filter within the m-tile), col = li (tap within the n-tile)
     float *o = parts + (int64_t)blockIdx.x * (G::CO * G::KK + G::CO);
@@ -1164,13 +1187,20 @@ using C3_84s = CN<9, 9, 64, 3, 1, 1>;     // conv3, one sample per workgroup (sm
 // bf16 update batches: conv2 two samples per workgroup (the filter registers loaded once for both:
 // 44.9 -> 39.0 us per C4 minibatch; fp32 keeps one, its two-sample tile would not leave room for
 // a second workgroup per CU); conv3 as fp32 (4 or 1 samples per workgroup ran slower).  Same-box
-// sweep, profiles/r04_conv_fwd_bf16_sweep.txt
+// sweep, profiles/r04_conv_fwd_bf16_sweep.txt.  With bf16 storage (xh: bf16 weights, 104 instead of
+// 170 VGPRs) conv2 is back on one sample per workgroup (32.6 -> 29.5 us); conv1 / conv3 keep two
+// (conv1 with 4: 40.7, 1: 32.2 vs 32.3; conv3 with 4: 25.7, 1: 24.7 vs 21.9; round 5, same box)
 using C2_84b = CN<20, 20, 32, 4, 2, 2>;
+using C2_84x = CN<20, 20, 32, 4, 2, 1>;
 using C3_84b = CN<9, 9, 64, 3, 1, 2>;
 constexpr int kConv2BfFS = 1;              // 2 (filter blocks split over two workgroups): 52.2 us
 constexpr int kConvFwdSmallWG = 1024;     // FS = 2 up to this many workgroups (R <= 512)
 constexpr int kConv1PairsFrom = 512;     // bf16: kConv1Spb samples per conv1 forward workgroup from this many rows
 constexpr int kConv1Spb = 2;
+#ifndef GS_C1WG_DEPTH
+#define GS_C1WG_DEPTH 1
+#endif
+constexpr int kConv1WgradDepth = GS_C1WG_DEPTH;   // units in flight in the bf16 conv1 weight gradient
 constexpr int kConv1Bands4Below = 256;    // conv1 in 4 bands below this many 2-band workgroups
 
 using C1_84 = C1<4, 84, 84>;
@@ -1227,7 +1257,8 @@ int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int
     GS_REQUIRE(R > 0 && obs && dA && parts && dW1 && db1, "conv1_lds_wgrad: bad argument");
     constexpr int n = C1_84::CO * C1_84::KK, stride = n + C1_84::CO;
     if (bf)
-        hipLaunchKernelGGL(k_conv1_wgrad_bf<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
+        hipLaunchKernelGGL((k_conv1_wgrad_bf<C1_84, kConv1WgradDepth>), dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T,
+                           N, R, dA, parts);
     else
         hipLaunchKernelGGL(k_conv1_wgrad<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
     GS_LAUNCH_CHECK("k_conv1_wgrad");
@@ -1253,7 +1284,7 @@ bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cou
 // small batches (the rollout's policy act): one sample per workgroup group and FS = 2 filter
 // splits, so R = 128 rows still launch 256 workgroups; the update's minibatches keep FS = 1
 // G: fp32 update batches, GB: bf16 update batches, G1: small batches (FS = 2)
-template <class G, class G1, class GB, int FSB = 1>
+template <class G, class G1, class GB, int FSB = 1, class GX = GB>
 int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const float *bias, void *out, bool bf, bool xh)
 {
     const float *Wt = static_cast<const float *>(Wv);
@@ -1267,10 +1298,12 @@ int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const 
         if (xh) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16);
         else if (bf) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
         else hipLaunchKernelGGL((k_conv_fwd<G1, false, 2>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
+    } else if (xh) {
+        const dim3 grid((unsigned)((R + GX::SPB - 1) / GX::SPB * FSB));
+        hipLaunchKernelGGL((k_conv_fwd<GX, true, FSB, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16);
     } else if (bf) {
         const dim3 grid((unsigned)((R + GB::SPB - 1) / GB::SPB * FSB));
-        if (xh) hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16);
-        else hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
+        hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
     } else {
         const dim3 grid((unsigned)((R + G::SPB - 1) / G::SPB));
         hipLaunchKernelGGL((k_conv_fwd<G>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
@@ -1284,7 +1317,7 @@ int conv23_lds_fwd(hipStream_t s, bool bf, bool xh, int layer, int R, const void
 {
     GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
     GS_REQUIRE(!xh || bf, "conv23_lds_fwd: bf16 activation storage needs bf16 operands");
-    if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS>(s, R, in, Wt, bias, out, bf, xh);
+    if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS, C2_84x>(s, R, in, Wt, bias, out, bf, xh);
     return launch_conv_fwd<C3_84, C3_84s, C3_84b>(s, R, in, Wt, bias, out, bf, xh);
 }
 
