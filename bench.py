@@ -595,10 +595,12 @@ def main():
                                  in_shape=tuple(pm.in_shape), n_actions=pm.n_actions, valid=cfg.valid_actions,
                                  clip=cfg.clip_range, ent_coef=cfg.ent_coef, lr=cfg.policy_lr, threads=cores)
         cpu = {"value": round(r["env_steps_per_s"], 2), "unit": "env_steps/s", "cores": r["threads"], "kind": "port",
-               "sample": (f"8 vector steps of the torch-CPU NatureCNN policy on {N} envs + 3 of "
-                          f"{r['minibatches_per_rollout']} minibatch steps (B={cfg.batch_size}), extrapolated; env "
+               "sample": (f"{r['sample_steps']} vector steps of the torch-CPU NatureCNN policy on {N} envs + "
+                          f"{r['sample_minibatches']} of {r['minibatches_per_rollout']} minibatch steps "
+                          f"(B={cfg.batch_size}), each after one untimed, extrapolated to the rollout / update; env "
                           f"emulation excluded; wall {r['wall_s']:.1f}s"),
-               "step_ms": round(r["step_s"] * 1e3, 3), "minibatch_ms": round(r["minibatch_s"] * 1e3, 3), **host}
+               "step_ms": round(r["step_s"] * 1e3, 3), "minibatch_ms": round(r["minibatch_s"] * 1e3, 3),
+               "window_minibatch_ms": [round(x * 1e3, 3) for x in r["window_minibatch_s"]], **host}
     elif cpu is None and rank == 0 and world == 1 and args.cpu_minibatches != 0:
         from oracle.cpu_ppo import run_cpu_baseline
         r = run_cpu_baseline(n_envs=N, n_steps=T, batch=cfg.batch_size, n_epochs=cfg.n_epochs,

@@ -182,13 +182,15 @@ class _CNNActorCritic(nn.Module):
 
 
 def run_cpu_baseline_cnn(n_envs=256, n_steps=256, batch=1024, n_epochs=15, in_shape=(4, 84, 84), n_actions=18,
-                         valid=(0, 3, 4), hidden=512, clip=0.2, ent_coef=0.01, lr=3e-4, sample_steps=8,
-                         sample_minibatches=3, threads=None, seed=42):
+                         valid=(0, 3, 4), hidden=512, clip=0.2, ent_coef=0.01, lr=3e-4, sample_steps=64,
+                         sample_minibatches=40, threads=None, seed=42):
     """Bounded CPU sample of the pixel path (C4/C5): `sample_steps` vector steps of the rollout
     policy forward + sampling and `sample_minibatches` full minibatch steps (forward, masked PPO
-    loss, backward, clip, Adam), each extrapolated to the full rollout / update.  The frame source
-    is a pre-made u8 stack (the reference's ALE emulation and preprocessing run in ale-py C++,
-    not available here): env cost is EXCLUDED, which flatters the CPU number."""
+    loss, backward, clip, Adam), each extrapolated to the full rollout / update (defaults: about
+    12 s of CPU work at the C4 shapes on 16 cores), after one untimed step of each.  The frame
+    source is a pre-made u8 stack (the reference's ALE emulation and preprocessing run in ale-py
+    C++, not available here): env cost is EXCLUDED, which flatters the CPU number.  The timed
+    minibatches are also reported in windows of `sample_minibatches // 10` (their spread)."""
     from .cnn_ref import dist_terms
     if threads:
         torch.set_num_threads(int(threads))
@@ -198,9 +200,10 @@ def run_cpu_baseline_cnn(n_envs=256, n_steps=256, batch=1024, n_epochs=15, in_sh
     opt = torch.optim.Adam(model.parameters(), lr=lr)
     g = torch.Generator().manual_seed(seed)
     obs = torch.randint(0, 256, (n_envs, *in_shape), dtype=torch.uint8, generator=g)
-    t0 = time.perf_counter()
     with torch.inference_mode():
-        for _ in range(sample_steps):
+        for i in range(sample_steps + 1):
+            if i == 1:
+                t0 = time.perf_counter()      # after one untimed step
             logits, v = model(obs)
             a = torch.distributions.Categorical(logits=logits).sample()
             dist_terms(logits, a, valid)
@@ -213,8 +216,10 @@ def run_cpu_baseline_cnn(n_envs=256, n_steps=256, batch=1024, n_epochs=15, in_sh
     old_v = torch.zeros(batch)
     adv = torch.randn(batch, generator=g)
     ret = adv.clone()
-    t2 = time.perf_counter()
-    for _ in range(sample_minibatches):
+    marks = []
+    for i in range(sample_minibatches + 1):
+        if i == 1:
+            t2 = time.perf_counter()          # after one untimed minibatch
         a_n = (adv - adv.mean()) / (adv.std() + 1e-8)
         logits, v = model(mb_obs)
         lp, H = dist_terms(logits, act, valid)
@@ -228,13 +233,20 @@ def run_cpu_baseline_cnn(n_envs=256, n_steps=256, batch=1024, n_epochs=15, in_sh
         torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
         opt.step()
         loss.item()
+        if i >= 1:
+            marks.append(time.perf_counter())
     t3 = time.perf_counter()
     per_step = (t1 - t0) / sample_steps
     per_mb = (t3 - t2) / sample_minibatches
     n_mb = n_envs * n_steps // batch * n_epochs
     total = per_step * n_steps + per_mb * n_mb
+    w = max(1, sample_minibatches // 10)
+    edges = [t2] + marks
+    windows = [(edges[min(j + w, len(edges) - 1)] - edges[j]) / (min(j + w, len(edges) - 1) - j)
+               for j in range(0, len(edges) - 1, w)]
     return dict(env_steps_per_s=n_envs * n_steps / total, step_s=per_step, minibatch_s=per_mb,
-                minibatches_per_rollout=n_mb, wall_s=t3 - t0, threads=torch.get_num_threads())
+                minibatches_per_rollout=n_mb, wall_s=t3 - t0, threads=torch.get_num_threads(),
+                sample_steps=sample_steps, sample_minibatches=sample_minibatches, window_minibatch_s=windows)
 
 
 _ = ppo_ref

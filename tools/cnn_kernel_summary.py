@@ -6,8 +6,9 @@ bytes; separate passes).  Every minibatch dispatches the same 28 kernels in the 
 by its position in the minibatch and the three runs line up position by position.
 
 Per kernel: average duration over the measured minibatches, algorithmic FLOPs (2 x MACs of the
-layer's product) and algorithmic bytes (each operand read once, each output written once, fp32
-activations, u8 frames), the HBM bytes the counters saw (2 x FETCH_SIZE + WRITE_SIZE, KB -> B:
+layer's product) and algorithmic bytes (each operand read once, each output written once, u8
+frames; fp32 activations, or with --bf16 the bf16 update's storage: bf16 activations, dh and
+weight operands), the HBM bytes the counters saw (2 x FETCH_SIZE + WRITE_SIZE, KB -> B:
 the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md), the MFMA fraction against the dense
 peak of the operand type and the HBM fraction against 8 TB/s.
 
@@ -42,26 +43,32 @@ SEQ_FC_SPLIT = SEQ_FC[:4] + [("fc_fwd_splitk_sum", "k_fc_sum")] + SEQ_FC[4:]
 SEQ = SEQ_FC
 
 
-def nature_work(B, A=18, C=4, H=84, W=84):
-    """(flops, bytes) per MFMA layer product of one minibatch of B rows."""
+def nature_work(B, A=18, C=4, H=84, W=84, store16=False):
+    """(flops, bytes) per MFMA layer product of one minibatch of B rows.  store16: the bf16 update's
+    storage (gs_cnn.hip trunk_bf16_storage) — the activations a1 / a2 / a3, dh and the weight
+    operands cross HBM as bf16; gradients, h, z and biases stay fp32."""
     f = 4
+    ea = ew = ed = 2 if store16 else f          # activation / weight-operand / dh element bytes
     h1, w1, c1, K1 = (H - 8) // 4 + 1, (W - 8) // 4 + 1, 32, C * 64
     h2, w2, c2, K2 = (h1 - 4) // 2 + 1, (w1 - 4) // 2 + 1, 64, c1 * 16
     h3, w3, c3, K3 = h2 - 2, w2 - 2, 64, c2 * 9
     F, HID, A1 = c3 * h3 * w3, 512, A + 1
     frames = B * C * H * W                     # u8
-    a1, a2, a3 = B * h1 * w1 * c1 * f, B * h2 * w2 * c2 * f, B * F * f
+    n1, n2, n3 = B * h1 * w1 * c1, B * h2 * w2 * c2, B * F     # activation elements
     hb, zb = B * HID * f, B * A1 * f
-    W1, W2, W3, Wf, Wh = c1 * K1 * f, c2 * K2 * f, c3 * K3 * f, HID * F * f, A1 * HID * f
+    p1, p2, p3, pf, Wh = c1 * K1, c2 * K2, c3 * K3, HID * F, A1 * HID * f     # weight elements
     m1, m2, m3, mf, mh = B * h1 * w1 * c1 * K1, B * h2 * w2 * c2 * K2, B * h3 * w3 * c3 * K3, B * F * HID, B * HID * A1
     return {
-        "conv1_fwd": (2 * m1, frames + W1 + a1), "conv2_fwd": (2 * m2, a1 + W2 + a2),
-        "conv3_fwd": (2 * m3, a2 + W3 + a3), "fc_fwd": (2 * mf, a3 + Wf + hb), "heads_fwd": (2 * mh, hb + Wh + zb),
-        "heads_wgrad": (2 * mh, zb + hb + Wh), "fc_wgrad": (2 * mf, hb + a3 + Wf), "fc_dgrad": (2 * mf, hb + Wf + a3), "fc_dgrad_relu_mask": (2 * mf, hb + Wf + 2 * a3),
-        "conv3_wgrad": (2 * m3, a2 + a3 + W3), "conv3_dgrad": (2 * m3, a3 + W3 + 2 * a2),   # + the ReLU mask read
-        "conv2_wgrad": (2 * m2, a1 + a2 + W2), "conv2_dgrad": (2 * m2, a2 + W2 + 2 * a1),
-        "conv1_wgrad": (2 * m1, frames + a1 + W1),
-        "head_loss": (4 * mh, hb + Wh + zb + hb),    # z = h Wh^T and the dWh partials (+ dh out)
+        "conv1_fwd": (2 * m1, frames + p1 * ew + n1 * ea), "conv2_fwd": (2 * m2, n1 * ea + p2 * ew + n2 * ea),
+        "conv3_fwd": (2 * m3, n2 * ea + p3 * ew + n3 * ea), "fc_fwd": (2 * mf, n3 * ea + pf * ew + hb),
+        "heads_fwd": (2 * mh, hb + Wh + zb), "heads_wgrad": (2 * mh, zb + hb + Wh),
+        "fc_wgrad": (2 * mf, B * HID * ed + n3 * ea + pf * f),
+        "fc_dgrad": (2 * mf, B * HID * ed + pf * ew + n3 * f),
+        "fc_dgrad_relu_mask": (2 * mf, B * HID * ed + pf * ew + n3 * f + n3 * ea),     # + the ReLU mask read
+        "conv3_wgrad": (2 * m3, n2 * ea + n3 * f + p3 * f), "conv3_dgrad": (2 * m3, n3 * f + p3 * ew + n2 * f + n2 * ea),
+        "conv2_wgrad": (2 * m2, n1 * ea + n2 * f + p2 * f), "conv2_dgrad": (2 * m2, n2 * f + p2 * ew + n1 * f + n1 * ea),
+        "conv1_wgrad": (2 * m1, frames + n1 * f + p1 * f),
+        "head_loss": (4 * mh, hb + Wh + zb + B * HID * ed),    # z = h Wh^T and the dWh partials (+ dh out)
     }
 
 
@@ -131,7 +138,7 @@ def main():
                                  "WRITE_SIZE"))[a.skip:]
     for mb in trace + fetch + write:
         check_seq(mb)
-    work = nature_work(a.batch)
+    work = nature_work(a.batch, store16=a.bf16)
     peak = PEAK_BF16_MFMA if a.bf16 else PEAK_F32_MFMA
     kernels = {}
     tot_us = tot_bytes = tot_alg = 0.0
