@@ -1128,19 +1128,21 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     GS_STAMP_END(7)
 }
 
-// [dWh | dbh] = the k_cnn_head_loss partials summed in workgroup order (64 outputs per workgroup,
-// 4 thread groups over contiguous partial ranges, combined in group order); the last workgroup
-// writes the minibatch record (and sets the KL stop)
+// [dWh | dbh] = the k_cnn_head_loss partials summed in workgroup order (kWsumOut outputs per
+// workgroup, kWsumGroups thread groups over contiguous partial ranges, 32 loads of a group in
+// flight, combined in group order); the last workgroup writes the minibatch record (and sets the
+// KL stop).  16 outputs x 16 groups ran slower (10.2 vs 7.9 us: 64-B row segments)
+constexpr int kWsumOut = 64, kWsumGroups = 256 / kWsumOut;
 __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__ wpart, int nparts, CnnLayout L,
                                                        float *__restrict__ G, const double *__restrict__ part, int B,
                                                        LossArgs la, float *__restrict__ metrics,
                                                        int32_t *__restrict__ stop)
 {
-    __shared__ float red[4][64];
+    __shared__ float red[kWsumGroups][kWsumOut];
     const int tid = threadIdx.x, HID = L.HID, A = L.A;
     const int64_t nout = head_part_out(L), pstride = head_part_stride(L);
     const int64_t pad = (int64_t)(head_part_rows(L) - (A + 1)) * (HID + 1);     // the zero rows skipped
-    if ((int64_t)blockIdx.x * 64 >= nout) {
+    if ((int64_t)blockIdx.x * kWsumOut >= nout) {
         // the record: the 13 loss sums over the partials, 16 threads per sum (strided, in order),
         // then the 16 in order; thread 0 writes it from a one-partial view of the totals
         __shared__ double msum[kSums][16];
@@ -1168,13 +1170,13 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
         return;
     }
     if (stop && *stop) return;
-    const int o = tid & 63, g = tid >> 6;
-    const int64_t out = (int64_t)blockIdx.x * 64 + o;
+    const int o = tid % kWsumOut, g = tid / kWsumOut;
+    const int64_t out = (int64_t)blockIdx.x * kWsumOut + o;
     const int64_t oc0 = out < nout ? out : nout - 1;
     const int64_t oc = oc0 < (int64_t)(A + 1) * (HID + 1) ? oc0 : oc0 + pad;     // its partial column
-    const int w0 = (g * nparts) / 4, w1 = ((g + 1) * nparts) / 4;
+    const int w0 = (g * nparts) / kWsumGroups, w1 = ((g + 1) * nparts) / kWsumGroups;
     float sacc = 0.f;
-    constexpr int NB = 8;
+    constexpr int NB = 32;
     for (int w = w0; w < w1; w += NB) {
         float t[NB];
 #pragma unroll
@@ -1186,6 +1188,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
     red[g][o] = sacc;
     __syncthreads();
     if (g == 0 && out < nout) {
+        static_assert(kWsumGroups == 4, "the round-4 combine order");
         const float v = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
         const int64_t nh = (int64_t)(A + 1) * (HID + 1);
         const int a = (int)(out / (HID + 1)), c = (int)(out - (int64_t)a * (HID + 1));
@@ -1679,8 +1682,8 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
     const int rc = L.A <= 18 ? by_prec(std::integral_constant<int, 18>{}) : by_prec(std::integral_constant<int, kAMax>{});
     if (rc) return rc;
     const int64_t nout = head_part_out(L);
-    hipLaunchKernelGGL(k_cnn_head_wsum, dim3((unsigned)((nout + 63) / 64 + 1)), dim3(256), 0, s, w.parts, (int)nb, L,
-                       G, w.loss_part, (int)B, la, metrics, stop);
+    hipLaunchKernelGGL(k_cnn_head_wsum, dim3((unsigned)((nout + kWsumOut - 1) / kWsumOut + 1)), dim3(256), 0, s,
+                       w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop);
     GS_LAUNCH_CHECK("k_cnn_head_wsum");
     return GS_OK;
 }

@@ -649,6 +649,16 @@ __global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ 
 // owns filters [16 w, 16 w + 16) with all their taps in registers; every wave walks every
 // position tile.  k-step group g = one (ky, kx) tap x 16 channels: lane quarter q takes
 // channels 4q .. 4q + 3 of the group, one ds_read_b128 feeding 4 MFMAs.
+// bf16-storage pitch (elements): the least >= lo, a multiple of 4, that sits npos position strides
+// (of CSH elements) away modulo the 32 banks
+constexpr int bf16_pitch(int lo, int npos, int CSH)
+{
+    int r = lo;
+    while (r % 4 != 0 || (r / 2) % 32 != (npos * CSH / 2) % 32) r += 2;
+    return r;
+}
+constexpr int round4(int v) { return (v + 3) / 4 * 4; }
+
 template <int H_, int W_, int C_, int K_, int S_, int SPB_>
 struct CN {
     static constexpr int H = H_, W = W_, C = C_, K = K_, S = S_, SPB = SPB_, CO = 64;
@@ -659,6 +669,20 @@ struct CN {
     static constexpr int M = SPB * OHW;                    // positions per workgroup
     static constexpr int MT = (M + 15) / 16;
     static_assert((S * CS) % 64 == 8 && C % 16 == 0, "padding / channel grouping");
+    // the bf16-storage tile (k_conv_fwd XH): the input split into S x S phase planes (plane
+    // (y % S, x % S) holds rows y / S, columns x / S), so output position (oy, ox) and tap (ky, kx)
+    // read plane (ky % S, kx % S) at row oy + ky / S, column ox + kx / S: consecutive output
+    // positions are one position stride apart in every plane.  With that stride 2 (mod 4) dwords
+    // (CSH = C + 4: 18 / 34 dwords) and a plane row OW strides further (mod 32 banks), the 8-B
+    // operand reads of 16 consecutive output positions start on 16 distinct even banks (the fp32
+    // layout's 36-dword stride put two positions on every bank pair: half the LDS cycles of the
+    // bf16 conv forwards were bank conflicts)
+    static constexpr int CSH = C + 4;
+    static constexpr int PW_ = (W + S - 1) / S, PH_ = (H + S - 1) / S;     // plane columns / rows
+    static constexpr int RPH = bf16_pitch(PW_ * CSH, OW, CSH);              // plane-row pitch
+    static constexpr int PLH = round4(PH_ * RPH);                           // plane pitch
+    static constexpr int SPH = bf16_pitch(S * S * PLH, OHW, CSH);           // sample pitch
+    static_assert((CSH / 2) % 4 == 2 && CSH % 4 == 0, "bf16 position stride");
 };
 
 constexpr int kConvFwdBurst = 16;      // float4 loads per thread per staging burst of k_conv_fwd
@@ -683,7 +707,16 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
     // stride CS stays in elements, so a position is S CS / 2 = 36 (mod 64) dwords from the next
     // and the 16 positions of an 8-B operand read land on distinct banks
     using XT = typename std::conditional<BF, uint16_t, float>::type;
-    constexpr int XS = G::SPB * G::H * G::W * G::CS;
+    // tile geometry (elements): position stride, row pitch, plane pitch, sample pitch; XD phase
+    // planes per axis (XH: the S x S split of CN::CSH, else one plane of the fp32 layout)
+    constexpr int XD = XH ? G::S : 1;
+    constexpr int PS = XH ? G::CSH : G::CS, RP = XH ? G::RPH : G::W * G::CS, PLP = XH ? G::PLH : 0;
+    constexpr int SP = XH ? G::SPH : G::H * RP;
+    constexpr int XS = G::SPB * SP;
+    auto poff = [](int pos) {      // staged offset of input position pos of the sample group
+        const int q = pos / (G::H * G::W), r = pos - q * (G::H * G::W), y = r / G::W, x = r - y * G::W;
+        return q * SP + ((y % XD) * XD + x % XD) * PLP + (y / XD) * RP + (x / XD) * PS;
+    };
     static_assert(FS == 1 || (FS - 1) * NFB * G::MT * 4 * 64 * 4 <= XS * (int)sizeof(XT),
                   "the k-range partials fit the staging tile");
     __shared__ __attribute__((aligned(16))) XT xs[XS];
@@ -725,7 +758,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
                     const int e = e0 + tid + 256 * j;
                     if (e < NE) {
                         const int pos = e / C4, c4 = e - pos * C4;
-                        *reinterpret_cast<uint2 *>(xs + pos * G::CS + 4 * c4) = v[j];
+                        *reinterpret_cast<uint2 *>(xs + poff(pos) + 4 * c4) = v[j];
                     }
                 }
             }
@@ -765,7 +798,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
         const int pc = p < G::M ? p : 0;
         const int q = pc / G::OHW, pos = pc - q * G::OHW;
         const int oy = pos / G::OW, ox = pos - oy * G::OW;
-        abase[t] = (q * G::H * G::W + oy * G::S * G::W + ox * G::S) * G::CS + 4 * lq;
+        abase[t] = q * SP + oy * (G::S / XD) * RP + ox * (G::S / XD) * PS + 4 * lq;
     }
     f32x4 acc[G::MT];
 #pragma unroll
@@ -774,7 +807,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
     auto goff = [&](int g) {       // LDS offset of k-step group g (one tap x 16 channels)
         const int tap = g / CG, cb = (g - tap * CG) * 16;
         const int ky = tap / G::K, kx = tap - ky * G::K;
-        return (ky * G::W + kx) * G::CS + cb;
+        return ((ky % XD) * XD + kx % XD) * PLP + (ky / XD) * RP + (kx / XD) * PS + cb;
     };
     if constexpr (BF) {
         // GS_HP_BF16: groups g, g + 1 as one 16x16x32 bf16 MFMA (element j < 4: channel 4q + j of
