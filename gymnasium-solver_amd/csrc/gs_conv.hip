@@ -703,9 +703,8 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
     constexpr int NGW = G::NG / FS;                // k-step groups per wave
     static_assert(G::NG % FS == 0 && (!BF || NGW % 2 == 0), "k-step groups split evenly (bf16: in pairs)");
     // BF (GS_HP_BF16): the tile is staged as bf16 (rounded once, at the store — the same value
-    // the fp32 tile gave at each operand read), half the LDS bytes and reads; the position
-    // stride CS stays in elements, so a position is S CS / 2 = 36 (mod 64) dwords from the next
-    // and the 16 positions of an 8-B operand read land on distinct banks
+    // the fp32 tile gave at each operand read), half the LDS bytes and reads; with bf16 storage
+    // (XH) in the phase-plane layout of CN::CSH, else in the fp32 layout's element strides
     using XT = typename std::conditional<BF, uint16_t, float>::type;
     // tile geometry (elements): position stride, row pitch, plane pitch, sample pitch; XD phase
     // planes per axis (XH: the S x S split of CN::CSH, else one plane of the fp32 layout)
@@ -904,6 +903,12 @@ struct CD {
     static constexpr int M = SPB * NY * NX;                   // positions per wave
     static constexpr int MT = (M + 15) / 16;
     static_assert(H % S == 0 && W % S == 0 && K % S == 0 && NTHR <= 512 && CW % 16 == 0, "shape");
+    // the bf16 tile (BF): position stride CSH = CO + 4 (34 dwords, 2 mod 4) and padded row / sample
+    // pitches, so the 8-B operand reads of 16 consecutive class positions start on 16 distinct even
+    // banks (CS's 36-dword stride put two on every bank pair)
+    static constexpr int CSH = CO + 4;
+    static constexpr int RPH = bf16_pitch(PW * CSH, NX, CSH);
+    static constexpr int SPH = bf16_pitch(PH * RPH, NY * NX, CSH);
 };
 
 // XH: the mask's activation stored as bf16, the filters read from the update's bf16 weight copy
@@ -911,10 +916,11 @@ template <class G, bool BF = false, bool XH = false>
 __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict__ dY, const act_t<XH> *__restrict__ act,
                                                     int R, const act_t<XH> *__restrict__ Wt, float *__restrict__ dX)
 {
-    // BF: dY staged as bf16 (rounded once at the store; CS = 72 elements = 36 dwords between
-    // positions: the 8-B operand reads of 16 positions stay on distinct banks)
+    // BF: dY staged as bf16 (rounded once at the store) in the CD::CSH / RPH / SPH layout
     using YT = typename std::conditional<BF, uint16_t, float>::type;
-    __shared__ __attribute__((aligned(16))) YT ys[G::SPB * G::PH * G::PW * G::CS];
+    // tile geometry (elements): position stride, row pitch, sample pitch
+    constexpr int PS = BF ? G::CSH : G::CS, RP = BF ? G::RPH : G::PW * G::CS, SP = BF ? G::SPH : G::PH * RP;
+    __shared__ __attribute__((aligned(16))) YT ys[G::SPB * SP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
     const int cls = wave / G::NNC, chunk = wave - cls * G::NNC;
@@ -962,7 +968,7 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
                     const int q = e / (G::PH * G::PW * C4);
                     const int rem = e - q * (G::PH * G::PW * C4);
                     const int pos = rem / C4, c4 = rem - pos * C4;
-                    YT *dst = ys + (q * G::PH * G::PW + pos) * G::CS + 4 * c4;
+                    YT *dst = ys + q * SP + (pos / G::PW) * RP + (pos % G::PW) * PS + 4 * c4;
                     if constexpr (BF) {
                         typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
                         bf16x4 h;
@@ -984,7 +990,7 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
         const int pc = p < G::M ? p : 0;
         const int q = pc / (G::NY * G::NX), rem = pc - q * (G::NY * G::NX);
         const int yy = rem / G::NX, xx = rem - yy * G::NX;
-        abase[t] = (q * G::PH * G::PW + (yy + G::PAD) * G::PW + xx + G::PAD) * G::CS + 4 * lq;
+        abase[t] = q * SP + (yy + G::PAD) * RP + (xx + G::PAD) * PS + 4 * lq;
     }
     f32x4 acc[G::MT][G::NT];
 #pragma unroll
@@ -997,7 +1003,7 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
         auto goff = [&](int g) {
             const int tap = g / (G::CO / 16), cb = (g - tap * (G::CO / 16)) * 16;
             const int dky = tap / G::KT, dkx = tap - dky * G::KT;
-            return -(dky * G::PW + dkx) * G::CS + cb;
+            return -(dky * RP + dkx * PS) + cb;
         };
 #pragma unroll
         for (int gp = 0; gp < G::NGRP / 2; ++gp) {
@@ -1020,7 +1026,7 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
     for (int g = 0; g < G::NGRP; ++g) {
         const int tap = g / (G::CO / 16), cb = (g - tap * (G::CO / 16)) * 16;
         const int dky = tap / G::KT, dkx = tap - dky * G::KT;
-        const int off = -(dky * G::PW + dkx) * G::CS + cb;
+        const int off = -(dky * RP + dkx * PS) + cb;
         const float *yf = reinterpret_cast<const float *>(ys);
 #pragma unroll
         for (int t = 0; t < G::MT; ++t) {
