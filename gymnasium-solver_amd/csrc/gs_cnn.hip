@@ -899,11 +899,15 @@ __device__ __forceinline__ float bf16r(float x) { return (float)(__bf16)x; }
 // 4 (mod 64) banks x a multiple of 4 keeps 16 consecutive rows on distinct banks)
 __host__ __device__ constexpr int head_zs(int A1) { return (A1 + 3) & ~3; }
 
+// the z partials' slice pitch: kHeadRows rows of ZS plus 4 floats, so the float4 stores of 16
+// consecutive slices fall on distinct bank quads (a pitch of 16 (mod 32) dwords put 8 on each)
+__host__ __device__ constexpr int head_qs(int ZS) { return kHeadRows * ZS + 4 * (((kHeadRows * ZS / 4) & 1) ^ 1); }
+
 size_t head_loss_lds(const CnnLayout &L)
 {
     const int ZS = head_zs(L.A + 1);
     return sizeof(float) * ((size_t)kHeadRows * (L.HID + kHeadSlices) + (size_t)L.HID * ZS +
-                            (size_t)kHeadSlices * kHeadRows * ZS + (size_t)kHeadRows * ZS);
+                            (size_t)kHeadSlices * head_qs(ZS) + (size_t)kHeadRows * ZS);
 }
 
 
@@ -925,9 +929,10 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     const int tid = threadIdx.x, A = L.A, A1 = A + 1, HID = L.HID, HS = HID + kHeadSlices, ZS = head_zs(A1);
     const int r0 = blockIdx.x * kHeadRows;
     float *hs = lds;                                  // [kHeadRows][HS] (kHeadSlices banks between rows)
+    const int QS = head_qs(ZS);
     float *wt = hs + kHeadRows * HS;                  // [HID][ZS]: Wh transposed (policy rows, then value)
-    float *zp = wt + HID * ZS;                        // [kHeadSlices][kHeadRows][ZS]
-    float *zs = zp + kHeadSlices * kHeadRows * ZS;    // [kHeadRows][ZS]: z, then dz
+    float *zp = wt + HID * ZS;                        // [kHeadSlices][QS]: [kHeadRows][ZS] + pad
+    float *zs = zp + kHeadSlices * QS;                // [kHeadRows][ZS]: z, then dz
     // staging: one burst of clamped, unconditional loads (h rows and Wp as float4, the value row,
     // the minibatch's advantages for the normalisation and this workgroup's rows' fields, both
     // through the sampler indices), then the LDS stores (Wh transposed).  head_fused() keeps the
@@ -965,7 +970,10 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
             th[j] = *reinterpret_cast<const float4 *>(h + (int64_t)min(r0 + r, B - 1) * HID + 4 * c4);
         }
 #pragma unroll
-        for (int j = 0; j < NW; ++j) tw[j] = wp4[min(tid + 256 * j, np4 - 1)];
+        for (int j = 0; j < NW; ++j) {
+            const int u = min(tid + 256 * j, np4 - 1);
+            tw[j] = wp4[(u % A) * H4 + u / A];
+        }
 #pragma unroll
         for (int j = 0; j < NV; ++j) tv[j] = P[L.oWv + min(tid + 256 * j, HID - 1)];
         if (!pre) {
@@ -987,7 +995,10 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
         for (int j = 0; j < NW; ++j) {
             const int u = tid + 256 * j;
             if (u < np4) {
-                const int a = (4 * u) / HID, c = 4 * u - a * HID;     // 4 consecutive columns of row a
+                // load u took row a = u % A, columns 4 (u / A) .. + 3: consecutive lanes store
+                // consecutive a (round 5: lanes along the columns stored 4 ZS dwords apart, 32-way
+                // bank conflicts on the transposed tile)
+                const int a = u % A, c = 4 * (u / A);
                 wt[(c + 0) * ZS + a] = tw[j].x;
                 wt[(c + 1) * ZS + a] = tw[j].y;
                 wt[(c + 2) * ZS + a] = tw[j].z;
@@ -1036,7 +1047,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 #pragma unroll
         for (int c = 0; c < NZ; ++c)
             if (4 * c < ZS)
-                *reinterpret_cast<float4 *>(zp + (q * kHeadRows + r) * ZS + 4 * c) =
+                *reinterpret_cast<float4 *>(zp + q * QS + r * ZS + 4 * c) =
                     make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
     }
     __syncthreads();
@@ -1044,7 +1055,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     for (int o = tid; o < kHeadRows * A1; o += 256) {
         const int r = o / A1, a = o - r * A1;
         float z = 0.f;
-        for (int q = 0; q < kHeadSlices; ++q) z += zp[(q * kHeadRows + r) * ZS + a];
+        for (int q = 0; q < kHeadSlices; ++q) z += zp[q * QS + r * ZS + a];
         zs[r * ZS + a] = z + (a < A ? P[L.obp + a] : P[L.obv]);
     }
     __syncthreads();
@@ -1892,6 +1903,13 @@ extern "C" size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows)
 {
     if (check_cnn(dims) || rows < 1) return 0;
     return carve(nullptr, CnnLayout::make(dims), rows).bytes;
+}
+
+extern "C" int64_t gs_cnn_workspace_hidden_offset(gs_cnn_dims dims, int64_t rows)
+{
+    if (check_cnn(dims) || rows < 1) return -1;
+    char *base = reinterpret_cast<char *>((uintptr_t)4096);     // never dereferenced: offsets only
+    return (int64_t)(reinterpret_cast<char *>(carve(base, CnnLayout::make(dims), rows).h) - base);
 }
 
 #ifdef GS_STAMPS

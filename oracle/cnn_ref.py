@@ -94,8 +94,13 @@ class _Bf16Linear(torch.autograd.Function):
         return dx, dw, gy.sum(0), None
 
 
-def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False):
+def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False, fc_mask=None):
     """-> (masked logits (B,A) with -inf for invalid actions, value (B,), hidden (B,512)).
+
+    fc_mask: (B, 512) bool, the fc layer's ReLU decisions taken as given (h = u * mask) instead of
+    u > 0 — the device's own decisions, for a teacher-forced comparison where a pre-activation
+    within rounding of zero has its sign decided by the summation order (see fc_preact); None:
+    plain ReLU.
 
     bf16=True: the device's GS_HP_BF16 mode (SURVEY.md Appendix A "Precision modes") — every
     convolution product, the fc layer's three products and the heads' forward / weight gradient
@@ -109,7 +114,11 @@ def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False):
     for i, s in enumerate(spec["strides"]):
         x = F.relu(conv(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], s))
     x = x.flatten(1)
-    h = F.relu(lin(x, params["mlp.0.weight"], params["mlp.0.bias"], ("fwd", "dx", "dw")))
+    u = lin(x, params["mlp.0.weight"], params["mlp.0.bias"], ("fwd", "dx", "dw"))
+    if fc_mask is not None:
+        h = u * torch.as_tensor(np.asarray(fc_mask, bool)).to(u.dtype)
+    else:
+        h = F.relu(u)
     logits = lin(h, params["policy_head.weight"], params["policy_head.bias"], ("fwd", "dw"))
     if valid is not None:
         mask = torch.ones_like(logits, dtype=torch.bool)
@@ -133,8 +142,25 @@ def dist_terms(logits, actions, valid):
     return lp, ent
 
 
+def fc_preact(flat, shapes, obs_u8, spec=NATURE):
+    """(u, mag): the fc layer's fp32 pre-activations u = a3 Wf^T + bf as forward computes them, and
+    the float64 sums of its terms' magnitudes |a3| |Wf|^T + |bf| (a ReLU decision with |u| far
+    below ~1e-6 mag is decided by the summation order)."""
+    params = unflatten(flat, shapes)
+    with torch.no_grad():
+        x = torch.as_tensor(obs_u8)
+        x = x.to(torch.float32) / 255.0
+        for i, st in enumerate(spec["strides"]):
+            x = F.relu(F.conv2d(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], stride=st))
+        x = x.flatten(1)
+        w, b = params["mlp.0.weight"], params["mlp.0.bias"]
+        u = F.linear(x, w, b)
+        mag = x.to(torch.float64).abs() @ w.to(torch.float64).abs().T + b.to(torch.float64).abs()
+    return u.numpy(), mag.numpy()
+
+
 def loss_and_grads(flat, shapes, obs_u8, actions, old_logp, old_values, adv, ret, *, valid, clip, clip_vf,
-                   vf_coef, ent_coef, normalize="batch", bf16=False):
+                   vf_coef, ent_coef, normalize="batch", bf16=False, fc_mask=None):
     """(loss, metrics, flat grads, logits, values) of losses_for_batch + backward (bf16: see forward)."""
     params = {k: v.clone().requires_grad_(True) for k, v in unflatten(flat, shapes).items()}
     adv = torch.as_tensor(np.asarray(adv, np.float32))
@@ -148,7 +174,7 @@ def loss_and_grads(flat, shapes, obs_u8, actions, old_logp, old_values, adv, ret
         metrics["roll/adv/norm/std"] = float(adv_n.std())
     else:
         adv_n = adv
-    logits, value, _ = forward(params, obs_u8, valid, bf16=bf16)
+    logits, value, _ = forward(params, obs_u8, valid, bf16=bf16, fc_mask=fc_mask)
     new_lp, H = dist_terms(logits, actions, valid)
     ratio = torch.exp(new_lp - old_logp)
     pl = -torch.min(adv_n * ratio, adv_n * torch.clamp(ratio, 1.0 - clip, 1.0 + clip)).mean()
