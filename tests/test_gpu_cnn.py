@@ -315,9 +315,12 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
       norms 1e-4 relative, the new parameters within 2e-6 except where Adam's sign-like step on a
       noise-level gradient moves a weight (at most 1e-4 of the weights, never more than 2 lr), and
       within 2e-5 relative L2; the step's clipped gradient within 1e-3 relative L2 (measured 2.1e-4
-      at step 0 on the GPU), all but 0.2 % of its entries within 2e-5 x max|g| (ReLU decisions of
-      near-zero conv pre-activations flip with the summation order at B = 1024) and every entry
-      within 1e-3 x max|g|.  An fc unit whose pre-activation is within rounding of zero has its
+      at step 0 on the GPU) and every entry within 1e-3 x max|g|; the share of entries off by
+      more than 2e-5 x max|g| at most 0.2 % in the median step and 1 % in the worst (ReLU
+      decisions of near-zero conv pre-activations flip with the summation order at B = 1024 and
+      move the entries those units feed: 3.3 K of 1.69 M at one step of a round-5 run, so a
+      per-step 0.2 % bar sat at the edge of the state's luck while an arithmetic error moves every
+      step).  An fc unit whose pre-activation is within rounding of zero has its
       ReLU decided by the summation order, and a flip there moves a whole 3136-entry row of dWf by
       up to 1e-3 x max|g| (round 5: a rounding-level change in the head kernel flipped one at step
       6), so the oracle takes the device's fc decisions (h > 0 of the step, read from the
@@ -453,7 +456,8 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
         dg = np.abs(g_dev.astype(np.float64) - gc)
         worst["g_off"] = max(worst.get("g_off", 0), int((dg > 2e-5 * gm).sum()))
         worst["g_rel"] = max(worst.get("g_rel", 0.0), rl(g_dev, gc))
-        need((dg > 2e-5 * gm).sum() <= 2e-3 * dg.size and dg.max() <= 1e-3 * gm,
+        worst.setdefault("g_off_share", []).append(float((dg > 2e-5 * gm).mean()))
+        need((dg > 2e-5 * gm).sum() <= 1e-2 * dg.size and dg.max() <= 1e-3 * gm,
              ("grad entries", k, int((dg > 2e-5 * gm).sum()), float(dg.max() / gm)))
         need(rl(g_dev, gc) < 1e-3, ("grad rel L2", k, rl(g_dev, gc)))
         comp = {"cnn": 0.0, "mlp": 0.0, "policy_head": 0.0, "value_head": 0.0}
@@ -477,6 +481,8 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
         need(rl(p_dev, p1) < 2e-5, ("params rel L2", k, rl(p_dev, p1)))
     print(f"{prec} teacher-forced: {worst}")
     assert not fails, fails
+    if prec == "fp32":
+        assert np.median(worst["g_off_share"]) <= 2e-3, worst["g_off_share"]
     if prec == "bf16":
         # each step's clipped gradient within 2e-2 of the emulation's and under half its distance
         # to the fp32 oracle's (test_cnn_bf16_update_step_vs_bf16_oracle's bars)
