@@ -66,6 +66,15 @@ struct C1 {
     }
 };
 
+// frame_src (below) from an index value already loaded (iv < 0: no sampler, row r itself);
+// 32-bit division (sampler indices are int32)
+__device__ __forceinline__ int64_t frame_src_of(int64_t iv, int64_t r, int64_t T, int64_t N)
+{
+    if (iv < 0) return r;
+    const int32_t i = (int32_t)iv, env = i / (int32_t)T, t = i - env * (int32_t)T;
+    return (int64_t)t * N + env;
+}
+
 __device__ __forceinline__ int64_t frame_src(const int32_t *idx, int64_t r, int64_t T, int64_t N)
 {
     if (!idx) return r;
@@ -338,11 +347,15 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
 
     uint32_t fv[PF];
     float4 dv[PD];
+    const int n_units = R * NU;
+    int32_t ixn = idx ? idx[min((int)blockIdx.x, n_units - 1) / NU] : 0;   // as k_conv1_wgrad_bf
     auto rows_of = [&](int unit) { return min(UR, G::OH - (unit % NU) * UR); };
     auto load = [&](int unit) {
         const int r = unit / NU, oy0 = (unit % NU) * UR;
         const int P = rows_of(unit) * G::OW;
-        const uint8_t *base = obs + frame_src(idx, r, T, N) * (int64_t)(G::C * G::H * G::W);
+        const int64_t fsrc = frame_src_of(idx ? (int64_t)ixn : -1, r, T, N);
+        if (idx) ixn = idx[min(unit + (int)gridDim.x, n_units - 1) / NU];
+        const uint8_t *base = obs + fsrc * (int64_t)(G::C * G::H * G::W);
         const int y0 = oy0 * G::S;
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
@@ -384,7 +397,6 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
         }
     };
 
-    const int n_units = R * NU;
     int unit = blockIdx.x;
     if (unit < n_units) {
         load(unit);
@@ -498,10 +510,17 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
 
     uint32_t fv[D][PF];
     float4 dv[D][PD];
+    const int n_units = R * NU;
+    // the sampler index of the next unit to load, loaded one load issue ahead and before that
+    // issue's tile loads: the index -> frame address chain had put a memory latency in front of
+    // every unit's loads
+    int32_t ixn = idx ? idx[min((int)blockIdx.x, n_units - 1) / NU] : 0;
     auto load = [&](auto sc, int unit) {
         constexpr int S = decltype(sc)::value;
         const int r = unit / NU, oy0 = (unit % NU) * UR;
-        const uint8_t *base = obs + frame_src(idx, r, T, N) * (int64_t)(G::C * G::H * G::W);
+        const int64_t fsrc = frame_src_of(idx ? (int64_t)ixn : -1, r, T, N);
+        if (idx) ixn = idx[min(unit + (int)gridDim.x, n_units - 1) / NU];
+        const uint8_t *base = obs + fsrc * (int64_t)(G::C * G::H * G::W);
         const int y0 = oy0 * G::S;
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
@@ -554,7 +573,6 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
         }
     };
 
-    const int n_units = R * NU;
     auto U = [&](int it) { return (int)blockIdx.x + it * (int)gridDim.x; };     // this workgroup's it-th unit
     using I0 = std::integral_constant<int, 0>;
     // units 0 .. D-1 in flight, unit 0 stored; then unit D into its set
