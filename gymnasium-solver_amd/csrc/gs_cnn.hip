@@ -183,7 +183,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     {
         const int64_t wparts = std::max({(int64_t)kSplitW1 * L.c1 * L.K1, (int64_t)kSplitW2 * L.c2 * (L.K2 + 1),
                                          (int64_t)kSplitW3 * L.c3 * (L.K3 + 1),
-                                         (int64_t)kConv1WgradWG * (L.c1 * L.K1 + L.c1),
+                                         (int64_t)std::max(kConv1WgradWG, kConv1WgradBfWG) * (L.c1 * L.K1 + L.c1),
                                          (int64_t)kConvWgradWG * 64 * (std::max(L.K2, L.K3) + 1)});
         const int64_t cparts = (int64_t)kColParts * std::max(std::max(L.HID, L.c3), L.A + 1);
         const int64_t gparts = std::max({(int64_t)splits_for(R, L.HID, L.F) * R * L.HID,
@@ -1910,6 +1910,15 @@ extern "C" int64_t gs_cnn_workspace_hidden_offset(gs_cnn_dims dims, int64_t rows
     if (check_cnn(dims) || rows < 1) return -1;
     char *base = reinterpret_cast<char *>((uintptr_t)4096);     // never dereferenced: offsets only
     return (int64_t)(reinterpret_cast<char *>(carve(base, CnnLayout::make(dims), rows).h) - base);
+}
+
+extern "C" int64_t gs_cnn_workspace_act_offset(gs_cnn_dims dims, int64_t rows, int layer)
+{
+    if (check_cnn(dims) || rows < 1 || layer < 1 || layer > 4) return -1;
+    char *base = reinterpret_cast<char *>((uintptr_t)4096);     // never dereferenced: offsets only
+    const CnnWs w = carve(base, CnnLayout::make(dims), rows);
+    const float *a = layer == 1 ? w.a1 : layer == 2 ? w.a2 : layer == 3 ? w.a3 : w.h;
+    return (int64_t)(reinterpret_cast<const char *>(a) - base);
 }
 
 #ifdef GS_STAMPS

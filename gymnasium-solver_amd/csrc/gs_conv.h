@@ -5,7 +5,19 @@
 
 namespace gs {
 
-constexpr int kConv1WgradWG = 256;     // workgroups (= partials) of the conv1 weight gradient
+#ifndef GS_C1WGF_BUFS
+#define GS_C1WGF_BUFS 1
+#endif
+constexpr int kConv1WgradF32Bufs = GS_C1WGF_BUFS;              // LDS tile buffers of the fp32 form
+constexpr int kConv1WgradWG = kConv1WgradF32Bufs == 1 ? 512 : 256;   // its workgroups (= partials)
+#ifndef GS_C1WG_BUFS
+#define GS_C1WG_BUFS 1
+#endif
+constexpr int kConv1WgradBfBufs = GS_C1WG_BUFS;                // LDS tile buffers of the bf16 form
+#ifndef GS_C1WG_WGS
+#define GS_C1WG_WGS (GS_C1WG_BUFS == 1 ? 512 : 256)
+#endif
+constexpr int kConv1WgradBfWG = GS_C1WG_WGS;                   // its workgroups (= partials)
 constexpr int kConvWgradWG = 256;      // workgroups (= partials) of the conv2 / conv3 weight gradients
 
 bool conv1_lds_supported(int C, int H, int W);

@@ -26,6 +26,33 @@
 #include "gs_gemm.h"
 
 namespace gs {
+
+#ifdef GS_STAMPS
+// diagnostic (GS_STAMPS builds only): per-phase cycles of k_conv1_wgrad_bf's unit loop, thread 0
+// of workgroup 0, summed over its units; read by gs_debug_conv_stamps (tools/cnn_stamp_run.py)
+__device__ unsigned long long g_conv_stamp_acc[8];
+__device__ unsigned long long g_conv_stamp_cnt[1];
+#define C1S_DECL                                                                   \
+    unsigned long long c1s_t = 0, c1s_acc[6] = {0, 0, 0, 0, 0, 0};                \
+    const bool c1s_on = threadIdx.x == 0 && blockIdx.x == 0;                        \
+    if (c1s_on) c1s_t = __builtin_amdgcn_s_memtime();
+#define C1S_MARK(i)                                                                \
+    if (c1s_on) {                                                                  \
+        const unsigned long long c1s_n = __builtin_amdgcn_s_memtime();             \
+        c1s_acc[i] += c1s_n - c1s_t;                                               \
+        c1s_t = c1s_n;                                                             \
+    }
+#define C1S_END                                                                    \
+    if (c1s_on) {                                                                  \
+        for (int j = 0; j < 6; ++j) atomicAdd(&g_conv_stamp_acc[j], c1s_acc[j]);   \
+        atomicAdd(&g_conv_stamp_cnt[0], 1ull);                                     \
+    }
+#else
+#define C1S_DECL
+#define C1S_MARK(i)
+#define C1S_END
+#endif
+
 namespace {
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c)
@@ -310,8 +337,9 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
 // A unit is 5 output rows of one sample (4 per sample at 84 x 84): its 24-row frame band
 // (fp32) and 100 x 32 dA rows fit twice in LDS, so the next unit's global loads (held in
 // registers) run under the current unit's MFMAs.  parts layout: [workgroup][CO * KK + CO]
-template <class G>
-__global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
+template <class G, int NBUF = 2>
+__global__ __launch_bounds__(256, NBUF == 1 ? 2 : 1) void k_conv1_wgrad(const uint8_t *__restrict__ obs,
+                                                                        const int32_t *__restrict__ idx,
                                                      int64_t T, int64_t N, int R, const float *__restrict__ dA,
                                                      float *__restrict__ parts)
 {
@@ -324,8 +352,8 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
     constexpr int NF = G::C * UIR * G::W4;              // u32 words of a frame band
     constexpr int NDA = UPP * (G::CO / 4);              // float4 of a dA unit
     constexpr int PF = (NF + 255) / 256, PD = (NDA + 255) / 256;
-    __shared__ __attribute__((aligned(16))) float fr[2][G::C * UIR * G::W];
-    __shared__ __attribute__((aligned(16))) float da[2][UPP * DS];
+    __shared__ __attribute__((aligned(16))) float fr[NBUF][G::C * UIR * G::W];
+    __shared__ __attribute__((aligned(16))) float da[NBUF][UPP * DS];
     __shared__ float dbred[8][G::CO];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
@@ -404,7 +432,7 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
     }
     __syncthreads();
     for (int it = 0; unit < n_units; ++it, unit += gridDim.x) {
-        const int buf = it & 1;
+        const int buf = NBUF == 2 ? (it & 1) : 0;
         const int next = unit + gridDim.x;
         if (next < n_units) load(next);                  // in flight during this unit's MFMAs
         const int P = rows_of(unit) * G::OW;
@@ -426,7 +454,8 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
                 acc[1][nt] = mfma(a1, bv[nt], acc[1][nt]);
             }
         }
-        if (next < n_units) store(buf ^ 1);
+        if (NBUF == 1) __syncthreads();                 // one buffer: every wave's operand reads done
+        if (next < n_units) store(NBUF == 2 ? buf ^ 1 : 0);
         __syncthreads();
     }
     // partial out: D row = lq * 4 + j (filter within the m-tile), col = li (tap within the n-tile)
@@ -458,8 +487,8 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t *__restrict__
 // Same parts layout as k_conv1_wgrad.  D units' loads in flight (register sets, unit i in set
 // i % D; the two LDS buffers as before): one workgroup per CU at one wave per SIMD, so the loads
 // of the next unit alone left each unit waiting out a memory latency.
-template <class G, int D = 1>
-__global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restrict__ obs,
+template <class G, int D = 1, int NBUF = 2>
+__global__ __launch_bounds__(256, NBUF == 1 ? 2 : 1) void k_conv1_wgrad_bf(const uint8_t *__restrict__ obs,
                                                         const int32_t *__restrict__ idx, int64_t T, int64_t N, int R,
                                                         const float *__restrict__ dA, float *__restrict__ parts)
 {
@@ -481,17 +510,18 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
     static_assert(4 * (XS - 1) + G::K - 1 >= G::W - 1, "sub-rows cover the row");
     static_assert(XS - 1 >= G::OW, "a sub-row's last element is a padding position");
     static_assert((DTS / 2) % 64 == 4 && (G::K * XS / 2) % 64 == 32 && (XS / 2) % 4 == 0, "bank layout");
-    __shared__ __attribute__((aligned(16))) __bf16 fb[2][FBN];
-    __shared__ __attribute__((aligned(16))) __bf16 dat[2][G::CO * DTS];
+    __shared__ __attribute__((aligned(16))) __bf16 fb[NBUF][FBN];
+    __shared__ __attribute__((aligned(16))) __bf16 dat[NBUF][G::CO * DTS];
     __shared__ float4 dbred[256];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lq = lane >> 4;
+    C1S_DECL
     // zero both buffers once: sub-row elements past the row and padding slots are never written
     {
-        constexpr int Z = (2 * FBN + 2 * G::CO * DTS) * 2 / 16;
+        constexpr int Z = (NBUF * FBN + NBUF * G::CO * DTS) * 2 / 16;
         uint4 *z0 = reinterpret_cast<uint4 *>(&fb[0][0]);
         uint4 *z1 = reinterpret_cast<uint4 *>(&dat[0][0]);
-        constexpr int ZF = 2 * FBN * 2 / 16;
+        constexpr int ZF = NBUF * FBN * 2 / 16;
         for (int i = tid; i < Z; i += 256) {
             if (i < ZF) z0[i] = make_uint4(0u, 0u, 0u, 0u);
             else z1[i - ZF] = make_uint4(0u, 0u, 0u, 0u);
@@ -584,12 +614,13 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
     if (U(0) < n_units) store(I0{}, 0);
     __syncthreads();
     if (U(D) < n_units) load(I0{}, U(D));
+    C1S_MARK(4)                                         // prologue: first unit staged
     for (int it0 = 0; U(it0) < n_units; it0 += D) {
       static_for<0, D>([&](auto uc) -> bool {
         constexpr int u = decltype(uc)::value;
         const int it = it0 + u;
         if (U(it) >= n_units) return false;
-        const int buf = it & 1;
+        const int buf = NBUF == 2 ? (it & 1) : 0;
 #pragma unroll
         for (int m = 0; m < NBLK; ++m) {
             const int gi = 4 * m + lq;
@@ -606,10 +637,15 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
                 acc[1][nt] = mfma16_bf16(a1, bv[nt], acc[1][nt]);
             }
         }
+        C1S_MARK(0)                                     // MFMAs (LDS operand reads)
         constexpr int nv = (u + 1) % D;                 // the set holding unit it + 1
-        if (U(it + 1) < n_units) store(std::integral_constant<int, nv>{}, buf ^ 1);
+        if (NBUF == 1) __syncthreads();                 // one buffer: every wave's operand reads done
+        if (U(it + 1) < n_units) store(std::integral_constant<int, nv>{}, NBUF == 2 ? buf ^ 1 : 0);
+        C1S_MARK(1)                                     // next unit's tiles landed + LDS stores
         __syncthreads();
+        C1S_MARK(2)                                     // barrier
         if (U(it + 1 + D) < n_units) load(std::integral_constant<int, nv>{}, U(it + 1 + D));
+        C1S_MARK(3)                                     // load issue
         return true;
       });
     }
@@ -634,6 +670,8 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_bf(const uint8_t *__restric
         }
         o[G::CO * G::KK + tid] = t;
     }
+    C1S_MARK(5)                                         // partial out
+    C1S_END
 }
 
 // out[i] = sum over partials p of parts[p * stride + i] in order p = 0, 1, ... (four
@@ -1306,7 +1344,7 @@ int conv1_lds_fwd(hipStream_t s, bool bf, bool xh, int R, const uint8_t *obs, co
     return GS_OK;
 }
 
-int conv1_lds_wgrad_parts() { return kConv1WgradWG; }
+int conv1_lds_wgrad_parts() { return std::max(kConv1WgradWG, kConv1WgradBfWG); }
 
 int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
                     const float *dA, float *parts, float *dW1, float *db1)
@@ -1314,19 +1352,18 @@ int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int
     GS_REQUIRE(R > 0 && obs && dA && parts && dW1 && db1, "conv1_lds_wgrad: bad argument");
     constexpr int n = C1_84::CO * C1_84::KK, stride = n + C1_84::CO;
     if (bf)
-        hipLaunchKernelGGL((k_conv1_wgrad_bf<C1_84, kConv1WgradDepth>), dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T,
-                           N, R, dA, parts);
+        hipLaunchKernelGGL((k_conv1_wgrad_bf<C1_84, kConv1WgradDepth, kConv1WgradBfBufs>), dim3(kConv1WgradBfWG), dim3(256),
+                           0, s, obs, idx, T, N, R, dA, parts);
     else
-        hipLaunchKernelGGL(k_conv1_wgrad<C1_84>, dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T, N, R, dA, parts);
+        hipLaunchKernelGGL((k_conv1_wgrad<C1_84, kConv1WgradF32Bufs>), dim3(kConv1WgradWG), dim3(256), 0, s, obs, idx, T,
+                           N, R, dA, parts);
     GS_LAUNCH_CHECK("k_conv1_wgrad");
+    const int np = bf ? kConv1WgradBfWG : kConv1WgradWG;
     if (db1 == dW1 + n) {      // the flat layout keeps conv1's bias right after its weight: one sum
-        hipLaunchKernelGGL(k_sum_partials, dim3((stride + 63) / 64), dim3(256), 0, s, parts, kConv1WgradWG,
-                           (int64_t)stride, stride, dW1);
+        return sum_parts4(s, parts, np, stride, stride, dW1);
     } else {
-        hipLaunchKernelGGL(k_sum_partials, dim3((n + 63) / 64), dim3(256), 0, s, parts, kConv1WgradWG,
-                           (int64_t)stride, n, dW1);
-        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, parts + n, kConv1WgradWG, (int64_t)stride,
-                           C1_84::CO, db1);
+        hipLaunchKernelGGL(k_sum_partials, dim3((n + 63) / 64), dim3(256), 0, s, parts, np, (int64_t)stride, n, dW1);
+        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, parts + n, np, (int64_t)stride, C1_84::CO, db1);
     }
     GS_LAUNCH_CHECK("k_sum_partials");
     return GS_OK;
@@ -1433,3 +1470,12 @@ int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const vo
 }
 
 }  // namespace gs
+
+#ifdef GS_STAMPS
+extern "C" int gs_debug_conv_stamps(unsigned long long *acc_out, unsigned long long *cnt_out)
+{
+    GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(gs::g_conv_stamp_acc), sizeof(unsigned long long) * 8));
+    GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(gs::g_conv_stamp_cnt), sizeof(unsigned long long)));
+    return GS_OK;
+}
+#endif

@@ -78,6 +78,9 @@ int conv_wgrad_nhwc(hipStream_t s, bool bf16, const ConvGeom &g, const float *in
 // over split z of K; then sum_parts_wb scatters column N of each row into db
 int gemm_wgrad_bias(hipStream_t s, bool bf16, int64_t M, int64_t N, int64_t K, const float *dY, int64_t lddy, const float *X,
                     int64_t ldx, float *parts, int splits);
+// out[i] = sum over p of parts[p pstride + i] (float4 loads; np >= 64, n and pstride multiples of 4,
+// parts 16-B aligned)
+int sum_parts4(hipStream_t s, const float *parts, int np, int64_t pstride, int64_t n, float *out);
 int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int rows, int ncols, float *dW,
                  float *db);
 // out[i] = (bias/relu epilogue of) sum_{p < np} parts[p*n + i], fixed order; C = row length

@@ -113,6 +113,7 @@ def _load():
         "gs_cnn_param_count": (i64, [CnnDims]),
         "gs_cnn_workspace_bytes": (sz, [CnnDims, i64]),
         "gs_cnn_workspace_hidden_offset": (i64, [CnnDims, i64]),
+        "gs_cnn_workspace_act_offset": (i64, [CnnDims, i64, ctypes.c_int]),
         "gs_cnn_policy_act": (ctypes.c_int, [vp, CnnDims, vp, i64, ctypes.c_int, u64, u64, vp, vp, vp, vp, vp, vp, vp]),
         "gs_cnn_ppo_loss": (ctypes.c_int, [vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, vp, vp, vp, vp]),
         "gs_cnn_ppo_update": (ctypes.c_int, [vp, vp, vp, vp, CnnDims, PPOHparams, RolloutViewU8, vp, i64, i64, i64,
@@ -165,7 +166,7 @@ EXPORTED = ("gs_abi_version", "gs_last_error", "gs_build_source_hash", "gs_norma
             "gs_ppo_workspace_bytes", "gs_ppo_minibatch_step", "gs_ppo_loss", "gs_mlp_activation_stats", "gs_ppo_stage", "gs_ppo_update",
             "gs_ppo_update_global", "gs_ppo_update_workspace_bytes",
             "gs_ppo_graph_cache_info", "gs_ppo_exchange_inside_bwd",
-            "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_workspace_hidden_offset", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
+            "gs_cnn_param_count", "gs_cnn_workspace_bytes", "gs_cnn_workspace_hidden_offset", "gs_cnn_workspace_act_offset", "gs_cnn_policy_act", "gs_cnn_ppo_loss", "gs_cnn_ppo_update",
             "gs_cnn_ppo_update_global",
             "gs_gemm_f32", "gs_fc_gemm", "gs_cartpole_reset", "gs_cartpole_step", "gs_atari_preprocess", "gs_atari_render", "gs_atari_env_reset", "gs_atari_env_step", "gs_comm_unique_id",
             "gs_comm_init", "gs_comm_xgmi_create", "gs_comm_xgmi_connect", "gs_comm_status", "gs_comm_error_record",

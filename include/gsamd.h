@@ -46,7 +46,8 @@ extern "C" {
  * gs_ppo_global_adv_stats, gs_ppo_global_records, gs_cnn_ppo_update_global, gs_fc_gemm and
  * gs_episode_window; version 5 added the obs_store argument of gs_cnn_policy_act; version 6 added
  * gs_normalize_advantages(_scratch_bytes), gs_cnn_activation_stats, gs_build_source_hash,
- * gs_comm_xgmi_reset, gs_cnn_workspace_hidden_offset and the parts argument of gs_fc_gemm). */
+ * gs_comm_xgmi_reset, gs_cnn_workspace_hidden_offset / _act_offset and the parts argument of
+ * gs_fc_gemm). */
 #define GS_ABI_VERSION 6
 int gs_abi_version(void);
 const char *gs_last_error(void);
@@ -379,6 +380,10 @@ size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows);
  * (after relu): after gs_cnn_ppo_update / _global it holds the last minibatch step's values (the
  * device's fc ReLU decisions, which a teacher-forced comparison takes over); -1 on a bad shape. */
 int64_t gs_cnn_workspace_hidden_offset(gs_cnn_dims dims, int64_t rows);
+/* The same for the convolution activations: layer 1, 2, 3 -> a1, a2, a3 (NHWC, fp32 in the fp32
+ * update: the device's conv ReLU decisions of the last minibatch step), 4 -> the fc output as
+ * above; -1 on a bad shape or layer. */
+int64_t gs_cnn_workspace_act_offset(gs_cnn_dims dims, int64_t rows, int layer);
 /* policy_act on N frame stacks obs_dev (N, in_c, in_h, in_w): mode 0 sample / 1 argmax /
  * 2 replay (as gs_policy_act); masked actions are never drawn.  obs_store_dev (may be NULL): the
  * rollout buffer's obs row, receives a copy of obs_dev (written by the first convolution from the

@@ -94,13 +94,14 @@ class _Bf16Linear(torch.autograd.Function):
         return dx, dw, gy.sum(0), None
 
 
-def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False, fc_mask=None):
+def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False, fc_mask=None, conv_masks=None):
     """-> (masked logits (B,A) with -inf for invalid actions, value (B,), hidden (B,512)).
 
     fc_mask: (B, 512) bool, the fc layer's ReLU decisions taken as given (h = u * mask) instead of
     u > 0 — the device's own decisions, for a teacher-forced comparison where a pre-activation
     within rounding of zero has its sign decided by the summation order (see fc_preact); None:
-    plain ReLU.
+    plain ReLU.  conv_masks: the same for the three convolutions, (B, C, H, W) bool each (see
+    relu_decisions).
 
     bf16=True: the device's GS_HP_BF16 mode (SURVEY.md Appendix A "Precision modes") — every
     convolution product, the fc layer's three products and the heads' forward / weight gradient
@@ -112,7 +113,11 @@ def forward(params: dict, obs_u8, valid=None, spec=NATURE, bf16=False, fc_mask=N
     conv = (lambda x, w, b, s: _Bf16Conv.apply(x, w, b, s)) if bf16 else (lambda x, w, b, s: F.conv2d(x, w, b, stride=s))
     lin = (lambda x, w, b, r: _Bf16Linear.apply(x, w, b, r)) if bf16 else (lambda x, w, b, r: F.linear(x, w, b))
     for i, s in enumerate(spec["strides"]):
-        x = F.relu(conv(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], s))
+        u = conv(x, params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"], s)
+        if conv_masks is not None:
+            x = u * torch.as_tensor(np.asarray(conv_masks[i], bool)).to(u.dtype)
+        else:
+            x = F.relu(u)
     x = x.flatten(1)
     u = lin(x, params["mlp.0.weight"], params["mlp.0.bias"], ("fwd", "dx", "dw"))
     if fc_mask is not None:
@@ -159,8 +164,46 @@ def fc_preact(flat, shapes, obs_u8, spec=NATURE):
     return u.numpy(), mag.numpy()
 
 
+def relu_decisions(flat, shapes, obs_u8, masks, spec=NATURE):
+    """Teacher-forced ReLU decisions: masks = the device's (conv1, conv2, conv3 as (B, C, H, W) bool,
+    fc as (B, 512) bool).  Walks the fp32 forward with each layer's input built from the given
+    decisions of the layers before it, and returns per layer (n, rel): the number of units whose
+    given decision differs from the sign of the oracle's own fp32 pre-activation u, and the
+    largest |u| / mag over them, mag the float64 sum of the pre-activation's term magnitudes
+    (|x| |w| over the receptive field + |b|) — a decision with rel far below 1e-5 is one the
+    summation order decides (the fc layer: as fc_preact)."""
+    params = unflatten(flat, shapes)
+    out = []
+    with torch.no_grad():
+        x = torch.as_tensor(obs_u8).to(torch.float32) / 255.0
+        for i, st in enumerate(spec["strides"]):
+            w, b = params[f"cnn.{2 * i}.weight"], params[f"cnn.{2 * i}.bias"]
+            u = F.conv2d(x, w, b, stride=st)
+            m = torch.as_tensor(np.asarray(masks[i], bool))
+            diff = ((u > 0) != m).nonzero().tolist()
+            rel = 0.0
+            k = w.shape[-1]
+            for (r, c, y, xx) in diff:
+                patch = x[r, :, y * st:y * st + k, xx * st:xx * st + k].to(torch.float64).abs()
+                mag = float((patch * w[c].to(torch.float64).abs()).sum() + abs(float(b[c])))
+                rel = max(rel, abs(float(u[r, c, y, xx])) / max(mag, 1e-30))
+            out.append((len(diff), rel))
+            x = u * m.to(u.dtype)
+        x = x.flatten(1)
+        w, b = params["mlp.0.weight"], params["mlp.0.bias"]
+        u = F.linear(x, w, b)
+        m = torch.as_tensor(np.asarray(masks[3], bool))
+        diff = ((u > 0) != m).nonzero().tolist()
+        rel = 0.0
+        for (r, j) in diff:
+            mag = float((x[r].to(torch.float64).abs() * w[j].to(torch.float64).abs()).sum() + abs(float(b[j])))
+            rel = max(rel, abs(float(u[r, j])) / max(mag, 1e-30))
+        out.append((len(diff), rel))
+    return out
+
+
 def loss_and_grads(flat, shapes, obs_u8, actions, old_logp, old_values, adv, ret, *, valid, clip, clip_vf,
-                   vf_coef, ent_coef, normalize="batch", bf16=False, fc_mask=None):
+                   vf_coef, ent_coef, normalize="batch", bf16=False, fc_mask=None, conv_masks=None):
     """(loss, metrics, flat grads, logits, values) of losses_for_batch + backward (bf16: see forward)."""
     params = {k: v.clone().requires_grad_(True) for k, v in unflatten(flat, shapes).items()}
     adv = torch.as_tensor(np.asarray(adv, np.float32))
@@ -174,7 +217,7 @@ def loss_and_grads(flat, shapes, obs_u8, actions, old_logp, old_values, adv, ret
         metrics["roll/adv/norm/std"] = float(adv_n.std())
     else:
         adv_n = adv
-    logits, value, _ = forward(params, obs_u8, valid, bf16=bf16, fc_mask=fc_mask)
+    logits, value, _ = forward(params, obs_u8, valid, bf16=bf16, fc_mask=fc_mask, conv_masks=conv_masks)
     new_lp, H = dist_terms(logits, actions, valid)
     ratio = torch.exp(new_lp - old_logp)
     pl = -torch.min(adv_n * ratio, adv_n * torch.clamp(ratio, 1.0 - clip, 1.0 + clip)).mean()

@@ -34,9 +34,9 @@ PEAK_HBM = 8000.0         # GB/s
 SEQ_FC = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd", "k_conv_fwd"),
           ("fc_fwd", "k_fc"), ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
           ("fc_wgrad", "k_fc"), ("fc_dgrad_relu_mask", "k_fc"),
-          ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts_wb"),
-          ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts_wb"),
-          ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_partials"),
+          ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts"),
+          ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts"),
+          ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_parts"),
           ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
 # the fp32 update (round 5): the fc forward as two K halves + k_fc_sum (the bias + ReLU epilogue)
 SEQ_FC_SPLIT = SEQ_FC[:4] + [("fc_fwd_splitk_sum", "k_fc_sum")] + SEQ_FC[4:]
@@ -76,6 +76,8 @@ def short(name):
     m = re.search(r"\b(k_\w+)", name)
     if m and m.group(1) == "k_conv1_wgrad_bf":    # the bf16 conv1 weight gradient (same position)
         return "k_conv1_wgrad"
+    if m and m.group(1) in ("k_sum_parts_wb", "k_sum_partials", "k_sum_parts4"):   # the partial sums (scalar / float4)
+        return "k_sum_parts"
     if m and m.group(1) == "k_fc16":      # the fp32 fc kernels on 16x16x4 MFMA blocks (same positions)
         return "k_fc"
     return m.group(1) if m else None
