@@ -30,12 +30,15 @@ namespace gs {
 #ifdef GS_STAMPS
 // diagnostic (GS_STAMPS builds only): per-phase cycles of k_conv1_wgrad_bf's unit loop, thread 0
 // of workgroup 0, summed over its units; read by gs_debug_conv_stamps (tools/cnn_stamp_run.py)
-__device__ unsigned long long g_conv_stamp_acc[8];
-__device__ unsigned long long g_conv_stamp_cnt[1];
-#define C1S_DECL                                                                   \
+// slot sets: 0 k_conv1_wgrad_bf, 1 / 2 k_conv_wgrad conv2 / conv3 (per-sample loop)
+__device__ unsigned long long g_conv_stamp_acc[3][8];
+__device__ unsigned long long g_conv_stamp_cnt[3];
+#define C1S_DECL_K(k)                                                              \
     unsigned long long c1s_t = 0, c1s_acc[6] = {0, 0, 0, 0, 0, 0};                \
     const bool c1s_on = threadIdx.x == 0 && blockIdx.x == 0;                        \
+    const int c1s_k = (k);                                                         \
     if (c1s_on) c1s_t = __builtin_amdgcn_s_memtime();
+#define C1S_DECL C1S_DECL_K(0)
 #define C1S_MARK(i)                                                                \
     if (c1s_on) {                                                                  \
         const unsigned long long c1s_n = __builtin_amdgcn_s_memtime();             \
@@ -44,11 +47,12 @@ __device__ unsigned long long g_conv_stamp_cnt[1];
     }
 #define C1S_END                                                                    \
     if (c1s_on) {                                                                  \
-        for (int j = 0; j < 6; ++j) atomicAdd(&g_conv_stamp_acc[j], c1s_acc[j]);   \
-        atomicAdd(&g_conv_stamp_cnt[0], 1ull);                                     \
+        for (int j = 0; j < 6; ++j) atomicAdd(&g_conv_stamp_acc[c1s_k][j], c1s_acc[j]); \
+        atomicAdd(&g_conv_stamp_cnt[c1s_k], 1ull);                                 \
     }
 #else
 #define C1S_DECL
+#define C1S_DECL_K(k)
 #define C1S_MARK(i)
 #define C1S_END
 #endif
@@ -1157,9 +1161,12 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
 #pragma unroll
         for (int nt = 0; nt < X::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     float db = 0.f;
+    C1S_DECL_K(G::KK == 512 ? 1 : 2)
+    C1S_MARK(4)                                         // prologue
 
     for (int r = blockIdx.x; r < R; r += gridDim.x) {
         __syncthreads();
+        C1S_MARK(3)                                     // loop-top barrier
         {   // input activation [pos][c] with stride CSX, dY [pos][co] with stride DS (zero rows past OHW)
             // every load of the sample in one burst (one memory latency per sample; 8 per burst
             // took 2 - 3 round trips)
@@ -1207,7 +1214,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
                 }
             }
         }
+        C1S_MARK(1)                                     // staging burst landed + LDS stores
         __syncthreads();
+        C1S_MARK(2)                                     // barrier
         {   // bias partial: thread (co = tid % 64, group tid / 64) sums positions group, group + 4, ...
             const int co = tid & 63, grp = tid >> 6;
             for (int p = grp; p < G::OHW; p += 4) db += ds[p * X::DS + co];
@@ -1261,6 +1270,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
 #pragma unroll
                 for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = mfma(a[mt], bv[nt], acc[mt][nt]);
         }
+        C1S_MARK(0)                                     // bias partial + gathers + MFMAs
     }
     // partial: D row = lq * 4 + j (filter in the m-tile), col = li (patch column in the n-tile)
     float *o = parts + (int64_t)blockIdx.x * G::CO * (G::KK + 1);
@@ -1274,6 +1284,8 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
     dbred[tid >> 6][tid & 63] = db;
     __syncthreads();
     if (tid < G::CO) o[(int64_t)tid * (G::KK + 1) + G::KK] = (dbred[0][tid] + dbred[1][tid]) + (dbred[2][tid] + dbred[3][tid]);
+    C1S_MARK(5)                                         // partial out
+    C1S_END
 }
 
 using C2_84 = CN<20, 20, 32, 4, 2, 1>;    // conv2: 20x20x32 -> 9x9x64
@@ -1474,8 +1486,8 @@ int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const vo
 #ifdef GS_STAMPS
 extern "C" int gs_debug_conv_stamps(unsigned long long *acc_out, unsigned long long *cnt_out)
 {
-    GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(gs::g_conv_stamp_acc), sizeof(unsigned long long) * 8));
-    GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(gs::g_conv_stamp_cnt), sizeof(unsigned long long)));
+    GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(gs::g_conv_stamp_acc), sizeof(unsigned long long) * 24));
+    GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(gs::g_conv_stamp_cnt), sizeof(unsigned long long) * 3));
     return GS_OK;
 }
 #endif

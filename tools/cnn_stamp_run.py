@@ -72,16 +72,22 @@ def main():
     if a.bf16 and hasattr(lib, "gs_debug_conv_stamps"):
         # k_conv1_wgrad_bf's unit loop (csrc/gs_conv.hip C1S_MARK), workgroup 0, per launch
         lib.gs_debug_conv_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        c_acc, c_cnt = np.zeros(8, np.uint64), np.zeros(1, np.uint64)
+        c_acc, c_cnt = np.zeros(24, np.uint64), np.zeros(3, np.uint64)
         lib.gs_debug_conv_stamps(c_acc.ctypes.data, c_cnt.ctypes.data)
-        cn = max(float(c_cnt[0]), 1.0)
-        names = ["MFMAs (LDS operand reads)", "tiles landed + LDS stores", "barrier", "load issue",
-                 "prologue", "partial out"]
-        cper = c_acc[:6].astype(np.float64) / cn
-        print(f"k_conv1_wgrad_bf workgroup 0 over {int(cn)} launches (all launches of the process): "
-              f"{cper.sum():8.0f} cyc = {cper.sum() / 2.4e3:6.2f} us")
-        for nm, v in zip(names, cper):
-            print(f"    {nm:28s} {v:8.0f} cyc  {v / 2.4e3:6.2f} us")
+        c_acc = c_acc.reshape(3, 8)
+        sets = [("k_conv1_wgrad_bf", ["MFMAs (LDS operand reads)", "tiles landed + LDS stores", "barrier",
+                                      "load issue", "prologue", "partial out"]),
+                ("k_conv_wgrad conv2", ["bias + gathers + MFMAs", "staging burst + LDS stores", "barrier",
+                                        "loop-top barrier", "prologue", "partial out"]),
+                ("k_conv_wgrad conv3", ["bias + gathers + MFMAs", "staging burst + LDS stores", "barrier",
+                                        "loop-top barrier", "prologue", "partial out"])]
+        for k, (kn, names) in enumerate(sets):
+            cn = max(float(c_cnt[k]), 1.0)
+            cper = c_acc[k, :6].astype(np.float64) / cn
+            print(f"{kn} workgroup 0 over {int(cn)} launches (all launches of the process): "
+                  f"{cper.sum():8.0f} cyc = {cper.sum() / 2.4e3:6.2f} us")
+            for nm, v in zip(names, cper):
+                print(f"    {nm:28s} {v:8.0f} cyc  {v / 2.4e3:6.2f} us")
 
 
 if __name__ == "__main__":
