@@ -1272,18 +1272,21 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
         }
         C1S_MARK(0)                                     // bias partial + gathers + MFMAs
     }
-    // partial: D row = lq * 4 + j (filter in the m-tile), col = li (patch column in the n-tile)
+    // partial in MFMA tile order (k_sum_parts_tiles): accumulator (m-tile mt, n-tile g) of lane l at
+    // float4 (mt * NTG + g) * 64 + l — one 1-KB contiguous store per wave instruction (the
+    // [filter][column] rows had taken 144 scalar stores per thread in 64-B pieces: 4.5 us of a
+    // conv3 workgroup's 21); then the 64 db values
+    constexpr int NTG = 4 * X::NTW;                     // n-tiles of the patch columns
+    static_assert(16 * NTG == G::KK && G::CO == 64, "tile-order partial");
     float *o = parts + (int64_t)blockIdx.x * G::CO * (G::KK + 1);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < X::NTW; ++nt)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                o[(int64_t)(16 * mt + lq * 4 + j) * (G::KK + 1) + 16 * (wave * X::NTW + nt) + li] = acc[mt][nt][j];
+            reinterpret_cast<f32x4 *>(o)[(mt * NTG + wave * X::NTW + nt) * 64 + lane] = acc[mt][nt];
     dbred[tid >> 6][tid & 63] = db;
     __syncthreads();
-    if (tid < G::CO) o[(int64_t)tid * (G::KK + 1) + G::KK] = (dbred[0][tid] + dbred[1][tid]) + (dbred[2][tid] + dbred[3][tid]);
+    if (tid < G::CO) o[(int64_t)G::CO * G::KK + tid] = (dbred[0][tid] + dbred[1][tid]) + (dbred[2][tid] + dbred[3][tid]);
     C1S_MARK(5)                                         // partial out
     C1S_END
 }
@@ -1478,7 +1481,7 @@ int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const vo
         launch_conv_wgrad<C3_84>(s, bf, xh, nwg, R, in, dY, parts);
     }
     GS_LAUNCH_CHECK("k_conv_wgrad");
-    return sum_parts_wb(s, parts, nwg, (int64_t)64 * (KK + 1), 64, KK, dW, db);
+    return sum_parts_tiles(s, parts, nwg, (int64_t)64 * (KK + 1), KK, dW, db);
 }
 
 }  // namespace gs

@@ -81,6 +81,9 @@ int gemm_wgrad_bias(hipStream_t s, bool bf16, int64_t M, int64_t N, int64_t K, c
 // out[i] = sum over p of parts[p pstride + i] (float4 loads; np >= 64, n and pstride multiples of 4,
 // parts 16-B aligned)
 int sum_parts4(hipStream_t s, const float *parts, int np, int64_t pstride, int64_t n, float *out);
+// [dW | db] of 64-filter conv weight gradients from partials in MFMA tile order (k_conv_wgrad's
+// layout, gs_conv.hip): the sums of sum_parts_wb, scattered to dW [64][ncols] and db [64]
+int sum_parts_tiles(hipStream_t s, const float *parts, int np, int64_t pstride, int ncols, float *dW, float *db);
 int sum_parts_wb(hipStream_t s, const float *parts, int np, int64_t pstride, int rows, int ncols, float *dW,
                  float *db);
 // out[i] = (bias/relu epilogue of) sum_{p < np} parts[p*n + i], fixed order; C = row length

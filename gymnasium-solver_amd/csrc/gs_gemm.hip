@@ -420,6 +420,43 @@ __global__ __launch_bounds__(256) void k_sum_parts_wb(const float *__restrict__ 
     else db[co] = v;
 }
 
+// The conv2 / conv3 weight-gradient partials in MFMA tile order (k_conv_wgrad): per partial, the
+// 64 x ncols dW tile as float4 (mt * NTG + g) * 64 + lane holding rows 16 mt + 4 (lane / 16) + j,
+// column 16 g + lane % 16 (j = 0..3), then the 64 db values.  The same partial chains and tree as
+// k_sum_parts_wb (each output's sum bit-identical), the outputs scattered to dW [64][ncols] / db.
+__global__ __launch_bounds__(256) void k_sum_parts_tiles(const float *__restrict__ parts, int np, int64_t pstride,
+                                                         int ncols, float *__restrict__ dW, float *__restrict__ db)
+{
+    __shared__ float red[4][64];
+    const int jj = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + jj;
+    const int64_t n = (int64_t)64 * (ncols + 1);
+    float a = 0.f;
+    if (i < n) {
+        int p = g;
+        for (; p + 28 < np; p += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = parts[(int64_t)(p + 4 * u) * pstride + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; p < np; p += 4) a += parts[(int64_t)p * pstride + i];
+    }
+    red[g][jj] = a;
+    __syncthreads();
+    if (g != 0 || i >= n) return;
+    const float v = (red[0][jj] + red[1][jj]) + (red[2][jj] + red[3][jj]);
+    const int64_t nt = (int64_t)64 * ncols;
+    if (i >= nt) {
+        db[i - nt] = v;
+        return;
+    }
+    const int j = (int)(i & 3), lane = (int)((i >> 2) & 63);
+    const int q = (int)(i >> 8), ntg = ncols / 16, mt = q / ntg, gt = q - mt * ntg;
+    dW[(int64_t)(16 * mt + 4 * (lane >> 4) + j) * ncols + 16 * gt + (lane & 15)] = v;
+}
+
 // The same sums with float4 loads, for many partials of a short row (the conv1 weight gradient's
 // 512 x 8224): 64 outputs per workgroup as 16 float4 columns x 16 partial groups (group g:
 // p = g, g + 16, ..., 8 loads in flight), the group sums added in group order — four times the
@@ -488,6 +525,16 @@ int sum_parts4(hipStream_t s, const float *parts, int np, int64_t pstride, int64
     hipLaunchKernelGGL(k_sum_parts4<false>, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, parts, np, pstride, n,
                        0, out, nullptr);
     GS_LAUNCH_CHECK("k_sum_parts4");
+    return GS_OK;
+}
+
+int sum_parts_tiles(hipStream_t s, const float *parts, int np, int64_t pstride, int ncols, float *dW, float *db)
+{
+    GS_REQUIRE(np >= 1 && ncols >= 16 && ncols % 16 == 0, "sum_parts_tiles: bad sizes");
+    const int64_t n = (int64_t)64 * (ncols + 1);
+    hipLaunchKernelGGL(k_sum_parts_tiles, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, parts, np, pstride, ncols, dW,
+                       db);
+    GS_LAUNCH_CHECK("k_sum_parts_tiles");
     return GS_OK;
 }
 

@@ -76,7 +76,7 @@ def short(name):
     m = re.search(r"\b(k_\w+)", name)
     if m and m.group(1) == "k_conv1_wgrad_bf":    # the bf16 conv1 weight gradient (same position)
         return "k_conv1_wgrad"
-    if m and m.group(1) in ("k_sum_parts_wb", "k_sum_partials", "k_sum_parts4"):   # the partial sums (scalar / float4)
+    if m and m.group(1) in ("k_sum_parts_wb", "k_sum_partials", "k_sum_parts4", "k_sum_parts_tiles"):   # partial sums
         return "k_sum_parts"
     if m and m.group(1) == "k_fc16":      # the fp32 fc kernels on 16x16x4 MFMA blocks (same positions)
         return "k_fc"
