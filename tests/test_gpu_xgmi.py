@@ -363,6 +363,12 @@ def test_cnn_global_mode_teacher_forced_vs_single_run_and_oracle(tmp_path, cuda)
         the step's state happens to hold — one step of a round-5 run moved 3.6 K of 1.69 M
         entries (0.21 %) at 4.7e-4 x max|g| and 7.5e-4 relative L2 — while an arithmetic error
         moves every step);
+      * the single run also against the oracle under the single run's own ReLU decisions (read
+        from its workspace, gs_cnn_workspace_act_offset): every differing decision undecidable
+        (|u| <= 1e-5 of its terms' magnitudes, at most 32 per conv layer and 8 in the fc), then
+        the clipped gradient within 2e-5 relative L2, every entry within 1e-4 x max|g| and at
+        most 1e-4 of them beyond 2e-5 x max|g| — the arithmetic alone, at every step whose clip
+        decisions are not within rounding;
       * replicas bitwise identical (gradient + parameters digest per step).
     A step where some row's policy ratio or value change sits within 1e-5 (relative) of a clip
     boundary in the oracle is decided by rounding: a z product summed in another order flips that
@@ -390,7 +396,20 @@ def test_cnn_global_mode_teacher_forced_vs_single_run_and_oracle(tmp_path, cuda)
     idx = agent.prefetcher.upload(0)
     hp = agent.hparams()
     st = {"p": [], "m": [], "v": []}
-    g1, p1 = [], []
+    g1, p1, dev_masks = [], [], []
+    # the single run's ReLU decisions of each step (a1 / a2 / a3 / h > 0 in its workspace), which
+    # the oracle takes over for the single-run comparison (test_gpu_cnn.py's 8-minibatch test)
+    act_shapes = [(20, 20, 32), (9, 9, 64), (7, 7, 64), (512,)]
+    act_offs = [int(lib.gs_cnn_workspace_act_offset(pm.dims, B, layer)) for layer in (1, 2, 3, 4)]
+
+    def decisions():
+        out = []
+        for off, sh in zip(act_offs, act_shapes):
+            n = B * int(np.prod(sh))
+            assert off >= 0 and off % 4 == 0 and off + 4 * n <= agent.workspace.numel()
+            a = agent.workspace[off:off + 4 * n].view(torch.float32).view(B, *sh) > 0
+            out.append((a.permute(0, 3, 1, 2) if len(sh) == 3 else a).cpu().numpy())
+        return out
     for k in range(K):
         for key, t in (("p", pm.params), ("m", agent.adam_m), ("v", agent.adam_v)):
             st[key].append(t.cpu().numpy())
@@ -400,6 +419,7 @@ def test_cnn_global_mode_teacher_forced_vs_single_run_and_oracle(tmp_path, cuda)
               "gs_cnn_ppo_update")
         g1.append(agent.grads.cpu().numpy())
         p1.append(pm.params.cpu().numpy())
+        dev_masks.append(decisions())
     torch.cuda.synchronize()
     rec1 = agent.metrics_buf.cpu().numpy()
     ii = idx.cpu().numpy().astype(np.int64)[:K * B]
@@ -449,6 +469,25 @@ def test_cnn_global_mode_teacher_forced_vs_single_run_and_oracle(tmp_path, cuda)
             ambiguous.append(k)
         _, _, _, gc, _ = C.clip_and_adam(p_ref, g, shapes, to_ref(st["m"][k]), to_ref(st["v"][k]), k + 1, float(hp.lr))
         gm = np.abs(gc).max()
+        # the single run against the oracle under the single run's own ReLU decisions: every
+        # differing decision undecidable (|u| <= 1e-5 of its terms' magnitudes), then the arithmetic
+        # bars of test_gpu_cnn.py's 8-minibatch test (unless a clip decision sits within rounding)
+        dm = dev_masks[k]
+        dec = C.relu_decisions(p_ref, shapes, rows[0][sl], dm)
+        worst.setdefault("relu_decisions_single", []).append([n_ for n_, _ in dec])
+        for (n_, r_), cap, name in zip(dec, (32, 32, 32, 8), ("conv1", "conv2", "conv3", "fc")):
+            need(n_ <= cap and r_ <= 1e-5, ("single relu decisions", k, name, n_, r_))
+        _, _, gf, _, _ = C.loss_and_grads(p_ref, shapes, *(x[sl] for x in rows), conv_masks=dm[:3], fc_mask=dm[3],
+                                          **kw)
+        _, _, _, gcf, _ = C.clip_and_adam(p_ref, gf, shapes, to_ref(st["m"][k]), to_ref(st["v"][k]), k + 1,
+                                          float(hp.lr))
+        gr1 = to_ref(g1[k])
+        dgf = np.abs(gr1.astype(np.float64) - gcf)
+        gmf = np.abs(gcf).max()
+        worst["single_forced"] = max(worst.get("single_forced", 0.0), rl(gr1, gcf))
+        if not amb:
+            need(rl(gr1, gcf) < 2e-5 and dgf.max() <= 1e-4 * gmf and (dgf > 2e-5 * gmf).sum() <= 1e-4 * dgf.size,
+                 ("single forced", k, rl(gr1, gcf), float(dgf.max() / gmf), int((dgf > 2e-5 * gmf).sum())))
         for tag, rec, gd in (("single", rec1, g1[k]), ("global", rec2, g2[k])):
             dl = abs(rec[k, M["loss"]] - loss) / max(1.0, abs(loss))
             need(dl < 1e-5, (tag, "loss", k, float(rec[k, M["loss"]]), loss))
