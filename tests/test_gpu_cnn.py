@@ -410,6 +410,7 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
     states, grads, masks = [tuple(to_ref(t) for t in state)], [None], [None]
     for n in range(1, K + 1):
         restore()
+        torch.cuda.synchronize()               # the restore copies ran on the current stream, run on s
         with torch.cuda.stream(s):
             run(n)
         torch.cuda.synchronize()
