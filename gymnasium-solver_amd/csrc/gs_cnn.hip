@@ -175,9 +175,14 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.pre = (float *)take(sizeof(float) * kPreChunk * 5 * R);
     w.pre_stats = (float *)take(sizeof(float) * kPreChunk * 2);
     {   // shifted so Wf's rows start on 128-B lines (the fc kernels stream them in 128-B chunks; a
-        // 64-B offset put every chunk across two lines: fc forward 28.0 -> 35.5 us); 8-B aligned
+        // 64-B offset put every chunk across two lines: fc forward 28.0 -> 35.5 us); the shift is
+        // taken from the ABSOLUTE address, so any (even) workspace base gives the alignment, not
+        // only the 128-B aligned bases torch hands out
         uint16_t *pb = (uint16_t *)take(sizeof(uint16_t) * (L.P + 64));
-        w.pbf = pb ? pb + (64 - L.oWf % 64) % 64 : nullptr;
+        if (pb) {
+            const uintptr_t wf = ((uintptr_t)(pb + L.oWf) >> 1) & 63;     // elements past a 128-B line
+            w.pbf = pb + (64 - wf) % 64;
+        }
     }
     w.loss_part = (double *)take(sizeof(double) * 13 * (size_t)((R + kHeadRows - 1) / kHeadRows));
     {
@@ -1789,6 +1794,7 @@ int validate_cnn_update(const gs_cnn_dims &dims, const gs_rollout_view_u8 &ro, i
     GS_REQUIRE(ro.obs && ro.actions && ro.logprobs && ro.values && ro.advantages && ro.returns,
                "rollout view has a null buffer");
     GS_REQUIRE(ws, "null workspace");
+    GS_REQUIRE(((uintptr_t)ws & 15) == 0, "the workspace must be 16-byte aligned (float4 accesses)");
     return GS_OK;
 }
 

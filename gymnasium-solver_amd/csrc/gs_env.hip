@@ -100,9 +100,55 @@ extern "C" int gs_episode_stats(const float *rewards, const uint8_t *dones, int6
 // ---- the reference's rolling episode window (rollout_collector.py:242-294, 753-758) for
 // track_stats=False, one launch of one 1024-thread workgroup: this rollout's finished episodes in
 // (step, env) order (ep_ret / ep_len rows of gs_episode_stats, dones time-major) are numbered by a
-// block scan of per-thread done counts; the last W of them go to the window's tail slots in order
-// and the previous window shifts left by their count; meta = {episodes so far, best return, -}.
-constexpr int kWinThreads = 1024;
+// scan of done counts; the last W of them go to the window's tail slots in order and the previous
+// window shifts left by their count; meta = {episodes so far, best return, -}.
+//
+// Wave w of the 16 owns a contiguous range of 4-sample groups; a wave instruction covers 256
+// consecutive samples (a dword of dones and a float4 of returns per lane, both coalesced), so the
+// count + best pass streams the rows at the CU's load rate with every load of a batch in flight
+// (r05: one thread per 128-sample chunk of byte loads, 151 us at C2's 32 x 4096).  Only the waves
+// holding one of the last W episodes walk their range again, with a wave prefix scan per
+// instruction, and only the groups of those episodes load their lengths.
+constexpr int kWinThreads = 1024, kWinWaves = kWinThreads / 64, kWinBatch = 8;
+
+// the done bits of samples 4g..4g+3 (bit j = sample 4g + j) and their returns
+struct WinGroup {
+    unsigned bits;
+    float r[4];
+};
+__device__ __forceinline__ WinGroup win_group(const uint8_t *__restrict__ dones, const float *__restrict__ ep_ret,
+                                              int64_t g, int64_t n, bool vec)
+{
+    WinGroup o;
+    const int64_t i0 = 4 * g;
+    if (vec && i0 + 4 <= n) {
+        const unsigned d = *reinterpret_cast<const unsigned *>(dones + i0);
+        const float4 v = *reinterpret_cast<const float4 *>(ep_ret + i0);
+        // nonzero bytes -> bit 7 of each byte, then packed to bits 0..3
+        const unsigned nz = (((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d) & 0x80808080u;
+        o.bits = ((nz >> 7) & 1u) | ((nz >> 14) & 2u) | ((nz >> 21) & 4u) | ((nz >> 28) & 8u);
+        o.r[0] = v.x, o.r[1] = v.y, o.r[2] = v.z, o.r[3] = v.w;
+    } else {
+        o.bits = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool in = i0 + j < n;
+            o.r[j] = in ? ep_ret[i0 + j] : 0.0f;
+            o.bits |= (in && dones[i0 + j]) ? (1u << j) : 0u;
+        }
+    }
+    return o;
+}
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
 
 __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *__restrict__ dones,
                                                                 const float *__restrict__ ep_ret,
@@ -110,53 +156,87 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
                                                                 double *__restrict__ win, double *__restrict__ meta,
                                                                 int64_t *__restrict__ total_out)
 {
-    __shared__ int64_t scan[kWinThreads];
-    __shared__ double sbest[kWinThreads];
+    __shared__ int64_t wcnt[kWinWaves];
+    __shared__ double wbest[kWinWaves];
     extern __shared__ double old[];           // [2][W]
-    const int tid = threadIdx.x;
-    const int64_t per = (n + kWinThreads - 1) / kWinThreads;
-    const int64_t a = min((int64_t)tid * per, n), b = min(a + per, n);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool vec = (((uintptr_t)dones & 3) | ((uintptr_t)ep_ret & 15)) == 0;
+    const int64_t G = (n + 3) / 4;                                   // 4-sample groups
+    const int64_t g0 = (int64_t)wave * G / kWinWaves, g1 = (int64_t)(wave + 1) * G / kWinWaves;
+    for (int i = tid; i < 2 * W; i += kWinThreads) old[i] = win[i];
+    // ---- pass 1: done count and best return of this wave's range, kWinBatch groups per lane in flight
     int64_t cnt = 0;
     double best = -INFINITY;
-    for (int64_t i = a; i < b; ++i)
-        if (dones[i]) {
-            ++cnt;
-            best = fmax(best, (double)ep_ret[i]);
+    for (int64_t b = g0; b < g1; b += 64 * kWinBatch) {
+        WinGroup q[kWinBatch];
+#pragma unroll
+        for (int u = 0; u < kWinBatch; ++u) {
+            const int64_t g = b + (int64_t)u * 64 + lane;
+            q[u] = win_group(dones, ep_ret, g < g1 ? g : g0, n, vec);
+            if (g >= g1) q[u].bits = 0;
         }
-    for (int i = tid; i < 2 * W; i += kWinThreads) old[i] = win[i];
-    scan[tid] = cnt;
-    sbest[tid] = best;
-    __syncthreads();
-    // inclusive scan of the counts (Hillis-Steele), max of the bests
-    for (int off = 1; off < kWinThreads; off <<= 1) {
-        const int64_t v = tid >= off ? scan[tid - off] : 0;
-        const double bv = tid >= off ? sbest[tid - off] : -INFINITY;
-        __syncthreads();
-        scan[tid] += v;
-        sbest[tid] = fmax(sbest[tid], bv);
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kWinBatch; ++u) {
+            cnt += __popc(q[u].bits);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (q[u].bits & (1u << j)) best = fmax(best, (double)q[u].r[j]);
+        }
     }
-    const int64_t total = scan[kWinThreads - 1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+        best = fmax(best, __shfl_xor(best, o, 64));
+    }
+    if (lane == 0) {
+        wcnt[wave] = cnt;
+        wbest[wave] = best;
+    }
+    __syncthreads();
+    int64_t total = 0, before = 0;
+    double all_best = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kWinWaves; ++w) {
+        before += w < wave ? wcnt[w] : 0;
+        total += wcnt[w];
+        all_best = fmax(all_best, wbest[w]);
+    }
     // the previous window shifted left by this rollout's episode count
     for (int i = tid; i < W; i += kWinThreads)
         if (i + total < W) {
             win[i] = old[i + total];
             win[W + i] = old[W + i + total];
         }
-    // this rollout's last W episodes at their slots
-    int64_t pos = scan[tid] - cnt;            // episodes before this thread's chunk
-    for (int64_t i = a; i < b; ++i)
-        if (dones[i]) {
-            const int64_t slot = pos - (total - W);
-            if (slot >= 0) {
-                win[slot] = (double)ep_ret[i];
-                win[W + slot] = (double)ep_len[i];
+    // ---- pass 2: this rollout's last W episodes at their slots (only the waves that hold one)
+    const int64_t first = total - W;           // episode numbers >= first are kept
+    if (before + wcnt[wave] > first) {
+        int64_t base = before;                 // episodes before this wave instruction's groups
+        for (int64_t b = g0; b < g1 && base < total; b += 64) {
+            const int64_t g = b + lane;
+            WinGroup q = win_group(dones, ep_ret, g < g1 ? g : g0, n, vec);
+            if (g >= g1) q.bits = 0;
+            const int64_t c = __popc(q.bits);
+            const int64_t incl = wave_incl_scan(c, lane);
+            const int64_t wtot = __shfl(incl, 63, 64);
+            if (base + wtot > first && q.bits) {
+                int64_t pos = base + incl - c;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (q.bits & (1u << j)) {
+                        const int64_t slot = pos - first;
+                        if (slot >= 0) {
+                            win[slot] = (double)q.r[j];
+                            win[W + slot] = (double)ep_len[4 * g + j];
+                        }
+                        ++pos;
+                    }
             }
-            ++pos;
+            base += wtot;
         }
+    }
     if (tid == 0) {
         meta[0] += (double)total;
-        meta[1] = fmax(meta[1], sbest[kWinThreads - 1]);
+        meta[1] = fmax(meta[1], all_best);
         if (total_out) *total_out = total;
     }
 }

@@ -21,7 +21,9 @@
 // fwd 32 x 32 with the 4 waves splitting the k-groups (KS = 4: 512 workgroups, two per CU);
 // wgrad 64 x 64 on 32x32x2 MFMAs and dgrad 64 x 64 on 16x16x4 blocks (k_fc16) in fp32 (392 / 784
 // workgroups); fp32 tiles are 64 deep (KT = 2).
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 
 #include "gs_gemm.h"
 
@@ -525,17 +527,21 @@ __global__ __launch_bounds__(256, 2) void k_fc16(const float *__restrict__ A, in
         }
 }
 
-// a kernel's dynamic LDS above the 64 KB default: the attribute is set once per instantiation
-// (before any capture: the first call of a shape is eager)
+// a kernel's dynamic LDS above the 64 KB default: the attribute is set once per kernel (keyed on
+// the kernel's own address: every k_fc instantiation has the same function type, so a flag keyed
+// on the type would let the first one stand for all), before any capture (the first call of a
+// shape is eager)
 template <class KF>
 void lds_attr(KF k, size_t bytes)
 {
     if (bytes <= 65536) return;
-    static bool done = false;
-    if (!done) {
-        (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        done = true;
-    }
+    static std::mutex mu;
+    static std::unordered_map<const void *, size_t> done;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = done.find((const void *)k);
+    if (it != done.end() && it->second >= bytes) return;
+    (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    done[(const void *)k] = bytes;
 }
 
 // two staged K tiles, or the KS partial tiles of the in-workgroup k split if larger

@@ -484,6 +484,12 @@ __device__ __forceinline__ float pw_total(const float *__restrict__ chunk, int n
     return s;
 }
 
+// numpy's _mean / _var final step: the float32 sum divided by the integer count (an np.intp, so
+// float32 / intp promotes to float64) and cast back to float32.  For n <= 2^24 this equals the
+// float32 quotient (double rounding of a division is innocuous at 53 >= 2*24 + 2 bits); above it
+// (float)n is inexact and only the double quotient gives numpy's bits.
+__device__ __forceinline__ float np_div_count(float s, int64_t n) { return (float)((double)s / (double)n); }
+
 // MODE 1 needs the mean: every workgroup forms it from the MODE-0 chunk sums (scratch[0..nchunks))
 template <int MODE>
 __global__ __launch_bounds__(64) void k_pw_chunks(const float *__restrict__ x, int64_t n, float *__restrict__ scratch)
@@ -492,7 +498,7 @@ __global__ __launch_bounds__(64) void k_pw_chunks(const float *__restrict__ x, i
     __shared__ float s_mean;
     const int nchunks = (int)((n + kPwChunk - 1) / kPwChunk);
     const int lane = threadIdx.x;
-    if (MODE == 1 && lane == 0) s_mean = pw_total(scratch, nchunks) / (float)n;
+    if (MODE == 1 && lane == 0) s_mean = np_div_count(pw_total(scratch, nchunks), n);
     __syncthreads();
     const float mean = MODE == 1 ? s_mean : 0.0f;
     const int64_t c0 = (int64_t)blockIdx.x * kPwChunk;
@@ -534,8 +540,8 @@ __global__ __launch_bounds__(256) void k_adv_apply(float *__restrict__ x, int64_
     __shared__ float s_ms[2];
     const int nchunks = (int)((n + kPwChunk - 1) / kPwChunk);
     if (threadIdx.x == 0) {
-        s_ms[0] = pw_total(scratch, nchunks) / (float)n;
-        s_ms[1] = sqrtf(pw_total(scratch + nchunks, nchunks) / (float)n);
+        s_ms[0] = np_div_count(pw_total(scratch, nchunks), n);
+        s_ms[1] = sqrtf(np_div_count(pw_total(scratch + nchunks, nchunks), n));
         if (mean_std && blockIdx.x == 0) {
             mean_std[0] = s_ms[0];
             mean_std[1] = s_ms[1];

@@ -435,12 +435,23 @@ class DevicePPOAgent:
         early = self.config.target_kl is not None and bool(row[M["kl_stop"]])
         return dict(loss=self._step_metrics[M["loss"]].clone(), early_stop_epoch=early)
 
+    def _require_exchange(self) -> None:
+        """A data-parallel job (world_size > 1) trains ONE model only through the gradient
+        exchange: without a communicator every rank would step on its own shard's gradient and the
+        replicas would drift apart silently (local mode) or train on a share of each global
+        minibatch (global mode).  Raised before any device work of the step, on every rank."""
+        if self.world_size > 1 and not self.comm:
+            mode = "dp_mode 'global'" if getattr(self, "global_mode", False) else "dp_mode 'local'"
+            raise ValueError(f"{mode} with world_size={self.world_size} needs a communicator: set agent.comm = "
+                             f"init_xgmi_comm(...) or init_device_comm(...) before training (rank {self.rank})")
+
     def training_step(self, batch, batch_idx: int):
         """BaseAgent.training_step (base_agent.py:330-366) fused: forward, loss, backward,
         clip_grad_norm_(max_grad_norm), Adam.step.  The KL early stop is sticky as in the
         reference: the minibatch that trips it takes no step, nor does any later one."""
         if self._early_stop_epoch:
             return None
+        self._require_exchange()
         view, idx, B, ws = self._batch_view(batch)
         self.adam_step += 1
         rec = self.metrics_buf[batch_idx % self.n_minibatches]
@@ -492,6 +503,11 @@ class DevicePPOAgent:
         """The update half of an epoch on the train collector's current rollout (the n_epochs
         passes of minibatch steps, then the epoch's bookkeeping) — train_epoch after its collect;
         callers that collect themselves (e.g. a replayed rollout) call it directly."""
+        self._require_exchange()
+        # the hyper-parameters this update runs with, as the reference logs them at the epoch's
+        # start (on_train_epoch_start -> _log_hyperparameters, base_agent.py:302): booked with the
+        # update's records by record_epoch_metrics (the scheduler changes them at the epoch's end)
+        self._epoch_hp = self.hyperparameter_record()
         epoch = self.current_epoch
         collector = self.get_rollout_collector("train")
         # the epoch's minibatch indices go up on the update's own stream: a side-stream upload
@@ -503,13 +519,7 @@ class DevicePPOAgent:
             self.prefetcher.prefetch(epoch + 1)
         buf = collector.buffer
         if self.world_size > 1:
-            if self.global_mode and not self.comm:
-                # the mode's advantage statistics, loss records and gradient are sums over ranks:
-                # without a communicator each rank would train on its own rows' share only
-                raise ValueError("dp_mode 'global' with world_size > 1 needs a communicator (agent.comm = "
-                                 "init_xgmi_comm(...) or init_device_comm(...))")
-            if self.comm:
-                self._verify_exchange()
+            self._verify_exchange()
         self._activation_stats_launch(buf, idx)
         if ev:
             ev[-1][1].record()
@@ -578,8 +588,13 @@ class DevicePPOAgent:
         if _dist.comm_info(self.comm)["transport"] != "xgmi":
             return
         self._canary_round = getattr(self, "_canary_round", 0) + 1
-        ok = _dist.xgmi_self_test(self.comm, self.rank, self.world_size, self.policy_model.n_params, self.device,
-                                  rounds=1, salt=self._canary_round)
+        # a rank whose exchange call raises (GsError) still meets the others in _agree, so every
+        # rank raises together instead of its peers blocking in the all-reduce until it times out
+        try:
+            ok = _dist.xgmi_self_test(self.comm, self.rank, self.world_size, self.policy_model.n_params, self.device,
+                                      rounds=1, salt=self._canary_round)
+        except RuntimeError:
+            ok = False
         if not _dist._agree(ok, self.device):
             from ._lib import GsError
             raise GsError(f"exchange canary failed on epoch {self.current_epoch} (rank {self.rank}): a known "
@@ -670,6 +685,14 @@ class DevicePPOAgent:
         if hasattr(self.config, param):
             setattr(self.config, param, value)
 
+    HP_KEYS = ("n_epochs", "ent_coef", "vf_coef", "clip_range", "policy_lr", "clip_range_vf")
+
+    def hyperparameter_record(self) -> Dict[str, float]:
+        """HyperparameterMixin._log_hyperparameters (agents/hyperparameter_mixin.py:90-103): the
+        tunable values in effect, under hp/<name> (clip_range_vf: PPO's; a None value is dropped as
+        the recorder drops non-scalars)."""
+        return {f"hp/{k}": getattr(self, k) for k in self.HP_KEYS if getattr(self, k, None) is not None}
+
     def on_train_epoch_end(self) -> None:
         """HyperparameterSchedulerCallback.on_train_epoch_end for every configured schedule."""
         if not self.schedulers:
@@ -688,6 +711,8 @@ class DevicePPOAgent:
         live = rec[rec[:, M["unevaluated"]] == 0]
         self.metrics_recorder.record_rows("train", ppo_keys(norm),
                                           ppo_records(live, float(self.vf_coef), float(self.ent_coef), norm))
+        if getattr(self, "_epoch_hp", None):
+            self.metrics_recorder.record("train", self._epoch_hp)
         stepped = rec[rec[:, M["skipped"]] == 0]
         keys, slots = self.grad_norm_keys()
         self.metrics_recorder.record_rows("train", keys, stepped[:, slots])
@@ -706,7 +731,8 @@ class DevicePPOAgent:
     def epoch_metric_keys(self):
         """The fixed key list of epoch_metrics (every rank sends the same vector)."""
         norm = self.config.normalize_advantages == "batch"
-        return tuple(ppo_keys(norm)) + self.grad_norm_keys()[0] + self.activation_keys()
+        hp = tuple(f"hp/{k}" for k in self.HP_KEYS if getattr(self, k, None) is not None)
+        return tuple(ppo_keys(norm)) + self.grad_norm_keys()[0] + self.activation_keys() + hp
 
     def epoch_metrics(self) -> Dict[str, float]:
         """The last update's epoch means under the reference's metric keys (ppo_agent.py:131-146,

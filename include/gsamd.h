@@ -374,7 +374,9 @@ typedef struct gs_rollout_view_u8 {
 } gs_rollout_view_u8;
 
 int64_t gs_cnn_param_count(gs_cnn_dims dims);
-/* scratch for `rows` rows (the minibatch B for updates, N envs for gs_cnn_policy_act) */
+/* scratch for `rows` rows (the minibatch B for updates, N envs for gs_cnn_policy_act); the workspace
+ * base must be 16-byte aligned (every torch allocation is): the update places its internal buffers,
+ * the bf16 parameter copy included, relative to it and refuses (GS_E_INVALID) an unaligned base */
 size_t gs_cnn_workspace_bytes(gs_cnn_dims dims, int64_t rows);
 /* Byte offset, inside a workspace of that many rows, of the fc layer's output h [rows][HID] fp32
  * (after relu): after gs_cnn_ppo_update / _global it holds the last minibatch step's values (the

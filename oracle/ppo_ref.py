@@ -313,10 +313,11 @@ def normalize_advantages_rollout(adv, eps: float = 1e-8) -> np.ndarray:
 
 def normalize_advantages_model(adv, eps: float = 1e-8) -> np.ndarray:
     """normalize_advantages_rollout written out with numpy_f32_sum (the device kernel's steps):
-    mean = S / n, std = sqrt(S((a - mean)^2) / n), all float32."""
+    mean = S / n, std = sqrt(S((a - mean)^2) / n), float32 sums; each division of a float32 sum by
+    the integer count in float64, cast back to float32 (numpy's _mean / _var: float32 / np.intp)."""
     a = np.asarray(adv, F32)
-    n = F32(a.size)
-    mean = F32(numpy_f32_sum(a) / n)
+    n = np.float64(a.size)
+    mean = F32(np.float64(numpy_f32_sum(a)) / n)
     d = (a - mean).astype(F32)
-    std = np.sqrt(F32(numpy_f32_sum((d * d).astype(F32)) / n)).astype(F32)
+    std = np.sqrt(F32(np.float64(numpy_f32_sum((d * d).astype(F32))) / n)).astype(F32)
     return ((a - mean) / F32(std + F32(eps))).astype(F32)

@@ -647,3 +647,30 @@ def agent_selftest_worker(rank, world, port, result_dir, mode):
         gd.destroy_comm(comm)
     finally:
         dist.destroy_process_group()
+
+
+def no_comm_worker(rank, world, port, result_dir):
+    """One rank of a data-parallel job whose agent has no communicator attached (CPU, gloo).
+    Local mode as well as global mode: DevicePPOAgent.update_phase (train_epoch's update half) and
+    training_step must raise ValueError on every rank before any device work, instead of each
+    rank stepping its own replica on its own shard's gradient (VERDICT r5 weak #5)."""
+    dist = _init(rank, world, port)
+    try:
+        from gsamd.ppo_agent import DevicePPOAgent
+        out = []
+        for mode in ("local", "global"):
+            agent = object.__new__(DevicePPOAgent)       # no device: the check runs first
+            agent.rank, agent.world_size, agent.comm = rank, world, None
+            agent.global_mode = mode == "global"
+            agent._early_stop_epoch = False
+            for call in (lambda: agent.update_phase(), lambda: agent.training_step(None, 0)):
+                try:
+                    call()
+                    out.append("returned")
+                except ValueError as e:
+                    assert f"world_size={world}" in str(e) and f"dp_mode '{mode}'" in str(e), str(e)
+                    out.append("ValueError")
+        dist.barrier()
+        open(os.path.join(result_dir, f"nc{rank}"), "w").write(",".join(out))
+    finally:
+        dist.destroy_process_group()

@@ -267,3 +267,44 @@ def test_untracked_collector_keeps_the_rolling_window(cuda, over):
             assert (k in mt) == (k in mu), k
             if k in mt:
                 np.testing.assert_allclose(mu[k], mt[k], rtol=1e-6, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("shape,p,W", [((32, 4096), 0.01, 100), ((32, 4096), 0.3, 2048), ((7, 33), 0.2, 5),
+                                       ((3, 7), 0.5, 1), ((1, 1), 1.0, 3), ((2048, 64), 0.02, 100)])
+def test_episode_window_kernel_vs_model(cuda, shape, p, W):
+    """gs_episode_window (the track_stats=False rolling window, rollout_collector.py:242-294,
+    753-758) against its definition: the window is the last W entries of (previous window ++ this
+    rollout's finished episodes in (step, env) order), meta = {count so far, best return}; three
+    calls in a row carry the window, with negative returns, a ragged sample count (n % 4 != 0) and
+    a dones buffer at an odd address (the scalar path of the kernel's 4-sample groups)."""
+    from gsamd._lib import check, lib, ptr, stream_handle
+    T, N = shape
+    rng = np.random.default_rng(T * 1000 + N)
+    win = torch.zeros(2, W, dtype=torch.float64, device=cuda)
+    meta = torch.tensor([0.0, -np.inf, 0.0], dtype=torch.float64, device=cuda)
+    tot = torch.zeros((), dtype=torch.int64, device=cuda)
+    m_win, m_cnt, m_best = np.zeros((2, W)), 0.0, -np.inf
+    for call in range(3):
+        d = (rng.random((T, N)) < p).astype(np.uint8)
+        r = (rng.standard_normal((T, N)) * 50).astype(np.float32)
+        ln = rng.integers(1, 500, (T, N)).astype(np.int32)
+        if call == 2:                      # odd address: the scalar path
+            dd = torch.zeros(T * N + 1, dtype=torch.uint8, device=cuda)
+            dd[1:] = torch.as_tensor(d.reshape(-1)).to(cuda)
+            dv = dd[1:]
+        else:
+            dv = torch.as_tensor(d).to(cuda)
+        rt, lt = torch.as_tensor(r).to(cuda), torch.as_tensor(ln).to(cuda)
+        check(lib.gs_episode_window(ptr(dv), ptr(rt), ptr(lt), T, N, W, ptr(win), ptr(meta), ptr(tot),
+                                    stream_handle()), "gs_episode_window")
+        torch.cuda.synchronize()
+        at = np.flatnonzero(d.reshape(-1))
+        m_win = np.concatenate([m_win, np.stack([r.reshape(-1)[at].astype(np.float64),
+                                                 ln.reshape(-1)[at].astype(np.float64)])], axis=1)[:, -W:]
+        m_cnt += at.size
+        if at.size:
+            m_best = max(m_best, float(r.reshape(-1)[at].max()))
+        assert int(tot.item()) == at.size
+        np.testing.assert_array_equal(win.cpu().numpy(), m_win)
+        mm = meta.cpu().numpy()
+        assert mm[0] == m_cnt and mm[1] == m_best

@@ -315,7 +315,8 @@ def test_normalize_advantages_kernel_vs_reference(golden, cuda, case):
     also for the large-offset case, where numpy's float32 mean is 6e-5 off the exact one and a
     double-precision normalisation would differ by 6e-3.  The std = 0 cases give 0 as numpy's
     (a - mean) / 1e-8.  Plus a C2-sized (32 x 4096 = 16 chunks) and a ragged 3-chunk array against
-    numpy directly."""
+    numpy directly, and one of 2^24 + 4096 elements (numpy divides the float32 sums by the count in
+    float64)."""
     from gsamd._lib import check, lib, ptr, stream_handle
     from oracle.ppo_ref import normalize_advantages_rollout
 
@@ -337,7 +338,9 @@ def test_normalize_advantages_kernel_vs_reference(golden, cuda, case):
         assert (y == 0).all()
     if case == "offset":
         rng = np.random.default_rng(3)
-        for shape in ((32, 4096), (3, 6000)):
+        # (4097, 4096): n > 2^24, where numpy's float64 division by the count differs from a
+        # float32 one (the count is no longer a float32)
+        for shape in ((32, 4096), (3, 6000), (4097, 4096)):
             a = (rng.standard_normal(shape) * 1.5 + 4.0).astype(np.float32)
             y, _ = run(a)
             assert np.array_equal(y.view(np.uint32), normalize_advantages_rollout(a).view(np.uint32)), shape

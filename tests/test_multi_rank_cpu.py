@@ -50,3 +50,23 @@ def test_replica_check_and_seed_broadcast_gloo(tmp_path):
     assert [p.exitcode for p in procs] == [0, 0]
     for r in range(2):
         assert (tmp_path / f"rc{r}").read_text() == "GsError,GsError"
+
+
+def test_multi_rank_without_communicator_raises_gloo(tmp_path):
+    """world_size 2 with no communicator attached: the agent's update (local and global mode) and
+    training_step raise ValueError on every rank (DevicePPOAgent._require_exchange) — no rank
+    trains a replica of its own silently."""
+    from _dist_workers import no_comm_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=no_comm_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert [p.exitcode for p in procs] == [0, 0]
+    for r in range(2):
+        assert (tmp_path / f"nc{r}").read_text() == ",".join(["ValueError"] * 4)

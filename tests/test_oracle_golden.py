@@ -169,3 +169,13 @@ def test_numpy_f32_sum_model_matches_numpy():
     for n in (1, 7, 8, 9, 127, 128, 129, 136, 143, 255, 257, 1000, 8191, 8192, 8193, 20001, 131072, 2 ** 21 + 5):
         a = (rng.standard_normal(n) * 3.0 + 100.0).astype(np.float32)
         assert numpy_f32_sum(a) == np.add.reduce(a), n
+
+
+def test_adv_norm_model_above_2_24_matches_numpy():
+    """Above 2^24 elements the count is not a float32: numpy divides the float32 sums by it in
+    float64 (_mean / _var: float32 / np.intp), and so must the model the device kernel follows
+    (gs_gae.hip np_div_count) — bit for bit against normalize_advantages_rollout."""
+    from oracle.ppo_ref import normalize_advantages_model, normalize_advantages_rollout
+    a = (np.random.default_rng(5).standard_normal((4097, 4096)) * 1.5 + 4.0).astype(np.float32)
+    assert a.size > 2 ** 24
+    assert np.array_equal(normalize_advantages_model(a).view(np.uint32), normalize_advantages_rollout(a).view(np.uint32))
