@@ -148,6 +148,7 @@ struct Workspace {
     float *part1;    // (ceil(B/64), H1, D+1) dW1|db1 partials per 64-row block
     float *sumsq;    // (n_slots)  per-tile sum of squared gradients
     float *kl4;      // (4)        global mode: the step's approx_kl share, exchanged in place
+    double *act_parts;  // GS_HP_ACT_STATS on the unfused chain: k_mlp_act_stats parts of the step
     int32_t *f_act;  // (B)        gathered minibatch fields (written by k_fwd_hidden)
     float *f_olp, *f_ov, *f_adv, *f_ret;
     int n_slots;
@@ -186,7 +187,12 @@ struct FusedFwd {
     float *dz;                 // (B, A+1) dLoss/dlogits | dLoss/dvalue of the current step
     const int64_t *step_base;
     int k_local;
+    // GS_HP_ACT_STATS: (n, B/16, H2/16, 12) u32 per forward workgroup — the dead counts of its 16
+    // h1 columns and its 16 h2 columns (one byte per column, 4 per word), then the float bits of
+    // {sum z1, sum z1^2, sum z2, sum z2^2}; null = the forward computes no statistics
+    uint32_t *act;
 };
+constexpr int kActRec = 12;    // u32 words of one forward workgroup's activation-statistics record
 
 struct LossArgs {
     float clip_lo, clip_hi;     // f32(1 - clip), f32(1 + clip) (torch clamp casts scalars to f32)
@@ -323,7 +329,12 @@ int launch_clip_adam(float *P, const Layout &L, float *G, float *M, float *V, co
 // activation statistics parts of the MLP backbone (k_mlp_act_stats): ceil(R/16) x
 // 2 * (2 + max(H1, H2)) doubles
 int launch_act_stats(const float *P, const Layout &L, const float *obs, const int32_t *idx, int64_t T, int64_t N,
-                     int64_t R, double *part, hipStream_t s);
+                     int64_t R, double *part, hipStream_t s, const int64_t *step_base = nullptr);
+// GS_HP_ACT_STATS: one step's parts -> its record's GS_M_ACT slots (unfused chain; skipped after a
+// KL stop), and the fused chain's per-workgroup records of n steps -> their records
+int launch_act_parts_record(const Layout &L, int64_t R, const double *part, const int32_t *stop, float *metrics,
+                            const int64_t *step_base, hipStream_t s);
+int launch_act_stats_fused(const Layout &L, int64_t B, int64_t n, const uint32_t *act, float *metrics, hipStream_t s);
 // fused update, exchange launched behind k_bwd: step ff.k_local's head record from the exchanged G
 int launch_head_sq(const Layout &L, const float *G, float scale, const FusedFwd &ff, hipStream_t s);
 int launch_reduce_part1(const float *part1, const Layout &L, int nrb, float *G, const int32_t *stop, hipStream_t s);

@@ -288,7 +288,11 @@ __device__ __forceinline__ void loss_row(const float (&z)[AMAX + 1], int A, int 
 constexpr int kFwdAdamThreads = GS_FWD_ADAM_NT;
 static_assert(kFwdAdamThreads == 256 || kFwdAdamThreads == 512, "lagged forward: 256 or 512 threads");
 
-template <class S, bool FUSED, bool ADAM = false>
+// STATS (GS_HP_ACT_STATS, fused chain): the workgroup also records the activation statistics of its
+// rows (FusedFwd::act, kActRec words): dead counts of the 16 h1 columns of chunk cb and of its 16 h2
+// columns and the float sums of z and z^2 of both (the pre-activation values of the forward hooks on
+// backbone.0 / backbone.2, utils/models.py:121-147), on the block's last wave after the h2 epilogue
+template <class S, bool FUSED, bool ADAM = false, bool STATS = false>
 __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
     const float *__restrict__ P, Layout Lrt, const float *__restrict__ obs, const int32_t *__restrict__ idx, int T,
     int N, int rows, float *__restrict__ x_out, float *__restrict__ h1_out, float *__restrict__ h2_out,
@@ -800,12 +804,62 @@ __global__ __launch_bounds__(ADAM ? kFwdAdamThreads : 256) void k_fwd_hidden(
         float h = 0.0f;
         if (c0 + col < H2) {
             h = s + b2s[col];
+            // the pre-activation z2 into this thread's own partial slot (read above, by it alone)
+            if constexpr (STATS) red[tid] = h;
             h = h > 0.0f ? h : 0.0f;
             if (h2_out && r0 + row < rows) h2_out[(int64_t)(r0 + row) * H2 + c0 + col] = h;
+        } else if constexpr (STATS) {
+            red[tid] = 0.0f;
         }
         h2s[row * 17 + col] = h;
     }
     __syncthreads();
+    if constexpr (STATS) {
+        // lanes 0..15: h1 column cb*16 + c (z1 = x W1^T + b1 from the LDS operands, h1_quad's
+        // order), lanes 16..31: h2 column c0 + c (red); 16 rows each (fused: B % 16 == 0)
+        if (wave == NT / 64 - 1 && lane < 32) {
+            const bool l2 = lane >= 16;
+            const int c = lane & 15;
+            const bool have = l2 ? c0 + c < H2 : cb * kTile + c < H1;
+            const int k1 = min(cb * kTile + c, H1 - 1);
+            float w1[8];
+#pragma unroll
+            for (int d = 0; d < 8; ++d) w1[d] = d < D ? W1s[k1 * D + d] : 0.0f;
+            const float bk = b1s[k1];
+            float sz = 0.0f, sq = 0.0f;
+            unsigned dead = 0;
+#pragma unroll 4
+            for (int i = 0; i < kTile; ++i) {
+                float z;
+                if (l2) {
+                    z = red[i * kTile + c];
+                } else {
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int d = 0; d < 8; ++d)
+                        if (d < D) acc = fmaf(xs[i * D + d], w1[d], acc);
+                    z = acc + bk;
+                }
+                sz += z;
+                sq += z * z;
+                dead += fabsf(z) < 1e-6f ? 1u : 0u;
+            }
+            if (!have) sz = 0.0f, sq = 0.0f, dead = 0u;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                sz += __shfl_xor(sz, o, 64);
+                sq += __shfl_xor(sq, o, 64);
+            }
+            const unsigned word = dead | (__shfl_down(dead, 1, 64) << 8) | (__shfl_down(dead, 2, 64) << 16) |
+                                  (__shfl_down(dead, 3, 64) << 24);
+            uint32_t *out = ff.act + ((kstep * gridDim.y + rb) * gridDim.x + cb) * kActRec;
+            if ((c & 3) == 0) out[(l2 ? 4 : 0) + (c >> 2)] = word;
+            if (c == 0) {
+                out[8 + (l2 ? 2 : 0)] = __float_as_uint(sz);
+                out[9 + (l2 ? 2 : 0)] = __float_as_uint(sq);
+            }
+        }
+    }
     // relu'(h2) bits of each row's 16 columns (a 512-thread block: on wave 4, beside the heads)
     const int hm = tid - (NT == 512 ? 256 : 0);
     if (h2mask && hm >= 0 && hm < kTile && r0 + hm < rows) {
@@ -3192,9 +3246,11 @@ __host__ __device__ inline int act_part_stride(const Layout &L) { return 2 * (2 
 
 __global__ __launch_bounds__(256) void k_mlp_act_stats(const float *__restrict__ P, Layout L,
                                                        const float *__restrict__ obs, const int32_t *__restrict__ idx,
-                                                       int T, int N, int R, double *__restrict__ part)
+                                                       int T, int N, int R, double *__restrict__ part,
+                                                       const int64_t *__restrict__ step_base)
 {
     extern __shared__ float lds[];
+    if (step_base && idx) idx += *step_base * R;      // graph chunk replay: this step's rows
     __shared__ double sred[2 * 272];
     const int tid = threadIdx.x, D = L.D, H1 = L.H1, H2 = L.H2;
     const int r0 = blockIdx.x * kActRows, nr = min(kActRows, R - r0);
@@ -3249,13 +3305,71 @@ __global__ __launch_bounds__(256) void k_mlp_act_stats(const float *__restrict__
 }
 
 int launch_act_stats(const float *P, const Layout &L, const float *obs, const int32_t *idx, int64_t T, int64_t N,
-                     int64_t R, double *part, hipStream_t s)
+                     int64_t R, double *part, hipStream_t s, const int64_t *step_base)
 {
     const size_t lds = sizeof(float) * (size_t)kActRows * (L.D + L.H1);
     GS_REQUIRE(lds <= 64 * 1024, "activation stats: obs_dim + hidden1 too large");
     const unsigned nb = (unsigned)((R + kActRows - 1) / kActRows);
-    hipLaunchKernelGGL(k_mlp_act_stats, dim3(nb), dim3(256), lds, s, P, L, obs, idx, (int)T, (int)N, (int)R, part);
+    hipLaunchKernelGGL(k_mlp_act_stats, dim3(nb), dim3(256), lds, s, P, L, obs, idx, (int)T, (int)N, (int)R, part,
+                       step_base);
     GS_LAUNCH_CHECK("k_mlp_act_stats");
+    return GS_OK;
+}
+
+// GS_HP_ACT_STATS on the unfused chain: one step's k_mlp_act_stats parts -> its record's GS_M_ACT
+// slots (the arithmetic of k_act_stats_fused over the parts' double sums and counts).  A minibatch
+// after a KL stop is never evaluated: the record stays as the loss kernel leaves it.
+__global__ __launch_bounds__(256) void k_act_parts_record(const double *__restrict__ part, int nparts, int H1, int H2,
+                                                          int R, const int32_t *__restrict__ stop,
+                                                          float *__restrict__ metrics,
+                                                          const int64_t *__restrict__ step_base)
+{
+    __shared__ double sred[4 * (256 + 16)];
+    __shared__ unsigned smax[2];
+    if (stop && *stop) return;
+    const int tid = threadIdx.x, HM = H1 > H2 ? H1 : H2, stride = 2 * (2 + HM);
+    if (tid < 2) smax[tid] = 0u;
+    __syncthreads();
+    double dsum[2] = {0.0, 0.0};
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        const int H = l == 0 ? H1 : H2, off = l * (2 + HM) + 2;
+        unsigned mx = 0u;
+        for (int j = tid; j < H; j += 256) {
+            double cnt = 0.0;
+            for (int p = 0; p < nparts; ++p) cnt += part[(int64_t)p * stride + off + j];
+            dsum[l] += cnt;
+            mx = (unsigned)cnt > mx ? (unsigned)cnt : mx;
+        }
+        atomicMax(&smax[l], mx);
+    }
+    double zs[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int p = tid; p < nparts; p += 256)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) zs[q] += part[(int64_t)p * stride + (q >> 1) * (2 + HM) + (q & 1)];
+    block_reduce<2>(dsum, sred);
+    block_reduce<4>(zs, sred);
+    if (tid == 0) {
+        float *rec = metrics + (step_base ? *step_base : 0) * GS_NUM_METRICS + GS_M_ACT;
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+            const double n = (double)R * (double)(l == 0 ? H1 : H2);
+            const double s1 = zs[2 * l], s2 = zs[2 * l + 1];
+            const double var = (s2 - s1 * s1 / n) / (n - 1.0);
+            rec[4 * l + 0] = (float)(s1 / n);
+            rec[4 * l + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
+            rec[4 * l + 2] = (float)(dsum[l] / n);
+            rec[4 * l + 3] = (float)((double)smax[l] / (double)R);
+        }
+    }
+}
+
+int launch_act_parts_record(const Layout &L, int64_t R, const double *part, const int32_t *stop, float *metrics,
+                            const int64_t *step_base, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_act_parts_record, dim3(1), dim3(256), 0, s, part, (int)((R + kActRows - 1) / kActRows), L.H1,
+                       L.H2, (int)R, stop, metrics, step_base);
+    GS_LAUNCH_CHECK("k_act_parts_record");
     return GS_OK;
 }
 
@@ -3354,51 +3468,116 @@ int launch_fwd_fused(const float *params, const Layout &L, int64_t B, const Fuse
                      const Workspace &ws, const int32_t *stop, hipStream_t s, const AdamFwd *af)
 {
     const dim3 grid((unsigned)((L.H2 + kTile - 1) / kTile), (unsigned)((B + kTile - 1) / kTile));
+    // GS_HP_ACT_STATS (ff.act): the STATS instantiations, whose epilogue records the activation
+    // statistics (compile-time shapes with D <= 8 and at most one h1 chunk per column block)
+    GS_REQUIRE(!ff.act || (L.D <= 8 && L.H1 <= L.H2), "activation statistics in the fused forward: D <= 8, H1 <= H2");
     return with_shape(L, B, [&](auto sh) {
         using Sh = decltype(sh);
-        const float *no_obs = nullptr;
-        const int32_t *no_idx = nullptr;
-        float *no_copy = nullptr;
-        if (la.bf16) {      // the bf16 mode (GS_HP_BF16)
-            if constexpr (bf16_shape<Sh>() && lagged_shape<Sh>()) {
-                using Sb = Bf16Shape<Sh>;
-                if (af) {
+        auto go = [&](auto stats) -> int {
+            constexpr bool ST = decltype(stats)::value && (Sh::H1c > 0);
+            const float *no_obs = nullptr;
+            const int32_t *no_idx = nullptr;
+            float *no_copy = nullptr;
+            if (la.bf16) {      // the bf16 mode (GS_HP_BF16)
+                if constexpr (bf16_shape<Sh>() && lagged_shape<Sh>()) {
+                    using Sb = Bf16Shape<Sh>;
+                    if (af) {
+                        GS_REQUIRE((af->part1 ? af->aa.nrb > 0 : af->aa.nrb == 0) && af->aa.n_slots <= 512,
+                                   "lagged Adam: bad slot / partial counts");
+                        hipLaunchKernelGGL((k_fwd_hidden<Sb, true, true, ST>), grid, dim3(kFwdAdamThreads),
+                                           fwd_lds_bytes(L), s, params, L, no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1,
+                                           ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la, ws.h2mask, *af);
+                    } else {
+                        hipLaunchKernelGGL((k_fwd_hidden<Sb, true, false, ST>), grid, dim3(256), fwd_lds_bytes(L), s,
+                                           params, L, no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart,
+                                           no_copy, stop, RowGather{}, ff, la, ws.h2mask, AdamFwd{});
+                    }
+                    GS_LAUNCH_CHECK("k_fwd_hidden<fused, bf16>");
+                    return GS_OK;
+                } else {
+                    GS_REQUIRE(false, "precision bf16: no bf16 instantiation of the MLP chain for this shape");
+                }
+            }
+            if (af) {   // forward carrying the previous minibatch's clip + Adam (dW1|db1 partials)
+                if constexpr (lagged_shape<Sh>()) {
                     GS_REQUIRE((af->part1 ? af->aa.nrb > 0 : af->aa.nrb == 0) && af->aa.n_slots <= 512,
                                "lagged Adam: bad slot / partial counts");
-                    hipLaunchKernelGGL((k_fwd_hidden<Sb, true, true>), grid, dim3(kFwdAdamThreads), fwd_lds_bytes(L),
-                                       s, params, L, no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart,
-                                       no_copy, stop, RowGather{}, ff, la, ws.h2mask, *af);
+                    hipLaunchKernelGGL((k_fwd_hidden<Sh, true, true, ST>), grid, dim3(kFwdAdamThreads),
+                                       fwd_lds_bytes(L), s, params, L, no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1,
+                                       ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la, ws.h2mask, *af);
+                    GS_LAUNCH_CHECK("k_fwd_hidden<fused, adam>");
+                    return GS_OK;
                 } else {
-                    hipLaunchKernelGGL((k_fwd_hidden<Sb, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L,
-                                       no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop,
-                                       RowGather{}, ff, la, ws.h2mask);
+                    GS_REQUIRE(false, "lagged Adam: no compile-time instantiation for this shape");
                 }
-                GS_LAUNCH_CHECK("k_fwd_hidden<fused, bf16>");
-                return GS_OK;
-            } else {
-                GS_REQUIRE(false, "precision bf16: no bf16 instantiation of the MLP chain for this shape");
             }
-        }
-        if (af) {   // forward carrying the previous minibatch's clip + Adam (dW1|db1 partials)
-            if constexpr (lagged_shape<Sh>()) {
-                GS_REQUIRE((af->part1 ? af->aa.nrb > 0 : af->aa.nrb == 0) && af->aa.n_slots <= 512,
-                           "lagged Adam: bad slot / partial counts");
-                hipLaunchKernelGGL((k_fwd_hidden<Sh, true, true>), grid, dim3(kFwdAdamThreads), fwd_lds_bytes(L), s,
-                                   params, L,
-                                   no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop,
-                                   RowGather{}, ff, la, ws.h2mask, *af);
-                GS_LAUNCH_CHECK("k_fwd_hidden<fused, adam>");
-                return GS_OK;
-            } else {
-                GS_REQUIRE(false, "lagged Adam: no compile-time instantiation for this shape");
-            }
-        }
-        hipLaunchKernelGGL((k_fwd_hidden<Sh, true>), grid, dim3(256), fwd_lds_bytes(L), s, params, L, no_obs, no_idx,
-                           0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop, RowGather{}, ff, la,
-                           ws.h2mask);
-        GS_LAUNCH_CHECK("k_fwd_hidden<fused>");
-        return GS_OK;
+            hipLaunchKernelGGL((k_fwd_hidden<Sh, true, false, ST>), grid, dim3(256), fwd_lds_bytes(L), s, params, L,
+                               no_obs, no_idx, 0, 0, (int)B, ws.x, ws.h1, ws.h2, ws.zpart, no_copy, stop, RowGather{},
+                               ff, la, ws.h2mask, AdamFwd{});
+            GS_LAUNCH_CHECK("k_fwd_hidden<fused>");
+            return GS_OK;
+        };
+        return ff.act ? go(std::true_type{}) : go(std::false_type{});
     });
+}
+
+// ---- GS_HP_ACT_STATS on the fused chain: one workgroup per minibatch step turns its forward
+// workgroups' records (FusedFwd::act) into the record's GS_M_ACT slots: per layer the per-neuron
+// dead counts summed over the row blocks (fraction of the B rows; dead_pct their mean, dead_max
+// their max), and mean / unbiased std of z over B x H from the float partial sums (double).
+__global__ __launch_bounds__(256) void k_act_stats_fused(const uint32_t *__restrict__ act, int nrb, int ncb, int H1,
+                                                         int H2, int B, float *__restrict__ metrics)
+{
+    __shared__ double sred[4 * (256 + 16)];
+    __shared__ unsigned smax[2];
+    const int64_t k = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint32_t *a = act + k * (int64_t)nrb * ncb * kActRec;
+    if (tid < 2) smax[tid] = 0u;
+    __syncthreads();
+    double dsum[2] = {0.0, 0.0};            // per layer: the neurons' dead counts summed
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        const int H = l == 0 ? H1 : H2;
+        unsigned mx = 0u;
+        for (int j = tid; j < H; j += 256) {
+            const int cb = j / kTile, c = j % kTile;
+            unsigned cnt = 0u;
+            for (int rb = 0; rb < nrb; ++rb)
+                cnt += (a[(rb * ncb + cb) * kActRec + 4 * l + (c >> 2)] >> (8 * (c & 3))) & 0xffu;
+            dsum[l] += (double)cnt;
+            mx = cnt > mx ? cnt : mx;
+        }
+        atomicMax(&smax[l], mx);
+    }
+    double zs[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int w = tid; w < nrb * ncb; w += 256)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) zs[q] += (double)__uint_as_float(a[w * kActRec + 8 + q]);
+    block_reduce<2>(dsum, sred);
+    block_reduce<4>(zs, sred);
+    if (tid == 0) {
+        float *rec = metrics + k * GS_NUM_METRICS + GS_M_ACT;
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+            const double H = l == 0 ? H1 : H2, n = (double)B * H;
+            const double s1 = zs[2 * l], s2 = zs[2 * l + 1];
+            const double var = (s2 - s1 * s1 / n) / (n - 1.0);
+            rec[4 * l + 0] = (float)(s1 / n);
+            rec[4 * l + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
+            rec[4 * l + 2] = (float)(dsum[l] / n);
+            rec[4 * l + 3] = (float)((double)smax[l] / (double)B);
+        }
+    }
+}
+
+int launch_act_stats_fused(const Layout &L, int64_t B, int64_t n, const uint32_t *act, float *metrics, hipStream_t s)
+{
+    const int nrb = (int)(B / kTile), ncb = (L.H2 + kTile - 1) / kTile;
+    hipLaunchKernelGGL(k_act_stats_fused, dim3((unsigned)n), dim3(256), 0, s, act, nrb, ncb, L.H1, L.H2, (int)B,
+                       metrics);
+    GS_LAUNCH_CHECK("k_act_stats_fused");
+    return GS_OK;
 }
 
 int launch_gather_all(const Layout &L, int64_t B, int64_t n, const int32_t *idx, const float *obs,

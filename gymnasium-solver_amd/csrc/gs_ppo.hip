@@ -47,6 +47,8 @@ Workspace carve_workspace(void *base, const Layout &L, int64_t B)
     const int comm_slots = kXgmiMaxWG;   // the xGMI exchange writes one partial per workgroup
     w.sumsq = take((size_t)(w.n_slots > comm_slots ? w.n_slots : comm_slots));
     w.kl4 = take(4);
+    // k_mlp_act_stats parts of one step: ceil(B/16) x 2 (2 + max(H1, H2)) doubles
+    w.act_parts = (double *)take((size_t)((B + kTile - 1) / kTile) * 4 * (2 + (L.H1 > L.H2 ? L.H1 : L.H2)));
     w.bytes = off;
     return w;
 }
@@ -183,6 +185,7 @@ struct FusedWs {
     float *headsq;          // (n, H2/16 + 1, 2) role C's {policy, value} head sums of squares
     double *normsq;         // (n) squared total norm per step
     float *p1, *m1, *v1;    // the lagged chain's second parameter set (params | adam_m | adam_v)
+    uint32_t *act;          // GS_HP_ACT_STATS: (n, B/16, H2/16, kActRec) forward-workgroup records
     size_t bytes;       // whole update workspace (step + fused)
 };
 
@@ -209,6 +212,7 @@ FusedWs carve_fused(void *base, const Layout &L, int64_t B, int64_t n)
     f.p1 = (float *)take(sizeof(float) * (size_t)L.P);
     f.m1 = (float *)take(sizeof(float) * (size_t)L.P);
     f.v1 = (float *)take(sizeof(float) * (size_t)L.P);
+    f.act = (uint32_t *)take(sizeof(uint32_t) * (size_t)n * (size_t)(B / kTile) * (size_t)n_col_blocks(L.H2) * kActRec);
     f.bytes = off;
     return f;
 }
@@ -229,6 +233,7 @@ struct StepArgs {
     LossArgs la;
     AdamArgs aa;
     bool sum_exchange;      // global mode: every rank's gradient is its share of the global mean (sum, no 1/world)
+    bool act_stats;         // GS_HP_ACT_STATS (not in global mode): activation statistics into the records
 };
 
 // glob != nullptr: gs_ppo_update_global's global-minibatch mode (include/gsamd.h)
@@ -251,6 +256,7 @@ StepArgs make_step_args(const gs_ppo_hparams &hp, const Layout &L, int64_t B, in
     a.la.target_kl = hp.target_kl;
     a.la.normalize = hp.normalize_adv;
     a.la.bf16 = (hp.flags & GS_HP_BF16) ? 1 : 0;
+    a.act_stats = (hp.flags & GS_HP_ACT_STATS) && !glob;
     const double b1 = hp.adam_beta1, b2 = hp.adam_beta2;
     a.aa.max_norm = hp.max_grad_norm;
     a.aa.one_minus_b1 = (float)(1.0 - b1);
@@ -295,6 +301,11 @@ int enqueue_step(float *P, float *G, float *M, float *V, const Layout &L, const 
     int rc = launch_fwd_hidden(P, L, ro.obs, idx, ro.T, ro.N, B, ws.x, ws.h1, ws.h2, ws.zpart, nullptr, stop, &rg, s,
                                ws.h2mask);
     if (rc) return rc;
+    // the step's activation statistics under the parameters its loss uses, before the loss kernel
+    // (which may set the KL stop: the tripping minibatch is evaluated, so it keeps its statistics)
+    if (sa.act_stats && ((rc = launch_act_stats(P, L, ro.obs, idx, ro.T, ro.N, B, ws.act_parts, s, sa.la.step_base)) ||
+                         (rc = launch_act_parts_record(L, B, ws.act_parts, stop, metrics, sa.la.step_base, s))))
+        return rc;
     rc = launch_loss(P, L, B, ws, sa.la, metrics, stop, s);
     if (rc) return rc;
     if (sa.la.kl_part) {    // global mode's KL stop: this rank's approx_kl share summed over ranks first
@@ -614,6 +625,7 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
         ff0.headsq = fw.headsq;
         ff0.normsq = fw.normsq;
         ff0.dz = ws.dz;
+        if ((hp.flags & GS_HP_ACT_STATS) && !glob) ff0.act = fw.act;
         rc = launch_gather_all(L, batch, n_minibatches, idx, ro.obs, ro.actions, ro.logprobs, ro.values,
                                ro.advantages, ro.returns, ro.T, ro.N, hp.normalize_adv, ff0, metrics, s,
                                glob ? glob->adv_stats : nullptr);
@@ -667,7 +679,9 @@ static int ppo_update(float *params, float *grads, float *adam_m, float *adam_v,
             }
         }
         StepArgs sa = make_step_args(hp, L, batch, 1);
-        return launch_metrics_all(L, batch, n_minibatches, ff0, sa.la, metrics, s);
+        const int rc3 = launch_metrics_all(L, batch, n_minibatches, ff0, sa.la, metrics, s);
+        if (rc3 || !ff0.act) return rc3;
+        return launch_act_stats_fused(L, batch, n_minibatches, ff0.act, metrics, s);
     };
     // Adam's bias corrections (computed in double on the host, exactly as
     // torch.optim.Adam's single-tensor path does) change every step; eager launches pass

@@ -16,15 +16,18 @@ import torch  # noqa: F401  (load torch's HIP runtime before the library)
 LIB_PATH = os.environ.get("GSAMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsamd.so")
 
 GS_OK, GS_E_INVALID, GS_E_HIP, GS_E_COMM = 0, -1, -2, -3
-GS_ABI_VERSION = 6          # include/gsamd.h: the argument lists this binding declares
-GS_NUM_METRICS = 24
+GS_ABI_VERSION = 7          # include/gsamd.h: the argument lists this binding declares
+GS_NUM_METRICS = 40
 METRIC_SLOTS = (
     "loss", "policy_loss", "value_loss", "entropy", "clip_fraction", "clip_fraction_vf",
     "explained_var", "kl", "approx_kl", "adv_norm_mean", "adv_norm_std", "kl_stop", "grad_norm",
     "skipped", "unevaluated", "res1",
     # pre-clip per-component gradient norms (utils/models.py:196-230)
     "gn_backbone", "gn_policy_head", "gn_value_head", "gn_mlp", "res20", "res21", "res22", "res23",
+    # GS_HP_ACT_STATS: per hooked layer {mean, std, dead_pct, dead_max} (utils/models.py:121-147)
+    *(f"act{l}_{k}" for l in range(4) for k in ("mean", "std", "dead_pct", "dead_max")),
 )
+ACT_SLOT = 24                # GS_M_ACT
 M = {name: i for i, name in enumerate(METRIC_SLOTS)}
 
 
@@ -41,6 +44,7 @@ class PPOHparams(ctypes.Structure):
 
 
 GS_HP_BF16 = 1      # include/gsamd.h: bf16 MFMA operands in the NatureCNN update
+GS_HP_ACT_STATS = 2  # include/gsamd.h: per-minibatch activation statistics into the records (GS_M_ACT)
 
 
 class RolloutView(ctypes.Structure):

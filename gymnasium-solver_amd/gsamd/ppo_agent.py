@@ -24,7 +24,7 @@ import torch
 
 import ctypes
 
-from ._lib import GS_HP_BF16, GS_NUM_METRICS, M, PPOGlobal, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
+from ._lib import ACT_SLOT, GS_HP_ACT_STATS, GS_HP_BF16, GS_NUM_METRICS, M, PPOGlobal, PPOHparams, RolloutView, RolloutViewU8, check, lib, ptr, stream_handle
 from .atari_env import DeviceAtariVecEnv
 from .config import device_env_kind
 from .cnn import DeviceCNNActorCritic
@@ -350,10 +350,20 @@ class DevicePPOAgent:
         self.prefetcher = IndexStreamPrefetcher(self.data_len, c.n_epochs, int(torch.initial_seed()), self.device)
         return None
 
+    @property
+    def device_activation_stats(self) -> bool:
+        """The update records every evaluated minibatch's activation statistics into its record
+        (GS_HP_ACT_STATS: the reference's forward hooks recorded by every training_step,
+        base_agent.py:335-347) — with track_stats, on the MLP path (the NatureCNN update computes
+        its statistics with a separate forward, _activation_stats_launch), not in global mode."""
+        return self.track_stats and not self.is_pixel and not getattr(self, "global_mode", False)
+
     def hparams(self) -> PPOHparams:
         c = self.config
         tkl = c.target_kl if c.target_kl is not None else 0.0
         flags = GS_HP_BF16 if str(getattr(c, "precision", "fp32")) == "bf16" else 0
+        if self.device_activation_stats:
+            flags |= GS_HP_ACT_STATS
         return PPOHparams(float(self.clip_range), float(self.clip_range_vf), float(self.vf_coef), float(self.ent_coef),
                           float(c.max_grad_norm if c.max_grad_norm is not None else 0.0), float(self.policy_lr),
                           0.9, 0.999, 1e-8, float(tkl), 1 if c.normalize_advantages == "batch" else 0, flags)
@@ -467,6 +477,9 @@ class DevicePPOAgent:
                                             ptr(idx), B, self.adam_step, ptr(rec), ptr(self.stop_flag),
                                             ptr(ws), self.comm, stream_handle()), "gs_ppo_minibatch_step")
         row = self._record_step(rec)
+        if self.device_activation_stats:         # training_step's hook record (base_agent.py:340-343)
+            keys = self.activation_keys()
+            self.metrics_recorder.record("train", dict(zip(keys, row[ACT_SLOT:ACT_SLOT + len(keys)].tolist())))
         if self.config.target_kl is not None and row[M["kl_stop"]]:
             self._early_stop_epoch = True
             self.adam_step -= 1              # the tripping minibatch took no optimizer step
@@ -608,7 +621,7 @@ class DevicePPOAgent:
         stream ahead of it (gs_mlp_activation_stats / gs_cnn_activation_stats; SURVEY §8b:
         diagnostics may be computed per epoch).  Off with track_stats=False."""
         self._act_pending = False
-        if self.global_mode or not self.track_stats or idx is None:
+        if self.global_mode or not self.track_stats or idx is None or self.device_activation_stats:
             return
         if self.is_pixel:
             if getattr(self, "_act_stats", None) is None:
@@ -716,7 +729,12 @@ class DevicePPOAgent:
         stepped = rec[rec[:, M["skipped"]] == 0]
         keys, slots = self.grad_norm_keys()
         self.metrics_recorder.record_rows("train", keys, stepped[:, slots])
-        if getattr(self, "_act_pending", False) and self.is_pixel:
+        if self.device_activation_stats:
+            # every evaluated minibatch's statistics (the update's GS_M_ACT slots), as the reference
+            # records them once per training_step — their epoch mean is the recorder's
+            keys = self.activation_keys()
+            self.metrics_recorder.record_rows("train", keys, live[:, ACT_SLOT:ACT_SLOT + len(keys)])
+        elif getattr(self, "_act_pending", False) and self.is_pixel:
             self.metrics_recorder.record("train", dict(zip(self.activation_keys(),
                                                            self._act_stats.cpu().numpy().tolist())))
         elif getattr(self, "_act_pending", False):

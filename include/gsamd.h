@@ -47,8 +47,9 @@ extern "C" {
  * gs_episode_window; version 5 added the obs_store argument of gs_cnn_policy_act; version 6 added
  * gs_normalize_advantages(_scratch_bytes), gs_cnn_activation_stats, gs_build_source_hash,
  * gs_comm_xgmi_reset, gs_cnn_workspace_hidden_offset / _act_offset and the parts argument of
- * gs_fc_gemm). */
-#define GS_ABI_VERSION 6
+ * gs_fc_gemm; version 7 widened the metric record to 40 floats (the GS_M_ACT activation-statistics
+ * slots of GS_HP_ACT_STATS updates). */
+#define GS_ABI_VERSION 7
 int gs_abi_version(void);
 const char *gs_last_error(void);
 /* sha256 prefix (16 hex digits) of the kernel sources this library was compiled from: path "mlp"
@@ -200,12 +201,21 @@ typedef struct gs_ppo_hparams {
  * elsewhere).  The single-step MLP entries (gs_ppo_minibatch_step, gs_ppo_loss, gs_ppo_stage)
  * stay fp32. */
 #define GS_HP_BF16 1
+/* Activation statistics per minibatch (the reference's forward hooks, utils/models.py:121-147,
+ * recorded by every BaseAgent.training_step, agents/base_agent.py:335-347): the update also writes,
+ * into the record of every minibatch whose loss it evaluates, {mean, unbiased std, dead_pct,
+ * dead_max} of each hooked layer's pre-activation output z over the minibatch's rows, under the
+ * parameters that minibatch's loss used (dead: |z| < 1e-6; dead_pct / dead_max the mean / max over
+ * neurons of the fraction of rows) — GS_M_ACT + 4 l + {0, 1, 2, 3} for layer l (MLP: backbone.0,
+ * backbone.2; NatureCNN: cnn.0, cnn.2, cnn.4, mlp.0).  gs_ppo_update / gs_ppo_minibatch_step /
+ * gs_cnn_ppo_update; not the global-minibatch entries.  Off: those slots stay 0. */
+#define GS_HP_ACT_STATS 2
 
 /* Per-minibatch metric record written by the loss kernel (floats, GS_NUM_METRICS each).
  * KL early stop (agents/base_agent.py:330-366, sticky): the minibatch whose approx_kl exceeds
  * target_kl keeps its loss metrics with KL_STOP = SKIPPED = 1 (no optimizer step); every later
  * one is zeros with SKIPPED = KL_STOP = UNEVALUATED = 1 (its loss was never computed). */
-#define GS_NUM_METRICS 24
+#define GS_NUM_METRICS 40
 enum gs_metric_slot {
     GS_M_LOSS = 0, GS_M_POLICY_LOSS, GS_M_VALUE_LOSS, GS_M_ENTROPY, GS_M_CLIP_FRAC,
     GS_M_CLIP_FRAC_VF, GS_M_EXPLAINED_VAR, GS_M_KL, GS_M_APPROX_KL, GS_M_ADV_NORM_MEAN,
@@ -214,7 +224,9 @@ enum gs_metric_slot {
      * at agents/base_agent.py:607-608): MLP backbone | NatureCNN cnn trunk, policy_head,
      * value_head, and the NatureCNN mlp (fc) trunk (0 for the MLP policy) */
     GS_M_GN_BACKBONE, GS_M_GN_POLICY_HEAD, GS_M_GN_VALUE_HEAD, GS_M_GN_MLP,
-    GS_M_RES20, GS_M_RES21, GS_M_RES22, GS_M_RES23
+    GS_M_RES20, GS_M_RES21, GS_M_RES22, GS_M_RES23,
+    /* GS_HP_ACT_STATS: 4 layers x {mean, std, dead_pct, dead_max} of the pre-activation outputs */
+    GS_M_ACT = 24
 };
 
 size_t gs_ppo_workspace_bytes(gs_mlp_dims dims, int64_t batch);

@@ -76,6 +76,28 @@ def forward(flat, dims, obs, bf16=False):
     return logits.astype(F32), value.astype(F32), acts
 
 
+def activation_stats(flat, dims, obs, bf16=False):
+    """The forward hooks' statistics of the backbone's Linear layers (utils/models.py:121-147,
+    registered on backbone.0 / backbone.2): for each layer's pre-activation output z (B, H) —
+    mean and unbiased std over all of z, and the per-neuron fraction of rows with |z| < 1e-6,
+    averaged (dead_pct) and maximised (dead_max) over neurons.  Returns [mean, std, dead_pct,
+    dead_max] per layer, flattened (the GS_M_ACT slot order); float64 statistics of the float32 z."""
+    P = unflatten(flat, dims)
+    x = np.asarray(obs, F32)
+    out = []
+    for i in range(len(dims) - 2):
+        W, b = P[f"backbone.{2 * i}.weight"], P[f"backbone.{2 * i}.bias"]
+        if bf16 and i > 0:
+            z = ((bf16_round(x) @ bf16_round(W).T).astype(F32) + b).astype(F32)
+        else:
+            z = (x @ W.T + b).astype(F32)
+        zd = z.astype(np.float64)
+        dead = (np.abs(z) < F32(1e-6)).mean(axis=0)
+        out += [zd.mean(), zd.std(ddof=1), dead.mean(), dead.max()]
+        x = np.maximum(z, F32(0))
+    return np.array(out, np.float64)
+
+
 def log_softmax(logits):
     m = logits.max(axis=1, keepdims=True)
     z = logits - m

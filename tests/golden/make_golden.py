@@ -419,7 +419,19 @@ def make_trajectory_rollnorm():
     make_trajectory(out_name="trajectory_rollnorm.npz", normalize="rollout")
 
 
-def make_trajectory(target_kl=None, out_name="trajectory.npz", normalize="batch"):
+def make_trajectory_stats():
+    """The trajectory with the reference's per-training-step diagnostics recorded as
+    BaseAgent.training_step records them (agents/base_agent.py:330-366): the forward hooks'
+    activation statistics of every evaluated minibatch (utils/models.py:121-147, 184-190) and the
+    pre-clip gradient norms of every stepped one (base_agent.py:607-608); the hyper-parameters
+    logged at every epoch start (_log_hyperparameters, base_agent.py:302,
+    hyperparameter_mixin.py:90-103); and a linear policy_lr schedule applied by the reference's
+    HyperparameterSchedulerCallback through _change_optimizers_lr (callback_builder.py:108-113),
+    so hp/policy_lr and the Adam step size change between epochs."""
+    make_trajectory(out_name="trajectory_stats.npz", stats=True, lr_schedule=(1e-3, 2e-4, 0.0, 96.0))
+
+
+def make_trajectory(target_kl=None, out_name="trajectory.npz", normalize="batch", stats=False, lr_schedule=None):
     """CartPole-v1:ppo shapes (C1: N=8, T=32, B=256, E=20) for 3 rollouts, through the
     reference's own training-step logic (agents/base_agent.py:330-366): the sticky KL early
     stop (`_early_stop_epoch`, never reset) skips the triggering minibatch's optimizer step and
@@ -440,12 +452,33 @@ def make_trajectory(target_kl=None, out_name="trajectory.npz", normalize="batch"
     agent, recs = _agent(model, cfg)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     traj_holder = {}
+    hp_recs, act_recs, gn_recs, bounds = [], [], [], []
+    sched = None
+    if stats:
+        # the agent attributes _log_hyperparameters / _change_optimizers_lr read
+        agent.n_epochs, agent.policy_lr = E, opt.param_groups[0]["lr"]
+        agent.optimizers = lambda: opt
+        recorder = agent.metrics_recorder
+        rec_hp = types.SimpleNamespace(record=lambda ns, d: hp_recs.append(dict(d)))
+    if lr_schedule is not None:
+        from trainer_callbacks.hyperparameter_scheduler import HyperparameterSchedulerCallback
+        sv, ev, s0, s1 = lr_schedule
+        sched = HyperparameterSchedulerCallback(schedule="linear", parameter="policy_lr", start_value=sv, end_value=ev,
+                                                start_step=s0, end_step=s1,
+                                                set_value_fn=lambda m, v: m._change_optimizers_lr(v))
+        sched_module = types.SimpleNamespace(get_rollout_collector=lambda stage: collector,
+                                             _change_optimizers_lr=agent._change_optimizers_lr)
     from utils.random import get_global_torch_generator
     loader = None
     rec = {k: [] for k in ["actions", "logp", "values", "adv", "ret", "obs", "rewards", "dones", "order", "losses"]}
     evaluated, stepped, roll_metrics, action_dist = [], [], [], []
     early_stop = False                 # BaseAgent._early_stop_epoch: set once, never reset
     for epoch in range(3):
+        if stats:               # on_train_epoch_start -> _log_hyperparameters (base_agent.py:302)
+            agent.metrics_recorder = rec_hp
+            agent._log_hyperparameters()
+            agent.metrics_recorder = recorder
+            bounds.append((len(act_recs), len(gn_recs)))
         traj = collector.collect()
         traj_holder["t"] = traj
         m = collector.get_metrics()
@@ -463,7 +496,11 @@ def make_trajectory(target_kl=None, out_name="trajectory.npz", normalize="batch"
                 rec["losses"].append(np.nan)
                 continue
             opt.zero_grad()
+            model._track_activations = stats         # BaseAgent.training_step (base_agent.py:336-347)
             res = agent.losses_for_batch(batch, bi)
+            if stats:
+                act_recs.append(model.compute_activation_stats())
+                model._track_activations = False
             evaluated.append(1)
             rec["losses"].append(float(res["loss"].item()))
             if res["early_stop_epoch"]:
@@ -471,9 +508,13 @@ def make_trajectory(target_kl=None, out_name="trajectory.npz", normalize="batch"
                 stepped.append(0)
                 continue
             res["loss"].backward()
+            if stats:                                # _backpropagate_and_step (base_agent.py:607-608)
+                gn_recs.append(model.compute_grad_norms())
             torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
             opt.step()
             stepped.append(1)
+        if sched is not None:      # HyperparameterSchedulerCallback.on_train_epoch_end
+            sched.on_train_epoch_end(None, sched_module)
         loader.sampler.set_epoch(epoch)
         order = np.asarray(list(iter(loader.sampler)), np.int64)
         rec["order"].append(order)
@@ -497,7 +538,17 @@ def make_trajectory(target_kl=None, out_name="trajectory.npz", normalize="batch"
     out["roll_metric_names"], out["roll_metric_values"] = _metrics_arrays(roll_metrics)
     out["action_dist"] = np.asarray(action_dist)
     out["train_metric_names"], out["train_metric_values"] = _metrics_arrays(recs)
-    if target_kl is None and normalize == "batch":
+    if stats:
+        # per-record values and the per-epoch means of each key (MetricsRecorder.compute_epoch_means)
+        out["hp_names"], out["hp_values"] = _metrics_arrays(hp_recs)
+        out["act_names"], out["act_values"] = _metrics_arrays(act_recs)
+        out["gn_names"], out["gn_values"] = _metrics_arrays(gn_recs)
+        ends = bounds[1:] + [(len(act_recs), len(gn_recs))]
+        out["act_epoch_means"] = np.stack([out["act_values"][a0:a1].mean(axis=0)
+                                           for (a0, _), (a1, _) in zip(bounds, ends)])
+        out["gn_epoch_means"] = np.stack([out["gn_values"][g0:g1].mean(axis=0) for (_, g0), (_, g1) in zip(bounds, ends)])
+        out["lr_schedule"] = np.array(lr_schedule if lr_schedule is not None else (0.0,) * 4, np.float64)
+    if target_kl is None and normalize == "batch" and not stats:
         # evaluate_episodes on a second collector (the device agent's "val" stage: same env
         # shape, seed + 1000), deterministic, 20 episodes over 8 envs
         eval_env = SyntheticVecEnv(n_envs=N, obs_dim=D, n_actions=A, episode_len=20, seed=42 + 1000,

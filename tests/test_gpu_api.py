@@ -75,6 +75,14 @@ def test_losses_for_batch_on_reference_tensor_batch(golden, cuda, tag):
     assert set(gn) <= set(got), set(gn) - set(got)
     for k in gn:
         np.testing.assert_allclose(got[k], gn[k], rtol=1e-5, err_msg=k)
+    # training_step's forward-hook record (base_agent.py:335-347): the single-step chain writes the
+    # minibatch's activation statistics into its record (GS_HP_ACT_STATS)
+    acts = dict(zip([str(x) for x in z[f"{tag}/activation_names"]], z[f"{tag}/activation_values"]))
+    assert set(acts) <= set(got), set(acts) - set(got)
+    B = len(z[f"{tag}/actions"])
+    for k, want in acts.items():
+        tol = 1.0 / B if k.endswith(("dead_pct", "dead_max")) else 1e-5 + 1e-5 * abs(want)
+        assert abs(got[k] - want) <= tol, (k, got[k], want)
 
 
 def _replay_trajectory(agent, z, cuda, check_metrics=True):
@@ -344,3 +352,45 @@ def test_normalize_advantages_kernel_vs_reference(golden, cuda, case):
             a = (rng.standard_normal(shape) * 1.5 + 4.0).astype(np.float32)
             y, _ = run(a)
             assert np.array_equal(y.view(np.uint32), normalize_advantages_rollout(a).view(np.uint32)), shape
+
+
+def test_training_diagnostics_vs_reference(golden, cuda):
+    """The per-epoch diagnostics the reference's BaseAgent records (trajectory_stats.npz, made by
+    the reference's own code): opt/activations/* as the epoch mean over every evaluated minibatch's
+    forward-hook values (utils/models.py:121-147 via training_step, base_agent.py:335-347 — the
+    device update writes each minibatch's statistics into its record, GS_HP_ACT_STATS),
+    opt/grads/norm/* over the stepped minibatches (base_agent.py:607-608), and hp/* logged at every
+    epoch start (base_agent.py:302, hyperparameter_mixin.py:90-103) under a linear policy_lr schedule
+    (HyperparameterSchedulerCallback -> _change_optimizers_lr), so hp/policy_lr and the Adam step
+    size change between epochs.  Bars: activation mean / std 1e-5 (+1e-5 relative), dead fractions
+    1/B, grad norms 1e-4 relative, hp exact, losses 1e-4 (the north-star bar)."""
+    from gsamd._lib import M
+    z = golden("trajectory_stats.npz")
+    N, T, E, B, D, A = (int(x) for x in z["dims"])
+    sv, ev, s0, s1 = (float(x) for x in z["lr_schedule"])
+    sched = {"policy_lr": {"schedule": "linear", "start_value": sv, "end_value": ev, "start": None,
+                           "end": s1 * N, "warmup": 0.0}}
+    agent = _trajectory_agent(cuda, z, schedules=sched)
+    assert agent.device_activation_stats
+    coll = agent.get_rollout_collector("train")
+    hp_names, act_names, gn_names = ([str(x) for x in z[k]] for k in ("hp_names", "act_names", "gn_names"))
+    losses = []
+    for ep in range(3):
+        acts = torch.as_tensor(z["actions"][ep].reshape(N, T).T.copy()).to(cuda)
+        coll.collect(replay_actions=acts)
+        agent.update_phase()
+        torch.cuda.synchronize()
+        losses.append(agent.metrics_buf[:, M["loss"]].cpu().numpy().astype(np.float64))
+        got = agent.epoch_metrics()
+        for j, k in enumerate(hp_names):
+            assert got[k] == z["hp_values"][ep][j], (ep, k, got[k], z["hp_values"][ep][j])
+        for j, k in enumerate(act_names):
+            want = z["act_epoch_means"][ep][j]
+            tol = 1.0 / B if k.endswith(("dead_pct", "dead_max")) else 1e-5 + 1e-5 * abs(want)
+            assert abs(got[k] - want) <= tol, (ep, k, got[k], want)
+        for j, k in enumerate(gn_names):
+            np.testing.assert_allclose(got[k], z["gn_epoch_means"][ep][j], rtol=1e-4, err_msg=f"{ep} {k}")
+    np.testing.assert_allclose(np.concatenate(losses), z["losses"], atol=1e-4, rtol=0)
+    p = agent.policy_model.params.cpu().numpy().astype(np.float64)
+    p_ref = z["params_final"].astype(np.float64)
+    assert np.linalg.norm(p - p_ref) / np.linalg.norm(p_ref) < 1e-4

@@ -382,8 +382,11 @@ def test_update_first_minibatches_vs_numpy_oracle(cuda, use_graph):
     dims = (pm.obs_dim, pm.hidden_dims[0], pm.hidden_dims[1], pm.n_actions)
     p = pm.params.cpu().numpy()
     n, B = 8, agent.batch_size
+    from gsamd._lib import GS_HP_ACT_STATS, ACT_SLOT
+    hp = agent.hparams()
+    hp.flags |= GS_HP_ACT_STATS          # every minibatch's activation statistics into its record
     check(lib.gs_ppo_update(pm.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
-                            agent.adam_v.data_ptr(), pm.dims, agent.hparams(), coll.buffer.view(), idx_dev.data_ptr(),
+                            agent.adam_v.data_ptr(), pm.dims, hp, coll.buffer.view(), idx_dev.data_ptr(),
                             B, n, 0, agent.metrics_buf.data_ptr(), agent.stop_flag.data_ptr(),
                             agent.workspace.data_ptr(), agent.workspace.numel(), None, 1 if use_graph else 0,
                             torch.cuda.current_stream().cuda_stream), "gs_ppo_update")
@@ -404,6 +407,13 @@ def test_update_first_minibatches_vs_numpy_oracle(cuda, use_graph):
         loss, _, g = R.ppo_loss_and_grads(p, dims, *(f[rows] for f in fields), clip=cfg.clip_range,
                                           clip_vf=cfg.clip_range_vf, vf_coef=cfg.vf_coef, ent_coef=cfg.ent_coef)
         np.testing.assert_allclose(losses[k], loss, rtol=1e-5, atol=1e-6, err_msg=f"minibatch {k}")
+        # the forward hooks' statistics of this step's rows under the parameters its loss used
+        # (utils/models.py:121-147): mean / std 1e-5, dead fractions 1/B
+        st = R.activation_stats(p, dims, fields[0][rows])
+        got = rec[k, ACT_SLOT:ACT_SLOT + 8]
+        for j in range(8):
+            tol = 1.0 / B if j % 4 >= 2 else 1e-5 * (1.0 + abs(st[j]))
+            assert abs(got[j] - st[j]) <= tol, (k, j, got[j], st[j])
         # per-component pre-clip norms (utils/models.py:196-230), written by the next forward's
         # lagged step (the last one by k_clip_adam)
         g64 = g.astype(np.float64)
@@ -423,7 +433,7 @@ def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph
     """gs_ppo_update's fused chain (gathered fields, head combine + loss rows inside the
     forward) against the 4-launch chain on the same rollout: bit-identical parameters and
     minibatch losses within 1e-6 relative (metric sums are added in another order)."""
-    from gsamd._lib import check, lib
+    from gsamd._lib import ACT_SLOT, GS_HP_ACT_STATS, check, lib
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     out = []
@@ -437,8 +447,10 @@ def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph
         idx = agent.prefetcher.upload(0)
         small = int(lib.gs_ppo_workspace_bytes(agent.policy_model.dims, agent.batch_size))
         assert agent.workspace.numel() > small      # the BASELINE shapes have a fused chain
+        hp = agent.hparams()
+        hp.flags |= GS_HP_ACT_STATS      # both chains record the activation statistics
         check(lib.gs_ppo_update(agent.policy_model.params.data_ptr(), agent.grads.data_ptr(), agent.adam_m.data_ptr(),
-                                agent.adam_v.data_ptr(), agent.policy_model.dims, agent.hparams(), coll.buffer.view(),
+                                agent.adam_v.data_ptr(), agent.policy_model.dims, hp, coll.buffer.view(),
                                 idx.data_ptr(), agent.batch_size, agent.n_minibatches, 0, agent.metrics_buf.data_ptr(),
                                 agent.stop_flag.data_ptr(), agent.workspace.data_ptr(),
                                 agent.workspace.numel() if fused else small, None, 1 if use_graph else 0,
@@ -453,8 +465,16 @@ def test_fused_update_chain_equals_unfused(cuda, env, variant, n_envs, use_graph
     # 4-launch chain re-reads the head gradients in double (k_component_norms)
     from gsamd._lib import M
     gn = [M[k] for k in ("gn_backbone", "gn_policy_head", "gn_value_head")]
-    rest = [c for c in range(m0.shape[1]) if c not in gn]
+    act = list(range(ACT_SLOT, ACT_SLOT + 8))
+    rest = [c for c in range(m0.shape[1]) if c not in gn + act]
     np.testing.assert_allclose(m0[:, rest], m1[:, rest], rtol=1e-6, atol=1e-7)
+    # activation statistics: the fused forward's epilogue (float partial sums per workgroup, its
+    # MFMA's z2) against the unfused chain's k_mlp_act_stats (double sums, sequential z2)
+    B = 256 if env == "CartPole-v1" else 64
+    assert np.abs(m0[:, act]).sum() > 0
+    for j, c in enumerate(act):
+        tol = 1.0 / B if j % 4 >= 2 else 1e-5 * (1.0 + np.abs(m1[:, c]))
+        assert (np.abs(m0[:, c] - m1[:, c]) <= tol).all(), (c, np.abs(m0[:, c] - m1[:, c]).max())
     bad = np.argwhere(~np.isclose(m0[:, gn], m1[:, gn], rtol=1e-4, atol=1e-7))
     assert len(bad) == 0, [(int(r), gn[c], m0[r], m1[r]) for r, c in bad[:4]]
 

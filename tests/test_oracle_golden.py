@@ -179,3 +179,22 @@ def test_adv_norm_model_above_2_24_matches_numpy():
     a = (np.random.default_rng(5).standard_normal((4097, 4096)) * 1.5 + 4.0).astype(np.float32)
     assert a.size > 2 ** 24
     assert np.array_equal(normalize_advantages_model(a).view(np.uint32), normalize_advantages_rollout(a).view(np.uint32))
+
+
+@pytest.mark.parametrize("tag", ["cartpole", "lunar_ent"])
+def test_activation_stats_oracle_vs_reference(golden, tag):
+    """oracle/ppo_ref.py activation_stats against the reference's forward-hook values recorded on
+    the same batch (ppo_step.npz activation_names / values: utils/models.py:121-147 on backbone.0 /
+    backbone.2): mean / std within 1e-6 relative, dead fractions exact."""
+    from oracle import ppo_ref as R
+    z = golden("ppo_step.npz")
+    D, H1, H2, A, B = (int(x) for x in z[f"{tag}/dims"])
+    got = R.activation_stats(z[f"{tag}/params0"], (D, H1, H2, A), z[f"{tag}/obs"])
+    ref = dict(zip([str(x) for x in z[f"{tag}/activation_names"]], z[f"{tag}/activation_values"]))
+    for li, layer in enumerate(("backbone.0", "backbone.2")):
+        for ki, k in enumerate(("mean", "std", "dead_pct", "dead_max")):
+            want = ref[f"opt/activations/{layer}/{k}"]
+            if ki >= 2:
+                assert got[4 * li + ki] == want, (layer, k)
+            else:
+                np.testing.assert_allclose(got[4 * li + ki], want, rtol=1e-6, atol=1e-9, err_msg=f"{layer}/{k}")

@@ -51,3 +51,21 @@ def test_config_schedule_forms():
     assert a[0].end_step == 10_000.0
     with pytest.raises(ValueError):
         build_schedulers({"n_envs": c.schedules["policy_lr"]}, 1e5, 8)
+
+
+def test_scheduled_lr_matches_reference_hp_log():
+    """trajectory_stats.npz's hp/policy_lr per epoch (the reference's HyperparameterSchedulerCallback
+    applied at each epoch end through _change_optimizers_lr, logged by _log_hyperparameters at the
+    next epoch start) equals gsamd.schedules on the same spec, bit for bit."""
+    import os
+    import numpy as np
+    from gsamd.schedules import build_schedulers
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trajectory_stats.npz"))
+    N, T = (int(x) for x in z["dims"][:2])
+    sv, ev, s0, s1 = (float(x) for x in z["lr_schedule"])
+    sch = build_schedulers({"policy_lr": {"schedule": "linear", "start_value": sv, "end_value": ev, "start": None,
+                                          "end": s1 * N, "warmup": 0.0}}, None, N)[0]
+    names = [str(x) for x in z["hp_names"]]
+    lr = [float(row[names.index("hp/policy_lr")]) for row in z["hp_values"]]
+    assert lr[0] == sv
+    assert [sch.value(T * (e + 1)) for e in range(len(lr) - 1)] == lr[1:]
