@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(_lib.lib, n), f"libgsamd.so does not export {n}"
     assert set(names) == set(_lib.EXPORTED)
-    assert _lib.lib.gs_abi_version() == _lib.GS_ABI_VERSION == 6
+    assert _lib.lib.gs_abi_version() == _lib.GS_ABI_VERSION == 7
 
 
 def test_library_is_gfx950_code_object():
