@@ -101,6 +101,12 @@ struct CnnWs {
     float *pre_stats;      // [kPreChunk][2]: their advantage mean / std
     uint16_t *pbf;         // [P]: the parameters as bf16, the weight operands of a bf16 update
                            // with bf16 trunk storage (act16_trunk), refreshed by every Adam step
+    // GS_HP_ACT_STATS: the hooked layers' (cnn.0, cnn.2, cnn.4, mlp.0) per-neuron dead counters
+    // (zero between steps: the step's reducer clears what it read) and per-wave {sum z, sum z^2}
+    // slots of the forward epilogues; act_fb: the 16 statistics of the fallback (separate forward)
+    uint32_t *act_cnt;
+    float *act_part;
+    double *act_fb;
     size_t bytes;
 };
 
@@ -142,6 +148,26 @@ __host__ __device__ inline int64_t head_part_stride(const CnnLayout &L)
 __host__ __device__ inline int64_t head_part_out(const CnnLayout &L)
 {
     return (int64_t)(L.A + 1) * (L.HID + 1) + L.HID;
+}
+
+// GS_HP_ACT_STATS bookkeeping: the hooked layers' neuron counts (cnn.0 / cnn.2 / cnn.4 outputs,
+// mlp.0) and the statistics slots a stats-epilogue forward of R rows can write per layer (the
+// largest over the precision modes)
+inline int act_neurons(const CnnLayout &L, int l)
+{
+    return l == 0 ? L.h1 * L.w1 * L.c1 : l == 1 ? L.h2 * L.w2 * L.c2 : l == 2 ? L.h3 * L.w3 * L.c3 : L.HID;
+}
+inline int64_t act_neurons_total(const CnnLayout &L)
+{
+    return (int64_t)act_neurons(L, 0) + act_neurons(L, 1) + act_neurons(L, 2) + act_neurons(L, 3);
+}
+inline int64_t act_slots_cap(const CnnLayout &L, int64_t R)
+{
+    int64_t m = fc_fwd_act_slots(R, L.HID);
+    for (int layer = 1; layer <= 3; ++layer)
+        for (int mode = 0; mode < 3; ++mode)
+            m = std::max<int64_t>(m, conv_fwd_act_slots(layer, (int)R, mode > 0, mode > 1));
+    return m;
 }
 
 CnnWs carve(void *base, const CnnLayout &L, int64_t R)
@@ -200,6 +226,9 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
         const int64_t hparts = (R + kHeadRows - 1) / kHeadRows * head_part_stride(L);
         w.parts = (float *)take(sizeof(float) * std::max({wparts, cparts, gparts, hparts}));
     }
+    w.act_cnt = (uint32_t *)take(sizeof(uint32_t) * (size_t)act_neurons_total(L));
+    w.act_part = (float *)take(sizeof(float) * 2 * (size_t)act_slots_cap(L, R) * 4);
+    w.act_fb = (double *)take(sizeof(double) * 16);
     w.bytes = off;
     return w;
 }
@@ -1473,13 +1502,15 @@ inline const void *wop(const float *P, const CnnWs &w, int64_t off, bool xh)
 // (obs_copy: the rollout's obs row, written by conv1 from the frames it loads anyway; xh: a1 / a2
 // / a3 stored as bf16, act16_trunk)
 int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  bool bf, uint8_t *obs_copy = nullptr, bool xh = false)
+                  bool bf, uint8_t *obs_copy = nullptr, bool xh = false, const ActOut *ao = nullptr)
 {
     int rc;
     GS_REQUIRE(!xh || act16_trunk(L, bf, true), "bf16 activation storage: LDS trunk kernels only");
+    // ao (GS_HP_ACT_STATS): the LDS kernels' statistics epilogues (act_stats_epilogues checked it)
+    const ActOut none{};
     if (conv1_lds_supported(L.C, L.H, L.W)) {
         if ((rc = conv1_lds_fwd(s, bf, xh, (int)R, fs.obs, fs.idx, fs.T, fs.N, wop(P, w, L.oW1, xh), P + L.ob1, w.a1,
-                                obs_copy)))
+                                obs_copy, ao ? ao[0] : none)))
             return rc;
     } else {
         if (obs_copy && obs_copy != fs.obs)
@@ -1487,12 +1518,14 @@ int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
         if ((rc = conv_fwd_u8(s, bf, geom1(L, R), fs, P + L.oW1, P + L.ob1, w.a1))) return rc;
     }
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_fwd(s, bf, xh, 2, (int)R, w.a1, wop(P, w, L.oW2, xh), P + L.ob2, w.a2))) return rc;
+        if ((rc = conv23_lds_fwd(s, bf, xh, 2, (int)R, w.a1, wop(P, w, L.oW2, xh), P + L.ob2, w.a2, ao ? ao[1] : none)))
+            return rc;
     } else if ((rc = conv_fwd_nhwc(s, bf, geom2(L, R), w.a1, P + L.oW2, P + L.ob2, w.a2))) {
         return rc;
     }
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_fwd(s, bf, xh, 3, (int)R, w.a2, wop(P, w, L.oW3, xh), P + L.ob3, w.a3))) return rc;
+        if ((rc = conv23_lds_fwd(s, bf, xh, 3, (int)R, w.a2, wop(P, w, L.oW3, xh), P + L.ob3, w.a3, ao ? ao[2] : none)))
+            return rc;
     } else if ((rc = conv_fwd_nhwc(s, bf, geom3(L, R), w.a2, P + L.oW3, P + L.ob3, w.a3))) {
         return rc;
     }
@@ -1501,9 +1534,10 @@ int forward_convs(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
 
 // conv trunk + fc for R rows (h)
 int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, const CnnWs &w, hipStream_t s,
-                  bool bf, bool lib_fc = false, const int32_t *stop = nullptr, bool xh = false)
+                  bool bf, bool lib_fc = false, const int32_t *stop = nullptr, bool xh = false,
+                  const ActOut *ao = nullptr)
 {
-    int rc = forward_convs(P, L, fs, R, w, s, bf, nullptr, xh);
+    int rc = forward_convs(P, L, fs, R, w, s, bf, nullptr, xh, ao);
     if (rc) return rc;
     // fc: h = relu(a3 Wf^T + bf): the fc kernels (gs_fc.hip, bias + ReLU epilogue; fc_path: the
     // update), else the engine's split-K partials summed with the bias + ReLU epilogue
@@ -1511,7 +1545,7 @@ int forward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_
     // sweep but slower inside the update: 43.6 + 5.0 us vs 46.0, round 5 — not used here)
     if (lib_fc)
         return fc_gemm(s, 0, bf, R, L.HID, L.F, w.a3, L.F, wop(P, w, L.oWf, xh), L.F, w.h, L.HID, P + L.obf, stop,
-                       nullptr, xh);
+                       nullptr, xh, ao ? ao[3] : ActOut{});
     const int sf = splits_for(R, L.HID, L.F);
     if (sf == 1) {
         if ((rc = gemm_f32(s, bf, false, true, R, L.HID, L.F, w.a3, L.F, P + L.oWf, L.F, w.h, L.HID, 0.f, P + L.obf,
@@ -1833,6 +1867,98 @@ int refresh_params_bf16(const float *P, const CnnLayout &L, const gs_ppo_hparams
     return GS_OK;
 }
 
+// ---- GS_HP_ACT_STATS (the reference's forward hooks on cnn.0 / cnn.2 / cnn.4 / mlp.0,
+// utils/models.py:121-147, recorded per training step at agents/base_agent.py:335-347)
+// the update's forward kernels carry the statistics epilogues (the LDS convolutions and the fc
+// kernel at update batch sizes)
+bool act_stats_epilogues(const CnnLayout &L, int64_t B, bool lib_fc)
+{
+    return lib_fc && conv1_lds_supported(L.C, L.H, L.W) && conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2) &&
+           conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3) && B * 2 > 1024;
+}
+
+void act_outs(const CnnLayout &L, int64_t B, const CnnWs &w, ActOut (&ao)[4])
+{
+    const int64_t cap = 2 * act_slots_cap(L, B);
+    int64_t off = 0;
+    for (int l = 0; l < 4; ++l) {
+        ao[l].cnt = w.act_cnt + off;
+        ao[l].part = w.act_part + l * cap;
+        off += act_neurons(L, l);
+    }
+}
+
+// the fallback: a separate fp32 forward of the minibatch without ReLU epilogues (the trunk the
+// update then runs overwrites the activations) -> out[16] (gs_cnn_activation_stats' kernels)
+int act_stats_forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, hipStream_t s,
+                      double *out);
+
+struct CnnActRec {
+    const uint32_t *cnt[4];
+    const float *part[4];
+    int neurons[4];
+    int slots[4];
+};
+
+// one workgroup per layer: the step's dead counts (summed; max; then cleared for the next step)
+// and its slots' sums in slot order -> the record's GS_M_ACT slots, unless the KL stop left the
+// minibatch unevaluated.  fb (the fallback): the 16 statistics computed ahead, copied in.
+__global__ __launch_bounds__(256) void k_cnn_act_record(CnnActRec ar, int rows, const double *__restrict__ fb,
+                                                        float *__restrict__ rec)
+{
+    __shared__ double sred[2 * (256 + 16)];
+    __shared__ unsigned smax;
+    const int l = blockIdx.x, tid = threadIdx.x;
+    const bool live = rec[GS_M_UNEVALUATED] == 0.0f;
+    if (fb) {
+        if (live && tid < 4) rec[GS_M_ACT + 4 * l + tid] = (float)fb[4 * l + tid];
+        return;
+    }
+    uint32_t *cnt = const_cast<uint32_t *>(ar.cnt[l]);
+    if (tid == 0) smax = 0u;
+    __syncthreads();
+    double v[2] = {0.0, 0.0};
+    unsigned mx = 0u;
+    for (int j = tid; j < ar.neurons[l]; j += 256) {
+        const unsigned c = cnt[j];
+        cnt[j] = 0u;
+        v[0] += (double)c;
+        mx = c > mx ? c : mx;
+    }
+    atomicMax(&smax, mx);
+    double z[2] = {0.0, 0.0};
+    for (int j = tid; j < ar.slots[l]; j += 256) {
+        z[0] += (double)ar.part[l][2 * j];
+        z[1] += (double)ar.part[l][2 * j + 1];
+    }
+    wg_reduce<2>(v, sred);
+    wg_reduce<2>(z, sred);
+    if (tid == 0 && live) {
+        const double n = (double)rows * (double)ar.neurons[l];
+        const double var = (z[1] - z[0] * z[0] / n) / (n - 1.0);
+        rec[GS_M_ACT + 4 * l + 0] = (float)(z[0] / n);
+        rec[GS_M_ACT + 4 * l + 1] = (float)sqrt(var > 0.0 ? var : 0.0);
+        rec[GS_M_ACT + 4 * l + 2] = (float)(v[0] / n);
+        rec[GS_M_ACT + 4 * l + 3] = (float)((double)smax / (double)rows);
+    }
+}
+
+int act_record(const CnnLayout &L, int64_t B, bool bf, bool xh, const CnnWs &w, bool epi, float *rec, hipStream_t s)
+{
+    CnnActRec ar{};
+    ActOut ao[4];
+    act_outs(L, B, w, ao);
+    for (int l = 0; l < 4; ++l) {
+        ar.cnt[l] = ao[l].cnt;
+        ar.part[l] = ao[l].part;
+        ar.neurons[l] = act_neurons(L, l);
+        ar.slots[l] = l < 3 ? conv_fwd_act_slots(l + 1, (int)B, bf, xh) : fc_fwd_act_slots(B, L.HID);
+    }
+    hipLaunchKernelGGL(k_cnn_act_record, dim3(4), dim3(256), 0, s, ar, (int)B, epi ? nullptr : w.act_fb, rec);
+    GS_LAUNCH_CHECK("k_cnn_act_record");
+    return GS_OK;
+}
+
 // pre / pre_stats (the local update's fused path): this minibatch's fields and advantage
 // statistics, gathered ahead by k_cnn_gather_chunk; the head + loss kernel reads them contiguously
 int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const gs_ppo_hparams &hp,
@@ -1864,8 +1990,17 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         // the fc layer's forward, weight and input gradients on the fc kernels (gs_fc.hip; dbf comes
         // from the head kernels), in the operand precision of the update
         const bool lib_fc = fc_path(L, B);
-        if ((rc = forward_trunk(P, L, fs, B, w, s, bf, lib_fc, stop, xh))) return rc;
+        // GS_HP_ACT_STATS: the forward epilogues record the hooked layers' statistics, or (shapes
+        // without them) a separate fp32 forward computes them first, on the same parameters
+        const bool stats = (hp.flags & GS_HP_ACT_STATS) && !gl;
+        const bool epi = stats && act_stats_epilogues(L, B, lib_fc);
+        ActOut ao[4];
+        if (epi) act_outs(L, B, w, ao);
+        if (stats && !epi && (rc = act_stats_forward(P, L, fs, B, w, s, w.act_fb))) return rc;
+        if ((rc = forward_trunk(P, L, fs, B, w, s, bf, lib_fc, stop, xh, epi ? ao : nullptr))) return rc;
         if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s, bf, xh))) return rc;
+        // after the loss kernel: the record says whether this minibatch was evaluated
+        if (stats && (rc = act_record(L, B, bf, xh, w, epi, metrics, s))) return rc;
         if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc, xh))) return rc;
     } else {
         hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
@@ -2048,6 +2183,8 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     // the fused head + loss path reads each minibatch's fields gathered ahead (kPreChunk at a time)
     const bool pre = head_fused(L, batch);
     if ((rc = refresh_params_bf16(params, L, hp, batch, w, s))) return rc;
+    if (hp.flags & GS_HP_ACT_STATS)      // the statistics epilogues' dead counters start at zero
+        GS_HIP(hipMemsetAsync(w.act_cnt, 0, sizeof(uint32_t) * (size_t)act_neurons_total(L), s));
     for (int64_t k = 0; k < n_minibatches; ++k) {
         const int64_t slot = k % kPreChunk;
         if (pre && slot == 0) {
@@ -2077,6 +2214,15 @@ extern "C" int gs_cnn_activation_stats(const float *params, gs_cnn_dims dims, gs
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
     const FrameSrc fs{ro.obs, idx, ro.T, ro.N};
+    return act_stats_forward(params, L, fs, batch, w, s, stats_out);
+}
+
+namespace gs {
+namespace {
+int act_stats_forward(const float *params, const CnnLayout &L, const FrameSrc &fs, int64_t batch, const CnnWs &w,
+                      hipStream_t s, double *stats_out)
+{
+    int rc;
     // the trunk on the generic fp32 engine without the ReLU epilogues: each layer's output is its
     // pre-activation (what the reference's Conv2d / Linear hooks see); the statistics kernel then
     // applies the ReLU in place for the next layer
@@ -2109,3 +2255,6 @@ extern "C" int gs_cnn_activation_stats(const float *params, gs_cnn_dims dims, gs
     GS_LAUNCH_CHECK("k_act_stats_final");
     return GS_OK;
 }
+
+}  // namespace
+}  // namespace gs

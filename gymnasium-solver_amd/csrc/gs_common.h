@@ -409,4 +409,33 @@ __device__ __forceinline__ void act_st(act_t<XH> *p, int64_t i, float v)
     else p[i] = v;
 }
 
+// GS_HP_ACT_STATS in the NatureCNN forward epilogues (the reference's forward hooks on cnn.0 / cnn.2
+// / cnn.4 / mlp.0, utils/models.py:121-147): per neuron of the layer (a sample's output index) the
+// count of pre-activation values |z| < 1e-6 — integer atomics, so the counts do not depend on the
+// order — and per wave {sum z, sum z^2} (float) in slot [workgroup * 4 + wave], added in slot
+// order by the step's reducer (k_cnn_act_record), which also zeroes the counts it read.
+struct ActOut {
+    uint32_t *cnt;
+    float *part;
+};
+__device__ __forceinline__ void act_acc(const ActOut &ao, float z, int64_t neuron, float &s, float &q)
+{
+    s += z;
+    q += z * z;
+    if (fabsf(z) < 1e-6f) atomicAdd(ao.cnt + neuron, 1u);
+}
+// every lane of the wave calls it (the xor tree needs the whole wave); lane 0 writes the slot
+__device__ __forceinline__ void act_flush(const ActOut &ao, int64_t slot, float s, float q)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        q += __shfl_xor(q, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ao.part[2 * slot] = s;
+        ao.part[2 * slot + 1] = q;
+    }
+}
+
 }  // namespace gs

@@ -27,8 +27,9 @@ bool conv1_lds_supported(int C, int H, int W);
 // bf16 (gs_common.h act_bf16: the operand bits the bf16 mode rounds to anyway) and the forward /
 // input-gradient filters come from the update's bf16 weight copy, so those pointers are void:
 // fp32 or bf16 elements by xh (biases stay fp32)
+// ao (GS_HP_ACT_STATS, update batches only): the forward's epilogue records the activation statistics
 int conv1_lds_fwd(hipStream_t s, bool bf, bool xh, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
-                  const void *W1, const float *b1, void *out, uint8_t *obs_copy = nullptr);
+                  const void *W1, const float *b1, void *out, uint8_t *obs_copy = nullptr, ActOut ao = ActOut{});
 // dW1 = sum_rows dA1^T . patches, db1 = column sums of dA1; parts: kConv1WgradWG x (32*256 + 32) floats
 int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
                     const float *dA, float *parts, float *dW1, float *db1);
@@ -37,7 +38,9 @@ int conv1_lds_wgrad_parts();
 // NHWC, LDS-resident samples (layer = 2 or 3)
 bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cout);
 int conv23_lds_fwd(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const void *Wt,
-                   const float *bias, void *out);
+                   const float *bias, void *out, ActOut ao = ActOut{});
+// statistics slots (workgroup x 4 waves) of an update batch's stats-epilogue forward of layer 1 / 2 / 3
+int conv_fwd_act_slots(int layer, int R, bool bf, bool xh);
 // input gradient of conv2 / conv3 masked by ReLU'(act) (act = the layer's input activation):
 // dX = (dY conv^T W) * (act > 0), NHWC fp32
 int conv23_lds_dgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const float *dY, const void *act,

@@ -218,11 +218,13 @@ __device__ __forceinline__ void stage_bands_bf16(uint16_t *fr, const uint8_t *__
 // loaded once for all of them
 // XH: a1 stored as bf16 and W1 read from the update's bf16 weight copy (bf16 updates,
 // gs_common.h act_bf16)
-template <class G, bool BF = false, int SPB = 1, bool XH = false>
+// AS (GS_HP_ACT_STATS): the epilogue also records the activation statistics of the pre-activation
+// outputs (gs_common.h ActOut; neuron = output position x 32 + filter)
+template <class G, bool BF = false, int SPB = 1, bool XH = false, bool AS = false>
 __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ obs, const int32_t *__restrict__ idx,
                                                    int64_t T, int64_t N, const act_t<XH> *__restrict__ W1,
                                                    const float *__restrict__ b1, act_t<XH> *__restrict__ out,
-                                                   uint8_t *__restrict__ obs_copy, int R)
+                                                   uint8_t *__restrict__ obs_copy, int R, ActOut ao = ActOut{})
 {
     static_assert(SPB == 1 || BF, "several samples per workgroup: bf16 staging only");
     static_assert(!XH || BF, "bf16 activation storage: bf16 operands only");
@@ -269,6 +271,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
         const int oy = pc / G::OW, ox = pc - oy * G::OW;
         abase[t] = (oy * G::S + (lq >> 1)) * G::W + ox * G::S + 4 * (lq & 1);
     }
+    float as_s = 0.0f, as_q = 0.0f;                     // AS: this lane's sums of z and z^2
 #pragma unroll
     for (int q = 0; q < SPB; ++q) {
         const int r = r0 + q;
@@ -331,10 +334,12 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
                 if (p < P) {
                     const float v = acc[t][j] + bb;
                     act_st<XH>(o, (int64_t)p * G::CO + co, v > 0.f ? v : 0.f);
+                    if constexpr (AS) act_acc(ao, v, (int64_t)(oy0 * G::OW + p) * G::CO + co, as_s, as_q);
                 }
             }
         }
     }
+    if constexpr (AS) act_flush(ao, (int64_t)blockIdx.x * 4 + wave, as_s, as_q);
 }
 
 // dW1[co][tap] and db1[co] partials of one workgroup over units blockIdx.x, + gridDim.x, ...
@@ -753,9 +758,12 @@ constexpr int kConvFwdBurst = 16;      // float4 loads per thread per staging bu
 // XH (bf16 updates): input and output activations stored as bf16 (gs_common.h act_bf16: the
 // staging copies the stored operand bits, the epilogue rounds once) and the filters read from the
 // update's bf16 weight copy
-template <class G, bool BF = false, int FS = 1, bool XH = false>
+// AS (GS_HP_ACT_STATS): the epilogue also records the activation statistics of the pre-activation
+// outputs (gs_common.h ActOut; neuron = output position x 64 + filter)
+template <class G, bool BF = false, int FS = 1, bool XH = false, bool AS = false>
 __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ in, int R, const act_t<XH> *__restrict__ Wt,
-                                                  const float *__restrict__ bias, act_t<XH> *__restrict__ out)
+                                                  const float *__restrict__ bias, act_t<XH> *__restrict__ out,
+                                                  ActOut ao = ActOut{})
 {
     static_assert(FS == 1 || FS == 2 || FS == 4, "filter split");
     static_assert(!XH || BF, "bf16 activation storage: bf16 operands only");
@@ -915,7 +923,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
                 for (int j = 0; j < 4; ++j)
                     red[((((kr - 1) * NFB + wave % NFB) * G::MT + t) * 4 + j) * 64 + lane] = acc[t][j];
         __syncthreads();
-        if (kr > 0) return;
+        if (kr > 0) {
+            if constexpr (AS) act_flush(ao, (int64_t)blockIdx.x * 4 + wave, 0.0f, 0.0f);
+            return;
+        }
         for (int q = 1; q < FS; ++q)
 #pragma unroll
             for (int t = 0; t < G::MT; ++t)
@@ -927,6 +938,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
     const int co = 16 * fb + li;
     const float bb = bias[co];
     act_t<XH> *o = out + (int64_t)r0 * G::OHW * G::CO;
+    float as_s = 0.0f, as_q = 0.0f;
 #pragma unroll
     for (int t = 0; t < G::MT; ++t)
 #pragma unroll
@@ -935,8 +947,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
             if (p < nsamp * G::OHW) {
                 const float v = acc[t][j] + bb;
                 act_st<XH>(o, (int64_t)p * G::CO + co, v > 0.f ? v : 0.f);
+                if constexpr (AS) act_acc(ao, v, (int64_t)(p % G::OHW) * G::CO + co, as_s, as_q);
             }
         }
+    if constexpr (AS) act_flush(ao, (int64_t)blockIdx.x * 4 + wave, as_s, as_q);
 }
 
 // ---- conv2 / conv3 input gradient (transposed convolution) with the ReLU mask of the layer
@@ -1321,8 +1335,34 @@ using C1_84q = C1<4, 84, 84, 4>;          // 4 bands per sample (small batches)
 bool conv1_lds_supported(int C, int H, int W) { return C == 4 && H == 84 && W == 84; }
 
 int conv1_lds_fwd(hipStream_t s, bool bf, bool xh, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
-                  const void *W1v, const float *b1, void *out, uint8_t *obs_copy)
+                  const void *W1v, const float *b1, void *out, uint8_t *obs_copy, ActOut ao)
 {
+    if (ao.cnt) {     // GS_HP_ACT_STATS: the update's batch forms with the statistics epilogue
+        const float *W1 = static_cast<const float *>(W1v);
+        const uint16_t *W1h = static_cast<const uint16_t *>(W1v);
+        GS_REQUIRE(R > 0 && obs && W1 && b1 && out && !obs_copy && (int64_t)R * 2 >= kConv1Bands4Below,
+                   "conv1_lds_fwd: activation statistics on an update batch only");
+        GS_REQUIRE(!xh || bf, "conv1_lds_fwd: bf16 activation storage needs bf16 operands");
+        float *o32 = static_cast<float *>(out);
+        uint16_t *o16 = static_cast<uint16_t *>(out);
+        if (bf && R >= kConv1PairsFrom) {
+            const dim3 grid((unsigned)(C1_84::NB * ((R + kConv1Spb - 1) / kConv1Spb)));
+            if (xh) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, kConv1Spb, true, true>), grid, dim3(256), 0, s, obs, idx,
+                                       T, N, W1h, b1, o16, obs_copy, R, ao);
+            else hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, kConv1Spb, false, true>), grid, dim3(256), 0, s, obs, idx,
+                                    T, N, W1, b1, o32, obs_copy, R, ao);
+        } else {
+            const dim3 grid((unsigned)(C1_84::NB * R));
+            if (xh) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, 1, true, true>), grid, dim3(256), 0, s, obs, idx, T, N,
+                                       W1h, b1, o16, obs_copy, R, ao);
+            else if (bf) hipLaunchKernelGGL((k_conv1_fwd<C1_84, true, 1, false, true>), grid, dim3(256), 0, s, obs, idx, T,
+                                            N, W1, b1, o32, obs_copy, R, ao);
+            else hipLaunchKernelGGL((k_conv1_fwd<C1_84, false, 1, false, true>), grid, dim3(256), 0, s, obs, idx, T, N, W1,
+                                    b1, o32, obs_copy, R, ao);
+        }
+        GS_LAUNCH_CHECK("k_conv1_fwd<stats>");
+        return GS_OK;
+    }
     const float *W1 = static_cast<const float *>(W1v);
     const uint16_t *W1h = static_cast<const uint16_t *>(W1v);
     GS_REQUIRE(R > 0 && obs && W1 && b1 && out, "conv1_lds_fwd: bad argument");
@@ -1394,7 +1434,8 @@ bool conv23_lds_supported(int layer, int H, int W, int C, int k, int st, int Cou
 // splits, so R = 128 rows still launch 256 workgroups; the update's minibatches keep FS = 1
 // G: fp32 update batches, GB: bf16 update batches, G1: small batches (FS = 2)
 template <class G, class G1, class GB, int FSB = 1, class GX = GB>
-int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const float *bias, void *out, bool bf, bool xh)
+int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const float *bias, void *out, bool bf, bool xh,
+                    ActOut ao)
 {
     const float *Wt = static_cast<const float *>(Wv);
     const uint16_t *Wh = static_cast<const uint16_t *>(Wv);
@@ -1402,6 +1443,21 @@ int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const 
     const uint16_t *i16 = static_cast<const uint16_t *>(in);
     float *o32 = static_cast<float *>(out);
     uint16_t *o16 = static_cast<uint16_t *>(out);
+    if (ao.cnt) {     // GS_HP_ACT_STATS: the update's batch forms with the statistics epilogue
+        GS_REQUIRE((int64_t)R * 2 > kConvFwdSmallWG, "conv_fwd: activation statistics on an update batch only");
+        if (xh) {
+            const dim3 grid((unsigned)((R + GX::SPB - 1) / GX::SPB * FSB));
+            hipLaunchKernelGGL((k_conv_fwd<GX, true, FSB, true, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16, ao);
+        } else if (bf) {
+            const dim3 grid((unsigned)((R + GB::SPB - 1) / GB::SPB * FSB));
+            hipLaunchKernelGGL((k_conv_fwd<GB, true, FSB, false, true>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32, ao);
+        } else {
+            const dim3 grid((unsigned)((R + G::SPB - 1) / G::SPB));
+            hipLaunchKernelGGL((k_conv_fwd<G, false, 1, false, true>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32, ao);
+        }
+        GS_LAUNCH_CHECK("k_conv_fwd<stats>");
+        return GS_OK;
+    }
     if ((int64_t)R * 2 <= kConvFwdSmallWG) {
         const dim3 grid((unsigned)(2 * R));
         if (xh) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16);
@@ -1422,12 +1478,24 @@ int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const 
 }
 
 int conv23_lds_fwd(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const void *Wt,
-                   const float *bias, void *out)
+                   const float *bias, void *out, ActOut ao)
 {
     GS_REQUIRE(R > 0 && in && Wt && bias && out, "conv23_lds_fwd: bad argument");
     GS_REQUIRE(!xh || bf, "conv23_lds_fwd: bf16 activation storage needs bf16 operands");
-    if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS, C2_84x>(s, R, in, Wt, bias, out, bf, xh);
-    return launch_conv_fwd<C3_84, C3_84s, C3_84b>(s, R, in, Wt, bias, out, bf, xh);
+    if (layer == 2) return launch_conv_fwd<C2_84, C2_84, C2_84b, kConv2BfFS, C2_84x>(s, R, in, Wt, bias, out, bf, xh, ao);
+    return launch_conv_fwd<C3_84, C3_84s, C3_84b>(s, R, in, Wt, bias, out, bf, xh, ao);
+}
+
+// the statistics slots (workgroups x 4 waves) an update batch's stats-epilogue conv forward writes
+int conv_fwd_act_slots(int layer, int R, bool bf, bool xh)
+{
+    if (layer == 1)
+        return 4 * C1_84::NB * ((bf && R >= kConv1PairsFrom) ? (R + kConv1Spb - 1) / kConv1Spb : R);
+    if (layer == 2)
+        return 4 * (xh   ? (R + C2_84x::SPB - 1) / C2_84x::SPB * kConv2BfFS
+                    : bf ? (R + C2_84b::SPB - 1) / C2_84b::SPB * kConv2BfFS
+                         : (R + C2_84::SPB - 1) / C2_84::SPB);
+    return 4 * (bf ? (R + C3_84b::SPB - 1) / C3_84b::SPB : (R + C3_84::SPB - 1) / C3_84::SPB);
 }
 
 template <class G>

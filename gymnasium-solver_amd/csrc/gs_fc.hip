@@ -204,12 +204,16 @@ __device__ __forceinline__ void static_for(F &&f)
 // unconditional (the last tiles re-load a clamped tile) so the compiler's wait counts stay exact.
 // H16 (bf16 updates): bit 1 — A, bit 2 — B, bit 4 — the mask operand aux are bf16-stored
 // activations (gs_common.h act_bf16), 2 B per element
-template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, int PD, int KT, int H16 = 0>
+// AS (GS_HP_ACT_STATS, the bias + ReLU forward): the epilogue also records the activation statistics
+// of the pre-activation outputs (gs_common.h ActOut; neuron = output column)
+template <int BM, int BN, int WGM, int KS, bool BF, bool AK, bool BKC, int EPI, int PD, int KT, int H16 = 0,
+          bool AS = false>
 __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int64_t lda, const void *__restrict__ Bv,
                                                int64_t ldb, float *__restrict__ C, int64_t ldc, int M, int N, int K,
                                                const void *__restrict__ auxv, const int32_t *__restrict__ stop,
-                                               int64_t sC, int gm)
+                                               int64_t sC, int gm, ActOut ao = ActOut{})
 {
+    static_assert(!AS || EPI == kEpiBiasRelu, "activation statistics: the bias + ReLU forward");
     static_assert(H16 == 0 || BF, "bf16 operand storage: bf16 MFMA operands only");
     static_assert(!(H16 & 4) || EPI == kEpiMask, "a bf16 aux is the mask operand");
     using AT = typename std::conditional<(H16 & 1) != 0, uint16_t, float>::type;
@@ -344,7 +348,12 @@ __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int6
                     for (int v = 0; v < 16; ++v)
                         red[(((ks - 1) * (4 / KS) + wmn) * TM * TN + i * TN + j) * 16 * 64 + v * 64 + lane] = acc[i][j][v];
         __syncthreads();
-        if (ks > 0) return;
+        if (ks > 0) {
+            if constexpr (AS)
+                act_flush(ao, ((int64_t)blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * blockIdx.z)) * 4 +
+                                  (threadIdx.x >> 6), 0.0f, 0.0f);
+            return;
+        }
         for (int q = 1; q < KS; ++q)
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -354,6 +363,7 @@ __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int6
                     for (int v = 0; v < 16; ++v)
                         acc[i][j][v] += red[(((q - 1) * (4 / KS) + wmn) * TM * TN + i * TN + j) * 16 * 64 + v * 64 + lane];
     }
+    float as_s = 0.0f, as_q = 0.0f;
     // epilogue: D col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5) of each 32 x 32 sub-tile
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -369,12 +379,16 @@ __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int6
                 float x = acc[i][j][v];
                 if constexpr (EPI == kEpiBiasRelu) {
                     x += bn;
+                    if constexpr (AS) act_acc(ao, x, gn, as_s, as_q);
                     x = x > 0.0f ? x : 0.0f;
                 }
                 if constexpr (EPI == kEpiMask) x = act_ld<(H16 & 4) != 0>(aux, (int64_t)gm * ldc + gn) > 0.0f ? x : 0.0f;
                 C[(int64_t)gm * ldc + gn] = x;
             }
         }
+    if constexpr (AS)
+        act_flush(ao, ((int64_t)blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * blockIdx.z)) * 4 +
+                          (threadIdx.x >> 6), as_s, as_q);
 }
 
 // k_fc16: the fp32 form on v_mfma_f32_16x16x4_f32 (exact fp32) — a wave's (BM/WGM) x (BN/WGN)
@@ -557,16 +571,37 @@ template <int BM, int BN, int WGM, int KS, bool AK, bool BKC, int EPI, int PD32,
           bool MI16 = false, int H16 = 0>
 int launch_fc(hipStream_t s, bool bf, const void *A, int64_t lda, const void *B, int64_t ldb, float *C, int64_t ldc,
               int64_t M, int64_t N, int64_t K, const void *aux, const int32_t *stop, int gm, int splits = 1,
-              int64_t sC = 0)
+              int64_t sC = 0, ActOut ao = ActOut{})
 {
     const dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
     GS_REQUIRE(H16 == 0 || (bf && splits == 1), "k_fc: bf16 operand storage needs bf16 operands, no K split");
     K /= splits;
+    if constexpr (EPI == kEpiBiasRelu) {
+        if (ao.cnt) {    // GS_HP_ACT_STATS: the statistics epilogue (slots: workgroups x 4 waves)
+            GS_REQUIRE(splits == 1, "k_fc: activation statistics without a K split");
+            if (bf) {
+                constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, true, KT16>();
+                auto k = k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16, H16, true>;
+                lds_attr(k, L);
+                hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop,
+                                   sC, gm, ao);
+            } else {
+                constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, false, KT32>();
+                auto k = k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32, 0, true>;
+                lds_attr(k, L);
+                hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop,
+                                   sC, gm, ao);
+            }
+            GS_LAUNCH_CHECK("k_fc<stats>");
+            return GS_OK;
+        }
+    }
     if (bf) {
         constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, true, KT16>();
         auto k = k_fc<BM, BN, WGM, KS, true, AK, BKC, EPI, PD16, KT16, H16>;
         lds_attr(k, L);
-        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm,
+                           ActOut{});
     } else if (MI16 && FC_MI16) {
         constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, false, KT32>();
         auto k = k_fc16<BM, BN, WGM, KS, AK, BKC, EPI, PD32, KT32>;
@@ -577,7 +612,8 @@ int launch_fc(hipStream_t s, bool bf, const void *A, int64_t lda, const void *B,
         constexpr size_t L = fc_lds_bytes<BM, BN, WGM, KS, false, KT32>();
         auto k = k_fc<BM, BN, WGM, KS, false, AK, BKC, EPI, PD32, KT32>;
         lds_attr(k, L);
-        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm);
+        hipLaunchKernelGGL(k, grid, dim3(256), L, s, A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, aux, stop, sC, gm,
+                           ActOut{});
     }
     GS_LAUNCH_CHECK("k_fc");
     return GS_OK;
@@ -663,8 +699,9 @@ int fc_fwd_partials(hipStream_t s, int splits, int64_t M, int64_t N, int64_t K, 
 
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const void *A, int64_t lda,
             const void *B, int64_t ldb, float *C, int64_t ldc, const void *aux, const int32_t *stop, float *parts,
-            bool act16)
+            bool act16, ActOut ao)
 {
+    GS_REQUIRE(!ao.cnt || (op == 0 && !parts), "fc_gemm: activation statistics: the single-pass forward only");
     GS_REQUIRE(op >= 0 && op <= 2, "fc_gemm: op %d", op);
     GS_REQUIRE(fc_supported(op, M, N, K, lda, ldb, ldc), "fc_gemm: shape %lld x %lld x %lld (op %d) not supported",
                (long long)M, (long long)N, (long long)K, op);
@@ -685,9 +722,9 @@ int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, c
         }
         if (act16)      // A = a3, B = Wf: bf16 storage
             return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1, false, 3>(
-                s, true, A, lda, B, ldb, C, ldc, M, N, K, aux, stop, 4);
-        return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(s, bf16, A, lda, B, ldb, C,
-                                                                                           ldc, M, N, K, aux, stop, 4);
+                s, true, A, lda, B, ldb, C, ldc, M, N, K, aux, stop, 4, 1, 0, ao);
+        return launch_fc<32, 32, 1, 4, true, true, kEpiBiasRelu, FC_PD_FWD32, FC_PD_FWD16, 2, 1>(
+            s, bf16, A, lda, B, ldb, C, ldc, M, N, K, aux, stop, 4, 1, 0, ao);
     }
     if (op == 1) {   // wgrad: C = A^T B with A [K][M], B [K][N] (the round-5 sweep's 16x16x4 form: 46.2
                      // vs 47.9 us back to back, 46.9 vs 46.7 inside the update — kept on 32x32x2)
@@ -714,7 +751,8 @@ extern "C" int gs_fc_gemm(int op, int bf16, int64_t M, int64_t N, int64_t K, con
                           void *stream)
 {
     GS_REQUIRE(A && B && C, "gs_fc_gemm: null operand");
-    return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux, nullptr, parts);
+    return fc_gemm((hipStream_t)stream, op, bf16 != 0, M, N, K, A, lda, B, ldb, C, ldc, aux, nullptr, parts, false,
+                   ActOut{});
 }
 
 #ifdef GS_FC_SWEEP
@@ -775,3 +813,8 @@ extern "C" int gs_debug_fc_variant(int op, int v, int bf16, int64_t M, int64_t N
     return GS_E_INVALID;
 }
 #endif
+
+namespace gs {
+// statistics slots of the fc forward's stats epilogue (32 x 32 tiles, 4 waves each)
+int fc_fwd_act_slots(int64_t M, int64_t N) { return (int)(4 * ((N + 31) / 32) * ((M + 31) / 32)); }
+}  // namespace gs

@@ -50,7 +50,10 @@ bool fc_supported(int op, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
 // update's bf16 weight copy) — so the operand pointers are void
 int fc_gemm(hipStream_t s, int op, bool bf16, int64_t M, int64_t N, int64_t K, const void *A, int64_t lda,
             const void *B, int64_t ldb, float *C, int64_t ldc, const void *aux, const int32_t *stop = nullptr,
-            float *parts = nullptr, bool act16 = false);
+            float *parts = nullptr, bool act16 = false, ActOut ao = ActOut{});
+// ao (GS_HP_ACT_STATS): op 0's bias + ReLU epilogue records the activation statistics of the
+// pre-activation outputs (neuron = column), in fc_fwd_act_slots(M, N) slots
+int fc_fwd_act_slots(int64_t M, int64_t N);
 // the fc forward product as split-K fp32 partials (no epilogue) for small row counts (the
 // rollout): C + z M ldc = A[:, z K/splits ..] B[:, z K/splits ..]^T for z < splits;
 // fc_fwd_splits picks the split (1 when the plain tiles already fill the chip)

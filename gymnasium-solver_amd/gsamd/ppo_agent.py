@@ -11,7 +11,7 @@ agents/ppo/ppo_agent.py:10-152):
   get_rollout_collector(stage)                DeviceRolloutCollector
 and the fast path the trainer uses instead of per-minibatch Python:
   train_epoch()                               rollout + the whole update phase in one C-ABI call
-Metrics are kept on device, one 24-float record per minibatch, and converted to the
+Metrics are kept on device, one 40-float record per minibatch, and converted to the
 reference's metric keys once per epoch (the reference pays ~20 .item() syncs per
 minibatch, SURVEY.md §3 Boundaries).
 """
@@ -33,7 +33,7 @@ from .rollout import DeviceCartPoleVecEnv, DeviceRolloutCollector, DeviceSynthet
 from .samplers import IndexStreamPrefetcher, MultiPassRandomSampler, index_stream, rank_share
 from .distributed import allreduce_sum_f64, broadcast_int, check_replicas, comm_status, world_active
 from . import distributed as _dist
-from .metrics import NUM_SUMS, MetricsRecorder, activation_stats, ppo_keys, ppo_records
+from .metrics import NUM_SUMS, MetricsRecorder, ppo_keys, ppo_records
 from .schedules import SCHEDULABLE, build_schedulers
 
 STAGES = ("train",)
@@ -353,10 +353,11 @@ class DevicePPOAgent:
     @property
     def device_activation_stats(self) -> bool:
         """The update records every evaluated minibatch's activation statistics into its record
-        (GS_HP_ACT_STATS: the reference's forward hooks recorded by every training_step,
-        base_agent.py:335-347) — with track_stats, on the MLP path (the NatureCNN update computes
-        its statistics with a separate forward, _activation_stats_launch), not in global mode."""
-        return self.track_stats and not self.is_pixel and not getattr(self, "global_mode", False)
+        (GS_HP_ACT_STATS: the reference's forward hooks, utils/models.py:121-147, recorded by every
+        training_step, base_agent.py:335-347; MLP: backbone.{0,2}, NatureCNN: cnn.{0,2,4} and mlp.0,
+        models.py:419-422) — with track_stats, not in global mode (a rank holds a share of each
+        global minibatch)."""
+        return self.track_stats and not getattr(self, "global_mode", False)
 
     def hparams(self) -> PPOHparams:
         c = self.config
@@ -533,7 +534,6 @@ class DevicePPOAgent:
         buf = collector.buffer
         if self.world_size > 1:
             self._verify_exchange()
-        self._activation_stats_launch(buf, idx)
         if ev:
             ev[-1][1].record()
         if self.global_mode:
@@ -612,33 +612,6 @@ class DevicePPOAgent:
             from ._lib import GsError
             raise GsError(f"exchange canary failed on epoch {self.current_epoch} (rank {self.rank}): a known "
                           f"vector did not come back as its exact rank-order mean through the xGMI exchange")
-
-    def _activation_stats_launch(self, buf, idx) -> None:
-        """The reference records opt/activations/<layer>/* on every training_step
-        (base_agent.py:336-347, utils/models.py:120-190; MLP: backbone.{0,2}, NatureCNN: cnn.{0,2,4}
-        and mlp.0, models.py:419-422); the device agent computes them once per epoch, on the
-        epoch's first minibatch with the parameters that minibatch's step reads, on the update's
-        stream ahead of it (gs_mlp_activation_stats / gs_cnn_activation_stats; SURVEY §8b:
-        diagnostics may be computed per epoch).  Off with track_stats=False."""
-        self._act_pending = False
-        if self.global_mode or not self.track_stats or idx is None or self.device_activation_stats:
-            return
-        if self.is_pixel:
-            if getattr(self, "_act_stats", None) is None:
-                self._act_stats = torch.zeros(16, dtype=torch.float64, device=self.device)
-            check(lib.gs_cnn_activation_stats(ptr(self.policy_model.params), self.policy_model.dims, buf.view(),
-                                              ptr(idx), self.batch_size, ptr(self._act_stats), ptr(self.workspace),
-                                              stream_handle()), "gs_cnn_activation_stats")
-            self._act_pending = True
-            return
-        dims = self.policy_model.dims
-        nparts = (self.batch_size + 15) // 16
-        width = 2 * (2 + max(int(dims.hidden1), int(dims.hidden2)))
-        if getattr(self, "_act_parts", None) is None or self._act_parts.numel() != nparts * width:
-            self._act_parts = torch.zeros(nparts * width, dtype=torch.float64, device=self.device)
-        check(lib.gs_mlp_activation_stats(ptr(self.policy_model.params), dims, buf.view(), ptr(idx), self.batch_size,
-                                          ptr(self._act_parts), stream_handle()), "gs_mlp_activation_stats")
-        self._act_pending = True
 
     CNN_ACTIVATION_LAYERS = ("cnn.0", "cnn.2", "cnn.4", "mlp.0")
 
@@ -734,14 +707,6 @@ class DevicePPOAgent:
             # records them once per training_step — their epoch mean is the recorder's
             keys = self.activation_keys()
             self.metrics_recorder.record_rows("train", keys, live[:, ACT_SLOT:ACT_SLOT + len(keys)])
-        elif getattr(self, "_act_pending", False) and self.is_pixel:
-            self.metrics_recorder.record("train", dict(zip(self.activation_keys(),
-                                                           self._act_stats.cpu().numpy().tolist())))
-        elif getattr(self, "_act_pending", False):
-            dims = self.policy_model.dims
-            parts = self._act_parts.cpu().numpy().reshape((self.batch_size + 15) // 16, -1)
-            self.metrics_recorder.record("train", activation_stats(parts, self.batch_size,
-                                                                   (int(dims.hidden1), int(dims.hidden2))))
         if self.config.target_kl is not None and (rec[:, M["kl_stop"]] != 0).any():
             self._early_stop_epoch = True        # sticky, as BaseAgent._early_stop_epoch
         return rec

@@ -551,28 +551,93 @@ def test_cnn_activation_stats_vs_reference(golden, cuda, tag):
             assert abs(got - want) <= tol, (n, k, got, want)
 
 
-def test_cnn_agent_records_activation_stats(cuda):
-    """The pixel agent records the NatureCNN's activation statistics once per epoch under the
-    reference's keys (base_agent.py:335-347 -> opt/activations/{cnn.0,cnn.2,cnn.4,mlp.0}/*), taken
-    on the epoch's first minibatch before its step: equal to gs_cnn_activation_stats on that
-    minibatch with the pre-update parameters."""
+def _cnn_stats_update(cuda, env, over, n_up):
+    """A pixel agent with its first rollout collected; run(k) restores the initial state and runs the
+    first k minibatches of the update (gs_cnn_ppo_update with the agent's hparams, GS_HP_ACT_STATS
+    included), returning the records."""
     from gsamd._lib import check, lib, ptr, stream_handle
     from gsamd.config import load_config
     from gsamd.ppo_agent import DevicePPOAgent
     torch.manual_seed(0)
-    cfg = load_config("ALE-Breakout-v5", "rgb_ppo", overrides=dict(env_dynamics="synthetic", n_envs=8, n_steps=32,
-                                                                   batch_size=64, n_epochs=1))
+    cfg = load_config(env, "rgb_ppo", overrides=dict(env_dynamics="synthetic", **over))
     agent = DevicePPOAgent(cfg, device=cuda, use_graph=False, track_stats=True)
-    p0 = agent.policy_model.params.clone()
-    agent.train_epoch()
-    m = agent.epoch_metrics()
-    keys = [f"opt/activations/{n}/{k}" for n in ("cnn.0", "cnn.2", "cnn.4", "mlp.0")
-            for k in ("mean", "std", "dead_pct", "dead_max")]
-    assert set(keys) <= set(m), set(keys) - set(m)
+    assert agent.device_activation_stats
+    coll = agent.get_rollout_collector("train")
+    coll.collect()
     idx = agent.prefetcher.upload(0)
-    ws = torch.empty(int(lib.gs_cnn_workspace_bytes(agent.policy_model.dims, 64)), dtype=torch.uint8, device=cuda)
-    out = torch.zeros(16, dtype=torch.float64, device=cuda)
-    check(lib.gs_cnn_activation_stats(ptr(p0), agent.policy_model.dims, agent.get_rollout_collector("train").buffer.view(),
-                                      ptr(idx), 64, ptr(out), ptr(ws), stream_handle()), "gs_cnn_activation_stats")
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(np.array([m[k] for k in keys]), out.cpu().numpy())
+    pm = agent.policy_model
+    st0 = [t.clone() for t in (pm.params, agent.adam_m, agent.adam_v)]
+
+    def run(k):
+        for t, t0 in zip((pm.params, agent.adam_m, agent.adam_v), st0):
+            t.copy_(t0)
+        agent.metrics_buf.zero_()
+        if k:
+            check(lib.gs_cnn_ppo_update(ptr(pm.params), ptr(agent.grads), ptr(agent.adam_m), ptr(agent.adam_v), pm.dims,
+                                        agent.hparams(), coll.buffer.view(), ptr(idx), agent.batch_size, k, 0,
+                                        ptr(agent.metrics_buf), ptr(agent.stop_flag), ptr(agent.workspace), None,
+                                        stream_handle()), "gs_cnn_ppo_update")
+        torch.cuda.synchronize()
+        return agent.metrics_buf[:k].cpu().numpy().copy()
+
+    def ref_stats(k):    # gs_cnn_activation_stats (separate fp32 forward) before step k
+        run(k)
+        out = torch.zeros(16, dtype=torch.float64, device=cuda)
+        check(lib.gs_cnn_activation_stats(ptr(pm.params), pm.dims, coll.buffer.view(), ptr(idx[k * agent.batch_size:]),
+                                          agent.batch_size, ptr(out), ptr(agent.workspace), stream_handle()),
+              "gs_cnn_activation_stats")
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+    return agent, run, ref_stats
+
+
+def test_cnn_agent_records_activation_stats(cuda):
+    """The pixel agent records the NatureCNN's activation statistics under the reference's keys
+    (base_agent.py:335-347 -> opt/activations/{cnn.0,cnn.2,cnn.4,mlp.0}/*) as the epoch mean over
+    every minibatch of the update, each taken under the parameters that minibatch's loss used (the
+    reference's per-training_step hook record): at B = 64 the update computes them with the separate
+    fp32 forward (gs_cnn_activation_stats' kernels) before each step, so every minibatch's values are
+    those of gs_cnn_activation_stats on its rows and pre-step parameters, bit for bit."""
+    from gsamd._lib import ACT_SLOT
+    agent, run, ref_stats = _cnn_stats_update(cuda, "ALE-Breakout-v5", dict(n_envs=8, n_steps=32, batch_size=64,
+                                                                           n_epochs=1), 4)
+    n = agent.n_minibatches
+    assert n == 4
+    rec = run(n)
+    for k in range(n):
+        np.testing.assert_array_equal(rec[k, ACT_SLOT:ACT_SLOT + 16], ref_stats(k).astype(np.float32), err_msg=str(k))
+    # through the agent's epoch bookkeeping: the epoch means of those records
+    run(0)
+    agent.update_phase()
+    m = agent.epoch_metrics()
+    keys = agent.activation_keys()
+    assert len(keys) == 16 and set(keys) <= set(m)
+    want = rec[:, ACT_SLOT:ACT_SLOT + 16].astype(np.float64).mean(axis=0)
+    np.testing.assert_allclose(np.array([m[k] for k in keys]), want, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_cnn_update_activation_stats_epilogues(cuda, prec):
+    """The production batch (B = 1024, Pong): the statistics come from the update's own forward
+    kernels (the conv1 / conv2 / conv3 LDS convolutions' and the fc kernel's epilogues: integer dead
+    counters, per-wave sums), for every minibatch under the parameters its loss used.  Against
+    gs_cnn_activation_stats (a separate fp32 forward) on the same rows and pre-step parameters: fp32
+    mean / std within 1e-5 x std (+ 1e-7), dead fractions within 1/B; bf16 (the forward's operands
+    rounded to bf16) mean / std within 2e-2 x std, dead fractions within 4/B."""
+    from gsamd._lib import ACT_SLOT
+    over = dict(n_envs=32, n_steps=32, n_epochs=3)
+    if prec == "bf16":
+        over["precision"] = "bf16"
+    agent, run, ref_stats = _cnn_stats_update(cuda, "ALE-Pong-v5", over, 3)
+    B, n = agent.batch_size, agent.n_minibatches
+    assert B == 1024 and n == 3
+    rec = run(n)
+    rtol, dtol = (1e-5, 1.0 / B) if prec == "fp32" else (2e-2, 4.0 / B)
+    for k in range(n):
+        ref, got = ref_stats(k), rec[k, ACT_SLOT:ACT_SLOT + 16].astype(np.float64)
+        for l in range(4):
+            sd = ref[4 * l + 1]
+            for j in range(4):
+                tol = rtol * sd + 1e-7 if j < 2 else dtol
+                assert abs(got[4 * l + j] - ref[4 * l + j]) <= tol, (prec, k, l, j, got[4 * l + j], ref[4 * l + j])
+    assert np.isfinite(rec[:, ACT_SLOT:ACT_SLOT + 16]).all() and (rec[:, ACT_SLOT + 1::4] > 0).all()
