@@ -555,6 +555,12 @@ def cnn_global_tf_worker(rank, world, port, result_dir, ref_path, states_path):
                                           ptr(agent._adv_sums), ptr(agent._adv_stats), s), "gs_ppo_global_adv_stats")
         hp = agent.hparams()
         grads, params, digests = [], [], []
+        # every step's conv / fc ReLU decisions of this rank's padded row share (a1 / a2 / a3 / h > 0
+        # in its workspace, NCHW), bit-packed per row: the parent assembles the global minibatch's
+        # decisions from the ranks' shares for the oracle (the global run's arithmetic bars)
+        act_shapes = [(20, 20, 32), (9, 9, 64), (7, 7, 64), (512,)]
+        act_offs = [int(lib.gs_cnn_workspace_act_offset(pm.dims, B, layer)) for layer in (1, 2, 3, 4)]
+        masks = [[] for _ in act_shapes]
         for k in range(K):
             for t, name in ((pm.params, "p"), (agent.adam_m, "m"), (agent.adam_v, "v")):
                 t.copy_(torch.from_numpy(np.ascontiguousarray(st[name][k])).to(dev))
@@ -566,6 +572,11 @@ def cnn_global_tf_worker(rank, world, port, result_dir, ref_path, states_path):
                   "gs_cnn_ppo_update_global")
             g_k, p_k = agent.grads.cpu().numpy(), pm.params.cpu().numpy()
             digests.append(hashlib.sha256(g_k.tobytes() + p_k.tobytes()).hexdigest())
+            for li, (off, sh) in enumerate(zip(act_offs, act_shapes)):
+                nel = B * int(np.prod(sh))
+                a = agent.workspace[off:off + 4 * nel].view(torch.float32).view(B, *sh) > 0
+                a = a.permute(0, 3, 1, 2) if len(sh) == 3 else a
+                masks[li].append(np.packbits(a.reshape(B, -1).cpu().numpy(), axis=1))
             if rank == 0:
                 grads.append(g_k)
                 params.append(p_k)
@@ -573,7 +584,8 @@ def cnn_global_tf_worker(rank, world, port, result_dir, ref_path, states_path):
               "gs_ppo_global_records")
         torch.cuda.synchronize()
         comm_status(comm)
-        out = dict(rec=agent.metrics_buf.cpu().numpy(), digests=np.array(digests))
+        out = dict(rec=agent.metrics_buf.cpu().numpy(), digests=np.array(digests),
+                   shares=agent._gidx.cpu().numpy(), **{f"mask{li}": np.stack(m) for li, m in enumerate(masks)})
         if rank == 0:
             out.update(g=np.stack(grads), p=np.stack(params))
         np.savez(os.path.join(result_dir, f"tf{rank}.npz"), **out)

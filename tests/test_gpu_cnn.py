@@ -334,7 +334,9 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
       bf16 (against the
       bf16 emulation, oracle/cnn_ref.py bf16=True): loss 1e-4 of its scale, every step's clipped
       gradient within 2e-2 of the emulation's and under half its distance to the fp32 oracle's
-      (the bars of test_cnn_bf16_update_step_vs_bf16_oracle, at every one of the 8 steps).
+      (the bars of test_cnn_bf16_update_step_vs_bf16_oracle, at every one of the 8 steps), and
+      every step's new parameters: the Adam step on the device's gradient at the fp32 bars, and
+      within 3 lr per weight / 0.5 of the update's norm of the emulation's own clip + Adam.
     * Free-running (oracle and device each on their own trajectory, measured 1e-4 loss and 8.5e-5
       parameter deviation after 8 fp32 steps on the first GPU run — Adam amplifies reassociation-level
       gradient differences of near-zero-gradient weights): fp32 losses within 5e-4 relative,
@@ -463,6 +465,22 @@ def test_cnn_update_first_minibatches_vs_oracle(cuda, prec):
             _, _, _, gc32, _ = C.clip_and_adam(p, g32, shapes, m, v, k + 1, lr)
             worst["emu_vs_f32"].append((round(rl(g_dev, gc), 5), round(rl(g_dev, gc32), 5)))
             need(d_loss < 1e-4, ("loss", k, float(rec[k, M["loss"]]), loss))
+            # the step's new parameters (the bf16 mode's clip + Adam is fp32): (1) exactly the Adam
+            # step (torch's single-tensor Adam, cnn_ref.clip_and_adam with no clipping) on the device's own
+            # clipped gradient — 2e-6 except where Adam's sign-like step on a noise-level gradient
+            # moves a weight (at most 1e-4 of them, never more than 2 lr); (2) against the emulation's
+            # clip + Adam on ITS gradient (within 2e-2 of the device's, above): every weight within
+            # 3 lr and the update p1 - p within 0.5 of its norm (Adam rescales each weight's step by
+            # its own moment, so the gradient's relative difference reaches the update unevenly)
+            pa = C.clip_and_adam(p, g_dev.astype(np.float32), shapes, m, v, k + 1, lr, max_norm=1e30)[0]
+            d = np.abs(p_dev.astype(np.float64) - pa)
+            du = np.linalg.norm((p_dev.astype(np.float64) - p) - (p1 - p)) / np.linalg.norm(p1.astype(np.float64) - p)
+            de = float(np.abs(p_dev.astype(np.float64) - p1).max())
+            worst.setdefault("bf16_params", []).append((int((d > 2e-6).sum()), float(f"{d.max():.2e}"),
+                                                        float(f"{du:.3e}"), float(f"{de:.2e}")))
+            need((d > 2e-6).sum() <= max(1, int(1e-4 * d.size)) and d.max() <= 2 * lr,
+                 ("bf16 params vs Adam on the device gradient", k, int((d > 2e-6).sum()), float(d.max())))
+            need(de <= 3 * lr and du < 0.5, ("bf16 params vs the emulation's clip + Adam", k, de, du))
             continue
         # the clipped gradient: at B = 1024 a few pre-activations sit within rounding of 0, so a
         # ReLU decision flips between the device's and the oracle's summation order and moves the
