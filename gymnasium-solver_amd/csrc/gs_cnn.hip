@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     GS_STAMP(5)
     if (tid == 0)
         for (int q = 0; q < kSums; ++q) part[(int64_t)blockIdx.x * kSums + q] = acc[q];
-    float *wp = wpart + (int64_t)blockIdx.x * head_part_stride(L);
+    float *wp = wpart + (int64_t)blockIdx.x * HID;      // this workgroup's dbf partial
     for (int j = tid; j < HID; j += 256) {
         float w[4 * NZ];
 #pragma unroll
@@ -1127,9 +1127,6 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
                                         : make_float4(0.f, 0.f, 0.f, 0.f);
             w[4 * c] = t.x, w[4 * c + 1] = t.y, w[4 * c + 2] = t.z, w[4 * c + 3] = t.w;
         }
-        float g[4 * NZ];
-#pragma unroll
-        for (int a = 0; a < 4 * NZ; ++a) g[a] = 0.f;
         float dbf = 0.f;      // this workgroup's rows of dbf[j] = sum_b dh[b][j] (the fc bias gradient)
 #pragma unroll 1
         for (int r = 0; r < kHeadRows; ++r) {      // rolled: a short instruction stream (cold i-cache)
@@ -1153,41 +1150,35 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
                 else static_cast<float *>(dhv)[(int64_t)(r0 + r) * HID + j] = dhj;
                 dbf += dhj;
             }
-            // this workgroup's share of dWh[a][j] = sum_r dz[r][a] h[r][j] (rows in order)
-            const float hb = BF ? bf16r(hv) : hv;
-#pragma unroll
-            for (int a = 0; a < 4 * NZ; ++a) g[a] = fmaf(BF ? bf16r(d[a]) : d[a], hb, g[a]);
         }
-        // every padded row stored (rows past A1 are zeros, never summed): no per-row branches
-        static_assert(4 * NZ == 4 * (((AM <= 18 ? 18 : kAMax) + 4) / 4), "head_part_rows");
-#pragma unroll
-        for (int a = 0; a < 4 * NZ; ++a) wp[a * (HID + 1) + j] = g[a];
-        wp[(int64_t)(4 * NZ) * (HID + 1) + j] = dbf;
+        wp[j] = dbf;
     }
-    GS_STAMP(6)
-    if (tid < A1) {     // the bias column: sum of the (unrounded) dz rows
-        float sb = 0.f;
-        for (int r = 0; r < kHeadRows; ++r) sb += zs[r * ZS + tid];
-        wp[tid * (HID + 1) + HID] = sb;
-    }
-    GS_STAMP_END(7)
+    GS_STAMP_END(6)
 }
 
-// [dWh | dbh] = the k_cnn_head_loss partials summed in workgroup order (kWsumOut outputs per
-// workgroup, kWsumGroups thread groups over contiguous partial ranges, 32 loads of a group in
-// flight, combined in group order); the last workgroup writes the minibatch record (and sets the
-// KL stop).  16 outputs x 16 groups ran slower (10.2 vs 7.9 us: 64-B row segments)
-constexpr int kWsumOut = 64, kWsumGroups = 256 / kWsumOut;
-__global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__ wpart, int nparts, CnnLayout L,
-                                                       float *__restrict__ G, const double *__restrict__ part, int B,
-                                                       LossArgs la, float *__restrict__ metrics,
-                                                       int32_t *__restrict__ stop)
+// [dWh | dbh] = dz^T [h | 1] over all B rows of the minibatch, dbf = the k_cnn_head_loss dbf partials
+// summed in workgroup order, and the minibatch record — one launch, no per-workgroup [dWh | dbh]
+// partials (round 5 wrote 256 of them, 10 MB per minibatch, and summed them in a second pass).
+// Workgroup x < HID / 32 (1024 threads): h columns [32 x, 32 x + 32) for every head row a < A1;
+// thread (c = tid & 31, slice q = tid >> 5) takes rows q, q + 32, ... of each kWgChunk-row chunk
+// (its h loads all in flight at once, coalesced 128-B rows) against the chunk's dz staged in LDS
+// (rows padded to float4), fp32 FMA (BF: both operands rounded to bf16, the emulation's product); the
+// 32 slices added in slice order.  Then its dbf columns over the partials (32 ranges, in order).  The
+// last workgroup: dbh (column sums of dz, rows in order) and the record from the loss partials (sets
+// the KL stop).
+constexpr int kWgChunk = 1024, kWgCols = 32, kWgSlices = 32, kWgRows = kWgChunk / kWgSlices;
+template <int AM, bool BF>
+__global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict__ h, const float *__restrict__ dz,
+                                                         const float *__restrict__ dbf_part, int nparts, CnnLayout L,
+                                                         float *__restrict__ G, const double *__restrict__ part, int B,
+                                                         LossArgs la, float *__restrict__ metrics,
+                                                         int32_t *__restrict__ stop)
 {
-    __shared__ float red[kWsumGroups][kWsumOut];
-    const int tid = threadIdx.x, HID = L.HID, A = L.A;
-    const int64_t nout = head_part_out(L), pstride = head_part_stride(L);
-    const int64_t pad = (int64_t)(head_part_rows(L) - (A + 1)) * (HID + 1);     // the zero rows skipped
-    if ((int64_t)blockIdx.x * kWsumOut >= nout) {
+    constexpr int AP = (AM + 1 + 3) & ~3;      // head rows padded to float4 (accumulators)
+    extern __shared__ float lds[];             // max(kWgChunk x AP dz, kWgSlices x kWgCols x (AP + 1) partials)
+    const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
+    const int ncb = (HID + kWgCols - 1) / kWgCols;
+    if ((int)blockIdx.x == ncb) {
         // the record: the 13 loss sums over the partials, 16 threads per sum (strided, in order),
         // then the 16 in order; thread 0 writes it from a one-partial view of the totals
         __shared__ double msum[kSums][16];
@@ -1197,6 +1188,13 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
             double v = 0.0;
             for (int b = j; b < nparts; b += 16) v += part[(int64_t)b * kSums + q];
             msum[q][j] = v;
+        }
+        // dbh[a] = sum_r dz[r][a] (rows in order, unrounded), unless the step is stopped
+        if (!(stop && *stop) && tid >= 256 && tid < 256 + A1) {
+            const int a2 = tid - 256;
+            float sb = 0.f;
+            for (int r = 0; r < B; ++r) sb += dz[(int64_t)r * A1 + a2];
+            G[a2 < A ? L.obp + a2 : L.obv] = sb;
         }
         __syncthreads();
         if (tid < kSums) {
@@ -1215,32 +1213,68 @@ __global__ __launch_bounds__(256) void k_cnn_head_wsum(const float *__restrict__
         return;
     }
     if (stop && *stop) return;
-    const int o = tid % kWsumOut, g = tid / kWsumOut;
-    const int64_t out = (int64_t)blockIdx.x * kWsumOut + o;
-    const int64_t oc0 = out < nout ? out : nout - 1;
-    const int64_t oc = oc0 < (int64_t)(A + 1) * (HID + 1) ? oc0 : oc0 + pad;     // its partial column
-    const int w0 = (g * nparts) / kWsumGroups, w1 = ((g + 1) * nparts) / kWsumGroups;
-    float sacc = 0.f;
-    constexpr int NB = 32;
-    for (int w = w0; w < w1; w += NB) {
-        float t[NB];
+    const int c = tid & (kWgCols - 1), q = tid >> 5;
+    const int col = blockIdx.x * kWgCols + c;
+    const int colc = col < HID ? col : HID - 1;
+    float g[AP];
 #pragma unroll
-        for (int j = 0; j < NB; ++j) t[j] = wpart[(int64_t)min(w + j, w1 - 1) * pstride + oc];
+    for (int a = 0; a < AP; ++a) g[a] = 0.f;
+    for (int r0 = 0; r0 < B; r0 += kWgChunk) {
+        const int nr = min(kWgChunk, B - r0);
+        float hv[kWgRows];                     // rows q, q + 32, ... of the chunk: every load in flight
 #pragma unroll
-        for (int j = 0; j < NB; ++j)
-            if (w + j < w1) sacc += t[j];
+        for (int j = 0; j < kWgRows; ++j) hv[j] = h[(int64_t)(r0 + min(q + kWgSlices * j, nr - 1)) * HID + colc];
+        if (r0 > 0) __syncthreads();           // the previous chunk's dz reads are done
+        for (int u = tid; u < nr * AP; u += 1024) {
+            const int r = u / AP, a = u - r * AP;
+            lds[u] = a < A1 ? dz[(int64_t)(r0 + r) * A1 + a] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < kWgRows; ++j) {
+            const int r = q + kWgSlices * j;
+            if (r >= nr) break;
+            const float hb = BF ? bf16r(hv[j]) : hv[j];
+#pragma unroll
+            for (int a4 = 0; a4 < AP; a4 += 4) {
+                const float4 d = *reinterpret_cast<const float4 *>(lds + r * AP + a4);
+                g[a4 + 0] = fmaf(BF ? bf16r(d.x) : d.x, hb, g[a4 + 0]);
+                g[a4 + 1] = fmaf(BF ? bf16r(d.y) : d.y, hb, g[a4 + 1]);
+                g[a4 + 2] = fmaf(BF ? bf16r(d.z) : d.z, hb, g[a4 + 2]);
+                g[a4 + 3] = fmaf(BF ? bf16r(d.w) : d.w, hb, g[a4 + 3]);
+            }
+        }
     }
-    red[g][o] = sacc;
+    // this workgroup's dbf columns: the partials of the workgroups in order, 32 ranges of them
+    float fs = 0.f;
+    {
+        const int w0 = (q * nparts) / kWgSlices, w1 = ((q + 1) * nparts) / kWgSlices;
+        for (int w = w0; w < w1; ++w) fs += dbf_part[(int64_t)w * HID + colc];
+    }
+    __syncthreads();                           // the dz tile is dead: the slice partials reuse its LDS
+    float *red = lds;                          // [slice][col][AP + 1]
+    constexpr int RS = AP + 1;
+#pragma unroll
+    for (int a = 0; a < AP; ++a) red[(q * kWgCols + c) * RS + a] = g[a];
+    red[(q * kWgCols + c) * RS + AP] = fs;
     __syncthreads();
-    if (g == 0 && out < nout) {
-        static_assert(kWsumGroups == 4, "the round-4 combine order");
-        const float v = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
-        const int64_t nh = (int64_t)(A + 1) * (HID + 1);
-        const int a = (int)(out / (HID + 1)), c = (int)(out - (int64_t)a * (HID + 1));
-        const int64_t dst = out >= nh ? L.obf + (out - nh)
-                            : c < HID ? (a < A ? L.oWp + (int64_t)a * HID + c : L.oWv + c) : (a < A ? L.obp + a : L.obv);
-        G[dst] = v;
+    for (int o = tid; o < kWgCols * (A1 + 1); o += 1024) {
+        const int cc = o % kWgCols, a = o / kWgCols, cl = blockIdx.x * kWgCols + cc;
+        if (cl >= HID) continue;
+        const int slot = a < A1 ? a : AP;
+        float v = 0.f;
+#pragma unroll 8
+        for (int k = 0; k < kWgSlices; ++k) v += red[(k * kWgCols + cc) * RS + slot];
+        G[a < A ? L.oWp + (int64_t)a * HID + cl : a == A ? L.oWv + cl : L.obf + cl] = v;
     }
+}
+
+template <int AM>
+constexpr size_t head_wgrad_lds()
+{
+    constexpr int AP = (AM + 1 + 3) & ~3;
+    constexpr size_t d = (size_t)kWgChunk * AP, r = (size_t)kWgSlices * kWgCols * (AP + 1);
+    return sizeof(float) * (d > r ? d : r);
 }
 
 // ---- dhpre[r][j] = h > 0 ? sum_a dz[r][a] Wp[a][j] + dz[r][A] Wv[j] : 0
@@ -1731,11 +1765,22 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
     auto by_prec = [&](auto am) { return dh16 ? go(am, T{}, T{}) : bf ? go(am, T{}, F{}) : go(am, F{}, F{}); };
     const int rc = L.A <= 18 ? by_prec(std::integral_constant<int, 18>{}) : by_prec(std::integral_constant<int, kAMax>{});
     if (rc) return rc;
-    const int64_t nout = head_part_out(L);
-    hipLaunchKernelGGL(k_cnn_head_wsum, dim3((unsigned)((nout + kWsumOut - 1) / kWsumOut + 1)), dim3(256), 0, s,
-                       w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop);
-    GS_LAUNCH_CHECK("k_cnn_head_wsum");
-    return GS_OK;
+    const unsigned ncb = (unsigned)((L.HID + kWgCols - 1) / kWgCols);
+    auto wg = [&](auto am, auto bfc) {
+        constexpr int AM = decltype(am)::value;
+        constexpr bool BF = decltype(bfc)::value;
+        static std::once_flag attrs;      // > 64 KB of dynamic LDS (the update is never graph-captured)
+        std::call_once(attrs, [] {
+            (void)hipFuncSetAttribute((const void *)k_cnn_head_wgrad<AM, BF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)head_wgrad_lds<AM>());
+        });
+        hipLaunchKernelGGL((k_cnn_head_wgrad<AM, BF>), dim3(ncb + 1), dim3(1024), head_wgrad_lds<AM>(), s, w.h, w.dz,
+                           w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop);
+        GS_LAUNCH_CHECK("k_cnn_head_wgrad");
+        return GS_OK;
+    };
+    return L.A <= 18 ? (bf ? wg(std::integral_constant<int, 18>{}, T{}) : wg(std::integral_constant<int, 18>{}, F{}))
+                     : (bf ? wg(std::integral_constant<int, kAMax>{}, T{}) : wg(std::integral_constant<int, kAMax>{}, F{}));
 }
 
 
