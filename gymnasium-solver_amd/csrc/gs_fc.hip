@@ -785,6 +785,13 @@ extern "C" int gs_debug_fc_variant(int op, int v, int bf16, int64_t M, int64_t N
         case 5: return split([&](int S) { return launch_fc<64, 64, 2, 2, true, true, kEpiStore, 2, 2, 1, 1>(
                                  s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 2, EBR{});
         case 6: return launch_fc<64, 32, 1, 4, true, true, kEpiBiasRelu, 3, 3, 2, 1>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, aux, nullptr, 4);
+        // round 6: 128 x 128 tiles (2 x 2 waves of 64 x 64, a quarter of the
+        // L2 -> LDS bytes per MFMA of the 32 x 32 tiles) split over K so 224 / 256 workgroups fill the
+        // chip, the bias + ReLU epilogue in the ordered sum
+        case 7: return split([&](int S) { return launch_fc<128, 128, 2, 1, true, true, kEpiStore, 2, 2, 1, 1>(
+                                 s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 7, EBR{});
+        case 8: return split([&](int S) { return launch_fc<128, 64, 2, 1, true, true, kEpiStore, 2, 2, 1, 1>(
+                                 s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 7, EBR{});
         default: break;
         }
     } else if (op == 1) {
@@ -796,6 +803,10 @@ extern "C" int gs_debug_fc_variant(int op, int v, int bf16, int64_t M, int64_t N
                                  s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 2, EST{});
         case 4: return launch_fc<64, 64, 1, 4, false, false, kEpiStore, 2, 2, 4, 2>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 8);
         case 5: return launch_fc<64, 64, 2, 1, false, false, kEpiStore, 2, 2, 2, 1, true>(s, bf, A, lda, B, ldb, C, ldc, M, N, K, nullptr, nullptr, 8);
+        case 6: return split([&](int S) { return launch_fc<128, 128, 2, 1, false, false, kEpiStore, 2, 2, 1, 1>(
+                                 s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 2, EST{});
+        case 7: return split([&](int S) { return launch_fc<128, 128, 2, 1, false, false, kEpiStore, 2, 2, 1, 1>(
+                                 s, bf, A, lda, B, ldb, parts, N, M, N, K, nullptr, nullptr, 4, S, M * N); }, 4, EST{});
         default: break;
         }
     } else if (op == 2) {

@@ -52,7 +52,7 @@ def main():
                 ref = torch.where(aux.double() > 0, ref, torch.zeros_like(ref))
             scale = (rd(opA).abs() @ rd(opB).abs()).max().item() + 1.0
             bar = 2e-6 * scale * max(1.0, K ** 0.5 / 8)
-            for v in range(8):
+            for v in range(10):
                 out = torch.full((M, N), float("nan"), device=dev)
 
                 def run():
