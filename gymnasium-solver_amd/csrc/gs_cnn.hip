@@ -517,7 +517,7 @@ __device__ __forceinline__ void act_select_wave(const float *__restrict__ zsum, 
 // per-env act kernel.
 constexpr int kActMaxSplits = 16, kActMaxHid = 512;
 
-template <int AM>
+template <int AM, int NPS = kActMaxSplits>
 __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ parts, int np, int64_t pstride,
                                                       int64_t R, const float *__restrict__ P, CnnLayout L, int mode,
                                                       uint64_t seed, uint64_t counter, int64_t *__restrict__ actions,
@@ -529,7 +529,8 @@ __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ 
     __shared__ __attribute__((aligned(16))) float red2[(AM + 1) * 8];
     const int64_t r = blockIdx.x;
     const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
-    float t[NJ][kActMaxSplits], bfv[NJ], w[NJ][AM + 1];
+    static_assert(NPS <= kActMaxSplits, "split slots");
+    float t[NJ][NPS], bfv[NJ], w[NJ][AM + 1];
 #pragma unroll
     for (int u = 0; u < NJ; ++u) {
         const int j = min(tid + 256 * u, HID - 1);
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ 
         // register merge stalls the burst (slices past np, rows past A and j past HID are zeroed
         // by the factors below: exact)
 #pragma unroll
-        for (int p = 0; p < kActMaxSplits; ++p) t[u][p] = parts[(int64_t)min(p, np - 1) * pstride + r * HID + j];
+        for (int p = 0; p < NPS; ++p) t[u][p] = parts[(int64_t)min(p, np - 1) * pstride + r * HID + j];
         bfv[u] = P[L.obf + j];
 #pragma unroll
         for (int a = 0; a < AM + 1; ++a) w[u][a] = a < A ? P[L.oWp + (int64_t)a * HID + j] : P[L.oWv + j];
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_act(const float *__restrict__ 
     for (int u = 0; u < NJ; ++u) {
         float hv = 0.f;
 #pragma unroll
-        for (int p = 0; p < kActMaxSplits; ++p) hv += t[u][p] * (float)(p < np);
+        for (int p = 0; p < NPS; ++p) hv += t[u][p] * (float)(p < np);
         hv += bfv[u];
         hv = (hv > 0.f ? hv : 0.f) * (float)(tid + 256 * u < HID);
 #pragma unroll
@@ -1189,14 +1190,35 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
             for (int b = j; b < nparts; b += 16) v += part[(int64_t)b * kSums + q];
             msum[q][j] = v;
         }
-        // dbh[a] = sum_r dz[r][a] (rows in order, unrounded), unless the step is stopped
-        if (!(stop && *stop) && tid >= 256 && tid < 256 + A1) {
-            const int a2 = tid - 256;
-            float sb = 0.f;
-            for (int r = 0; r < B; ++r) sb += dz[(int64_t)r * A1 + a2];
-            G[a2 < A ? L.obp + a2 : L.obv] = sb;
+        // dbh[a] = sum_r dz[r][a] (unrounded): thread (a = tid & 31, slice q = tid >> 5) sums the
+        // q-th of 32 contiguous row ranges in row order, 8 loads in flight, then the slices in order
+        // (the first form, one thread per column over all B rows, waited out B dependent L2 loads:
+        // 83 us of the head's 90)
+        __shared__ float dbr[kWgSlices][kAMax + 2];
+        const bool live = !(stop && *stop);
+        {
+            const int q = tid >> 5, rs = (B + kWgSlices - 1) / kWgSlices;
+            const int ra = min(B, q * rs), rb = min(B, ra + rs);
+            for (int a2 = tid & 31; a2 < A1 && live; a2 += 32) {
+                float v = 0.f;
+                int r = ra;
+                for (; r + 8 <= rb; r += 8) {
+                    float t[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) t[u] = dz[(int64_t)(r + u) * A1 + a2];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v += t[u];
+                }
+                for (; r < rb; ++r) v += dz[(int64_t)r * A1 + a2];
+                dbr[q][a2] = v;
+            }
         }
         __syncthreads();
+        if (live && tid < A1) {
+            float sb = 0.f;
+            for (int q = 0; q < kWgSlices; ++q) sb += dbr[q][tid];
+            G[tid < A ? L.obp + tid : L.obv] = sb;
+        }
         if (tid < kSums) {
             double v = 0.0;
             for (int j = 0; j < 16; ++j) v += msum[tid][j];
@@ -2146,7 +2168,11 @@ extern "C" int gs_cnn_policy_act(const float *params, gs_cnn_dims dims, const ui
     GS_REQUIRE(sf <= kActMaxSplits && L.HID <= kActMaxHid, "gs_cnn_policy_act: fc splits %d / hidden %d exceed "
                "the act kernel's %d / %d", sf, L.HID, kActMaxSplits, kActMaxHid);
     const dim3 grid((unsigned)N);
-    if (L.A <= 18)
+    // the rollout shapes' 7 fc splits load 8 slots, not kActMaxSplits (the slots past sf add 0)
+    if (L.A <= 18 && sf <= 8)
+        hipLaunchKernelGGL((k_cnn_head_act<18, 8>), grid, dim3(256), 0, s, w.parts, sf, N * L.HID, N, params, L, mode,
+                           rng_seed, rng_counter, actions, logp, value, clock);
+    else if (L.A <= 18)
         hipLaunchKernelGGL(k_cnn_head_act<18>, grid, dim3(256), 0, s, w.parts, sf, N * L.HID, N, params, L, mode,
                            rng_seed, rng_counter, actions, logp, value, clock);
     else

@@ -1178,56 +1178,61 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
     C1S_DECL_K(G::KK == 512 ? 1 : 2)
     C1S_MARK(4)                                         // prologue
 
+    // input activation [pos][c] with stride CSX, dY [pos][co] with stride DS (zero rows past OHW):
+    // every load of a sample in one burst of BATCH float4 per thread, and the NEXT sample's burst
+    // issued right after this one's LDS stores, so its memory latency runs under this sample's
+    // MFMAs (round 5 waited each burst out: 7.0 / 4.8 of the 25 / 21 us of a conv2 / conv3
+    // workgroup, profiles/r05_conv_wgrad_stamps.txt)
+    // XH: the bf16 input in 16-B units of 8 channels (every load of the burst 16 B wide, so the
+    // two kinds share registers without a merge that would wait on each load)
+    constexpr int XU = XH ? 8 : 4;     // input elements per 16-B unit
+    constexpr int NXU = G::H * G::W * G::C / XU, ND4 = X::PP * G::CO / 4;
+    constexpr int NE = NXU + ND4, BATCH = (NE + 255) / 256;
+    static_assert(G::C % XU == 0, "whole units per position");
+    static_assert(BATCH <= kWgradBurstMax, "one staging burst per sample");
+    float4 v[BATCH];
+    auto burst = [&](int r) {
+        const act_t<XH> *xin = in + (int64_t)r * G::H * G::W * G::C;
+        const float *dyin = dY + (int64_t)r * G::OHW * G::CO;
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) {
+            const int e = tid + 256 * j;
+            if (e < NXU) {
+                v[j] = *reinterpret_cast<const float4 *>(xin + XU * (int64_t)e);
+            } else {
+                const int d = e - NXU;
+                const int p = d / (G::CO / 4);
+                v[j] = (e < NE && p < G::OHW) ? *reinterpret_cast<const float4 *>(dyin + 4 * (int64_t)d)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    if ((int)blockIdx.x < R) burst(blockIdx.x);
+
     for (int r = blockIdx.x; r < R; r += gridDim.x) {
         __syncthreads();
         C1S_MARK(3)                                     // loop-top barrier
-        {   // input activation [pos][c] with stride CSX, dY [pos][co] with stride DS (zero rows past OHW)
-            // every load of the sample in one burst (one memory latency per sample; 8 per burst
-            // took 2 - 3 round trips)
-            // XH: the bf16 input in 16-B units of 8 channels (every load of the burst 16 B wide, so
-            // the two kinds share registers without a merge that would wait on each load)
-            constexpr int XU = XH ? 8 : 4;     // input elements per 16-B unit
-            constexpr int NXU = G::H * G::W * G::C / XU, ND4 = X::PP * G::CO / 4;
-            constexpr int NE = NXU + ND4, BATCH = (NE + 255) / 256 <= kWgradBurstMax ? (NE + 255) / 256 : 8;
-            static_assert(G::C % XU == 0, "whole units per position");
-            const act_t<XH> *xin = in + (int64_t)r * G::H * G::W * G::C;
-            const float *dyin = dY + (int64_t)r * G::OHW * G::CO;
-            for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
-                float4 v[BATCH];
 #pragma unroll
-                for (int j = 0; j < BATCH; ++j) {
-                    const int e = e0 + tid + 256 * j;
-                    if (e < NXU) {
-                        v[j] = *reinterpret_cast<const float4 *>(xin + XU * (int64_t)e);
-                    } else {
-                        const int d = e - NXU;
-                        const int p = d / (G::CO / 4);
-                        v[j] = (e < NE && p < G::OHW) ? *reinterpret_cast<const float4 *>(dyin + 4 * (int64_t)d)
-                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
+        for (int j = 0; j < BATCH; ++j) {
+            const int e = tid + 256 * j;
+            if (e < NXU) {
+                const int pos = e / (G::C / XU), cu = e - pos * (G::C / XU);
+                float *dst = xs + pos * X::CSX + XU * cu;
+                if constexpr (XH) {     // 8 stored bf16 -> their exact fp32 values
+                    const uint4 h = make_uint4(__float_as_uint(v[j].x), __float_as_uint(v[j].y),
+                                               __float_as_uint(v[j].z), __float_as_uint(v[j].w));
+                    *reinterpret_cast<float4 *>(dst) = bf16x4_f32(make_uint2(h.x, h.y));
+                    *reinterpret_cast<float4 *>(dst + 4) = bf16x4_f32(make_uint2(h.z, h.w));
+                } else {
+                    *reinterpret_cast<float4 *>(dst) = v[j];
                 }
-#pragma unroll
-                for (int j = 0; j < BATCH; ++j) {
-                    const int e = e0 + tid + 256 * j;
-                    if (e < NXU) {
-                        const int pos = e / (G::C / XU), cu = e - pos * (G::C / XU);
-                        float *dst = xs + pos * X::CSX + XU * cu;
-                        if constexpr (XH) {     // 8 stored bf16 -> their exact fp32 values
-                            const uint4 h = make_uint4(__float_as_uint(v[j].x), __float_as_uint(v[j].y),
-                                                       __float_as_uint(v[j].z), __float_as_uint(v[j].w));
-                            *reinterpret_cast<float4 *>(dst) = bf16x4_f32(make_uint2(h.x, h.y));
-                            *reinterpret_cast<float4 *>(dst + 4) = bf16x4_f32(make_uint2(h.z, h.w));
-                        } else {
-                            *reinterpret_cast<float4 *>(dst) = v[j];
-                        }
-                    } else if (e < NE) {
-                        const int d = e - NXU;
-                        const int p = d / (G::CO / 4), c4 = d - p * (G::CO / 4);
-                        *reinterpret_cast<float4 *>(ds + p * X::DS + 4 * c4) = v[j];
-                    }
-                }
+            } else if (e < NE) {
+                const int d = e - NXU;
+                const int p = d / (G::CO / 4), c4 = d - p * (G::CO / 4);
+                *reinterpret_cast<float4 *>(ds + p * X::DS + 4 * c4) = v[j];
             }
         }
+        if (r + (int)gridDim.x < R) burst(r + gridDim.x);     // the next sample's loads in flight
         C1S_MARK(1)                                     // staging burst landed + LDS stores
         __syncthreads();
         C1S_MARK(2)                                     // barrier
@@ -1319,6 +1324,10 @@ using C2_84x = CN<20, 20, 32, 4, 2, 1>;
 using C3_84b = CN<9, 9, 64, 3, 1, 2>;
 constexpr int kConv2BfFS = 1;              // 2 (filter blocks split over two workgroups): 52.2 us
 constexpr int kConvFwdSmallWG = 1024;     // FS = 2 up to this many workgroups (R <= 512)
+#ifndef GS_CONV_TINY_FS
+#define GS_CONV_TINY_FS 2
+#endif
+constexpr int kConvTinyFS = GS_CONV_TINY_FS;     // fp32 FS up to kConvFwdSmallWG workgroups (4: R <= 256)
 constexpr int kConv1PairsFrom = 512;     // bf16: kConv1Spb samples per conv1 forward workgroup from this many rows
 constexpr int kConv1Spb = 2;
 #ifndef GS_C1WG_DEPTH
@@ -1458,7 +1467,11 @@ int launch_conv_fwd(hipStream_t s, int R, const void *in, const void *Wv, const 
         GS_LAUNCH_CHECK("k_conv_fwd<stats>");
         return GS_OK;
     }
-    if ((int64_t)R * 2 <= kConvFwdSmallWG) {
+    if (kConvTinyFS > 2 && !bf && (int64_t)R * kConvTinyFS <= kConvFwdSmallWG) {
+        // the fp32 policy act at rollout sizes: kConvTinyFS workgroups per sample
+        const dim3 grid((unsigned)(kConvTinyFS * R));
+        hipLaunchKernelGGL((k_conv_fwd<G1, false, kConvTinyFS>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);
+    } else if ((int64_t)R * 2 <= kConvFwdSmallWG) {
         const dim3 grid((unsigned)(2 * R));
         if (xh) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2, true>), grid, dim3(256), 0, s, i16, R, Wh, bias, o16);
         else if (bf) hipLaunchKernelGGL((k_conv_fwd<G1, true, 2>), grid, dim3(256), 0, s, i32, R, Wt, bias, o32);

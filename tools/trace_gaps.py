@@ -10,7 +10,8 @@ from collections import defaultdict
 
 
 def short(name):
-    n = re.sub(r"\(.*$", "", name)
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*$", "", n)
     n = re.sub(r"<.*$", "", n.replace("void ", ""))
     return n.split("::")[-1]
 
