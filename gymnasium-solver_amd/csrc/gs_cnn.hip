@@ -1167,7 +1167,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 // 32 slices added in slice order.  Then its dbf columns over the partials (32 ranges, in order).  The
 // last workgroup: dbh (column sums of dz, rows in order) and the record from the loss partials (sets
 // the KL stop).
-constexpr int kWgChunk = 1024, kWgCols = 32, kWgSlices = 32, kWgRows = kWgChunk / kWgSlices;
+constexpr int kWgChunk = 512, kWgCols = 32, kWgSlices = 32, kWgRows = kWgChunk / kWgSlices;
 template <int AM, bool BF>
 __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict__ h, const float *__restrict__ dz,
                                                          const float *__restrict__ dbf_part, int nparts, CnnLayout L,
@@ -1184,10 +1184,17 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
         // then the 16 in order; thread 0 writes it from a one-partial view of the totals
         __shared__ double msum[kSums][16];
         __shared__ double tot[kSums];
-        if (tid < kSums * 16) {
+        if (tid < kSums * 16) {     // 8 loads in flight per group (b ascending: the same sum)
             const int q = tid >> 4, j = tid & 15;
             double v = 0.0;
-            for (int b = j; b < nparts; b += 16) v += part[(int64_t)b * kSums + q];
+            for (int b0 = j; b0 < nparts; b0 += 16 * 8) {
+                double t[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t[u] = part[(int64_t)min(b0 + 16 * u, nparts - 1) * kSums + q];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (b0 + 16 * u < nparts) v += t[u];
+            }
             msum[q][j] = v;
         }
         // dbh[a] = sum_r dz[r][a] (unrounded): thread (a = tid & 31, slice q = tid >> 5) sums the
@@ -1241,15 +1248,44 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
     float g[AP];
 #pragma unroll
     for (int a = 0; a < AP; ++a) g[a] = 0.f;
+    constexpr int SPT = kWgChunk * AP / 1024;      // dz staging units per thread
+    static_assert(kWgChunk * AP % 1024 == 0, "whole dz staging units per thread");
+    // this workgroup's dbf columns: the partials of the workgroups in order, 32 ranges of them
+    // (loads issued here, 8 in flight per group, so they land under the chunk's loads)
+    float fs = 0.f;
+    {
+        const int w0 = (q * nparts) / kWgSlices, w1 = ((q + 1) * nparts) / kWgSlices;
+        for (int w = w0; w < w1; w += 8) {
+            float t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = dbf_part[min(w + u, w1 - 1) * HID + colc];     // 32-bit offsets
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (w + u < w1) fs += t[u];
+        }
+    }
     for (int r0 = 0; r0 < B; r0 += kWgChunk) {
         const int nr = min(kWgChunk, B - r0);
-        float hv[kWgRows];                     // rows q, q + 32, ... of the chunk: every load in flight
+        // every load of the chunk in flight at once: rows q, q + 32, ... of h, and the dz staging
+        // units tid + 1024 k (clamped, unconditional; the first form's staging loop waited out
+        // one load per iteration)
+        // (32-bit offsets from the chunk's uniform base: one VGPR per load address)
+        float hv[kWgRows], dv[SPT];
+        const float *hc = h + (int64_t)r0 * HID, *dc = dz + (int64_t)r0 * A1;
 #pragma unroll
-        for (int j = 0; j < kWgRows; ++j) hv[j] = h[(int64_t)(r0 + min(q + kWgSlices * j, nr - 1)) * HID + colc];
+        for (int j = 0; j < kWgRows; ++j) hv[j] = hc[min(q + kWgSlices * j, nr - 1) * HID + colc];
+#pragma unroll
+        for (int k = 0; k < SPT; ++k) {
+            const int u = tid + 1024 * k, r = u / AP, a = u - r * AP;
+            dv[k] = dc[min(r, nr - 1) * A1 + min(a, A1 - 1)];
+        }
         if (r0 > 0) __syncthreads();           // the previous chunk's dz reads are done
-        for (int u = tid; u < nr * AP; u += 1024) {
-            const int r = u / AP, a = u - r * AP;
-            lds[u] = a < A1 ? dz[(int64_t)(r0 + r) * A1 + a] : 0.f;
+        // BF: dz rounded to its bf16 operand value once here, not by each of the 32 column threads
+#pragma unroll
+        for (int k = 0; k < SPT; ++k) {
+            const int u = tid + 1024 * k, r = u / AP, a = u - r * AP;
+            const float v = (r < nr && a < A1) ? dv[k] : 0.f;
+            lds[u] = BF ? bf16r(v) : v;
         }
         __syncthreads();
 #pragma unroll 4
@@ -1260,18 +1296,12 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
 #pragma unroll
             for (int a4 = 0; a4 < AP; a4 += 4) {
                 const float4 d = *reinterpret_cast<const float4 *>(lds + r * AP + a4);
-                g[a4 + 0] = fmaf(BF ? bf16r(d.x) : d.x, hb, g[a4 + 0]);
-                g[a4 + 1] = fmaf(BF ? bf16r(d.y) : d.y, hb, g[a4 + 1]);
-                g[a4 + 2] = fmaf(BF ? bf16r(d.z) : d.z, hb, g[a4 + 2]);
-                g[a4 + 3] = fmaf(BF ? bf16r(d.w) : d.w, hb, g[a4 + 3]);
+                g[a4 + 0] = fmaf(d.x, hb, g[a4 + 0]);
+                g[a4 + 1] = fmaf(d.y, hb, g[a4 + 1]);
+                g[a4 + 2] = fmaf(d.z, hb, g[a4 + 2]);
+                g[a4 + 3] = fmaf(d.w, hb, g[a4 + 3]);
             }
         }
-    }
-    // this workgroup's dbf columns: the partials of the workgroups in order, 32 ranges of them
-    float fs = 0.f;
-    {
-        const int w0 = (q * nparts) / kWgSlices, w1 = ((q + 1) * nparts) / kWgSlices;
-        for (int w = w0; w < w1; ++w) fs += dbf_part[(int64_t)w * HID + colc];
     }
     __syncthreads();                           // the dz tile is dead: the slice partials reuse its LDS
     float *red = lds;                          // [slice][col][AP + 1]

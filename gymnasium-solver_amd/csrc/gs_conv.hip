@@ -1149,6 +1149,12 @@ struct WG2 {
 };
 
 constexpr int kWgradBurstMax = 24;      // float4 per thread of one staging burst (conv2: 18, conv3: 9)
+#ifndef GS_WGRAD_PF
+#define GS_WGRAD_PF 1
+#endif
+// the layers (bit 0: conv2, bit 1: conv3) whose weight gradient issues the next sample's staging
+// burst before this sample's MFMAs (same-box A/B)
+constexpr int kWgradPrefetch = GS_WGRAD_PF;
 // XH: the input activation stored as bf16 (staged to LDS as its exact fp32 value)
 template <class G, bool BF = false, bool XH = false>
 __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict__ in, const float *__restrict__ dY, int R,
@@ -1190,6 +1196,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
     constexpr int NE = NXU + ND4, BATCH = (NE + 255) / 256;
     static_assert(G::C % XU == 0, "whole units per position");
     static_assert(BATCH <= kWgradBurstMax, "one staging burst per sample");
+    constexpr bool PF = (kWgradPrefetch & (G::C == 32 ? 1 : 2)) != 0;     // conv2: C = 32, conv3: 64
     float4 v[BATCH];
     auto burst = [&](int r) {
         const act_t<XH> *xin = in + (int64_t)r * G::H * G::W * G::C;
@@ -1207,11 +1214,12 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
             }
         }
     };
-    if ((int)blockIdx.x < R) burst(blockIdx.x);
+    if (PF && (int)blockIdx.x < R) burst(blockIdx.x);
 
     for (int r = blockIdx.x; r < R; r += gridDim.x) {
         __syncthreads();
         C1S_MARK(3)                                     // loop-top barrier
+        if (!PF) burst(r);
 #pragma unroll
         for (int j = 0; j < BATCH; ++j) {
             const int e = tid + 256 * j;
@@ -1232,7 +1240,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
                 *reinterpret_cast<float4 *>(ds + p * X::DS + 4 * c4) = v[j];
             }
         }
-        if (r + (int)gridDim.x < R) burst(r + gridDim.x);     // the next sample's loads in flight
+        if (PF && r + (int)gridDim.x < R) burst(r + gridDim.x);     // the next sample's loads in flight
         C1S_MARK(1)                                     // staging burst landed + LDS stores
         __syncthreads();
         C1S_MARK(2)                                     // barrier
@@ -1325,7 +1333,7 @@ using C3_84b = CN<9, 9, 64, 3, 1, 2>;
 constexpr int kConv2BfFS = 1;              // 2 (filter blocks split over two workgroups): 52.2 us
 constexpr int kConvFwdSmallWG = 1024;     // FS = 2 up to this many workgroups (R <= 512)
 #ifndef GS_CONV_TINY_FS
-#define GS_CONV_TINY_FS 2
+#define GS_CONV_TINY_FS 4
 #endif
 constexpr int kConvTinyFS = GS_CONV_TINY_FS;     // fp32 FS up to kConvFwdSmallWG workgroups (4: R <= 256)
 constexpr int kConv1PairsFrom = 512;     // bf16: kConv1Spb samples per conv1 forward workgroup from this many rows
