@@ -91,7 +91,7 @@ struct CnnLayout {
 };
 
 struct CnnWs {
-    float *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dh, *da3, *da2, *da1;
+    float *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dzp, *dh, *da3, *da2, *da1;
     int32_t *f_act;
     float *f_olp, *f_ov, *f_adv, *f_ret;
     double *norm_part;
@@ -112,6 +112,7 @@ struct CnnWs {
 
 constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block sums them)
 constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
+constexpr int kConv1NormMax = 1024;   // k_conv1_sum_norm sum blocks (conv1 [dW1 | db1] <= 64 K floats)
 constexpr int kPreChunk = 16;      // minibatches per ahead-of-time fields gather (k_cnn_gather_chunk)
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
 #ifndef GS_HEAD_ROWS
@@ -188,6 +189,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.h = (float *)take(sizeof(float) * R * L.HID);
     w.z = (float *)take(sizeof(float) * R * (L.A + 1));
     w.dz = (float *)take(sizeof(float) * R * (L.A + 1));
+    w.dzp = (float *)take(sizeof(float) * R * head_part_rows(L));    // dz padded (k_cnn_head_wgrad's operand)
     w.dh = (float *)take(sizeof(float) * R * L.HID);
     w.da3 = (float *)take(sizeof(float) * R * L.F);
     w.da2 = (float *)take(sizeof(float) * L.rows2(R) * L.c2);
@@ -197,7 +199,8 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_ov = (float *)take(sizeof(float) * R);
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
-    w.norm_part = (double *)take(sizeof(double) * kNormBlocks * 5);   // total + 4 component partials
+    // total + 4 component partials, then k_conv1_sum_norm's conv1 partials
+    w.norm_part = (double *)take(sizeof(double) * (kNormBlocks * 5 + kConv1NormMax));
     w.pre = (float *)take(sizeof(float) * kPreChunk * 5 * R);
     w.pre_stats = (float *)take(sizeof(float) * kPreChunk * 2);
     {   // shifted so Wf's rows start on 128-B lines (the fc kernels stream them in 128-B chunks; a
@@ -951,9 +954,9 @@ size_t head_loss_lds(const CnnLayout &L)
 template <int AM, bool BF, bool DH16 = false>
 __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__ h, const float *__restrict__ P,
                                                        CnnLayout L, int B, CnnFields fl, LossArgs la,
-                                                       float *__restrict__ dz, void *__restrict__ dhv,
-                                                       float *__restrict__ wpart, double *__restrict__ part,
-                                                       const int32_t *__restrict__ stop)
+                                                       float *__restrict__ dz, float *__restrict__ dzp,
+                                                       void *__restrict__ dhv, float *__restrict__ wpart,
+                                                       double *__restrict__ part, const int32_t *__restrict__ stop)
 {
     static_assert(!DH16 || BF, "bf16 dh storage: bf16 operands only");
     constexpr int NZ = (AM + 1 + 3) / 4;               // float4 chunks of a padded head row
@@ -1119,6 +1122,14 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     GS_STAMP(5)
     if (tid == 0)
         for (int q = 0; q < kSums; ++q) part[(int64_t)blockIdx.x * kSums + q] = acc[q];
+    {   // the rows' dz for k_cnn_head_wgrad: padded to AP columns (zeros past A1), BF: the bf16 operand
+        constexpr int AP = (AM + 1 + 3) & ~3;
+        if (tid < kHeadRows * AP) {
+            const int row = tid / AP, c = tid - row * AP;
+            const float v = c < A1 ? zs[row * ZS + c] : 0.f;
+            if (r0 + row < B) dzp[(int64_t)(r0 + row) * AP + c] = BF ? bf16r(v) : v;
+        }
+    }
     float *wp = wpart + (int64_t)blockIdx.x * HID;      // this workgroup's dbf partial
     for (int j = tid; j < HID; j += 256) {
         float w[4 * NZ];
@@ -1160,23 +1171,26 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 // [dWh | dbh] = dz^T [h | 1] over all B rows of the minibatch, dbf = the k_cnn_head_loss dbf partials
 // summed in workgroup order, and the minibatch record — one launch, no per-workgroup [dWh | dbh]
 // partials (round 5 wrote 256 of them, 10 MB per minibatch, and summed them in a second pass).
-// Workgroup x < HID / 32 (1024 threads): h columns [32 x, 32 x + 32) for every head row a < A1;
-// thread (c = tid & 31, slice q = tid >> 5) takes rows q, q + 32, ... of each kWgChunk-row chunk
-// (its h loads all in flight at once, coalesced 128-B rows) against the chunk's dz staged in LDS
-// (rows padded to float4), fp32 FMA (BF: both operands rounded to bf16, the emulation's product); the
-// 32 slices added in slice order.  Then its dbf columns over the partials (32 ranges, in order).  The
-// last workgroup: dbh (column sums of dz, rows in order) and the record from the loss partials (sets
-// the KL stop).
-constexpr int kWgChunk = 512, kWgCols = 32, kWgSlices = 32, kWgRows = kWgChunk / kWgSlices;
+// Workgroup x < HID / 64 (1024 threads = 16 waves): h columns [64 x, 64 x + 64), one per lane, for
+// every head row a < A1; wave q takes rows q, q + 16, ... (its h loads 32 rows at a time, all in
+// flight, 256-B coalesced), against the row's dz from dzp — k_cnn_head_loss's copy of dz padded to
+// AP columns (BF: rounded to the bf16 operand) — at a wave-uniform address, so the 80 / 144 B of a
+// row come through the scalar cache into SGPRs (the first form broadcast them from LDS: 5 - 9
+// ds_read_b128 per row per wave, LDS-bound at 18 us); fp32 FMA (BF: h rounded to bf16 as well); the
+// 16 slices added in slice order.  Then its dbf columns over the partials (16 ranges, in order).
+// The last workgroup: dbh (column sums of the unrounded dz) and the record from the loss partials
+// (sets the KL stop).
+constexpr int kWgCols = 64, kWgSlices = 16, kWgRows = 32, kDbhSlices = 32;
 template <int AM, bool BF>
 __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict__ h, const float *__restrict__ dz,
+                                                         const float *__restrict__ dzp,
                                                          const float *__restrict__ dbf_part, int nparts, CnnLayout L,
                                                          float *__restrict__ G, const double *__restrict__ part, int B,
                                                          LossArgs la, float *__restrict__ metrics,
                                                          int32_t *__restrict__ stop)
 {
     constexpr int AP = (AM + 1 + 3) & ~3;      // head rows padded to float4 (accumulators)
-    extern __shared__ float lds[];             // max(kWgChunk x AP dz, kWgSlices x kWgCols x (AP + 1) partials)
+    extern __shared__ float lds[];             // kWgSlices x kWgCols x (AP + 1) slice partials
     const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
     const int ncb = (HID + kWgCols - 1) / kWgCols;
     if ((int)blockIdx.x == ncb) {
@@ -1201,10 +1215,10 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
         // q-th of 32 contiguous row ranges in row order, 8 loads in flight, then the slices in order
         // (the first form, one thread per column over all B rows, waited out B dependent L2 loads:
         // 83 us of the head's 90)
-        __shared__ float dbr[kWgSlices][kAMax + 2];
+        __shared__ float dbr[kDbhSlices][kAMax + 2];
         const bool live = !(stop && *stop);
         {
-            const int q = tid >> 5, rs = (B + kWgSlices - 1) / kWgSlices;
+            const int q = tid >> 5, rs = (B + kDbhSlices - 1) / kDbhSlices;
             const int ra = min(B, q * rs), rb = min(B, ra + rs);
             for (int a2 = tid & 31; a2 < A1 && live; a2 += 32) {
                 float v = 0.f;
@@ -1223,7 +1237,7 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
         __syncthreads();
         if (live && tid < A1) {
             float sb = 0.f;
-            for (int q = 0; q < kWgSlices; ++q) sb += dbr[q][tid];
+            for (int q = 0; q < kDbhSlices; ++q) sb += dbr[q][tid];
             G[tid < A ? L.obp + tid : L.obv] = sb;
         }
         if (tid < kSums) {
@@ -1242,16 +1256,15 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
         return;
     }
     if (stop && *stop) return;
-    const int c = tid & (kWgCols - 1), q = tid >> 5;
+    const int c = tid & (kWgCols - 1);
+    const int q = __builtin_amdgcn_readfirstlane(tid >> 6);     // the wave's row slice (uniform)
     const int col = blockIdx.x * kWgCols + c;
     const int colc = col < HID ? col : HID - 1;
     float g[AP];
 #pragma unroll
     for (int a = 0; a < AP; ++a) g[a] = 0.f;
-    constexpr int SPT = kWgChunk * AP / 1024;      // dz staging units per thread
-    static_assert(kWgChunk * AP % 1024 == 0, "whole dz staging units per thread");
-    // this workgroup's dbf columns: the partials of the workgroups in order, 32 ranges of them
-    // (loads issued here, 8 in flight per group, so they land under the chunk's loads)
+    // this workgroup's dbf columns: the partials of the workgroups in order, 16 ranges of them
+    // (loads issued first, 8 in flight per group, so they land under the row loads)
     float fs = 0.f;
     {
         const int w0 = (q * nparts) / kWgSlices, w1 = ((q + 1) * nparts) / kWgSlices;
@@ -1264,46 +1277,20 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
                 if (w + u < w1) fs += t[u];
         }
     }
-    for (int r0 = 0; r0 < B; r0 += kWgChunk) {
-        const int nr = min(kWgChunk, B - r0);
-        // every load of the chunk in flight at once: rows q, q + 32, ... of h, and the dz staging
-        // units tid + 1024 k (clamped, unconditional; the first form's staging loop waited out
-        // one load per iteration)
-        // (32-bit offsets from the chunk's uniform base: one VGPR per load address)
-        float hv[kWgRows], dv[SPT];
-        const float *hc = h + (int64_t)r0 * HID, *dc = dz + (int64_t)r0 * A1;
+    const int nrow = (B - q + kWgSlices - 1) / kWgSlices;       // rows q, q + 16, ... < B
+    for (int m0 = 0; m0 < nrow; m0 += kWgRows) {
+        float hv[kWgRows];
 #pragma unroll
-        for (int j = 0; j < kWgRows; ++j) hv[j] = hc[min(q + kWgSlices * j, nr - 1) * HID + colc];
-#pragma unroll
-        for (int k = 0; k < SPT; ++k) {
-            const int u = tid + 1024 * k, r = u / AP, a = u - r * AP;
-            dv[k] = dc[min(r, nr - 1) * A1 + min(a, A1 - 1)];
-        }
-        if (r0 > 0) __syncthreads();           // the previous chunk's dz reads are done
-        // BF: dz rounded to its bf16 operand value once here, not by each of the 32 column threads
-#pragma unroll
-        for (int k = 0; k < SPT; ++k) {
-            const int u = tid + 1024 * k, r = u / AP, a = u - r * AP;
-            const float v = (r < nr && a < A1) ? dv[k] : 0.f;
-            lds[u] = BF ? bf16r(v) : v;
-        }
-        __syncthreads();
+        for (int j = 0; j < kWgRows; ++j) hv[j] = h[min(q + kWgSlices * (m0 + j), B - 1) * HID + colc];
 #pragma unroll 4
         for (int j = 0; j < kWgRows; ++j) {
-            const int r = q + kWgSlices * j;
-            if (r >= nr) break;
+            if (m0 + j >= nrow) break;
+            const float *dr = dzp + (q + kWgSlices * (m0 + j)) * AP;     // uniform: scalar loads
             const float hb = BF ? bf16r(hv[j]) : hv[j];
 #pragma unroll
-            for (int a4 = 0; a4 < AP; a4 += 4) {
-                const float4 d = *reinterpret_cast<const float4 *>(lds + r * AP + a4);
-                g[a4 + 0] = fmaf(d.x, hb, g[a4 + 0]);
-                g[a4 + 1] = fmaf(d.y, hb, g[a4 + 1]);
-                g[a4 + 2] = fmaf(d.z, hb, g[a4 + 2]);
-                g[a4 + 3] = fmaf(d.w, hb, g[a4 + 3]);
-            }
+            for (int a = 0; a < AP; ++a) g[a] = fmaf(dr[a], hb, g[a]);
         }
     }
-    __syncthreads();                           // the dz tile is dead: the slice partials reuse its LDS
     float *red = lds;                          // [slice][col][AP + 1]
     constexpr int RS = AP + 1;
 #pragma unroll
@@ -1325,8 +1312,7 @@ template <int AM>
 constexpr size_t head_wgrad_lds()
 {
     constexpr int AP = (AM + 1 + 3) & ~3;
-    constexpr size_t d = (size_t)kWgChunk * AP, r = (size_t)kWgSlices * kWgCols * (AP + 1);
-    return sizeof(float) * (d > r ? d : r);
+    return sizeof(float) * (size_t)kWgSlices * kWgCols * (AP + 1);
 }
 
 // ---- dhpre[r][j] = h > 0 ? sum_a dz[r][a] Wp[a][j] + dz[r][A] Wv[j] : 0
@@ -1362,17 +1348,17 @@ __device__ __forceinline__ void add_sq(double (&s)[5], double g2, int c)
 // part[0 .. nb): the block partials of the whole gradient; part[nb (1 + c) + b]: component c's
 // (c = cnn trunk, mlp trunk, policy_head, value_head: flat ranges split at cut[0..2]) for the
 // per-component norms (utils/models.py:196-230)
-__global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__ G, int64_t n, double *__restrict__ part,
-                                                       const int32_t *__restrict__ stop, int64_t cut0, int64_t cut1,
-                                                       int64_t cut2)
+// block b of nb over G[0, n), element k's component by k + koff (the kernel below and the conv1
+// sum's norm blocks)
+__device__ __forceinline__ void norm_partials_block(const float *__restrict__ G, int64_t n, int64_t koff,
+                                                    double *__restrict__ part, int b, int nb, int64_t cut0,
+                                                    int64_t cut1, int64_t cut2, double *sred)
 {
-    if (stop && *stop) return;
-    __shared__ double sred[5 * (256 + 16)];
     double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    // float4 chunks (G is 256-B aligned), NB of them in flight per thread, then the scalar tail
-    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
+    // float4 chunks (G is 16-B aligned), NB of them in flight per thread, then the scalar tail
+    const int64_t n4 = n / 4, stride = (int64_t)nb * 256;
     constexpr int NB = 8;
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += stride * NB) {
+    for (int64_t i0 = (int64_t)b * 256 + threadIdx.x; i0 < n4; i0 += stride * NB) {
         float4 t[NB];
 #pragma unroll
         for (int j = 0; j < NB; ++j) t[j] = reinterpret_cast<const float4 *>(G)[min(i0 + stride * j, n4 - 1)];
@@ -1383,18 +1369,94 @@ __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__
             const float e[4] = {t[j].x, t[j].y, t[j].z, t[j].w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int64_t k = 4 * i + q;
+                const int64_t k = 4 * i + q + koff;
                 const double g = (double)e[q];
                 add_sq(s, g * g, (k >= cut0) + (k >= cut1) + (k >= cut2));
             }
         }
     }
-    for (int64_t k = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) {
+    for (int64_t k = 4 * n4 + (int64_t)b * 256 + threadIdx.x; k < n; k += stride) {
         const double g = (double)G[k];
-        add_sq(s, g * g, (k >= cut0) + (k >= cut1) + (k >= cut2));
+        add_sq(s, g * g, (k + koff >= cut0) + (k + koff >= cut1) + (k + koff >= cut2));
     }
     wg_reduce<5>(s, sred);
-    if (threadIdx.x < 5) part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s[threadIdx.x];
+    if (threadIdx.x < 5) part[(int64_t)threadIdx.x * nb + b] = s[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__ G, int64_t n, double *__restrict__ part,
+                                                       const int32_t *__restrict__ stop, int64_t cut0, int64_t cut1,
+                                                       int64_t cut2)
+{
+    if (stop && *stop) return;
+    __shared__ double sred[5 * (256 + 16)];
+    norm_partials_block(G, n, 0, part, blockIdx.x, gridDim.x, cut0, cut1, cut2, sred);
+}
+
+// ---- one launch for the end of the backward (no exchange follows): blocks [0, nsum) sum conv1's
+// [dW1 | db1] (G[0, n1)) from its weight-gradient partials exactly as k_sum_parts4 (the same float4
+// chains and group tree: bit-identical), each also writing the double sum of squares of its
+// outputs to part1[b] (component: the cnn trunk); blocks [nsum, nsum + kNormBlocks) write the
+// norm partials of G[n1, n) as k_norm_partials — the conv2 / conv3 / fc / head gradients, final
+// before this launch.  The clip + Adam launch adds part1 to the total and the trunk's component.
+// Replaces the conv1 sum and the norm pass (two launches, 4.8 + 5.8 us per C4 minibatch).
+__global__ __launch_bounds__(256) void k_conv1_sum_norm(const float *__restrict__ parts, int np, int64_t pstride,
+                                                        int64_t n1, int nsum, float *__restrict__ G, int64_t n,
+                                                        double *__restrict__ part, double *__restrict__ part1,
+                                                        const int32_t *__restrict__ stop, int64_t cut0, int64_t cut1,
+                                                        int64_t cut2)
+{
+    __shared__ double sred[5 * (256 + 16)];
+    if ((int)blockIdx.x >= nsum) {
+        if (stop && *stop) return;
+        norm_partials_block(G + n1, n - n1, n1, part, (int)blockIdx.x - nsum, kNormBlocks, cut0, cut1, cut2, sred);
+        return;
+    }
+    __shared__ float4 red[16][16];
+    __shared__ double sq[16];
+    const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int64_t i4 = (int64_t)blockIdx.x * 16 + c;
+    const bool ok = 4 * i4 < n1;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+        const float4 *src = reinterpret_cast<const float4 *>(parts) + i4;
+        const int64_t ps4 = pstride / 4;
+        int p = g;
+        for (; p + 112 < np; p += 128) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(p + 16 * u) * ps4];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a.x += v[u].x, a.y += v[u].y, a.z += v[u].z, a.w += v[u].w;
+        }
+        for (; p < np; p += 16) {
+            const float4 v = src[(int64_t)p * ps4];
+            a.x += v.x, a.y += v.y, a.z += v.z, a.w += v.w;
+        }
+    }
+    red[g][c] = a;
+    __syncthreads();
+    if (g == 0) {
+        float4 t = red[0][c];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) {
+            const float4 v = red[k][c];
+            t.x += v.x, t.y += v.y, t.z += v.z, t.w += v.w;
+        }
+        double q2 = 0.0;
+        if (ok) {
+            reinterpret_cast<float4 *>(G)[i4] = t;
+            const double e[4] = {(double)t.x, (double)t.y, (double)t.z, (double)t.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) q2 += e[q] * e[q];
+        }
+        sq[c] = q2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double v = 0.0;
+        for (int k = 0; k < 16; ++k) v += sq[k];
+        part1[blockIdx.x] = v;
+    }
 }
 
 // ---- the fields and advantage statistics of gridDim.x consecutive minibatches (workgroup k: sampler
@@ -1436,7 +1498,8 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
                                                         float *__restrict__ M, float *__restrict__ V, int64_t n,
                                                         const double *__restrict__ part, int nparts, AdamArgs aa,
                                                         float *__restrict__ metrics, const int32_t *__restrict__ stop,
-                                                        uint16_t *__restrict__ Pbf)
+                                                        uint16_t *__restrict__ Pbf, const double *__restrict__ part1,
+                                                        int nparts1)
 {
     if (stop && *stop) {
         // a job-wide stop (the exchange ORs the ranks' stop bits): no step on any rank
@@ -1467,12 +1530,14 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     double s[1] = {0.0};
     for (int k = threadIdx.x; k < nparts; k += 256) s[0] += part[k];
+    for (int k = threadIdx.x; k < nparts1; k += 256) s[0] += part1[k];      // conv1's (k_conv1_sum_norm)
     wg_reduce<1>(s, sred);
     if ((int)blockIdx.x == last && metrics) {     // per-component norms (utils/models.py:196-230)
         double c[4] = {0.0, 0.0, 0.0, 0.0};
         for (int k = threadIdx.x; k < nparts; k += 256)
 #pragma unroll
             for (int q = 0; q < 4; ++q) c[q] += part[(int64_t)(1 + q) * nparts + k];
+        for (int k = threadIdx.x; k < nparts1; k += 256) c[0] += part1[k];
         __shared__ double cred[4 * (256 + 16)];
         wg_reduce<4>(c, cred);
         if (threadIdx.x == 0) {
@@ -1656,7 +1721,8 @@ int forward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t R, c
 }
 
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc = false, bool xh = false);
+                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc = false, bool xh = false,
+                   int *nsum1 = nullptr);
 
 int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
              const int32_t *stop, hipStream_t s, bool bf)
@@ -1678,8 +1744,10 @@ int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, 
 }
 
 // the trunk's backward from dh (fc, then the convolutions)
+// nsum1 (no exchange follows): conv1's sum and the norm partials in one launch, k_conv1_sum_norm,
+// where the layout allows (*nsum1 = its sum blocks, else 0: the caller runs k_norm_partials)
 int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
-                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc, bool xh)
+                   const int32_t *stop, hipStream_t s, bool bf, bool lib_fc, bool xh, int *nsum1)
 {
     int rc;
     const int64_t m2 = L.rows2(B), m3 = L.rows3(B);
@@ -1734,8 +1802,22 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
                            L.h1, L.w1, L.c1, L.k2, L.s2, L.h2, L.w2, w.da1);
     }
     // conv1 (no input gradient): patches re-read from the u8 frames
-    if (conv1_lds_supported(L.C, L.H, L.W))
+    if (conv1_lds_supported(L.C, L.H, L.W)) {
+        const int64_t n1 = L.ob1 + L.c1;      // conv1's [dW1 | db1] at the front of the flat gradient
+        const int ns = (int)((n1 / 4 + 15) / 16);
+        if (nsum1 && L.oW1 == 0 && L.ob1 == (int64_t)L.c1 * L.K1 && n1 % 4 == 0 && ns <= kConv1NormMax) {
+            int np = 0;
+            if ((rc = conv1_lds_wgrad(s, bf, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1,
+                                      &np)))
+                return rc;
+            hipLaunchKernelGGL(k_conv1_sum_norm, dim3((unsigned)(ns + kNormBlocks)), dim3(256), 0, s, w.parts, np, n1,
+                               n1, ns, G, L.P, w.norm_part, w.norm_part + 5 * kNormBlocks, stop, L.oWf, L.oWp, L.oWv);
+            GS_LAUNCH_CHECK("k_conv1_sum_norm");
+            *nsum1 = ns;
+            return GS_OK;
+        }
         return conv1_lds_wgrad(s, bf, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1);
+    }
     if ((rc = colsum(w.da1, L.rows1(B), L.c1, w.parts, G + L.ob1, s))) return rc;
     return conv_wgrad_u8(s, bf, geom1(L, B), fs, w.da1, w.parts, kSplitW1, G + L.oW1);
 }
@@ -1808,7 +1890,7 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
         });
         hipLaunchKernelGGL((k_cnn_head_loss<AM, BF, DH16>), dim3(nb), dim3(256), l1, s, w.h, P, L, (int)B, fl, la,
-                           w.dz, (void *)w.dh, w.parts, w.loss_part, stop);
+                           w.dz, w.dzp, (void *)w.dh, w.parts, w.loss_part, stop);
         GS_LAUNCH_CHECK("k_cnn_head_loss");
         return GS_OK;
     };
@@ -1826,7 +1908,7 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
             (void)hipFuncSetAttribute((const void *)k_cnn_head_wgrad<AM, BF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)head_wgrad_lds<AM>());
         });
-        hipLaunchKernelGGL((k_cnn_head_wgrad<AM, BF>), dim3(ncb + 1), dim3(1024), head_wgrad_lds<AM>(), s, w.h, w.dz,
+        hipLaunchKernelGGL((k_cnn_head_wgrad<AM, BF>), dim3(ncb + 1), dim3(1024), head_wgrad_lds<AM>(), s, w.h, w.dz, w.dzp,
                            w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop);
         GS_LAUNCH_CHECK("k_cnn_head_wgrad");
         return GS_OK;
@@ -2070,6 +2152,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
     // weight operands stored as bf16 between the kernels — half the bytes, the same operand values
     // and ReLU signs
     const bool xh = trunk_bf16_storage(L, hp, B);
+    int nsum1 = 0;     // k_conv1_sum_norm's sum blocks (0: the separate norm pass)
     GS_REQUIRE(!gl || head_fused(L, B), "global mode: the fused head + loss kernels do not fit this shape");
     if (head_fused(L, B)) {
         CnnFields fl{idx, ro.T, ro.N, ro.actions, ro.logprobs, ro.values, ro.advantages, ro.returns};
@@ -2098,7 +2181,7 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s, bf, xh))) return rc;
         // after the loss kernel: the record says whether this minibatch was evaluated
         if (stats && (rc = act_record(L, B, bf, xh, w, epi, metrics, s))) return rc;
-        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc, xh))) return rc;
+        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc, xh, comm ? nullptr : &nsum1))) return rc;
     } else {
         hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
                            ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv,
@@ -2116,11 +2199,12 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         // divides by batch_global), so the sum over ranks is the gradient itself
         aa.grad_scale = gl ? 1.0f : 1.0f / (float)world;
     }
-    hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
-                       L.oWv);
+    if (!nsum1)
+        hipLaunchKernelGGL(k_norm_partials, dim3(kNormBlocks), dim3(256), 0, s, G, L.P, w.norm_part, stop, L.oWf, L.oWp,
+                           L.oWv);
     const unsigned nadam = (unsigned)((L.P / 4 + 256 * kAdamQuads - 1) / (256 * kAdamQuads) + 1);
     hipLaunchKernelGGL(k_clip_adam_flat, dim3(nadam), dim3(256), 0, s, P, G, Mm, Vv, L.P, w.norm_part, kNormBlocks, aa,
-                       metrics, stop, xh ? w.pbf : nullptr);
+                       metrics, stop, xh ? w.pbf : nullptr, w.norm_part + 5 * kNormBlocks, nsum1);
     GS_LAUNCH_CHECK("k_clip_adam_flat");
     return GS_OK;
 }

@@ -31,8 +31,9 @@ bool conv1_lds_supported(int C, int H, int W);
 int conv1_lds_fwd(hipStream_t s, bool bf, bool xh, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
                   const void *W1, const float *b1, void *out, uint8_t *obs_copy = nullptr, ActOut ao = ActOut{});
 // dW1 = sum_rows dA1^T . patches, db1 = column sums of dA1; parts: kConv1WgradWG x (32*256 + 32) floats
+// np_out: only the partials (their count written there); the caller sums them
 int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
-                    const float *dA, float *parts, float *dW1, float *db1);
+                    const float *dA, float *parts, float *dW1, float *db1, int *np_out = nullptr);
 int conv1_lds_wgrad_parts();
 // conv2 (20x20x32 -> 9x9x64, k4 s2) / conv3 (9x9x64 -> 7x7x64, k3 s1) forward with bias + ReLU,
 // NHWC, LDS-resident samples (layer = 2 or 3)

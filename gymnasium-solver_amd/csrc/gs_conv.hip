@@ -1419,7 +1419,7 @@ int conv1_lds_fwd(hipStream_t s, bool bf, bool xh, int R, const uint8_t *obs, co
 int conv1_lds_wgrad_parts() { return std::max(kConv1WgradWG, kConv1WgradBfWG); }
 
 int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int32_t *idx, int64_t T, int64_t N,
-                    const float *dA, float *parts, float *dW1, float *db1)
+                    const float *dA, float *parts, float *dW1, float *db1, int *np_out)
 {
     GS_REQUIRE(R > 0 && obs && dA && parts && dW1 && db1, "conv1_lds_wgrad: bad argument");
     constexpr int n = C1_84::CO * C1_84::KK, stride = n + C1_84::CO;
@@ -1431,6 +1431,10 @@ int conv1_lds_wgrad(hipStream_t s, bool bf, int R, const uint8_t *obs, const int
                            N, R, dA, parts);
     GS_LAUNCH_CHECK("k_conv1_wgrad");
     const int np = bf ? kConv1WgradBfWG : kConv1WgradWG;
+    if (np_out) {       // the caller sums the partials ([dW1 | db1] rows of stride n + CO)
+        *np_out = np;
+        return GS_OK;
+    }
     if (db1 == dW1 + n) {      // the flat layout keeps conv1's bias right after its weight: one sum
         return sum_parts4(s, parts, np, stride, stride, dW1);
     } else {
