@@ -92,6 +92,8 @@ struct CnnLayout {
 
 struct CnnWs {
     float *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dzp, *dh, *da3, *da2, *da1;
+    float *hw_part;        // k_cnn_head_wgrad's per-workgroup blocks
+    uint32_t *hw_cnt;      // its per-column-block arrival counters (zeroed by every update entry)
     int32_t *f_act;
     float *f_olp, *f_ov, *f_adv, *f_ret;
     double *norm_part;
@@ -113,6 +115,9 @@ struct CnnWs {
 constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block sums them)
 constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
 constexpr int kConv1NormMax = 1024;   // k_conv1_sum_norm sum blocks (conv1 [dW1 | db1] <= 64 K floats)
+// k_cnn_head_wgrad: 64-column blocks x kHwSplits row ranges, kHwRows rows of loads in flight,
+// kDbhSlices row ranges of the dbh sums; at most kHwMaxCb column blocks (HID <= 512: head_fused)
+constexpr int kHwCols = 64, kHwSplits = 8, kHwRows = 8, kDbhSlices = 8, kHwMaxCb = 8;
 constexpr int kPreChunk = 16;      // minibatches per ahead-of-time fields gather (k_cnn_gather_chunk)
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
 #ifndef GS_HEAD_ROWS
@@ -190,6 +195,8 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.z = (float *)take(sizeof(float) * R * (L.A + 1));
     w.dz = (float *)take(sizeof(float) * R * (L.A + 1));
     w.dzp = (float *)take(sizeof(float) * R * head_part_rows(L));    // dz padded (k_cnn_head_wgrad's operand)
+    w.hw_part = (float *)take(sizeof(float) * kHwMaxCb * kHwSplits * (kAMax + 2) * kHwCols);
+    w.hw_cnt = (uint32_t *)take(sizeof(uint32_t) * kHwMaxCb);
     w.dh = (float *)take(sizeof(float) * R * L.HID);
     w.da3 = (float *)take(sizeof(float) * R * L.F);
     w.da2 = (float *)take(sizeof(float) * L.rows2(R) * L.c2);
@@ -1169,31 +1176,35 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
 }
 
 // [dWh | dbh] = dz^T [h | 1] over all B rows of the minibatch, dbf = the k_cnn_head_loss dbf partials
-// summed in workgroup order, and the minibatch record — one launch, no per-workgroup [dWh | dbh]
-// partials (round 5 wrote 256 of them, 10 MB per minibatch, and summed them in a second pass).
-// Workgroup x < HID / 64 (1024 threads = 16 waves): h columns [64 x, 64 x + 64), one per lane, for
-// every head row a < A1; wave q takes rows q, q + 16, ... (its h loads 32 rows at a time, all in
-// flight, 256-B coalesced), against the row's dz from dzp — k_cnn_head_loss's copy of dz padded to
-// AP columns (BF: rounded to the bf16 operand) — at a wave-uniform address, so the 80 / 144 B of a
-// row come through the scalar cache into SGPRs (the first form broadcast them from LDS: 5 - 9
-// ds_read_b128 per row per wave, LDS-bound at 18 us); fp32 FMA (BF: h rounded to bf16 as well); the
-// 16 slices added in slice order.  Then its dbf columns over the partials (16 ranges, in order).
-// The last workgroup: dbh (column sums of the unrounded dz) and the record from the loss partials
+// summed in order, and the minibatch record — one launch (round 5 wrote 256 per-workgroup
+// [dWh | dbh] partials, 10 MB per minibatch, and summed them in a second pass).
+// Workgroup (x, y), x < HID / 64 column blocks, y < kHwSplits row ranges (256 threads): thread
+// (cg = tid & 15, slice q = tid >> 4) owns columns 64 x + 4 cg .. + 3 (float4 h loads) and rows
+// q, q + 16, ... of the range, against the range's dz rows staged in LDS from dzp (k_cnn_head_loss's
+// copy padded to AP columns; BF: rounded to the bf16 operand); fp32 FMA (BF: h rounded too), 8 rows
+// of loads in flight.  The 16 slices are added in a fixed tree (lane xor 16, 32, then the 4 waves in
+// order) together with the range's dbf partials; the workgroup's [dWh | dbh-free | dbf] block goes to
+// hw_part, and the last workgroup of column block x to finish (an agent-scope counter, reset by that
+// workgroup) adds the kHwSplits blocks in y order into G.  Round-6 forms measured first: 16 / 8
+// workgroups of 1024 threads with dz broadcast from LDS (18 us, LDS-bound: every wave re-read
+// every dz row) or through scalar loads (26.6 us: a scalar-load latency per 4 rows per wave).
+// The extra workgroup: dbh (column sums of the unrounded dz) and the record from the loss partials
 // (sets the KL stop).
-constexpr int kWgCols = 64, kWgSlices = 16, kWgRows = 32, kDbhSlices = 32;
+__host__ __device__ constexpr int head_ap(int AM) { return (AM + 1 + 3) & ~3; }
 template <int AM, bool BF>
-__global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict__ h, const float *__restrict__ dz,
-                                                         const float *__restrict__ dzp,
-                                                         const float *__restrict__ dbf_part, int nparts, CnnLayout L,
-                                                         float *__restrict__ G, const double *__restrict__ part, int B,
-                                                         LossArgs la, float *__restrict__ metrics,
-                                                         int32_t *__restrict__ stop)
+__global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict__ h, const float *__restrict__ dz,
+                                                        const float *__restrict__ dzp,
+                                                        const float *__restrict__ dbf_part, int nparts, CnnLayout L,
+                                                        float *__restrict__ G, const double *__restrict__ part, int B,
+                                                        LossArgs la, float *__restrict__ metrics,
+                                                        int32_t *__restrict__ stop, float *__restrict__ hw_part,
+                                                        uint32_t *__restrict__ hw_cnt)
 {
-    constexpr int AP = (AM + 1 + 3) & ~3;      // head rows padded to float4 (accumulators)
-    extern __shared__ float lds[];             // kWgSlices x kWgCols x (AP + 1) slice partials
+    constexpr int AP = head_ap(AM);            // head rows padded to float4 (accumulators)
+    extern __shared__ float lds[];             // the range's dz rows, then the waves' partials
     const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
-    const int ncb = (HID + kWgCols - 1) / kWgCols;
-    if ((int)blockIdx.x == ncb) {
+    const int ncb = (HID + kHwCols - 1) / kHwCols;
+    if ((int)blockIdx.x == ncb * kHwSplits) {
         // the record: the 13 loss sums over the partials, 16 threads per sum (strided, in order),
         // then the 16 in order; thread 0 writes it from a one-partial view of the totals
         __shared__ double msum[kSums][16];
@@ -1212,9 +1223,10 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
             msum[q][j] = v;
         }
         // dbh[a] = sum_r dz[r][a] (unrounded): thread (a = tid & 31, slice q = tid >> 5) sums the
-        // q-th of 32 contiguous row ranges in row order, 8 loads in flight, then the slices in order
-        // (the first form, one thread per column over all B rows, waited out B dependent L2 loads:
-        // 83 us of the head's 90)
+        // q-th of 8 contiguous row ranges in row order, 32 loads in flight (4 memory latencies at
+        // B = 1024; 8 in flight had made this workgroup the launch's long pole: 16 latencies, the
+        // kernel 20.6 us), then the slices in order (the first form, one thread per column over all
+        // B rows, waited out B dependent loads)
         __shared__ float dbr[kDbhSlices][kAMax + 2];
         const bool live = !(stop && *stop);
         {
@@ -1223,12 +1235,12 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
             for (int a2 = tid & 31; a2 < A1 && live; a2 += 32) {
                 float v = 0.f;
                 int r = ra;
-                for (; r + 8 <= rb; r += 8) {
-                    float t[8];
+                for (; r + 32 <= rb; r += 32) {
+                    float t[32];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) t[u] = dz[(int64_t)(r + u) * A1 + a2];
+                    for (int u = 0; u < 32; ++u) t[u] = dz[(int64_t)(r + u) * A1 + a2];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) v += t[u];
+                    for (int u = 0; u < 32; ++u) v += t[u];
                 }
                 for (; r < rb; ++r) v += dz[(int64_t)r * A1 + a2];
                 dbr[q][a2] = v;
@@ -1255,64 +1267,133 @@ __global__ __launch_bounds__(1024) void k_cnn_head_wgrad(const float *__restrict
         }
         return;
     }
-    if (stop && *stop) return;
-    const int c = tid & (kWgCols - 1);
-    const int q = __builtin_amdgcn_readfirstlane(tid >> 6);     // the wave's row slice (uniform)
-    const int col = blockIdx.x * kWgCols + c;
-    const int colc = col < HID ? col : HID - 1;
-    float g[AP];
-#pragma unroll
-    for (int a = 0; a < AP; ++a) g[a] = 0.f;
-    // this workgroup's dbf columns: the partials of the workgroups in order, 16 ranges of them
-    // (loads issued first, 8 in flight per group, so they land under the row loads)
-    float fs = 0.f;
+    if (stop && *stop) return;      // (the update entry zeroes hw_cnt: a stopped launch leaves it)
+    const int x = (int)blockIdx.x % ncb, y = (int)blockIdx.x / ncb;
+    const int cg = tid & 15, q = tid >> 4, lane = tid & 63, wave = tid >> 6;
+    const int col0 = x * kHwCols + 4 * cg;
+    const int colc = min(col0, HID - 4);       // HID % 4 == 0 (head_fused)
+    const int rlo = (int)((int64_t)y * B / kHwSplits), rhi = (int)((int64_t)(y + 1) * B / kHwSplits);
+    const int nr = rhi - rlo;
+    const int pw0 = (int)((int64_t)y * nparts / kHwSplits), pw1 = (int)((int64_t)(y + 1) * nparts / kHwSplits);
+    // the range's dz rows -> LDS (contiguous in dzp: nr x AP floats, float4 units, all in flight)
     {
-        const int w0 = (q * nparts) / kWgSlices, w1 = ((q + 1) * nparts) / kWgSlices;
-        for (int w = w0; w < w1; w += 8) {
-            float t[8];
+        constexpr int MAXU = 9;      // float4 units per thread: nr <= 256 rows (B <= 2048) x 36 / 4 / 256
+        const float4 *src = reinterpret_cast<const float4 *>(dzp + (int64_t)rlo * AP);
+        const int nu = nr * AP / 4;
+        float4 t[MAXU];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] = dbf_part[min(w + u, w1 - 1) * HID + colc];     // 32-bit offsets
+        for (int u = 0; u < MAXU; ++u) t[u] = src[min(tid + 256 * u, nu - 1)];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (w + u < w1) fs += t[u];
-        }
+        for (int u = 0; u < MAXU; ++u)
+            if (tid + 256 * u < nu) reinterpret_cast<float4 *>(lds)[tid + 256 * u] = t[u];
     }
-    const int nrow = (B - q + kWgSlices - 1) / kWgSlices;       // rows q, q + 16, ... < B
-    for (int m0 = 0; m0 < nrow; m0 += kWgRows) {
-        float hv[kWgRows];
-#pragma unroll
-        for (int j = 0; j < kWgRows; ++j) hv[j] = h[min(q + kWgSlices * (m0 + j), B - 1) * HID + colc];
-#pragma unroll 4
-        for (int j = 0; j < kWgRows; ++j) {
-            if (m0 + j >= nrow) break;
-            const float *dr = dzp + (q + kWgSlices * (m0 + j)) * AP;     // uniform: scalar loads
-            const float hb = BF ? bf16r(hv[j]) : hv[j];
-#pragma unroll
-            for (int a = 0; a < AP; ++a) g[a] = fmaf(dr[a], hb, g[a]);
-        }
+    // this thread's dbf partials of the range (slice q: pw0 + q, pw0 + q + 16, ...), in order
+    float4 fs = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int w = pw0 + q; w < pw1; w += 16) {
+        const float4 t = *reinterpret_cast<const float4 *>(dbf_part + (int64_t)w * HID + colc);
+        fs.x += t.x, fs.y += t.y, fs.z += t.z, fs.w += t.w;
     }
-    float *red = lds;                          // [slice][col][AP + 1]
-    constexpr int RS = AP + 1;
-#pragma unroll
-    for (int a = 0; a < AP; ++a) red[(q * kWgCols + c) * RS + a] = g[a];
-    red[(q * kWgCols + c) * RS + AP] = fs;
     __syncthreads();
-    for (int o = tid; o < kWgCols * (A1 + 1); o += 1024) {
-        const int cc = o % kWgCols, a = o / kWgCols, cl = blockIdx.x * kWgCols + cc;
-        if (cl >= HID) continue;
-        const int slot = a < A1 ? a : AP;
-        float v = 0.f;
-#pragma unroll 8
-        for (int k = 0; k < kWgSlices; ++k) v += red[(k * kWgCols + cc) * RS + slot];
-        G[a < A ? L.oWp + (int64_t)a * HID + cl : a == A ? L.oWv + cl : L.obf + cl] = v;
+    float g[AP][4];
+#pragma unroll
+    for (int a = 0; a < AP; ++a) g[a][0] = g[a][1] = g[a][2] = g[a][3] = 0.f;
+    const int nrq = (nr - q + 15) / 16;        // this slice's rows: q, q + 16, ... < nr
+    for (int m0 = 0; m0 < nrq; m0 += kHwRows) {
+        float4 hv[kHwRows];
+#pragma unroll
+        for (int j = 0; j < kHwRows; ++j)
+            hv[j] = *reinterpret_cast<const float4 *>(h + (int64_t)(rlo + min(q + 16 * (m0 + j), nr - 1)) * HID + colc);
+#pragma unroll 2
+        for (int j = 0; j < kHwRows; ++j) {
+            if (m0 + j >= nrq) break;
+            const float *dr = lds + (q + 16 * (m0 + j)) * AP;
+            const float hb[4] = {BF ? bf16r(hv[j].x) : hv[j].x, BF ? bf16r(hv[j].y) : hv[j].y,
+                                 BF ? bf16r(hv[j].z) : hv[j].z, BF ? bf16r(hv[j].w) : hv[j].w};
+#pragma unroll
+            for (int a4 = 0; a4 < AP; a4 += 4) {
+                const float4 d = *reinterpret_cast<const float4 *>(dr + a4);
+                const float dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) g[a4 + e][k] = fmaf(dv[e], hb[k], g[a4 + e][k]);
+            }
+        }
     }
+    // the 4 slices of a wave (lanes 16 apart): xor 16, then 32
+#pragma unroll
+    for (int a = 0; a < AP; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float v = g[a][k];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            g[a][k] = v;
+        }
+    {
+        float f[4] = {fs.x, fs.y, fs.z, fs.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f[k] += __shfl_xor(f[k], 16);
+            f[k] += __shfl_xor(f[k], 32);
+        }
+        fs = make_float4(f[0], f[1], f[2], f[3]);
+    }
+    __syncthreads();                           // the dz rows are dead: the wave partials reuse the LDS
+    constexpr int RS = AP + 1;                 // [wave][64 columns][AP dWh rows + dbf]
+    float *red = lds;
+    if (lane < 16) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float *o = red + (wave * kHwCols + 4 * cg + k) * RS;
+#pragma unroll
+            for (int a = 0; a < AP; ++a) o[a] = g[a][k];
+            o[AP] = k == 0 ? fs.x : k == 1 ? fs.y : k == 2 ? fs.z : fs.w;
+        }
+    }
+    __syncthreads();
+    // this workgroup's block: rows a < A1 (dWp rows, the dWv row) and row A1 (dbf), 64 columns
+    float *blk = hw_part + (int64_t)(x * kHwSplits + y) * (A1 + 1) * kHwCols;
+    for (int o = tid; o < kHwCols * (A1 + 1); o += 256) {
+        const int cc = o % kHwCols, a = o / kHwCols;
+        const int slot = a < A1 ? a : AP;
+        const float v = (red[(0 * kHwCols + cc) * RS + slot] + red[(1 * kHwCols + cc) * RS + slot]) +
+                        (red[(2 * kHwCols + cc) * RS + slot] + red[(3 * kHwCols + cc) * RS + slot]);
+        blk[o] = v;
+    }
+    // the last of the column block's kHwSplits workgroups adds their blocks in y order
+    __shared__ int s_last;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(hw_cnt + x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (uint32_t)(kHwSplits - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const float *cb = hw_part + (int64_t)x * kHwSplits * (A1 + 1) * kHwCols;
+    for (int o = tid; o < kHwCols * (A1 + 1); o += 256) {
+        const int cc = o % kHwCols, a = o / kHwCols, cl = x * kHwCols + cc;
+        float t[kHwSplits];
+#pragma unroll
+        for (int yy = 0; yy < kHwSplits; ++yy)
+            t[yy] = __hip_atomic_load(cb + (int64_t)yy * (A1 + 1) * kHwCols + o, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+        float v = 0.f;
+#pragma unroll
+        for (int yy = 0; yy < kHwSplits; ++yy) v += t[yy];
+        if (cl < HID) G[a < A ? L.oWp + (int64_t)a * HID + cl : a == A ? L.oWv + cl : L.obf + cl] = v;
+    }
+    if (tid == 0) __hip_atomic_store(hw_cnt + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int AM>
 constexpr size_t head_wgrad_lds()
 {
-    constexpr int AP = (AM + 1 + 3) & ~3;
-    return sizeof(float) * (size_t)kWgSlices * kWgCols * (AP + 1);
+    constexpr int AP = head_ap(AM);
+    constexpr size_t d = (size_t)256 * AP, r = (size_t)4 * kHwCols * (AP + 1);     // dz rows (<= 256), partials
+    return sizeof(float) * (d > r ? d : r);
 }
 
 // ---- dhpre[r][j] = h > 0 ? sum_a dz[r][a] Wp[a][j] + dz[r][A] Wv[j] : 0
@@ -1899,7 +1980,8 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
     auto by_prec = [&](auto am) { return dh16 ? go(am, T{}, T{}) : bf ? go(am, T{}, F{}) : go(am, F{}, F{}); };
     const int rc = L.A <= 18 ? by_prec(std::integral_constant<int, 18>{}) : by_prec(std::integral_constant<int, kAMax>{});
     if (rc) return rc;
-    const unsigned ncb = (unsigned)((L.HID + kWgCols - 1) / kWgCols);
+    const unsigned ncb = (unsigned)((L.HID + kHwCols - 1) / kHwCols);
+    GS_REQUIRE(ncb <= (unsigned)kHwMaxCb && B <= 2048, "k_cnn_head_wgrad: %u column blocks / %lld rows", ncb, (long long)B);
     auto wg = [&](auto am, auto bfc) {
         constexpr int AM = decltype(am)::value;
         constexpr bool BF = decltype(bfc)::value;
@@ -1908,8 +1990,9 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
             (void)hipFuncSetAttribute((const void *)k_cnn_head_wgrad<AM, BF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)head_wgrad_lds<AM>());
         });
-        hipLaunchKernelGGL((k_cnn_head_wgrad<AM, BF>), dim3(ncb + 1), dim3(1024), head_wgrad_lds<AM>(), s, w.h, w.dz, w.dzp,
-                           w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop);
+        hipLaunchKernelGGL((k_cnn_head_wgrad<AM, BF>), dim3(ncb * kHwSplits + 1), dim3(256), head_wgrad_lds<AM>(), s, w.h,
+                           w.dz, w.dzp, w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop, w.hw_part,
+                           w.hw_cnt);
         GS_LAUNCH_CHECK("k_cnn_head_wgrad");
         return GS_OK;
     };
@@ -2338,6 +2421,7 @@ extern "C" int gs_cnn_ppo_update_global(float *params, float *grads, float *adam
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
     if ((rc = refresh_params_bf16(params, L, hp, batch, w, s))) return rc;
+    GS_HIP(hipMemsetAsync(w.hw_cnt, 0, sizeof(uint32_t) * kHwMaxCb, s));     // k_cnn_head_wgrad's counters
     for (int64_t k = 0; k < n_minibatches; ++k) {
         const CnnGlobalStep gl{frame_idx + k * batch, glob->adv_stats ? glob->adv_stats + 2 * k : nullptr,
                                glob->metric_sums + kNumSumsGlobal * k, glob->batch_global};
@@ -2368,6 +2452,7 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     // the fused head + loss path reads each minibatch's fields gathered ahead (kPreChunk at a time)
     const bool pre = head_fused(L, batch);
     if ((rc = refresh_params_bf16(params, L, hp, batch, w, s))) return rc;
+    GS_HIP(hipMemsetAsync(w.hw_cnt, 0, sizeof(uint32_t) * kHwMaxCb, s));     // k_cnn_head_wgrad's counters
     if (hp.flags & GS_HP_ACT_STATS)      // the statistics epilogues' dead counters start at zero
         GS_HIP(hipMemsetAsync(w.act_cnt, 0, sizeof(uint32_t) * (size_t)act_neurons_total(L), s));
     for (int64_t k = 0; k < n_minibatches; ++k) {
