@@ -93,7 +93,6 @@ struct CnnLayout {
 struct CnnWs {
     float *a1, *cols2, *a2, *cols3, *a3, *h, *z, *dz, *dzp, *dh, *da3, *da2, *da1;
     float *hw_part;        // k_cnn_head_wgrad's per-workgroup blocks
-    uint32_t *hw_cnt;      // its per-column-block arrival counters (zeroed by every update entry)
     int32_t *f_act;
     float *f_olp, *f_ov, *f_adv, *f_ret;
     double *norm_part;
@@ -196,7 +195,6 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.dz = (float *)take(sizeof(float) * R * (L.A + 1));
     w.dzp = (float *)take(sizeof(float) * R * head_part_rows(L));    // dz padded (k_cnn_head_wgrad's operand)
     w.hw_part = (float *)take(sizeof(float) * kHwMaxCb * kHwSplits * (kAMax + 2) * kHwCols);
-    w.hw_cnt = (uint32_t *)take(sizeof(uint32_t) * kHwMaxCb);
     w.dh = (float *)take(sizeof(float) * R * L.HID);
     w.da3 = (float *)take(sizeof(float) * R * L.F);
     w.da2 = (float *)take(sizeof(float) * L.rows2(R) * L.c2);
@@ -207,7 +205,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
     // total + 4 component partials, then k_conv1_sum_norm's conv1 partials
-    w.norm_part = (double *)take(sizeof(double) * (kNormBlocks * 5 + kConv1NormMax));
+    w.norm_part = (double *)take(sizeof(double) * (kNormBlocks * 5 + 5 * (kConv1NormMax + kHwMaxCb)));
     w.pre = (float *)take(sizeof(float) * kPreChunk * 5 * R);
     w.pre_stats = (float *)take(sizeof(float) * kPreChunk * 2);
     {   // shifted so Wf's rows start on 128-B lines (the fc kernels stream them in 128-B chunks; a
@@ -1175,21 +1173,22 @@ __global__ __launch_bounds__(256) void k_cnn_head_loss(const float *__restrict__
     GS_STAMP_END(6)
 }
 
-// [dWh | dbh] = dz^T [h | 1] over all B rows of the minibatch, dbf = the k_cnn_head_loss dbf partials
-// summed in order, and the minibatch record — one launch (round 5 wrote 256 per-workgroup
-// [dWh | dbh] partials, 10 MB per minibatch, and summed them in a second pass).
-// Workgroup (x, y), x < HID / 64 column blocks, y < kHwSplits row ranges (256 threads): thread
-// (cg = tid & 15, slice q = tid >> 4) owns columns 64 x + 4 cg .. + 3 (float4 h loads) and rows
-// q, q + 16, ... of the range, against the range's dz rows staged in LDS from dzp (k_cnn_head_loss's
-// copy padded to AP columns; BF: rounded to the bf16 operand); fp32 FMA (BF: h rounded too), 8 rows
-// of loads in flight.  The 16 slices are added in a fixed tree (lane xor 16, 32, then the 4 waves in
-// order) together with the range's dbf partials; the workgroup's [dWh | dbh-free | dbf] block goes to
-// hw_part, and the last workgroup of column block x to finish (an agent-scope counter, reset by that
-// workgroup) adds the kHwSplits blocks in y order into G.  Round-6 forms measured first: 16 / 8
-// workgroups of 1024 threads with dz broadcast from LDS (18 us, LDS-bound: every wave re-read
-// every dz row) or through scalar loads (26.6 us: a scalar-load latency per 4 rows per wave).
-// The extra workgroup: dbh (column sums of the unrounded dz) and the record from the loss partials
-// (sets the KL stop).
+// [dWh | dbf] = dz^T [h | 1] over all B rows of the minibatch as kHwSplits blocks per 64-column
+// block, dbh and the minibatch record — round 5 wrote 256 per-workgroup [dWh | dbh] partials (10 MB
+// per minibatch) and summed them in a second launch.  Workgroup (x, y), x < HID / 64 column blocks,
+// y < kHwSplits row ranges (256 threads): thread (cg = tid & 15, slice q = tid >> 4) owns columns
+// 64 x + 4 cg .. + 3 (float4 h loads, issued first) and rows q, q + 16, ... of the range, against
+// the range's dz rows staged in LDS from dzp (k_cnn_head_loss's copy padded to AP columns; BF:
+// rounded to the bf16 operand); fp32 FMA (BF: h rounded too).  The 16 slices are added in a fixed
+// tree (lane xor 16, 32, then the 4 waves in order) with the range's dbf partials, and the block
+// [dWh | dbf] goes to hw_part; head_combine_block adds the kHwSplits blocks in y order — inside the
+// fused tail (k_conv1_sum_norm) when no exchange follows, else in k_head_combine.  Round-6 forms
+// measured first: 16 / 8 workgroups of 1024 threads with dz broadcast from LDS (18 us, LDS-bound)
+// or through scalar loads (26.6 us: a scalar-load latency per 4 rows per wave); this form with an
+// agent-scope arrival counter and the last arrival combining (20.6 us: the release fence's L2
+// write-back and the counter round trip took 4.7 us of workgroup 0's 16, phase stamps).  The extra
+// workgroup: dbh (column sums of the unrounded dz) and the record from the loss partials (sets the
+// KL stop).
 __host__ __device__ constexpr int head_ap(int AM) { return (AM + 1 + 3) & ~3; }
 template <int AM, bool BF>
 __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict__ h, const float *__restrict__ dz,
@@ -1197,14 +1196,14 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
                                                         const float *__restrict__ dbf_part, int nparts, CnnLayout L,
                                                         float *__restrict__ G, const double *__restrict__ part, int B,
                                                         LossArgs la, float *__restrict__ metrics,
-                                                        int32_t *__restrict__ stop, float *__restrict__ hw_part,
-                                                        uint32_t *__restrict__ hw_cnt)
+                                                        int32_t *__restrict__ stop, float *__restrict__ hw_part)
 {
     constexpr int AP = head_ap(AM);            // head rows padded to float4 (accumulators)
     extern __shared__ float lds[];             // the range's dz rows, then the waves' partials
     const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
     const int ncb = (HID + kHwCols - 1) / kHwCols;
     if ((int)blockIdx.x == ncb * kHwSplits) {
+        GS_STAMP_BEGIN_IF(1, true)
         // the record: the 13 loss sums over the partials, 16 threads per sum (strided, in order),
         // then the 16 in order; thread 0 writes it from a one-partial view of the totals
         __shared__ double msum[kSums][16];
@@ -1222,6 +1221,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
             }
             msum[q][j] = v;
         }
+        GS_STAMP(0)
         // dbh[a] = sum_r dz[r][a] (unrounded): thread (a = tid & 31, slice q = tid >> 5) sums the
         // q-th of 8 contiguous row ranges in row order, 32 loads in flight (4 memory latencies at
         // B = 1024; 8 in flight had made this workgroup the launch's long pole: 16 latencies, the
@@ -1246,7 +1246,9 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
                 dbr[q][a2] = v;
             }
         }
+        GS_STAMP(1)
         __syncthreads();
+        GS_STAMP(2)
         if (live && tid < A1) {
             float sb = 0.f;
             for (int q = 0; q < kDbhSlices; ++q) sb += dbr[q][tid];
@@ -1258,6 +1260,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
             tot[tid] = v;
         }
         __syncthreads();
+        GS_STAMP(3)
         if (tid == 0) {
             cnn_write_metrics(tot, 1, B, la, metrics, stop);
             if (la.sums_out) {      // global mode: this rank's raw sums (gs_ppo_global_records' layout)
@@ -1265,9 +1268,11 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
                 for (int q = kSums; q < kNumSumsGlobal; ++q) la.sums_out[q] = 0.0;
             }
         }
+        GS_STAMP_END(4)
         return;
     }
-    if (stop && *stop) return;      // (the update entry zeroes hw_cnt: a stopped launch leaves it)
+    if (stop && *stop) return;
+    GS_STAMP_BEGIN_IF(2, blockIdx.x == 0)
     const int x = (int)blockIdx.x % ncb, y = (int)blockIdx.x / ncb;
     const int cg = tid & 15, q = tid >> 4, lane = tid & 63, wave = tid >> 6;
     const int col0 = x * kHwCols + 4 * cg;
@@ -1275,6 +1280,16 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
     const int rlo = (int)((int64_t)y * B / kHwSplits), rhi = (int)((int64_t)(y + 1) * B / kHwSplits);
     const int nr = rhi - rlo;
     const int pw0 = (int)((int64_t)y * nparts / kHwSplits), pw1 = (int)((int64_t)(y + 1) * nparts / kHwSplits);
+    // this slice's rows q, q + 16, ... < nr: the first kHwRows rows' h loads issued before anything
+    // else (their latency runs under the dz staging)
+    const int nrq = (nr - q + 15) / 16;
+    float4 hv[kHwRows];
+    auto load_h = [&](int m0) {
+#pragma unroll
+        for (int j = 0; j < kHwRows; ++j)
+            hv[j] = *reinterpret_cast<const float4 *>(h + (int64_t)(rlo + min(q + 16 * (m0 + j), nr - 1)) * HID + colc);
+    };
+    load_h(0);
     // the range's dz rows -> LDS (contiguous in dzp: nr x AP floats, float4 units, all in flight)
     {
         constexpr int MAXU = 9;      // float4 units per thread: nr <= 256 rows (B <= 2048) x 36 / 4 / 256
@@ -1287,22 +1302,21 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
         for (int u = 0; u < MAXU; ++u)
             if (tid + 256 * u < nu) reinterpret_cast<float4 *>(lds)[tid + 256 * u] = t[u];
     }
+    GS_STAMP(0)
     // this thread's dbf partials of the range (slice q: pw0 + q, pw0 + q + 16, ...), in order
     float4 fs = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int w = pw0 + q; w < pw1; w += 16) {
         const float4 t = *reinterpret_cast<const float4 *>(dbf_part + (int64_t)w * HID + colc);
         fs.x += t.x, fs.y += t.y, fs.z += t.z, fs.w += t.w;
     }
+    GS_STAMP(1)
     __syncthreads();
+    GS_STAMP(2)
     float g[AP][4];
 #pragma unroll
     for (int a = 0; a < AP; ++a) g[a][0] = g[a][1] = g[a][2] = g[a][3] = 0.f;
-    const int nrq = (nr - q + 15) / 16;        // this slice's rows: q, q + 16, ... < nr
     for (int m0 = 0; m0 < nrq; m0 += kHwRows) {
-        float4 hv[kHwRows];
-#pragma unroll
-        for (int j = 0; j < kHwRows; ++j)
-            hv[j] = *reinterpret_cast<const float4 *>(h + (int64_t)(rlo + min(q + 16 * (m0 + j), nr - 1)) * HID + colc);
+        if (m0 > 0) load_h(m0);
 #pragma unroll 2
         for (int j = 0; j < kHwRows; ++j) {
             if (m0 + j >= nrq) break;
@@ -1320,6 +1334,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
             }
         }
     }
+    GS_STAMP(3)
     // the 4 slices of a wave (lanes 16 apart): xor 16, then 32
 #pragma unroll
     for (int a = 0; a < AP; ++a)
@@ -1339,6 +1354,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
         }
         fs = make_float4(f[0], f[1], f[2], f[3]);
     }
+    GS_STAMP(4)
     __syncthreads();                           // the dz rows are dead: the wave partials reuse the LDS
     constexpr int RS = AP + 1;                 // [wave][64 columns][AP dWh rows + dbf]
     float *red = lds;
@@ -1361,31 +1377,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
                         (red[(2 * kHwCols + cc) * RS + slot] + red[(3 * kHwCols + cc) * RS + slot]);
         blk[o] = v;
     }
-    // the last of the column block's kHwSplits workgroups adds their blocks in y order
-    __shared__ int s_last;
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(hw_cnt + x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (uint32_t)(kHwSplits - 1);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    const float *cb = hw_part + (int64_t)x * kHwSplits * (A1 + 1) * kHwCols;
-    for (int o = tid; o < kHwCols * (A1 + 1); o += 256) {
-        const int cc = o % kHwCols, a = o / kHwCols, cl = x * kHwCols + cc;
-        float t[kHwSplits];
-#pragma unroll
-        for (int yy = 0; yy < kHwSplits; ++yy)
-            t[yy] = __hip_atomic_load(cb + (int64_t)yy * (A1 + 1) * kHwCols + o, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-        float v = 0.f;
-#pragma unroll
-        for (int yy = 0; yy < kHwSplits; ++yy) v += t[yy];
-        if (cl < HID) G[a < A ? L.oWp + (int64_t)a * HID + cl : a == A ? L.oWv + cl : L.obf + cl] = v;
-    }
-    if (tid == 0) __hip_atomic_store(hw_cnt + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    GS_STAMP_END(5)
 }
 
 template <int AM>
@@ -1429,6 +1421,45 @@ __device__ __forceinline__ void add_sq(double (&s)[5], double g2, int c)
 // part[0 .. nb): the block partials of the whole gradient; part[nb (1 + c) + b]: component c's
 // (c = cnn trunk, mlp trunk, policy_head, value_head: flat ranges split at cut[0..2]) for the
 // per-component norms (utils/models.py:196-230)
+// column block x of the head weight gradient: the kHwSplits blocks of k_cnn_head_wgrad added in y
+// order into G (dWp rows, the dWv row, dbf).  sq (the fused norm tail): also the squared-norm
+// partials of those outputs — and, in block 0, of dbh (bp, bv: final, the head kernel's record
+// workgroup wrote them) — as {total, cnn, mlp, policy_head, value_head} in sred's first 5
+__device__ void head_combine_block(int x, const CnnLayout &L, const float *__restrict__ hw_part, float *__restrict__ G,
+                                   bool sq, double *s, double *sred)
+{
+    const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
+    const float *cb = hw_part + (int64_t)x * kHwSplits * (A1 + 1) * kHwCols;
+    for (int q = 0; q < 5; ++q) s[q] = 0.0;
+    for (int o = tid; o < kHwCols * (A1 + 1); o += 256) {
+        const int cc = o % kHwCols, a = o / kHwCols, cl = x * kHwCols + cc;
+        float t[kHwSplits];
+#pragma unroll
+        for (int yy = 0; yy < kHwSplits; ++yy) t[yy] = cb[(int64_t)yy * (A1 + 1) * kHwCols + o];
+        float v = 0.f;
+#pragma unroll
+        for (int yy = 0; yy < kHwSplits; ++yy) v += t[yy];
+        if (cl >= HID) continue;
+        G[a < A ? L.oWp + (int64_t)a * HID + cl : a == A ? L.oWv + cl : L.obf + cl] = v;
+        // components: policy rows, the value row, dbf (the mlp trunk's bias)
+        if (sq) add_sq(*reinterpret_cast<double (*)[5]>(s), (double)v * (double)v, a < A ? 2 : a == A ? 3 : 1);
+    }
+    if (sq && x == 0 && tid < A1) {
+        const double v = (double)G[tid < A ? L.obp + tid : L.obv];
+        add_sq(*reinterpret_cast<double (*)[5]>(s), v * v, tid < A ? 2 : 3);
+    }
+    if (sq) wg_reduce<5>(*reinterpret_cast<double (*)[5]>(s), sred);
+}
+
+// the combine as its own launch (an exchange follows the backward, or the fused tail does not fit)
+__global__ __launch_bounds__(256) void k_head_combine(CnnLayout L, const float *__restrict__ hw_part,
+                                                      float *__restrict__ G, const int32_t *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    double s[5];
+    head_combine_block(blockIdx.x, L, hw_part, G, false, s, nullptr);
+}
+
 // block b of nb over G[0, n), element k's component by k + koff (the kernel below and the conv1
 // sum's norm blocks)
 __device__ __forceinline__ void norm_partials_block(const float *__restrict__ G, int64_t n, int64_t koff,
@@ -1476,20 +1507,30 @@ __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__
 // ---- one launch for the end of the backward (no exchange follows): blocks [0, nsum) sum conv1's
 // [dW1 | db1] (G[0, n1)) from its weight-gradient partials exactly as k_sum_parts4 (the same float4
 // chains and group tree: bit-identical), each also writing the double sum of squares of its
-// outputs to part1[b] (component: the cnn trunk); blocks [nsum, nsum + kNormBlocks) write the
-// norm partials of G[n1, n) as k_norm_partials — the conv2 / conv3 / fc / head gradients, final
-// before this launch.  The clip + Adam launch adds part1 to the total and the trunk's component.
-// Replaces the conv1 sum and the norm pass (two launches, 4.8 + 5.8 us per C4 minibatch).
+// outputs (component: the cnn trunk); blocks [nsum, nsum + ncb) add the head weight gradient's
+// blocks (head_combine_block: dWp, dWv, dbf) with their squares by component; blocks
+// [nsum + ncb, + kNormBlocks) write the norm partials of G[n1, obf) (conv2 / conv3 / Wf: final
+// before this launch) as k_norm_partials.  part1: [5][nsum + ncb] {total, cnn, mlp, policy,
+// value}; the clip + Adam launch adds them to its sums.  Replaces the conv1 sum, the head combine
+// and the norm pass (three launches).
 __global__ __launch_bounds__(256) void k_conv1_sum_norm(const float *__restrict__ parts, int np, int64_t pstride,
-                                                        int64_t n1, int nsum, float *__restrict__ G, int64_t n,
+                                                        int64_t n1, int nsum, int ncb, CnnLayout L,
+                                                        const float *__restrict__ hw_part, float *__restrict__ G,
                                                         double *__restrict__ part, double *__restrict__ part1,
-                                                        const int32_t *__restrict__ stop, int64_t cut0, int64_t cut1,
-                                                        int64_t cut2)
+                                                        const int32_t *__restrict__ stop)
 {
     __shared__ double sred[5 * (256 + 16)];
+    const int nx = nsum + ncb;
     if ((int)blockIdx.x >= nsum) {
         if (stop && *stop) return;
-        norm_partials_block(G + n1, n - n1, n1, part, (int)blockIdx.x - nsum, kNormBlocks, cut0, cut1, cut2, sred);
+        if ((int)blockIdx.x < nx) {
+            double s5[5];
+            head_combine_block((int)blockIdx.x - nsum, L, hw_part, G, true, s5, sred);
+            if (threadIdx.x < 5) part1[(int64_t)threadIdx.x * nx + blockIdx.x] = s5[threadIdx.x];
+            return;
+        }
+        norm_partials_block(G + n1, L.obf - n1, n1, part, (int)blockIdx.x - nx, kNormBlocks, L.oWf, L.oWp, L.oWv,
+                            sred);
         return;
     }
     __shared__ float4 red[16][16];
@@ -1536,7 +1577,9 @@ __global__ __launch_bounds__(256) void k_conv1_sum_norm(const float *__restrict_
     if (threadIdx.x == 0) {
         double v = 0.0;
         for (int k = 0; k < 16; ++k) v += sq[k];
-        part1[blockIdx.x] = v;
+        part1[blockIdx.x] = v;                        // total
+        part1[(int64_t)nx + blockIdx.x] = v;          // cnn
+        for (int q = 2; q < 5; ++q) part1[(int64_t)q * nx + blockIdx.x] = 0.0;
     }
 }
 
@@ -1611,14 +1654,16 @@ __global__ __launch_bounds__(256) void k_clip_adam_flat(float *__restrict__ Pm, 
     }
     double s[1] = {0.0};
     for (int k = threadIdx.x; k < nparts; k += 256) s[0] += part[k];
-    for (int k = threadIdx.x; k < nparts1; k += 256) s[0] += part1[k];      // conv1's (k_conv1_sum_norm)
+    for (int k = threadIdx.x; k < nparts1; k += 256) s[0] += part1[k];      // k_conv1_sum_norm's [5][nparts1]
     wg_reduce<1>(s, sred);
     if ((int)blockIdx.x == last && metrics) {     // per-component norms (utils/models.py:196-230)
         double c[4] = {0.0, 0.0, 0.0, 0.0};
         for (int k = threadIdx.x; k < nparts; k += 256)
 #pragma unroll
             for (int q = 0; q < 4; ++q) c[q] += part[(int64_t)(1 + q) * nparts + k];
-        for (int k = threadIdx.x; k < nparts1; k += 256) c[0] += part1[k];
+        for (int k = threadIdx.x; k < nparts1; k += 256)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[q] += part1[(int64_t)(1 + q) * nparts1 + k];
         __shared__ double cred[4 * (256 + 16)];
         wg_reduce<4>(c, cred);
         if (threadIdx.x == 0) {
@@ -1805,6 +1850,17 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
                    const int32_t *stop, hipStream_t s, bool bf, bool lib_fc = false, bool xh = false,
                    int *nsum1 = nullptr);
 
+// the fused tail (k_conv1_sum_norm: conv1's sum, the head combine and the norm partials in one
+// launch) fits this layout: the LDS conv1 weight gradient, conv1's [dW1 | db1] at the front of the
+// flat gradient in float4 units, the head after the fc bias
+inline bool fused_tail_ok(const CnnLayout &L)
+{
+    const int64_t n1 = L.ob1 + L.c1;
+    return conv1_lds_supported(L.C, L.H, L.W) && L.oW1 == 0 && L.ob1 == (int64_t)L.c1 * L.K1 && n1 % 4 == 0 &&
+           (n1 / 4 + 15) / 16 <= kConv1NormMax && L.obf > n1 && L.oWp == L.obf + L.HID &&
+           (L.HID + kHwCols - 1) / kHwCols <= kHwMaxCb;
+}
+
 int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
              const int32_t *stop, hipStream_t s, bool bf)
 {
@@ -1886,15 +1942,17 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     if (conv1_lds_supported(L.C, L.H, L.W)) {
         const int64_t n1 = L.ob1 + L.c1;      // conv1's [dW1 | db1] at the front of the flat gradient
         const int ns = (int)((n1 / 4 + 15) / 16);
-        if (nsum1 && L.oW1 == 0 && L.ob1 == (int64_t)L.c1 * L.K1 && n1 % 4 == 0 && ns <= kConv1NormMax) {
+        if (nsum1) {     // the caller deferred the head combine to this launch (fused_tail_ok)
+            GS_REQUIRE(fused_tail_ok(L), "backward_trunk: the fused tail does not fit this layout");
+            const int ncb = (L.HID + kHwCols - 1) / kHwCols;
             int np = 0;
             if ((rc = conv1_lds_wgrad(s, bf, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1,
                                       &np)))
                 return rc;
-            hipLaunchKernelGGL(k_conv1_sum_norm, dim3((unsigned)(ns + kNormBlocks)), dim3(256), 0, s, w.parts, np, n1,
-                               n1, ns, G, L.P, w.norm_part, w.norm_part + 5 * kNormBlocks, stop, L.oWf, L.oWp, L.oWv);
+            hipLaunchKernelGGL(k_conv1_sum_norm, dim3((unsigned)(ns + ncb + kNormBlocks)), dim3(256), 0, s, w.parts, np,
+                               n1, n1, ns, ncb, L, w.hw_part, G, w.norm_part, w.norm_part + 5 * kNormBlocks, stop);
             GS_LAUNCH_CHECK("k_conv1_sum_norm");
-            *nsum1 = ns;
+            *nsum1 = ns + ncb;
             return GS_OK;
         }
         return conv1_lds_wgrad(s, bf, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1);
@@ -1956,8 +2014,11 @@ bool head_fused(const CnnLayout &L, int64_t B)
            B <= 2048 && kHeadRows <= 256;
 }
 
+// defer: the head weight gradient's blocks are combined by the fused tail (k_conv1_sum_norm), else
+// by k_head_combine right here
 int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFields &fl, const CnnWs &w,
-                     const LossArgs &la, float *G, float *metrics, int32_t *stop, hipStream_t s, bool bf, bool dh16)
+                     const LossArgs &la, float *G, float *metrics, int32_t *stop, hipStream_t s, bool bf, bool dh16,
+                     bool defer)
 {
     const unsigned nb = (unsigned)((B + kHeadRows - 1) / kHeadRows);
     const size_t l1 = head_loss_lds(L);
@@ -1991,9 +2052,12 @@ int launch_head_loss(const float *P, const CnnLayout &L, int64_t B, const CnnFie
                                       (int)head_wgrad_lds<AM>());
         });
         hipLaunchKernelGGL((k_cnn_head_wgrad<AM, BF>), dim3(ncb * kHwSplits + 1), dim3(256), head_wgrad_lds<AM>(), s, w.h,
-                           w.dz, w.dzp, w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop, w.hw_part,
-                           w.hw_cnt);
+                           w.dz, w.dzp, w.parts, (int)nb, L, G, w.loss_part, (int)B, la, metrics, stop, w.hw_part);
         GS_LAUNCH_CHECK("k_cnn_head_wgrad");
+        if (!defer) {
+            hipLaunchKernelGGL(k_head_combine, dim3(ncb), dim3(256), 0, s, L, w.hw_part, G, stop);
+            GS_LAUNCH_CHECK("k_head_combine");
+        }
         return GS_OK;
     };
     return L.A <= 18 ? (bf ? wg(std::integral_constant<int, 18>{}, T{}) : wg(std::integral_constant<int, 18>{}, F{}))
@@ -2261,10 +2325,11 @@ int cnn_step(float *P, float *G, float *Mm, float *Vv, const CnnLayout &L, const
         if (epi) act_outs(L, B, w, ao);
         if (stats && !epi && (rc = act_stats_forward(P, L, fs, B, w, s, w.act_fb))) return rc;
         if ((rc = forward_trunk(P, L, fs, B, w, s, bf, lib_fc, stop, xh, epi ? ao : nullptr))) return rc;
-        if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s, bf, xh))) return rc;
+        const bool defer = !comm && fused_tail_ok(L);      // the head combine in the fused tail
+        if ((rc = launch_head_loss(P, L, B, fl, w, la, G, metrics, stop, s, bf, xh, defer))) return rc;
         // after the loss kernel: the record says whether this minibatch was evaluated
         if (stats && (rc = act_record(L, B, bf, xh, w, epi, metrics, s))) return rc;
-        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc, xh, comm ? nullptr : &nsum1))) return rc;
+        if ((rc = backward_trunk(P, L, fs, B, w, G, stop, s, bf, lib_fc, xh, defer ? &nsum1 : nullptr))) return rc;
     } else {
         hipLaunchKernelGGL(k_gather_fields, dim3(nblk(B)), dim3(256), 0, s, idx, B, ro.T, ro.N, ro.actions,
                            ro.logprobs, ro.values, ro.advantages, ro.returns, w.f_act, w.f_olp, w.f_ov, w.f_adv,
@@ -2421,7 +2486,6 @@ extern "C" int gs_cnn_ppo_update_global(float *params, float *grads, float *adam
     const CnnLayout L = CnnLayout::make(dims);
     const CnnWs w = carve(workspace, L, batch);
     if ((rc = refresh_params_bf16(params, L, hp, batch, w, s))) return rc;
-    GS_HIP(hipMemsetAsync(w.hw_cnt, 0, sizeof(uint32_t) * kHwMaxCb, s));     // k_cnn_head_wgrad's counters
     for (int64_t k = 0; k < n_minibatches; ++k) {
         const CnnGlobalStep gl{frame_idx + k * batch, glob->adv_stats ? glob->adv_stats + 2 * k : nullptr,
                                glob->metric_sums + kNumSumsGlobal * k, glob->batch_global};
@@ -2452,7 +2516,6 @@ extern "C" int gs_cnn_ppo_update(float *params, float *grads, float *adam_m, flo
     // the fused head + loss path reads each minibatch's fields gathered ahead (kPreChunk at a time)
     const bool pre = head_fused(L, batch);
     if ((rc = refresh_params_bf16(params, L, hp, batch, w, s))) return rc;
-    GS_HIP(hipMemsetAsync(w.hw_cnt, 0, sizeof(uint32_t) * kHwMaxCb, s));     // k_cnn_head_wgrad's counters
     if (hp.flags & GS_HP_ACT_STATS)      // the statistics epilogues' dead counters start at zero
         GS_HIP(hipMemsetAsync(w.act_cnt, 0, sizeof(uint32_t) * (size_t)act_neurons_total(L), s));
     for (int64_t k = 0; k < n_minibatches; ++k) {

@@ -69,6 +69,20 @@ def main():
     print(f"k_cnn_head_loss workgroup 0 over {int(n)} launches: {tot:8.0f} cyc = {tot / 2.4e3:6.2f} us at 2.4 GHz")
     for i, ph in enumerate(PHASES):
         print(f"    {ph:28s} {per[i]:8.0f} cyc  {per[i] / 2.4e3:6.2f} us")
+    # k_cnn_head_wgrad: slot 1 its record workgroup, slot 2 main workgroup 0 (round 6)
+    for k, kn, names in ((1, "k_cnn_head_wgrad record workgroup", ["loss-sum partials", "dbh row ranges",
+                                                                   "barrier", "dbh / totals", "record"]),
+                         (2, "k_cnn_head_wgrad workgroup 0", ["dz rows -> LDS", "dbf partials", "barrier",
+                                                              "h loads + FMAs", "slice shuffles",
+                                                              "wave partials + block out"])):
+        nk = float(cnt[k] - cnt0[k])
+        if nk <= 0:
+            continue
+        pk = acc[k] / nk
+        print(f"{kn} over {int(nk)} launches: {pk[:len(names)].sum():8.0f} cyc = "
+              f"{pk[:len(names)].sum() / 2.4e3:6.2f} us")
+        for i, ph in enumerate(names):
+            print(f"    {ph:28s} {pk[i]:8.0f} cyc  {pk[i] / 2.4e3:6.2f} us")
     if a.bf16 and hasattr(lib, "gs_debug_conv_stamps"):
         # k_conv1_wgrad_bf's unit loop (csrc/gs_conv.hip C1S_MARK), workgroup 0, per launch
         lib.gs_debug_conv_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
