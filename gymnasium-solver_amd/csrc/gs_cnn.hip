@@ -115,8 +115,8 @@ constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block
 constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
 constexpr int kConv1NormMax = 1024;   // k_conv1_sum_norm sum blocks (conv1 [dW1 | db1] <= 64 K floats)
 // k_cnn_head_wgrad: 64-column blocks x kHwSplits row ranges, kHwRows rows of loads in flight,
-// kDbhSlices row ranges of the dbh sums; at most kHwMaxCb column blocks (HID <= 512: head_fused)
-constexpr int kHwCols = 64, kHwSplits = 8, kHwRows = 8, kDbhSlices = 8, kHwMaxCb = 8;
+// kDbhSlices row slices of a range's dbh sums; at most kHwMaxCb column blocks (HID <= 512: head_fused)
+constexpr int kHwCols = 64, kHwSplits = 16, kHwRows = 4, kDbhSlices = 8, kHwMaxCb = 8;
 constexpr int kPreChunk = 16;      // minibatches per ahead-of-time fields gather (k_cnn_gather_chunk)
 constexpr int kColParts = 1024; // bias-gradient column sums: at most this many row partitions
 #ifndef GS_HEAD_ROWS
@@ -194,7 +194,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.z = (float *)take(sizeof(float) * R * (L.A + 1));
     w.dz = (float *)take(sizeof(float) * R * (L.A + 1));
     w.dzp = (float *)take(sizeof(float) * R * head_part_rows(L));    // dz padded (k_cnn_head_wgrad's operand)
-    w.hw_part = (float *)take(sizeof(float) * kHwMaxCb * kHwSplits * (kAMax + 2) * kHwCols);
+    w.hw_part = (float *)take(sizeof(float) * kHwMaxCb * kHwSplits * (kAMax + 3) * kHwCols);
     w.dh = (float *)take(sizeof(float) * R * L.HID);
     w.da3 = (float *)take(sizeof(float) * R * L.F);
     w.da2 = (float *)take(sizeof(float) * L.rows2(R) * L.c2);
@@ -1222,45 +1222,14 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
             msum[q][j] = v;
         }
         GS_STAMP(0)
-        // dbh[a] = sum_r dz[r][a] (unrounded): thread (a = tid & 31, slice q = tid >> 5) sums the
-        // q-th of 8 contiguous row ranges in row order, 32 loads in flight (4 memory latencies at
-        // B = 1024; 8 in flight had made this workgroup the launch's long pole: 16 latencies, the
-        // kernel 20.6 us), then the slices in order (the first form, one thread per column over all
-        // B rows, waited out B dependent loads)
-        __shared__ float dbr[kDbhSlices][kAMax + 2];
-        const bool live = !(stop && *stop);
-        {
-            const int q = tid >> 5, rs = (B + kDbhSlices - 1) / kDbhSlices;
-            const int ra = min(B, q * rs), rb = min(B, ra + rs);
-            for (int a2 = tid & 31; a2 < A1 && live; a2 += 32) {
-                float v = 0.f;
-                int r = ra;
-                for (; r + 32 <= rb; r += 32) {
-                    float t[32];
-#pragma unroll
-                    for (int u = 0; u < 32; ++u) t[u] = dz[(int64_t)(r + u) * A1 + a2];
-#pragma unroll
-                    for (int u = 0; u < 32; ++u) v += t[u];
-                }
-                for (; r < rb; ++r) v += dz[(int64_t)r * A1 + a2];
-                dbr[q][a2] = v;
-            }
-        }
-        GS_STAMP(1)
         __syncthreads();
-        GS_STAMP(2)
-        if (live && tid < A1) {
-            float sb = 0.f;
-            for (int q = 0; q < kDbhSlices; ++q) sb += dbr[q][tid];
-            G[tid < A ? L.obp + tid : L.obv] = sb;
-        }
         if (tid < kSums) {
             double v = 0.0;
             for (int j = 0; j < 16; ++j) v += msum[tid][j];
             tot[tid] = v;
         }
         __syncthreads();
-        GS_STAMP(3)
+        GS_STAMP(1)
         if (tid == 0) {
             cnn_write_metrics(tot, 1, B, la, metrics, stop);
             if (la.sums_out) {      // global mode: this rank's raw sums (gs_ppo_global_records' layout)
@@ -1268,7 +1237,7 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
                 for (int q = kSums; q < kNumSumsGlobal; ++q) la.sums_out[q] = 0.0;
             }
         }
-        GS_STAMP_END(4)
+        GS_STAMP_END(2)
         return;
     }
     if (stop && *stop) return;
@@ -1290,9 +1259,21 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
             hv[j] = *reinterpret_cast<const float4 *>(h + (int64_t)(rlo + min(q + 16 * (m0 + j), nr - 1)) * HID + colc);
     };
     load_h(0);
+    // column block 0 also sums dbh over the range (the unrounded dz): thread t < A1 kDbhSlices takes
+    // column t % A1 of the t / A1-th contiguous row slice, its loads in flight with the others
+    constexpr int kDbhRows = 16;      // rows per slice: nr <= 128 (B <= 2048)
+    const int rps = (nr + kDbhSlices - 1) / kDbhSlices;
+    const bool dbh_thr = x == 0 && tid < A1 * kDbhSlices;
+    const int da = dbh_thr ? tid % A1 : 0, dsl = dbh_thr ? tid / A1 : 0;
+    float dbt[kDbhRows];
+    if (dbh_thr) {
+#pragma unroll
+        for (int u = 0; u < kDbhRows; ++u)
+            dbt[u] = dz[(int64_t)(rlo + min(dsl * rps + u, nr - 1)) * A1 + da];
+    }
     // the range's dz rows -> LDS (contiguous in dzp: nr x AP floats, float4 units, all in flight)
     {
-        constexpr int MAXU = 9;      // float4 units per thread: nr <= 256 rows (B <= 2048) x 36 / 4 / 256
+        constexpr int MAXU = 5;      // float4 units per thread: nr <= 128 rows (B <= 2048) x 36 / 4 / 256
         const float4 *src = reinterpret_cast<const float4 *>(dzp + (int64_t)rlo * AP);
         const int nu = nr * AP / 4;
         float4 t[MAXU];
@@ -1368,8 +1349,25 @@ __global__ __launch_bounds__(256) void k_cnn_head_wgrad(const float *__restrict_
         }
     }
     __syncthreads();
-    // this workgroup's block: rows a < A1 (dWp rows, the dWv row) and row A1 (dbf), 64 columns
-    float *blk = hw_part + (int64_t)(x * kHwSplits + y) * (A1 + 1) * kHwCols;
+    // this workgroup's block: rows a < A1 (dWp rows, the dWv row), row A1 (dbf), 64 columns, and in
+    // column block 0 row A1 + 1: the range's dbh (its slices added in order)
+    float *blk = hw_part + (int64_t)(x * kHwSplits + y) * (A1 + 2) * kHwCols;
+    if (x == 0) {
+        __shared__ float dbr[kDbhSlices][kAMax + 2];
+        if (dbh_thr) {
+            float v = 0.f;
+#pragma unroll
+            for (int u = 0; u < kDbhRows; ++u)
+                if (u < rps && dsl * rps + u < nr) v += dbt[u];
+            dbr[dsl][da] = v;
+        }
+        __syncthreads();
+        if (tid < A1) {
+            float v = 0.f;
+            for (int k = 0; k < kDbhSlices; ++k) v += dbr[k][tid];
+            blk[(A1 + 1) * kHwCols + tid] = v;
+        }
+    }
     for (int o = tid; o < kHwCols * (A1 + 1); o += 256) {
         const int cc = o % kHwCols, a = o / kHwCols;
         const int slot = a < A1 ? a : AP;
@@ -1429,13 +1427,14 @@ __device__ void head_combine_block(int x, const CnnLayout &L, const float *__res
                                    bool sq, double *s, double *sred)
 {
     const int tid = threadIdx.x, HID = L.HID, A = L.A, A1 = A + 1;
-    const float *cb = hw_part + (int64_t)x * kHwSplits * (A1 + 1) * kHwCols;
+    const int BS = (A1 + 2) * kHwCols;          // block stride: dWh rows, dbf, dbh (column block 0)
+    const float *cb = hw_part + (int64_t)x * kHwSplits * BS;
     for (int q = 0; q < 5; ++q) s[q] = 0.0;
     for (int o = tid; o < kHwCols * (A1 + 1); o += 256) {
         const int cc = o % kHwCols, a = o / kHwCols, cl = x * kHwCols + cc;
         float t[kHwSplits];
 #pragma unroll
-        for (int yy = 0; yy < kHwSplits; ++yy) t[yy] = cb[(int64_t)yy * (A1 + 1) * kHwCols + o];
+        for (int yy = 0; yy < kHwSplits; ++yy) t[yy] = cb[(int64_t)yy * BS + o];
         float v = 0.f;
 #pragma unroll
         for (int yy = 0; yy < kHwSplits; ++yy) v += t[yy];
@@ -1444,9 +1443,15 @@ __device__ void head_combine_block(int x, const CnnLayout &L, const float *__res
         // components: policy rows, the value row, dbf (the mlp trunk's bias)
         if (sq) add_sq(*reinterpret_cast<double (*)[5]>(s), (double)v * (double)v, a < A ? 2 : a == A ? 3 : 1);
     }
-    if (sq && x == 0 && tid < A1) {
-        const double v = (double)G[tid < A ? L.obp + tid : L.obv];
-        add_sq(*reinterpret_cast<double (*)[5]>(s), v * v, tid < A ? 2 : 3);
+    if (x == 0 && tid < A1) {      // dbh: the ranges' sums in y order
+        float t[kHwSplits];
+#pragma unroll
+        for (int yy = 0; yy < kHwSplits; ++yy) t[yy] = cb[(int64_t)yy * BS + (A1 + 1) * kHwCols + tid];
+        float v = 0.f;
+#pragma unroll
+        for (int yy = 0; yy < kHwSplits; ++yy) v += t[yy];
+        G[tid < A ? L.obp + tid : L.obv] = v;
+        if (sq) add_sq(*reinterpret_cast<double (*)[5]>(s), (double)v * (double)v, tid < A ? 2 : 3);
     }
     if (sq) wg_reduce<5>(*reinterpret_cast<double (*)[5]>(s), sred);
 }

@@ -70,8 +70,7 @@ def main():
     for i, ph in enumerate(PHASES):
         print(f"    {ph:28s} {per[i]:8.0f} cyc  {per[i] / 2.4e3:6.2f} us")
     # k_cnn_head_wgrad: slot 1 its record workgroup, slot 2 main workgroup 0 (round 6)
-    for k, kn, names in ((1, "k_cnn_head_wgrad record workgroup", ["loss-sum partials", "dbh row ranges",
-                                                                   "barrier", "dbh / totals", "record"]),
+    for k, kn, names in ((1, "k_cnn_head_wgrad record workgroup", ["loss-sum partials", "totals", "record"]),
                          (2, "k_cnn_head_wgrad workgroup 0", ["dz rows -> LDS", "dbf partials", "barrier",
                                                               "h loads + FMAs", "slice shuffles",
                                                               "wave partials + block out"])):
