@@ -658,7 +658,10 @@ def main():
                        "exchange_in_bwd": in_bwd,
                        "exchange_self_test": dict(gd_self_test) if comm is not None else None,
                        "comm": comm_info, "same_device": bool(args.same_device),
-                       "dp_mode": args.dp_mode},
+                       "dp_mode": args.dp_mode,
+                       # the reference's training_step diagnostics (opt/activations/*, per-step
+                       # records) are a track_stats option; the timed region runs without them
+                       "track_stats": False, "activation_stats_in_timed_region": False},
             "roofline": roofline,
             "rooflines": rooflines,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},
