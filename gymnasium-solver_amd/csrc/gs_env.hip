@@ -109,7 +109,7 @@ extern "C" int gs_episode_stats(const float *rewards, const uint8_t *dones, int6
 // (r05: one thread per 128-sample chunk of byte loads, 151 us at C2's 32 x 4096).  Only the waves
 // holding one of the last W episodes walk their range again, with a wave prefix scan per
 // instruction, and only the groups of those episodes load their lengths.
-constexpr int kWinThreads = 1024, kWinWaves = kWinThreads / 64, kWinBatch = 8;
+constexpr int kWinThreads = 1024, kWinWaves = kWinThreads / 64, kWinBatch = 12, kWinBatch2 = 8;
 
 // the done bits of samples 4g..4g+3 (bit j = sample 4g + j) and their returns
 struct WinGroup {
@@ -207,31 +207,52 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
             win[i] = old[i + total];
             win[W + i] = old[W + i + total];
         }
-    // ---- pass 2: this rollout's last W episodes at their slots (only the waves that hold one)
+    // ---- pass 2: this rollout's last W episodes at their slots (only the waves that hold one).
+    // Lane l owns the contiguous groups [g0 + l C, g0 + (l + 1) C) of the wave's range: it counts its
+    // dones (loads kWinBatch2 at a time), a wave scan gives its first episode number, and it walks
+    // its groups again (L1 / L2-hot) writing the kept ones — every lane at once (the first form
+    // walked the wave's range 64 groups per step with a wave scan each: 32 dependent load rounds at
+    // the C2 shape, 49 us of the kernel's time)
     const int64_t first = total - W;           // episode numbers >= first are kept
     if (before + wcnt[wave] > first) {
-        int64_t base = before;                 // episodes before this wave instruction's groups
-        for (int64_t b = g0; b < g1 && base < total; b += 64) {
-            const int64_t g = b + lane;
-            WinGroup q = win_group(dones, ep_ret, g < g1 ? g : g0, n, vec);
-            if (g >= g1) q.bits = 0;
-            const int64_t c = __popc(q.bits);
-            const int64_t incl = wave_incl_scan(c, lane);
-            const int64_t wtot = __shfl(incl, 63, 64);
-            if (base + wtot > first && q.bits) {
-                int64_t pos = base + incl - c;
+        const int64_t C = (g1 - g0 + 63) / 64;
+        const int64_t lg0 = min(g1, g0 + lane * C), lg1 = min(g1, lg0 + C);
+        int64_t c = 0;
+        for (int64_t b = lg0; b < lg1; b += kWinBatch2) {
+            WinGroup q[kWinBatch2];
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (q.bits & (1u << j)) {
-                        const int64_t slot = pos - first;
-                        if (slot >= 0) {
-                            win[slot] = (double)q.r[j];
-                            win[W + slot] = (double)ep_len[4 * g + j];
-                        }
-                        ++pos;
-                    }
+            for (int u = 0; u < kWinBatch2; ++u) {
+                const int64_t g = b + u;
+                q[u] = win_group(dones, ep_ret, g < lg1 ? g : lg0, n, vec);
+                if (g >= lg1) q[u].bits = 0;
             }
-            base += wtot;
+#pragma unroll
+            for (int u = 0; u < kWinBatch2; ++u) c += __popc(q[u].bits);
+        }
+        const int64_t incl = wave_incl_scan(c, lane);
+        int64_t pos = before + incl - c;       // this lane's first episode number
+        if (pos + c > first) {
+            for (int64_t b = lg0; b < lg1; b += kWinBatch2) {
+                WinGroup q[kWinBatch2];
+#pragma unroll
+                for (int u = 0; u < kWinBatch2; ++u) {
+                    const int64_t g = b + u;
+                    q[u] = win_group(dones, ep_ret, g < lg1 ? g : lg0, n, vec);
+                    if (g >= lg1) q[u].bits = 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kWinBatch2; ++u)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (q[u].bits & (1u << j)) {
+                            const int64_t slot = pos - first;
+                            if (slot >= 0) {
+                                win[slot] = (double)q[u].r[j];
+                                win[W + slot] = (double)ep_len[4 * (b + u) + j];
+                            }
+                            ++pos;
+                        }
+            }
         }
     }
     if (tid == 0) {
