@@ -31,8 +31,8 @@ namespace gs {
 // diagnostic (GS_STAMPS builds only): per-phase cycles of k_conv1_wgrad_bf's unit loop, thread 0
 // of workgroup 0, summed over its units; read by gs_debug_conv_stamps (tools/cnn_stamp_run.py)
 // slot sets: 0 k_conv1_wgrad_bf, 1 / 2 k_conv_wgrad conv2 / conv3 (per-sample loop)
-__device__ unsigned long long g_conv_stamp_acc[3][8];
-__device__ unsigned long long g_conv_stamp_cnt[3];
+__device__ unsigned long long g_conv_stamp_acc[5][8];
+__device__ unsigned long long g_conv_stamp_cnt[5];
 #define C1S_DECL_K(k)                                                              \
     unsigned long long c1s_t = 0, c1s_acc[6] = {0, 0, 0, 0, 0, 0};                \
     const bool c1s_on = threadIdx.x == 0 && blockIdx.x == 0;                        \
@@ -795,6 +795,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
     const int r0 = sg * G::SPB;
     const int nsamp = min(G::SPB, R - r0);
 
+    C1S_DECL_K((FS == 4 && !BF) ? (G::C == 32 ? 3 : 4) : 0)
     // this wave's 16 filters, its k-step groups: b[g] = W[16 fb + li][16 (g0 + g) + 4 lq .. + 3]
     float4 b[NGW];
 #pragma unroll
@@ -856,7 +857,9 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
             }
         }
     }
+    C1S_MARK(0)                                     // weights + staging burst + LDS stores
     __syncthreads();
+    C1S_MARK(1)                                     // barrier
 
     int abase[G::MT];
 #pragma unroll
@@ -911,6 +914,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
             if (t + 1 < G::MT) acc[t + 1] = mfma(a1.w, b[g].w, acc[t + 1]);
         }
     }
+    C1S_MARK(2)                                     // MFMAs
     if constexpr (FS > 1) {
         // the k ranges 1 .. FS-1 of each filter block through LDS (the staging tile is free once
         // every wave has passed the barrier), added to range 0 in range order
@@ -927,6 +931,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
             if constexpr (AS) act_flush(ao, (int64_t)blockIdx.x * 4 + wave, 0.0f, 0.0f);
             return;
         }
+        C1S_MARK(3)                                 // k-range partials through LDS
         for (int q = 1; q < FS; ++q)
 #pragma unroll
             for (int t = 0; t < G::MT; ++t)
@@ -951,6 +956,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
             }
         }
     if constexpr (AS) act_flush(ao, (int64_t)blockIdx.x * 4 + wave, as_s, as_q);
+    C1S_MARK(4)                                     // epilogue
+    if constexpr (FS == 4 && !BF) {
+        C1S_END
+    }
 }
 
 // ---- conv2 / conv3 input gradient (transposed convolution) with the ReLU mask of the layer
@@ -1582,8 +1591,8 @@ int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const vo
 #ifdef GS_STAMPS
 extern "C" int gs_debug_conv_stamps(unsigned long long *acc_out, unsigned long long *cnt_out)
 {
-    GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(gs::g_conv_stamp_acc), sizeof(unsigned long long) * 24));
-    GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(gs::g_conv_stamp_cnt), sizeof(unsigned long long) * 3));
+    GS_HIP(hipMemcpyFromSymbol(acc_out, HIP_SYMBOL(gs::g_conv_stamp_acc), sizeof(unsigned long long) * 40));
+    GS_HIP(hipMemcpyFromSymbol(cnt_out, HIP_SYMBOL(gs::g_conv_stamp_cnt), sizeof(unsigned long long) * 5));
     return GS_OK;
 }
 #endif

@@ -116,12 +116,17 @@ struct WinGroup {
     unsigned bits;
     float r[4];
 };
+// VEC (the host checked 4-B dones / 16-B returns alignment and n % 4 == 0): one unconditional 4-B
+// and one 16-B load per group, so a batch of groups keeps all its loads in flight (a runtime
+// alignment test inside the batch made the compiler wait on every group's loads: the window kernel
+// ran at ~20 GB/s)
+template <bool VEC>
 __device__ __forceinline__ WinGroup win_group(const uint8_t *__restrict__ dones, const float *__restrict__ ep_ret,
-                                              int64_t g, int64_t n, bool vec)
+                                              int64_t g, int64_t n)
 {
     WinGroup o;
     const int64_t i0 = 4 * g;
-    if (vec && i0 + 4 <= n) {
+    if constexpr (VEC) {
         const unsigned d = *reinterpret_cast<const unsigned *>(dones + i0);
         const float4 v = *reinterpret_cast<const float4 *>(ep_ret + i0);
         // nonzero bytes -> bit 7 of each byte, then packed to bits 0..3
@@ -150,6 +155,7 @@ __device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane)
     return v;
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *__restrict__ dones,
                                                                 const float *__restrict__ ep_ret,
                                                                 const int32_t *__restrict__ ep_len, int64_t n, int W,
@@ -160,7 +166,6 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
     __shared__ double wbest[kWinWaves];
     extern __shared__ double old[];           // [2][W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool vec = (((uintptr_t)dones & 3) | ((uintptr_t)ep_ret & 15)) == 0;
     const int64_t G = (n + 3) / 4;                                   // 4-sample groups
     const int64_t g0 = (int64_t)wave * G / kWinWaves, g1 = (int64_t)(wave + 1) * G / kWinWaves;
     for (int i = tid; i < 2 * W; i += kWinThreads) old[i] = win[i];
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
 #pragma unroll
         for (int u = 0; u < kWinBatch; ++u) {
             const int64_t g = b + (int64_t)u * 64 + lane;
-            q[u] = win_group(dones, ep_ret, g < g1 ? g : g0, n, vec);
+            q[u] = win_group<VEC>(dones, ep_ret, g < g1 ? g : g0, n);
             if (g >= g1) q[u].bits = 0;
         }
 #pragma unroll
@@ -223,7 +228,7 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
 #pragma unroll
             for (int u = 0; u < kWinBatch2; ++u) {
                 const int64_t g = b + u;
-                q[u] = win_group(dones, ep_ret, g < lg1 ? g : lg0, n, vec);
+                q[u] = win_group<VEC>(dones, ep_ret, g < lg1 ? g : lg0, n);
                 if (g >= lg1) q[u].bits = 0;
             }
 #pragma unroll
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
 #pragma unroll
                 for (int u = 0; u < kWinBatch2; ++u) {
                     const int64_t g = b + u;
-                    q[u] = win_group(dones, ep_ret, g < lg1 ? g : lg0, n, vec);
+                    q[u] = win_group<VEC>(dones, ep_ret, g < lg1 ? g : lg0, n);
                     if (g >= lg1) q[u].bits = 0;
                 }
 #pragma unroll
@@ -267,8 +272,13 @@ extern "C" int gs_episode_window(const uint8_t *dones, const float *ep_ret, cons
 {
     GS_REQUIRE(T >= 0 && N >= 0 && W >= 1 && W <= 2048, "gs_episode_window: bad shape (W in [1, 2048])");
     GS_REQUIRE(dones && ep_ret && ep_len && window && meta, "gs_episode_window: null buffer");
-    hipLaunchKernelGGL(k_episode_window, dim3(1), dim3(kWinThreads), sizeof(double) * 2 * W, (hipStream_t)stream,
-                       dones, ep_ret, ep_len, T * N, (int)W, window, meta, total_out);
+    const bool vec = ((((uintptr_t)dones & 3) | ((uintptr_t)ep_ret & 15)) == 0) && (T * N) % 4 == 0;
+    if (vec)
+        hipLaunchKernelGGL(k_episode_window<true>, dim3(1), dim3(kWinThreads), sizeof(double) * 2 * W,
+                           (hipStream_t)stream, dones, ep_ret, ep_len, T * N, (int)W, window, meta, total_out);
+    else
+        hipLaunchKernelGGL(k_episode_window<false>, dim3(1), dim3(kWinThreads), sizeof(double) * 2 * W,
+                           (hipStream_t)stream, dones, ep_ret, ep_len, T * N, (int)W, window, meta, total_out);
     GS_LAUNCH_CHECK("k_episode_window");
     return GS_OK;
 }

@@ -85,9 +85,9 @@ def main():
     if a.bf16 and hasattr(lib, "gs_debug_conv_stamps"):
         # k_conv1_wgrad_bf's unit loop (csrc/gs_conv.hip C1S_MARK), workgroup 0, per launch
         lib.gs_debug_conv_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        c_acc, c_cnt = np.zeros(24, np.uint64), np.zeros(3, np.uint64)
+        c_acc, c_cnt = np.zeros(40, np.uint64), np.zeros(5, np.uint64)
         lib.gs_debug_conv_stamps(c_acc.ctypes.data, c_cnt.ctypes.data)
-        c_acc = c_acc.reshape(3, 8)
+        c_acc = c_acc.reshape(5, 8)
         sets = [("k_conv1_wgrad_bf", ["MFMAs (LDS operand reads)", "tiles landed + LDS stores", "barrier",
                                       "load issue", "prologue", "partial out"]),
                 ("k_conv_wgrad conv2", ["bias + gathers + MFMAs", "staging burst + LDS stores", "barrier",
