@@ -244,6 +244,8 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
     // wave w: filters [16 nt, 16 nt + 16) with nt = w / 2, position tiles w % 2, w % 2 + 2, ...
     // (7 or 6 of the 13 per band: balanced to within one tile)
     const int nt = wave >> 1, tpar = wave & 1;
+    const int co = nt * 16 + li;
+    const float bb = b1[co];      // the epilogue's bias, loaded with the filters
     float4 b[G::KS / 4];
 #pragma unroll
     for (int g = 0; g < G::KS / 4; ++g) {
@@ -323,8 +325,6 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const uint8_t *__restrict__ o
         }
         // epilogue: D row = lq * 4 + j (position), col = li (filter)
         act_t<XH> *o = out + ((int64_t)r * G::OH * G::OW + oy0 * G::OW) * G::CO;
-        const int co = nt * 16 + li;
-        const float bb = b1[co];
     #pragma unroll
         for (int t = 0; t < TMW; ++t) {
             if (tpar + 2 * t >= G::MT) break;
@@ -796,6 +796,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
     const int nsamp = min(G::SPB, R - r0);
 
     C1S_DECL_K((FS == 4 && !BF) ? (G::C == 32 ? 3 : 4) : 0)
+    // the epilogue's bias, loaded with the filters (loaded at the epilogue it put a memory latency
+    // in front of the first store: 3.7 of the rollout conv2's 10.5 us in the stamps)
+    const int co = 16 * fb + li;
+    const float bb = bias[co];
     // this wave's 16 filters, its k-step groups: b[g] = W[16 fb + li][16 (g0 + g) + 4 lq .. + 3]
     float4 b[NGW];
 #pragma unroll
@@ -940,8 +944,6 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const act_t<XH> *__restrict__ 
                     acc[t][j] += red[((((q - 1) * NFB + wave % NFB) * G::MT + t) * 4 + j) * 64 + lane];
     }
     // epilogue: D row = lq * 4 + j (position), col = li (filter 16 fb + li)
-    const int co = 16 * fb + li;
-    const float bb = bias[co];
     act_t<XH> *o = out + (int64_t)r0 * G::OHW * G::CO;
     float as_s = 0.0f, as_q = 0.0f;
 #pragma unroll

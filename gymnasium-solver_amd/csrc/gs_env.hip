@@ -282,13 +282,137 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
     }
 }
 
+// The same window from 16-sample units (VEC16: 16-B aligned dones, n % 16 == 0): a dword-quad of
+// dones per lane and unit, so the count pass reads 1 byte per sample instead of 5 (the returns are
+// loaded only where an episode ended); kWinUnits units per lane in flight.  Wave w owns a
+// contiguous unit range; pass 2 as in k_episode_window (contiguous per-lane chunks, one wave scan).
+constexpr int kWinUnits = 8;
+__device__ __forceinline__ unsigned done_mask16(uint4 d)
+{
+    auto nz4 = [](unsigned x) {      // nonzero bytes -> bit 7 of each byte -> bits 0..3
+        const unsigned nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+        return ((nz >> 7) & 1u) | ((nz >> 14) & 2u) | ((nz >> 21) & 4u) | ((nz >> 28) & 8u);
+    };
+    return nz4(d.x) | (nz4(d.y) << 4) | (nz4(d.z) << 8) | (nz4(d.w) << 12);
+}
+
+__global__ __launch_bounds__(kWinThreads) void k_episode_window16(const uint8_t *__restrict__ dones,
+                                                                  const float *__restrict__ ep_ret,
+                                                                  const int32_t *__restrict__ ep_len, int64_t n,
+                                                                  int W, double *__restrict__ win,
+                                                                  double *__restrict__ meta,
+                                                                  int64_t *__restrict__ total_out)
+{
+    __shared__ int64_t wcnt[kWinWaves];
+    __shared__ double wbest[kWinWaves];
+    extern __shared__ double old[];           // [2][W]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint4 *d16 = reinterpret_cast<const uint4 *>(dones);
+    const int64_t U = n / 16;
+    const int64_t u0 = (int64_t)wave * U / kWinWaves, u1 = (int64_t)(wave + 1) * U / kWinWaves;
+    for (int i = tid; i < 2 * W; i += kWinThreads) old[i] = win[i];
+    // ---- pass 1: done count and best return of this wave's range
+    int64_t cnt = 0;
+    double best = -INFINITY;
+    for (int64_t b = u0; b < u1; b += 64 * kWinUnits) {
+        unsigned m[kWinUnits];
+#pragma unroll
+        for (int k = 0; k < kWinUnits; ++k) {
+            const int64_t u = b + (int64_t)k * 64 + lane;
+            m[k] = done_mask16(d16[u < u1 ? u : u0]);
+            if (u >= u1) m[k] = 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kWinUnits; ++k) {
+            cnt += __popc(m[k]);
+            const int64_t base = 16 * (b + (int64_t)k * 64 + lane);
+            for (unsigned mm = m[k]; mm; mm &= mm - 1u)
+                best = fmax(best, (double)ep_ret[base + __ffs(mm) - 1]);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+        best = fmax(best, __shfl_xor(best, o, 64));
+    }
+    if (lane == 0) {
+        wcnt[wave] = cnt;
+        wbest[wave] = best;
+    }
+    __syncthreads();
+    int64_t total = 0, before = 0;
+    double all_best = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kWinWaves; ++w) {
+        before += w < wave ? wcnt[w] : 0;
+        total += wcnt[w];
+        all_best = fmax(all_best, wbest[w]);
+    }
+    for (int i = tid; i < W; i += kWinThreads)
+        if (i + total < W) {
+            win[i] = old[i + total];
+            win[W + i] = old[W + i + total];
+        }
+    // ---- pass 2: the last W episodes, lane l over the contiguous units [u0 + l C, u0 + (l + 1) C)
+    const int64_t first = total - W;
+    if (before + wcnt[wave] > first) {
+        const int64_t C = (u1 - u0 + 63) / 64;
+        const int64_t lu0 = min(u1, u0 + lane * C), lu1 = min(u1, lu0 + C);
+        int64_t c = 0;
+        for (int64_t b = lu0; b < lu1; b += kWinUnits) {
+            unsigned m[kWinUnits];
+#pragma unroll
+            for (int k = 0; k < kWinUnits; ++k) {
+                const int64_t u = b + k;
+                m[k] = done_mask16(d16[u < lu1 ? u : lu0]);
+                if (u >= lu1) m[k] = 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < kWinUnits; ++k) c += __popc(m[k]);
+        }
+        const int64_t incl = wave_incl_scan(c, lane);
+        int64_t pos = before + incl - c;
+        if (pos + c > first) {
+            for (int64_t b = lu0; b < lu1; b += kWinUnits) {
+                unsigned m[kWinUnits];
+#pragma unroll
+                for (int k = 0; k < kWinUnits; ++k) {
+                    const int64_t u = b + k;
+                    m[k] = done_mask16(d16[u < lu1 ? u : lu0]);
+                    if (u >= lu1) m[k] = 0u;
+                }
+#pragma unroll
+                for (int k = 0; k < kWinUnits; ++k)
+                    for (unsigned mm = m[k]; mm; mm &= mm - 1u) {
+                        const int64_t slot = pos - first;
+                        if (slot >= 0) {
+                            const int64_t i = 16 * (b + k) + __ffs(mm) - 1;
+                            win[slot] = (double)ep_ret[i];
+                            win[W + slot] = (double)ep_len[i];
+                        }
+                        ++pos;
+                    }
+            }
+        }
+    }
+    if (tid == 0) {
+        meta[0] += (double)total;
+        meta[1] = fmax(meta[1], all_best);
+        if (total_out) *total_out = total;
+    }
+}
+
 extern "C" int gs_episode_window(const uint8_t *dones, const float *ep_ret, const int32_t *ep_len, int64_t T,
                                  int64_t N, int64_t W, double *window, double *meta, int64_t *total_out, void *stream)
 {
     GS_REQUIRE(T >= 0 && N >= 0 && W >= 1 && W <= 2048, "gs_episode_window: bad shape (W in [1, 2048])");
     GS_REQUIRE(dones && ep_ret && ep_len && window && meta, "gs_episode_window: null buffer");
+    const bool vec16 = ((uintptr_t)dones & 15) == 0 && (T * N) % 16 == 0;
     const bool vec = ((((uintptr_t)dones & 3) | ((uintptr_t)ep_ret & 15)) == 0) && (T * N) % 4 == 0;
-    if (vec)
+    if (vec16)
+        hipLaunchKernelGGL(k_episode_window16, dim3(1), dim3(kWinThreads), sizeof(double) * 2 * W,
+                           (hipStream_t)stream, dones, ep_ret, ep_len, T * N, (int)W, window, meta, total_out);
+    else if (vec)
         hipLaunchKernelGGL(k_episode_window<true>, dim3(1), dim3(kWinThreads), sizeof(double) * 2 * W,
                            (hipStream_t)stream, dones, ep_ret, ep_len, T * N, (int)W, window, meta, total_out);
     else
