@@ -67,21 +67,24 @@ __global__ __launch_bounds__(256) void k_episode_stats(const float *__restrict__
     if (e >= N) return;
     float r = run_ret[e];
     int32_t l = run_len[e];
-    // kEpBatch steps' loads in flight at once (clamped, unconditional), then the same step-order
-    // arithmetic (a load per step had made this a T-latency chain: 33 us at C5's 128 steps)
+    // kEpBatch steps' loads in flight at once, then the same step-order arithmetic (a load per
+    // step had made this a T-latency chain: 33 us at C5's 128 steps); the empty asm keeps the
+    // compiler from sinking the loads back into their steps
     constexpr int kEpBatch = 16;
-    for (int64_t t0 = 0; t0 < T; t0 += kEpBatch) {
+    int64_t t0 = 0;
+    for (; t0 + kEpBatch <= T; t0 += kEpBatch) {
         float rw[kEpBatch];
-        uint8_t dn[kEpBatch];
+        uint32_t dn[kEpBatch];
 #pragma unroll
         for (int u = 0; u < kEpBatch; ++u) {
-            const int64_t o = (t0 + u < T ? t0 + u : T - 1) * N + e;
+            const int64_t o = (t0 + u) * N + e;
             rw[u] = rewards[o];
             dn[u] = dones[o];
         }
 #pragma unroll
+        for (int u = 0; u < kEpBatch; ++u) asm volatile("" ::"v"(rw[u]), "v"(dn[u]));
+#pragma unroll
         for (int u = 0; u < kEpBatch; ++u) {
-            if (t0 + u >= T) break;
             const int64_t o = (t0 + u) * N + e;
             r += rw[u];
             l += 1;
@@ -92,6 +95,18 @@ __global__ __launch_bounds__(256) void k_episode_stats(const float *__restrict__
                 r = 0.0f;
                 l = 0;
             }
+        }
+    }
+    for (int64_t t = t0; t < T; ++t) {
+        const int64_t o = t * N + e;
+        r += rewards[o];
+        l += 1;
+        const bool d = dones[o] != 0;
+        ep_ret[o] = d ? r : 0.0f;
+        ep_len[o] = d ? l : 0;
+        if (d) {
+            r = 0.0f;
+            l = 0;
         }
     }
     run_ret[e] = r;

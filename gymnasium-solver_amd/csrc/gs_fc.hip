@@ -262,6 +262,14 @@ __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int6
 
     Stage<BM, BF, AK, KT, (H16 & 1) != 0> sa[PD];
     Stage<BN, BF, BKC, KT, (H16 & 2) != 0> sb[PD];
+    // the bias + ReLU epilogue's bias, loaded before the K loop (at the epilogue it put a memory
+    // latency in front of the stores)
+    float bn[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int gn = min(n0 + wn + 32 * j + l32, N - 1);
+        bn[j] = EPI == kEpiBiasRelu ? act_ld<(H16 & 4) != 0>(aux, gn) : 0.0f;
+    }
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -371,14 +379,13 @@ __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int6
         for (int j = 0; j < TN; ++j) {
             const int gn = n0 + wn + 32 * j + l32;
             if (gn >= N) continue;
-            const float bn = EPI == kEpiBiasRelu ? act_ld<(H16 & 4) != 0>(aux, gn) : 0.0f;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int gm = m0 + wm + 32 * i + (v & 3) + 8 * (v >> 2) + 4 * lh;
                 if (gm >= M) continue;
                 float x = acc[i][j][v];
                 if constexpr (EPI == kEpiBiasRelu) {
-                    x += bn;
+                    x += bn[j];
                     if constexpr (AS) act_acc(ao, x, gn, as_s, as_q);
                     x = x > 0.0f ? x : 0.0f;
                 }
