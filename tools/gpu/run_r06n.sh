@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${TAG:-r06n}; mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)" >&2; shift; "$@"; rc=$?; echo "rc=$rc" >&2; return $rc; }
-SEL="tests/test_gpu_agent.py tests/test_gpu_api.py tests/test_gpu_cnn.py tests/test_gpu_atari.py" OUT=${TAG:-r06n} TMO=500 \
+SEL="tests/test_gpu_agent.py tests/test_gpu_api.py tests/test_gpu_cnn.py tests/test_gpu_atari.py tests/test_gpu_gemm.py" OUT=${TAG:-r06n} TMO=500 \
     bash tools/gpu/run_tests.sh > $O/tests_summary.txt 2>&1 || { echo "tests failed" >&2; exit 1; }
 for w in C2 C5; do
   step trace-$w timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/$w -o c --output-format csv \
