@@ -270,6 +270,21 @@ __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int6
         const int gn = min(n0 + wn + 32 * j + l32, N - 1);
         bn[j] = EPI == kEpiBiasRelu ? act_ld<(H16 & 4) != 0>(aux, gn) : 0.0f;
     }
+    // the masked epilogue's relu' operands (the input gradient's activation), likewise
+    float mk[EPI == kEpiMask ? TM : 1][EPI == kEpiMask ? TN : 1][EPI == kEpiMask ? 16 : 1];
+    if constexpr (EPI == kEpiMask) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int gn = min(n0 + wn + 32 * j + l32, N - 1);
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const int gm = min(m0 + wm + 32 * i + (v & 3) + 8 * (v >> 2) + 4 * lh, M - 1);
+                    mk[i][j][v] = act_ld<(H16 & 4) != 0>(aux, (int64_t)gm * ldc + gn);
+                }
+            }
+    }
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -389,7 +404,7 @@ __global__ __launch_bounds__(256, 2) void k_fc(const void *__restrict__ Av, int6
                     if constexpr (AS) act_acc(ao, x, gn, as_s, as_q);
                     x = x > 0.0f ? x : 0.0f;
                 }
-                if constexpr (EPI == kEpiMask) x = act_ld<(H16 & 4) != 0>(aux, (int64_t)gm * ldc + gn) > 0.0f ? x : 0.0f;
+                if constexpr (EPI == kEpiMask) x = mk[i][j][v] > 0.0f ? x : 0.0f;
                 C[(int64_t)gm * ldc + gn] = x;
             }
         }
