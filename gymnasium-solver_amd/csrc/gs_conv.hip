@@ -1066,6 +1066,28 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
             }
         }
     }
+    // the epilogue's ReLU mask (the layer input at this lane's output elements), loaded after the
+    // staging burst so the loads run under the MFMAs (loaded at the epilogue they put a memory
+    // latency in front of its stores; loaded with the weights they raised the register peak of the
+    // staging phase: conv3 192 -> 230 VGPRs); 32-bit offsets from the workgroup's first sample
+    // conv3's bf16 forms (conv2's 512-thread tile went 100 -> 176 VGPRs, the fp32 conv3 to one wave per SIMD)
+    constexpr bool MKP = G::NCLS == 1 && BF;
+    float mkv[MKP ? G::MT : 1][4][MKP ? G::NT : 1];
+    if constexpr (MKP) {
+        const act_t<XH> *ab = act + (int64_t)r0 * G::H * G::W * G::C;
+#pragma unroll
+        for (int t = 0; t < G::MT; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int p = t * 16 + lq * 4 + j;
+                const int q = p / (G::NY * G::NX), rem = p - q * (G::NY * G::NX);
+                const bool ok = p < G::M && q < nsamp;
+                const int yy = rem / G::NX, xx = rem - yy * G::NX;
+                const int off = ok ? ((q * G::H + G::S * yy + py) * G::W + G::S * xx + px) * G::C + c0 + li : 0;
+#pragma unroll
+                for (int nt = 0; nt < G::NT; ++nt) mkv[t][j][nt] = act_ld<XH>(ab, off + 16 * nt);
+            }
+    }
     __syncthreads();
 
     int abase[G::MT];
@@ -1138,7 +1160,8 @@ __global__ __launch_bounds__(G::NTHR) void k_conv_dgrad(const float *__restrict_
             const int64_t e = (((int64_t)(r0 + q) * G::H + y) * G::W + x) * G::C + c0 + li;
 #pragma unroll
             for (int nt = 0; nt < G::NT; ++nt)
-                dX[e + 16 * nt] = act_ld<XH>(act, e + 16 * nt) > 0.f ? acc[t][nt][j] : 0.f;
+                dX[e + 16 * nt] = (MKP ? mkv[MKP ? t : 0][j][MKP ? nt : 0] : act_ld<XH>(act, e + 16 * nt)) > 0.f
+                                      ? acc[t][nt][j] : 0.f;
         }
 }
 

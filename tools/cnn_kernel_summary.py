@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel rooflines of the NatureCNN minibatch step (C4 shapes) from three rocprofv3 runs of
 tools/cnn_kernel_run.py: --kernel-trace (durations), --pmc FETCH_SIZE and --pmc WRITE_SIZE (HBM
-bytes; separate passes).  Every minibatch dispatches the same 28 kernels in the same order
-(gs_cnn.hip cnn_step: gather, forward, loss, backward, norm, clip+Adam), so each dispatch is named
+bytes; separate passes).  Every minibatch dispatches the same kernels in the same order
+(gs_cnn.hip cnn_step: forward, head + loss, head weight gradient, backward, the fused tail, clip + Adam), so each dispatch is named
 by its position in the minibatch and the three runs line up position by position.
 
 Per kernel: average duration over the measured minibatches, algorithmic FLOPs (2 x MACs of the
@@ -32,12 +32,14 @@ PEAK_HBM = 8000.0         # GB/s
 # (gs_cnn.hip cnn_step): the fc layer's three products on the hand-written k_fc kernels
 # (csrc/gs_fc.hip), the fused head + loss pair, the LDS-resident conv kernels
 SEQ_FC = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd", "k_conv_fwd"),
-          ("fc_fwd", "k_fc"), ("head_loss", "k_cnn_head_loss"), ("head_wsum_metrics", "k_cnn_head_wsum"),
+          ("fc_fwd", "k_fc"), ("head_loss", "k_cnn_head_loss"), ("head_wgrad_metrics", "k_cnn_head_wgrad"),
           ("fc_wgrad", "k_fc"), ("fc_dgrad_relu_mask", "k_fc"),
           ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts"),
           ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts"),
-          ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"), ("conv1_wgrad_sum", "k_sum_parts"),
-          ("norm_partials", "k_norm_partials"), ("clip_adam", "k_clip_adam_flat")]
+          ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"),
+          ("conv1_sum_head_combine_norm", "k_conv1_sum_norm"), ("clip_adam", "k_clip_adam_flat")]
+# (round 6: the head weight gradient's own kernel replaced k_cnn_head_wsum, and the fused backward
+# tail k_conv1_sum_norm replaced the conv1 partial sum and k_norm_partials)
 # the fp32 update (round 5): the fc forward as two K halves + k_fc_sum (the bias + ReLU epilogue)
 SEQ_FC_SPLIT = SEQ_FC[:4] + [("fc_fwd_splitk_sum", "k_fc_sum")] + SEQ_FC[4:]
 SEQ = SEQ_FC
@@ -68,7 +70,8 @@ def nature_work(B, A=18, C=4, H=84, W=84, store16=False):
         "conv3_wgrad": (2 * m3, n2 * ea + n3 * f + p3 * f), "conv3_dgrad": (2 * m3, n3 * f + p3 * ew + n2 * f + n2 * ea),
         "conv2_wgrad": (2 * m2, n1 * ea + n2 * f + p2 * f), "conv2_dgrad": (2 * m2, n2 * f + p2 * ew + n1 * f + n1 * ea),
         "conv1_wgrad": (2 * m1, frames + n1 * f + p1 * f),
-        "head_loss": (4 * mh, hb + Wh + zb + B * HID * ed),    # z = h Wh^T and the dWh partials (+ dh out)
+        "head_loss": (4 * mh, hb + Wh + zb + B * HID * ed),    # z = h Wh^T and dh = relu'(h) (dz Wh) (+ dh out)
+        "head_wgrad_metrics": (2 * mh, hb + zb + Wh),          # [dWh | dbf] = dz^T [h | 1]
     }
 
 

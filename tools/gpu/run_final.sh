@@ -17,7 +17,10 @@ for v in "" "--bf16"; do
   step cnn-write$v timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/${d}_write \
       -o pmc -- python tools/cnn_kernel_run.py $v > $O/${d}_write.log 2>&1 || exit 1
 done
-python tools/cnn_kernel_summary.py $O > $O/c4_kernels.json &&
-python tools/cnn_kernel_summary.py $O --bf16 --prefix cnnbf > $O/c4_kernels_bf16.json &&
-cp $O/c4_kernels.json profiles/c4_kernels.json && cp $O/c4_kernels_bf16.json profiles/c4_kernels_bf16.json || exit 1
+# the tables (host-side reductions: a failure here leaves the old tables, whose source hash then
+# does not match, and the lines report no C4 traffic rather than stopping)
+python tools/cnn_kernel_summary.py $O > $O/c4_kernels.json 2> $O/c4_kernels.err &&
+python tools/cnn_kernel_summary.py $O --bf16 --prefix cnnbf > $O/c4_kernels_bf16.json 2>> $O/c4_kernels.err &&
+cp $O/c4_kernels.json profiles/c4_kernels.json && cp $O/c4_kernels_bf16.json profiles/c4_kernels_bf16.json ||
+    echo "c4 kernel tables failed (see $O/c4_kernels.err)" >&2
 TAG=${TAG:-final} bash tools/gpu/run_lines.sh
