@@ -98,6 +98,7 @@ struct CnnWs {
     double *norm_part;
     double *loss_part;     // kSums per loss row block
     float *parts;          // split-K weight-gradient partials / bias column-sum partials
+    float *parts3, *parts2;     // conv3 / conv2 weight-gradient partials summed in the fused tail
     float *pre;            // [kPreChunk][5][R]: minibatches' gathered fields (act bits, olp, ov, adv, ret)
     float *pre_stats;      // [kPreChunk][2]: their advantage mean / std
     uint16_t *pbf;         // [P]: the parameters as bf16, the weight operands of a bf16 update
@@ -114,6 +115,7 @@ struct CnnWs {
 constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block sums them)
 constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
 constexpr int kConv1NormMax = 1024;   // k_conv1_sum_norm sum blocks (conv1 [dW1 | db1] <= 64 K floats)
+constexpr int kTailPartsMax = 4096;   // the fused tail's squared-norm partials (conv1 + head + conv3 + conv2 blocks)
 // k_cnn_head_wgrad: 64-column blocks x kHwSplits row ranges, kHwRows rows of loads in flight,
 // kDbhSlices row slices of a range's dbh sums; at most kHwMaxCb column blocks (HID <= 512: head_fused)
 constexpr int kHwCols = 64, kHwSplits = 16, kHwRows = 4, kDbhSlices = 8, kHwMaxCb = 8;
@@ -205,7 +207,7 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
     w.f_adv = (float *)take(sizeof(float) * R);
     w.f_ret = (float *)take(sizeof(float) * R);
     // total + 4 component partials, then k_conv1_sum_norm's conv1 partials
-    w.norm_part = (double *)take(sizeof(double) * (kNormBlocks * 5 + 5 * (kConv1NormMax + kHwMaxCb)));
+    w.norm_part = (double *)take(sizeof(double) * (kNormBlocks * 5 + 5 * kTailPartsMax));
     w.pre = (float *)take(sizeof(float) * kPreChunk * 5 * R);
     w.pre_stats = (float *)take(sizeof(float) * kPreChunk * 2);
     {   // shifted so Wf's rows start on 128-B lines (the fc kernels stream them in 128-B chunks; a
@@ -234,6 +236,10 @@ CnnWs carve(void *base, const CnnLayout &L, int64_t R)
         const int64_t hparts = (R + kHeadRows - 1) / kHeadRows * head_part_stride(L);
         w.parts = (float *)take(sizeof(float) * std::max({wparts, cparts, gparts, hparts}));
     }
+    // the fused tail's conv3 / conv2 weight-gradient partials (kept apart from w.parts, which the
+    // conv1 weight gradient fills before the tail sums them)
+    w.parts3 = (float *)take(sizeof(float) * (size_t)kConvWgradWG * 64 * (L.K3 + 1));
+    w.parts2 = (float *)take(sizeof(float) * (size_t)kConvWgradWG * 64 * (L.K2 + 1));
     w.act_cnt = (uint32_t *)take(sizeof(uint32_t) * (size_t)act_neurons_total(L));
     w.act_part = (float *)take(sizeof(float) * 2 * (size_t)act_slots_cap(L, R) * 4);
     w.act_fb = (double *)take(sizeof(double) * 16);
@@ -1509,6 +1515,61 @@ __global__ __launch_bounds__(256) void k_norm_partials(const float *__restrict__
     norm_partials_block(G, n, 0, part, blockIdx.x, gridDim.x, cut0, cut1, cut2, sred);
 }
 
+// block b of k_sum_parts_tiles (gs_gemm.hip: the conv2 / conv3 weight-gradient partials in MFMA
+// tile order, 64 outputs per block, four interleaved chains per output added in a fixed tree — the
+// same arithmetic, so dW / db are bit-identical), restated here for the fused tail, with the
+// double sum of squares of its outputs returned through sred[0] (thread 0)
+__device__ double sum_tiles_block(const float *__restrict__ parts, int np, int64_t pstride, int ncols,
+                                  float *__restrict__ dW, float *__restrict__ db, int b, double *sred)
+{
+    float(*red)[64] = reinterpret_cast<float(*)[64]>(sred);       // [4][64] floats in the double buffer
+    const int jj = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t i = (int64_t)b * 64 + jj;
+    const int64_t n = (int64_t)64 * (ncols + 1);
+    float a = 0.f;
+    if (i < n) {
+        int p = g;
+        for (; p + 28 < np; p += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = parts[(int64_t)(p + 4 * u) * pstride + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; p < np; p += 4) a += parts[(int64_t)p * pstride + i];
+    }
+    red[g][jj] = a;
+    __syncthreads();
+    double q2 = 0.0;
+    if (g == 0 && i < n) {
+        const float v = (red[0][jj] + red[1][jj]) + (red[2][jj] + red[3][jj]);
+        q2 = (double)v * (double)v;
+        const int64_t nt = (int64_t)64 * ncols;
+        if (i >= nt) {
+            db[i - nt] = v;
+        } else {
+            const int j = (int)(i & 3), lane = (int)((i >> 2) & 63);
+            const int q = (int)(i >> 8), ntg = ncols / 16, mt = q / ntg, gt = q - mt * ntg;
+            dW[(int64_t)(16 * mt + 4 * (lane >> 4) + j) * ncols + 16 * gt + (lane & 15)] = v;
+        }
+    }
+    __syncthreads();      // red is dead: the square sum reuses the buffer
+    double t[1] = {q2};
+    wg_reduce<1>(t, sred);
+    return t[0];
+}
+
+// the conv2 / conv3 weight-gradient sums the fused tail takes over (partials, their count and
+// stride, the patch width, the outputs, the tail's blocks for them)
+struct TailSum {
+    const float *parts;
+    int np;
+    int64_t pstride;
+    int ncols;
+    float *dW, *db;
+    int nblk;
+};
+
 // ---- one launch for the end of the backward (no exchange follows): blocks [0, nsum) sum conv1's
 // [dW1 | db1] (G[0, n1)) from its weight-gradient partials exactly as k_sum_parts4 (the same float4
 // chains and group tree: bit-identical), each also writing the double sum of squares of its
@@ -1522,20 +1583,34 @@ __global__ __launch_bounds__(256) void k_conv1_sum_norm(const float *__restrict_
                                                         int64_t n1, int nsum, int ncb, CnnLayout L,
                                                         const float *__restrict__ hw_part, float *__restrict__ G,
                                                         double *__restrict__ part, double *__restrict__ part1,
-                                                        const int32_t *__restrict__ stop)
+                                                        const int32_t *__restrict__ stop, TailSum t3, TailSum t2)
 {
     __shared__ double sred[5 * (256 + 16)];
-    const int nx = nsum + ncb;
+    // blocks: [0, nsum) conv1 | [nsum, nsum + ncb) head | conv3 sums | conv2 sums | norm blocks
+    const int nh = nsum + ncb, n3 = nh + t3.nblk, nx = n3 + t2.nblk;
     if ((int)blockIdx.x >= nsum) {
         if (stop && *stop) return;
-        if ((int)blockIdx.x < nx) {
+        if ((int)blockIdx.x < nh) {
             double s5[5];
             head_combine_block((int)blockIdx.x - nsum, L, hw_part, G, true, s5, sred);
             if (threadIdx.x < 5) part1[(int64_t)threadIdx.x * nx + blockIdx.x] = s5[threadIdx.x];
             return;
         }
-        norm_partials_block(G + n1, L.obf - n1, n1, part, (int)blockIdx.x - nx, kNormBlocks, L.oWf, L.oWp, L.oWv,
-                            sred);
+        if ((int)blockIdx.x < nx) {      // conv3 / conv2 weight-gradient sums (component: the cnn trunk)
+            const bool c3 = (int)blockIdx.x < n3;
+            const TailSum &ts = c3 ? t3 : t2;
+            const double q2 = sum_tiles_block(ts.parts, ts.np, ts.pstride, ts.ncols, ts.dW, ts.db,
+                                              (int)blockIdx.x - (c3 ? nh : n3), sred);
+            if (threadIdx.x == 0) {
+                part1[blockIdx.x] = q2;
+                part1[(int64_t)nx + blockIdx.x] = q2;
+                for (int q = 2; q < 5; ++q) part1[(int64_t)q * nx + blockIdx.x] = 0.0;
+            }
+            return;
+        }
+        // the rest of the trunk gradient: Wf (conv2 / conv3 come from their sums above)
+        norm_partials_block(G + L.oWf, L.obf - L.oWf, L.oWf, part, (int)blockIdx.x - nx, kNormBlocks, L.oWf, L.oWp,
+                            L.oWv, sred);
         return;
     }
     __shared__ float4 red[16][16];
@@ -1861,9 +1936,13 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
 inline bool fused_tail_ok(const CnnLayout &L)
 {
     const int64_t n1 = L.ob1 + L.c1;
+    // (the tail also sums the LDS conv2 / conv3 weight gradients' partials: their [dW | db] fill
+    // [n1, oWf), and its norm blocks cover only Wf)
     return conv1_lds_supported(L.C, L.H, L.W) && L.oW1 == 0 && L.ob1 == (int64_t)L.c1 * L.K1 && n1 % 4 == 0 &&
            (n1 / 4 + 15) / 16 <= kConv1NormMax && L.obf > n1 && L.oWp == L.obf + L.HID &&
-           (L.HID + kHwCols - 1) / kHwCols <= kHwMaxCb;
+           (L.HID + kHwCols - 1) / kHwCols <= kHwMaxCb &&
+           conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3) &&
+           conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2) && L.oW2 == n1 && L.oWf == L.ob3 + L.c3;
 }
 
 int backward(const float *P, const CnnLayout &L, const FrameSrc &fs, int64_t B, const CnnWs &w, float *G,
@@ -1914,7 +1993,10 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // conv3 (dY3 = da3 as [m3][c3])
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
-        if ((rc = conv23_lds_wgrad(s, bf, xh, 3, (int)B, w.a2, w.da3, w.parts, G + L.oW3, G + L.ob3))) return rc;
+        // the fused tail (nsum1) sums these partials itself: its own buffer, no sum launch here
+        if ((rc = conv23_lds_wgrad(s, bf, xh, 3, (int)B, w.a2, w.da3, nsum1 ? w.parts3 : w.parts, G + L.oW3, G + L.ob3,
+                                   !nsum1)))
+            return rc;
     } else if ((rc = conv_wgrad_nhwc(s, bf, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) {
         return rc;
     }
@@ -1930,7 +2012,9 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // conv2
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_wgrad(s, bf, xh, 2, (int)B, w.a1, w.da2, w.parts, G + L.oW2, G + L.ob2))) return rc;
+        if ((rc = conv23_lds_wgrad(s, bf, xh, 2, (int)B, w.a1, w.da2, nsum1 ? w.parts2 : w.parts, G + L.oW2, G + L.ob2,
+                                   !nsum1)))
+            return rc;
     } else if ((rc = conv_wgrad_nhwc(s, bf, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) {
         return rc;
     }
@@ -1954,10 +2038,15 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
             if ((rc = conv1_lds_wgrad(s, bf, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1,
                                       &np)))
                 return rc;
-            hipLaunchKernelGGL(k_conv1_sum_norm, dim3((unsigned)(ns + ncb + kNormBlocks)), dim3(256), 0, s, w.parts, np,
-                               n1, n1, ns, ncb, L, w.hw_part, G, w.norm_part, w.norm_part + 5 * kNormBlocks, stop);
+            // conv3 / conv2 weight-gradient sums (k_sum_parts_tiles' blocks: 64 outputs each)
+            const TailSum t3{w.parts3, kConvWgradWG, (int64_t)64 * (L.K3 + 1), L.K3, G + L.oW3, G + L.ob3, L.K3 + 1};
+            const TailSum t2{w.parts2, kConvWgradWG, (int64_t)64 * (L.K2 + 1), L.K2, G + L.oW2, G + L.ob2, L.K2 + 1};
+            const int nx = ns + ncb + t3.nblk + t2.nblk;
+            GS_REQUIRE(nx <= kTailPartsMax, "the fused tail's %d partial blocks exceed %d", nx, kTailPartsMax);
+            hipLaunchKernelGGL(k_conv1_sum_norm, dim3((unsigned)(nx + kNormBlocks)), dim3(256), 0, s, w.parts, np, n1, n1,
+                               ns, ncb, L, w.hw_part, G, w.norm_part, w.norm_part + 5 * kNormBlocks, stop, t3, t2);
             GS_LAUNCH_CHECK("k_conv1_sum_norm");
-            *nsum1 = ns + ncb;
+            *nsum1 = nx;
             return GS_OK;
         }
         return conv1_lds_wgrad(s, bf, (int)B, fs.obs, fs.idx, fs.T, fs.N, w.da1, w.parts, G + L.oW1, G + L.ob1);

@@ -46,8 +46,9 @@ int conv_fwd_act_slots(int layer, int R, bool bf, bool xh);
 // dX = (dY conv^T W) * (act > 0), NHWC fp32
 int conv23_lds_dgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const float *dY, const void *act,
                      const void *Wt, float *dX);
-// dW (64 x patch) and db (64) of conv2 / conv3; parts: kConvWgradWG x 64 x (patch + 1) floats
+// dW (64 x patch) and db (64) of conv2 / conv3; parts: kConvWgradWG x 64 x (patch + 1) floats.
+// sum = false: only the partials (the caller's fused tail sums them, k_sum_parts_tiles' order)
 int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const float *dY, float *parts,
-                     float *dW, float *db);
+                     float *dW, float *db, bool sum = true);
 
 }  // namespace gs

@@ -1594,7 +1594,7 @@ void launch_conv_wgrad(hipStream_t s, bool bf, bool xh, int nwg, int R, const vo
 }
 
 int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const void *in, const float *dY, float *parts,
-                     float *dW, float *db)
+                     float *dW, float *db, bool sum)
 {
     GS_REQUIRE(R > 0 && in && dY && parts && dW && db, "conv23_lds_wgrad: bad argument");
     GS_REQUIRE(!xh || bf, "conv23_lds_wgrad: bf16 activation storage needs bf16 operands");
@@ -1608,6 +1608,7 @@ int conv23_lds_wgrad(hipStream_t s, bool bf, bool xh, int layer, int R, const vo
         launch_conv_wgrad<C3_84>(s, bf, xh, nwg, R, in, dY, parts);
     }
     GS_LAUNCH_CHECK("k_conv_wgrad");
+    if (!sum) return GS_OK;
     return sum_parts_tiles(s, parts, nwg, (int64_t)64 * (KK + 1), KK, dW, db);
 }
 
