@@ -115,7 +115,11 @@ struct CnnWs {
 constexpr int kNormBlocks = 256;   // norm partial blocks (every clip/Adam block sums them)
 constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
 constexpr int kConv1NormMax = 1024;   // k_conv1_sum_norm sum blocks (conv1 [dW1 | db1] <= 64 K floats)
-constexpr int kTailPartsMax = 4096;   // the fused tail's squared-norm partials (conv1 + head + conv3 + conv2 blocks)
+constexpr int kTailPartsMax = 4096;
+#ifndef GS_TAIL_CONV_SUMS
+#define GS_TAIL_CONV_SUMS 1
+#endif
+constexpr bool kTailConvSums = GS_TAIL_CONV_SUMS != 0;   // the fused tail also sums conv2 / conv3 (A/B switch)   // the fused tail's squared-norm partials (conv1 + head + conv3 + conv2 blocks)
 // k_cnn_head_wgrad: 64-column blocks x kHwSplits row ranges, kHwRows rows of loads in flight,
 // kDbhSlices row slices of a range's dbh sums; at most kHwMaxCb column blocks (HID <= 512: head_fused)
 constexpr int kHwCols = 64, kHwSplits = 16, kHwRows = 4, kDbhSlices = 8, kHwMaxCb = 8;
@@ -1608,9 +1612,10 @@ __global__ __launch_bounds__(256) void k_conv1_sum_norm(const float *__restrict_
             }
             return;
         }
-        // the rest of the trunk gradient: Wf (conv2 / conv3 come from their sums above)
-        norm_partials_block(G + L.oWf, L.obf - L.oWf, L.oWf, part, (int)blockIdx.x - nx, kNormBlocks, L.oWf, L.oWp,
-                            L.oWv, sred);
+        // the rest of the trunk gradient: Wf (conv2 / conv3 come from their sums above, unless the
+        // tail does not take them: then from n1)
+        const int64_t a0 = t3.nblk ? L.oWf : n1;
+        norm_partials_block(G + a0, L.obf - a0, a0, part, (int)blockIdx.x - nx, kNormBlocks, L.oWf, L.oWp, L.oWv, sred);
         return;
     }
     __shared__ float4 red[16][16];
@@ -1994,8 +1999,9 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     // conv3 (dY3 = da3 as [m3][c3])
     if (conv23_lds_supported(3, L.h2, L.w2, L.c2, L.k3, L.s3, L.c3)) {
         // the fused tail (nsum1) sums these partials itself: its own buffer, no sum launch here
-        if ((rc = conv23_lds_wgrad(s, bf, xh, 3, (int)B, w.a2, w.da3, nsum1 ? w.parts3 : w.parts, G + L.oW3, G + L.ob3,
-                                   !nsum1)))
+        const bool ts = nsum1 && kTailConvSums;
+        if ((rc = conv23_lds_wgrad(s, bf, xh, 3, (int)B, w.a2, w.da3, ts ? w.parts3 : w.parts, G + L.oW3, G + L.ob3,
+                                   !ts)))
             return rc;
     } else if ((rc = conv_wgrad_nhwc(s, bf, geom3(L, B), w.a2, w.da3, w.parts, kSplitW3, G + L.oW3, G + L.ob3))) {
         return rc;
@@ -2012,8 +2018,8 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
     }
     // conv2
     if (conv23_lds_supported(2, L.h1, L.w1, L.c1, L.k2, L.s2, L.c2)) {
-        if ((rc = conv23_lds_wgrad(s, bf, xh, 2, (int)B, w.a1, w.da2, nsum1 ? w.parts2 : w.parts, G + L.oW2, G + L.ob2,
-                                   !nsum1)))
+        if ((rc = conv23_lds_wgrad(s, bf, xh, 2, (int)B, w.a1, w.da2, nsum1 && kTailConvSums ? w.parts2 : w.parts,
+                                   G + L.oW2, G + L.ob2, !(nsum1 && kTailConvSums))))
             return rc;
     } else if ((rc = conv_wgrad_nhwc(s, bf, geom2(L, B), w.a1, w.da2, w.parts, kSplitW2, G + L.oW2, G + L.ob2))) {
         return rc;
@@ -2039,8 +2045,10 @@ int backward_trunk(const float *P, const CnnLayout &L, const FrameSrc &fs, int64
                                       &np)))
                 return rc;
             // conv3 / conv2 weight-gradient sums (k_sum_parts_tiles' blocks: 64 outputs each)
-            const TailSum t3{w.parts3, kConvWgradWG, (int64_t)64 * (L.K3 + 1), L.K3, G + L.oW3, G + L.ob3, L.K3 + 1};
-            const TailSum t2{w.parts2, kConvWgradWG, (int64_t)64 * (L.K2 + 1), L.K2, G + L.oW2, G + L.ob2, L.K2 + 1};
+            const TailSum t3{w.parts3, kConvWgradWG, (int64_t)64 * (L.K3 + 1), L.K3, G + L.oW3, G + L.ob3,
+                             kTailConvSums ? L.K3 + 1 : 0};
+            const TailSum t2{w.parts2, kConvWgradWG, (int64_t)64 * (L.K2 + 1), L.K2, G + L.oW2, G + L.ob2,
+                             kTailConvSums ? L.K2 + 1 : 0};
             const int nx = ns + ncb + t3.nblk + t2.nblk;
             GS_REQUIRE(nx <= kTailPartsMax, "the fused tail's %d partial blocks exceed %d", nx, kTailPartsMax);
             hipLaunchKernelGGL(k_conv1_sum_norm, dim3((unsigned)(nx + kNormBlocks)), dim3(256), 0, s, w.parts, np, n1, n1,
