@@ -117,9 +117,13 @@ constexpr int kAdamQuads = 4;      // float4 of parameters per clip/Adam thread
 constexpr int kConv1NormMax = 1024;   // k_conv1_sum_norm sum blocks (conv1 [dW1 | db1] <= 64 K floats)
 constexpr int kTailPartsMax = 4096;
 #ifndef GS_TAIL_CONV_SUMS
-#define GS_TAIL_CONV_SUMS 1
+#define GS_TAIL_CONV_SUMS 0
 #endif
-constexpr bool kTailConvSums = GS_TAIL_CONV_SUMS != 0;   // the fused tail also sums conv2 / conv3 (A/B switch)   // the fused tail's squared-norm partials (conv1 + head + conv3 + conv2 blocks)
+// the fused tail also sums the conv2 / conv3 weight-gradient partials (1) or k_sum_parts_tiles does
+// after each weight gradient (0, kept): same-box A/B, C4 bf16 update 316.2 / 315.9 vs 310.2 /
+// 311.2 us per minibatch (gpurun_out/r06r) — the tail's 164-VGPR blocks sum the 72 MB slower than
+// the two dedicated launches
+constexpr bool kTailConvSums = GS_TAIL_CONV_SUMS != 0;   // the fused tail's squared-norm partials (conv1 + head + conv3 + conv2 blocks)
 // k_cnn_head_wgrad: 64-column blocks x kHwSplits row ranges, kHwRows rows of loads in flight,
 // kDbhSlices row slices of a range's dbh sums; at most kHwMaxCb column blocks (HID <= 512: head_fused)
 constexpr int kHwCols = 64, kHwSplits = 16, kHwRows = 4, kDbhSlices = 8, kHwMaxCb = 8;

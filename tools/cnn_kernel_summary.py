@@ -34,12 +34,13 @@ PEAK_HBM = 8000.0         # GB/s
 SEQ_FC = [("conv1_fwd", "k_conv1_fwd"), ("conv2_fwd", "k_conv_fwd"), ("conv3_fwd", "k_conv_fwd"),
           ("fc_fwd", "k_fc"), ("head_loss", "k_cnn_head_loss"), ("head_wgrad_metrics", "k_cnn_head_wgrad"),
           ("fc_wgrad", "k_fc"), ("fc_dgrad_relu_mask", "k_fc"),
-          ("conv3_wgrad", "k_conv_wgrad"), ("conv3_dgrad", "k_conv_dgrad"),
-          ("conv2_wgrad", "k_conv_wgrad"), ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"),
-          ("tail_sums_head_combine_norm", "k_conv1_sum_norm"), ("clip_adam", "k_clip_adam_flat")]
+          ("conv3_wgrad", "k_conv_wgrad"), ("conv3_wgrad_sum", "k_sum_parts"),
+          ("conv3_dgrad", "k_conv_dgrad"), ("conv2_wgrad", "k_conv_wgrad"), ("conv2_wgrad_sum", "k_sum_parts"),
+          ("conv2_dgrad", "k_conv_dgrad"), ("conv1_wgrad", "k_conv1_wgrad"),
+          ("tail_conv1_sum_head_combine_norm", "k_conv1_sum_norm"), ("clip_adam", "k_clip_adam_flat")]
 # (round 6: the head weight gradient's own kernel replaced k_cnn_head_wsum; the fused backward tail
-# k_conv1_sum_norm sums the conv1 / conv2 / conv3 weight-gradient partials, adds the head blocks and
-# writes the norm partials, replacing three partial-sum launches and k_norm_partials)
+# k_conv1_sum_norm sums conv1's weight-gradient partials, adds the head blocks and writes the norm
+# partials, replacing the conv1 partial sum and k_norm_partials)
 # the fp32 update (round 5): the fc forward as two K halves + k_fc_sum (the bias + ReLU epilogue)
 SEQ_FC_SPLIT = SEQ_FC[:4] + [("fc_fwd_splitk_sum", "k_fc_sum")] + SEQ_FC[4:]
 SEQ = SEQ_FC
