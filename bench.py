@@ -449,6 +449,8 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
+    if args.warmup < 2 and not args.no_graph:
+        _log("[bench] warning: --warmup < 2 times the rollout graph's capture (second collect)")
     tw = time.perf_counter()
     for _ in range(args.warmup):
         agent.train_epoch()
@@ -661,7 +663,10 @@ def main():
                        "dp_mode": args.dp_mode,
                        # the reference's training_step diagnostics (opt/activations/*, per-step
                        # records) are a track_stats option; the timed region runs without them
-                       "track_stats": False, "activation_stats_in_timed_region": False},
+                       "track_stats": False, "activation_stats_in_timed_region": False,
+                       # the rollout's step graph is captured on the second collect (the first runs
+                       # eagerly and allocates): with --warmup < 2 the capture is inside the timed region
+                       "rollout_graph_capture_in_timed_region": (not args.no_graph) and args.warmup < 2},
             "roofline": roofline,
             "rooflines": rooflines,
             "stages_us": {k: round(v, 3) for k, v in stage_us.items()},
