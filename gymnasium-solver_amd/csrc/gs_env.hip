@@ -298,9 +298,15 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window(const uint8_t *_
 }
 
 // The same window from 16-sample units (VEC16: 16-B aligned dones, n % 16 == 0): a dword-quad of
-// dones per lane and unit, so the count pass reads 1 byte per sample instead of 5 (the returns are
-// loaded only where an episode ended); kWinUnits units per lane in flight.  Wave w owns a
-// contiguous unit range; pass 2 as in k_episode_window (contiguous per-lane chunks, one wave scan).
+// dones per unit (1 byte per sample read; the returns / lengths loaded only where an episode ended,
+// each row's first episode per lane in one round of loads).
+// Wave w owns the units [w 64 R, (w + 1) 64 R), R = ceil(U / 1024) rows of 64 (lane l: unit
+// 64 k + l of row k, coalesced): one pass counts them (kWinUnits rows in flight; the masks stay in
+// registers when R <= kWinUnits), the wave totals number the waves' first episodes, and each row's
+// wave scan numbers its lanes' episodes while they gather their returns (best) and write the kept
+// (return, length) pairs — round 6: the count and numbering passes had been two walks with a
+// per-lane chunk count in between (14.4 us at C2's 32 x 4096; thread-contiguous chunks instead,
+// uncoalesced, measured 16.7).
 constexpr int kWinUnits = 8;
 __device__ __forceinline__ unsigned done_mask16(uint4 d)
 {
@@ -309,6 +315,16 @@ __device__ __forceinline__ unsigned done_mask16(uint4 d)
         return ((nz >> 7) & 1u) | ((nz >> 14) & 2u) | ((nz >> 21) & 4u) | ((nz >> 28) & 8u);
     };
     return nz4(d.x) | (nz4(d.y) << 4) | (nz4(d.z) << 8) | (nz4(d.w) << 12);
+}
+
+__device__ __forceinline__ int wave_incl_scan32(int v, int lane)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
 }
 
 __global__ __launch_bounds__(kWinThreads) void k_episode_window16(const uint8_t *__restrict__ dones,
@@ -323,94 +339,103 @@ __global__ __launch_bounds__(kWinThreads) void k_episode_window16(const uint8_t 
     extern __shared__ double old[];           // [2][W]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint4 *d16 = reinterpret_cast<const uint4 *>(dones);
-    const int64_t U = n / 16;
-    const int64_t u0 = (int64_t)wave * U / kWinWaves, u1 = (int64_t)(wave + 1) * U / kWinWaves;
+    const int64_t U = n / 16, R = (U + kWinThreads - 1) / kWinThreads;
+    const int64_t wb = min(U, (int64_t)wave * 64 * R), we = min(U, wb + 64 * R);
+    const bool held = R <= kWinUnits;          // block-uniform: the masks fit the registers
     for (int i = tid; i < 2 * W; i += kWinThreads) old[i] = win[i];
-    // ---- pass 1: done count and best return of this wave's range
-    int64_t cnt = 0;
-    double best = -INFINITY;
-    for (int64_t b = u0; b < u1; b += 64 * kWinUnits) {
-        unsigned m[kWinUnits];
+    // rows b .. b + kWinUnits - 1 of this wave's range: lane's unit of each, 0 past the range
+    unsigned m[kWinUnits];
+    auto load_rows = [&](int64_t b) {
 #pragma unroll
         for (int k = 0; k < kWinUnits; ++k) {
-            const int64_t u = b + (int64_t)k * 64 + lane;
-            m[k] = done_mask16(d16[u < u1 ? u : u0]);
-            if (u >= u1) m[k] = 0u;
+            const int64_t u = wb + (b + k) * 64 + lane;
+            m[k] = done_mask16(d16[u < we ? u : wb]);
+            if (u >= we) m[k] = 0u;
         }
+    };
+    // ---- count pass
+    int c = 0;
+    if (wb < we) {
+        for (int64_t b = 0; b < R; b += kWinUnits) {
+            load_rows(b);
 #pragma unroll
-        for (int k = 0; k < kWinUnits; ++k) {
-            cnt += __popc(m[k]);
-            const int64_t base = 16 * (b + (int64_t)k * 64 + lane);
-            for (unsigned mm = m[k]; mm; mm &= mm - 1u)
-                best = fmax(best, (double)ep_ret[base + __ffs(mm) - 1]);
+            for (int k = 0; k < kWinUnits; ++k) c += __popc(m[k]);
         }
-    }
+    } else {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        cnt += __shfl_xor(cnt, o, 64);
-        best = fmax(best, __shfl_xor(best, o, 64));
+        for (int k = 0; k < kWinUnits; ++k) m[k] = 0u;
     }
-    if (lane == 0) {
-        wcnt[wave] = cnt;
-        wbest[wave] = best;
-    }
+    c = wave_incl_scan32(c, lane);
+    if (lane == 63) wcnt[wave] = c;
     __syncthreads();
-    int64_t total = 0, before = 0;
-    double all_best = -INFINITY;
+    int64_t total = 0, run = 0;
 #pragma unroll
     for (int w = 0; w < kWinWaves; ++w) {
-        before += w < wave ? wcnt[w] : 0;
+        run += w < wave ? wcnt[w] : 0;
         total += wcnt[w];
-        all_best = fmax(all_best, wbest[w]);
     }
+    // the previous window shifted left by this rollout's episode count
     for (int i = tid; i < W; i += kWinThreads)
         if (i + total < W) {
             win[i] = old[i + total];
             win[W + i] = old[W + i + total];
         }
-    // ---- pass 2: the last W episodes, lane l over the contiguous units [u0 + l C, u0 + (l + 1) C)
+    // ---- numbering pass: row k's wave scan gives each lane its first episode number; the lane
+    // gathers its episodes' returns (best) and writes the kept ones (numbers >= total - W)
     const int64_t first = total - W;
-    if (before + wcnt[wave] > first) {
-        const int64_t C = (u1 - u0 + 63) / 64;
-        const int64_t lu0 = min(u1, u0 + lane * C), lu1 = min(u1, lu0 + C);
-        int64_t c = 0;
-        for (int64_t b = lu0; b < lu1; b += kWinUnits) {
-            unsigned m[kWinUnits];
+    double best = -INFINITY;
+    if (wcnt[wave] > 0) {
+        for (int64_t b = 0; b < R; b += kWinUnits) {
+            if (!held) load_rows(b);          // second walk (L2-hot)
+            // each row's first episode of the lane: its return and length loaded for all rows at
+            // once (one round; further episodes of a unit, rarer, load in their own rounds)
+            float r1[kWinUnits];
+            int l1[kWinUnits];
 #pragma unroll
             for (int k = 0; k < kWinUnits; ++k) {
-                const int64_t u = b + k;
-                m[k] = done_mask16(d16[u < lu1 ? u : lu0]);
-                if (u >= lu1) m[k] = 0u;
+                const int64_t unit = wb + (b + k) * 64 + lane;
+                const int64_t i = m[k] ? 16 * unit + __ffs(m[k]) - 1 : 0;
+                r1[k] = ep_ret[i];
+                l1[k] = ep_len[i];
             }
 #pragma unroll
-            for (int k = 0; k < kWinUnits; ++k) c += __popc(m[k]);
-        }
-        const int64_t incl = wave_incl_scan(c, lane);
-        int64_t pos = before + incl - c;
-        if (pos + c > first) {
-            for (int64_t b = lu0; b < lu1; b += kWinUnits) {
-                unsigned m[kWinUnits];
+            for (int k = 0; k < kWinUnits; ++k) asm volatile("" ::"v"(r1[k]), "v"(l1[k]));
 #pragma unroll
-                for (int k = 0; k < kWinUnits; ++k) {
-                    const int64_t u = b + k;
-                    m[k] = done_mask16(d16[u < lu1 ? u : lu0]);
-                    if (u >= lu1) m[k] = 0u;
-                }
-#pragma unroll
-                for (int k = 0; k < kWinUnits; ++k)
-                    for (unsigned mm = m[k]; mm; mm &= mm - 1u) {
-                        const int64_t slot = pos - first;
-                        if (slot >= 0) {
-                            const int64_t i = 16 * (b + k) + __ffs(mm) - 1;
-                            win[slot] = (double)ep_ret[i];
-                            win[W + slot] = (double)ep_len[i];
-                        }
-                        ++pos;
+            for (int k = 0; k < kWinUnits; ++k) {
+                const int ck = __popc(m[k]);
+                const int incl = wave_incl_scan32(ck, lane);
+                int64_t pos = run + incl - ck;
+                run += __shfl(incl, 63, 64);
+                const int64_t unit = wb + (b + k) * 64 + lane;
+                unsigned mm = m[k];
+                float r = r1[k];
+                int len = l1[k];
+                while (mm) {
+                    best = fmax(best, (double)r);
+                    const int64_t slot = pos - first;
+                    if (slot >= 0) {
+                        win[slot] = (double)r;
+                        win[W + slot] = (double)len;
                     }
+                    ++pos;
+                    mm &= mm - 1u;
+                    if (mm) {
+                        const int64_t i = 16 * unit + __ffs(mm) - 1;
+                        r = ep_ret[i];
+                        len = ep_len[i];
+                    }
+                }
             }
         }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = fmax(best, __shfl_xor(best, o, 64));
+    if (lane == 0) wbest[wave] = best;
+    __syncthreads();
     if (tid == 0) {
+        double all_best = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < kWinWaves; ++w) all_best = fmax(all_best, wbest[w]);
         meta[0] += (double)total;
         meta[1] = fmax(meta[1], all_best);
         if (total_out) *total_out = total;

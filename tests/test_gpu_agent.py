@@ -270,7 +270,8 @@ def test_untracked_collector_keeps_the_rolling_window(cuda, over):
 
 
 @pytest.mark.parametrize("shape,p,W", [((32, 4096), 0.01, 100), ((32, 4096), 0.3, 2048), ((7, 33), 0.2, 5),
-                                       ((3, 7), 0.5, 1), ((1, 1), 1.0, 3), ((2048, 64), 0.02, 100)])
+                                       ((3, 7), 0.5, 1), ((1, 1), 1.0, 3), ((2048, 64), 0.02, 100),
+                                       ((512, 1024), 0.01, 100), ((4, 16), 0.5, 7), ((1, 16), 0.0, 4)])
 def test_episode_window_kernel_vs_model(cuda, shape, p, W):
     """gs_episode_window (the track_stats=False rolling window, rollout_collector.py:242-294,
     753-758) against its definition: the window is the last W entries of (previous window ++ this
