@@ -1230,9 +1230,13 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
     constexpr int NE = NXU + ND4, BATCH = (NE + 255) / 256;
     static_assert(G::C % XU == 0, "whole units per position");
     static_assert(BATCH <= kWgradBurstMax, "one staging burst per sample");
-    constexpr bool PF = (kWgradPrefetch & (G::C == 32 ? 1 : 2)) != 0;     // conv2: C = 32, conv3: 64
-    float4 v[BATCH];
+    // fp32 keeps the round-5 form (the burst loaded and stored inside the loop): the prefetch form
+    // measured no faster there, and the fp32 kernels compiled from its structure ran 11 us slower
+    // even with the prefetch off (same box, DESIGN §4.2 "Open")
+    constexpr bool PF = BF && (kWgradPrefetch & (G::C == 32 ? 1 : 2)) != 0;     // conv2: C = 32, conv3: 64
+    float4 v[PF ? BATCH : 1];
     auto burst = [&](int r) {
+        if constexpr (PF) {
         const act_t<XH> *xin = in + (int64_t)r * G::H * G::W * G::C;
         const float *dyin = dY + (int64_t)r * G::OHW * G::CO;
 #pragma unroll
@@ -1247,13 +1251,52 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
                                               : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
+        }
     };
     if (PF && (int)blockIdx.x < R) burst(blockIdx.x);
 
     for (int r = blockIdx.x; r < R; r += gridDim.x) {
         __syncthreads();
         C1S_MARK(3)                                     // loop-top barrier
-        if (!PF) burst(r);
+        if constexpr (!PF) {     // the round-5 form: this sample's burst, then its LDS stores
+            const act_t<XH> *xin = in + (int64_t)r * G::H * G::W * G::C;
+            const float *dyin = dY + (int64_t)r * G::OHW * G::CO;
+            for (int e0 = 0; e0 < NE; e0 += 256 * BATCH) {
+                float4 u[BATCH];
+#pragma unroll
+                for (int j = 0; j < BATCH; ++j) {
+                    const int e = e0 + tid + 256 * j;
+                    if (e < NXU) {
+                        u[j] = *reinterpret_cast<const float4 *>(xin + XU * (int64_t)e);
+                    } else {
+                        const int d = e - NXU;
+                        const int p = d / (G::CO / 4);
+                        u[j] = (e < NE && p < G::OHW) ? *reinterpret_cast<const float4 *>(dyin + 4 * (int64_t)d)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < BATCH; ++j) {
+                    const int e = e0 + tid + 256 * j;
+                    if (e < NXU) {
+                        const int pos = e / (G::C / XU), cu = e - pos * (G::C / XU);
+                        float *dst = xs + pos * X::CSX + XU * cu;
+                        if constexpr (XH) {
+                            const uint4 h = make_uint4(__float_as_uint(u[j].x), __float_as_uint(u[j].y),
+                                                       __float_as_uint(u[j].z), __float_as_uint(u[j].w));
+                            *reinterpret_cast<float4 *>(dst) = bf16x4_f32(make_uint2(h.x, h.y));
+                            *reinterpret_cast<float4 *>(dst + 4) = bf16x4_f32(make_uint2(h.z, h.w));
+                        } else {
+                            *reinterpret_cast<float4 *>(dst) = u[j];
+                        }
+                    } else if (e < NE) {
+                        const int d = e - NXU;
+                        const int p = d / (G::CO / 4), c4 = d - p * (G::CO / 4);
+                        *reinterpret_cast<float4 *>(ds + p * X::DS + 4 * c4) = u[j];
+                    }
+                }
+            }
+        } else {
 #pragma unroll
         for (int j = 0; j < BATCH; ++j) {
             const int e = tid + 256 * j;
@@ -1274,7 +1317,8 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(const act_t<XH> *__restrict_
                 *reinterpret_cast<float4 *>(ds + p * X::DS + 4 * c4) = v[j];
             }
         }
-        if (PF && r + (int)gridDim.x < R) burst(r + gridDim.x);     // the next sample's loads in flight
+        if (r + (int)gridDim.x < R) burst(r + gridDim.x);     // the next sample's loads in flight
+        }
         C1S_MARK(1)                                     // staging burst landed + LDS stores
         __syncthreads();
         C1S_MARK(2)                                     // barrier
